@@ -1,0 +1,120 @@
+#!/usr/bin/env python
+"""Headline benchmark: DLRM training throughput (examples/sec, whole node) on
+Criteo-1TB-shaped synthetic data at 1/2/4/8 MI355X (BASELINE.json metric).
+
+Model (MLPerf DLRM / TorchRec-DLRM shape): 13 dense + 26 sparse features,
+MLPerf Criteo-Terabyte cardinalities (max-ind-range 40M, 188M rows total),
+embedding dim 128 (fp32 tables, ~96 GB), bottom MLP 13-512-256-128, dot
+interaction, top MLP 479-1024-1024-512-256-1, bf16 compute / fp32 master.
+Embeddings: table-wise sharded across ranks (all on one GPU at N=1), fused
+row-wise Adagrad; dense: fused AdamW, all-reduced over RCCL.
+Weak scaling: --batch is per GPU; value = global examples / second.
+
+Launch: python bench.py [--gpus 1]; for N>1 via
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("TDFO_BENCH_BATCH", 8192)),
+                    help="per-GPU batch (weak scaling)")
+    ap.add_argument("--rows", default="1tb", choices=["1tb", "kaggle", "tiny"])
+    ap.add_argument("--model", default="dlrm", choices=["dlrm", "dcnv2"])
+    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--pool", type=int, default=8, help="pre-generated device batches")
+    ap.add_argument("--dist", default="uniform", choices=["uniform", "zipf"])
+    return ap.parse_args(argv)
+
+
+def main(argv=None):
+    args = parse(argv)
+    from tdfo_amd.parallel.dist import init_distributed, reset
+    from tdfo_amd.models.dlrm import (CRITEO_1TB_ROWS, CRITEO_KAGGLE_ROWS, MLPERF_MULTIHOT,
+                                      DLRMConfig, DLRMTrainer)
+    from tdfo_amd.data.synthetic import SyntheticCriteo
+    from tdfo_amd.ops import _ext
+
+    info = init_distributed("cuda")
+    world = info.world_size
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    if not _ext.load():
+        raise RuntimeError("native HIP library failed to load")
+    rows = {"1tb": CRITEO_1TB_ROWS, "kaggle": CRITEO_KAGGLE_ROWS,
+            "tiny": [1000] * 26}[args.rows]
+    if args.model == "dlrm":
+        cfg = DLRMConfig(table_rows=list(rows))
+    else:
+        cfg = DLRMConfig(table_rows=list(rows), interaction="dcn", pooling=list(MLPERF_MULTIHOT),
+                         top=[1024, 1024, 512, 256, 1])
+    B = args.batch
+    t0 = time.time()
+    tr = DLRMTrainer(cfg, B, info.device, group=info.group, rank=info.rank, world_size=world)
+    data = SyntheticCriteo(cfg.table_rows, B, pooling=cfg.pooling_factors(), device=info.device,
+                           seed=1, rank=info.rank, dist=args.dist)
+    pool = [data.next() for _ in range(args.pool)]
+    torch.cuda.synchronize()
+    setup_s = time.time() - t0
+    use_graph = (not args.no_graph) and world == 1
+
+    def run(n, start):
+        for i in range(n):
+            tr.load_batch(*pool[(start + i) % len(pool)])
+            tr.step()
+
+    run(args.warmup, 0)
+    if use_graph:
+        tr.capture_graph(warmup=1)
+    torch.cuda.synchronize()
+    tr.pop_loss()
+    if world > 1:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    run(args.steps, args.warmup)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    el = time.perf_counter() - t
+    if world > 1:
+        x = torch.tensor([el], dtype=torch.float64, device=info.device)
+        torch.distributed.all_reduce(x, op=torch.distributed.ReduceOp.MAX)
+        el = float(x.item())
+    loss = tr.pop_loss() / max(1, args.steps * B)
+    ms = el / args.steps * 1e3
+    value = B * world * args.steps / el
+    if info.rank == 0:
+        print(json.dumps({"plan": tr.plan.summary(), "setup_s": round(setup_s, 1),
+                          "train_loss": round(loss, 4), "graph": use_graph,
+                          "dense_tflops": round(cfg.dense_flops_per_example() * value / 1e12, 1)}),
+              file=sys.stderr)
+        print(json.dumps({
+            "metric": "examples/sec (whole node) DLRM on Criteo-1TB-shaped synthetic",
+            "value": round(value, 1), "unit": "examples/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic (Criteo-1TB-shaped, uniform ids, random-init embeddings)",
+            "config": {"model": "DLRM" if args.model == "dlrm" else "DCN-v2",
+                       "global_batch": B * world, "seq_len": None,
+                       "parallelism": (f"tw-sharded-emb x{world} + dp{world}" if world > 1
+                                       else "single-gpu"),
+                       "tables": f"criteo-{args.rows}", "embedding_dim": cfg.embedding_dim,
+                       "per_gpu_batch": B}}), flush=True)
+    reset()
+
+
+if __name__ == "__main__":
+    main()

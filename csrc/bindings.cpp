@@ -1,0 +1,345 @@
+// torch op registrations for the tdfo_amd HIP kernels (namespace torch.ops.tdfo).
+//
+// Every op is an out-variant: callers own all buffers, so the ops can be
+// captured into a hipGraph (torch.cuda.CUDAGraph) and replayed without
+// allocation. Shapes, dtypes, strides and alignment are validated on the host
+// before any launch (a mis-shaped launch can fault the GPU).
+#include <ATen/ATen.h>
+#include <ATen/hip/HIPContext.h>
+#include <torch/library.h>
+
+#include "tdfo_kernels.h"
+
+namespace {
+
+using at::Tensor;
+
+hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
+
+const uint16_t* bf16_ptr(const Tensor& t) {
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, "expected bf16 tensor");
+  return reinterpret_cast<const uint16_t*>(t.data_ptr());
+}
+uint16_t* bf16_mut(const Tensor& t) {
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16, "expected bf16 tensor");
+  return reinterpret_cast<uint16_t*>(t.data_ptr());
+}
+void check_dev(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+}
+void check_2d_rowmajor(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.dim() == 2, name, " must be 2-D");
+  TORCH_CHECK(t.stride(1) == 1, name, " must have unit inner stride");
+}
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+// ------------------------------------------------------------------ gemm
+void gemm(const Tensor& a, bool a_col, const Tensor& b, bool b_col,
+          const c10::optional<Tensor>& bias, bool relu,
+          const c10::optional<Tensor>& mask, const c10::optional<Tensor>& out,
+          const c10::optional<Tensor>& out32, int64_t splits) {
+  check_dev(a, "a"); check_dev(b, "b");
+  check_2d_rowmajor(a, "a"); check_2d_rowmajor(b, "b");
+  const int64_t M = a_col ? a.size(1) : a.size(0);
+  const int64_t K = a_col ? a.size(0) : a.size(1);
+  const int64_t N = b_col ? b.size(1) : b.size(0);
+  const int64_t Kb = b_col ? b.size(0) : b.size(1);
+  TORCH_CHECK(K == Kb, "gemm: K mismatch ", K, " vs ", Kb);
+  TORCH_CHECK(K % 64 == 0 && K > 0, "gemm: K must be a positive multiple of 64, got ", K);
+  TORCH_CHECK(M > 0 && N > 0, "gemm: empty output");
+  TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0, "gemm: ld must be multiple of 8");
+  TORCH_CHECK(aligned16(a.data_ptr()) && aligned16(b.data_ptr()), "gemm: operands must be 16-B aligned");
+  if (a_col) TORCH_CHECK(M % 8 == 0 && M >= 8, "gemm: col-layout A needs M % 8 == 0");
+  if (b_col) TORCH_CHECK(N % 8 == 0 && N >= 8, "gemm: col-layout B needs N % 8 == 0");
+  TORCH_CHECK(splits >= 1 && splits <= K / 64, "gemm: bad split count");
+  tdfo::GemmArgs g{};
+  g.A = bf16_ptr(a); g.lda = a.stride(0); g.a_col = a_col;
+  g.B = bf16_ptr(b); g.ldb = b.stride(0); g.b_col = b_col;
+  g.M = (int)M; g.N = (int)N; g.K = (int)K; g.splits = (int)splits;
+  if (bias) {
+    check_dev(*bias, "bias");
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->is_contiguous() && bias->numel() == N,
+                "gemm: bias must be fp32 [N]");
+    g.bias = bias->data_ptr<float>();
+  }
+  g.relu = relu;
+  if (mask) {
+    check_2d_rowmajor(*mask, "mask");
+    TORCH_CHECK(mask->size(0) == M && mask->size(1) == N, "gemm: mask shape");
+    g.mask = bf16_ptr(*mask); g.ldm = mask->stride(0);
+  }
+  TORCH_CHECK(out || out32, "gemm: need an output");
+  if (out) {
+    check_2d_rowmajor(*out, "out");
+    TORCH_CHECK(out->size(0) == M && out->size(1) == N, "gemm: out shape");
+    g.C = bf16_mut(*out); g.ldc = out->stride(0);
+    TORCH_CHECK(splits == 1, "gemm: bf16 output requires splits == 1");
+  }
+  if (out32) {
+    TORCH_CHECK(out32->scalar_type() == at::kFloat && out32->is_contiguous(), "gemm: out32 fp32 contiguous");
+    TORCH_CHECK(out32->numel() >= splits * M * N, "gemm: out32 too small");
+    g.C32 = out32->data_ptr<float>(); g.ldc32 = N;
+  }
+  tdfo::gemm_bf16(g, cur_stream());
+}
+
+// ----------------------------------------------------------- interaction
+tdfo::SlotMap make_slots(at::IntArrayRef off, at::IntArrayRef stride, int64_t F) {
+  TORCH_CHECK((int64_t)off.size() >= F && (int64_t)stride.size() >= F, "slot map too short");
+  tdfo::SlotMap m{};
+  for (int64_t i = 0; i < F && i < 32; ++i) { m.off[i] = off[i]; m.stride[i] = stride[i]; }
+  return m;
+}
+
+void check_inter(int64_t F, int64_t D) {
+  TORCH_CHECK(F >= 2 && F <= 32, "interaction: F must be in [2, 32]");
+  TORCH_CHECK(D == 32 || D == 64 || D == 128 || D == 256, "interaction: D must be 32/64/128/256");
+}
+
+void check_slots_fit(const Tensor& emb, const tdfo::SlotMap& m, int64_t F, int64_t D, int64_t B) {
+  for (int64_t i = 1; i < F; ++i) {
+    TORCH_CHECK(m.off[i] % 8 == 0 && m.stride[i] % 8 == 0, "slot offsets must be multiples of 8");
+    TORCH_CHECK(m.off[i] >= 0 && m.off[i] + (B - 1) * m.stride[i] + D <= emb.numel(),
+                "interaction: slot ", i, " out of range");
+  }
+}
+
+void interaction_fwd(const Tensor& dense, const Tensor& emb, at::IntArrayRef off,
+                     at::IntArrayRef stride, int64_t F, int64_t D, const Tensor& out) {
+  check_dev(dense, "dense"); check_dev(emb, "emb"); check_dev(out, "out");
+  check_inter(F, D); check_2d_rowmajor(dense, "dense"); check_2d_rowmajor(out, "out");
+  const int64_t B = dense.size(0);
+  TORCH_CHECK(dense.size(1) >= D && dense.stride(0) % 8 == 0, "dense shape");
+  TORCH_CHECK(out.size(0) == B && out.size(1) >= D + F * (F - 1) / 2 && out.size(1) % 8 == 0 &&
+              out.stride(0) == out.size(1), "interaction out must be [B, ldo] contiguous, ldo%8==0");
+  TORCH_CHECK(emb.is_contiguous() && aligned16(emb.data_ptr()) && aligned16(dense.data_ptr()) &&
+              aligned16(out.data_ptr()), "alignment");
+  auto m = make_slots(off, stride, F);
+  check_slots_fit(emb, m, F, D, B);
+  tdfo::interaction_fwd(bf16_ptr(dense), dense.stride(0), bf16_ptr(emb), m, (int)F, (int)D,
+                        (int)B, bf16_mut(out), out.stride(0), cur_stream());
+}
+
+void interaction_bwd(const Tensor& dz, const Tensor& dense, const Tensor& emb,
+                     at::IntArrayRef off, at::IntArrayRef stride, int64_t F, int64_t D,
+                     const Tensor& d_dense, const Tensor& d_emb, at::IntArrayRef doff,
+                     at::IntArrayRef dstride, bool relu_mask) {
+  check_dev(dz, "dz"); check_dev(dense, "dense"); check_dev(emb, "emb");
+  check_dev(d_dense, "d_dense"); check_dev(d_emb, "d_emb");
+  check_inter(F, D);
+  check_2d_rowmajor(dz, "dz"); check_2d_rowmajor(dense, "dense"); check_2d_rowmajor(d_dense, "d_dense");
+  const int64_t B = dense.size(0);
+  TORCH_CHECK(dz.size(0) == B && dz.size(1) >= D + F * (F - 1) / 2, "dz shape");
+  TORCH_CHECK(d_dense.size(0) == B && d_dense.size(1) >= D, "d_dense shape");
+  TORCH_CHECK(dz.stride(0) % 8 == 0 && aligned16(dz.data_ptr()), "dz alignment");
+  TORCH_CHECK(emb.is_contiguous() && d_emb.is_contiguous(), "emb contiguous");
+  auto m = make_slots(off, stride, F);
+  auto dm = make_slots(doff, dstride, F);
+  check_slots_fit(emb, m, F, D, B);
+  check_slots_fit(d_emb, dm, F, D, B);
+  tdfo::interaction_bwd(bf16_ptr(dz), dz.stride(0), bf16_ptr(dense), dense.stride(0),
+                        bf16_ptr(emb), m, (int)F, (int)D, (int)B, bf16_mut(d_dense),
+                        d_dense.stride(0), bf16_mut(d_emb), dm, relu_mask, cur_stream());
+}
+
+// ------------------------------------------------------------- embedding
+void check_i64(const Tensor& t, const char* n) {
+  check_dev(t, n);
+  TORCH_CHECK(t.scalar_type() == at::kLong && t.is_contiguous(), n, " must be contiguous int64");
+}
+
+void embedding_bag_fwd(const Tensor& W, const Tensor& row_offset, const Tensor& indices,
+                       const Tensor& offsets, const Tensor& out_off,
+                       const c10::optional<Tensor>& psw, int64_t T, int64_t B, bool mean,
+                       const Tensor& out, int64_t out_stride) {
+  check_dev(W, "W"); check_2d_rowmajor(W, "W");
+  TORCH_CHECK(W.scalar_type() == at::kFloat && W.is_contiguous(), "W must be contiguous fp32");
+  const int64_t D = W.size(1);
+  TORCH_CHECK(D == 16 || D == 32 || D == 64 || D == 128 || D == 256 || D == 512, "embedding D unsupported");
+  check_i64(row_offset, "row_offset"); check_i64(indices, "indices");
+  check_i64(offsets, "offsets"); check_i64(out_off, "out_off");
+  TORCH_CHECK(row_offset.numel() == T && out_off.numel() == T && offsets.numel() == T * B + 1,
+              "embedding: table/bag count mismatch");
+  check_dev(out, "out"); TORCH_CHECK(out.is_contiguous(), "out contiguous");
+  TORCH_CHECK(out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kFloat, "out dtype");
+  TORCH_CHECK(out_stride % 4 == 0, "out_stride must be a multiple of 4");
+  tdfo::EmbFwdArgs a{};
+  a.W = W.data_ptr<float>(); a.D = (int)D;
+  a.row_offset = row_offset.data_ptr<int64_t>(); a.indices = indices.data_ptr<int64_t>();
+  a.offsets = offsets.data_ptr<int64_t>(); a.out_off = out_off.data_ptr<int64_t>();
+  if (psw) {
+    TORCH_CHECK(psw->scalar_type() == at::kFloat && psw->numel() == indices.numel(), "psw");
+    a.psw = psw->data_ptr<float>();
+  }
+  a.T = (int)T; a.B = (int)B; a.mean = mean; a.out_stride = out_stride;
+  a.out = out.data_ptr(); a.out_bf16 = out.scalar_type() == at::kBFloat16;
+  tdfo::embedding_bag_fwd(a, cur_stream());
+}
+
+void embedding_bwd(const Tensor& W, const Tensor& row_offset, const Tensor& indices,
+                   const Tensor& offsets, const Tensor& grad_off,
+                   const c10::optional<Tensor>& psw, int64_t T, int64_t B, bool mean,
+                   int64_t key_bits, const Tensor& grad, int64_t grad_stride, int64_t opt,
+                   const c10::optional<Tensor>& state1, const c10::optional<Tensor>& state2,
+                   const Tensor& hyper, double eps, double beta1, double beta2,
+                   double weight_decay, const c10::optional<Tensor>& dense_grad) {
+  check_dev(W, "W");
+  TORCH_CHECK(W.scalar_type() == at::kFloat && W.is_contiguous() && W.dim() == 2, "W fp32 2-D");
+  const int64_t D = W.size(1);
+  TORCH_CHECK(D == 16 || D == 32 || D == 64 || D == 128 || D == 256 || D == 512, "embedding D unsupported");
+  check_i64(row_offset, "row_offset"); check_i64(indices, "indices");
+  check_i64(offsets, "offsets"); check_i64(grad_off, "grad_off");
+  TORCH_CHECK(offsets.numel() == T * B + 1 && grad_off.numel() == T && row_offset.numel() == T, "bwd counts");
+  TORCH_CHECK(key_bits >= 1 && key_bits <= 64, "key_bits");
+  TORCH_CHECK(grad.is_contiguous() && (grad.scalar_type() == at::kBFloat16 || grad.scalar_type() == at::kFloat), "grad");
+  TORCH_CHECK(hyper.scalar_type() == at::kFloat && hyper.numel() >= 2 && hyper.is_cuda(), "hyper fp32[>=2] on device");
+  const int64_t nnz = indices.numel();
+  TORCH_CHECK(nnz < (1LL << 31), "nnz too large");
+  tdfo::EmbBwdArgs a{};
+  a.W = W.data_ptr<float>(); a.D = (int)D;
+  a.row_offset = row_offset.data_ptr<int64_t>(); a.indices = indices.data_ptr<int64_t>();
+  a.offsets = offsets.data_ptr<int64_t>(); a.grad_off = grad_off.data_ptr<int64_t>();
+  if (psw) a.psw = psw->data_ptr<float>();
+  a.T = (int)T; a.B = (int)B; a.mean = mean; a.nnz = nnz; a.key_bits = (int)key_bits;
+  a.grad = grad.data_ptr(); a.grad_bf16 = grad.scalar_type() == at::kBFloat16; a.grad_stride = grad_stride;
+  a.opt = (int)opt;
+  const int64_t rows = W.size(0);
+  if (opt == tdfo::EMB_ROWWISE_ADAGRAD) {
+    TORCH_CHECK(state1 && state1->numel() == rows && state1->scalar_type() == at::kFloat, "rowwise state [rows]");
+  }
+  if (opt == tdfo::EMB_ADAGRAD || opt == tdfo::EMB_ADAM) {
+    TORCH_CHECK(state1 && state1->numel() == rows * D, "state1 [rows, D]");
+  }
+  if (opt == tdfo::EMB_ADAM) TORCH_CHECK(state2 && state2->numel() == rows * D, "state2 [rows, D]");
+  if (opt == tdfo::EMB_DENSE_GRAD) TORCH_CHECK(dense_grad && dense_grad->numel() == rows * D, "dense_grad");
+  if (state1) a.state1 = state1->data_ptr<float>();
+  if (state2) a.state2 = state2->data_ptr<float>();
+  if (dense_grad) a.dense_grad = dense_grad->data_ptr<float>();
+  a.hyper = hyper.data_ptr<float>();
+  a.eps = (float)eps; a.beta1 = (float)beta1; a.beta2 = (float)beta2; a.weight_decay = (float)weight_decay;
+  const size_t ws = tdfo::embedding_bwd_workspace(nnz, (int)D);
+  Tensor work = at::empty({(int64_t)ws}, W.options().dtype(at::kByte));
+  a.workspace = work.data_ptr(); a.workspace_bytes = ws;
+  tdfo::embedding_bwd_fused(a, cur_stream());
+}
+
+// --------------------------------------------------------------- optim
+void dense_optimizer(const Tensor& p, const Tensor& g, const c10::optional<Tensor>& m,
+                     const c10::optional<Tensor>& v, const c10::optional<Tensor>& p_bf16,
+                     int64_t opt, const Tensor& hyper, double beta1, double beta2, double eps,
+                     double wd, double momentum, const c10::optional<Tensor>& found_inf) {
+  check_dev(p, "p"); check_dev(g, "g");
+  TORCH_CHECK(p.scalar_type() == at::kFloat && g.scalar_type() == at::kFloat && p.is_contiguous() &&
+              g.is_contiguous() && p.numel() == g.numel(), "p/g fp32 contiguous same size");
+  TORCH_CHECK(p.numel() % 4 == 0, "flat buffer must be padded to a multiple of 4");
+  TORCH_CHECK(hyper.is_cuda() && hyper.scalar_type() == at::kFloat && hyper.numel() >= 3, "hyper [lr, step, gscale]");
+  tdfo::DenseOptArgs a{};
+  a.p = p.data_ptr<float>(); a.g = g.data_ptr<float>(); a.n = p.numel(); a.opt = (int)opt;
+  const bool need_m = opt == tdfo::OPT_ADAMW || opt == tdfo::OPT_ADAM || opt == tdfo::OPT_ADAGRAD ||
+                      (opt == tdfo::OPT_SGD && momentum != 0.0);
+  if (need_m) { TORCH_CHECK(m && m->numel() == p.numel(), "m state"); a.m = m->data_ptr<float>(); }
+  if (opt == tdfo::OPT_ADAMW || opt == tdfo::OPT_ADAM) {
+    TORCH_CHECK(v && v->numel() == p.numel(), "v state"); a.v = v->data_ptr<float>();
+  }
+  if (p_bf16) { TORCH_CHECK(p_bf16->numel() == p.numel(), "p_bf16 size"); a.p_bf16 = bf16_mut(*p_bf16); }
+  a.hyper = hyper.data_ptr<float>();
+  a.beta1 = (float)beta1; a.beta2 = (float)beta2; a.eps = (float)eps;
+  a.weight_decay = (float)wd; a.momentum = (float)momentum;
+  if (found_inf) a.found_inf = found_inf->data_ptr<float>();
+  tdfo::dense_optimizer(a, cur_stream());
+}
+
+void check_finite(const Tensor& g, const Tensor& found) {
+  check_dev(g, "g");
+  TORCH_CHECK(g.scalar_type() == at::kFloat && g.is_contiguous(), "g fp32");
+  tdfo::check_finite(g.data_ptr<float>(), g.numel(), found.data_ptr<float>(), cur_stream());
+}
+
+void cast_bf16(const Tensor& x, const Tensor& y) {
+  TORCH_CHECK(x.is_contiguous() && y.is_contiguous() && x.numel() == y.numel(), "cast shapes");
+  tdfo::cast_f32_bf16(x.data_ptr<float>(), bf16_mut(y), x.numel(), cur_stream());
+}
+
+// ------------------------------------------------------------ loss etc.
+void head_bce(const Tensor& H, const Tensor& w, const Tensor& b, const Tensor& label,
+              double inv_n, bool relu_mask, const Tensor& logits, const Tensor& dH,
+              const Tensor& part) {
+  check_dev(H, "H"); check_2d_rowmajor(H, "H"); check_2d_rowmajor(dH, "dH");
+  const int64_t B = H.size(0), K = H.size(1);
+  TORCH_CHECK(K == 64 || K == 128 || K == 256 || K == 512 || K == 1024, "head K unsupported");
+  TORCH_CHECK(w.numel() == K && b.numel() == 1 && label.numel() == B && logits.numel() == B, "head shapes");
+  TORCH_CHECK(label.scalar_type() == at::kFloat && logits.scalar_type() == at::kFloat, "head fp32 label/logits");
+  TORCH_CHECK(dH.size(0) == B && dH.size(1) == K, "dH shape");
+  const int nparts = tdfo::head_bce_parts((int)B);
+  TORCH_CHECK(part.numel() >= nparts * (K + 2), "part too small");
+  tdfo::head_bce(bf16_ptr(H), H.stride(0), (int)B, (int)K, w.data_ptr<float>(), b.data_ptr<float>(),
+                 label.data_ptr<float>(), (float)inv_n, relu_mask, logits.data_ptr<float>(),
+                 bf16_mut(dH), dH.stride(0), part.data_ptr<float>(), nparts, cur_stream());
+}
+
+void reduce_rows(const Tensor& inp, int64_t rows, int64_t n, int64_t ld, const Tensor& out,
+                 bool accumulate, double scale) {
+  check_dev(inp, "inp");
+  TORCH_CHECK(inp.scalar_type() == at::kFloat && out.scalar_type() == at::kFloat, "fp32");
+  TORCH_CHECK(inp.numel() >= (rows - 1) * ld + n && out.numel() >= n, "reduce_rows bounds");
+  tdfo::reduce_rows(inp.data_ptr<float>(), (int)rows, n, ld, out.data_ptr<float>(), accumulate,
+                    (float)scale, cur_stream());
+}
+
+void colsum(const Tensor& x, const Tensor& out, bool accumulate) {
+  check_dev(x, "x"); check_2d_rowmajor(x, "x");
+  const int64_t M = x.size(0), N = x.size(1);
+  TORCH_CHECK(N % 8 == 0 && x.stride(0) % 8 == 0 && aligned16(x.data_ptr()), "colsum alignment");
+  TORCH_CHECK(out.numel() == N && out.scalar_type() == at::kFloat, "colsum out");
+  const int np = tdfo::colsum_parts((int)M);
+  Tensor part = at::empty({np, N}, out.options());
+  tdfo::colsum_bf16(bf16_ptr(x), (int)M, (int)N, x.stride(0), part.data_ptr<float>(), np,
+                    out.data_ptr<float>(), accumulate, cur_stream());
+}
+
+void auc_hist(const Tensor& logits, const Tensor& labels, int64_t nb, const Tensor& hist) {
+  TORCH_CHECK(hist.scalar_type() == at::kLong && hist.numel() == 2 * nb, "hist int64 [2*nb]");
+  TORCH_CHECK(logits.numel() == labels.numel(), "auc sizes");
+  tdfo::auc_hist(logits.data_ptr<float>(), labels.data_ptr<float>(), (int)logits.numel(), (int)nb,
+                 reinterpret_cast<unsigned long long*>(hist.data_ptr<int64_t>()), cur_stream());
+}
+
+}  // namespace
+
+TORCH_LIBRARY(tdfo, m) {
+  m.def("gemm(Tensor a, bool a_col, Tensor b, bool b_col, Tensor? bias, bool relu, Tensor? mask, "
+        "Tensor(a!)? out, Tensor(b!)? out32, int splits) -> ()");
+  m.def("interaction_fwd(Tensor dense, Tensor emb, int[] off, int[] stride, int F, int D, Tensor(a!) out) -> ()");
+  m.def("interaction_bwd(Tensor dz, Tensor dense, Tensor emb, int[] off, int[] stride, int F, int D, "
+        "Tensor(a!) d_dense, Tensor(b!) d_emb, int[] doff, int[] dstride, bool relu_mask) -> ()");
+  m.def("embedding_bag_fwd(Tensor W, Tensor row_offset, Tensor indices, Tensor offsets, Tensor out_off, "
+        "Tensor? psw, int T, int B, bool mean, Tensor(a!) out, int out_stride) -> ()");
+  m.def("embedding_bwd(Tensor(a!) W, Tensor row_offset, Tensor indices, Tensor offsets, Tensor grad_off, "
+        "Tensor? psw, int T, int B, bool mean, int key_bits, Tensor grad, int grad_stride, int opt, "
+        "Tensor(b!)? state1, Tensor(c!)? state2, Tensor hyper, float eps, float beta1, float beta2, "
+        "float weight_decay, Tensor(d!)? dense_grad) -> ()");
+  m.def("dense_optimizer(Tensor(a!) p, Tensor g, Tensor(b!)? m, Tensor(c!)? v, Tensor(d!)? p_bf16, int opt, "
+        "Tensor hyper, float beta1, float beta2, float eps, float wd, float momentum, Tensor? found_inf) -> ()");
+  m.def("check_finite(Tensor g, Tensor(a!) found) -> ()");
+  m.def("cast_bf16(Tensor x, Tensor(a!) y) -> ()");
+  m.def("head_bce(Tensor H, Tensor w, Tensor b, Tensor label, float inv_n, bool relu_mask, "
+        "Tensor(a!) logits, Tensor(b!) dH, Tensor(c!) part) -> ()");
+  m.def("reduce_rows(Tensor inp, int rows, int n, int ld, Tensor(a!) out, bool accumulate, float scale) -> ()");
+  m.def("colsum(Tensor x, Tensor(a!) out, bool accumulate) -> ()");
+  m.def("auc_hist(Tensor logits, Tensor labels, int nb, Tensor(a!) hist) -> ()");
+}
+
+TORCH_LIBRARY_IMPL(tdfo, CUDA, m) {
+  m.impl("gemm", gemm);
+  m.impl("interaction_fwd", interaction_fwd);
+  m.impl("interaction_bwd", interaction_bwd);
+  m.impl("embedding_bag_fwd", embedding_bag_fwd);
+  m.impl("embedding_bwd", embedding_bwd);
+  m.impl("dense_optimizer", dense_optimizer);
+  m.impl("check_finite", check_finite);
+  m.impl("cast_bf16", cast_bf16);
+  m.impl("head_bce", head_bce);
+  m.impl("reduce_rows", reduce_rows);
+  m.impl("colsum", colsum);
+  m.impl("auc_hist", auc_hist);
+}

@@ -1,0 +1,66 @@
+// Shared device helpers for the tdfo_amd HIP kernels (gfx950 / CDNA4 only).
+//
+// Conventions used by every kernel in csrc/kernels:
+//   * bf16 tensors are passed as raw uint16_t storage (no torch types in kernels).
+//   * wave = 64 lanes; blocks are multiples of 64 threads.
+//   * launchers are plain C++ functions taking a hipStream_t so they can be
+//     captured in hipGraphs (no allocation / sync inside a launcher).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define TDFO_LDS __attribute__((address_space(3)))
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(4))) short s16x4_t;
+typedef __attribute__((ext_vector_type(8))) short s16x8_t;
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;
+typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+
+namespace tdfo {
+
+__device__ __forceinline__ float bf2f(uint16_t v) {
+  return __uint_as_float(((uint32_t)v) << 16);
+}
+
+// Round-to-nearest-even f32 -> bf16 via the native cast (v_cvt_pk_bf16_f32 on
+// gfx950), which keeps NaN a NaN (MI355X_MICROARCH.md, correctness boundaries).
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(uint16_t, b);
+}
+
+__device__ __forceinline__ uint32_t pack2bf(float a, float b) {
+  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Bijective XCD-aware remap of a 1-D workgroup id (cdna_hip_programming.md §5,
+// "XCD swizzle must be bijective"): consecutive remapped ids land on one XCD,
+// so tiles that share an operand panel share that XCD's L2.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+}  // namespace tdfo
+
+#define TDFO_CHECK_HIP(expr)                                                   \
+  do {                                                                         \
+    hipError_t _e = (expr);                                                    \
+    if (_e != hipSuccess) {                                                    \
+      fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(_e),        \
+              __FILE__, __LINE__);                                             \
+    }                                                                          \
+  } while (0)

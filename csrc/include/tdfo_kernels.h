@@ -1,0 +1,126 @@
+// Host-side launcher API of the tdfo_amd HIP kernels. Included by the torch
+// bindings (csrc/bindings.cpp) and implemented in csrc/kernels/*.hip. Nothing
+// here depends on torch, so kernel files compile in seconds.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace tdfo {
+
+// ---------------------------------------------------------------- GEMM ----
+// C[M,N] = op(A) * op(B), bf16 inputs, fp32 MFMA accumulation.
+//   a_col == 0: A stored [M][K] (K contiguous, row stride lda)
+//   a_col == 1: A stored [K][M] (M contiguous, row stride lda)
+//   b_col == 0: B stored [N][K] (i.e. torch Linear weight layout)
+//   b_col == 1: B stored [K][N]
+// Epilogue (in order): +bias[n] (fp32), relu, *= (mask[m,n] > 0), then store
+// bf16 C and/or fp32 C32 (C32 + z*M*ldc32 for split-K slice z).
+struct GemmArgs {
+  const uint16_t* A; int64_t lda; int a_col;
+  const uint16_t* B; int64_t ldb; int b_col;
+  int M, N, K, splits;
+  const float* bias;
+  int relu;
+  const uint16_t* mask; int64_t ldm;
+  uint16_t* C; int64_t ldc;
+  float* C32; int64_t ldc32;
+};
+void gemm_bf16(const GemmArgs& a, hipStream_t s);
+
+// ------------------------------------------------------ interaction ----
+// DLRM dot interaction over F <= 32 features of width D (one of 16/32/64/128).
+// Feature 0 comes from `dense` ([B, ld_dense]); feature f >= 1 from
+// emb + off[f] + b * stride[f] (element units). Output row b of `out`
+// ([B, ldo]) = [dense_b (D) | tril(X X^T, -1) (F(F-1)/2) | 0 ...].
+struct SlotMap { int64_t off[32]; int64_t stride[32]; };
+void interaction_fwd(const uint16_t* dense, int64_t ld_dense,
+                     const uint16_t* emb, const SlotMap& slots, int F, int D,
+                     int B, uint16_t* out, int64_t ldo, hipStream_t s);
+// Backward: dZ [B, ldz] -> d_emb (same slot layout as forward emb) and
+// d_dense = (passthrough + interaction grad) * (dense > 0 if relu_mask).
+void interaction_bwd(const uint16_t* dz, int64_t ldz, const uint16_t* dense,
+                     int64_t ld_dense, const uint16_t* emb,
+                     const SlotMap& slots, int F, int D, int B,
+                     uint16_t* d_dense, int64_t ld_ddense, uint16_t* d_emb,
+                     const SlotMap& dslots, int relu_mask, hipStream_t s);
+
+// -------------------------------------------------------- embedding ----
+// Table-batched pooled lookup. Bag j = t*B + b (t table, b sample) owns
+// indices[offsets[j] .. offsets[j+1]); table t's rows start at
+// row_offset[t] in the fused weight buffer W ([rows, D] fp32).
+// out + b*out_stride + out_off[t] gets the pooled (sum or mean) row.
+struct EmbFwdArgs {
+  const float* W; int D;
+  const int64_t* row_offset;   // [T] (device)
+  const int64_t* indices;      // [nnz] (device)
+  const int64_t* offsets;      // [T*B+1] (device)
+  const int64_t* out_off;      // [T] (device) element offsets
+  const float* psw;            // per-sample weights [nnz] or null
+  int T, B, mean;
+  int64_t out_stride;
+  void* out; int out_bf16;
+};
+void embedding_bag_fwd(const EmbFwdArgs& a, hipStream_t s);
+
+// Fused backward + optimizer (no float atomics, deterministic):
+//   1. keys = row_offset[t] + index, vals = bag id; radix sort by key;
+//   2. fixed-size chunks of the sorted list segment-reduce grads (fp32);
+//   3. rows whose run crosses a chunk edge are combined in chunk order;
+//   4. the optimizer is applied once per unique row.
+enum EmbOpt { EMB_SGD = 0, EMB_ROWWISE_ADAGRAD = 1, EMB_ADAM = 2,
+              EMB_ADAGRAD = 3, EMB_DENSE_GRAD = 4 };
+struct EmbBwdArgs {
+  float* W; int D;
+  const int64_t* row_offset; const int64_t* indices; const int64_t* offsets;
+  const int64_t* grad_off;     // [T] element offsets into grad
+  const float* psw;
+  int T, B, mean; int64_t nnz; int key_bits;
+  const void* grad; int grad_bf16; int64_t grad_stride;
+  int opt;
+  float* state1; float* state2;  // rowwise: state1[rows]; adam: m, v [rows, D]
+  const float* hyper;          // device: [lr, step]
+  float eps, beta1, beta2, weight_decay;
+  float* dense_grad;           // EMB_DENSE_GRAD: accumulate into [rows, D]
+  void* workspace; size_t workspace_bytes;
+};
+size_t embedding_bwd_workspace(int64_t nnz, int D);
+void embedding_bwd_fused(const EmbBwdArgs& a, hipStream_t s);
+
+// ------------------------------------------------------------ optim ----
+// Flat fused optimizer over one contiguous fp32 parameter buffer.
+enum DenseOpt { OPT_ADAMW = 0, OPT_ADAM = 1, OPT_SGD = 2, OPT_ADAGRAD = 3 };
+struct DenseOptArgs {
+  float* p; const float* g; float* m; float* v; uint16_t* p_bf16;
+  int64_t n; int opt;
+  const float* hyper;   // device: [lr, step, grad_scale]
+  float beta1, beta2, eps, weight_decay, momentum;
+  const float* found_inf;  // optional device flag: skip update if > 0
+};
+void dense_optimizer(const DenseOptArgs& a, hipStream_t s);
+// found_inf[0] = any(!isfinite(g)) over n (caller zeroes it first).
+void check_finite(const float* g, int64_t n, float* found_inf, hipStream_t s);
+void cast_f32_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t s);
+
+// ---------------------------------------------------- loss / reduce ----
+// Fused last layer (K -> 1) + sigmoid BCE-with-logits + backward:
+//   logit = H.w + b; loss partials; dlogit = (sigmoid(logit) - y) * inv_n
+//   dH = dlogit * w * (H > 0 if relu_mask) ; partials of dw, db.
+// part: [gridDim, K + 2] fp32 rows = [dw (K) | db | loss_sum].
+void head_bce(const uint16_t* H, int64_t ldh, int B, int K, const float* w,
+              const float* b, const float* label, float inv_n, int relu_mask,
+              float* logits, uint16_t* dH, int64_t lddh, float* part,
+              int nparts, hipStream_t s);
+int head_bce_parts(int B);
+// out[j] (=|+=) sum_r in[r*ld + j], j < n, fixed order (deterministic).
+void reduce_rows(const float* in, int rows, int64_t n, int64_t ld, float* out,
+                 int accumulate, float scale, hipStream_t s);
+// out[n] = sum_m x[m, n] (bf16 in). part must hold parts(M)*N floats.
+void colsum_bf16(const uint16_t* x, int M, int N, int64_t ldx, float* part,
+                 int nparts, float* out, int accumulate, hipStream_t s);
+int colsum_parts(int M);
+// AUC histogram: hist[2*nb]: [neg counts | pos counts] of sigmoid(logit)
+// bucketed uniformly on [0, 1] (tf.keras.metrics.AUC-style thresholds).
+void auc_hist(const float* logits, const float* labels, int n, int nb,
+              unsigned long long* hist, hipStream_t s);
+
+}  // namespace tdfo

@@ -1,0 +1,216 @@
+// bf16 MFMA GEMM with fused epilogue for the DLRM / DCN-v2 / tower MLPs.
+//
+// One kernel template covers the three products of a Linear layer without
+// ever materialising a transposed copy:
+//   forward  y  = x  W^T   A=[M][K] (a_col=0)  B=W [N][K]   (b_col=0)
+//   dgrad    dx = dy W     A=[M][K] (a_col=0)  B=W as [K][N] (b_col=1)
+//   wgrad    dW = dy^T x   A=dy as [K][M] (a_col=1) B=x as [K][N] (b_col=1)
+// "col" operands are staged row-linear into LDS and read as MFMA fragments
+// with the gfx950 transposing LDS read ds_read_b64_tr_b16
+// (cdna_hip_programming.md §5.5 T10); "row" operands are read with
+// ds_read_b128. Both LDS images are XOR-swizzled on the *global source*
+// address (glds writes lane-linear, rule 21) so every fragment read is
+// bank-conflict free (swizzles checked against the lane groups of
+// MI355X_MICROARCH.md §LDS).
+//
+// Tile 128x128x64, 256 threads = 4 waves in 2x2, each wave 64x64 = 4x4
+// v_mfma_f32_16x16x32_bf16 tiles. Operands are staged with
+// global_load_lds_dwordx4 into a 2-deep LDS ring (64 KiB) so the next
+// K-tile's loads overlap this tile's MFMAs. Block ids are XCD-remapped.
+// Split-K (gridDim.z) writes fp32 slabs reduced by reduce_rows().
+#include "tdfo_common.h"
+#include "tdfo_kernels.h"
+
+namespace tdfo {
+namespace {
+
+constexpr int BM = 128, BN = 128, BK = 64;
+constexpr int TILE_BYTES = BM * BK * 2;            // 16 KiB per operand
+constexpr int STAGE_BYTES = 2 * TILE_BYTES;        // A + B
+constexpr int SMEM_BYTES = 2 * STAGE_BYTES;        // double buffered
+
+typedef __attribute__((address_space(1))) const void* gptr_t;
+
+__device__ __forceinline__ void glds16(const void* src, TDFO_LDS char* dst) {
+  __builtin_amdgcn_global_load_lds((gptr_t)src, (TDFO_LDS void*)dst, 16, 0, 0);
+}
+
+// swizzle of the 16-B chunk index for [k][128] (256-B row) images, chosen so
+// the tr-read pattern below touches 32 distinct 8-B slots per half-wave.
+__device__ __forceinline__ int swz_col(int k) {
+  return ((k & 3) | (((k >> 3) & 1) << 2)) << 1;
+}
+
+// Stage a [128 rows][64 k] tile of a row operand (K contiguous).
+__device__ __forceinline__ void stage_row(const uint16_t* g, int64_t ld,
+                                          int row0, int rows, int k0,
+                                          TDFO_LDS char* tile, int w, int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int ii = w * 4 + i;
+    const int r = ii * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ (r & 7);
+    int gr = row0 + r;
+    gr = gr < rows ? gr : rows - 1;
+    glds16(g + (int64_t)gr * ld + k0 + c * 8, tile + ii * 1024);
+  }
+}
+
+// Stage a [64 k][128 cols] tile of a col operand (M/N contiguous).
+__device__ __forceinline__ void stage_col(const uint16_t* g, int64_t ld,
+                                          int col0, int cols, int k0,
+                                          TDFO_LDS char* tile, int w, int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int ii = w * 4 + i;
+    const int kr = ii * 4 + (lane >> 4);
+    const int c = (lane & 15) ^ swz_col(kr);
+    int gc = col0 + c * 8;
+    gc = gc <= cols - 8 ? gc : cols - 8;
+    glds16(g + (int64_t)(k0 + kr) * ld + gc, tile + ii * 1024);
+  }
+}
+
+// MFMA operand fragment (16 rows x 32 k) of a row image: lane l holds
+// row r0 + (l&15), k = 32*ks + 8*(l>>4) + j.
+__device__ __forceinline__ bf16x8_t frag_row(const TDFO_LDS char* tile, int r0,
+                                             int ks, int lane) {
+  const int r = r0 + (lane & 15);
+  const int c = (ks * 4 + (lane >> 4)) ^ (r & 7);
+  return *(const TDFO_LDS bf16x8_t*)(tile + r * 128 + c * 16);
+}
+
+// Same fragment from a [k][128] col image via two transposing reads: the
+// 16-lane group g = l>>4 reads rows k0..k0+3 (k0 = 32ks + 8g + 4h) x 16 cols;
+// lane 4q+p supplies row q, cols 4p..4p+3 and receives column (l&15).
+__device__ __forceinline__ bf16x8_t frag_col(const TDFO_LDS char* tile, int c0,
+                                             int ks, int lane) {
+  const int i = lane & 15, g = lane >> 4;
+  const int q = i >> 2, p = i & 3;
+  const int m = c0 + 4 * p;
+  s16x4_t v[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int k = ks * 32 + 8 * g + 4 * h + q;
+    const int off = k * 256 + (((m >> 3) ^ swz_col(k)) << 4) + ((m & 7) << 1);
+    v[h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (TDFO_LDS s16x4_t*)(tile + off));
+  }
+  s16x8_t r = {v[0][0], v[0][1], v[0][2], v[0][3],
+               v[1][0], v[1][1], v[1][2], v[1][3]};
+  return __builtin_bit_cast(bf16x8_t, r);
+}
+
+template <bool A_COL, bool B_COL>
+__global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  TDFO_LDS char* smem = (TDFO_LDS char*)smem_raw;
+
+  const int tiles_m = (p.M + BM - 1) / BM, tiles_n = (p.N + BN - 1) / BN;
+  const int wg = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int tm = wg / tiles_n, tn = wg - tm * tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int ktiles = p.K / BK;
+  const int per = (ktiles + p.splits - 1) / p.splits;
+  const int kt0 = blockIdx.z * per;
+  const int kt1 = min(ktiles, kt0 + per);
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wr = w >> 1, wc = w & 1;
+
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  auto stage = [&](int buf, int kt) {
+    TDFO_LDS char* ta = smem + buf * STAGE_BYTES;
+    TDFO_LDS char* tb = ta + TILE_BYTES;
+    const int k0 = kt * BK;
+    if (A_COL) stage_col(p.A, p.lda, m0, p.M, k0, ta, w, lane);
+    else       stage_row(p.A, p.lda, m0, p.M, k0, ta, w, lane);
+    if (B_COL) stage_col(p.B, p.ldb, n0, p.N, k0, tb, w, lane);
+    else       stage_row(p.B, p.ldb, n0, p.N, k0, tb, w, lane);
+  };
+
+  if (kt0 < kt1) {
+    stage(0, kt0);
+    __syncthreads();
+    int cur = 0;
+    for (int kt = kt0; kt < kt1; ++kt) {
+      if (kt + 1 < kt1) stage(cur ^ 1, kt + 1);
+      const TDFO_LDS char* ta = smem + cur * STAGE_BYTES;
+      const TDFO_LDS char* tb = ta + TILE_BYTES;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        bf16x8_t af[4], bfr[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          af[i] = A_COL ? frag_col(ta, wr * 64 + i * 16, ks, lane)
+                        : frag_row(ta, wr * 64 + i * 16, ks, lane);
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          bfr[j] = B_COL ? frag_col(tb, wc * 64 + j * 16, ks, lane)
+                         : frag_row(tb, wc * 64 + j * 16, ks, lane);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j],
+                                                                acc[i][j], 0, 0, 0);
+      }
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+
+  // Epilogue. C/D map of 16x16x32: col = lane&15, row = 4*(lane>>4) + reg.
+  float* c32 = p.C32 ? p.C32 + (int64_t)blockIdx.z * p.M * p.ldc32 : nullptr;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int n = n0 + wc * 64 + j * 16 + (lane & 15);
+    if (n >= p.N) continue;
+    const float bias = p.bias ? p.bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wr * 64 + i * 16 + 4 * (lane >> 4) + r;
+        if (m >= p.M) continue;
+        float v = acc[i][j][r] + bias;
+        if (p.relu) v = fmaxf(v, 0.f);
+        if (p.mask && !(bf2f(p.mask[(int64_t)m * p.ldm + n]) > 0.f)) v = 0.f;
+        if (p.C) p.C[(int64_t)m * p.ldc + n] = f2bf(v);
+        if (c32) c32[(int64_t)m * p.ldc32 + n] = v;
+      }
+    }
+  }
+}
+
+template <bool AC, bool BC>
+void launch(const GemmArgs& a, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    TDFO_CHECK_HIP(hipFuncSetAttribute((const void*)gemm_kernel<AC, BC>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       SMEM_BYTES));
+    attr = true;
+  }
+  const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  dim3 grid(tiles, 1, a.splits);
+  hipLaunchKernelGGL((gemm_kernel<AC, BC>), grid, dim3(256), SMEM_BYTES, s, a);
+}
+
+}  // namespace
+
+void gemm_bf16(const GemmArgs& a, hipStream_t s) {
+  if (a.a_col) {
+    if (a.b_col) launch<true, true>(a, s); else launch<true, false>(a, s);
+  } else {
+    if (a.b_col) launch<false, true>(a, s); else launch<false, false>(a, s);
+  }
+}
+
+}  // namespace tdfo

@@ -1,0 +1,248 @@
+// DLRM pairwise-dot feature interaction on MFMA (K24 in SURVEY.md §2.3).
+//
+// Forward, one wave per sample: the sample's F<=32 feature rows X [F, D] are
+// loaded straight into registers in the operand layout of
+// v_mfma_f32_32x32x16_bf16 (lane l: row l&31, k = 8*(l>>5)+j). Because
+// Z = X X^T uses X as both A and B, the same registers feed both operands:
+// D/16 MFMAs produce the 32x32 Gram matrix with no LDS traffic. The strict
+// lower triangle is packed through a per-wave LDS row so the output row
+// [dense | tril | 0-pad] leaves with one 16-B store per lane.
+//
+// Backward, one wave per sample: dX = S X with S the symmetric matrix built
+// from dZ. S comes from an LDS copy of the dZ row; X is staged in LDS and
+// read as the MFMA B operand with ds_read_b64_tr_b16 (k = feature index).
+// The concat passthrough (dZ[:, :D]) and the bottom-MLP ReLU mask are fused
+// into the dense-slot store, and embedding-slot gradients are written
+// directly in the layout the embedding backward / all-to-all consumes.
+//
+// Feature rows are addressed through a SlotMap so the kernels read the
+// pooled embeddings in place from the all-to-all receive buffer (no permute).
+#include "tdfo_common.h"
+#include "tdfo_kernels.h"
+
+namespace tdfo {
+namespace {
+
+constexpr int WAVES = 4;
+
+__device__ __forceinline__ const uint16_t* feat_row(const uint16_t* dense,
+                                                    int64_t ld_dense,
+                                                    const uint16_t* emb,
+                                                    const SlotMap& sm, int i,
+                                                    int F, int b) {
+  if (i >= F) return nullptr;
+  if (i == 0) return dense + (int64_t)b * ld_dense;
+  return emb + sm.off[i] + (int64_t)b * sm.stride[i];
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void inter_fwd_kernel(
+    const uint16_t* __restrict__ dense, int64_t ld_dense,
+    const uint16_t* __restrict__ emb, SlotMap sm, int F, int B,
+    uint16_t* __restrict__ out, int64_t ldo) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  uint16_t* row = (uint16_t*)smem_raw + w * ldo;
+  constexpr int KS = D / 16;
+  const int P = F * (F - 1) / 2;
+  // zero the pad tail once; it is never overwritten
+  for (int e = D + P + lane; e < ldo; e += 64) row[e] = 0;
+
+  const int i = lane & 31, h = lane >> 5;
+  const int iters = (B + gridDim.x * WAVES - 1) / (gridDim.x * WAVES);
+  for (int it = 0; it < iters; ++it) {
+    const int b = (it * gridDim.x + blockIdx.x) * WAVES + w;
+    const bool valid = b < B;
+    if (valid) {
+      const uint16_t* rp = feat_row(dense, ld_dense, emb, sm, i, F, b);
+      bf16x8_t fr[KS];
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        if (rp) fr[s] = *(const bf16x8_t*)(rp + 16 * s + 8 * h);
+        else    fr[s] = __builtin_bit_cast(bf16x8_t, (s16x8_t){0,0,0,0,0,0,0,0});
+      }
+      f32x16_t acc = {};
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fr[s], fr[s], acc, 0, 0, 0);
+      // dense passthrough into LDS row
+      const uint16_t* dp = dense + (int64_t)b * ld_dense;
+      for (int c = lane; c < D / 8; c += 64)
+        *(uint4*)(row + c * 8) = *(const uint4*)(dp + c * 8);
+      const int col = lane & 31;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int rr = (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (rr < F && col < rr) row[D + rr * (rr - 1) / 2 + col] = f2bf(acc[r]);
+      }
+    }
+    __syncthreads();
+    if (valid) {
+      uint16_t* op = out + (int64_t)b * ldo;
+      for (int c = lane; c < ldo / 8; c += 64)
+        *(uint4*)(op + c * 8) = *(const uint4*)(row + c * 8);
+    }
+    __syncthreads();
+  }
+}
+
+// swizzle (16-B chunk xor) of the X image rows for conflict-free tr reads
+template <int D>
+__device__ __forceinline__ int xswz(int j) {
+  return (D >= 128) ? ((j & 3) << 2) : 0;
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void inter_bwd_kernel(
+    const uint16_t* __restrict__ dz, int64_t ldz,
+    const uint16_t* __restrict__ dense, int64_t ld_dense,
+    const uint16_t* __restrict__ emb, SlotMap sm, int F, int B,
+    uint16_t* __restrict__ d_dense, int64_t ld_ddense,
+    uint16_t* __restrict__ d_emb, SlotMap dsm, int relu_mask) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  constexpr int XB = 32 * D * 2;  // X image bytes per wave
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int ldz_al = (int)((ldz + 7) & ~7LL);
+  char* base = smem_raw + w * (XB + ldz_al * 2);
+  char* xs = base;
+  uint16_t* zrow = (uint16_t*)(base + XB);
+  constexpr int CPR = D / 8;  // 16-B chunks per X row
+  const int h = lane >> 5;
+
+  // rows >= F of the image stay zero for every sample
+  for (int c = lane; c < 32 * CPR; c += 64) {
+    const int j = c / CPR;
+    if (j >= F) *(uint4*)(xs + c * 16) = make_uint4(0, 0, 0, 0);
+  }
+
+  const int iters = (B + gridDim.x * WAVES - 1) / (gridDim.x * WAVES);
+  for (int it = 0; it < iters; ++it) {
+    const int b = (it * gridDim.x + blockIdx.x) * WAVES + w;
+    const bool valid = b < B;
+    if (valid) {
+      const uint16_t* zp = dz + (int64_t)b * ldz;
+      for (int c = lane; c < ldz_al / 8; c += 64) {
+        if (c * 8 + 8 <= ldz) *(uint4*)(zrow + c * 8) = *(const uint4*)(zp + c * 8);
+        else for (int e = c * 8; e < ldz_al; ++e) zrow[e] = e < ldz ? zp[e] : 0;
+      }
+      for (int c = lane; c < F * CPR; c += 64) {
+        const int j = c / CPR, ch = c - j * CPR;
+        const uint16_t* rp = feat_row(dense, ld_dense, emb, sm, j, F, b);
+        *(uint4*)(xs + j * D * 2 + ((ch ^ xswz<D>(j)) << 4)) =
+            *(const uint4*)(rp + ch * 8);
+      }
+    }
+    __syncthreads();
+    if (valid) {
+      // A operand: S[i][k], i = lane&31, k = 16ks + 8h + jj
+      const int i = lane & 31;
+      bf16x8_t sa[2];
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        s16x8_t t;
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+          const int k = 16 * ks + 8 * h + jj;
+          uint16_t v = 0;
+          if (i < F && k < F && i != k) {
+            const int hi = i > k ? i : k, lo = i > k ? k : i;
+            v = zrow[D + hi * (hi - 1) / 2 + lo];
+          }
+          t[jj] = (short)v;
+        }
+        sa[ks] = __builtin_bit_cast(bf16x8_t, t);
+      }
+      const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
+#pragma unroll
+      for (int nt = 0; nt < D / 32; ++nt) {
+        f32x16_t acc = {};
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          s16x4_t v[2];
+#pragma unroll
+          for (int hf = 0; hf < 2; ++hf) {
+            const int j = 16 * ks + 8 * (g >> 1) + 4 * hf + q;
+            const int d = 32 * nt + 16 * (g & 1) + 4 * pp;
+            const int off = j * D * 2 + (((d >> 3) ^ xswz<D>(j)) << 4) + ((d & 7) << 1);
+            v[hf] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((TDFO_LDS s16x4_t*)(
+                (TDFO_LDS char*)xs + off));
+          }
+          s16x8_t bb = {v[0][0], v[0][1], v[0][2], v[0][3],
+                        v[1][0], v[1][1], v[1][2], v[1][3]};
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+              sa[ks], __builtin_bit_cast(bf16x8_t, bb), acc, 0, 0, 0);
+        }
+        const int d = 32 * nt + (lane & 31);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int ii = (r & 3) + 8 * (r >> 2) + 4 * h;
+          if (ii >= F) continue;
+          float val = acc[r];
+          if (ii == 0) {
+            val += bf2f(zrow[d]);
+            if (relu_mask) {
+              const uint16_t xv = *(const uint16_t*)(xs + (((d >> 3) ^ xswz<D>(0)) << 4) + ((d & 7) << 1));
+              if (!(bf2f(xv) > 0.f)) val = 0.f;
+            }
+            d_dense[(int64_t)b * ld_ddense + d] = f2bf(val);
+          } else {
+            d_emb[dsm.off[ii] + (int64_t)b * dsm.stride[ii] + d] = f2bf(val);
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+int grid_for(int B) {
+  int waves = (B + WAVES - 1) / WAVES;
+  return waves < 2048 ? waves : 2048;
+}
+
+}  // namespace
+
+void interaction_fwd(const uint16_t* dense, int64_t ld_dense,
+                     const uint16_t* emb, const SlotMap& slots, int F, int D,
+                     int B, uint16_t* out, int64_t ldo, hipStream_t s) {
+  if (B <= 0) return;
+  const size_t smem = (size_t)WAVES * ldo * 2;
+  dim3 grid(grid_for(B));
+#define TDFO_IFWD(DD)                                                          \
+  hipLaunchKernelGGL(inter_fwd_kernel<DD>, grid, dim3(256), smem, s, dense,    \
+                     ld_dense, emb, slots, F, B, out, ldo)
+  switch (D) {
+    case 32: TDFO_IFWD(32); break;
+    case 64: TDFO_IFWD(64); break;
+    case 128: TDFO_IFWD(128); break;
+    case 256: TDFO_IFWD(256); break;
+  }
+#undef TDFO_IFWD
+}
+
+void interaction_bwd(const uint16_t* dz, int64_t ldz, const uint16_t* dense,
+                     int64_t ld_dense, const uint16_t* emb,
+                     const SlotMap& slots, int F, int D, int B,
+                     uint16_t* d_dense, int64_t ld_ddense, uint16_t* d_emb,
+                     const SlotMap& dslots, int relu_mask, hipStream_t s) {
+  if (B <= 0) return;
+  const int ldz_al = (int)((ldz + 7) & ~7LL);
+  const size_t smem = (size_t)WAVES * (32 * D * 2 + ldz_al * 2);
+  dim3 grid(grid_for(B));
+#define TDFO_IBWD(DD)                                                          \
+  if (smem > 65536)                                                            \
+    TDFO_CHECK_HIP(hipFuncSetAttribute((const void*)inter_bwd_kernel<DD>,      \
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem));               \
+  hipLaunchKernelGGL(inter_bwd_kernel<DD>, grid, dim3(256), smem, s, dz, ldz,  \
+                     dense, ld_dense, emb, slots, F, B, d_dense, ld_ddense,    \
+                     d_emb, dslots, relu_mask)
+  switch (D) {
+    case 32: TDFO_IBWD(32); break;
+    case 64: TDFO_IBWD(64); break;
+    case 128: TDFO_IBWD(128); break;
+    case 256: TDFO_IBWD(256); break;
+  }
+#undef TDFO_IBWD
+}
+
+}  // namespace tdfo

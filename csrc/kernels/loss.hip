@@ -1,0 +1,178 @@
+// Loss head, deterministic reductions and the device-side AUC histogram.
+//
+// head_bce fuses the final K->1 layer, sigmoid BCE-with-logits (K5), its
+// gradient, the ReLU mask of the layer below and the partial sums of dW/db:
+// one pass over H produces everything the backward needs (the reference runs
+// these as separate XLA / torch ops: jax-flax/train.py:35, torchrec-style
+// BCE). Cross-sample sums go to per-block fp32 partial rows that
+// reduce_rows() adds in a fixed order, so gradients are bitwise reproducible.
+// auc_hist replaces the host-side tf.keras AUC of jax-flax/train_dp.py:215
+// (a per-step device->host sync) with on-device counts.
+#include "tdfo_common.h"
+#include "tdfo_kernels.h"
+
+namespace tdfo {
+namespace {
+
+constexpr int HEAD_SPB = 64;  // samples per block
+
+template <int K>
+__global__ __launch_bounds__(256) void head_bce_kernel(
+    const uint16_t* __restrict__ H, int64_t ldh, int B,
+    const float* __restrict__ w, const float* __restrict__ bptr,
+    const float* __restrict__ label, float inv_n, int relu_mask,
+    float* __restrict__ logits, uint16_t* __restrict__ dH, int64_t lddh,
+    float* __restrict__ part) {
+  constexpr int EPL = K / 64;
+  __shared__ float red[4][K + 2];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int e0 = lane * EPL;
+  float wr[EPL], dw[EPL];
+#pragma unroll
+  for (int u = 0; u < EPL; ++u) { wr[u] = w[e0 + u]; dw[u] = 0.f; }
+  const float bias = bptr[0];
+  float db = 0.f, lsum = 0.f;
+  const int s0 = blockIdx.x * HEAD_SPB;
+  for (int si = wv; si < HEAD_SPB; si += 4) {
+    const int s = s0 + si;
+    if (s >= B) break;
+    const uint16_t* hp = H + (int64_t)s * ldh + e0;
+    float hv[EPL];
+#pragma unroll
+    for (int u = 0; u < EPL; ++u) hv[u] = bf2f(hp[u]);
+    float d = 0.f;
+#pragma unroll
+    for (int u = 0; u < EPL; ++u) d += hv[u] * wr[u];
+    const float x = wave_sum(d) + bias;
+    const float y = label[s];
+    const float sig = 1.f / (1.f + __expf(-x));
+    const float g = (sig - y) * inv_n;
+    if (lane == 0) {
+      logits[s] = x;
+      lsum += fmaxf(x, 0.f) - x * y + log1pf(__expf(-fabsf(x)));
+      db += g;
+    }
+    uint16_t* dp = dH + (int64_t)s * lddh + e0;
+#pragma unroll
+    for (int u = 0; u < EPL; ++u) {
+      float gh = g * wr[u];
+      if (relu_mask && !(hv[u] > 0.f)) gh = 0.f;
+      dp[u] = f2bf(gh);
+      dw[u] += g * hv[u];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < EPL; ++u) red[wv][e0 + u] = dw[u];
+  if (lane == 0) { red[wv][K] = db; red[wv][K + 1] = lsum; }
+  __syncthreads();
+  for (int j = threadIdx.x; j < K + 2; j += 256)
+    part[(int64_t)blockIdx.x * (K + 2) + j] =
+        red[0][j] + red[1][j] + red[2][j] + red[3][j];
+}
+
+__global__ void reduce_rows_kernel(const float* __restrict__ in, int rows,
+                                   int64_t n, int64_t ld, float* __restrict__ out,
+                                   int accumulate, float scale) {
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n;
+       j += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int r = 0; r < rows; ++r) s += in[(int64_t)r * ld + j];
+    s *= scale;
+    out[j] = accumulate ? out[j] + s : s;
+  }
+}
+
+constexpr int COLSUM_RPB = 64;
+
+__global__ __launch_bounds__(256) void colsum_kernel(const uint16_t* __restrict__ x,
+                                                     int M, int N, int64_t ldx,
+                                                     float* __restrict__ part) {
+  const int c0 = (blockIdx.x * 256 + threadIdx.x) * 8;
+  if (c0 >= N) return;
+  const int r0 = blockIdx.y * COLSUM_RPB;
+  const int r1 = min(M, r0 + COLSUM_RPB);
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int r = r0; r < r1; ++r) {
+    const uint4 v = *(const uint4*)(x + (int64_t)r * ldx + c0);
+    const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      acc[2 * q] += bf2f((uint16_t)(u[q] & 0xffff));
+      acc[2 * q + 1] += bf2f((uint16_t)(u[q] >> 16));
+    }
+  }
+  float* pp = part + (int64_t)blockIdx.y * N + c0;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) pp[q] = acc[q];
+}
+
+__global__ __launch_bounds__(256) void auc_hist_kernel(
+    const float* __restrict__ logits, const float* __restrict__ labels, int n,
+    int nb, unsigned long long* __restrict__ hist) {
+  extern __shared__ unsigned int lh[];
+  for (int i = threadIdx.x; i < 2 * nb; i += 256) lh[i] = 0;
+  __syncthreads();
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const float p = 1.f / (1.f + __expf(-logits[i]));
+    int bkt = (int)(p * nb);
+    bkt = bkt < 0 ? 0 : (bkt >= nb ? nb - 1 : bkt);
+    atomicAdd(&lh[(labels[i] > 0.5f ? nb : 0) + bkt], 1u);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2 * nb; i += 256)
+    if (lh[i]) atomicAdd(&hist[i], (unsigned long long)lh[i]);
+}
+
+}  // namespace
+
+int head_bce_parts(int B) { return (B + HEAD_SPB - 1) / HEAD_SPB; }
+
+void head_bce(const uint16_t* H, int64_t ldh, int B, int K, const float* w,
+              const float* b, const float* label, float inv_n, int relu_mask,
+              float* logits, uint16_t* dH, int64_t lddh, float* part,
+              int nparts, hipStream_t s) {
+  if (B <= 0) return;
+  dim3 grid(nparts);
+#define TDFO_HB(KK)                                                            \
+  hipLaunchKernelGGL(head_bce_kernel<KK>, grid, dim3(256), 0, s, H, ldh, B, w, \
+                     b, label, inv_n, relu_mask, logits, dH, lddh, part)
+  switch (K) {
+    case 64: TDFO_HB(64); break;
+    case 128: TDFO_HB(128); break;
+    case 256: TDFO_HB(256); break;
+    case 512: TDFO_HB(512); break;
+    case 1024: TDFO_HB(1024); break;
+  }
+#undef TDFO_HB
+}
+
+void reduce_rows(const float* in, int rows, int64_t n, int64_t ld, float* out,
+                 int accumulate, float scale, hipStream_t s) {
+  if (n <= 0) return;
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3(blocks), dim3(256), 0, s, in,
+                     rows, n, ld, out, accumulate, scale);
+}
+
+int colsum_parts(int M) { return (M + COLSUM_RPB - 1) / COLSUM_RPB; }
+
+void colsum_bf16(const uint16_t* x, int M, int N, int64_t ldx, float* part,
+                 int nparts, float* out, int accumulate, hipStream_t s) {
+  if (M <= 0 || N <= 0) return;
+  dim3 grid((N / 8 + 255) / 256, nparts);
+  hipLaunchKernelGGL(colsum_kernel, grid, dim3(256), 0, s, x, M, N, ldx, part);
+  reduce_rows(part, nparts, N, N, out, accumulate, 1.f, s);
+}
+
+void auc_hist(const float* logits, const float* labels, int n, int nb,
+              unsigned long long* hist, hipStream_t s) {
+  if (n <= 0) return;
+  int blocks = (n + 255) / 256;
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(auc_hist_kernel, dim3(blocks), dim3(256),
+                     (size_t)2 * nb * sizeof(unsigned int), s, logits, labels,
+                     n, nb, hist);
+}
+
+}  // namespace tdfo

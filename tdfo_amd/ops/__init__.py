@@ -1,0 +1,161 @@
+"""Device-dispatching functional ops.
+
+GPU tensors -> hand-written HIP kernels (``torch.ops.tdfo``, must be built);
+CPU tensors -> fp32 torch references (``tdfo_amd.ops.reference``). All ops
+are out-variants so engines can preallocate buffers and capture hipGraphs.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import reference as ref
+from ._ext import available as native_available  # noqa: F401
+from ._ext import ops as _native
+from .reference import (EMB_ADAGRAD, EMB_ADAM, EMB_DENSE_GRAD, EMB_ROWWISE_ADAGRAD,  # noqa: F401
+                        EMB_SGD, OPT_ADAGRAD, OPT_ADAM, OPT_ADAMW, OPT_SGD, key_bits_for)
+
+
+def _gpu(t: torch.Tensor) -> bool:
+    return t.is_cuda
+
+
+def gemm(a, a_col, b, b_col, bias=None, relu=False, mask=None, out=None, out32=None, splits=1):
+    if _gpu(a):
+        _native().gemm(a, a_col, b, b_col, bias, relu, mask, out, out32, splits)
+    else:
+        ref.gemm(a, a_col, b, b_col, bias, relu, mask, out, out32, splits)
+
+
+def linear_fwd(x, w, bias=None, relu=False, out=None):
+    """out = act(x @ w^T + bias); x [M,K] bf16, w [N,K] bf16."""
+    if out is None:
+        out = torch.empty(x.shape[0], w.shape[0], dtype=torch.bfloat16, device=x.device)
+    gemm(x, False, w, False, bias, relu, None, out, None, 1)
+    return out
+
+
+def linear_dgrad(dy, w, mask=None, out=None):
+    """out = (dy @ w) * (mask > 0); dy [M,N], w [N,K]."""
+    if out is None:
+        out = torch.empty(dy.shape[0], w.shape[1], dtype=torch.bfloat16, device=dy.device)
+    gemm(dy, False, w, True, None, False, mask, out, None, 1)
+    return out
+
+
+def wgrad_splits(M: int, N: int, K: int, target_blocks: int = 512) -> int:
+    tiles = ((M + 127) // 128) * ((N + 127) // 128)
+    kt = K // 64
+    s = max(1, min(kt // 2 if kt >= 2 else 1, -(-target_blocks // tiles)))
+    return s
+
+
+def linear_wgrad(dy, x, out, slab=None, splits=None, accumulate=False):
+    """out[N,K] (fp32) = dy^T @ x with dy [M,N], x [M,K]; split-K over M."""
+    N, K, M = dy.shape[1], x.shape[1], dy.shape[0]
+    if splits is None:
+        splits = wgrad_splits(N, K, M)
+    if splits == 1 and not accumulate:
+        gemm(dy, True, x, True, None, False, None, None, out, 1)
+        return out
+    if slab is None:
+        slab = torch.empty(splits * N * K, dtype=torch.float32, device=dy.device)
+    gemm(dy, True, x, True, None, False, None, None, slab, splits)
+    reduce_rows(slab, splits, N * K, N * K, out, accumulate, 1.0)
+    return out
+
+
+def interaction_fwd(dense, emb, off, stride, F, D, out):
+    if _gpu(dense):
+        _native().interaction_fwd(dense, emb, list(off), list(stride), F, D, out)
+    else:
+        ref.interaction_fwd(dense, emb, off, stride, F, D, out)
+
+
+def interaction_bwd(dz, dense, emb, off, stride, F, D, d_dense, d_emb, doff, dstride, relu_mask):
+    if _gpu(dz):
+        _native().interaction_bwd(dz, dense, emb, list(off), list(stride), F, D, d_dense, d_emb,
+                                  list(doff), list(dstride), relu_mask)
+    else:
+        ref.interaction_bwd(dz, dense, emb, off, stride, F, D, d_dense, d_emb, doff, dstride,
+                            relu_mask)
+
+
+def embedding_bag_fwd(W, row_offset, indices, offsets, out_off, T, B, out, out_stride, mean=False,
+                      psw=None):
+    if _gpu(W):
+        _native().embedding_bag_fwd(W, row_offset, indices, offsets, out_off, psw, T, B, mean, out,
+                                    out_stride)
+    else:
+        ref.embedding_bag_fwd(W, row_offset, indices, offsets, out_off, psw, T, B, mean, out,
+                              out_stride)
+
+
+def embedding_bwd(W, row_offset, indices, offsets, grad_off, T, B, grad, grad_stride, opt, hyper,
+                  state1=None, state2=None, eps=1e-8, beta1=0.9, beta2=0.999, weight_decay=0.0,
+                  key_bits=None, mean=False, psw=None, dense_grad=None):
+    if key_bits is None:
+        key_bits = key_bits_for(W.shape[0])
+    if _gpu(W):
+        _native().embedding_bwd(W, row_offset, indices, offsets, grad_off, psw, T, B, mean,
+                                key_bits, grad, grad_stride, opt, state1, state2, hyper, eps,
+                                beta1, beta2, weight_decay, dense_grad)
+    else:
+        ref.embedding_bwd(W, row_offset, indices, offsets, grad_off, psw, T, B, mean, key_bits,
+                          grad, grad_stride, opt, state1, state2, hyper, eps, beta1, beta2,
+                          weight_decay, dense_grad)
+
+
+def dense_optimizer(p, g, m, v, p_bf16, opt, hyper, beta1=0.9, beta2=0.999, eps=1e-8, wd=0.0,
+                    momentum=0.0, found_inf=None):
+    if _gpu(p):
+        _native().dense_optimizer(p, g, m, v, p_bf16, opt, hyper, beta1, beta2, eps, wd, momentum,
+                                  found_inf)
+    else:
+        ref.dense_optimizer(p, g, m, v, p_bf16, opt, hyper, beta1, beta2, eps, wd, momentum,
+                            found_inf)
+
+
+def check_finite(g, found):
+    if _gpu(g):
+        _native().check_finite(g, found)
+    else:
+        ref.check_finite(g, found)
+
+
+def head_parts(B: int) -> int:
+    return (B + 63) // 64
+
+
+def head_bce(H, w, b, label, inv_n, relu_mask, logits, dH, part):
+    if _gpu(H):
+        _native().head_bce(H, w, b, label, inv_n, relu_mask, logits, dH, part)
+    else:
+        ref.head_bce(H, w, b, label, inv_n, relu_mask, logits, dH, part)
+
+
+def reduce_rows(inp, rows, n, ld, out, accumulate=False, scale=1.0):
+    if _gpu(inp):
+        _native().reduce_rows(inp, rows, n, ld, out, accumulate, scale)
+    else:
+        ref.reduce_rows(inp, rows, n, ld, out, accumulate, scale)
+
+
+def colsum(x, out, accumulate=False):
+    if _gpu(x):
+        _native().colsum(x, out, accumulate)
+    else:
+        ref.colsum(x, out, accumulate)
+
+
+def auc_hist(logits, labels, nb, hist):
+    if _gpu(logits):
+        _native().auc_hist(logits, labels, nb, hist)
+    else:
+        ref.auc_hist(logits, labels, nb, hist)
+
+
+def cast_bf16(x, y):
+    if _gpu(x):
+        _native().cast_bf16(x, y)
+    else:
+        ref.cast_bf16(x, y)

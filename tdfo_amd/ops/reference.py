@@ -1,0 +1,299 @@
+"""Pure-torch fp32 reference implementations of every native op.
+
+These are (a) the CPU execution path of the framework (BASELINE config 1:
+DLRM-tiny on CPU through the same engine code) and (b) the numerical oracles
+the GPU tests compare the HIP kernels against. Semantics mirror the kernels
+exactly, including bf16 rounding of bf16 outputs and the optimizer formulas.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+EMB_SGD, EMB_ROWWISE_ADAGRAD, EMB_ADAM, EMB_ADAGRAD, EMB_DENSE_GRAD = range(5)
+OPT_ADAMW, OPT_ADAM, OPT_SGD, OPT_ADAGRAD = range(4)
+
+
+def _f(t: torch.Tensor) -> torch.Tensor:
+    return t.float()
+
+
+def gemm(a, a_col, b, b_col, bias=None, relu=False, mask=None, out=None, out32=None, splits=1):
+    A = _f(a).t() if a_col else _f(a)          # [M, K]
+    Bm = _f(b) if b_col else _f(b).t()         # [K, N]
+    c = A @ Bm
+    if bias is not None:
+        c = c + bias.float()
+    if relu:
+        c = c.clamp_min(0)
+    if mask is not None:
+        c = c * (mask.float() > 0)
+    if out is not None:
+        out.copy_(c.to(out.dtype))
+    if out32 is not None:
+        M, N = c.shape
+        # split-K semantics: slice 0 holds the full sum, other slices zero
+        flat = out32.view(-1)
+        flat[: M * N].copy_(c.reshape(-1))
+        if splits > 1:
+            flat[M * N: splits * M * N].zero_()
+
+
+def interaction_fwd(dense, emb, off, stride, F, D, out):
+    B = dense.shape[0]
+    rows = [_f(dense[:, :D])]
+    flat = emb.reshape(-1)
+    ar = torch.arange(B, device=dense.device)
+    for i in range(1, F):
+        idx = off[i] + ar[:, None] * stride[i] + torch.arange(D, device=dense.device)[None, :]
+        rows.append(_f(flat[idx]))
+    X = torch.stack(rows, 1)                   # [B, F, D]
+    Z = torch.bmm(X, X.transpose(1, 2))
+    li, lj = torch.tril_indices(F, F, offset=-1, device=dense.device)
+    tri = Z[:, li, lj]
+    out.zero_()
+    out[:, :D] = dense[:, :D].to(out.dtype)
+    out[:, D:D + tri.shape[1]] = tri.to(out.dtype)
+
+
+def interaction_bwd(dz, dense, emb, off, stride, F, D, d_dense, d_emb, doff, dstride, relu_mask):
+    B = dense.shape[0]
+    dev = dense.device
+    flat = emb.reshape(-1)
+    ar = torch.arange(B, device=dev)
+    cols = torch.arange(D, device=dev)
+    rows = [_f(dense[:, :D])]
+    for i in range(1, F):
+        rows.append(_f(flat[off[i] + ar[:, None] * stride[i] + cols[None, :]]))
+    X = torch.stack(rows, 1)
+    P = F * (F - 1) // 2
+    li, lj = torch.tril_indices(F, F, offset=-1, device=dev)
+    S = torch.zeros(B, F, F, device=dev)
+    g = _f(dz[:, D:D + P])
+    S[:, li, lj] = g
+    S[:, lj, li] = g
+    dX = torch.bmm(S, X)
+    dd = dX[:, 0] + _f(dz[:, :D])
+    if relu_mask:
+        dd = dd * (X[:, 0] > 0)
+    d_dense[:, :D] = dd.to(d_dense.dtype)
+    dflat = d_emb.reshape(-1)
+    for i in range(1, F):
+        idx = doff[i] + ar[:, None] * dstride[i] + cols[None, :]
+        dflat[idx.reshape(-1)] = dX[:, i].reshape(-1).to(d_emb.dtype)
+
+
+def embedding_bag_fwd(W, row_offset, indices, offsets, out_off, psw, T, B, mean, out, out_stride):
+    D = W.shape[1]
+    dev = W.device
+    lengths = offsets[1:] - offsets[:-1]
+    bag = torch.repeat_interleave(torch.arange(T * B, device=dev), lengths)
+    t = bag // B
+    rows = row_offset[t] + indices
+    vals = W[rows].float()
+    if psw is not None:
+        vals = vals * psw.float()[:, None]
+    pooled = torch.zeros(T * B, D, device=dev)
+    pooled.index_add_(0, bag, vals)
+    if mean:
+        pooled = pooled / lengths.clamp_min(1).float()[:, None]
+    tt = torch.arange(T, device=dev).repeat_interleave(B)
+    bb = torch.arange(B, device=dev).repeat(T)
+    base = bb * out_stride + out_off[tt]
+    idx = base[:, None] + torch.arange(D, device=dev)[None, :]
+    out.view(-1)[idx.reshape(-1)] = pooled.reshape(-1).to(out.dtype)
+
+
+def embedding_grad_rows(W, row_offset, indices, offsets, grad_off, psw, T, B, mean, grad, grad_stride):
+    """Return (unique global rows [U], summed fp32 grads [U, D])."""
+    D = W.shape[1]
+    dev = W.device
+    lengths = offsets[1:] - offsets[:-1]
+    bag = torch.repeat_interleave(torch.arange(T * B, device=dev), lengths)
+    t = bag // B
+    b = bag - t * B
+    keys = row_offset[t] + indices
+    base = b * grad_stride + grad_off[t]
+    g = grad.reshape(-1)[(base[:, None] + torch.arange(D, device=dev)[None, :]).reshape(-1)]
+    g = g.float().view(-1, D)
+    scale = torch.ones(keys.shape[0], device=dev)
+    if psw is not None:
+        scale = scale * psw.float()
+    if mean:
+        scale = scale / lengths[bag].float()
+    g = g * scale[:, None]
+    uniq, inv = torch.unique(keys, return_inverse=True)
+    acc = torch.zeros(uniq.shape[0], D, device=dev)
+    acc.index_add_(0, inv, g)
+    return uniq, acc
+
+
+def embedding_bwd(W, row_offset, indices, offsets, grad_off, psw, T, B, mean, key_bits, grad,
+                  grad_stride, opt, state1, state2, hyper, eps, beta1, beta2, weight_decay,
+                  dense_grad):
+    rows, g = embedding_grad_rows(W, row_offset, indices, offsets, grad_off, psw, T, B, mean,
+                                  grad, grad_stride)
+    if rows.numel() == 0:
+        return
+    lr = float(hyper[0])
+    w = W[rows]
+    if opt == EMB_SGD:
+        w = w - lr * (g + weight_decay * w)
+    elif opt == EMB_ROWWISE_ADAGRAD:
+        gg = g + weight_decay * w
+        st = state1[rows] + (gg * gg).mean(1)
+        state1[rows] = st
+        w = w - (lr / (st.sqrt() + eps))[:, None] * gg
+    elif opt == EMB_ADAGRAD:
+        gg = g + weight_decay * w
+        st = state1.view(W.shape)[rows] + gg * gg
+        state1.view(W.shape)[rows] = st
+        w = w - lr * gg / (st.sqrt() + eps)
+    elif opt == EMB_ADAM:
+        step = float(hyper[1])
+        m = state1.view(W.shape)[rows] * beta1 + (1 - beta1) * g
+        v = state2.view(W.shape)[rows] * beta2 + (1 - beta2) * g * g
+        state1.view(W.shape)[rows] = m
+        state2.view(W.shape)[rows] = v
+        bc1 = 1 - beta1 ** step
+        bc2 = 1 - beta2 ** step
+        w = w - lr * ((m / bc1) / ((v / bc2).sqrt() + eps) + weight_decay * w)
+    elif opt == EMB_DENSE_GRAD:
+        dense_grad.view(W.shape)[rows] += g
+        return
+    else:
+        raise ValueError(f"unknown embedding optimizer {opt}")
+    W[rows] = w
+
+
+def dense_optimizer(p, g, m, v, p_bf16, opt, hyper, beta1, beta2, eps, wd, momentum, found_inf):
+    if found_inf is not None and float(found_inf.reshape(-1)[0]) > 0:
+        return
+    lr, step, gs = (float(x) for x in hyper[:3])
+    gg = g * gs
+    if opt in (OPT_ADAMW, OPT_ADAM):
+        if opt == OPT_ADAM:
+            gg = gg + wd * p
+        else:
+            p.mul_(1 - lr * wd)
+        m.mul_(beta1).add_(gg, alpha=1 - beta1)
+        v.mul_(beta2).addcmul_(gg, gg, value=1 - beta2)
+        bc1 = 1 - beta1 ** step
+        bc2 = 1 - beta2 ** step
+        p.sub_(lr * (m / bc1) / ((v / bc2).sqrt() + eps))
+    elif opt == OPT_SGD:
+        gg = gg + wd * p
+        if momentum != 0:
+            if step > 1:
+                m.mul_(momentum).add_(gg)
+            else:
+                m.copy_(gg)
+            gg = m
+        p.sub_(lr * gg)
+    elif opt == OPT_ADAGRAD:
+        gg = gg + wd * p
+        m.addcmul_(gg, gg)
+        p.sub_(lr * gg / (m.sqrt() + eps))
+    else:
+        raise ValueError(opt)
+    if p_bf16 is not None:
+        p_bf16.copy_(p.to(torch.bfloat16))
+
+
+def check_finite(g, found):
+    if not torch.isfinite(g).all():
+        found.fill_(1.0)
+
+
+def head_parts(B: int) -> int:
+    return (B + 63) // 64
+
+
+def head_bce(H, w, b, label, inv_n, relu_mask, logits, dH, part):
+    h = _f(H)
+    x = h @ w.float() + b.float()
+    y = label.float()
+    logits.copy_(x)
+    loss = x.clamp_min(0) - x * y + torch.log1p(torch.exp(-x.abs()))
+    g = (torch.sigmoid(x) - y) * inv_n
+    dh = g[:, None] * w.float()[None, :]
+    if relu_mask:
+        dh = dh * (h > 0)
+    dH.copy_(dh.to(dH.dtype))
+    K = h.shape[1]
+    part.view(-1)[: part.numel()].zero_()
+    pv = part.view(-1)[: K + 2]
+    pv[:K] = (g[:, None] * h).sum(0)
+    pv[K] = g.sum()
+    pv[K + 1] = loss.sum()
+
+
+def reduce_rows(inp, rows, n, ld, out, accumulate, scale):
+    flat = inp.reshape(-1)
+    s = torch.zeros(n, device=inp.device)
+    for r in range(rows):
+        s += flat[r * ld: r * ld + n]
+    s *= scale
+    o = out.view(-1)[:n]
+    if accumulate:
+        o += s
+    else:
+        o.copy_(s)
+
+
+def colsum(x, out, accumulate):
+    s = _f(x).sum(0)
+    if accumulate:
+        out += s
+    else:
+        out.copy_(s)
+
+
+def auc_hist(logits, labels, nb, hist):
+    p = torch.sigmoid(logits.float())
+    bkt = (p * nb).long().clamp(0, nb - 1)
+    pos = labels.float() > 0.5
+    hist[:nb] += torch.bincount(bkt[~pos], minlength=nb)
+    hist[nb:] += torch.bincount(bkt[pos], minlength=nb)
+
+
+def cast_bf16(x, y):
+    y.copy_(x.to(torch.bfloat16))
+
+
+def exact_auc(scores: torch.Tensor, labels: torch.Tensor) -> float:
+    """Rank-based (Mann-Whitney) ROC-AUC with tie handling."""
+    s = scores.double().cpu()
+    y = labels.double().cpu() > 0.5
+    n_pos = int(y.sum())
+    n_neg = y.numel() - n_pos
+    if n_pos == 0 or n_neg == 0:
+        return float("nan")
+    order = torch.argsort(s)
+    ranks = torch.empty_like(s)
+    ranks[order] = torch.arange(1, s.numel() + 1, dtype=torch.float64)
+    # average ranks for ties
+    uniq, inv, counts = torch.unique(s, return_inverse=True, return_counts=True)
+    sums = torch.zeros(uniq.numel(), dtype=torch.float64).index_add_(0, inv, ranks)
+    ranks = (sums / counts)[inv]
+    return float((ranks[y].sum() - n_pos * (n_pos + 1) / 2) / (n_pos * n_neg))
+
+
+def hist_auc(hist: torch.Tensor) -> float:
+    """AUC from a [neg | pos] bucket histogram (trapezoid over thresholds)."""
+    h = hist.double().cpu()
+    nb = h.numel() // 2
+    neg, pos = h[:nb], h[nb:]
+    tp = torch.cat([pos.flip(0).cumsum(0), pos.new_zeros(0)])
+    fp = neg.flip(0).cumsum(0)
+    P, N = pos.sum(), neg.sum()
+    if P == 0 or N == 0:
+        return float("nan")
+    tpr = torch.cat([torch.zeros(1, dtype=torch.float64), tp / P])
+    fpr = torch.cat([torch.zeros(1, dtype=torch.float64), fp / N])
+    return float(torch.trapz(tpr, fpr))
+
+
+def key_bits_for(rows: int) -> int:
+    return max(1, math.ceil(math.log2(max(2, rows))))

@@ -1,0 +1,142 @@
+"""Embedding sharding planner sized for MI355X (288 GB HBM3E per GPU).
+
+Plays the role of torchrec's default planner behind DMP
+(torchrec/train.py:241-247 of the reference, which picks a sharding type per
+table) and of TF's MinSizePartitioner for the parameter-server path
+(tensorflow2/train_ps.py:55-58), with an explicit, deterministic cost model:
+
+* memory per shard = rows x D x 4 B (fp32 weights) + optimizer state
+  (rowwise-Adagrad 1 float/row, Adagrad D, Adam 2D floats/row);
+* compute per shard ~ HBM bytes gathered + updated per step
+  (global batch x pooling factor x D x 4 B x ~3);
+* communication per table-wise shard = pooled bf16 rows all-to-all'd
+  (global batch x D x 2 B each way) over 7 point-to-point xGMI links.
+
+Sharding kinds:
+  table_wise   whole table on one rank (pooled-embedding all-to-all)
+  row_wise     rows split in contiguous blocks across all ranks (id
+               bucketize + all-to-all of ids and looked-up rows)
+  column_wise  D split across ranks; each column block is a table-wise shard
+  data_parallel  replicated (tiny tables; gradient all-reduce)
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
+
+from .tables import EmbOptimConfig, TableConfig
+
+HBM_BYTES = 288 * 10**9
+GiB = 1 << 30
+
+
+@dataclass
+class TableShard:
+    table: int
+    kind: str                      # table_wise | row_wise | column_wise | data_parallel
+    ranks: List[int]
+    row_blocks: List[int] = field(default_factory=list)   # row_wise: rows per rank
+    col_blocks: List[int] = field(default_factory=list)   # column_wise: cols per rank
+
+
+@dataclass
+class ShardingPlan:
+    world_size: int
+    shards: List[TableShard]
+    mem_bytes: List[int]
+    cost: List[float]
+
+    def kind_of(self, t: int) -> str:
+        return self.shards[t].kind
+
+    def tables_on(self, rank: int, kind: str = "table_wise") -> List[int]:
+        return [s.table for s in self.shards if s.kind == kind and rank in s.ranks]
+
+    def summary(self) -> Dict:
+        kinds: Dict[str, int] = {}
+        for s in self.shards:
+            kinds[s.kind] = kinds.get(s.kind, 0) + 1
+        return {"world_size": self.world_size, "kinds": kinds,
+                "mem_GiB": [round(m / GiB, 2) for m in self.mem_bytes],
+                "cost": [round(c, 3) for c in self.cost]}
+
+
+def _mem_per_row(dim: int, optim: EmbOptimConfig) -> int:
+    return 4 * (dim + optim.state_floats_per_row(dim))
+
+
+def plan_sharding(tables: Sequence[TableConfig], world_size: int, optim: EmbOptimConfig,
+                  batch_per_rank: int = 8192, pooling: Optional[Sequence[float]] = None,
+                  hbm_bytes: int = HBM_BYTES, reserve_frac: float = 0.15,
+                  strategy: str = "auto", dp_max_bytes: int = 0) -> ShardingPlan:
+    """Deterministic greedy planner.
+
+    strategy: "auto" (table-wise with row-wise fallback for tables that fit
+    no rank), "table_wise", "row_wise", "column_wise" (tables split evenly by
+    columns), "data_parallel".
+    """
+    W = world_size
+    cap = int(hbm_bytes * (1.0 - reserve_frac))
+    T = len(tables)
+    pooling = list(pooling) if pooling is not None else [1.0] * T
+    gb = batch_per_rank * W
+    mem = [0] * W
+    cost = [0.0] * W
+    shards: List[Optional[TableShard]] = [None] * T
+
+    def tcost(t: int) -> float:
+        d = tables[t].embedding_dim
+        return gb * pooling[t] * d * 4 * 3 / 1e9 + gb * d * 2 * 2 / 1e9
+
+    order = sorted(range(T), key=lambda t: (-tcost(t), -tables[t].num_embeddings, t))
+
+    def row_wise(t: int):
+        rows = tables[t].num_embeddings
+        blk = -(-rows // W)                  # owner(id) = id // blk
+        blocks = [max(0, min(blk, rows - r * blk)) for r in range(W)]
+        per_row = _mem_per_row(tables[t].embedding_dim, optim)
+        for r in range(W):
+            mem[r] += blocks[r] * per_row
+            cost[r] += tcost(t) / W
+        return TableShard(t, "row_wise", list(range(W)), row_blocks=blocks)
+
+    def column_wise(t: int):
+        d = tables[t].embedding_dim
+        nb = min(W, max(1, d // 32))
+        base = (d // nb) // 8 * 8
+        cols = [base] * nb
+        cols[-1] += d - base * nb
+        ranks = sorted(range(W), key=lambda r: (cost[r], mem[r], r))[:nb]
+        for i, r in enumerate(ranks):
+            mem[r] += tables[t].num_embeddings * 4 * (cols[i] + optim.state_floats_per_row(cols[i]))
+            cost[r] += tcost(t) * cols[i] / d
+        return TableShard(t, "column_wise", ranks, col_blocks=cols)
+
+    for t in order:
+        tb = tables[t].num_embeddings * _mem_per_row(tables[t].embedding_dim, optim)
+        if strategy == "data_parallel" or (strategy == "auto" and tb <= dp_max_bytes):
+            for r in range(W):
+                mem[r] += tb
+                cost[r] += tcost(t) / W
+            shards[t] = TableShard(t, "data_parallel", list(range(W)))
+            continue
+        if strategy == "row_wise" and W > 1:
+            shards[t] = row_wise(t)
+            continue
+        if strategy == "column_wise" and W > 1:
+            shards[t] = column_wise(t)
+            continue
+        cand = [r for r in range(W) if mem[r] + tb <= cap]
+        if not cand:
+            if W == 1:
+                raise MemoryError(f"table {tables[t].name} ({tb / GiB:.1f} GiB) exceeds HBM budget")
+            shards[t] = row_wise(t)
+            continue
+        r = min(cand, key=lambda r: (cost[r], mem[r], r))
+        mem[r] += tb
+        cost[r] += tcost(t)
+        shards[t] = TableShard(t, "table_wise", [r])
+    for r in range(W):
+        if mem[r] > cap:
+            raise MemoryError(f"rank {r} needs {mem[r] / GiB:.1f} GiB > budget {cap / GiB:.1f} GiB")
+    return ShardingPlan(W, shards, mem, cost)  # type: ignore[arg-type]

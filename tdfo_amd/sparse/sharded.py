@@ -1,0 +1,328 @@
+"""Sharded pooled embeddings (the north-star engine behind DLRM / DCN-v2, and
+the in-node replacement of the reference's parameter-server path).
+
+Reference capabilities this covers:
+  * TorchRec DMP sharded EmbeddingCollection (torchrec/train.py:235-254):
+    input-dist all-to-all of ids, local TBE lookup, output-dist all-to-all
+    of embeddings, reverse in backward with a fused optimizer.
+  * TF ParameterServerStrategy partitioned variables (tensorflow2/
+    train_ps.py:55-61): variables partitioned over "PS" tasks, pulled and
+    pushed every step -> here HBM-resident table/row shards exchanged by
+    RCCL all-to-all over xGMI, synchronously.
+
+Design (MI355X-first):
+  * table-wise (TW) shards: a rank owns whole tables; ids go to the owner,
+    the owner pools the *global* batch of its tables with one HIP launch,
+    writing straight into the all-to-all send buffer in [src][b][tables x D]
+    order, and the receiver's interaction kernel reads the pooled rows in
+    place through a slot map (no permute kernel in either direction).
+    Shapes are static for fixed pooling factors, so the exchange is
+    hipGraph-capturable and needs no split exchange.
+  * row-wise (RW) shards: ids are bucketed by owner block, exchanged with
+    data-dependent splits, looked up unpooled by the owner, returned, and
+    pooled at the requester by the same embedding kernel (the received rows
+    act as a table); gradients travel back per id and the owner's fused
+    sort-based backward merges duplicates across requesters.
+  * bf16 on the wire for embeddings/gradients, fp32 in HBM tables.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+from .planner import ShardingPlan
+from .tables import EmbOptimConfig, TableBatchedEmbedding, TableConfig
+
+
+def _a2a(out, inp, out_splits, in_splits, group, async_op=False):
+    return dist.all_to_all_single(out, inp, output_split_sizes=out_splits,
+                                  input_split_sizes=in_splits, group=group, async_op=async_op)
+
+
+class ShardedEmbeddingBags:
+    """Pooled embedding features of one width D over a sharding plan.
+
+    Input ``ids``: int64, original table order, table t occupying ``B * L_t``
+    entries (bag b of table t = ids[base_t + b*L_t : base_t + (b+1)*L_t]).
+    Output: ``self.recv`` (bf16) plus ``slot_off`` / ``slot_stride`` giving, per
+    feature (table), the element offset and per-sample stride of its pooled
+    row inside ``recv`` — the layout the interaction / concat consumers read.
+    """
+
+    def __init__(self, tables: Sequence[TableConfig], plan: ShardingPlan, rank: int,
+                 batch_size: int, pooling: Sequence[int], device, optim: EmbOptimConfig,
+                 group=None, seed: int = 0, mean: bool = False):
+        self.tables = list(tables)
+        self.T = len(self.tables)
+        dims = {t.embedding_dim for t in self.tables}
+        assert len(dims) == 1, "ShardedEmbeddingBags needs one embedding width"
+        self.D = D = dims.pop()
+        self.plan = plan
+        self.world = W = plan.world_size
+        self.rank = rank
+        self.B = B = int(batch_size)
+        self.L = [int(x) for x in pooling]
+        self.device = torch.device(device)
+        self.group = group
+        self.mean = mean
+        self.optim = optim
+        for s in plan.shards:
+            if s.kind not in ("table_wise", "row_wise"):
+                raise NotImplementedError(f"sharding kind {s.kind} not supported for pooled bags")
+        # ---- id layout in the input (original order)
+        self.in_base = [0] * self.T
+        acc = 0
+        for t in range(self.T):
+            self.in_base[t] = acc
+            acc += B * self.L[t]
+        self.nnz_local = acc
+        # ---- table-wise group
+        self.tw_tables = [[s.table for s in plan.shards if s.kind == "table_wise" and s.ranks[0] == r]
+                          for r in range(W)]
+        mine = self.tw_tables[rank]
+        self.tw_mine = mine
+        self.dsum = [len(ts) * D for ts in self.tw_tables]
+        self.tw_store = TableBatchedEmbedding([self.tables[t].num_embeddings for t in mine], D,
+                                              device, optim,
+                                              init_ranges=[self.tables[t].init_range or
+                                                           (1.0 / self.tables[t].num_embeddings) ** 0.5
+                                                           for t in mine],
+                                              seed=seed * 1000 + rank)
+        # send order: tables grouped by owner
+        order = [t for r in range(W) for t in self.tw_tables[r]]
+        self.tw_send_counts = [sum(B * self.L[t] for t in self.tw_tables[r]) for r in range(W)]
+        self.tw_recv_count = sum(B * self.L[t] for t in mine)
+        perm = torch.cat([torch.arange(self.in_base[t], self.in_base[t] + B * self.L[t])
+                          for t in order]) if order else torch.zeros(0, dtype=torch.int64)
+        self.tw_identity = bool(W == 1 and torch.equal(perm, torch.arange(perm.numel()))
+                                and len(order) == self.T)
+        self.tw_perm = perm.to(self.device)
+        # owner-side virtual tables v = (src s, local table i)
+        nv = W * len(mine)
+        lens = []
+        v_row_off, v_out_off = [], []
+        for s in range(W):
+            for i, t in enumerate(mine):
+                lens += [self.L[t]] * B
+                v_row_off.append(self.tw_store.row_offset_host[i])
+                v_out_off.append(s * B * self.dsum[rank] + i * D)
+        self.tw_nv = nv
+        offs = torch.zeros(len(lens) + 1, dtype=torch.int64)
+        if lens:
+            offs[1:] = torch.cumsum(torch.tensor(lens, dtype=torch.int64), 0)
+        self.tw_v_offsets = offs.to(self.device)
+        self.tw_v_row_off = torch.tensor(v_row_off, dtype=torch.int64, device=self.device)
+        self.tw_v_out_off = torch.tensor(v_out_off, dtype=torch.int64, device=self.device)
+        # buffers
+        bf = torch.bfloat16
+        self.tw_send_ids = torch.empty(self.nnz_local_tw(), dtype=torch.int64, device=self.device)
+        self.tw_recv_ids = torch.empty(W * self.tw_recv_count, dtype=torch.int64, device=self.device)
+        self.tw_pooled = torch.empty(max(1, W * B * self.dsum[rank]), dtype=bf, device=self.device)
+        self.tw_recv_sizes = [B * self.dsum[r] for r in range(W)]
+        self.tw_recv_base = [sum(self.tw_recv_sizes[:r]) for r in range(W)]
+        tw_total = sum(self.tw_recv_sizes)
+        # ---- row-wise group (dynamic splits)
+        self.rw_tables = [s.table for s in plan.shards if s.kind == "row_wise"]
+        self.rw_col = {t: j * D for j, t in enumerate(self.rw_tables)}
+        self.rw_width = len(self.rw_tables) * D
+        if self.rw_tables:
+            blocks = []
+            for t in self.rw_tables:
+                rows = self.tables[t].num_embeddings
+                blk = -(-rows // W)
+                blocks.append(blk)
+            self.rw_block = torch.tensor(blocks, dtype=torch.int64, device=self.device)
+            self.rw_block_host = blocks
+            my_rows = [max(0, min(blocks[j], self.tables[t].num_embeddings - rank * blocks[j]))
+                       for j, t in enumerate(self.rw_tables)]
+            self.rw_store = TableBatchedEmbedding(
+                my_rows, D, device, optim,
+                init_ranges=[self.tables[t].init_range or (1.0 / self.tables[t].num_embeddings) ** 0.5
+                             for t in self.rw_tables], seed=seed * 1000 + 500 + rank)
+            rw_ids_idx = torch.cat([torch.arange(self.in_base[t], self.in_base[t] + B * self.L[t])
+                                    for t in self.rw_tables])
+            self.rw_in_idx = rw_ids_idx.to(self.device)
+            tab = torch.cat([torch.full((B * self.L[t],), j, dtype=torch.int64)
+                             for j, t in enumerate(self.rw_tables)])
+            self.rw_tab = tab.to(self.device)
+            bag = torch.cat([torch.arange(B).repeat_interleave(self.L[t]) + j * B
+                             for j, t in enumerate(self.rw_tables)])
+            self.rw_bag = bag.to(self.device)      # bag id (j*B + b) per rw id
+            lens = torch.tensor([self.L[t] for t in self.rw_tables], dtype=torch.int64)
+            bag_len = lens.repeat_interleave(B)
+            boffs = torch.zeros(bag_len.numel() + 1, dtype=torch.int64)
+            boffs[1:] = torch.cumsum(bag_len, 0)
+            self.rw_bag_offsets = boffs.to(self.device)
+            self.rw_out_off = torch.tensor([tw_total + j * D for j in range(len(self.rw_tables))],
+                                           dtype=torch.int64, device=self.device)
+        self.recv = torch.zeros(tw_total + B * self.rw_width, dtype=bf, device=self.device)
+        self.d_recv = torch.zeros_like(self.recv)
+        self.d_pooled = torch.empty_like(self.tw_pooled)
+        # ---- consumer slot map (per feature/table)
+        self.slot_off: List[int] = [0] * self.T
+        self.slot_stride: List[int] = [0] * self.T
+        for r in range(W):
+            for i, t in enumerate(self.tw_tables[r]):
+                self.slot_off[t] = self.tw_recv_base[r] + i * D
+                self.slot_stride[t] = self.dsum[r]
+        for t in self.rw_tables:
+            self.slot_off[t] = tw_total + self.rw_col[t]
+            self.slot_stride[t] = self.rw_width
+        self._pending = None
+        self._rw_state = None
+
+    def nnz_local_tw(self) -> int:
+        return sum(self.tw_send_counts)
+
+    # ------------------------------------------------------------ forward
+    def forward(self, ids: torch.Tensor) -> torch.Tensor:
+        self.forward_start(ids)
+        self.forward_wait()
+        return self.recv
+
+    def forward_start(self, ids: torch.Tensor):
+        W, B = self.world, self.B
+        if self.tw_identity:
+            self.tw_send_ids = ids
+            self.tw_recv_ids = ids
+        else:
+            torch.index_select(ids, 0, self.tw_perm, out=self.tw_send_ids)
+            if W > 1:
+                _a2a(self.tw_recv_ids, self.tw_send_ids, [self.tw_recv_count] * W,
+                     self.tw_send_counts, self.group)
+            else:
+                self.tw_recv_ids = self.tw_send_ids
+        if self.tw_nv:
+            self.tw_store.forward(self.tw_recv_ids, self.tw_v_offsets, self.tw_v_row_off, self.tw_nv,
+                                  B, self.tw_pooled if W > 1 else self.recv, self.tw_v_out_off,
+                                  self.dsum[self.rank], mean=self.mean)
+        work = None
+        tw_total = sum(self.tw_recv_sizes)
+        if W > 1:
+            work = _a2a(self.recv[:tw_total], self.tw_pooled[: W * B * self.dsum[self.rank]],
+                        self.tw_recv_sizes, [B * self.dsum[self.rank]] * W, self.group,
+                        async_op=True)
+        if self.rw_tables:
+            self._rw_forward(ids)
+        self._pending = work
+
+    def forward_wait(self):
+        if self._pending is not None:
+            self._pending.wait()
+            self._pending = None
+
+    # row-wise: dynamic splits
+    def _rw_forward(self, ids: torch.Tensor):
+        W, D = self.world, self.D
+        gid = ids.index_select(0, self.rw_in_idx)
+        blk = self.rw_block[self.rw_tab]
+        owner = torch.clamp(gid // blk, max=W - 1)
+        local = gid - owner * blk
+        order = torch.argsort(owner, stable=True)
+        send_counts = torch.bincount(owner, minlength=W)
+        if W > 1:
+            recv_counts = torch.empty_like(send_counts)
+            dist.all_to_all_single(recv_counts, send_counts, group=self.group)
+        else:
+            recv_counts = send_counts
+        sc = send_counts.tolist()
+        rc = recv_counts.tolist()
+        key = self.rw_store.row_offset[self.rw_tab] + local
+        send_keys = key.index_select(0, order)
+        recv_keys = torch.empty(sum(rc), dtype=torch.int64, device=self.device)
+        if W > 1:
+            _a2a(recv_keys, send_keys, rc, sc, self.group)
+        else:
+            recv_keys = send_keys
+        n_r = recv_keys.numel()
+        rows = torch.empty(max(1, n_r), D, dtype=torch.float32, device=self.device)
+        if n_r:
+            ar = torch.arange(n_r + 1, dtype=torch.int64, device=self.device)
+            self.rw_store.forward(recv_keys, ar, torch.zeros(1, dtype=torch.int64, device=self.device),
+                                  1, n_r, rows, torch.zeros(1, dtype=torch.int64, device=self.device),
+                                  D)
+        back = torch.empty(order.numel(), D, dtype=torch.float32, device=self.device)
+        if W > 1:
+            _a2a(back, rows[:n_r], sc, rc, self.group)
+        else:
+            back = rows[:n_r]
+        # back[i] is the row of rw id order[i]; pool into recv via position map
+        pos = torch.empty_like(order)
+        pos[order] = torch.arange(order.numel(), device=self.device)
+        nrw = len(self.rw_tables)
+        zeros_ro = torch.zeros(nrw, dtype=torch.int64, device=self.device)
+        from .. import ops
+        ops.embedding_bag_fwd(back.contiguous() if back.numel() else
+                              torch.zeros(1, D, device=self.device),
+                              zeros_ro, pos, self.rw_bag_offsets, self.rw_out_off, nrw, self.B,
+                              self.recv, self.rw_width, mean=self.mean)
+        self._rw_state = (order, sc, rc, recv_keys)
+
+    # ----------------------------------------------------------- backward
+    def backward_start(self, d_recv: Optional[torch.Tensor] = None):
+        """Start the gradient exchange (async on GPU). ``d_recv`` defaults to
+        ``self.d_recv`` (same layout as ``self.recv``)."""
+        d_recv = self.d_recv if d_recv is None else d_recv
+        W, B = self.world, self.B
+        tw_total = sum(self.tw_recv_sizes)
+        work = None
+        if W > 1:
+            work = _a2a(self.d_pooled[: W * B * self.dsum[self.rank]], d_recv[:tw_total],
+                        [B * self.dsum[self.rank]] * W, self.tw_recv_sizes, self.group,
+                        async_op=True)
+        self._bw = (work, d_recv)
+
+    def backward_finish(self, hyper: torch.Tensor):
+        work, d_recv = self._bw
+        W, B = self.world, self.B
+        if work is not None:
+            work.wait()
+        grad = self.d_pooled if W > 1 else d_recv
+        if self.tw_nv:
+            self.tw_store.backward_update(self.tw_recv_ids, self.tw_v_offsets, self.tw_v_row_off,
+                                          self.tw_nv, B, grad, self.tw_v_out_off,
+                                          self.dsum[self.rank], hyper, mean=self.mean)
+        if self.rw_tables:
+            self._rw_backward(d_recv, hyper)
+        self._bw = None
+
+    def _rw_backward(self, d_recv, hyper):
+        order, sc, rc, recv_keys = self._rw_state
+        D, W = self.D, self.world
+        tw_total = sum(self.tw_recv_sizes)
+        nrw = len(self.rw_tables)
+        # per rw id (send order): its bag's pooled gradient
+        bag = self.rw_bag.index_select(0, order)
+        j = bag // self.B
+        b = bag - j * self.B
+        base = tw_total + b * self.rw_width + j * D
+        idx = base[:, None] + torch.arange(D, device=self.device)[None, :]
+        g = d_recv.index_select(0, idx.reshape(-1)).view(-1, D)
+        if self.mean:
+            lens = torch.tensor([self.L[t] for t in self.rw_tables], device=self.device)
+            g = g / lens[j].to(g.dtype)[:, None]
+        gr = torch.empty(recv_keys.numel(), D, dtype=g.dtype, device=self.device)
+        if W > 1:
+            _a2a(gr, g.contiguous(), rc, sc, self.group)
+        else:
+            gr = g.contiguous()
+        n_r = recv_keys.numel()
+        if n_r:
+            ar = torch.arange(n_r + 1, dtype=torch.int64, device=self.device)
+            z = torch.zeros(1, dtype=torch.int64, device=self.device)
+            self.rw_store.backward_update(recv_keys, ar, z, 1, n_r, gr, z, D, hyper)
+        del nrw
+
+    # -------------------------------------------------------------- state
+    def state_dict(self):
+        d = {"tw": self.tw_store.state_dict()}
+        if self.rw_tables:
+            d["rw"] = self.rw_store.state_dict()
+        return d
+
+    def load_state_dict(self, d):
+        self.tw_store.load_state_dict(d["tw"])
+        if self.rw_tables:
+            self.rw_store.load_state_dict(d["rw"])

@@ -1,0 +1,148 @@
+"""Embedding table configs and the table-batched embedding store.
+
+``TableBatchedEmbedding`` keeps every table of one embedding width in a single
+fused fp32 buffer ``[sum(rows), D]`` (one allocation, sized for 288 GB HBM)
+with per-table row offsets, so one HIP launch serves all tables (the role of
+fbgemm's TBE in torchrec/models.py:150-164 of the reference). Its backward is
+fused with the optimizer (rowwise-Adagrad / Adam / Adagrad / SGD) and never
+materialises a dense embedding gradient (contrast reference quirk Q1, where
+JAX all-reduces full-table gradients: jax-flax/train_dp.py:63).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import torch
+
+from .. import ops
+
+EMB_OPTIMIZERS = {
+    "sgd": ops.EMB_SGD,
+    "rowwise_adagrad": ops.EMB_ROWWISE_ADAGRAD,
+    "exact_rowwise_adagrad": ops.EMB_ROWWISE_ADAGRAD,
+    "adam": ops.EMB_ADAM,
+    "adagrad": ops.EMB_ADAGRAD,
+    "dense_grad": ops.EMB_DENSE_GRAD,
+}
+
+
+@dataclass
+class TableConfig:
+    name: str
+    num_embeddings: int
+    embedding_dim: int
+    feature_names: List[str] = field(default_factory=list)
+    pooling: str = "sum"            # "sum" | "mean" | "none" (sequence)
+    init_range: Optional[float] = None  # uniform(-r, r); default sqrt(1/num_embeddings)
+
+    def __post_init__(self):
+        if not self.feature_names:
+            self.feature_names = [self.name]
+
+    @property
+    def bytes_fp32(self) -> int:
+        return self.num_embeddings * self.embedding_dim * 4
+
+
+@dataclass
+class EmbOptimConfig:
+    name: str = "rowwise_adagrad"
+    lr: float = 0.01
+    eps: float = 1e-8
+    beta1: float = 0.9
+    beta2: float = 0.999
+    weight_decay: float = 0.0
+    initial_accumulator: float = 0.0
+
+    @property
+    def code(self) -> int:
+        return EMB_OPTIMIZERS[self.name]
+
+    def state_floats_per_row(self, dim: int) -> int:
+        c = self.code
+        if c == ops.EMB_ROWWISE_ADAGRAD:
+            return 1
+        if c == ops.EMB_ADAGRAD:
+            return dim
+        if c == ops.EMB_ADAM:
+            return 2 * dim
+        return 0
+
+
+class TableBatchedEmbedding:
+    """All tables of one width in one fused buffer, with a fused optimizer.
+
+    ``row_counts`` lists the rows this store holds per (local) table — for a
+    row-wise shard that is the shard's slice, for a column-wise shard the
+    table's full rows at the shard's width.
+    """
+
+    def __init__(self, row_counts: Sequence[int], dim: int, device, optim: EmbOptimConfig,
+                 init_ranges: Optional[Sequence[float]] = None, seed: int = 0,
+                 dtype=torch.float32):
+        self.dim = int(dim)
+        self.row_counts = [int(r) for r in row_counts]
+        self.num_tables = len(self.row_counts)
+        self.device = torch.device(device)
+        self.optim = optim
+        offs = [0]
+        for r in self.row_counts:
+            offs.append(offs[-1] + r)
+        self.total_rows = offs[-1]
+        self.row_offset_host = offs[:-1]
+        self.row_offset = torch.tensor(offs[:-1], dtype=torch.int64, device=self.device)
+        self.weight = torch.empty(max(1, self.total_rows), self.dim, dtype=dtype, device=self.device)
+        gen = torch.Generator(device=self.device)
+        gen.manual_seed(seed)
+        for t, r in enumerate(self.row_counts):
+            if r == 0:
+                continue
+            rng = init_ranges[t] if init_ranges is not None else math.sqrt(1.0 / max(1, r))
+            self.weight[offs[t]: offs[t] + r].uniform_(-rng, rng, generator=gen)
+        c = optim.code
+        self.state1 = self.state2 = None
+        if c == ops.EMB_ROWWISE_ADAGRAD:
+            self.state1 = torch.full((max(1, self.total_rows),), optim.initial_accumulator,
+                                     dtype=torch.float32, device=self.device)
+        elif c == ops.EMB_ADAGRAD:
+            self.state1 = torch.full_like(self.weight, optim.initial_accumulator)
+        elif c == ops.EMB_ADAM:
+            self.state1 = torch.zeros_like(self.weight)
+            self.state2 = torch.zeros_like(self.weight)
+        self.key_bits = ops.key_bits_for(self.total_rows)
+
+    # ------------------------------------------------------------------
+    def forward(self, indices, offsets, row_offset, T, B, out, out_off, out_stride, mean=False,
+                psw=None):
+        """Pooled lookup over ``T`` (virtual) tables of ``B`` bags each."""
+        ops.embedding_bag_fwd(self.weight, row_offset, indices, offsets, out_off, T, B, out,
+                              out_stride, mean=mean, psw=psw)
+
+    def backward_update(self, indices, offsets, row_offset, T, B, grad, grad_off, grad_stride,
+                        hyper, mean=False, psw=None, dense_grad=None):
+        o = self.optim
+        ops.embedding_bwd(self.weight, row_offset, indices, offsets, grad_off, T, B, grad,
+                          grad_stride, o.code, hyper, state1=self.state1, state2=self.state2,
+                          eps=o.eps, beta1=o.beta1, beta2=o.beta2, weight_decay=o.weight_decay,
+                          key_bits=self.key_bits, mean=mean, psw=psw, dense_grad=dense_grad)
+
+    def table_weight(self, t: int) -> torch.Tensor:
+        s = self.row_offset_host[t]
+        return self.weight[s: s + self.row_counts[t]]
+
+    def state_dict(self):
+        d = {"weight": self.weight}
+        if self.state1 is not None:
+            d["state1"] = self.state1
+        if self.state2 is not None:
+            d["state2"] = self.state2
+        return d
+
+    def load_state_dict(self, d):
+        self.weight.copy_(d["weight"])
+        if self.state1 is not None and "state1" in d:
+            self.state1.copy_(d["state1"])
+        if self.state2 is not None and "state2" in d:
+            self.state2.copy_(d["state2"])

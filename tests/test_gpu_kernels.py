@@ -1,0 +1,333 @@
+"""HIP kernel numerics vs the fp32 torch references (run on MI355X).
+
+Each test builds inputs on the GPU, runs the native op (torch.ops.tdfo.*),
+and compares against tdfo_amd.ops.reference on the same data in fp32.
+"""
+import pytest
+import torch
+
+from tdfo_amd import ops
+from tdfo_amd.ops import reference as ref
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _native():
+    from tdfo_amd.ops import _ext
+
+    assert _ext.load(), "native library must load on the GPU box"
+
+
+def bf(x):
+    return x.to(torch.bfloat16)
+
+
+def rel_err(a, b):
+    a, b = a.float(), b.float()
+    return float((a - b).abs().max() / (b.abs().max() + 1e-6))
+
+
+# ------------------------------------------------------------------ GEMM
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (300, 200, 192), (8192, 1024, 512),
+                                   (1000, 72, 128), (64, 512, 1024)])
+@pytest.mark.parametrize("a_col,b_col", [(False, False), (False, True), (True, True)])
+def test_gemm_layouts(M, N, K, a_col, b_col):
+    if a_col and M % 8:
+        pytest.skip("col A needs M%8")
+    if b_col and N % 8:
+        pytest.skip("col B needs N%8")
+    torch.manual_seed(0)
+    A = bf(torch.randn(K, M, device=DEV) if a_col else torch.randn(M, K, device=DEV))
+    B = bf(torch.randn(K, N, device=DEV) if b_col else torch.randn(N, K, device=DEV))
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    out32 = torch.empty(M * N, device=DEV)
+    ops.gemm(A, a_col, B, b_col, None, False, None, out, out32, 1)
+    exp = torch.empty(M * N, device=DEV)
+    ref.gemm(A, a_col, B, b_col, None, False, None, None, exp, 1)
+    assert rel_err(out32.view(M, N), exp.view(M, N)) < 1e-4
+    assert rel_err(out, exp.view(M, N)) < 1e-2
+
+
+def test_gemm_asymmetric_identity():
+    # A = I with asymmetric B catches row/col swaps in the C map (guide §3)
+    n = 128
+    A = bf(torch.eye(n, device=DEV))                       # [M=128, K=128]
+    Bs = bf(torch.arange(64 * n, device=DEV, dtype=torch.float32).view(64, n) % 97)  # [N][K]
+    out32 = torch.empty(n * 64, device=DEV)
+    ops.gemm(A, False, Bs, False, None, False, None, None, out32, 1)
+    assert torch.equal(out32.view(n, 64), Bs.float().t())
+    # col-layout B ([K][N]) and col-layout A ([K][M]) with the same data
+    out32b = torch.empty(n * 64, device=DEV)
+    ops.gemm(A, True, Bs.t().contiguous(), True, None, False, None, None, out32b, 1)
+    assert torch.equal(out32b.view(n, 64), Bs.float().t())
+
+
+def test_gemm_epilogue_bias_relu_mask():
+    torch.manual_seed(1)
+    M, N, K = 513, 256, 128
+    A = bf(torch.randn(M, K, device=DEV))
+    W = bf(torch.randn(N, K, device=DEV))
+    bias = torch.randn(N, device=DEV)
+    mask = bf(torch.randn(M, N, device=DEV))
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    ops.gemm(A, False, W, False, bias, True, mask, out, None, 1)
+    exp = torch.empty(M, N, dtype=torch.bfloat16, device=DEV)
+    ref.gemm(A, False, W, False, bias, True, mask, exp, None, 1)
+    assert rel_err(out, exp) < 1e-2
+
+
+def test_gemm_strided_out_and_splitk():
+    torch.manual_seed(2)
+    M, N, K = 256, 512, 8192
+    dy = bf(torch.randn(K, M, device=DEV))
+    x = bf(torch.randn(K, N, device=DEV))
+    out = torch.empty(M * N, device=DEV)
+    ops.linear_wgrad(dy, x, out, splits=8)
+    exp = dy.float().t() @ x.float()
+    assert rel_err(out.view(M, N), exp) < 1e-4
+    big = torch.zeros(64, 1024, dtype=torch.bfloat16, device=DEV)
+    view = big[:, 256:512]
+    a = bf(torch.randn(64, 128, device=DEV))
+    w = bf(torch.randn(256, 128, device=DEV))
+    ops.linear_fwd(a, w, None, False, out=view)
+    assert rel_err(view, a.float() @ w.float().t()) < 1e-2
+    assert big[:, :256].abs().sum() == 0 and big[:, 512:].abs().sum() == 0
+
+
+# ----------------------------------------------------------- interaction
+@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("B", [1, 37, 1024])
+def test_interaction(D, B):
+    torch.manual_seed(3)
+    F = 27
+    T = F - 1
+    dense = bf(torch.randn(B, D, device=DEV)).abs()
+    dense[:, ::3] = -dense[:, ::3]
+    emb = bf(torch.randn(B * T * D, device=DEV))
+    off = [0] + [t * D for t in range(T)]
+    stride = [0] + [T * D] * T
+    ldo = ((D + F * (F - 1) // 2 + 63) // 64) * 64
+    out = torch.full((B, ldo), 7.0, dtype=torch.bfloat16, device=DEV)
+    ops.interaction_fwd(dense, emb, off, stride, F, D, out)
+    exp = torch.empty_like(out)
+    ref.interaction_fwd(dense, emb, off, stride, F, D, exp)
+    assert rel_err(out, exp) < 1e-2
+    dz = bf(torch.randn(B, ldo, device=DEV))
+    dd = torch.zeros(B, D, dtype=torch.bfloat16, device=DEV)
+    de = torch.zeros_like(emb)
+    ops.interaction_bwd(dz, dense, emb, off, stride, F, D, dd, de, off, stride, True)
+    edd = torch.zeros_like(dd)
+    ede = torch.zeros_like(emb)
+    ref.interaction_bwd(dz, dense, emb, off, stride, F, D, edd, ede, off, stride, True)
+    assert rel_err(dd, edd) < 2e-2
+    assert rel_err(de, ede) < 2e-2
+
+
+# ------------------------------------------------------------- embedding
+def _emb_case(T, B, rows, D, L, skew, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    lens = torch.randint(0, L + 1, (T * B,), generator=g) if L > 1 else torch.ones(T * B, dtype=torch.long)
+    offsets = torch.zeros(T * B + 1, dtype=torch.long)
+    offsets[1:] = lens.cumsum(0)
+    nnz = int(offsets[-1])
+    idx = []
+    for j in range(T * B):
+        t = j // B
+        n = int(lens[j])
+        if skew:
+            idx.append(torch.randint(0, min(3, rows[t]), (n,), generator=g))
+        else:
+            idx.append(torch.randint(0, rows[t], (n,), generator=g))
+    indices = torch.cat(idx) if nnz else torch.zeros(0, dtype=torch.long)
+    ro = torch.zeros(T, dtype=torch.long)
+    ro[1:] = torch.tensor(rows[:-1]).cumsum(0)
+    W = torch.randn(sum(rows), D, generator=g)
+    return W, ro, indices, offsets
+
+
+@pytest.mark.parametrize("D", [16, 64, 128])
+@pytest.mark.parametrize("L,mean", [(1, False), (5, False), (5, True)])
+def test_embedding_fwd(D, L, mean):
+    T, B = 4, 300
+    rows = [100, 7, 5000, 1]
+    W, ro, idx, offs = _emb_case(T, B, rows, D, L, False)
+    W, ro, idx, offs = (x.to(DEV) for x in (W, ro, idx, offs))
+    out_off = torch.tensor([t * D for t in range(T)], device=DEV)
+    out = torch.zeros(B * T * D, dtype=torch.bfloat16, device=DEV)
+    ops.embedding_bag_fwd(W, ro, idx, offs, out_off, T, B, out, T * D, mean=mean)
+    exp = torch.zeros(B * T * D, device=DEV)
+    ref.embedding_bag_fwd(W, ro, idx, offs, out_off, None, T, B, mean, exp, T * D)
+    assert rel_err(out, exp) < 1e-2
+
+
+@pytest.mark.parametrize("opt", [ops.EMB_SGD, ops.EMB_ROWWISE_ADAGRAD, ops.EMB_ADAM,
+                                 ops.EMB_ADAGRAD, ops.EMB_DENSE_GRAD])
+@pytest.mark.parametrize("skew", [False, True])
+@pytest.mark.parametrize("D", [32, 128])
+def test_embedding_bwd_fused(opt, skew, D):
+    T, B, L = 3, 700, 3
+    rows = [50, 9000, 4]
+    W, ro, idx, offs = _emb_case(T, B, rows, D, L, skew, seed=1)
+    W, ro, idx, offs = (x.to(DEV) for x in (W, ro, idx, offs))
+    goff = torch.tensor([t * D for t in range(T)], device=DEV)
+    grad = torch.randn(B * T * D, device=DEV)
+    hyper = torch.tensor([0.05, 3.0], device=DEV)
+
+    def states():
+        s1 = s2 = dg = None
+        if opt == ops.EMB_ROWWISE_ADAGRAD:
+            s1 = torch.rand(W.shape[0], device=DEV)
+        elif opt in (ops.EMB_ADAGRAD, ops.EMB_ADAM):
+            s1 = torch.rand(W.numel(), device=DEV)
+        if opt == ops.EMB_ADAM:
+            s2 = torch.rand(W.numel(), device=DEV)
+        if opt == ops.EMB_DENSE_GRAD:
+            dg = torch.zeros(W.numel(), device=DEV)
+        return s1, s2, dg
+
+    s1, s2, dg = states()
+    Wn = W.clone()
+    e1 = s1.clone() if s1 is not None else None
+    e2 = s2.clone() if s2 is not None else None
+    edg = dg.clone() if dg is not None else None
+    ops.embedding_bwd(Wn, ro, idx, offs, goff, T, B, grad, T * D, opt, hyper, state1=s1,
+                      state2=s2, weight_decay=0.01, dense_grad=dg)
+    We = W.clone()
+    ref.embedding_bwd(We, ro, idx, offs, goff, None, T, B, False, 20, grad, T * D, opt, e1, e2,
+                      hyper, 1e-8, 0.9, 0.999, 0.01, edg)
+    torch.cuda.synchronize()
+    assert (Wn - We).abs().max() < 1e-4 * max(1.0, We.abs().max().item())
+    if s1 is not None:
+        assert (s1 - e1).abs().max() < 1e-3 * max(1.0, e1.abs().max().item())
+    if dg is not None:
+        assert (dg - edg).abs().max() < 1e-4 * max(1.0, edg.abs().max().item())
+
+
+def test_embedding_bwd_deterministic():
+    T, B, D = 2, 4096, 128
+    rows = [3, 100000]
+    W, ro, idx, offs = _emb_case(T, B, rows, D, 4, True, seed=5)
+    W, ro, idx, offs = (x.to(DEV) for x in (W, ro, idx, offs))
+    goff = torch.tensor([0, D], device=DEV)
+    grad = torch.randn(B * T * D, device=DEV)
+    hyper = torch.tensor([0.1, 1.0], device=DEV)
+    outs = []
+    for _ in range(2):
+        Wn = W.clone()
+        s1 = torch.zeros(W.shape[0], device=DEV)
+        ops.embedding_bwd(Wn, ro, idx, offs, goff, T, B, grad, T * D, ops.EMB_ROWWISE_ADAGRAD,
+                          hyper, state1=s1)
+        outs.append(Wn)
+    assert torch.equal(outs[0], outs[1])
+
+
+# ------------------------------------------------------------ loss/optim
+@pytest.mark.parametrize("K", [64, 256])
+def test_head_bce(K):
+    torch.manual_seed(4)
+    B = 1000
+    H = bf(torch.randn(B, K, device=DEV))
+    w = torch.randn(K, device=DEV)
+    b = torch.randn(1, device=DEV)
+    y = (torch.rand(B, device=DEV) > 0.5).float()
+    np_ = ops.head_parts(B)
+    logits = torch.empty(B, device=DEV)
+    dH = torch.empty_like(H)
+    part = torch.empty(np_ * (K + 2), device=DEV)
+    ops.head_bce(H, w, b, y, 1.0 / B, True, logits, dH, part)
+    red = torch.empty(K + 2, device=DEV)
+    ops.reduce_rows(part, np_, K + 2, K + 2, red)
+    el, edH, ep = torch.empty_like(logits), torch.empty_like(dH), torch.zeros(np_ * (K + 2), device=DEV)
+    ref.head_bce(H, w, b, y, 1.0 / B, True, el, edH, ep)
+    assert rel_err(logits, el) < 1e-4
+    assert rel_err(dH, edH) < 1e-2
+    assert rel_err(red, ep[: K + 2]) < 1e-4
+
+
+def test_colsum_reduce():
+    x = bf(torch.randn(1000, 512, device=DEV))
+    out = torch.empty(512, device=DEV)
+    ops.colsum(x, out)
+    assert rel_err(out, x.float().sum(0)) < 1e-4
+
+
+@pytest.mark.parametrize("opt", [ops.OPT_ADAMW, ops.OPT_ADAM, ops.OPT_SGD, ops.OPT_ADAGRAD])
+def test_dense_optimizer(opt):
+    n = 4096 + 64
+    p = torch.randn(n, device=DEV)
+    g = torch.randn(n, device=DEV)
+    m = torch.rand(n, device=DEV)
+    v = torch.rand(n, device=DEV)
+    hyper = torch.tensor([1e-2, 5.0, 0.5], device=DEV)
+    pb = torch.empty(n, dtype=torch.bfloat16, device=DEV)
+    P, M, V = p.clone(), m.clone(), v.clone()
+    ops.dense_optimizer(p, g, m, v, pb, opt, hyper, wd=0.01, momentum=0.9 if opt == ops.OPT_SGD else 0.0)
+    ref.dense_optimizer(P, g, M, V, None, opt, hyper, 0.9, 0.999, 1e-8, 0.01,
+                        0.9 if opt == ops.OPT_SGD else 0.0, None)
+    assert (p - P).abs().max() < 1e-5
+    assert torch.equal(pb, p.to(torch.bfloat16))
+
+
+def test_auc_hist():
+    logits = torch.randn(10000, device=DEV)
+    y = (torch.rand(10000, device=DEV) < torch.sigmoid(logits)).float()
+    h = torch.zeros(2 * 200, dtype=torch.long, device=DEV)
+    ops.auc_hist(logits, y, 200, h)
+    e = torch.zeros_like(h)
+    ref.auc_hist(logits, y, 200, e)
+    assert torch.equal(h, e)
+    assert abs(ref.hist_auc(h) - ref.exact_auc(logits, y)) < 5e-3
+
+
+# ---------------------------------------------------------- end-to-end
+def test_dlrm_step_matches_cpu():
+    from tdfo_amd.data.synthetic import SyntheticCriteo
+    from tdfo_amd.models.dlrm import DLRMConfig, DLRMTrainer
+
+    cfg = DLRMConfig(embedding_dim=64, table_rows=[1000, 20, 5000, 300, 3], bottom=[128, 64],
+                     top=[128, 64, 1], dense_lr=3e-3, emb_lr=0.05)
+    B = 256
+    gpu = DLRMTrainer(cfg, B, DEV)
+    cpu = DLRMTrainer(cfg, B, "cpu")
+    cpu.emb.tw_store.weight.copy_(gpu.emb.tw_store.weight.cpu())
+    cpu.fp.p.copy_(gpu.fp.p.cpu())
+    cpu.fp.sync_bf16()
+    data = SyntheticCriteo(cfg.table_rows, B, device="cpu", seed=3)
+    lg, lc = [], []
+    for _ in range(20):
+        batch = data.next()
+        gpu.load_batch(*(x.to(DEV) for x in batch))
+        cpu.load_batch(*batch)
+        gpu.step()
+        cpu.step()
+        lg.append(gpu.pop_loss() / B)
+        lc.append(cpu.pop_loss() / B)
+    for a, b in zip(lg, lc):
+        assert abs(a - b) < 0.02, (lg, lc)
+    assert sum(lg[-5:]) < sum(lg[:5])
+
+
+def test_dlrm_graph_replay_matches_eager():
+    from tdfo_amd.data.synthetic import SyntheticCriteo
+    from tdfo_amd.models.dlrm import DLRMConfig, DLRMTrainer
+
+    cfg = DLRMConfig(embedding_dim=128, table_rows=[1000, 20, 5000], bottom=[128],
+                     top=[256, 1])
+    B = 512
+    a = DLRMTrainer(cfg, B, DEV)
+    b = DLRMTrainer(cfg, B, DEV)
+    data = SyntheticCriteo(cfg.table_rows, B, device=DEV, seed=4)
+    batches = [data.next() for _ in range(6)]
+    for t in (a, b):
+        t.load_batch(*batches[0])
+    b.capture_graph(warmup=1)
+    a.step()  # replicate the capture warmup on the eager trainer
+    for x in batches[1:]:
+        a.load_batch(*x)
+        b.load_batch(*x)
+        a.step()
+        b.step()
+    torch.cuda.synchronize()
+    assert torch.allclose(a.fp.p, b.fp.p, atol=1e-5)
