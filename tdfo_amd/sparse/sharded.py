@@ -316,6 +316,33 @@ class ShardedEmbeddingBags:
         del nrw
 
     # -------------------------------------------------------------- state
+    def _local_slices(self, t: int):
+        """(store, local_table_index, row_start, row_stop) of table t here, or None."""
+        if t in self.tw_mine:
+            return self.tw_store, self.tw_mine.index(t), 0, self.tables[t].num_embeddings
+        if t in self.rw_tables:
+            j = self.rw_tables.index(t)
+            blk = self.rw_block_host[j]
+            lo = min(self.rank * blk, self.tables[t].num_embeddings)
+            hi = min(lo + blk, self.tables[t].num_embeddings)
+            return self.rw_store, j, lo, hi
+        return None
+
+    def set_table_weight(self, t: int, full: torch.Tensor):
+        """Copy this rank's part of table ``t`` from the full [rows, D] tensor."""
+        sl = self._local_slices(t)
+        if sl is not None and sl[3] > sl[2]:
+            store, i, lo, hi = sl
+            store.table_weight(i).copy_(full[lo:hi].to(store.weight.device))
+
+    def get_table_weight(self, t: int):
+        """This rank's (row_start, rows view) of table ``t``, or None."""
+        sl = self._local_slices(t)
+        if sl is None:
+            return None
+        store, i, lo, hi = sl
+        return lo, store.table_weight(i)
+
     def state_dict(self):
         d = {"tw": self.tw_store.state_dict()}
         if self.rw_tables:
@@ -326,3 +353,4 @@ class ShardedEmbeddingBags:
         self.tw_store.load_state_dict(d["tw"])
         if self.rw_tables:
             self.rw_store.load_state_dict(d["rw"])
+
