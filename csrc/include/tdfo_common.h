@@ -9,6 +9,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <stdexcept>
+#include <string>
+
 #define TDFO_LDS __attribute__((address_space(3)))
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
@@ -56,11 +59,14 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 
 }  // namespace tdfo
 
+// Host-side HIP errors are fatal for the op: throw, so torch raises a Python
+// error instead of launching dependent kernels on garbage.
 #define TDFO_CHECK_HIP(expr)                                                   \
   do {                                                                         \
     hipError_t _e = (expr);                                                    \
     if (_e != hipSuccess) {                                                    \
-      fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(_e),        \
-              __FILE__, __LINE__);                                             \
+      throw std::runtime_error(std::string("HIP error ") +                     \
+                               hipGetErrorString(_e) + " at " + __FILE__ +     \
+                               ":" + std::to_string(__LINE__));                \
     }                                                                          \
   } while (0)

@@ -13,14 +13,17 @@
 // MI355X and are order-dependent) and load-balanced under skew
 // (cdna_hip_programming.md Appendix B "Scatter / gather / embedding"):
 //   keys   : key = row_offset[t] + id, val = position, bag_of[position]
-//   sort   : hipcub radix sort on the key bits actually used
+//   sort   : rocprim onesweep radix sort on the key bits actually used
+//            (32-bit keys whenever the shard has < 2^32 rows)
 //   chunks : each wave reduces a fixed 32-entry chunk of the sorted list; runs
 //            fully inside the chunk are finished (optimizer applied) in place,
 //            runs crossing a chunk edge leave fp32 partials (head/tail slabs)
 //   combine: the chunk where a crossing run starts adds the following chunks'
 //            head partials in order and applies the optimizer once.
 // Every unique row is updated exactly once per step, in a fixed order.
-#include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
+
+#include <type_traits>
 
 #include "tdfo_common.h"
 #include "tdfo_kernels.h"
@@ -81,256 +84,428 @@ __global__ __launch_bounds__(256) void emb_fwd_kernel(EmbFwdArgs a) {
 }
 
 // ---------------------------------------------------------- backward ----
-constexpr int CH = 32;  // sorted entries per chunk (one wave)
+template <int D>
+struct BwdCfg {
+  static constexpr int EPL = D >= 64 ? D / 64 : 1;                  // elements per lane
+  static constexpr int CH = EPL <= 2 ? 32 : (EPL == 4 ? 16 : 8);    // entries per wave
+};
 
-__global__ void emb_keys_kernel(const int64_t* __restrict__ row_offset,
-                                const int64_t* __restrict__ indices,
-                                const int64_t* __restrict__ offsets, int T,
-                                int B, uint64_t* __restrict__ keys,
-                                int32_t* __restrict__ vals,
-                                int32_t* __restrict__ bag_of) {
-  const int64_t nbags = (int64_t)T * B;
+// keys[p] = row_offset[t] + id, vals[p] = p, goff[p] = offset of p's pooled
+// gradient row, gscale[p] = per-id scale (psw, 1/len for mean) if needed.
+template <typename K>
+__global__ void emb_keys_kernel(const EmbBwdArgs a, K* __restrict__ keys,
+                                int32_t* __restrict__ vals, int64_t* __restrict__ goff,
+                                float* __restrict__ gscale, int32_t* __restrict__ tail_count) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *tail_count = 0;  // read by later kernels
+  const int64_t nbags = (int64_t)a.T * a.B;
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nbags;
        j += (int64_t)gridDim.x * blockDim.x) {
-    const int t = (int)(j / B);
-    const int64_t ro = row_offset[t];
-    for (int64_t p = offsets[j]; p < offsets[j + 1]; ++p) {
-      keys[p] = (uint64_t)(ro + indices[p]);
+    const int t = (int)(j / a.B);
+    const int b = (int)(j - (int64_t)t * a.B);
+    const int64_t ro = a.row_offset[t];
+    const int64_t go = (int64_t)b * a.grad_stride + a.grad_off[t];
+    const int64_t s0 = a.offsets[j], s1 = a.offsets[j + 1];
+    const float inv = (a.mean && s1 > s0) ? 1.f / (float)(s1 - s0) : 1.f;
+    for (int64_t p = s0; p < s1; ++p) {
+      keys[p] = (K)(ro + a.indices[p]);
       vals[p] = (int32_t)p;
-      bag_of[p] = (int32_t)j;
+      goff[p] = go;
+      if (gscale) gscale[p] = (a.psw ? a.psw[p] : 1.f) * inv;
     }
   }
 }
-
-template <int D>
-struct RowAcc {
-  static constexpr int EPL = D >= 64 ? D / 64 : 1;  // elements per lane
-  float v[EPL];
-};
 
 template <int D>
 __device__ __forceinline__ int elem0(int lane) {
   return D >= 64 ? lane * (D / 64) : lane;
 }
 
-template <int D>
-__device__ __forceinline__ void acc_grad(RowAcc<D>& acc, const EmbBwdArgs& a,
-                                         int bag, float scale, int lane) {
-  const int t = bag / a.B, b = bag - t * a.B;
-  const int64_t o = (int64_t)b * a.grad_stride + a.grad_off[t];
-  const int e0 = elem0<D>(lane);
-  if (D < 64 && e0 >= D) return;
-  if (a.grad_bf16) {
-    const uint16_t* g = (const uint16_t*)a.grad + o + e0;
-    if constexpr (RowAcc<D>::EPL == 2) {
-      const uint32_t u = *(const uint32_t*)g;
-      acc.v[0] += scale * bf2f((uint16_t)(u & 0xffff));
-      acc.v[1] += scale * bf2f((uint16_t)(u >> 16));
-    } else {
-#pragma unroll
-      for (int u = 0; u < RowAcc<D>::EPL; ++u) acc.v[u] += scale * bf2f(g[u]);
-    }
+template <typename K>
+__device__ __forceinline__ K rdlane(K v, int l) {
+  if constexpr (sizeof(K) == 4) {
+    return (K)__builtin_amdgcn_readlane((uint32_t)v, l);
   } else {
-    const float* g = (const float*)a.grad + o + e0;
-#pragma unroll
-    for (int u = 0; u < RowAcc<D>::EPL; ++u) acc.v[u] += scale * g[u];
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, l);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)((uint64_t)v >> 32), l);
+    return (K)(((uint64_t)hi << 32) | lo);
   }
 }
 
+__device__ __forceinline__ float rdlanef(float v, int l) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+
 template <int D>
-__device__ __forceinline__ void apply_update(const EmbBwdArgs& a, uint64_t row,
-                                             const RowAcc<D>& acc, int lane) {
-  constexpr int EPL = RowAcc<D>::EPL;
+__device__ __forceinline__ void load_row(float (&wv)[BwdCfg<D>::EPL], const float* w) {
+  constexpr int EPL = BwdCfg<D>::EPL;
+  if constexpr (EPL == 2) {
+    const float2 v = *(const float2*)w; wv[0] = v.x; wv[1] = v.y;
+  } else if constexpr (EPL == 4) {
+    const float4 v = *(const float4*)w; wv[0] = v.x; wv[1] = v.y; wv[2] = v.z; wv[3] = v.w;
+  } else if constexpr (EPL == 8) {
+    const float4 v0 = *(const float4*)w, v1 = *(const float4*)(w + 4);
+    wv[0] = v0.x; wv[1] = v0.y; wv[2] = v0.z; wv[3] = v0.w;
+    wv[4] = v1.x; wv[5] = v1.y; wv[6] = v1.z; wv[7] = v1.w;
+  } else {
+    wv[0] = w[0];
+  }
+}
+
+// raw gradient row slice (bf16 or fp32), branch-free
+template <int D, bool GB>
+struct GradRaw {
+  using T = typename std::conditional<GB, uint16_t, float>::type;
+  T v[BwdCfg<D>::EPL];
+};
+
+template <int D, bool GB>
+__device__ __forceinline__ void load_grad_raw(GradRaw<D, GB>& r, const void* grad, int64_t off) {
+  constexpr int EPL = BwdCfg<D>::EPL;
+  if constexpr (GB) {
+    const uint16_t* gp = (const uint16_t*)grad + off;
+    if constexpr (EPL == 2) {
+      const uint32_t v = *(const uint32_t*)gp;
+      r.v[0] = (uint16_t)(v & 0xffff); r.v[1] = (uint16_t)(v >> 16);
+    } else if constexpr (EPL == 4) {
+      const uint2 v = *(const uint2*)gp;
+      r.v[0] = (uint16_t)(v.x & 0xffff); r.v[1] = (uint16_t)(v.x >> 16);
+      r.v[2] = (uint16_t)(v.y & 0xffff); r.v[3] = (uint16_t)(v.y >> 16);
+    } else if constexpr (EPL == 8) {
+      const uint4 v = *(const uint4*)gp;
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        r.v[2 * q] = (uint16_t)(w[q] & 0xffff); r.v[2 * q + 1] = (uint16_t)(w[q] >> 16);
+      }
+    } else {
+      r.v[0] = gp[0];
+    }
+  } else {
+    const float* gp = (const float*)grad + off;
+#pragma unroll
+    for (int u = 0; u < EPL; ++u) r.v[u] = gp[u];
+  }
+}
+
+template <int D, bool GB>
+__device__ __forceinline__ float raw_f(const GradRaw<D, GB>& r, int u) {
+  if constexpr (GB) return bf2f(r.v[u]);
+  else return r.v[u];
+}
+
+struct OptScalars { float lr, bc1, bc2; };
+
+__device__ __forceinline__ OptScalars opt_scalars(const EmbBwdArgs& a) {
+  OptScalars o;
+  o.lr = a.hyper[0];
+  const float step = a.hyper[1];
+  o.bc1 = 1.f - powf(a.beta1, step);
+  o.bc2 = 1.f - powf(a.beta2, step);
+  return o;
+}
+
+// One optimizer update of one row; `wv` = current weights (prefetched).
+template <int D, int OPT>
+__device__ __forceinline__ void update_row(const EmbBwdArgs& a, const OptScalars& o,
+                                           uint64_t row, const float (&acc)[BwdCfg<D>::EPL],
+                                           float (&wv)[BwdCfg<D>::EPL], float st_row, int lane) {
+  constexpr int EPL = BwdCfg<D>::EPL;
   const int e0 = elem0<D>(lane);
   const bool act = D >= 64 || e0 < D;
-  const float lr = a.hyper[0];
   float* w = a.W + row * D + e0;
-  float g[EPL], wv[EPL];
+  if constexpr (OPT == EMB_DENSE_GRAD) {
+    float* dg = a.dense_grad + row * D + e0;
 #pragma unroll
-  for (int u = 0; u < EPL; ++u) {
-    wv[u] = act ? w[u] : 0.f;
-    g[u] = acc.v[u];
-  }
-  switch (a.opt) {
-    case EMB_SGD:
+    for (int u = 0; u < EPL; ++u) if (act) dg[u] += acc[u];
+    return;
+  } else {
+    if constexpr (OPT == EMB_SGD) {
 #pragma unroll
-      for (int u = 0; u < EPL; ++u) wv[u] -= lr * (g[u] + a.weight_decay * wv[u]);
-      break;
-    case EMB_ROWWISE_ADAGRAD: {
-      float sq = 0.f;
+      for (int u = 0; u < EPL; ++u) wv[u] -= o.lr * (acc[u] + a.weight_decay * wv[u]);
+    } else if constexpr (OPT == EMB_ROWWISE_ADAGRAD) {
+      float g[EPL], sq = 0.f;
 #pragma unroll
       for (int u = 0; u < EPL; ++u) {
-        g[u] += a.weight_decay * wv[u];
+        g[u] = acc[u] + a.weight_decay * wv[u];
         sq += act ? g[u] * g[u] : 0.f;
       }
-      sq = wave_sum(sq) / (float)D;
-      const float st = a.state1[row] + sq;
-      if (lane == 0) a.state1[row] = st;
-      const float mult = lr / (sqrtf(st) + a.eps);
+      sq = wave_sum(sq) * (1.f / (float)D);
+      const float stv = st_row + sq;
+      if (lane == 0) a.state1[row] = stv;
+      const float mult = o.lr / (sqrtf(stv) + a.eps);
 #pragma unroll
       for (int u = 0; u < EPL; ++u) wv[u] -= mult * g[u];
-      break;
-    }
-    case EMB_ADAGRAD: {
-      float* st = a.state1 + row * D + e0;
+    } else if constexpr (OPT == EMB_ADAGRAD) {
+      float* stp = a.state1 + row * D + (act ? e0 : 0);
 #pragma unroll
       for (int u = 0; u < EPL; ++u) {
-        if (!act) break;
-        const float gg = g[u] + a.weight_decay * wv[u];
-        const float s2 = st[u] + gg * gg;
-        st[u] = s2;
-        wv[u] -= lr * gg / (sqrtf(s2) + a.eps);
+        const float gg = acc[u] + a.weight_decay * wv[u];
+        const float s2 = stp[u] + gg * gg;
+        if (act) stp[u] = s2;
+        wv[u] -= o.lr * gg / (sqrtf(s2) + a.eps);
       }
-      break;
-    }
-    case EMB_ADAM: {
-      // decoupled weight decay, bias-corrected (fbgemm-style fused Adam)
-      const float step = a.hyper[1];
-      const float bc1 = 1.f - powf(a.beta1, step), bc2 = 1.f - powf(a.beta2, step);
-      float* m = a.state1 + row * D + e0;
-      float* v = a.state2 + row * D + e0;
+    } else {  // EMB_ADAM, decoupled weight decay, bias-corrected (fbgemm-style)
+      float* m = a.state1 + row * D + (act ? e0 : 0);
+      float* v = a.state2 + row * D + (act ? e0 : 0);
 #pragma unroll
       for (int u = 0; u < EPL; ++u) {
-        if (!act) break;
-        const float mm = a.beta1 * m[u] + (1.f - a.beta1) * g[u];
-        const float vv = a.beta2 * v[u] + (1.f - a.beta2) * g[u] * g[u];
-        m[u] = mm; v[u] = vv;
-        wv[u] -= lr * ((mm / bc1) / (sqrtf(vv / bc2) + a.eps) + a.weight_decay * wv[u]);
+        const float mm = a.beta1 * m[u] + (1.f - a.beta1) * acc[u];
+        const float vv = a.beta2 * v[u] + (1.f - a.beta2) * acc[u] * acc[u];
+        if (act) { m[u] = mm; v[u] = vv; }
+        wv[u] -= o.lr * ((mm / o.bc1) / (sqrtf(vv / o.bc2) + a.eps) + a.weight_decay * wv[u]);
       }
-      break;
     }
-    case EMB_DENSE_GRAD: {
-      float* dg = a.dense_grad + row * D + e0;
+    if (act) {
+      if constexpr (EPL == 2) {
+        *(float2*)w = make_float2(wv[0], wv[1]);
+      } else if constexpr (EPL == 4) {
+        *(float4*)w = make_float4(wv[0], wv[1], wv[2], wv[3]);
+      } else {
 #pragma unroll
-      for (int u = 0; u < EPL; ++u) if (act) dg[u] += g[u];
-      return;
+        for (int u = 0; u < EPL; ++u) w[u] = wv[u];
+      }
     }
   }
-#pragma unroll
-  for (int u = 0; u < EPL; ++u) if (act) w[u] = wv[u];
 }
 
-__device__ __forceinline__ uint64_t readlane64(uint64_t v, int l) {
-  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)v, l);
-  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(v >> 32), l);
-  return ((uint64_t)hi << 32) | lo;
-}
-
-template <int D>
+// One wave = one chunk of CH sorted entries. Every gradient row of the chunk
+// and every weight row it may update are loaded up front with no control
+// flow between the loads (hipcc keeps all of them in flight); runs are then
+// reduced in registers in sorted order and each run that finishes inside the
+// chunk gets exactly one optimizer update.
+template <int D, typename K, bool GB, int OPT>
 __global__ __launch_bounds__(256) void emb_chunk_kernel(
-    EmbBwdArgs a, const uint64_t* __restrict__ keys,
-    const int32_t* __restrict__ vals, const int32_t* __restrict__ bag_of,
-    float* __restrict__ head, float* __restrict__ tail) {
-  constexpr int EPL = RowAcc<D>::EPL;
+    EmbBwdArgs a, const K* __restrict__ keys, const int32_t* __restrict__ vals,
+    const int64_t* __restrict__ goff, const float* __restrict__ gscale,
+    float* __restrict__ head, float* __restrict__ tail, int32_t* __restrict__ tail_list,
+    int32_t* __restrict__ tail_count) {
+  constexpr int EPL = BwdCfg<D>::EPL, CH = BwdCfg<D>::CH;
+  constexpr bool NEED_W = OPT != EMB_DENSE_GRAD;
   const int lane = threadIdx.x & 63;
   const int64_t c = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t start = c * CH;
   if (start >= a.nnz) return;
+  const OptScalars o = opt_scalars(a);
   const int64_t end = min(start + (int64_t)CH, a.nnz);
   const int len = (int)(end - start);
-  uint64_t mykey = 0; int mypos = 0;
-  if (lane < len) { mykey = keys[start + lane]; mypos = vals[start + lane]; }
-  const uint64_t first = readlane64(mykey, 0);
-  const bool from_before = start > 0 && keys[start - 1] == first;
-  const bool continues = end < a.nnz && keys[end] == readlane64(mykey, len - 1);
-
-  RowAcc<D> acc;
-#pragma unroll
-  for (int u = 0; u < EPL; ++u) acc.v[u] = 0.f;
-  uint64_t cur = first;
-  bool started_here = !from_before;
+  const int li = lane < len ? lane : len - 1;     // lanes >= len duplicate the last entry
+  const K mykey = keys[start + li];
+  const int mypos = vals[start + li];
+  const int64_t mygoff = goff[mypos];
+  const float mysc = gscale ? gscale[mypos] : 1.f;
+  const K prevk = start > 0 ? keys[start - 1] : (K)0;
+  const K nextk = end < a.nnz ? keys[end] : (K)0;
+  const K kup = __shfl_up(mykey, 1, 64);
+  const K kdn = __shfl_down(mykey, 1, 64);
+  const bool is_start = lane < len && (lane == 0 ? (start == 0 || prevk != mykey) : kup != mykey);
+  const bool is_end = lane < len && (lane == len - 1 ? (end == a.nnz || nextk != mykey)
+                                                     : kdn != mykey);
+  const uint64_t smask = __ballot(is_start), emask = __ballot(is_end);
+  const bool from_before = !(smask & 1ull);
+  uint64_t fmask = emask;                                     // runs finishing here
+  if (from_before && emask) fmask &= ~(emask & (~emask + 1));  // first run is not ours
+  const float st_l = OPT == EMB_ROWWISE_ADAGRAD ? a.state1[(uint64_t)mykey] : 0.f;
   const int e0 = elem0<D>(lane);
-  for (int p = 0; p < len; ++p) {
-    const uint64_t k = readlane64(mykey, p);
-    if (k != cur) {
-      if (started_here) {
-        apply_update<D>(a, cur, acc, lane);
-      } else if (D >= 64 || e0 < D) {
+  const bool act = D >= 64 || e0 < D;
+  const int e0c = act ? e0 : 0;
+
+  GradRaw<D, GB> g[CH];
+  float wr[CH][EPL];
 #pragma unroll
-        for (int u = 0; u < EPL; ++u) head[c * D + e0 + u] = acc.v[u];
+  for (int p = 0; p < CH; ++p) {
+    const int64_t go = (int64_t)rdlane((uint64_t)mygoff, p);
+    load_grad_raw<D, GB>(g[p], a.grad, go + e0c);
+    if constexpr (NEED_W) load_row<D>(wr[p], a.W + (uint64_t)rdlane(mykey, p) * D + e0c);
+  }
+  float acc[EPL];
+#pragma unroll
+  for (int u = 0; u < EPL; ++u) acc[u] = 0.f;
+#pragma unroll
+  for (int p = 0; p < CH; ++p) {
+    if (p < len) {
+      const float sc = rdlanef(mysc, p);
+#pragma unroll
+      for (int u = 0; u < EPL; ++u) acc[u] += sc * raw_f<D, GB>(g[p], u);
+      if ((emask >> p) & 1ull) {
+        if ((fmask >> p) & 1ull) {
+          float wv[EPL];
+#pragma unroll
+          for (int u = 0; u < EPL; ++u) wv[u] = NEED_W ? wr[p][u] : 0.f;
+          update_row<D, OPT>(a, o, (uint64_t)rdlane(mykey, p), acc, wv, rdlanef(st_l, p), lane);
+        } else if (act) {
+#pragma unroll
+          for (int u = 0; u < EPL; ++u) head[c * D + e0 + u] = acc[u];
+        }
+#pragma unroll
+        for (int u = 0; u < EPL; ++u) acc[u] = 0.f;
       }
-#pragma unroll
-      for (int u = 0; u < EPL; ++u) acc.v[u] = 0.f;
-      cur = k;
-      started_here = true;
     }
-    const int pos = __builtin_amdgcn_readlane(mypos, p);
-    const int bag = bag_of[pos];
-    float scale = a.psw ? a.psw[pos] : 1.f;
-    if (a.mean) scale /= (float)(a.offsets[bag + 1] - a.offsets[bag]);
-    acc_grad<D>(acc, a, bag, scale, lane);
   }
-  float* dst = nullptr;
-  if (!continues) {
-    if (started_here) apply_update<D>(a, cur, acc, lane);
-    else dst = head + c * D;
-  } else {
-    dst = (started_here ? tail : head) + c * D;
-  }
-  if (dst && (D >= 64 || e0 < D)) {
+  if (!((emask >> (len - 1)) & 1ull)) {                       // last run continues
+    const bool started_here = smask != 0;
+    if (act) {
+      float* dst = (started_here ? tail : head) + c * D + e0;
 #pragma unroll
-    for (int u = 0; u < EPL; ++u) dst[e0 + u] = acc.v[u];
+      for (int u = 0; u < EPL; ++u) dst[u] = acc[u];
+    }
+    if (started_here && lane == 0) {
+      const int slot = atomicAdd(tail_count, 1);
+      if (slot < (int)((a.nnz + CH - 1) / CH)) tail_list[slot] = (int32_t)c;
+    }
   }
 }
 
-template <int D>
+// Runs crossing chunk edges: the chunk where a run starts adds the head
+// partials of the chunks the run covers (found by binary search), in chunk
+// order with 8 loads in flight, and applies the optimizer once.
+template <int D, typename K, int OPT>
 __global__ __launch_bounds__(256) void emb_combine_kernel(
-    EmbBwdArgs a, const uint64_t* __restrict__ keys,
-    const float* __restrict__ head, const float* __restrict__ tail) {
-  constexpr int EPL = RowAcc<D>::EPL;
+    EmbBwdArgs a, const K* __restrict__ keys, const float* __restrict__ head,
+    const float* __restrict__ tail, const int32_t* __restrict__ tail_list,
+    const int32_t* __restrict__ tail_count) {
+  constexpr int EPL = BwdCfg<D>::EPL, CH = BwdCfg<D>::CH;
   const int lane = threadIdx.x & 63;
-  const int64_t c = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int64_t start = c * CH;
-  if (start >= a.nnz) return;
-  const int64_t end = min(start + (int64_t)CH, a.nnz);
-  if (end >= a.nnz) return;
-  const uint64_t last = keys[end - 1];
-  if (keys[end] != last) return;                    // no run leaves this chunk
-  // keys are sorted: keys[start-1] == last means the whole chunk is a middle
-  // piece of a run owned by an earlier chunk
-  if (start > 0 && keys[start - 1] == last) return;
+  const int nw = (gridDim.x * blockDim.x) >> 6;
+  const int n = min(*tail_count, (int)((a.nnz + CH - 1) / CH));
   const int e0 = elem0<D>(lane);
   const bool act = D >= 64 || e0 < D;
-  RowAcc<D> acc;
+  const int e0c = act ? e0 : 0;
+  const OptScalars o = opt_scalars(a);
+  for (int i = ((blockIdx.x * blockDim.x + threadIdx.x) >> 6); i < n; i += nw) {
+    const int64_t c = tail_list[i];
+    const int64_t endc = min((c + 1) * CH, a.nnz);
+    const K last = keys[endc - 1];
+    float acc[EPL];
 #pragma unroll
-  for (int u = 0; u < EPL; ++u) acc.v[u] = act ? tail[c * D + e0 + u] : 0.f;
-  int64_t j = c + 1;
-  while (true) {
+    for (int u = 0; u < EPL; ++u) acc[u] = act ? tail[c * D + e0 + u] : 0.f;
+    int64_t lo = endc, hi = a.nnz;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (keys[mid] == last) lo = mid + 1; else hi = mid;
+    }
+    const int64_t jlast = (lo - 1) / CH;
+    for (int64_t j0 = c + 1; j0 <= jlast; j0 += 8) {
+      float hv[8][EPL];
 #pragma unroll
-    for (int u = 0; u < EPL; ++u) if (act) acc.v[u] += head[j * D + e0 + u];
-    const int64_t ej = min((j + 1) * CH, a.nnz);
-    if (ej < a.nnz && keys[ej] == last) ++j;
-    else break;
+      for (int q = 0; q < 8; ++q) {
+        const int64_t j = min(j0 + q, jlast);
+#pragma unroll
+        for (int u = 0; u < EPL; ++u) hv[q][u] = head[j * D + e0c + u];
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        if (j0 + q <= jlast && act) {
+#pragma unroll
+          for (int u = 0; u < EPL; ++u) acc[u] += hv[q][u];
+        }
+      }
+    }
+    float wv[EPL];
+#pragma unroll
+    for (int u = 0; u < EPL; ++u) wv[u] = 0.f;
+    if constexpr (OPT != EMB_DENSE_GRAD) load_row<D>(wv, a.W + (uint64_t)last * D + e0c);
+    const float st = OPT == EMB_ROWWISE_ADAGRAD ? a.state1[(uint64_t)last] : 0.f;
+    update_row<D, OPT>(a, o, (uint64_t)last, acc, wv, st, lane);
   }
-  apply_update<D>(a, last, acc, lane);
 }
 
 struct WsLayout {
-  size_t keys_in, keys_out, vals_in, vals_out, bag_of, head, tail, cub, total;
-  size_t cub_bytes;
+  size_t keys_in, keys_out, vals_in, vals_out, goff, gscale, head, tail, tlist, tcount, cub;
+  size_t total, cub_bytes;
 };
 
 inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
 
+using SortCfg = rocprim::default_config;
+
+template <typename K>
+size_t sort_bytes(int64_t nnz) {
+  size_t b = 0;
+  rocprim::radix_sort_pairs<SortCfg>(nullptr, b, (K*)nullptr, (K*)nullptr, (int32_t*)nullptr,
+                                     (int32_t*)nullptr, (size_t)nnz, 0, (int)(8 * sizeof(K)));
+  return b;
+}
+
+int ch_for(int D) { return D <= 128 ? 32 : (D == 256 ? 16 : 8); }
+
 WsLayout ws_layout(int64_t nnz, int D) {
   WsLayout L;
-  const int64_t nch = (nnz + CH - 1) / CH;
-  size_t cub_bytes = 0;
-  hipcub::DeviceRadixSort::SortPairs(nullptr, cub_bytes, (uint64_t*)nullptr,
-                                     (uint64_t*)nullptr, (int32_t*)nullptr,
-                                     (int32_t*)nullptr, (int)nnz, 0, 64);
+  const int64_t nch = (nnz + ch_for(D) - 1) / ch_for(D);
+  const size_t b64 = sort_bytes<uint64_t>(nnz), b32 = sort_bytes<uint32_t>(nnz);
+  const size_t cub_bytes = b64 > b32 ? b64 : b32;
   size_t o = 0;
   L.keys_in = o;  o += al(nnz * 8);
   L.keys_out = o; o += al(nnz * 8);
   L.vals_in = o;  o += al(nnz * 4);
   L.vals_out = o; o += al(nnz * 4);
-  L.bag_of = o;   o += al(nnz * 4);
+  L.goff = o;     o += al(nnz * 8);
+  L.gscale = o;   o += al(nnz * 4);
   L.head = o;     o += al((size_t)nch * D * 4);
   L.tail = o;     o += al((size_t)nch * D * 4);
+  L.tlist = o;    o += al((size_t)nch * 4);
+  L.tcount = o;   o += al(16);
   L.cub = o;      o += al(cub_bytes);
   L.cub_bytes = cub_bytes;
   L.total = o;
   return L;
+}
+
+template <int D, typename K, int OPT>
+void bwd_impl(const EmbBwdArgs& a, const WsLayout& L, hipStream_t s) {
+  char* ws = (char*)a.workspace;
+  K* keys_in = (K*)(ws + L.keys_in);
+  K* keys_out = (K*)(ws + L.keys_out);
+  int32_t* vals_in = (int32_t*)(ws + L.vals_in);
+  int32_t* vals_out = (int32_t*)(ws + L.vals_out);
+  int64_t* goff = (int64_t*)(ws + L.goff);
+  float* gscale = (a.psw || a.mean) ? (float*)(ws + L.gscale) : nullptr;
+  float* head = (float*)(ws + L.head);
+  float* tail = (float*)(ws + L.tail);
+  int32_t* tlist = (int32_t*)(ws + L.tlist);
+  int32_t* tcount = (int32_t*)(ws + L.tcount);
+  const int64_t nbags = (int64_t)a.T * a.B;
+  int64_t kb = (nbags + 255) / 256;
+  if (kb > 4096) kb = 4096;
+  hipLaunchKernelGGL(emb_keys_kernel<K>, dim3(kb), dim3(256), 0, s, a, keys_in, vals_in, goff,
+                     gscale, tcount);
+  TDFO_CHECK_HIP(hipGetLastError());
+  size_t cub_bytes = L.cub_bytes;
+  TDFO_CHECK_HIP(rocprim::radix_sort_pairs<SortCfg>(ws + L.cub, cub_bytes, keys_in, keys_out,
+                                                    vals_in, vals_out, (size_t)a.nnz, 0,
+                                                    a.key_bits, s));
+  constexpr int CH = BwdCfg<D>::CH;
+  const int64_t nch = (a.nnz + CH - 1) / CH;
+  const int64_t blocks = (nch + 3) / 4;
+  if (a.grad_bf16)
+    hipLaunchKernelGGL((emb_chunk_kernel<D, K, true, OPT>), dim3(blocks), dim3(256), 0, s, a,
+                       keys_out, vals_out, goff, gscale, head, tail, tlist, tcount);
+  else
+    hipLaunchKernelGGL((emb_chunk_kernel<D, K, false, OPT>), dim3(blocks), dim3(256), 0, s, a,
+                       keys_out, vals_out, goff, gscale, head, tail, tlist, tcount);
+  TDFO_CHECK_HIP(hipGetLastError());
+  int64_t cblocks = (nch + 3) / 4;
+  if (cblocks > 1024) cblocks = 1024;
+  hipLaunchKernelGGL((emb_combine_kernel<D, K, OPT>), dim3(cblocks), dim3(256), 0, s, a,
+                     keys_out, head, tail, tlist, tcount);
+  TDFO_CHECK_HIP(hipGetLastError());
+}
+
+template <int D, typename K>
+void bwd_opt(const EmbBwdArgs& a, const WsLayout& L, hipStream_t s) {
+  switch (a.opt) {
+    case EMB_SGD: bwd_impl<D, K, EMB_SGD>(a, L, s); break;
+    case EMB_ROWWISE_ADAGRAD: bwd_impl<D, K, EMB_ROWWISE_ADAGRAD>(a, L, s); break;
+    case EMB_ADAM: bwd_impl<D, K, EMB_ADAM>(a, L, s); break;
+    case EMB_ADAGRAD: bwd_impl<D, K, EMB_ADAGRAD>(a, L, s); break;
+    case EMB_DENSE_GRAD: bwd_impl<D, K, EMB_DENSE_GRAD>(a, L, s); break;
+    default: throw std::runtime_error("unknown embedding optimizer");
+  }
+}
+
+template <int D>
+void bwd_dispatch(const EmbBwdArgs& a, const WsLayout& L, hipStream_t s) {
+  if (a.key_bits <= 32) bwd_opt<D, uint32_t>(a, L, s);
+  else bwd_opt<D, uint64_t>(a, L, s);
 }
 
 }  // namespace
@@ -365,40 +540,14 @@ size_t embedding_bwd_workspace(int64_t nnz, int D) {
 void embedding_bwd_fused(const EmbBwdArgs& a, hipStream_t s) {
   if (a.nnz <= 0) return;
   const WsLayout L = ws_layout(a.nnz, a.D);
-  char* ws = (char*)a.workspace;
-  uint64_t* keys_in = (uint64_t*)(ws + L.keys_in);
-  uint64_t* keys_out = (uint64_t*)(ws + L.keys_out);
-  int32_t* vals_in = (int32_t*)(ws + L.vals_in);
-  int32_t* vals_out = (int32_t*)(ws + L.vals_out);
-  int32_t* bag_of = (int32_t*)(ws + L.bag_of);
-  float* head = (float*)(ws + L.head);
-  float* tail = (float*)(ws + L.tail);
-
-  const int64_t nbags = (int64_t)a.T * a.B;
-  int64_t kb = (nbags + 255) / 256;
-  if (kb > 4096) kb = 4096;
-  hipLaunchKernelGGL(emb_keys_kernel, dim3(kb), dim3(256), 0, s, a.row_offset,
-                     a.indices, a.offsets, a.T, a.B, keys_in, vals_in, bag_of);
-  size_t cub_bytes = L.cub_bytes;
-  hipcub::DeviceRadixSort::SortPairs(ws + L.cub, cub_bytes, keys_in, keys_out,
-                                     vals_in, vals_out, (int)a.nnz, 0,
-                                     a.key_bits, s);
-  const int64_t nch = (a.nnz + CH - 1) / CH;
-  const int64_t blocks = (nch + 3) / 4;
-#define TDFO_EB(DD)                                                            \
-  hipLaunchKernelGGL(emb_chunk_kernel<DD>, dim3(blocks), dim3(256), 0, s, a,   \
-                     keys_out, vals_out, bag_of, head, tail);                  \
-  hipLaunchKernelGGL(emb_combine_kernel<DD>, dim3(blocks), dim3(256), 0, s, a, \
-                     keys_out, head, tail)
   switch (a.D) {
-    case 16: TDFO_EB(16); break;
-    case 32: TDFO_EB(32); break;
-    case 64: TDFO_EB(64); break;
-    case 128: TDFO_EB(128); break;
-    case 256: TDFO_EB(256); break;
-    case 512: TDFO_EB(512); break;
+    case 16: bwd_dispatch<16>(a, L, s); break;
+    case 32: bwd_dispatch<32>(a, L, s); break;
+    case 64: bwd_dispatch<64>(a, L, s); break;
+    case 128: bwd_dispatch<128>(a, L, s); break;
+    case 256: bwd_dispatch<256>(a, L, s); break;
+    case 512: bwd_dispatch<512>(a, L, s); break;
   }
-#undef TDFO_EB
 }
 
 }  // namespace tdfo

@@ -166,24 +166,68 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs p) {
     }
   }
 
-  // Epilogue. C/D map of 16x16x32: col = lane&15, row = 4*(lane>>4) + reg.
-  float* c32 = p.C32 ? p.C32 + (int64_t)blockIdx.z * p.M * p.ldc32 : nullptr;
+  // Epilogue: bias + ReLU in registers, then the 128x128 fp32 tile is staged
+  // through the (now idle) 64-KiB LDS ring so global traffic leaves as
+  // coalesced 16-B accesses (mask loads, bf16 stores, fp32 stores).
+  // C/D map of 16x16x32: col = lane&15, row = 4*(lane>>4) + reg.
+  float* ctile = (float*)smem_raw;   // [128][128] fp32, 16-B chunks XOR-swizzled
+  __syncthreads();
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int n = n0 + wc * 64 + j * 16 + (lane & 15);
-    if (n >= p.N) continue;
-    const float bias = p.bias ? p.bias[n] : 0.f;
+    const int cl = wc * 64 + j * 16 + (lane & 15);
+    const int n = n0 + cl;
+    const float bias = (p.bias && n < p.N) ? p.bias[n] : 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wr * 64 + i * 16 + 4 * (lane >> 4) + r;
-        if (m >= p.M) continue;
+        const int rl = wr * 64 + i * 16 + 4 * (lane >> 4) + r;
         float v = acc[i][j][r] + bias;
         if (p.relu) v = fmaxf(v, 0.f);
-        if (p.mask && !(bf2f(p.mask[(int64_t)m * p.ldm + n]) > 0.f)) v = 0.f;
-        if (p.C) p.C[(int64_t)m * p.ldc + n] = f2bf(v);
-        if (c32) c32[(int64_t)m * p.ldc32 + n] = v;
+        const int chunk = (cl >> 2) ^ (rl & 31);
+        ctile[rl * 128 + chunk * 4 + (cl & 3)] = v;
+      }
+    }
+  }
+  __syncthreads();
+  float* c32 = p.C32 ? p.C32 + (int64_t)blockIdx.z * p.M * p.ldc32 : nullptr;
+  const bool nfull = (n0 + BN <= p.N) && ((p.N & 7) == 0);
+#pragma unroll 2
+  for (int it = 0; it < 8; ++it) {
+    const int c = it * 256 + tid;          // 8-column group id in the tile
+    const int rl = c >> 4, cg = (c & 15) * 8;
+    const int m = m0 + rl;
+    if (m >= p.M) continue;
+    const float4 lo = *(const float4*)(ctile + rl * 128 + (((cg >> 2) ^ (rl & 31)) << 2));
+    const float4 hi = *(const float4*)(ctile + rl * 128 + ((((cg >> 2) + 1) ^ (rl & 31)) << 2));
+    float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    const int n = n0 + cg;
+    if (nfull || n + 8 <= p.N) {
+      if (p.mask) {
+        const uint4 mk = *(const uint4*)(p.mask + (int64_t)m * p.ldm + n);
+        const uint32_t mu[4] = {mk.x, mk.y, mk.z, mk.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (!(bf2f((uint16_t)(mu[q] & 0xffff)) > 0.f)) v[2 * q] = 0.f;
+          if (!(bf2f((uint16_t)(mu[q] >> 16)) > 0.f)) v[2 * q + 1] = 0.f;
+        }
+      }
+      if (p.C) {
+        *(uint4*)(p.C + (int64_t)m * p.ldc + n) =
+            make_uint4(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]),
+                       pack2bf(v[6], v[7]));
+      }
+      if (c32) {
+        float* o = c32 + (int64_t)m * p.ldc32 + n;
+        *(float4*)o = make_float4(v[0], v[1], v[2], v[3]);
+        *(float4*)(o + 4) = make_float4(v[4], v[5], v[6], v[7]);
+      }
+    } else {
+      for (int q = 0; q < 8 && n + q < p.N; ++q) {
+        float x = v[q];
+        if (p.mask && !(bf2f(p.mask[(int64_t)m * p.ldm + n + q]) > 0.f)) x = 0.f;
+        if (p.C) p.C[(int64_t)m * p.ldc + n + q] = f2bf(x);
+        if (c32) c32[(int64_t)m * p.ldc32 + n + q] = x;
       }
     }
   }
@@ -201,6 +245,7 @@ void launch(const GemmArgs& a, hipStream_t s) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   dim3 grid(tiles, 1, a.splits);
   hipLaunchKernelGGL((gemm_kernel<AC, BC>), grid, dim3(256), SMEM_BYTES, s, a);
+  TDFO_CHECK_HIP(hipGetLastError());
 }
 
 }  // namespace

@@ -217,6 +217,7 @@ void interaction_fwd(const uint16_t* dense, int64_t ld_dense,
     case 128: TDFO_IFWD(128); break;
     case 256: TDFO_IFWD(256); break;
   }
+  TDFO_CHECK_HIP(hipGetLastError());
 #undef TDFO_IFWD
 }
 
@@ -242,6 +243,7 @@ void interaction_bwd(const uint16_t* dz, int64_t ldz, const uint16_t* dense,
     case 128: TDFO_IBWD(128); break;
     case 256: TDFO_IBWD(256); break;
   }
+  TDFO_CHECK_HIP(hipGetLastError());
 #undef TDFO_IBWD
 }
 

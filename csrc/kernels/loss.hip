@@ -14,7 +14,7 @@
 namespace tdfo {
 namespace {
 
-constexpr int HEAD_SPB = 64;  // samples per block
+constexpr int HEAD_SPB = 16;  // samples per block (4 per wave)
 
 template <int K>
 __global__ __launch_bounds__(256) void head_bce_kernel(
@@ -70,40 +70,75 @@ __global__ __launch_bounds__(256) void head_bce_kernel(
         red[0][j] + red[1][j] + red[2][j] + red[3][j];
 }
 
-__global__ void reduce_rows_kernel(const float* __restrict__ in, int rows,
-                                   int64_t n, int64_t ld, float* __restrict__ out,
-                                   int accumulate, float scale) {
-  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n;
-       j += (int64_t)gridDim.x * blockDim.x) {
-    float s = 0.f;
-    for (int r = 0; r < rows; ++r) s += in[(int64_t)r * ld + j];
-    s *= scale;
-    out[j] = accumulate ? out[j] + s : s;
+// out[j] = sum_r in[r*ld + j]: COLS columns x (256/COLS) row phases per
+// block, fixed-order LDS combine (bitwise reproducible).
+template <int COLS>
+__global__ __launch_bounds__(256) void reduce_rows_kernel(
+    const float* __restrict__ in, int rows, int64_t n, int64_t ld,
+    float* __restrict__ out, int accumulate, float scale) {
+  constexpr int PH = 256 / COLS;
+  __shared__ float red[PH][COLS];
+  const int c = threadIdx.x % COLS, ph = threadIdx.x / COLS;
+  for (int64_t j0 = (int64_t)blockIdx.x * COLS; j0 < n; j0 += (int64_t)gridDim.x * COLS) {
+    const int64_t j = j0 + c;
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    if (j < n) {
+      int r = ph;
+      for (; r + 3 * PH < rows; r += 4 * PH) {
+        s0 += in[(int64_t)r * ld + j];
+        s1 += in[(int64_t)(r + PH) * ld + j];
+        s2 += in[(int64_t)(r + 2 * PH) * ld + j];
+        s3 += in[(int64_t)(r + 3 * PH) * ld + j];
+      }
+      for (; r < rows; r += PH) s0 += in[(int64_t)r * ld + j];
+    }
+    red[ph][c] = (s0 + s1) + (s2 + s3);
+    __syncthreads();
+    if (ph == 0 && j < n) {
+      float t = 0.f;
+#pragma unroll
+      for (int q = 0; q < PH; ++q) t += red[q][c];
+      t *= scale;
+      out[j] = accumulate ? out[j] + t : t;
+    }
+    __syncthreads();
   }
 }
 
-constexpr int COLSUM_RPB = 64;
+constexpr int COLSUM_CHUNKS = 16;
 
+// Column sums of a bf16 [M, N] matrix: block = 64 columns (8 x 16-B groups)
+// x 32 row phases over one of COLSUM_CHUNKS row chunks.
 __global__ __launch_bounds__(256) void colsum_kernel(const uint16_t* __restrict__ x,
                                                      int M, int N, int64_t ldx,
                                                      float* __restrict__ part) {
-  const int c0 = (blockIdx.x * 256 + threadIdx.x) * 8;
-  if (c0 >= N) return;
-  const int r0 = blockIdx.y * COLSUM_RPB;
-  const int r1 = min(M, r0 + COLSUM_RPB);
+  __shared__ float red[32][65];
+  const int cg = threadIdx.x & 7, ph = threadIdx.x >> 3;
+  const int c0 = blockIdx.x * 64 + cg * 8;
+  const int rows_per = (M + COLSUM_CHUNKS - 1) / COLSUM_CHUNKS;
+  const int r0 = blockIdx.y * rows_per;
+  const int r1 = min(M, r0 + rows_per);
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int r = r0; r < r1; ++r) {
-    const uint4 v = *(const uint4*)(x + (int64_t)r * ldx + c0);
-    const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+  if (c0 < N) {
+    for (int r = r0 + ph; r < r1; r += 32) {
+      const uint4 v = *(const uint4*)(x + (int64_t)r * ldx + c0);
+      const uint32_t u[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      acc[2 * q] += bf2f((uint16_t)(u[q] & 0xffff));
-      acc[2 * q + 1] += bf2f((uint16_t)(u[q] >> 16));
+      for (int q = 0; q < 4; ++q) {
+        acc[2 * q] += bf2f((uint16_t)(u[q] & 0xffff));
+        acc[2 * q + 1] += bf2f((uint16_t)(u[q] >> 16));
+      }
     }
   }
-  float* pp = part + (int64_t)blockIdx.y * N + c0;
 #pragma unroll
-  for (int q = 0; q < 8; ++q) pp[q] = acc[q];
+  for (int q = 0; q < 8; ++q) red[ph][cg * 8 + q] = acc[q];
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const int col = blockIdx.x * 64 + threadIdx.x;
+    float t = 0.f;
+    for (int q = 0; q < 32; ++q) t += red[q][threadIdx.x];
+    if (col < N) part[(int64_t)blockIdx.y * N + col] = t;
+  }
 }
 
 __global__ __launch_bounds__(256) void auc_hist_kernel(
@@ -149,18 +184,24 @@ void head_bce(const uint16_t* H, int64_t ldh, int B, int K, const float* w,
 void reduce_rows(const float* in, int rows, int64_t n, int64_t ld, float* out,
                  int accumulate, float scale, hipStream_t s) {
   if (n <= 0) return;
-  int64_t blocks = (n + 255) / 256;
-  if (blocks > 4096) blocks = 4096;
-  hipLaunchKernelGGL(reduce_rows_kernel, dim3(blocks), dim3(256), 0, s, in,
-                     rows, n, ld, out, accumulate, scale);
+  if (n >= 16384) {
+    int64_t blocks = (n + 63) / 64;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(reduce_rows_kernel<64>, dim3(blocks), dim3(256), 0, s, in,
+                       rows, n, ld, out, accumulate, scale);
+  } else {
+    int64_t blocks = (n + 15) / 16;
+    hipLaunchKernelGGL(reduce_rows_kernel<16>, dim3(blocks), dim3(256), 0, s, in,
+                       rows, n, ld, out, accumulate, scale);
+  }
 }
 
-int colsum_parts(int M) { return (M + COLSUM_RPB - 1) / COLSUM_RPB; }
+int colsum_parts(int M) { return COLSUM_CHUNKS; }
 
 void colsum_bf16(const uint16_t* x, int M, int N, int64_t ldx, float* part,
                  int nparts, float* out, int accumulate, hipStream_t s) {
   if (M <= 0 || N <= 0) return;
-  dim3 grid((N / 8 + 255) / 256, nparts);
+  dim3 grid((N + 63) / 64, COLSUM_CHUNKS);
   hipLaunchKernelGGL(colsum_kernel, grid, dim3(256), 0, s, x, M, N, ldx, part);
   reduce_rows(part, nparts, N, N, out, accumulate, 1.f, s);
 }

@@ -8,7 +8,7 @@ mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
 ok_or_fail() { [ "$1" -eq 0 ] || [ "$1" -eq 1 ]; }
 if [ "${RUN_TESTS:-1}" = "1" ]; then
-  timeout -k 10 ${TEST_TIMEOUT:-900} python -m pytest tests -m gpu -q ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
+  timeout -k 10 ${TEST_TIMEOUT:-900} python -m pytest tests -m gpu -q ${PYTEST_ARGS:-} ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/pytest_gpu.log 2>&1
   rc=$?; echo "pytest rc=$rc"; tail -30 gpurun_out/pytest_gpu.log
   ok_or_fail $rc || exit $rc
 fi

@@ -123,7 +123,7 @@ def check_finite(g, found):
 
 
 def head_parts(B: int) -> int:
-    return (B + 63) // 64
+    return (B + 15) // 16
 
 
 def head_bce(H, w, b, label, inv_n, relu_mask, logits, dH, part):

@@ -331,3 +331,40 @@ def test_dlrm_graph_replay_matches_eager():
         b.step()
     torch.cuda.synchronize()
     assert torch.allclose(a.fp.p, b.fp.p, atol=1e-5)
+
+
+def test_embedding_bwd_graph_replay_large():
+    """Bench-scale fused backward (213k ids, skewed + uniform tables) captured
+    in a hipGraph and replayed must match eager execution bit for bit."""
+    T, B, D = 26, 8192, 128
+    rows = [3, 10, 4000, 2_000_000] + [50_000] * 22
+    g = torch.Generator(device="cpu").manual_seed(7)
+    idx = torch.cat([torch.randint(0, r, (B,), generator=g) for r in rows]).to(DEV)
+    offs = torch.arange(T * B + 1, device=DEV)
+    ro = torch.zeros(T, dtype=torch.long)
+    ro[1:] = torch.tensor(rows[:-1]).cumsum(0)
+    ro = ro.to(DEV)
+    W0 = torch.randn(sum(rows), D, device=DEV) * 0.01
+    goff = torch.tensor([t * D for t in range(T)], device=DEV)
+    grad = (torch.randn(B * T * D, device=DEV) * 0.01).to(torch.bfloat16)
+    hyper = torch.tensor([0.05, 1.0], device=DEV)
+    We, se = W0.clone(), torch.zeros(W0.shape[0], device=DEV)
+    for _ in range(3):
+        ops.embedding_bwd(We, ro, idx, offs, goff, T, B, grad, T * D, ops.EMB_ROWWISE_ADAGRAD,
+                          hyper, state1=se)
+    Wg, sg = W0.clone(), torch.zeros(W0.shape[0], device=DEV)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ops.embedding_bwd(Wg, ro, idx, offs, goff, T, B, grad, T * D, ops.EMB_ROWWISE_ADAGRAD,
+                          hyper, state1=sg)
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        ops.embedding_bwd(Wg, ro, idx, offs, goff, T, B, grad, T * D, ops.EMB_ROWWISE_ADAGRAD,
+                          hyper, state1=sg)
+    graph.replay()
+    graph.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(We, Wg)
+    assert torch.equal(se, sg)
