@@ -135,10 +135,11 @@ class ShardedEmbeddingBags:
                 blocks.append(blk)
             self.rw_block = torch.tensor(blocks, dtype=torch.int64, device=self.device)
             self.rw_block_host = blocks
-            my_rows = [max(0, min(blocks[j], self.tables[t].num_embeddings - rank * blocks[j]))
-                       for j, t in enumerate(self.rw_tables)]
+            # every rank allocates a full block per table (the last block is
+            # padded) so row offsets agree across ranks and requesters can
+            # send ready-made row keys
             self.rw_store = TableBatchedEmbedding(
-                my_rows, D, device, optim,
+                blocks, D, device, optim,
                 init_ranges=[self.tables[t].init_range or (1.0 / self.tables[t].num_embeddings) ** 0.5
                              for t in self.rw_tables], seed=seed * 1000 + 500 + rank)
             rw_ids_idx = torch.cat([torch.arange(self.in_base[t], self.in_base[t] + B * self.L[t])
@@ -333,7 +334,7 @@ class ShardedEmbeddingBags:
         sl = self._local_slices(t)
         if sl is not None and sl[3] > sl[2]:
             store, i, lo, hi = sl
-            store.table_weight(i).copy_(full[lo:hi].to(store.weight.device))
+            store.table_weight(i)[: hi - lo].copy_(full[lo:hi].to(store.weight.device))
 
     def get_table_weight(self, t: int):
         """This rank's (row_start, rows view) of table ``t``, or None."""
@@ -341,7 +342,7 @@ class ShardedEmbeddingBags:
         if sl is None:
             return None
         store, i, lo, hi = sl
-        return lo, store.table_weight(i)
+        return lo, store.table_weight(i)[: max(0, hi - lo)]
 
     def state_dict(self):
         d = {"tw": self.tw_store.state_dict()}

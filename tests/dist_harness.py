@@ -15,6 +15,22 @@ def _free_port():
     return p
 
 
+def _to_bytes(obj):
+    import io
+
+    import torch
+    buf = io.BytesIO()
+    torch.save(obj, buf)        # by value: no shared-memory fds outlive the worker
+    return buf.getvalue()
+
+
+def _from_bytes(b):
+    import io
+
+    import torch
+    return torch.load(io.BytesIO(b), weights_only=True)
+
+
 def _worker(rank, world, port, fn, args, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
@@ -24,7 +40,7 @@ def _worker(rank, world, port, fn, args, q):
         from tdfo_amd.parallel import dist as tdist
         tdist.init_distributed("cpu", "gloo", timeout_s=120)
         out = fn(rank, world, *args)
-        q.put((rank, "ok", out))
+        q.put((rank, "ok", _to_bytes(out)))
         tdist.reset()
     except Exception:  # pragma: no cover
         q.put((rank, "err", traceback.format_exc()))
@@ -43,7 +59,7 @@ def run_distributed(fn, world, *args, timeout=300):
             rank, status, out = q.get(timeout=timeout)
             if status != "ok":
                 raise RuntimeError(f"rank {rank} failed:\n{out}")
-            res[rank] = out
+            res[rank] = _from_bytes(out)
     finally:
         for p in procs:
             p.join(timeout=30)
