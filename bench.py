@@ -68,7 +68,7 @@ def main(argv=None):
     pool = [data.next() for _ in range(args.pool)]
     torch.cuda.synchronize()
     setup_s = time.time() - t0
-    use_graph = (not args.no_graph) and world == 1
+    use_graph = not args.no_graph
 
     def run(n, start):
         for i in range(n):

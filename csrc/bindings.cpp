@@ -37,7 +37,8 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 
 void gemm(const Tensor& a, bool a_col, const Tensor& b, bool b_col,
           const c10::optional<Tensor>& bias, bool relu,
           const c10::optional<Tensor>& mask, const c10::optional<Tensor>& out,
-          const c10::optional<Tensor>& out32, int64_t splits) {
+          const c10::optional<Tensor>& out32, int64_t splits, const c10::optional<Tensor>& mul,
+          const c10::optional<Tensor>& add, const c10::optional<Tensor>& out2) {
   check_dev(a, "a"); check_dev(b, "b");
   check_2d_rowmajor(a, "a"); check_2d_rowmajor(b, "b");
   const int64_t M = a_col ? a.size(1) : a.size(0);
@@ -80,6 +81,19 @@ void gemm(const Tensor& a, bool a_col, const Tensor& b, bool b_col,
     TORCH_CHECK(out32->numel() >= splits * M * N, "gemm: out32 too small");
     g.C32 = out32->data_ptr<float>(); g.ldc32 = N;
   }
+  auto check_mn = [&](const c10::optional<Tensor>& t, const char* name) {
+    check_2d_rowmajor(*t, name);
+    TORCH_CHECK(t->size(0) == M && t->size(1) == N && t->stride(0) % 8 == 0 &&
+                aligned16(t->data_ptr()), "gemm: ", name, " must be [M, N], 16-B aligned rows");
+  };
+  if (mul) { check_mn(mul, "mul"); g.mul = bf16_ptr(*mul); g.ldmul = mul->stride(0); }
+  if (add) { check_mn(add, "add"); g.add = bf16_ptr(*add); g.ldadd = add->stride(0); }
+  if (out2) {
+    check_mn(out2, "out2");
+    TORCH_CHECK(splits == 1, "gemm: out2 requires splits == 1");
+    g.C2 = bf16_mut(*out2); g.ldc2 = out2->stride(0);
+  }
+  TORCH_CHECK(!(mul || add) || out2, "gemm: mul/add need out2");
   tdfo::gemm_bf16(g, cur_stream());
 }
 
@@ -140,6 +154,47 @@ void interaction_bwd(const Tensor& dz, const Tensor& dense, const Tensor& emb,
   tdfo::interaction_bwd(bf16_ptr(dz), dz.stride(0), bf16_ptr(dense), dense.stride(0),
                         bf16_ptr(emb), m, (int)F, (int)D, (int)B, bf16_mut(d_dense),
                         d_dense.stride(0), bf16_mut(d_emb), dm, relu_mask, cur_stream());
+}
+
+// ----------------------------------------------------------- elementwise
+void concat_features(const Tensor& dense, const Tensor& emb, at::IntArrayRef off,
+                     at::IntArrayRef stride, int64_t F, int64_t D, const Tensor& out) {
+  check_dev(dense, "dense"); check_2d_rowmajor(dense, "dense");
+  const int64_t B = dense.size(0);
+  TORCH_CHECK(D % 8 == 0 && F <= 32 && F >= 1, "concat: D % 8 and F <= 32");
+  TORCH_CHECK(out.is_contiguous() && out.numel() == B * F * D, "concat: out [B, F*D]");
+  TORCH_CHECK(dense.stride(0) % 8 == 0 && aligned16(dense.data_ptr()), "concat alignment");
+  auto m = make_slots(off, stride, F);
+  check_slots_fit(emb, m, F, D, B);
+  tdfo::concat_features(bf16_ptr(dense), dense.stride(0), bf16_ptr(emb), m, (int)F, (int)D,
+                        (int)B, bf16_mut(out), cur_stream());
+}
+
+void split_features(const Tensor& dx, int64_t F, int64_t D, const Tensor& dense,
+                    const Tensor& d_dense, const Tensor& d_emb, at::IntArrayRef doff,
+                    at::IntArrayRef dstride, bool relu_mask) {
+  check_dev(dx, "dx");
+  const int64_t B = dense.size(0);
+  TORCH_CHECK(dx.is_contiguous() && dx.numel() == B * F * D && D % 8 == 0, "split: dx [B, F*D]");
+  check_2d_rowmajor(d_dense, "d_dense");
+  TORCH_CHECK(d_dense.stride(0) % 8 == 0 && dense.stride(0) % 8 == 0, "split alignment");
+  auto m = make_slots(doff, dstride, F);
+  check_slots_fit(d_emb, m, F, D, B);
+  tdfo::split_features(bf16_ptr(dx), (int)F, (int)D, (int)B, bf16_ptr(dense), dense.stride(0),
+                       bf16_mut(d_dense), d_dense.stride(0), bf16_mut(d_emb), m, relu_mask,
+                       cur_stream());
+}
+
+void cross_bwd(const Tensor& dout, const Tensor& x0, const Tensor& y, const Tensor& dy,
+               const Tensor& dx0, bool accumulate, bool add_dout) {
+  const int64_t n = dout.numel();
+  for (auto* t : {&dout, &x0, &y, &dy, &dx0}) {
+    TORCH_CHECK(t->is_contiguous() && t->numel() == n && t->scalar_type() == at::kBFloat16 &&
+                aligned16(t->data_ptr()), "cross_bwd: contiguous bf16 same-size tensors");
+  }
+  TORCH_CHECK(n % 8 == 0, "cross_bwd: numel % 8");
+  tdfo::cross_bwd(bf16_ptr(dout), bf16_ptr(x0), bf16_ptr(y), n, bf16_mut(dy), bf16_mut(dx0),
+                  accumulate, add_dout, cur_stream());
 }
 
 // ------------------------------------------------------------- embedding
@@ -308,7 +363,14 @@ void auc_hist(const Tensor& logits, const Tensor& labels, int64_t nb, const Tens
 
 TORCH_LIBRARY(tdfo, m) {
   m.def("gemm(Tensor a, bool a_col, Tensor b, bool b_col, Tensor? bias, bool relu, Tensor? mask, "
-        "Tensor(a!)? out, Tensor(b!)? out32, int splits) -> ()");
+        "Tensor(a!)? out, Tensor(b!)? out32, int splits, Tensor? mul=None, Tensor? add=None, "
+        "Tensor(c!)? out2=None) -> ()");
+  m.def("concat_features(Tensor dense, Tensor emb, int[] off, int[] stride, int F, int D, "
+        "Tensor(a!) out) -> ()");
+  m.def("split_features(Tensor dx, int F, int D, Tensor dense, Tensor(a!) d_dense, "
+        "Tensor(b!) d_emb, int[] doff, int[] dstride, bool relu_mask) -> ()");
+  m.def("cross_bwd(Tensor dout, Tensor x0, Tensor y, Tensor(a!) dy, Tensor(b!) dx0, "
+        "bool accumulate, bool add_dout) -> ()");
   m.def("interaction_fwd(Tensor dense, Tensor emb, int[] off, int[] stride, int F, int D, Tensor(a!) out) -> ()");
   m.def("interaction_bwd(Tensor dz, Tensor dense, Tensor emb, int[] off, int[] stride, int F, int D, "
         "Tensor(a!) d_dense, Tensor(b!) d_emb, int[] doff, int[] dstride, bool relu_mask) -> ()");
@@ -331,6 +393,9 @@ TORCH_LIBRARY(tdfo, m) {
 
 TORCH_LIBRARY_IMPL(tdfo, CUDA, m) {
   m.impl("gemm", gemm);
+  m.impl("concat_features", concat_features);
+  m.impl("split_features", split_features);
+  m.impl("cross_bwd", cross_bwd);
   m.impl("interaction_fwd", interaction_fwd);
   m.impl("interaction_bwd", interaction_bwd);
   m.impl("embedding_bag_fwd", embedding_bag_fwd);

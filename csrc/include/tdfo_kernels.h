@@ -24,6 +24,11 @@ struct GemmArgs {
   const uint16_t* mask; int64_t ldm;
   uint16_t* C; int64_t ldc;
   float* C32; int64_t ldc32;
+  // optional second output C2 = (mul ? mul * v : v) + (add ? add : 0), used by
+  // the DCN-v2 cross layer (x0 * (U h + b) + x_l) and residual dgrads.
+  const uint16_t* mul; int64_t ldmul;
+  const uint16_t* add; int64_t ldadd;
+  uint16_t* C2; int64_t ldc2;
 };
 void gemm_bf16(const GemmArgs& a, hipStream_t s);
 
@@ -43,6 +48,21 @@ void interaction_bwd(const uint16_t* dz, int64_t ldz, const uint16_t* dense,
                      const SlotMap& slots, int F, int D, int B,
                      uint16_t* d_dense, int64_t ld_ddense, uint16_t* d_emb,
                      const SlotMap& dslots, int relu_mask, hipStream_t s);
+
+// ------------------------------------------------------ elementwise ----
+// out[b, f*D + d] = f == 0 ? dense[b, d] : emb[off[f] + b*stride[f] + d]
+void concat_features(const uint16_t* dense, int64_t ld_dense, const uint16_t* emb,
+                     const SlotMap& slots, int F, int D, int B, uint16_t* out,
+                     hipStream_t s);
+// inverse of concat_features; the dense slot is multiplied by (dense > 0)
+// when relu_mask (ReLU of the bottom MLP's last layer).
+void split_features(const uint16_t* dx, int F, int D, int B, const uint16_t* dense,
+                    int64_t ld_dense, uint16_t* d_dense, int64_t ld_ddense,
+                    uint16_t* d_emb, const SlotMap& dslots, int relu_mask, hipStream_t s);
+// DCN-v2 cross backward: dy = dout * x0 ;
+// dx0 = (accumulate ? dx0 : 0) + dout * y + (add_dout ? dout : 0)
+void cross_bwd(const uint16_t* dout, const uint16_t* x0, const uint16_t* y, int64_t n,
+               uint16_t* dy, uint16_t* dx0, int accumulate, int add_dout, hipStream_t s);
 
 // -------------------------------------------------------- embedding ----
 // Table-batched pooled lookup. Bag j = t*B + b (t table, b sample) owns

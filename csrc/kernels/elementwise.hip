@@ -1,0 +1,128 @@
+// Memory-bound glue of the DCN-v2 path: feature concat / split (reading and
+// writing the pooled embeddings in place in the all-to-all buffers through a
+// SlotMap) and the cross-layer backward. All accesses are 16-B vectors
+// (cdna_hip_programming.md Guideline 13); one 8-element group per thread.
+#include "tdfo_common.h"
+#include "tdfo_kernels.h"
+
+namespace tdfo {
+namespace {
+
+__global__ __launch_bounds__(256) void concat_kernel(const uint16_t* __restrict__ dense,
+                                                     int64_t ld_dense,
+                                                     const uint16_t* __restrict__ emb,
+                                                     SlotMap sm, int F, int D, int B,
+                                                     uint16_t* __restrict__ out) {
+  const int gpr = D / 8;                       // 8-element groups per feature row
+  const int64_t total = (int64_t)B * F * gpr;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int g = (int)(i % gpr);
+    const int64_t bf = i / gpr;
+    const int f = (int)(bf % F);
+    const int64_t b = bf / F;
+    const uint16_t* src = f == 0 ? dense + b * ld_dense : emb + sm.off[f] + b * sm.stride[f];
+    *(uint4*)(out + (b * F + f) * D + g * 8) = *(const uint4*)(src + g * 8);
+  }
+}
+
+__global__ __launch_bounds__(256) void split_kernel(const uint16_t* __restrict__ dx, int F,
+                                                    int D, int B,
+                                                    const uint16_t* __restrict__ dense,
+                                                    int64_t ld_dense,
+                                                    uint16_t* __restrict__ d_dense,
+                                                    int64_t ld_ddense,
+                                                    uint16_t* __restrict__ d_emb, SlotMap sm,
+                                                    int relu_mask) {
+  const int gpr = D / 8;
+  const int64_t total = (int64_t)B * F * gpr;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int g = (int)(i % gpr);
+    const int64_t bf = i / gpr;
+    const int f = (int)(bf % F);
+    const int64_t b = bf / F;
+    uint4 v = *(const uint4*)(dx + (b * F + f) * D + g * 8);
+    if (f == 0) {
+      if (relu_mask) {
+        const uint4 h = *(const uint4*)(dense + b * ld_dense + g * 8);
+        uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+        const uint32_t hh[4] = {h.x, h.y, h.z, h.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          uint32_t lo = vv[q] & 0xffff, hi = vv[q] >> 16;
+          if (!(bf2f((uint16_t)(hh[q] & 0xffff)) > 0.f)) lo = 0;
+          if (!(bf2f((uint16_t)(hh[q] >> 16)) > 0.f)) hi = 0;
+          vv[q] = lo | (hi << 16);
+        }
+        v = make_uint4(vv[0], vv[1], vv[2], vv[3]);
+      }
+      *(uint4*)(d_dense + b * ld_ddense + g * 8) = v;
+    } else {
+      *(uint4*)(d_emb + sm.off[f] + b * sm.stride[f] + g * 8) = v;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void cross_bwd_kernel(const uint16_t* __restrict__ dout,
+                                                        const uint16_t* __restrict__ x0,
+                                                        const uint16_t* __restrict__ y,
+                                                        int64_t n8, uint16_t* __restrict__ dy,
+                                                        uint16_t* __restrict__ dx0,
+                                                        int accumulate, int add_dout) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const uint4 a = ((const uint4*)dout)[i], b = ((const uint4*)x0)[i], c = ((const uint4*)y)[i];
+    uint4 d0 = accumulate ? ((const uint4*)dx0)[i] : make_uint4(0, 0, 0, 0);
+    const uint32_t av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w},
+                   cv[4] = {c.x, c.y, c.z, c.w};
+    uint32_t dv[4] = {d0.x, d0.y, d0.z, d0.w};
+    uint32_t ov[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float a0 = bf2f((uint16_t)(av[q] & 0xffff)), a1 = bf2f((uint16_t)(av[q] >> 16));
+      const float b0 = bf2f((uint16_t)(bv[q] & 0xffff)), b1 = bf2f((uint16_t)(bv[q] >> 16));
+      const float c0 = bf2f((uint16_t)(cv[q] & 0xffff)), c1 = bf2f((uint16_t)(cv[q] >> 16));
+      const float e0 = bf2f((uint16_t)(dv[q] & 0xffff)), e1 = bf2f((uint16_t)(dv[q] >> 16));
+      ov[q] = pack2bf(a0 * b0, a1 * b1);
+      const float r0 = add_dout ? a0 : 0.f, r1 = add_dout ? a1 : 0.f;
+      dv[q] = pack2bf(e0 + a0 * c0 + r0, e1 + a1 * c1 + r1);
+    }
+    ((uint4*)dy)[i] = make_uint4(ov[0], ov[1], ov[2], ov[3]);
+    ((uint4*)dx0)[i] = make_uint4(dv[0], dv[1], dv[2], dv[3]);
+  }
+}
+
+int grid_of(int64_t n) {
+  int64_t b = (n + 255) / 256;
+  return (int)(b < 1 ? 1 : (b > 8192 ? 8192 : b));
+}
+
+}  // namespace
+
+void concat_features(const uint16_t* dense, int64_t ld_dense, const uint16_t* emb,
+                     const SlotMap& slots, int F, int D, int B, uint16_t* out, hipStream_t s) {
+  const int64_t n = (int64_t)B * F * (D / 8);
+  hipLaunchKernelGGL(concat_kernel, dim3(grid_of(n)), dim3(256), 0, s, dense, ld_dense, emb,
+                     slots, F, D, B, out);
+  TDFO_CHECK_HIP(hipGetLastError());
+}
+
+void split_features(const uint16_t* dx, int F, int D, int B, const uint16_t* dense,
+                    int64_t ld_dense, uint16_t* d_dense, int64_t ld_ddense, uint16_t* d_emb,
+                    const SlotMap& dslots, int relu_mask, hipStream_t s) {
+  const int64_t n = (int64_t)B * F * (D / 8);
+  hipLaunchKernelGGL(split_kernel, dim3(grid_of(n)), dim3(256), 0, s, dx, F, D, B, dense,
+                     ld_dense, d_dense, ld_ddense, d_emb, dslots, relu_mask);
+  TDFO_CHECK_HIP(hipGetLastError());
+}
+
+void cross_bwd(const uint16_t* dout, const uint16_t* x0, const uint16_t* y, int64_t n,
+               uint16_t* dy, uint16_t* dx0, int accumulate, int add_dout, hipStream_t s) {
+  const int64_t n8 = n / 8;
+  hipLaunchKernelGGL(cross_bwd_kernel, dim3(grid_of(n8)), dim3(256), 0, s, dout, x0, y, n8, dy,
+                     dx0, accumulate, add_dout);
+  TDFO_CHECK_HIP(hipGetLastError());
+}
+
+}  // namespace tdfo

@@ -217,6 +217,32 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs p) {
             make_uint4(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]),
                        pack2bf(v[6], v[7]));
       }
+      if (p.C2) {
+        float w2[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) w2[q] = v[q];
+        if (p.mul) {
+          const uint4 mv = *(const uint4*)(p.mul + (int64_t)m * p.ldmul + n);
+          const uint32_t mu[4] = {mv.x, mv.y, mv.z, mv.w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            w2[2 * q] *= bf2f((uint16_t)(mu[q] & 0xffff));
+            w2[2 * q + 1] *= bf2f((uint16_t)(mu[q] >> 16));
+          }
+        }
+        if (p.add) {
+          const uint4 av = *(const uint4*)(p.add + (int64_t)m * p.ldadd + n);
+          const uint32_t au[4] = {av.x, av.y, av.z, av.w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            w2[2 * q] += bf2f((uint16_t)(au[q] & 0xffff));
+            w2[2 * q + 1] += bf2f((uint16_t)(au[q] >> 16));
+          }
+        }
+        *(uint4*)(p.C2 + (int64_t)m * p.ldc2 + n) =
+            make_uint4(pack2bf(w2[0], w2[1]), pack2bf(w2[2], w2[3]), pack2bf(w2[4], w2[5]),
+                       pack2bf(w2[6], w2[7]));
+      }
       if (c32) {
         float* o = c32 + (int64_t)m * p.ldc32 + n;
         *(float4*)o = make_float4(v[0], v[1], v[2], v[3]);
@@ -228,6 +254,12 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs p) {
         if (p.mask && !(bf2f(p.mask[(int64_t)m * p.ldm + n + q]) > 0.f)) x = 0.f;
         if (p.C) p.C[(int64_t)m * p.ldc + n + q] = f2bf(x);
         if (c32) c32[(int64_t)m * p.ldc32 + n + q] = x;
+        if (p.C2) {
+          float x2 = x;
+          if (p.mul) x2 *= bf2f(p.mul[(int64_t)m * p.ldmul + n + q]);
+          if (p.add) x2 += bf2f(p.add[(int64_t)m * p.ldadd + n + q]);
+          p.C2[(int64_t)m * p.ldc2 + n + q] = f2bf(x2);
+        }
       }
     }
   }

@@ -186,6 +186,7 @@ class DLRMTrainer:
             self.dcn_h = [z(B, cfg.dcn_rank) for _ in range(L)]         # V^T x_l
             self.dcn_y = [z(B, self.top_in) for _ in range(L)]          # U h + b
             self.dcn_dx = [z(B, self.top_in) for _ in range(L + 1)]
+            self.dcn_dx0acc = z(B, self.top_in)
             self.dcn_dh = z(B, cfg.dcn_rank)
             self.dcn_dy = z(B, self.top_in)
         self.logits = z(B, dt=torch.float32)
@@ -261,18 +262,51 @@ class DLRMTrainer:
         if dx is not None:
             ops.linear_dgrad(dy, fp.bf16(name + ".w"), mask=x if x_is_relu else None, out=dx)
 
-    def _forward_backward(self):
-        cfg, fp, B = self.cfg, self.fp, self.B
-        D, F = cfg.embedding_dim, self.F
+    # ---------------------------------------------------------- stages
+    # The step is a fixed sequence of compute stages ("c", hipGraph-capturable)
+    # and communication stages ("m", RCCL collectives issued eagerly so they
+    # overlap with the next compute stage on their own stream).
+    def _stages(self):
         emb = self.emb
-        emb.forward_start(self.ids)
-        # bottom MLP
+        return [
+            ("c", lambda: emb.stage_fwd_prep(self.ids)),
+            ("m", emb.stage_fwd_ids_exchange),
+            ("c", emb.stage_fwd_lookup),
+            ("m", emb.stage_fwd_out_exchange),
+            ("c", self._s_bottom_fwd),
+            ("m", self._m_fwd_wait),
+            ("c", self._s_top),
+            ("m", emb.backward_start),
+            ("c", self._s_bottom_bwd),
+            ("m", self._m_allreduce_start),
+            ("m", emb.backward_wait),
+            ("c", self._s_emb_update),
+            ("m", self._m_allreduce_wait),
+            ("c", self._s_dense_update),
+        ]
+
+    def _forward_backward(self):
+        for _, fn in self._stages():
+            fn()
+
+    def _s_bottom_fwd(self):
+        fp = self.fp
         h = self.x0
         for i, (name, a, b) in enumerate(self.bottom_layers):
             ops.linear_fwd(h, fp.bf16(name + ".w"), fp.param(name + ".b"), relu=True,
                            out=self.bot_act[i])
             h = self.bot_act[i]
-        emb.forward_wait()
+
+    def _m_fwd_wait(self):
+        self.emb.forward_wait()
+        if self.emb.rw_tables:
+            self.emb._rw_forward(self.ids)
+
+    def _s_top(self):
+        cfg, fp, B = self.cfg, self.fp, self.B
+        D, F = cfg.embedding_dim, self.F
+        emb = self.emb
+        h = self.bot_act[-1]
         if cfg.interaction == "dot":
             ops.interaction_fwd(h, emb.recv, self.slot_off, self.slot_stride, F, D, self.zbuf)
             t = self.zbuf
@@ -284,13 +318,11 @@ class DLRMTrainer:
             t = self.top_act[i]
         K = self.head_k
         head = fp.param("head")
-        dlast = self.top_grad[-1]
         ops.head_bce(t, head[:K], head[K:], self.label, 1.0 / (B * self.world), True, self.logits,
-                     dlast, self.head_part)
+                     self.top_grad[-1], self.head_part)
         ops.reduce_rows(self.head_part, self.nparts, K + 1, K + 2, fp.grad("head"))
         ops.reduce_rows(self.head_part[K + 1:], self.nparts, 1, K + 2, self.loss_sum,
                         accumulate=True)
-        # top MLP backward
         for i in reversed(range(len(self.top_layers))):
             name = self.top_layers[i][0]
             x = self.top_act[i - 1] if i > 0 else t_in(self)
@@ -299,89 +331,125 @@ class DLRMTrainer:
             else:
                 dx = self.dz if cfg.interaction == "dot" else self.dcn_dx[-1]
             self._linear_bwd(name, x, self.top_grad[i], dx, x_is_relu=i > 0)
-        # interaction backward -> embedding grads (a2a layout) + bottom grad
         if cfg.interaction == "dot":
             ops.interaction_bwd(self.dz, h, emb.recv, self.slot_off, self.slot_stride, F, D,
                                 self.bot_grad[-1], emb.d_recv, self.slot_off, self.slot_stride,
                                 True)
         else:
             self._dcn_backward(h)
-        emb.backward_start()
-        # bottom MLP backward
+
+    def _s_bottom_bwd(self):
         for i in reversed(range(len(self.bottom_layers))):
             name = self.bottom_layers[i][0]
             x = self.bot_act[i - 1] if i > 0 else self.x0
             dx = self.bot_grad[i - 1] if i > 0 else None
             self._linear_bwd(name, x, self.bot_grad[i], dx, x_is_relu=i > 0)
-        work = None
+
+    def _m_allreduce_start(self):
+        self._ar_work = None
         if self.world > 1:
-            work = dist.all_reduce(fp.g, group=self.group, async_op=True)
+            self._ar_work = dist.all_reduce(self.fp.g, group=self.group, async_op=True)
+
+    def _s_emb_update(self):
         self.emb_hyper[1:2].add_(1.0)
-        emb.backward_finish(self.emb_hyper)
-        if work is not None:
-            work.wait()
+        self.emb.stage_bwd_update(self.emb_hyper)
+
+    def _m_allreduce_wait(self):
+        if self.emb.rw_tables:
+            self.emb._rw_backward(self.emb.d_recv, self.emb_hyper)
+        if self._ar_work is not None:
+            self._ar_work.wait()
+            self._ar_work = None
+
+    def _s_dense_update(self):
+        fp = self.fp
         self.dense_hyper[1:2].add_(1.0)
         ops.dense_optimizer(fp.p, fp.g, fp.m, fp.v, fp.p_bf16, self.dense_opt, self.dense_hyper,
-                            wd=cfg.dense_wd)
+                            wd=self.cfg.dense_wd)
 
-    # DCN-v2 cross network: x_{l+1} = x0 * (U (V^T x_l) + b) + x_l
+    # DCN-v2 cross network: x_{l+1} = x0 * (U (V^T x_l) + b) + x_l. The
+    # Hadamard product and the residual are fused into the U-GEMM epilogue
+    # (out2 = x0 * (acc + b) + x_l), the residual of the backward into the
+    # V-dgrad epilogue.
     def _dcn_forward(self, h):
         cfg, fp, D, F = self.cfg, self.fp, self.cfg.embedding_dim, self.F
         x0 = self.dcn_x[0]
-        emb = self.emb
-        ops.concat_features(h, emb.recv, self.slot_off, self.slot_stride, F, D, x0)
+        ops.concat_features(h, self.emb.recv, self.slot_off, self.slot_stride, F, D, x0)
         for i in range(cfg.dcn_layers):
             ops.linear_fwd(self.dcn_x[i], fp.bf16(f"dcn{i}.v"), None, relu=False, out=self.dcn_h[i])
-            ops.linear_fwd(self.dcn_h[i], fp.bf16(f"dcn{i}.u"), fp.param(f"dcn{i}.b"), relu=False,
-                           out=self.dcn_y[i])
-            ops.cross_combine(x0, self.dcn_y[i], self.dcn_x[i], self.dcn_x[i + 1])
+            ops.gemm(self.dcn_h[i], False, fp.bf16(f"dcn{i}.u"), False, fp.param(f"dcn{i}.b"),
+                     False, None, self.dcn_y[i], None, 1, mul=x0, add=self.dcn_x[i],
+                     out2=self.dcn_x[i + 1])
         return self.dcn_x[-1]
 
     def _dcn_backward(self, h):
         cfg, fp, D, F = self.cfg, self.fp, self.cfg.embedding_dim, self.F
         L = cfg.dcn_layers
         x0 = self.dcn_x[0]
-        # dcn_dx[L] holds d x_L (written by the first top layer's dgrad)
-        dx0_acc = self.dcn_dx[0]
+        acc = self.dcn_dx0acc
         for i in reversed(range(L)):
             dxo = self.dcn_dx[i + 1]
-            # dy = dxo * x0 ; dx0 += dxo * y ; dx_l = dxo + (dy U) V
-            ops.cross_backward(dxo, x0, self.dcn_y[i], self.dcn_dy, dx0_acc, i == L - 1)
+            # dy = dxo * x0 ; acc (+)= dxo * y (+ dxo at i == 0: x_0's residual)
+            ops.cross_bwd(dxo, x0, self.dcn_y[i], self.dcn_dy, acc, i != L - 1, i == 0)
             ops.linear_wgrad(self.dcn_dy, self.dcn_h[i], fp.grad(f"dcn{i}.u").view(-1),
                              slab=self.slab)
             ops.colsum(self.dcn_dy, fp.grad(f"dcn{i}.b"))
             ops.linear_dgrad(self.dcn_dy, fp.bf16(f"dcn{i}.u"), out=self.dcn_dh)
             ops.linear_wgrad(self.dcn_dh, self.dcn_x[i], fp.grad(f"dcn{i}.v").view(-1),
                              slab=self.slab)
-            dst = self.dcn_dx[i] if i > 0 else self.dcn_dy
-            ops.linear_dgrad(self.dcn_dh, fp.bf16(f"dcn{i}.v"), out=dst)
-            ops.add_(dst, dxo)
-            if i == 0:
-                ops.add_(dx0_acc, dst)
-        ops.split_features(dx0_acc, h, self.slot_off, self.slot_stride, F, D, self.bot_grad[-1],
-                           self.emb.d_recv, True)
+            # dx_i = dh V + (i > 0 ? dxo : acc)
+            ops.gemm(self.dcn_dh, False, fp.bf16(f"dcn{i}.v"), True, None, False, None, None, None,
+                     1, add=dxo if i > 0 else acc, out2=self.dcn_dx[i])
+        ops.split_features(self.dcn_dx[0], F, D, h, self.bot_grad[-1], self.emb.d_recv,
+                           self.slot_off, self.slot_stride, True)
 
     def step(self):
         """One training step on the batch in the static buffers."""
         if self.graph is not None:
-            self.graph.replay()
+            if isinstance(self.graph, list):
+                for kind, item in self.graph:
+                    item.replay() if kind == "c" else item()
+            else:
+                self.graph.replay()
         else:
             self._forward_backward()
         self.steps += 1
 
-    def capture_graph(self, warmup: int = 2):
-        """Capture the step into a hipGraph (single process only)."""
-        assert self.device.type == "cuda" and self.world == 1
+    def capture_graph(self, warmup: int = 2, staged: Optional[bool] = None):
+        """Capture the step into hipGraphs. Single process: one graph for the
+        whole step. Multi-process: one graph per compute stage, with the RCCL
+        exchanges issued eagerly between replays (they overlap the next stage)."""
+        assert self.device.type == "cuda"
+        if not self.emb.graph_capturable:
+            return
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(warmup):
                 self._forward_backward()
         torch.cuda.current_stream().wait_stream(s)
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
-            self._forward_backward()
-        self.graph = g
+        torch.cuda.synchronize()
+        if staged is None:
+            staged = self.world > 1
+        if not staged:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._forward_backward()
+            self.graph = g
+            return
+        pool = torch.cuda.graph_pool_handle()
+        seq = []
+        for kind, fn in self._stages():
+            if kind == "c":
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g, pool=pool):
+                    fn()
+                seq.append(("c", g))
+            else:
+                fn()          # dry exchange keeps every rank's collective sequence aligned
+                seq.append(("m", fn))
+        torch.cuda.synchronize()
+        self.graph = seq
 
     def pop_loss(self) -> float:
         """Mean training loss since the last call (one device->host read)."""

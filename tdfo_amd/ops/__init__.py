@@ -19,11 +19,12 @@ def _gpu(t: torch.Tensor) -> bool:
     return t.is_cuda
 
 
-def gemm(a, a_col, b, b_col, bias=None, relu=False, mask=None, out=None, out32=None, splits=1):
+def gemm(a, a_col, b, b_col, bias=None, relu=False, mask=None, out=None, out32=None, splits=1,
+         mul=None, add=None, out2=None):
     if _gpu(a):
-        _native().gemm(a, a_col, b, b_col, bias, relu, mask, out, out32, splits)
+        _native().gemm(a, a_col, b, b_col, bias, relu, mask, out, out32, splits, mul, add, out2)
     else:
-        ref.gemm(a, a_col, b, b_col, bias, relu, mask, out, out32, splits)
+        ref.gemm(a, a_col, b, b_col, bias, relu, mask, out, out32, splits, mul, add, out2)
 
 
 def linear_fwd(x, w, bias=None, relu=False, out=None):
@@ -159,3 +160,25 @@ def cast_bf16(x, y):
         _native().cast_bf16(x, y)
     else:
         ref.cast_bf16(x, y)
+
+
+def concat_features(dense, emb, off, stride, F, D, out):
+    if _gpu(dense):
+        _native().concat_features(dense, emb, list(off), list(stride), F, D, out)
+    else:
+        ref.concat_features(dense, emb, off, stride, F, D, out)
+
+
+def split_features(dx, F, D, dense, d_dense, d_emb, doff, dstride, relu_mask):
+    if _gpu(dx):
+        _native().split_features(dx, F, D, dense, d_dense, d_emb, list(doff), list(dstride),
+                                 relu_mask)
+    else:
+        ref.split_features(dx, F, D, dense, d_dense, d_emb, doff, dstride, relu_mask)
+
+
+def cross_bwd(dout, x0, y, dy, dx0, accumulate, add_dout=False):
+    if _gpu(dout):
+        _native().cross_bwd(dout, x0, y, dy, dx0, accumulate, add_dout)
+    else:
+        ref.cross_bwd(dout, x0, y, dy, dx0, accumulate, add_dout)

@@ -19,7 +19,8 @@ def _f(t: torch.Tensor) -> torch.Tensor:
     return t.float()
 
 
-def gemm(a, a_col, b, b_col, bias=None, relu=False, mask=None, out=None, out32=None, splits=1):
+def gemm(a, a_col, b, b_col, bias=None, relu=False, mask=None, out=None, out32=None, splits=1,
+         mul=None, add=None, out2=None):
     A = _f(a).t() if a_col else _f(a)          # [M, K]
     Bm = _f(b) if b_col else _f(b).t()         # [K, N]
     c = A @ Bm
@@ -31,6 +32,11 @@ def gemm(a, a_col, b, b_col, bias=None, relu=False, mask=None, out=None, out32=N
         c = c * (mask.float() > 0)
     if out is not None:
         out.copy_(c.to(out.dtype))
+    if out2 is not None:
+        c2 = c * mul.float() if mul is not None else c
+        if add is not None:
+            c2 = c2 + add.float()
+        out2.copy_(c2.to(out2.dtype))
     if out32 is not None:
         M, N = c.shape
         # split-K semantics: slice 0 holds the full sum, other slices zero
@@ -297,3 +303,41 @@ def hist_auc(hist: torch.Tensor) -> float:
 
 def key_bits_for(rows: int) -> int:
     return max(1, math.ceil(math.log2(max(2, rows))))
+
+
+def _gather_slots(emb, off, stride, F, D, B, dev):
+    flat = emb.reshape(-1)
+    ar = torch.arange(B, device=dev)
+    cols = torch.arange(D, device=dev)
+    return [flat[off[i] + ar[:, None] * stride[i] + cols[None, :]] for i in range(1, F)]
+
+
+def concat_features(dense, emb, off, stride, F, D, out):
+    B = dense.shape[0]
+    parts = [dense[:, :D]] + _gather_slots(emb, off, stride, F, D, B, dense.device)
+    out.view(B, F * D).copy_(torch.cat([p.to(out.dtype) for p in parts], 1))
+
+
+def split_features(dx, F, D, dense, d_dense, d_emb, doff, dstride, relu_mask):
+    B = dense.shape[0]
+    x = dx.reshape(B, F, D)
+    d0 = x[:, 0].float()
+    if relu_mask:
+        d0 = d0 * (dense[:, :D].float() > 0)
+    d_dense[:, :D] = d0.to(d_dense.dtype)
+    dflat = d_emb.reshape(-1)
+    ar = torch.arange(B, device=dx.device)
+    cols = torch.arange(D, device=dx.device)
+    for i in range(1, F):
+        idx = doff[i] + ar[:, None] * dstride[i] + cols[None, :]
+        dflat[idx.reshape(-1)] = x[:, i].reshape(-1).to(d_emb.dtype)
+
+
+def cross_bwd(dout, x0, y, dy, dx0, accumulate, add_dout=False):
+    a = dout.float()
+    dy.copy_((a * x0.float()).to(dy.dtype))
+    base = dx0.float() if accumulate else torch.zeros_like(a)
+    res = base + a * y.float()
+    if add_dout:
+        res = res + a
+    dx0.copy_(res.to(dx0.dtype))

@@ -184,29 +184,49 @@ class ShardedEmbeddingBags:
         return self.recv
 
     def forward_start(self, ids: torch.Tensor):
-        W, B = self.world, self.B
+        self.stage_fwd_prep(ids)
+        self.stage_fwd_ids_exchange()
+        self.stage_fwd_lookup()
+        self.stage_fwd_out_exchange()
+        if self.rw_tables:
+            self._rw_forward(ids)
+
+    @property
+    def graph_capturable(self) -> bool:
+        """Static shapes only (no row-wise tables with data-dependent splits)."""
+        return not self.rw_tables
+
+    # -- stages (compute stages are hipGraph-capturable; exchanges are RCCL)
+    def stage_fwd_prep(self, ids: torch.Tensor):
         if self.tw_identity:
             self.tw_send_ids = ids
             self.tw_recv_ids = ids
         else:
             torch.index_select(ids, 0, self.tw_perm, out=self.tw_send_ids)
-            if W > 1:
-                _a2a(self.tw_recv_ids, self.tw_send_ids, [self.tw_recv_count] * W,
-                     self.tw_send_counts, self.group)
-            else:
+            if self.world == 1:
                 self.tw_recv_ids = self.tw_send_ids
+
+    def stage_fwd_ids_exchange(self):
+        W = self.world
+        if W > 1 and not self.tw_identity:
+            _a2a(self.tw_recv_ids, self.tw_send_ids, [self.tw_recv_count] * W,
+                 self.tw_send_counts, self.group)
+
+    def stage_fwd_lookup(self):
+        W, B = self.world, self.B
         if self.tw_nv:
             self.tw_store.forward(self.tw_recv_ids, self.tw_v_offsets, self.tw_v_row_off, self.tw_nv,
                                   B, self.tw_pooled if W > 1 else self.recv, self.tw_v_out_off,
                                   self.dsum[self.rank], mean=self.mean)
+
+    def stage_fwd_out_exchange(self):
+        W, B = self.world, self.B
         work = None
-        tw_total = sum(self.tw_recv_sizes)
         if W > 1:
+            tw_total = sum(self.tw_recv_sizes)
             work = _a2a(self.recv[:tw_total], self.tw_pooled[: W * B * self.dsum[self.rank]],
                         self.tw_recv_sizes, [B * self.dsum[self.rank]] * W, self.group,
                         async_op=True)
-        if self.rw_tables:
-            self._rw_forward(ids)
         self._pending = work
 
     def forward_wait(self):
@@ -275,16 +295,26 @@ class ShardedEmbeddingBags:
                         async_op=True)
         self._bw = (work, d_recv)
 
-    def backward_finish(self, hyper: torch.Tensor):
+    def backward_wait(self):
         work, d_recv = self._bw
-        W, B = self.world, self.B
         if work is not None:
             work.wait()
+        self._bw = (None, d_recv)
+
+    def stage_bwd_update(self, hyper: torch.Tensor):
+        """Fused sort-based backward + optimizer on this rank's table-wise shards."""
+        d_recv = self._bw[1] if getattr(self, "_bw", None) else self.d_recv
+        W, B = self.world, self.B
         grad = self.d_pooled if W > 1 else d_recv
         if self.tw_nv:
             self.tw_store.backward_update(self.tw_recv_ids, self.tw_v_offsets, self.tw_v_row_off,
                                           self.tw_nv, B, grad, self.tw_v_out_off,
                                           self.dsum[self.rank], hyper, mean=self.mean)
+
+    def backward_finish(self, hyper: torch.Tensor):
+        self.backward_wait()
+        d_recv = self._bw[1]
+        self.stage_bwd_update(hyper)
         if self.rw_tables:
             self._rw_backward(d_recv, hyper)
         self._bw = None

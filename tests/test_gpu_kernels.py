@@ -309,7 +309,8 @@ def test_dlrm_step_matches_cpu():
     assert sum(lg[-5:]) < sum(lg[:5])
 
 
-def test_dlrm_graph_replay_matches_eager():
+@pytest.mark.parametrize("staged", [False, True])
+def test_dlrm_graph_replay_matches_eager(staged):
     from tdfo_amd.data.synthetic import SyntheticCriteo
     from tdfo_amd.models.dlrm import DLRMConfig, DLRMTrainer
 
@@ -322,7 +323,7 @@ def test_dlrm_graph_replay_matches_eager():
     batches = [data.next() for _ in range(6)]
     for t in (a, b):
         t.load_batch(*batches[0])
-    b.capture_graph(warmup=1)
+    b.capture_graph(warmup=1, staged=staged)
     a.step()  # replicate the capture warmup on the eager trainer
     for x in batches[1:]:
         a.load_batch(*x)
@@ -368,3 +369,68 @@ def test_embedding_bwd_graph_replay_large():
     torch.cuda.synchronize()
     assert torch.equal(We, Wg)
     assert torch.equal(se, sg)
+
+
+def test_gemm_out2_mul_add():
+    torch.manual_seed(5)
+    M, N, K = 300, 256, 128
+    A = bf(torch.randn(M, K, device=DEV))
+    W = bf(torch.randn(N, K, device=DEV))
+    bias = torch.randn(N, device=DEV)
+    mul = bf(torch.randn(M, N, device=DEV))
+    add = bf(torch.randn(M, N, device=DEV))
+    y, o2 = (torch.empty(M, N, dtype=torch.bfloat16, device=DEV) for _ in range(2))
+    ops.gemm(A, False, W, False, bias, False, None, y, None, 1, mul=mul, add=add, out2=o2)
+    ey, eo2 = (torch.empty(M, N, dtype=torch.bfloat16, device=DEV) for _ in range(2))
+    ref.gemm(A, False, W, False, bias, False, None, ey, None, 1, mul=mul, add=add, out2=eo2)
+    assert rel_err(y, ey) < 1e-2 and rel_err(o2, eo2) < 2e-2
+
+
+def test_concat_split_cross_bwd():
+    torch.manual_seed(6)
+    B, F, D = 100, 5, 64
+    T = F - 1
+    dense = bf(torch.randn(B, D, device=DEV))
+    emb = bf(torch.randn(B * T * D, device=DEV))
+    off = [0] + [t * D for t in range(T)]
+    stride = [0] + [T * D] * T
+    out = torch.empty(B, F * D, dtype=torch.bfloat16, device=DEV)
+    ops.concat_features(dense, emb, off, stride, F, D, out)
+    exp = torch.empty_like(out)
+    ref.concat_features(dense, emb, off, stride, F, D, exp)
+    assert torch.equal(out, exp)
+    dd, de = torch.zeros_like(dense), torch.zeros_like(emb)
+    ops.split_features(out, F, D, dense, dd, de, off, stride, True)
+    edd, ede = torch.zeros_like(dense), torch.zeros_like(emb)
+    ref.split_features(out, F, D, dense, edd, ede, off, stride, True)
+    assert torch.equal(dd, edd) and torch.equal(de, ede)
+    a, b, c = (bf(torch.randn(B * 64, device=DEV)) for _ in range(3))
+    dy, dx0 = bf(torch.randn(B * 64, device=DEV)), bf(torch.randn(B * 64, device=DEV))
+    e_dy, e_dx0 = dy.clone(), dx0.clone()
+    ops.cross_bwd(a, b, c, dy, dx0, True, True)
+    ref.cross_bwd(a, b, c, e_dy, e_dx0, True, True)
+    assert rel_err(dy, e_dy) < 1e-2 and rel_err(dx0, e_dx0) < 1e-2
+
+
+def test_dcn_step_matches_cpu():
+    from tdfo_amd.data.synthetic import SyntheticCriteo
+    from tdfo_amd.models.dlrm import DLRMConfig, DLRMTrainer
+
+    cfg = DLRMConfig(embedding_dim=64, table_rows=[1000, 20, 5000, 300], bottom=[128, 64],
+                     top=[128, 64, 1], interaction="dcn", dcn_layers=2, dcn_rank=64,
+                     pooling=[2, 1, 3, 1], dense_lr=1e-3, emb_lr=0.05)
+    B = 256
+    gpu = DLRMTrainer(cfg, B, DEV)
+    cpu = DLRMTrainer(cfg, B, "cpu")
+    cpu.emb.tw_store.weight.copy_(gpu.emb.tw_store.weight.cpu())
+    cpu.fp.p.copy_(gpu.fp.p.cpu())
+    cpu.fp.sync_bf16()
+    data = SyntheticCriteo(cfg.table_rows, B, pooling=cfg.pooling, device="cpu", seed=3)
+    for _ in range(10):
+        batch = data.next()
+        gpu.load_batch(*(x.to(DEV) for x in batch))
+        cpu.load_batch(*batch)
+        gpu.step()
+        cpu.step()
+        a, b = gpu.pop_loss() / B, cpu.pop_loss() / B
+        assert abs(a - b) < 0.02, (a, b)
