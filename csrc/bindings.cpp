@@ -69,7 +69,7 @@ void gemm(const Tensor& a, bool a_col, const Tensor& b, bool b_col,
     TORCH_CHECK(mask->size(0) == M && mask->size(1) == N, "gemm: mask shape");
     g.mask = bf16_ptr(*mask); g.ldm = mask->stride(0);
   }
-  TORCH_CHECK(out || out32, "gemm: need an output");
+  TORCH_CHECK(out || out32 || out2, "gemm: need an output");
   if (out) {
     check_2d_rowmajor(*out, "out");
     TORCH_CHECK(out->size(0) == M && out->size(1) == N, "gemm: out shape");
@@ -195,6 +195,28 @@ void cross_bwd(const Tensor& dout, const Tensor& x0, const Tensor& y, const Tens
   TORCH_CHECK(n % 8 == 0, "cross_bwd: numel % 8");
   tdfo::cross_bwd(bf16_ptr(dout), bf16_ptr(x0), bf16_ptr(y), n, bf16_mut(dy), bf16_mut(dx0),
                   accumulate, add_dout, cur_stream());
+}
+
+// ------------------------------------------------------------ radix sort
+std::tuple<Tensor, Tensor> sort_pairs(const Tensor& keys, const Tensor& vals, int64_t key_bits) {
+  check_dev(keys, "keys"); check_dev(vals, "vals");
+  TORCH_CHECK(keys.is_contiguous() && vals.is_contiguous() && vals.scalar_type() == at::kInt &&
+              keys.numel() == vals.numel(), "sort_pairs: contiguous keys, int32 vals");
+  TORCH_CHECK(keys.scalar_type() == at::kLong || keys.scalar_type() == at::kInt, "keys int32/int64");
+  const int64_t n = keys.numel();
+  Tensor ka = keys.clone(), va = vals.clone();
+  Tensor kb = at::empty_like(ka), vb = at::empty_like(va);
+  Tensor ws = at::empty({(int64_t)tdfo::radix_sort_workspace(n)}, keys.options().dtype(at::kByte));
+  int r;
+  if (keys.scalar_type() == at::kLong)
+    r = tdfo::radix_sort_pairs_u64(reinterpret_cast<uint64_t*>(ka.data_ptr()), va.data_ptr<int32_t>(),
+                                   reinterpret_cast<uint64_t*>(kb.data_ptr()), vb.data_ptr<int32_t>(),
+                                   n, (int)key_bits, ws.data_ptr(), cur_stream());
+  else
+    r = tdfo::radix_sort_pairs_u32(reinterpret_cast<uint32_t*>(ka.data_ptr()), va.data_ptr<int32_t>(),
+                                   reinterpret_cast<uint32_t*>(kb.data_ptr()), vb.data_ptr<int32_t>(),
+                                   n, (int)key_bits, ws.data_ptr(), cur_stream());
+  return r ? std::make_tuple(kb, vb) : std::make_tuple(ka, va);
 }
 
 // ------------------------------------------------------------- embedding
@@ -383,6 +405,7 @@ TORCH_LIBRARY(tdfo, m) {
   m.def("dense_optimizer(Tensor(a!) p, Tensor g, Tensor(b!)? m, Tensor(c!)? v, Tensor(d!)? p_bf16, int opt, "
         "Tensor hyper, float beta1, float beta2, float eps, float wd, float momentum, Tensor? found_inf) -> ()");
   m.def("check_finite(Tensor g, Tensor(a!) found) -> ()");
+  m.def("sort_pairs(Tensor keys, Tensor vals, int key_bits) -> (Tensor, Tensor)");
   m.def("cast_bf16(Tensor x, Tensor(a!) y) -> ()");
   m.def("head_bce(Tensor H, Tensor w, Tensor b, Tensor label, float inv_n, bool relu_mask, "
         "Tensor(a!) logits, Tensor(b!) dH, Tensor(c!) part) -> ()");
@@ -402,6 +425,7 @@ TORCH_LIBRARY_IMPL(tdfo, CUDA, m) {
   m.impl("embedding_bwd", embedding_bwd);
   m.impl("dense_optimizer", dense_optimizer);
   m.impl("check_finite", check_finite);
+  m.impl("sort_pairs", sort_pairs);
   m.impl("cast_bf16", cast_bf16);
   m.impl("head_bce", head_bce);
   m.impl("reduce_rows", reduce_rows);

@@ -64,6 +64,16 @@ void split_features(const uint16_t* dx, int F, int D, int B, const uint16_t* den
 void cross_bwd(const uint16_t* dout, const uint16_t* x0, const uint16_t* y, int64_t n,
                uint16_t* dy, uint16_t* dx0, int accumulate, int add_dout, hipStream_t s);
 
+// ------------------------------------------------------ radix sort ----
+// Stable LSD radix sort of (key, value) pairs on the low `key_bits` bits.
+// ka/va hold the input; kb/vb are scratch of the same size. Returns 1 if the
+// sorted result ended in (kb, vb), 0 if in (ka, va). ws: radix_sort_workspace(n).
+size_t radix_sort_workspace(int64_t n);
+int radix_sort_pairs_u32(uint32_t* ka, int32_t* va, uint32_t* kb, int32_t* vb, int64_t n,
+                         int key_bits, void* ws, hipStream_t s);
+int radix_sort_pairs_u64(uint64_t* ka, int32_t* va, uint64_t* kb, int32_t* vb, int64_t n,
+                         int key_bits, void* ws, hipStream_t s);
+
 // -------------------------------------------------------- embedding ----
 // Table-batched pooled lookup. Bag j = t*B + b (t table, b sample) owns
 // indices[offsets[j] .. offsets[j+1]); table t's rows start at

@@ -13,16 +13,14 @@
 // MI355X and are order-dependent) and load-balanced under skew
 // (cdna_hip_programming.md Appendix B "Scatter / gather / embedding"):
 //   keys   : key = row_offset[t] + id, val = position, bag_of[position]
-//   sort   : rocprim onesweep radix sort on the key bits actually used
-//            (32-bit keys whenever the shard has < 2^32 rows)
+//   sort   : in-house stable LSD radix sort (radix_sort.hip) on the key bits
+//            actually used (32-bit keys whenever the shard has < 2^32 rows)
 //   chunks : each wave reduces a fixed 32-entry chunk of the sorted list; runs
 //            fully inside the chunk are finished (optimizer applied) in place,
 //            runs crossing a chunk edge leave fp32 partials (head/tail slabs)
 //   combine: the chunk where a crossing run starts adds the following chunks'
 //            head partials in order and applies the optimizer once.
 // Every unique row is updated exactly once per step, in a fixed order.
-#include <rocprim/device/device_radix_sort.hpp>
-
 #include <type_traits>
 
 #include "tdfo_common.h"
@@ -410,29 +408,17 @@ __global__ __launch_bounds__(256) void emb_combine_kernel(
 }
 
 struct WsLayout {
-  size_t keys_in, keys_out, vals_in, vals_out, goff, gscale, head, tail, tlist, tcount, cub;
-  size_t total, cub_bytes;
+  size_t keys_in, keys_out, vals_in, vals_out, goff, gscale, head, tail, tlist, tcount, sortws;
+  size_t total;
 };
 
 inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
-
-using SortCfg = rocprim::default_config;
-
-template <typename K>
-size_t sort_bytes(int64_t nnz) {
-  size_t b = 0;
-  rocprim::radix_sort_pairs<SortCfg>(nullptr, b, (K*)nullptr, (K*)nullptr, (int32_t*)nullptr,
-                                     (int32_t*)nullptr, (size_t)nnz, 0, (int)(8 * sizeof(K)));
-  return b;
-}
 
 int ch_for(int D) { return D <= 128 ? 32 : (D == 256 ? 16 : 8); }
 
 WsLayout ws_layout(int64_t nnz, int D) {
   WsLayout L;
   const int64_t nch = (nnz + ch_for(D) - 1) / ch_for(D);
-  const size_t b64 = sort_bytes<uint64_t>(nnz), b32 = sort_bytes<uint32_t>(nnz);
-  const size_t cub_bytes = b64 > b32 ? b64 : b32;
   size_t o = 0;
   L.keys_in = o;  o += al(nnz * 8);
   L.keys_out = o; o += al(nnz * 8);
@@ -444,8 +430,7 @@ WsLayout ws_layout(int64_t nnz, int D) {
   L.tail = o;     o += al((size_t)nch * D * 4);
   L.tlist = o;    o += al((size_t)nch * 4);
   L.tcount = o;   o += al(16);
-  L.cub = o;      o += al(cub_bytes);
-  L.cub_bytes = cub_bytes;
+  L.sortws = o;   o += al(radix_sort_workspace(nnz));
   L.total = o;
   return L;
 }
@@ -469,10 +454,14 @@ void bwd_impl(const EmbBwdArgs& a, const WsLayout& L, hipStream_t s) {
   hipLaunchKernelGGL(emb_keys_kernel<K>, dim3(kb), dim3(256), 0, s, a, keys_in, vals_in, goff,
                      gscale, tcount);
   TDFO_CHECK_HIP(hipGetLastError());
-  size_t cub_bytes = L.cub_bytes;
-  TDFO_CHECK_HIP(rocprim::radix_sort_pairs<SortCfg>(ws + L.cub, cub_bytes, keys_in, keys_out,
-                                                    vals_in, vals_out, (size_t)a.nnz, 0,
-                                                    a.key_bits, s));
+  int in_b;
+  if constexpr (sizeof(K) == 4)
+    in_b = radix_sort_pairs_u32(keys_in, vals_in, keys_out, vals_out, a.nnz, a.key_bits,
+                                ws + L.sortws, s);
+  else
+    in_b = radix_sort_pairs_u64(keys_in, vals_in, keys_out, vals_out, a.nnz, a.key_bits,
+                                ws + L.sortws, s);
+  if (!in_b) { keys_out = keys_in; vals_out = vals_in; }
   constexpr int CH = BwdCfg<D>::CH;
   const int64_t nch = (a.nnz + CH - 1) / CH;
   const int64_t blocks = (nch + 3) / 4;

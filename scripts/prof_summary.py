@@ -1,20 +1,31 @@
-"""Summarise a rocprofv3 kernel-trace CSV: per-kernel totals and one step."""
+"""Summarise a rocprofv3 kernel-trace CSV: per-kernel totals (optionally per
+step), ignoring setup kernels (data generation / table init)."""
+import argparse
 import csv
-import sys
 from collections import defaultdict
 
-path = sys.argv[1]
-rows = list(csv.DictReader(open(path)))
+SETUP = ("distribution_elementwise", "FillFunctor", "index_elementwise", "gemvt", "arange",
+         "CatArrayBatchedCopy", "fillBuffer", "BUnaryFunctor", "remainder")
+
+ap = argparse.ArgumentParser()
+ap.add_argument("csv")
+ap.add_argument("--steps", type=int, default=0, help="divide totals by this many steps")
+args = ap.parse_args()
+rows = list(csv.DictReader(open(args.csv)))
 tot = defaultdict(float)
 cnt = defaultdict(int)
 for r in rows:
-    d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
     n = r["Kernel_Name"]
-    n = n[:90]
-    tot[n] += d
-    cnt[n] += 1
+    if any(s in n for s in SETUP):
+        continue
+    d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+    short = n.split("(")[0].replace("void ", "").replace("tdfo::(anonymous namespace)::", "tdfo::")
+    short = short[:80]
+    tot[short] += d
+    cnt[short] += 1
 T = sum(tot.values())
-print(f"{'total_us':>10} {'calls':>6} {'avg_us':>8}  kernel")
-for n, t in sorted(tot.items(), key=lambda x: -x[1])[:40]:
-    print(f"{t:10.1f} {cnt[n]:6d} {t / cnt[n]:8.1f}  {n}")
-print(f"sum {T:.1f} us")
+div = max(1, args.steps)
+print(f"{'us/step':>9} {'calls/step':>10} {'avg_us':>8} {'share':>6}  kernel")
+for n, t in sorted(tot.items(), key=lambda x: -x[1]):
+    print(f"{t / div:9.1f} {cnt[n] / div:10.1f} {t / cnt[n]:8.1f} {100 * t / T:5.1f}%  {n}")
+print(f"total kernel time per step: {T / div:.1f} us")

@@ -182,3 +182,13 @@ def cross_bwd(dout, x0, y, dy, dx0, accumulate, add_dout=False):
         _native().cross_bwd(dout, x0, y, dy, dx0, accumulate, add_dout)
     else:
         ref.cross_bwd(dout, x0, y, dy, dx0, accumulate, add_dout)
+
+
+def sort_pairs(keys, vals, key_bits):
+    """Stable radix sort of (keys, int32 vals) on the low key_bits bits."""
+    if _gpu(keys):
+        return _native().sort_pairs(keys, vals, key_bits)
+    mask = (1 << key_bits) - 1
+    k = keys & mask if key_bits < 63 else keys
+    order = torch.sort(k, stable=True).indices
+    return keys[order], vals[order]

@@ -434,3 +434,17 @@ def test_dcn_step_matches_cpu():
         cpu.step()
         a, b = gpu.pop_loss() / B, cpu.pop_loss() / B
         assert abs(a - b) < 0.02, (a, b)
+
+
+@pytest.mark.parametrize("n", [1, 1000, 4096, 4097, 213_000, 1_500_000])
+@pytest.mark.parametrize("dtype,bits", [(torch.int32, 28), (torch.int64, 40)])
+def test_radix_sort_matches_stable_torch_sort(n, dtype, bits):
+    g = torch.Generator(device="cpu").manual_seed(n)
+    keys = torch.randint(0, 1 << bits, (n,), generator=g, dtype=torch.int64)
+    keys[: n // 3] = keys[: n // 3] % 7          # heavy duplicates
+    keys = keys.to(dtype).to(DEV)
+    vals = torch.arange(n, dtype=torch.int32, device=DEV)
+    k, v = ops.sort_pairs(keys, vals, bits)
+    ek, ei = torch.sort(keys, stable=True)
+    assert torch.equal(k, ek)
+    assert torch.equal(v, ei.to(torch.int32))
