@@ -59,9 +59,9 @@ void gemm(const Tensor& a, bool a_col, const Tensor& b, bool b_col,
   g.M = (int)M; g.N = (int)N; g.K = (int)K; g.splits = (int)splits;
   if (bias) {
     check_dev(*bias, "bias");
-    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->is_contiguous() && bias->numel() == N,
-                "gemm: bias must be fp32 [N]");
-    g.bias = bias->data_ptr<float>();
+    TORCH_CHECK(bias->scalar_type() == at::kFloat && bias->dim() == 1 && bias->numel() == N,
+                "gemm: bias must be fp32 [N] (any stride)");
+    g.bias = bias->data_ptr<float>(); g.bias_stride = bias->stride(0);
   }
   g.relu = relu;
   if (mask) {
@@ -119,7 +119,8 @@ void check_slots_fit(const Tensor& emb, const tdfo::SlotMap& m, int64_t F, int64
 }
 
 void interaction_fwd(const Tensor& dense, const Tensor& emb, at::IntArrayRef off,
-                     at::IntArrayRef stride, int64_t F, int64_t D, const Tensor& out) {
+                     at::IntArrayRef stride, int64_t F, int64_t D, const Tensor& out,
+                     int64_t ones_col) {
   check_dev(dense, "dense"); check_dev(emb, "emb"); check_dev(out, "out");
   check_inter(F, D); check_2d_rowmajor(dense, "dense"); check_2d_rowmajor(out, "out");
   const int64_t B = dense.size(0);
@@ -131,7 +132,7 @@ void interaction_fwd(const Tensor& dense, const Tensor& emb, at::IntArrayRef off
   auto m = make_slots(off, stride, F);
   check_slots_fit(emb, m, F, D, B);
   tdfo::interaction_fwd(bf16_ptr(dense), dense.stride(0), bf16_ptr(emb), m, (int)F, (int)D,
-                        (int)B, bf16_mut(out), out.stride(0), cur_stream());
+                        (int)B, bf16_mut(out), out.stride(0), (int)ones_col, cur_stream());
 }
 
 void interaction_bwd(const Tensor& dz, const Tensor& dense, const Tensor& emb,
@@ -393,7 +394,8 @@ TORCH_LIBRARY(tdfo, m) {
         "Tensor(b!) d_emb, int[] doff, int[] dstride, bool relu_mask) -> ()");
   m.def("cross_bwd(Tensor dout, Tensor x0, Tensor y, Tensor(a!) dy, Tensor(b!) dx0, "
         "bool accumulate, bool add_dout) -> ()");
-  m.def("interaction_fwd(Tensor dense, Tensor emb, int[] off, int[] stride, int F, int D, Tensor(a!) out) -> ()");
+  m.def("interaction_fwd(Tensor dense, Tensor emb, int[] off, int[] stride, int F, int D, Tensor(a!) out, "
+        "int ones_col=-1) -> ()");
   m.def("interaction_bwd(Tensor dz, Tensor dense, Tensor emb, int[] off, int[] stride, int F, int D, "
         "Tensor(a!) d_dense, Tensor(b!) d_emb, int[] doff, int[] dstride, bool relu_mask) -> ()");
   m.def("embedding_bag_fwd(Tensor W, Tensor row_offset, Tensor indices, Tensor offsets, Tensor out_off, "

@@ -19,7 +19,7 @@ struct GemmArgs {
   const uint16_t* A; int64_t lda; int a_col;
   const uint16_t* B; int64_t ldb; int b_col;
   int M, N, K, splits;
-  const float* bias;
+  const float* bias; int64_t bias_stride;   // bias[n * bias_stride]
   int relu;
   const uint16_t* mask; int64_t ldm;
   uint16_t* C; int64_t ldc;
@@ -40,7 +40,7 @@ void gemm_bf16(const GemmArgs& a, hipStream_t s);
 struct SlotMap { int64_t off[32]; int64_t stride[32]; };
 void interaction_fwd(const uint16_t* dense, int64_t ld_dense,
                      const uint16_t* emb, const SlotMap& slots, int F, int D,
-                     int B, uint16_t* out, int64_t ldo, hipStream_t s);
+                     int B, uint16_t* out, int64_t ldo, int ones_col, hipStream_t s);
 // Backward: dZ [B, ldz] -> d_emb (same slot layout as forward emb) and
 // d_dense = (passthrough + interaction grad) * (dense > 0 if relu_mask).
 void interaction_bwd(const uint16_t* dz, int64_t ldz, const uint16_t* dense,

@@ -176,7 +176,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs p) {
   for (int j = 0; j < 4; ++j) {
     const int cl = wc * 64 + j * 16 + (lane & 15);
     const int n = n0 + cl;
-    const float bias = (p.bias && n < p.N) ? p.bias[n] : 0.f;
+    const float bias = (p.bias && n < p.N) ? p.bias[(int64_t)n * p.bias_stride] : 0.f;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
 #pragma unroll

@@ -39,14 +39,15 @@ template <int D>
 __global__ __launch_bounds__(256) void inter_fwd_kernel(
     const uint16_t* __restrict__ dense, int64_t ld_dense,
     const uint16_t* __restrict__ emb, SlotMap sm, int F, int B,
-    uint16_t* __restrict__ out, int64_t ldo) {
+    uint16_t* __restrict__ out, int64_t ldo, int ones_col) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   uint16_t* row = (uint16_t*)smem_raw + w * ldo;
   constexpr int KS = D / 16;
   const int P = F * (F - 1) / 2;
-  // zero the pad tail once; it is never overwritten
-  for (int e = D + P + lane; e < ldo; e += 64) row[e] = 0;
+  // pad tail written once (zeros, plus the constant-1 column that carries the
+  // next layer's bias through its GEMM); never overwritten afterwards
+  for (int e = D + P + lane; e < ldo; e += 64) row[e] = e == ones_col ? (uint16_t)0x3f80 : 0;
 
   const int i = lane & 31, h = lane >> 5;
   const int iters = (B + gridDim.x * WAVES - 1) / (gridDim.x * WAVES);
@@ -204,13 +205,13 @@ int grid_for(int B) {
 
 void interaction_fwd(const uint16_t* dense, int64_t ld_dense,
                      const uint16_t* emb, const SlotMap& slots, int F, int D,
-                     int B, uint16_t* out, int64_t ldo, hipStream_t s) {
+                     int B, uint16_t* out, int64_t ldo, int ones_col, hipStream_t s) {
   if (B <= 0) return;
   const size_t smem = (size_t)WAVES * ldo * 2;
   dim3 grid(grid_for(B));
 #define TDFO_IFWD(DD)                                                          \
   hipLaunchKernelGGL(inter_fwd_kernel<DD>, grid, dim3(256), smem, s, dense,    \
-                     ld_dense, emb, slots, F, B, out, ldo)
+                     ld_dense, emb, slots, F, B, out, ldo, ones_col)
   switch (D) {
     case 32: TDFO_IFWD(32); break;
     case 64: TDFO_IFWD(64); break;

@@ -4,10 +4,10 @@
 // in-house (instead of rocprim's onesweep, whose ordered-block-id path was
 // observed to fault under hipGraph replay on gfx950) so the whole sort is a
 // fixed, capture-safe sequence of 3 kernels per 8-bit digit:
-//   hist    : one 4096-item tile per block, LDS digit histogram -> [tile][256]
+//   hist    : one 1024-item tile per block, LDS digit histogram -> [tile][256]
 //   scan    : 256 threads, thread d scans digit d's column over tiles, then a
 //             block scan of the 256 digit totals gives each digit's base
-//   scatter : per tile, 16 rounds of 256 items; the stable rank of an item
+//   scatter : per tile, 4 rounds of 256 items; the stable rank of an item
 //             among equal digits is found with 8 wave ballots (lanes with the
 //             same digit), per-wave digit counts in LDS and a running count
 //             per digit, so the order of equal keys is the input order.
@@ -19,8 +19,8 @@ namespace tdfo {
 namespace {
 
 constexpr int RS_THREADS = 256;
-constexpr int RS_ROUNDS = 16;
-constexpr int RS_TILE = RS_THREADS * RS_ROUNDS;   // 4096 items per tile
+constexpr int RS_ROUNDS = 4;
+constexpr int RS_TILE = RS_THREADS * RS_ROUNDS;   // 1024 items per tile
 
 template <typename K>
 __global__ __launch_bounds__(256) void rs_hist_kernel(const K* __restrict__ keys, int64_t n,

@@ -5,7 +5,9 @@ import csv
 from collections import defaultdict
 
 SETUP = ("distribution_elementwise", "FillFunctor", "index_elementwise", "gemvt", "arange",
-         "CatArrayBatchedCopy", "fillBuffer", "BUnaryFunctor", "remainder")
+         "CatArrayBatchedCopy", "fillBuffer", "BUnaryFunctor", "remainder", "AUnaryFunctor",
+         "CUDAFunctor_add<", "log1p", "sigmoid", "bfloat16_copy", "direct_copy",
+         "elementwise_kernel_manual_unroll")
 
 ap = argparse.ArgumentParser()
 ap.add_argument("csv")
@@ -19,7 +21,8 @@ for r in rows:
     if any(s in n for s in SETUP):
         continue
     d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-    short = n.split("(")[0].replace("void ", "").replace("tdfo::(anonymous namespace)::", "tdfo::")
+    short = n.replace("(anonymous namespace)::", "").replace("void ", "")
+    short = short.split("(")[0]
     short = short[:80]
     tot[short] += d
     cnt[short] += 1

@@ -105,12 +105,39 @@ class DLRMConfig:
         return 3.0 * f
 
 
+@dataclass
+class Lin:
+    """A linear layer in the augmented layout: W is stored [out, wcols] with
+    the bias in column ``bcol``; the layer's input buffer holds 1.0 in column
+    ``bcol``. If ``bcol < in_k`` the bias rides inside the forward GEMM's K
+    (free), otherwise it is read by the epilogue. Either way the weight-grad
+    GEMM over the augmented input produces the bias gradient in column
+    ``bcol`` — no separate bias-reduction kernels."""
+    name: str
+    in_real: int
+    in_k: int
+    out: int
+    bcol: int
+    wcols: int
+
+    @property
+    def bias_in_k(self) -> bool:
+        return self.bcol < self.in_k
+
+
+def make_lin(name: str, in_real: int, out: int) -> Lin:
+    in_k = pad64(in_real)
+    if in_real < in_k:
+        return Lin(name, in_real, in_k, out, in_real, in_k)
+    return Lin(name, in_real, in_k, out, in_k, in_k + 8)
+
+
 class DLRMTrainer:
     """Explicit-step DLRM/DCN-v2 trainer over a sharded embedding engine.
 
     ``batch_size`` is per rank (weak scaling). Works on CPU (torch reference
-    ops, gloo) and on MI355X (HIP kernels, RCCL); optionally captures the
-    step in a hipGraph (single process).
+    ops, gloo) and on MI355X (HIP kernels, RCCL); the step can be captured in
+    hipGraphs (whole step single-process, per compute stage multi-process).
     """
 
     def __init__(self, cfg: DLRMConfig, batch_size: int, device, group=None, rank: int = 0,
@@ -126,6 +153,7 @@ class DLRMTrainer:
         self.F = F = T + 1
         assert cfg.bottom[-1] == D, "bottom MLP must end at the embedding dim"
         assert cfg.top[-1] == 1
+        assert cfg.interaction != "dcn" or cfg.dcn_rank % 64 == 0, "dcn_rank must be a multiple of 64"
         torch.manual_seed(cfg.seed)
         # ------------------------------------------------------ embeddings
         optim = EmbOptimConfig(cfg.emb_opt, lr=cfg.emb_lr, eps=cfg.emb_eps)
@@ -135,28 +163,27 @@ class DLRMTrainer:
         self.emb = ShardedEmbeddingBags(tables, self.plan, rank, B, cfg.pooling_factors(), dev,
                                         optim, group=group, seed=cfg.seed)
         # ------------------------------------------------------ dense params
-        self.in_pad = pad64(cfg.num_dense)
         fp = FlatParams()
-        self.bottom_layers = []
-        dims = [self.in_pad] + cfg.bottom
-        for i, (a, b) in enumerate(zip(dims[:-1], dims[1:])):
-            fp.add(f"bot{i}.w", (b, a))
-            fp.add(f"bot{i}.b", (b,))
-            self.bottom_layers.append((f"bot{i}", a, b))
+        dims = [cfg.num_dense] + cfg.bottom
+        self.bottom_layers = [make_lin(f"bot{i}", a, b)
+                              for i, (a, b) in enumerate(zip(dims[:-1], dims[1:]))]
         if cfg.interaction == "dot":
-            self.top_in = pad64(D + F * (F - 1) // 2)
+            self.top_real = D + F * (F - 1) // 2
         else:
-            self.top_in = F * D
+            self.top_real = F * D
+        tdims = [self.top_real] + cfg.top[:-1]
+        self.top_layers = [make_lin(f"top{i}", a, b)
+                           for i, (a, b) in enumerate(zip(tdims[:-1], tdims[1:]))]
+        for L in self.bottom_layers + self.top_layers:
+            fp.add(L.name + ".w", (L.out, L.wcols))
+        self.dcn_u = []
+        if cfg.interaction == "dcn":
+            Wd = self.top_real
             for i in range(cfg.dcn_layers):
-                fp.add(f"dcn{i}.v", (cfg.dcn_rank, self.top_in))
-                fp.add(f"dcn{i}.u", (self.top_in, cfg.dcn_rank))
-                fp.add(f"dcn{i}.b", (self.top_in,))
-        self.top_layers = []
-        tdims = [self.top_in] + cfg.top[:-1]
-        for i, (a, b) in enumerate(zip(tdims[:-1], tdims[1:])):
-            fp.add(f"top{i}.w", (b, a))
-            fp.add(f"top{i}.b", (b,))
-            self.top_layers.append((f"top{i}", a, b))
+                fp.add(f"dcn{i}.v", (cfg.dcn_rank, Wd))
+                u = make_lin(f"dcn{i}.u", cfg.dcn_rank, Wd)
+                self.dcn_u.append(u)
+                fp.add(u.name + ".w", (u.out, u.wcols))
         self.head_k = tdims[-1]
         fp.add("head", (self.head_k + 1,))           # [w (K) | b]
         opt = DENSE_OPTS[cfg.dense_opt]
@@ -164,42 +191,52 @@ class DLRMTrainer:
         fp.finalize(dev, with_adam=opt in (ops.OPT_ADAMW, ops.OPT_ADAM))
         self.fp = fp
         self._init_dense()
-        # broadcast dense params from rank 0 (replicated dense arch)
-        if world_size > 1:
+        if world_size > 1:                            # replicated dense arch
             dist.broadcast(fp.p, src=0, group=group)
         fp.sync_bf16()
         # ------------------------------------------------------ buffers
         bf = torch.bfloat16
-        z = lambda *s, dt=bf: torch.zeros(*s, dtype=dt, device=dev)  # noqa: E731
-        self.x0 = z(B, self.in_pad)
+
+        def z(*shape, dt=bf):
+            return torch.zeros(*shape, dtype=dt, device=dev)
+
+        def act_in(L: Lin):
+            t = z(B, L.wcols)
+            t[:, L.bcol] = 1.0
+            return t
+
+        # input buffer of every layer (augmented), output of the last bottom
+        # layer / last top layer are plain
+        self.x0 = act_in(self.bottom_layers[0])
+        self.bot_in = [self.x0] + [act_in(L) for L in self.bottom_layers[1:]]
+        self.h_out = z(B, D)
+        self.bot_grad = [z(B, L.out) for L in self.bottom_layers]
+        self.top_in = [act_in(L) for L in self.top_layers]
+        self.t_out = z(B, self.head_k)
+        self.top_grad = [z(B, L.out) for L in self.top_layers]
+        self.dz = z(B, self.top_layers[0].in_k)
         self.label = z(B, dt=torch.float32)
         self.ids = torch.zeros(self.emb.nnz_local, dtype=torch.int64, device=dev)
-        self.bot_act = [z(B, b) for (_, _, b) in self.bottom_layers]
-        self.bot_grad = [z(B, b) for (_, _, b) in self.bottom_layers]
-        self.zbuf = z(B, self.top_in)
-        self.dz = z(B, self.top_in)
-        self.top_act = [z(B, b) for (_, _, b) in self.top_layers]
-        self.top_grad = [z(B, b) for (_, _, b) in self.top_layers]
         if cfg.interaction == "dcn":
-            L = cfg.dcn_layers
-            self.dcn_x = [z(B, self.top_in) for _ in range(L + 1)]      # x_0 .. x_L
-            self.dcn_h = [z(B, cfg.dcn_rank) for _ in range(L)]         # V^T x_l
-            self.dcn_y = [z(B, self.top_in) for _ in range(L)]          # U h + b
-            self.dcn_dx = [z(B, self.top_in) for _ in range(L + 1)]
-            self.dcn_dx0acc = z(B, self.top_in)
-            self.dcn_dh = z(B, cfg.dcn_rank)
-            self.dcn_dy = z(B, self.top_in)
+            Lc, Wd, r = cfg.dcn_layers, self.top_real, cfg.dcn_rank
+            # x_0 .. x_{L-1} plain; x_L is top0's (augmented) input buffer
+            self.dcn_x = [z(B, Wd) for _ in range(Lc)] + [self.top_in[0]]
+            self.dcn_h = [act_in(u) for u in self.dcn_u]      # V^T x_l (+ ones col)
+            self.dcn_y = [z(B, Wd) for _ in range(Lc)]         # U h + b
+            self.dcn_dx = [z(B, Wd) for _ in range(Lc + 1)]
+            self.dcn_dx0acc = z(B, Wd)
+            self.dcn_dh = z(B, r)
+            self.dcn_dy = z(B, Wd)
         self.logits = z(B, dt=torch.float32)
         self.nparts = ops.head_parts(B)
         self.head_part = z(self.nparts * (self.head_k + 2), dt=torch.float32)
         self.loss_sum = z(1, dt=torch.float32)
         max_slab = 1
-        for (_, a, b) in self.bottom_layers + self.top_layers:
-            s = ops.wgrad_splits(b, a, B)
-            max_slab = max(max_slab, s * a * b)
+        for L in self.bottom_layers + self.top_layers + self.dcn_u:
+            max_slab = max(max_slab, ops.wgrad_splits(L.out, L.wcols, B) * L.out * L.wcols)
         if cfg.interaction == "dcn":
-            s = ops.wgrad_splits(cfg.dcn_rank, self.top_in, B)
-            max_slab = max(max_slab, s * cfg.dcn_rank * self.top_in)
+            s_ = ops.wgrad_splits(cfg.dcn_rank, self.top_real, B)
+            max_slab = max(max_slab, s_ * cfg.dcn_rank * self.top_real)
         self.slab = z(max_slab, dt=torch.float32)
         self.dense_hyper = torch.tensor([cfg.dense_lr, 0.0, 1.0], dtype=torch.float32, device=dev)
         self.emb_hyper = torch.tensor([cfg.emb_lr, 0.0], dtype=torch.float32, device=dev)
@@ -208,34 +245,28 @@ class DLRMTrainer:
         self.graph = None
         self.steps = 0
 
+    # for tests / checkpoints: (weight [out, in_real], bias [out]) views
+    def weight(self, name: str):
+        L = next(L for L in self.bottom_layers + self.top_layers + self.dcn_u if L.name == name)
+        W = self.fp.param(name + ".w")
+        return W[:, :L.in_real], W[:, L.bcol]
+
     # --------------------------------------------------------------- init
     def _init_dense(self):
         g = torch.Generator(device="cpu")
         g.manual_seed(self.cfg.seed + 7)
         fp = self.fp
-
-        def init_linear(name, out_f, in_f, real_in):
-            w = torch.randn(out_f, real_in, generator=g) * math.sqrt(2.0 / (real_in + out_f))
-            b = torch.randn(out_f, generator=g) * math.sqrt(1.0 / out_f)
-            W = fp.param(name + ".w")
+        for L in self.bottom_layers + self.top_layers + self.dcn_u:
+            W = fp.param(L.name + ".w")
             W.zero_()
-            W[:, :real_in] = w.to(W.device)
-            fp.param(name + ".b").copy_(b)
-
-        dims_real = [self.cfg.num_dense] + self.cfg.bottom
-        for i, (name, a, b) in enumerate(self.bottom_layers):
-            init_linear(name, b, a, dims_real[i])
-        F, D = self.F, self.cfg.embedding_dim
-        real_top_in = D + F * (F - 1) // 2 if self.cfg.interaction == "dot" else self.top_in
-        tdims_real = [real_top_in] + self.cfg.top[:-1]
-        for i, (name, a, b) in enumerate(self.top_layers):
-            init_linear(name, b, a, tdims_real[i])
+            w = torch.randn(L.out, L.in_real, generator=g) * math.sqrt(2.0 / (L.in_real + L.out))
+            W[:, :L.in_real] = w.to(W.device)
+            if not L.name.startswith("dcn"):
+                W[:, L.bcol] = (torch.randn(L.out, generator=g) * math.sqrt(1.0 / L.out)).to(W.device)
         if self.cfg.interaction == "dcn":
+            r, w = self.cfg.dcn_rank, self.top_real
             for i in range(self.cfg.dcn_layers):
-                r, w = self.cfg.dcn_rank, self.top_in
                 fp.param(f"dcn{i}.v").copy_(torch.randn(r, w, generator=g) * math.sqrt(2.0 / (r + w)))
-                fp.param(f"dcn{i}.u").copy_(torch.randn(w, r, generator=g) * math.sqrt(2.0 / (r + w)))
-                fp.param(f"dcn{i}.b").zero_()
         K = self.head_k
         h = fp.param("head")
         h[:K] = (torch.randn(K, generator=g) * math.sqrt(2.0 / (K + 1))).to(h.device)
@@ -252,15 +283,20 @@ class DLRMTrainer:
         self.ids.copy_(ids, non_blocking=True)
         self.label.copy_(label, non_blocking=True)
 
-    # --------------------------------------------------------------- step
-    def _linear_bwd(self, name, x, dy, dx, x_is_relu):
-        """wgrad + bias grad (+ dgrad into dx, masked by x > 0 if x_is_relu)."""
+    # ------------------------------------------------------------- layers
+    def _fwd(self, L: Lin, x, out, relu=True):
+        W = self.fp.bf16(L.name + ".w")
+        bias = None if L.bias_in_k else self.fp.param(L.name + ".w")[:, L.bcol]
+        ops.gemm(x[:, :L.in_k], False, W[:, :L.in_k], False, bias, relu, None, out, None, 1)
+
+    def _bwd(self, L: Lin, x, dy, dx, x_is_relu):
+        """weight+bias grad (augmented wgrad) and dgrad into dx (masked by x>0)."""
         fp = self.fp
-        gw = fp.grad(name + ".w")
-        ops.linear_wgrad(dy, x, gw.view(-1), slab=self.slab)
-        ops.colsum(dy, fp.grad(name + ".b"))
+        ops.linear_wgrad(dy, x, fp.grad(L.name + ".w").view(-1), slab=self.slab)
         if dx is not None:
-            ops.linear_dgrad(dy, fp.bf16(name + ".w"), mask=x if x_is_relu else None, out=dx)
+            W = fp.bf16(L.name + ".w")
+            ops.gemm(dy, False, W[:, :L.in_k], True, None, False,
+                     x[:, :L.in_k] if x_is_relu else None, dx, None, 1)
 
     # ---------------------------------------------------------- stages
     # The step is a fixed sequence of compute stages ("c", hipGraph-capturable)
@@ -290,12 +326,10 @@ class DLRMTrainer:
             fn()
 
     def _s_bottom_fwd(self):
-        fp = self.fp
-        h = self.x0
-        for i, (name, a, b) in enumerate(self.bottom_layers):
-            ops.linear_fwd(h, fp.bf16(name + ".w"), fp.param(name + ".b"), relu=True,
-                           out=self.bot_act[i])
-            h = self.bot_act[i]
+        n = len(self.bottom_layers)
+        for i, L in enumerate(self.bottom_layers):
+            out = self.bot_in[i + 1][:, :L.out] if i + 1 < n else self.h_out
+            self._fwd(L, self.bot_in[i], out)
 
     def _m_fwd_wait(self):
         self.emb.forward_wait()
@@ -306,31 +340,31 @@ class DLRMTrainer:
         cfg, fp, B = self.cfg, self.fp, self.B
         D, F = cfg.embedding_dim, self.F
         emb = self.emb
-        h = self.bot_act[-1]
+        h = self.h_out
+        L0 = self.top_layers[0]
         if cfg.interaction == "dot":
-            ops.interaction_fwd(h, emb.recv, self.slot_off, self.slot_stride, F, D, self.zbuf)
-            t = self.zbuf
+            ops.interaction_fwd(h, emb.recv, self.slot_off, self.slot_stride, F, D, self.top_in[0],
+                                L0.bcol)
         else:
-            t = self._dcn_forward(h)
-        for i, (name, a, b) in enumerate(self.top_layers):
-            ops.linear_fwd(t, fp.bf16(name + ".w"), fp.param(name + ".b"), relu=True,
-                           out=self.top_act[i])
-            t = self.top_act[i]
+            self._dcn_forward(h)
+        n = len(self.top_layers)
+        for i, L in enumerate(self.top_layers):
+            out = self.top_in[i + 1][:, :L.out] if i + 1 < n else self.t_out
+            self._fwd(L, self.top_in[i], out)
         K = self.head_k
         head = fp.param("head")
-        ops.head_bce(t, head[:K], head[K:], self.label, 1.0 / (B * self.world), True, self.logits,
-                     self.top_grad[-1], self.head_part)
+        ops.head_bce(self.t_out, head[:K], head[K:], self.label, 1.0 / (B * self.world), True,
+                     self.logits, self.top_grad[-1], self.head_part)
         ops.reduce_rows(self.head_part, self.nparts, K + 1, K + 2, fp.grad("head"))
         ops.reduce_rows(self.head_part[K + 1:], self.nparts, 1, K + 2, self.loss_sum,
                         accumulate=True)
-        for i in reversed(range(len(self.top_layers))):
-            name = self.top_layers[i][0]
-            x = self.top_act[i - 1] if i > 0 else t_in(self)
+        for i in reversed(range(n)):
+            L = self.top_layers[i]
             if i > 0:
                 dx = self.top_grad[i - 1]
             else:
                 dx = self.dz if cfg.interaction == "dot" else self.dcn_dx[-1]
-            self._linear_bwd(name, x, self.top_grad[i], dx, x_is_relu=i > 0)
+            self._bwd(L, self.top_in[i], self.top_grad[i], dx, x_is_relu=i > 0)
         if cfg.interaction == "dot":
             ops.interaction_bwd(self.dz, h, emb.recv, self.slot_off, self.slot_stride, F, D,
                                 self.bot_grad[-1], emb.d_recv, self.slot_off, self.slot_stride,
@@ -340,10 +374,9 @@ class DLRMTrainer:
 
     def _s_bottom_bwd(self):
         for i in reversed(range(len(self.bottom_layers))):
-            name = self.bottom_layers[i][0]
-            x = self.bot_act[i - 1] if i > 0 else self.x0
+            L = self.bottom_layers[i]
             dx = self.bot_grad[i - 1] if i > 0 else None
-            self._linear_bwd(name, x, self.bot_grad[i], dx, x_is_relu=i > 0)
+            self._bwd(L, self.bot_in[i], self.bot_grad[i], dx, x_is_relu=i > 0)
 
     def _m_allreduce_start(self):
         self._ar_work = None
@@ -373,29 +406,35 @@ class DLRMTrainer:
     # V-dgrad epilogue.
     def _dcn_forward(self, h):
         cfg, fp, D, F = self.cfg, self.fp, self.cfg.embedding_dim, self.F
+        Wd = self.top_real
         x0 = self.dcn_x[0]
         ops.concat_features(h, self.emb.recv, self.slot_off, self.slot_stride, F, D, x0)
         for i in range(cfg.dcn_layers):
-            ops.linear_fwd(self.dcn_x[i], fp.bf16(f"dcn{i}.v"), None, relu=False, out=self.dcn_h[i])
-            ops.gemm(self.dcn_h[i], False, fp.bf16(f"dcn{i}.u"), False, fp.param(f"dcn{i}.b"),
-                     False, None, self.dcn_y[i], None, 1, mul=x0, add=self.dcn_x[i],
-                     out2=self.dcn_x[i + 1])
-        return self.dcn_x[-1]
+            u = self.dcn_u[i]
+            ops.linear_fwd(self.dcn_x[i][:, :Wd], fp.bf16(f"dcn{i}.v"), None, relu=False,
+                           out=self.dcn_h[i][:, :u.in_real])
+            Uw = fp.bf16(u.name + ".w")
+            ops.gemm(self.dcn_h[i][:, :u.in_k], False, Uw[:, :u.in_k], False,
+                     None if u.bias_in_k else fp.param(u.name + ".w")[:, u.bcol], False, None,
+                     self.dcn_y[i], None, 1, mul=x0, add=self.dcn_x[i][:, :Wd],
+                     out2=self.dcn_x[i + 1][:, :Wd])
 
     def _dcn_backward(self, h):
         cfg, fp, D, F = self.cfg, self.fp, self.cfg.embedding_dim, self.F
-        L = cfg.dcn_layers
+        Lc, Wd = cfg.dcn_layers, self.top_real
         x0 = self.dcn_x[0]
         acc = self.dcn_dx0acc
-        for i in reversed(range(L)):
+        for i in reversed(range(Lc)):
+            u = self.dcn_u[i]
             dxo = self.dcn_dx[i + 1]
             # dy = dxo * x0 ; acc (+)= dxo * y (+ dxo at i == 0: x_0's residual)
-            ops.cross_bwd(dxo, x0, self.dcn_y[i], self.dcn_dy, acc, i != L - 1, i == 0)
-            ops.linear_wgrad(self.dcn_dy, self.dcn_h[i], fp.grad(f"dcn{i}.u").view(-1),
+            ops.cross_bwd(dxo, x0, self.dcn_y[i], self.dcn_dy, acc, i != Lc - 1, i == 0)
+            ops.linear_wgrad(self.dcn_dy, self.dcn_h[i], fp.grad(u.name + ".w").view(-1),
                              slab=self.slab)
-            ops.colsum(self.dcn_dy, fp.grad(f"dcn{i}.b"))
-            ops.linear_dgrad(self.dcn_dy, fp.bf16(f"dcn{i}.u"), out=self.dcn_dh)
-            ops.linear_wgrad(self.dcn_dh, self.dcn_x[i], fp.grad(f"dcn{i}.v").view(-1),
+            Uw = fp.bf16(u.name + ".w")
+            ops.gemm(self.dcn_dy, False, Uw[:, :u.in_k], True, None, False, None, self.dcn_dh,
+                     None, 1)
+            ops.linear_wgrad(self.dcn_dh, self.dcn_x[i][:, :Wd], fp.grad(f"dcn{i}.v").view(-1),
                              slab=self.slab)
             # dx_i = dh V + (i > 0 ? dxo : acc)
             ops.gemm(self.dcn_dh, False, fp.bf16(f"dcn{i}.v"), True, None, False, None, None, None,
@@ -461,31 +500,25 @@ class DLRMTrainer:
     @torch.no_grad()
     def predict(self) -> torch.Tensor:
         """Forward only on the static batch; returns logits [B] (fp32)."""
-        cfg, fp, D, F = self.cfg, self.fp, self.cfg.embedding_dim, self.F
+        cfg = self.cfg
         self.emb.forward(self.ids)
-        h = self.x0
-        for i, (name, a, b) in enumerate(self.bottom_layers):
-            ops.linear_fwd(h, fp.bf16(name + ".w"), fp.param(name + ".b"), relu=True,
-                           out=self.bot_act[i])
-            h = self.bot_act[i]
+        self._s_bottom_fwd()
+        L0 = self.top_layers[0]
         if cfg.interaction == "dot":
-            ops.interaction_fwd(h, self.emb.recv, self.slot_off, self.slot_stride, F, D, self.zbuf)
-            t = self.zbuf
+            ops.interaction_fwd(self.h_out, self.emb.recv, self.slot_off, self.slot_stride, self.F,
+                                cfg.embedding_dim, self.top_in[0], L0.bcol)
         else:
-            t = self._dcn_forward(h)
-        for i, (name, a, b) in enumerate(self.top_layers):
-            ops.linear_fwd(t, fp.bf16(name + ".w"), fp.param(name + ".b"), relu=True,
-                           out=self.top_act[i])
-            t = self.top_act[i]
+            self._dcn_forward(self.h_out)
+        n = len(self.top_layers)
+        for i, L in enumerate(self.top_layers):
+            out = self.top_in[i + 1][:, :L.out] if i + 1 < n else self.t_out
+            self._fwd(L, self.top_in[i], out)
         K = self.head_k
-        head = fp.param("head")
-        return t.float() @ head[:K] + head[K]
+        head = self.fp.param("head")
+        return self.t_out.float() @ head[:K] + head[K]
 
     def state_dict(self):
         return {"dense": self.fp.state_dict(), "emb": self.emb.state_dict(),
                 "dense_m": self.fp.m, "dense_v": self.fp.v, "dense_hyper": self.dense_hyper,
                 "emb_hyper": self.emb_hyper}
 
-
-def t_in(tr: "DLRMTrainer"):
-    return tr.zbuf if tr.cfg.interaction == "dot" else tr.dcn_x[-1]

@@ -65,11 +65,11 @@ def linear_wgrad(dy, x, out, slab=None, splits=None, accumulate=False):
     return out
 
 
-def interaction_fwd(dense, emb, off, stride, F, D, out):
+def interaction_fwd(dense, emb, off, stride, F, D, out, ones_col=-1):
     if _gpu(dense):
-        _native().interaction_fwd(dense, emb, list(off), list(stride), F, D, out)
+        _native().interaction_fwd(dense, emb, list(off), list(stride), F, D, out, ones_col)
     else:
-        ref.interaction_fwd(dense, emb, off, stride, F, D, out)
+        ref.interaction_fwd(dense, emb, off, stride, F, D, out, ones_col)
 
 
 def interaction_bwd(dz, dense, emb, off, stride, F, D, d_dense, d_emb, doff, dstride, relu_mask):

@@ -46,7 +46,7 @@ def gemm(a, a_col, b, b_col, bias=None, relu=False, mask=None, out=None, out32=N
             flat[M * N: splits * M * N].zero_()
 
 
-def interaction_fwd(dense, emb, off, stride, F, D, out):
+def interaction_fwd(dense, emb, off, stride, F, D, out, ones_col=-1):
     B = dense.shape[0]
     rows = [_f(dense[:, :D])]
     flat = emb.reshape(-1)
@@ -61,6 +61,8 @@ def interaction_fwd(dense, emb, off, stride, F, D, out):
     out.zero_()
     out[:, :D] = dense[:, :D].to(out.dtype)
     out[:, D:D + tri.shape[1]] = tri.to(out.dtype)
+    if ones_col >= 0:
+        out[:, ones_col] = 1.0
 
 
 def interaction_bwd(dz, dense, emb, off, stride, F, D, d_dense, d_emb, doff, dstride, relu_mask):

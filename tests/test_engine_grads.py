@@ -9,16 +9,29 @@ from tdfo_amd.models.dlrm import DLRMConfig, DLRMTrainer
 
 
 def autograd_reference(tr: DLRMTrainer, dense, ids, label):
+    """fp32 autograd of the same model; returns grads in the engine's
+    augmented parameter layout (bias in column bcol of each weight)."""
     cfg, fp = tr.cfg, tr.fp
     B, D, F = tr.B, cfg.embedding_dim, tr.F
-    params = {n: fp.param(n).detach().clone().requires_grad_(True) for n in fp.names()}
+    lins = tr.bottom_layers + tr.top_layers + tr.dcn_u
+    P = {}
+    for L in lins:
+        Wf = fp.param(L.name + ".w")
+        P[L.name + ".W"] = Wf[:, :L.in_real].detach().clone().requires_grad_(True)
+        P[L.name + ".b"] = Wf[:, L.bcol].detach().clone().requires_grad_(True)
+    for i in range(cfg.dcn_layers if cfg.interaction == "dcn" else 0):
+        P[f"dcn{i}.v"] = fp.param(f"dcn{i}.v").detach().clone().requires_grad_(True)
+    P["head"] = fp.param("head").detach().clone().requires_grad_(True)
     tabs = [tr.emb.get_table_weight(t)[1].detach().clone().requires_grad_(True)
             for t in range(cfg.num_tables)]
-    x = torch.zeros(B, tr.in_pad)
-    x[:, :cfg.num_dense] = dense
-    x = x.bfloat16().float()
-    for name, a, b in tr.bottom_layers:
-        x = torch.relu(x @ params[name + ".w"].t() + params[name + ".b"])
+
+    def lin(L, x, relu=True):
+        y = x @ P[L.name + ".W"].t() + P[L.name + ".b"]
+        return torch.relu(y) if relu else y
+
+    x = dense.float().bfloat16().float()
+    for L in tr.bottom_layers:
+        x = lin(L, x)
     feats = [x]
     off = 0
     for t, Lt in enumerate(cfg.pooling_factors()):
@@ -30,29 +43,36 @@ def autograd_reference(tr: DLRMTrainer, dense, ids, label):
         Z = torch.bmm(X, X.transpose(1, 2))
         li, lj = torch.tril_indices(F, F, offset=-1)
         t = torch.cat([x, Z[:, li, lj]], 1)
-        t = Fn.pad(t, (0, tr.top_in - t.shape[1]))
     else:
         x0 = X.reshape(B, F * D)
         xl = x0
-        for i in range(cfg.dcn_layers):
-            h = xl @ params[f"dcn{i}.v"].t()
-            y = h @ params[f"dcn{i}.u"].t() + params[f"dcn{i}.b"]
-            xl = x0 * y + xl
+        for i, u in enumerate(tr.dcn_u):
+            h = xl @ P[f"dcn{i}.v"].t()
+            xl = x0 * lin(u, h, relu=False) + xl
         t = xl
-    for name, a, b in tr.top_layers:
-        t = torch.relu(t @ params[name + ".w"].t() + params[name + ".b"])
+    for L in tr.top_layers:
+        t = lin(L, t)
     K = tr.head_k
-    logit = t @ params["head"][:K] + params["head"][K]
+    logit = t @ P["head"][:K] + P["head"][K]
     loss = Fn.binary_cross_entropy_with_logits(logit, label)
     loss.backward()
-    return {n: p.grad for n, p in params.items()}, [tb.grad for tb in tabs]
+    out = {}
+    for L in lins:
+        g = torch.zeros(L.out, L.wcols)
+        g[:, :L.in_real] = P[L.name + ".W"].grad
+        g[:, L.bcol] = P[L.name + ".b"].grad
+        out[L.name + ".w"] = g
+    for i in range(cfg.dcn_layers if cfg.interaction == "dcn" else 0):
+        out[f"dcn{i}.v"] = P[f"dcn{i}.v"].grad
+    out["head"] = P["head"].grad
+    return out, [tb.grad for tb in tabs]
 
 
 @pytest.mark.parametrize("interaction", ["dot", "dcn"])
 def test_engine_gradients_match_autograd(interaction):
     torch.manual_seed(0)
     cfg = DLRMConfig(embedding_dim=32, table_rows=[100, 20, 300], bottom=[64, 32],
-                     top=[64, 32, 1], interaction=interaction, dcn_layers=2, dcn_rank=32,
+                     top=[64, 32, 1], interaction=interaction, dcn_layers=2, dcn_rank=64,
                      pooling=[2, 1, 3], dense_opt="sgd", dense_lr=0.0, emb_opt="dense_grad")
     B = 64
     tr = DLRMTrainer(cfg, B, "cpu")
