@@ -5,8 +5,8 @@
 // observed to fault under hipGraph replay on gfx950) so the whole sort is a
 // fixed, capture-safe sequence of 3 kernels per 8-bit digit:
 //   hist    : one 1024-item tile per block, LDS digit histogram -> [tile][256]
-//   scan    : 256 threads, thread d scans digit d's column over tiles, then a
-//             block scan of the 256 digit totals gives each digit's base
+//   scan    : 16 threads per digit scan digit d's column over tiles and emit
+//             the digit totals (each scatter block scans those into bases)
 //   scatter : per tile, 4 rounds of 256 items; the stable rank of an item
 //             among equal digits is found with 8 wave ballots (lanes with the
 //             same digit), per-wave digit counts in LDS and a running count
@@ -39,36 +39,30 @@ __global__ __launch_bounds__(256) void rs_hist_kernel(const K* __restrict__ keys
   hist[(int64_t)blockIdx.x * 256 + t] = cnt[t];
 }
 
-__global__ __launch_bounds__(256) void rs_scan_kernel(int32_t* __restrict__ hist, int ntiles,
-                                                      int32_t* __restrict__ base) {
-  __shared__ int tot[256];
-  const int d = threadIdx.x;
+// Column scan of the [tile][256] histogram: 4 blocks x 1024 threads; block b
+// owns digits [64b, 64b+64), 16 threads per digit each scan a contiguous run
+// of tiles, partial sums are combined in LDS, then every thread rewrites its
+// run as exclusive prefixes. Digit totals go to `tot` (the scatter kernel
+// turns them into digit bases).
+__global__ __launch_bounds__(1024) void rs_scan_kernel(int32_t* __restrict__ hist, int ntiles,
+                                                       int32_t* __restrict__ tot) {
+  __shared__ int part[16][64];
+  const int dl = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const int d = blockIdx.x * 64 + dl;
+  const int per = (ntiles + 15) / 16;
+  const int t0 = ph * per, t1 = min(ntiles, t0 + per);
+  int s = 0;
+  for (int t = t0; t < t1; ++t) s += hist[(int64_t)t * 256 + d];
+  part[ph][dl] = s;
+  __syncthreads();
   int run = 0;
-  int t = 0;
-  for (; t + 4 <= ntiles; t += 4) {
-    const int c0 = hist[(int64_t)t * 256 + d], c1 = hist[(int64_t)(t + 1) * 256 + d];
-    const int c2 = hist[(int64_t)(t + 2) * 256 + d], c3 = hist[(int64_t)(t + 3) * 256 + d];
-    hist[(int64_t)t * 256 + d] = run;
-    hist[(int64_t)(t + 1) * 256 + d] = run + c0;
-    hist[(int64_t)(t + 2) * 256 + d] = run + c0 + c1;
-    hist[(int64_t)(t + 3) * 256 + d] = run + c0 + c1 + c2;
-    run += c0 + c1 + c2 + c3;
-  }
-  for (; t < ntiles; ++t) {
+  for (int q = 0; q < ph; ++q) run += part[q][dl];
+  if (ph == 15) tot[d] = run + s;
+  for (int t = t0; t < t1; ++t) {
     const int c = hist[(int64_t)t * 256 + d];
     hist[(int64_t)t * 256 + d] = run;
     run += c;
   }
-  tot[d] = run;
-  __syncthreads();
-  // exclusive scan of the 256 digit totals (Hillis-Steele in LDS)
-  for (int off = 1; off < 256; off <<= 1) {
-    const int v = d >= off ? tot[d - off] : 0;
-    __syncthreads();
-    tot[d] += v;
-    __syncthreads();
-  }
-  base[d] = tot[d] - run;
 }
 
 template <typename K>
@@ -78,14 +72,24 @@ __global__ __launch_bounds__(256) void rs_scatter_kernel(const K* __restrict__ k
                                                          int32_t* __restrict__ vout, int64_t n,
                                                          int shift,
                                                          const int32_t* __restrict__ hist,
-                                                         const int32_t* __restrict__ base) {
+                                                         const int32_t* __restrict__ tot) {
   __shared__ int run[256];
   __shared__ int wcnt[4][256];
   __shared__ int start[256];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  // digit bases: exclusive scan of the 256 digit totals (Hillis-Steele)
+  const int mytot = tot[t];
+  start[t] = mytot;
+  __syncthreads();
+  for (int off = 1; off < 256; off <<= 1) {
+    const int v = t >= off ? start[t - off] : 0;
+    __syncthreads();
+    start[t] += v;
+    __syncthreads();
+  }
+  start[t] = start[t] - mytot + hist[(int64_t)blockIdx.x * 256 + t];
   run[t] = 0;
   wcnt[0][t] = wcnt[1][t] = wcnt[2][t] = wcnt[3][t] = 0;
-  start[t] = base[t] + hist[(int64_t)blockIdx.x * 256 + t];
   __syncthreads();
   const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
   const int64_t tbase = (int64_t)blockIdx.x * RS_TILE;
@@ -131,7 +135,7 @@ int sort_impl(K* ka, int32_t* va, K* kb, int32_t* vb, int64_t n, int key_bits, i
   for (int p = 0; p < passes; ++p) {
     const int shift = 8 * p;
     hipLaunchKernelGGL(rs_hist_kernel<K>, dim3(ntiles), dim3(256), 0, s, kin, n, shift, hist);
-    hipLaunchKernelGGL(rs_scan_kernel, dim3(1), dim3(256), 0, s, hist, ntiles, base);
+    hipLaunchKernelGGL(rs_scan_kernel, dim3(4), dim3(1024), 0, s, hist, ntiles, base);
     hipLaunchKernelGGL(rs_scatter_kernel<K>, dim3(ntiles), dim3(256), 0, s, kin, vin, kout, vout,
                        n, shift, hist, base);
     TDFO_CHECK_HIP(hipGetLastError());
