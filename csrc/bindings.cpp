@@ -382,6 +382,38 @@ void auc_hist(const Tensor& logits, const Tensor& labels, int64_t nb, const Tens
                  reinterpret_cast<unsigned long long*>(hist.data_ptr<int64_t>()), cur_stream());
 }
 
+void two_tower(const Tensor& X, const Tensor& P, const Tensor& labels, double inv_n,
+               const Tensor& logits, const c10::optional<Tensor>& dX,
+               const c10::optional<Tensor>& part) {
+  check_dev(X, "X"); check_2d_rowmajor(X, "X");
+  const int64_t B = X.size(0);
+  TORCH_CHECK(X.scalar_type() == at::kFloat && X.size(1) >= 114 && X.stride(0) % 4 == 0 &&
+              aligned16(X.data_ptr()), "two_tower: X fp32 [B, >=114], 16B-aligned rows");
+  TORCH_CHECK(P.scalar_type() == at::kFloat && P.numel() >= tdfo::TT_NPARAM, "two_tower: P");
+  TORCH_CHECK(logits.scalar_type() == at::kFloat && logits.numel() == B, "two_tower: logits");
+  tdfo::TwoTowerArgs a{};
+  a.X = X.data_ptr<float>(); a.ldx = X.stride(0);
+  a.P = P.data_ptr<float>();
+  a.B = (int)B; a.inv_n = (float)inv_n;
+  a.logits = logits.data_ptr<float>();
+  const bool train = dX.has_value();
+  if (train) {
+    TORCH_CHECK(part.has_value(), "two_tower: train needs part");
+    const Tensor& d = *dX;
+    check_2d_rowmajor(d, "dX");
+    TORCH_CHECK(d.scalar_type() == at::kFloat && d.size(0) == B && d.size(1) >= 112 &&
+                d.stride(0) % 4 == 0 && aligned16(d.data_ptr()), "two_tower: dX");
+    TORCH_CHECK(labels.scalar_type() == at::kFloat && labels.numel() == B, "two_tower: labels");
+    TORCH_CHECK(part->scalar_type() == at::kFloat &&
+                part->numel() >= (int64_t)tdfo::two_tower_parts((int)B) * tdfo::TT_PART_LD &&
+                aligned16(part->data_ptr()), "two_tower: part");
+    a.labels = labels.data_ptr<float>();
+    a.dX = d.data_ptr<float>(); a.lddx = d.stride(0);
+    a.part = part->data_ptr<float>();
+  }
+  tdfo::two_tower(a, train ? 1 : 0, cur_stream());
+}
+
 }  // namespace
 
 TORCH_LIBRARY(tdfo, m) {
@@ -414,6 +446,8 @@ TORCH_LIBRARY(tdfo, m) {
   m.def("reduce_rows(Tensor inp, int rows, int n, int ld, Tensor(a!) out, bool accumulate, float scale) -> ()");
   m.def("colsum(Tensor x, Tensor(a!) out, bool accumulate) -> ()");
   m.def("auc_hist(Tensor logits, Tensor labels, int nb, Tensor(a!) hist) -> ()");
+  m.def("two_tower(Tensor X, Tensor P, Tensor labels, float inv_n, Tensor(a!) logits, "
+        "Tensor(b!)? dX, Tensor(c!)? part) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(tdfo, CUDA, m) {
@@ -433,4 +467,5 @@ TORCH_LIBRARY_IMPL(tdfo, CUDA, m) {
   m.impl("reduce_rows", reduce_rows);
   m.impl("colsum", colsum);
   m.impl("auc_hist", auc_hist);
+  m.impl("two_tower", two_tower);
 }

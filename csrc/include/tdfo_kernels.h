@@ -153,4 +153,23 @@ int colsum_parts(int M);
 void auc_hist(const float* logits, const float* labels, int n, int nb,
               unsigned long long* hist, hipStream_t s);
 
+// ------------------------------------------------------- two-tower ----
+// Fused TwoTower step (two_tower.hip). X: [B, ldx] fp32 with the user
+// embedding at cols [0,16) and the 98-wide item-tower input at [16,114).
+// P: 2400 flat params. train=1 also writes dX (embedding grads, cols [0,112))
+// and part[block][TT_PART_LD] = [dP (2400) | loss_sum].
+constexpr int TT_NPARAM = 2400;
+constexpr int TT_PART_LD = 2432;
+struct TwoTowerArgs {
+  const float* X; int64_t ldx;
+  const float* P;
+  const float* labels; float inv_n;
+  int B;
+  float* logits;
+  float* dX; int64_t lddx;
+  float* part;
+};
+int two_tower_parts(int B);
+void two_tower(const TwoTowerArgs& a, int train, hipStream_t s);
+
 }  // namespace tdfo

@@ -95,7 +95,7 @@ def build_data(force: bool = False) -> Path | None:
     srcs = sorted((CSRC / "data").glob("*.cpp"))
     if not srcs:
         return None
-    key = _digest(srcs + list((CSRC / "data").glob("*.h")), "data-v1")
+    key = _digest(srcs + list((CSRC / "data").glob("*.h")), "data-v2")
     stamp = BUILD / "data.stamp"
     if not force and DATA_LIB.exists() and stamp.exists() and stamp.read_text() == key:
         return DATA_LIB
@@ -103,7 +103,7 @@ def build_data(force: bool = False) -> Path | None:
     LIBDIR.mkdir(parents=True, exist_ok=True)
     tmp = DATA_LIB.with_suffix(".so.tmp")
     _run(["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", *map(str, srcs),
-          "-o", str(tmp)])
+          "-o", str(tmp), "-lz"])
     os.replace(tmp, DATA_LIB)
     stamp.write_text(key)
     return DATA_LIB

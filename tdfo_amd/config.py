@@ -84,6 +84,9 @@ class Config:
     emb_learning_rate: float = 0.01
     dense_optimizer: str = "adamw"
     hip_graph: bool = True
+    emb_update: str = "sparse"        # two_tower: sparse (fused row Adam) | dense (optax parity)
+    tower_init: str = ""              # two_tower: flax | keras ("" = by entrypoint flavor)
+    data_on_device: bool = True       # keep processed splits resident in HBM
     log_every: int = 100
     eval_every: int = 0
     ckpt_dir: str = ""

@@ -192,3 +192,19 @@ def sort_pairs(keys, vals, key_bits):
     k = keys & mask if key_bits < 63 else keys
     order = torch.sort(k, stable=True).indices
     return keys[order], vals[order]
+
+
+TT_NPARAM = ref.TT_NPARAM
+TT_PART_LD = ref.TT_PART_LD
+
+
+def two_tower_parts(B: int) -> int:
+    return (B + ref.TT_SPB - 1) // ref.TT_SPB
+
+
+def two_tower(X, P, labels, inv_n, logits, dX=None, part=None):
+    """Fused TwoTower forward (+ BCE + backward when dX/part given)."""
+    if _gpu(X):
+        _native().two_tower(X, P, labels, float(inv_n), logits, dX, part)
+    else:
+        ref.two_tower(X, P, labels, inv_n, logits, dX, part)

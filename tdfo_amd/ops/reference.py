@@ -343,3 +343,55 @@ def cross_bwd(dout, x0, y, dy, dx0, accumulate, add_dout=False):
     if add_dout:
         res = res + a
     dx0.copy_(res.to(dx0.dtype))
+
+
+TT_NPARAM = 2400
+TT_PART_LD = 2432
+TT_SPB = 128
+
+
+def two_tower_unpack(P):
+    """Flat TwoTower params -> dict of Flax-convention tensors (kernel [in, out])."""
+    E = 16
+    o = 0
+    out = {}
+    for name, rows in (("user_fc1", 16), ("user_fc2", 16), ("item_fc1", 98), ("item_fc2", 16)):
+        out[name + ".kernel"] = P[o: o + rows * E].view(rows, E)
+        o += rows * E
+        out[name + ".bias"] = P[o: o + E]
+        o += E
+    return out
+
+
+def two_tower_forward(X, P):
+    """fp32 forward of the towers (jax-flax/models.py:72-102). X [B, >=114]."""
+    p = two_tower_unpack(P)
+    xu, xi = X[:, :16], X[:, 16:114]
+    hu = xu @ p["user_fc1.kernel"] + p["user_fc1.bias"]
+    u = torch.nn.functional.silu(hu) @ p["user_fc2.kernel"] + p["user_fc2.bias"]
+    hi = xi @ p["item_fc1.kernel"] + p["item_fc1.bias"]
+    iv = torch.nn.functional.silu(hi) @ p["item_fc2.kernel"] + p["item_fc2.bias"]
+    return (u * iv).sum(1)
+
+
+def two_tower(X, P, labels, inv_n, logits, dX=None, part=None):
+    """Oracle of tdfo::two_tower via autograd. part rows follow the kernel:
+    one row per 128-sample block, [dP | loss_sum]."""
+    if dX is None:
+        with torch.no_grad():
+            logits.copy_(two_tower_forward(X.float(), P.float()))
+        return
+    B = X.shape[0]
+    Xr = X[:, :114].detach().float().clone().requires_grad_(True)
+    Pr = P[:TT_NPARAM].detach().float().clone().requires_grad_(True)
+    lg = two_tower_forward(Xr, Pr)
+    y = labels.float()
+    per = torch.nn.functional.binary_cross_entropy_with_logits(lg, y, reduction="none")
+    (per.sum() * inv_n).backward()
+    logits.copy_(lg.detach())
+    dX[:, :112].copy_(Xr.grad[:, :112])
+    nparts = (B + TT_SPB - 1) // TT_SPB
+    pv = part.view(-1)[: nparts * TT_PART_LD].view(nparts, TT_PART_LD)
+    pv.zero_()
+    pv[0, :TT_NPARAM] = Pr.grad
+    pv[0, TT_NPARAM] = per.detach().sum()

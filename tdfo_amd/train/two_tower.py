@@ -1,0 +1,170 @@
+"""TwoTower training driver behind the reference-compatible entrypoints.
+
+  mode "single": jax-flax/train.py:95-164, tensorflow2/train.py:22-57
+  mode "dp"    : jax-flax/train_dp.py:144-247, tensorflow2/train_dp.py:107-188
+                 (one process per GPU, RCCL; per-device batch x world = global)
+  mode "ps"    : tensorflow2/train_ps.py:125-165 — parameter servers become
+                 sharded embedding tables in HBM (all-to-all over xGMI); the
+                 ckpt/ backup/ log/ directories are kept (ModelCheckpoint,
+                 BackupAndRestore and TensorBoard equivalents).
+
+Log lines follow the reference formats; every epoch also
+appends a JSON line to ``metrics_file`` (or ``log/metrics.jsonl`` for ps).
+"""
+from __future__ import annotations
+
+import json
+import math
+import os
+import time
+from pathlib import Path
+from typing import Dict, List, Optional
+
+import torch
+
+from ..config import Config
+from ..data.columnar import DeviceColumns
+from ..data import goodreads as G
+from ..models.two_tower import TwoTowerConfig, TwoTowerTrainer
+from ..parallel.dist import init_distributed
+from ..utils import checkpoint as ckpt
+
+TRAIN_DTYPES = {"label": torch.float32, "avg_rating": torch.float32, "num_pages": torch.float32}
+ID_COLS = ["user_id", "item_id", "language", "is_ebook", "format", "publisher", "pub_decade"]
+
+
+def _load_split(cfg: Config, which: str) -> Dict:
+    pattern = cfg.train_data if which == "train" else cfg.eval_data
+    if cfg.write_format == "tfrecord" or pattern.endswith(".tfrecord"):
+        cols = G.read_tfrecord_columns(str(cfg.data_dir / "tfrecord" / pattern))
+    else:
+        cols = G.read_parquet_columns(str(cfg.data_dir / "parquet" / pattern))
+    keep = ID_COLS + ["avg_rating", "num_pages", "label"]
+    return {k: cols[k] for k in keep}
+
+
+def _dtypes():
+    d = dict(TRAIN_DTYPES)
+    d.update({k: torch.int64 for k in ID_COLS})
+    return d
+
+
+def _log(line: str, rank: int):
+    if rank == 0:
+        print(line, flush=True)
+
+
+def run(cfg: Config, mode: str = "single", flavor: str = "flax", out_dir: str = ".",
+        device: Optional[str] = None) -> List[Dict]:
+    if cfg.use_tpu:
+        raise ValueError("use_tpu: TPUs are not a target of this framework (MI355X only)")
+    if not cfg.size_map:
+        raise FileNotFoundError(f"{cfg.data_dir}/size_map.json missing: run preprocessing first")
+    if device is None:
+        device = "cuda" if torch.cuda.is_available() else "cpu"
+    info = init_distributed(device) if mode in ("dp", "ps") else None
+    rank = info.rank if info else 0
+    world = info.world_size if info else 1
+    dev = info.device if info else torch.device(device if device != "cuda" else "cuda:0")
+    group = info.group if info else None
+    out = Path(out_dir)
+
+    train_cols, eval_cols = _load_split(cfg, "train"), _load_split(cfg, "eval")
+    n_train, n_eval = len(train_cols["label"]), len(eval_cols["label"])
+    _log(f"===== train size: {n_train:,}, eval size: {n_eval:,} =====", rank)
+    if mode != "single":
+        _log(f"===== num devices: {world} =====\n", rank)
+    data_dev = dev if cfg.data_on_device else torch.device("cpu")
+    train = DeviceColumns(train_cols, data_dev, _dtypes())
+    evald = DeviceColumns(eval_cols, data_dev, _dtypes())
+
+    B, EB = cfg.per_device_train_batch_size, cfg.per_device_eval_batch_size
+    init = cfg.tower_init or ("keras" if flavor == "keras" else "flax")
+    tcfg = TwoTowerConfig(dict(cfg.size_map), cfg.embed_dim, cfg.learning_rate, cfg.weight_decay,
+                          init=init, emb_update=cfg.emb_update, seed=cfg.seed)
+    strategy = None
+    if mode == "ps":
+        strategy = cfg.sharding.strategy if cfg.sharding.strategy != "auto" else "row_wise"
+    tr = TwoTowerTrainer(tcfg, B, dev, group=group, rank=rank, world_size=world,
+                         eval_batch_size=EB if mode != "ps" else B, emb_sharding=strategy)
+    if mode == "ps":
+        EB = B       # the sharded engine has one static batch shape
+    drop_last = mode != "single"
+    start_epoch = 1
+    backup = out / "backup"
+    if mode == "ps":
+        for d in ("ckpt", "backup", "log"):
+            (out / d).mkdir(parents=True, exist_ok=True)
+        man = ckpt.load_manifest(str(backup))
+        if man is not None and man["world_size"] == world:
+            st = ckpt.load_sharded(str(backup), rank, world)
+            tr.load_state_dict({k: v.to(dev) for k, v in st["tensors"].items()})
+            start_epoch = int(st["meta"]["epoch"]) + 1
+            _log(f"===== restored from backup: resuming at epoch {start_epoch} =====", rank)
+    metrics_path = cfg.metrics_file or (str(out / "log" / "metrics.jsonl") if mode == "ps" else "")
+    history: List[Dict] = []
+    use_graph = (cfg.hip_graph and dev.type == "cuda" and mode == "single")
+    for epoch in range(start_epoch, cfg.n_epochs + 1):
+        t0 = time.perf_counter()
+        steps = 0
+        for batch in train.batches(B, shuffle=True, seed=cfg.seed, epoch=epoch,
+                                   drop_last=drop_last, rank=rank, world_size=world):
+            b = tr.load_batch({k: v.to(dev, non_blocking=True) for k, v in batch.items()})
+            if b == 0:
+                continue
+            tr.step()
+            steps += 1
+            if use_graph and tr.graph is None and b == B and steps >= 2:
+                tr.capture_graph()
+            if cfg.max_steps and steps >= cfg.max_steps:
+                break
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        tr_loss, tr_auc = tr.pop_metrics()
+        ex_s = steps * B * world / max(el, 1e-9)
+        if flavor == "keras":
+            _log(f"Epoch {epoch} train loss: {tr_loss:.4f}, train auc: {tr_auc:.4f}", rank)
+        elif mode == "single":
+            _log(f"\nEpoch {epoch} train loss: {tr_loss:.4f}", rank)
+        else:
+            _log(f"\nEpoch {epoch} train loss: {tr_loss:.4f}, roc_auc: {tr_auc:.4f}", rank)
+        for batch in evald.batches(EB, shuffle=False, drop_last=False, rank=rank,
+                                   world_size=world):
+            if len(batch["label"]) == 0 and tr.sharded is None:
+                continue
+            tr.load_batch({k: v.to(dev, non_blocking=True) for k, v in batch.items()},
+                          eval_mode=True)
+            tr.evaluate_batch()
+        ev_loss, ev_auc = tr.pop_metrics(eval_mode=True)
+        if flavor == "keras":
+            _log(f"Epoch {epoch} eval loss: {ev_loss:.4f}, eval auc: {ev_auc:.4f}", rank)
+        elif mode == "single":
+            _log(f"\nEpoch {epoch} eval loss: {ev_loss:.4f}", rank)
+        else:
+            _log(f"\nEpoch {epoch} eval loss: {ev_loss:.4f}, roc_auc: {ev_auc:.4f}", rank)
+        rec = {"epoch": epoch, "train_loss": tr_loss, "train_auc": tr_auc, "eval_loss": ev_loss,
+               "eval_auc": ev_auc, "steps": steps, "examples_per_sec": ex_s, "world_size": world}
+        history.append(rec)
+        _log(f"[throughput] epoch {epoch}: {ex_s:,.0f} examples/s over {world} device(s)", rank)
+        if metrics_path and rank == 0:
+            Path(metrics_path).parent.mkdir(parents=True, exist_ok=True)
+            with open(metrics_path, "a") as f:
+                f.write(json.dumps(rec) + "\n")
+        if mode == "ps":
+            state = {k: v for k, v in tr.state_dict().items()}
+            bar = (lambda: torch.distributed.barrier()) if world > 1 else None
+            ckpt.save_sharded(str(out / "ckpt" / f"epoch_{epoch}"), rank, world, epoch, state,
+                              {"epoch": epoch}, barrier=bar)
+            ckpt.save_sharded(str(backup), rank, world, epoch, state, {"epoch": epoch},
+                              barrier=bar)
+    params = tr.flax_params()
+    if rank == 0 and flavor == "flax":
+        ckpt.save_flax_params(params, str(out / "model_params.pt"))
+    if mode == "ps" and rank == 0:
+        # training finished: BackupAndRestore deletes its backup on success
+        for f in backup.glob("*"):
+            f.unlink()
+    if info is not None and world > 1:
+        torch.distributed.barrier()
+    return history
