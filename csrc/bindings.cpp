@@ -414,6 +414,40 @@ void two_tower(const Tensor& X, const Tensor& P, const Tensor& labels, double in
   tdfo::two_tower(a, train ? 1 : 0, cur_stream());
 }
 
+void linear_xent(const Tensor& H, const Tensor& W, const Tensor& bias, const Tensor& labels,
+                 double eps, int64_t ignore, const Tensor& dH, const Tensor& lossv,
+                 const c10::optional<Tensor>& dW, const c10::optional<Tensor>& db) {
+  check_dev(H, "H");
+  TORCH_CHECK(H.scalar_type() == at::kFloat && H.dim() == 2 && H.size(1) == 16 &&
+              H.is_contiguous() && aligned16(H.data_ptr()), "linear_xent: H fp32 [N,16]");
+  const int64_t N = H.size(0), V = W.size(0);
+  TORCH_CHECK(W.scalar_type() == at::kFloat && W.dim() == 2 && W.size(1) == 16 &&
+              W.is_contiguous() && aligned16(W.data_ptr()), "linear_xent: W fp32 [V,16]");
+  TORCH_CHECK(bias.scalar_type() == at::kFloat && bias.numel() == V && bias.is_contiguous(),
+              "linear_xent: bias [V]");
+  TORCH_CHECK(labels.scalar_type() == at::kLong && labels.numel() == N && labels.is_contiguous(),
+              "linear_xent: labels int64 [N]");
+  TORCH_CHECK(dH.scalar_type() == at::kFloat && dH.sizes() == H.sizes() && dH.is_contiguous() &&
+              aligned16(dH.data_ptr()), "linear_xent: dH");
+  TORCH_CHECK(lossv.scalar_type() == at::kFloat && lossv.numel() == N, "linear_xent: lossv");
+  TORCH_CHECK(N < (1 << 30) && V < (1ll << 31), "linear_xent: sizes");
+  tdfo::LinearXentArgs a{};
+  a.H = H.data_ptr<float>(); a.W = W.data_ptr<float>(); a.bias = bias.data_ptr<float>();
+  a.labels = labels.data_ptr<int64_t>();
+  a.N = (int)N; a.V = V; a.ignore = (int)ignore; a.eps = (float)eps;
+  a.dH = dH.data_ptr<float>(); a.lossv = lossv.data_ptr<float>();
+  if (dW.has_value()) {
+    TORCH_CHECK(db.has_value() && dW->sizes() == W.sizes() && dW->is_contiguous() &&
+                dW->scalar_type() == at::kFloat && aligned16(dW->data_ptr()) &&
+                db->numel() == V && db->scalar_type() == at::kFloat, "linear_xent: dW/db");
+    a.dW = dW->data_ptr<float>(); a.db = db->data_ptr<float>();
+  }
+  Tensor ws = at::empty({(int64_t)tdfo::linear_xent_workspace((int)N, V)},
+                        H.options().dtype(at::kByte));
+  a.workspace = ws.data_ptr();
+  tdfo::linear_xent(a, cur_stream());
+}
+
 }  // namespace
 
 TORCH_LIBRARY(tdfo, m) {
@@ -446,6 +480,8 @@ TORCH_LIBRARY(tdfo, m) {
   m.def("reduce_rows(Tensor inp, int rows, int n, int ld, Tensor(a!) out, bool accumulate, float scale) -> ()");
   m.def("colsum(Tensor x, Tensor(a!) out, bool accumulate) -> ()");
   m.def("auc_hist(Tensor logits, Tensor labels, int nb, Tensor(a!) hist) -> ()");
+  m.def("linear_xent(Tensor H, Tensor W, Tensor bias, Tensor labels, float eps, int ignore, "
+        "Tensor(a!) dH, Tensor(b!) lossv, Tensor(c!)? dW, Tensor(d!)? db) -> ()");
   m.def("two_tower(Tensor X, Tensor P, Tensor labels, float inv_n, Tensor(a!) logits, "
         "Tensor(b!)? dX, Tensor(c!)? part) -> ()");
 }
@@ -468,4 +504,5 @@ TORCH_LIBRARY_IMPL(tdfo, CUDA, m) {
   m.impl("colsum", colsum);
   m.impl("auc_hist", auc_hist);
   m.impl("two_tower", two_tower);
+  m.impl("linear_xent", linear_xent);
 }

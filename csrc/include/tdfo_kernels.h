@@ -172,4 +172,21 @@ struct TwoTowerArgs {
 int two_tower_parts(int B);
 void two_tower(const TwoTowerArgs& a, int train, hipStream_t s);
 
+// ----------------------------------------------------- linear + xent ----
+// Fused Linear(16 -> V) + CrossEntropy(ignore_index, label_smoothing=eps),
+// forward and backward without materialising logits (linear_xent.hip).
+struct LinearXentArgs {
+  const float* H;          // [N, 16]
+  const float* W;          // [V, 16]
+  const float* bias;       // [V]
+  const int64_t* labels;   // [N]
+  int N; int64_t V; int ignore; float eps;
+  float* dH;               // [N, 16] (scaled by 1/n_valid)
+  float* lossv;            // [N] per-token loss (0 for ignored)
+  float* dW; float* db;    // optional [V, 16], [V]
+  void* workspace;
+};
+size_t linear_xent_workspace(int N, int64_t V);
+void linear_xent(const LinearXentArgs& a, hipStream_t s);
+
 }  // namespace tdfo

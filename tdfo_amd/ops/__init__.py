@@ -208,3 +208,11 @@ def two_tower(X, P, labels, inv_n, logits, dX=None, part=None):
         _native().two_tower(X, P, labels, float(inv_n), logits, dX, part)
     else:
         ref.two_tower(X, P, labels, inv_n, logits, dX, part)
+
+
+def linear_xent(H, W, bias, labels, eps, ignore, dH, lossv, dW=None, db=None):
+    """Fused Linear(16->V) + label-smoothed CrossEntropy, fwd+bwd (no logits)."""
+    if _gpu(H):
+        _native().linear_xent(H, W, bias, labels, float(eps), int(ignore), dH, lossv, dW, db)
+    else:
+        ref.linear_xent(H, W, bias, labels, eps, ignore, dH, lossv, dW, db)

@@ -395,3 +395,21 @@ def two_tower(X, P, labels, inv_n, logits, dX=None, part=None):
     pv.zero_()
     pv[0, :TT_NPARAM] = Pr.grad
     pv[0, TT_NPARAM] = per.detach().sum()
+
+
+def linear_xent(H, W, bias, labels, eps, ignore, dH, lossv, dW=None, db=None):
+    """Oracle: logits = H W^T + b; CrossEntropy(ignore_index, label_smoothing)
+    mean over non-ignored tokens; per-token loss in lossv, grads of the mean."""
+    Hr = H.detach().float().clone().requires_grad_(True)
+    Wr = W.detach().float().clone().requires_grad_(True)
+    br = bias.detach().float().clone().requires_grad_(True)
+    logits = Hr @ Wr.t() + br
+    per = torch.nn.functional.cross_entropy(logits, labels, ignore_index=ignore,
+                                            label_smoothing=eps, reduction="none")
+    nv = max(1, int((labels != ignore).sum()))
+    (per.sum() / nv).backward()
+    lossv.copy_(per.detach())
+    dH.copy_(Hr.grad)
+    if dW is not None:
+        dW.copy_(Wr.grad)
+        db.copy_(br.grad)
