@@ -1,0 +1,394 @@
+"""Bert4Rec (reference torchrec/models.py + torchrec/train.py), MI355X layout.
+
+Architecture (kept 1:1, including the reference's quirks):
+  item embedding (V = n_items + 2, uniform[-1, 1], PAD id 0 embedded: Q9)
+  + learned positional encoding randn(T, E)
+  -> LayerNorm over [T, E] jointly (Q10) -> dropout
+  -> n_layers x pre-norm transformer block
+       x + drop(MHA(LN(x)))   (key-padding mask, masked_fill(-1e9), softmax, dropout)
+       x + drop(FFN(LN(x)))   (E -> 4E ReLU dropout -> E), then block dropout
+  -> Linear(E, V) + CrossEntropy(ignore_index=0, label_smoothing=0.1)
+
+What is different on MI355X:
+  * the output projection + loss is ``tdfo::linear_xent``: online softmax
+    over vocab splits, forward and backward fused, the [B*T, V] logits are
+    never written (the reference's largest tensor);
+  * the item table lives in a table-batched fp32 store updated by the
+    sort-based fused Adam inside backward (TorchRec DMP ``fused_params``
+    semantics) — locally, replicated with a sparse (ids, row-grad)
+    all-gather for DDP mode, or sharded (``model_parallel``) through the
+    all-to-all embedding engine;
+  * all dense parameters sit in one flat buffer updated by one fused Adam
+    launch (torch.optim.Adam semantics: L2 weight decay added to the grad);
+  * the whole single-GPU step (encoder fwd/bwd included) is captured into
+    one hipGraph (the encoder is ~100 tiny ops at E=16, T=20).
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Optional
+
+import torch
+import torch.distributed as dist
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .. import ops
+from ..optim.flat import FlatOptimizer
+from ..sparse.tables import EmbOptimConfig, TableBatchedEmbedding, TableConfig
+
+PAD_ID = 0
+METRICS_K = (10, 20, 50)
+
+
+# ------------------------------------------------------------------ encoder
+class MultiHeadedAttention(nn.Module):
+    def __init__(self, num_heads: int, dim: int, dropout: float = 0.1):
+        super().__init__()
+        assert dim % num_heads == 0          # torchrec/models.py:40
+        self.d_k = dim // num_heads
+        self.h = num_heads
+        self.linear_layers = nn.ModuleList([nn.Linear(dim, dim) for _ in range(3)])
+        self.output_linear = nn.Linear(dim, dim)
+        self.dropout = nn.Dropout(dropout)
+
+    def forward(self, x, mask):
+        B, T, _ = x.shape
+        w = torch.cat([l.weight for l in self.linear_layers], 0)       # one QKV GEMM
+        b = torch.cat([l.bias for l in self.linear_layers], 0)
+        qkv = F.linear(x, w, b).view(B, T, 3, self.h, self.d_k).permute(2, 0, 3, 1, 4)
+        q, k, v = qkv[0], qkv[1], qkv[2]
+        scores = torch.matmul(q, k.transpose(-2, -1)) / math.sqrt(self.d_k)
+        scores = scores.masked_fill(~mask, -1e9)
+        p = self.dropout(torch.softmax(scores, dim=-1))
+        out = torch.matmul(p, v).transpose(1, 2).reshape(B, T, self.h * self.d_k)
+        return self.output_linear(out)
+
+
+class FeedForward(nn.Module):
+    def __init__(self, dim: int, dropout: float = 0.1):
+        super().__init__()
+        self.w_1 = nn.Linear(dim, 4 * dim)
+        self.w_2 = nn.Linear(4 * dim, dim)
+        self.dropout = nn.Dropout(dropout)
+
+    def forward(self, x):
+        return self.w_2(self.dropout(F.relu(self.w_1(x))))
+
+
+class SublayerConnection(nn.Module):
+    def __init__(self, dim: int, dropout: float):
+        super().__init__()
+        self.norm = nn.LayerNorm(dim)
+        self.dropout = nn.Dropout(dropout)
+
+    def forward(self, x, fn):
+        return x + self.dropout(fn(self.norm(x)))       # pre-norm (torchrec/models.py:102-106)
+
+
+class TransformerBlock(nn.Module):
+    def __init__(self, dim: int, heads: int, dropout: float):
+        super().__init__()
+        self.attention = MultiHeadedAttention(heads, dim, dropout)
+        self.feed_forward = FeedForward(dim, dropout)
+        self.input_sublayer = SublayerConnection(dim, dropout)
+        self.output_sublayer = SublayerConnection(dim, dropout)
+        self.dropout = nn.Dropout(dropout)
+
+    def forward(self, x, mask):
+        x = self.input_sublayer(x, lambda y: self.attention(y, mask))
+        x = self.output_sublayer(x, self.feed_forward)
+        return self.dropout(x)
+
+
+# ---------------------------------------------------------- item embedding
+class _SeqEmbFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, ids, anchor, owner):
+        ctx.owner = owner
+        return owner._lookup(ids)
+
+    @staticmethod
+    def backward(ctx, grad):
+        ctx.owner._update(grad.contiguous())
+        return None, None, None
+
+
+class ItemEmbedding(nn.Module):
+    """Replicated item table with the fused sparse Adam in backward.
+    ``group``/``world`` > 1: DDP semantics (row grads averaged over ranks)
+    via one all-gather of ids and row grads instead of a dense all-reduce."""
+
+    def __init__(self, vocab: int, dim: int, n_tokens: int, optim: EmbOptimConfig, device,
+                 group=None, world: int = 1, seed: int = 0):
+        super().__init__()
+        self.store = TableBatchedEmbedding([vocab], dim, device, optim, init_ranges=[1.0],
+                                           seed=seed)
+        self.D = dim
+        self.N = n_tokens
+        self.group, self.world = group, world
+        self.hyper = torch.tensor([optim.lr, 0.0], dtype=torch.float32, device=device)
+        self.offsets = torch.arange(n_tokens * world + 1, dtype=torch.int64, device=device)
+        self.zero = torch.zeros(1, dtype=torch.int64, device=device)
+        self.out = torch.zeros(n_tokens, dim, dtype=torch.float32, device=device)
+        if world > 1:
+            self.g_ids = torch.zeros(world * n_tokens, dtype=torch.int64, device=device)
+            self.g_grad = torch.zeros(world * n_tokens, dim, dtype=torch.float32, device=device)
+        self._anchor = nn.Parameter(torch.zeros(1, device=device))
+        self._ids = None
+
+    @property
+    def weight(self):
+        return self.store.weight
+
+    def _lookup(self, ids):
+        n = ids.numel()
+        out = self.out[:n]
+        self.store.forward(ids, self.offsets[: n + 1], self.zero, 1, n, out, self.zero, self.D)
+        self._ids = ids
+        return out.clone()
+
+    def _update(self, grad):
+        ids = self._ids
+        n = ids.numel()
+        self.hyper[1:2].add_(1.0)
+        if self.world > 1:
+            dist.all_gather_into_tensor(self.g_ids[: self.world * n], ids, group=self.group)
+            dist.all_gather_into_tensor(self.g_grad[: self.world * n], grad, group=self.group)
+            self.g_grad.mul_(1.0 / self.world)
+            ids, grad, n = self.g_ids[: self.world * n], self.g_grad[: self.world * n], self.world * n
+        self.store.backward_update(ids, self.offsets[: n + 1], self.zero, 1, n, grad, self.zero,
+                                   self.D, self.hyper)
+
+    def forward(self, ids):
+        if self.training and torch.is_grad_enabled():
+            return _SeqEmbFn.apply(ids, self._anchor, self)
+        return self._lookup(ids)
+
+
+class _LinearXentFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, H, W, b, labels, eps):
+        N = H.shape[0]
+        dH = torch.empty_like(H)
+        lossv = torch.empty(N, dtype=torch.float32, device=H.device)
+        dW = torch.empty_like(W)
+        db = torch.empty_like(b)
+        ops.linear_xent(H, W, b, labels, eps, PAD_ID, dH, lossv, dW, db)
+        nv = (labels != PAD_ID).sum().clamp_min(1).to(torch.float32)
+        ctx.save_for_backward(dH, dW, db)
+        return lossv.sum() / nv
+
+    @staticmethod
+    def backward(ctx, g):
+        dH, dW, db = ctx.saved_tensors
+        return dH * g, dW * g, db * g, None, None
+
+
+def linear_cross_entropy(H, W, b, labels, eps=0.1):
+    """mean CE(ignore_index=0, label_smoothing=eps) of H @ W^T + b, fused."""
+    return _LinearXentFn.apply(H.contiguous(), W, b, labels.contiguous(), eps)
+
+
+class Bert4Rec(nn.Module):
+    """Reference parameter names are preserved (state_dict() keys match
+    torchrec's Bert4Rec except the item table, exported by the trainer)."""
+
+    def __init__(self, vocab_size: int, max_len: int, embed_dim: int, num_heads: int,
+                 num_layers: int, dropout: float = 0.1):
+        super().__init__()
+        self.vocab_size, self.max_len, self.emb_dim = vocab_size, max_len, embed_dim
+        self.positional_encoding = nn.Parameter(torch.randn(max_len, embed_dim))
+        self.layernorm = nn.LayerNorm([max_len, embed_dim])
+        self.emb_dropout = nn.Dropout(dropout)
+        self.transformer_blocks = nn.ModuleList(
+            [TransformerBlock(embed_dim, num_heads, dropout) for _ in range(num_layers)])
+        self.out = nn.Linear(embed_dim, vocab_size)
+
+    def encode(self, item_emb: torch.Tensor, seqs: torch.Tensor) -> torch.Tensor:
+        """item_emb [B, T, E] (looked-up rows), seqs [B, T] ids -> hidden [B, T, E]."""
+        mask = (seqs != PAD_ID).unsqueeze(1).unsqueeze(1)          # [B, 1, 1, T] key mask
+        x = self.emb_dropout(self.layernorm(item_emb + self.positional_encoding))
+        for blk in self.transformer_blocks:
+            x = blk(x, mask)
+        return x
+
+
+# ------------------------------------------------------------------ metrics
+def recall_ndcg_sums(scores: torch.Tensor) -> torch.Tensor:
+    """scores [B, 1 + negs], positive in column 0 (torchrec/train.py:52-78).
+    Returns per-metric SUMS over the batch in the order
+    [Recall@10, Recall@20, Recall@50, NDCG@10, NDCG@20, NDCG@50]."""
+    rank = (scores[:, 1:] > scores[:, :1]).sum(1)                     # 0-based rank of the positive
+    rec = [(rank < k).float().sum() for k in METRICS_K]
+    ndcg = [torch.where(rank < k, 1.0 / torch.log2(rank.float() + 2.0),
+                        torch.zeros_like(rank, dtype=torch.float32)).sum() for k in METRICS_K]
+    return torch.stack(rec + ndcg)
+
+
+METRIC_NAMES = [f"Recall@{k}" for k in METRICS_K] + [f"NDCG@{k}" for k in METRICS_K]
+
+
+# ------------------------------------------------------------------ trainer
+class Bert4RecTrainer:
+    """One rank of Bert4Rec training. mode: "local" | "ddp" | "dmp"."""
+
+    def __init__(self, n_items: int, max_len: int = 20, embed_dim: int = 16, n_heads: int = 2,
+                 n_layers: int = 2, batch_size: int = 16, lr: float = 3e-4, wd: float = 1e-4,
+                 device="cpu", mode: str = "local", group=None, rank: int = 0, world: int = 1,
+                 dropout: float = 0.1, seed: int = 42, label_smoothing: float = 0.1):
+        self.V = n_items + 2                     # 0 = PAD, n_items + 1 = MASK
+        self.T, self.E, self.B = max_len, embed_dim, batch_size
+        self.device = dev = torch.device(device)
+        self.mode, self.group, self.rank, self.world = mode, group, rank, world
+        self.eps = label_smoothing
+        torch.manual_seed(seed)
+        self.model = Bert4Rec(self.V, max_len, embed_dim, n_heads, n_layers, dropout).to(dev)
+        emb_opt = EmbOptimConfig("adam", lr=lr, weight_decay=wd)
+        ntok = batch_size * max_len
+        if mode == "dmp":
+            from ..sparse.modules import ShardedEmbeddingModule
+            tab = TableConfig("item_embedding", self.V, embed_dim, init_range=1.0)
+            self.item = ShardedEmbeddingModule([tab], ntok, [1], emb_opt, dev, world_size=world,
+                                               rank=rank, group=group, seed=seed)
+            full = TableBatchedEmbedding([self.V], embed_dim, dev, emb_opt, init_ranges=[1.0],
+                                         seed=seed)
+            self.item.set_table_weight(0, full.weight)      # identical init on every rank
+            del full
+        else:
+            self.item = ItemEmbedding(self.V, embed_dim, ntok, emb_opt, dev,
+                                      group=group if mode == "ddp" else None,
+                                      world=world if mode == "ddp" else 1, seed=seed)
+        if world > 1:     # identical dense init on all ranks (DDP broadcasts from rank 0)
+            for p in self.model.parameters():
+                dist.broadcast(p.data, 0, group=group)
+        self.opt = FlatOptimizer(self.model.parameters(), "adam", lr=lr, weight_decay=wd,
+                                 group=group if world > 1 else None)
+        self.seqs = torch.zeros(batch_size, max_len, dtype=torch.int64, device=dev)
+        self.labels = torch.zeros(batch_size, max_len, dtype=torch.int64, device=dev)
+        self.loss_sum = torch.zeros(1, dtype=torch.float64, device=dev)
+        self.steps = 0
+        self.metric_sums = torch.zeros(len(METRIC_NAMES) + 1, dtype=torch.float64, device=dev)
+        self.graph = None
+        self._static_loss = None
+
+    # ------------------------------------------------------------ train
+    def _embed(self, seqs):
+        B, T = seqs.shape
+        flat = seqs.reshape(-1)
+        if self.mode == "dmp":
+            return self.item(flat)[0].view(B, T, self.E)
+        return self.item(flat).view(B, T, self.E)
+
+    def _fwd_bwd(self, seqs, labels):
+        self.model.train()
+        self.item.train()
+        x = self._embed(seqs)
+        h = self.model.encode(x, seqs)
+        loss = linear_cross_entropy(h.reshape(-1, self.E), self.model.out.weight,
+                                    self.model.out.bias, labels.reshape(-1), self.eps)
+        loss.backward()
+        return loss
+
+    def _step_body(self, seqs, labels):
+        self.opt.grad.zero_()
+        loss = self._fwd_bwd(seqs, labels)
+        self.opt.all_reduce_grads(average=True)
+        self.opt.step()
+        self.loss_sum.add_(loss.detach().double())
+        return loss
+
+    def load_batch(self, seqs, labels):
+        b = seqs.shape[0]
+        assert b == self.B, "Bert4Rec steps use full batches"
+        self.seqs.copy_(seqs, non_blocking=True)
+        self.labels.copy_(labels, non_blocking=True)
+
+    def step(self):
+        if self.graph is not None:
+            self.graph.replay()
+        else:
+            self._step_body(self.seqs, self.labels)
+        self.steps += 1
+
+    def capture_graph(self, warmup: int = 2):
+        """Whole step (encoder fwd/bwd, fused xent, fused embedding Adam,
+        flat Adam) in one hipGraph; single process only."""
+        if self.device.type != "cuda" or self.world > 1:
+            return
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                self._step_body(self.seqs, self.labels)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._step_body(self.seqs, self.labels)
+        torch.cuda.synchronize()
+        self.graph = g
+
+    def pop_loss(self) -> float:
+        """Average training loss since the last call, averaged over ranks."""
+        v = torch.stack([self.loss_sum[0], torch.tensor(float(self.steps), dtype=torch.float64,
+                                                        device=self.device)])
+        if self.world > 1:
+            dist.all_reduce(v, group=self.group)
+        self.loss_sum.zero_()
+        self.steps = 0
+        return float(v[0] / max(1.0, float(v[1])))
+
+    # ------------------------------------------------------------ eval
+    @torch.no_grad()
+    def eval_batch(self, seqs: torch.Tensor, candidates: torch.Tensor):
+        """Score the last position against 1 + 100 candidates (no [B, V]
+        logits: gathered output rows only) and accumulate metric sums."""
+        self.model.eval()
+        self.item.eval()
+        B = seqs.shape[0]
+        if self.mode == "dmp" and B < self.B:     # sharded engine has a static shape
+            pad = torch.zeros(self.B - B, self.T, dtype=seqs.dtype, device=seqs.device)
+            seqs_p = torch.cat([seqs, pad])
+        else:
+            seqs_p = seqs
+        h = self.model.encode(self._embed(seqs_p), seqs_p)[:B, -1, :]         # [B, E]
+        w = self.model.out.weight[candidates]                                # [B, C, E]
+        scores = torch.einsum("bce,be->bc", w, h) + self.model.out.bias[candidates]
+        self.metric_sums[:-1] += recall_ndcg_sums(scores).double()
+        self.metric_sums[-1] += B
+
+    def pop_metrics(self) -> Dict[str, float]:
+        v = self.metric_sums.clone()
+        if self.world > 1:
+            dist.all_reduce(v, group=self.group)
+        self.metric_sums.zero_()
+        n = max(1.0, float(v[-1]))
+        return {k: float(v[i]) / n for i, k in enumerate(METRIC_NAMES)}
+
+    # ------------------------------------------------------------ state
+    def item_table(self) -> torch.Tensor:
+        if self.mode == "dmp":
+            full = torch.zeros(self.V, self.E, dtype=torch.float32, device=self.device)
+            part = self.item.engine.get_table_weight(0)
+            if part is not None:
+                lo, w = part
+                full[lo: lo + w.shape[0]].copy_(w)
+            if self.world > 1:
+                dist.all_reduce(full, group=self.group)
+            return full
+        return self.item.weight[: self.V]
+
+    def state_dict(self) -> Dict[str, torch.Tensor]:
+        """torchrec Bert4Rec key layout (torchrec/models.py:132-223)."""
+        sd = {}
+        for k, v in self.model.state_dict().items():
+            if k == "positional_encoding":
+                k = "history.positional_encoding"
+            elif k.startswith("layernorm."):
+                k = "history." + k
+            sd[k] = v
+        sd["history.embed_collection.embeddings.item_embedding.weight"] = self.item_table()
+        if self.mode == "ddp":
+            sd = {"module." + k: v for k, v in sd.items()}
+        return sd

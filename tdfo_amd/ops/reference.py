@@ -382,12 +382,13 @@ def two_tower(X, P, labels, inv_n, logits, dX=None, part=None):
             logits.copy_(two_tower_forward(X.float(), P.float()))
         return
     B = X.shape[0]
-    Xr = X[:, :114].detach().float().clone().requires_grad_(True)
-    Pr = P[:TT_NPARAM].detach().float().clone().requires_grad_(True)
-    lg = two_tower_forward(Xr, Pr)
-    y = labels.float()
-    per = torch.nn.functional.binary_cross_entropy_with_logits(lg, y, reduction="none")
-    (per.sum() * inv_n).backward()
+    with torch.enable_grad():
+        Xr = X[:, :114].detach().float().clone().requires_grad_(True)
+        Pr = P[:TT_NPARAM].detach().float().clone().requires_grad_(True)
+        lg = two_tower_forward(Xr, Pr)
+        y = labels.float()
+        per = torch.nn.functional.binary_cross_entropy_with_logits(lg, y, reduction="none")
+        (per.sum() * inv_n).backward()
     logits.copy_(lg.detach())
     dX[:, :112].copy_(Xr.grad[:, :112])
     nparts = (B + TT_SPB - 1) // TT_SPB
@@ -400,14 +401,15 @@ def two_tower(X, P, labels, inv_n, logits, dX=None, part=None):
 def linear_xent(H, W, bias, labels, eps, ignore, dH, lossv, dW=None, db=None):
     """Oracle: logits = H W^T + b; CrossEntropy(ignore_index, label_smoothing)
     mean over non-ignored tokens; per-token loss in lossv, grads of the mean."""
-    Hr = H.detach().float().clone().requires_grad_(True)
-    Wr = W.detach().float().clone().requires_grad_(True)
-    br = bias.detach().float().clone().requires_grad_(True)
-    logits = Hr @ Wr.t() + br
-    per = torch.nn.functional.cross_entropy(logits, labels, ignore_index=ignore,
-                                            label_smoothing=eps, reduction="none")
-    nv = max(1, int((labels != ignore).sum()))
-    (per.sum() / nv).backward()
+    with torch.enable_grad():
+        Hr = H.detach().float().clone().requires_grad_(True)
+        Wr = W.detach().float().clone().requires_grad_(True)
+        br = bias.detach().float().clone().requires_grad_(True)
+        logits = Hr @ Wr.t() + br
+        per = torch.nn.functional.cross_entropy(logits, labels, ignore_index=ignore,
+                                                label_smoothing=eps, reduction="none")
+        nv = max(1, int((labels != ignore).sum()))
+        (per.sum() / nv).backward()
     lossv.copy_(per.detach())
     dH.copy_(Hr.grad)
     if dW is not None:
