@@ -52,6 +52,11 @@ def lib():
             L.tdfo_loader_release.argtypes = [C.c_void_p, C.c_int]
             L.tdfo_loader_destroy.restype = None
             L.tdfo_loader_destroy.argtypes = [C.c_void_p]
+            L.tdfo_synth_criteo.restype = None
+            L.tdfo_synth_criteo.argtypes = [C.c_uint64, C.c_int, C.c_int64, C.c_int, C.c_int,
+                                            C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_double,
+                                            C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                            C.c_void_p, C.c_int]
             _lib = L
     return _lib
 

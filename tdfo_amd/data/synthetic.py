@@ -4,8 +4,10 @@ data / random-init embeddings").
 Dense features are log-normal-ish like log(1 + count) Criteo integers, ids
 are uniform (default) or Zipf-skewed per table, labels follow a fixed random
 logistic "teacher" over the dense features and a hash of the ids so the
-loss is learnable. Generation runs on-device (no host round trip); the C++
-host generator in csrc/data backs the host pipeline (see loader.py).
+loss is learnable. ``SyntheticCriteo`` generates on the device (no host round
+trip); ``HostSyntheticCriteo`` is the multi-threaded C++ twin
+(csrc/data/synthetic.cpp, counter-based so every batch is reproducible
+independently) used for CPU runs and host-pipeline benchmarks.
 """
 from __future__ import annotations
 
@@ -57,3 +59,46 @@ class SyntheticCriteo:
         label = (torch.rand(B, generator=self.gen, device=self.device)
                  < torch.sigmoid(score)).float()
         return dense, torch.cat(ids), label
+
+
+class HostSyntheticCriteo:
+    """Same teacher as ``SyntheticCriteo``, generated on the host by the C++
+    library (pinned output when ``pin``); batch ``i`` is a pure function of
+    (seed, rank, i), so a resumed run regenerates exactly the same stream."""
+
+    def __init__(self, table_rows: Sequence[int], batch_size: int, num_dense: int = 13,
+                 pooling: Optional[Sequence[int]] = None, seed: int = 0, dist: str = "uniform",
+                 zipf_alpha: float = 1.05, rank: int = 0, threads: int = 4, pin: bool = False):
+        import numpy as np
+        self.rows = np.asarray([int(r) for r in table_rows], dtype=np.int64)
+        self.T = len(self.rows)
+        self.B = int(batch_size)
+        self.num_dense = num_dense
+        self.L = np.asarray(list(pooling) if pooling is not None else [1] * self.T,
+                            dtype=np.int32)
+        self.seed, self.rank, self.threads = seed, rank, threads
+        self.dist = 1 if dist == "zipf" else 0
+        self.alpha = zipf_alpha
+        g = torch.Generator(device="cpu")
+        g.manual_seed(seed)
+        self.w_dense = (torch.randn(num_dense, generator=g) / num_dense ** 0.5).contiguous()
+        self.table_bias = (torch.randn(self.T, 64, generator=g) * 0.5).contiguous()
+        self.index = 0
+        nnz = int((self.L.astype(np.int64) * self.B).sum())
+        mk = (lambda t: t.pin_memory()) if pin else (lambda t: t)
+        self._bufs = [(mk(torch.empty(self.B, num_dense)), mk(torch.empty(nnz, dtype=torch.int64)),
+                       mk(torch.empty(self.B))) for _ in range(2)]
+
+    def batch(self, index: int):
+        from .native import lib
+        dense, ids, label = self._bufs[index & 1]
+        lib().tdfo_synth_criteo(self.seed, self.rank, index, self.B, self.num_dense, self.T,
+                                self.rows.ctypes.data, self.L.ctypes.data, self.dist, self.alpha,
+                                self.w_dense.data_ptr(), self.table_bias.data_ptr(),
+                                dense.data_ptr(), ids.data_ptr(), label.data_ptr(), self.threads)
+        return dense, ids, label
+
+    def next(self):
+        out = self.batch(self.index)
+        self.index += 1
+        return out

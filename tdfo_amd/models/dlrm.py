@@ -522,3 +522,23 @@ class DLRMTrainer:
                 "dense_m": self.fp.m, "dense_v": self.fp.v, "dense_hyper": self.dense_hyper,
                 "emb_hyper": self.emb_hyper}
 
+    def flat_state(self):
+        """Flat name -> tensor view of every piece of training state (for the
+        sharded checkpoint: each rank saves its own embedding shards)."""
+        out = {"dense.p": self.fp.p, "dense_hyper": self.dense_hyper, "emb_hyper": self.emb_hyper}
+        if self.fp.m is not None:
+            out["dense.m"] = self.fp.m
+        if self.fp.v is not None:
+            out["dense.v"] = self.fp.v
+        for grp, sd in self.emb.state_dict().items():
+            for k, v in sd.items():
+                out[f"emb.{grp}.{k}"] = v
+        return out
+
+    def load_flat_state(self, d):
+        for k, v in self.flat_state().items():
+            if k not in d:
+                raise KeyError(f"checkpoint is missing {k}")
+            v.copy_(d[k].to(v.device))
+        self.fp.sync_bf16()
+

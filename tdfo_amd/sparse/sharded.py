@@ -69,7 +69,7 @@ class ShardedEmbeddingBags:
         self.mean = mean
         self.optim = optim
         for s in plan.shards:
-            if s.kind not in ("table_wise", "row_wise"):
+            if s.kind not in ("table_wise", "row_wise", "data_parallel"):
                 raise NotImplementedError(f"sharding kind {s.kind} not supported for pooled bags")
         # ---- id layout in the input (original order)
         self.in_base = [0] * self.T
@@ -158,7 +158,48 @@ class ShardedEmbeddingBags:
             self.rw_bag_offsets = boffs.to(self.device)
             self.rw_out_off = torch.tensor([tw_total + j * D for j in range(len(self.rw_tables))],
                                            dtype=torch.int64, device=self.device)
-        self.recv = torch.zeros(tw_total + B * self.rw_width, dtype=bf, device=self.device)
+        # ---- data-parallel (replicated) group: local lookup, gradient
+        # all-gather, identical deterministic update on every rank
+        self.dp_tables = [s.table for s in plan.shards if s.kind == "data_parallel"]
+        self.dp_width = len(self.dp_tables) * D
+        self.dp_base = tw_total + B * self.rw_width
+        if self.dp_tables:
+            dpt = self.dp_tables
+            self.dp_store = TableBatchedEmbedding(
+                [self.tables[t].num_embeddings for t in dpt], D, device, optim,
+                init_ranges=[self.tables[t].init_range or (1.0 / self.tables[t].num_embeddings) ** 0.5
+                             for t in dpt], seed=seed * 1000 + 777)        # same on all ranks
+            self.dp_in_idx = torch.cat([torch.arange(self.in_base[t], self.in_base[t] + B * self.L[t])
+                                        for t in dpt]).to(self.device)
+            self.dp_nid = int(self.dp_in_idx.numel())
+
+            def bag_offsets(nb):
+                lens = torch.tensor([self.L[t] for t in dpt], dtype=torch.int64).repeat_interleave(nb)
+                o = torch.zeros(lens.numel() + 1, dtype=torch.int64)
+                o[1:] = torch.cumsum(lens, 0)
+                return o.to(self.device)
+
+            self.dp_offsets = bag_offsets(B)
+            self.dp_out_off = torch.tensor([self.dp_base + j * D for j in range(len(dpt))],
+                                           dtype=torch.int64, device=self.device)
+            self.dp_ids = torch.zeros(self.dp_nid, dtype=torch.int64, device=self.device)
+            if W > 1:
+                self.dp_g_offsets = bag_offsets(W * B)
+                self.dp_g_ids = torch.zeros(W * self.dp_nid, dtype=torch.int64, device=self.device)
+                self.dp_g_grad = torch.zeros(W * B * self.dp_width, dtype=bf, device=self.device)
+                self.dp_g_goff = torch.tensor([j * D for j in range(len(dpt))], dtype=torch.int64,
+                                              device=self.device)
+                # gathered (rank-major) ids -> table-major over W*B bags
+                src = []
+                base = 0
+                for t in dpt:
+                    n_t = B * self.L[t]
+                    for r in range(W):
+                        src.append(torch.arange(r * self.dp_nid + base, r * self.dp_nid + base + n_t))
+                    base += n_t
+                self.dp_g_perm = torch.cat(src).to(self.device)
+                self.dp_g_ids_t = torch.zeros_like(self.dp_g_ids)
+        self.recv = torch.zeros(self.dp_base + B * self.dp_width, dtype=bf, device=self.device)
         self.d_recv = torch.zeros_like(self.recv)
         self.d_pooled = torch.empty_like(self.tw_pooled)
         # ---- consumer slot map (per feature/table)
@@ -171,6 +212,9 @@ class ShardedEmbeddingBags:
         for t in self.rw_tables:
             self.slot_off[t] = tw_total + self.rw_col[t]
             self.slot_stride[t] = self.rw_width
+        for j, t in enumerate(self.dp_tables):
+            self.slot_off[t] = self.dp_base + j * D
+            self.slot_stride[t] = self.dp_width
         self._pending = None
         self._rw_state = None
 
@@ -198,6 +242,8 @@ class ShardedEmbeddingBags:
 
     # -- stages (compute stages are hipGraph-capturable; exchanges are RCCL)
     def stage_fwd_prep(self, ids: torch.Tensor):
+        if self.dp_tables:
+            torch.index_select(ids, 0, self.dp_in_idx, out=self.dp_ids)
         if self.tw_identity:
             self.tw_send_ids = ids
             self.tw_recv_ids = ids
@@ -208,12 +254,20 @@ class ShardedEmbeddingBags:
 
     def stage_fwd_ids_exchange(self):
         W = self.world
+        if self.dp_tables and W > 1:
+            dist.all_gather_into_tensor(self.dp_g_ids, self.dp_ids, group=self.group)
         if W > 1 and not self.tw_identity:
             _a2a(self.tw_recv_ids, self.tw_send_ids, [self.tw_recv_count] * W,
                  self.tw_send_counts, self.group)
 
     def stage_fwd_lookup(self):
         W, B = self.world, self.B
+        if self.dp_tables:
+            self.dp_store.forward(self.dp_ids, self.dp_offsets, self.dp_store.row_offset,
+                                  len(self.dp_tables), B, self.recv, self.dp_out_off,
+                                  self.dp_width, mean=self.mean)
+            if W > 1:
+                torch.index_select(self.dp_g_ids, 0, self.dp_g_perm, out=self.dp_g_ids_t)
         if self.tw_nv:
             self.tw_store.forward(self.tw_recv_ids, self.tw_v_offsets, self.tw_v_row_off, self.tw_nv,
                                   B, self.tw_pooled if W > 1 else self.recv, self.tw_v_out_off,
@@ -293,12 +347,20 @@ class ShardedEmbeddingBags:
             work = _a2a(self.d_pooled[: W * B * self.dsum[self.rank]], d_recv[:tw_total],
                         [B * self.dsum[self.rank]] * W, self.tw_recv_sizes, self.group,
                         async_op=True)
+        self._dp_work = None
+        if W > 1 and self.dp_tables:
+            self._dp_work = dist.all_gather_into_tensor(
+                self.dp_g_grad, d_recv[self.dp_base: self.dp_base + B * self.dp_width],
+                group=self.group, async_op=True)
         self._bw = (work, d_recv)
 
     def backward_wait(self):
         work, d_recv = self._bw
         if work is not None:
             work.wait()
+        if getattr(self, "_dp_work", None) is not None:
+            self._dp_work.wait()
+            self._dp_work = None
         self._bw = (None, d_recv)
 
     def stage_bwd_update(self, hyper: torch.Tensor):
@@ -310,6 +372,16 @@ class ShardedEmbeddingBags:
             self.tw_store.backward_update(self.tw_recv_ids, self.tw_v_offsets, self.tw_v_row_off,
                                           self.tw_nv, B, grad, self.tw_v_out_off,
                                           self.dsum[self.rank], hyper, mean=self.mean)
+        if self.dp_tables:
+            ndp = len(self.dp_tables)
+            if W > 1:
+                self.dp_store.backward_update(self.dp_g_ids_t, self.dp_g_offsets,
+                                              self.dp_store.row_offset, ndp, W * B, self.dp_g_grad,
+                                              self.dp_g_goff, self.dp_width, hyper, mean=self.mean)
+            else:
+                self.dp_store.backward_update(self.dp_ids, self.dp_offsets, self.dp_store.row_offset,
+                                              ndp, B, d_recv, self.dp_out_off, self.dp_width, hyper,
+                                              mean=self.mean)
 
     def backward_finish(self, hyper: torch.Tensor):
         self.backward_wait()
@@ -351,6 +423,9 @@ class ShardedEmbeddingBags:
         """(store, local_table_index, row_start, row_stop) of table t here, or None."""
         if t in self.tw_mine:
             return self.tw_store, self.tw_mine.index(t), 0, self.tables[t].num_embeddings
+        if t in self.dp_tables:
+            j = self.dp_tables.index(t)
+            return self.dp_store, j, 0, self.tables[t].num_embeddings
         if t in self.rw_tables:
             j = self.rw_tables.index(t)
             blk = self.rw_block_host[j]
@@ -378,10 +453,14 @@ class ShardedEmbeddingBags:
         d = {"tw": self.tw_store.state_dict()}
         if self.rw_tables:
             d["rw"] = self.rw_store.state_dict()
+        if self.dp_tables:
+            d["dp"] = self.dp_store.state_dict()
         return d
 
     def load_state_dict(self, d):
         self.tw_store.load_state_dict(d["tw"])
         if self.rw_tables:
             self.rw_store.load_state_dict(d["rw"])
+        if self.dp_tables:
+            self.dp_store.load_state_dict(d["dp"])
 

@@ -61,7 +61,7 @@ def _emb_worker(rank, world, strategy, B, L):
     return feats, d_recv, shards, [list(emb.slot_off), list(emb.slot_stride)]
 
 
-@pytest.mark.parametrize("strategy,world", [("table_wise", 2), ("row_wise", 2),
+@pytest.mark.parametrize("strategy,world", [("table_wise", 2), ("row_wise", 2), ("data_parallel", 2),
                                             ("table_wise", 3), ("row_wise", 3)])
 def test_sharded_embedding_fwd_bwd(strategy, world):
     B, L = 6, [1, 2, 1, 3, 1]
@@ -123,7 +123,7 @@ def _dlrm_worker(rank, world, B, steps, strategy):
     return tr.fp.p.clone(), tabs
 
 
-@pytest.mark.parametrize("strategy", ["table_wise", "row_wise"])
+@pytest.mark.parametrize("strategy", ["table_wise", "row_wise", "data_parallel"])
 def test_dlrm_data_parallel_matches_single_process(strategy):
     B, steps = 8, 3
     multi = run_distributed(_dlrm_worker, 2, B, steps, strategy)
