@@ -19,7 +19,9 @@ import torch
 class SyntheticCriteo:
     def __init__(self, table_rows: Sequence[int], batch_size: int, num_dense: int = 13,
                  pooling: Optional[Sequence[int]] = None, device="cpu", seed: int = 0,
-                 dist: str = "uniform", zipf_alpha: float = 1.05, rank: int = 0):
+                 dist: str = "uniform", zipf_alpha: float = 1.05, rank: int = 0, stream: int = 0):
+        """``seed`` fixes the teacher (labels' ground truth); ``stream`` picks an
+        independent sample stream of the same task (e.g. held-out eval)."""
         self.rows = [int(r) for r in table_rows]
         self.T = len(self.rows)
         self.B = int(batch_size)
@@ -29,7 +31,7 @@ class SyntheticCriteo:
         self.dist = dist
         self.alpha = zipf_alpha
         self.gen = torch.Generator(device=self.device)
-        self.gen.manual_seed(seed * 7919 + rank)
+        self.gen.manual_seed(seed * 7919 + rank + stream * 1_000_003)
         g = torch.Generator(device="cpu")
         g.manual_seed(seed)   # teacher shared by all ranks
         self.w_dense = (torch.randn(num_dense, generator=g) / num_dense ** 0.5).to(self.device)
@@ -68,7 +70,8 @@ class HostSyntheticCriteo:
 
     def __init__(self, table_rows: Sequence[int], batch_size: int, num_dense: int = 13,
                  pooling: Optional[Sequence[int]] = None, seed: int = 0, dist: str = "uniform",
-                 zipf_alpha: float = 1.05, rank: int = 0, threads: int = 4, pin: bool = False):
+                 zipf_alpha: float = 1.05, rank: int = 0, threads: int = 4, pin: bool = False,
+                 stream: int = 0):
         import numpy as np
         self.rows = np.asarray([int(r) for r in table_rows], dtype=np.int64)
         self.T = len(self.rows)
@@ -76,7 +79,7 @@ class HostSyntheticCriteo:
         self.num_dense = num_dense
         self.L = np.asarray(list(pooling) if pooling is not None else [1] * self.T,
                             dtype=np.int32)
-        self.seed, self.rank, self.threads = seed, rank, threads
+        self.seed, self.rank, self.threads, self.stream = seed, rank, threads, stream
         self.dist = 1 if dist == "zipf" else 0
         self.alpha = zipf_alpha
         g = torch.Generator(device="cpu")
@@ -92,7 +95,7 @@ class HostSyntheticCriteo:
     def batch(self, index: int):
         from .native import lib
         dense, ids, label = self._bufs[index & 1]
-        lib().tdfo_synth_criteo(self.seed, self.rank, index, self.B, self.num_dense, self.T,
+        lib().tdfo_synth_criteo(self.seed + self.stream * 1_000_003, self.rank, index, self.B, self.num_dense, self.T,
                                 self.rows.ctypes.data, self.L.ctypes.data, self.dist, self.alpha,
                                 self.w_dense.data_ptr(), self.table_bias.data_ptr(),
                                 dense.data_ptr(), ids.data_ptr(), label.data_ptr(), self.threads)

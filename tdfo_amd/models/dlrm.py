@@ -294,9 +294,12 @@ class DLRMTrainer:
         fp = self.fp
         ops.linear_wgrad(dy, x, fp.grad(L.name + ".w").view(-1), slab=self.slab)
         if dx is not None:
+            # dgrad only over the columns dx holds (the padded K tail of the
+            # augmented layout, bias column included, has no gradient consumer)
+            n = min(dx.shape[1], L.in_k)
             W = fp.bf16(L.name + ".w")
-            ops.gemm(dy, False, W[:, :L.in_k], True, None, False,
-                     x[:, :L.in_k] if x_is_relu else None, dx, None, 1)
+            ops.gemm(dy, False, W[:, :n], True, None, False,
+                     x[:, :n] if x_is_relu else None, dx[:, :n], None, 1)
 
     # ---------------------------------------------------------- stages
     # The step is a fixed sequence of compute stages ("c", hipGraph-capturable)

@@ -93,7 +93,7 @@ class TableBatchedEmbedding:
         self.total_rows = offs[-1]
         self.row_offset_host = offs[:-1]
         self.row_offset = torch.tensor(offs[:-1], dtype=torch.int64, device=self.device)
-        self.weight = torch.empty(max(1, self.total_rows), self.dim, dtype=dtype, device=self.device)
+        self.weight = torch.zeros(max(1, self.total_rows), self.dim, dtype=dtype, device=self.device)
         gen = torch.Generator(device=self.device)
         gen.manual_seed(seed)
         for t, r in enumerate(self.row_counts):

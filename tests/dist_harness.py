@@ -53,16 +53,34 @@ def run_distributed(fn, world, *args, timeout=300):
     procs = [ctx.Process(target=_worker, args=(r, world, port, fn, args, q)) for r in range(world)]
     for p in procs:
         p.start()
+    import queue
+    import time
     res = {}
+    failed = False
     try:
-        for _ in range(world):
-            rank, status, out = q.get(timeout=timeout)
+        deadline = time.time() + timeout
+        while len(res) < world:
+            try:
+                rank, status, out = q.get(timeout=0.5)
+            except queue.Empty:
+                dead = [i for i, p in enumerate(procs) if p.exitcode not in (None, 0)
+                        and i not in res]
+                if dead:
+                    failed = True
+                    raise RuntimeError(f"rank(s) {dead} died with exit codes "
+                                       f"{[procs[i].exitcode for i in dead]}")
+                if time.time() > deadline:
+                    failed = True
+                    raise TimeoutError("distributed test timed out")
+                continue
             if status != "ok":
+                failed = True
                 raise RuntimeError(f"rank {rank} failed:\n{out}")
             res[rank] = _from_bytes(out)
     finally:
         for p in procs:
-            p.join(timeout=30)
+            p.join(timeout=1 if failed else 30)
             if p.is_alive():
                 p.kill()
+                p.join(timeout=10)
     return [res[r] for r in range(world)]
