@@ -34,19 +34,33 @@ void check_2d_rowmajor(const Tensor& t, const char* name) {
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 // ------------------------------------------------------------------ gemm
-void gemm(const Tensor& a, bool a_col, const Tensor& b, bool b_col,
+void gemm(const Tensor& a_in, bool a_col, const Tensor& b_in, bool b_col,
           const c10::optional<Tensor>& bias, bool relu,
           const c10::optional<Tensor>& mask, const c10::optional<Tensor>& out,
           const c10::optional<Tensor>& out32, int64_t splits, const c10::optional<Tensor>& mul,
           const c10::optional<Tensor>& add, const c10::optional<Tensor>& out2) {
-  check_dev(a, "a"); check_dev(b, "b");
-  check_2d_rowmajor(a, "a"); check_2d_rowmajor(b, "b");
+  check_dev(a_in, "a"); check_dev(b_in, "b");
+  check_2d_rowmajor(a_in, "a"); check_2d_rowmajor(b_in, "b");
+  const int64_t Ka = a_col ? a_in.size(0) : a_in.size(1);
+  const int64_t Kb = b_col ? b_in.size(0) : b_in.size(1);
+  TORCH_CHECK(Ka == Kb && Ka > 0, "gemm: K mismatch ", Ka, " vs ", Kb);
+  // The kernel consumes whole 64-deep K tiles. A K tail (only tiny layers:
+  // e.g. the dgrad of a 16- or 32-wide layer) is zero-padded here, once,
+  // instead of predicating the hot loop.
+  Tensor a = a_in, b = b_in;
+  if (Ka % 64) {
+    const int64_t Kp = (Ka + 63) / 64 * 64;
+    auto pad = [&](const Tensor& t, bool col) {
+      Tensor z = col ? at::zeros({Kp, t.size(1)}, t.options()) : at::zeros({t.size(0), Kp}, t.options());
+      if (col) z.narrow(0, 0, Ka).copy_(t); else z.narrow(1, 0, Ka).copy_(t);
+      return z;
+    };
+    a = pad(a_in, a_col);
+    b = pad(b_in, b_col);
+  }
   const int64_t M = a_col ? a.size(1) : a.size(0);
   const int64_t K = a_col ? a.size(0) : a.size(1);
   const int64_t N = b_col ? b.size(1) : b.size(0);
-  const int64_t Kb = b_col ? b.size(0) : b.size(1);
-  TORCH_CHECK(K == Kb, "gemm: K mismatch ", K, " vs ", Kb);
-  TORCH_CHECK(K % 64 == 0 && K > 0, "gemm: K must be a positive multiple of 64, got ", K);
   TORCH_CHECK(M > 0 && N > 0, "gemm: empty output");
   TORCH_CHECK(a.stride(0) % 8 == 0 && b.stride(0) % 8 == 0, "gemm: ld must be multiple of 8");
   TORCH_CHECK(aligned16(a.data_ptr()) && aligned16(b.data_ptr()), "gemm: operands must be 16-B aligned");
@@ -107,7 +121,8 @@ tdfo::SlotMap make_slots(at::IntArrayRef off, at::IntArrayRef stride, int64_t F)
 
 void check_inter(int64_t F, int64_t D) {
   TORCH_CHECK(F >= 2 && F <= 32, "interaction: F must be in [2, 32]");
-  TORCH_CHECK(D == 32 || D == 64 || D == 128 || D == 256, "interaction: D must be 32/64/128/256");
+  TORCH_CHECK(D == 16 || D == 32 || D == 64 || D == 128 || D == 256,
+              "interaction: D must be 16/32/64/128/256");
 }
 
 void check_slots_fit(const Tensor& emb, const tdfo::SlotMap& m, int64_t F, int64_t D, int64_t B) {
@@ -344,7 +359,8 @@ void head_bce(const Tensor& H, const Tensor& w, const Tensor& b, const Tensor& l
               const Tensor& part) {
   check_dev(H, "H"); check_2d_rowmajor(H, "H"); check_2d_rowmajor(dH, "dH");
   const int64_t B = H.size(0), K = H.size(1);
-  TORCH_CHECK(K == 64 || K == 128 || K == 256 || K == 512 || K == 1024, "head K unsupported");
+  TORCH_CHECK(K == 16 || K == 32 || K == 64 || K == 128 || K == 256 || K == 512 || K == 1024,
+              "head K unsupported");
   TORCH_CHECK(w.numel() == K && b.numel() == 1 && label.numel() == B && logits.numel() == B, "head shapes");
   TORCH_CHECK(label.scalar_type() == at::kFloat && logits.scalar_type() == at::kFloat, "head fp32 label/logits");
   TORCH_CHECK(dH.size(0) == B && dH.size(1) == K, "dH shape");
@@ -448,6 +464,54 @@ void linear_xent(const Tensor& H, const Tensor& W, const Tensor& bias, const Ten
   tdfo::linear_xent(a, cur_stream());
 }
 
+void check_offsets(const Tensor& off, int64_t B) {
+  check_dev(off, "offsets");
+  TORCH_CHECK(off.scalar_type() == at::kLong && off.is_contiguous() && off.numel() == B + 1,
+              "offsets must be int64 [B+1]");
+}
+
+void jagged_to_dense(const Tensor& values, const Tensor& offsets, int64_t T, double pad,
+                     const Tensor& out) {
+  check_dev(values, "values");
+  const int64_t B = out.size(0);
+  check_offsets(offsets, B);
+  TORCH_CHECK(values.scalar_type() == at::kFloat && values.dim() == 2 && values.is_contiguous(),
+              "values fp32 [nnz, D]");
+  const int64_t D = values.size(1);
+  TORCH_CHECK(out.scalar_type() == at::kFloat && out.is_contiguous() && out.dim() == 3 &&
+              out.size(1) == T && out.size(2) == D, "out fp32 [B, T, D]");
+  TORCH_CHECK(D % 4 != 0 || (aligned16(values.data_ptr()) && aligned16(out.data_ptr())),
+              "jagged_to_dense alignment");
+  tdfo::jagged_to_dense(values.data_ptr<float>(), offsets.data_ptr<int64_t>(), (int)B, (int)T,
+                        (int)D, (float)pad, out.data_ptr<float>(), cur_stream());
+}
+
+void dense_to_jagged(const Tensor& dense, const Tensor& offsets, const Tensor& vgrad) {
+  check_dev(dense, "dense");
+  TORCH_CHECK(dense.scalar_type() == at::kFloat && dense.dim() == 3 && dense.is_contiguous(),
+              "dense fp32 [B, T, D]");
+  const int64_t B = dense.size(0), T = dense.size(1), D = dense.size(2);
+  check_offsets(offsets, B);
+  TORCH_CHECK(vgrad.scalar_type() == at::kFloat && vgrad.dim() == 2 && vgrad.size(1) == D &&
+              vgrad.is_contiguous(), "vgrad fp32 [nnz, D]");
+  TORCH_CHECK(D % 4 != 0 || (aligned16(vgrad.data_ptr()) && aligned16(dense.data_ptr())),
+              "dense_to_jagged alignment");
+  tdfo::dense_to_jagged(dense.data_ptr<float>(), offsets.data_ptr<int64_t>(), (int)B, (int)T,
+                        (int)D, vgrad.size(0), vgrad.data_ptr<float>(), cur_stream());
+}
+
+void jagged_ids_to_dense(const Tensor& values, const Tensor& offsets, int64_t pad,
+                         const Tensor& out) {
+  check_dev(values, "values");
+  TORCH_CHECK(values.scalar_type() == at::kLong && values.is_contiguous(), "ids int64");
+  TORCH_CHECK(out.scalar_type() == at::kLong && out.dim() == 2 && out.is_contiguous(),
+              "out int64 [B, T]");
+  const int64_t B = out.size(0), T = out.size(1);
+  check_offsets(offsets, B);
+  tdfo::jagged_ids_to_dense(values.data_ptr<int64_t>(), offsets.data_ptr<int64_t>(), (int)B,
+                            (int)T, pad, out.data_ptr<int64_t>(), cur_stream());
+}
+
 }  // namespace
 
 TORCH_LIBRARY(tdfo, m) {
@@ -482,6 +546,9 @@ TORCH_LIBRARY(tdfo, m) {
   m.def("auc_hist(Tensor logits, Tensor labels, int nb, Tensor(a!) hist) -> ()");
   m.def("linear_xent(Tensor H, Tensor W, Tensor bias, Tensor labels, float eps, int ignore, "
         "Tensor(a!) dH, Tensor(b!) lossv, Tensor(c!)? dW, Tensor(d!)? db) -> ()");
+  m.def("jagged_to_dense(Tensor values, Tensor offsets, int T, float pad, Tensor(a!) out) -> ()");
+  m.def("dense_to_jagged(Tensor dense, Tensor offsets, Tensor(a!) vgrad) -> ()");
+  m.def("jagged_ids_to_dense(Tensor values, Tensor offsets, int pad, Tensor(a!) out) -> ()");
   m.def("two_tower(Tensor X, Tensor P, Tensor labels, float inv_n, Tensor(a!) logits, "
         "Tensor(b!)? dX, Tensor(c!)? part) -> ()");
 }
@@ -505,4 +572,7 @@ TORCH_LIBRARY_IMPL(tdfo, CUDA, m) {
   m.impl("auc_hist", auc_hist);
   m.impl("two_tower", two_tower);
   m.impl("linear_xent", linear_xent);
+  m.impl("jagged_to_dense", jagged_to_dense);
+  m.impl("dense_to_jagged", dense_to_jagged);
+  m.impl("jagged_ids_to_dense", jagged_ids_to_dense);
 }

@@ -189,4 +189,12 @@ struct LinearXentArgs {
 size_t linear_xent_workspace(int N, int64_t V);
 void linear_xent(const LinearXentArgs& a, hipStream_t s);
 
+// ----------------------------------------------------------- jagged ----
+void jagged_to_dense(const float* values, const int64_t* off, int B, int T, int D, float pad,
+                     float* out, hipStream_t s);
+void dense_to_jagged(const float* dense, const int64_t* off, int B, int T, int D, int64_t nnz,
+                     float* vgrad, hipStream_t s);
+void jagged_ids_to_dense(const int64_t* values, const int64_t* off, int B, int T, int64_t pad,
+                         int64_t* out, hipStream_t s);
+
 }  // namespace tdfo

@@ -154,8 +154,11 @@ __global__ __launch_bounds__(256) void inter_bwd_kernel(
         sa[ks] = __builtin_bit_cast(bf16x8_t, t);
       }
       const int g = lane >> 4, li = lane & 15, q = li >> 2, pp = li & 3;
+      // D = 16: one 32-wide column tile whose upper half reads past the row
+      // (finite LDS data, never stored)
+      constexpr int NT = D >= 32 ? D / 32 : 1;
 #pragma unroll
-      for (int nt = 0; nt < D / 32; ++nt) {
+      for (int nt = 0; nt < NT; ++nt) {
         f32x16_t acc = {};
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
@@ -174,6 +177,7 @@ __global__ __launch_bounds__(256) void inter_bwd_kernel(
               sa[ks], __builtin_bit_cast(bf16x8_t, bb), acc, 0, 0, 0);
         }
         const int d = 32 * nt + (lane & 31);
+        if (D < 32 && d >= D) continue;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int ii = (r & 3) + 8 * (r >> 2) + 4 * h;
@@ -213,6 +217,7 @@ void interaction_fwd(const uint16_t* dense, int64_t ld_dense,
   hipLaunchKernelGGL(inter_fwd_kernel<DD>, grid, dim3(256), smem, s, dense,    \
                      ld_dense, emb, slots, F, B, out, ldo, ones_col)
   switch (D) {
+    case 16: TDFO_IFWD(16); break;
     case 32: TDFO_IFWD(32); break;
     case 64: TDFO_IFWD(64); break;
     case 128: TDFO_IFWD(128); break;
@@ -239,6 +244,7 @@ void interaction_bwd(const uint16_t* dz, int64_t ldz, const uint16_t* dense,
                      dense, ld_dense, emb, slots, F, B, d_dense, ld_ddense,    \
                      d_emb, dslots, relu_mask)
   switch (D) {
+    case 16: TDFO_IBWD(16); break;
     case 32: TDFO_IBWD(32); break;
     case 64: TDFO_IBWD(64); break;
     case 128: TDFO_IBWD(128); break;

@@ -22,12 +22,13 @@
 #include "tdfo_common.h"
 #include "tdfo_kernels.h"
 
+#include <algorithm>
+
 namespace tdfo {
 namespace {
 
 constexpr int XE = 16;          // hidden width (embed_dim)
 constexpr int XP = 20;          // partial record: m, s, acc[16], pad
-constexpr int TILE = 1024;      // W rows staged per LDS tile
 
 __global__ __launch_bounds__(1024) void xent_compact_kernel(const int64_t* __restrict__ labels,
                                                             int N, int ignore,
@@ -66,80 +67,87 @@ __global__ __launch_bounds__(1024) void xent_compact_kernel(const int64_t* __res
   if (t == 0) *count = base;
 }
 
-__global__ __launch_bounds__(256) void xent_pass1_kernel(const float* __restrict__ H,
-                                                         const float* __restrict__ W,
-                                                         const float* __restrict__ bias, int64_t V,
-                                                         int64_t VS, int S,
-                                                         const int32_t* __restrict__ idx,
-                                                         const int32_t* __restrict__ count,
-                                                         float* __restrict__ part,
-                                                         float* __restrict__ wpart) {
-  __shared__ __attribute__((aligned(16))) float Wt[TILE][XE];
-  __shared__ float bt[TILE];
+// One wave per block: lane = token. W rows are wave-uniform, so they come
+// through scalar loads (s_load_dwordx16, SGPR operands of the FMAs) — no LDS
+// broadcast, which would cost 4 ds_read_b128 (32 LDS clocks) per row.
+__global__ __launch_bounds__(64) void xent_pass1_kernel(const float* __restrict__ H,
+                                                        const float* __restrict__ W,
+                                                        const float* __restrict__ bias, int64_t V,
+                                                        int64_t VS, int S,
+                                                        const int32_t* __restrict__ idx,
+                                                        const int32_t* __restrict__ count,
+                                                        float* __restrict__ part,
+                                                        float* __restrict__ wpart) {
   const int s = blockIdx.x, chunk = blockIdx.y, t = threadIdx.x;
   const int nv = *count;
-  const bool want_wsum = chunk == 0;
-  if (chunk * 256 >= nv && !want_wsum) return;
-  const int j = chunk * 256 + t;
+  const int64_t v0 = (int64_t)s * VS, v1 = min(V, v0 + VS);
+  if (chunk == 0 && t <= XE) {      // column sums of [W | b] over this split
+    float a = 0.f;
+    if (t < XE)
+      for (int64_t r = v0; r < v1; ++r) a += W[r * XE + t];
+    else
+      for (int64_t r = v0; r < v1; ++r) a += bias[r];
+    wpart[(int64_t)s * (XE + 1) + t] = a;
+  }
+  if (chunk * 64 >= nv) return;
+  const int j = chunk * 64 + t;
   const bool valid = j < nv;
   float h[XE];
-  if (valid) {
-    const float* hr = H + (int64_t)idx[j] * XE;
+  const float* hr = H + (int64_t)idx[valid ? j : 0] * XE;
 #pragma unroll
-    for (int k = 0; k < XE; k += 4) {
-      const float4 q = *(const float4*)(hr + k);
-      h[k] = q.x; h[k + 1] = q.y; h[k + 2] = q.z; h[k + 3] = q.w;
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < XE; ++k) h[k] = 0.f;
+  for (int k = 0; k < XE; k += 4) {
+    const float4 q = *(const float4*)(hr + k);
+    h[k] = q.x; h[k + 1] = q.y; h[k + 2] = q.z; h[k + 3] = q.w;
   }
   float m = -INFINITY, sum = 0.f, acc[XE];
 #pragma unroll
   for (int k = 0; k < XE; ++k) acc[k] = 0.f;
-  float wsum_k = 0.f;     // thread t < 17 accumulates column t of [W | b] over rows
-  const int64_t v0 = (int64_t)s * VS, v1 = min(V, v0 + VS);
-  for (int64_t r0 = v0; r0 < v1; r0 += TILE) {
-    const int n = (int)min<int64_t>(TILE, v1 - r0);
-    __syncthreads();
-    for (int q = t; q < n * (XE / 4); q += 256)
-      *(float4*)(&Wt[q >> 2][(q & 3) * 4]) = *(const float4*)(W + (r0 + (q >> 2)) * XE + (q & 3) * 4);
-    for (int q = t; q < n; q += 256) bt[q] = bias[r0 + q];
-    __syncthreads();
-    if (want_wsum && t < XE + 1) {
-      float a = 0.f;
-      if (t < XE)
-        for (int r = 0; r < n; ++r) a += Wt[r][t];
-      else
-        for (int r = 0; r < n; ++r) a += bt[r];
-      wsum_k += a;
+  // 4 rows per iteration: 4 scalar row loads in flight, one rescale check
+  int64_t r = v0;
+  for (; r + 4 <= v1; r += 4) {
+    float z[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float* wr = W + (r + q) * XE;     // uniform -> scalar loads
+      float a = bias[r + q];
+#pragma unroll
+      for (int k = 0; k < XE; ++k) a = fmaf(wr[k], h[k], a);
+      z[q] = a;
     }
-    if (valid) {
-      for (int r = 0; r < n; ++r) {
-        const float4 w0 = *(const float4*)(&Wt[r][0]);
-        const float4 w1 = *(const float4*)(&Wt[r][4]);
-        const float4 w2 = *(const float4*)(&Wt[r][8]);
-        const float4 w3 = *(const float4*)(&Wt[r][12]);
-        const float wr[XE] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w,
-                              w2.x, w2.y, w2.z, w2.w, w3.x, w3.y, w3.z, w3.w};
-        float z = bt[r];
+    const float zm = fmaxf(fmaxf(z[0], z[1]), fmaxf(z[2], z[3]));
+    if (zm > m) {
+      const float c = __expf(m - zm);
+      sum *= c;
 #pragma unroll
-        for (int k = 0; k < XE; ++k) z = fmaf(wr[k], h[k], z);
-        if (z > m) {
-          const float c = __expf(m - z);
-          sum *= c;
+      for (int k = 0; k < XE; ++k) acc[k] *= c;
+      m = zm;
+    }
 #pragma unroll
-          for (int k = 0; k < XE; ++k) acc[k] *= c;
-          m = z;
-        }
-        const float e = __expf(z - m);
-        sum += e;
+    for (int q = 0; q < 4; ++q) {
+      const float* wr = W + (r + q) * XE;
+      const float e = __expf(z[q] - m);
+      sum += e;
 #pragma unroll
-        for (int k = 0; k < XE; ++k) acc[k] = fmaf(e, wr[k], acc[k]);
-      }
+      for (int k = 0; k < XE; ++k) acc[k] = fmaf(e, wr[k], acc[k]);
     }
   }
-  if (want_wsum && t < XE + 1) wpart[(int64_t)s * (XE + 1) + t] = wsum_k;
+  for (; r < v1; ++r) {
+    const float* wr = W + r * XE;
+    float z = bias[r];
+#pragma unroll
+    for (int k = 0; k < XE; ++k) z = fmaf(wr[k], h[k], z);
+    if (z > m) {
+      const float c = __expf(m - z);
+      sum *= c;
+#pragma unroll
+      for (int k = 0; k < XE; ++k) acc[k] *= c;
+      m = z;
+    }
+    const float e = __expf(z - m);
+    sum += e;
+#pragma unroll
+    for (int k = 0; k < XE; ++k) acc[k] = fmaf(e, wr[k], acc[k]);
+  }
   if (valid) {
     float* p = part + ((int64_t)j * S + s) * XP;
     p[0] = m;
@@ -230,8 +238,8 @@ __global__ __launch_bounds__(256) void xent_merge_kernel(const float* __restrict
     dH[(int64_t)n * XE + k] = scale * (acc[k] * inv - (1.f - eps) * wy[k] - eps * ws[k] / (float)V);
 }
 
-constexpr int WG_CHUNK = 512;
-
+// One thread per vocab row; the tokens are wave-uniform (scalar loads of
+// idx, H row, lse and label), so the loop body is pure VALU.
 __global__ __launch_bounds__(256) void xent_wgrad_kernel(const float* __restrict__ H,
                                                          const float* __restrict__ W,
                                                          const float* __restrict__ bias,
@@ -242,55 +250,36 @@ __global__ __launch_bounds__(256) void xent_wgrad_kernel(const float* __restrict
                                                          const float* __restrict__ lse,
                                                          float* __restrict__ dW,
                                                          float* __restrict__ db) {
-  __shared__ __attribute__((aligned(16))) float Hs[WG_CHUNK][XE];
-  __shared__ float Ls[WG_CHUNK];
-  __shared__ int Ys[WG_CHUNK];
-  const int t = threadIdx.x;
-  const int64_t v = (int64_t)blockIdx.x * 256 + t;
+  const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const bool valid = v < V;
+  const int64_t vr = valid ? v : V - 1;
   const int nv = *count;
   const float scale = 1.f / (float)max(1, nv);
   const float off = eps / (float)V, hit = 1.f - eps;
-  float w[XE], g[XE], gb = 0.f, b = 0.f;
+  float w[XE], g[XE], gb = 0.f;
 #pragma unroll
-  for (int k = 0; k < XE; ++k) { w[k] = 0.f; g[k] = 0.f; }
-  if (valid) {
-#pragma unroll
-    for (int k = 0; k < XE; k += 4) {
-      const float4 q = *(const float4*)(W + v * XE + k);
-      w[k] = q.x; w[k + 1] = q.y; w[k + 2] = q.z; w[k + 3] = q.w;
-    }
-    b = bias[v];
+  for (int k = 0; k < XE; k += 4) {
+    const float4 q = *(const float4*)(W + vr * XE + k);
+    w[k] = q.x; w[k + 1] = q.y; w[k + 2] = q.z; w[k + 3] = q.w;
   }
-  for (int c0 = 0; c0 < nv; c0 += WG_CHUNK) {
-    const int n = min(WG_CHUNK, nv - c0);
-    __syncthreads();
-    for (int q = t; q < n * (XE / 4); q += 256) {
-      const int r = q >> 2;
-      *(float4*)(&Hs[r][(q & 3) * 4]) = *(const float4*)(H + (int64_t)idx[c0 + r] * XE + (q & 3) * 4);
-    }
-    for (int q = t; q < n; q += 256) {
-      Ls[q] = lse[c0 + q];
-      Ys[q] = (int)labels[idx[c0 + q]];
-    }
-    __syncthreads();
-    for (int r = 0; r < n; ++r) {
-      const float4 h0 = *(const float4*)(&Hs[r][0]);
-      const float4 h1 = *(const float4*)(&Hs[r][4]);
-      const float4 h2 = *(const float4*)(&Hs[r][8]);
-      const float4 h3 = *(const float4*)(&Hs[r][12]);
-      const float hr[XE] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z, h1.w,
-                            h2.x, h2.y, h2.z, h2.w, h3.x, h3.y, h3.z, h3.w};
-      float z = b;
+  const float b = bias[vr];
 #pragma unroll
-      for (int k = 0; k < XE; ++k) z = fmaf(w[k], hr[k], z);
-      float dz = __expf(z - Ls[r]) - off;
-      if ((int64_t)Ys[r] == v) dz -= hit;
-      dz *= scale;
-      gb += dz;
+  for (int k = 0; k < XE; ++k) g[k] = 0.f;
+#pragma unroll 2
+  for (int j = 0; j < nv; ++j) {
+    const int n = idx[j];
+    const float* hr = H + (int64_t)n * XE;     // uniform -> scalar loads
+    const float l = lse[j];
+    const int64_t y = labels[n];
+    float z = b;
 #pragma unroll
-      for (int k = 0; k < XE; ++k) g[k] = fmaf(dz, hr[k], g[k]);
-    }
+    for (int k = 0; k < XE; ++k) z = fmaf(w[k], hr[k], z);
+    float dz = __expf(z - l) - off;
+    if (y == v) dz -= hit;
+    dz *= scale;
+    gb += dz;
+#pragma unroll
+    for (int k = 0; k < XE; ++k) g[k] = fmaf(dz, hr[k], g[k]);
   }
   if (valid) {
 #pragma unroll
@@ -302,9 +291,12 @@ __global__ __launch_bounds__(256) void xent_wgrad_kernel(const float* __restrict
 
 }  // namespace
 
-void linear_xent_splits(int64_t V, int64_t* VS, int* S) {
-  int64_t vs = TILE;
-  while ((V + vs - 1) / vs > 512) vs += TILE;
+// ~8 waves per SIMD for pass1 (one wave per (split, 64-token chunk)); the
+// number of valid tokens is device-side, so size for the capacity N.
+void linear_xent_splits(int N, int64_t V, int64_t* VS, int* S) {
+  const int chunks = std::max(1, (N + 63) / 64);
+  int64_t want = std::min<int64_t>(8192, std::max<int64_t>(64, 16384 / chunks));
+  int64_t vs = std::max<int64_t>(64, (V + want - 1) / want);
   *VS = vs;
   *S = (int)((V + vs - 1) / vs);
 }
@@ -312,7 +304,7 @@ void linear_xent_splits(int64_t V, int64_t* VS, int* S) {
 size_t linear_xent_workspace(int N, int64_t V) {
   int64_t VS;
   int S;
-  linear_xent_splits(V, &VS, &S);
+  linear_xent_splits(N, V, &VS, &S);
   // idx[N] + count + lse[N] (ints/floats) + part[N][S][XP] + wpart[S][17]
   return (size_t)(2 * N + 16) * 4 + (size_t)N * S * XP * 4 + (size_t)S * (XE + 1) * 4 + 256;
 }
@@ -321,7 +313,7 @@ void linear_xent(const LinearXentArgs& a, hipStream_t s) {
   if (a.N <= 0) return;
   int64_t VS;
   int S;
-  linear_xent_splits(a.V, &VS, &S);
+  linear_xent_splits(a.N, a.V, &VS, &S);
   char* ws = (char*)a.workspace;
   int32_t* idx = (int32_t*)ws;
   int32_t* count = idx + a.N;
@@ -331,8 +323,8 @@ void linear_xent(const LinearXentArgs& a, hipStream_t s) {
   float* wpart = part + (int64_t)a.N * S * XP;
   hipLaunchKernelGGL(xent_compact_kernel, dim3(1), dim3(1024), 0, s, a.labels, a.N, a.ignore, idx,
                      count, a.dH, a.lossv);
-  const int chunks = (a.N + 255) / 256;
-  hipLaunchKernelGGL(xent_pass1_kernel, dim3(S, chunks), dim3(256), 0, s, a.H, a.W, a.bias, a.V, VS,
+  const int chunks = (a.N + 63) / 64;
+  hipLaunchKernelGGL(xent_pass1_kernel, dim3(S, chunks), dim3(64), 0, s, a.H, a.W, a.bias, a.V, VS,
                      S, idx, count, part, wpart);
   hipLaunchKernelGGL(xent_merge_kernel, dim3((a.N + 3) / 4), dim3(256), 0, s, a.H, a.W, a.bias,
                      a.labels, a.V, S, a.eps, idx, count, part, wpart, lse, a.dH, a.lossv);

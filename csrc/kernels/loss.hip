@@ -23,13 +23,14 @@ __global__ __launch_bounds__(256) void head_bce_kernel(
     const float* __restrict__ label, float inv_n, int relu_mask,
     float* __restrict__ logits, uint16_t* __restrict__ dH, int64_t lddh,
     float* __restrict__ part) {
-  constexpr int EPL = K / 64;
+  constexpr int EPL = K >= 64 ? K / 64 : 1;   // K < 64: lanes >= K idle
   __shared__ float red[4][K + 2];
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int e0 = lane * EPL;
+  const bool act = e0 < K;
   float wr[EPL], dw[EPL];
 #pragma unroll
-  for (int u = 0; u < EPL; ++u) { wr[u] = w[e0 + u]; dw[u] = 0.f; }
+  for (int u = 0; u < EPL; ++u) { wr[u] = act ? w[e0 + u] : 0.f; dw[u] = 0.f; }
   const float bias = bptr[0];
   float db = 0.f, lsum = 0.f;
   const int s0 = blockIdx.x * HEAD_SPB;
@@ -39,7 +40,7 @@ __global__ __launch_bounds__(256) void head_bce_kernel(
     const uint16_t* hp = H + (int64_t)s * ldh + e0;
     float hv[EPL];
 #pragma unroll
-    for (int u = 0; u < EPL; ++u) hv[u] = bf2f(hp[u]);
+    for (int u = 0; u < EPL; ++u) hv[u] = act ? bf2f(hp[u]) : 0.f;
     float d = 0.f;
 #pragma unroll
     for (int u = 0; u < EPL; ++u) d += hv[u] * wr[u];
@@ -53,16 +54,20 @@ __global__ __launch_bounds__(256) void head_bce_kernel(
       db += g;
     }
     uint16_t* dp = dH + (int64_t)s * lddh + e0;
+    if (act) {
 #pragma unroll
-    for (int u = 0; u < EPL; ++u) {
-      float gh = g * wr[u];
-      if (relu_mask && !(hv[u] > 0.f)) gh = 0.f;
-      dp[u] = f2bf(gh);
-      dw[u] += g * hv[u];
+      for (int u = 0; u < EPL; ++u) {
+        float gh = g * wr[u];
+        if (relu_mask && !(hv[u] > 0.f)) gh = 0.f;
+        dp[u] = f2bf(gh);
+        dw[u] += g * hv[u];
+      }
     }
   }
+  if (act) {
 #pragma unroll
-  for (int u = 0; u < EPL; ++u) red[wv][e0 + u] = dw[u];
+    for (int u = 0; u < EPL; ++u) red[wv][e0 + u] = dw[u];
+  }
   if (lane == 0) { red[wv][K] = db; red[wv][K + 1] = lsum; }
   __syncthreads();
   for (int j = threadIdx.x; j < K + 2; j += 256)
@@ -172,6 +177,8 @@ void head_bce(const uint16_t* H, int64_t ldh, int B, int K, const float* w,
   hipLaunchKernelGGL(head_bce_kernel<KK>, grid, dim3(256), 0, s, H, ldh, B, w, \
                      b, label, inv_n, relu_mask, logits, dH, lddh, part)
   switch (K) {
+    case 16: TDFO_HB(16); break;
+    case 32: TDFO_HB(32); break;
     case 64: TDFO_HB(64); break;
     case 128: TDFO_HB(128); break;
     case 256: TDFO_HB(256); break;

@@ -216,3 +216,25 @@ def linear_xent(H, W, bias, labels, eps, ignore, dH, lossv, dW=None, db=None):
         _native().linear_xent(H, W, bias, labels, float(eps), int(ignore), dH, lossv, dW, db)
     else:
         ref.linear_xent(H, W, bias, labels, eps, ignore, dH, lossv, dW, db)
+
+
+def jagged_to_dense(values, offsets, T, pad, out):
+    """values [nnz, D] fp32 + offsets [B+1] -> out [B, T, D] (pad fill)."""
+    if _gpu(values):
+        _native().jagged_to_dense(values, offsets, int(T), float(pad), out)
+    else:
+        ref.jagged_to_dense(values, offsets, T, pad, out)
+
+
+def dense_to_jagged(dense, offsets, vgrad):
+    if _gpu(dense):
+        _native().dense_to_jagged(dense, offsets, vgrad)
+    else:
+        ref.dense_to_jagged(dense, offsets, vgrad)
+
+
+def jagged_ids_to_dense(values, offsets, pad, out):
+    if _gpu(values):
+        _native().jagged_ids_to_dense(values, offsets, int(pad), out)
+    else:
+        ref.jagged_ids_to_dense(values, offsets, pad, out)

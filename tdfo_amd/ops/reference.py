@@ -415,3 +415,35 @@ def linear_xent(H, W, bias, labels, eps, ignore, dH, lossv, dW=None, db=None):
     if dW is not None:
         dW.copy_(Wr.grad)
         db.copy_(br.grad)
+
+
+def _bag_positions(offsets, T):
+    lens = (offsets[1:] - offsets[:-1])
+    B = lens.numel()
+    nnz = int(offsets[-1])
+    bag = torch.repeat_interleave(torch.arange(B, device=offsets.device), lens)
+    pos = torch.arange(nnz, device=offsets.device) - offsets[:-1][bag]
+    return bag, pos
+
+
+def jagged_to_dense(values, offsets, T, pad, out):
+    out.fill_(pad)
+    bag, pos = _bag_positions(offsets, T)
+    keep = pos < T
+    out[bag[keep], pos[keep]] = values[keep].to(out.dtype)
+
+
+def dense_to_jagged(dense, offsets, vgrad):
+    T = dense.shape[1]
+    bag, pos = _bag_positions(offsets, T)
+    vgrad.zero_()
+    keep = pos < T
+    vgrad[keep] = dense[bag[keep], pos[keep]]
+
+
+def jagged_ids_to_dense(values, offsets, pad, out):
+    T = out.shape[1]
+    out.fill_(pad)
+    bag, pos = _bag_positions(offsets, T)
+    keep = pos < T
+    out[bag[keep], pos[keep]] = values[keep]

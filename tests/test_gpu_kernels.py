@@ -97,7 +97,7 @@ def test_gemm_strided_out_and_splitk():
 
 
 # ----------------------------------------------------------- interaction
-@pytest.mark.parametrize("D", [64, 128])
+@pytest.mark.parametrize("D", [16, 32, 64, 128])
 @pytest.mark.parametrize("B", [1, 37, 1024])
 def test_interaction(D, B):
     torch.manual_seed(3)
@@ -448,3 +448,68 @@ def test_radix_sort_matches_stable_torch_sort(n, dtype, bits):
     ek, ei = torch.sort(keys, stable=True)
     assert torch.equal(k, ek)
     assert torch.equal(v, ei.to(torch.int32))
+
+
+def test_dlrm_small_hidden_layers_match_cpu():
+    """Hidden widths below the 64-wide K padding (augmented bias inside K)."""
+    from tdfo_amd.data.synthetic import SyntheticCriteo
+    from tdfo_amd.models.dlrm import DLRMConfig, DLRMTrainer
+
+    cfg = DLRMConfig(embedding_dim=16, table_rows=[300, 40, 500, 70], bottom=[32, 16],
+                     top=[32, 1], dense_lr=3e-3, emb_lr=0.05)
+    B = 64
+    gpu = DLRMTrainer(cfg, B, DEV)
+    cpu = DLRMTrainer(cfg, B, "cpu")
+    cpu.emb.tw_store.weight.copy_(gpu.emb.tw_store.weight.cpu())
+    cpu.fp.p.copy_(gpu.fp.p.cpu())
+    cpu.fp.sync_bf16()
+    data = SyntheticCriteo(cfg.table_rows, B, device="cpu", seed=3)
+    for _ in range(10):
+        batch = data.next()
+        gpu.load_batch(*(x.to(DEV) for x in batch))
+        cpu.load_batch(*batch)
+        gpu.step()
+        cpu.step()
+        assert abs(gpu.pop_loss() - cpu.pop_loss()) / B < 0.02
+
+
+@pytest.mark.parametrize("K", [16, 32, 100])
+@pytest.mark.parametrize("a_col,b_col", [(False, False), (False, True), (True, True)])
+def test_gemm_k_tail_padding(K, a_col, b_col):
+    torch.manual_seed(K)
+    M, N = 96, 80
+    A = bf(torch.randn(K, M, device=DEV) if a_col else torch.randn(M, K, device=DEV))
+    Bm = bf(torch.randn(K, N, device=DEV) if b_col else torch.randn(N, K, device=DEV))
+    out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+    ops.gemm(A, a_col, Bm, b_col, out=out)
+    a = A.float().t() if a_col else A.float()
+    b = Bm.float() if b_col else Bm.float().t()
+    assert rel_err(out, a @ b) < 2e-2
+
+
+@pytest.mark.parametrize("D", [1, 16, 6])
+def test_jagged_dense_roundtrip(D):
+    torch.manual_seed(D)
+    lens = torch.randint(0, 30, (37,))
+    off = torch.zeros(38, dtype=torch.int64)
+    off[1:] = torch.cumsum(lens, 0)
+    nnz = int(off[-1])
+    vals = torch.randn(nnz, D)
+    T = 20
+    out = torch.empty(37, T, D, device=DEV)
+    ops.jagged_to_dense(vals.to(DEV), off.to(DEV), T, -2.0, out)
+    ref_out = torch.empty(37, T, D)
+    ref.jagged_to_dense(vals, off, T, -2.0, ref_out)
+    assert torch.equal(out.cpu(), ref_out)
+    g = torch.randn(37, T, D)
+    vg = torch.empty(nnz, D, device=DEV)
+    ops.dense_to_jagged(g.to(DEV), off.to(DEV), vg)
+    rg = torch.empty(nnz, D)
+    ref.dense_to_jagged(g, off, rg)
+    assert torch.equal(vg.cpu(), rg)
+    ids = torch.randint(0, 1000, (nnz,))
+    oi = torch.empty(37, T, dtype=torch.int64, device=DEV)
+    ops.jagged_ids_to_dense(ids.to(DEV), off.to(DEV), 0, oi)
+    ri = torch.empty(37, T, dtype=torch.int64)
+    ref.jagged_ids_to_dense(ids, off, 0, ri)
+    assert torch.equal(oi.cpu(), ri)
