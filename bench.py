@@ -36,7 +36,18 @@ def parse(argv=None):
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--pool", type=int, default=8, help="pre-generated device batches")
     ap.add_argument("--dist", default="uniform", choices=["uniform", "zipf"])
+    ap.add_argument("--sharding", default="auto",
+                    choices=["auto", "table_wise", "row_wise", "data_parallel"])
     return ap.parse_args(argv)
+
+
+def parallelism(plan, world: int) -> str:
+    """e.g. "dp8 dense + emb table_wise x8" (embedding sharding kinds from the plan)."""
+    if world == 1:
+        return "single-gpu"
+    short = {"table_wise": "tw", "row_wise": "rw", "data_parallel": "dp", "column_wise": "cw"}
+    kinds = "+".join(f"{short.get(k, k)}{n}" for k, n in sorted(plan.summary()["kinds"].items()))
+    return f"dp{world} dense + emb[{kinds} tables] over {world} ranks"
 
 
 def main(argv=None):
@@ -56,10 +67,10 @@ def main(argv=None):
     rows = {"1tb": CRITEO_1TB_ROWS, "kaggle": CRITEO_KAGGLE_ROWS,
             "tiny": [1000] * 26}[args.rows]
     if args.model == "dlrm":
-        cfg = DLRMConfig(table_rows=list(rows))
+        cfg = DLRMConfig(table_rows=list(rows), sharding=args.sharding)
     else:
         cfg = DLRMConfig(table_rows=list(rows), interaction="dcn", pooling=list(MLPERF_MULTIHOT),
-                         top=[1024, 1024, 512, 256, 1])
+                         top=[1024, 1024, 512, 256, 1], sharding=args.sharding)
     B = args.batch
     t0 = time.time()
     tr = DLRMTrainer(cfg, B, info.device, group=info.group, rank=info.rank, world_size=world)
@@ -109,8 +120,7 @@ def main(argv=None):
             "data": "synthetic (Criteo-1TB-shaped, uniform ids, random-init embeddings)",
             "config": {"model": "DLRM" if args.model == "dlrm" else "DCN-v2",
                        "global_batch": B * world, "seq_len": None,
-                       "parallelism": (f"tw-sharded-emb x{world} + dp{world}" if world > 1
-                                       else "single-gpu"),
+                       "parallelism": parallelism(tr.plan, world),
                        "tables": f"criteo-{args.rows}", "embedding_dim": cfg.embedding_dim,
                        "per_gpu_batch": B}}), flush=True)
     reset()

@@ -55,6 +55,12 @@ def init_distributed(device: Optional[str] = None, backend: Optional[str] = None
     rank, world, local = env_world()
     if device is None:
         device = "cuda" if torch.cuda.is_available() else "cpu"
+    # Rehearsal knobs for a 1-GPU box: TDFO_SHARE_DEVICE=1 puts every rank on
+    # cuda:0 and TDFO_DIST_BACKEND=gloo swaps RCCL (which refuses two ranks on
+    # one GPU) for gloo, so the multi-rank step logic runs on real kernels.
+    if os.environ.get("TDFO_SHARE_DEVICE") == "1":
+        local = 0
+    backend = backend or os.environ.get("TDFO_DIST_BACKEND") or None
     if device == "cuda":
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
@@ -68,7 +74,7 @@ def init_distributed(device: Optional[str] = None, backend: Optional[str] = None
         os.environ.setdefault("MASTER_PORT", "29500")
         if not dist.is_initialized():
             kw = {}
-            if dev.type == "cuda":
+            if dev.type == "cuda" and backend == "nccl":
                 kw["device_id"] = dev
             dist.init_process_group(backend=backend, rank=rank, world_size=world,
                                     timeout=datetime.timedelta(seconds=timeout_s), **kw)
