@@ -518,6 +518,7 @@ TORCH_LIBRARY(tdfo, m) {
   m.def("gemm(Tensor a, bool a_col, Tensor b, bool b_col, Tensor? bias, bool relu, Tensor? mask, "
         "Tensor(a!)? out, Tensor(b!)? out32, int splits, Tensor? mul=None, Tensor? add=None, "
         "Tensor(c!)? out2=None) -> ()");
+  m.def("gemm_policy(int p) -> int", [](int64_t p) { return (int64_t)tdfo::gemm_policy((int)p); });
   m.def("concat_features(Tensor dense, Tensor emb, int[] off, int[] stride, int F, int D, "
         "Tensor(a!) out) -> ()");
   m.def("split_features(Tensor dx, int F, int D, Tensor dense, Tensor(a!) d_dense, "

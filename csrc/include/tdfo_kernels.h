@@ -29,8 +29,12 @@ struct GemmArgs {
   const uint16_t* mul; int64_t ldmul;
   const uint16_t* add; int64_t ldadd;
   uint16_t* C2; int64_t ldc2;
+  int abl;   // perf-ablation bits (0 in production): 1 skip A loads, 2 skip B loads, 4 skip all in-loop loads
 };
 void gemm_bf16(const GemmArgs& a, hipStream_t s);
+// Tile-shape policy for gemm_bf16 (0 auto, 1 128x128 only, 2 256x128 only);
+// p < 0 just reads it. Returns the previous policy.
+int gemm_policy(int p);
 
 // ------------------------------------------------------ interaction ----
 // DLRM dot interaction over F <= 32 features of width D (one of 16/32/64/128).

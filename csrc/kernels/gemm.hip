@@ -41,34 +41,78 @@ __device__ __forceinline__ int swz_col(int k) {
   return ((k & 3) | (((k >> 3) & 1) << 2)) << 1;
 }
 
-// Stage a [128 rows][64 k] tile of a row operand (K contiguous).
+// One 1-KiB global_load_lds piece (index ii in 0..15) of a [128 rows][64 k]
+// image of a row operand (K contiguous): 8 rows x 128 B per piece.
+__device__ __forceinline__ void glds_row(const uint16_t* g, int64_t ld, int row0, int rows,
+                                         int k0, TDFO_LDS char* tile, int ii, int lane) {
+  const int r = ii * 8 + (lane >> 3);
+  const int c = (lane & 7) ^ (r & 7);
+  int gr = row0 + r;
+  gr = gr < rows ? gr : rows - 1;
+  glds16(g + (int64_t)gr * ld + k0 + c * 8, tile + ii * 1024);
+}
+
+// One piece (ii in 0..15) of a [64 k][128 cols] image of a col operand
+// (M/N contiguous): 4 k-rows x 256 B per piece.
+__device__ __forceinline__ void glds_col(const uint16_t* g, int64_t ld, int col0, int cols,
+                                         int k0, TDFO_LDS char* tile, int ii, int lane) {
+  const int kr = ii * 4 + (lane >> 4);
+  const int c = (lane & 15) ^ swz_col(kr);
+  int gc = col0 + c * 8;
+  gc = gc <= cols - 8 ? gc : cols - 8;
+  glds16(g + (int64_t)(k0 + kr) * ld + gc, tile + ii * 1024);
+}
+
+// The same pieces issued through inline asm (M0 = wave-uniform LDS base). The
+// compiler does not see these as LDS DMA, so it does not put a vmcnt(0)
+// before every ds_read that might alias an in-flight DMA (it cannot tell the
+// ring slots apart inside one LDS array); the big kernel orders its reads
+// itself with counted vmcnt + s_barrier. The kernel issues no other vector
+// memory ops in its main loop, so those counts are exact.
+__device__ __forceinline__ void glds16_asm(const void* src, TDFO_LDS char* dst) {
+  const uint32_t lds = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)dst);
+  asm volatile("s_mov_b32 m0, %1\n\tglobal_load_lds_dwordx4 %0, off"
+               :: "v"(src), "s"(lds) : "memory", "m0");
+}
+
+template <bool COL>
+__device__ __forceinline__ void glds_piece_asm(const uint16_t* g, int64_t ld, int x0, int xs,
+                                               int k0, TDFO_LDS char* tile, int ii, int lane) {
+  if (COL) {
+    const int kr = ii * 4 + (lane >> 4);
+    const int c = (lane & 15) ^ swz_col(kr);
+    int gc = x0 + c * 8;
+    gc = gc <= xs - 8 ? gc : xs - 8;
+    glds16_asm(g + (int64_t)(k0 + kr) * ld + gc, tile + ii * 1024);
+  } else {
+    const int r = ii * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ (r & 7);
+    int gr = x0 + r;
+    gr = gr < xs ? gr : xs - 1;
+    glds16_asm(g + (int64_t)gr * ld + k0 + c * 8, tile + ii * 1024);
+  }
+}
+
+template <bool COL>
+__device__ __forceinline__ void glds_piece(const uint16_t* g, int64_t ld, int x0, int xs, int k0,
+                                           TDFO_LDS char* tile, int ii, int lane) {
+  if (COL) glds_col(g, ld, x0, xs, k0, tile, ii, lane);
+  else     glds_row(g, ld, x0, xs, k0, tile, ii, lane);
+}
+
+// Stage a whole 16-KiB image with the 4 waves of a 256-thread block.
 __device__ __forceinline__ void stage_row(const uint16_t* g, int64_t ld,
                                           int row0, int rows, int k0,
                                           TDFO_LDS char* tile, int w, int lane) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int ii = w * 4 + i;
-    const int r = ii * 8 + (lane >> 3);
-    const int c = (lane & 7) ^ (r & 7);
-    int gr = row0 + r;
-    gr = gr < rows ? gr : rows - 1;
-    glds16(g + (int64_t)gr * ld + k0 + c * 8, tile + ii * 1024);
-  }
+  for (int i = 0; i < 4; ++i) glds_row(g, ld, row0, rows, k0, tile, w * 4 + i, lane);
 }
 
-// Stage a [64 k][128 cols] tile of a col operand (M/N contiguous).
 __device__ __forceinline__ void stage_col(const uint16_t* g, int64_t ld,
                                           int col0, int cols, int k0,
                                           TDFO_LDS char* tile, int w, int lane) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int ii = w * 4 + i;
-    const int kr = ii * 4 + (lane >> 4);
-    const int c = (lane & 15) ^ swz_col(kr);
-    int gc = col0 + c * 8;
-    gc = gc <= cols - 8 ? gc : cols - 8;
-    glds16(g + (int64_t)(k0 + kr) * ld + gc, tile + ii * 1024);
-  }
+  for (int i = 0; i < 4; ++i) glds_col(g, ld, col0, cols, k0, tile, w * 4 + i, lane);
 }
 
 // MFMA operand fragment (16 rows x 32 k) of a row image: lane l holds
@@ -101,76 +145,16 @@ __device__ __forceinline__ bf16x8_t frag_col(const TDFO_LDS char* tile, int c0,
   return __builtin_bit_cast(bf16x8_t, r);
 }
 
-template <bool A_COL, bool B_COL>
-__global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs p) {
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  TDFO_LDS char* smem = (TDFO_LDS char*)smem_raw;
-
-  const int tiles_m = (p.M + BM - 1) / BM, tiles_n = (p.N + BN - 1) / BN;
-  const int wg = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  const int tm = wg / tiles_n, tn = wg - tm * tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
-
-  const int ktiles = p.K / BK;
-  const int per = (ktiles + p.splits - 1) / p.splits;
-  const int kt0 = blockIdx.z * per;
-  const int kt1 = min(ktiles, kt0 + per);
-
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wr = w >> 1, wc = w & 1;
-
-  f32x4_t acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-
-  auto stage = [&](int buf, int kt) {
-    TDFO_LDS char* ta = smem + buf * STAGE_BYTES;
-    TDFO_LDS char* tb = ta + TILE_BYTES;
-    const int k0 = kt * BK;
-    if (A_COL) stage_col(p.A, p.lda, m0, p.M, k0, ta, w, lane);
-    else       stage_row(p.A, p.lda, m0, p.M, k0, ta, w, lane);
-    if (B_COL) stage_col(p.B, p.ldb, n0, p.N, k0, tb, w, lane);
-    else       stage_row(p.B, p.ldb, n0, p.N, k0, tb, w, lane);
-  };
-
-  if (kt0 < kt1) {
-    stage(0, kt0);
-    __syncthreads();
-    int cur = 0;
-    for (int kt = kt0; kt < kt1; ++kt) {
-      if (kt + 1 < kt1) stage(cur ^ 1, kt + 1);
-      const TDFO_LDS char* ta = smem + cur * STAGE_BYTES;
-      const TDFO_LDS char* tb = ta + TILE_BYTES;
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        bf16x8_t af[4], bfr[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          af[i] = A_COL ? frag_col(ta, wr * 64 + i * 16, ks, lane)
-                        : frag_row(ta, wr * 64 + i * 16, ks, lane);
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          bfr[j] = B_COL ? frag_col(tb, wc * 64 + j * 16, ks, lane)
-                         : frag_row(tb, wc * 64 + j * 16, ks, lane);
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j],
-                                                                acc[i][j], 0, 0, 0);
-      }
-      __syncthreads();
-      cur ^= 1;
-    }
-  }
-
-  // Epilogue: bias + ReLU in registers, then the 128x128 fp32 tile is staged
-  // through the (now idle) 64-KiB LDS ring so global traffic leaves as
-  // coalesced 16-B accesses (mask loads, bf16 stores, fp32 stores).
-  // C/D map of 16x16x32: col = lane&15, row = 4*(lane>>4) + reg.
-  float* ctile = (float*)smem_raw;   // [128][128] fp32, 16-B chunks XOR-swizzled
+// Epilogue shared by both tile shapes: bias + ReLU in registers, then the
+// ROWS x 128 fp32 tile is staged through the (now idle) LDS ring so global
+// traffic leaves as coalesced 16-B accesses (mask loads, bf16 stores, fp32
+// stores, DCN Hadamard/residual second output).
+// C/D map of 16x16x32: col = lane&15, row = 4*(lane>>4) + reg.
+template <int ROWS, int NT>
+__device__ __forceinline__ void epilogue(const GemmArgs& p, const f32x4_t (&acc)[4][4],
+                                         char* smem_raw, int m0, int n0, int wr, int wc,
+                                         int lane, int tid) {
+  float* ctile = (float*)smem_raw;   // [ROWS][128] fp32, 16-B chunks XOR-swizzled
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -193,8 +177,8 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs p) {
   float* c32 = p.C32 ? p.C32 + (int64_t)blockIdx.z * p.M * p.ldc32 : nullptr;
   const bool nfull = (n0 + BN <= p.N) && ((p.N & 7) == 0);
 #pragma unroll 2
-  for (int it = 0; it < 8; ++it) {
-    const int c = it * 256 + tid;          // 8-column group id in the tile
+  for (int it = 0; it < ROWS * 16 / NT; ++it) {
+    const int c = it * NT + tid;           // 8-column group id in the tile
     const int rl = c >> 4, cg = (c & 15) * 8;
     const int m = m0 + rl;
     if (m >= p.M) continue;
@@ -265,6 +249,165 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs p) {
   }
 }
 
+// 16 MFMAs of one 64-deep K step for a wave's 64x64 sub-tile (two 32-deep
+// halves). ta/tb: 16-KiB images holding the wave's A rows / B cols at
+// a_r0 / b_c0.
+template <bool A_COL, bool B_COL>
+__device__ __forceinline__ void mfma_k64(f32x4_t (&acc)[4][4], const TDFO_LDS char* ta,
+                                         int a_r0, const TDFO_LDS char* tb, int b_c0, int lane) {
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    bf16x8_t af[4], bfr[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      af[i] = A_COL ? frag_col(ta, a_r0 + i * 16, ks, lane) : frag_row(ta, a_r0 + i * 16, ks, lane);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      bfr[j] = B_COL ? frag_col(tb, b_c0 + j * 16, ks, lane) : frag_row(tb, b_c0 + j * 16, ks, lane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Small-tile kernel: 128x128x64, 4 waves (2x2 of 64x64), 2-deep glds ring,
+// 64 KiB LDS -> 2 blocks per CU. Used when the problem has too few 256x128
+// tiles to fill the chip.
+template <bool A_COL, bool B_COL>
+__global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  TDFO_LDS char* smem = (TDFO_LDS char*)smem_raw;
+
+  const int tiles_m = (p.M + BM - 1) / BM, tiles_n = (p.N + BN - 1) / BN;
+  const int wg = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int tm = wg / tiles_n, tn = wg - tm * tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int ktiles = p.K / BK;
+  const int per = (ktiles + p.splits - 1) / p.splits;
+  const int kt0 = blockIdx.z * per;
+  const int kt1 = min(ktiles, kt0 + per);
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wr = w >> 1, wc = w & 1;
+
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  auto stage = [&](int buf, int kt) {
+    TDFO_LDS char* ta = smem + buf * STAGE_BYTES;
+    TDFO_LDS char* tb = ta + TILE_BYTES;
+    const int k0 = kt * BK;
+    if (A_COL) stage_col(p.A, p.lda, m0, p.M, k0, ta, w, lane);
+    else       stage_row(p.A, p.lda, m0, p.M, k0, ta, w, lane);
+    if (B_COL) stage_col(p.B, p.ldb, n0, p.N, k0, tb, w, lane);
+    else       stage_row(p.B, p.ldb, n0, p.N, k0, tb, w, lane);
+  };
+
+  if (kt0 < kt1) {
+    stage(0, kt0);
+    __syncthreads();
+    int cur = 0;
+    for (int kt = kt0; kt < kt1; ++kt) {
+      if (kt + 1 < kt1) stage(cur ^ 1, kt + 1);
+      const TDFO_LDS char* ta = smem + cur * STAGE_BYTES;
+      mfma_k64<A_COL, B_COL>(acc, ta, wr * 64, ta + TILE_BYTES, wc * 64, lane);
+      __syncthreads();
+      cur ^= 1;
+    }
+  }
+  epilogue<BM, 256>(p, acc, smem_raw, m0, n0, wr, wc, lane, tid);
+}
+
+// ---------------------------------------------------------------------------
+// Large-tile kernel: 256x128x64, 8 waves (4 along M x 2 along N, each 64x64),
+// 3-deep glds ring (3 x 48 KiB = 144 KiB LDS, 1 block per CU, 2 waves per
+// SIMD). Two K tiles stay in flight across each barrier: the wait before the
+// barrier is a counted vmcnt (6 pieces per thread per tile), the barrier is a
+// raw s_barrier (no vmcnt(0) drain, cdna_hip_programming.md "Pipelining
+// across barriers"), and the ring slot being refilled is the one every wave
+// finished reading before that barrier. Twice the FLOP per staged byte of the
+// 128x128 tile, which is what bounds that kernel on these short-K problems.
+constexpr int LBM = 256;
+constexpr int LSTAGE = 3 * TILE_BYTES;             // A (2 images) + B
+constexpr int LNSTAGE = 3;
+constexpr int LSMEM = LNSTAGE * LSTAGE;            // 144 KiB >= 256x128 fp32 epilogue tile
+
+template <bool A_COL, bool B_COL>
+__global__ __launch_bounds__(512, 1) void gemm_big_kernel(GemmArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  TDFO_LDS char* smem = (TDFO_LDS char*)smem_raw;
+
+  const int tiles_m = (p.M + LBM - 1) / LBM, tiles_n = (p.N + BN - 1) / BN;
+  const int wg = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int tm = wg / tiles_n, tn = wg - tm * tiles_n;
+  const int m0 = tm * LBM, n0 = tn * BN;
+
+  const int ktiles = p.K / BK;
+  const int per = (ktiles + p.splits - 1) / p.splits;
+  const int kt0 = blockIdx.z * per;
+  const int nk = min(ktiles, kt0 + per) - kt0;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wr = w >> 1, wc = w & 1;
+
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  // 6 pieces per thread per K tile: A images 2 x 16 pieces over 8 waves,
+  // B image 16 pieces over 8 waves.
+  auto stage = [&](int buf, int kt) {
+    TDFO_LDS char* ta = smem + buf * LSTAGE;
+    TDFO_LDS char* tb = ta + 2 * TILE_BYTES;
+    const int k0 = kt * BK;
+    if (!(p.abl & 1))
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int ii = w * 4 + i, half = ii >> 4;
+      glds_piece_asm<A_COL>(p.A, p.lda, m0 + half * 128, p.M, k0, ta + half * TILE_BYTES,
+                            ii & 15, lane);
+    }
+    if (!(p.abl & 2))
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      glds_piece_asm<B_COL>(p.B, p.ldb, n0, p.N, k0, tb, w * 2 + i, lane);
+  };
+
+  if (nk > 0) {
+    stage(0, kt0);
+    if (nk > 1) stage(1, kt0 + 1);
+    int cur = 0;
+    for (int t = 0; t < nk; ++t) {
+      if (t + 1 < nk && !p.abl) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      if (t + 2 < nk && !(p.abl & 4)) stage(cur == 0 ? 2 : cur - 1, kt0 + t + 2);
+      const TDFO_LDS char* ta = smem + cur * LSTAGE;
+      mfma_k64<A_COL, B_COL>(acc, ta + (wr >> 1) * TILE_BYTES, (wr & 1) * 64,
+                             ta + 2 * TILE_BYTES, wc * 64, lane);
+      cur = cur == 2 ? 0 : cur + 1;
+    }
+  }
+  epilogue<LBM, 512>(p, acc, smem_raw, m0, n0, wr, wc, lane, tid);
+}
+
+// 0 auto, 1 small tiles only, 2 large tiles only. Default 1: inside the
+// graph-replayed DLRM-1TB step the 128x128 kernel measured 0.725-0.728 ms/step
+// vs 0.735-0.736 with auto (profiles/gemm_tile_ab.md), although the 256x128
+// kernel wins 2-7 % on the N=1024 shapes in isolation.
+int g_policy = 1;
+
 template <bool AC, bool BC>
 void launch(const GemmArgs& a, hipStream_t s) {
   static bool attr = false;
@@ -272,15 +415,35 @@ void launch(const GemmArgs& a, hipStream_t s) {
     TDFO_CHECK_HIP(hipFuncSetAttribute((const void*)gemm_kernel<AC, BC>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize,
                                        SMEM_BYTES));
+    TDFO_CHECK_HIP(hipFuncSetAttribute((const void*)gemm_big_kernel<AC, BC>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, LSMEM));
     attr = true;
   }
-  const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
-  dim3 grid(tiles, 1, a.splits);
-  hipLaunchKernelGGL((gemm_kernel<AC, BC>), grid, dim3(256), SMEM_BYTES, s, a);
+  const int tn = (a.N + BN - 1) / BN;
+  const int small_tiles = ((a.M + BM - 1) / BM) * tn;
+  const int big_tiles = ((a.M + LBM - 1) / LBM) * tn;
+  GemmArgs b = a;
+  b.abl = g_policy >= 8 ? g_policy - 8 : 0;      // perf ablations (policy 9..15), big kernel
+  // auto: the 256x128 kernel once it alone fills every CU (measured on the
+  // DLRM-1TB shapes: ahead from 256 blocks up, behind below), else 128x128
+  bool big = g_policy >= 2 || (g_policy == 0 && big_tiles * a.splits >= 256);
+  if (big) {
+    dim3 grid(big_tiles, 1, a.splits);
+    hipLaunchKernelGGL((gemm_big_kernel<AC, BC>), grid, dim3(512), LSMEM, s, b);
+  } else {
+    dim3 grid(small_tiles, 1, a.splits);
+    hipLaunchKernelGGL((gemm_kernel<AC, BC>), grid, dim3(256), SMEM_BYTES, s, a);
+  }
   TDFO_CHECK_HIP(hipGetLastError());
 }
 
 }  // namespace
+
+int gemm_policy(int p) {
+  const int old = g_policy;
+  if (p >= 0) g_policy = p;
+  return old;
+}
 
 void gemm_bf16(const GemmArgs& a, hipStream_t s) {
   if (a.a_col) {

@@ -49,6 +49,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=8192)
     ap.add_argument("--only", default="")
+    ap.add_argument("--policies", default="0", help="comma list of GEMM tile policies to A/B")
+    ap.add_argument("--gemm-only", action="store_true")
     args = ap.parse_args()
     dev = "cuda"
     B = args.batch
@@ -65,6 +67,18 @@ def main():
         dx = torch.empty(M, K, device=dev, dtype=bf)
         gw = torch.empty(N * K, device=dev)
         fl = 2.0 * M * N * K
+        for pol in [int(p) for p in args.policies.split(",")]:
+            ops.gemm_policy(pol)
+            t_f = timeit(lambda: ops.linear_fwd(x, w, bias, True, out=y))
+            t_d = timeit(lambda: ops.linear_dgrad(dy, w, mask=x, out=dx))
+            t_w = timeit(lambda: ops.linear_wgrad(dy, x, gw))
+            print(json.dumps({"case": name, "policy": pol, "fwd_us": round(t_f, 1),
+                              "fwd_TF": round(fl / t_f / 1e6, 1), "dgrad_us": round(t_d, 1),
+                              "dgrad_TF": round(fl / t_d / 1e6, 1), "wgrad_us": round(t_w, 1),
+                              "wgrad_TF": round(fl / t_w / 1e6, 1)}), flush=True)
+        ops.gemm_policy(0)
+        if args.gemm_only:
+            continue
         t_f = timeit(lambda: ops.linear_fwd(x, w, bias, True, out=y))
         t_t = timeit(lambda: torch.nn.functional.linear(x, w, bias.to(bf)))
         t_d = timeit(lambda: ops.linear_dgrad(dy, w, mask=x, out=dx))
@@ -81,6 +95,8 @@ def main():
                "torch_wgrad_us": round(t_tw, 1), "colsum_us": round(t_cs, 1)}
         print(json.dumps(rec), flush=True)
         out.append(rec)
+    if args.gemm_only:
+        return
     # interaction + embedding + head
     F, D, T = 27, 128, 26
     dense = torch.randn(B, D, device=dev).to(bf)

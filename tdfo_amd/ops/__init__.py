@@ -27,6 +27,12 @@ def gemm(a, a_col, b, b_col, bias=None, relu=False, mask=None, out=None, out32=N
         ref.gemm(a, a_col, b, b_col, bias, relu, mask, out, out32, splits, mul, add, out2)
 
 
+def gemm_policy(p: int = -1) -> int:
+    """GEMM tile-shape policy of the native library: 0 auto, 1 128x128 tiles
+    only, 2 256x128 tiles only; p < 0 only reads it. Returns the previous one."""
+    return int(_native().gemm_policy(p))
+
+
 def linear_fwd(x, w, bias=None, relu=False, out=None):
     """out = act(x @ w^T + bias); x [M,K] bf16, w [N,K] bf16."""
     if out is None:

@@ -30,10 +30,19 @@ def rel_err(a, b):
 
 
 # ------------------------------------------------------------------ GEMM
+@pytest.fixture(params=[1, 2], ids=["tile128", "tile256"])
+def gemm_pol(request):
+    """Run a GEMM test once per tile kernel (128x128 2-stage / 256x128 3-stage)."""
+    old = ops.gemm_policy(request.param)
+    yield request.param
+    ops.gemm_policy(old)
+
+
 @pytest.mark.parametrize("M,N,K", [(128, 128, 64), (300, 200, 192), (8192, 1024, 512),
-                                   (1000, 72, 128), (64, 512, 1024)])
+                                   (1000, 72, 128), (64, 512, 1024), (777, 264, 320),
+                                   (2048, 1032, 128)])
 @pytest.mark.parametrize("a_col,b_col", [(False, False), (False, True), (True, True)])
-def test_gemm_layouts(M, N, K, a_col, b_col):
+def test_gemm_layouts(M, N, K, a_col, b_col, gemm_pol):
     if a_col and M % 8:
         pytest.skip("col A needs M%8")
     if b_col and N % 8:
@@ -50,7 +59,7 @@ def test_gemm_layouts(M, N, K, a_col, b_col):
     assert rel_err(out, exp.view(M, N)) < 1e-2
 
 
-def test_gemm_asymmetric_identity():
+def test_gemm_asymmetric_identity(gemm_pol):
     # A = I with asymmetric B catches row/col swaps in the C map (guide §3)
     n = 128
     A = bf(torch.eye(n, device=DEV))                       # [M=128, K=128]
@@ -64,7 +73,7 @@ def test_gemm_asymmetric_identity():
     assert torch.equal(out32b.view(n, 64), Bs.float().t())
 
 
-def test_gemm_epilogue_bias_relu_mask():
+def test_gemm_epilogue_bias_relu_mask(gemm_pol):
     torch.manual_seed(1)
     M, N, K = 513, 256, 128
     A = bf(torch.randn(M, K, device=DEV))
@@ -78,7 +87,7 @@ def test_gemm_epilogue_bias_relu_mask():
     assert rel_err(out, exp) < 1e-2
 
 
-def test_gemm_strided_out_and_splitk():
+def test_gemm_strided_out_and_splitk(gemm_pol):
     torch.manual_seed(2)
     M, N, K = 256, 512, 8192
     dy = bf(torch.randn(K, M, device=DEV))
@@ -371,7 +380,7 @@ def test_embedding_bwd_graph_replay_large():
     assert torch.equal(se, sg)
 
 
-def test_gemm_out2_mul_add():
+def test_gemm_out2_mul_add(gemm_pol):
     torch.manual_seed(5)
     M, N, K = 300, 256, 128
     A = bf(torch.randn(M, K, device=DEV))
@@ -475,7 +484,7 @@ def test_dlrm_small_hidden_layers_match_cpu():
 
 @pytest.mark.parametrize("K", [16, 32, 100])
 @pytest.mark.parametrize("a_col,b_col", [(False, False), (False, True), (True, True)])
-def test_gemm_k_tail_padding(K, a_col, b_col):
+def test_gemm_k_tail_padding(K, a_col, b_col, gemm_pol):
     torch.manual_seed(K)
     M, N = 96, 80
     A = bf(torch.randn(K, M, device=DEV) if a_col else torch.randn(M, K, device=DEV))
