@@ -162,6 +162,8 @@ void interaction_bwd(const Tensor& dz, const Tensor& dense, const Tensor& emb,
   TORCH_CHECK(dz.size(0) == B && dz.size(1) >= D + F * (F - 1) / 2, "dz shape");
   TORCH_CHECK(d_dense.size(0) == B && d_dense.size(1) >= D, "d_dense shape");
   TORCH_CHECK(dz.stride(0) % 8 == 0 && aligned16(dz.data_ptr()), "dz alignment");
+  TORCH_CHECK(d_dense.stride(0) % 8 == 0 && aligned16(d_dense.data_ptr()) &&
+              aligned16(d_emb.data_ptr()), "d_dense / d_emb alignment (16-B row stores)");
   TORCH_CHECK(emb.is_contiguous() && d_emb.is_contiguous(), "emb contiguous");
   auto m = make_slots(off, stride, F);
   auto dm = make_slots(doff, dstride, F);
@@ -518,6 +520,8 @@ TORCH_LIBRARY(tdfo, m) {
   m.def("gemm(Tensor a, bool a_col, Tensor b, bool b_col, Tensor? bias, bool relu, Tensor? mask, "
         "Tensor(a!)? out, Tensor(b!)? out32, int splits, Tensor? mul=None, Tensor? add=None, "
         "Tensor(c!)? out2=None) -> ()");
+  m.def("radix_sort_max_bits(int b) -> int",
+        [](int64_t v) { return (int64_t)tdfo::radix_sort_max_bits((int)v); });
   m.def("gemm_policy(int p) -> int", [](int64_t p) { return (int64_t)tdfo::gemm_policy((int)p); });
   m.def("concat_features(Tensor dense, Tensor emb, int[] off, int[] stride, int F, int D, "
         "Tensor(a!) out) -> ()");

@@ -106,6 +106,11 @@ __global__ __launch_bounds__(256) void inter_bwd_kernel(
   const int ldz_al = (int)((ldz + 7) & ~7LL);
   char* base = smem_raw + w * (XB + ldz_al * 2);
   char* xs = base;
+  // dX image [32][D] aliases the X image (same chunk swizzle): column tile nt
+  // is written only after its MFMAs consumed X's same columns, and the
+  // ReLU-mask read of X row 0, column d happens in the lane that then
+  // overwrites it
+  uint16_t* ys = (uint16_t*)base;
   uint16_t* zrow = (uint16_t*)(base + XB);
   constexpr int CPR = D / 8;  // 16-B chunks per X row
   const int h = lane >> 5;
@@ -176,6 +181,8 @@ __global__ __launch_bounds__(256) void inter_bwd_kernel(
           acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
               sa[ks], __builtin_bit_cast(bf16x8_t, bb), acc, 0, 0, 0);
         }
+        // dX rows -> per-wave bf16 image ys [32][D] (row 0 gets the concat
+        // passthrough dZ[:, :D] and the bottom-MLP ReLU mask here)
         const int d = 32 * nt + (lane & 31);
         if (D < 32 && d >= D) continue;
 #pragma unroll
@@ -189,11 +196,19 @@ __global__ __launch_bounds__(256) void inter_bwd_kernel(
               const uint16_t xv = *(const uint16_t*)(xs + (((d >> 3) ^ xswz<D>(0)) << 4) + ((d & 7) << 1));
               if (!(bf2f(xv) > 0.f)) val = 0.f;
             }
-            d_dense[(int64_t)b * ld_ddense + d] = f2bf(val);
-          } else {
-            d_emb[dsm.off[ii] + (int64_t)b * dsm.stride[ii] + d] = f2bf(val);
           }
+          *(uint16_t*)((char*)ys + ii * D * 2 + (((d >> 3) ^ xswz<D>(ii)) << 4) + ((d & 7) << 1)) =
+              f2bf(val);
         }
+      }
+      // coalesced 16-B stores of the F gradient rows into their slots (the
+      // wave's own LDS image: in-wave LDS order, no barrier needed)
+      for (int c = lane; c < F * CPR; c += 64) {
+        const int j = c / CPR, ch = c - j * CPR;
+        const uint4 v = *(const uint4*)((const char*)ys + j * D * 2 + ((ch ^ xswz<D>(j)) << 4));
+        uint16_t* dst = j == 0 ? d_dense + (int64_t)b * ld_ddense
+                               : d_emb + dsm.off[j] + (int64_t)b * dsm.stride[j];
+        *(uint4*)(dst + ch * 8) = v;
       }
     }
     __syncthreads();

@@ -1,16 +1,19 @@
 // Deterministic LSD radix sort of (key, int32 value) pairs for gfx950.
 //
 // Used by the fused embedding backward to group duplicate row ids. Written
-// in-house (instead of rocprim's onesweep, whose ordered-block-id path was
-// observed to fault under hipGraph replay on gfx950) so the whole sort is a
-// fixed, capture-safe sequence of 3 kernels per 8-bit digit:
-//   hist    : one 1024-item tile per block, LDS digit histogram -> [tile][256]
-//   scan    : 16 threads per digit scan digit d's column over tiles and emit
-//             the digit totals (each scatter block scans those into bases)
-//   scatter : per tile, 4 rounds of 256 items; the stable rank of an item
-//             among equal digits is found with 8 wave ballots (lanes with the
-//             same digit), per-wave digit counts in LDS and a running count
-//             per digit, so the order of equal keys is the input order.
+// in-house (rocprim's onesweep, with its ordered-block-id counter, was
+// observed to fault under hipGraph replay on gfx950) as a fixed,
+// capture-safe kernel sequence. At DLRM sizes (~2e5 keys) launches dominate,
+// so passes use up to 10-bit digits (28-bit keys: 10/9/9 = 3 passes) and the
+// per-pass histogram is produced by the previous pass's scatter:
+//   hist    : pass-0 digit histogram per 1024-item tile ([tile][bins])
+//   scan    : column scan -> per-tile exclusive prefixes + digit totals
+//   scatter : per tile, digit bases = scan(totals) + tile prefix; stable ranks
+//             from one wave ballot per digit bit and per-wave digit counts in
+//             LDS; scatter; and count the NEXT pass's digits of the written
+//             items into the next histogram (int atomics: order-independent)
+// Three histogram buffers rotate: pass p reads H[p%3], counts into H[(p+1)%3]
+// (zeroed by pass p-1 or the hist kernel) and zeroes H[(p+2)%3].
 // Stable + fixed order => bitwise-reproducible downstream reductions.
 #include "tdfo_common.h"
 #include "tdfo_kernels.h"
@@ -21,78 +24,104 @@ namespace {
 constexpr int RS_THREADS = 256;
 constexpr int RS_ROUNDS = 4;
 constexpr int RS_TILE = RS_THREADS * RS_ROUNDS;   // 1024 items per tile
+constexpr int RS_WAVES = RS_THREADS / 64;
+constexpr int RS_MAXB = 10;                       // digit bits per pass (<= 1024 bins)
+constexpr int RS_MAXBINS = 1 << RS_MAXB;
 
 template <typename K>
 __global__ __launch_bounds__(256) void rs_hist_kernel(const K* __restrict__ keys, int64_t n,
-                                                      int shift, int32_t* __restrict__ hist) {
-  __shared__ int cnt[256];
-  const int t = threadIdx.x;
-  cnt[t] = 0;
+                                                      int shift, int bits,
+                                                      int32_t* __restrict__ hist,
+                                                      int32_t* __restrict__ hzero) {
+  __shared__ int cnt[RS_MAXBINS];
+  const int t = threadIdx.x, nb = 1 << bits;
+  for (int d = t; d < RS_MAXBINS; d += RS_THREADS) hzero[(int64_t)blockIdx.x * RS_MAXBINS + d] = 0;
+  for (int d = t; d < nb; d += RS_THREADS) cnt[d] = 0;
   __syncthreads();
   const int64_t base = (int64_t)blockIdx.x * RS_TILE;
-#pragma unroll 4
+#pragma unroll
   for (int r = 0; r < RS_ROUNDS; ++r) {
     const int64_t i = base + r * RS_THREADS + t;
-    if (i < n) atomicAdd(&cnt[(int)((keys[i] >> shift) & 255)], 1);
+    if (i < n) atomicAdd(&cnt[(int)((keys[i] >> shift) & (nb - 1))], 1);
   }
   __syncthreads();
-  hist[(int64_t)blockIdx.x * 256 + t] = cnt[t];
+  for (int d = t; d < nb; d += RS_THREADS) hist[(int64_t)blockIdx.x * nb + d] = cnt[d];
 }
 
-// Column scan of the [tile][256] histogram: 4 blocks x 1024 threads; block b
-// owns digits [64b, 64b+64), 16 threads per digit each scan a contiguous run
-// of tiles, partial sums are combined in LDS, then every thread rewrites its
-// run as exclusive prefixes. Digit totals go to `tot` (the scatter kernel
-// turns them into digit bases).
+// Column scan of the [tile][nb] histogram: 1024-thread blocks, 64 digits per
+// block, 16 threads per digit scan contiguous runs of tiles. Rewrites
+// hist[tile][d] as the exclusive prefix over tiles; digit totals -> tot.
 __global__ __launch_bounds__(1024) void rs_scan_kernel(int32_t* __restrict__ hist, int ntiles,
-                                                       int32_t* __restrict__ tot) {
+                                                       int nb, int32_t* __restrict__ tot) {
   __shared__ int part[16][64];
   const int dl = threadIdx.x & 63, ph = threadIdx.x >> 6;
   const int d = blockIdx.x * 64 + dl;
   const int per = (ntiles + 15) / 16;
-  const int t0 = ph * per, t1 = min(ntiles, t0 + per);
+  const int t0 = ph * per, t1 = d < nb ? min(ntiles, t0 + per) : t0;   // d >= nb: idle
   int s = 0;
-  for (int t = t0; t < t1; ++t) s += hist[(int64_t)t * 256 + d];
+  for (int t = t0; t < t1; ++t) s += hist[(int64_t)t * nb + d];
   part[ph][dl] = s;
   __syncthreads();
   int run = 0;
   for (int q = 0; q < ph; ++q) run += part[q][dl];
-  if (ph == 15) tot[d] = run + s;
+  if (ph == 15 && d < nb) tot[d] = run + s;
   for (int t = t0; t < t1; ++t) {
-    const int c = hist[(int64_t)t * 256 + d];
-    hist[(int64_t)t * 256 + d] = run;
+    const int c = hist[(int64_t)t * nb + d];
+    hist[(int64_t)t * nb + d] = run;
     run += c;
   }
 }
 
+// Per tile: digit bases (exclusive scan of the digit totals + this tile's
+// prefix), stable ranks from wave ballots (one per digit bit) and per-wave
+// digit counts, scatter; and the next pass's digit counts into hnext.
 template <typename K>
-__global__ __launch_bounds__(256) void rs_scatter_kernel(const K* __restrict__ kin,
-                                                         const int32_t* __restrict__ vin,
-                                                         K* __restrict__ kout,
-                                                         int32_t* __restrict__ vout, int64_t n,
-                                                         int shift,
-                                                         const int32_t* __restrict__ hist,
-                                                         const int32_t* __restrict__ tot) {
-  __shared__ int run[256];
-  __shared__ int wcnt[4][256];
-  __shared__ int start[256];
+__global__ __launch_bounds__(256) void rs_scatter_kernel(
+    const K* __restrict__ kin, const int32_t* __restrict__ vin, K* __restrict__ kout,
+    int32_t* __restrict__ vout, int64_t n, int shift, int bits, int next_shift, int next_bits,
+    const int32_t* __restrict__ hist, const int32_t* __restrict__ tot,
+    int32_t* __restrict__ hnext, int32_t* __restrict__ hzero) {
+  __shared__ int start[RS_MAXBINS];
+  __shared__ int run[RS_MAXBINS];
+  __shared__ int wcnt[RS_WAVES][RS_MAXBINS];
+  __shared__ int wsum[RS_WAVES];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  // digit bases: exclusive scan of the 256 digit totals (Hillis-Steele)
-  const int mytot = tot[t];
-  start[t] = mytot;
-  __syncthreads();
-  for (int off = 1; off < 256; off <<= 1) {
-    const int v = t >= off ? start[t - off] : 0;
-    __syncthreads();
-    start[t] += v;
-    __syncthreads();
+  const int nb = 1 << bits, per_t = nb / RS_THREADS > 0 ? nb / RS_THREADS : 1;
+  const int tile = blockIdx.x;
+  const int nnb = next_shift >= 0 ? 1 << next_bits : 0;
+  for (int d = t; d < RS_MAXBINS; d += RS_THREADS) hzero[(int64_t)tile * RS_MAXBINS + d] = 0;
+  // exclusive scan of the digit totals: thread t owns digits [t*per_t, +per_t)
+  int loc[RS_MAXBINS / RS_THREADS];
+  int mysum = 0;
+#pragma unroll
+  for (int j = 0; j < RS_MAXBINS / RS_THREADS; ++j) {
+    const int d = t * per_t + j;
+    loc[j] = (j < per_t && d < nb) ? tot[d] : 0;
+    mysum += loc[j];
   }
-  start[t] = start[t] - mytot + hist[(int64_t)blockIdx.x * 256 + t];
-  run[t] = 0;
-  wcnt[0][t] = wcnt[1][t] = wcnt[2][t] = wcnt[3][t] = 0;
+  int x = mysum;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  for (int q = t; q < RS_WAVES * RS_MAXBINS; q += RS_THREADS) (&wcnt[0][0])[q] = 0;
+  __syncthreads();
+  int acc = x - mysum;
+  for (int q = 0; q < w; ++q) acc += wsum[q];
+#pragma unroll
+  for (int j = 0; j < RS_MAXBINS / RS_THREADS; ++j) {
+    const int d = t * per_t + j;
+    if (j < per_t && d < nb) {
+      start[d] = acc + hist[(int64_t)tile * nb + d];
+      run[d] = 0;
+      acc += loc[j];
+    }
+  }
   __syncthreads();
   const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  const int64_t tbase = (int64_t)blockIdx.x * RS_TILE;
+  const int64_t tbase = (int64_t)tile * RS_TILE;
   for (int r = 0; r < RS_ROUNDS; ++r) {
     const int64_t i = tbase + r * RS_THREADS + t;
     const bool valid = i < n;
@@ -102,11 +131,10 @@ __global__ __launch_bounds__(256) void rs_scatter_kernel(const K* __restrict__ k
     if (valid) {
       k = kin[i];
       v = vin[i];
-      dg = (int)((k >> shift) & 255);
+      dg = (int)((k >> shift) & (nb - 1));
     }
     uint64_t m = __ballot(valid);
-#pragma unroll
-    for (int b = 0; b < 8; ++b) {
+    for (int b = 0; b < bits; ++b) {
       const uint64_t bb = __ballot((dg >> b) & 1);
       m &= ((dg >> b) & 1) ? bb : ~bb;
     }
@@ -114,30 +142,52 @@ __global__ __launch_bounds__(256) void rs_scatter_kernel(const K* __restrict__ k
     if (valid && rank == 0) wcnt[w][dg] = __popcll(m);
     __syncthreads();
     if (valid) {
-      int pos = start[dg] + run[dg] + rank;
+      int64_t pos = start[dg] + run[dg] + rank;
       for (int q = 0; q < w; ++q) pos += wcnt[q][dg];
       kout[pos] = k;
       vout[pos] = v;
+      if (nnb) atomicAdd(&hnext[(pos / RS_TILE) * nnb + (int)((k >> next_shift) & (nnb - 1))], 1);
     }
     __syncthreads();
-    run[t] += wcnt[0][t] + wcnt[1][t] + wcnt[2][t] + wcnt[3][t];
-    wcnt[0][t] = wcnt[1][t] = wcnt[2][t] = wcnt[3][t] = 0;
+    for (int d = t; d < nb; d += RS_THREADS) {
+      int c = 0;
+#pragma unroll
+      for (int q = 0; q < RS_WAVES; ++q) { c += wcnt[q][d]; wcnt[q][d] = 0; }
+      run[d] += c;
+    }
     __syncthreads();
   }
 }
 
+int g_max_bits = 10;  // digit bits per pass (<= RS_MAXB): 28-bit keys -> 10/9/9 (fastest measured)
+
 template <typename K>
-int sort_impl(K* ka, int32_t* va, K* kb, int32_t* vb, int64_t n, int key_bits, int32_t* hist,
-              int32_t* base, hipStream_t s) {
+int sort_impl(K* ka, int32_t* va, K* kb, int32_t* vb, int64_t n, int key_bits, int32_t* ws,
+              hipStream_t s) {
   const int ntiles = (int)((n + RS_TILE - 1) / RS_TILE);
-  const int passes = (key_bits + 7) / 8;
+  const int kbits = key_bits < 1 ? 1 : key_bits;
+  const int passes = (kbits + g_max_bits - 1) / g_max_bits;
+  int pbits[8], pshift[8];
+  for (int p = 0, sh = 0; p < passes; ++p) {   // e.g. 28 bits -> 10, 9, 9
+    pbits[p] = (kbits - sh + (passes - p) - 1) / (passes - p);
+    pshift[p] = sh;
+    sh += pbits[p];
+  }
+  const int64_t hsz = (int64_t)ntiles * RS_MAXBINS;
+  int32_t* H[3] = {ws, ws + hsz, ws + 2 * hsz};
+  int32_t* tot = ws + 3 * hsz;
+  hipLaunchKernelGGL(rs_hist_kernel<K>, dim3(ntiles), dim3(RS_THREADS), 0, s, ka, n, pshift[0],
+                     pbits[0], H[0], H[1]);
+  TDFO_CHECK_HIP(hipGetLastError());
   K* kin = ka; int32_t* vin = va; K* kout = kb; int32_t* vout = vb;
   for (int p = 0; p < passes; ++p) {
-    const int shift = 8 * p;
-    hipLaunchKernelGGL(rs_hist_kernel<K>, dim3(ntiles), dim3(256), 0, s, kin, n, shift, hist);
-    hipLaunchKernelGGL(rs_scan_kernel, dim3(4), dim3(1024), 0, s, hist, ntiles, base);
-    hipLaunchKernelGGL(rs_scatter_kernel<K>, dim3(ntiles), dim3(256), 0, s, kin, vin, kout, vout,
-                       n, shift, hist, base);
+    const int nb = 1 << pbits[p];
+    hipLaunchKernelGGL(rs_scan_kernel, dim3((nb + 63) / 64), dim3(1024), 0, s, H[p % 3], ntiles,
+                       nb, tot);
+    const bool last = p + 1 == passes;
+    hipLaunchKernelGGL(rs_scatter_kernel<K>, dim3(ntiles), dim3(RS_THREADS), 0, s, kin, vin,
+                       kout, vout, n, pshift[p], pbits[p], last ? -1 : pshift[p + 1],
+                       last ? 0 : pbits[p + 1], H[p % 3], tot, H[(p + 1) % 3], H[(p + 2) % 3]);
     TDFO_CHECK_HIP(hipGetLastError());
     K* tk = kin; kin = kout; kout = tk;
     int32_t* tv = vin; vin = vout; vout = tv;
@@ -147,25 +197,27 @@ int sort_impl(K* ka, int32_t* va, K* kb, int32_t* vb, int64_t n, int key_bits, i
 
 }  // namespace
 
+int radix_sort_max_bits(int b) {
+  const int old = g_max_bits;
+  if (b >= 4 && b <= RS_MAXB) g_max_bits = b;
+  return old;
+}
+
 size_t radix_sort_workspace(int64_t n) {
   const int64_t ntiles = (n + RS_TILE - 1) / RS_TILE;
-  return (size_t)(ntiles * 256 + 256) * sizeof(int32_t);
+  return (size_t)(3 * ntiles * RS_MAXBINS + RS_MAXBINS) * sizeof(int32_t);
 }
 
 int radix_sort_pairs_u32(uint32_t* ka, int32_t* va, uint32_t* kb, int32_t* vb, int64_t n,
                          int key_bits, void* ws, hipStream_t s) {
   if (n <= 0) return 0;
-  const int64_t ntiles = (n + RS_TILE - 1) / RS_TILE;
-  int32_t* hist = (int32_t*)ws;
-  return sort_impl<uint32_t>(ka, va, kb, vb, n, key_bits, hist, hist + ntiles * 256, s);
+  return sort_impl<uint32_t>(ka, va, kb, vb, n, key_bits, (int32_t*)ws, s);
 }
 
 int radix_sort_pairs_u64(uint64_t* ka, int32_t* va, uint64_t* kb, int32_t* vb, int64_t n,
                          int key_bits, void* ws, hipStream_t s) {
   if (n <= 0) return 0;
-  const int64_t ntiles = (n + RS_TILE - 1) / RS_TILE;
-  int32_t* hist = (int32_t*)ws;
-  return sort_impl<uint64_t>(ka, va, kb, vb, n, key_bits, hist, hist + ntiles * 256, s);
+  return sort_impl<uint64_t>(ka, va, kb, vb, n, key_bits, (int32_t*)ws, s);
 }
 
 }  // namespace tdfo

@@ -51,6 +51,7 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--policies", default="0", help="comma list of GEMM tile policies to A/B")
     ap.add_argument("--gemm-only", action="store_true")
+    ap.add_argument("--wsplits", default="", help="comma list of wgrad split counts to time")
     args = ap.parse_args()
     dev = "cuda"
     B = args.batch
@@ -76,7 +77,13 @@ def main():
                               "fwd_TF": round(fl / t_f / 1e6, 1), "dgrad_us": round(t_d, 1),
                               "dgrad_TF": round(fl / t_d / 1e6, 1), "wgrad_us": round(t_w, 1),
                               "wgrad_TF": round(fl / t_w / 1e6, 1)}), flush=True)
-        ops.gemm_policy(0)
+        ops.gemm_policy(1)
+        if args.wsplits:
+            for sp in [int(v) for v in args.wsplits.split(",")]:
+                slab = torch.empty(sp * N * K, device=dev)
+                t_w = timeit(lambda: ops.linear_wgrad(dy, x, gw, slab=slab, splits=sp))
+                print(json.dumps({"case": name, "wgrad_splits": sp, "wgrad_us": round(t_w, 1)}),
+                      flush=True)
         if args.gemm_only:
             continue
         t_f = timeit(lambda: ops.linear_fwd(x, w, bias, True, out=y))

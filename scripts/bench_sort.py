@@ -1,0 +1,23 @@
+#!/usr/bin/env python
+"""Radix sort (embedding-backward key sort) timing vs digit width, one process."""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from tdfo_amd import ops  # noqa: E402
+from tdfo_amd.ops import _ext  # noqa: E402
+from bench_kernels import timeit  # noqa: E402
+
+_ext.load()
+nat = torch.ops.tdfo
+for n in (213_000, 1_700_000):
+    keys = torch.randint(0, 188_000_000, (n,), device="cuda", dtype=torch.int32)
+    vals = torch.arange(n, dtype=torch.int32, device="cuda")
+    for b in (6, 7, 8, 9, 10):
+        nat.radix_sort_max_bits(b)
+        t = timeit(lambda: ops.sort_pairs(keys, vals, 28))
+        print(json.dumps({"n": n, "max_bits": b, "sort_us": round(t, 1)}), flush=True)
+nat.radix_sort_max_bits(10)

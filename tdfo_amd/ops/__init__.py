@@ -50,9 +50,12 @@ def linear_dgrad(dy, w, mask=None, out=None):
 
 
 def wgrad_splits(M: int, N: int, K: int, target_blocks: int = 512) -> int:
+    """Split-K count for a weight-grad GEMM (K = batch): ~target_blocks blocks,
+    but every split keeps >= 8 K tiles (measured on MI355X: bot/top3 wgrads run
+    18.8 us at 16 splits vs 22.7 us at 64; top1 is best at 8)."""
     tiles = ((M + 127) // 128) * ((N + 127) // 128)
     kt = K // 64
-    s = max(1, min(kt // 2 if kt >= 2 else 1, -(-target_blocks // tiles)))
+    s = max(1, min(max(1, kt // 8), -(-target_blocks // tiles)))
     return s
 
 
