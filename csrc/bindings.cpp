@@ -4,6 +4,8 @@
 // captured into a hipGraph (torch.cuda.CUDAGraph) and replayed without
 // allocation. Shapes, dtypes, strides and alignment are validated on the host
 // before any launch (a mis-shaped launch can fault the GPU).
+#include <cmath>
+
 #include <ATen/ATen.h>
 #include <ATen/hip/HIPContext.h>
 #include <torch/library.h>
@@ -172,6 +174,87 @@ void interaction_bwd(const Tensor& dz, const Tensor& dense, const Tensor& emb,
   tdfo::interaction_bwd(bf16_ptr(dz), dz.stride(0), bf16_ptr(dense), dense.stride(0),
                         bf16_ptr(emb), m, (int)F, (int)D, (int)B, bf16_mut(d_dense),
                         d_dense.stride(0), bf16_mut(d_emb), dm, relu_mask, cur_stream());
+}
+
+// ------------------------------------------------------------ attention
+tdfo::AttnArgs attn_args(const Tensor& qkv, const Tensor& ids, int64_t H, double rate,
+                         int64_t seed, const c10::optional<Tensor>& step, int64_t pad_id) {
+  check_dev(qkv, "qkv"); check_dev(ids, "ids");
+  TORCH_CHECK(qkv.scalar_type() == at::kFloat && qkv.is_contiguous() && qkv.dim() == 3,
+              "attention: qkv fp32 contiguous [B, T, 3E]");
+  TORCH_CHECK(ids.scalar_type() == at::kLong && ids.is_contiguous() && ids.dim() == 2 &&
+              ids.size(0) == qkv.size(0) && ids.size(1) == qkv.size(1), "attention: ids int64 [B, T]");
+  const int64_t E3 = qkv.size(2);
+  TORCH_CHECK(E3 % 3 == 0 && H > 0 && (E3 / 3) % H == 0, "attention: 3E must split into H heads");
+  TORCH_CHECK(qkv.size(1) <= 64, "attention: T <= 64");
+  TORCH_CHECK(rate >= 0.0 && rate < 1.0, "attention: dropout rate in [0, 1)");
+  tdfo::AttnArgs a{};
+  a.qkv = qkv.data_ptr<float>(); a.ids = ids.data_ptr<int64_t>();
+  a.B = (int)qkv.size(0); a.T = (int)qkv.size(1); a.H = (int)H; a.dk = (int)(E3 / 3 / H);
+  a.scale = 1.f / std::sqrt((float)a.dk); a.rate = (float)rate; a.seed = seed; a.pad_id = pad_id;
+  if (step) {
+    check_dev(*step, "step");
+    TORCH_CHECK(step->scalar_type() == at::kLong && step->numel() >= 1, "attention: step int64");
+    a.step = step->data_ptr<int64_t>();
+  }
+  return a;
+}
+
+void attention_fwd(const Tensor& qkv, const Tensor& ids, int64_t H, double rate, int64_t seed,
+                   const c10::optional<Tensor>& step, int64_t pad_id, const Tensor& out) {
+  auto a = attn_args(qkv, ids, H, rate, seed, step, pad_id);
+  check_dev(out, "out");
+  TORCH_CHECK(out.scalar_type() == at::kFloat && out.is_contiguous() &&
+              out.numel() == qkv.numel() / 3, "attention: out fp32 [B, T, E]");
+  a.out = out.data_ptr<float>();
+  tdfo::attention_fwd(a, cur_stream());
+}
+
+void attention_bwd(const Tensor& qkv, const Tensor& ids, const Tensor& dout, int64_t H,
+                   double rate, int64_t seed, const c10::optional<Tensor>& step, int64_t pad_id,
+                   const Tensor& dqkv) {
+  auto a = attn_args(qkv, ids, H, rate, seed, step, pad_id);
+  check_dev(dout, "dout"); check_dev(dqkv, "dqkv");
+  TORCH_CHECK(dout.scalar_type() == at::kFloat && dout.is_contiguous() &&
+              dout.numel() == qkv.numel() / 3, "attention: dout fp32 [B, T, E]");
+  TORCH_CHECK(dqkv.scalar_type() == at::kFloat && dqkv.is_contiguous() &&
+              dqkv.numel() == qkv.numel(), "attention: dqkv fp32 [B, T, 3E]");
+  a.dout = dout.data_ptr<float>(); a.dqkv = dqkv.data_ptr<float>();
+  tdfo::attention_bwd(a, cur_stream());
+}
+
+// ------------------------------------------------------------ layernorm
+void check_f32c(const Tensor& t, const char* name) {
+  check_dev(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kFloat && t.is_contiguous(), name, " must be fp32 contiguous");
+}
+
+void layernorm_fwd(const Tensor& x, int64_t n, double eps, const Tensor& gamma, const Tensor& beta,
+                   const Tensor& y, const Tensor& mean, const Tensor& rstd) {
+  check_f32c(x, "x"); check_f32c(gamma, "gamma"); check_f32c(beta, "beta");
+  check_f32c(y, "y"); check_f32c(mean, "mean"); check_f32c(rstd, "rstd");
+  TORCH_CHECK(n > 0 && n <= 1024 && x.numel() % n == 0, "layernorm: n in (0, 1024] dividing x");
+  const int64_t M = x.numel() / n;
+  TORCH_CHECK(gamma.numel() == n && beta.numel() == n && y.numel() == x.numel() &&
+              mean.numel() >= M && rstd.numel() >= M, "layernorm: shapes");
+  tdfo::layernorm_fwd(x.data_ptr<float>(), M, (int)n, (float)eps, gamma.data_ptr<float>(),
+                      beta.data_ptr<float>(), y.data_ptr<float>(), mean.data_ptr<float>(),
+                      rstd.data_ptr<float>(), cur_stream());
+}
+
+void layernorm_bwd(const Tensor& x, const Tensor& g, int64_t n, const Tensor& gamma,
+                   const Tensor& mean, const Tensor& rstd, const Tensor& dx, const Tensor& part,
+                   const Tensor& dgb) {
+  check_f32c(x, "x"); check_f32c(g, "g"); check_f32c(gamma, "gamma"); check_f32c(mean, "mean");
+  check_f32c(rstd, "rstd"); check_f32c(dx, "dx"); check_f32c(part, "part"); check_f32c(dgb, "dgb");
+  TORCH_CHECK(n > 0 && n <= 1024 && x.numel() % n == 0, "layernorm: n");
+  const int64_t M = x.numel() / n;
+  TORCH_CHECK(g.numel() == x.numel() && dx.numel() == x.numel() && gamma.numel() == n &&
+              mean.numel() >= M && rstd.numel() >= M && dgb.numel() == 2 * n &&
+              part.numel() >= (int64_t)tdfo::layernorm_parts(M) * 2 * n, "layernorm_bwd: shapes");
+  tdfo::layernorm_bwd(x.data_ptr<float>(), g.data_ptr<float>(), M, (int)n, gamma.data_ptr<float>(),
+                      mean.data_ptr<float>(), rstd.data_ptr<float>(), dx.data_ptr<float>(),
+                      part.data_ptr<float>(), dgb.data_ptr<float>(), cur_stream());
 }
 
 // ----------------------------------------------------------- elementwise
@@ -523,6 +606,15 @@ TORCH_LIBRARY(tdfo, m) {
   m.def("radix_sort_max_bits(int b) -> int",
         [](int64_t v) { return (int64_t)tdfo::radix_sort_max_bits((int)v); });
   m.def("gemm_policy(int p) -> int", [](int64_t p) { return (int64_t)tdfo::gemm_policy((int)p); });
+  m.def("attention_fwd(Tensor qkv, Tensor ids, int H, float rate, int seed, Tensor? step, int pad_id, "
+        "Tensor(a!) out) -> ()");
+  m.def("attention_bwd(Tensor qkv, Tensor ids, Tensor dout, int H, float rate, int seed, Tensor? step, "
+        "int pad_id, Tensor(a!) dqkv) -> ()");
+  m.def("layernorm_fwd(Tensor x, int n, float eps, Tensor gamma, Tensor beta, Tensor(a!) y, "
+        "Tensor(b!) mean, Tensor(c!) rstd) -> ()");
+  m.def("layernorm_bwd(Tensor x, Tensor g, int n, Tensor gamma, Tensor mean, Tensor rstd, "
+        "Tensor(a!) dx, Tensor(b!) part, Tensor(c!) dgb) -> ()");
+  m.def("layernorm_parts(int M) -> int", [](int64_t M) { return (int64_t)tdfo::layernorm_parts(M); });
   m.def("concat_features(Tensor dense, Tensor emb, int[] off, int[] stride, int F, int D, "
         "Tensor(a!) out) -> ()");
   m.def("split_features(Tensor dx, int F, int D, Tensor dense, Tensor(a!) d_dense, "
@@ -560,6 +652,10 @@ TORCH_LIBRARY(tdfo, m) {
 
 TORCH_LIBRARY_IMPL(tdfo, CUDA, m) {
   m.impl("gemm", gemm);
+  m.impl("attention_fwd", attention_fwd);
+  m.impl("attention_bwd", attention_bwd);
+  m.impl("layernorm_fwd", layernorm_fwd);
+  m.impl("layernorm_bwd", layernorm_bwd);
   m.impl("concat_features", concat_features);
   m.impl("split_features", split_features);
   m.impl("cross_bwd", cross_bwd);

@@ -195,6 +195,28 @@ struct LinearXentArgs {
 size_t linear_xent_workspace(int N, int64_t V);
 void linear_xent(const LinearXentArgs& a, hipStream_t s);
 
+// -------------------------------------------------------- attention ----
+// Fused small-T MHA core (attention.hip): qkv [B,T,3E] fp32 (q|k|v, each
+// H x dk), key-padding mask from ids != pad_id, dropout(rate) from a counter
+// hash of (seed, *step, b, h, i, j). out/dout [B,T,E], dqkv [B,T,3E].
+struct AttnArgs {
+  const float* qkv; const int64_t* ids;
+  const float* dout; float* out; float* dqkv;
+  int B, T, H, dk; float scale, rate; int64_t seed; const int64_t* step; int64_t pad_id;
+};
+void attention_fwd(const AttnArgs& a, hipStream_t s);
+void attention_bwd(const AttnArgs& a, hipStream_t s);
+
+// ------------------------------------------------------- layernorm ----
+// Row LayerNorm over the last n <= 1024 elements (layernorm.hip).
+int layernorm_parts(int64_t M);
+void layernorm_fwd(const float* x, int64_t M, int n, float eps, const float* gamma,
+                   const float* beta, float* y, float* mean, float* rstd, hipStream_t s);
+// part: layernorm_parts(M) * 2n floats; dgamma_dbeta: [2n] = [dgamma | dbeta]
+void layernorm_bwd(const float* x, const float* g, int64_t M, int n, const float* gamma,
+                   const float* mean, const float* rstd, float* dx, float* part,
+                   float* dgamma_dbeta, hipStream_t s);
+
 // ----------------------------------------------------------- jagged ----
 void jagged_to_dense(const float* values, const int64_t* off, int B, int T, int D, float pad,
                      float* out, hipStream_t s);

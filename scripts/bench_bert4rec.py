@@ -20,7 +20,12 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--torch-encoder", action="store_true",
+                    help="torch reference attention/LayerNorm instead of the HIP kernels")
     a = ap.parse_args()
+    if a.torch_encoder:
+        import tdfo_amd.models.bert4rec as m
+        m.USE_FUSED = False
     dev = "cuda"
     T = 20
     tr = Bert4RecTrainer(a.items, T, 16, 2, 2, a.batch, device=dev)
@@ -46,7 +51,7 @@ def main():
     torch.cuda.synchronize()
     el = time.perf_counter() - t
     print(json.dumps({"model": "bert4rec", "batch": a.batch, "vocab": a.items + 2,
-                      "graph": not a.no_graph, "ms_per_step": round(el / a.steps * 1e3, 4),
+                      "graph": not a.no_graph, "fused_encoder": not a.torch_encoder, "ms_per_step": round(el / a.steps * 1e3, 4),
                       "sequences_per_sec": round(a.batch * a.steps / el, 1),
                       "loss": round(tr.pop_loss(), 4)}))
 

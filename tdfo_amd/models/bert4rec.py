@@ -41,6 +41,77 @@ PAD_ID = 0
 METRICS_K = (10, 20, 50)
 
 
+# ---------------------------------------------------- fused HIP encoder ops
+# On GPU the attention core (scores, key-padding mask, softmax, dropout, P.V)
+# and every LayerNorm run as hand-written kernels (csrc/kernels/attention.hip,
+# layernorm.hip); on CPU the same modules run the torch reference ops.
+USE_FUSED = True
+
+
+def _fused(x: torch.Tensor) -> bool:
+    return USE_FUSED and x.is_cuda
+
+
+class _AttnCoreFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, qkv, ids, H, rate, seed, step):
+        qkv = qkv.contiguous()
+        B, T, E3 = qkv.shape
+        out = torch.empty(B, T, E3 // 3, dtype=qkv.dtype, device=qkv.device)
+        ops.attention_fwd(qkv, ids, H, rate, seed, step, PAD_ID, out)
+        ctx.save_for_backward(qkv, ids, step)
+        ctx.cfg = (H, rate, seed)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        qkv, ids, step = ctx.saved_tensors
+        H, rate, seed = ctx.cfg
+        dqkv = torch.empty_like(qkv)
+        ops.attention_bwd(qkv, ids, g.contiguous(), H, rate, seed, step, PAD_ID, dqkv)
+        return dqkv, None, None, None, None, None
+
+
+class _LayerNormFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, n, eps):
+        x = x.contiguous()
+        M = x.numel() // n
+        y = torch.empty_like(x)
+        mean = torch.empty(M, dtype=torch.float32, device=x.device)
+        rstd = torch.empty_like(mean)
+        ops.layernorm_fwd(x, n, eps, gamma, beta, y, mean, rstd)
+        ctx.save_for_backward(x, gamma, mean, rstd)
+        ctx.n = n
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x, gamma, mean, rstd = ctx.saved_tensors
+        n = ctx.n
+        M = x.numel() // n
+        dx = torch.empty_like(x)
+        part = torch.empty(ops.layernorm_parts(M) * 2 * n, dtype=torch.float32, device=x.device)
+        dgb = torch.empty(2 * n, dtype=torch.float32, device=x.device)
+        ops.layernorm_bwd(x, g.contiguous(), n, gamma, mean, rstd, dx, part, dgb)
+        return dx, dgb[:n].view_as(gamma), dgb[n:].view_as(gamma), None, None
+
+
+def layer_norm(x: torch.Tensor, ln: nn.LayerNorm) -> torch.Tensor:
+    if _fused(x):
+        n = ln.weight.numel()
+        return _LayerNormFn.apply(x, ln.weight, ln.bias, n, ln.eps)
+    return ln(x)
+
+
+class KeyPad:
+    """Attention context of the fused path: item ids (key-padding mask is
+    ids != PAD) and the device step counter that keys the dropout hash."""
+
+    def __init__(self, ids: torch.Tensor, step: Optional[torch.Tensor]):
+        self.ids, self.step = ids, step
+
+
 # ------------------------------------------------------------------ encoder
 class MultiHeadedAttention(nn.Module):
     def __init__(self, num_heads: int, dim: int, dropout: float = 0.1):
@@ -51,11 +122,17 @@ class MultiHeadedAttention(nn.Module):
         self.linear_layers = nn.ModuleList([nn.Linear(dim, dim) for _ in range(3)])
         self.output_linear = nn.Linear(dim, dim)
         self.dropout = nn.Dropout(dropout)
+        self.seed = 0x5EED                 # per-layer dropout-hash seed (set by Bert4Rec)
 
     def forward(self, x, mask):
         B, T, _ = x.shape
         w = torch.cat([l.weight for l in self.linear_layers], 0)       # one QKV GEMM
         b = torch.cat([l.bias for l in self.linear_layers], 0)
+        if isinstance(mask, KeyPad):
+            rate = self.dropout.p if self.training else 0.0
+            core = _AttnCoreFn.apply(F.linear(x, w, b), mask.ids, self.h, rate, self.seed,
+                                     mask.step)
+            return self.output_linear(core)
         qkv = F.linear(x, w, b).view(B, T, 3, self.h, self.d_k).permute(2, 0, 3, 1, 4)
         q, k, v = qkv[0], qkv[1], qkv[2]
         scores = torch.matmul(q, k.transpose(-2, -1)) / math.sqrt(self.d_k)
@@ -83,7 +160,7 @@ class SublayerConnection(nn.Module):
         self.dropout = nn.Dropout(dropout)
 
     def forward(self, x, fn):
-        return x + self.dropout(fn(self.norm(x)))       # pre-norm (torchrec/models.py:102-106)
+        return x + self.dropout(fn(layer_norm(x, self.norm)))   # pre-norm (torchrec/models.py:102-106)
 
 
 class TransformerBlock(nn.Module):
@@ -204,11 +281,19 @@ class Bert4Rec(nn.Module):
         self.transformer_blocks = nn.ModuleList(
             [TransformerBlock(embed_dim, num_heads, dropout) for _ in range(num_layers)])
         self.out = nn.Linear(embed_dim, vocab_size)
+        for i, blk in enumerate(self.transformer_blocks):
+            blk.attention.seed = 0x5EED + 7919 * i
+        # device step counter for the fused attention's dropout hash (advanced
+        # once per training step by the trainer, inside the captured graph)
+        self.register_buffer("rng_step", torch.zeros(1, dtype=torch.int64), persistent=False)
 
     def encode(self, item_emb: torch.Tensor, seqs: torch.Tensor) -> torch.Tensor:
         """item_emb [B, T, E] (looked-up rows), seqs [B, T] ids -> hidden [B, T, E]."""
-        mask = (seqs != PAD_ID).unsqueeze(1).unsqueeze(1)          # [B, 1, 1, T] key mask
-        x = self.emb_dropout(self.layernorm(item_emb + self.positional_encoding))
+        if _fused(item_emb):
+            mask = KeyPad(seqs.contiguous(), self.rng_step)
+        else:
+            mask = (seqs != PAD_ID).unsqueeze(1).unsqueeze(1)      # [B, 1, 1, T] key mask
+        x = self.emb_dropout(layer_norm(item_emb + self.positional_encoding, self.layernorm))
         for blk in self.transformer_blocks:
             x = blk(x, mask)
         return x
@@ -295,6 +380,7 @@ class Bert4RecTrainer:
         loss = self._fwd_bwd(seqs, labels)
         self.opt.all_reduce_grads(average=True)
         self.opt.step()
+        self.model.rng_step.add_(1)
         self.loss_sum.add_(loss.detach().double())
         return loss
 

@@ -247,3 +247,39 @@ def jagged_ids_to_dense(values, offsets, pad, out):
         _native().jagged_ids_to_dense(values, offsets, int(pad), out)
     else:
         ref.jagged_ids_to_dense(values, offsets, pad, out)
+
+
+def attention_fwd(qkv, ids, H, rate, seed, step, pad_id, out):
+    """Fused small-T MHA core: qkv [B,T,3E] fp32 -> out [B,T,E] (key-padding
+    mask from ids != pad_id, hash dropout keyed by (seed, step[0]))."""
+    if _gpu(qkv):
+        _native().attention_fwd(qkv, ids, int(H), float(rate), int(seed), step, int(pad_id), out)
+    else:
+        ref.attention_fwd(qkv, ids, H, rate, seed, step, pad_id, out)
+
+
+def attention_bwd(qkv, ids, dout, H, rate, seed, step, pad_id, dqkv):
+    if _gpu(qkv):
+        _native().attention_bwd(qkv, ids, dout, int(H), float(rate), int(seed), step,
+                                int(pad_id), dqkv)
+    else:
+        ref.attention_bwd(qkv, ids, dout, H, rate, seed, step, pad_id, dqkv)
+
+
+def layernorm_parts(M: int) -> int:
+    return int(_native().layernorm_parts(int(M))) if native_available() else 1
+
+
+def layernorm_fwd(x, n, eps, gamma, beta, y, mean, rstd):
+    if _gpu(x):
+        _native().layernorm_fwd(x, int(n), float(eps), gamma, beta, y, mean, rstd)
+    else:
+        ref.layernorm_fwd(x, n, eps, gamma, beta, y, mean, rstd)
+
+
+def layernorm_bwd(x, g, n, gamma, mean, rstd, dx, part, dgb):
+    """dgb [2n] = [dgamma | dbeta]; part: layernorm_parts(M) * 2n scratch (GPU)."""
+    if _gpu(x):
+        _native().layernorm_bwd(x, g, int(n), gamma, mean, rstd, dx, part, dgb)
+    else:
+        ref.layernorm_bwd(x, g, n, gamma, mean, rstd, dx, dgb)

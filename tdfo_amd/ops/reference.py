@@ -447,3 +447,81 @@ def jagged_ids_to_dense(values, offsets, pad, out):
     bag, pos = _bag_positions(offsets, T)
     keep = pos < T
     out[bag[keep], pos[keep]] = values[keep]
+
+
+# ------------------------------------------------ Bert4Rec attention / LN
+_M32 = 0xFFFFFFFF
+
+
+def _hash3(a, b, c):
+    """Same counter hash as csrc/kernels/attention.hip (uint32 arithmetic in int64)."""
+    h = ((a * 0x9E3779B1) & _M32) ^ (((b + 0x7F4A7C15) * 0x85EBCA77) & _M32) ^ \
+        (((c + 0x165667B1) * 0xC2B2AE3D) & _M32)
+    h = h & _M32
+    h = h ^ (h >> 16)
+    h = (h * 0x85EBCA6B) & _M32
+    h = h ^ (h >> 13)
+    h = (h * 0xC2B2AE35) & _M32
+    h = h ^ (h >> 16)
+    return h
+
+
+def attn_keep_scale(B: int, H: int, T: int, rate: float, seed: int, step: int, device):
+    """[B, H, T, T] dropout multiplier (keep / (1 - rate) or 0) of the fused kernel."""
+    if rate <= 0:
+        return torch.ones(B, H, T, T, device=device)
+    a = (seed ^ ((step * 0x632BE5AB) & _M32)) & _M32
+    bh = torch.arange(B * H, dtype=torch.int64, device=device).view(B, H, 1, 1)
+    i = torch.arange(T, dtype=torch.int64, device=device).view(1, 1, T, 1)
+    j = torch.arange(T, dtype=torch.int64, device=device).view(1, 1, 1, T)
+    r = _hash3(torch.full((1,), a, dtype=torch.int64, device=device), bh * 64 + i, j)
+    keep = (r >> 8).to(torch.float32) * (1.0 / 16777216.0) >= rate
+    return keep.to(torch.float32) / (1.0 - rate)
+
+
+def attention_core(qkv, ids, H, rate, seed, step, pad_id):
+    """Differentiable torch reference of the fused kernel: qkv [B,T,3E] -> [B,T,E]."""
+    B, T, E3 = qkv.shape
+    E = E3 // 3
+    dk = E // H
+    q, k, v = qkv.view(B, T, 3, H, dk).permute(2, 0, 3, 1, 4)
+    s = (q / math.sqrt(dk)) @ k.transpose(-2, -1)
+    mask = (ids != pad_id).view(B, 1, 1, T)
+    s = s.masked_fill(~mask, -1e9)
+    p = torch.softmax(s, dim=-1) * attn_keep_scale(B, H, T, rate, seed, step, qkv.device)
+    return (p @ v).transpose(1, 2).reshape(B, T, E)
+
+
+def attention_fwd(qkv, ids, H, rate, seed, step, pad_id, out):
+    out.copy_(attention_core(qkv, ids, H, rate, seed, int(step[0]) if step is not None else 0,
+                             pad_id))
+
+
+def attention_bwd(qkv, ids, dout, H, rate, seed, step, pad_id, dqkv):
+    x = qkv.detach().requires_grad_(True)
+    with torch.enable_grad():
+        o = attention_core(x, ids, H, rate, seed, int(step[0]) if step is not None else 0,
+                           pad_id)
+        (g,) = torch.autograd.grad(o, x, dout)
+    dqkv.copy_(g)
+
+
+def layernorm_fwd(x, n, eps, gamma, beta, y, mean, rstd):
+    xv = x.reshape(-1, n)
+    mu = xv.mean(1)
+    var = xv.var(1, unbiased=False)
+    rs = torch.rsqrt(var + eps)
+    y.view(-1, n).copy_((xv - mu[:, None]) * rs[:, None] * gamma.view(1, n) + beta.view(1, n))
+    mean[: mu.numel()].copy_(mu)
+    rstd[: rs.numel()].copy_(rs)
+
+
+def layernorm_bwd(x, g, n, gamma, mean, rstd, dx, dgb):
+    xv, gv = x.reshape(-1, n), g.reshape(-1, n)
+    M = xv.shape[0]
+    xh = (xv - mean[:M, None]) * rstd[:M, None]
+    gg = gv * gamma.view(1, n)
+    dxv = rstd[:M, None] * (gg - gg.mean(1, keepdim=True) - xh * (gg * xh).mean(1, keepdim=True))
+    dx.view(-1, n).copy_(dxv)
+    dgb[:n].copy_((gv * xh).sum(0))
+    dgb[n:].copy_(gv.sum(0))

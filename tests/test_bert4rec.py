@@ -174,3 +174,26 @@ def test_bert4rec_distributed_matches_single(mode):
     for o in outs:
         for k, v in ref_sd.items():
             torch.testing.assert_close(o["sd"][k], v, rtol=tol, atol=tol, msg=k)
+
+
+def test_reference_attention_core_matches_model_math():
+    """CPU: the fused kernels' torch reference (hash dropout off) equals the
+    reference model's attention (masked_fill(-1e9), softmax, P.V)."""
+    import math
+
+    from tdfo_amd.ops import reference as ref
+
+    torch.manual_seed(0)
+    B, T, E, H = 4, 20, 16, 2
+    qkv = torch.randn(B, T, 3 * E)
+    ids = torch.randint(0, 9, (B, T))
+    out = torch.empty(B, T, E)
+    ref.attention_fwd(qkv, ids, H, 0.0, 1, None, 0, out)
+    dk = E // H
+    q, k, v = qkv.view(B, T, 3, H, dk).permute(2, 0, 3, 1, 4)
+    s = (q @ k.transpose(-2, -1) / math.sqrt(dk)).masked_fill((ids == 0).view(B, 1, 1, T), -1e9)
+    exp = (torch.softmax(s, -1) @ v).transpose(1, 2).reshape(B, T, E)
+    assert torch.allclose(out, exp, atol=1e-6)
+    keep = ref.attn_keep_scale(B, H, T, 0.1, 5, 3, "cpu")
+    frac = float((keep == 0).float().mean())
+    assert 0.05 < frac < 0.15                  # ~rate of the elements dropped
