@@ -94,6 +94,8 @@ class Config:
     resume: bool = False
     metrics_file: str = ""
     max_steps: int = 0
+    profile_steps: str = ""           # "START:COUNT" -> roctx profile_window (§5.1)
+    debug_checks: bool = False        # embedding id bounds checks on every lookup (§5.2)
     sharding: ShardingConfig = field(default_factory=ShardingConfig)
     synthetic: SyntheticConfig = field(default_factory=SyntheticConfig)
 

@@ -11,12 +11,24 @@ JAX all-reduces full-table gradients: jax-flax/train_dp.py:63).
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
 
 import torch
 
 from .. import ops
+
+# Debug bounds checks on every lookup (TDFO_CHECK_IDS=1 or config
+# ``debug_checks = true``): out-of-range ids raise instead of reading
+# another table's rows (or faulting the GPU).
+DEBUG_CHECKS = os.environ.get("TDFO_CHECK_IDS", "0") == "1"
+
+
+def set_debug_checks(on: bool) -> None:
+    global DEBUG_CHECKS
+    DEBUG_CHECKS = bool(on)
+
 
 EMB_OPTIMIZERS = {
     "sgd": ops.EMB_SGD,
@@ -114,9 +126,31 @@ class TableBatchedEmbedding:
         self.key_bits = ops.key_bits_for(self.total_rows)
 
     # ------------------------------------------------------------------
+    def check_ids(self, indices, offsets, row_offset, T, B):
+        """Debug bounds check: every id of virtual table v must be
+        in [0, rows of the table whose rows start at row_offset[v]). Host sync;
+        skipped during hipGraph capture. Raises IndexError naming the table."""
+        if indices.numel() == 0 or (indices.is_cuda and torch.cuda.is_current_stream_capturing()):
+            return
+        starts = torch.tensor(self.row_offset_host, dtype=torch.int64, device=indices.device)
+        counts = torch.tensor(self.row_counts, dtype=torch.int64, device=indices.device)
+        ro = row_offset.to(indices.device).view(-1)[:T]
+        tab = torch.searchsorted(starts, ro, right=True) - 1          # virtual -> physical
+        bag = torch.searchsorted(offsets[: T * B + 1], torch.arange(
+            indices.numel(), device=indices.device), right=True) - 1
+        v = torch.clamp(bag // B, 0, T - 1)
+        lim = counts[tab[v]]
+        bad = (indices < 0) | (indices >= lim)
+        if bool(bad.any()):
+            p = int(bad.nonzero()[0, 0])
+            raise IndexError(f"embedding id {int(indices[p])} out of range for table "
+                             f"{int(tab[v[p]])} ({int(lim[p])} rows) at position {p}")
+
     def forward(self, indices, offsets, row_offset, T, B, out, out_off, out_stride, mean=False,
                 psw=None):
         """Pooled lookup over ``T`` (virtual) tables of ``B`` bags each."""
+        if DEBUG_CHECKS:
+            self.check_ids(indices, offsets, row_offset, T, B)
         ops.embedding_bag_fwd(self.weight, row_offset, indices, offsets, out_off, T, B, out,
                               out_stride, mean=mean, psw=psw)
 

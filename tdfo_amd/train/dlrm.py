@@ -32,7 +32,9 @@ from ..data.synthetic import HostSyntheticCriteo, SyntheticCriteo
 from ..models.dlrm import (CRITEO_1TB_ROWS, CRITEO_KAGGLE_ROWS, MLPERF_MULTIHOT, DLRMConfig,
                            DLRMTrainer)
 from ..parallel.dist import init_distributed
+from ..sparse import tables as _tables
 from ..utils import checkpoint as ckpt
+from ..utils.profiling import ProfileWindow, StepTimer, trace_range
 
 TINY_ROWS = [40_000] * 26          # DLRM-tiny: ~1M embedding rows (BASELINE config 1)
 
@@ -96,6 +98,8 @@ def run(cfg: Config, mode: str = "single", out_dir: str = ".",
         device = "cuda" if torch.cuda.is_available() else "cpu"
     info = init_distributed(device)
     rank, world, dev, group = info.rank, info.world_size, info.device, info.group
+    if cfg.debug_checks:
+        _tables.set_debug_checks(True)
     if mode == "single" and world > 1:
         raise ValueError("train.py is single-process; use train_dp.py / train_ps.py for >1 rank")
     if mode == "dp":
@@ -132,12 +136,20 @@ def run(cfg: Config, mode: str = "single", out_dir: str = ".",
     t0 = time.perf_counter()
     last_t, last_step = t0, start
     step = start
+    prof = ProfileWindow(cfg.profile_steps or None)
+    timer = StepTimer(enabled=dev.type == "cuda")
     while step < total_steps:
-        dense, ids, label = data.next()
-        tr.load_batch(dense.to(dev, non_blocking=True), ids.to(dev, non_blocking=True),
-                      label.to(dev, non_blocking=True))
-        tr.step()
+        prof.before_step(step)
+        with trace_range("load_batch"):
+            dense, ids, label = data.next()
+            tr.load_batch(dense.to(dev, non_blocking=True), ids.to(dev, non_blocking=True),
+                          label.to(dev, non_blocking=True))
+        timer.start()
+        with trace_range("train_step"):
+            tr.step()
+        timer.stop()
         step += 1
+        prof.after_step(step)
         if use_graph and tr.graph is None and step - start == 2:
             tr.capture_graph(warmup=0)
         if fault_at and step == fault_at and rank == fault_rank:
@@ -156,8 +168,12 @@ def run(cfg: Config, mode: str = "single", out_dir: str = ".",
             now = time.perf_counter()
             ex_s = n * B * world / max(now - last_t, 1e-9)
             rec = {"step": step, "train_loss": loss, "examples_per_sec": ex_s}
+            dev_ms = timer.mean_ms()
+            if dev_ms is not None:
+                rec["device_ms_per_step"] = dev_ms
             if cfg.eval_every and (step % cfg.eval_every == 0 or step == total_steps):
-                rec.update(evaluate(tr, cfg, dcfg, B, dev, rank, world, group))
+                with trace_range("eval"):
+                    rec.update(evaluate(tr, cfg, dcfg, B, dev, rank, world, group))
             _log(rank, "step {step} train loss: {train_loss:.4f}, {examples_per_sec:,.0f} ex/s"
                  .format(**rec) + (f", eval loss: {rec['eval_loss']:.4f}, "
                                    f"eval auc: {rec['eval_auc']:.4f}" if "eval_auc" in rec else ""))
@@ -167,7 +183,8 @@ def run(cfg: Config, mode: str = "single", out_dir: str = ".",
                     f.write(json.dumps(rec) + "\n")
             last_t, last_step = time.perf_counter(), step
         if cfg.ckpt_dir and cfg.ckpt_every and step % cfg.ckpt_every == 0:
-            save(tr, cfg.ckpt_dir, step, rank, world, meta)
+            with trace_range("checkpoint"):
+                save(tr, cfg.ckpt_dir, step, rank, world, meta)
     if cfg.ckpt_dir:
         save(tr, cfg.ckpt_dir, step, rank, world, meta)
     return {"history": history, "steps": step, "trainer": tr}

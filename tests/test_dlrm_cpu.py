@@ -82,3 +82,40 @@ def test_auc_helpers():
     yy = (torch.rand(5000) < torch.sigmoid(2 * logits)).float()
     ref.auc_hist(logits, yy, 1000, h)
     assert abs(ref.hist_auc(h) - ref.exact_auc(logits, yy)) < 2e-3
+
+
+def test_debug_id_bounds_check_raises():
+    """§5.2: with debug checks on, an out-of-range id raises before the lookup."""
+    import pytest
+
+    from tdfo_amd.sparse import tables as T
+    from tdfo_amd.sparse.tables import EmbOptimConfig, TableBatchedEmbedding
+
+    st = TableBatchedEmbedding([10, 20], 8, "cpu", EmbOptimConfig("sgd"))
+    B = 2
+    ids = torch.tensor([3, 9, 19, 0])             # table0: 3, 9 ; table1: 19, 0
+    offs = torch.arange(5)
+    out = torch.zeros(B, 16)
+    oo = torch.tensor([0, 8])
+    T.set_debug_checks(True)
+    try:
+        st.forward(ids, offs, st.row_offset, 2, B, out, oo, 16)       # in range: fine
+        bad = torch.tensor([3, 10, 19, 0])        # 10 >= 10 rows of table 0
+        with pytest.raises(IndexError):
+            st.forward(bad, offs, st.row_offset, 2, B, out, oo, 16)
+    finally:
+        T.set_debug_checks(False)
+
+
+def test_profiling_helpers_cpu():
+    from tdfo_amd.utils.profiling import ProfileWindow, StepTimer, parse_window, trace_range
+
+    assert parse_window("5:3") == (5, 3) and parse_window("") is None
+    with trace_range("x"):
+        pass
+    t = StepTimer(enabled=False)
+    t.start(); t.stop()
+    assert t.mean_ms() is None
+    w = ProfileWindow("1:2")
+    for s in range(4):
+        w.before_step(s); w.after_step(s + 1)
