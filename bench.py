@@ -39,7 +39,7 @@ def parse(argv=None):
     ap.add_argument("--pool", type=int, default=8, help="pre-generated device batches")
     ap.add_argument("--dist", default="uniform", choices=["uniform", "zipf"])
     ap.add_argument("--sharding", default="auto",
-                    choices=["auto", "table_wise", "row_wise", "data_parallel"])
+                    choices=["auto", "table_wise", "row_wise", "column_wise", "data_parallel"])
     return ap.parse_args(argv)
 
 

@@ -19,4 +19,5 @@ run() {
 run tw1tb --steps 5 --warmup 2 --batch 4096 &&
 run kaggle_auto --rows kaggle --steps 5 --warmup 2 --batch 4096 &&
 run dcn_rw --model dcnv2 --rows kaggle --sharding row_wise --steps 3 --warmup 1 --batch 2048 &&
-run dp_tables --rows tiny --sharding data_parallel --steps 3 --warmup 1 --batch 2048
+run dp_tables --rows tiny --sharding data_parallel --steps 3 --warmup 1 --batch 2048 &&
+run cw_kaggle --rows kaggle --sharding column_wise --steps 3 --warmup 1 --batch 2048

@@ -102,10 +102,10 @@ def plan_sharding(tables: Sequence[TableConfig], world_size: int, optim: EmbOpti
 
     def column_wise(t: int):
         d = tables[t].embedding_dim
-        nb = min(W, max(1, d // 32))
-        base = (d // nb) // 8 * 8
-        cols = [base] * nb
-        cols[-1] += d - base * nb
+        nb = min(W, max(2, d // 32))
+        while nb > 1 and (d % nb or (d // nb) % 8):      # equal blocks, 8-col aligned
+            nb -= 1
+        cols = [d // nb] * nb
         ranks = sorted(range(W), key=lambda r: (cost[r], mem[r], r))[:nb]
         for i, r in enumerate(ranks):
             mem[r] += tables[t].num_embeddings * 4 * (cols[i] + optim.state_floats_per_row(cols[i]))

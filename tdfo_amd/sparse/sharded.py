@@ -23,6 +23,11 @@ Design (MI355X-first):
     pooled at the requester by the same embedding kernel (the received rows
     act as a table); gradients travel back per id and the owner's fused
     sort-based backward merges duplicates across requesters.
+  * column-wise (CW) shards: block k of a table (columns [c0, c0 + Dc)) is
+    looked up by its rank exactly like a table-wise shard of width Dc, its
+    ids travel in a second id all-to-all, its pooled pieces ride in the same
+    pooled all-to-all, and the receiver assembles each CW feature's D-wide
+    row from the pieces (strided copies; the reverse for gradients).
   * bf16 on the wire for embeddings/gradients, fp32 in HBM tables.
 """
 from __future__ import annotations
@@ -69,7 +74,7 @@ class ShardedEmbeddingBags:
         self.mean = mean
         self.optim = optim
         for s in plan.shards:
-            if s.kind not in ("table_wise", "row_wise", "data_parallel"):
+            if s.kind not in ("table_wise", "row_wise", "data_parallel", "column_wise"):
                 raise NotImplementedError(f"sharding kind {s.kind} not supported for pooled bags")
         # ---- id layout in the input (original order)
         self.in_base = [0] * self.T
@@ -78,12 +83,30 @@ class ShardedEmbeddingBags:
             self.in_base[t] = acc
             acc += B * self.L[t]
         self.nnz_local = acc
+        # ---- column-wise blocks: block k of table t = columns [c0, c0 + Dc) on
+        # its own rank, looked up like a table-wise shard of width Dc; the
+        # consumer's D-wide rows are assembled after the pooled all-to-all
+        self.cw_tables = [s.table for s in plan.shards if s.kind == "column_wise"]
+        self.cw_blocks = {}
+        for s in plan.shards:
+            if s.kind == "column_wise":
+                c0, lst = 0, []
+                for r, w in zip(s.ranks, s.col_blocks):
+                    lst.append((r, c0, w))
+                    c0 += w
+                assert c0 == D and len({r for r, _, _ in lst}) == len(lst), "bad column blocks"
+                self.cw_blocks[s.table] = lst
+        widths = {w for lst in self.cw_blocks.values() for (_, _, w) in lst}
+        assert len(widths) <= 1, "column-wise blocks must share one width"
+        self.Dc = Dc = widths.pop() if widths else 0
+        self.cw_owned = [[(t, c0) for t in self.cw_tables for (r, c0, _) in self.cw_blocks[t]
+                          if r == rr] for rr in range(W)]
         # ---- table-wise group
         self.tw_tables = [[s.table for s in plan.shards if s.kind == "table_wise" and s.ranks[0] == r]
                           for r in range(W)]
         mine = self.tw_tables[rank]
         self.tw_mine = mine
-        self.dsum = [len(ts) * D for ts in self.tw_tables]
+        self.dsum = [len(ts) * D + len(self.cw_owned[r]) * Dc for r, ts in enumerate(self.tw_tables)]
         self.tw_store = TableBatchedEmbedding([self.tables[t].num_embeddings for t in mine], D,
                                               device, optim,
                                               init_ranges=[self.tables[t].init_range or
@@ -123,6 +146,34 @@ class ShardedEmbeddingBags:
         self.tw_recv_sizes = [B * self.dsum[r] for r in range(W)]
         self.tw_recv_base = [sum(self.tw_recv_sizes[:r]) for r in range(W)]
         tw_total = sum(self.tw_recv_sizes)
+        if self.cw_tables:
+            cmine = self.cw_owned[rank]
+            self.cw_store = TableBatchedEmbedding(
+                [self.tables[t].num_embeddings for t, _ in cmine], Dc, device, optim,
+                init_ranges=[self.tables[t].init_range or (1.0 / self.tables[t].num_embeddings) ** 0.5
+                             for t, _ in cmine], seed=seed * 1000 + 300 + rank)
+            corder = [t for r in range(W) for t, _ in self.cw_owned[r]]
+            self.cw_send_counts = [sum(B * self.L[t] for t, _ in self.cw_owned[r]) for r in range(W)]
+            self.cw_recv_count = sum(B * self.L[t] for t, _ in cmine)
+            self.cw_perm = torch.cat([torch.arange(self.in_base[t], self.in_base[t] + B * self.L[t])
+                                      for t in corder]).to(self.device)
+            self.cw_send_ids = torch.empty(sum(self.cw_send_counts), dtype=torch.int64,
+                                           device=self.device)
+            self.cw_recv_ids = torch.empty(W * self.cw_recv_count, dtype=torch.int64,
+                                           device=self.device)
+            lens, ro, oo = [], [], []
+            for s_ in range(W):
+                for k, (t, _) in enumerate(cmine):
+                    lens += [self.L[t]] * B
+                    ro.append(self.cw_store.row_offset_host[k])
+                    oo.append(s_ * B * self.dsum[rank] + len(mine) * D + k * Dc)
+            self.cw_nv = W * len(cmine)
+            co = torch.zeros(len(lens) + 1, dtype=torch.int64)
+            if lens:
+                co[1:] = torch.cumsum(torch.tensor(lens, dtype=torch.int64), 0)
+            self.cw_v_offsets = co.to(self.device)
+            self.cw_v_row_off = torch.tensor(ro, dtype=torch.int64, device=self.device)
+            self.cw_v_out_off = torch.tensor(oo, dtype=torch.int64, device=self.device)
         # ---- row-wise group (dynamic splits)
         self.rw_tables = [s.table for s in plan.shards if s.kind == "row_wise"]
         self.rw_col = {t: j * D for j, t in enumerate(self.rw_tables)}
@@ -199,7 +250,9 @@ class ShardedEmbeddingBags:
                     base += n_t
                 self.dp_g_perm = torch.cat(src).to(self.device)
                 self.dp_g_ids_t = torch.zeros_like(self.dp_g_ids)
-        self.recv = torch.zeros(self.dp_base + B * self.dp_width, dtype=bf, device=self.device)
+        self.cw_base = self.dp_base + B * self.dp_width
+        self.cw_width = len(self.cw_tables) * D
+        self.recv = torch.zeros(self.cw_base + B * self.cw_width, dtype=bf, device=self.device)
         self.d_recv = torch.zeros_like(self.recv)
         self.d_pooled = torch.empty_like(self.tw_pooled)
         # ---- consumer slot map (per feature/table)
@@ -215,6 +268,16 @@ class ShardedEmbeddingBags:
         for j, t in enumerate(self.dp_tables):
             self.slot_off[t] = self.dp_base + j * D
             self.slot_stride[t] = self.dp_width
+        # CW pieces: (src offset in the pooled a2a region, stride) -> (dst in
+        # the assembled CW region, stride), B x Dc elements each
+        self.cw_pieces = []
+        for j, t in enumerate(self.cw_tables):
+            self.slot_off[t] = self.cw_base + j * D
+            self.slot_stride[t] = self.cw_width
+            for (r, c0, w) in self.cw_blocks[t]:
+                k = self.cw_owned[r].index((t, c0))
+                src = self.tw_recv_base[r] + len(self.tw_tables[r]) * D + k * Dc
+                self.cw_pieces.append((src, self.dsum[r], self.cw_base + j * D + c0, self.cw_width))
         self._pending = None
         self._rw_state = None
 
@@ -241,7 +304,24 @@ class ShardedEmbeddingBags:
         return not self.rw_tables
 
     # -- stages (compute stages are hipGraph-capturable; exchanges are RCCL)
+    def _cw_views(self, buf):
+        B, Dc = self.B, self.Dc
+        for src, sst, dst, dstr in self.cw_pieces:
+            yield (buf.as_strided((B, Dc), (sst, 1), src), buf.as_strided((B, Dc), (dstr, 1), dst))
+
+    def _cw_assemble(self, buf):
+        for a, b in self._cw_views(buf):
+            b.copy_(a)
+
+    def _cw_disassemble(self, buf):
+        for a, b in self._cw_views(buf):
+            a.copy_(b)
+
     def stage_fwd_prep(self, ids: torch.Tensor):
+        if self.cw_tables:
+            torch.index_select(ids, 0, self.cw_perm, out=self.cw_send_ids)
+            if self.world == 1:
+                self.cw_recv_ids = self.cw_send_ids
         if self.dp_tables:
             torch.index_select(ids, 0, self.dp_in_idx, out=self.dp_ids)
         if self.tw_identity:
@@ -259,6 +339,9 @@ class ShardedEmbeddingBags:
         if W > 1 and not self.tw_identity:
             _a2a(self.tw_recv_ids, self.tw_send_ids, [self.tw_recv_count] * W,
                  self.tw_send_counts, self.group)
+        if W > 1 and self.cw_tables:
+            _a2a(self.cw_recv_ids, self.cw_send_ids, [self.cw_recv_count] * W,
+                 self.cw_send_counts, self.group)
 
     def stage_fwd_lookup(self):
         W, B = self.world, self.B
@@ -272,6 +355,10 @@ class ShardedEmbeddingBags:
             self.tw_store.forward(self.tw_recv_ids, self.tw_v_offsets, self.tw_v_row_off, self.tw_nv,
                                   B, self.tw_pooled if W > 1 else self.recv, self.tw_v_out_off,
                                   self.dsum[self.rank], mean=self.mean)
+        if self.cw_tables and self.cw_nv:
+            self.cw_store.forward(self.cw_recv_ids, self.cw_v_offsets, self.cw_v_row_off,
+                                  self.cw_nv, B, self.tw_pooled if W > 1 else self.recv,
+                                  self.cw_v_out_off, self.dsum[self.rank], mean=self.mean)
 
     def stage_fwd_out_exchange(self):
         W, B = self.world, self.B
@@ -287,6 +374,8 @@ class ShardedEmbeddingBags:
         if self._pending is not None:
             self._pending.wait()
             self._pending = None
+        if self.cw_tables:
+            self._cw_assemble(self.recv)
 
     # row-wise: dynamic splits
     def _rw_forward(self, ids: torch.Tensor):
@@ -342,6 +431,8 @@ class ShardedEmbeddingBags:
         d_recv = self.d_recv if d_recv is None else d_recv
         W, B = self.world, self.B
         tw_total = sum(self.tw_recv_sizes)
+        if self.cw_tables:
+            self._cw_disassemble(d_recv)
         work = None
         if W > 1:
             work = _a2a(self.d_pooled[: W * B * self.dsum[self.rank]], d_recv[:tw_total],
@@ -371,6 +462,10 @@ class ShardedEmbeddingBags:
         if self.tw_nv:
             self.tw_store.backward_update(self.tw_recv_ids, self.tw_v_offsets, self.tw_v_row_off,
                                           self.tw_nv, B, grad, self.tw_v_out_off,
+                                          self.dsum[self.rank], hyper, mean=self.mean)
+        if self.cw_tables and self.cw_nv:
+            self.cw_store.backward_update(self.cw_recv_ids, self.cw_v_offsets, self.cw_v_row_off,
+                                          self.cw_nv, B, grad, self.cw_v_out_off,
                                           self.dsum[self.rank], hyper, mean=self.mean)
         if self.dp_tables:
             ndp = len(self.dp_tables)
@@ -419,8 +514,24 @@ class ShardedEmbeddingBags:
         del nrw
 
     # -------------------------------------------------------------- state
+    def table_cols(self, t: int):
+        """(col_start, width) of this rank's column block of table t (D-wide
+        for every non-column-wise table held here), or None."""
+        if t in self.cw_blocks:
+            for r, c0, w in self.cw_blocks[t]:
+                if r == self.rank:
+                    return c0, w
+            return None
+        return (0, self.D) if self._local_slices(t) is not None else None
+
     def _local_slices(self, t: int):
         """(store, local_table_index, row_start, row_stop) of table t here, or None."""
+        if t in self.cw_blocks:
+            cols = [c0 for (r, c0, _) in self.cw_blocks[t] if r == self.rank]
+            if not cols:
+                return None
+            k = self.cw_owned[self.rank].index((t, cols[0]))
+            return self.cw_store, k, 0, self.tables[t].num_embeddings
         if t in self.tw_mine:
             return self.tw_store, self.tw_mine.index(t), 0, self.tables[t].num_embeddings
         if t in self.dp_tables:
@@ -439,7 +550,8 @@ class ShardedEmbeddingBags:
         sl = self._local_slices(t)
         if sl is not None and sl[3] > sl[2]:
             store, i, lo, hi = sl
-            store.table_weight(i)[: hi - lo].copy_(full[lo:hi].to(store.weight.device))
+            c0, w = self.table_cols(t)
+            store.table_weight(i)[: hi - lo].copy_(full[lo:hi, c0:c0 + w].to(store.weight.device))
 
     def get_table_weight(self, t: int):
         """This rank's (row_start, rows view) of table ``t``, or None."""
@@ -451,6 +563,8 @@ class ShardedEmbeddingBags:
 
     def state_dict(self):
         d = {"tw": self.tw_store.state_dict()}
+        if self.cw_tables:
+            d["cw"] = self.cw_store.state_dict()
         if self.rw_tables:
             d["rw"] = self.rw_store.state_dict()
         if self.dp_tables:
@@ -459,6 +573,8 @@ class ShardedEmbeddingBags:
 
     def load_state_dict(self, d):
         self.tw_store.load_state_dict(d["tw"])
+        if self.cw_tables:
+            self.cw_store.load_state_dict(d["cw"])
         if self.rw_tables:
             self.rw_store.load_state_dict(d["rw"])
         if self.dp_tables:

@@ -57,12 +57,13 @@ def _emb_worker(rank, world, strategy, B, L):
     for t in range(len(ROWS)):
         r = emb.get_table_weight(t)
         if r is not None:
-            shards[t] = (r[0], r[1].clone())
+            shards[t] = (r[0], emb.table_cols(t)[0], r[1].clone())
     return feats, d_recv, shards, [list(emb.slot_off), list(emb.slot_stride)]
 
 
 @pytest.mark.parametrize("strategy,world", [("table_wise", 2), ("row_wise", 2), ("data_parallel", 2),
-                                            ("table_wise", 3), ("row_wise", 3)])
+                                            ("column_wise", 2), ("table_wise", 3), ("row_wise", 3),
+                                            ("column_wise", 3)])
 def test_sharded_embedding_fwd_bwd(strategy, world):
     B, L = 6, [1, 2, 1, 3, 1]
     res = run_distributed(_emb_worker, world, strategy, B, L)
@@ -88,17 +89,19 @@ def test_sharded_embedding_fwd_bwd(strategy, world):
                 for i in ids[b]:
                     new[t][i] -= 0.5 * gb[b]
     for rank in range(world):
-        for t, (lo, w) in res[rank][2].items():
-            assert torch.allclose(w, new[t][lo:lo + w.shape[0]], atol=1e-2), (rank, t)
+        for t, (lo, c0, w) in res[rank][2].items():
+            exp = new[t][lo:lo + w.shape[0], c0:c0 + w.shape[1]]
+            assert torch.allclose(w, exp, atol=1e-2), (rank, t)
 
 
-def _dlrm_worker(rank, world, B, steps, strategy):
+def _dlrm_worker(rank, world, B, steps, strategy, emb_opt="rowwise_adagrad"):
     from tdfo_amd.data.synthetic import SyntheticCriteo
     from tdfo_amd.models.dlrm import DLRMConfig, DLRMTrainer
     from tdfo_amd.parallel.dist import get_info
 
     cfg = DLRMConfig(embedding_dim=32, table_rows=ROWS, bottom=[64, 32], top=[64, 32, 1],
-                     dense_lr=1e-2, emb_lr=0.05, sharding=strategy, pooling=[1, 2, 1, 1, 1])
+                     dense_lr=1e-2, emb_lr=0.05, sharding=strategy, pooling=[1, 2, 1, 1, 1],
+                     emb_opt=emb_opt)
     tr = DLRMTrainer(cfg, B, "cpu", group=get_info().group, rank=rank, world_size=world)
     g = torch.Generator().manual_seed(5)
     for t, r in enumerate(ROWS):
@@ -119,19 +122,22 @@ def _dlrm_worker(rank, world, B, steps, strategy):
     for t in range(len(ROWS)):
         r = tr.emb.get_table_weight(t)
         if r is not None:
-            tabs[t] = (r[0], r[1].clone())
+            tabs[t] = (r[0], tr.emb.table_cols(t)[0], r[1].clone())
     return tr.fp.p.clone(), tabs
 
 
-@pytest.mark.parametrize("strategy", ["table_wise", "row_wise", "data_parallel"])
+@pytest.mark.parametrize("strategy", ["table_wise", "row_wise", "data_parallel", "column_wise"])
 def test_dlrm_data_parallel_matches_single_process(strategy):
     B, steps = 8, 3
-    multi = run_distributed(_dlrm_worker, 2, B, steps, strategy)
-    single = run_distributed(_dlrm_worker, 1, 2 * B, steps, "table_wise")[0]
+    # row-wise Adagrad keeps one state per row *per column block* under CW
+    # (as TorchRec CW shards do), so CW is checked with elementwise Adagrad
+    opt = "adagrad" if strategy == "column_wise" else "rowwise_adagrad"
+    multi = run_distributed(_dlrm_worker, 2, B, steps, strategy, opt)
+    single = run_distributed(_dlrm_worker, 1, 2 * B, steps, "table_wise", opt)[0]
     p1, tabs1 = single
     for rank in range(2):
         p, tabs = multi[rank]
         assert torch.allclose(p, p1, atol=2e-4), (rank, (p - p1).abs().max())
-        for t, (lo, w) in tabs.items():
-            ref = tabs1[t][1][lo:lo + w.shape[0]]
+        for t, (lo, c0, w) in tabs.items():
+            ref = tabs1[t][2][lo:lo + w.shape[0], c0:c0 + w.shape[1]]
             assert torch.allclose(w, ref, atol=2e-4), (rank, t, (w - ref).abs().max())
