@@ -456,6 +456,23 @@ void head_bce(const Tensor& H, const Tensor& w, const Tensor& b, const Tensor& l
                  bf16_mut(dH), dH.stride(0), part.data_ptr<float>(), nparts, cur_stream());
 }
 
+void head_reduce(const Tensor& part, int64_t nparts, int64_t K, const Tensor& grad,
+                 const Tensor& loss_acc, at::TensorList bumps) {
+  check_f32c(part, "part"); check_f32c(grad, "grad"); check_f32c(loss_acc, "loss_acc");
+  TORCH_CHECK(part.numel() >= nparts * (K + 2) && grad.numel() >= K + 1 && loss_acc.numel() >= 1,
+              "head_reduce: shapes");
+  TORCH_CHECK(bumps.size() <= 4, "head_reduce: at most 4 step counters");
+  tdfo::HeadBumps hb{};
+  hb.n = (int)bumps.size();
+  for (size_t i = 0; i < bumps.size(); ++i) {
+    check_f32c(bumps[i], "bump");
+    TORCH_CHECK(bumps[i].numel() >= 2, "head_reduce: counters are [lr, step, ...]");
+    hb.p[i] = bumps[i].data_ptr<float>();
+  }
+  tdfo::head_reduce(part.data_ptr<float>(), (int)nparts, (int)K, grad.data_ptr<float>(),
+                    loss_acc.data_ptr<float>(), hb, cur_stream());
+}
+
 void reduce_rows(const Tensor& inp, int64_t rows, int64_t n, int64_t ld, const Tensor& out,
                  bool accumulate, double scale) {
   check_dev(inp, "inp");
@@ -638,6 +655,8 @@ TORCH_LIBRARY(tdfo, m) {
   m.def("cast_bf16(Tensor x, Tensor(a!) y) -> ()");
   m.def("head_bce(Tensor H, Tensor w, Tensor b, Tensor label, float inv_n, bool relu_mask, "
         "Tensor(a!) logits, Tensor(b!) dH, Tensor(c!) part) -> ()");
+  m.def("head_reduce(Tensor part, int nparts, int K, Tensor(a!) grad, Tensor(b!) loss_acc, "
+        "Tensor(c!)[] bumps) -> ()");
   m.def("reduce_rows(Tensor inp, int rows, int n, int ld, Tensor(a!) out, bool accumulate, float scale) -> ()");
   m.def("colsum(Tensor x, Tensor(a!) out, bool accumulate) -> ()");
   m.def("auc_hist(Tensor logits, Tensor labels, int nb, Tensor(a!) hist) -> ()");
@@ -669,6 +688,7 @@ TORCH_LIBRARY_IMPL(tdfo, CUDA, m) {
   m.impl("cast_bf16", cast_bf16);
   m.impl("head_bce", head_bce);
   m.impl("reduce_rows", reduce_rows);
+  m.impl("head_reduce", head_reduce);
   m.impl("colsum", colsum);
   m.impl("auc_hist", auc_hist);
   m.impl("two_tower", two_tower);

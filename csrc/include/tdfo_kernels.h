@@ -147,6 +147,11 @@ void head_bce(const uint16_t* H, int64_t ldh, int B, int K, const float* w,
               float* logits, uint16_t* dH, int64_t lddh, float* part,
               int nparts, hipStream_t s);
 int head_bce_parts(int B);
+// grad[0..K] = sum over parts of part[:, 0..K]; loss_acc[0] += sum part[:, K+1];
+// bump.p[i][1] += 1 for each step counter (fp32 [lr, step, ...] hyper vectors).
+struct HeadBumps { float* p[4]; int n; };
+void head_reduce(const float* part, int nparts, int K, float* grad, float* loss_acc,
+                 const HeadBumps& bumps, hipStream_t s);
 // out[j] (=|+=) sum_r in[r*ld + j], j < n, fixed order (deterministic).
 void reduce_rows(const float* in, int rows, int64_t n, int64_t ld, float* out,
                  int accumulate, float scale, hipStream_t s);

@@ -110,6 +110,44 @@ __global__ __launch_bounds__(256) void reduce_rows_kernel(
   }
 }
 
+// Head epilogue in one launch: grad[j] = sum_r part[r][j] (j <= K) and
+// loss_acc[0] += sum_r part[r][K+1] with reduce_rows' fixed-order structure
+// (16 columns x 16 row phases per block), plus the step counters
+// bump[i][1] += 1 of the optimizers that run later in the step (saves two
+// reduce launches and two counter-increment launches).
+__global__ __launch_bounds__(256) void head_reduce_kernel(const float* __restrict__ part,
+                                                          int nparts, int K,
+                                                          float* __restrict__ grad,
+                                                          float* __restrict__ loss_acc,
+                                                          HeadBumps bumps) {
+  constexpr int COLS = 16, PH = 256 / COLS;
+  __shared__ float red[PH][COLS];
+  const int ld = K + 2;
+  const int c = threadIdx.x % COLS, ph = threadIdx.x / COLS;
+  const int j = blockIdx.x * COLS + c;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (j < ld) {
+    int r = ph;
+    for (; r + 3 * PH < nparts; r += 4 * PH) {
+      s0 += part[(int64_t)r * ld + j];
+      s1 += part[(int64_t)(r + PH) * ld + j];
+      s2 += part[(int64_t)(r + 2 * PH) * ld + j];
+      s3 += part[(int64_t)(r + 3 * PH) * ld + j];
+    }
+    for (; r < nparts; r += PH) s0 += part[(int64_t)r * ld + j];
+  }
+  red[ph][c] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (ph == 0 && j < ld) {
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < PH; ++q) t += red[q][c];
+    if (j <= K) grad[j] = t;
+    else loss_acc[0] += t;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < bumps.n) bumps.p[threadIdx.x][1] += 1.f;
+}
+
 constexpr int COLSUM_CHUNKS = 16;
 
 // Column sums of a bf16 [M, N] matrix: block = 64 columns (8 x 16-B groups)
@@ -204,6 +242,13 @@ void reduce_rows(const float* in, int rows, int64_t n, int64_t ld, float* out,
 }
 
 int colsum_parts(int M) { return COLSUM_CHUNKS; }
+
+void head_reduce(const float* part, int nparts, int K, float* grad, float* loss_acc,
+                 const HeadBumps& bumps, hipStream_t s) {
+  hipLaunchKernelGGL(head_reduce_kernel, dim3((K + 2 + 15) / 16), dim3(256), 0, s, part, nparts,
+                     K, grad, loss_acc, bumps);
+  TDFO_CHECK_HIP(hipGetLastError());
+}
 
 void colsum_bf16(const uint16_t* x, int M, int N, int64_t ldx, float* part,
                  int nparts, float* out, int accumulate, hipStream_t s) {

@@ -400,9 +400,10 @@ class DLRMTrainer:
         head = fp.param("head")
         ops.head_bce(self.t_out, head[:K], head[K:], self.label, 1.0 / (B * self.world), True,
                      self.logits, self.top_grad[-1], self.head_part)
-        ops.reduce_rows(self.head_part, self.nparts, K + 1, K + 2, fp.grad("head"))
-        ops.reduce_rows(self.head_part[K + 1:], self.nparts, 1, K + 2, self.loss_sum,
-                        accumulate=True)
+        # head grad + loss accumulation + this step's optimizer step counters
+        # (read later in the step by the embedding and dense updates): one launch
+        ops.head_reduce(self.head_part, self.nparts, K, fp.grad("head"), self.loss_sum,
+                        (self.dense_hyper, self.emb_hyper))
         for i in reversed(range(n)):
             L = self.top_layers[i]
             if i > 0:
@@ -431,7 +432,6 @@ class DLRMTrainer:
             self._ar_work = dist.all_reduce(self.fp.g, group=self.group, async_op=True)
 
     def _s_emb_update(self):
-        self.emb_hyper[1:2].add_(1.0)
         self.emb.stage_bwd_update(self.emb_hyper)
 
     def _m_allreduce_wait(self):
@@ -444,7 +444,6 @@ class DLRMTrainer:
     def _s_dense_update(self):
         self._join(self._es)
         fp = self.fp
-        self.dense_hyper[1:2].add_(1.0)
         ops.dense_optimizer(fp.p, fp.g, fp.m, fp.v, fp.p_bf16, self.dense_opt, self.dense_hyper,
                             wd=self.cfg.dense_wd)
 

@@ -150,6 +150,15 @@ def reduce_rows(inp, rows, n, ld, out, accumulate=False, scale=1.0):
         ref.reduce_rows(inp, rows, n, ld, out, accumulate, scale)
 
 
+def head_reduce(part, nparts, K, grad, loss_acc, bumps=()):
+    """grad[:K+1] = column sums of part[:, :K+1]; loss_acc += sum part[:, K+1];
+    bump[1] += 1 for each step-counter vector in ``bumps`` (one launch)."""
+    if _gpu(part):
+        _native().head_reduce(part, int(nparts), int(K), grad, loss_acc, list(bumps))
+    else:
+        ref.head_reduce(part, nparts, K, grad, loss_acc, bumps)
+
+
 def colsum(x, out, accumulate=False):
     if _gpu(x):
         _native().colsum(x, out, accumulate)

@@ -250,6 +250,14 @@ def reduce_rows(inp, rows, n, ld, out, accumulate, scale):
         o.copy_(s)
 
 
+def head_reduce(part, nparts, K, grad, loss_acc, bumps=()):
+    p = part[: nparts * (K + 2)].view(nparts, K + 2)
+    grad[: K + 1].copy_(p[:, : K + 1].sum(0))
+    loss_acc[:1] += p[:, K + 1].sum()
+    for b in bumps:
+        b[1:2] += 1.0
+
+
 def colsum(x, out, accumulate):
     s = _f(x).sum(0)
     if accumulate:

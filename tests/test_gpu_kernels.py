@@ -522,3 +522,18 @@ def test_jagged_dense_roundtrip(D):
     ri = torch.empty(37, T, dtype=torch.int64)
     ref.jagged_ids_to_dense(ids, off, 0, ri)
     assert torch.equal(oi.cpu(), ri)
+
+
+def test_head_reduce_and_step_bumps():
+    torch.manual_seed(11)
+    nparts, K = 37, 256
+    part = torch.randn(nparts * (K + 2), device=DEV)
+    grad = torch.empty(K + 1, device=DEV)
+    loss = torch.tensor([1.5], device=DEV)
+    h1 = torch.tensor([0.1, 4.0, 1.0], device=DEV)
+    h2 = torch.tensor([0.2, 9.0], device=DEV)
+    ops.head_reduce(part, nparts, K, grad, loss, (h1, h2))
+    p = part.view(nparts, K + 2).double()
+    assert torch.allclose(grad.double(), p[:, : K + 1].sum(0), atol=1e-4)
+    assert abs(float(loss) - (1.5 + float(p[:, K + 1].sum()))) < 1e-3
+    assert float(h1[1]) == 5.0 and float(h2[1]) == 10.0 and float(h1[0]) == pytest.approx(0.1)
