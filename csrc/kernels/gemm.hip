@@ -150,8 +150,8 @@ __device__ __forceinline__ bf16x8_t frag_col(const TDFO_LDS char* tile, int c0,
 // traffic leaves as coalesced 16-B accesses (mask loads, bf16 stores, fp32
 // stores, DCN Hadamard/residual second output).
 // C/D map of 16x16x32: col = lane&15, row = 4*(lane>>4) + reg.
-template <int ROWS, int NT>
-__device__ __forceinline__ void epilogue(const GemmArgs& p, const f32x4_t (&acc)[4][4],
+template <int ROWS, int NT, int MI = 4>
+__device__ __forceinline__ void epilogue(const GemmArgs& p, const f32x4_t (&acc)[MI][4],
                                          char* smem_raw, int m0, int n0, int wr, int wc,
                                          int lane, int tid) {
   float* ctile = (float*)smem_raw;   // [ROWS][128] fp32, 16-B chunks XOR-swizzled
@@ -162,10 +162,10 @@ __device__ __forceinline__ void epilogue(const GemmArgs& p, const f32x4_t (&acc)
     const int n = n0 + cl;
     const float bias = (p.bias && n < p.N) ? p.bias[(int64_t)n * p.bias_stride] : 0.f;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < MI; ++i) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int rl = wr * 64 + i * 16 + 4 * (lane >> 4) + r;
+        const int rl = wr * (MI * 16) + i * 16 + 4 * (lane >> 4) + r;
         float v = acc[i][j][r] + bias;
         if (p.relu) v = fmaxf(v, 0.f);
         const int chunk = (cl >> 2) ^ (rl & 31);
@@ -252,20 +252,20 @@ __device__ __forceinline__ void epilogue(const GemmArgs& p, const f32x4_t (&acc)
 // 16 MFMAs of one 64-deep K step for a wave's 64x64 sub-tile (two 32-deep
 // halves). ta/tb: 16-KiB images holding the wave's A rows / B cols at
 // a_r0 / b_c0.
-template <bool A_COL, bool B_COL>
-__device__ __forceinline__ void mfma_k64(f32x4_t (&acc)[4][4], const TDFO_LDS char* ta,
+template <bool A_COL, bool B_COL, int MI = 4>
+__device__ __forceinline__ void mfma_k64(f32x4_t (&acc)[MI][4], const TDFO_LDS char* ta,
                                          int a_r0, const TDFO_LDS char* tb, int b_c0, int lane) {
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) {
-    bf16x8_t af[4], bfr[4];
+    bf16x8_t af[MI], bfr[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MI; ++i)
       af[i] = A_COL ? frag_col(ta, a_r0 + i * 16, ks, lane) : frag_row(ta, a_r0 + i * 16, ks, lane);
 #pragma unroll
     for (int j = 0; j < 4; ++j)
       bfr[j] = B_COL ? frag_col(tb, b_c0 + j * 16, ks, lane) : frag_row(tb, b_c0 + j * 16, ks, lane);
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
@@ -273,18 +273,22 @@ __device__ __forceinline__ void mfma_k64(f32x4_t (&acc)[4][4], const TDFO_LDS ch
 }
 
 // ---------------------------------------------------------------------------
-// Small-tile kernel: 128x128x64, 4 waves (2x2 of 64x64), 2-deep glds ring,
-// 64 KiB LDS -> 2 blocks per CU. Used when the problem has too few 256x128
-// tiles to fill the chip.
-template <bool A_COL, bool B_COL>
+// Small-tile kernel: BMT x 128 x 64 (BMT = 128, or 64 for row-layout A when
+// the 128-row grid leaves CUs idle), 4 waves (2x2 of (BMT/2)x64), 2-deep glds
+// ring (2 x (BMT + 128) x 64 x 2 B of LDS) -> 2+ blocks per CU.
+template <int BMT, bool A_COL, bool B_COL>
 __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs p) {
+  static_assert(BMT == 128 || !A_COL, "64-row tiles need a row-layout A");
+  constexpr int MI = BMT / 32;                   // 16-row fragments per wave
+  constexpr int A_BYTES = BMT * BK * 2;
+  constexpr int ST = A_BYTES + TILE_BYTES;
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   TDFO_LDS char* smem = (TDFO_LDS char*)smem_raw;
 
-  const int tiles_m = (p.M + BM - 1) / BM, tiles_n = (p.N + BN - 1) / BN;
+  const int tiles_m = (p.M + BMT - 1) / BMT, tiles_n = (p.N + BN - 1) / BN;
   const int wg = xcd_remap(blockIdx.x, tiles_m * tiles_n);
   const int tm = wg / tiles_n, tn = wg - tm * tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
+  const int m0 = tm * BMT, n0 = tn * BN;
 
   const int ktiles = p.K / BK;
   const int per = (ktiles + p.splits - 1) / p.splits;
@@ -294,18 +298,22 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs p) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wr = w >> 1, wc = w & 1;
 
-  f32x4_t acc[4][4];
+  f32x4_t acc[MI][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
   auto stage = [&](int buf, int kt) {
-    TDFO_LDS char* ta = smem + buf * STAGE_BYTES;
-    TDFO_LDS char* tb = ta + TILE_BYTES;
+    TDFO_LDS char* ta = smem + buf * ST;
+    TDFO_LDS char* tb = ta + A_BYTES;
     const int k0 = kt * BK;
     if (A_COL) stage_col(p.A, p.lda, m0, p.M, k0, ta, w, lane);
-    else       stage_row(p.A, p.lda, m0, p.M, k0, ta, w, lane);
+    else {
+#pragma unroll
+      for (int i = 0; i < BMT / 32; ++i)
+        glds_row(p.A, p.lda, m0, p.M, k0, ta, w * (BMT / 32) + i, lane);
+    }
     if (B_COL) stage_col(p.B, p.ldb, n0, p.N, k0, tb, w, lane);
     else       stage_row(p.B, p.ldb, n0, p.N, k0, tb, w, lane);
   };
@@ -316,13 +324,13 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs p) {
     int cur = 0;
     for (int kt = kt0; kt < kt1; ++kt) {
       if (kt + 1 < kt1) stage(cur ^ 1, kt + 1);
-      const TDFO_LDS char* ta = smem + cur * STAGE_BYTES;
-      mfma_k64<A_COL, B_COL>(acc, ta, wr * 64, ta + TILE_BYTES, wc * 64, lane);
+      const TDFO_LDS char* ta = smem + cur * ST;
+      mfma_k64<A_COL, B_COL, MI>(acc, ta, wr * (BMT / 2), ta + A_BYTES, wc * 64, lane);
       __syncthreads();
       cur ^= 1;
     }
   }
-  epilogue<BM, 256>(p, acc, smem_raw, m0, n0, wr, wc, lane, tid);
+  epilogue<BMT, 256, MI>(p, acc, smem_raw, m0, n0, wr, wc, lane, tid);
 }
 
 // ---------------------------------------------------------------------------
@@ -402,7 +410,8 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(GemmArgs p) {
   epilogue<LBM, 512>(p, acc, smem_raw, m0, n0, wr, wc, lane, tid);
 }
 
-// 0 auto, 1 small tiles only, 2 large tiles only. Default 1: inside the
+// 0 auto, 1 small tiles only (64-row tiles when 128-row ones underfill),
+// 2 large tiles only, 3 128x128 tiles only. Default 1: inside the
 // graph-replayed DLRM-1TB step the 128x128 kernel measured 0.725-0.728 ms/step
 // vs 0.735-0.736 with auto (profiles/gemm_tile_ab.md), although the 256x128
 // kernel wins 2-7 % on the N=1024 shapes in isolation.
@@ -412,7 +421,7 @@ template <bool AC, bool BC>
 void launch(const GemmArgs& a, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
-    TDFO_CHECK_HIP(hipFuncSetAttribute((const void*)gemm_kernel<AC, BC>,
+    TDFO_CHECK_HIP(hipFuncSetAttribute((const void*)gemm_kernel<128, AC, BC>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize,
                                        SMEM_BYTES));
     TDFO_CHECK_HIP(hipFuncSetAttribute((const void*)gemm_big_kernel<AC, BC>,
@@ -426,13 +435,24 @@ void launch(const GemmArgs& a, hipStream_t s) {
   b.abl = g_policy >= 8 ? g_policy - 8 : 0;      // perf ablations (policy 9..15), big kernel
   // auto: the 256x128 kernel once it alone fills every CU (measured on the
   // DLRM-1TB shapes: ahead from 256 blocks up, behind below), else 128x128
-  bool big = g_policy >= 2 || (g_policy == 0 && big_tiles * a.splits >= 256);
+  bool big = (g_policy >= 2 && g_policy != 3) || (g_policy == 0 && big_tiles * a.splits >= 256);
   if (big) {
     dim3 grid(big_tiles, 1, a.splits);
     hipLaunchKernelGGL((gemm_big_kernel<AC, BC>), grid, dim3(512), LSMEM, s, b);
   } else {
+    if constexpr (!AC) {
+      // 64-row tiles when 128-row tiles leave CUs idle (bottom MLP, top3)
+      if (small_tiles * a.splits < 256 && g_policy != 3) {
+        const int t64 = ((a.M + 63) / 64) * tn;
+        dim3 grid(t64, 1, a.splits);
+        hipLaunchKernelGGL((gemm_kernel<64, AC, BC>), grid, dim3(256),
+                           2 * (64 * BK * 2 + TILE_BYTES), s, a);
+        TDFO_CHECK_HIP(hipGetLastError());
+        return;
+      }
+    }
     dim3 grid(small_tiles, 1, a.splits);
-    hipLaunchKernelGGL((gemm_kernel<AC, BC>), grid, dim3(256), SMEM_BYTES, s, a);
+    hipLaunchKernelGGL((gemm_kernel<128, AC, BC>), grid, dim3(256), SMEM_BYTES, s, a);
   }
   TDFO_CHECK_HIP(hipGetLastError());
 }
