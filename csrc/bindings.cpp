@@ -405,7 +405,8 @@ void embedding_bwd(const Tensor& W, const Tensor& row_offset, const Tensor& indi
 void dense_optimizer(const Tensor& p, const Tensor& g, const c10::optional<Tensor>& m,
                      const c10::optional<Tensor>& v, const c10::optional<Tensor>& p_bf16,
                      int64_t opt, const Tensor& hyper, double beta1, double beta2, double eps,
-                     double wd, double momentum, const c10::optional<Tensor>& found_inf) {
+                     double wd, double momentum, const c10::optional<Tensor>& found_inf,
+                     at::TensorList seg_slabs, at::IntArrayRef seg_start, at::IntArrayRef seg_splits) {
   check_dev(p, "p"); check_dev(g, "g");
   TORCH_CHECK(p.scalar_type() == at::kFloat && g.scalar_type() == at::kFloat && p.is_contiguous() &&
               g.is_contiguous() && p.numel() == g.numel(), "p/g fp32 contiguous same size");
@@ -424,6 +425,20 @@ void dense_optimizer(const Tensor& p, const Tensor& g, const c10::optional<Tenso
   a.beta1 = (float)beta1; a.beta2 = (float)beta2; a.eps = (float)eps;
   a.weight_decay = (float)wd; a.momentum = (float)momentum;
   if (found_inf) a.found_inf = found_inf->data_ptr<float>();
+  TORCH_CHECK(seg_slabs.size() <= 16 && seg_start.size() == seg_slabs.size() &&
+              seg_splits.size() == seg_slabs.size(), "dense_optimizer: <= 16 matching segments");
+  a.nseg = (int)seg_slabs.size();
+  for (size_t k = 0; k < seg_slabs.size(); ++k) {
+    const Tensor& sl = seg_slabs[k];
+    check_dev(sl, "seg slab");
+    TORCH_CHECK(sl.scalar_type() == at::kFloat && sl.is_contiguous() && aligned16(sl.data_ptr()),
+                "seg slab fp32 contiguous 16-B aligned");
+    const int64_t S = seg_splits[k], len = S > 0 ? sl.numel() / S : 0;
+    TORCH_CHECK(S >= 1 && len * S == sl.numel() && len % 4 == 0 && seg_start[k] % 4 == 0 &&
+                seg_start[k] + len <= p.numel(), "dense_optimizer: segment shape/alignment");
+    a.seg_start[k] = seg_start[k]; a.seg_len[k] = len; a.seg_splits[k] = (int)S;
+    a.seg_ptr[k] = sl.data_ptr<float>();
+  }
   tdfo::dense_optimizer(a, cur_stream());
 }
 
@@ -649,7 +664,8 @@ TORCH_LIBRARY(tdfo, m) {
         "Tensor(b!)? state1, Tensor(c!)? state2, Tensor hyper, float eps, float beta1, float beta2, "
         "float weight_decay, Tensor(d!)? dense_grad) -> ()");
   m.def("dense_optimizer(Tensor(a!) p, Tensor g, Tensor(b!)? m, Tensor(c!)? v, Tensor(d!)? p_bf16, int opt, "
-        "Tensor hyper, float beta1, float beta2, float eps, float wd, float momentum, Tensor? found_inf) -> ()");
+        "Tensor hyper, float beta1, float beta2, float eps, float wd, float momentum, Tensor? found_inf, "
+        "Tensor[] seg_slabs, int[] seg_start, int[] seg_splits) -> ()");
   m.def("check_finite(Tensor g, Tensor(a!) found) -> ()");
   m.def("sort_pairs(Tensor keys, Tensor vals, int key_bits) -> (Tensor, Tensor)");
   m.def("cast_bf16(Tensor x, Tensor(a!) y) -> ()");

@@ -131,6 +131,13 @@ struct DenseOptArgs {
   const float* hyper;   // device: [lr, step, grad_scale]
   float beta1, beta2, eps, weight_decay, momentum;
   const float* found_inf;  // optional device flag: skip update if > 0
+  // optional gradient segments: elements [seg_start, +seg_len) take their
+  // gradient as the sum of seg_splits slabs seg_ptr[s * seg_len + j] (the
+  // split-K partials of a weight-grad GEMM) instead of g
+  int nseg;
+  int64_t seg_start[16], seg_len[16];
+  int seg_splits[16];
+  const float* seg_ptr[16];
 };
 void dense_optimizer(const DenseOptArgs& a, hipStream_t s);
 // found_inf[0] = any(!isfinite(g)) over n (caller zeroes it first).

@@ -20,7 +20,24 @@ __global__ __launch_bounds__(256) void dense_opt_kernel(DenseOptArgs a) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
        i += stride) {
     float4 p = ((float4*)a.p)[i];
-    float4 g = ((const float4*)a.g)[i];
+    float4 g;
+    int sk = -1;
+    const int64_t e = 4 * i;
+    for (int k = 0; k < a.nseg; ++k)
+      if (e >= a.seg_start[k] && e < a.seg_start[k] + a.seg_len[k]) sk = k;
+    if (sk < 0) {
+      g = ((const float4*)a.g)[i];
+    } else {
+      // split-K weight-grad slabs of one layer, summed in fixed order here
+      // instead of by a separate reduce launch
+      const int64_t o = e - a.seg_start[sk], L = a.seg_len[sk];
+      const float* sp = a.seg_ptr[sk];
+      g = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int q = 0; q < a.seg_splits[sk]; ++q) {
+        const float4 t = *(const float4*)(sp + q * L + o);
+        g.x += t.x; g.y += t.y; g.z += t.z; g.w += t.w;
+      }
+    }
     float pv[4] = {p.x, p.y, p.z, p.w};
     float gv[4] = {g.x * gs, g.y * gs, g.z * gs, g.w * gs};
     if (a.opt == OPT_ADAMW || a.opt == OPT_ADAM) {

@@ -241,6 +241,19 @@ class DLRMTrainer:
             s_ = ops.wgrad_splits(cfg.dcn_rank, self.top_real, B)
             max_slab = max(max_slab, s_ * cfg.dcn_rank * self.top_real)
         self.slab = z(max_slab, dt=torch.float32)
+        # One process on a GPU: each MLP layer's split-K weight-grad partials
+        # get their own slab and are summed inside the fused optimizer pass
+        # (no reduce launch per layer). With >1 rank the grads are reduced
+        # first because the all-reduce needs them.
+        self.wslab = {}
+        self._segments = []
+        if dev.type == "cuda" and world_size == 1:
+            for L in self.bottom_layers + self.top_layers:
+                S = ops.wgrad_splits(L.out, L.wcols, B)
+                if S > 1:
+                    sl = z(S * L.out * L.wcols, dt=torch.float32)
+                    self.wslab[L.name] = (sl, S)
+                    self._segments.append((fp.offset(L.name + ".w"), sl, S))
         self.dense_hyper = torch.tensor([cfg.dense_lr, 0.0, 1.0], dtype=torch.float32, device=dev)
         self.emb_hyper = torch.tensor([cfg.emb_lr, 0.0], dtype=torch.float32, device=dev)
         self.slot_off = [0] + list(self.emb.slot_off)
@@ -302,12 +315,20 @@ class DLRMTrainer:
     def _bwd(self, L: Lin, x, dy, dx, x_is_relu):
         """weight+bias grad (augmented wgrad) and dgrad into dx (masked by x>0)."""
         fp = self.fp
+
+        def wgrad():
+            if L.name in self.wslab:          # partials only; summed by the optimizer
+                sl, S = self.wslab[L.name]
+                ops.gemm(dy, True, x, True, None, False, None, None, sl, S)
+            else:
+                ops.linear_wgrad(dy, x, fp.grad(L.name + ".w").view(-1), slab=self.slab)
+
         if self._ws is not None:
             self._ws.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(self._ws):
-                ops.linear_wgrad(dy, x, fp.grad(L.name + ".w").view(-1), slab=self.slab)
+                wgrad()
         else:
-            ops.linear_wgrad(dy, x, fp.grad(L.name + ".w").view(-1), slab=self.slab)
+            wgrad()
         if dx is not None:
             # dgrad only over the columns dx holds (the padded K tail of the
             # augmented layout, bias column included, has no gradient consumer)
@@ -445,7 +466,7 @@ class DLRMTrainer:
         self._join(self._es)
         fp = self.fp
         ops.dense_optimizer(fp.p, fp.g, fp.m, fp.v, fp.p_bf16, self.dense_opt, self.dense_hyper,
-                            wd=self.cfg.dense_wd)
+                            wd=self.cfg.dense_wd, segments=self._segments)
 
     # DCN-v2 cross network: x_{l+1} = x0 * (U (V^T x_l) + b) + x_l. The
     # Hadamard product and the residual are fused into the U-GEMM epilogue

@@ -116,11 +116,20 @@ def embedding_bwd(W, row_offset, indices, offsets, grad_off, T, B, grad, grad_st
 
 
 def dense_optimizer(p, g, m, v, p_bf16, opt, hyper, beta1=0.9, beta2=0.999, eps=1e-8, wd=0.0,
-                    momentum=0.0, found_inf=None):
+                    momentum=0.0, found_inf=None, segments=()):
+    """Fused flat optimizer. ``segments``: (start, slab, splits) triples whose
+    elements take sum_s slab.view(splits, -1)[s] as their gradient (split-K
+    weight-grad partials reduced inside the optimizer pass)."""
     if _gpu(p):
         _native().dense_optimizer(p, g, m, v, p_bf16, opt, hyper, beta1, beta2, eps, wd, momentum,
-                                  found_inf)
+                                  found_inf, [s[1] for s in segments],
+                                  [int(s[0]) for s in segments], [int(s[2]) for s in segments])
     else:
+        if segments:
+            g = g.clone()
+            for start, slab, splits in segments:
+                n = slab.numel() // splits
+                g[start:start + n] = slab.view(splits, n).sum(0)
         ref.dense_optimizer(p, g, m, v, p_bf16, opt, hyper, beta1, beta2, eps, wd, momentum,
                             found_inf)
 

@@ -47,6 +47,9 @@ class FlatParams:
         off, shape = self._views[name]
         return buf[off: off + int(math.prod(shape))].view(shape)
 
+    def offset(self, name) -> int:
+        return self._views[name][0]
+
     def param(self, name):
         return self._view(self.p, name)
 

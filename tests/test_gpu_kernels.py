@@ -537,3 +537,21 @@ def test_head_reduce_and_step_bumps():
     assert torch.allclose(grad.double(), p[:, : K + 1].sum(0), atol=1e-4)
     assert abs(float(loss) - (1.5 + float(p[:, K + 1].sum()))) < 1e-3
     assert float(h1[1]) == 5.0 and float(h2[1]) == 10.0 and float(h1[0]) == pytest.approx(0.1)
+
+
+def test_dense_optimizer_slab_segments():
+    """Split-K weight-grad slabs summed inside the optimizer == reduce then step."""
+    torch.manual_seed(12)
+    n = 4096
+    p = torch.randn(n, device=DEV)
+    g = torch.randn(n, device=DEV)
+    slab = torch.randn(3 * 1024, device=DEV)
+    hyper = torch.tensor([1e-2, 1.0, 1.0], device=DEV)
+    p1, m1, v1 = p.clone(), torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
+    ops.dense_optimizer(p1, g, m1, v1, None, ops.OPT_ADAMW, hyper, wd=0.01,
+                        segments=[(1024, slab, 3)])
+    g2 = g.clone()
+    g2[1024:2048] = slab.view(3, 1024).sum(0)
+    p2, m2, v2 = p.clone(), torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
+    ops.dense_optimizer(p2, g2, m2, v2, None, ops.OPT_ADAMW, hyper, wd=0.01)
+    assert torch.allclose(p1, p2, atol=1e-6) and torch.allclose(m1, m2, atol=1e-6)
