@@ -635,6 +635,8 @@ TORCH_LIBRARY(tdfo, m) {
   m.def("gemm(Tensor a, bool a_col, Tensor b, bool b_col, Tensor? bias, bool relu, Tensor? mask, "
         "Tensor(a!)? out, Tensor(b!)? out32, int splits, Tensor? mul=None, Tensor? add=None, "
         "Tensor(c!)? out2=None) -> ()");
+  m.def("radix_sort_sep_hist(int v) -> int",
+        [](int64_t v) { return (int64_t)tdfo::radix_sort_sep_hist((int)v); });
   m.def("radix_sort_max_bits(int b) -> int",
         [](int64_t v) { return (int64_t)tdfo::radix_sort_max_bits((int)v); });
   m.def("gemm_policy(int p) -> int", [](int64_t p) { return (int64_t)tdfo::gemm_policy((int)p); });

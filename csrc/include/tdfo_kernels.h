@@ -75,6 +75,8 @@ void cross_bwd(const uint16_t* dout, const uint16_t* x0, const uint16_t* y, int6
 size_t radix_sort_workspace(int64_t n);
 // digit bits per radix pass (4..10); returns the previous value (b < 4: read only)
 int radix_sort_max_bits(int b);
+// 1: per-pass hist kernels, 0: next-pass hist counted by the scatter (atomics)
+int radix_sort_sep_hist(int v);
 int radix_sort_pairs_u32(uint32_t* ka, int32_t* va, uint32_t* kb, int32_t* vb, int64_t n,
                          int key_bits, void* ws, hipStream_t s);
 int radix_sort_pairs_u64(uint64_t* ka, int32_t* va, uint64_t* kb, int32_t* vb, int64_t n,

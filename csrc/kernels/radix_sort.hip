@@ -183,6 +183,11 @@ __global__ __launch_bounds__(256) void rs_scatter_kernel(
 
 int g_max_bits = 10;  // digit bits per pass (<= RS_MAXB): 28-bit keys -> 10/9/9 (fastest measured)
 
+// 1: each pass's histogram from its own coalesced hist kernel; 0: counted by
+// the previous pass's scatter with global atomics (scattered addresses:
+// slow at large n, see profiles/sort_digit_ab.jsonl)
+int g_sep_hist = 1;
+
 template <typename K>
 int sort_impl(K* ka, int32_t* va, K* kb, int32_t* vb, int64_t n, int key_bits, int32_t* ws,
               hipStream_t s) {
@@ -204,9 +209,13 @@ int sort_impl(K* ka, int32_t* va, K* kb, int32_t* vb, int64_t n, int key_bits, i
   K* kin = ka; int32_t* vin = va; K* kout = kb; int32_t* vout = vb;
   for (int p = 0; p < passes; ++p) {
     const int nb = 1 << pbits[p];
+    if (g_sep_hist && p > 0) {
+      hipLaunchKernelGGL(rs_hist_kernel<K>, dim3(ntiles), dim3(RS_THREADS), 0, s, kin, n,
+                         pshift[p], pbits[p], H[p % 3], H[(p + 1) % 3]);
+    }
     hipLaunchKernelGGL(rs_scan_kernel, dim3((nb + 63) / 64), dim3(1024), 0, s, H[p % 3], ntiles,
                        nb, tot);
-    const bool last = p + 1 == passes;
+    const bool last = p + 1 == passes || g_sep_hist;   // sep: next hist by its own kernel
     hipLaunchKernelGGL(rs_scatter_kernel<K>, dim3(ntiles), dim3(RS_THREADS), 0, s, kin, vin,
                        kout, vout, n, pshift[p], pbits[p], last ? -1 : pshift[p + 1],
                        last ? 0 : pbits[p + 1], H[p % 3], tot, H[(p + 1) % 3], H[(p + 2) % 3]);
@@ -218,6 +227,12 @@ int sort_impl(K* ka, int32_t* va, K* kb, int32_t* vb, int64_t n, int key_bits, i
 }
 
 }  // namespace
+
+int radix_sort_sep_hist(int v) {
+  const int old = g_sep_hist;
+  if (v >= 0) g_sep_hist = v ? 1 : 0;
+  return old;
+}
 
 int radix_sort_max_bits(int b) {
   const int old = g_max_bits;

@@ -16,8 +16,9 @@ nat = torch.ops.tdfo
 for n in (213_000, 1_700_000):
     keys = torch.randint(0, 188_000_000, (n,), device="cuda", dtype=torch.int32)
     vals = torch.arange(n, dtype=torch.int32, device="cuda")
-    for b in (7, 8, 9, 10):
+    for b, sep in ((8, 0), (10, 0), (8, 1), (10, 1)):
         nat.radix_sort_max_bits(b)
+        nat.radix_sort_sep_hist(sep)
         t = timeit(lambda: ops.sort_pairs(keys, vals, 28))
         # the same sort inside a hipGraph (device time, no host launch cost)
         ops.sort_pairs(keys, vals, 28)
@@ -26,6 +27,7 @@ for n in (213_000, 1_700_000):
         with torch.cuda.graph(g):
             ops.sort_pairs(keys, vals, 28)
         tg = timeit(g.replay)
-        print(json.dumps({"n": n, "max_bits": b, "sort_us": round(t, 1),
+        print(json.dumps({"n": n, "max_bits": b, "sep_hist": sep, "sort_us": round(t, 1),
                           "graph_sort_us": round(tg, 1)}), flush=True)
 nat.radix_sort_max_bits(10)
+nat.radix_sort_sep_hist(1)
