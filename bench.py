@@ -66,7 +66,7 @@ def main(argv=None):
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     if not _ext.load():
         raise RuntimeError("native HIP library failed to load")
-    if os.environ.get("TDFO_GEMM_POLICY"):
+    if os.environ.get("TDFO_GEMM_POLICY"):      # override the trainer's per-model choice
         from tdfo_amd import ops
         ops.gemm_policy(int(os.environ["TDFO_GEMM_POLICY"]))
     rows = {"1tb": CRITEO_1TB_ROWS, "kaggle": CRITEO_KAGGLE_ROWS,

@@ -90,25 +90,31 @@ struct BwdCfg {
 
 // keys[p] = row_offset[t] + id, vals[p] = p, goff[p] = offset of p's pooled
 // gradient row, gscale[p] = per-id scale (psw, 1/len for mean) if needed.
+// One thread per position (coalesced stores, balanced under multi-hot
+// pooling); its bag is found by binary search over the bag offsets.
 template <typename K>
 __global__ void emb_keys_kernel(const EmbBwdArgs a, K* __restrict__ keys,
                                 int32_t* __restrict__ vals, int64_t* __restrict__ goff,
                                 float* __restrict__ gscale, int32_t* __restrict__ tail_count) {
   if (blockIdx.x == 0 && threadIdx.x == 0) *tail_count = 0;  // read by later kernels
   const int64_t nbags = (int64_t)a.T * a.B;
-  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < nbags;
-       j += (int64_t)gridDim.x * blockDim.x) {
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < a.nnz;
+       p += (int64_t)gridDim.x * blockDim.x) {
+    int64_t lo = 0, hi = nbags;                 // last bag j with offsets[j] <= p
+    while (hi - lo > 1) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (a.offsets[mid] <= p) lo = mid; else hi = mid;
+    }
+    const int64_t j = lo;
     const int t = (int)(j / a.B);
     const int b = (int)(j - (int64_t)t * a.B);
-    const int64_t ro = a.row_offset[t];
-    const int64_t go = (int64_t)b * a.grad_stride + a.grad_off[t];
-    const int64_t s0 = a.offsets[j], s1 = a.offsets[j + 1];
-    const float inv = (a.mean && s1 > s0) ? 1.f / (float)(s1 - s0) : 1.f;
-    for (int64_t p = s0; p < s1; ++p) {
-      keys[p] = (K)(ro + a.indices[p]);
-      vals[p] = (int32_t)p;
-      goff[p] = go;
-      if (gscale) gscale[p] = (a.psw ? a.psw[p] : 1.f) * inv;
+    keys[p] = (K)(a.row_offset[t] + a.indices[p]);
+    vals[p] = (int32_t)p;
+    goff[p] = (int64_t)b * a.grad_stride + a.grad_off[t];
+    if (gscale) {
+      const int64_t s0 = a.offsets[j], s1 = a.offsets[j + 1];
+      const float inv = (a.mean && s1 > s0) ? 1.f / (float)(s1 - s0) : 1.f;
+      gscale[p] = (a.psw ? a.psw[p] : 1.f) * inv;
     }
   }
 }
@@ -448,9 +454,8 @@ void bwd_impl(const EmbBwdArgs& a, const WsLayout& L, hipStream_t s) {
   float* tail = (float*)(ws + L.tail);
   int32_t* tlist = (int32_t*)(ws + L.tlist);
   int32_t* tcount = (int32_t*)(ws + L.tcount);
-  const int64_t nbags = (int64_t)a.T * a.B;
-  int64_t kb = (nbags + 255) / 256;
-  if (kb > 4096) kb = 4096;
+  int64_t kb = (a.nnz + 255) / 256;
+  if (kb > 8192) kb = 8192;
   hipLaunchKernelGGL(emb_keys_kernel<K>, dim3(kb), dim3(256), 0, s, a, keys_in, vals_in, goff,
                      gscale, tcount);
   TDFO_CHECK_HIP(hipGetLastError());

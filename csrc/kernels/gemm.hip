@@ -412,11 +412,12 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(GemmArgs p) {
 
 // 0 auto, 1 small tiles only (64-row tiles when 128-row ones underfill),
 // 2 large tiles only, 3 128x128 tiles only, 4 = 1 with 256x128 tiles for
-// the weight-grad (col-A) GEMMs. Default 1: inside the
-// graph-replayed DLRM-1TB step the 128x128 kernel measured 0.725-0.728 ms/step
-// vs 0.735-0.736 with auto (profiles/gemm_tile_ab.md), although the 256x128
-// kernel wins 2-7 % on the N=1024 shapes in isolation.
-int g_policy = 1;
+// the weight-grad (col-A) GEMMs. Auto (default) takes the 256x128 kernel only
+// for GEMMs with >= 1024 128x128 tiles: in the graph-replayed DLRM-1TB step
+// (<= 512 tiles per GEMM) 128x128 measured 0.725-0.728 ms/step vs 0.735 with
+// the 256x128 kernel from 256 blocks up (profiles/gemm_tile_ab.md); on the
+// DCN-v2 cross layers (1728 tiles) 256x128 is ahead (3.19 vs 3.28 ms/step).
+int g_policy = 0;
 
 template <bool AC, bool BC>
 void launch(const GemmArgs& a, hipStream_t s) {
@@ -434,16 +435,15 @@ void launch(const GemmArgs& a, hipStream_t s) {
   const int big_tiles = ((a.M + LBM - 1) / LBM) * tn;
   GemmArgs b = a;
   b.abl = g_policy >= 8 ? g_policy - 8 : 0;      // perf ablations (policy 9..15), big kernel
-  // auto: the 256x128 kernel once it alone fills every CU (measured on the
-  // DLRM-1TB shapes: ahead from 256 blocks up, behind below), else 128x128
-  bool big = (g_policy >= 2 && g_policy != 3 && g_policy != 4) || (g_policy == 4 && AC) || (g_policy == 0 && big_tiles * a.splits >= 256);
+  bool big = (g_policy >= 2 && g_policy != 3 && g_policy != 4) || (g_policy == 4 && AC) ||
+             (g_policy == 0 && small_tiles * a.splits >= 1024);
   if (big) {
     dim3 grid(big_tiles, 1, a.splits);
     hipLaunchKernelGGL((gemm_big_kernel<AC, BC>), grid, dim3(512), LSMEM, s, b);
   } else {
     if constexpr (!AC) {
       // 64-row tiles when 128-row tiles leave CUs idle (bottom MLP, top3)
-      if (small_tiles * a.splits < 256 && g_policy != 3) {
+      if (small_tiles * a.splits < 256 && g_policy != 3 && g_policy != 2) {
         const int t64 = ((a.M + 63) / 64) * tn;
         dim3 grid(t64, 1, a.splits);
         hipLaunchKernelGGL((gemm_kernel<64, AC, BC>), grid, dim3(256),

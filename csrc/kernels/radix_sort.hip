@@ -48,34 +48,35 @@ __global__ __launch_bounds__(256) void rs_hist_kernel(const K* __restrict__ keys
   for (int d = t; d < nb; d += RS_THREADS) hist[(int64_t)blockIdx.x * nb + d] = cnt[d];
 }
 
-// Column scan of the [tile][nb] histogram: 1024-thread blocks, 64 digits per
-// block, 16 threads per digit each own a contiguous run of tiles. Each thread
-// loads its whole run (up to 32 tiles) into registers with no dependency
-// between the loads, so the scan costs ~two memory latencies instead of one
-// per tile. Rewrites hist[tile][d] as the exclusive prefix over tiles; digit
-// totals -> tot. Runs longer than 32 tiles (> 512 tiles) take a plain loop.
+// Column scan of the [tile][nb] histogram: 1024-thread blocks, 32 digits per
+// block, 32 threads per digit each own a contiguous run of tiles. Each thread
+// loads its whole run (up to 64 tiles, i.e. inputs up to 2M keys) into
+// registers with no dependency between the loads, so the scan costs ~two
+// memory latencies instead of one per tile. Rewrites hist[tile][d] as the
+// exclusive prefix over tiles; digit totals -> tot. Longer runs loop.
+constexpr int SCAN_DPB = 32, SCAN_PH = 1024 / SCAN_DPB, SCAN_RUN = 64;
+
 __global__ __launch_bounds__(1024) void rs_scan_kernel(int32_t* __restrict__ hist, int ntiles,
                                                        int nb, int32_t* __restrict__ tot) {
-  constexpr int RUN = 32;
-  __shared__ int part[16][64];
-  const int dl = threadIdx.x & 63, ph = threadIdx.x >> 6;
-  const int d = blockIdx.x * 64 + dl;
-  const int per = (ntiles + 15) / 16;
+  __shared__ int part[SCAN_PH][SCAN_DPB];
+  const int dl = threadIdx.x % SCAN_DPB, ph = threadIdx.x / SCAN_DPB;
+  const int d = blockIdx.x * SCAN_DPB + dl;
+  const int per = (ntiles + SCAN_PH - 1) / SCAN_PH;
   const int t0 = ph * per, t1 = d < nb ? min(ntiles, t0 + per) : t0;   // d >= nb: idle
   int s = 0;
-  if (per <= RUN) {
-    int c[RUN];
+  if (per <= SCAN_RUN) {
+    int c[SCAN_RUN];
 #pragma unroll
-    for (int q = 0; q < RUN; ++q) c[q] = (t0 + q < t1) ? hist[(int64_t)(t0 + q) * nb + d] : 0;
+    for (int q = 0; q < SCAN_RUN; ++q) c[q] = (t0 + q < t1) ? hist[(int64_t)(t0 + q) * nb + d] : 0;
 #pragma unroll
-    for (int q = 0; q < RUN; ++q) s += c[q];
+    for (int q = 0; q < SCAN_RUN; ++q) s += c[q];
     part[ph][dl] = s;
     __syncthreads();
     int run = 0;
     for (int q = 0; q < ph; ++q) run += part[q][dl];
-    if (ph == 15 && d < nb) tot[d] = run + s;
+    if (ph == SCAN_PH - 1 && d < nb) tot[d] = run + s;
 #pragma unroll
-    for (int q = 0; q < RUN; ++q) {
+    for (int q = 0; q < SCAN_RUN; ++q) {
       if (t0 + q < t1) hist[(int64_t)(t0 + q) * nb + d] = run;
       run += c[q];
     }
@@ -86,7 +87,7 @@ __global__ __launch_bounds__(1024) void rs_scan_kernel(int32_t* __restrict__ his
   __syncthreads();
   int run = 0;
   for (int q = 0; q < ph; ++q) run += part[q][dl];
-  if (ph == 15 && d < nb) tot[d] = run + s;
+  if (ph == SCAN_PH - 1 && d < nb) tot[d] = run + s;
   for (int t = t0; t < t1; ++t) {
     const int c = hist[(int64_t)t * nb + d];
     hist[(int64_t)t * nb + d] = run;
@@ -213,8 +214,8 @@ int sort_impl(K* ka, int32_t* va, K* kb, int32_t* vb, int64_t n, int key_bits, i
       hipLaunchKernelGGL(rs_hist_kernel<K>, dim3(ntiles), dim3(RS_THREADS), 0, s, kin, n,
                          pshift[p], pbits[p], H[p % 3], H[(p + 1) % 3]);
     }
-    hipLaunchKernelGGL(rs_scan_kernel, dim3((nb + 63) / 64), dim3(1024), 0, s, H[p % 3], ntiles,
-                       nb, tot);
+    hipLaunchKernelGGL(rs_scan_kernel, dim3((nb + SCAN_DPB - 1) / SCAN_DPB), dim3(1024), 0, s,
+                       H[p % 3], ntiles, nb, tot);
     const bool last = p + 1 == passes || g_sep_hist;   // sep: next hist by its own kernel
     hipLaunchKernelGGL(rs_scatter_kernel<K>, dim3(ntiles), dim3(RS_THREADS), 0, s, kin, vin,
                        kout, vout, n, pshift[p], pbits[p], last ? -1 : pshift[p + 1],

@@ -24,6 +24,7 @@ once into a hipGraph and replayed (no tracing compiler):
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
 
@@ -158,6 +159,11 @@ class DLRMTrainer:
         assert cfg.top[-1] == 1
         assert cfg.interaction != "dcn" or cfg.dcn_rank % 64 == 0, "dcn_rank must be a multiple of 64"
         torch.manual_seed(cfg.seed)
+        if self.device.type == "cuda" and not os.environ.get("TDFO_GEMM_POLICY"):
+            # GEMM tile policy measured per workload (profiles/gemm_tile_ab.md):
+            # DCN-v2's wide cross layers run best on 256x128 tiles throughout,
+            # DLRM's <= 1024-wide MLPs on 128x128 / 64x128 tiles
+            ops.gemm_policy(2 if cfg.interaction == "dcn" else 0)
         # ------------------------------------------------------ embeddings
         optim = EmbOptimConfig(cfg.emb_opt, lr=cfg.emb_lr, eps=cfg.emb_eps)
         tables = cfg.tables()
