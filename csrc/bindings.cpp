@@ -257,6 +257,41 @@ void layernorm_bwd(const Tensor& x, const Tensor& g, int64_t n, const Tensor& ga
                       part.data_ptr<float>(), dgb.data_ptr<float>(), cur_stream());
 }
 
+// ---------------------------------------------------------- batch gather
+void gather_columns(at::TensorList src, const c10::optional<Tensor>& idx, int64_t row0, int64_t n,
+                    at::TensorList dst, at::IntArrayRef dst_stride) {
+  TORCH_CHECK(src.size() == dst.size() && src.size() == dst_stride.size() && src.size() <= 16 &&
+              !src.empty(), "gather_columns: 1..16 matching columns");
+  tdfo::GatherColsArgs a{};
+  a.ncols = (int)src.size(); a.n = n; a.row0 = row0;
+  int64_t rows = -1;
+  for (size_t c = 0; c < src.size(); ++c) {
+    check_dev(src[c], "src"); check_dev(dst[c], "dst");
+    TORCH_CHECK(src[c].is_contiguous() && src[c].dim() == 1, "gather_columns: 1-D contiguous columns");
+    rows = rows < 0 ? src[c].numel() : rows;
+    TORCH_CHECK(src[c].numel() == rows, "gather_columns: ragged columns");
+    const auto st = src[c].scalar_type();
+    a.src_dtype[c] = st == at::kChar ? 0 : st == at::kShort ? 1 : st == at::kInt ? 2 :
+                     st == at::kLong ? 3 : st == at::kFloat ? 4 : -1;
+    TORCH_CHECK(a.src_dtype[c] >= 0, "gather_columns: src dtype i8/i16/i32/i64/f32");
+    const auto dt = dst[c].scalar_type();
+    TORCH_CHECK(dt == at::kLong || dt == at::kFloat, "gather_columns: dst int64 or fp32");
+    TORCH_CHECK(dst_stride[c] >= 1 && (n == 0 || dst[c].storage_offset() >= 0) &&
+                (n - 1) * dst_stride[c] < dst[c].numel(), "gather_columns: dst too small");
+    a.src[c] = src[c].data_ptr(); a.dst[c] = dst[c].data_ptr();
+    a.dst_int[c] = dt == at::kLong; a.dst_stride[c] = dst_stride[c];
+  }
+  if (idx) {
+    check_dev(*idx, "idx");
+    TORCH_CHECK(idx->scalar_type() == at::kLong && idx->is_contiguous() && idx->numel() >= n,
+                "gather_columns: idx int64 [n]");
+    a.idx = idx->data_ptr<int64_t>();
+  } else {
+    TORCH_CHECK(row0 >= 0 && row0 + n <= rows, "gather_columns: row range");
+  }
+  tdfo::gather_columns(a, cur_stream());
+}
+
 // ----------------------------------------------------------- elementwise
 void concat_features(const Tensor& dense, const Tensor& emb, at::IntArrayRef off,
                      at::IntArrayRef stride, int64_t F, int64_t D, const Tensor& out) {
@@ -649,6 +684,7 @@ TORCH_LIBRARY(tdfo, m) {
   m.def("layernorm_bwd(Tensor x, Tensor g, int n, Tensor gamma, Tensor mean, Tensor rstd, "
         "Tensor(a!) dx, Tensor(b!) part, Tensor(c!) dgb) -> ()");
   m.def("layernorm_parts(int M) -> int", [](int64_t M) { return (int64_t)tdfo::layernorm_parts(M); });
+  m.def("gather_columns(Tensor[] src, Tensor? idx, int row0, int n, Tensor(a!)[] dst, int[] dst_stride) -> ()");
   m.def("concat_features(Tensor dense, Tensor emb, int[] off, int[] stride, int F, int D, "
         "Tensor(a!) out) -> ()");
   m.def("split_features(Tensor dx, int F, int D, Tensor dense, Tensor(a!) d_dense, "
@@ -693,6 +729,7 @@ TORCH_LIBRARY_IMPL(tdfo, CUDA, m) {
   m.impl("attention_bwd", attention_bwd);
   m.impl("layernorm_fwd", layernorm_fwd);
   m.impl("layernorm_bwd", layernorm_bwd);
+  m.impl("gather_columns", gather_columns);
   m.impl("concat_features", concat_features);
   m.impl("split_features", split_features);
   m.impl("cross_bwd", cross_bwd);

@@ -231,6 +231,17 @@ void layernorm_bwd(const float* x, const float* g, int64_t M, int n, const float
                    const float* mean, const float* rstd, float* dx, float* part,
                    float* dgamma_dbeta, hipStream_t s);
 
+// ------------------------------------------------------ batch gather ----
+// out_c[i * dst_stride_c] = convert(src_c[idx ? idx[i] : row0 + i]) for every
+// column c < ncols and row i < n. src dtype codes: 0 i8, 1 i16, 2 i32, 3 i64,
+// 4 f32; dst is int64 (dst_int) or fp32.
+struct GatherColsArgs {
+  const void* src[16]; int src_dtype[16];
+  void* dst[16]; int dst_int[16]; int64_t dst_stride[16];
+  int ncols; int64_t n; const int64_t* idx; int64_t row0;
+};
+void gather_columns(const GatherColsArgs& a, hipStream_t s);
+
 // ----------------------------------------------------------- jagged ----
 void jagged_to_dense(const float* values, const int64_t* off, int B, int T, int D, float pad,
                      float* out, hipStream_t s);

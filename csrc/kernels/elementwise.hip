@@ -126,3 +126,55 @@ void cross_bwd(const uint16_t* dout, const uint16_t* x0, const uint16_t* y, int6
 }
 
 }  // namespace tdfo
+
+// ------------------------------------------------------------------------
+// Batch assembly from HBM-resident columns (tdfo_amd/data/columnar.py): one
+// launch gathers row idx[i] (or row0 + i) of every column, converts it
+// (int8/16/32/64 or fp32 -> int64 or fp32) and stores it at
+// out_c + i * out_stride_c. Replaces one index_select + one copy per column
+// per step (22 launches for TwoTower) with a single kernel.
+namespace tdfo {
+namespace {
+
+template <typename T>
+__device__ __forceinline__ double load_as(const void* p, int64_t r) {
+  return (double)((const T*)p)[r];
+}
+
+__global__ __launch_bounds__(256) void gather_columns_kernel(GatherColsArgs a) {
+  const int64_t total = a.n * a.ncols;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int c = (int)(e / a.n);
+    const int64_t i = e - (int64_t)c * a.n;
+    const int64_t r = a.idx ? a.idx[i] : a.row0 + i;
+    const void* src = a.src[c];
+    double v;
+    switch (a.src_dtype[c]) {
+      case 0: v = load_as<int8_t>(src, r); break;
+      case 1: v = load_as<int16_t>(src, r); break;
+      case 2: v = load_as<int32_t>(src, r); break;
+      case 3: v = load_as<int64_t>(src, r); break;
+      default: v = load_as<float>(src, r); break;
+    }
+    if (a.dst_int[c]) {
+      ((int64_t*)a.dst[c])[i * a.dst_stride[c]] =
+          a.src_dtype[c] == 3 ? ((const int64_t*)src)[r] : (int64_t)v;
+    } else {
+      ((float*)a.dst[c])[i * a.dst_stride[c]] = (float)v;
+    }
+  }
+}
+
+}  // namespace
+
+void gather_columns(const GatherColsArgs& a, hipStream_t s) {
+  const int64_t total = a.n * a.ncols;
+  if (total <= 0) return;
+  int64_t blocks = (total + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(gather_columns_kernel, dim3(blocks), dim3(256), 0, s, a);
+  TDFO_CHECK_HIP(hipGetLastError());
+}
+
+}  // namespace tdfo

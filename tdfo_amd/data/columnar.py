@@ -13,7 +13,7 @@ torchrec/data.py:58 split_dataset_by_node) — same contract as the C++
 """
 from __future__ import annotations
 
-from typing import Dict, Iterator, Optional
+from typing import Dict, Iterator, Optional, Tuple
 
 import numpy as np
 import torch
@@ -43,9 +43,13 @@ class DeviceColumns:
         g = torch.Generator().manual_seed(int(seed) * 1_000_003 + int(epoch))
         return torch.randperm(self.n, generator=g).to(self.device)
 
-    def batches(self, batch_size: int, shuffle: bool = False, seed: int = 0, epoch: int = 0,
-                drop_last: bool = False, rank: int = 0,
-                world_size: int = 1) -> Iterator[Dict[str, torch.Tensor]]:
+    def batch_slices(self, batch_size: int, shuffle: bool = False, seed: int = 0, epoch: int = 0,
+                     drop_last: bool = False, rank: int = 0,
+                     world_size: int = 1) -> Iterator[Tuple[Optional[torch.Tensor], int, int]]:
+        """This rank's rows of each global batch as (idx or None, row0, n):
+        rows idx[:n] of the permutation, or the contiguous range [row0, row0+n).
+        Trainers gather them straight into their static buffers
+        (``ops.gather_columns``: one launch per batch)."""
         B, W = int(batch_size), int(world_size)
         perm = self.permutation(seed, epoch) if shuffle else None
         gb = B * W
@@ -57,11 +61,17 @@ class DeviceColumns:
             else:
                 per, rem = divmod(avail, W)
                 s, n = g0 + rank * per + min(rank, rem), per + (1 if rank < rem else 0)
-            if n == 0:
-                yield {k: v[:0] for k, v in self.cols.items()}
-                continue
-            if perm is None:
+            if perm is None or n == 0:
+                yield None, s, n
+            else:
+                yield perm[s: s + n], 0, n
+
+    def batches(self, batch_size: int, shuffle: bool = False, seed: int = 0, epoch: int = 0,
+                drop_last: bool = False, rank: int = 0,
+                world_size: int = 1) -> Iterator[Dict[str, torch.Tensor]]:
+        for idx, s, n in self.batch_slices(batch_size, shuffle, seed, epoch, drop_last, rank,
+                                           world_size):
+            if idx is None:
                 yield {k: v[s: s + n] for k, v in self.cols.items()}
             else:
-                idx = perm[s: s + n]
                 yield {k: v.index_select(0, idx) for k, v in self.cols.items()}

@@ -194,6 +194,32 @@ class TwoTowerTrainer:
         self._cur_b = b
         return b
 
+    def load_columns(self, cols: Dict[str, torch.Tensor], idx: Optional[torch.Tensor], row0: int,
+                     n: int, eval_mode: bool = False) -> int:
+        """``load_batch`` straight from HBM-resident columns: rows idx[:n] (or
+        [row0, row0 + n)) of every column are gathered, converted and stored
+        into the static buffers by one ``gather_columns`` launch."""
+        cap = self.EB if eval_mode else self.B
+        assert n <= cap and (n > 0 or self.sharded is not None), (n, cap)
+        stride = n
+        if self.sharded is not None:
+            assert n <= self.B, "sharded eval batches must not exceed the train batch"
+            stride = self.B
+            if n < self.B:
+                self.ids[: self.T * self.B].zero_()
+        src = [cols[f] for f in FEATURES] + [cols["avg_rating"], cols["num_pages"]]
+        dst = [self.ids[t * stride:] for t in range(self.T)] + \
+              [self.X.view(-1)[112:], self.X.view(-1)[113:]]
+        st = [1] * self.T + [self.X.shape[1], self.X.shape[1]]
+        if "label" in cols:
+            src.append(cols["label"])
+            dst.append(self.labels)
+            st.append(1)
+        if n:
+            ops.gather_columns(src, idx, row0, n, dst, st)
+        self._cur_b = n
+        return n
+
     # ------------------------------------------------------------ step
     def _lookup(self, b: int):
         if self.sharded is not None:

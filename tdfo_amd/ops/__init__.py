@@ -301,3 +301,15 @@ def layernorm_bwd(x, g, n, gamma, mean, rstd, dx, part, dgb):
         _native().layernorm_bwd(x, g, int(n), gamma, mean, rstd, dx, part, dgb)
     else:
         ref.layernorm_bwd(x, g, n, gamma, mean, rstd, dx, dgb)
+
+
+def gather_columns(src, idx, row0, n, dst, dst_stride):
+    """dst[c].flatten()[i * dst_stride[c]] = src[c][idx[i] if idx is not None else row0 + i]
+    (dtype-converting, one launch for all columns on GPU)."""
+    if _gpu(src[0]):
+        _native().gather_columns(list(src), idx, int(row0), int(n), list(dst),
+                                 [int(s) for s in dst_stride])
+    else:
+        for s, d, st in zip(src, dst, dst_stride):
+            v = s.index_select(0, idx[:n]) if idx is not None else s[row0: row0 + n]
+            d.view(-1)[: (n - 1) * st + 1: st].copy_(v.to(d.dtype)) if n else None

@@ -107,9 +107,16 @@ def run(cfg: Config, mode: str = "single", flavor: str = "flax", out_dir: str = 
     for epoch in range(start_epoch, cfg.n_epochs + 1):
         t0 = time.perf_counter()
         steps = 0
-        for batch in train.batches(B, shuffle=True, seed=cfg.seed, epoch=epoch,
-                                   drop_last=drop_last, rank=rank, world_size=world):
-            b = tr.load_batch({k: v.to(dev, non_blocking=True) for k, v in batch.items()})
+        # HBM-resident columns: one gather launch per batch straight into the
+        # trainer's static buffers; host-resident columns: per-column H2D
+        for idx, s, n in train.batch_slices(B, shuffle=True, seed=cfg.seed, epoch=epoch,
+                                            drop_last=drop_last, rank=rank, world_size=world):
+            if train.device == dev:
+                b = tr.load_columns(train.cols, idx, s, n)
+            else:
+                cols = {k: (v[s: s + n] if idx is None else v.index_select(0, idx.cpu()))
+                        for k, v in train.cols.items()}
+                b = tr.load_batch({k: v.to(dev, non_blocking=True) for k, v in cols.items()})
             if b == 0:
                 continue
             tr.step()
@@ -129,12 +136,15 @@ def run(cfg: Config, mode: str = "single", flavor: str = "flax", out_dir: str = 
             _log(f"\nEpoch {epoch} train loss: {tr_loss:.4f}", rank)
         else:
             _log(f"\nEpoch {epoch} train loss: {tr_loss:.4f}, roc_auc: {tr_auc:.4f}", rank)
-        for batch in evald.batches(EB, shuffle=False, drop_last=False, rank=rank,
-                                   world_size=world):
-            if len(batch["label"]) == 0 and tr.sharded is None:
+        for idx, s, n in evald.batch_slices(EB, shuffle=False, drop_last=False, rank=rank,
+                                            world_size=world):
+            if n == 0 and tr.sharded is None:
                 continue
-            tr.load_batch({k: v.to(dev, non_blocking=True) for k, v in batch.items()},
-                          eval_mode=True)
+            if evald.device == dev:
+                tr.load_columns(evald.cols, idx, s, n, eval_mode=True)
+            else:
+                tr.load_batch({k: v[s: s + n].to(dev, non_blocking=True)
+                               for k, v in evald.cols.items()}, eval_mode=True)
             tr.evaluate_batch()
         ev_loss, ev_auc = tr.pop_metrics(eval_mode=True)
         if flavor == "keras":

@@ -555,3 +555,21 @@ def test_dense_optimizer_slab_segments():
     p2, m2, v2 = p.clone(), torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
     ops.dense_optimizer(p2, g2, m2, v2, None, ops.OPT_ADAMW, hyper, wd=0.01)
     assert torch.allclose(p1, p2, atol=1e-6) and torch.allclose(m1, m2, atol=1e-6)
+
+
+def test_gather_columns_matches_index_select():
+    torch.manual_seed(13)
+    N, n = 5000, 777
+    src = [torch.randint(-100, 100, (N,), device=DEV, dtype=dt)
+           for dt in (torch.int8, torch.int16, torch.int32, torch.int64)]
+    src.append(torch.randn(N, device=DEV))
+    idx = torch.randperm(N, device=DEV)[:n]
+    outi = torch.zeros(4, n, dtype=torch.int64, device=DEV)
+    X = torch.zeros(n, 9, device=DEV)
+    dst = [outi[i] for i in range(4)] + [X.view(-1)[5:]]
+    ops.gather_columns(src, idx, 0, n, dst, [1, 1, 1, 1, 9])
+    for i in range(4):
+        assert torch.equal(outi[i], src[i].index_select(0, idx).long())
+    assert torch.equal(X[:, 5], src[4].index_select(0, idx))
+    ops.gather_columns(src[:1], None, 100, n, [outi[0]], [1])   # contiguous range
+    assert torch.equal(outi[0], src[0][100:100 + n].long())
