@@ -43,6 +43,14 @@ def parse(argv=None):
     return ap.parse_args(argv)
 
 
+# Stock PyTorch-ROCm eager DLRM (nn.EmbeddingBag + nn.Linear, bf16 autocast,
+# sparse Adagrad / AdamW) measured on one MI355X with the same shapes
+# (scripts/baseline_torch_dlrm.py, profiles/torch_eager_baseline_dlrm.jsonl);
+# BASELINE.md protocol item (a). For N GPUs it is scaled by N (perfect
+# scaling assumed for the baseline).
+EAGER_BASELINE_EX_S = {"1tb": 608463.1, "kaggle": 518563.4}
+
+
 def parallelism(plan, world: int) -> str:
     """e.g. "dp8 dense + emb table_wise x8" (embedding sharding kinds from the plan)."""
     if world == 1:
@@ -123,7 +131,11 @@ def main(argv=None):
             "metric": "examples/sec (whole node) DLRM on Criteo-1TB-shaped synthetic",
             "value": round(value, 1), "unit": "examples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": (round(value / (EAGER_BASELINE_EX_S[args.rows] * world), 2)
+                            if args.model == "dlrm" and args.rows in EAGER_BASELINE_EX_S
+                            and args.batch == 8192 else None),
+            "dtype": "bf16",
             "data": "synthetic (Criteo-1TB-shaped, uniform ids, random-init embeddings)",
             "config": {"model": "DLRM" if args.model == "dlrm" else "DCN-v2",
                        "global_batch": B * world, "seq_len": None,
