@@ -29,6 +29,7 @@ inline double u01(uint64_t h) { return (double)(h >> 11) * (1.0 / 90071992547409
 extern "C" {
 
 // ids are table-major: table t holds B * pooling[t] ids. dist: 0 uniform, 1 zipf.
+// w_dense: [num_dense]; table_bias: [T, 64] (label model: per-table bias by id % 64).
 void tdfo_synth_criteo(uint64_t seed, int rank, int64_t batch_index, int B, int num_dense, int T,
                        const int64_t* rows, const int* pooling, int dist, double alpha,
                        const float* w_dense, const float* table_bias, float* dense, int64_t* ids,
