@@ -390,12 +390,74 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(GemmArgs p) {
       glds_piece_asm<B_COL>(p.B, p.ldb, n0, p.N, k0, tb, w * 2 + i, lane);
   };
 
-  if (nk > 0) {
+  // Fragment-pipelined main loop (default): one raw barrier per K tile, in
+  // the middle of it. Iteration t: issue tile t+2's DMA, read tile t's k=32..63
+  // fragments, MFMAs on its k=0..31 fragments (read last iteration) hide that
+  // read, then wait for tile t+1 + barrier, read tile t+1's k=0..31
+  // fragments, and the k=32..63 MFMAs hide those. Ring-slot reuse: slot
+  // (t+2)%3 was last read before iteration t-1's barrier (each wave drains
+  // its LDS reads with lgkmcnt(0) before that barrier).
+  if (nk > 0 && !(p.abl & 16)) {
+    const TDFO_LDS char* tAo = smem + (wr >> 1) * TILE_BYTES;
+    const TDFO_LDS char* tBo = smem + 2 * TILE_BYTES;
+    const int a_r0 = (wr & 1) * 64, b_c0 = wc * 64;
+    auto frags = [&](int buf, int ks, bf16x8_t (&af)[4], bf16x8_t (&bfr)[4]) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        af[i] = A_COL ? frag_col(tAo + buf * LSTAGE, a_r0 + i * 16, ks, lane)
+                      : frag_row(tAo + buf * LSTAGE, a_r0 + i * 16, ks, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        bfr[j] = B_COL ? frag_col(tBo + buf * LSTAGE, b_c0 + j * 16, ks, lane)
+                       : frag_row(tBo + buf * LSTAGE, b_c0 + j * 16, ks, lane);
+    };
+    auto mm = [&](const bf16x8_t (&af)[4], const bf16x8_t (&bfr)[4]) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    };
+    stage(0, kt0);
+    if (nk > 1) stage(1, kt0 + 1);
+    if (nk > 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    bf16x8_t a0[4], b0[4], a1[4], b1[4];
+    frags(0, 0, a0, b0);
+    int cur = 0;
+    // steady state (straight-line body so the compiler's lgkmcnt waits only
+    // cover the reads each MFMA group actually consumes); last tile peeled
+    for (int t = 0; t + 1 < nk; ++t) {
+      __builtin_amdgcn_sched_barrier(0);
+      const bool pre = t + 2 < nk;
+      if (pre) stage(cur == 0 ? 2 : cur - 1, kt0 + t + 2);
+      frags(cur, 1, a1, b1);
+      __builtin_amdgcn_sched_barrier(0);
+      mm(a0, b0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (pre) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+      else     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      cur = cur == 2 ? 0 : cur + 1;
+      frags(cur, 0, a0, b0);
+      __builtin_amdgcn_sched_barrier(0);
+      mm(a1, b1);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    frags(cur, 1, a1, b1);
+    mm(a0, b0);
+    mm(a1, b1);
+  } else if (nk > 0) {
     stage(0, kt0);
     if (nk > 1) stage(1, kt0 + 1);
     int cur = 0;
     for (int t = 0; t < nk; ++t) {
-      if (t + 1 < nk && !p.abl) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      if (t + 1 < nk && !(p.abl & 7)) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
       else            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
@@ -412,7 +474,8 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(GemmArgs p) {
 
 // 0 auto, 1 small tiles only (64-row tiles when 128-row ones underfill),
 // 2 large tiles only, 3 128x128 tiles only, 4 = 1 with 256x128 tiles for
-// the weight-grad (col-A) GEMMs. Auto (default) takes the 256x128 kernel only
+// the weight-grad (col-A) GEMMs, 5 = auto with 64-row tiles below 512
+// 128x128 tiles (instead of 256). Auto (default) takes the 256x128 kernel only
 // for GEMMs with >= 1024 128x128 tiles: in the graph-replayed DLRM-1TB step
 // (<= 512 tiles per GEMM) 128x128 measured 0.725-0.728 ms/step vs 0.735 with
 // the 256x128 kernel from 256 blocks up (profiles/gemm_tile_ab.md); on the
@@ -443,7 +506,8 @@ void launch(const GemmArgs& a, hipStream_t s) {
   } else {
     if constexpr (!AC) {
       // 64-row tiles when 128-row tiles leave CUs idle (bottom MLP, top3)
-      if (small_tiles * a.splits < 256 && g_policy != 3 && g_policy != 2) {
+      const int thr64 = g_policy == 5 ? 512 : 256;
+      if (small_tiles * a.splits < thr64 && g_policy != 3 && g_policy != 2) {
         const int t64 = ((a.M + 63) / 64) * tn;
         dim3 grid(t64, 1, a.splits);
         hipLaunchKernelGGL((gemm_kernel<64, AC, BC>), grid, dim3(256),
