@@ -34,8 +34,8 @@ def parse(argv=None):
     ap.add_argument("--rows", default="1tb", choices=["1tb", "kaggle", "tiny"])
     ap.add_argument("--model", default="dlrm", choices=["dlrm", "dcnv2"])
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--overlap", action="store_true",
-                    help="side streams for wgrads / embedding work")
+    ap.add_argument("--overlap", nargs="?", const="all", default="",
+                    help="side streams: 'all' (wgrads + embedding work) or 'wgrad'")
     ap.add_argument("--pool", type=int, default=8, help="pre-generated device batches")
     ap.add_argument("--dist", default="uniform", choices=["uniform", "zipf"])
     ap.add_argument("--sharding", default="auto",
@@ -81,11 +81,11 @@ def main(argv=None):
             "tiny": [1000] * 26}[args.rows]
     if args.model == "dlrm":
         cfg = DLRMConfig(table_rows=list(rows), sharding=args.sharding,
-                         overlap=args.overlap)
+                         overlap=(args.overlap if args.overlap == 'wgrad' else bool(args.overlap)))
     else:
         cfg = DLRMConfig(table_rows=list(rows), interaction="dcn", pooling=list(MLPERF_MULTIHOT),
                          top=[1024, 1024, 512, 256, 1], sharding=args.sharding,
-                         overlap=args.overlap)
+                         overlap=(args.overlap if args.overlap == 'wgrad' else bool(args.overlap)))
     B = args.batch
     t0 = time.time()
     tr = DLRMTrainer(cfg, B, info.device, group=info.group, rank=info.rank, world_size=world)

@@ -185,6 +185,10 @@ __device__ __forceinline__ void epilogue(const GemmArgs& p, const f32x4_t (&acc)
     const float4 lo = *(const float4*)(ctile + rl * 128 + (((cg >> 2) ^ (rl & 31)) << 2));
     const float4 hi = *(const float4*)(ctile + rl * 128 + ((((cg >> 2) + 1) ^ (rl & 31)) << 2));
     float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    if (p.abl & 64) {                  // perf ablation: LDS staging only, no global stores
+      asm volatile("" :: "v"(lo.x), "v"(lo.y), "v"(lo.z), "v"(lo.w), "v"(hi.x), "v"(hi.y), "v"(hi.z), "v"(hi.w));
+      continue;
+    }
     const int n = n0 + cg;
     if (nfull || n + 8 <= p.N) {
       if (p.mask) {
@@ -468,6 +472,13 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(GemmArgs p) {
                              ta + 2 * TILE_BYTES, wc * 64, lane);
       cur = cur == 2 ? 0 : cur + 1;
     }
+  }
+  if (p.abl & 32) {                 // perf ablation: keep acc live, skip the epilogue
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) asm volatile("" :: "v"(acc[i][j]));
+    return;
   }
   epilogue<LBM, 512>(p, acc, smem_raw, m0, n0, wr, wc, lane, tid);
 }
