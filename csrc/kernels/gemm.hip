@@ -149,7 +149,11 @@ __device__ __forceinline__ bf16x8_t frag_col(const TDFO_LDS char* tile, int c0,
 // ROWS x 128 fp32 tile is staged through the (now idle) LDS ring so global
 // traffic leaves as coalesced 16-B accesses (mask loads, bf16 stores, fp32
 // stores, DCN Hadamard/residual second output).
-// C/D map of 16x16x32: col = lane&15, row = 4*(lane>>4) + reg.
+// The MFMAs run with the B (output-column) fragment as the A operand, so the
+// accumulator holds C transposed: lane l, register r of fragment (i, j) is
+// C[row 16i + (l&15)][col 16j + 4(l>>4) + r] -- four consecutive columns of
+// one row, staged with one 16-B LDS write per fragment (16 per lane instead
+// of 64 scalar writes).
 template <int ROWS, int NT, int MI = 4>
 __device__ __forceinline__ void epilogue(const GemmArgs& p, const f32x4_t (&acc)[MI][4],
                                          char* smem_raw, int m0, int n0, int wr, int wc,
@@ -158,19 +162,24 @@ __device__ __forceinline__ void epilogue(const GemmArgs& p, const f32x4_t (&acc)
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int cl = wc * 64 + j * 16 + (lane & 15);
-    const int n = n0 + cl;
-    const float bias = (p.bias && n < p.N) ? p.bias[(int64_t)n * p.bias_stride] : 0.f;
+    const int cl = wc * 64 + j * 16 + 4 * (lane >> 4);       // first of 4 columns
+    float bias[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = n0 + cl + r;
+      bias[r] = (p.bias && n < p.N) ? p.bias[(int64_t)n * p.bias_stride] : 0.f;
+    }
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
+      const int rl = wr * (MI * 16) + i * 16 + (lane & 15);
+      float v[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int rl = wr * (MI * 16) + i * 16 + 4 * (lane >> 4) + r;
-        float v = acc[i][j][r] + bias;
-        if (p.relu) v = fmaxf(v, 0.f);
-        const int chunk = (cl >> 2) ^ (rl & 31);
-        ctile[rl * 128 + chunk * 4 + (cl & 3)] = v;
+        v[r] = acc[i][j][r] + bias[r];
+        if (p.relu) v[r] = fmaxf(v[r], 0.f);
       }
+      const int chunk = (cl >> 2) ^ (rl & 31);
+      *(float4*)(ctile + rl * 128 + chunk * 4) = make_float4(v[0], v[1], v[2], v[3]);
     }
   }
   __syncthreads();
@@ -272,7 +281,7 @@ __device__ __forceinline__ void mfma_k64(f32x4_t (&acc)[MI][4], const TDFO_LDS c
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
   }
 }
 
@@ -420,7 +429,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(GemmArgs p) {
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     };
     stage(0, kt0);
     if (nk > 1) stage(1, kt0 + 1);
