@@ -675,6 +675,8 @@ TORCH_LIBRARY(tdfo, m) {
   m.def("radix_sort_max_bits(int b) -> int",
         [](int64_t v) { return (int64_t)tdfo::radix_sort_max_bits((int)v); });
   m.def("gemm_policy(int p) -> int", [](int64_t p) { return (int64_t)tdfo::gemm_policy((int)p); });
+  m.def("linear_xent_impl(int p) -> int",
+        [](int64_t p) { return (int64_t)tdfo::linear_xent_impl((int)p); });
   m.def("attention_fwd(Tensor qkv, Tensor ids, int H, float rate, int seed, Tensor? step, int pad_id, "
         "Tensor(a!) out) -> ()");
   m.def("attention_bwd(Tensor qkv, Tensor ids, Tensor dout, int H, float rate, int seed, Tensor? step, "

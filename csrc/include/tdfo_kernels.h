@@ -207,6 +207,9 @@ struct LinearXentArgs {
   void* workspace;
 };
 size_t linear_xent_workspace(int N, int64_t V);
+// 1: f32-input MFMA pass1/wgrad (default), 0: VALU kernels; <0 queries.
+// Returns the previous setting.
+int linear_xent_impl(int impl);
 void linear_xent(const LinearXentArgs& a, hipStream_t s);
 
 // -------------------------------------------------------- attention ----

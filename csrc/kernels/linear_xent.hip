@@ -7,15 +7,21 @@
 // the reference writes and re-reads a [B*T, V] fp32 logits tensor; here:
 //
 //   compact : valid tokens (label != ignore) -> idx[], n_valid (device)
-//   pass1   : grid (vocab split s, token chunk); each thread owns one token,
-//             streams its split's W rows through LDS (broadcast reads) and
-//             keeps an online-softmax state (m, s, acc = sum_v e^{z_v-m} W_v)
-//             -> part[token][s]; chunk-0 blocks also emit sum_v W_v, sum_v b_v
-//   merge   : one wave per token merges the splits: lse, loss, and
+//   pass1   : grid (vocab split s, 128-token block); one wave per block runs
+//             a flash-attention-style pass on the f32-input MFMA
+//             (v_mfma_f32_16x16x4_f32, exact f32): per 16-row W tile and
+//             16-token group, X = W H^T (bias as the C input), a per-token
+//             running max (shared by the 4 lane rows), P = e^{X-m}, and
+//             O^T += W^T P^T with P taken straight from the accumulator
+//             registers -> part[token][s] = (m, sum, O); block-row 0 also
+//             emits sum_v W_v, sum_v b_v
+//   merge   : one 256-thread block per token merges the splits: lse, loss,
 //             dH = scale * (E_p[W] - (1-eps) W_y - eps/V sum_v W_v)
-//   wgrad   : one thread per vocab row v, tokens staged in LDS:
-//             dz = scale * (e^{z-lse} - eps/V - (1-eps)[v==y]);
-//             dW_v = sum_n dz H_n, db_v = sum_n dz   (no atomics)
+//   wgrad   : one wave per run of 16-row tiles: X^T = H W^T on the MFMA,
+//             dz = scale * (e^{z-lse} - eps/V - (1-eps)[v==y]) in registers,
+//             dW^T += H^T dz^T on the MFMA, db_v = sum_n dz (no atomics)
+//   (impl 0 keeps the earlier VALU pass1/wgrad: lane = token / lane = row,
+//    W or H rows through scalar loads — an A/B point for the MFMA path.)
 //
 // loss_n = lse - (1-eps) z_y - eps * mean_v z_v, mean_v z_v = (H.sumW + sumb)/V;
 // scale = 1 / n_valid (mean over non-ignored tokens, torch semantics).
@@ -157,7 +163,19 @@ __global__ __launch_bounds__(64) void xent_pass1_kernel(const float* __restrict_
   }
 }
 
-// one wave per valid token
+// One 256-thread block per valid token: threads stride over the splits,
+// then a wave shuffle + LDS combine of the online-softmax states.
+__device__ __forceinline__ void sm_combine(float& m, float& s, float* acc, float om, float os,
+                                           const float* oacc) {
+  const float nm = fmaxf(m, om);
+  const float c0 = (m == -INFINITY) ? 0.f : __expf(m - nm);
+  const float c1 = (om == -INFINITY) ? 0.f : __expf(om - nm);
+  s = s * c0 + os * c1;
+#pragma unroll
+  for (int k = 0; k < XE; ++k) acc[k] = acc[k] * c0 + oacc[k] * c1;
+  m = nm;
+}
+
 __global__ __launch_bounds__(256) void xent_merge_kernel(const float* __restrict__ H,
                                                          const float* __restrict__ W,
                                                          const float* __restrict__ bias,
@@ -169,58 +187,64 @@ __global__ __launch_bounds__(256) void xent_merge_kernel(const float* __restrict
                                                          const float* __restrict__ wpart,
                                                          float* __restrict__ lse_out,
                                                          float* __restrict__ dH,
-                                                         float* __restrict__ lossv) {
-  const int lane = threadIdx.x & 63;
-  const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
+                                                         float* __restrict__ lossv,
+                                                         float* __restrict__ htok,
+                                                         int32_t* __restrict__ ytok) {
+  __shared__ float red[4][XP + XE + 1];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int j = blockIdx.x;
   const int nv = *count;
   if (j >= nv) return;
   const float scale = 1.f / (float)max(1, nv);
-  // merge online-softmax states over splits
-  float m = -INFINITY, sum = 0.f, acc[XE];
+  float m = -INFINITY, sum = 0.f, acc[XE], ws[XE + 1];
 #pragma unroll
   for (int k = 0; k < XE; ++k) acc[k] = 0.f;
-  const float* p0 = part + (int64_t)j * S * XP;
-  for (int s = lane; s < S; s += 64) {
-    const float* p = p0 + (int64_t)s * XP;
-    const float pm = p[0];
-    if (pm == -INFINITY) continue;
-    const float nm = fmaxf(m, pm);
-    const float c0 = __expf(m - nm), c1 = __expf(pm - nm);
-    sum = sum * c0 + p[1] * c1;
-#pragma unroll
-    for (int k = 0; k < XE; ++k) acc[k] = acc[k] * c0 + p[2 + k] * c1;
-    m = nm;
-  }
-  // wave reduction of (m, sum, acc)
-  for (int off = 32; off > 0; off >>= 1) {
-    const float om = __shfl_xor(m, off);
-    const float os = __shfl_xor(sum, off);
-    const float nm = fmaxf(m, om);
-    const float c0 = (m == -INFINITY) ? 0.f : __expf(m - nm);
-    const float c1 = (om == -INFINITY) ? 0.f : __expf(om - nm);
-    sum = sum * c0 + os * c1;
-#pragma unroll
-    for (int k = 0; k < XE; ++k) {
-      const float oa = __shfl_xor(acc[k], off);
-      acc[k] = acc[k] * c0 + oa * c1;
-    }
-    m = nm;
-  }
-  // sum_v [W_v | b_v]
-  float ws[XE + 1];
 #pragma unroll
   for (int k = 0; k <= XE; ++k) ws[k] = 0.f;
-  for (int s = lane; s < S; s += 64) {
+  const float* p0 = part + (int64_t)j * S * XP;
+  for (int s = tid; s < S; s += 256) {
+    const f32x4_t* p = (const f32x4_t*)(p0 + (int64_t)s * XP);
+    float r[XP];
 #pragma unroll
-    for (int k = 0; k <= XE; ++k) ws[k] += wpart[(int64_t)s * (XE + 1) + k];
+    for (int q = 0; q < XP / 4; ++q) {
+      const f32x4_t v = p[q];
+      r[4 * q] = v[0]; r[4 * q + 1] = v[1]; r[4 * q + 2] = v[2]; r[4 * q + 3] = v[3];
+    }
+    if (r[0] != -INFINITY) sm_combine(m, sum, acc, r[0], r[1], r + 2);
+    const float* wp = wpart + (int64_t)s * (XE + 1);
+#pragma unroll
+    for (int k = 0; k <= XE; ++k) ws[k] += wp[k];
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    float o[XE];
+#pragma unroll
+    for (int k = 0; k < XE; ++k) o[k] = __shfl_xor(acc[k], off);
+    sm_combine(m, sum, acc, __shfl_xor(m, off), __shfl_xor(sum, off), o);
   }
 #pragma unroll
   for (int k = 0; k <= XE; ++k) ws[k] = wave_sum(ws[k]);
-  if (lane != 0) return;
+  if (lane == 0) {
+    red[w][0] = m;
+    red[w][1] = sum;
+#pragma unroll
+    for (int k = 0; k < XE; ++k) red[w][2 + k] = acc[k];
+#pragma unroll
+    for (int k = 0; k <= XE; ++k) red[w][XP + k] = ws[k];
+  }
+  __syncthreads();
+  if (tid != 0) return;
+  for (int q = 1; q < 4; ++q) {
+    sm_combine(m, sum, acc, red[q][0], red[q][1], &red[q][2]);
+#pragma unroll
+    for (int k = 0; k <= XE; ++k) ws[k] += red[q][XP + k];
+  }
   const int n = idx[j];
   const float* hr = H + (int64_t)n * XE;
   int64_t y = labels[n];
   if (y < 0 || y >= V) y = 0;   // host validates; never read out of bounds
+  ytok[j] = (int32_t)y;
+#pragma unroll
+  for (int k = 0; k < XE; k += 4) *(f32x4_t*)(htok + (int64_t)j * XE + k) = *(const f32x4_t*)(hr + k);
   const float* wy = W + y * XE;
   float zy = bias[y], zmean = ws[XE];
 #pragma unroll
@@ -234,8 +258,13 @@ __global__ __launch_bounds__(256) void xent_merge_kernel(const float* __restrict
   lossv[n] = lse - (1.f - eps) * zy - eps * zmean;
   const float inv = 1.f / sum;
 #pragma unroll
-  for (int k = 0; k < XE; ++k)
-    dH[(int64_t)n * XE + k] = scale * (acc[k] * inv - (1.f - eps) * wy[k] - eps * ws[k] / (float)V);
+  for (int k = 0; k < XE; k += 4) {
+    float d[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      d[e] = scale * (acc[k + e] * inv - (1.f - eps) * wy[k + e] - eps * ws[k + e] / (float)V);
+    *(float4*)(dH + (int64_t)n * XE + k) = make_float4(d[0], d[1], d[2], d[3]);
+  }
 }
 
 // One thread per vocab row; the tokens are wave-uniform (scalar loads of
@@ -289,28 +318,449 @@ __global__ __launch_bounds__(256) void xent_wgrad_kernel(const float* __restrict
   }
 }
 
+
+// ------------------------------------------------------------ MFMA path --
+// v_mfma_f32_16x16x4_f32 lane maps (16x16 tiles, lane l: t = l&15, g = l>>4):
+// A[i=t][k=g], B[k=g][j=t], C/D[row 4g+r][col t]. The hidden dim (16) is the
+// contraction of the first product; it is walked as k-step s <-> dim 4g+s, so
+// every W/H operand of it is one float4 per lane.
+constexpr int XG = 8;           // 16-token groups per wave (128 tokens)
+// Logits are produced in log2 units (H and b pre-scaled by log2 e), so every
+// softmax term is one v_sub + v_exp_f32.
+constexpr float LOG2E = 1.4426950408889634f;
+constexpr float LN2 = 0.6931471805599453f;
+
+__device__ __forceinline__ float exp2_fast(float x) { return __builtin_amdgcn_exp2f(x); }
+
+__device__ __forceinline__ f32x4_t mfma4(float a, float b, f32x4_t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float max4rows(float v) {     // max over lanes t, t+16, t+32, t+48
+  v = fmaxf(v, __shfl_xor(v, 16));
+  return fmaxf(v, __shfl_xor(v, 32));
+}
+
+__device__ __forceinline__ float sum4rows(float v) {
+  v += __shfl_xor(v, 16);
+  return v + __shfl_xor(v, 32);
+}
+
+struct XentTile {               // one 16-row W tile in both operand layouts
+  f32x4_t wa;                   // W[r0+t][4g..4g+3]
+  float wb[4];                  // W[r0+4g+r][t]
+  float bb[4];                  // bias[r0+4g+r]
+};
+
+__device__ __forceinline__ void xent_load_tile(XentTile& T, const float* __restrict__ W,
+                                               const float* __restrict__ bias, int64_t r0,
+                                               int64_t v1, int t, int g) {
+  const int64_t ra = min(r0 + t, v1 - 1);
+  T.wa = *(const f32x4_t*)(W + ra * XE + 4 * g);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int64_t rb = min(r0 + 4 * g + r, v1 - 1);
+    T.wb[r] = W[rb * XE + t];
+    T.bb[r] = bias[rb];
+  }
+}
+
+// Lazy rescaling: the running max m (log2 units) only moves when a logit
+// exceeds it by more than XTH (2^12 headroom keeps p and the sums far from
+// overflow); the (m, sum, O) triple is consistent for any m, so the merge is
+// unaffected.
+constexpr float XTH = 12.f;
+
+// One 16-row tile of the online softmax for NG token groups: X = W H^T (bias
+// as C input), lazy max update, P = 2^{X-m}, O^T += W^T P^T.
+template <int NG>
+__device__ __forceinline__ void xent_pass1_tile(const XentTile& T, const f32x4_t* hb,
+                                                const float* bb, f32x4_t* o, float* m,
+                                                float* sum) {
+  f32x4_t x[NG];
+  bool up = false;
+#pragma unroll
+  for (int q = 0; q < NG; ++q) {
+    x[q] = (f32x4_t){bb[0], bb[1], bb[2], bb[3]};
+    x[q] = mfma4(T.wa[0], hb[q][0], x[q]);
+    x[q] = mfma4(T.wa[1], hb[q][1], x[q]);
+    x[q] = mfma4(T.wa[2], hb[q][2], x[q]);
+    x[q] = mfma4(T.wa[3], hb[q][3], x[q]);
+    up |= fmaxf(fmaxf(x[q][0], x[q][1]), fmaxf(x[q][2], x[q][3])) > m[q] + XTH;
+  }
+  if (__any(up)) {                         // wave-uniform; first tile and rare after
+#pragma unroll
+    for (int q = 0; q < NG; ++q) {
+      const float mx = max4rows(fmaxf(fmaxf(x[q][0], x[q][1]), fmaxf(x[q][2], x[q][3])));
+      const float nm = fmaxf(m[q], mx);     // finite: row r0 of a tile is always valid
+      const float c = exp2_fast(m[q] - nm);
+      sum[q] *= c;
+      o[q] *= c;
+      m[q] = nm;
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < NG; ++q) {
+    float p[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) p[r] = exp2_fast(x[q][r] - m[q]);
+    sum[q] += (p[0] + p[1]) + (p[2] + p[3]);
+    o[q] = mfma4(T.wb[0], p[0], o[q]);
+    o[q] = mfma4(T.wb[1], p[1], o[q]);
+    o[q] = mfma4(T.wb[2], p[2], o[q]);
+    o[q] = mfma4(T.wb[3], p[3], o[q]);
+  }
+}
+
+// Full tiles: a wave-uniform tile pointer plus constant per-lane offsets
+// (no clamps, no masks), two tiles per iteration from a 2-slot register ring.
+__device__ __forceinline__ void xent_load_full(XentTile& T, const float* __restrict__ Wt,
+                                               const float* __restrict__ bt, int la, int t, int g) {
+  T.wa = *(const f32x4_t*)(Wt + la);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    T.wb[r] = Wt[(4 * g + r) * XE + t];
+    T.bb[r] = bt[4 * g + r];
+  }
+}
+
+template <int NG>
+__device__ __forceinline__ void xent_pass1_body(const float* __restrict__ H,
+                                                const float* __restrict__ W,
+                                                const float* __restrict__ bias, int64_t v0,
+                                                int64_t v1, int S, int s,
+                                                const int32_t* __restrict__ idx, int nv,
+                                                int tok0, float* __restrict__ part, int t, int g) {
+  f32x4_t hb[NG], o[NG];
+  float m[NG], sum[NG];
+#pragma unroll
+  for (int q = 0; q < NG; ++q) {
+    const int j = tok0 + 16 * q + t;
+    hb[q] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    if (j < nv) hb[q] = *(const f32x4_t*)(H + (int64_t)idx[j] * XE + 4 * g) * LOG2E;
+    o[q] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    m[q] = -INFINITY;
+    sum[q] = 0.f;
+  }
+  const int la = t * XE + 4 * g;
+  const int nfull = (int)((v1 - v0) / 16);
+  const float* Wt = W + v0 * XE;
+  const float* bt = bias + v0;
+  XentTile ta, tb;
+  if (nfull > 0) xent_load_full(ta, Wt, bt, la, t, g);
+  if (nfull > 1) xent_load_full(tb, Wt + 16 * XE, bt + 16, la, t, g);
+  for (int i = 0; i < nfull; i += 2) {
+    {
+      const XentTile cur = ta;
+      if (i + 2 < nfull) xent_load_full(ta, Wt + (i + 2) * 16 * XE, bt + (i + 2) * 16, la, t, g);
+      float bb[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bb[r] = cur.bb[r] * LOG2E;
+      xent_pass1_tile<NG>(cur, hb, bb, o, m, sum);
+    }
+    if (i + 1 < nfull) {
+      const XentTile cur = tb;
+      if (i + 3 < nfull) xent_load_full(tb, Wt + (i + 3) * 16 * XE, bt + (i + 3) * 16, la, t, g);
+      float bb[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bb[r] = cur.bb[r] * LOG2E;
+      xent_pass1_tile<NG>(cur, hb, bb, o, m, sum);
+    }
+  }
+  const int64_t r0 = v0 + 16 * (int64_t)nfull;
+  if (r0 < v1) {                           // ragged last tile of the vocabulary
+    XentTile cur;
+    xent_load_tile(cur, W, bias, r0, v1, t, g);
+    float bb[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bb[r] = r0 + 4 * g + r < v1 ? cur.bb[r] * LOG2E : -INFINITY;
+    xent_pass1_tile<NG>(cur, hb, bb, o, m, sum);
+  }
+#pragma unroll
+  for (int q = 0; q < NG; ++q) {
+    const float tot = sum4rows(sum[q]);
+    const int j = tok0 + 16 * q + t;
+    if (j < nv) {
+      float* p = part + ((int64_t)j * S + s) * XP;
+      *(f32x4_t*)(p + 2 + 4 * g) = o[q];     // O^T[4g+r][t] = O[t][4g+r]
+      if (g == 0) {
+        p[0] = m[q] * LN2;
+        p[1] = tot;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void xent_pass1_mfma_kernel(const float* __restrict__ H,
+                                                             const float* __restrict__ W,
+                                                             const float* __restrict__ bias,
+                                                             int64_t V, int64_t VS, int S,
+                                                             const int32_t* __restrict__ idx,
+                                                             const int32_t* __restrict__ count,
+                                                             float* __restrict__ part,
+                                                             float* __restrict__ wpart) {
+  const int s = blockIdx.x, l = threadIdx.x, t = l & 15, g = l >> 4;
+  const int nv = *count;
+  const int tok0 = blockIdx.y * 16 * XG;
+  const int ng = min(XG, max(0, (nv - tok0 + 15) / 16));
+  const int64_t v0 = (int64_t)s * VS, v1 = min(V, v0 + VS);
+  if (blockIdx.y == 0) {          // column sums of [W | b] over the split
+    f32x4_t cs = {0.f, 0.f, 0.f, 0.f};
+    float bs = 0.f;
+    for (int64_t r = v0 + t; r < v1; r += 16) cs += *(const f32x4_t*)(W + r * XE + 4 * g);
+    for (int64_t r = v0 + l; r < v1; r += 64) bs += bias[r];
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) cs[e] += __shfl_xor(cs[e], off);
+    bs = wave_sum(bs);
+    float* wp = wpart + (int64_t)s * (XE + 1);
+    if (t == 0) *(f32x4_t*)(wp + 4 * g) = cs;
+    if (l == 0) wp[XE] = bs;
+  }
+  switch (ng) {
+#define XCASE(n) \
+    case n: xent_pass1_body<n>(H, W, bias, v0, v1, S, s, idx, nv, tok0, part, t, g); break;
+    XCASE(1) XCASE(2) XCASE(3) XCASE(4) XCASE(5) XCASE(6) XCASE(7) XCASE(8)
+#undef XCASE
+    default: break;
+  }
+}
+
+// wgrad token operands, staged by the merge kernel as htok[j][16] (H rows in
+// valid-token order) and ytok[j] (int32 labels): no idx indirection here.
+// Padding tokens get hb = 0 (no dW contribution), lse = +inf (e = 0) and
+// y = -1; their constant -eps/V terms in db are removed once per run.
+struct XentTok {
+  f32x4_t ha;                   // H[tok t][4g..4g+3] * log2 e  (A of X^T = H W^T)
+  float hb[4];                  // H[tok 4g+r][t] * scale       (A of dW^T = H^T dz^T)
+  float lse[4];                 // per C row 4g+r, log2 units
+  int y[4];
+};
+
+__device__ __forceinline__ void xent_load_tok(XentTok& K, const float* __restrict__ htok,
+                                              const int32_t* __restrict__ ytok,
+                                              const float* __restrict__ lse, int j0, int nv,
+                                              float scale, int t, int g) {
+  const int ja = j0 + t;
+  K.ha = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  if (ja < nv) K.ha = *(const f32x4_t*)(htok + (int64_t)ja * XE + 4 * g) * LOG2E;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int jb = j0 + 4 * g + r;
+    const bool ok = jb < nv;
+    K.hb[r] = ok ? htok[(int64_t)jb * XE + t] * scale : 0.f;
+    K.lse[r] = ok ? lse[jb] * LOG2E : INFINITY;
+    K.y[r] = ok ? ytok[jb] : -1;
+  }
+}
+
+// One 16-row tile for NG token groups: X^T = H W^T (bias as C input), dz in
+// registers, dW^T = H^T dz^T; writes dW rows (float4 per lane) and db.
+template <int NG>
+__device__ __forceinline__ void xent_wgrad_tile(const XentTok* K, f32x4_t wa, float b, int v,
+                                                int64_t V, float off, float hit, float pad_off,
+                                                float scale, float* __restrict__ dW,
+                                                float* __restrict__ db, int g) {
+  f32x4_t dw[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  float dbs = 0.f;
+#pragma unroll
+  for (int q = 0; q < NG; ++q) {
+    f32x4_t x = {b, b, b, b};
+    x = mfma4(K[q].ha[0], wa[0], x);
+    x = mfma4(K[q].ha[1], wa[1], x);
+    x = mfma4(K[q].ha[2], wa[2], x);
+    x = mfma4(K[q].ha[3], wa[3], x);
+    float dz[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float d = exp2_fast(x[r] - K[q].lse[r]) - off;
+      if (K[q].y[r] == v) d -= hit;
+      dz[r] = d;
+    }
+    dbs += (dz[0] + dz[1]) + (dz[2] + dz[3]);
+    f32x4_t& acc = dw[q & 1];
+    acc = mfma4(K[q].hb[0], dz[0], acc);
+    acc = mfma4(K[q].hb[1], dz[1], acc);
+    acc = mfma4(K[q].hb[2], dz[2], acc);
+    acc = mfma4(K[q].hb[3], dz[3], acc);
+  }
+  dbs = (sum4rows(dbs) + pad_off) * scale;
+  if (v < V) {
+    *(f32x4_t*)(dW + (int64_t)v * XE + 4 * g) = dw[0] + dw[1];    // dW^T[4g+r][v]
+    if (g == 0) db[v] = dbs;
+  }
+}
+
+// Full tiles read through a wave-uniform tile pointer + constant lane
+// offsets from a 2-slot register ring (two tiles per iteration).
+template <int NG>
+__device__ __forceinline__ void xent_wgrad_body(const float* __restrict__ W,
+                                                const float* __restrict__ bias, int64_t V,
+                                                float eps, int64_t tile0, int tpw,
+                                                const float* __restrict__ htok,
+                                                const int32_t* __restrict__ ytok,
+                                                const float* __restrict__ lse, int nv, int tok0,
+                                                float* __restrict__ dW, float* __restrict__ db,
+                                                int t, int g) {
+  const float scale = 1.f / (float)max(1, nv);
+  const float off = eps / (float)V, hit = 1.f - eps;
+  XentTok K[NG];
+#pragma unroll
+  for (int q = 0; q < NG; ++q) xent_load_tok(K[q], htok, ytok, lse, tok0 + 16 * q, nv, scale, t, g);
+  const float pad_off = (float)(16 * NG - min(nv - tok0, 16 * NG)) * off;
+  const int64_t tile1 = min(tile0 + tpw, V / 16);        // full tiles
+  const int nfull = (int)max<int64_t>(0, tile1 - tile0);
+  const int la = t * XE + 4 * g;
+  const float* Wt = W + tile0 * 16 * XE;
+  const float* bt = bias + tile0 * 16;
+  const int vb = (int)(tile0 * 16) + t;
+  f32x4_t wa0, wa1;
+  float b0, b1;
+  if (nfull > 0) { wa0 = *(const f32x4_t*)(Wt + la); b0 = bt[t]; }
+  if (nfull > 1) { wa1 = *(const f32x4_t*)(Wt + 16 * XE + la); b1 = bt[16 + t]; }
+  for (int i = 0; i < nfull; i += 2) {
+    {
+      const f32x4_t wa = wa0;
+      const float b = b0 * LOG2E;
+      if (i + 2 < nfull) {
+        wa0 = *(const f32x4_t*)(Wt + (i + 2) * 16 * XE + la);
+        b0 = bt[(i + 2) * 16 + t];
+      }
+      xent_wgrad_tile<NG>(K, wa, b, vb + 16 * i, V, off, hit, pad_off, scale, dW, db, g);
+    }
+    if (i + 1 < nfull) {
+      const f32x4_t wa = wa1;
+      const float b = b1 * LOG2E;
+      if (i + 3 < nfull) {
+        wa1 = *(const f32x4_t*)(Wt + (i + 3) * 16 * XE + la);
+        b1 = bt[(i + 3) * 16 + t];
+      }
+      xent_wgrad_tile<NG>(K, wa, b, vb + 16 * (i + 1), V, off, hit, pad_off, scale, dW, db, g);
+    }
+  }
+  const int64_t rt = V / 16;                             // ragged last tile
+  if (V % 16 != 0 && rt >= tile0 && rt < tile0 + tpw) {
+    const int64_t vr = min(rt * 16 + t, V - 1);
+    const f32x4_t wa = *(const f32x4_t*)(W + vr * XE + 4 * g);
+    xent_wgrad_tile<NG>(K, wa, bias[vr] * LOG2E, (int)(rt * 16) + t, V, off, hit, pad_off, scale,
+                        dW, db, g);
+  }
+}
+
+// grid (runs of `tpw` 16-row tiles, 128-token blocks). Block-row 0 writes
+// dW/db; block-row k > 0 writes slab k-1 ([V][16] + [V]), summed by
+// xent_slab_reduce_kernel — no atomics, fixed order.
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void xent_wgrad_mfma_kernel(const float* __restrict__ W,
+                                                             const float* __restrict__ bias,
+                                                             int64_t V, float eps, int tpw,
+                                                             const float* __restrict__ htok,
+                                                             const int32_t* __restrict__ ytok,
+                                                             const int32_t* __restrict__ count,
+                                                             const float* __restrict__ lse,
+                                                             float* __restrict__ dW,
+                                                             float* __restrict__ db,
+                                                             float* __restrict__ slab) {
+  const int l = threadIdx.x, t = l & 15, g = l >> 4;
+  const int nv = *count;
+  const int tb = blockIdx.y, tok0 = tb * 16 * XG;
+  const int ng = min(XG, max(0, (nv - tok0 + 15) / 16));
+  if (tb > 0 && ng == 0) return;
+  float* dWo = dW;
+  float* dbo = db;
+  if (tb > 0) {
+    dWo = slab + (int64_t)(tb - 1) * V * (XE + 1);
+    dbo = dWo + V * XE;
+  }
+  const int64_t tile0 = (int64_t)blockIdx.x * tpw;
+  switch (ng) {
+#define XCASE(n)                                                                            \
+    case n:                                                                                 \
+      xent_wgrad_body<n>(W, bias, V, eps, tile0, tpw, htok, ytok, lse, nv, tok0, dWo, dbo, \
+                         t, g);                                                             \
+      break;
+    XCASE(1) XCASE(2) XCASE(3) XCASE(4) XCASE(5) XCASE(6) XCASE(7) XCASE(8)
+#undef XCASE
+    default: {                    // no valid token: dW = db = 0 for this run
+      const int64_t r1 = min((tile0 + tpw) * 16, V);
+      for (int64_t v = tile0 * 16 + t; v < r1; v += 16) {
+        *(f32x4_t*)(dWo + v * XE + 4 * g) = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+        if (g == 0) dbo[v] = 0.f;
+      }
+    }
+  }
+}
+
+// dW/db += the active slabs (token blocks 1..nblk-1), fixed order.
+__global__ __launch_bounds__(256) void xent_slab_reduce_kernel(int64_t V,
+                                                               const int32_t* __restrict__ count,
+                                                               const float* __restrict__ slab,
+                                                               float* __restrict__ dW,
+                                                               float* __restrict__ db) {
+  const int nblk = (*count + 16 * XG - 1) / (16 * XG);
+  if (nblk <= 1) return;
+  const int64_t n4 = V * XE / 4;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4 + V;
+       i += (int64_t)gridDim.x * 256) {
+    if (i < n4) {
+      f32x4_t a = ((f32x4_t*)dW)[i];
+      for (int k = 1; k < nblk; ++k)
+        a += ((const f32x4_t*)(slab + (int64_t)(k - 1) * V * (XE + 1)))[i];
+      ((f32x4_t*)dW)[i] = a;
+    } else {
+      const int64_t v = i - n4;
+      float a = db[v];
+      for (int k = 1; k < nblk; ++k) a += slab[(int64_t)(k - 1) * V * (XE + 1) + V * XE + v];
+      db[v] = a;
+    }
+  }
+}
+
 }  // namespace
 
-// ~8 waves per SIMD for pass1 (one wave per (split, 64-token chunk)); the
+int g_xent_impl = 1;           // 1: MFMA pass1/wgrad, 0: VALU kernels
+
+// VALU pass1: ~8 waves per SIMD (one wave per (split, 64-token chunk)).
+// MFMA pass1: ~2048 splits of whole 16-row tiles per 128-token block. The
 // number of valid tokens is device-side, so size for the capacity N.
 void linear_xent_splits(int N, int64_t V, int64_t* VS, int* S) {
-  const int chunks = std::max(1, (N + 63) / 64);
-  int64_t want = std::min<int64_t>(8192, std::max<int64_t>(64, 16384 / chunks));
-  int64_t vs = std::max<int64_t>(64, (V + want - 1) / want);
+  int64_t vs;
+  if (g_xent_impl == 1) {
+    const int blocks = std::max(1, (N + 16 * XG - 1) / (16 * XG));
+    const int64_t want = std::max(64, std::min(2048, 8192 / blocks));
+    vs = std::max<int64_t>(16, (V + want - 1) / want);
+    vs = (vs + 15) / 16 * 16;
+  } else {
+    const int chunks = std::max(1, (N + 63) / 64);
+    int64_t want = std::min<int64_t>(8192, std::max<int64_t>(64, 16384 / chunks));
+    vs = std::max<int64_t>(64, (V + want - 1) / want);
+  }
   *VS = vs;
   *S = (int)((V + vs - 1) / vs);
 }
+
+int linear_xent_impl(int impl) {
+  const int old = g_xent_impl;
+  if (impl >= 0) g_xent_impl = impl ? 1 : 0;
+  return old;
+}
+
+static int xent_blocks(int N) { return std::max(1, (N + 16 * XG - 1) / (16 * XG)); }
 
 size_t linear_xent_workspace(int N, int64_t V) {
   int64_t VS;
   int S;
   linear_xent_splits(N, V, &VS, &S);
-  // idx[N] + count + lse[N] (ints/floats) + part[N][S][XP] + wpart[S][17]
-  return (size_t)(2 * N + 16) * 4 + (size_t)N * S * XP * 4 + (size_t)S * (XE + 1) * 4 + 256;
+  // idx[N] + count + lse[N] + ytok[N] (ints/floats) + htok[N][16] + part[N][S][XP]
+  // + wpart[S][17] + wgrad slabs[(blocks-1)][V][17]
+  return (size_t)(3 * N + 16) * 4 + (size_t)N * XE * 4 + (size_t)N * S * XP * 4 +
+         (size_t)S * (XE + 1) * 4 + (size_t)(xent_blocks(N) - 1) * V * (XE + 1) * 4 + 512;
 }
 
 void linear_xent(const LinearXentArgs& a, hipStream_t s) {
   if (a.N <= 0) return;
+  if (a.V <= 0 || a.V >= (int64_t(1) << 31))
+    throw std::runtime_error("linear_xent: vocab must be in [1, 2^31)");
   int64_t VS;
   int S;
   linear_xent_splits(a.N, a.V, &VS, &S);
@@ -321,16 +771,37 @@ void linear_xent(const LinearXentArgs& a, hipStream_t s) {
   float* part = lse + a.N;
   part = (float*)(((uintptr_t)part + 15) & ~(uintptr_t)15);
   float* wpart = part + (int64_t)a.N * S * XP;
+  int32_t* ytok = (int32_t*)(wpart + (int64_t)S * (XE + 1));
+  float* htok = (float*)(((uintptr_t)(ytok + a.N) + 15) & ~(uintptr_t)15);
+  float* slab = htok + (int64_t)a.N * XE;
   hipLaunchKernelGGL(xent_compact_kernel, dim3(1), dim3(1024), 0, s, a.labels, a.N, a.ignore, idx,
                      count, a.dH, a.lossv);
-  const int chunks = (a.N + 63) / 64;
-  hipLaunchKernelGGL(xent_pass1_kernel, dim3(S, chunks), dim3(64), 0, s, a.H, a.W, a.bias, a.V, VS,
-                     S, idx, count, part, wpart);
-  hipLaunchKernelGGL(xent_merge_kernel, dim3((a.N + 3) / 4), dim3(256), 0, s, a.H, a.W, a.bias,
-                     a.labels, a.V, S, a.eps, idx, count, part, wpart, lse, a.dH, a.lossv);
-  if (a.dW)
-    hipLaunchKernelGGL(xent_wgrad_kernel, dim3((unsigned)((a.V + 255) / 256)), dim3(256), 0, s,
-                       a.H, a.W, a.bias, a.labels, a.V, a.eps, idx, count, lse, a.dW, a.db);
+  const int blocks = xent_blocks(a.N);
+  if (g_xent_impl == 1) {
+    hipLaunchKernelGGL(xent_pass1_mfma_kernel, dim3(S, blocks), dim3(64), 0, s, a.H, a.W, a.bias,
+                       a.V, VS, S, idx, count, part, wpart);
+  } else {
+    const int chunks = (a.N + 63) / 64;
+    hipLaunchKernelGGL(xent_pass1_kernel, dim3(S, chunks), dim3(64), 0, s, a.H, a.W, a.bias, a.V,
+                       VS, S, idx, count, part, wpart);
+  }
+  hipLaunchKernelGGL(xent_merge_kernel, dim3(a.N), dim3(256), 0, s, a.H, a.W, a.bias, a.labels,
+                     a.V, S, a.eps, idx, count, part, wpart, lse, a.dH, a.lossv, htok, ytok);
+  if (a.dW) {
+    if (g_xent_impl == 1) {
+      const int64_t tiles = (a.V + 15) / 16;
+      const int tpw = (int)std::max<int64_t>(1, (tiles + 4095) / 4096);
+      hipLaunchKernelGGL(xent_wgrad_mfma_kernel,
+                         dim3((unsigned)((tiles + tpw - 1) / tpw), blocks), dim3(64), 0, s, a.W,
+                         a.bias, a.V, a.eps, tpw, htok, ytok, count, lse, a.dW, a.db, slab);
+      if (blocks > 1)
+        hipLaunchKernelGGL(xent_slab_reduce_kernel, dim3(2048), dim3(256), 0, s, a.V, count,
+                           slab, a.dW, a.db);
+    } else {
+      hipLaunchKernelGGL(xent_wgrad_kernel, dim3((unsigned)((a.V + 255) / 256)), dim3(256), 0, s,
+                         a.H, a.W, a.bias, a.labels, a.V, a.eps, idx, count, lse, a.dW, a.db);
+    }
+  }
   TDFO_CHECK_HIP(hipGetLastError());
 }
 

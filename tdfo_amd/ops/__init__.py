@@ -33,6 +33,12 @@ def gemm_policy(p: int = -1) -> int:
     return int(_native().gemm_policy(p))
 
 
+def linear_xent_impl(p: int = -1) -> int:
+    """Fused Linear+CE kernel family: 1 f32-input MFMA (default), 0 VALU;
+    p < 0 only reads it. Returns the previous one."""
+    return int(_native().linear_xent_impl(p))
+
+
 def linear_fwd(x, w, bias=None, relu=False, out=None):
     """out = act(x @ w^T + bias); x [M,K] bf16, w [N,K] bf16."""
     if out is None:

@@ -17,10 +17,20 @@ def _native():
     assert _ext.load(), "native library must load on the GPU box"
 
 
-@pytest.mark.parametrize("V,N", [(10, 7), (1000, 320), (4099, 1030), (600_001, 320)])
-def test_linear_xent_kernel_matches_reference(V, N):
+@pytest.fixture(params=[1, 0], ids=["mfma", "valu"])
+def xent_impl(request):
+    old = ops.linear_xent_impl(request.param)
+    yield request.param
+    ops.linear_xent_impl(old)
+
+
+@pytest.mark.parametrize("V,N,hs", [(10, 7, 1.0), (1000, 320, 1.0), (4099, 1030, 1.0),
+                                    (600_001, 320, 1.0), (5003, 200, 12.0)])
+def test_linear_xent_kernel_matches_reference(V, N, hs, xent_impl):
+    """hs scales H: large logits exercise the running-max rescale; N=1030
+    (~410 valid tokens) takes the multi-block token paths."""
     torch.manual_seed(N)
-    H = torch.randn(N, 16, device=DEV)
+    H = torch.randn(N, 16, device=DEV) * hs
     W = torch.randn(V, 16, device=DEV) * 0.2
     b = torch.randn(V, device=DEV) * 0.1
     y = torch.randint(1, V, (N,), device=DEV)
@@ -36,7 +46,7 @@ def test_linear_xent_kernel_matches_reference(V, N):
         assert err < 2e-4, (name, err)
 
 
-def test_linear_xent_all_ignored():
+def test_linear_xent_all_ignored(xent_impl):
     N, V = 64, 100
     H = torch.randn(N, 16, device=DEV)
     W = torch.randn(V, 16, device=DEV)
