@@ -1,0 +1,56 @@
+#!/usr/bin/env python
+"""Our HIP GEMM vs torch.matmul (hipBLASLt) on the DLRM MLP shapes, bf16,
+same process, CUDA-event timing over many iterations."""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from tdfo_amd import ops  # noqa: E402
+
+SHAPES = [(8192, 1024, 512), (8192, 1024, 1024), (8192, 512, 1024), (8192, 256, 512),
+          (8192, 512, 256), (8192, 256, 128)]
+
+
+def timeit(fn, it=200):
+    for _ in range(10):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(it):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / it * 1e3
+
+
+def main():
+    bf = torch.bfloat16
+    for M, N, K in SHAPES:
+        x = torch.randn(M, K, device="cuda").to(bf)
+        w = torch.randn(N, K, device="cuda").to(bf)
+        b = torch.randn(N, device="cuda").to(bf)
+        y = torch.empty(M, N, device="cuda", dtype=bf)
+        dy = torch.randn(M, N, device="cuda").to(bf)
+        dx = torch.empty(M, K, device="cuda", dtype=bf)
+        gw = torch.empty(N * K, device="cuda")
+        ours = timeit(lambda: ops.linear_fwd(x, w, None, True, out=y))
+        ours_d = timeit(lambda: ops.linear_dgrad(dy, w, mask=x, out=dx))
+        ours_w = timeit(lambda: ops.linear_wgrad(dy, x, gw))
+        blas = timeit(lambda: torch.nn.functional.linear(x, w, b))
+        blas_relu = timeit(lambda: torch.relu(torch.nn.functional.linear(x, w, b)))
+        blas_d = timeit(lambda: dy @ w)
+        blas_w = timeit(lambda: dy.t() @ x)
+        tf = 2 * M * N * K / 1e12
+        print(json.dumps({"M": M, "N": N, "K": K, "ours_fwd_us": round(ours, 2),
+                          "blas_fwd_us": round(blas, 2), "blas_fwd_relu_us": round(blas_relu, 2),
+                          "ours_dgrad_us": round(ours_d, 2), "blas_dgrad_us": round(blas_d, 2),
+                          "ours_wgrad_us": round(ours_w, 2), "blas_wgrad_us": round(blas_w, 2),
+                          "ours_fwd_tflops": round(tf / ours * 1e6, 1),
+                          "blas_fwd_tflops": round(tf / blas * 1e6, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -271,6 +271,9 @@ class DLRMTrainer:
         # size 1 the embedding lookup/update run beside the bottom MLP. The
         # forks/joins are stream-event edges, so a captured hipGraph keeps the
         # concurrency as parallel branches.
+        # multi-rank: top wgrads after the interaction backward, so the
+        # embedding-grad all-to-all overlaps them (per-layer buffers: no reuse)
+        self._defer_top_wgrad = world_size > 1 and cfg.interaction == "dot"
         on_gpu = dev.type == "cuda" and bool(cfg.overlap)
         self._ws = torch.cuda.Stream(device=dev) if on_gpu else None
         self._es = (torch.cuda.Stream(device=dev)
@@ -320,16 +323,16 @@ class DLRMTrainer:
         bias = None if L.bias_in_k else self.fp.param(L.name + ".w")[:, L.bcol]
         ops.gemm(x[:, :L.in_k], False, W[:, :L.in_k], False, bias, relu, None, out, None, 1)
 
-    def _bwd(self, L: Lin, x, dy, dx, x_is_relu):
-        """weight+bias grad (augmented wgrad) and dgrad into dx (masked by x>0)."""
+    def _bwd(self, L: Lin, x, dy, dx, x_is_relu, wgrad_now: bool = True):
+        """weight+bias grad (augmented wgrad) and dgrad into dx (masked by x>0).
+        wgrad_now=False leaves the weight grad to a later `_wgrad` call."""
         fp = self.fp
+        if not wgrad_now:
+            self._dgrad(L, x, dy, dx, x_is_relu)
+            return
 
         def wgrad():
-            if L.name in self.wslab:          # partials only; summed by the optimizer
-                sl, S = self.wslab[L.name]
-                ops.gemm(dy, True, x, True, None, False, None, None, sl, S)
-            else:
-                ops.linear_wgrad(dy, x, fp.grad(L.name + ".w").view(-1), slab=self.slab)
+            self._wgrad(L, x, dy)
 
         if self._ws is not None:
             self._ws.wait_stream(torch.cuda.current_stream())
@@ -337,11 +340,21 @@ class DLRMTrainer:
                 wgrad()
         else:
             wgrad()
+        self._dgrad(L, x, dy, dx, x_is_relu)
+
+    def _wgrad(self, L: Lin, x, dy):
+        if L.name in self.wslab:              # partials only; summed by the optimizer
+            sl, S = self.wslab[L.name]
+            ops.gemm(dy, True, x, True, None, False, None, None, sl, S)
+        else:
+            ops.linear_wgrad(dy, x, self.fp.grad(L.name + ".w").view(-1), slab=self.slab)
+
+    def _dgrad(self, L: Lin, x, dy, dx, x_is_relu):
         if dx is not None:
             # dgrad only over the columns dx holds (the padded K tail of the
             # augmented layout, bias column included, has no gradient consumer)
             n = min(dx.shape[1], L.in_k)
-            W = fp.bf16(L.name + ".w")
+            W = self.fp.bf16(L.name + ".w")
             ops.gemm(dy, False, W[:, :n], True, None, False,
                      x[:, :n] if x_is_relu else None, dx[:, :n], None, 1)
 
@@ -374,6 +387,7 @@ class DLRMTrainer:
             ("m", self._m_fwd_wait),
             ("c", self._s_top),
             ("m", emb.backward_start),
+            ("c", self._s_top_wgrad),           # overlaps the embedding-grad exchange
             ("c", self._s_bottom_bwd),
             ("m", self._m_allreduce_start),
             ("m", emb.backward_wait),
@@ -439,7 +453,8 @@ class DLRMTrainer:
                 dx = self.top_grad[i - 1]
             else:
                 dx = self.dz if cfg.interaction == "dot" else self.dcn_dx[-1]
-            self._bwd(L, self.top_in[i], self.top_grad[i], dx, x_is_relu=i > 0)
+            self._bwd(L, self.top_in[i], self.top_grad[i], dx, x_is_relu=i > 0,
+                      wgrad_now=not self._defer_top_wgrad)
         if cfg.interaction == "dot":
             ops.interaction_bwd(self.dz, h, emb.recv, self.slot_off, self.slot_stride, F, D,
                                 self.bot_grad[-1], emb.d_recv, self.slot_off, self.slot_stride,
@@ -447,6 +462,13 @@ class DLRMTrainer:
         else:
             self._dcn_backward(h)
         self._join(self._ws)
+
+    def _s_top_wgrad(self):
+        """Top-MLP weight grads, deferred past the interaction backward when the
+        embedding grads go over the network (their all-to-all runs meanwhile)."""
+        if self._defer_top_wgrad:
+            for i in reversed(range(len(self.top_layers))):
+                self._wgrad(self.top_layers[i], self.top_in[i], self.top_grad[i])
 
     def _s_bottom_bwd(self):
         for i in reversed(range(len(self.bottom_layers))):
