@@ -145,6 +145,20 @@ __device__ __forceinline__ bf16x8_t frag_col(const TDFO_LDS char* tile, int c0,
   return __builtin_bit_cast(bf16x8_t, r);
 }
 
+// Output tile and K-split of this block. The grid is 1-D over tiles x splits
+// and remapped so that each XCD receives a contiguous run of that space: with
+// split-K, one XCD then works on one K-range (its own slices of A and B), so
+// the operands a split re-reads across its tiles stay in that XCD's L2.
+struct TileIdx {
+  int tm, tn, split;
+};
+__device__ __forceinline__ TileIdx tile_of(int tiles_m, int tiles_n, int splits) {
+  const int tiles = tiles_m * tiles_n;
+  const int w = xcd_remap(blockIdx.x, tiles * splits);
+  const int split = w / tiles, t = w - split * tiles;
+  return {t / tiles_n, t - (t / tiles_n) * tiles_n, split};
+}
+
 // Epilogue shared by both tile shapes: bias + ReLU in registers, then the
 // ROWS x 128 fp32 tile is staged through the (now idle) LDS ring so global
 // traffic leaves as coalesced 16-B accesses (mask loads, bf16 stores, fp32
@@ -157,7 +171,7 @@ __device__ __forceinline__ bf16x8_t frag_col(const TDFO_LDS char* tile, int c0,
 template <int ROWS, int NT, int MI = 4>
 __device__ __forceinline__ void epilogue(const GemmArgs& p, const f32x4_t (&acc)[MI][4],
                                          char* smem_raw, int m0, int n0, int wr, int wc,
-                                         int lane, int tid) {
+                                         int lane, int tid, int split) {
   float* ctile = (float*)smem_raw;   // [ROWS][128] fp32, 16-B chunks XOR-swizzled
   __syncthreads();
 #pragma unroll
@@ -183,7 +197,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs& p, const f32x4_t (&acc)
     }
   }
   __syncthreads();
-  float* c32 = p.C32 ? p.C32 + (int64_t)blockIdx.z * p.M * p.ldc32 : nullptr;
+  float* c32 = p.C32 ? p.C32 + (int64_t)split * p.M * p.ldc32 : nullptr;
   const bool nfull = (n0 + BN <= p.N) && ((p.N & 7) == 0);
 #pragma unroll 2
   for (int it = 0; it < ROWS * 16 / NT; ++it) {
@@ -299,13 +313,12 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs p) {
   TDFO_LDS char* smem = (TDFO_LDS char*)smem_raw;
 
   const int tiles_m = (p.M + BMT - 1) / BMT, tiles_n = (p.N + BN - 1) / BN;
-  const int wg = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  const int tm = wg / tiles_n, tn = wg - tm * tiles_n;
-  const int m0 = tm * BMT, n0 = tn * BN;
+  const TileIdx ti = tile_of(tiles_m, tiles_n, p.splits);
+  const int m0 = ti.tm * BMT, n0 = ti.tn * BN;
 
   const int ktiles = p.K / BK;
   const int per = (ktiles + p.splits - 1) / p.splits;
-  const int kt0 = blockIdx.z * per;
+  const int kt0 = ti.split * per;
   const int kt1 = min(ktiles, kt0 + per);
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -343,7 +356,7 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs p) {
       cur ^= 1;
     }
   }
-  epilogue<BMT, 256, MI>(p, acc, smem_raw, m0, n0, wr, wc, lane, tid);
+  epilogue<BMT, 256, MI>(p, acc, smem_raw, m0, n0, wr, wc, lane, tid, ti.split);
 }
 
 // ---------------------------------------------------------------------------
@@ -366,13 +379,12 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(GemmArgs p) {
   TDFO_LDS char* smem = (TDFO_LDS char*)smem_raw;
 
   const int tiles_m = (p.M + LBM - 1) / LBM, tiles_n = (p.N + BN - 1) / BN;
-  const int wg = xcd_remap(blockIdx.x, tiles_m * tiles_n);
-  const int tm = wg / tiles_n, tn = wg - tm * tiles_n;
-  const int m0 = tm * LBM, n0 = tn * BN;
+  const TileIdx ti = tile_of(tiles_m, tiles_n, p.splits);
+  const int m0 = ti.tm * LBM, n0 = ti.tn * BN;
 
   const int ktiles = p.K / BK;
   const int per = (ktiles + p.splits - 1) / p.splits;
-  const int kt0 = blockIdx.z * per;
+  const int kt0 = ti.split * per;
   const int nk = min(ktiles, kt0 + per) - kt0;
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -489,7 +501,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(GemmArgs p) {
       for (int j = 0; j < 4; ++j) asm volatile("" :: "v"(acc[i][j]));
     return;
   }
-  epilogue<LBM, 512>(p, acc, smem_raw, m0, n0, wr, wc, lane, tid);
+  epilogue<LBM, 512>(p, acc, smem_raw, m0, n0, wr, wc, lane, tid, ti.split);
 }
 
 // 0 auto, 1 small tiles only (64-row tiles when 128-row ones underfill),
@@ -521,7 +533,7 @@ void launch(const GemmArgs& a, hipStream_t s) {
   bool big = (g_policy >= 2 && g_policy != 3 && g_policy != 4) || (g_policy == 4 && AC) ||
              (g_policy == 0 && small_tiles * a.splits >= 1024);
   if (big) {
-    dim3 grid(big_tiles, 1, a.splits);
+    dim3 grid(big_tiles * a.splits);
     hipLaunchKernelGGL((gemm_big_kernel<AC, BC>), grid, dim3(512), LSMEM, s, b);
   } else {
     if constexpr (!AC) {
@@ -529,14 +541,14 @@ void launch(const GemmArgs& a, hipStream_t s) {
       const int thr64 = g_policy == 5 ? 512 : 256;
       if (small_tiles * a.splits < thr64 && g_policy != 3 && g_policy != 2) {
         const int t64 = ((a.M + 63) / 64) * tn;
-        dim3 grid(t64, 1, a.splits);
+        dim3 grid(t64 * a.splits);
         hipLaunchKernelGGL((gemm_kernel<64, AC, BC>), grid, dim3(256),
                            2 * (64 * BK * 2 + TILE_BYTES), s, a);
         TDFO_CHECK_HIP(hipGetLastError());
         return;
       }
     }
-    dim3 grid(small_tiles, 1, a.splits);
+    dim3 grid(small_tiles * a.splits);
     hipLaunchKernelGGL((gemm_kernel<128, AC, BC>), grid, dim3(256), SMEM_BYTES, s, a);
   }
   TDFO_CHECK_HIP(hipGetLastError());
