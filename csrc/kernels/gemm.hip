@@ -172,6 +172,25 @@ template <int ROWS, int NT, int MI = 4>
 __device__ __forceinline__ void epilogue(const GemmArgs& p, const f32x4_t (&acc)[MI][4],
                                          char* smem_raw, int m0, int n0, int wr, int wc,
                                          int lane, int tid, int split) {
+  // Plain fp32 output (split-K weight-grad slabs): each lane already holds 4
+  // consecutive columns (16 B) of a row per fragment, so store straight from
+  // the accumulators -- no LDS round trip, no barrier; 64-B row runs per
+  // 4-lane group.
+  if (p.C32 && !p.C && !p.C2 && !p.bias && !p.relu && !p.mask && (p.ldc32 & 3) == 0 &&
+      (p.N & 3) == 0 && !(p.abl & 224)) {   // abl 128: force the LDS path (A/B)
+    float* c32 = p.C32 + (int64_t)split * p.M * p.ldc32;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wc * 64 + j * 16 + 4 * (lane >> 4);
+      if (n >= p.N) continue;
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int m = m0 + wr * (MI * 16) + i * 16 + (lane & 15);
+        if (m < p.M) *(f32x4_t*)(c32 + (int64_t)m * p.ldc32 + n) = acc[i][j];
+      }
+    }
+    return;
+  }
   float* ctile = (float*)smem_raw;   // [ROWS][128] fp32, 16-B chunks XOR-swizzled
   __syncthreads();
 #pragma unroll
@@ -530,8 +549,10 @@ void launch(const GemmArgs& a, hipStream_t s) {
   const int big_tiles = ((a.M + LBM - 1) / LBM) * tn;
   GemmArgs b = a;
   b.abl = g_policy >= 8 ? g_policy - 8 : 0;      // perf ablations (policy 9..15), big kernel
-  bool big = (g_policy >= 2 && g_policy != 3 && g_policy != 4) || (g_policy == 4 && AC) ||
-             (g_policy == 0 && small_tiles * a.splits >= 1024);
+  if (g_policy == 6) b.abl = 128;                // auto, fp32 slabs through the LDS epilogue
+  bool big = (g_policy >= 2 && g_policy != 3 && g_policy != 4 && g_policy != 6) ||
+             (g_policy == 4 && AC) ||
+             ((g_policy == 0 || g_policy == 6) && small_tiles * a.splits >= 1024);
   if (big) {
     dim3 grid(big_tiles * a.splits);
     hipLaunchKernelGGL((gemm_big_kernel<AC, BC>), grid, dim3(512), LSMEM, s, b);
@@ -543,13 +564,13 @@ void launch(const GemmArgs& a, hipStream_t s) {
         const int t64 = ((a.M + 63) / 64) * tn;
         dim3 grid(t64 * a.splits);
         hipLaunchKernelGGL((gemm_kernel<64, AC, BC>), grid, dim3(256),
-                           2 * (64 * BK * 2 + TILE_BYTES), s, a);
+                           2 * (64 * BK * 2 + TILE_BYTES), s, b);
         TDFO_CHECK_HIP(hipGetLastError());
         return;
       }
     }
     dim3 grid(small_tiles * a.splits);
-    hipLaunchKernelGGL((gemm_kernel<128, AC, BC>), grid, dim3(256), SMEM_BYTES, s, a);
+    hipLaunchKernelGGL((gemm_kernel<128, AC, BC>), grid, dim3(256), SMEM_BYTES, s, b);
   }
   TDFO_CHECK_HIP(hipGetLastError());
 }
