@@ -168,6 +168,24 @@ __device__ __forceinline__ TileIdx tile_of(int tiles_m, int tiles_n, int splits)
 // C[row 16i + (l&15)][col 16j + 4(l>>4) + r] -- four consecutive columns of
 // one row, staged with one 16-B LDS write per fragment (16 per lane instead
 // of 64 scalar writes).
+// Register-direct epilogue preconditions: whole tile in range, every touched
+// operand row 16-B aligned (8 bf16 / 4 fp32 columns).
+__device__ __forceinline__ bool al16(const void* q) { return ((uintptr_t)q & 15) == 0; }
+__device__ __forceinline__ bool direct_ok(const GemmArgs& p, int m0, int n0, int rows) {
+  if (p.abl & (224 | 256)) return false;           // ablations / forced LDS path
+  // operand reads (ReLU mask, DCN mul/add) in this layout are 32-B row runs;
+  // the LDS path reads them as 256-B rows (measured: DCN-v2 3.16 vs 3.05 ms)
+  if (p.mask || p.mul || p.add) return false;
+  if (m0 + rows > p.M || n0 + 128 > p.N) return false;
+  if (p.C && ((p.ldc & 7) || !al16(p.C))) return false;
+  if (p.mask && ((p.ldm & 7) || !al16(p.mask))) return false;
+  if (p.C2 && ((p.ldc2 & 7) || !al16(p.C2))) return false;
+  if (p.mul && ((p.ldmul & 7) || !al16(p.mul))) return false;
+  if (p.add && ((p.ldadd & 7) || !al16(p.add))) return false;
+  if (p.C32 && ((p.ldc32 & 3) || !al16(p.C32))) return false;
+  return true;
+}
+
 template <int ROWS, int NT, int MI = 4>
 __device__ __forceinline__ void epilogue(const GemmArgs& p, const f32x4_t (&acc)[MI][4],
                                          char* smem_raw, int m0, int n0, int wr, int wc,
@@ -187,6 +205,87 @@ __device__ __forceinline__ void epilogue(const GemmArgs& p, const f32x4_t (&acc)
       for (int i = 0; i < MI; ++i) {
         const int m = m0 + wr * (MI * 16) + i * 16 + (lane & 15);
         if (m < p.M) *(f32x4_t*)(c32 + (int64_t)m * p.ldc32 + n) = acc[i][j];
+      }
+    }
+    return;
+  }
+  // Full tiles with 16-B aligned operands: no LDS round trip either. Row
+  // fragments (i, i+1) are paired and v_permlane16_swap exchanges 4-column
+  // groups between lane rows g and g^1, after which every lane holds 8
+  // consecutive columns (16 B of bf16) of ONE row: lanes of even g row i,
+  // odd g row i+1 (guide T21 with the 16-lane swap). Same store count as the
+  // LDS path, no staging writes/reads and no barrier.
+  if (direct_ok(p, m0, n0, ROWS)) {
+    const int rho = lane & 15, g = lane >> 4;
+    float* c32 = p.C32 ? p.C32 + (int64_t)split * p.M * p.ldc32 : nullptr;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int cl = wc * 64 + j * 16 + 4 * g;
+      float bias[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        bias[r] = p.bias ? p.bias[(int64_t)(n0 + cl + r) * p.bias_stride] : 0.f;
+      const int n = n0 + wc * 64 + j * 16 + 8 * (g >> 1);
+#pragma unroll
+      for (int i = 0; i < MI; i += 2) {
+        float v[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float a = acc[i][j][r] + bias[r], b = acc[i + 1][j][r] + bias[r];
+          if (p.relu) {
+            a = fmaxf(a, 0.f);
+            b = fmaxf(b, 0.f);
+          }
+          const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b),
+                                                           false, false);
+          v[r] = __uint_as_float(sw[0]);
+          v[4 + r] = __uint_as_float(sw[1]);
+        }
+        const int m = m0 + wr * (MI * 16) + (i + (g & 1)) * 16 + rho;
+        if (p.mask) {
+          const uint4 mk = *(const uint4*)(p.mask + (int64_t)m * p.ldm + n);
+          const uint32_t mu[4] = {mk.x, mk.y, mk.z, mk.w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            if (!(bf2f((uint16_t)(mu[q] & 0xffff)) > 0.f)) v[2 * q] = 0.f;
+            if (!(bf2f((uint16_t)(mu[q] >> 16)) > 0.f)) v[2 * q + 1] = 0.f;
+          }
+        }
+        if (p.C)
+          *(uint4*)(p.C + (int64_t)m * p.ldc + n) =
+              make_uint4(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]),
+                         pack2bf(v[6], v[7]));
+        if (p.C2) {
+          float w2[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) w2[q] = v[q];
+          if (p.mul) {
+            const uint4 mv = *(const uint4*)(p.mul + (int64_t)m * p.ldmul + n);
+            const uint32_t mu[4] = {mv.x, mv.y, mv.z, mv.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              w2[2 * q] *= bf2f((uint16_t)(mu[q] & 0xffff));
+              w2[2 * q + 1] *= bf2f((uint16_t)(mu[q] >> 16));
+            }
+          }
+          if (p.add) {
+            const uint4 av = *(const uint4*)(p.add + (int64_t)m * p.ldadd + n);
+            const uint32_t au[4] = {av.x, av.y, av.z, av.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              w2[2 * q] += bf2f((uint16_t)(au[q] & 0xffff));
+              w2[2 * q + 1] += bf2f((uint16_t)(au[q] >> 16));
+            }
+          }
+          *(uint4*)(p.C2 + (int64_t)m * p.ldc2 + n) =
+              make_uint4(pack2bf(w2[0], w2[1]), pack2bf(w2[2], w2[3]), pack2bf(w2[4], w2[5]),
+                         pack2bf(w2[6], w2[7]));
+        }
+        if (c32) {
+          float* o = c32 + (int64_t)m * p.ldc32 + n;
+          *(float4*)o = make_float4(v[0], v[1], v[2], v[3]);
+          *(float4*)(o + 4) = make_float4(v[4], v[5], v[6], v[7]);
+        }
       }
     }
     return;
@@ -549,10 +648,11 @@ void launch(const GemmArgs& a, hipStream_t s) {
   const int big_tiles = ((a.M + LBM - 1) / LBM) * tn;
   GemmArgs b = a;
   b.abl = g_policy >= 8 ? g_policy - 8 : 0;      // perf ablations (policy 9..15), big kernel
-  if (g_policy == 6) b.abl = 128;                // auto, fp32 slabs through the LDS epilogue
-  bool big = (g_policy >= 2 && g_policy != 3 && g_policy != 4 && g_policy != 6) ||
-             (g_policy == 4 && AC) ||
-             ((g_policy == 0 || g_policy == 6) && small_tiles * a.splits >= 1024);
+  if (g_policy == 6) b.abl = 128;                // auto, every output through the LDS epilogue
+  if (g_policy == 7) b.abl = 256;                // auto, bf16 outputs through the LDS epilogue
+  const bool autop = g_policy == 0 || g_policy == 6 || g_policy == 7;
+  bool big = (g_policy >= 2 && g_policy != 3 && g_policy != 4 && !autop) ||
+             (g_policy == 4 && AC) || (autop && small_tiles * a.splits >= 1024);
   if (big) {
     dim3 grid(big_tiles * a.splits);
     hipLaunchKernelGGL((gemm_big_kernel<AC, BC>), grid, dim3(512), LSMEM, s, b);
