@@ -120,8 +120,13 @@ struct EmbBwdArgs {
   float eps, beta1, beta2, weight_decay;
   float* dense_grad;           // EMB_DENSE_GRAD: accumulate into [rows, D]
   void* workspace; size_t workspace_bytes;
+  int segsort;                 // one id per bag, distinct tables: per-table LDS sort allowed
 };
 size_t embedding_bwd_workspace(int64_t nnz, int D);
+// One-hot batches (nnz == T*B, B <= 8192): per-table LDS sort in one launch
+// (1, default) or the device-wide radix sort (0); v < 0 queries. Returns the
+// previous setting.
+int embedding_segsort(int v);
 void embedding_bwd_fused(const EmbBwdArgs& a, hipStream_t s);
 
 // ------------------------------------------------------------ optim ----

@@ -119,6 +119,131 @@ __global__ void emb_keys_kernel(const EmbBwdArgs a, K* __restrict__ keys,
   }
 }
 
+// ------------------------------------------- one-hot: per-table LDS sort ----
+// When every bag holds exactly one id (nnz == T*B, Criteo one-hot) and
+// B <= SEG_MAX, table t's ids are the contiguous positions [t*B, (t+1)*B),
+// and sorting them by row inside the table is the whole job: the composite
+// (row_offset[t] + id) order across tables is just table order. One
+// 1024-thread block per table sorts its <= 8192 (row, position) pairs in LDS
+// with a stable LSD radix sort (6-bit digits, only as many passes as the
+// table's largest id needs) and also writes the keys kernel's per-position
+// outputs -- replacing emb_keys_kernel + the device-wide sort (3 passes of
+// hist/scan/scatter over all tables) with one launch.
+//   per pass: digit ranks inside a wave by ballot matching (6 ballots per
+//   element), per-(digit, slot, wave) counts, one block-wide exclusive scan
+//   over them in (digit, slot, wave) order, scatter into LDS, re-read.
+constexpr int SEG_MAX = 8192;
+constexpr int SEG_THREADS = 1024;
+constexpr int SEG_K = SEG_MAX / SEG_THREADS;        // elements per thread
+constexpr int SEG_BITS = 6;
+constexpr int SEG_BINS = 1 << SEG_BITS;
+constexpr int SEG_WAVES = SEG_THREADS / 64;
+constexpr int SEG_CNT = SEG_BINS * SEG_K * SEG_WAVES;   // 8192 counters
+
+template <typename K>
+__global__ __launch_bounds__(SEG_THREADS) void emb_segsort_kernel(
+    const EmbBwdArgs a, K* __restrict__ keys_out, int32_t* __restrict__ vals_out,
+    int64_t* __restrict__ goff, float* __restrict__ gscale, int32_t* __restrict__ tail_count) {
+  __shared__ uint32_t skey[SEG_MAX];
+  __shared__ uint32_t sval[SEG_MAX];
+  __shared__ uint32_t cnt[SEG_CNT];
+  __shared__ uint32_t wsum[SEG_WAVES];
+  __shared__ uint32_t smax[SEG_WAVES];
+  const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (t == 0 && tid == 0) *tail_count = 0;          // read by later kernels
+  const int n = a.B;
+  const int64_t s0 = (int64_t)t * a.B;
+  uint32_t key[SEG_K], val[SEG_K];
+  uint32_t kmax = 0;
+#pragma unroll
+  for (int k = 0; k < SEG_K; ++k) {
+    const int i = k * SEG_THREADS + tid;
+    if (i < n) {
+      const int64_t p = s0 + i;
+      key[k] = (uint32_t)a.indices[p];
+      val[k] = (uint32_t)i;
+      kmax = max(kmax, key[k]);
+      goff[p] = (int64_t)i * a.grad_stride + a.grad_off[t];
+      if (gscale) gscale[p] = a.psw ? a.psw[p] : 1.f;
+    } else {
+      key[k] = 0xffffffffu;                          // sorts after every real id
+      val[k] = 0;
+    }
+  }
+  // passes needed for this table's largest id
+  for (int off = 32; off > 0; off >>= 1) kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, off));
+  if (lane == 0) smax[w] = kmax;
+  __syncthreads();
+  uint32_t bmax = 0;
+  for (int q = 0; q < SEG_WAVES; ++q) bmax = max(bmax, smax[q]);
+  const int bits = bmax ? 32 - __clz(bmax) : 1;
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  for (int shift = 0; shift < bits; shift += SEG_BITS) {
+    for (int c = tid; c < SEG_CNT; c += SEG_THREADS) cnt[c] = 0;
+    __syncthreads();
+    uint32_t rank[SEG_K];
+    int dig[SEG_K];
+#pragma unroll
+    for (int k = 0; k < SEG_K; ++k) {
+      // invalid slots carry the all-ones key: digit 63 in every pass
+      const int d = (int)((key[k] >> shift) & (SEG_BINS - 1));
+      uint64_t peers = ~0ull;
+#pragma unroll
+      for (int b = 0; b < SEG_BITS; ++b) {
+        const uint64_t bal = __ballot((d >> b) & 1);
+        peers &= ((d >> b) & 1) ? bal : ~bal;
+      }
+      rank[k] = (uint32_t)__popcll(peers & lt);
+      dig[k] = d;
+      if ((peers & lt) == 0) cnt[(d * SEG_K + k) * SEG_WAVES + w] = (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+    // exclusive scan of cnt in (digit, slot, wave) order: 8 entries per thread
+    uint32_t loc[SEG_CNT / SEG_THREADS];
+    uint32_t run = 0;
+#pragma unroll
+    for (int q = 0; q < SEG_CNT / SEG_THREADS; ++q) {
+      loc[q] = run;
+      run += cnt[tid * (SEG_CNT / SEG_THREADS) + q];
+    }
+    uint32_t incl = run;                             // wave inclusive scan of the totals
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t o = (uint32_t)__shfl_up((int)incl, off);
+      if (lane >= off) incl += o;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    uint32_t base = incl - run;
+    for (int q = 0; q < w; ++q) base += wsum[q];
+#pragma unroll
+    for (int q = 0; q < SEG_CNT / SEG_THREADS; ++q)
+      cnt[tid * (SEG_CNT / SEG_THREADS) + q] = base + loc[q];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < SEG_K; ++k) {
+      const uint32_t dst = cnt[(dig[k] * SEG_K + k) * SEG_WAVES + w] + rank[k];
+      skey[dst] = key[k];
+      sval[dst] = val[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < SEG_K; ++k) {
+      key[k] = skey[k * SEG_THREADS + tid];
+      val[k] = sval[k * SEG_THREADS + tid];
+    }
+    __syncthreads();
+  }
+  const K kb = (K)a.row_offset[t];
+#pragma unroll
+  for (int k = 0; k < SEG_K; ++k) {
+    const int i = k * SEG_THREADS + tid;
+    if (i < n) {
+      keys_out[s0 + i] = kb + (K)key[k];
+      vals_out[s0 + i] = (int32_t)(s0 + val[k]);
+    }
+  }
+}
+
 template <int D>
 __device__ __forceinline__ int elem0(int lane) {
   return D >= 64 ? lane * (D / 64) : lane;
@@ -413,6 +538,8 @@ __global__ __launch_bounds__(256) void emb_combine_kernel(
   }
 }
 
+int g_emb_segsort = 1;   // one-hot batches: per-table LDS sort (0: device-wide radix sort)
+
 struct WsLayout {
   size_t keys_in, keys_out, vals_in, vals_out, goff, gscale, head, tail, tlist, tcount, sortws;
   size_t total;
@@ -456,16 +583,24 @@ void bwd_impl(const EmbBwdArgs& a, const WsLayout& L, hipStream_t s) {
   int32_t* tcount = (int32_t*)(ws + L.tcount);
   int64_t kb = (a.nnz + 255) / 256;
   if (kb > 8192) kb = 8192;
-  hipLaunchKernelGGL(emb_keys_kernel<K>, dim3(kb), dim3(256), 0, s, a, keys_in, vals_in, goff,
-                     gscale, tcount);
+  const bool onehot = g_emb_segsort && a.segsort && a.nnz == (int64_t)a.T * a.B &&
+                      a.B <= SEG_MAX && !a.mean;
+  int in_b = 1;
+  if (onehot) {
+    hipLaunchKernelGGL(emb_segsort_kernel<K>, dim3(a.T), dim3(SEG_THREADS), 0, s, a, keys_out,
+                       vals_out, goff, gscale, tcount);
+  } else {
+    hipLaunchKernelGGL(emb_keys_kernel<K>, dim3(kb), dim3(256), 0, s, a, keys_in, vals_in, goff,
+                       gscale, tcount);
+    TDFO_CHECK_HIP(hipGetLastError());
+    if constexpr (sizeof(K) == 4)
+      in_b = radix_sort_pairs_u32(keys_in, vals_in, keys_out, vals_out, a.nnz, a.key_bits,
+                                  ws + L.sortws, s);
+    else
+      in_b = radix_sort_pairs_u64(keys_in, vals_in, keys_out, vals_out, a.nnz, a.key_bits,
+                                  ws + L.sortws, s);
+  }
   TDFO_CHECK_HIP(hipGetLastError());
-  int in_b;
-  if constexpr (sizeof(K) == 4)
-    in_b = radix_sort_pairs_u32(keys_in, vals_in, keys_out, vals_out, a.nnz, a.key_bits,
-                                ws + L.sortws, s);
-  else
-    in_b = radix_sort_pairs_u64(keys_in, vals_in, keys_out, vals_out, a.nnz, a.key_bits,
-                                ws + L.sortws, s);
   if (!in_b) { keys_out = keys_in; vals_out = vals_in; }
   constexpr int CH = BwdCfg<D>::CH;
   const int64_t nch = (a.nnz + CH - 1) / CH;
@@ -525,6 +660,12 @@ void embedding_bag_fwd(const EmbFwdArgs& a, hipStream_t s) {
     case 512: TDFO_EF(512); break;
   }
 #undef TDFO_EF
+}
+
+int embedding_segsort(int v) {
+  const int old = g_emb_segsort;
+  if (v >= 0) g_emb_segsort = v ? 1 : 0;
+  return old;
 }
 
 size_t embedding_bwd_workspace(int64_t nnz, int D) {

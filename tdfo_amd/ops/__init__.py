@@ -33,6 +33,12 @@ def gemm_policy(p: int = -1) -> int:
     return int(_native().gemm_policy(p))
 
 
+def embedding_segsort(v: int = -1) -> int:
+    """One-hot embedding backward sort: 1 per-table LDS sort (default), 0 the
+    device-wide radix sort; v < 0 only reads it. Returns the previous one."""
+    return int(_native().embedding_segsort(v))
+
+
 def linear_xent_impl(p: int = -1) -> int:
     """Fused Linear+CE kernel family: 1 f32-input MFMA (default), 0 VALU;
     p < 0 only reads it. Returns the previous one."""
@@ -108,13 +114,16 @@ def embedding_bag_fwd(W, row_offset, indices, offsets, out_off, T, B, out, out_s
 
 def embedding_bwd(W, row_offset, indices, offsets, grad_off, T, B, grad, grad_stride, opt, hyper,
                   state1=None, state2=None, eps=1e-8, beta1=0.9, beta2=0.999, weight_decay=0.0,
-                  key_bits=None, mean=False, psw=None, dense_grad=None):
+                  key_bits=None, mean=False, psw=None, dense_grad=None, segsort=False):
+    """Fused sort-based backward + optimizer. segsort=True promises one id per
+    bag and that no two virtual tables share rows (then a one-launch per-table
+    LDS sort replaces the device-wide radix sort)."""
     if key_bits is None:
         key_bits = key_bits_for(W.shape[0])
     if _gpu(W):
         _native().embedding_bwd(W, row_offset, indices, offsets, grad_off, psw, T, B, mean,
                                 key_bits, grad, grad_stride, opt, state1, state2, hyper, eps,
-                                beta1, beta2, weight_decay, dense_grad)
+                                beta1, beta2, weight_decay, dense_grad, bool(segsort))
     else:
         ref.embedding_bwd(W, row_offset, indices, offsets, grad_off, psw, T, B, mean, key_bits,
                           grad, grad_stride, opt, state1, state2, hyper, eps, beta1, beta2,

@@ -132,6 +132,9 @@ class ShardedEmbeddingBags:
                 v_row_off.append(self.tw_store.row_offset_host[i])
                 v_out_off.append(s * B * self.dsum[rank] + i * D)
         self.tw_nv = nv
+        # one id per bag and one source rank: every virtual table is its own
+        # physical table, so per-table sorts give the global (row) grouping
+        self.tw_segsort = W == 1 and all(self.L[t] == 1 for t in mine)
         offs = torch.zeros(len(lens) + 1, dtype=torch.int64)
         if lens:
             offs[1:] = torch.cumsum(torch.tensor(lens, dtype=torch.int64), 0)
@@ -462,7 +465,8 @@ class ShardedEmbeddingBags:
         if self.tw_nv:
             self.tw_store.backward_update(self.tw_recv_ids, self.tw_v_offsets, self.tw_v_row_off,
                                           self.tw_nv, B, grad, self.tw_v_out_off,
-                                          self.dsum[self.rank], hyper, mean=self.mean)
+                                          self.dsum[self.rank], hyper, mean=self.mean,
+                                          segsort=self.tw_segsort)
         if self.cw_tables and self.cw_nv:
             self.cw_store.backward_update(self.cw_recv_ids, self.cw_v_offsets, self.cw_v_row_off,
                                           self.cw_nv, B, grad, self.cw_v_out_off,

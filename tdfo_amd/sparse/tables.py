@@ -155,12 +155,13 @@ class TableBatchedEmbedding:
                               out_stride, mean=mean, psw=psw)
 
     def backward_update(self, indices, offsets, row_offset, T, B, grad, grad_off, grad_stride,
-                        hyper, mean=False, psw=None, dense_grad=None):
+                        hyper, mean=False, psw=None, dense_grad=None, segsort=False):
         o = self.optim
         ops.embedding_bwd(self.weight, row_offset, indices, offsets, grad_off, T, B, grad,
                           grad_stride, o.code, hyper, state1=self.state1, state2=self.state2,
                           eps=o.eps, beta1=o.beta1, beta2=o.beta2, weight_decay=o.weight_decay,
-                          key_bits=self.key_bits, mean=mean, psw=psw, dense_grad=dense_grad)
+                          key_bits=self.key_bits, mean=mean, psw=psw, dense_grad=dense_grad,
+                          segsort=segsort)
 
     def table_weight(self, t: int) -> torch.Tensor:
         s = self.row_offset_host[t]

@@ -214,6 +214,38 @@ def test_embedding_bwd_fused(opt, skew, D):
         assert (dg - edg).abs().max() < 1e-4 * max(1.0, edg.abs().max().item())
 
 
+@pytest.mark.parametrize("B", [700, 8192])
+@pytest.mark.parametrize("skew", [False, True])
+@pytest.mark.parametrize("opt", [ops.EMB_ROWWISE_ADAGRAD, ops.EMB_ADAM])
+def test_embedding_bwd_onehot_segsort(B, skew, opt):
+    """One id per bag: the per-table LDS sort must give bit-identical updates
+    to the device-wide radix sort, and match the fp32 reference."""
+    T, D = 3, 128
+    rows = [50, 9000, 70000]
+    W, ro, idx, offs = _emb_case(T, B, rows, D, 1, skew, seed=7)
+    W, ro, idx, offs = (x.to(DEV) for x in (W, ro, idx, offs))
+    goff = torch.tensor([t * D for t in range(T)], device=DEV)
+    grad = torch.randn(B * T * D, device=DEV)
+    hyper = torch.tensor([0.05, 3.0], device=DEV)
+    n1 = W.shape[0] if opt == ops.EMB_ROWWISE_ADAGRAD else W.numel()
+    s1 = torch.rand(n1, device=DEV)
+    s2 = torch.rand(W.numel(), device=DEV) if opt == ops.EMB_ADAM else None
+    res = []
+    for seg in (True, False):
+        Wn, a1 = W.clone(), s1.clone()
+        a2 = s2.clone() if s2 is not None else None
+        ops.embedding_bwd(Wn, ro, idx, offs, goff, T, B, grad, T * D, opt, hyper, state1=a1,
+                          state2=a2, segsort=seg)
+        res.append((Wn, a1))
+    torch.cuda.synchronize()
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    We, e1 = W.clone(), s1.clone()
+    e2 = s2.clone() if s2 is not None else None
+    ref.embedding_bwd(We, ro, idx, offs, goff, None, T, B, False, 20, grad, T * D, opt, e1, e2,
+                      hyper, 1e-8, 0.9, 0.999, 0.0, None)
+    assert (res[0][0] - We).abs().max() < 1e-4 * max(1.0, We.abs().max().item())
+
+
 def test_embedding_bwd_deterministic():
     T, B, D = 2, 4096, 128
     rows = [3, 100000]
