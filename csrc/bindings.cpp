@@ -223,6 +223,74 @@ void attention_bwd(const Tensor& qkv, const Tensor& ids, const Tensor& dout, int
   tdfo::attention_bwd(a, cur_stream());
 }
 
+void check_f32c(const Tensor& t, const char* name);
+// ------------------------------------------------------- encoder layer
+// params: [Wqkv [3E,E], bqkv, Wo [E,E], bo, g1, be1, g2, be2, W1 [FF,E], b1,
+// W2 [E,FF], b2]; saved: [qkv, ctx, x1, f]
+tdfo::EncArgs enc_args(const Tensor& x, const Tensor& ids, const c10::optional<Tensor>& step,
+                       at::TensorList params, int64_t H, double rate, int64_t seed,
+                       int64_t pad_id, double eps, at::TensorList saved) {
+  TORCH_CHECK(x.dim() == 3, "encoder_layer: x [B, T, E]");
+  TORCH_CHECK(params.size() == 12 && saved.size() == 4, "encoder_layer: 12 params, 4 saved");
+  const int64_t B = x.size(0), T = x.size(1), E = x.size(2);
+  const int64_t FF = params[8].size(0);
+  const int64_t want[12] = {3 * E * E, 3 * E, E * E, E, E, E, E, E, FF * E, FF, E * FF, E};
+  for (int i = 0; i < 12; ++i) {
+    check_f32c(params[i], "encoder param");
+    TORCH_CHECK(params[i].numel() == want[i], "encoder_layer: param ", i, " has ",
+                params[i].numel(), " elements, expected ", want[i]);
+  }
+  check_f32c(x, "x");
+  check_dev(ids, "ids");
+  TORCH_CHECK(ids.scalar_type() == at::kLong && ids.is_contiguous() && ids.numel() == B * T,
+              "encoder_layer: ids int64 [B, T]");
+  const int64_t wsv[4] = {B * T * 3 * E, B * T * E, B * T * E, B * T * FF};
+  for (int i = 0; i < 4; ++i) {
+    check_f32c(saved[i], "encoder saved");
+    TORCH_CHECK(saved[i].numel() == wsv[i], "encoder_layer: saved tensor ", i, " size");
+  }
+  TORCH_CHECK(tdfo::encoder_layer_supported((int)T, (int)E, (int)H, (int)FF),
+              "encoder_layer: unsupported shape");
+  tdfo::EncArgs a{};
+  a.B = (int)B; a.T = (int)T; a.E = (int)E; a.H = (int)H; a.FF = (int)FF;
+  a.rate = (float)rate; a.seed = seed; a.pad_id = pad_id; a.eps = (float)eps;
+  if (step) {
+    check_dev(*step, "step");
+    TORCH_CHECK(step->scalar_type() == at::kLong, "encoder_layer: step int64");
+    a.step = step->data_ptr<int64_t>();
+  }
+  a.x = x.data_ptr<float>(); a.ids = ids.data_ptr<int64_t>();
+  const float** pp[12] = {&a.wqkv, &a.bqkv, &a.wo, &a.bo, &a.g1, &a.be1,
+                          &a.g2, &a.be2, &a.w1, &a.b1, &a.w2, &a.b2};
+  for (int i = 0; i < 12; ++i) *pp[i] = params[i].data_ptr<float>();
+  a.qkv = saved[0].data_ptr<float>(); a.ctx = saved[1].data_ptr<float>();
+  a.x1 = saved[2].data_ptr<float>(); a.f = saved[3].data_ptr<float>();
+  return a;
+}
+
+void encoder_layer_fwd(const Tensor& x, const Tensor& ids, const c10::optional<Tensor>& step,
+                       at::TensorList params, int64_t H, double rate, int64_t seed,
+                       int64_t pad_id, double eps, at::TensorList saved, const Tensor& y) {
+  auto a = enc_args(x, ids, step, params, H, rate, seed, pad_id, eps, saved);
+  check_f32c(y, "y");
+  TORCH_CHECK(y.numel() == x.numel(), "encoder_layer: y [B, T, E]");
+  a.y = y.data_ptr<float>();
+  tdfo::encoder_layer_fwd(a, cur_stream());
+}
+
+void encoder_layer_bwd(const Tensor& x, const Tensor& ids, const c10::optional<Tensor>& step,
+                       at::TensorList params, int64_t H, double rate, int64_t seed,
+                       int64_t pad_id, double eps, at::TensorList saved, const Tensor& dy,
+                       const Tensor& dx, const Tensor& part, const Tensor& grad) {
+  auto a = enc_args(x, ids, step, params, H, rate, seed, pad_id, eps, saved);
+  check_f32c(dy, "dy"); check_f32c(dx, "dx"); check_f32c(part, "part"); check_f32c(grad, "grad");
+  const int64_t P = tdfo::encoder_param_count(a.E, a.FF);
+  TORCH_CHECK(dy.numel() == x.numel() && dx.numel() == x.numel(), "encoder_layer: dy/dx");
+  TORCH_CHECK(part.numel() >= (int64_t)a.B * P && grad.numel() >= P, "encoder_layer: part/grad");
+  a.dy = dy.data_ptr<float>(); a.dx = dx.data_ptr<float>(); a.part = part.data_ptr<float>();
+  tdfo::encoder_layer_bwd(a, grad.data_ptr<float>(), cur_stream());
+}
+
 // ------------------------------------------------------------ layernorm
 void check_f32c(const Tensor& t, const char* name) {
   check_dev(t, name);
@@ -682,6 +750,17 @@ TORCH_LIBRARY(tdfo, m) {
         [](int64_t v) { return (int64_t)tdfo::embedding_segsort((int)v); });
   m.def("linear_xent_impl(int p) -> int",
         [](int64_t p) { return (int64_t)tdfo::linear_xent_impl((int)p); });
+  m.def("encoder_param_count(int E, int FF) -> int",
+        [](int64_t E, int64_t FF) { return (int64_t)tdfo::encoder_param_count((int)E, (int)FF); });
+  m.def("encoder_layer_supported(int T, int E, int H, int FF) -> bool",
+        [](int64_t T, int64_t E, int64_t H, int64_t FF) {
+          return tdfo::encoder_layer_supported((int)T, (int)E, (int)H, (int)FF);
+        });
+  m.def("encoder_layer_fwd(Tensor x, Tensor ids, Tensor? step, Tensor[] params, int H, float rate, "
+        "int seed, int pad_id, float eps, Tensor(a!)[] saved, Tensor(b!) y) -> ()");
+  m.def("encoder_layer_bwd(Tensor x, Tensor ids, Tensor? step, Tensor[] params, int H, float rate, "
+        "int seed, int pad_id, float eps, Tensor[] saved, Tensor dy, Tensor(a!) dx, "
+        "Tensor(b!) part, Tensor(c!) grad) -> ()");
   m.def("attention_fwd(Tensor qkv, Tensor ids, int H, float rate, int seed, Tensor? step, int pad_id, "
         "Tensor(a!) out) -> ()");
   m.def("attention_bwd(Tensor qkv, Tensor ids, Tensor dout, int H, float rate, int seed, Tensor? step, "
@@ -733,6 +812,8 @@ TORCH_LIBRARY(tdfo, m) {
 TORCH_LIBRARY_IMPL(tdfo, CUDA, m) {
   m.impl("gemm", gemm);
   m.impl("attention_fwd", attention_fwd);
+  m.impl("encoder_layer_fwd", encoder_layer_fwd);
+  m.impl("encoder_layer_bwd", encoder_layer_bwd);
   m.impl("attention_bwd", attention_bwd);
   m.impl("layernorm_fwd", layernorm_fwd);
   m.impl("layernorm_bwd", layernorm_bwd);

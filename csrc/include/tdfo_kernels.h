@@ -229,6 +229,24 @@ struct AttnArgs {
 void attention_fwd(const AttnArgs& a, hipStream_t s);
 void attention_bwd(const AttnArgs& a, hipStream_t s);
 
+// --------------------------------------------------- encoder layer ----
+// Fused Bert4Rec transformer block (encoder.hip), fp32, one workgroup per
+// sequence. x/y/dx [B,T,E]; saves qkv [B,T,3E], ctx [B,T,E], x1 [B,T,E],
+// f [B,T,FF]; part [B][encoder_param_count(E, FF)].
+struct EncArgs {
+  int B, T, E, H, FF; float rate; int64_t seed; const int64_t* step; int64_t pad_id; float eps;
+  const float* x; const int64_t* ids;
+  const float *wqkv, *bqkv, *wo, *bo, *g1, *be1, *g2, *be2, *w1, *b1, *w2, *b2;
+  float *y, *qkv, *ctx, *x1, *f;
+  const float* dy; float* dx; float* part;
+};
+int encoder_param_count(int E, int FF);
+bool encoder_layer_supported(int T, int E, int H, int FF);
+void encoder_layer_fwd(const EncArgs& a, hipStream_t s);
+// grad: [encoder_param_count] = [dWqkv | dbqkv | dWo | dbo | dg1 | dbe1 | dg2 |
+// dbe2 | dW1 | db1 | dW2 | db2]
+void encoder_layer_bwd(const EncArgs& a, float* grad, hipStream_t s);
+
 // ------------------------------------------------------- layernorm ----
 // Row LayerNorm over the last n <= 1024 elements (layernorm.hip).
 int layernorm_parts(int64_t M);

@@ -35,6 +35,16 @@ __device__ __forceinline__ const uint16_t* feat_row(const uint16_t* dense,
   return emb + sm.off[i] + (int64_t)b * sm.stride[i];
 }
 
+// Each wave owns its LDS region and its samples, and LDS executes a wave's
+// instructions in order, so a wave-local fence (no block barrier) orders its
+// cross-lane LDS writes and reads; the waves of a block never wait for each
+// other, so one wave's global loads overlap another's MFMAs and stores.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 template <int D>
 __global__ __launch_bounds__(256) void inter_fwd_kernel(
     const uint16_t* __restrict__ dense, int64_t ld_dense,
@@ -77,13 +87,13 @@ __global__ __launch_bounds__(256) void inter_fwd_kernel(
         if (rr < F && col < rr) row[D + rr * (rr - 1) / 2 + col] = f2bf(acc[r]);
       }
     }
-    __syncthreads();
+    wave_sync();
     if (valid) {
       uint16_t* op = out + (int64_t)b * ldo;
       for (int c = lane; c < ldo / 8; c += 64)
         *(uint4*)(op + c * 8) = *(const uint4*)(row + c * 8);
     }
-    __syncthreads();
+    wave_sync();
   }
 }
 
@@ -138,7 +148,7 @@ __global__ __launch_bounds__(256) void inter_bwd_kernel(
             *(const uint4*)(rp + ch * 8);
       }
     }
-    __syncthreads();
+    wave_sync();
     if (valid) {
       // A operand: S[i][k], i = lane&31, k = 16ks + 8h + jj
       const int i = lane & 31;
@@ -211,7 +221,7 @@ __global__ __launch_bounds__(256) void inter_bwd_kernel(
         *(uint4*)(dst + ch * 8) = v;
       }
     }
-    __syncthreads();
+    wave_sync();
   }
 }
 

@@ -46,6 +46,9 @@ METRICS_K = (10, 20, 50)
 # and every LayerNorm run as hand-written kernels (csrc/kernels/attention.hip,
 # layernorm.hip); on CPU the same modules run the torch reference ops.
 USE_FUSED = True
+# whole transformer block in one fwd / one bwd kernel (encoder.hip); False
+# keeps the per-op path (fused attention core + LayerNorm kernels, torch GEMMs)
+USE_FUSED_BLOCK = True
 
 
 def _fused(x: torch.Tensor) -> bool:
@@ -95,6 +98,54 @@ class _LayerNormFn(torch.autograd.Function):
         dgb = torch.empty(2 * n, dtype=torch.float32, device=x.device)
         ops.layernorm_bwd(x, g.contiguous(), n, gamma, mean, rstd, dx, part, dgb)
         return dx, dgb[:n].view_as(gamma), dgb[n:].view_as(gamma), None, None
+
+
+class _EncoderLayerFn(torch.autograd.Function):
+    """Whole pre-norm transformer block as two HIP kernels (encoder.hip)."""
+
+    @staticmethod
+    def forward(ctx, x, ids, step, H, rate, seed, eps, *params):
+        x = x.contiguous()
+        B, T, E = x.shape
+        FF = params[8].shape[0]
+        dev = x.device
+        saved = [torch.empty(B, T, 3 * E, device=dev), torch.empty(B, T, E, device=dev),
+                 torch.empty(B, T, E, device=dev), torch.empty(B, T, FF, device=dev)]
+        y = torch.empty_like(x)
+        params = [p.contiguous() for p in params]
+        ops.encoder_layer_fwd(x, ids, step, params, H, rate, seed, PAD_ID, eps, saved, y)
+        ctx.save_for_backward(x, ids, step, *params, *saved)
+        ctx.cfg = (H, rate, seed, eps)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        t = ctx.saved_tensors
+        x, ids, step, params, saved = t[0], t[1], t[2], list(t[3:15]), list(t[15:])
+        H, rate, seed, eps = ctx.cfg
+        B, T, E = x.shape
+        FF = params[8].shape[0]
+        P = ops.encoder_param_count(E, FF)
+        part = torch.empty(B * P, device=x.device)
+        grad = torch.empty(P, device=x.device)
+        dx = torch.empty_like(x)
+        ops.encoder_layer_bwd(x, ids, step, params, H, rate, seed, PAD_ID, eps, saved,
+                              dy.contiguous(), dx, part, grad)
+        grads, o = [], 0
+        for p in params:
+            grads.append(grad[o:o + p.numel()].view_as(p))
+            o += p.numel()
+        return (dx, None, None, None, None, None, None, *grads)
+
+
+_ENC_OK: Dict[tuple, bool] = {}
+
+
+def _fused_block_ok(T: int, E: int, H: int, FF: int) -> bool:
+    k = (T, E, H, FF)
+    if k not in _ENC_OK:
+        _ENC_OK[k] = ops.encoder_layer_supported(T, E, H, FF)
+    return _ENC_OK[k]
 
 
 def layer_norm(x: torch.Tensor, ln: nn.LayerNorm) -> torch.Tensor:
@@ -172,7 +223,22 @@ class TransformerBlock(nn.Module):
         self.output_sublayer = SublayerConnection(dim, dropout)
         self.dropout = nn.Dropout(dropout)
 
+    def _fused_params(self):
+        att, ff = self.attention, self.feed_forward
+        return [torch.cat([l.weight for l in att.linear_layers], 0),
+                torch.cat([l.bias for l in att.linear_layers], 0),
+                att.output_linear.weight, att.output_linear.bias,
+                self.input_sublayer.norm.weight, self.input_sublayer.norm.bias,
+                self.output_sublayer.norm.weight, self.output_sublayer.norm.bias,
+                ff.w_1.weight, ff.w_1.bias, ff.w_2.weight, ff.w_2.bias]
+
     def forward(self, x, mask):
+        att = self.attention
+        if (USE_FUSED_BLOCK and isinstance(mask, KeyPad) and x.is_cuda
+                and _fused_block_ok(x.shape[1], x.shape[2], att.h, self.feed_forward.w_1.out_features)):
+            rate = self.dropout.p if self.training else 0.0
+            return _EncoderLayerFn.apply(x, mask.ids, mask.step, att.h, rate, att.seed,
+                                         self.input_sublayer.norm.eps, *self._fused_params())
         x = self.input_sublayer(x, lambda y: self.attention(y, mask))
         x = self.output_sublayer(x, self.feed_forward)
         return self.dropout(x)

@@ -33,6 +33,28 @@ def gemm_policy(p: int = -1) -> int:
     return int(_native().gemm_policy(p))
 
 
+def encoder_layer_supported(T: int, E: int, H: int, FF: int) -> bool:
+    return bool(_native().encoder_layer_supported(T, E, H, FF))
+
+
+def encoder_param_count(E: int, FF: int) -> int:
+    return int(_native().encoder_param_count(E, FF))
+
+
+def encoder_layer_fwd(x, ids, step, params, H, rate, seed, pad_id, eps, saved, y):
+    """Fused pre-norm transformer block forward (GPU only); saved = [qkv, ctx,
+    x1, f] buffers the backward reads."""
+    _native().encoder_layer_fwd(x, ids, step, list(params), H, rate, seed, pad_id, eps,
+                                list(saved), y)
+
+
+def encoder_layer_bwd(x, ids, step, params, H, rate, seed, pad_id, eps, saved, dy, dx, part,
+                      grad):
+    """dx and the flat parameter gradient (summed over sequences in order)."""
+    _native().encoder_layer_bwd(x, ids, step, list(params), H, rate, seed, pad_id, eps,
+                                list(saved), dy, dx, part, grad)
+
+
 def embedding_segsort(v: int = -1) -> int:
     """One-hot embedding backward sort: 1 per-table LDS sort (default), 0 the
     device-wide radix sort; v < 0 only reads it. Returns the previous one."""

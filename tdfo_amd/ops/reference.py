@@ -533,3 +533,39 @@ def layernorm_bwd(x, g, n, gamma, mean, rstd, dx, dgb):
     dx.view(-1, n).copy_(dxv)
     dgb[:n].copy_((gv * xh).sum(0))
     dgb[n:].copy_(gv.sum(0))
+
+
+# ------------------------------------------------------------ encoder layer
+ENC_SITE_A, ENC_SITE_F, ENC_SITE_G, ENC_SITE_BLK = 1, 2, 3, 4
+
+
+def enc_site_mul(B: int, T: int, N: int, rate: float, seed: int, step: int, site: int, device):
+    """[B, T, N] dropout multiplier of sublayer site ``site`` in the fused
+    encoder-layer kernel (csrc/kernels/encoder.hip::site_mul)."""
+    if rate <= 0:
+        return torch.ones(B, T, N, device=device)
+    sd = (seed ^ ((step * 0x632BE5AB) & _M32)) & _M32
+    a = (sd ^ ((site * 0x27D4EB2F) & _M32)) & _M32
+    bt = (torch.arange(B, dtype=torch.int64, device=device).view(B, 1, 1) * 64 +
+          torch.arange(T, dtype=torch.int64, device=device).view(1, T, 1))
+    n = torch.arange(N, dtype=torch.int64, device=device).view(1, 1, N)
+    r = _hash3(torch.full((1,), a, dtype=torch.int64, device=device), bt, n)
+    keep = (r >> 8).to(torch.float32) * (1.0 / 16777216.0) >= rate
+    return keep.to(torch.float32) / (1.0 - rate)
+
+
+def encoder_layer(x, ids, params, H, rate, seed, step, pad_id=0, eps=1e-5):
+    """Differentiable torch reference of the fused pre-norm transformer block
+    (same math and dropout masks as csrc/kernels/encoder.hip)."""
+    wqkv, bqkv, wo, bo, g1, be1, g2, be2, w1, b1, w2, b2 = params
+    B, T, E = x.shape
+    dev = x.device
+    m = lambda site, N: enc_site_mul(B, T, N, rate, seed, step, site, dev)  # noqa: E731
+    h1 = torch.nn.functional.layer_norm(x, (E,), g1, be1, eps)
+    qkv = h1 @ wqkv.t() + bqkv
+    ctx = attention_core(qkv, ids, H, rate, seed, step, pad_id)
+    x1 = x + (ctx @ wo.t() + bo) * m(ENC_SITE_A, E)
+    h2 = torch.nn.functional.layer_norm(x1, (E,), g2, be2, eps)
+    f = torch.relu(h2 @ w1.t() + b1) * m(ENC_SITE_F, w1.shape[0])
+    x2 = x1 + (f @ w2.t() + b2) * m(ENC_SITE_G, E)
+    return x2 * m(ENC_SITE_BLK, E)

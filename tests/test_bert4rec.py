@@ -197,3 +197,23 @@ def test_reference_attention_core_matches_model_math():
     keep = ref.attn_keep_scale(B, H, T, 0.1, 5, 3, "cpu")
     frac = float((keep == 0).float().mean())
     assert 0.05 < frac < 0.15                  # ~rate of the elements dropped
+
+
+def test_encoder_layer_reference_matches_block():
+    """ops.reference.encoder_layer (the fused kernel's oracle) is the same math
+    as the module path of TransformerBlock when dropout is off."""
+    import torch
+
+    from tdfo_amd.models import bert4rec as m
+    from tdfo_amd.ops import reference as ref
+
+    torch.manual_seed(0)
+    B, T, E, H = 4, 9, 16, 2
+    blk = m.TransformerBlock(E, H, 0.0).eval()
+    x = torch.randn(B, T, E)
+    ids = torch.randint(0, 5, (B, T))
+    mask = (ids != 0).unsqueeze(1).unsqueeze(1)
+    exp = blk(x, mask)
+    got = ref.encoder_layer(x, ids, blk._fused_params(), H, 0.0, 1, 0, 0,
+                            blk.input_sublayer.norm.eps)
+    assert torch.allclose(got, exp, atol=1e-5, rtol=1e-5)
