@@ -463,7 +463,7 @@ void embedding_bwd(const Tensor& W, const Tensor& row_offset, const Tensor& indi
                    int64_t key_bits, const Tensor& grad, int64_t grad_stride, int64_t opt,
                    const c10::optional<Tensor>& state1, const c10::optional<Tensor>& state2,
                    const Tensor& hyper, double eps, double beta1, double beta2,
-                   double weight_decay, const c10::optional<Tensor>& dense_grad, bool segsort) {
+                   double weight_decay, const c10::optional<Tensor>& dense_grad, int64_t segsort) {
   check_dev(W, "W");
   TORCH_CHECK(W.scalar_type() == at::kFloat && W.is_contiguous() && W.dim() == 2, "W fp32 2-D");
   const int64_t D = W.size(1);
@@ -498,9 +498,9 @@ void embedding_bwd(const Tensor& W, const Tensor& row_offset, const Tensor& indi
   if (dense_grad) a.dense_grad = dense_grad->data_ptr<float>();
   a.hyper = hyper.data_ptr<float>();
   a.eps = (float)eps; a.beta1 = (float)beta1; a.beta2 = (float)beta2; a.weight_decay = (float)weight_decay;
-  // caller's promise: one id per bag and each virtual table a distinct
-  // physical table (rows of different segments never coincide)
-  a.segsort = segsort && nnz == T * B;
+  // caller's promise: one id per bag; virtual tables = segsort runs x
+  // physical tables, run-major (only runs of the same table share rows)
+  a.segsort = (segsort > 0 && nnz == T * B && T % segsort == 0) ? (int)segsort : 0;
   const size_t ws = tdfo::embedding_bwd_workspace(nnz, (int)D);
   Tensor work = at::empty({(int64_t)ws}, W.options().dtype(at::kByte));
   a.workspace = work.data_ptr(); a.workspace_bytes = ws;
@@ -786,7 +786,7 @@ TORCH_LIBRARY(tdfo, m) {
   m.def("embedding_bwd(Tensor(a!) W, Tensor row_offset, Tensor indices, Tensor offsets, Tensor grad_off, "
         "Tensor? psw, int T, int B, bool mean, int key_bits, Tensor grad, int grad_stride, int opt, "
         "Tensor(b!)? state1, Tensor(c!)? state2, Tensor hyper, float eps, float beta1, float beta2, "
-        "float weight_decay, Tensor(d!)? dense_grad, bool segsort) -> ()");
+        "float weight_decay, Tensor(d!)? dense_grad, int segsort) -> ()");
   m.def("dense_optimizer(Tensor(a!) p, Tensor g, Tensor(b!)? m, Tensor(c!)? v, Tensor(d!)? p_bf16, int opt, "
         "Tensor hyper, float beta1, float beta2, float eps, float wd, float momentum, Tensor? found_inf, "
         "Tensor[] seg_slabs, int[] seg_start, int[] seg_splits) -> ()");

@@ -120,7 +120,10 @@ struct EmbBwdArgs {
   float eps, beta1, beta2, weight_decay;
   float* dense_grad;           // EMB_DENSE_GRAD: accumulate into [rows, D]
   void* workspace; size_t workspace_bytes;
-  int segsort;                 // one id per bag, distinct tables: per-table LDS sort allowed
+  // one id per bag and T = R runs x Tp physical tables (virtual table v =
+  // run * Tp + table, runs of a table share its rows): per-table LDS sorts
+  // (+ a run merge when R > 1) replace the radix sort. 0: not applicable.
+  int segsort;
 };
 size_t embedding_bwd_workspace(int64_t nnz, int D);
 // One-hot batches (nnz == T*B, B <= 8192): per-table LDS sort in one launch

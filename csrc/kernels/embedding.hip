@@ -244,6 +244,64 @@ __global__ __launch_bounds__(SEG_THREADS) void emb_segsort_kernel(
   }
 }
 
+// Multi-source one-hot (world > 1): a physical table's ids arrive as R runs
+// (one per source rank, virtual table v = run * Tp + table), each sorted by
+// emb_segsort_kernel. One block per run places every element at its final
+// position: its index in its own run plus, for every other run, the number
+// of keys that sort before it there (ties: earlier runs first = the stable
+// order of the positions). Each thread owns 8 consecutive keys, binary-
+// searches the first and walks forward for the rest.
+template <typename K>
+__global__ __launch_bounds__(SEG_THREADS) void emb_runmerge_kernel(
+    int Tp, int R, int B, const K* __restrict__ kin, const int32_t* __restrict__ vin,
+    K* __restrict__ kout, int32_t* __restrict__ vout) {
+  __shared__ K other[SEG_MAX];
+  const int v = blockIdx.x, tid = threadIdx.x;
+  const int run = v / Tp, p = v - run * Tp;
+  const int64_t src = (int64_t)v * B;
+  const int i0 = tid * SEG_K;
+  K key[SEG_K];
+  int64_t pos[SEG_K];
+#pragma unroll
+  for (int k = 0; k < SEG_K; ++k) {
+    const int i = i0 + k;
+    key[k] = i < B ? kin[src + i] : (K)0;
+    pos[k] = i;
+  }
+  for (int r = 0; r < R; ++r) {
+    if (r == run) continue;
+    const int64_t o = (int64_t)(r * Tp + p) * B;
+    __syncthreads();
+    for (int i = tid; i < B; i += SEG_THREADS) other[i] = kin[o + i];
+    __syncthreads();
+    const bool le = r < run;               // earlier run: equal keys go first
+    // first key: count of other[] before key[0] (binary search)
+    int lo = 0, hi = B;
+    if (i0 < B) {
+      while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        const bool before = le ? other[mid] <= key[0] : other[mid] < key[0];
+        if (before) lo = mid + 1; else hi = mid;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < SEG_K; ++k) {
+      if (i0 + k >= B) break;
+      while (lo < B && (le ? other[lo] <= key[k] : other[lo] < key[k])) ++lo;
+      pos[k] += lo;
+    }
+  }
+  const int64_t base = (int64_t)p * R * B;
+#pragma unroll
+  for (int k = 0; k < SEG_K; ++k) {
+    const int i = i0 + k;
+    if (i < B) {
+      kout[base + pos[k]] = key[k];
+      vout[base + pos[k]] = vin[src + i];
+    }
+  }
+}
+
 template <int D>
 __device__ __forceinline__ int elem0(int lane) {
   return D >= 64 ? lane * (D / 64) : lane;
@@ -583,12 +641,21 @@ void bwd_impl(const EmbBwdArgs& a, const WsLayout& L, hipStream_t s) {
   int32_t* tcount = (int32_t*)(ws + L.tcount);
   int64_t kb = (a.nnz + 255) / 256;
   if (kb > 8192) kb = 8192;
-  const bool onehot = g_emb_segsort && a.segsort && a.nnz == (int64_t)a.T * a.B &&
-                      a.B <= SEG_MAX && !a.mean;
+  const int R = a.segsort;                 // runs per physical table (0: off)
+  const bool onehot = g_emb_segsort && R > 0 && a.T % R == 0 &&
+                      a.nnz == (int64_t)a.T * a.B && a.B <= SEG_MAX && !a.mean;
   int in_b = 1;
   if (onehot) {
-    hipLaunchKernelGGL(emb_segsort_kernel<K>, dim3(a.T), dim3(SEG_THREADS), 0, s, a, keys_out,
-                       vals_out, goff, gscale, tcount);
+    if (R == 1) {
+      hipLaunchKernelGGL(emb_segsort_kernel<K>, dim3(a.T), dim3(SEG_THREADS), 0, s, a, keys_out,
+                         vals_out, goff, gscale, tcount);
+    } else {
+      hipLaunchKernelGGL(emb_segsort_kernel<K>, dim3(a.T), dim3(SEG_THREADS), 0, s, a, keys_in,
+                         vals_in, goff, gscale, tcount);
+      TDFO_CHECK_HIP(hipGetLastError());
+      hipLaunchKernelGGL(emb_runmerge_kernel<K>, dim3(a.T), dim3(SEG_THREADS), 0, s, a.T / R, R,
+                         a.B, keys_in, vals_in, keys_out, vals_out);
+    }
   } else {
     hipLaunchKernelGGL(emb_keys_kernel<K>, dim3(kb), dim3(256), 0, s, a, keys_in, vals_in, goff,
                        gscale, tcount);

@@ -136,16 +136,17 @@ def embedding_bag_fwd(W, row_offset, indices, offsets, out_off, T, B, out, out_s
 
 def embedding_bwd(W, row_offset, indices, offsets, grad_off, T, B, grad, grad_stride, opt, hyper,
                   state1=None, state2=None, eps=1e-8, beta1=0.9, beta2=0.999, weight_decay=0.0,
-                  key_bits=None, mean=False, psw=None, dense_grad=None, segsort=False):
-    """Fused sort-based backward + optimizer. segsort=True promises one id per
-    bag and that no two virtual tables share rows (then a one-launch per-table
-    LDS sort replaces the device-wide radix sort)."""
+                  key_bits=None, mean=False, psw=None, dense_grad=None, segsort=0):
+    """Fused sort-based backward + optimizer. segsort=R > 0 promises one id
+    per bag and that the T virtual tables are R runs (run-major) of T/R
+    physical tables, only runs of the same table sharing rows; then per-table
+    LDS sorts (+ a run merge for R > 1) replace the device-wide radix sort."""
     if key_bits is None:
         key_bits = key_bits_for(W.shape[0])
     if _gpu(W):
         _native().embedding_bwd(W, row_offset, indices, offsets, grad_off, psw, T, B, mean,
                                 key_bits, grad, grad_stride, opt, state1, state2, hyper, eps,
-                                beta1, beta2, weight_decay, dense_grad, bool(segsort))
+                                beta1, beta2, weight_decay, dense_grad, int(segsort))
     else:
         ref.embedding_bwd(W, row_offset, indices, offsets, grad_off, psw, T, B, mean, key_bits,
                           grad, grad_stride, opt, state1, state2, hyper, eps, beta1, beta2,

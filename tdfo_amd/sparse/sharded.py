@@ -132,9 +132,13 @@ class ShardedEmbeddingBags:
                 v_row_off.append(self.tw_store.row_offset_host[i])
                 v_out_off.append(s * B * self.dsum[rank] + i * D)
         self.tw_nv = nv
-        # one id per bag and one source rank: every virtual table is its own
-        # physical table, so per-table sorts give the global (row) grouping
-        self.tw_segsort = W == 1 and all(self.L[t] == 1 for t in mine)
+        # one id per bag: virtual tables are W runs (one per source rank) of
+        # the local tables -> per-table LDS sorts + run merge in the backward.
+        # Measured (scripts/bench_segsort.py, B=8192): 110 vs 142 us at W=1,
+        # 134 vs 140 at W=2, but 207 vs 135 at W=8 (few large blocks) -> only
+        # up to 2 runs; beyond that the device-wide radix sort wins.
+        onehot = bool(mine) and all(self.L[t] == 1 for t in mine)
+        self.tw_segsort = W if (onehot and W <= 2) else 0
         offs = torch.zeros(len(lens) + 1, dtype=torch.int64)
         if lens:
             offs[1:] = torch.cumsum(torch.tensor(lens, dtype=torch.int64), 0)

@@ -155,7 +155,7 @@ class TableBatchedEmbedding:
                               out_stride, mean=mean, psw=psw)
 
     def backward_update(self, indices, offsets, row_offset, T, B, grad, grad_off, grad_stride,
-                        hyper, mean=False, psw=None, dense_grad=None, segsort=False):
+                        hyper, mean=False, psw=None, dense_grad=None, segsort=0):
         o = self.optim
         ops.embedding_bwd(self.weight, row_offset, indices, offsets, grad_off, T, B, grad,
                           grad_stride, o.code, hyper, state1=self.state1, state2=self.state2,

@@ -231,7 +231,7 @@ def test_embedding_bwd_onehot_segsort(B, skew, opt):
     s1 = torch.rand(n1, device=DEV)
     s2 = torch.rand(W.numel(), device=DEV) if opt == ops.EMB_ADAM else None
     res = []
-    for seg in (True, False):
+    for seg in (1, 0):
         Wn, a1 = W.clone(), s1.clone()
         a2 = s2.clone() if s2 is not None else None
         ops.embedding_bwd(Wn, ro, idx, offs, goff, T, B, grad, T * D, opt, hyper, state1=a1,
@@ -244,6 +244,35 @@ def test_embedding_bwd_onehot_segsort(B, skew, opt):
     ref.embedding_bwd(We, ro, idx, offs, goff, None, T, B, False, 20, grad, T * D, opt, e1, e2,
                       hyper, 1e-8, 0.9, 0.999, 0.0, None)
     assert (res[0][0] - We).abs().max() < 1e-4 * max(1.0, We.abs().max().item())
+
+
+@pytest.mark.parametrize("R", [2, 8])
+def test_embedding_bwd_onehot_multirun(R):
+    """World > 1 layout: each physical table's ids arrive as R runs (virtual
+    tables v = run * Tp + table sharing the table's rows). Per-run LDS sorts +
+    run merge must match the radix-sort path bit for bit."""
+    Tp, B, D = 3, 2048, 128
+    rows = [50, 9000, 70000]
+    g = torch.Generator().manual_seed(11)
+    T = R * Tp
+    ro_p = torch.tensor([0, 50, 9050])
+    ro = ro_p.repeat(R).to(DEV)
+    ids = torch.cat([torch.randint(0, min(rows[v % Tp], 40 if v % 2 else 10 ** 9), (B,), generator=g)
+                     for v in range(T)]).to(DEV)
+    offs = torch.arange(T * B + 1, device=DEV)
+    goff = torch.tensor([v * D for v in range(T)], device=DEV)
+    W = torch.randn(sum(rows), D, generator=g).to(DEV)
+    grad = torch.randn(B * T * D, generator=g).to(DEV)
+    hyper = torch.tensor([0.05, 3.0], device=DEV)
+    s1 = torch.rand(W.shape[0], device=DEV)
+    res = []
+    for seg in (R, 0):
+        Wn, a1 = W.clone(), s1.clone()
+        ops.embedding_bwd(Wn, ro, ids, offs, goff, T, B, grad, T * D, ops.EMB_ROWWISE_ADAGRAD,
+                          hyper, state1=a1, segsort=seg)
+        res.append((Wn, a1))
+    torch.cuda.synchronize()
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
 
 
 def test_embedding_bwd_deterministic():
