@@ -457,13 +457,10 @@ void embedding_bag_fwd(const Tensor& W, const Tensor& row_offset, const Tensor& 
   tdfo::embedding_bag_fwd(a, cur_stream());
 }
 
-void embedding_bwd(const Tensor& W, const Tensor& row_offset, const Tensor& indices,
-                   const Tensor& offsets, const Tensor& grad_off,
-                   const c10::optional<Tensor>& psw, int64_t T, int64_t B, bool mean,
-                   int64_t key_bits, const Tensor& grad, int64_t grad_stride, int64_t opt,
-                   const c10::optional<Tensor>& state1, const c10::optional<Tensor>& state2,
-                   const Tensor& hyper, double eps, double beta1, double beta2,
-                   double weight_decay, const c10::optional<Tensor>& dense_grad, int64_t segsort) {
+tdfo::EmbBwdArgs emb_bwd_args(const Tensor& W, const Tensor& row_offset, const Tensor& indices,
+                              const Tensor& offsets, const Tensor& grad_off,
+                              const c10::optional<Tensor>& psw, int64_t T, int64_t B, bool mean,
+                              int64_t key_bits, int64_t grad_stride, int64_t segsort) {
   check_dev(W, "W");
   TORCH_CHECK(W.scalar_type() == at::kFloat && W.is_contiguous() && W.dim() == 2, "W fp32 2-D");
   const int64_t D = W.size(1);
@@ -472,8 +469,6 @@ void embedding_bwd(const Tensor& W, const Tensor& row_offset, const Tensor& indi
   check_i64(offsets, "offsets"); check_i64(grad_off, "grad_off");
   TORCH_CHECK(offsets.numel() == T * B + 1 && grad_off.numel() == T && row_offset.numel() == T, "bwd counts");
   TORCH_CHECK(key_bits >= 1 && key_bits <= 64, "key_bits");
-  TORCH_CHECK(grad.is_contiguous() && (grad.scalar_type() == at::kBFloat16 || grad.scalar_type() == at::kFloat), "grad");
-  TORCH_CHECK(hyper.scalar_type() == at::kFloat && hyper.numel() >= 2 && hyper.is_cuda(), "hyper fp32[>=2] on device");
   const int64_t nnz = indices.numel();
   TORCH_CHECK(nnz < (1LL << 31), "nnz too large");
   tdfo::EmbBwdArgs a{};
@@ -482,7 +477,21 @@ void embedding_bwd(const Tensor& W, const Tensor& row_offset, const Tensor& indi
   a.offsets = offsets.data_ptr<int64_t>(); a.grad_off = grad_off.data_ptr<int64_t>();
   if (psw) a.psw = psw->data_ptr<float>();
   a.T = (int)T; a.B = (int)B; a.mean = mean; a.nnz = nnz; a.key_bits = (int)key_bits;
-  a.grad = grad.data_ptr(); a.grad_bf16 = grad.scalar_type() == at::kBFloat16; a.grad_stride = grad_stride;
+  a.grad_stride = grad_stride;
+  // caller's promise: one id per bag; virtual tables = segsort runs x
+  // physical tables, run-major (only runs of the same table share rows)
+  a.segsort = (segsort > 0 && nnz == T * B && T % segsort == 0) ? (int)segsort : 0;
+  return a;
+}
+
+void emb_bwd_opt_args(tdfo::EmbBwdArgs& a, const Tensor& W, const Tensor& grad, int64_t opt,
+                      const c10::optional<Tensor>& state1, const c10::optional<Tensor>& state2,
+                      const Tensor& hyper, double eps, double beta1, double beta2,
+                      double weight_decay, const c10::optional<Tensor>& dense_grad) {
+  const int64_t D = W.size(1);
+  TORCH_CHECK(grad.is_contiguous() && (grad.scalar_type() == at::kBFloat16 || grad.scalar_type() == at::kFloat), "grad");
+  TORCH_CHECK(hyper.scalar_type() == at::kFloat && hyper.numel() >= 2 && hyper.is_cuda(), "hyper fp32[>=2] on device");
+  a.grad = grad.data_ptr(); a.grad_bf16 = grad.scalar_type() == at::kBFloat16;
   a.opt = (int)opt;
   const int64_t rows = W.size(0);
   if (opt == tdfo::EMB_ROWWISE_ADAGRAD) {
@@ -498,13 +507,57 @@ void embedding_bwd(const Tensor& W, const Tensor& row_offset, const Tensor& indi
   if (dense_grad) a.dense_grad = dense_grad->data_ptr<float>();
   a.hyper = hyper.data_ptr<float>();
   a.eps = (float)eps; a.beta1 = (float)beta1; a.beta2 = (float)beta2; a.weight_decay = (float)weight_decay;
-  // caller's promise: one id per bag; virtual tables = segsort runs x
-  // physical tables, run-major (only runs of the same table share rows)
-  a.segsort = (segsort > 0 && nnz == T * B && T % segsort == 0) ? (int)segsort : 0;
-  const size_t ws = tdfo::embedding_bwd_workspace(nnz, (int)D);
-  Tensor work = at::empty({(int64_t)ws}, W.options().dtype(at::kByte));
+}
+
+void set_emb_ws(tdfo::EmbBwdArgs& a, const Tensor& work) {
+  const size_t ws = tdfo::embedding_bwd_workspace(a.nnz, a.D);
+  check_dev(work, "workspace");
+  TORCH_CHECK(work.is_contiguous() && (size_t)work.nbytes() >= ws, "embedding workspace too small");
   a.workspace = work.data_ptr(); a.workspace_bytes = ws;
+}
+
+void embedding_bwd(const Tensor& W, const Tensor& row_offset, const Tensor& indices,
+                   const Tensor& offsets, const Tensor& grad_off,
+                   const c10::optional<Tensor>& psw, int64_t T, int64_t B, bool mean,
+                   int64_t key_bits, const Tensor& grad, int64_t grad_stride, int64_t opt,
+                   const c10::optional<Tensor>& state1, const c10::optional<Tensor>& state2,
+                   const Tensor& hyper, double eps, double beta1, double beta2,
+                   double weight_decay, const c10::optional<Tensor>& dense_grad, int64_t segsort) {
+  auto a = emb_bwd_args(W, row_offset, indices, offsets, grad_off, psw, T, B, mean, key_bits,
+                        grad_stride, segsort);
+  emb_bwd_opt_args(a, W, grad, opt, state1, state2, hyper, eps, beta1, beta2, weight_decay,
+                   dense_grad);
+  const size_t ws = tdfo::embedding_bwd_workspace(a.nnz, a.D);
+  Tensor work = at::empty({(int64_t)ws}, W.options().dtype(at::kByte));
+  set_emb_ws(a, work);
   tdfo::embedding_bwd_fused(a, cur_stream());
+}
+
+void embedding_bwd_prepare(const Tensor& W, const Tensor& row_offset, const Tensor& indices,
+                           const Tensor& offsets, const Tensor& grad_off,
+                           const c10::optional<Tensor>& psw, int64_t T, int64_t B, bool mean,
+                           int64_t key_bits, int64_t grad_stride, int64_t segsort,
+                           const Tensor& work) {
+  auto a = emb_bwd_args(W, row_offset, indices, offsets, grad_off, psw, T, B, mean, key_bits,
+                        grad_stride, segsort);
+  set_emb_ws(a, work);
+  tdfo::embedding_bwd_prepare(a, cur_stream());
+}
+
+void embedding_bwd_apply(const Tensor& W, const Tensor& row_offset, const Tensor& indices,
+                         const Tensor& offsets, const Tensor& grad_off,
+                         const c10::optional<Tensor>& psw, int64_t T, int64_t B, bool mean,
+                         int64_t key_bits, const Tensor& grad, int64_t grad_stride, int64_t opt,
+                         const c10::optional<Tensor>& state1, const c10::optional<Tensor>& state2,
+                         const Tensor& hyper, double eps, double beta1, double beta2,
+                         double weight_decay, const c10::optional<Tensor>& dense_grad,
+                         int64_t segsort, const Tensor& work) {
+  auto a = emb_bwd_args(W, row_offset, indices, offsets, grad_off, psw, T, B, mean, key_bits,
+                        grad_stride, segsort);
+  emb_bwd_opt_args(a, W, grad, opt, state1, state2, hyper, eps, beta1, beta2, weight_decay,
+                   dense_grad);
+  set_emb_ws(a, work);
+  tdfo::embedding_bwd_apply(a, cur_stream());
 }
 
 // --------------------------------------------------------------- optim
@@ -787,6 +840,17 @@ TORCH_LIBRARY(tdfo, m) {
         "Tensor? psw, int T, int B, bool mean, int key_bits, Tensor grad, int grad_stride, int opt, "
         "Tensor(b!)? state1, Tensor(c!)? state2, Tensor hyper, float eps, float beta1, float beta2, "
         "float weight_decay, Tensor(d!)? dense_grad, int segsort) -> ()");
+  m.def("embedding_bwd_workspace(int nnz, int D) -> int", [](int64_t nnz, int64_t D) {
+    return (int64_t)tdfo::embedding_bwd_workspace(nnz < 1 ? 1 : nnz, (int)D);
+  });
+  m.def("embedding_bwd_prepare(Tensor W, Tensor row_offset, Tensor indices, Tensor offsets, "
+        "Tensor grad_off, Tensor? psw, int T, int B, bool mean, int key_bits, int grad_stride, "
+        "int segsort, Tensor(a!) workspace) -> ()");
+  m.def("embedding_bwd_apply(Tensor(a!) W, Tensor row_offset, Tensor indices, Tensor offsets, "
+        "Tensor grad_off, Tensor? psw, int T, int B, bool mean, int key_bits, Tensor grad, "
+        "int grad_stride, int opt, Tensor(b!)? state1, Tensor(c!)? state2, Tensor hyper, "
+        "float eps, float beta1, float beta2, float weight_decay, Tensor(d!)? dense_grad, "
+        "int segsort, Tensor(e!) workspace) -> ()");
   m.def("dense_optimizer(Tensor(a!) p, Tensor g, Tensor(b!)? m, Tensor(c!)? v, Tensor(d!)? p_bf16, int opt, "
         "Tensor hyper, float beta1, float beta2, float eps, float wd, float momentum, Tensor? found_inf, "
         "Tensor[] seg_slabs, int[] seg_start, int[] seg_splits) -> ()");
@@ -825,6 +889,8 @@ TORCH_LIBRARY_IMPL(tdfo, CUDA, m) {
   m.impl("interaction_bwd", interaction_bwd);
   m.impl("embedding_bag_fwd", embedding_bag_fwd);
   m.impl("embedding_bwd", embedding_bwd);
+  m.impl("embedding_bwd_prepare", embedding_bwd_prepare);
+  m.impl("embedding_bwd_apply", embedding_bwd_apply);
   m.impl("dense_optimizer", dense_optimizer);
   m.impl("check_finite", check_finite);
   m.impl("sort_pairs", sort_pairs);

@@ -75,6 +75,8 @@ void cross_bwd(const uint16_t* dout, const uint16_t* x0, const uint16_t* y, int6
 size_t radix_sort_workspace(int64_t n);
 // digit bits per radix pass (4..10); returns the previous value (b < 4: read only)
 int radix_sort_max_bits(int b);
+// number of digit passes for key_bits (odd: the sorted result lands in (kb, vb))
+int radix_sort_passes(int key_bits);
 // 1: per-pass hist kernels, 0: next-pass hist counted by the scatter (atomics)
 int radix_sort_sep_hist(int v);
 int radix_sort_pairs_u32(uint32_t* ka, int32_t* va, uint32_t* kb, int32_t* vb, int64_t n,
@@ -131,6 +133,12 @@ size_t embedding_bwd_workspace(int64_t nnz, int D);
 // previous setting.
 int embedding_segsort(int v);
 void embedding_bwd_fused(const EmbBwdArgs& a, hipStream_t s);
+// The same in two halves around a workspace that persists between them:
+// prepare needs only the ids (keys, sort, gradient offsets) and can run on a
+// side stream while the dense forward/backward computes; apply does the
+// segment reduction + optimizer once the gradient exists.
+void embedding_bwd_prepare(const EmbBwdArgs& a, hipStream_t s);
+void embedding_bwd_apply(const EmbBwdArgs& a, hipStream_t s);
 
 // ------------------------------------------------------------ optim ----
 // Flat fused optimizer over one contiguous fp32 parameter buffer.

@@ -626,8 +626,8 @@ WsLayout ws_layout(int64_t nnz, int D) {
   return L;
 }
 
-template <int D, typename K, int OPT>
-void bwd_impl(const EmbBwdArgs& a, const WsLayout& L, hipStream_t s) {
+template <typename K>
+void prep_impl(const EmbBwdArgs& a, const WsLayout& L, hipStream_t s) {
   char* ws = (char*)a.workspace;
   K* keys_in = (K*)(ws + L.keys_in);
   K* keys_out = (K*)(ws + L.keys_out);
@@ -635,16 +635,10 @@ void bwd_impl(const EmbBwdArgs& a, const WsLayout& L, hipStream_t s) {
   int32_t* vals_out = (int32_t*)(ws + L.vals_out);
   int64_t* goff = (int64_t*)(ws + L.goff);
   float* gscale = (a.psw || a.mean) ? (float*)(ws + L.gscale) : nullptr;
-  float* head = (float*)(ws + L.head);
-  float* tail = (float*)(ws + L.tail);
-  int32_t* tlist = (int32_t*)(ws + L.tlist);
   int32_t* tcount = (int32_t*)(ws + L.tcount);
-  int64_t kb = (a.nnz + 255) / 256;
-  if (kb > 8192) kb = 8192;
   const int R = a.segsort;                 // runs per physical table (0: off)
   const bool onehot = g_emb_segsort && R > 0 && a.T % R == 0 &&
                       a.nnz == (int64_t)a.T * a.B && a.B <= SEG_MAX && !a.mean;
-  int in_b = 1;
   if (onehot) {
     if (R == 1) {
       hipLaunchKernelGGL(emb_segsort_kernel<K>, dim3(a.T), dim3(SEG_THREADS), 0, s, a, keys_out,
@@ -657,18 +651,36 @@ void bwd_impl(const EmbBwdArgs& a, const WsLayout& L, hipStream_t s) {
                          a.B, keys_in, vals_in, keys_out, vals_out);
     }
   } else {
-    hipLaunchKernelGGL(emb_keys_kernel<K>, dim3(kb), dim3(256), 0, s, a, keys_in, vals_in, goff,
-                       gscale, tcount);
+    // generate where an even/odd number of passes leaves the result in *_out
+    const bool odd = radix_sort_passes(a.key_bits) & 1;
+    K* k0 = odd ? keys_in : keys_out;
+    K* k1 = odd ? keys_out : keys_in;
+    int32_t* v0 = odd ? vals_in : vals_out;
+    int32_t* v1 = odd ? vals_out : vals_in;
+    int64_t kb = (a.nnz + 255) / 256;
+    if (kb > 8192) kb = 8192;
+    hipLaunchKernelGGL(emb_keys_kernel<K>, dim3(kb), dim3(256), 0, s, a, k0, v0, goff, gscale,
+                       tcount);
     TDFO_CHECK_HIP(hipGetLastError());
     if constexpr (sizeof(K) == 4)
-      in_b = radix_sort_pairs_u32(keys_in, vals_in, keys_out, vals_out, a.nnz, a.key_bits,
-                                  ws + L.sortws, s);
+      radix_sort_pairs_u32(k0, v0, k1, v1, a.nnz, a.key_bits, ws + L.sortws, s);
     else
-      in_b = radix_sort_pairs_u64(keys_in, vals_in, keys_out, vals_out, a.nnz, a.key_bits,
-                                  ws + L.sortws, s);
+      radix_sort_pairs_u64(k0, v0, k1, v1, a.nnz, a.key_bits, ws + L.sortws, s);
   }
   TDFO_CHECK_HIP(hipGetLastError());
-  if (!in_b) { keys_out = keys_in; vals_out = vals_in; }
+}
+
+template <int D, typename K, int OPT>
+void apply_impl(const EmbBwdArgs& a, const WsLayout& L, hipStream_t s) {
+  char* ws = (char*)a.workspace;
+  K* keys_out = (K*)(ws + L.keys_out);
+  int32_t* vals_out = (int32_t*)(ws + L.vals_out);
+  int64_t* goff = (int64_t*)(ws + L.goff);
+  float* gscale = (a.psw || a.mean) ? (float*)(ws + L.gscale) : nullptr;
+  float* head = (float*)(ws + L.head);
+  float* tail = (float*)(ws + L.tail);
+  int32_t* tlist = (int32_t*)(ws + L.tlist);
+  int32_t* tcount = (int32_t*)(ws + L.tcount);
   constexpr int CH = BwdCfg<D>::CH;
   const int64_t nch = (a.nnz + CH - 1) / CH;
   const int64_t blocks = (nch + 3) / 4;
@@ -689,11 +701,11 @@ void bwd_impl(const EmbBwdArgs& a, const WsLayout& L, hipStream_t s) {
 template <int D, typename K>
 void bwd_opt(const EmbBwdArgs& a, const WsLayout& L, hipStream_t s) {
   switch (a.opt) {
-    case EMB_SGD: bwd_impl<D, K, EMB_SGD>(a, L, s); break;
-    case EMB_ROWWISE_ADAGRAD: bwd_impl<D, K, EMB_ROWWISE_ADAGRAD>(a, L, s); break;
-    case EMB_ADAM: bwd_impl<D, K, EMB_ADAM>(a, L, s); break;
-    case EMB_ADAGRAD: bwd_impl<D, K, EMB_ADAGRAD>(a, L, s); break;
-    case EMB_DENSE_GRAD: bwd_impl<D, K, EMB_DENSE_GRAD>(a, L, s); break;
+    case EMB_SGD: apply_impl<D, K, EMB_SGD>(a, L, s); break;
+    case EMB_ROWWISE_ADAGRAD: apply_impl<D, K, EMB_ROWWISE_ADAGRAD>(a, L, s); break;
+    case EMB_ADAM: apply_impl<D, K, EMB_ADAM>(a, L, s); break;
+    case EMB_ADAGRAD: apply_impl<D, K, EMB_ADAGRAD>(a, L, s); break;
+    case EMB_DENSE_GRAD: apply_impl<D, K, EMB_DENSE_GRAD>(a, L, s); break;
     default: throw std::runtime_error("unknown embedding optimizer");
   }
 }
@@ -740,6 +752,18 @@ size_t embedding_bwd_workspace(int64_t nnz, int D) {
 }
 
 void embedding_bwd_fused(const EmbBwdArgs& a, hipStream_t s) {
+  embedding_bwd_prepare(a, s);
+  embedding_bwd_apply(a, s);
+}
+
+void embedding_bwd_prepare(const EmbBwdArgs& a, hipStream_t s) {
+  if (a.nnz <= 0) return;
+  const WsLayout L = ws_layout(a.nnz, a.D);
+  if (a.key_bits <= 32) prep_impl<uint32_t>(a, L, s);
+  else prep_impl<uint64_t>(a, L, s);
+}
+
+void embedding_bwd_apply(const EmbBwdArgs& a, hipStream_t s) {
   if (a.nnz <= 0) return;
   const WsLayout L = ws_layout(a.nnz, a.D);
   switch (a.D) {

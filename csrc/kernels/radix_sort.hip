@@ -229,6 +229,11 @@ int sort_impl(K* ka, int32_t* va, K* kb, int32_t* vb, int64_t n, int key_bits, i
 
 }  // namespace
 
+int radix_sort_passes(int key_bits) {
+  const int kbits = key_bits < 1 ? 1 : key_bits;
+  return (kbits + g_max_bits - 1) / g_max_bits;
+}
+
 int radix_sort_sep_hist(int v) {
   const int old = g_sep_hist;
   if (v >= 0) g_sep_hist = v ? 1 : 0;

@@ -274,6 +274,10 @@ class DLRMTrainer:
         # multi-rank: top wgrads after the interaction backward, so the
         # embedding-grad all-to-all overlaps them (per-layer buffers: no reuse)
         self._defer_top_wgrad = world_size > 1 and cfg.interaction == "dot"
+        # ids-only half of the embedding backward (keys + sort) on its own
+        # stream beside the top MLP: it needs no gradient, and its few
+        # latency-bound blocks leave the GEMMs most of the machine
+        self._ps = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
         on_gpu = dev.type == "cuda" and bool(cfg.overlap)
         self._ws = torch.cuda.Stream(device=dev) if on_gpu else None
         self._es = (torch.cuda.Stream(device=dev)
@@ -428,6 +432,10 @@ class DLRMTrainer:
         D, F = cfg.embedding_dim, self.F
         emb = self.emb
         self._join(self._es)
+        if self._ps is not None:
+            self._ps.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(self._ps):
+                emb.stage_bwd_prepare()
         h = self.h_out
         L0 = self.top_layers[0]
         if cfg.interaction == "dot":
@@ -462,6 +470,7 @@ class DLRMTrainer:
         else:
             self._dcn_backward(h)
         self._join(self._ws)
+        self._join(self._ps)
 
     def _s_top_wgrad(self):
         """Top-MLP weight grads, deferred past the interaction backward when the

@@ -153,6 +153,33 @@ def embedding_bwd(W, row_offset, indices, offsets, grad_off, T, B, grad, grad_st
                           weight_decay, dense_grad)
 
 
+def embedding_bwd_workspace(nnz: int, D: int) -> int:
+    return int(_native().embedding_bwd_workspace(int(nnz), int(D)))
+
+
+def embedding_bwd_prepare(W, row_offset, indices, offsets, grad_off, T, B, grad_stride, workspace,
+                          key_bits=None, mean=False, psw=None, segsort=0):
+    """First half of the fused embedding backward (GPU): keys, sort and
+    gradient offsets into ``workspace`` -- needs only the ids, so it can run
+    on a side stream before the gradient exists."""
+    if key_bits is None:
+        key_bits = key_bits_for(W.shape[0])
+    _native().embedding_bwd_prepare(W, row_offset, indices, offsets, grad_off, psw, T, B, mean,
+                                    key_bits, grad_stride, int(segsort), workspace)
+
+
+def embedding_bwd_apply(W, row_offset, indices, offsets, grad_off, T, B, grad, grad_stride, opt,
+                        hyper, workspace, state1=None, state2=None, eps=1e-8, beta1=0.9,
+                        beta2=0.999, weight_decay=0.0, key_bits=None, mean=False, psw=None,
+                        dense_grad=None, segsort=0):
+    """Second half: segment reduction + optimizer from a prepared workspace."""
+    if key_bits is None:
+        key_bits = key_bits_for(W.shape[0])
+    _native().embedding_bwd_apply(W, row_offset, indices, offsets, grad_off, psw, T, B, mean,
+                                  key_bits, grad, grad_stride, opt, state1, state2, hyper, eps,
+                                  beta1, beta2, weight_decay, dense_grad, int(segsort), workspace)
+
+
 def dense_optimizer(p, g, m, v, p_bf16, opt, hyper, beta1=0.9, beta2=0.999, eps=1e-8, wd=0.0,
                     momentum=0.0, found_inf=None, segments=()):
     """Fused flat optimizer. ``segments``: (start, slab, splits) triples whose

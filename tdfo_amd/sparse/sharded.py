@@ -461,16 +461,26 @@ class ShardedEmbeddingBags:
             self._dp_work = None
         self._bw = (None, d_recv)
 
+    def stage_bwd_prepare(self):
+        """Ids-only part of the table-wise shard backward (keys + sort): needs
+        no gradient, so the trainer runs it on a side stream during the dense
+        forward/backward (after stage_fwd_ids_exchange)."""
+        if self.tw_nv:
+            self.tw_store.backward_prepare(self.tw_recv_ids, self.tw_v_offsets, self.tw_v_row_off,
+                                           self.tw_nv, self.B, self.tw_v_out_off,
+                                           self.dsum[self.rank], mean=self.mean,
+                                           segsort=self.tw_segsort)
+
     def stage_bwd_update(self, hyper: torch.Tensor):
         """Fused sort-based backward + optimizer on this rank's table-wise shards."""
         d_recv = self._bw[1] if getattr(self, "_bw", None) else self.d_recv
         W, B = self.world, self.B
         grad = self.d_pooled if W > 1 else d_recv
         if self.tw_nv:
-            self.tw_store.backward_update(self.tw_recv_ids, self.tw_v_offsets, self.tw_v_row_off,
-                                          self.tw_nv, B, grad, self.tw_v_out_off,
-                                          self.dsum[self.rank], hyper, mean=self.mean,
-                                          segsort=self.tw_segsort)
+            self.tw_store.backward_apply(self.tw_recv_ids, self.tw_v_offsets, self.tw_v_row_off,
+                                         self.tw_nv, B, grad, self.tw_v_out_off,
+                                         self.dsum[self.rank], hyper, mean=self.mean,
+                                         segsort=self.tw_segsort)
         if self.cw_tables and self.cw_nv:
             self.cw_store.backward_update(self.cw_recv_ids, self.cw_v_offsets, self.cw_v_row_off,
                                           self.cw_nv, B, grad, self.cw_v_out_off,

@@ -163,6 +163,38 @@ class TableBatchedEmbedding:
                           key_bits=self.key_bits, mean=mean, psw=psw, dense_grad=dense_grad,
                           segsort=segsort)
 
+    def backward_prepare(self, indices, offsets, row_offset, T, B, grad_off, grad_stride,
+                         mean=False, psw=None, segsort=0):
+        """Ids-only half of the backward (keys + sort) into a persistent
+        workspace; GPU only (CPU: no-op, backward_apply does everything)."""
+        self._prepared = None
+        if not self.weight.is_cuda or indices.numel() == 0:
+            return
+        need = ops.embedding_bwd_workspace(indices.numel(), self.dim)
+        if getattr(self, "_bwd_ws", None) is None or self._bwd_ws.numel() < need:
+            self._bwd_ws = torch.empty(need, dtype=torch.uint8, device=self.weight.device)
+        ops.embedding_bwd_prepare(self.weight, row_offset, indices, offsets, grad_off, T, B,
+                                  grad_stride, self._bwd_ws, key_bits=self.key_bits, mean=mean,
+                                  psw=psw, segsort=segsort)
+        self._prepared = (indices.data_ptr(), indices.numel(), T, B)
+
+    def backward_apply(self, indices, offsets, row_offset, T, B, grad, grad_off, grad_stride,
+                       hyper, mean=False, psw=None, dense_grad=None, segsort=0):
+        """Gradient half after backward_prepare (falls back to the fused
+        backward_update when nothing was prepared for these ids)."""
+        key = (indices.data_ptr(), indices.numel(), T, B)
+        if getattr(self, "_prepared", None) != key:
+            return self.backward_update(indices, offsets, row_offset, T, B, grad, grad_off,
+                                        grad_stride, hyper, mean=mean, psw=psw,
+                                        dense_grad=dense_grad, segsort=segsort)
+        o = self.optim
+        ops.embedding_bwd_apply(self.weight, row_offset, indices, offsets, grad_off, T, B, grad,
+                                grad_stride, o.code, hyper, self._bwd_ws, state1=self.state1,
+                                state2=self.state2, eps=o.eps, beta1=o.beta1, beta2=o.beta2,
+                                weight_decay=o.weight_decay, key_bits=self.key_bits, mean=mean,
+                                psw=psw, dense_grad=dense_grad, segsort=segsort)
+        self._prepared = None
+
     def table_weight(self, t: int) -> torch.Tensor:
         s = self.row_offset_host[t]
         return self.weight[s: s + self.row_counts[t]]

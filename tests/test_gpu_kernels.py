@@ -275,6 +275,34 @@ def test_embedding_bwd_onehot_multirun(R):
     assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
 
 
+@pytest.mark.parametrize("segsort", [0, 1])
+def test_embedding_bwd_prepare_apply_matches_fused(segsort):
+    """The two-phase backward (ids-only prepare on another stream, then apply)
+    gives the fused result bit for bit."""
+    T, B, D = 3, 4096, 128
+    rows = [50, 9000, 70000]
+    W, ro, idx, offs = _emb_case(T, B, rows, D, 1 if segsort else 3, False, seed=9)
+    W, ro, idx, offs = (x.to(DEV) for x in (W, ro, idx, offs))
+    goff = torch.tensor([t * D for t in range(T)], device=DEV)
+    grad = torch.randn(B * T * D, device=DEV)
+    hyper = torch.tensor([0.05, 3.0], device=DEV)
+    s1 = torch.rand(W.shape[0], device=DEV)
+    Wf, sf = W.clone(), s1.clone()
+    ops.embedding_bwd(Wf, ro, idx, offs, goff, T, B, grad, T * D, ops.EMB_ROWWISE_ADAGRAD, hyper,
+                      state1=sf, segsort=segsort)
+    Wp, sp = W.clone(), s1.clone()
+    ws = torch.empty(ops.embedding_bwd_workspace(idx.numel(), D), dtype=torch.uint8, device=DEV)
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side):
+        ops.embedding_bwd_prepare(Wp, ro, idx, offs, goff, T, B, T * D, ws, segsort=segsort)
+    torch.cuda.current_stream().wait_stream(side)
+    ops.embedding_bwd_apply(Wp, ro, idx, offs, goff, T, B, grad, T * D, ops.EMB_ROWWISE_ADAGRAD,
+                            hyper, ws, state1=sp, segsort=segsort)
+    torch.cuda.synchronize()
+    assert torch.equal(Wf, Wp) and torch.equal(sf, sp)
+
+
 def test_embedding_bwd_deterministic():
     T, B, D = 2, 4096, 128
     rows = [3, 100000]
