@@ -83,10 +83,17 @@ def linear_dgrad(dy, w, mask=None, out=None):
     return out
 
 
-def wgrad_splits(M: int, N: int, K: int, target_blocks: int = 512) -> int:
+# split-K block target for weight grads. In-step A/B (XCD-remapped split-K,
+# direct fp32 slab stores): DLRM 0.621 ms at 256 vs 0.636-0.641 at 512, 0.646
+# at 1024, 0.670 at 128; DCN-v2 2.902 vs 3.003 (512), 3.200 (128).
+_WGRAD_TARGET = int(__import__("os").environ.get("TDFO_WGRAD_TARGET", "256"))
+
+
+def wgrad_splits(M: int, N: int, K: int, target_blocks: int = 0) -> int:
     """Split-K count for a weight-grad GEMM (K = batch): ~target_blocks blocks,
     but every split keeps >= 8 K tiles (measured on MI355X: bot/top3 wgrads run
     18.8 us at 16 splits vs 22.7 us at 64; top1 is best at 8)."""
+    target_blocks = target_blocks or _WGRAD_TARGET
     tiles = ((M + 127) // 128) * ((N + 127) // 128)
     kt = K // 64
     s = max(1, min(max(1, kt // 8), -(-target_blocks // tiles)))
