@@ -175,7 +175,8 @@ __device__ __forceinline__ bool direct_ok(const GemmArgs& p, int m0, int n0, int
   if (p.abl & (224 | 256)) return false;           // ablations / forced LDS path
   // operand reads (ReLU mask, DCN mul/add) in this layout are 32-B row runs;
   // the LDS path reads them as 256-B rows (measured: DCN-v2 3.16 vs 3.05 ms)
-  if (p.mask || p.mul || p.add) return false;
+  if (p.mul || p.add) return false;
+  if (p.mask && !(p.abl & 512)) return false;      // abl 512: masked dgrads direct too (A/B)
   if (m0 + rows > p.M || n0 + 128 > p.N) return false;
   if (p.C && ((p.ldc & 7) || !al16(p.C))) return false;
   if (p.mask && ((p.ldm & 7) || !al16(p.mask))) return false;
@@ -650,7 +651,8 @@ void launch(const GemmArgs& a, hipStream_t s) {
   b.abl = g_policy >= 8 ? g_policy - 8 : 0;      // perf ablations (policy 9..15), big kernel
   if (g_policy == 6) b.abl = 128;                // auto, every output through the LDS epilogue
   if (g_policy == 7) b.abl = 256;                // auto, bf16 outputs through the LDS epilogue
-  const bool autop = g_policy == 0 || g_policy == 6 || g_policy == 7;
+  if (g_policy == 17) b.abl = 512;               // auto, masked dgrads on the direct path
+  const bool autop = g_policy == 0 || g_policy == 6 || g_policy == 7 || g_policy == 17;
   bool big = (g_policy >= 2 && g_policy != 3 && g_policy != 4 && !autop) ||
              (g_policy == 4 && AC) || (autop && small_tiles * a.splits >= 1024);
   if (big) {
