@@ -33,7 +33,19 @@ __global__ __launch_bounds__(256) void dense_opt_kernel(DenseOptArgs a) {
       const int64_t o = e - a.seg_start[sk], L = a.seg_len[sk];
       const float* sp = a.seg_ptr[sk];
       g = make_float4(0.f, 0.f, 0.f, 0.f);
-      for (int q = 0; q < a.seg_splits[sk]; ++q) {
+      // slab loads issued 4 at a time (independent), summed in slab order
+      const int S = a.seg_splits[sk];
+      int q = 0;
+      for (; q + 4 <= S; q += 4) {
+        float4 t[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) t[u] = *(const float4*)(sp + (q + u) * L + o);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          g.x += t[u].x; g.y += t[u].y; g.z += t[u].z; g.w += t[u].w;
+        }
+      }
+      for (; q < S; ++q) {
         const float4 t = *(const float4*)(sp + q * L + o);
         g.x += t.x; g.y += t.y; g.z += t.z; g.w += t.w;
       }
