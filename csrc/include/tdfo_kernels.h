@@ -99,6 +99,7 @@ struct EmbFwdArgs {
   int T, B, mean;
   int64_t out_stride;
   void* out; int out_bf16;
+  int onehot;                  // caller's promise: offsets[j] == j (one id per bag)
 };
 void embedding_bag_fwd(const EmbFwdArgs& a, hipStream_t s);
 

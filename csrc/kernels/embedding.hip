@@ -30,6 +30,46 @@ namespace tdfo {
 namespace {
 
 // ----------------------------------------------------------- forward ----
+// One id per bag (offsets[j] == j): no offsets loads, and every lane group
+// keeps two bags' row gathers in flight (index load -> row load is the whole
+// dependency chain).
+template <int D, bool OUT_BF16>
+__global__ __launch_bounds__(256) void emb_fwd_onehot_kernel(EmbFwdArgs a) {
+  constexpr int LPB = (D / 4) < 64 ? (D / 4) : 64;  // lanes per bag
+  constexpr int BPW = 64 / LPB;                     // bags per wave
+  const int lane = threadIdx.x & 63;
+  const int sub = lane / LPB, sl = lane - sub * LPB;
+  const int64_t nbags = (int64_t)a.T * a.B;
+  const int64_t wave0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t step = ((int64_t)gridDim.x * blockDim.x >> 6) * BPW;
+  for (int64_t j0 = wave0 * BPW + sub; j0 < nbags; j0 += 2 * step) {
+    const int64_t j1 = j0 + step;
+    const bool has1 = j1 < nbags;
+    const int t0 = (int)(j0 / a.B), t1 = has1 ? (int)(j1 / a.B) : t0;
+    const int64_t id0 = a.indices[j0], id1 = has1 ? a.indices[j1] : id0;
+    const float* r0 = a.W + (a.row_offset[t0] + id0) * D;
+    const float* r1 = a.W + (a.row_offset[t1] + id1) * D;
+    for (int c = sl * 4; c < D; c += LPB * 4) {
+      const float4 v0 = *(const float4*)(r0 + c);
+      const float4 v1 = *(const float4*)(r1 + c);
+      const float w0 = a.psw ? a.psw[j0] : 1.f, w1 = a.psw ? a.psw[j1 < nbags ? j1 : j0] : 1.f;
+      const float4 o0 = make_float4(v0.x * w0, v0.y * w0, v0.z * w0, v0.w * w0);
+      const float4 o1 = make_float4(v1.x * w1, v1.y * w1, v1.z * w1, v1.w * w1);
+      const int64_t b0 = j0 - (int64_t)t0 * a.B, b1 = j1 - (int64_t)t1 * a.B;
+      const int64_t p0 = b0 * a.out_stride + a.out_off[t0] + c;
+      const int64_t p1 = b1 * a.out_stride + a.out_off[t1] + c;
+      if (OUT_BF16) {
+        *(uint2*)((uint16_t*)a.out + p0) = make_uint2(pack2bf(o0.x, o0.y), pack2bf(o0.z, o0.w));
+        if (has1)
+          *(uint2*)((uint16_t*)a.out + p1) = make_uint2(pack2bf(o1.x, o1.y), pack2bf(o1.z, o1.w));
+      } else {
+        *(float4*)((float*)a.out + p0) = o0;
+        if (has1) *(float4*)((float*)a.out + p1) = o1;
+      }
+    }
+  }
+}
+
 template <int D, bool OUT_BF16>
 __global__ __launch_bounds__(256) void emb_fwd_kernel(EmbFwdArgs a) {
   constexpr int LPB = (D / 4) < 64 ? (D / 4) : 64;  // lanes per bag
@@ -726,8 +766,13 @@ void embedding_bag_fwd(const EmbFwdArgs& a, hipStream_t s) {
   int64_t blocks = (waves + 3) / 4;
   if (blocks > 8192) blocks = 8192;
 #define TDFO_EF(DD)                                                            \
-  if (a.out_bf16) hipLaunchKernelGGL((emb_fwd_kernel<DD, true>), dim3(blocks), \
-                                     dim3(256), 0, s, a);                     \
+  if (a.onehot && !a.mean) {                                                   \
+    if (a.out_bf16) hipLaunchKernelGGL((emb_fwd_onehot_kernel<DD, true>),      \
+                                       dim3(blocks), dim3(256), 0, s, a);      \
+    else hipLaunchKernelGGL((emb_fwd_onehot_kernel<DD, false>), dim3(blocks),  \
+                            dim3(256), 0, s, a);                               \
+  } else if (a.out_bf16) hipLaunchKernelGGL((emb_fwd_kernel<DD, true>),        \
+                                            dim3(blocks), dim3(256), 0, s, a); \
   else hipLaunchKernelGGL((emb_fwd_kernel<DD, false>), dim3(blocks),           \
                           dim3(256), 0, s, a)
   switch (a.D) {

@@ -287,7 +287,8 @@ class ItemEmbedding(nn.Module):
     def _lookup(self, ids):
         n = ids.numel()
         out = self.out[:n]
-        self.store.forward(ids, self.offsets[: n + 1], self.zero, 1, n, out, self.zero, self.D)
+        self.store.forward(ids, self.offsets[: n + 1], self.zero, 1, n, out, self.zero, self.D,
+                           onehot=True)
         self._ids = ids
         return out.clone()
 

@@ -132,10 +132,12 @@ def interaction_bwd(dz, dense, emb, off, stride, F, D, d_dense, d_emb, doff, dst
 
 
 def embedding_bag_fwd(W, row_offset, indices, offsets, out_off, T, B, out, out_stride, mean=False,
-                      psw=None):
+                      psw=None, onehot=False):
+    """onehot=True promises offsets == arange (one id per bag): the kernel then
+    skips the offsets loads and keeps two bags' row gathers in flight."""
     if _gpu(W):
         _native().embedding_bag_fwd(W, row_offset, indices, offsets, out_off, psw, T, B, mean, out,
-                                    out_stride)
+                                    out_stride, bool(onehot))
     else:
         ref.embedding_bag_fwd(W, row_offset, indices, offsets, out_off, psw, T, B, mean, out,
                               out_stride)

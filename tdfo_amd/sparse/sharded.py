@@ -138,6 +138,7 @@ class ShardedEmbeddingBags:
         # 134 vs 140 at W=2, but 207 vs 135 at W=8 (few large blocks) -> only
         # up to 2 runs; beyond that the device-wide radix sort wins.
         onehot = bool(mine) and all(self.L[t] == 1 for t in mine)
+        self.tw_onehot = onehot
         self.tw_segsort = W if (onehot and W <= 2) else 0
         offs = torch.zeros(len(lens) + 1, dtype=torch.int64)
         if lens:
@@ -361,7 +362,8 @@ class ShardedEmbeddingBags:
         if self.tw_nv:
             self.tw_store.forward(self.tw_recv_ids, self.tw_v_offsets, self.tw_v_row_off, self.tw_nv,
                                   B, self.tw_pooled if W > 1 else self.recv, self.tw_v_out_off,
-                                  self.dsum[self.rank], mean=self.mean)
+                                  self.dsum[self.rank], mean=self.mean,
+                                  onehot=self.tw_onehot)
         if self.cw_tables and self.cw_nv:
             self.cw_store.forward(self.cw_recv_ids, self.cw_v_offsets, self.cw_v_row_off,
                                   self.cw_nv, B, self.tw_pooled if W > 1 else self.recv,

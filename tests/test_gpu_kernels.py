@@ -171,6 +171,26 @@ def test_embedding_fwd(D, L, mean):
     assert rel_err(out, exp) < 1e-2
 
 
+@pytest.mark.parametrize("D", [16, 128])
+@pytest.mark.parametrize("bf16_out,use_psw", [(True, False), (False, True)])
+def test_embedding_fwd_onehot_path(D, bf16_out, use_psw):
+    """onehot=True (no offsets loads, two bags in flight) == the general kernel."""
+    T, B = 5, 3001
+    rows = [100, 7, 5000, 1, 70000]
+    W, ro, idx, offs = _emb_case(T, B, rows, D, 1, False, seed=3)
+    W, ro, idx, offs = (x.to(DEV) for x in (W, ro, idx, offs))
+    out_off = torch.tensor([t * D for t in range(T)], device=DEV)
+    psw = torch.rand(idx.numel(), device=DEV) if use_psw else None
+    dt = torch.bfloat16 if bf16_out else torch.float32
+    outs = []
+    for oh in (True, False):
+        out = torch.zeros(B * T * D, dtype=dt, device=DEV)
+        ops.embedding_bag_fwd(W, ro, idx, offs, out_off, T, B, out, T * D, psw=psw, onehot=oh)
+        outs.append(out)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("opt", [ops.EMB_SGD, ops.EMB_ROWWISE_ADAGRAD, ops.EMB_ADAM,
                                  ops.EMB_ADAGRAD, ops.EMB_DENSE_GRAD])
 @pytest.mark.parametrize("skew", [False, True])
