@@ -127,6 +127,7 @@ struct EmbBwdArgs {
   // run * Tp + table, runs of a table share its rows): per-table LDS sorts
   // (+ a run merge when R > 1) replace the radix sort. 0: not applicable.
   int segsort;
+  int goff_sorted;             // internal: grad offsets stored in sorted order
 };
 size_t embedding_bwd_workspace(int64_t nnz, int D);
 // One-hot batches (nnz == T*B, B <= 8192): per-table LDS sort in one launch

@@ -180,7 +180,7 @@ constexpr int SEG_BINS = 1 << SEG_BITS;
 constexpr int SEG_WAVES = SEG_THREADS / 64;
 constexpr int SEG_CNT = SEG_BINS * SEG_K * SEG_WAVES;   // 8192 counters
 
-template <typename K>
+template <typename K, bool SORTED_G>
 __global__ __launch_bounds__(SEG_THREADS) void emb_segsort_kernel(
     const EmbBwdArgs a, K* __restrict__ keys_out, int32_t* __restrict__ vals_out,
     int64_t* __restrict__ goff, float* __restrict__ gscale, int32_t* __restrict__ tail_count) {
@@ -203,8 +203,10 @@ __global__ __launch_bounds__(SEG_THREADS) void emb_segsort_kernel(
       key[k] = (uint32_t)a.indices[p];
       val[k] = (uint32_t)i;
       kmax = max(kmax, key[k]);
-      goff[p] = (int64_t)i * a.grad_stride + a.grad_off[t];
-      if (gscale) gscale[p] = a.psw ? a.psw[p] : 1.f;
+      if (!SORTED_G) {
+        goff[p] = (int64_t)i * a.grad_stride + a.grad_off[t];
+        if (gscale) gscale[p] = a.psw ? a.psw[p] : 1.f;
+      }
     } else {
       key[k] = 0xffffffffu;                          // sorts after every real id
       val[k] = 0;
@@ -274,12 +276,17 @@ __global__ __launch_bounds__(SEG_THREADS) void emb_segsort_kernel(
     __syncthreads();
   }
   const K kb = (K)a.row_offset[t];
+  const int64_t go = a.grad_off[t];
 #pragma unroll
   for (int k = 0; k < SEG_K; ++k) {
     const int i = k * SEG_THREADS + tid;
     if (i < n) {
       keys_out[s0 + i] = kb + (K)key[k];
       vals_out[s0 + i] = (int32_t)(s0 + val[k]);
+      if (SORTED_G) {     // gradient-row offset (and scale) already in sorted order
+        goff[s0 + i] = (int64_t)val[k] * a.grad_stride + go;
+        if (gscale) gscale[s0 + i] = a.psw ? a.psw[s0 + val[k]] : 1.f;
+      }
     }
   }
 }
@@ -518,8 +525,9 @@ __global__ __launch_bounds__(256) void emb_chunk_kernel(
   const int li = lane < len ? lane : len - 1;     // lanes >= len duplicate the last entry
   const K mykey = keys[start + li];
   const int mypos = vals[start + li];
-  const int64_t mygoff = goff[mypos];
-  const float mysc = gscale ? gscale[mypos] : 1.f;
+  const int64_t gi = a.goff_sorted ? start + li : mypos;   // sorted: no pos indirection
+  const int64_t mygoff = goff[gi];
+  const float mysc = gscale ? gscale[gi] : 1.f;
   const K prevk = start > 0 ? keys[start - 1] : (K)0;
   const K nextk = end < a.nnz ? keys[end] : (K)0;
   const K kup = __shfl_up(mykey, 1, 64);
@@ -666,6 +674,13 @@ WsLayout ws_layout(int64_t nnz, int D) {
   return L;
 }
 
+// prepare's choice of path (apply must read the layout prepare wrote)
+bool onehot_path(const EmbBwdArgs& a) {
+  const int R = a.segsort;
+  return g_emb_segsort && R > 0 && a.T % R == 0 && a.nnz == (int64_t)a.T * a.B &&
+         a.B <= SEG_MAX && !a.mean;
+}
+
 template <typename K>
 void prep_impl(const EmbBwdArgs& a, const WsLayout& L, hipStream_t s) {
   char* ws = (char*)a.workspace;
@@ -677,14 +692,12 @@ void prep_impl(const EmbBwdArgs& a, const WsLayout& L, hipStream_t s) {
   float* gscale = (a.psw || a.mean) ? (float*)(ws + L.gscale) : nullptr;
   int32_t* tcount = (int32_t*)(ws + L.tcount);
   const int R = a.segsort;                 // runs per physical table (0: off)
-  const bool onehot = g_emb_segsort && R > 0 && a.T % R == 0 &&
-                      a.nnz == (int64_t)a.T * a.B && a.B <= SEG_MAX && !a.mean;
-  if (onehot) {
+  if (onehot_path(a)) {
     if (R == 1) {
-      hipLaunchKernelGGL(emb_segsort_kernel<K>, dim3(a.T), dim3(SEG_THREADS), 0, s, a, keys_out,
-                         vals_out, goff, gscale, tcount);
+      hipLaunchKernelGGL((emb_segsort_kernel<K, true>), dim3(a.T), dim3(SEG_THREADS), 0, s, a,
+                         keys_out, vals_out, goff, gscale, tcount);
     } else {
-      hipLaunchKernelGGL(emb_segsort_kernel<K>, dim3(a.T), dim3(SEG_THREADS), 0, s, a, keys_in,
+      hipLaunchKernelGGL((emb_segsort_kernel<K, false>), dim3(a.T), dim3(SEG_THREADS), 0, s, a, keys_in,
                          vals_in, goff, gscale, tcount);
       TDFO_CHECK_HIP(hipGetLastError());
       hipLaunchKernelGGL(emb_runmerge_kernel<K>, dim3(a.T), dim3(SEG_THREADS), 0, s, a.T / R, R,
@@ -711,7 +724,9 @@ void prep_impl(const EmbBwdArgs& a, const WsLayout& L, hipStream_t s) {
 }
 
 template <int D, typename K, int OPT>
-void apply_impl(const EmbBwdArgs& a, const WsLayout& L, hipStream_t s) {
+void apply_impl(const EmbBwdArgs& a0, const WsLayout& L, hipStream_t s) {
+  EmbBwdArgs a = a0;
+  a.goff_sorted = onehot_path(a0) && a0.segsort == 1;
   char* ws = (char*)a.workspace;
   K* keys_out = (K*)(ws + L.keys_out);
   int32_t* vals_out = (int32_t*)(ws + L.vals_out);
