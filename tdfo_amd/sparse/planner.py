@@ -22,7 +22,7 @@ Sharding kinds:
 from __future__ import annotations
 
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional, Sequence
+from typing import Callable, Dict, List, Optional, Sequence
 
 from .tables import EmbOptimConfig, TableConfig
 
@@ -68,12 +68,21 @@ def _mem_per_row(dim: int, optim: EmbOptimConfig) -> int:
 def plan_sharding(tables: Sequence[TableConfig], world_size: int, optim: EmbOptimConfig,
                   batch_per_rank: int = 8192, pooling: Optional[Sequence[float]] = None,
                   hbm_bytes: int = HBM_BYTES, reserve_frac: float = 0.15,
-                  strategy: str = "auto", dp_max_bytes: int = 0) -> ShardingPlan:
+                  strategy: str = "auto", dp_max_bytes: int = 0,
+                  row_cost: Optional[Callable[[int], float]] = None) -> ShardingPlan:
     """Deterministic greedy planner.
 
     strategy: "auto" (table-wise with row-wise fallback for tables that fit
     no rank), "table_wise", "row_wise", "column_wise" (tables split evenly by
     columns), "data_parallel".
+
+    row_cost: optional per-lookup cost multiplier as a function of a table's
+    row count. Default: none -- measured on MI355X at the world-8 layout
+    (scripts/bench_emb_rank.py, profiles/emb_rank_w8.jsonl) a rank's
+    embedding time tracks its id count far more than its table sizes (a
+    4-row and a 40M-row table cost 85 vs 103 us per 65536 ids, while the
+    4-table ranks of the world-8 plan, holding only small tables, are the
+    slowest at 188 us vs 140-164 us for the 3-table ranks).
     """
     W = world_size
     cap = int(hbm_bytes * (1.0 - reserve_frac))
@@ -84,9 +93,12 @@ def plan_sharding(tables: Sequence[TableConfig], world_size: int, optim: EmbOpti
     cost = [0.0] * W
     shards: List[Optional[TableShard]] = [None] * T
 
+    rc = row_cost or (lambda rows: 1.0)
+
     def tcost(t: int) -> float:
         d = tables[t].embedding_dim
-        return gb * pooling[t] * d * 4 * 3 / 1e9 + gb * d * 2 * 2 / 1e9
+        return (gb * pooling[t] * d * 4 * 3 / 1e9 * rc(tables[t].num_embeddings)
+                + gb * d * 2 * 2 / 1e9)
 
     order = sorted(range(T), key=lambda t: (-tcost(t), -tables[t].num_embeddings, t))
 
