@@ -24,6 +24,7 @@ namespace tdfo {
 namespace {
 
 constexpr int WAVES = 4;
+constexpr int SLOT_BYTES = 64 * 8;   // backward: SlotMap copy at the LDS base
 
 __device__ __forceinline__ const uint16_t* feat_row(const uint16_t* dense,
                                                     int64_t ld_dense,
@@ -114,7 +115,15 @@ __global__ __launch_bounds__(256) void inter_bwd_kernel(
   constexpr int XB = 32 * D * 2;  // X image bytes per wave
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int ldz_al = (int)((ldz + 7) & ~7LL);
-  char* base = smem_raw + w * (XB + ldz_al * 2);
+  // slot offsets / strides in LDS: the unrolled chunk loads below index them
+  // per lane, which on the kernel-argument struct would go through scratch
+  int64_t* slot = (int64_t*)smem_raw;   // [0, 32): off, [32, 64): stride
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int q = 0; q < 32; ++q) { slot[q] = sm.off[q]; slot[32 + q] = sm.stride[q]; }
+  }
+  __syncthreads();
+  char* base = smem_raw + SLOT_BYTES + w * (XB + ldz_al * 2);
   char* xs = base;
   // dX image [32][D] aliases the X image (same chunk swizzle): column tile nt
   // is written only after its MFMAs consumed X's same columns, and the
@@ -123,6 +132,7 @@ __global__ __launch_bounds__(256) void inter_bwd_kernel(
   uint16_t* ys = (uint16_t*)base;
   uint16_t* zrow = (uint16_t*)(base + XB);
   constexpr int CPR = D / 8;  // 16-B chunks per X row
+  constexpr int XC = (32 * CPR + 63) / 64;  // X chunks per lane (F <= 32)
   const int h = lane >> 5;
 
   // rows >= F of the image stay zero for every sample
@@ -136,16 +146,32 @@ __global__ __launch_bounds__(256) void inter_bwd_kernel(
     const int b = (it * gridDim.x + blockIdx.x) * WAVES + w;
     const bool valid = b < B;
     if (valid) {
+      // every X chunk load is issued before the first LDS write, so the
+      // sample costs one HBM round trip instead of one per 64-chunk pass
+      // (each wave owns ~1 sample: the kernel is latency-bound otherwise)
+      s16x8_t xv[XC];
+#pragma unroll
+      for (int k = 0; k < XC; ++k) {
+        const int c = lane + 64 * k;
+        if (c < F * CPR) {
+          const int j = c / CPR, ch = c - j * CPR;
+          const uint16_t* rp = j == 0 ? dense + (int64_t)b * ld_dense
+                                      : emb + slot[j] + (int64_t)b * slot[32 + j];
+          xv[k] = *(const s16x8_t*)(rp + ch * 8);
+        }
+      }
       const uint16_t* zp = dz + (int64_t)b * ldz;
       for (int c = lane; c < ldz_al / 8; c += 64) {
         if (c * 8 + 8 <= ldz) *(uint4*)(zrow + c * 8) = *(const uint4*)(zp + c * 8);
         else for (int e = c * 8; e < ldz_al; ++e) zrow[e] = e < ldz ? zp[e] : 0;
       }
-      for (int c = lane; c < F * CPR; c += 64) {
-        const int j = c / CPR, ch = c - j * CPR;
-        const uint16_t* rp = feat_row(dense, ld_dense, emb, sm, j, F, b);
-        *(uint4*)(xs + j * D * 2 + ((ch ^ xswz<D>(j)) << 4)) =
-            *(const uint4*)(rp + ch * 8);
+#pragma unroll
+      for (int k = 0; k < XC; ++k) {
+        const int c = lane + 64 * k;
+        if (c < F * CPR) {
+          const int j = c / CPR, ch = c - j * CPR;
+          *(s16x8_t*)(xs + j * D * 2 + ((ch ^ xswz<D>(j)) << 4)) = xv[k];
+        }
       }
     }
     wave_sync();
@@ -259,7 +285,7 @@ void interaction_bwd(const uint16_t* dz, int64_t ldz, const uint16_t* dense,
                      const SlotMap& dslots, int relu_mask, hipStream_t s) {
   if (B <= 0) return;
   const int ldz_al = (int)((ldz + 7) & ~7LL);
-  const size_t smem = (size_t)WAVES * (32 * D * 2 + ldz_al * 2);
+  const size_t smem = SLOT_BYTES + (size_t)WAVES * (32 * D * 2 + ldz_al * 2);
   dim3 grid(grid_for(B));
 #define TDFO_IBWD(DD)                                                          \
   if (smem > 65536)                                                            \
