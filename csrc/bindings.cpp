@@ -613,6 +613,30 @@ void cast_bf16(const Tensor& x, const Tensor& y) {
   tdfo::cast_f32_bf16(x.data_ptr<float>(), bf16_mut(y), x.numel(), cur_stream());
 }
 
+void batch_load(const Tensor& dense, const Tensor& x0, const Tensor& ids, const Tensor& ids_dst,
+                const Tensor& label, const Tensor& label_dst) {
+  check_dev(dense, "dense"); check_dev(x0, "x0");
+  TORCH_CHECK(dense.dim() == 2 && dense.scalar_type() == at::kFloat && dense.stride(1) == 1,
+              "batch_load: dense fp32 [B, nd] row-major");
+  TORCH_CHECK(x0.dim() == 2 && x0.scalar_type() == at::kBFloat16 && x0.stride(1) == 1 &&
+              x0.size(0) == dense.size(0) && x0.size(1) >= dense.size(1), "batch_load: x0 bf16");
+  TORCH_CHECK(ids.scalar_type() == at::kLong && ids_dst.scalar_type() == at::kLong &&
+              ids.is_contiguous() && ids_dst.is_contiguous() && ids.numel() == ids_dst.numel(),
+              "batch_load: ids int64, same size");
+  TORCH_CHECK(aligned16(ids.data_ptr()) && aligned16(ids_dst.data_ptr()), "batch_load: ids alignment");
+  TORCH_CHECK(label.scalar_type() == at::kFloat && label_dst.scalar_type() == at::kFloat &&
+              label.is_contiguous() && label_dst.is_contiguous() &&
+              label.numel() == dense.size(0) && label_dst.numel() == dense.size(0),
+              "batch_load: label fp32 [B]");
+  TORCH_CHECK(ids.device() == x0.device() && label.device() == x0.device() &&
+              ids_dst.device() == x0.device() && label_dst.device() == x0.device(),
+              "batch_load: one device");
+  tdfo::batch_load(dense.data_ptr<float>(), (int)dense.size(1), dense.stride(0), bf16_mut(x0),
+                   x0.stride(0), ids.data_ptr<int64_t>(), ids_dst.data_ptr<int64_t>(), ids.numel(),
+                   label.data_ptr<float>(), label_dst.data_ptr<float>(), (int)dense.size(0),
+                   cur_stream());
+}
+
 // ------------------------------------------------------------ loss etc.
 void head_bce(const Tensor& H, const Tensor& w, const Tensor& b, const Tensor& label,
               double inv_n, bool relu_mask, const Tensor& logits, const Tensor& dH,
@@ -858,6 +882,8 @@ TORCH_LIBRARY(tdfo, m) {
   m.def("check_finite(Tensor g, Tensor(a!) found) -> ()");
   m.def("sort_pairs(Tensor keys, Tensor vals, int key_bits) -> (Tensor, Tensor)");
   m.def("cast_bf16(Tensor x, Tensor(a!) y) -> ()");
+  m.def("batch_load(Tensor dense, Tensor(a!) x0, Tensor ids, Tensor(b!) ids_dst, Tensor label, "
+        "Tensor(c!) label_dst) -> ()");
   m.def("head_bce(Tensor H, Tensor w, Tensor b, Tensor label, float inv_n, bool relu_mask, "
         "Tensor(a!) logits, Tensor(b!) dH, Tensor(c!) part) -> ()");
   m.def("head_reduce(Tensor part, int nparts, int K, Tensor(a!) grad, Tensor(b!) loss_acc, "
@@ -884,6 +910,7 @@ TORCH_LIBRARY_IMPL(tdfo, CUDA, m) {
   m.impl("layernorm_bwd", layernorm_bwd);
   m.impl("gather_columns", gather_columns);
   m.impl("concat_features", concat_features);
+  m.impl("batch_load", batch_load);
   m.impl("split_features", split_features);
   m.impl("cross_bwd", cross_bwd);
   m.impl("interaction_fwd", interaction_fwd);

@@ -163,6 +163,10 @@ void dense_optimizer(const DenseOptArgs& a, hipStream_t s);
 // found_inf[0] = any(!isfinite(g)) over n (caller zeroes it first).
 void check_finite(const float* g, int64_t n, float* found_inf, hipStream_t s);
 void cast_f32_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t s);
+// Batch inputs in one launch: ids copy, label copy, dense fp32 -> bf16 x0[:, :nd].
+void batch_load(const float* dense, int nd, int64_t ld_dense, uint16_t* x0, int64_t ldx,
+                const int64_t* ids, int64_t* ids_dst, int64_t n, const float* label,
+                float* label_dst, int B, hipStream_t s);
 
 // ---------------------------------------------------- loss / reduce ----
 // Fused last layer (K -> 1) + sigmoid BCE-with-logits + backward:

@@ -166,6 +166,34 @@ __global__ __launch_bounds__(256) void gather_columns_kernel(GatherColsArgs a) {
   }
 }
 
+
+// One launch for a training batch's host-visible inputs: the int64 ids, the
+// fp32 labels and the fp32 dense features cast into the bf16 bottom-MLP input
+// (row stride ldx, first nd columns). Replaces three copies and a cast kernel
+// per step (each small launch costs ~5 us of device time).
+__global__ __launch_bounds__(256) void batch_load_kernel(
+    const float* __restrict__ dense, int nd, int64_t ld_dense, uint16_t* __restrict__ x0,
+    int64_t ldx, const int64_t* __restrict__ ids, int64_t* __restrict__ ids_dst, int64_t n,
+    const float* __restrict__ label, float* __restrict__ label_dst, int B) {
+  const int64_t n2 = n / 2, nden = (int64_t)B * nd;
+  const int64_t total = n2 + (n & 1) + nden + B;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    if (i < n2) {
+      ((longlong2*)ids_dst)[i] = ((const longlong2*)ids)[i];
+    } else if (i < n2 + (n & 1)) {
+      ids_dst[n - 1] = ids[n - 1];
+    } else if (i < n2 + (n & 1) + nden) {
+      const int64_t e = i - n2 - (n & 1);
+      const int64_t b = e / nd;
+      const int c = (int)(e - b * nd);
+      x0[b * ldx + c] = f2bf(dense[b * ld_dense + c]);
+    } else {
+      const int64_t b = i - n2 - (n & 1) - nden;
+      label_dst[b] = label[b];
+    }
+  }
+}
 }  // namespace
 
 void gather_columns(const GatherColsArgs& a, hipStream_t s) {
@@ -174,6 +202,18 @@ void gather_columns(const GatherColsArgs& a, hipStream_t s) {
   int64_t blocks = (total + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(gather_columns_kernel, dim3(blocks), dim3(256), 0, s, a);
+  TDFO_CHECK_HIP(hipGetLastError());
+}
+
+void batch_load(const float* dense, int nd, int64_t ld_dense, uint16_t* x0, int64_t ldx,
+                const int64_t* ids, int64_t* ids_dst, int64_t n, const float* label,
+                float* label_dst, int B, hipStream_t s) {
+  const int64_t total = n / 2 + (n & 1) + (int64_t)B * nd + B;
+  if (total <= 0) return;
+  int64_t blocks = (total + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(batch_load_kernel, dim3(blocks), dim3(256), 0, s, dense, nd, ld_dense, x0,
+                     ldx, ids, ids_dst, n, label, label_dst, B);
   TDFO_CHECK_HIP(hipGetLastError());
 }
 

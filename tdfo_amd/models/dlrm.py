@@ -323,9 +323,8 @@ class DLRMTrainer:
         dense [B, num_dense] (any float dtype), ids flat int64 in table order
         (table t: B*L_t ids), label [B] float.
         """
-        self.x0[:, : self.cfg.num_dense].copy_(dense, non_blocking=True)
-        self.ids.copy_(ids, non_blocking=True)
-        self.label.copy_(label, non_blocking=True)
+        # device-resident batch: one fused launch (ids, labels, dense -> bf16)
+        ops.batch_load(dense, self.x0, ids, self.ids, label, self.label)
 
     # ------------------------------------------------------------- layers
     def _fwd(self, L: Lin, x, out, relu=True):

@@ -263,6 +263,17 @@ def cast_bf16(x, y):
         ref.cast_bf16(x, y)
 
 
+def batch_load(dense, x0, ids, ids_dst, label, label_dst):
+    """x0[:, :nd] = bf16(dense), ids_dst = ids, label_dst = label (one launch on GPU)."""
+    if _gpu(x0) and dense.is_cuda and ids.is_cuda and label.is_cuda and \
+            dense.dtype == torch.float32 and dense.stride(-1) == 1:
+        _native().batch_load(dense, x0, ids.contiguous(), ids_dst, label.contiguous(), label_dst)
+    else:
+        x0[:, :dense.shape[1]].copy_(dense, non_blocking=True)
+        ids_dst.copy_(ids, non_blocking=True)
+        label_dst.copy_(label, non_blocking=True)
+
+
 def concat_features(dense, emb, off, stride, F, D, out):
     if _gpu(dense):
         _native().concat_features(dense, emb, list(off), list(stride), F, D, out)

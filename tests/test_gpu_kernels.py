@@ -682,3 +682,22 @@ def test_gather_columns_matches_index_select():
     assert torch.equal(X[:, 5], src[4].index_select(0, idx))
     ops.gather_columns(src[:1], None, 100, n, [outi[0]], [1])   # contiguous range
     assert torch.equal(outi[0], src[0][100:100 + n].long())
+
+
+# ------------------------------------------------------------------ batch load
+@pytest.mark.parametrize("n", [8192 * 26, 4097])
+def test_batch_load_matches_copies(n):
+    B, nd, ldx = 1024, 13, 32
+    g = torch.Generator(device=DEV).manual_seed(3)
+    dense = torch.rand(B, nd, device=DEV, generator=g) * 5
+    ids = torch.randint(0, 1 << 40, (n,), device=DEV, generator=g)
+    label = (torch.rand(B, device=DEV, generator=g) > 0.5).float()
+    x0 = torch.full((B, ldx), 7.0, device=DEV, dtype=torch.bfloat16)
+    ids_dst = torch.empty_like(ids)
+    label_dst = torch.empty_like(label)
+    torch.ops.tdfo.batch_load(dense, x0, ids, ids_dst, label, label_dst)
+    torch.cuda.synchronize()
+    assert torch.equal(ids_dst, ids)
+    assert torch.equal(label_dst, label)
+    assert torch.equal(x0[:, :nd], dense.to(torch.bfloat16))
+    assert torch.all(x0[:, nd:] == 7.0)          # pad / bias columns untouched
