@@ -73,14 +73,21 @@ __global__ __launch_bounds__(256) void inter_fwd_kernel(
         if (rp) fr[s] = *(const bf16x8_t*)(rp + 16 * s + 8 * h);
         else    fr[s] = __builtin_bit_cast(bf16x8_t, (s16x8_t){0,0,0,0,0,0,0,0});
       }
+      // dense passthrough chunk, loaded with the feature rows (one HBM
+      // round trip per sample)
+      const uint16_t* dp = dense + (int64_t)b * ld_dense;
+      constexpr int PC = (D / 8 + 63) / 64;
+      s16x8_t pv[PC];
+#pragma unroll
+      for (int k = 0; k < PC; ++k)
+        if (lane + 64 * k < D / 8) pv[k] = *(const s16x8_t*)(dp + (lane + 64 * k) * 8);
       f32x16_t acc = {};
 #pragma unroll
       for (int s = 0; s < KS; ++s)
         acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fr[s], fr[s], acc, 0, 0, 0);
-      // dense passthrough into LDS row
-      const uint16_t* dp = dense + (int64_t)b * ld_dense;
-      for (int c = lane; c < D / 8; c += 64)
-        *(uint4*)(row + c * 8) = *(const uint4*)(dp + c * 8);
+#pragma unroll
+      for (int k = 0; k < PC; ++k)
+        if (lane + 64 * k < D / 8) *(s16x8_t*)(row + (lane + 64 * k) * 8) = pv[k];
       const int col = lane & 31;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
