@@ -10,14 +10,21 @@ Embeddings: table-wise sharded across ranks (all on one GPU at N=1), fused
 row-wise Adagrad; dense: fused AdamW, all-reduced over RCCL.
 Weak scaling: --batch is per GPU; value = global examples / second.
 
-Launch: python bench.py [--gpus 1]; for N>1 via
-  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+Launch: python bench.py [--gpus N]. With N > 1 and no WORLD_SIZE in the
+environment, bench.py starts the N rank processes itself (a child
+``torch.distributed.run`` on 127.0.0.1, before any GPU call) and exits with
+its code; the driver's own ``torch.distributed.run ... bench.py --gpus N``
+lands directly in the rank code. One rank per GPU over RCCL: N must not
+exceed the visible GPUs (the multi-rank rehearsal on one GPU sets
+TDFO_SHARE_DEVICE=1 TDFO_DIST_BACKEND=gloo explicitly).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -60,18 +67,53 @@ def parallelism(plan, world: int) -> str:
     return f"dp{world} dense + emb[{kinds} tables] over {world} ranks"
 
 
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def self_launch(args, argv) -> int:
+    """Start ``args.gpus`` rank processes (one per GPU) and return their exit
+    code. Runs before anything touches the GPU (device_count() does not
+    initialise HIP on this image)."""
+    n = args.gpus
+    share = os.environ.get("TDFO_SHARE_DEVICE") == "1"
+    if share and os.environ.get("TDFO_DIST_BACKEND", "nccl") == "nccl":
+        print(f"error: --gpus {n} with TDFO_SHARE_DEVICE=1 needs TDFO_DIST_BACKEND=gloo "
+              "(RCCL cannot put two ranks on one GPU)", file=sys.stderr)
+        return 2
+    if not share:
+        have = torch.cuda.device_count()
+        if have < n:
+            print(f"error: --gpus {n} but only {have} GPU(s) visible; bench.py runs one rank "
+                  "per GPU over RCCL (RCCL cannot put two ranks on one GPU). Refusing to "
+                  f"report an N=1 measurement as N={n}.", file=sys.stderr)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}",
+           os.path.abspath(__file__), *argv]
+    return subprocess.call(cmd)
+
+
 def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
     args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args, argv))
     from tdfo_amd.parallel.dist import init_distributed, reset
     from tdfo_amd.models.dlrm import (CRITEO_1TB_ROWS, CRITEO_KAGGLE_ROWS, MLPERF_MULTIHOT,
                                       DLRMConfig, DLRMTrainer)
     from tdfo_amd.data.synthetic import SyntheticCriteo
     from tdfo_amd.ops import _ext
 
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env != args.gpus:
+        raise SystemExit(f"error: --gpus {args.gpus} but WORLD_SIZE={world_env}")
     info = init_distributed("cuda")
     world = info.world_size
-    if world != args.gpus:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     if not _ext.load():
         raise RuntimeError("native HIP library failed to load")
     if os.environ.get("TDFO_GEMM_POLICY"):      # override the trainer's per-model choice
@@ -122,10 +164,12 @@ def main(argv=None):
     loss = tr.pop_loss() / max(1, args.steps * B)
     ms = el / args.steps * 1e3
     value = B * world * args.steps / el
+    sol = cfg.sol(B, world)
     if info.rank == 0:
         print(json.dumps({"plan": tr.plan.summary(), "setup_s": round(setup_s, 1),
                           "train_loss": round(loss, 4), "graph": use_graph,
-                          "dense_tflops": round(cfg.dense_flops_per_example() * value / 1e12, 1)}),
+                          "dense_tflops": round(cfg.dense_flops_per_example() * value / 1e12, 1),
+                          "sol": {k: round(v, 4) for k, v in sol.items()}}),
               file=sys.stderr)
         print(json.dumps({
             "metric": "examples/sec (whole node) DLRM on Criteo-1TB-shaped synthetic",
@@ -135,8 +179,10 @@ def main(argv=None):
             "vs_baseline": (round(value / (EAGER_BASELINE_EX_S[args.rows] * world), 2)
                             if args.model == "dlrm" and args.rows in EAGER_BASELINE_EX_S
                             and args.batch == 8192 else None),
+            "sol_ms": round(sol["sol_ms"], 4),
+            "frac_of_sol": round(sol["sol_ms"] / ms, 3),
             "dtype": "bf16",
-            "data": "synthetic (Criteo-1TB-shaped, uniform ids, random-init embeddings)",
+            "data": f"synthetic (Criteo-{args.rows}-shaped, {args.dist} ids, random-init embeddings)",
             "config": {"model": "DLRM" if args.model == "dlrm" else "DCN-v2",
                        "global_batch": B * world, "seq_len": None,
                        "parallelism": parallelism(tr.plan, world),

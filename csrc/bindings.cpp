@@ -561,6 +561,98 @@ void embedding_bwd_apply(const Tensor& W, const Tensor& row_offset, const Tensor
   tdfo::embedding_bwd_apply(a, cur_stream());
 }
 
+// ------------------------------------------------------- row-wise shards
+int64_t rw_meta_check(const Tensor& meta, int64_t nrw) {
+  check_i64(meta, "rw meta");
+  TORCH_CHECK(nrw >= 1 && meta.numel() == 5 * nrw + 1, "rw meta must hold 5*nrw+1 int64");
+  return nrw;
+}
+
+int64_t rw_bucketize_workspace(int64_t n, int64_t W) {
+  return (int64_t)tdfo::rw_bucketize_workspace(n, (int)W);
+}
+
+void rw_bucketize(const Tensor& ids, const Tensor& meta, int64_t nrw, int64_t W, int64_t B,
+                  int64_t cap, int64_t n, const Tensor& send, const Tensor& work,
+                  const Tensor& overflow) {
+  check_i64(ids, "ids"); rw_meta_check(meta, nrw); check_i64(send, "send");
+  TORCH_CHECK(W >= 1 && W <= 64, "rw: world size must be in [1, 64]");
+  TORCH_CHECK(send.numel() == W * (cap + 1), "rw send buffer must be [W][cap+1]");
+  TORCH_CHECK(nrw * B < (1LL << 31), "rw: bag keys must fit 31 bits");
+  check_dev(work, "rw workspace");
+  TORCH_CHECK((size_t)work.nbytes() >= tdfo::rw_bucketize_workspace(n, (int)W), "rw workspace too small");
+  check_dev(overflow, "overflow");
+  TORCH_CHECK(overflow.scalar_type() == at::kInt && overflow.numel() >= 1, "overflow int32[1]");
+  tdfo::RwBucketArgs a{};
+  a.ids = ids.data_ptr<int64_t>(); a.meta = meta.data_ptr<int64_t>();
+  a.nrw = (int)nrw; a.W = (int)W; a.B = (int)B; a.cap = cap; a.n = n;
+  a.send = send.data_ptr<int64_t>(); a.overflow = overflow.data_ptr<int32_t>();
+  tdfo::rw_bucketize(a, work.data_ptr(), cur_stream());
+}
+
+void rw_pool(const Tensor& Wt, const Tensor& recv, const Tensor& meta, int64_t nrw, int64_t W,
+             int64_t B, int64_t cap, bool mean, const Tensor& starts, const Tensor& out,
+             int64_t out_ld) {
+  check_dev(Wt, "W");
+  TORCH_CHECK(Wt.scalar_type() == at::kFloat && Wt.is_contiguous() && Wt.dim() == 2, "W fp32 2-D");
+  TORCH_CHECK(Wt.size(0) <= (1LL << 32), "rw: owner rows must fit 32-bit row keys");
+  const int64_t D = Wt.size(1);
+  TORCH_CHECK(D == 16 || D == 32 || D == 64 || D == 128 || D == 256, "rw_pool: D unsupported");
+  check_i64(recv, "recv"); rw_meta_check(meta, nrw);
+  TORCH_CHECK(recv.numel() == W * (cap + 1), "rw recv buffer must be [W][cap+1]");
+  check_dev(starts, "starts");
+  TORCH_CHECK(starts.scalar_type() == at::kInt && starts.numel() >= W * (nrw * B + 1), "starts int32");
+  check_dev(out, "out");
+  TORCH_CHECK(out.scalar_type() == at::kBFloat16 || out.scalar_type() == at::kFloat,
+              "rw_pool out must be bf16 or fp32");
+  TORCH_CHECK(out_ld >= nrw * D && out_ld % 4 == 0 && out.numel() >= W * B * out_ld, "rw_pool out size");
+  tdfo::RwPoolArgs a{};
+  a.Wt = Wt.data_ptr<float>(); a.D = (int)D; a.recv = recv.data_ptr<int64_t>();
+  a.meta = meta.data_ptr<int64_t>(); a.nrw = (int)nrw; a.W = (int)W; a.B = (int)B; a.cap = cap;
+  a.mean = mean; a.starts = starts.data_ptr<int32_t>(); a.out = out.data_ptr();
+  a.out_f32 = out.scalar_type() == at::kFloat; a.out_ld = out_ld;
+  tdfo::rw_pool(a, cur_stream());
+}
+
+tdfo::EmbBwdArgs emb_rw_args(const Tensor& W, int64_t Wsz, int64_t B, int64_t cap, bool mean,
+                             int64_t key_bits) {
+  check_dev(W, "W");
+  TORCH_CHECK(W.scalar_type() == at::kFloat && W.is_contiguous() && W.dim() == 2, "W fp32 2-D");
+  const int64_t D = W.size(1);
+  TORCH_CHECK(D == 16 || D == 32 || D == 64 || D == 128 || D == 256 || D == 512, "embedding D unsupported");
+  TORCH_CHECK(key_bits >= 1 && key_bits <= 64, "key_bits");
+  const int64_t nnz = Wsz * cap;
+  TORCH_CHECK(nnz < (1LL << 31), "rw: W*cap too large");
+  tdfo::EmbBwdArgs a{};
+  a.W = W.data_ptr<float>(); a.D = (int)D; a.T = 1; a.B = (int)B; a.mean = mean; a.nnz = nnz;
+  a.key_bits = (int)key_bits;
+  return a;
+}
+
+void embedding_bwd_prepare_rw(const Tensor& W, const Tensor& recv, const Tensor& meta, int64_t nrw,
+                              int64_t Wsz, int64_t B, int64_t cap, bool mean, int64_t key_bits,
+                              int64_t grad_ld, int64_t dummy_row, const Tensor& work) {
+  auto a = emb_rw_args(W, Wsz, B, cap, mean, key_bits);
+  check_i64(recv, "recv"); rw_meta_check(meta, nrw);
+  TORCH_CHECK(recv.numel() == Wsz * (cap + 1), "rw recv buffer must be [W][cap+1]");
+  TORCH_CHECK(dummy_row >= 0 && dummy_row < W.size(0), "rw scratch row out of range");
+  set_emb_ws(a, work);
+  tdfo::embedding_bwd_prepare_rw(a, recv.data_ptr<int64_t>(), meta.data_ptr<int64_t>(), (int)nrw,
+                                 (int)Wsz, cap, grad_ld, dummy_row, cur_stream());
+}
+
+void embedding_bwd_apply_rw(const Tensor& W, int64_t Wsz, int64_t B, int64_t cap, bool mean,
+                            int64_t key_bits, const Tensor& grad, int64_t opt,
+                            const c10::optional<Tensor>& state1, const c10::optional<Tensor>& state2,
+                            const Tensor& hyper, double eps, double beta1, double beta2,
+                            double weight_decay, const Tensor& work) {
+  auto a = emb_rw_args(W, Wsz, B, cap, mean, key_bits);
+  emb_bwd_opt_args(a, W, grad, opt, state1, state2, hyper, eps, beta1, beta2, weight_decay,
+                   c10::nullopt);
+  set_emb_ws(a, work);
+  tdfo::embedding_bwd_apply(a, cur_stream());
+}
+
 // --------------------------------------------------------------- optim
 void dense_optimizer(const Tensor& p, const Tensor& g, const c10::optional<Tensor>& m,
                      const c10::optional<Tensor>& v, const c10::optional<Tensor>& p_bf16,
@@ -876,6 +968,16 @@ TORCH_LIBRARY(tdfo, m) {
         "int grad_stride, int opt, Tensor(b!)? state1, Tensor(c!)? state2, Tensor hyper, "
         "float eps, float beta1, float beta2, float weight_decay, Tensor(d!)? dense_grad, "
         "int segsort, Tensor(e!) workspace) -> ()");
+  m.def("rw_bucketize_workspace(int n, int W) -> int", rw_bucketize_workspace);
+  m.def("rw_bucketize(Tensor ids, Tensor meta, int nrw, int W, int B, int cap, int n, "
+        "Tensor(a!) send, Tensor(b!) workspace, Tensor(c!) overflow) -> ()");
+  m.def("rw_pool(Tensor Wt, Tensor recv, Tensor meta, int nrw, int W, int B, int cap, bool mean, "
+        "Tensor(a!) starts, Tensor(b!) out, int out_ld) -> ()");
+  m.def("embedding_bwd_prepare_rw(Tensor W, Tensor recv, Tensor meta, int nrw, int Wsz, int B, "
+        "int cap, bool mean, int key_bits, int grad_ld, int dummy_row, Tensor(a!) workspace) -> ()");
+  m.def("embedding_bwd_apply_rw(Tensor(a!) W, int Wsz, int B, int cap, bool mean, int key_bits, "
+        "Tensor grad, int opt, Tensor(b!)? state1, Tensor(c!)? state2, Tensor hyper, float eps, "
+        "float beta1, float beta2, float weight_decay, Tensor(d!) workspace) -> ()");
   m.def("dense_optimizer(Tensor(a!) p, Tensor g, Tensor(b!)? m, Tensor(c!)? v, Tensor(d!)? p_bf16, int opt, "
         "Tensor hyper, float beta1, float beta2, float eps, float wd, float momentum, Tensor? found_inf, "
         "Tensor[] seg_slabs, int[] seg_start, int[] seg_splits) -> ()");
@@ -919,6 +1021,10 @@ TORCH_LIBRARY_IMPL(tdfo, CUDA, m) {
   m.impl("embedding_bwd", embedding_bwd);
   m.impl("embedding_bwd_prepare", embedding_bwd_prepare);
   m.impl("embedding_bwd_apply", embedding_bwd_apply);
+  m.impl("rw_bucketize", rw_bucketize);
+  m.impl("rw_pool", rw_pool);
+  m.impl("embedding_bwd_prepare_rw", embedding_bwd_prepare_rw);
+  m.impl("embedding_bwd_apply_rw", embedding_bwd_apply_rw);
   m.impl("dense_optimizer", dense_optimizer);
   m.impl("check_finite", check_finite);
   m.impl("sort_pairs", sort_pairs);

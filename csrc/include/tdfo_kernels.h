@@ -142,6 +142,38 @@ void embedding_bwd_fused(const EmbBwdArgs& a, hipStream_t s);
 void embedding_bwd_prepare(const EmbBwdArgs& a, hipStream_t s);
 void embedding_bwd_apply(const EmbBwdArgs& a, hipStream_t s);
 
+// --------------------------------------------------- row-wise shards ----
+// (rowwise.hip) Fixed-capacity row-wise exchange. meta (int64, device):
+// [in_base (nrw) | L (nrw) | blk (nrw) | lrow (nrw) | cum (nrw + 1)]:
+// table j's ids start at ids[in_base[j]], L[j] ids per bag, owner(id) =
+// min(id / blk[j], W - 1), owner-local row key = lrow[j] + id - owner*blk[j],
+// cum = prefix of B*L[j]. Buffers are [W][cap + 1] int64; entry =
+// (j*B + b) << 32 | row key; slot cap of segment o holds its count.
+struct RwBucketArgs {
+  const int64_t* ids; const int64_t* meta;
+  int nrw, W, B; int64_t cap; int64_t n;      // n = cum[nrw] rw ids
+  int64_t* send; int32_t* overflow;
+};
+size_t rw_bucketize_workspace(int64_t n, int W);
+void rw_bucketize(const RwBucketArgs& a, void* ws, hipStream_t s);
+// Owner side: out (bf16, or fp32 if out_f32; row (r*B + b), column j*D, row
+// stride out_ld) = pooled owned rows of requester r's bag (j, b); starts:
+// [W][nrw*B + 1] int32.
+struct RwPoolArgs {
+  const float* Wt; int D; const int64_t* recv; const int64_t* meta;
+  int nrw, W, B; int64_t cap; int mean;
+  int32_t* starts; void* out; int out_f32; int64_t out_ld;
+};
+void rw_pool(const RwPoolArgs& a, hipStream_t s);
+// Backward, owner side: keys/positions/gradient offsets of every received
+// entry into the embedding workspace (entry (r, i) reads its gradient row at
+// grad + (r*B + b)*grad_ld + j*D; empty slots update row `dummy_row`, a
+// scratch row the store keeps past its real rows), then the radix sort.
+// embedding_bwd_apply then runs with a.nnz = W*cap, a.segsort = 0.
+void embedding_bwd_prepare_rw(const EmbBwdArgs& a, const int64_t* recv, const int64_t* meta,
+                              int nrw, int W, int64_t cap, int64_t grad_ld, int64_t dummy_row,
+                              hipStream_t s);
+
 // ------------------------------------------------------------ optim ----
 // Flat fused optimizer over one contiguous fp32 parameter buffer.
 enum DenseOpt { OPT_ADAMW = 0, OPT_ADAM = 1, OPT_SGD = 2, OPT_ADAGRAD = 3 };

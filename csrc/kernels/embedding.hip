@@ -644,6 +644,45 @@ __global__ __launch_bounds__(256) void emb_combine_kernel(
   }
 }
 
+// Row-wise owner backward: entry (r, i) of the received [W][cap+1] exchange
+// buffer (rowwise.hip) -> key = owner-local row, val = position, gradient
+// row offset in the all-gathered [W][B][grad_ld] pooled gradients. Slots past
+// a segment's count point at the store's scratch row (their gradient row is
+// row 0: harmless, the scratch row is never read by a forward).
+template <typename K>
+__global__ void emb_rw_keys_kernel(const EmbBwdArgs a, const int64_t* __restrict__ recv,
+                                   const int64_t* __restrict__ meta, int nrw, int W,
+                                   int64_t cap, int64_t grad_ld, int64_t dummy_row,
+                                   K* __restrict__ keys, int32_t* __restrict__ vals,
+                                   int64_t* __restrict__ goff, float* __restrict__ gscale,
+                                   int32_t* __restrict__ tail_count) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) *tail_count = 0;
+  const int64_t* L = meta + nrw;
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < a.nnz;
+       p += (int64_t)gridDim.x * blockDim.x) {
+    const int r = (int)(p / cap);
+    const int64_t i = p - (int64_t)r * cap;
+    const int64_t* seg = recv + (int64_t)r * (cap + 1);
+    const int64_t cnt = seg[cap];
+    K key = (K)dummy_row;
+    int64_t go = 0;
+    float sc = 1.f;
+    if (i < cnt) {
+      const uint64_t v = (uint64_t)seg[i];
+      const int64_t bk = (int64_t)(v >> 32);
+      const int j = (int)(bk / a.B);
+      const int64_t b = bk - (int64_t)j * a.B;
+      key = (K)(v & 0xffffffffull);
+      go = ((int64_t)r * a.B + b) * grad_ld + (int64_t)j * a.D;
+      if (a.mean) sc = 1.f / (float)L[j];
+    }
+    keys[p] = key;
+    vals[p] = (int32_t)p;
+    goff[p] = go;
+    if (gscale) gscale[p] = sc;
+  }
+}
+
 int g_emb_segsort = 1;   // one-hot batches: per-table LDS sort (0: device-wide radix sort)
 
 struct WsLayout {
@@ -674,10 +713,12 @@ WsLayout ws_layout(int64_t nnz, int D) {
   return L;
 }
 
-// prepare's choice of path (apply must read the layout prepare wrote)
+// prepare's choice of path (apply must read the layout prepare wrote): a pure
+// function of the call's arguments -- the caller resolves the global A/B
+// toggle into a.segsort once and passes the same value to both halves
 bool onehot_path(const EmbBwdArgs& a) {
   const int R = a.segsort;
-  return g_emb_segsort && R > 0 && a.T % R == 0 && a.nnz == (int64_t)a.T * a.B &&
+  return R > 0 && a.T % R == 0 && a.nnz == (int64_t)a.T * a.B &&
          a.B <= SEG_MAX && !a.mean;
 }
 
@@ -821,6 +862,46 @@ void embedding_bwd_prepare(const EmbBwdArgs& a, hipStream_t s) {
   const WsLayout L = ws_layout(a.nnz, a.D);
   if (a.key_bits <= 32) prep_impl<uint32_t>(a, L, s);
   else prep_impl<uint64_t>(a, L, s);
+}
+
+template <typename K>
+void prep_rw_impl(const EmbBwdArgs& a, const WsLayout& L, const int64_t* recv,
+                  const int64_t* meta, int nrw, int W, int64_t cap, int64_t grad_ld,
+                  int64_t dummy_row, hipStream_t s) {
+  char* ws = (char*)a.workspace;
+  K* keys_in = (K*)(ws + L.keys_in);
+  K* keys_out = (K*)(ws + L.keys_out);
+  int32_t* vals_in = (int32_t*)(ws + L.vals_in);
+  int32_t* vals_out = (int32_t*)(ws + L.vals_out);
+  int64_t* goff = (int64_t*)(ws + L.goff);
+  float* gscale = a.mean ? (float*)(ws + L.gscale) : nullptr;
+  int32_t* tcount = (int32_t*)(ws + L.tcount);
+  const bool odd = radix_sort_passes(a.key_bits) & 1;
+  K* k0 = odd ? keys_in : keys_out;
+  K* k1 = odd ? keys_out : keys_in;
+  int32_t* v0 = odd ? vals_in : vals_out;
+  int32_t* v1 = odd ? vals_out : vals_in;
+  int64_t kb = (a.nnz + 255) / 256;
+  if (kb > 8192) kb = 8192;
+  hipLaunchKernelGGL(emb_rw_keys_kernel<K>, dim3(kb), dim3(256), 0, s, a, recv, meta, nrw, W,
+                     cap, grad_ld, dummy_row, k0, v0, goff, gscale, tcount);
+  TDFO_CHECK_HIP(hipGetLastError());
+  if constexpr (sizeof(K) == 4)
+    radix_sort_pairs_u32(k0, v0, k1, v1, a.nnz, a.key_bits, ws + L.sortws, s);
+  else
+    radix_sort_pairs_u64(k0, v0, k1, v1, a.nnz, a.key_bits, ws + L.sortws, s);
+  TDFO_CHECK_HIP(hipGetLastError());
+}
+
+void embedding_bwd_prepare_rw(const EmbBwdArgs& a, const int64_t* recv, const int64_t* meta,
+                              int nrw, int W, int64_t cap, int64_t grad_ld, int64_t dummy_row,
+                              hipStream_t s) {
+  if (a.nnz <= 0) return;
+  const WsLayout L = ws_layout(a.nnz, a.D);
+  if (a.key_bits <= 32)
+    prep_rw_impl<uint32_t>(a, L, recv, meta, nrw, W, cap, grad_ld, dummy_row, s);
+  else
+    prep_rw_impl<uint64_t>(a, L, recv, meta, nrw, W, cap, grad_ld, dummy_row, s);
 }
 
 void embedding_bwd_apply(const EmbBwdArgs& a, hipStream_t s) {

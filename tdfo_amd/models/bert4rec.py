@@ -370,8 +370,13 @@ class Bert4Rec(nn.Module):
 def recall_ndcg_sums(scores: torch.Tensor) -> torch.Tensor:
     """scores [B, 1 + negs], positive in column 0 (torchrec/train.py:52-78).
     Returns per-metric SUMS over the batch in the order
-    [Recall@10, Recall@20, Recall@50, NDCG@10, NDCG@20, NDCG@50]."""
-    rank = (scores[:, 1:] > scores[:, :1]).sum(1)                     # 0-based rank of the positive
+    [Recall@10, Recall@20, Recall@50, NDCG@10, NDCG@20, NDCG@50].
+
+    Tie rule: a negative scoring EQUAL to the positive ranks ahead of it
+    (pessimistic), so ties never inflate Recall/NDCG. The reference sorts
+    with torch.sort(-scores), whose order among ties is unspecified; no
+    reference fixture pins it (parity unpinned)."""
+    rank = (scores[:, 1:] >= scores[:, :1]).sum(1)                    # 0-based rank of the positive
     rec = [(rank < k).float().sum() for k in METRICS_K]
     ndcg = [torch.where(rank < k, 1.0 / torch.log2(rank.float() + 2.0),
                         torch.zeros_like(rank, dtype=torch.float32)).sum() for k in METRICS_K]

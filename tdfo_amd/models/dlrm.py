@@ -45,6 +45,12 @@ CRITEO_1TB_ROWS = [39884406, 39043, 17289, 7420, 20263, 3, 7120, 1543, 63, 38532
 CRITEO_KAGGLE_ROWS = [1460, 583, 10131227, 2202608, 305, 24, 12517, 633, 3, 93145, 5683, 8351593,
                       3194, 27, 14992, 5461306, 10, 5652, 2173, 4, 7046547, 18, 15, 286181, 105,
                       142572]
+# BASELINE config 5: a >1 TB table set for DCN-v2 row-wise sharding -- the
+# MLPerf Criteo-TB cardinalities with every table above 1M rows grown 12x
+# (an un-capped id space): 2.24 G rows, 1.16 TB of fp32 rows + row-wise
+# Adagrad state at D=128. Five tables exceed one GPU's 245 GB budget, so
+# the planner shards them row-wise; it fits 8 x 288 GB and not 4.
+DCN_GT1TB_ROWS = [r * 12 if r > 1_000_000 else r for r in CRITEO_1TB_ROWS]
 # MLPerf DLRM-DCNv2 synthetic multi-hot pooling factors.
 MLPERF_MULTIHOT = [3, 2, 1, 2, 6, 1, 1, 1, 1, 7, 3, 8, 1, 6, 9, 5, 1, 1, 1, 12, 100, 27, 10, 3, 1,
                    1]
@@ -75,6 +81,8 @@ class DLRMConfig:
     emb_lr: float = 0.01
     emb_eps: float = 1e-8
     sharding: str = "auto"                         # planner strategy
+    rw_capacity: float = 1.25                      # row-wise segment capacity (x n/W, +256)
+    rw_comm: str = "bf16"                          # row-wise reduce-scatter dtype (bf16 | fp32)
     overlap: object = False                        # side streams (GPU): False | True (wgrads +
     #   embedding work) | "wgrad" (weight grads only)
     #   (measured 0.744 vs 0.728 ms/step on DLRM-1TB: the overlapped kernels
@@ -108,6 +116,56 @@ class DLRMConfig:
         tdims = [tin] + self.top
         f += sum(2 * a * b for a, b in zip(tdims[:-1], tdims[1:]))
         return 3.0 * f
+
+    def dense_params(self) -> int:
+        F, D = self.num_tables + 1, self.embedding_dim
+        dims = [self.num_dense] + self.bottom
+        n = sum((a + 1) * b for a, b in zip(dims[:-1], dims[1:]))
+        tin = D + F * (F - 1) // 2 if self.interaction == "dot" else F * D
+        tdims = [tin] + self.top
+        n += sum((a + 1) * b for a, b in zip(tdims[:-1], tdims[1:]))
+        if self.interaction == "dcn":
+            n += self.dcn_layers * (2 * F * D * self.dcn_rank + F * D)
+        return n
+
+    def sol(self, batch: int, world: int = 1, mfma_flops: float = 1.5e15,
+            hbm_bw: float = 6.3e12, link_bw: float = 153e9) -> dict:
+        """Analytic speed-of-light of one training step per rank (weak scaling,
+        ideal table balance), from measured-achievable MI355X rates
+        (MI355X_MICROARCH.md: HBM 6.3 TB/s float4 copy; bf16 MFMA GEMMs
+        ~1.5 PF under DVFS; xGMI 153 GB/s per link, 7 links).
+
+        compute = dense FLOPs / mfma_flops + HBM bytes / hbm_bw, where the HBM
+        bytes are the irreducible ones: fp32 rows gathered (fwd) and
+        read+written (bwd update, + 8 B of row-wise optimizer state), bf16
+        pooled rows written/read, the interaction input/outputs, and the
+        fused AdamW pass (p, g, m, v read; p, m, v, bf16 shadow written).
+        comm (W > 1) = the pooled-embedding all-to-all bytes per peer (both
+        directions) over one xGMI link + the ring all-reduce of the dense
+        grads; it can overlap compute, so sol = max(compute, comm)."""
+        B, T, D = batch, self.num_tables, self.embedding_dim
+        F = T + 1
+        L = self.pooling_factors()
+        nnz = B * sum(L)
+        emb = nnz * D * 4 + B * T * D * 2                    # fwd gather + pooled out
+        emb += nnz * D * 2 + nnz * (D * 8 + 8) + nnz * 16    # bwd grads, row rw + state, ids/keys
+        if self.interaction == "dot":
+            inter = 2 * (B * F * D * 2) + 2 * B * (D + F * (F - 1) // 2) * 2
+        else:
+            inter = 4 * B * F * D * 2 * self.dcn_layers
+        P = self.dense_params()
+        opt = P * 4 * 4 + P * (4 * 3 + 2)
+        flops = self.dense_flops_per_example() * B
+        t_dense = flops / mfma_flops
+        t_hbm = (emb + inter + opt) / hbm_bw
+        compute = t_dense + t_hbm
+        comm = 0.0
+        if world > 1:
+            per_peer = B * T * D * 2 / world                  # pooled rows to one peer, one way
+            comm = 2 * per_peer / link_bw + 2 * (world - 1) / world * P * 4 / (7 * link_bw)
+        return {"sol_ms": max(compute, comm) * 1e3, "dense_ms": t_dense * 1e3,
+                "hbm_ms": t_hbm * 1e3, "comm_ms": comm * 1e3, "dense_gflop": flops / 1e9,
+                "hbm_mb": (emb + inter + opt) / 1e6}
 
 
 @dataclass
@@ -171,7 +229,8 @@ class DLRMTrainer:
         self.plan = plan or plan_sharding(tables, world_size, optim, batch_per_rank=B,
                                           pooling=cfg.pooling_factors(), strategy=cfg.sharding)
         self.emb = ShardedEmbeddingBags(tables, self.plan, rank, B, cfg.pooling_factors(), dev,
-                                        optim, group=group, seed=cfg.seed)
+                                        optim, group=group, seed=cfg.seed,
+                                        rw_capacity=cfg.rw_capacity, rw_comm=cfg.rw_comm)
         # ------------------------------------------------------ dense params
         fp = FlatParams()
         dims = [cfg.num_dense] + cfg.bottom
@@ -227,6 +286,7 @@ class DLRMTrainer:
         self.dz = z(B, self.top_layers[0].in_k)
         self.label = z(B, dt=torch.float32)
         self.ids = torch.zeros(self.emb.nnz_local, dtype=torch.int64, device=dev)
+        self.emb.bind_ids(self.ids)
         if cfg.interaction == "dcn":
             Lc, Wd, r = cfg.dcn_layers, self.top_real, cfg.dcn_rank
             # x_0 .. x_{L-1} plain; x_L is top0's (augmented) input buffer
@@ -391,8 +451,8 @@ class DLRMTrainer:
             lookup = ("c", self._s_emb_lookup_side)
         else:
             lookup = ("c", emb.stage_fwd_lookup)
-        return [
-            ("c", lambda: emb.stage_fwd_prep(self.ids)),
+        prep = [] if emb.fwd_prep_noop else [("c", lambda: emb.stage_fwd_prep(self.ids))]
+        return prep + [
             ("m", emb.stage_fwd_ids_exchange),
             lookup,
             ("m", emb.stage_fwd_out_exchange),
@@ -422,8 +482,6 @@ class DLRMTrainer:
     def _m_fwd_wait(self):
         self._join(self._ls)
         self.emb.forward_wait()
-        if self.emb.rw_tables:
-            self.emb._rw_forward(self.ids)
 
     def _s_emb_lookup_side(self):
         """One process: the pooled lookup (random row gathers, memory-bound)
@@ -513,8 +571,6 @@ class DLRMTrainer:
         self.emb.stage_bwd_update(self.emb_hyper)
 
     def _m_allreduce_wait(self):
-        if self.emb.rw_tables:
-            self.emb._rw_backward(self.emb.d_recv, self.emb_hyper)
         if self._ar_work is not None:
             self._ar_work.wait()
             self._ar_work = None
@@ -625,7 +681,9 @@ class DLRMTrainer:
         self.graph = seq
 
     def pop_loss(self) -> float:
-        """Mean training loss since the last call (one device->host read)."""
+        """Mean training loss since the last call (one device->host read);
+        also raises if a row-wise exchange overflowed meanwhile."""
+        self.emb.check_overflow()
         v = float(self.loss_sum.item())
         self.loss_sum.zero_()
         return v

@@ -57,8 +57,15 @@ def encoder_layer_bwd(x, ids, step, params, H, rate, seed, pad_id, eps, saved, d
 
 def embedding_segsort(v: int = -1) -> int:
     """One-hot embedding backward sort: 1 per-table LDS sort (default), 0 the
-    device-wide radix sort; v < 0 only reads it. Returns the previous one."""
+    device-wide radix sort; v < 0 only reads it. Returns the previous one.
+    Resolved into each backward's ``segsort`` argument when the backward is
+    prepared (``effective_segsort``), so toggling it between the prepare and
+    apply halves cannot change the workspace layout apply reads."""
     return int(_native().embedding_segsort(v))
+
+
+def effective_segsort(segsort: int) -> int:
+    return int(segsort) if segsort and embedding_segsort() else 0
 
 
 def linear_xent_impl(p: int = -1) -> int:
@@ -153,6 +160,7 @@ def embedding_bwd(W, row_offset, indices, offsets, grad_off, T, B, grad, grad_st
     if key_bits is None:
         key_bits = key_bits_for(W.shape[0])
     if _gpu(W):
+        segsort = effective_segsort(segsort)
         _native().embedding_bwd(W, row_offset, indices, offsets, grad_off, psw, T, B, mean,
                                 key_bits, grad, grad_stride, opt, state1, state2, hyper, eps,
                                 beta1, beta2, weight_decay, dense_grad, int(segsort))
@@ -187,6 +195,50 @@ def embedding_bwd_apply(W, row_offset, indices, offsets, grad_off, T, B, grad, g
     _native().embedding_bwd_apply(W, row_offset, indices, offsets, grad_off, psw, T, B, mean,
                                   key_bits, grad, grad_stride, opt, state1, state2, hyper, eps,
                                   beta1, beta2, weight_decay, dense_grad, int(segsort), workspace)
+
+
+def rw_bucketize_workspace(n: int, W: int) -> int:
+    return int(_native().rw_bucketize_workspace(int(n), int(W))) if native_available() else 1
+
+
+def rw_bucketize(ids, meta, nrw, W, B, cap, n, send, workspace, overflow):
+    """Row-wise bucketize into fixed-capacity per-owner segments (see
+    csrc/include/tdfo_kernels.h, "row-wise shards")."""
+    if _gpu(ids):
+        _native().rw_bucketize(ids, meta, int(nrw), int(W), int(B), int(cap), int(n), send,
+                               workspace, overflow)
+    else:
+        ref.rw_bucketize(ids, meta, nrw, W, B, cap, n, send, overflow)
+
+
+def rw_pool(Wt, recv, meta, nrw, W, B, cap, mean, starts, out, out_ld):
+    if _gpu(Wt):
+        _native().rw_pool(Wt, recv, meta, int(nrw), int(W), int(B), int(cap), bool(mean), starts,
+                          out, int(out_ld))
+    else:
+        ref.rw_pool(Wt, recv, meta, nrw, W, B, cap, mean, out, out_ld)
+
+
+def embedding_bwd_prepare_rw(Wt, recv, meta, nrw, W, B, cap, mean, key_bits, grad_ld, dummy_row,
+                             workspace):
+    """GPU: keys + sort of the received row-wise entries (ids only). CPU: no-op
+    (``embedding_bwd_apply_rw`` does everything)."""
+    if _gpu(Wt):
+        _native().embedding_bwd_prepare_rw(Wt, recv, meta, int(nrw), int(W), int(B), int(cap),
+                                           bool(mean), int(key_bits), int(grad_ld),
+                                           int(dummy_row), workspace)
+
+
+def embedding_bwd_apply_rw(Wt, recv, meta, nrw, W, B, cap, mean, key_bits, grad, grad_ld, opt,
+                           hyper, workspace, state1=None, state2=None, eps=1e-8, beta1=0.9,
+                           beta2=0.999, weight_decay=0.0):
+    if _gpu(Wt):
+        _native().embedding_bwd_apply_rw(Wt, int(W), int(B), int(cap), bool(mean), int(key_bits),
+                                         grad, int(opt), state1, state2, hyper, eps, beta1, beta2,
+                                         weight_decay, workspace)
+    else:
+        ref.rw_embedding_bwd(Wt, recv, meta, nrw, W, B, cap, mean, grad, grad_ld, opt, state1,
+                             state2, hyper, eps, beta1, beta2, weight_decay)
 
 
 def dense_optimizer(p, g, m, v, p_bf16, opt, hyper, beta1=0.9, beta2=0.999, eps=1e-8, wd=0.0,
@@ -265,8 +317,15 @@ def cast_bf16(x, y):
 
 def batch_load(dense, x0, ids, ids_dst, label, label_dst):
     """x0[:, :nd] = bf16(dense), ids_dst = ids, label_dst = label (one launch on GPU)."""
-    if _gpu(x0) and dense.is_cuda and ids.is_cuda and label.is_cuda and \
-            dense.dtype == torch.float32 and dense.stride(-1) == 1:
+    # the fused kernel needs fp32 row-major dense, int64 ids at a 16-B aligned
+    # address, fp32 labels and exactly matching sizes; anything else copies
+    if (_gpu(x0) and dense.is_cuda and ids.is_cuda and label.is_cuda
+            and dense.dtype == torch.float32 and dense.dim() == 2 and dense.stride(-1) == 1
+            and dense.shape[0] == x0.shape[0] and dense.shape[1] <= x0.shape[1]
+            and ids.dtype == torch.int64 and ids.is_contiguous() and ids.data_ptr() % 16 == 0
+            and ids.numel() == ids_dst.numel() and ids_dst.dtype == torch.int64
+            and label.dtype == torch.float32 and label.numel() == label_dst.numel()
+            and label_dst.dtype == torch.float32):
         _native().batch_load(dense, x0, ids.contiguous(), ids_dst, label.contiguous(), label_dst)
     else:
         x0[:, :dense.shape[1]].copy_(dense, non_blocking=True)

@@ -175,6 +175,83 @@ def embedding_bwd(W, row_offset, indices, offsets, grad_off, psw, T, B, mean, ke
     W[rows] = w
 
 
+def rw_unpack_meta(meta, nrw):
+    m = meta.to(torch.int64)
+    return m[:nrw], m[nrw:2 * nrw], m[2 * nrw:3 * nrw], m[3 * nrw:4 * nrw], m[4 * nrw:5 * nrw + 1]
+
+
+def rw_bucketize(ids, meta, nrw, W, B, cap, n, send, overflow):
+    """Reference of the row-wise bucketize (rowwise.hip): stable per-owner
+    segments of packed (bag key << 32 | owner-local row) entries, the count in
+    slot ``cap`` of each [cap + 1] segment, overflow flagged (sticky)."""
+    dev = ids.device
+    in_base, L, blk, lrow, cum = rw_unpack_meta(meta, nrw)
+    q = torch.arange(n, device=dev)
+    j = torch.searchsorted(cum[1:], q, right=True)
+    off = q - cum[j]
+    b = off // L[j]
+    gid = ids[in_base[j] + off]
+    owner = torch.clamp(gid // blk[j], max=W - 1)
+    row = lrow[j] + gid - owner * blk[j]
+    packed = ((j * B + b) << 32) | row
+    seg = send.view(W, cap + 1)
+    for o in range(W):
+        sel = packed[owner == o]
+        c = int(sel.numel())
+        if c > cap:
+            overflow.view(-1)[0] = 1
+            c = cap
+        seg[o, :c] = sel[:c]
+        seg[o, cap] = c
+
+
+def _rw_entries(recv, meta, nrw, W, B, cap):
+    """(requester, bag key, row key) of every valid received entry."""
+    seg = recv.view(W, cap + 1)
+    rs, keys, rows = [], [], []
+    for r in range(W):
+        c = int(seg[r, cap])
+        v = seg[r, :c]
+        rs.append(torch.full((c,), r, dtype=torch.int64, device=recv.device))
+        keys.append(v >> 32)
+        rows.append(v & 0xFFFFFFFF)
+    return torch.cat(rs), torch.cat(keys), torch.cat(rows)
+
+
+def rw_pool(Wt, recv, meta, nrw, W, B, cap, mean, out, out_ld):
+    D = Wt.shape[1]
+    _, L, _, _, _ = rw_unpack_meta(meta, nrw)
+    r, k, row = _rw_entries(recv, meta, nrw, W, B, cap)
+    j, b = k // B, k % B
+    acc = torch.zeros(W * B * nrw, D, device=Wt.device)
+    vals = Wt[row].float()
+    if mean:
+        vals = vals / L[j].float()[:, None]
+    acc.index_add_(0, (r * B + b) * nrw + j, vals)
+    o = out.view(-1)[: W * B * out_ld].view(W * B, out_ld)
+    o[:, : nrw * D] = acc.view(W * B, nrw * D).to(out.dtype)
+
+
+def rw_embedding_bwd(Wt, recv, meta, nrw, W, B, cap, mean, grad, grad_ld, opt, state1, state2,
+                     hyper, eps, beta1, beta2, weight_decay):
+    """Owner-side fused backward of the row-wise exchange: every received
+    entry (r, (j, b), row) takes gradient row grad[(r*B + b)*grad_ld + j*D:]."""
+    D = Wt.shape[1]
+    _, L, _, _, _ = rw_unpack_meta(meta, nrw)
+    r, k, row = _rw_entries(recv, meta, nrw, W, B, cap)
+    n = int(row.numel())
+    if n == 0:
+        return
+    j, b = k // B, k % B
+    base = (r * B + b) * grad_ld + j * D
+    g = grad.reshape(-1)[(base[:, None] + torch.arange(D, device=Wt.device)).reshape(-1)]
+    g = g.float().view(n, D).contiguous()
+    psw = (1.0 / L[j].float()) if mean else None
+    z = torch.zeros(1, dtype=torch.int64, device=Wt.device)
+    embedding_bwd(Wt, z, row, torch.arange(n + 1, device=Wt.device), z, psw, 1, n, False, 64,
+                  g, D, opt, state1, state2, hyper, eps, beta1, beta2, weight_decay, None)
+
+
 def dense_optimizer(p, g, m, v, p_bf16, opt, hyper, beta1, beta2, eps, wd, momentum, found_inf):
     if found_inf is not None and float(found_inf.reshape(-1)[0]) > 0:
         return

@@ -7,15 +7,24 @@ table) and of TF's MinSizePartitioner for the parameter-server path
 
 * memory per shard = rows x D x 4 B (fp32 weights) + optimizer state
   (rowwise-Adagrad 1 float/row, Adagrad D, Adam 2D floats/row);
-* compute per shard ~ HBM bytes gathered + updated per step
-  (global batch x pooling factor x D x 4 B x ~3);
-* communication per table-wise shard = pooled bf16 rows all-to-all'd
-  (global batch x D x 2 B each way) over 7 point-to-point xGMI links.
+* cost per shard, in microseconds per step on MI355X:
+  - lookup + fused update: ids x ID_NS (measured: a rank's embedding time
+    tracks its id count, ~1.4 ns per id fwd+bwd at D=128 --
+    profiles/emb_rank_w8.jsonl) scaled by D/128;
+  - xGMI: every peer link carries its share of the shard's exchange, both
+    directions (fwd values, bwd gradients), at LINK_GBS:
+      table-wise  the owner sends each peer that peer's B pooled rows (bf16)
+      row-wise    every rank reduce-scatters [W][B][D] bf16 partials and
+                  all-gathers the [B][D] gradients: B rows per link per
+                  direction, on every rank (W x the table-wise bytes)
+    The per-link terms assume all W-1 links run in parallel (a fully
+    connected xGMI node), i.e. the all-to-all is per-link bound.
 
 Sharding kinds:
   table_wise   whole table on one rank (pooled-embedding all-to-all)
   row_wise     rows split in contiguous blocks across all ranks (id
-               bucketize + all-to-all of ids and looked-up rows)
+               bucketize + all-to-all of ids, owner-side pooling, bf16
+               reduce-scatter of the pooled partials)
   column_wise  D split across ranks; each column block is a table-wise shard
   data_parallel  replicated (tiny tables; gradient all-reduce)
 """
@@ -28,6 +37,8 @@ from .tables import EmbOptimConfig, TableConfig
 
 HBM_BYTES = 288 * 10**9
 GiB = 1 << 30
+ID_NS = 1.4            # ns per looked-up id, fwd + fused bwd, D = 128 (measured)
+LINK_GBS = 153.0       # xGMI GB/s per direction per point-to-point link
 
 
 @dataclass
@@ -94,11 +105,21 @@ def plan_sharding(tables: Sequence[TableConfig], world_size: int, optim: EmbOpti
     shards: List[Optional[TableShard]] = [None] * T
 
     rc = row_cost or (lambda rows: 1.0)
+    B = batch_per_rank
+
+    def link_us(rows_per_link: float, d: int) -> float:
+        return 2 * rows_per_link * d * 2 / (LINK_GBS * 1e3) if W > 1 else 0.0
 
     def tcost(t: int) -> float:
+        """table-wise cost on the owner (us/step)"""
         d = tables[t].embedding_dim
-        return (gb * pooling[t] * d * 4 * 3 / 1e9 * rc(tables[t].num_embeddings)
-                + gb * d * 2 * 2 / 1e9)
+        ids = gb * pooling[t]
+        return ids * ID_NS * 1e-3 * d / 128 * rc(tables[t].num_embeddings) + link_us(B, d)
+
+    def rcost(t: int) -> float:
+        """row-wise cost on every rank (us/step)"""
+        d = tables[t].embedding_dim
+        return gb * pooling[t] / W * ID_NS * 1e-3 * d / 128 + link_us(B, d)
 
     order = sorted(range(T), key=lambda t: (-tcost(t), -tables[t].num_embeddings, t))
 
@@ -108,8 +129,8 @@ def plan_sharding(tables: Sequence[TableConfig], world_size: int, optim: EmbOpti
         blocks = [max(0, min(blk, rows - r * blk)) for r in range(W)]
         per_row = _mem_per_row(tables[t].embedding_dim, optim)
         for r in range(W):
-            mem[r] += blocks[r] * per_row
-            cost[r] += tcost(t) / W
+            mem[r] += (blk + (1 if r == 0 else 0)) * per_row   # padded block + scratch row
+            cost[r] += rcost(t)
         return TableShard(t, "row_wise", list(range(W)), row_blocks=blocks)
 
     def column_wise(t: int):
@@ -124,7 +145,15 @@ def plan_sharding(tables: Sequence[TableConfig], world_size: int, optim: EmbOpti
             cost[r] += tcost(t) * cols[i] / d
         return TableShard(t, "column_wise", ranks, col_blocks=cols)
 
+    # tables no single GPU can hold go row-wise first: their shares land on
+    # every rank, and the table-wise placement below must see that memory
+    if strategy == "auto" and W > 1:
+        for t in order:
+            if tables[t].num_embeddings * _mem_per_row(tables[t].embedding_dim, optim) > cap:
+                shards[t] = row_wise(t)
     for t in order:
+        if shards[t] is not None:
+            continue
         tb = tables[t].num_embeddings * _mem_per_row(tables[t].embedding_dim, optim)
         if strategy == "data_parallel" or (strategy == "auto" and tb <= dp_max_bytes):
             for r in range(W):

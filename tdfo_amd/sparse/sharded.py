@@ -46,6 +46,23 @@ def _a2a(out, inp, out_splits, in_splits, group, async_op=False):
                                   input_split_sizes=in_splits, group=group, async_op=async_op)
 
 
+class _Done:
+    def wait(self):
+        return None
+
+
+def _reduce_scatter(out, inp, group, async_op=False):
+    """reduce_scatter_tensor; over gloo with device tensors (the shared-GPU
+    rehearsal backend) it is emulated by an all-to-all + an in-order sum."""
+    if inp.is_cuda and dist.get_backend(group) == "gloo":
+        W = dist.get_world_size(group)
+        tmp = torch.empty_like(inp)
+        dist.all_to_all_single(tmp, inp, group=group)
+        out.copy_(tmp.view(W, -1).float().sum(0))
+        return _Done()
+    return dist.reduce_scatter_tensor(out, inp, group=group, async_op=async_op)
+
+
 class ShardedEmbeddingBags:
     """Pooled embedding features of one width D over a sharding plan.
 
@@ -58,7 +75,14 @@ class ShardedEmbeddingBags:
 
     def __init__(self, tables: Sequence[TableConfig], plan: ShardingPlan, rank: int,
                  batch_size: int, pooling: Sequence[int], device, optim: EmbOptimConfig,
-                 group=None, seed: int = 0, mean: bool = False):
+                 group=None, seed: int = 0, mean: bool = False, rw_capacity: float = 1.25,
+                 rw_comm: str = "bf16"):
+        """``rw_capacity``: per-owner segment capacity of the row-wise exchange
+        as a multiple of the uniform share n/W (+256); exceeding it raises
+        (``check_overflow``) instead of training on partial bags.
+        ``rw_comm``: dtype of the pooled partials' reduce-scatter ("bf16"
+        halves the bytes; "fp32" sums exactly as one process would, up to
+        fp32 association)."""
         self.tables = list(tables)
         self.T = len(self.tables)
         dims = {t.embedding_dim for t in self.tables}
@@ -182,41 +206,63 @@ class ShardedEmbeddingBags:
             self.cw_v_offsets = co.to(self.device)
             self.cw_v_row_off = torch.tensor(ro, dtype=torch.int64, device=self.device)
             self.cw_v_out_off = torch.tensor(oo, dtype=torch.int64, device=self.device)
-        # ---- row-wise group (dynamic splits)
+        # ---- row-wise group: fixed-capacity exchange (csrc/kernels/rowwise.hip).
+        # Ids are bucketed by owner block into [W][cap+1] segments, exchanged
+        # with one equal-split all-to-all, pooled per (requester, bag) at the
+        # owner and summed by a bf16 reduce-scatter; the backward all-gathers
+        # the pooled gradients and runs the fused sort-based update on the
+        # received entries. Static shapes: hipGraph-capturable, no host sync.
         self.rw_tables = [s.table for s in plan.shards if s.kind == "row_wise"]
         self.rw_col = {t: j * D for j, t in enumerate(self.rw_tables)}
         self.rw_width = len(self.rw_tables) * D
+        self.nrw = len(self.rw_tables)
         if self.rw_tables:
-            blocks = []
-            for t in self.rw_tables:
-                rows = self.tables[t].num_embeddings
-                blk = -(-rows // W)
-                blocks.append(blk)
-            self.rw_block = torch.tensor(blocks, dtype=torch.int64, device=self.device)
+            blocks = [-(-self.tables[t].num_embeddings // W) for t in self.rw_tables]
             self.rw_block_host = blocks
             # every rank allocates a full block per table (the last block is
-            # padded) so row offsets agree across ranks and requesters can
-            # send ready-made row keys
+            # padded) so owner-local row keys agree across ranks; one scratch
+            # row absorbs the padding entries of the backward
             self.rw_store = TableBatchedEmbedding(
                 blocks, D, device, optim,
                 init_ranges=[self.tables[t].init_range or (1.0 / self.tables[t].num_embeddings) ** 0.5
-                             for t in self.rw_tables], seed=seed * 1000 + 500 + rank)
-            rw_ids_idx = torch.cat([torch.arange(self.in_base[t], self.in_base[t] + B * self.L[t])
-                                    for t in self.rw_tables])
-            self.rw_in_idx = rw_ids_idx.to(self.device)
-            tab = torch.cat([torch.full((B * self.L[t],), j, dtype=torch.int64)
-                             for j, t in enumerate(self.rw_tables)])
-            self.rw_tab = tab.to(self.device)
-            bag = torch.cat([torch.arange(B).repeat_interleave(self.L[t]) + j * B
-                             for j, t in enumerate(self.rw_tables)])
-            self.rw_bag = bag.to(self.device)      # bag id (j*B + b) per rw id
-            lens = torch.tensor([self.L[t] for t in self.rw_tables], dtype=torch.int64)
-            bag_len = lens.repeat_interleave(B)
-            boffs = torch.zeros(bag_len.numel() + 1, dtype=torch.int64)
-            boffs[1:] = torch.cumsum(bag_len, 0)
-            self.rw_bag_offsets = boffs.to(self.device)
-            self.rw_out_off = torch.tensor([tw_total + j * D for j in range(len(self.rw_tables))],
-                                           dtype=torch.int64, device=self.device)
+                             for t in self.rw_tables], seed=seed * 1000 + 500 + rank,
+                scratch_rows=1)
+            if self.rw_store.total_rows + 1 >= 1 << 32:
+                raise ValueError("row-wise shard holds >= 2^32 rows on one rank (32-bit row keys)")
+            self.rw_dummy = self.rw_store.total_rows
+            Ls = [self.L[t] for t in self.rw_tables]
+            cum = [0]
+            for l_ in Ls:
+                cum.append(cum[-1] + B * l_)
+            self.rw_n = n = cum[-1]
+            meta = ([self.in_base[t] for t in self.rw_tables] + Ls + blocks
+                    + list(self.rw_store.row_offset_host) + cum)
+            self.rw_meta = torch.tensor(meta, dtype=torch.int64, device=self.device)
+            self.rw_cap = cap = self.rw_capacity(n, W, rw_capacity)
+            self.rw_send = torch.zeros(W * (cap + 1), dtype=torch.int64, device=self.device)
+            self.rw_recv = torch.zeros_like(self.rw_send) if W > 1 else self.rw_send
+            from .. import ops as _ops
+            self.rw_ws = torch.empty(_ops.rw_bucketize_workspace(n, W), dtype=torch.uint8,
+                                     device=self.device)
+            self.rw_overflow = torch.zeros(1, dtype=torch.int32, device=self.device)
+            self.rw_starts = torch.zeros(W * (self.nrw * B + 1), dtype=torch.int32,
+                                         device=self.device)
+            bf_ = torch.bfloat16
+            if rw_comm not in ("bf16", "fp32"):
+                raise ValueError(f"rw_comm must be bf16 or fp32, got {rw_comm}")
+            cdt = bf_ if rw_comm == "bf16" else torch.float32
+            self.rw_pbuf = (torch.zeros(W * B * self.rw_width, dtype=cdt, device=self.device)
+                            if W > 1 else None)
+            # fp32 partials are reduced into an fp32 landing buffer, then cast
+            self.rw_rs32 = (torch.zeros(B * self.rw_width, dtype=cdt, device=self.device)
+                            if W > 1 and cdt == torch.float32 else None)
+            self.rw_gbuf = (torch.zeros(W * B * self.rw_width, dtype=bf_, device=self.device)
+                            if W > 1 else None)
+            self.rw_bwd_ws = None
+            if self.device.type == "cuda":
+                self.rw_bwd_ws = torch.empty(_ops.embedding_bwd_workspace(W * cap, D),
+                                             dtype=torch.uint8, device=self.device)
+            self._rw_prepared = False
         # ---- data-parallel (replicated) group: local lookup, gradient
         # all-gather, identical deterministic update on every rank
         self.dp_tables = [s.table for s in plan.shards if s.kind == "data_parallel"]
@@ -292,6 +338,36 @@ class ShardedEmbeddingBags:
     def nnz_local_tw(self) -> int:
         return sum(self.tw_send_counts)
 
+    @staticmethod
+    def rw_capacity(n: int, W: int, factor: float) -> int:
+        if W == 1:
+            return max(1, n)
+        return max(1, min(n, -(-int(factor * n) // W) + 256))
+
+    def _rw_region(self, buf):
+        base = sum(self.tw_recv_sizes)
+        return buf[base: base + self.B * self.rw_width]
+
+    def check_overflow(self):
+        """Raise if any row-wise segment overflowed its capacity (host sync)."""
+        if self.rw_tables and int(self.rw_overflow.item()):
+            raise RuntimeError(
+                f"row-wise exchange capacity exceeded (cap {self.rw_cap} ids per owner, "
+                f"{self.rw_n} ids per rank): lookups were dropped; raise rw_capacity "
+                f"(skewed ids per owner block)")
+
+    @property
+    def fwd_prep_noop(self) -> bool:
+        """The forward prep stage launches nothing (one table-wise rank)."""
+        return self.tw_identity and not (self.cw_tables or self.dp_tables or self.rw_tables)
+
+    def bind_ids(self, ids: torch.Tensor):
+        """Alias the static id buffer where the table-wise exchange is the
+        identity (one rank): the lookup reads it in place."""
+        if self.tw_identity:
+            self.tw_send_ids = ids
+            self.tw_recv_ids = ids
+
     # ------------------------------------------------------------ forward
     def forward(self, ids: torch.Tensor) -> torch.Tensor:
         self.forward_start(ids)
@@ -303,13 +379,11 @@ class ShardedEmbeddingBags:
         self.stage_fwd_ids_exchange()
         self.stage_fwd_lookup()
         self.stage_fwd_out_exchange()
-        if self.rw_tables:
-            self._rw_forward(ids)
 
     @property
     def graph_capturable(self) -> bool:
-        """Static shapes only (no row-wise tables with data-dependent splits)."""
-        return not self.rw_tables
+        """Every sharding kind uses static shapes (fixed-capacity RW exchange)."""
+        return True
 
     # -- stages (compute stages are hipGraph-capturable; exchanges are RCCL)
     def _cw_views(self, buf):
@@ -339,6 +413,10 @@ class ShardedEmbeddingBags:
             torch.index_select(ids, 0, self.tw_perm, out=self.tw_send_ids)
             if self.world == 1:
                 self.tw_recv_ids = self.tw_send_ids
+        if self.rw_tables:
+            from .. import ops
+            ops.rw_bucketize(ids, self.rw_meta, self.nrw, self.world, self.B, self.rw_cap,
+                             self.rw_n, self.rw_send, self.rw_ws, self.rw_overflow)
 
     def stage_fwd_ids_exchange(self):
         W = self.world
@@ -350,6 +428,8 @@ class ShardedEmbeddingBags:
         if W > 1 and self.cw_tables:
             _a2a(self.cw_recv_ids, self.cw_send_ids, [self.cw_recv_count] * W,
                  self.cw_send_counts, self.group)
+        if W > 1 and self.rw_tables:
+            dist.all_to_all_single(self.rw_recv, self.rw_send, group=self.group)
 
     def stage_fwd_lookup(self):
         W, B = self.world, self.B
@@ -368,70 +448,36 @@ class ShardedEmbeddingBags:
             self.cw_store.forward(self.cw_recv_ids, self.cw_v_offsets, self.cw_v_row_off,
                                   self.cw_nv, B, self.tw_pooled if W > 1 else self.recv,
                                   self.cw_v_out_off, self.dsum[self.rank], mean=self.mean)
+        if self.rw_tables:
+            from .. import ops
+            out = self.rw_pbuf if W > 1 else self._rw_region(self.recv)
+            ops.rw_pool(self.rw_store.weight, self.rw_recv, self.rw_meta, self.nrw, W, B,
+                        self.rw_cap, self.mean, self.rw_starts, out, self.rw_width)
 
     def stage_fwd_out_exchange(self):
         W, B = self.world, self.B
-        work = None
+        works = []
         if W > 1:
             tw_total = sum(self.tw_recv_sizes)
-            work = _a2a(self.recv[:tw_total], self.tw_pooled[: W * B * self.dsum[self.rank]],
-                        self.tw_recv_sizes, [B * self.dsum[self.rank]] * W, self.group,
-                        async_op=True)
-        self._pending = work
+            if tw_total:
+                works.append(_a2a(self.recv[:tw_total],
+                                  self.tw_pooled[: W * B * self.dsum[self.rank]],
+                                  self.tw_recv_sizes, [B * self.dsum[self.rank]] * W, self.group,
+                                  async_op=True))
+            if self.rw_tables:
+                dst = self.rw_rs32 if self.rw_rs32 is not None else self._rw_region(self.recv)
+                works.append(_reduce_scatter(dst, self.rw_pbuf, self.group, async_op=True))
+        self._pending = works
 
     def forward_wait(self):
-        if self._pending is not None:
-            self._pending.wait()
-            self._pending = None
+        for w in self._pending or ():
+            w.wait()
+        self._pending = None
         if self.cw_tables:
             self._cw_assemble(self.recv)
-
-    # row-wise: dynamic splits
-    def _rw_forward(self, ids: torch.Tensor):
-        W, D = self.world, self.D
-        gid = ids.index_select(0, self.rw_in_idx)
-        blk = self.rw_block[self.rw_tab]
-        owner = torch.clamp(gid // blk, max=W - 1)
-        local = gid - owner * blk
-        order = torch.argsort(owner, stable=True)
-        send_counts = torch.bincount(owner, minlength=W)
-        if W > 1:
-            recv_counts = torch.empty_like(send_counts)
-            dist.all_to_all_single(recv_counts, send_counts, group=self.group)
-        else:
-            recv_counts = send_counts
-        sc = send_counts.tolist()
-        rc = recv_counts.tolist()
-        key = self.rw_store.row_offset[self.rw_tab] + local
-        send_keys = key.index_select(0, order)
-        recv_keys = torch.empty(sum(rc), dtype=torch.int64, device=self.device)
-        if W > 1:
-            _a2a(recv_keys, send_keys, rc, sc, self.group)
-        else:
-            recv_keys = send_keys
-        n_r = recv_keys.numel()
-        rows = torch.empty(max(1, n_r), D, dtype=torch.float32, device=self.device)
-        if n_r:
-            ar = torch.arange(n_r + 1, dtype=torch.int64, device=self.device)
-            self.rw_store.forward(recv_keys, ar, torch.zeros(1, dtype=torch.int64, device=self.device),
-                                  1, n_r, rows, torch.zeros(1, dtype=torch.int64, device=self.device),
-                                  D)
-        back = torch.empty(order.numel(), D, dtype=torch.float32, device=self.device)
-        if W > 1:
-            _a2a(back, rows[:n_r], sc, rc, self.group)
-        else:
-            back = rows[:n_r]
-        # back[i] is the row of rw id order[i]; pool into recv via position map
-        pos = torch.empty_like(order)
-        pos[order] = torch.arange(order.numel(), device=self.device)
-        nrw = len(self.rw_tables)
-        zeros_ro = torch.zeros(nrw, dtype=torch.int64, device=self.device)
-        from .. import ops
-        ops.embedding_bag_fwd(back.contiguous() if back.numel() else
-                              torch.zeros(1, D, device=self.device),
-                              zeros_ro, pos, self.rw_bag_offsets, self.rw_out_off, nrw, self.B,
-                              self.recv, self.rw_width, mean=self.mean)
-        self._rw_state = (order, sc, rc, recv_keys)
+        if self.rw_tables and self.rw_rs32 is not None:
+            from .. import ops
+            ops.cast_bf16(self.rw_rs32, self._rw_region(self.recv))
 
     # ----------------------------------------------------------- backward
     def backward_start(self, d_recv: Optional[torch.Tensor] = None):
@@ -452,15 +498,21 @@ class ShardedEmbeddingBags:
             self._dp_work = dist.all_gather_into_tensor(
                 self.dp_g_grad, d_recv[self.dp_base: self.dp_base + B * self.dp_width],
                 group=self.group, async_op=True)
+        self._rw_work = None
+        if W > 1 and self.rw_tables:
+            self._rw_work = dist.all_gather_into_tensor(self.rw_gbuf, self._rw_region(d_recv),
+                                                        group=self.group, async_op=True)
         self._bw = (work, d_recv)
 
     def backward_wait(self):
         work, d_recv = self._bw
         if work is not None:
             work.wait()
-        if getattr(self, "_dp_work", None) is not None:
-            self._dp_work.wait()
-            self._dp_work = None
+        for name in ("_dp_work", "_rw_work"):
+            w = getattr(self, name, None)
+            if w is not None:
+                w.wait()
+                setattr(self, name, None)
         self._bw = (None, d_recv)
 
     def stage_bwd_prepare(self):
@@ -472,6 +524,16 @@ class ShardedEmbeddingBags:
                                            self.tw_nv, self.B, self.tw_v_out_off,
                                            self.dsum[self.rank], mean=self.mean,
                                            segsort=self.tw_segsort)
+        if self.rw_tables:
+            self._rw_prepare()
+
+    def _rw_prepare(self):
+        from .. import ops
+        st = self.rw_store
+        ops.embedding_bwd_prepare_rw(st.weight, self.rw_recv, self.rw_meta, self.nrw, self.world,
+                                     self.B, self.rw_cap, self.mean, st.key_bits, self.rw_width,
+                                     self.rw_dummy, self.rw_bwd_ws)
+        self._rw_prepared = True
 
     def stage_bwd_update(self, hyper: torch.Tensor):
         """Fused sort-based backward + optimizer on this rank's table-wise shards."""
@@ -497,41 +559,23 @@ class ShardedEmbeddingBags:
                 self.dp_store.backward_update(self.dp_ids, self.dp_offsets, self.dp_store.row_offset,
                                               ndp, B, d_recv, self.dp_out_off, self.dp_width, hyper,
                                               mean=self.mean)
+        if self.rw_tables:
+            from .. import ops
+            if not self._rw_prepared:
+                self._rw_prepare()
+            st, o = self.rw_store, self.optim
+            grad = self.rw_gbuf if W > 1 else self._rw_region(d_recv)
+            ops.embedding_bwd_apply_rw(st.weight, self.rw_recv, self.rw_meta, self.nrw, W, B,
+                                       self.rw_cap, self.mean, st.key_bits, grad, self.rw_width,
+                                       o.code, hyper, self.rw_bwd_ws, state1=st.state1,
+                                       state2=st.state2, eps=o.eps, beta1=o.beta1, beta2=o.beta2,
+                                       weight_decay=o.weight_decay)
+            self._rw_prepared = False
 
     def backward_finish(self, hyper: torch.Tensor):
         self.backward_wait()
-        d_recv = self._bw[1]
         self.stage_bwd_update(hyper)
-        if self.rw_tables:
-            self._rw_backward(d_recv, hyper)
         self._bw = None
-
-    def _rw_backward(self, d_recv, hyper):
-        order, sc, rc, recv_keys = self._rw_state
-        D, W = self.D, self.world
-        tw_total = sum(self.tw_recv_sizes)
-        nrw = len(self.rw_tables)
-        # per rw id (send order): its bag's pooled gradient
-        bag = self.rw_bag.index_select(0, order)
-        j = bag // self.B
-        b = bag - j * self.B
-        base = tw_total + b * self.rw_width + j * D
-        idx = base[:, None] + torch.arange(D, device=self.device)[None, :]
-        g = d_recv.index_select(0, idx.reshape(-1)).view(-1, D)
-        if self.mean:
-            lens = torch.tensor([self.L[t] for t in self.rw_tables], device=self.device)
-            g = g / lens[j].to(g.dtype)[:, None]
-        gr = torch.empty(recv_keys.numel(), D, dtype=g.dtype, device=self.device)
-        if W > 1:
-            _a2a(gr, g.contiguous(), rc, sc, self.group)
-        else:
-            gr = g.contiguous()
-        n_r = recv_keys.numel()
-        if n_r:
-            ar = torch.arange(n_r + 1, dtype=torch.int64, device=self.device)
-            z = torch.zeros(1, dtype=torch.int64, device=self.device)
-            self.rw_store.backward_update(recv_keys, ar, z, 1, n_r, gr, z, D, hyper)
-        del nrw
 
     # -------------------------------------------------------------- state
     def table_cols(self, t: int):

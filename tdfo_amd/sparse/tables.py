@@ -93,7 +93,10 @@ class TableBatchedEmbedding:
 
     def __init__(self, row_counts: Sequence[int], dim: int, device, optim: EmbOptimConfig,
                  init_ranges: Optional[Sequence[float]] = None, seed: int = 0,
-                 dtype=torch.float32):
+                 dtype=torch.float32, scratch_rows: int = 0):
+        """``scratch_rows`` extra rows past the real ones (row ``total_rows``
+        onwards): targets for the padding entries of a fixed-capacity
+        exchange, updated with junk and never read by a lookup."""
         self.dim = int(dim)
         self.row_counts = [int(r) for r in row_counts]
         self.num_tables = len(self.row_counts)
@@ -105,7 +108,9 @@ class TableBatchedEmbedding:
         self.total_rows = offs[-1]
         self.row_offset_host = offs[:-1]
         self.row_offset = torch.tensor(offs[:-1], dtype=torch.int64, device=self.device)
-        self.weight = torch.zeros(max(1, self.total_rows), self.dim, dtype=dtype, device=self.device)
+        self.scratch_rows = int(scratch_rows)
+        nrows = max(1, self.total_rows + self.scratch_rows)
+        self.weight = torch.zeros(nrows, self.dim, dtype=dtype, device=self.device)
         gen = torch.Generator(device=self.device)
         gen.manual_seed(seed)
         for t, r in enumerate(self.row_counts):
@@ -116,14 +121,14 @@ class TableBatchedEmbedding:
         c = optim.code
         self.state1 = self.state2 = None
         if c == ops.EMB_ROWWISE_ADAGRAD:
-            self.state1 = torch.full((max(1, self.total_rows),), optim.initial_accumulator,
+            self.state1 = torch.full((nrows,), optim.initial_accumulator,
                                      dtype=torch.float32, device=self.device)
         elif c == ops.EMB_ADAGRAD:
             self.state1 = torch.full_like(self.weight, optim.initial_accumulator)
         elif c == ops.EMB_ADAM:
             self.state1 = torch.zeros_like(self.weight)
             self.state2 = torch.zeros_like(self.weight)
-        self.key_bits = ops.key_bits_for(self.total_rows)
+        self.key_bits = ops.key_bits_for(self.total_rows + self.scratch_rows)
 
     # ------------------------------------------------------------------
     def check_ids(self, indices, offsets, row_offset, T, B):
@@ -173,10 +178,12 @@ class TableBatchedEmbedding:
         need = ops.embedding_bwd_workspace(indices.numel(), self.dim)
         if getattr(self, "_bwd_ws", None) is None or self._bwd_ws.numel() < need:
             self._bwd_ws = torch.empty(need, dtype=torch.uint8, device=self.weight.device)
+        seg = ops.effective_segsort(segsort)       # fixed here for the apply half too
         ops.embedding_bwd_prepare(self.weight, row_offset, indices, offsets, grad_off, T, B,
                                   grad_stride, self._bwd_ws, key_bits=self.key_bits, mean=mean,
-                                  psw=psw, segsort=segsort)
+                                  psw=psw, segsort=seg)
         self._prepared = (indices.data_ptr(), indices.numel(), T, B)
+        self._prepared_segsort = seg
 
     def backward_apply(self, indices, offsets, row_offset, T, B, grad, grad_off, grad_stride,
                        hyper, mean=False, psw=None, dense_grad=None, segsort=0):
@@ -192,7 +199,8 @@ class TableBatchedEmbedding:
                                 grad_stride, o.code, hyper, self._bwd_ws, state1=self.state1,
                                 state2=self.state2, eps=o.eps, beta1=o.beta1, beta2=o.beta2,
                                 weight_decay=o.weight_decay, key_bits=self.key_bits, mean=mean,
-                                psw=psw, dense_grad=dense_grad, segsort=segsort)
+                                psw=psw, dense_grad=dense_grad,
+                                segsort=self._prepared_segsort)
         self._prepared = None
 
     def table_weight(self, t: int) -> torch.Tensor:

@@ -31,14 +31,18 @@ def _from_bytes(b):
     return torch.load(io.BytesIO(b), weights_only=True)
 
 
-def _worker(rank, world, port, fn, args, q):
+def _worker(rank, world, port, fn, args, q, device="cpu"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    if device == "cuda":
+        # every rank on cuda:0, gloo between them (RCCL refuses two ranks on
+        # one GPU): the multi-rank step runs on the real HIP kernels
+        os.environ.update(TDFO_SHARE_DEVICE="1", TDFO_DIST_BACKEND="gloo")
     try:
         import torch
         torch.set_num_threads(1)
         from tdfo_amd.parallel import dist as tdist
-        tdist.init_distributed("cpu", "gloo", timeout_s=120)
+        tdist.init_distributed(device, "gloo", timeout_s=120)
         out = fn(rank, world, *args)
         q.put((rank, "ok", _to_bytes(out)))
         tdist.reset()
@@ -46,11 +50,13 @@ def _worker(rank, world, port, fn, args, q):
         q.put((rank, "err", traceback.format_exc()))
 
 
-def run_distributed(fn, world, *args, timeout=300):
+def run_distributed(fn, world, *args, timeout=300, device="cpu"):
+    """``device="cuda"``: ranks share cuda:0 over gloo (fresh spawned processes)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, fn, args, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, fn, args, q, device))
+             for r in range(world)]
     for p in procs:
         p.start()
     import queue

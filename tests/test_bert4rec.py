@@ -108,6 +108,19 @@ def test_metrics_match_reference_formula():
         assert abs(float(got[3 + i]) - float(ndcg)) < 1e-6
 
 
+def test_metrics_ties_count_against_positive():
+    # an untrained / degenerate model scores every candidate the same: the
+    # positive must then rank last, not first (no optimistic hits)
+    scores = torch.zeros(4, 101)
+    got = recall_ndcg_sums(scores)
+    assert float(got.sum()) == 0.0
+    scores[:, 0] = 1.0
+    scores[:, 1:10] = 1.0               # 9 ties ahead -> rank 9: a hit at @10 only
+    got = recall_ndcg_sums(scores) / 4
+    assert float(got[0]) == 1.0
+    assert abs(float(got[3]) - 1.0 / math.log2(11)) < 1e-6
+
+
 def _batch(g, B, T, n_items, n_mask=3):
     base = torch.randint(1, n_items - T, (B, 1), generator=g)
     seqs = base + torch.arange(T)

@@ -442,6 +442,10 @@ def test_dlrm_graph_replay_matches_eager(staged):
     for t in (a, b):
         t.load_batch(*batches[0])
     b.capture_graph(warmup=1, staged=staged)
+    if staged:
+        # one rank: the prep stage is a no-op and is not captured (no empty graph)
+        assert all(kind == "m" or g is not None for kind, g in b.graph)
+        assert not b.emb.fwd_prep_noop or len(b._stages()) == 14
     a.step()  # replicate the capture warmup on the eager trainer
     for x in batches[1:]:
         a.load_batch(*x)
@@ -701,3 +705,29 @@ def test_batch_load_matches_copies(n):
     assert torch.equal(label_dst, label)
     assert torch.equal(x0[:, :nd], dense.to(torch.bfloat16))
     assert torch.all(x0[:, nd:] == 7.0)          # pad / bias columns untouched
+
+
+def test_load_batch_any_input_dtype_and_offset_views():
+    """DLRMTrainer.load_batch must take int32 ids, float64 labels and an ids
+    view at an odd int64 offset (e.g. a rank's slice of a global id tensor):
+    the fused kernel is used only when its contract holds, else copies."""
+    from tdfo_amd.models.dlrm import DLRMConfig, DLRMTrainer
+
+    cfg = DLRMConfig(embedding_dim=64, table_rows=[100, 50], bottom=[64], top=[64, 1])
+    B = 128
+    tr = DLRMTrainer(cfg, B, DEV)
+    g = torch.Generator(device=DEV).manual_seed(1)
+    dense = torch.rand(B, 13, device=DEV, generator=g)
+    ids = torch.randint(0, 50, (2 * B,), device=DEV, generator=g)
+    label = (torch.rand(B, device=DEV, generator=g) > 0.5).double()
+    tr.load_batch(dense, ids.int(), label)
+    big = torch.cat([torch.zeros(1, dtype=torch.int64, device=DEV), ids])
+    torch.cuda.synchronize()
+    assert torch.equal(tr.ids, ids) and torch.equal(tr.label, label.float())
+    tr.ids.zero_()
+    tr.load_batch(dense, big[1:], label.float())               # 8-B aligned, not 16
+    torch.cuda.synchronize()
+    assert torch.equal(tr.ids, ids)
+    assert torch.equal(tr.x0[:, :13], dense.to(torch.bfloat16))
+    tr.step()
+    torch.cuda.synchronize()

@@ -1,6 +1,6 @@
 import pytest
 
-from tdfo_amd.models.dlrm import CRITEO_1TB_ROWS, DLRMConfig
+from tdfo_amd.models.dlrm import CRITEO_1TB_ROWS, DCN_GT1TB_ROWS, MLPERF_MULTIHOT, DLRMConfig
 from tdfo_amd.sparse.planner import GiB, plan_sharding
 from tdfo_amd.sparse.tables import EmbOptimConfig
 
@@ -37,3 +37,33 @@ def test_plan_adam_state_counts():
     p = plan_sharding(cfg.tables(), 8, EmbOptimConfig("adam"))
     tot = sum(p.mem_bytes)
     assert tot > 2.9 * sum(t.bytes_fp32 for t in cfg.tables())
+
+
+def test_plan_config5_gt1tb_rowwise_fits_8_not_4():
+    """BASELINE config 5: DCN-v2 over a >1 TB table set, row-wise sharded
+    across 8 x 288 GB (the tables too big for one GPU go row-wise)."""
+    cfg = DLRMConfig(table_rows=DCN_GT1TB_ROWS, interaction="dcn", pooling=MLPERF_MULTIHOT)
+    opt = EmbOptimConfig("rowwise_adagrad")
+    total = sum(t.num_embeddings * (t.embedding_dim * 4 + 4) for t in cfg.tables())
+    assert total > 1e12
+    p = plan_sharding(cfg.tables(), 8, opt, pooling=MLPERF_MULTIHOT)
+    kinds = p.summary()["kinds"]
+    assert kinds.get("row_wise", 0) >= 4
+    big = [t for t in range(26) if cfg.table_rows[t] * 516 > 288e9 * 0.85]
+    assert all(p.kind_of(t) == "row_wise" for t in big)
+    assert max(p.mem_bytes) <= 288e9 * 0.85
+    assert sum(p.mem_bytes) >= total
+    for w in (1, 2, 4):
+        with pytest.raises(MemoryError):
+            plan_sharding(cfg.tables(), w, opt, pooling=MLPERF_MULTIHOT)
+
+
+def test_plan_cost_counts_xgmi():
+    cfg = DLRMConfig()
+    opt = EmbOptimConfig("rowwise_adagrad")
+    p1 = plan_sharding(cfg.tables(), 1, opt)
+    p8 = plan_sharding(cfg.tables(), 8, opt)
+    # weak scaling: per-rank lookup work is ~constant, the exchange adds link time
+    assert sum(p8.cost) / 8 > sum(p1.cost)
+    prw = plan_sharding(cfg.tables(), 8, opt, strategy="row_wise")
+    assert max(prw.cost) > max(p8.cost)          # RW moves W x the pooled bytes

@@ -94,14 +94,14 @@ def test_sharded_embedding_fwd_bwd(strategy, world):
             assert torch.allclose(w, exp, atol=1e-2), (rank, t)
 
 
-def _dlrm_worker(rank, world, B, steps, strategy, emb_opt="rowwise_adagrad"):
+def _dlrm_worker(rank, world, B, steps, strategy, emb_opt="rowwise_adagrad", rw_comm="fp32"):
     from tdfo_amd.data.synthetic import SyntheticCriteo
     from tdfo_amd.models.dlrm import DLRMConfig, DLRMTrainer
     from tdfo_amd.parallel.dist import get_info
 
     cfg = DLRMConfig(embedding_dim=32, table_rows=ROWS, bottom=[64, 32], top=[64, 32, 1],
                      dense_lr=1e-2, emb_lr=0.05, sharding=strategy, pooling=[1, 2, 1, 1, 1],
-                     emb_opt=emb_opt)
+                     emb_opt=emb_opt, rw_comm=rw_comm)
     tr = DLRMTrainer(cfg, B, "cpu", group=get_info().group, rank=rank, world_size=world)
     g = torch.Generator().manual_seed(5)
     for t, r in enumerate(ROWS):
