@@ -561,6 +561,26 @@ void embedding_bwd_apply(const Tensor& W, const Tensor& row_offset, const Tensor
   tdfo::embedding_bwd_apply(a, cur_stream());
 }
 
+void embedding_dense_update(const Tensor& W, const Tensor& grad, int64_t rows, int64_t opt,
+                            const c10::optional<Tensor>& state1, const c10::optional<Tensor>& state2,
+                            const Tensor& hyper, double eps, double beta1, double beta2,
+                            double weight_decay) {
+  check_dev(W, "W");
+  TORCH_CHECK(W.scalar_type() == at::kFloat && W.is_contiguous() && W.dim() == 2, "W fp32 2-D");
+  const int64_t D = W.size(1);
+  TORCH_CHECK(D == 16 || D == 32 || D == 64 || D == 128 || D == 256 || D == 512, "embedding D unsupported");
+  TORCH_CHECK(rows >= 0 && rows <= W.size(0), "rows out of range");
+  check_dev(grad, "grad");
+  TORCH_CHECK(grad.scalar_type() == at::kFloat && grad.is_contiguous() && grad.numel() >= rows * D,
+              "dense grad must be contiguous fp32 [rows, D]");
+  TORCH_CHECK(opt != tdfo::EMB_DENSE_GRAD, "dense update needs a real optimizer");
+  tdfo::EmbBwdArgs a{};
+  a.W = W.data_ptr<float>(); a.D = (int)D;
+  emb_bwd_opt_args(a, W, grad, opt, state1, state2, hyper, eps, beta1, beta2, weight_decay,
+                   c10::nullopt);
+  tdfo::embedding_dense_update(a, rows, grad.data_ptr<float>(), cur_stream());
+}
+
 // ------------------------------------------------------- row-wise shards
 int64_t rw_meta_check(const Tensor& meta, int64_t nrw) {
   check_i64(meta, "rw meta");
@@ -968,6 +988,9 @@ TORCH_LIBRARY(tdfo, m) {
         "int grad_stride, int opt, Tensor(b!)? state1, Tensor(c!)? state2, Tensor hyper, "
         "float eps, float beta1, float beta2, float weight_decay, Tensor(d!)? dense_grad, "
         "int segsort, Tensor(e!) workspace) -> ()");
+  m.def("embedding_dense_update(Tensor(a!) W, Tensor grad, int rows, int opt, Tensor(b!)? state1, "
+        "Tensor(c!)? state2, Tensor hyper, float eps, float beta1, float beta2, "
+        "float weight_decay) -> ()");
   m.def("rw_bucketize_workspace(int n, int W) -> int", rw_bucketize_workspace);
   m.def("rw_bucketize(Tensor ids, Tensor meta, int nrw, int W, int B, int cap, int n, "
         "Tensor(a!) send, Tensor(b!) workspace, Tensor(c!) overflow) -> ()");
@@ -1021,6 +1044,7 @@ TORCH_LIBRARY_IMPL(tdfo, CUDA, m) {
   m.impl("embedding_bwd", embedding_bwd);
   m.impl("embedding_bwd_prepare", embedding_bwd_prepare);
   m.impl("embedding_bwd_apply", embedding_bwd_apply);
+  m.impl("embedding_dense_update", embedding_dense_update);
   m.impl("rw_bucketize", rw_bucketize);
   m.impl("rw_pool", rw_pool);
   m.impl("embedding_bwd_prepare_rw", embedding_bwd_prepare_rw);

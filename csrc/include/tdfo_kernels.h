@@ -142,6 +142,10 @@ void embedding_bwd_fused(const EmbBwdArgs& a, hipStream_t s);
 void embedding_bwd_prepare(const EmbBwdArgs& a, hipStream_t s);
 void embedding_bwd_apply(const EmbBwdArgs& a, hipStream_t s);
 
+// Dense optimizer step over rows [0, rows) of W from a dense fp32 gradient
+// [rows, D] (a.opt, a.state1/2, a.hyper, eps/betas/wd as for the backward).
+void embedding_dense_update(const EmbBwdArgs& a, int64_t rows, const float* grad, hipStream_t s);
+
 // --------------------------------------------------- row-wise shards ----
 // (rowwise.hip) Fixed-capacity row-wise exchange. meta (int64, device):
 // [in_base (nrw) | L (nrw) | blk (nrw) | lrow (nrw) | cum (nrw + 1)]:

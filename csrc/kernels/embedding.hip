@@ -683,6 +683,53 @@ __global__ void emb_rw_keys_kernel(const EmbBwdArgs a, const int64_t* __restrict
   }
 }
 
+// Dense update of every row of a (replicated) table batch from a dense fp32
+// gradient [rows, D] -- the data-parallel tables' step after their gradient
+// all-reduce. One wave per row; rows with an all-zero gradient are left
+// untouched for SGD / row-wise Adagrad / Adagrad without weight decay, so the
+// result equals the sparse update of the touched rows.
+template <int D, int OPT>
+__global__ __launch_bounds__(256) void emb_dense_update_kernel(EmbBwdArgs a, int64_t rows,
+                                                              const float* __restrict__ g) {
+  constexpr int EPL = BwdCfg<D>::EPL;
+  const int lane = threadIdx.x & 63;
+  const int e0 = elem0<D>(lane);
+  const bool act = D >= 64 || e0 < D;
+  const int e0c = act ? e0 : 0;
+  const OptScalars o = opt_scalars(a);
+  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t row = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; row < rows;
+       row += nw) {
+    float acc[EPL], wv[EPL];
+    load_row<D>(acc, g + row * D + e0c);
+    load_row<D>(wv, a.W + row * D + e0c);
+    if (!act) {
+#pragma unroll
+      for (int u = 0; u < EPL; ++u) acc[u] = 0.f;
+    }
+    const float st = OPT == EMB_ROWWISE_ADAGRAD ? a.state1[row] : 0.f;
+    update_row<D, OPT>(a, o, (uint64_t)row, acc, wv, st, lane);
+  }
+}
+
+template <int D>
+void dense_update_dispatch(const EmbBwdArgs& a, int64_t rows, const float* g, hipStream_t s) {
+  int64_t blocks = (rows + 3) / 4;
+  if (blocks > 16384) blocks = 16384;
+  if (blocks < 1) return;
+#define TDFO_DU(OPT) hipLaunchKernelGGL((emb_dense_update_kernel<D, OPT>), dim3(blocks), dim3(256), \
+                                        0, s, a, rows, g)
+  switch (a.opt) {
+    case EMB_SGD: TDFO_DU(EMB_SGD); break;
+    case EMB_ROWWISE_ADAGRAD: TDFO_DU(EMB_ROWWISE_ADAGRAD); break;
+    case EMB_ADAM: TDFO_DU(EMB_ADAM); break;
+    case EMB_ADAGRAD: TDFO_DU(EMB_ADAGRAD); break;
+    default: throw std::runtime_error("embedding_dense_update: unsupported optimizer");
+  }
+#undef TDFO_DU
+  TDFO_CHECK_HIP(hipGetLastError());
+}
+
 int g_emb_segsort = 1;   // one-hot batches: per-table LDS sort (0: device-wide radix sort)
 
 struct WsLayout {
@@ -902,6 +949,17 @@ void embedding_bwd_prepare_rw(const EmbBwdArgs& a, const int64_t* recv, const in
     prep_rw_impl<uint32_t>(a, L, recv, meta, nrw, W, cap, grad_ld, dummy_row, s);
   else
     prep_rw_impl<uint64_t>(a, L, recv, meta, nrw, W, cap, grad_ld, dummy_row, s);
+}
+
+void embedding_dense_update(const EmbBwdArgs& a, int64_t rows, const float* grad, hipStream_t s) {
+  switch (a.D) {
+    case 16: dense_update_dispatch<16>(a, rows, grad, s); break;
+    case 32: dense_update_dispatch<32>(a, rows, grad, s); break;
+    case 64: dense_update_dispatch<64>(a, rows, grad, s); break;
+    case 128: dense_update_dispatch<128>(a, rows, grad, s); break;
+    case 256: dense_update_dispatch<256>(a, rows, grad, s); break;
+    case 512: dense_update_dispatch<512>(a, rows, grad, s); break;
+  }
 }
 
 void embedding_bwd_apply(const EmbBwdArgs& a, hipStream_t s) {

@@ -545,6 +545,7 @@ class DLRMTrainer:
                                 True)
         else:
             self._dcn_backward(h)
+        emb.stage_bwd_local(self.emb_hyper)        # replicated tables' dense grads
         self._join(self._ws)
         self._join(self._ps)
 

@@ -197,6 +197,18 @@ def embedding_bwd_apply(W, row_offset, indices, offsets, grad_off, T, B, grad, g
                                   beta1, beta2, weight_decay, dense_grad, int(segsort), workspace)
 
 
+def embedding_dense_update(W, grad, rows, opt, hyper, state1=None, state2=None, eps=1e-8,
+                           beta1=0.9, beta2=0.999, weight_decay=0.0):
+    """Optimizer step over rows [0, rows) of W from a dense fp32 gradient
+    (data-parallel tables after their gradient all-reduce)."""
+    if _gpu(W):
+        _native().embedding_dense_update(W, grad, int(rows), int(opt), state1, state2, hyper, eps,
+                                         beta1, beta2, weight_decay)
+    else:
+        ref.embedding_dense_update(W, grad, rows, opt, state1, state2, hyper, eps, beta1, beta2,
+                                   weight_decay)
+
+
 def rw_bucketize_workspace(n: int, W: int) -> int:
     return int(_native().rw_bucketize_workspace(int(n), int(W))) if native_available() else 1
 

@@ -175,6 +175,26 @@ def embedding_bwd(W, row_offset, indices, offsets, grad_off, psw, T, B, mean, ke
     W[rows] = w
 
 
+def embedding_dense_update(W, grad, rows, opt, state1, state2, hyper, eps, beta1, beta2,
+                           weight_decay):
+    """Dense step over rows [0, rows) from a dense [rows, D] gradient; rows with
+    an all-zero gradient are skipped like the kernel's no-op update (exact for
+    SGD / Adagrad / row-wise Adagrad without weight decay)."""
+    D = W.shape[1]
+    g = grad.reshape(-1)[: rows * D].view(rows, D).float()
+    if opt in (EMB_SGD, EMB_ROWWISE_ADAGRAD, EMB_ADAGRAD) and weight_decay == 0.0:
+        idx = torch.nonzero(g.abs().sum(1) > 0).view(-1)
+    else:
+        idx = torch.arange(rows, device=W.device)
+    n = int(idx.numel())
+    if n == 0:
+        return
+    z = torch.zeros(1, dtype=torch.int64, device=W.device)
+    embedding_bwd(W, z, idx, torch.arange(n + 1, device=W.device), z, None, 1, n, False, 64,
+                  g[idx].contiguous(), D, opt, state1, state2, hyper, eps, beta1, beta2,
+                  weight_decay, None)
+
+
 def rw_unpack_meta(meta, nrw):
     m = meta.to(torch.int64)
     return m[:nrw], m[nrw:2 * nrw], m[2 * nrw:3 * nrw], m[3 * nrw:4 * nrw], m[4 * nrw:5 * nrw + 1]

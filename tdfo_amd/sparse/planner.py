@@ -80,12 +80,19 @@ def plan_sharding(tables: Sequence[TableConfig], world_size: int, optim: EmbOpti
                   batch_per_rank: int = 8192, pooling: Optional[Sequence[float]] = None,
                   hbm_bytes: int = HBM_BYTES, reserve_frac: float = 0.15,
                   strategy: str = "auto", dp_max_bytes: int = 0,
-                  row_cost: Optional[Callable[[int], float]] = None) -> ShardingPlan:
+                  row_cost: Optional[Callable[[int], float]] = None,
+                  dp_max_rows: Optional[int] = None) -> ShardingPlan:
     """Deterministic greedy planner.
 
     strategy: "auto" (table-wise with row-wise fallback for tables that fit
     no rank), "table_wise", "row_wise", "column_wise" (tables split evenly by
     columns), "data_parallel".
+
+    dp_max_rows: "auto" replicates (data_parallel) every table with fewer
+    rows than this (default at W > 1: batch_per_rank // 2 -- a replicated
+    table's dense fp32 gradient all-reduce then moves fewer bytes than the
+    table-wise pooled all-to-all it replaces, 4 B x rows vs 2 B x batch per
+    column, and its lookups stay local).
 
     row_cost: optional per-lookup cost multiplier as a function of a table's
     row count. Default: none -- measured on MI355X at the world-8 layout
@@ -106,6 +113,8 @@ def plan_sharding(tables: Sequence[TableConfig], world_size: int, optim: EmbOpti
 
     rc = row_cost or (lambda rows: 1.0)
     B = batch_per_rank
+    if dp_max_rows is None:
+        dp_max_rows = batch_per_rank // 2 if W > 1 else 0
 
     def link_us(rows_per_link: float, d: int) -> float:
         return 2 * rows_per_link * d * 2 / (LINK_GBS * 1e3) if W > 1 else 0.0
@@ -155,7 +164,8 @@ def plan_sharding(tables: Sequence[TableConfig], world_size: int, optim: EmbOpti
         if shards[t] is not None:
             continue
         tb = tables[t].num_embeddings * _mem_per_row(tables[t].embedding_dim, optim)
-        if strategy == "data_parallel" or (strategy == "auto" and tb <= dp_max_bytes):
+        if strategy == "data_parallel" or (strategy == "auto" and (
+                tb <= dp_max_bytes or tables[t].num_embeddings < dp_max_rows)):
             for r in range(W):
                 mem[r] += tb
                 cost[r] += tcost(t) / W

@@ -57,7 +57,10 @@ def _reduce_scatter(out, inp, group, async_op=False):
     if inp.is_cuda and dist.get_backend(group) == "gloo":
         W = dist.get_world_size(group)
         tmp = torch.empty_like(inp)
-        dist.all_to_all_single(tmp, inp, group=group)
+        # explicit splits: gloo's equal-split device all-to-all mangles bf16
+        # (measured on the shared-GPU rehearsal); the split-size form is exact
+        n = inp.numel() // W
+        _a2a(tmp, inp, [n] * W, [n] * W, group)
         out.copy_(tmp.view(W, -1).float().sum(0))
         return _Done()
     return dist.reduce_scatter_tensor(out, inp, group=group, async_op=async_op)
@@ -76,7 +79,7 @@ class ShardedEmbeddingBags:
     def __init__(self, tables: Sequence[TableConfig], plan: ShardingPlan, rank: int,
                  batch_size: int, pooling: Sequence[int], device, optim: EmbOptimConfig,
                  group=None, seed: int = 0, mean: bool = False, rw_capacity: float = 1.25,
-                 rw_comm: str = "bf16"):
+                 rw_comm: str = "bf16", dp_dense_max_bytes: int = 256 << 20):
         """``rw_capacity``: per-owner segment capacity of the row-wise exchange
         as a multiple of the uniform share n/W (+256); exceeding it raises
         (``check_overflow``) instead of training on partial bags.
@@ -288,7 +291,18 @@ class ShardedEmbeddingBags:
             self.dp_out_off = torch.tensor([self.dp_base + j * D for j in range(len(dpt))],
                                            dtype=torch.int64, device=self.device)
             self.dp_ids = torch.zeros(self.dp_nid, dtype=torch.int64, device=self.device)
-            if W > 1:
+            # small replicated tables (the planner's default for W > 1): each
+            # rank's fused backward writes a dense fp32 gradient, one
+            # all-reduce sums it and every rank takes the same dense step --
+            # per-rank work and bytes independent of the batch size and W
+            dp_bytes = self.dp_store.total_rows * D * 4
+            self.dp_dense = W > 1 and dp_bytes <= dp_dense_max_bytes
+            if self.dp_dense:
+                self.dp_dgrad = torch.zeros(self.dp_store.total_rows, D, dtype=torch.float32,
+                                            device=self.device)
+            elif W > 1:
+                # large replicated tables: all-gather ids + pooled grads, and
+                # every rank applies the identical global-batch sparse update
                 self.dp_g_offsets = bag_offsets(W * B)
                 self.dp_g_ids = torch.zeros(W * self.dp_nid, dtype=torch.int64, device=self.device)
                 self.dp_g_grad = torch.zeros(W * B * self.dp_width, dtype=bf, device=self.device)
@@ -420,7 +434,7 @@ class ShardedEmbeddingBags:
 
     def stage_fwd_ids_exchange(self):
         W = self.world
-        if self.dp_tables and W > 1:
+        if self.dp_tables and W > 1 and not self.dp_dense:
             dist.all_gather_into_tensor(self.dp_g_ids, self.dp_ids, group=self.group)
         if W > 1 and not self.tw_identity:
             _a2a(self.tw_recv_ids, self.tw_send_ids, [self.tw_recv_count] * W,
@@ -437,7 +451,7 @@ class ShardedEmbeddingBags:
             self.dp_store.forward(self.dp_ids, self.dp_offsets, self.dp_store.row_offset,
                                   len(self.dp_tables), B, self.recv, self.dp_out_off,
                                   self.dp_width, mean=self.mean)
-            if W > 1:
+            if W > 1 and not self.dp_dense:
                 torch.index_select(self.dp_g_ids, 0, self.dp_g_perm, out=self.dp_g_ids_t)
         if self.tw_nv:
             self.tw_store.forward(self.tw_recv_ids, self.tw_v_offsets, self.tw_v_row_off, self.tw_nv,
@@ -480,6 +494,27 @@ class ShardedEmbeddingBags:
             ops.cast_bf16(self.rw_rs32, self._rw_region(self.recv))
 
     # ----------------------------------------------------------- backward
+    def stage_bwd_local(self, hyper: torch.Tensor, d_recv: Optional[torch.Tensor] = None):
+        """Local part of the backward that must precede the exchanges: the
+        dense gradient of the small replicated tables (zeroed + written by
+        the fused backward). Compute stage: the trainer runs it right after
+        the interaction backward."""
+        if self.dp_tables and self.world > 1 and self.dp_dense:
+            from .. import ops
+            d_recv = self.d_recv if d_recv is None else d_recv
+            st = self.dp_store
+            self.dp_dgrad.zero_()
+            ops.embedding_bwd(st.weight, st.row_offset, self.dp_ids, self.dp_offsets,
+                              self.dp_out_off, len(self.dp_tables), self.B, d_recv,
+                              self.dp_width, ops.EMB_DENSE_GRAD, hyper, key_bits=st.key_bits,
+                              mean=self.mean, dense_grad=self.dp_dgrad)
+
+    def backward(self, hyper: torch.Tensor, d_recv: Optional[torch.Tensor] = None):
+        """The whole backward in one call (tests / eager use)."""
+        self.stage_bwd_local(hyper, d_recv)
+        self.backward_start(d_recv)
+        self.backward_finish(hyper)
+
     def backward_start(self, d_recv: Optional[torch.Tensor] = None):
         """Start the gradient exchange (async on GPU). ``d_recv`` defaults to
         ``self.d_recv`` (same layout as ``self.recv``)."""
@@ -494,7 +529,9 @@ class ShardedEmbeddingBags:
                         [B * self.dsum[self.rank]] * W, self.tw_recv_sizes, self.group,
                         async_op=True)
         self._dp_work = None
-        if W > 1 and self.dp_tables:
+        if W > 1 and self.dp_tables and self.dp_dense:
+            self._dp_work = dist.all_reduce(self.dp_dgrad, group=self.group, async_op=True)
+        elif W > 1 and self.dp_tables:
             self._dp_work = dist.all_gather_into_tensor(
                 self.dp_g_grad, d_recv[self.dp_base: self.dp_base + B * self.dp_width],
                 group=self.group, async_op=True)
@@ -551,7 +588,14 @@ class ShardedEmbeddingBags:
                                           self.dsum[self.rank], hyper, mean=self.mean)
         if self.dp_tables:
             ndp = len(self.dp_tables)
-            if W > 1:
+            if W > 1 and self.dp_dense:
+                from .. import ops
+                st, o = self.dp_store, self.optim
+                ops.embedding_dense_update(st.weight, self.dp_dgrad, st.total_rows, o.code, hyper,
+                                           state1=st.state1, state2=st.state2, eps=o.eps,
+                                           beta1=o.beta1, beta2=o.beta2,
+                                           weight_decay=o.weight_decay)
+            elif W > 1:
                 self.dp_store.backward_update(self.dp_g_ids_t, self.dp_g_offsets,
                                               self.dp_store.row_offset, ndp, W * B, self.dp_g_grad,
                                               self.dp_g_goff, self.dp_width, hyper, mean=self.mean)

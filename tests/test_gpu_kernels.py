@@ -731,3 +731,34 @@ def test_load_batch_any_input_dtype_and_offset_views():
     assert torch.equal(tr.x0[:, :13], dense.to(torch.bfloat16))
     tr.step()
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("opt", [ops.EMB_ROWWISE_ADAGRAD, ops.EMB_SGD, ops.EMB_ADAGRAD,
+                                 ops.EMB_ADAM])
+@pytest.mark.parametrize("D", [32, 128])
+def test_embedding_dense_update_matches_reference(opt, D):
+    """Replicated tables' step from an all-reduced dense gradient (half the
+    rows untouched: they must not move for SGD / Adagrad variants)."""
+    rows = 3000
+    g = torch.Generator().manual_seed(D + opt)
+    W0 = torch.randn(rows, D, generator=g)
+    grad = torch.randn(rows, D, generator=g) * 0.1
+    grad[::2] = 0.0
+    s1 = s2 = None
+    if opt == ops.EMB_ROWWISE_ADAGRAD:
+        s1 = torch.rand(rows, generator=g)
+    elif opt == ops.EMB_ADAGRAD:
+        s1 = torch.rand(rows, D, generator=g)
+    elif opt == ops.EMB_ADAM:
+        s1, s2 = torch.zeros(rows, D), torch.zeros(rows, D)
+    hyper = torch.tensor([0.05, 3.0])
+    Wg = W0.to(DEV)
+    sg1 = s1.to(DEV) if s1 is not None else None
+    sg2 = s2.to(DEV) if s2 is not None else None
+    ops.embedding_dense_update(Wg, grad.to(DEV), rows, opt, hyper.to(DEV), state1=sg1, state2=sg2)
+    We, se1 = W0.clone(), s1.clone() if s1 is not None else None
+    se2 = s2.clone() if s2 is not None else None
+    ref.embedding_dense_update(We, grad, rows, opt, se1, se2, hyper, 1e-8, 0.9, 0.999, 0.0)
+    assert torch.allclose(Wg.cpu(), We, atol=1e-5, rtol=1e-5)
+    if opt != ops.EMB_ADAM:
+        assert torch.equal(Wg.cpu()[::2], W0[::2])

@@ -19,7 +19,7 @@ B = 256
 STEPS = 3
 
 
-def _worker(rank, world, Bk, strategy, graph, rw_comm):
+def _worker(rank, world, Bk, strategy, graph, rw_comm, emb_opt="rowwise_adagrad"):
     from tdfo_amd.data.synthetic import SyntheticCriteo
     from tdfo_amd.models.dlrm import DLRMConfig, DLRMTrainer
     from tdfo_amd.parallel.dist import get_info
@@ -27,8 +27,7 @@ def _worker(rank, world, Bk, strategy, graph, rw_comm):
     dev = get_info().device if world > 1 else torch.device("cuda", 0)
     cfg = DLRMConfig(embedding_dim=64, table_rows=ROWS, bottom=[128, 64], top=[128, 64, 1],
                      dense_opt="sgd", dense_lr=0.05, emb_lr=0.05, sharding=strategy,
-                     pooling=POOL, rw_comm=rw_comm, emb_opt="adagrad"
-                     if strategy == "column_wise" else "rowwise_adagrad")
+                     pooling=POOL, rw_comm=rw_comm, emb_opt=emb_opt)
     tr = DLRMTrainer(cfg, Bk, dev, group=get_info().group, rank=rank, world_size=world)
     g = torch.Generator().manual_seed(5)
     for t, r in enumerate(ROWS):
@@ -68,27 +67,33 @@ def _worker(rank, world, Bk, strategy, graph, rw_comm):
 
 @pytest.fixture(scope="module")
 def single():
-    """One process stepping the 2x batch (table-wise at world 1; the
-    column-wise comparison uses elementwise Adagrad on both sides)."""
+    """One process stepping the 2x batch (table-wise at world 1)."""
     cache = {}
 
-    def get(cw: bool):
-        if cw not in cache:
-            strategy = "column_wise" if cw else "table_wise"
-            cache[cw] = run_distributed(_worker, 1, 2 * B, strategy, True, "fp32",
-                                        device="cuda")[0]
-        return cache[cw]
+    def get(emb_opt: str):
+        if emb_opt not in cache:
+            cache[emb_opt] = run_distributed(_worker, 1, 2 * B, "table_wise", True, "fp32", emb_opt,
+                                             device="cuda")[0]
+        return cache[emb_opt]
     return get
 
 
-@pytest.mark.parametrize("strategy,graph,rw_comm", [
-    ("table_wise", True, "bf16"), ("table_wise", False, "bf16"),
-    ("row_wise", True, "fp32"), ("row_wise", True, "bf16"),
-    ("column_wise", True, "bf16"), ("data_parallel", True, "bf16")])
-def test_two_ranks_match_one_process(strategy, graph, rw_comm, single):
-    multi = run_distributed(_worker, 2, B, strategy, graph, rw_comm, device="cuda", timeout=600)
-    p1, tabs1, loss1 = single(strategy == "column_wise")
-    tol = 3e-3 if rw_comm == "fp32" or strategy != "row_wise" else 1e-2
+# Column-wise keeps one row-wise Adagrad state per column block (as TorchRec CW
+# shards do), so it is compared with elementwise Adagrad on both sides. The
+# bf16 row-wise reduce-scatter rounds pooled partials differently from one
+# process; row-wise Adagrad (lr / sqrt(mean g^2), zero initial state) turns
+# that into O(lr) differences on rows whose gradient is ~0, so that case is
+# compared under SGD (exactness of the exchange itself: the fp32 case).
+@pytest.mark.parametrize("strategy,graph,rw_comm,emb_opt", [
+    ("table_wise", True, "bf16", "rowwise_adagrad"), ("table_wise", False, "bf16", "rowwise_adagrad"),
+    ("row_wise", True, "fp32", "rowwise_adagrad"), ("row_wise", True, "bf16", "sgd"),
+    ("column_wise", True, "bf16", "adagrad"), ("data_parallel", True, "bf16", "rowwise_adagrad"),
+    ("auto", True, "bf16", "rowwise_adagrad")])
+def test_two_ranks_match_one_process(strategy, graph, rw_comm, emb_opt, single):
+    multi = run_distributed(_worker, 2, B, strategy, graph, rw_comm, emb_opt, device="cuda",
+                            timeout=600)
+    p1, tabs1, loss1 = single(emb_opt)
+    tol = 1e-2 if (strategy == "row_wise" and rw_comm == "bf16") else 3e-3
     loss = multi[0][2] + multi[1][2]
     assert abs(loss - loss1) / abs(loss1) < tol, (loss, loss1)
     for rank in range(2):

@@ -29,7 +29,7 @@ def global_ids(B, L, world, seed=1):
     return out, per_table
 
 
-def _emb_worker(rank, world, strategy, B, L):
+def _emb_worker(rank, world, strategy, B, L, dp_dense_max_bytes=256 << 20):
     from tdfo_amd.parallel.dist import get_info
     from tdfo_amd.sparse.planner import plan_sharding
     from tdfo_amd.sparse.sharded import ShardedEmbeddingBags
@@ -38,7 +38,8 @@ def _emb_worker(rank, world, strategy, B, L):
     tables = [TableConfig(f"t{i}", r, D) for i, r in enumerate(ROWS)]
     optim = EmbOptimConfig("sgd", lr=0.5)
     plan = plan_sharding(tables, world, optim, batch_per_rank=B, pooling=L, strategy=strategy)
-    emb = ShardedEmbeddingBags(tables, plan, rank, B, L, "cpu", optim, group=get_info().group)
+    emb = ShardedEmbeddingBags(tables, plan, rank, B, L, "cpu", optim, group=get_info().group,
+                               dp_dense_max_bytes=dp_dense_max_bytes)
     full = full_tables()
     for t in range(len(ROWS)):
         emb.set_table_weight(t, full[t])
@@ -51,8 +52,7 @@ def _emb_worker(rank, world, strategy, B, L):
     g = torch.Generator().manual_seed(100 + rank)
     emb.d_recv.copy_((torch.randn(emb.d_recv.numel(), generator=g) * 0.1).to(emb.d_recv.dtype))
     d_recv = emb.d_recv.float().clone()
-    emb.backward_start()
-    emb.backward_finish(torch.tensor([0.5, 1.0]))
+    emb.backward(torch.tensor([0.5, 1.0]))
     shards = {}
     for t in range(len(ROWS)):
         r = emb.get_table_weight(t)
@@ -61,12 +61,15 @@ def _emb_worker(rank, world, strategy, B, L):
     return feats, d_recv, shards, [list(emb.slot_off), list(emb.slot_stride)]
 
 
-@pytest.mark.parametrize("strategy,world", [("table_wise", 2), ("row_wise", 2), ("data_parallel", 2),
-                                            ("column_wise", 2), ("table_wise", 3), ("row_wise", 3),
-                                            ("column_wise", 3)])
-def test_sharded_embedding_fwd_bwd(strategy, world):
+@pytest.mark.parametrize("strategy,world,dp_dense", [
+    ("table_wise", 2, 1), ("row_wise", 2, 1), ("data_parallel", 2, 1), ("data_parallel", 2, 0),
+    ("column_wise", 2, 1), ("table_wise", 3, 1), ("row_wise", 3, 1), ("column_wise", 3, 1),
+    ("data_parallel", 3, 1)])
+def test_sharded_embedding_fwd_bwd(strategy, world, dp_dense):
+    """dp_dense=0 forces the large-replicated-table path (all-gathered ids +
+    pooled grads, global sparse update) instead of the dense-grad all-reduce."""
     B, L = 6, [1, 2, 1, 3, 1]
-    res = run_distributed(_emb_worker, world, strategy, B, L)
+    res = run_distributed(_emb_worker, world, strategy, B, L, (256 << 20) if dp_dense else 0)
     full = full_tables()
     ids_all, per_table = global_ids(B, L, world)
     # forward: pooled sums of bf16-rounded output
@@ -126,7 +129,8 @@ def _dlrm_worker(rank, world, B, steps, strategy, emb_opt="rowwise_adagrad", rw_
     return tr.fp.p.clone(), tabs
 
 
-@pytest.mark.parametrize("strategy", ["table_wise", "row_wise", "data_parallel", "column_wise"])
+@pytest.mark.parametrize("strategy", ["table_wise", "row_wise", "data_parallel", "column_wise",
+                                      "auto"])
 def test_dlrm_data_parallel_matches_single_process(strategy):
     B, steps = 8, 3
     # row-wise Adagrad keeps one state per row *per column block* under CW
