@@ -259,6 +259,8 @@ class DLRMTrainer:
         self.dense_opt = opt
         fp.finalize(dev, with_adam=opt in (ops.OPT_ADAMW, ops.OPT_ADAM))
         self.fp = fp
+        # gradient buckets: flat layout is [bottom MLP | top MLP, DCN, head]
+        self._ar_split = fp.offset(self.top_layers[0].name + ".w")
         self._init_dense()
         if world_size > 1:                            # replicated dense arch
             dist.broadcast(fp.p, src=0, group=group)
@@ -452,6 +454,7 @@ class DLRMTrainer:
         else:
             lookup = ("c", emb.stage_fwd_lookup)
         prep = [] if emb.fwd_prep_noop else [("c", lambda: emb.stage_fwd_prep(self.ids))]
+        top_wgrad = [("c", self._s_top_wgrad)] if self._defer_top_wgrad else []
         return prep + [
             ("m", emb.stage_fwd_ids_exchange),
             lookup,
@@ -460,9 +463,10 @@ class DLRMTrainer:
             ("m", self._m_fwd_wait),
             ("c", self._s_top),
             ("m", emb.backward_start),
-            ("c", self._s_top_wgrad),           # overlaps the embedding-grad exchange
+        ] + top_wgrad + [                       # (overlaps the embedding-grad exchange)
+            ("m", self._m_allreduce_top_start),  # top bucket || bottom bwd + embedding update
             ("c", self._s_bottom_bwd),
-            ("m", self._m_allreduce_start),
+            ("m", self._m_allreduce_start),      # bottom bucket
             ("m", emb.backward_wait),
             ("c", self._s_emb_update),
             ("m", self._m_allreduce_wait),
@@ -563,18 +567,33 @@ class DLRMTrainer:
             self._bwd(L, self.bot_in[i], self.bot_grad[i], dx, x_is_relu=i > 0)
         self._join(self._ws)
 
+    # Dense gradients are all-reduced in two buckets of the flat buffer, each
+    # issued as soon as its grads exist (the role of the DDP reducer,
+    # torchrec/train.py:255-260 of the reference): the top MLP (+ head, DCN
+    # cross layers) right after the top backward, overlapping the bottom MLP
+    # backward and the embedding update; the small bottom MLP after its
+    # backward.
+    def _m_allreduce_top_start(self):
+        self._ar_top = None
+        if self.world > 1:
+            self._ar_top = dist.all_reduce(self.fp.g[self._ar_split:], group=self.group,
+                                           async_op=True)
+
     def _m_allreduce_start(self):
         self._ar_work = None
         if self.world > 1:
-            self._ar_work = dist.all_reduce(self.fp.g, group=self.group, async_op=True)
+            self._ar_work = dist.all_reduce(self.fp.g[:self._ar_split], group=self.group,
+                                            async_op=True)
 
     def _s_emb_update(self):
         self.emb.stage_bwd_update(self.emb_hyper)
 
     def _m_allreduce_wait(self):
-        if self._ar_work is not None:
-            self._ar_work.wait()
-            self._ar_work = None
+        for name in ("_ar_top", "_ar_work"):
+            w = getattr(self, name, None)
+            if w is not None:
+                w.wait()
+                setattr(self, name, None)
 
     def _s_dense_update(self):
         self._join(self._es)
