@@ -492,8 +492,16 @@ constexpr int LSTAGE = 3 * TILE_BYTES;             // A (2 images) + B
 constexpr int LNSTAGE = 3;
 constexpr int LSMEM = LNSTAGE * LSTAGE;            // 144 KiB >= 256x128 fp32 epilogue tile
 
-template <bool A_COL, bool B_COL>
-__global__ __launch_bounds__(512, 1) void gemm_big_kernel(GemmArgs p) {
+// MI = 4: 8 waves (4 along M x 2 along N), 64x64 per wave, 2 waves per SIMD.
+// MI = 8: 4 waves (2 x 2), 128x64 per wave (32 accumulators), 1 wave per
+// SIMD: 1.33x the FLOP per LDS-read byte of the 64x64 wave tile (12 fragment
+// reads per 32 MFMAs instead of 8 per 16), the wave hides its own reads
+// between MFMAs (fragment double buffer) and the 3-deep ring keeps two K
+// tiles of DMA in flight.
+template <bool A_COL, bool B_COL, int MI>
+__global__ __launch_bounds__(MI == 4 ? 512 : 256, 1) void gemm_big_kernel(GemmArgs p) {
+  constexpr int NW = MI == 4 ? 8 : 4;               // waves
+  constexpr int APW = 32 / NW, BPW = 16 / NW;       // A / B pieces per wave per K tile
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   TDFO_LDS char* smem = (TDFO_LDS char*)smem_raw;
 
@@ -509,67 +517,70 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(GemmArgs p) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wr = w >> 1, wc = w & 1;
 
-  f32x4_t acc[4][4];
+  f32x4_t acc[MI][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
-  // 6 pieces per thread per K tile: A images 2 x 16 pieces over 8 waves,
-  // B image 16 pieces over 8 waves.
+  // 48 pieces per K tile (A: 2 images x 16, B: 16) spread over the waves.
   auto stage = [&](int buf, int kt) {
     TDFO_LDS char* ta = smem + buf * LSTAGE;
     TDFO_LDS char* tb = ta + 2 * TILE_BYTES;
     const int k0 = kt * BK;
     if (!(p.abl & 1))
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int ii = w * 4 + i, half = ii >> 4;
+    for (int i = 0; i < APW; ++i) {
+      const int ii = w * APW + i, half = ii >> 4;
       glds_piece_asm<A_COL>(p.A, p.lda, m0 + half * 128, p.M, k0, ta + half * TILE_BYTES,
                             ii & 15, lane);
     }
     if (!(p.abl & 2))
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-      glds_piece_asm<B_COL>(p.B, p.ldb, n0, p.N, k0, tb, w * 2 + i, lane);
+    for (int i = 0; i < BPW; ++i)
+      glds_piece_asm<B_COL>(p.B, p.ldb, n0, p.N, k0, tb, w * BPW + i, lane);
+  };
+  auto wait_one_ahead = [&]() {        // all but the youngest K tile's pieces landed
+    if constexpr (NW == 8) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)" ::: "memory");
   };
 
-  // Fragment-pipelined main loop (default): one raw barrier per K tile, in
-  // the middle of it. Iteration t: issue tile t+2's DMA, read tile t's k=32..63
+  // Fragment-pipelined main loop: one raw barrier per K tile, in the middle
+  // of it. Iteration t: issue tile t+2's DMA, read tile t's k=32..63
   // fragments, MFMAs on its k=0..31 fragments (read last iteration) hide that
   // read, then wait for tile t+1 + barrier, read tile t+1's k=0..31
   // fragments, and the k=32..63 MFMAs hide those. Ring-slot reuse: slot
   // (t+2)%3 was last read before iteration t-1's barrier (each wave drains
   // its LDS reads with lgkmcnt(0) before that barrier).
   if (nk > 0 && !(p.abl & 16)) {
-    const TDFO_LDS char* tAo = smem + (wr >> 1) * TILE_BYTES;
+    const TDFO_LDS char* tAo = smem + (MI == 4 ? (wr >> 1) : wr) * TILE_BYTES;
     const TDFO_LDS char* tBo = smem + 2 * TILE_BYTES;
-    const int a_r0 = (wr & 1) * 64, b_c0 = wc * 64;
-    auto frags = [&](int buf, int ks, bf16x8_t (&af)[4], bf16x8_t (&bfr)[4]) {
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        af[i] = A_COL ? frag_col(tAo + buf * LSTAGE, a_r0 + i * 16, ks, lane)
-                      : frag_row(tAo + buf * LSTAGE, a_r0 + i * 16, ks, lane);
+    const int a_r0 = MI == 4 ? (wr & 1) * 64 : 0, b_c0 = wc * 64;
+    auto frags = [&](int buf, int ks, bf16x8_t (&af)[MI], bf16x8_t (&bfr)[4]) {
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         bfr[j] = B_COL ? frag_col(tBo + buf * LSTAGE, b_c0 + j * 16, ks, lane)
                        : frag_row(tBo + buf * LSTAGE, b_c0 + j * 16, ks, lane);
-    };
-    auto mm = [&](const bf16x8_t (&af)[4], const bf16x8_t (&bfr)[4]) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < MI; ++i)
+        af[i] = A_COL ? frag_col(tAo + buf * LSTAGE, a_r0 + i * 16, ks, lane)
+                      : frag_row(tAo + buf * LSTAGE, a_r0 + i * 16, ks, lane);
+    };
+    auto mm = [&](const bf16x8_t (&af)[MI], const bf16x8_t (&bfr)[4]) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     };
     stage(0, kt0);
     if (nk > 1) stage(1, kt0 + 1);
-    if (nk > 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    if (nk > 1) wait_one_ahead();
     else        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    bf16x8_t a0[4], b0[4], a1[4], b1[4];
+    bf16x8_t a0[MI], b0[4], a1[MI], b1[4];
     frags(0, 0, a0, b0);
     int cur = 0;
     // steady state (straight-line body so the compiler's lgkmcnt waits only
@@ -582,7 +593,7 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(GemmArgs p) {
       __builtin_amdgcn_sched_barrier(0);
       mm(a0, b0);
       __builtin_amdgcn_sched_barrier(0);
-      if (pre) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+      if (pre) wait_one_ahead();
       else     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
@@ -601,26 +612,26 @@ __global__ __launch_bounds__(512, 1) void gemm_big_kernel(GemmArgs p) {
     if (nk > 1) stage(1, kt0 + 1);
     int cur = 0;
     for (int t = 0; t < nk; ++t) {
-      if (t + 1 < nk && !(p.abl & 7)) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      if (t + 1 < nk && !(p.abl & 7)) wait_one_ahead();
       else            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
       if (t + 2 < nk && !(p.abl & 4)) stage(cur == 0 ? 2 : cur - 1, kt0 + t + 2);
       const TDFO_LDS char* ta = smem + cur * LSTAGE;
-      mfma_k64<A_COL, B_COL>(acc, ta + (wr >> 1) * TILE_BYTES, (wr & 1) * 64,
-                             ta + 2 * TILE_BYTES, wc * 64, lane);
+      mfma_k64<A_COL, B_COL, MI>(acc, ta + (MI == 4 ? (wr >> 1) : wr) * TILE_BYTES,
+                                 MI == 4 ? (wr & 1) * 64 : 0, ta + 2 * TILE_BYTES, wc * 64, lane);
       cur = cur == 2 ? 0 : cur + 1;
     }
   }
   if (p.abl & 32) {                 // perf ablation: keep acc live, skip the epilogue
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j) asm volatile("" :: "v"(acc[i][j]));
     return;
   }
-  epilogue<LBM, 512>(p, acc, smem_raw, m0, n0, wr, wc, lane, tid, ti.split);
+  epilogue<LBM, NW * 64, MI>(p, acc, smem_raw, m0, n0, wr, wc, lane, tid, ti.split);
 }
 
 // 0 auto, 1 small tiles only (64-row tiles when 128-row ones underfill),
@@ -640,7 +651,9 @@ void launch(const GemmArgs& a, hipStream_t s) {
     TDFO_CHECK_HIP(hipFuncSetAttribute((const void*)gemm_kernel<128, AC, BC>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize,
                                        SMEM_BYTES));
-    TDFO_CHECK_HIP(hipFuncSetAttribute((const void*)gemm_big_kernel<AC, BC>,
+    TDFO_CHECK_HIP(hipFuncSetAttribute((const void*)gemm_big_kernel<AC, BC, 4>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, LSMEM));
+    TDFO_CHECK_HIP(hipFuncSetAttribute((const void*)gemm_big_kernel<AC, BC, 8>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, LSMEM));
     attr = true;
   }
@@ -648,16 +661,33 @@ void launch(const GemmArgs& a, hipStream_t s) {
   const int small_tiles = ((a.M + BM - 1) / BM) * tn;
   const int big_tiles = ((a.M + LBM - 1) / LBM) * tn;
   GemmArgs b = a;
-  b.abl = g_policy >= 8 ? g_policy - 8 : 0;      // perf ablations (policy 9..15), big kernel
+  b.abl = (g_policy >= 8 && g_policy < 16) ? g_policy - 8 : 0;  // perf ablations (9..15), big kernel
   if (g_policy == 6) b.abl = 128;                // auto, every output through the LDS epilogue
   if (g_policy == 7) b.abl = 256;                // auto, bf16 outputs through the LDS epilogue
   if (g_policy == 17) b.abl = 512;               // auto, masked dgrads on the direct path
-  const bool autop = g_policy == 0 || g_policy == 6 || g_policy == 7 || g_policy == 17;
+  const bool autop = g_policy == 0 || g_policy == 6 || g_policy == 7 || g_policy == 17 ||
+                     g_policy == 21 || g_policy == 22;
   bool big = (g_policy >= 2 && g_policy != 3 && g_policy != 4 && !autop) ||
              (g_policy == 4 && AC) || (autop && small_tiles * a.splits >= 1024);
+  // policy 20: the 4-wave 128x64-per-wave kernel for every GEMM; 21: auto
+  // with it in place of the 8-wave kernel; 22: auto with it for every GEMM
+  // that fills >= 128 CUs with 256x128 tiles
+  if (g_policy == 20 || (g_policy == 22 && big_tiles * a.splits >= 128)) {
+    b.abl = 0;
+    dim3 grid(big_tiles * a.splits);
+    hipLaunchKernelGGL((gemm_big_kernel<AC, BC, 8>), grid, dim3(256), LSMEM, s, b);
+    TDFO_CHECK_HIP(hipGetLastError());
+    return;
+  }
+  if (g_policy == 21 && small_tiles * a.splits >= 1024) {
+    dim3 grid(big_tiles * a.splits);
+    hipLaunchKernelGGL((gemm_big_kernel<AC, BC, 8>), grid, dim3(256), LSMEM, s, b);
+    TDFO_CHECK_HIP(hipGetLastError());
+    return;
+  }
   if (big) {
     dim3 grid(big_tiles * a.splits);
-    hipLaunchKernelGGL((gemm_big_kernel<AC, BC>), grid, dim3(512), LSMEM, s, b);
+    hipLaunchKernelGGL((gemm_big_kernel<AC, BC, 4>), grid, dim3(512), LSMEM, s, b);
   } else {
     if constexpr (!AC) {
       // 64-row tiles when 128-row tiles leave CUs idle (bottom MLP, top3)

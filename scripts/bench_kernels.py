@@ -37,11 +37,14 @@ def timeit(fn, iters=7, warm=3, reps=20):
     return ts[len(ts) // 2]
 
 
-def gemm_cases(B):
-    # (name, M, N, K): forward y = x W^T shapes of DLRM-1TB
+def gemm_cases(B, dcn=False):
+    # (name, M, N, K): forward y = x W^T shapes of DLRM-1TB (+ DCN-v2's cross
+    # layers V: 3456 -> 512, U: 512 -> 3456 and its 3456-wide top0)
     fwd = [("bot0", B, 512, 64), ("bot1", B, 256, 512), ("bot2", B, 128, 256),
            ("top0", B, 1024, 512), ("top1", B, 1024, 1024), ("top2", B, 512, 1024),
            ("top3", B, 256, 512)]
+    if dcn:
+        fwd += [("dcnV", B, 512, 3456), ("dcnU", B, 3456, 512), ("dcntop0", B, 1024, 3456)]
     return fwd
 
 
@@ -52,12 +55,13 @@ def main():
     ap.add_argument("--policies", default="0", help="comma list of GEMM tile policies to A/B")
     ap.add_argument("--gemm-only", action="store_true")
     ap.add_argument("--wsplits", default="", help="comma list of wgrad split counts to time")
+    ap.add_argument("--dcn", action="store_true", help="also the DCN-v2 cross-layer shapes")
     args = ap.parse_args()
     dev = "cuda"
     B = args.batch
     bf = torch.bfloat16
     out = []
-    for name, M, N, K in gemm_cases(B):
+    for name, M, N, K in gemm_cases(B, args.dcn):
         if args.only and args.only not in name:
             continue
         x = torch.randn(M, K, device=dev).to(bf)

@@ -734,6 +734,22 @@ class DLRMTrainer:
                 "dense_m": self.fp.m, "dense_v": self.fp.v, "dense_hyper": self.dense_hyper,
                 "emb_hyper": self.emb_hyper}
 
+    def dense_state(self):
+        """Replicated training state (dense params, moments, step counters)."""
+        d = {"p": self.fp.p, "dense_hyper": self.dense_hyper, "emb_hyper": self.emb_hyper}
+        if self.fp.m is not None:
+            d["m"] = self.fp.m
+        if self.fp.v is not None:
+            d["v"] = self.fp.v
+        return d
+
+    def load_dense_state(self, d):
+        for k, v in self.dense_state().items():
+            if k not in d:
+                raise KeyError(f"checkpoint is missing dense state {k}")
+            v.copy_(d[k].to(v.device))
+        self.fp.sync_bf16()
+
     def flat_state(self):
         """Flat name -> tensor view of every piece of training state (for the
         sharded checkpoint: each rank saves its own embedding shards)."""

@@ -34,6 +34,7 @@ from ..models.dlrm import (CRITEO_1TB_ROWS, CRITEO_KAGGLE_ROWS, MLPERF_MULTIHOT,
 from ..parallel.dist import init_distributed
 from ..sparse import tables as _tables
 from ..utils import checkpoint as ckpt
+from ..utils import sharded_ckpt
 from ..utils.profiling import ProfileWindow, StepTimer, trace_range
 
 TINY_ROWS = [40_000] * 26          # DLRM-tiny: ~1M embedding rows (BASELINE config 1)
@@ -123,9 +124,12 @@ def run(cfg: Config, mode: str = "single", out_dir: str = ".",
     if cfg.resume and cfg.ckpt_dir:
         latest = _latest(cfg.ckpt_dir)
         if latest is not None:
-            st = ckpt.load_sharded(str(latest), rank, world, expect_meta=meta)
-            tr.load_flat_state(st["tensors"])
-            start = int(st["step"])
+            if sharded_ckpt.is_v2(str(latest)):        # streamed, reshardable
+                start = sharded_ckpt.load(tr, str(latest), rank, world, expect_meta=meta)
+            else:                                       # legacy per-rank files (same plan)
+                st = ckpt.load_sharded(str(latest), rank, world, expect_meta=meta)
+                tr.load_flat_state(st["tensors"])
+                start = int(st["step"])
             data.seek(start)
             _log(rank, f"===== resumed from {latest} at step {start} =====")
     metrics_path = cfg.metrics_file
@@ -201,9 +205,13 @@ def _latest(ckpt_dir: str) -> Optional[Path]:
 
 
 def save(tr: DLRMTrainer, ckpt_dir: str, step: int, rank: int, world: int, meta: Dict):
+    """Streamed per-piece checkpoint (bounded host memory at TB scale), loadable
+    at any world size / sharding plan (utils/sharded_ckpt.py)."""
     barrier = (lambda: torch.distributed.barrier()) if world > 1 else None
-    ckpt.save_sharded(str(Path(ckpt_dir) / f"step_{step}"), rank, world, step, tr.flat_state(),
-                      meta, barrier=barrier)
+    if tr.device.type == "cuda":
+        torch.cuda.synchronize()
+    sharded_ckpt.save(tr, str(Path(ckpt_dir) / f"step_{step}"), step, rank, world, meta,
+                      barrier=barrier)
 
 
 @torch.no_grad()
