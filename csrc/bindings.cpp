@@ -506,7 +506,7 @@ void emb_bwd_opt_args(tdfo::EmbBwdArgs& a, const Tensor& W, const Tensor& grad, 
   if (state1) a.state1 = state1->data_ptr<float>();
   if (state2) a.state2 = state2->data_ptr<float>();
   if (dense_grad) a.dense_grad = dense_grad->data_ptr<float>();
-  a.hyper = hyper.data_ptr<float>();
+  a.hyper = hyper.data_ptr<float>(); a.hyper_n = (int)hyper.numel();
   a.eps = (float)eps; a.beta1 = (float)beta1; a.beta2 = (float)beta2; a.weight_decay = (float)weight_decay;
 }
 
@@ -813,7 +813,8 @@ void auc_hist(const Tensor& logits, const Tensor& labels, int64_t nb, const Tens
 
 void two_tower(const Tensor& X, const Tensor& P, const Tensor& labels, double inv_n,
                const Tensor& logits, const c10::optional<Tensor>& dX,
-               const c10::optional<Tensor>& part) {
+               const c10::optional<Tensor>& part, const c10::optional<Tensor>& loss_scale,
+               bool half) {
   check_dev(X, "X"); check_2d_rowmajor(X, "X");
   const int64_t B = X.size(0);
   TORCH_CHECK(X.scalar_type() == at::kFloat && X.size(1) >= 114 && X.stride(0) % 4 == 0 &&
@@ -824,6 +825,12 @@ void two_tower(const Tensor& X, const Tensor& P, const Tensor& labels, double in
   a.X = X.data_ptr<float>(); a.ldx = X.stride(0);
   a.P = P.data_ptr<float>();
   a.B = (int)B; a.inv_n = (float)inv_n;
+  a.half = half;
+  if (loss_scale) {
+    check_dev(*loss_scale, "loss_scale");
+    TORCH_CHECK(loss_scale->scalar_type() == at::kFloat && loss_scale->numel() >= 1, "loss_scale fp32");
+    a.loss_scale = loss_scale->data_ptr<float>();
+  }
   a.logits = logits.data_ptr<float>();
   const bool train = dX.has_value();
   if (train) {
@@ -1022,7 +1029,7 @@ TORCH_LIBRARY(tdfo, m) {
   m.def("dense_to_jagged(Tensor dense, Tensor offsets, Tensor(a!) vgrad) -> ()");
   m.def("jagged_ids_to_dense(Tensor values, Tensor offsets, int pad, Tensor(a!) out) -> ()");
   m.def("two_tower(Tensor X, Tensor P, Tensor labels, float inv_n, Tensor(a!) logits, "
-        "Tensor(b!)? dX, Tensor(c!)? part) -> ()");
+        "Tensor(b!)? dX, Tensor(c!)? part, Tensor? loss_scale, bool half) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(tdfo, CUDA, m) {

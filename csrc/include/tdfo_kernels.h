@@ -119,7 +119,9 @@ struct EmbBwdArgs {
   const void* grad; int grad_bf16; int64_t grad_stride;
   int opt;
   float* state1; float* state2;  // rowwise: state1[rows]; adam: m, v [rows, D]
-  const float* hyper;          // device: [lr, step]
+  const float* hyper;          // device: [lr, step (, grad scale (, skip flag))]
+  int hyper_n;                 // elements in hyper: > 2 -> grads x hyper[2] (loss-scale
+                               // unscale), > 3 -> no update at all if hyper[3] > 0
   float eps, beta1, beta2, weight_decay;
   float* dense_grad;           // EMB_DENSE_GRAD: accumulate into [rows, D]
   void* workspace; size_t workspace_bytes;
@@ -242,6 +244,9 @@ struct TwoTowerArgs {
   const float* X; int64_t ldx;
   const float* P;
   const float* labels; float inv_n;
+  const float* loss_scale;  // device scalar multiplying dlogit (dynamic loss scaling) or null
+  int half;                 // fp16 compute: inputs, weights, activations and gradients
+                            // rounded to fp16 at every layer boundary, fp32 accumulation
   int B;
   float* logits;
   float* dX; int64_t lddx;

@@ -427,7 +427,7 @@ __device__ __forceinline__ float raw_f(const GradRaw<D, GB>& r, int u) {
   else return r.v[u];
 }
 
-struct OptScalars { float lr, bc1, bc2; };
+struct OptScalars { float lr, bc1, bc2, gs; };
 
 __device__ __forceinline__ OptScalars opt_scalars(const EmbBwdArgs& a) {
   OptScalars o;
@@ -435,15 +435,24 @@ __device__ __forceinline__ OptScalars opt_scalars(const EmbBwdArgs& a) {
   const float step = a.hyper[1];
   o.bc1 = 1.f - powf(a.beta1, step);
   o.bc2 = 1.f - powf(a.beta2, step);
+  o.gs = a.hyper_n > 2 ? a.hyper[2] : 1.f;         // loss-scale unscale factor
   return o;
+}
+
+// Dynamic loss scaling: a step whose gradients were not finite updates nothing.
+__device__ __forceinline__ bool skip_step(const EmbBwdArgs& a) {
+  return a.hyper_n > 3 && a.hyper[3] > 0.f;
 }
 
 // One optimizer update of one row; `wv` = current weights (prefetched).
 template <int D, int OPT>
 __device__ __forceinline__ void update_row(const EmbBwdArgs& a, const OptScalars& o,
-                                           uint64_t row, const float (&acc)[BwdCfg<D>::EPL],
+                                           uint64_t row, const float (&acc_in)[BwdCfg<D>::EPL],
                                            float (&wv)[BwdCfg<D>::EPL], float st_row, int lane) {
   constexpr int EPL = BwdCfg<D>::EPL;
+  float acc[EPL];
+#pragma unroll
+  for (int u = 0; u < EPL; ++u) acc[u] = acc_in[u] * o.gs;
   const int e0 = elem0<D>(lane);
   const bool act = D >= 64 || e0 < D;
   float* w = a.W + row * D + e0;
@@ -518,7 +527,7 @@ __global__ __launch_bounds__(256) void emb_chunk_kernel(
   const int lane = threadIdx.x & 63;
   const int64_t c = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t start = c * CH;
-  if (start >= a.nnz) return;
+  if (start >= a.nnz || skip_step(a)) return;
   const OptScalars o = opt_scalars(a);
   const int64_t end = min(start + (int64_t)CH, a.nnz);
   const int len = (int)(end - start);
@@ -601,6 +610,7 @@ __global__ __launch_bounds__(256) void emb_combine_kernel(
   constexpr int EPL = BwdCfg<D>::EPL, CH = BwdCfg<D>::CH;
   const int lane = threadIdx.x & 63;
   const int nw = (gridDim.x * blockDim.x) >> 6;
+  if (skip_step(a)) return;
   const int n = min(*tail_count, (int)((a.nnz + CH - 1) / CH));
   const int e0 = elem0<D>(lane);
   const bool act = D >= 64 || e0 < D;
@@ -698,6 +708,7 @@ __global__ __launch_bounds__(256) void emb_dense_update_kernel(EmbBwdArgs a, int
   const int e0c = act ? e0 : 0;
   const OptScalars o = opt_scalars(a);
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  if (skip_step(a)) return;
   for (int64_t row = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; row < rows;
        row += nw) {
     float acc[EPL], wv[EPL];

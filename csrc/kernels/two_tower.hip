@@ -20,6 +20,8 @@
 //   [uW1 16x16 | ub1 16 | uW2 16x16 | ub2 16 | iW1 98x16 | ib1 16 | iW2 16x16 | ib2 16]
 // i.e. 150 "rows" of 16; row r < 17 -> (xu,1) x dh_u, r < 34 -> (a_u,1) x du,
 // r < 133 -> (xi,1) x dh_i, else (a_i,1) x di.
+#include <hip/hip_fp16.h>
+
 #include "tdfo_common.h"
 #include "tdfo_kernels.h"
 
@@ -34,14 +36,24 @@ constexpr int NP = AROWS * E;   // 2400
 
 __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
 
-template <bool TRAIN>
+// fp16 compute (the reference's mixed_precision path: Flax dtype=float16 on
+// GPU, jax-flax/models.py:142-151): values are rounded to fp16 where a
+// half-precision layer would store them; sums accumulate in fp32 like an
+// fp16 MFMA / XLA dot with fp32 accumulation.
+template <bool HALF>
+__device__ __forceinline__ float rnd(float x) {
+  if constexpr (HALF) return __half2float(__float2half(x));
+  else return x;
+}
+
+template <bool TRAIN, bool HALF>
 __global__ __launch_bounds__(SPB) void two_tower_kernel(TwoTowerArgs a) {
   __shared__ float Wl[NP];
   __shared__ float As[TRAIN ? SPB : 1][AROWS];
   __shared__ __attribute__((aligned(16))) float Gs[TRAIN ? SPB : 1][4 * E];
   __shared__ float red[SPB / 64];
   const int t = threadIdx.x;
-  for (int k = t; k < NP; k += SPB) Wl[k] = a.P[k];
+  for (int k = t; k < NP; k += SPB) Wl[k] = rnd<HALF>(a.P[k]);
   __syncthreads();
   const float* uW1 = Wl;
   const float* ub1 = Wl + 16 * E;
@@ -59,15 +71,17 @@ __global__ __launch_bounds__(SPB) void two_tower_kernel(TwoTowerArgs a) {
 #pragma unroll
   for (int k = 0; k < E; k += 4) {
     const float4 v = *(const float4*)(xr + k);
-    xu[k] = v.x; xu[k + 1] = v.y; xu[k + 2] = v.z; xu[k + 3] = v.w;
+    xu[k] = rnd<HALF>(v.x); xu[k + 1] = rnd<HALF>(v.y);
+    xu[k + 2] = rnd<HALF>(v.z); xu[k + 3] = rnd<HALF>(v.w);
   }
 #pragma unroll
   for (int k = 0; k < 96; k += 4) {
     const float4 v = *(const float4*)(xr + E + k);
-    xi[k] = v.x; xi[k + 1] = v.y; xi[k + 2] = v.z; xi[k + 3] = v.w;
+    xi[k] = rnd<HALF>(v.x); xi[k + 1] = rnd<HALF>(v.y);
+    xi[k + 2] = rnd<HALF>(v.z); xi[k + 3] = rnd<HALF>(v.w);
   }
-  xi[96] = xr[E + 96];
-  xi[97] = xr[E + 97];
+  xi[96] = rnd<HALF>(xr[E + 96]);
+  xi[97] = rnd<HALF>(xr[E + 97]);
 
   // ---- forward
   float hu[E], au[E], u[E], hi[E], ai[E], iv[E];
@@ -83,8 +97,10 @@ __global__ __launch_bounds__(SPB) void two_tower_kernel(TwoTowerArgs a) {
     for (int o = 0; o < E; ++o) hi[o] = fmaf(xi[k], iW1[k * E + o], hi[o]);
 #pragma unroll
   for (int o = 0; o < E; ++o) {
-    au[o] = hu[o] * sigm(hu[o]);
-    ai[o] = hi[o] * sigm(hi[o]);
+    hu[o] = rnd<HALF>(hu[o]);
+    hi[o] = rnd<HALF>(hi[o]);
+    au[o] = rnd<HALF>(hu[o] * sigm(hu[o]));
+    ai[o] = rnd<HALF>(hi[o] * sigm(hi[o]));
     u[o] = ub2[o];
     iv[o] = ib2[o];
   }
@@ -97,17 +113,24 @@ __global__ __launch_bounds__(SPB) void two_tower_kernel(TwoTowerArgs a) {
     }
   float logit = 0.f;
 #pragma unroll
+  for (int o = 0; o < E; ++o) {
+    u[o] = rnd<HALF>(u[o]);
+    iv[o] = rnd<HALF>(iv[o]);
+  }
+#pragma unroll
   for (int o = 0; o < E; ++o) logit = fmaf(u[o], iv[o], logit);
+  logit = rnd<HALF>(logit);
   if (valid) a.logits[s] = logit;
   if constexpr (!TRAIN) return;
 
   // ---- loss + backward
   const float y = valid ? a.labels[s] : 0.f;
   float loss = valid ? fmaxf(logit, 0.f) - logit * y + log1pf(__expf(-fabsf(logit))) : 0.f;
-  const float dl = valid ? (sigm(logit) - y) * a.inv_n : 0.f;
+  const float ls = a.loss_scale ? a.loss_scale[0] : 1.f;
+  const float dl = valid ? rnd<HALF>((sigm(logit) - y) * a.inv_n * ls) : 0.f;
   float du[E], di[E], dhu[E], dhi[E];
 #pragma unroll
-  for (int o = 0; o < E; ++o) { du[o] = dl * iv[o]; di[o] = dl * u[o]; }
+  for (int o = 0; o < E; ++o) { du[o] = rnd<HALF>(dl * iv[o]); di[o] = rnd<HALF>(dl * u[o]); }
 #pragma unroll
   for (int k = 0; k < E; ++k) {
     float gu = 0.f, gi = 0.f;
@@ -117,8 +140,8 @@ __global__ __launch_bounds__(SPB) void two_tower_kernel(TwoTowerArgs a) {
       gi = fmaf(iW2[k * E + o], di[o], gi);
     }
     const float su = sigm(hu[k]), si = sigm(hi[k]);
-    dhu[k] = gu * su * (1.f + hu[k] * (1.f - su));
-    dhi[k] = gi * si * (1.f + hi[k] * (1.f - si));
+    dhu[k] = rnd<HALF>(gu * su * (1.f + hu[k] * (1.f - su)));
+    dhi[k] = rnd<HALF>(gi * si * (1.f + hi[k] * (1.f - si)));
   }
   if (valid) {
     float* dxr = a.dX + s * a.lddx;
@@ -130,7 +153,7 @@ __global__ __launch_bounds__(SPB) void two_tower_kernel(TwoTowerArgs a) {
         float acc = 0.f;
 #pragma unroll
         for (int o = 0; o < E; ++o) acc = fmaf(uW1[(k + q) * E + o], dhu[o], acc);
-        g[q] = acc;
+        g[q] = rnd<HALF>(acc);
       }
       *(float4*)(dxr + k) = make_float4(g[0], g[1], g[2], g[3]);
     }
@@ -142,7 +165,7 @@ __global__ __launch_bounds__(SPB) void two_tower_kernel(TwoTowerArgs a) {
         float acc = 0.f;
 #pragma unroll
         for (int o = 0; o < E; ++o) acc = fmaf(iW1[(k + q) * E + o], dhi[o], acc);
-        g[q] = acc;
+        g[q] = rnd<HALF>(acc);
       }
       *(float4*)(dxr + E + k) = make_float4(g[0], g[1], g[2], g[3]);
     }
@@ -192,10 +215,14 @@ int two_tower_parts(int B) { return (B + SPB - 1) / SPB; }
 void two_tower(const TwoTowerArgs& a, int train, hipStream_t s) {
   if (a.B <= 0) return;
   const int grid = two_tower_parts(a.B);
-  if (train)
-    hipLaunchKernelGGL(two_tower_kernel<true>, dim3(grid), dim3(SPB), 0, s, a);
+  if (train && a.half)
+    hipLaunchKernelGGL((two_tower_kernel<true, true>), dim3(grid), dim3(SPB), 0, s, a);
+  else if (train)
+    hipLaunchKernelGGL((two_tower_kernel<true, false>), dim3(grid), dim3(SPB), 0, s, a);
+  else if (a.half)
+    hipLaunchKernelGGL((two_tower_kernel<false, true>), dim3(grid), dim3(SPB), 0, s, a);
   else
-    hipLaunchKernelGGL(two_tower_kernel<false>, dim3(grid), dim3(SPB), 0, s, a);
+    hipLaunchKernelGGL((two_tower_kernel<false, false>), dim3(grid), dim3(SPB), 0, s, a);
   TDFO_CHECK_HIP(hipGetLastError());
 }
 

@@ -61,6 +61,13 @@ class TwoTowerConfig:
     init: str = "flax"                 # "flax" (glorot_uniform) | "keras" (lecun_normal dense)
     emb_update: str = "sparse"         # "sparse" | "dense"
     seed: int = 42
+    # jax-flax/train_dp.py:28-29,42,55-81 + models.py:142-151: fp16 compute
+    # with Flax-style DynamicScale (loss x scale; non-finite grads skip the
+    # whole update, params and optimizer state untouched, and halve the
+    # scale; 2000 finite steps double it)
+    mixed_precision: bool = False
+    init_scale: float = 2.0 ** 15
+    growth_interval: int = 2000
 
     def __post_init__(self):
         if self.embed_dim != E:
@@ -145,7 +152,14 @@ class TwoTowerTrainer:
         self.M = torch.zeros(NPARAM, dtype=torch.float32, device=dev)
         self.V = torch.zeros(NPARAM, dtype=torch.float32, device=dev)
         self.hyper = torch.tensor([cfg.learning_rate, 0.0, 1.0], dtype=torch.float32, device=dev)
-        self.emb_hyper = torch.tensor([cfg.learning_rate, 0.0], dtype=torch.float32, device=dev)
+        self.mp = bool(cfg.mixed_precision)
+        # embedding hyper: [lr, step] or, with dynamic loss scaling, [lr, step,
+        # 1/scale, found_inf] (the fused embedding kernels unscale the grads
+        # and skip the update when found_inf > 0)
+        self.emb_hyper = torch.tensor([cfg.learning_rate, 0.0] + ([1.0, 0.0] if self.mp else []),
+                                      dtype=torch.float32, device=dev)
+        self.dyn_scale = torch.tensor([cfg.init_scale, 0.0], dtype=torch.float32, device=dev)
+        self.found_inf = torch.zeros(1, dtype=torch.float32, device=dev)
         # static step buffers (max batch = max(train, eval))
         nb = max(self.B, self.EB)
         self.X = torch.zeros(nb, LDX, dtype=torch.float32, device=dev)
@@ -237,53 +251,101 @@ class TwoTowerTrainer:
         self._lookup(b)
         inv_n = 1.0 / (b * self.world)
         ops.two_tower(self.X[:b], self.P, self.labels[:b], inv_n, self.logits[:b], self.dX[:b],
-                      self.part)
+                      self.part, loss_scale=self.dyn_scale[0:1] if self.mp else None,
+                      half=self.mp)
         nparts = ops.two_tower_parts(b)
         ops.reduce_rows(self.part, nparts, NPARAM + 1, ops.TT_PART_LD, self.G)
         ops.auc_hist(self.logits[:b], self.labels[:b], self.nbins, self.train_hist)
 
+    # ---------------------------------------------------- dynamic loss scale
+    def _mp_check(self, grads):
+        """Device-side finite check of every (scaled) gradient of the step, and
+        the unscale factors / skip flag the fused optimizers read: no host sync."""
+        if not self.mp:
+            return
+        self.found_inf.zero_()
+        for g in grads:
+            ops.check_finite(g.reshape(-1), self.found_inf)
+        inv = torch.reciprocal(self.dyn_scale[0:1])
+        self.hyper[2:3].copy_(inv)
+        self.emb_hyper[2:3].copy_(inv)
+        self.emb_hyper[3:4].copy_(self.found_inf)
+
+    def _mp_update_scale(self):
+        """Flax DynamicScale: backoff x0.5 on a non-finite step, growth x2
+        after ``growth_interval`` consecutive finite steps."""
+        if not self.mp:
+            return
+        f = self.found_inf
+        good = (self.dyn_scale[1:2] + 1.0) * (1.0 - f)
+        grow = (good >= float(self.cfg.growth_interval)).float()
+        scale = self.dyn_scale[0:1]
+        new = (1.0 - f) * scale * (1.0 + grow) + f * torch.clamp(scale * 0.5, min=1.0)
+        self.dyn_scale[0:1].copy_(new)
+        self.dyn_scale[1:2].copy_(good * (1.0 - grow))
+
+    def _bump(self, hyper):
+        """Advance an optimizer's step counter (not on a skipped step)."""
+        if self.mp:
+            hyper[1:2].add_(1.0 - self.found_inf)
+        else:
+            hyper[1:2].add_(1.0)
+
     def _dense_update(self):
         self.loss_sum.add_(self.G[NPARAM:NPARAM + 1].double())
-        self.hyper[1:2].add_(1.0)
+        self._bump(self.hyper)
         ops.dense_optimizer(self.P[:NPARAM], self.G[:NPARAM], self.M, self.V, None,
-                            ops.OPT_ADAMW, self.hyper, wd=self.cfg.weight_decay)
+                            ops.OPT_ADAMW, self.hyper, wd=self.cfg.weight_decay,
+                            found_inf=self.found_inf if self.mp else None)
 
     def _emb_update(self, ids, b_total, grad):
-        self.emb_hyper[1:2].add_(1.0)
+        self._bump(self.emb_hyper)
         offs = self.offsets_full[: self.T * b_total + 1]
         if self.cfg.emb_update == "sparse":
             self.emb.backward_update(ids, offs, self.emb.row_offset, self.T, b_total, grad,
                                      self.out_off, LDX, self.emb_hyper)
         else:
+            # raw (still scaled) dense gradient; the dense AdamW unscales by
+            # hyper[2] and skips on found_inf
             self.emb_grad.zero_()
             self.emb.backward_update(ids, offs, self.emb.row_offset, self.T, b_total, grad,
-                                     self.out_off, LDX, self.emb_hyper, dense_grad=self.emb_grad)
+                                     self.out_off, LDX, self.emb_hyper[:2],
+                                     dense_grad=self.emb_grad)
             ops.dense_optimizer(self.emb.weight.view(-1), self.emb_grad.view(-1),
                                 self.emb_m.view(-1), self.emb_v.view(-1), None, ops.OPT_ADAMW,
-                                self.hyper, wd=self.cfg.weight_decay)
+                                self.hyper, wd=self.cfg.weight_decay,
+                                found_inf=self.found_inf if self.mp else None)
 
     def _step_local(self, b: int):
         self._train_compute(b)
+        self._mp_check([self.G[:NPARAM], self.dX[:b, :112]])
         self._dense_update()
         self._emb_update(self.ids[: self.T * b], b, self.dX[:b])
+        self._mp_update_scale()
 
     def _step_dp(self, b: int):
         assert b == self.B, "data-parallel steps use full batches (drop_last)"
         self._train_compute(b)
         # dense grads + loss: one all-reduce of 2,401 floats
         dist.all_reduce(self.G[: NPARAM + 1], group=self.group)
-        self._dense_update()
         # sparse rows: all-gather (ids, row grads) of the global batch; every
         # rank applies the same deterministic update -> replicas stay equal
         W, T = self.world, self.T
         dist.all_gather_into_tensor(self.g_ids, self.ids[: T * b], group=self.group)
         dist.all_gather_into_tensor(self.g_dX, self.dX[:b], group=self.group)
+        # the finite check sees the global gradients: every rank skips together
+        self._mp_check([self.G[:NPARAM], self.g_dX[:, :112]])
+        self._dense_update()
         # regroup ids rank-major [W][T][b] -> table-major [T][W*b] (bag = t*W*b + r*b + j)
         gid = self.g_ids.view(W, T, b).transpose(0, 1).reshape(-1)
         self._emb_update(gid, W * b, self.g_dX)
+        self._mp_update_scale()
 
     def _step_sharded(self, b: int):
         assert b == self.B, "sharded training steps use full batches (drop_last)"
+        if self.mp:
+            raise NotImplementedError("mixed_precision is the train_dp.py path (replicated "
+                                      "tables), as in the reference")
         self._train_compute(b)
         if self.world > 1:
             dist.all_reduce(self.G[: NPARAM + 1], group=self.group)
@@ -329,7 +391,7 @@ class TwoTowerTrainer:
 
     def _state_tensors(self):
         ts = [self.P, self.M, self.V, self.hyper, self.emb_hyper, self.emb.weight, self.loss_sum,
-              self.train_hist]
+              self.train_hist, self.dyn_scale, self.found_inf]
         for x in (self.emb.state1, self.emb.state2):
             if x is not None:
                 ts.append(x)
@@ -346,7 +408,7 @@ class TwoTowerTrainer:
         if b == 0:
             return self.logits[:0]
         lg = self.logits[:b]
-        ops.two_tower(self.X[:b], self.P, self.labels[:b], 1.0, lg)
+        ops.two_tower(self.X[:b], self.P, self.labels[:b], 1.0, lg, half=self.mp)
         y = self.labels[:b]
         loss = torch.nn.functional.binary_cross_entropy_with_logits(lg, y, reduction="sum")
         self.loss_sum.add_(loss.double())
@@ -419,7 +481,7 @@ class TwoTowerTrainer:
 
     def state_dict(self):
         d = {"P": self.P, "M": self.M, "V": self.V, "hyper": self.hyper,
-             "emb_hyper": self.emb_hyper}
+             "emb_hyper": self.emb_hyper, "dyn_scale": self.dyn_scale}
         if self.sharded is not None:
             for grp, sd in self.sharded.state_dict().items():
                 d.update({f"emb.{grp}.{k}": v for k, v in sd.items()})

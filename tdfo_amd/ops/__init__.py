@@ -385,12 +385,14 @@ def two_tower_parts(B: int) -> int:
     return (B + ref.TT_SPB - 1) // ref.TT_SPB
 
 
-def two_tower(X, P, labels, inv_n, logits, dX=None, part=None):
-    """Fused TwoTower forward (+ BCE + backward when dX/part given)."""
+def two_tower(X, P, labels, inv_n, logits, dX=None, part=None, loss_scale=None, half=False):
+    """Fused TwoTower forward (+ BCE + backward when dX/part given).
+    ``half``: fp16 compute (mixed precision); ``loss_scale``: device scalar
+    multiplying the loss gradient (dynamic loss scaling)."""
     if _gpu(X):
-        _native().two_tower(X, P, labels, float(inv_n), logits, dX, part)
+        _native().two_tower(X, P, labels, float(inv_n), logits, dX, part, loss_scale, bool(half))
     else:
-        ref.two_tower(X, P, labels, inv_n, logits, dX, part)
+        ref.two_tower(X, P, labels, inv_n, logits, dX, part, loss_scale, half)
 
 
 def linear_xent(H, W, bias, labels, eps, ignore, dH, lossv, dW=None, db=None):

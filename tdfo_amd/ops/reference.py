@@ -140,10 +140,14 @@ def embedding_grad_rows(W, row_offset, indices, offsets, grad_off, psw, T, B, me
 def embedding_bwd(W, row_offset, indices, offsets, grad_off, psw, T, B, mean, key_bits, grad,
                   grad_stride, opt, state1, state2, hyper, eps, beta1, beta2, weight_decay,
                   dense_grad):
+    if hyper.numel() > 3 and float(hyper[3]) > 0:          # dynamic loss scale: skipped step
+        return
     rows, g = embedding_grad_rows(W, row_offset, indices, offsets, grad_off, psw, T, B, mean,
                                   grad, grad_stride)
     if rows.numel() == 0:
         return
+    if hyper.numel() > 2:
+        g = g * float(hyper[2])                             # loss-scale unscale
     lr = float(hyper[0])
     w = W[rows]
     if opt == EMB_SGD:
@@ -479,21 +483,24 @@ def two_tower_forward(X, P):
     return (u * iv).sum(1)
 
 
-def two_tower(X, P, labels, inv_n, logits, dX=None, part=None):
+def two_tower(X, P, labels, inv_n, logits, dX=None, part=None, loss_scale=None, half=False):
     """Oracle of tdfo::two_tower via autograd. part rows follow the kernel:
-    one row per 128-sample block, [dP | loss_sum]."""
+    one row per 128-sample block, [dP | loss_sum]. ``half``: the towers run
+    in float16 (autograd through fp16 ops); ``loss_scale`` scales the loss."""
+    dt = torch.float16 if half else torch.float32
     if dX is None:
         with torch.no_grad():
-            logits.copy_(two_tower_forward(X.float(), P.float()))
+            logits.copy_(two_tower_forward(X.float().to(dt), P.float().to(dt)).float())
         return
     B = X.shape[0]
+    ls = float(loss_scale.reshape(-1)[0]) if loss_scale is not None else 1.0
     with torch.enable_grad():
         Xr = X[:, :114].detach().float().clone().requires_grad_(True)
         Pr = P[:TT_NPARAM].detach().float().clone().requires_grad_(True)
-        lg = two_tower_forward(Xr, Pr)
+        lg = two_tower_forward(Xr.to(dt), Pr.to(dt)).float()
         y = labels.float()
         per = torch.nn.functional.binary_cross_entropy_with_logits(lg, y, reduction="none")
-        (per.sum() * inv_n).backward()
+        (per.sum() * (inv_n * ls)).backward()
     logits.copy_(lg.detach())
     dX[:, :112].copy_(Xr.grad[:, :112])
     nparts = (B + TT_SPB - 1) // TT_SPB

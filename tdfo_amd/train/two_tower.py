@@ -80,8 +80,11 @@ def run(cfg: Config, mode: str = "single", flavor: str = "flax", out_dir: str = 
 
     B, EB = cfg.per_device_train_batch_size, cfg.per_device_eval_batch_size
     init = cfg.tower_init or ("keras" if flavor == "keras" else "flax")
+    # mixed_precision is a train_dp.py key in the reference (jax-flax/config.toml:12,
+    # jax-flax/train_dp.py:170-177); the other entrypoints train in fp32
     tcfg = TwoTowerConfig(dict(cfg.size_map), cfg.embed_dim, cfg.learning_rate, cfg.weight_decay,
-                          init=init, emb_update=cfg.emb_update, seed=cfg.seed)
+                          init=init, emb_update=cfg.emb_update, seed=cfg.seed,
+                          mixed_precision=bool(cfg.mixed_precision) and mode == "dp")
     strategy = None
     if mode == "ps":
         strategy = cfg.sharding.strategy if cfg.sharding.strategy != "auto" else "row_wise"

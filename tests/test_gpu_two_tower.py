@@ -86,3 +86,44 @@ def test_two_tower_graph_replay_matches_eager():
     torch.testing.assert_close(a.P, b.P, rtol=0, atol=0)
     torch.testing.assert_close(a.emb.weight, b.emb.weight, rtol=0, atol=0)
     assert a.pop_metrics() == b.pop_metrics()
+
+
+@pytest.mark.parametrize("B", [100, 2048])
+def test_two_tower_kernel_fp16_with_loss_scale(B):
+    """fp16-compute variant (mixed_precision) with a device loss scale vs the
+    float16 autograd oracle (same scale)."""
+    torch.manual_seed(B)
+    X = torch.randn(B, 116, device=DEV) * 0.5
+    P = torch.zeros(ops.TT_NPARAM + 64, device=DEV)
+    P[:ops.TT_NPARAM] = init_dense_params("flax", 1).to(DEV) * 2
+    y = (torch.rand(B, device=DEV) < 0.4).float()
+    inv, scale = 1.0 / B, torch.tensor([1024.0], device=DEV)
+    nparts = ops.two_tower_parts(B)
+    lg, dX = torch.zeros(B, device=DEV), torch.zeros(B, 116, device=DEV)
+    part = torch.zeros(nparts, ops.TT_PART_LD, device=DEV)
+    ops.two_tower(X, P, y, inv, lg, dX, part, loss_scale=scale, half=True)
+    lr_, dXr = torch.zeros(B), torch.zeros(B, 116)
+    partr = torch.zeros(nparts, ops.TT_PART_LD)
+    ref.two_tower(X.cpu(), P.cpu(), y.cpu(), inv, lr_, dXr, partr, scale.cpu(), True)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(lg.cpu(), lr_, rtol=2e-2, atol=2e-2)
+    g, gr = part.sum(0).cpu()[:ops.TT_NPARAM], partr.sum(0)[:ops.TT_NPARAM]
+    assert float((g - gr).norm() / gr.norm()) < 2e-2
+    assert float((dX[:, :112].cpu() - dXr[:, :112]).norm() / dXr[:, :112].norm()) < 2e-2
+
+
+def test_mixed_precision_skip_on_gpu():
+    """The fused embedding kernels honour the skip flag / unscale on device."""
+    from tests.test_two_tower import test_mixed_precision_dynamic_scale_skips_non_finite as t
+    import tdfo_amd.models.two_tower as tt
+
+    orig = tt.TwoTowerTrainer.__init__
+
+    def on_gpu(self, cfg, B, device="cpu", **kw):
+        orig(self, cfg, B, DEV, **kw)
+    tt.TwoTowerTrainer.__init__ = on_gpu
+    try:
+        t("sparse")
+        t("dense")
+    finally:
+        tt.TwoTowerTrainer.__init__ = orig

@@ -176,3 +176,52 @@ def test_two_tower_distributed_matches_single(mode):
         assert abs(o["loss"] - ref["loss"]) < 10 * tol
     if mode == "dp":      # replicas stay identical
         torch.testing.assert_close(outs[0]["P"], outs[1]["P"], rtol=0, atol=0)
+
+
+@pytest.mark.parametrize("emb_update", ["sparse", "dense"])
+def test_mixed_precision_dynamic_scale_skips_non_finite(emb_update):
+    """jax-flax/train_dp.py:55-81: a step with non-finite (scaled) gradients
+    leaves params AND optimizer state untouched, does not advance Adam's step,
+    halves the loss scale; finite steps train and count towards growth."""
+    cfg = TwoTowerConfig(SM, learning_rate=5e-3, emb_update=emb_update, mixed_precision=True,
+                         growth_interval=3)
+    tr = TwoTowerTrainer(cfg, 64, "cpu")
+    tr.load_batch(make_batch(64, 1))
+    tr.step()
+    assert float(tr.dyn_scale[0]) == cfg.init_scale and float(tr.dyn_scale[1]) == 1
+    snap = [t.clone() for t in tr._state_tensors()[:6]] + \
+        [x.clone() for x in (tr.emb.state1, tr.emb.state2) if x is not None]
+    bad = make_batch(64, 2)
+    bad["avg_rating"][5] = float("inf")                   # poisons every dense grad
+    tr.load_batch(bad)
+    tr.step()
+    assert float(tr.found_inf[0]) == 1.0
+    assert float(tr.dyn_scale[0]) == cfg.init_scale / 2 and float(tr.dyn_scale[1]) == 0
+    now = [t for t in tr._state_tensors()[:6]] + \
+        [x for x in (tr.emb.state1, tr.emb.state2) if x is not None]
+    names = ["P", "M", "V", "hyper", "emb_hyper", "emb.weight", "state1", "state2"]
+    for n, a, b in zip(names, snap, now):
+        if n in ("hyper", "emb_hyper"):
+            assert torch.equal(a[:2], b[:2]), n            # lr + step counter unchanged
+        else:
+            assert torch.equal(a, b), n
+    for i in range(4):                                    # finite again: trains, grows at 3
+        tr.load_batch(make_batch(64, 10 + i))
+        tr.step()
+    assert float(tr.found_inf[0]) == 0.0
+    assert float(tr.dyn_scale[0]) == cfg.init_scale       # halved once, doubled once
+    assert not torch.equal(tr.P, snap[0])
+    assert float(tr.hyper[1]) == 5.0                      # 6 steps, 1 skipped
+
+
+def test_mixed_precision_matches_fp32_closely():
+    """fp16 compute with loss scaling trains like fp32 (same data, 20 steps)."""
+    losses = {}
+    for mp in (False, True):
+        cfg = TwoTowerConfig(SM, learning_rate=5e-3, mixed_precision=mp)
+        tr = TwoTowerTrainer(cfg, 128, "cpu")
+        for i in range(20):
+            tr.load_batch(make_batch(128, 100 + i))
+            tr.step()
+        losses[mp] = tr.pop_metrics(reduce=False)[0]
+    assert abs(losses[True] - losses[False]) < 2e-2 * abs(losses[False])
