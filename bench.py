@@ -38,7 +38,7 @@ def parse(argv=None):
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=int(os.environ.get("TDFO_BENCH_BATCH", 8192)),
                     help="per-GPU batch (weak scaling)")
-    ap.add_argument("--rows", default="1tb", choices=["1tb", "kaggle", "tiny"])
+    ap.add_argument("--rows", default="1tb", choices=["1tb", "kaggle", "tiny", "gt1tb"])
     ap.add_argument("--model", default="dlrm", choices=["dlrm", "dcnv2"])
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--overlap", nargs="?", const="all", default="",
@@ -47,6 +47,9 @@ def parse(argv=None):
     ap.add_argument("--dist", default="uniform", choices=["uniform", "zipf"])
     ap.add_argument("--sharding", default="auto",
                     choices=["auto", "table_wise", "row_wise", "column_wise", "data_parallel"])
+    ap.add_argument("--host-data", action="store_true",
+                    help="batches from the C++ host generator through pinned slots and a "
+                         "copy-stream H2D prefetcher (instead of a pool of device batches)")
     return ap.parse_args(argv)
 
 
@@ -104,8 +107,8 @@ def main(argv=None):
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(self_launch(args, argv))
     from tdfo_amd.parallel.dist import init_distributed, reset
-    from tdfo_amd.models.dlrm import (CRITEO_1TB_ROWS, CRITEO_KAGGLE_ROWS, MLPERF_MULTIHOT,
-                                      DLRMConfig, DLRMTrainer)
+    from tdfo_amd.models.dlrm import (CRITEO_1TB_ROWS, CRITEO_KAGGLE_ROWS, DCN_GT1TB_ROWS,
+                                      MLPERF_MULTIHOT, DLRMConfig, DLRMTrainer)
     from tdfo_amd.data.synthetic import SyntheticCriteo
     from tdfo_amd.ops import _ext
 
@@ -119,7 +122,7 @@ def main(argv=None):
     if os.environ.get("TDFO_GEMM_POLICY"):      # override the trainer's per-model choice
         from tdfo_amd import ops
         ops.gemm_policy(int(os.environ["TDFO_GEMM_POLICY"]))
-    rows = {"1tb": CRITEO_1TB_ROWS, "kaggle": CRITEO_KAGGLE_ROWS,
+    rows = {"1tb": CRITEO_1TB_ROWS, "kaggle": CRITEO_KAGGLE_ROWS, "gt1tb": DCN_GT1TB_ROWS,
             "tiny": [1000] * 26}[args.rows]
     if args.model == "dlrm":
         cfg = DLRMConfig(table_rows=list(rows), sharding=args.sharding,
@@ -131,16 +134,27 @@ def main(argv=None):
     B = args.batch
     t0 = time.time()
     tr = DLRMTrainer(cfg, B, info.device, group=info.group, rank=info.rank, world_size=world)
-    data = SyntheticCriteo(cfg.table_rows, B, pooling=cfg.pooling_factors(), device=info.device,
-                           seed=1, rank=info.rank, dist=args.dist)
-    pool = [data.next() for _ in range(args.pool)]
+    if args.host_data:
+        from tdfo_amd.data.prefetch import host_prefetcher
+        pf = host_prefetcher(cfg.table_rows, B, info.device, pooling=cfg.pooling_factors(),
+                             seed=1, rank=info.rank, dist=args.dist, threads=8)
+        pool = None
+    else:
+        data = SyntheticCriteo(cfg.table_rows, B, pooling=cfg.pooling_factors(),
+                               device=info.device, seed=1, rank=info.rank, dist=args.dist)
+        pool = [data.next() for _ in range(args.pool)]
     torch.cuda.synchronize()
     setup_s = time.time() - t0
     use_graph = not args.no_graph
 
     def run(n, start):
         for i in range(n):
-            tr.load_batch(*pool[(start + i) % len(pool)])
+            if pool is None:                   # host data plane: generation + H2D overlapped
+                batch, slot = pf.next()
+                tr.load_batch(*batch)
+                pf.release(slot)
+            else:
+                tr.load_batch(*pool[(start + i) % len(pool)])
             tr.step()
 
     run(args.warmup, 0)
@@ -182,7 +196,9 @@ def main(argv=None):
             "sol_ms": round(sol["sol_ms"], 4),
             "frac_of_sol": round(sol["sol_ms"] / ms, 3),
             "dtype": "bf16",
-            "data": f"synthetic (Criteo-{args.rows}-shaped, {args.dist} ids, random-init embeddings)",
+            "data": f"synthetic (Criteo-{args.rows}-shaped, {args.dist} ids, random-init embeddings"
+                    + (", C++ host generator + pinned copy-stream H2D)" if args.host_data
+                       else ", pre-generated device batches)"),
             "config": {"model": "DLRM" if args.model == "dlrm" else "DCN-v2",
                        "global_batch": B * world, "seq_len": None,
                        "parallelism": parallelism(tr.plan, world),

@@ -33,10 +33,11 @@ class ShardingConfig:
 @dataclass
 class SyntheticConfig:
     enabled: bool = False
-    rows: str = "tiny"                # tiny | kaggle | 1tb | list given in table_rows
+    rows: str = "tiny"                # tiny | kaggle | 1tb | gt1tb | list given in table_rows
     dist: str = "uniform"             # uniform | zipf
     zipf_alpha: float = 1.05
     num_batches: int = 100
+    host_data: bool = False           # GPU: C++ host generator -> pinned -> copy-stream H2D
 
 
 @dataclass

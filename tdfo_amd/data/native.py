@@ -161,6 +161,10 @@ class HostLoader:
             raise ValueError("invalid loader arguments")
         self.epoch = 0
         self.world, self.drop_last = world_size, drop_last
+        # H2D runs on its own stream (the compute stream only waits on an
+        # event), so copies of the next batch overlap the current step
+        self._copy_stream = (torch.cuda.Stream(self.device)
+                             if self.device is not None and self.device.type == "cuda" else None)
 
     def set_epoch(self, epoch: int):
         self.epoch = int(epoch)
@@ -185,12 +189,20 @@ class HostLoader:
                 pending = (slot, None)
                 yield {k: self.slots[slot][i][:r] for i, k in enumerate(self.names)}
             else:
-                out = {k: self.slots[slot][i][:r].to(self.device, non_blocking=True)
-                       for i, k in enumerate(self.names)}
                 ev = None
-                if self.device.type == "cuda":
-                    ev = torch.cuda.Event()
-                    ev.record()
+                if self._copy_stream is not None:
+                    cur = torch.cuda.current_stream(self.device)
+                    with torch.cuda.stream(self._copy_stream):
+                        out = {k: self.slots[slot][i][:r].to(self.device, non_blocking=True)
+                               for i, k in enumerate(self.names)}
+                        ev = torch.cuda.Event()
+                        ev.record(self._copy_stream)
+                    cur.wait_event(ev)
+                    for t in out.values():        # allocated on the copy stream, used on cur
+                        t.record_stream(cur)
+                else:
+                    out = {k: self.slots[slot][i][:r].to(self.device, non_blocking=True)
+                           for i, k in enumerate(self.names)}
                 if pending is not None:
                     if pending[1] is not None:
                         pending[1].synchronize()

@@ -1,0 +1,105 @@
+"""Host -> device input pipeline for the DLRM / DCN-v2 trainers.
+
+The role of the reference's ``prefetch_to_device(size=2)``
+(jax-flax/train_dp.py:210-211) and tf.data's AUTOTUNE prefetch
+(tensorflow2/data.py:171-210): the multi-threaded C++ generator
+(csrc/data/synthetic.cpp, or any host batch source with the same
+``batch(i)`` contract) fills pinned host slots on a background thread,
+``lookahead`` batches ahead; each batch is copied host -> device on a
+dedicated copy stream into one of two device staging slots, and the compute
+stream only waits on that copy's event. The trainer's ``load_batch`` then
+moves staging -> its static (graph-captured) inputs with one fused kernel,
+so the H2D of batch i+1 overlaps step i.
+
+Slot reuse is event-ordered both ways: a host slot is rewritten only after
+the H2D that read it completed (worker thread waits on that event), a
+device staging slot is overwritten only after the consumer's kernels that
+read it were enqueued and ran (copy stream waits on ``release``'s event).
+"""
+from __future__ import annotations
+
+from concurrent.futures import ThreadPoolExecutor
+from typing import Optional, Tuple
+
+import torch
+
+
+class HostPrefetcher:
+    def __init__(self, gen, device, start: int = 0, lookahead: int = 2):
+        """``gen``: host batch source with ``batch(i) -> (dense, ids, label)``
+        writing into pinned buffer set ``i % gen.nbuf`` (needs nbuf > lookahead)."""
+        if gen.nbuf <= lookahead:
+            raise ValueError("host generator needs more buffer sets than the lookahead")
+        self.gen = gen
+        self.dev = torch.device(device)
+        self.cuda = self.dev.type == "cuda"
+        self.L = int(lookahead)
+        self.H = gen.nbuf
+        self.copy = torch.cuda.Stream(self.dev) if self.cuda else None
+        d0, i0, l0 = gen._bufs[0]
+        self.stage = [(torch.empty(d0.shape, dtype=d0.dtype, device=self.dev),
+                       torch.empty(i0.shape, dtype=i0.dtype, device=self.dev),
+                       torch.empty(l0.shape, dtype=l0.dtype, device=self.dev)) for _ in range(2)]
+        self.h2d_ev = [None] * self.H
+        self.use_ev = [None, None]
+        self.pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="tdfo-prefetch")
+        self.futs = {}
+        self.i = int(start)
+        for j in range(self.i, self.i + self.L):
+            self._submit(j)
+
+    def _submit(self, j: int):
+        ev = self.h2d_ev[j % self.H]
+
+        def work():
+            if ev is not None:
+                ev.synchronize()            # the last H2D out of this host slot is done
+            return self.gen.batch(j)
+        self.futs[j] = self.pool.submit(work)
+
+    def next(self) -> Tuple[Tuple[torch.Tensor, torch.Tensor, torch.Tensor], int]:
+        """Device tensors (dense, ids, label) of the next batch (ordered on the
+        current stream) and their staging slot; call ``release(slot)`` once
+        the consumer has enqueued its reads of them."""
+        j = self.i
+        self.i += 1
+        host = self.futs.pop(j).result()
+        s = j & 1
+        dst = self.stage[s]
+        if self.cuda:
+            with torch.cuda.stream(self.copy):
+                if self.use_ev[s] is not None:
+                    self.copy.wait_event(self.use_ev[s])
+                for d, h in zip(dst, host):
+                    d.copy_(h, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(self.copy)
+            self.h2d_ev[j % self.H] = ev
+            torch.cuda.current_stream(self.dev).wait_event(ev)
+        else:
+            for d, h in zip(dst, host):
+                d.copy_(h)
+        self._submit(j + self.L)
+        return dst, s
+
+    def release(self, slot: int):
+        if self.cuda:
+            e = torch.cuda.Event()
+            e.record(torch.cuda.current_stream(self.dev))
+            self.use_ev[slot] = e
+
+    def close(self):
+        self.pool.shutdown(wait=True)
+
+
+def host_prefetcher(table_rows, batch: int, device, pooling=None, seed: int = 0, rank: int = 0,
+                    dist: str = "uniform", zipf_alpha: float = 1.05, threads: int = 4,
+                    start: int = 0, lookahead: int = 2, stream: int = 0,
+                    num_dense: int = 13) -> Optional[HostPrefetcher]:
+    """Prefetcher over the C++ synthetic Criteo generator (pinned host slots)."""
+    from .synthetic import HostSyntheticCriteo
+    cuda = torch.device(device).type == "cuda"
+    gen = HostSyntheticCriteo(table_rows, batch, num_dense, pooling=pooling, seed=seed, dist=dist,
+                              zipf_alpha=zipf_alpha, rank=rank, threads=threads, pin=cuda,
+                              stream=stream, nbuf=lookahead + 1)
+    return HostPrefetcher(gen, device, start=start, lookahead=lookahead)

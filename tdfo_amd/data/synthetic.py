@@ -71,7 +71,9 @@ class HostSyntheticCriteo:
     def __init__(self, table_rows: Sequence[int], batch_size: int, num_dense: int = 13,
                  pooling: Optional[Sequence[int]] = None, seed: int = 0, dist: str = "uniform",
                  zipf_alpha: float = 1.05, rank: int = 0, threads: int = 4, pin: bool = False,
-                 stream: int = 0):
+                 stream: int = 0, nbuf: int = 2):
+        """``nbuf`` output buffer sets; batch ``i`` is written into set
+        ``i % nbuf`` (a prefetcher keeps ``nbuf - 1`` batches in flight)."""
         import numpy as np
         self.rows = np.asarray([int(r) for r in table_rows], dtype=np.int64)
         self.T = len(self.rows)
@@ -89,12 +91,13 @@ class HostSyntheticCriteo:
         self.index = 0
         nnz = int((self.L.astype(np.int64) * self.B).sum())
         mk = (lambda t: t.pin_memory()) if pin else (lambda t: t)
+        self.nbuf = max(1, int(nbuf))
         self._bufs = [(mk(torch.empty(self.B, num_dense)), mk(torch.empty(nnz, dtype=torch.int64)),
-                       mk(torch.empty(self.B))) for _ in range(2)]
+                       mk(torch.empty(self.B))) for _ in range(self.nbuf)]
 
     def batch(self, index: int):
         from .native import lib
-        dense, ids, label = self._bufs[index & 1]
+        dense, ids, label = self._bufs[index % self.nbuf]
         lib().tdfo_synth_criteo(self.seed + self.stream * 1_000_003, self.rank, index, self.B, self.num_dense, self.T,
                                 self.rows.ctypes.data, self.L.ctypes.data, self.dist, self.alpha,
                                 self.w_dense.data_ptr(), self.table_bias.data_ptr(),

@@ -29,8 +29,8 @@ import torch
 from .. import ops
 from ..config import Config
 from ..data.synthetic import HostSyntheticCriteo, SyntheticCriteo
-from ..models.dlrm import (CRITEO_1TB_ROWS, CRITEO_KAGGLE_ROWS, MLPERF_MULTIHOT, DLRMConfig,
-                           DLRMTrainer)
+from ..models.dlrm import (CRITEO_1TB_ROWS, CRITEO_KAGGLE_ROWS, DCN_GT1TB_ROWS, MLPERF_MULTIHOT,
+                           DLRMConfig, DLRMTrainer)
 from ..parallel.dist import init_distributed
 from ..sparse import tables as _tables
 from ..utils import checkpoint as ckpt
@@ -43,8 +43,8 @@ TINY_ROWS = [40_000] * 26          # DLRM-tiny: ~1M embedding rows (BASELINE con
 def table_rows(cfg: Config) -> List[int]:
     if cfg.table_rows:
         return list(cfg.table_rows)
-    return {"tiny": TINY_ROWS, "kaggle": CRITEO_KAGGLE_ROWS,
-            "1tb": CRITEO_1TB_ROWS}[cfg.synthetic.rows]
+    return {"tiny": TINY_ROWS, "kaggle": CRITEO_KAGGLE_ROWS, "1tb": CRITEO_1TB_ROWS,
+            "gt1tb": DCN_GT1TB_ROWS}[cfg.synthetic.rows]
 
 
 def dlrm_config(cfg: Config, strategy: str) -> DLRMConfig:
@@ -60,23 +60,43 @@ def dlrm_config(cfg: Config, strategy: str) -> DLRMConfig:
 
 
 class _Data:
-    """Per-rank synthetic batch stream; batch i is reproducible after resume."""
+    """Per-rank synthetic batch stream; batch i is reproducible after resume.
 
-    def __init__(self, cfg: Config, dcfg: DLRMConfig, B: int, device, rank: int, seed_off: int):
+    CPU: the C++ host generator. GPU: the device generator, or with
+    ``synthetic.host_data`` the C++ generator behind the pinned, copy-stream
+    prefetcher (data/prefetch.py) -- the host data plane a real input
+    pipeline would use."""
+
+    def __init__(self, cfg: Config, dcfg: DLRMConfig, B: int, device, rank: int, seed_off: int,
+                 prefetch: bool = True):
         self.host = device.type == "cpu"
+        self.pf = None
         kw = dict(pooling=dcfg.pooling_factors(), seed=cfg.seed, rank=rank,
                   dist=cfg.synthetic.dist, stream=seed_off)
+        self._args = (cfg, dcfg, B, device, kw)
         if self.host:
             self.gen = HostSyntheticCriteo(dcfg.table_rows, B, dcfg.num_dense,
                                            zipf_alpha=cfg.synthetic.zipf_alpha, threads=4, **kw)
+        elif cfg.synthetic.host_data and prefetch:
+            self.pf = self._prefetcher(0)
         else:
             self.gen = SyntheticCriteo(dcfg.table_rows, B, dcfg.num_dense, device=device,
                                        zipf_alpha=cfg.synthetic.zipf_alpha, **kw)
         self.device = device
         self.i = 0
+        self._slot = None
+
+    def _prefetcher(self, start: int):
+        from ..data.prefetch import host_prefetcher
+        cfg, dcfg, B, device, kw = self._args
+        return host_prefetcher(dcfg.table_rows, B, device, num_dense=dcfg.num_dense,
+                               zipf_alpha=cfg.synthetic.zipf_alpha, start=start, **kw)
 
     def seek(self, i: int):
-        if self.host:
+        if self.pf is not None:
+            self.pf.close()
+            self.pf = self._prefetcher(i)
+        elif self.host:
             self.gen.index = i
         else:                  # device generator: replay the stream
             for _ in range(i - self.i):
@@ -85,6 +105,11 @@ class _Data:
 
     def next(self):
         self.i += 1
+        if self.pf is not None:
+            if self._slot is not None:
+                self.pf.release(self._slot)       # previous batch was consumed
+            batch, self._slot = self.pf.next()
+            return batch
         return self.gen.next()
 
 
@@ -221,7 +246,7 @@ def evaluate(tr: DLRMTrainer, cfg: Config, dcfg: DLRMConfig, B: int, dev, rank: 
     reduced over ranks. Uses the trainer's static buffers, so the current
     training batch is restored afterwards."""
     saved = (tr.x0[:, :dcfg.num_dense].clone(), tr.ids.clone(), tr.label.clone())
-    gen = _Data(cfg, dcfg, B, dev, rank, 7)
+    gen = _Data(cfg, dcfg, B, dev, rank, 7, prefetch=False)
     hist = torch.zeros(2 * 199, dtype=torch.int64, device=dev)
     loss = torch.zeros(2, dtype=torch.float64, device=dev)
     for _ in range(batches):
