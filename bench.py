@@ -137,7 +137,7 @@ def main(argv=None):
     if args.host_data:
         from tdfo_amd.data.prefetch import host_prefetcher
         pf = host_prefetcher(cfg.table_rows, B, info.device, pooling=cfg.pooling_factors(),
-                             seed=1, rank=info.rank, dist=args.dist, threads=12)
+                             seed=1, rank=info.rank, dist=args.dist, threads=8)
         pool = None
     else:
         data = SyntheticCriteo(cfg.table_rows, B, pooling=cfg.pooling_factors(),

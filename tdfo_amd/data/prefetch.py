@@ -11,13 +11,15 @@ stream only waits on that copy's event. The trainer's ``load_batch`` then
 moves staging -> its static (graph-captured) inputs with one fused kernel,
 so the H2D of batch i+1 overlaps step i.
 
-Slot reuse is event-ordered both ways: a host slot is rewritten only after
-the H2D that read it completed (worker thread waits on that event), a
-device staging slot is overwritten only after the consumer's kernels that
-read it were enqueued and ran (copy stream waits on ``release``'s event).
+Slot reuse is event-ordered both ways, checked on the launching thread by
+polling (never by blocking waits that would hold the GIL, never by
+device-side waits that make ROCm's async copy block the host): a host slot
+is rewritten only after the H2D that read it completed, a device staging
+slot is overwritten only after the consumer's kernels that read it ran.
 """
 from __future__ import annotations
 
+import time
 from concurrent.futures import ThreadPoolExecutor
 from typing import Optional, Tuple
 
@@ -25,37 +27,43 @@ import torch
 
 
 class HostPrefetcher:
-    def __init__(self, gen, device, start: int = 0, lookahead: int = 2):
+    def __init__(self, gen, device, start: int = 0, lookahead: int = 2, stages: int = 6):
         """``gen``: host batch source with ``batch(i) -> (dense, ids, label)``
-        writing into pinned buffer set ``i % gen.nbuf`` (needs nbuf > lookahead)."""
-        if gen.nbuf <= lookahead:
-            raise ValueError("host generator needs more buffer sets than the lookahead")
+        writing into pinned buffer set ``i % gen.nbuf`` (needs nbuf >=
+        lookahead + 2). ``stages`` device staging slots."""
+        if gen.nbuf < lookahead + 2:
+            raise ValueError("host generator needs >= lookahead + 2 buffer sets")
         self.gen = gen
         self.dev = torch.device(device)
         self.cuda = self.dev.type == "cuda"
         self.L = int(lookahead)
         self.H = gen.nbuf
+        self.S = int(stages)
         self.copy = torch.cuda.Stream(self.dev) if self.cuda else None
         d0, i0, l0 = gen._bufs[0]
         self.stage = [(torch.empty(d0.shape, dtype=d0.dtype, device=self.dev),
                        torch.empty(i0.shape, dtype=i0.dtype, device=self.dev),
-                       torch.empty(l0.shape, dtype=l0.dtype, device=self.dev)) for _ in range(2)]
+                       torch.empty(l0.shape, dtype=l0.dtype, device=self.dev))
+                      for _ in range(self.S)]
         self.h2d_ev = [None] * self.H
-        self.use_ev = [None, None]
+        self.use_ev = [None] * self.S
         self.pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="tdfo-prefetch")
         self.futs = {}
+        self.t_wait_gen = self.t_submit = 0.0      # host seconds blocked (diagnostics)
         self.i = int(start)
         for j in range(self.i, self.i + self.L):
             self._submit(j)
 
     def _submit(self, j: int):
+        # host slot j % H was last read by the H2D of batch j - H; with H >=
+        # L + 2 that copy was issued >= 2 steps ago, so this wait (on the
+        # launching thread, never inside the worker: a worker blocking in
+        # Event.synchronize() holds the GIL the launching thread needs) is
+        # back-pressure only when the GPU falls that far behind
         ev = self.h2d_ev[j % self.H]
-
-        def work():
-            if ev is not None:
-                ev.synchronize()            # the last H2D out of this host slot is done
-            return self.gen.batch(j)
-        self.futs[j] = self.pool.submit(work)
+        while ev is not None and not ev.query():
+            time.sleep(20e-6)       # poll: a spinning hipEventSynchronize steals a core
+        self.futs[j] = self.pool.submit(self.gen.batch, j)   # ctypes: GIL released
 
     def next(self) -> Tuple[Tuple[torch.Tensor, torch.Tensor, torch.Tensor], int]:
         """Device tensors (dense, ids, label) of the next batch (ordered on the
@@ -63,13 +71,21 @@ class HostPrefetcher:
         the consumer has enqueued its reads of them."""
         j = self.i
         self.i += 1
+        t0 = time.perf_counter()
         host = self.futs.pop(j).result()
-        s = j & 1
+        self.t_wait_gen += time.perf_counter() - t0
+        s = j % self.S
         dst = self.stage[s]
         if self.cuda:
+            # staging slot s was last read by batch j - S's load; check that on
+            # the host (a device-side wait on the copy stream makes ROCm's
+            # hipMemcpyAsync block the launching thread until the GPU gets
+            # there: measured 0.5 ms per step). With S above the depth the
+            # launching thread runs ahead, this poll only bites as back-pressure.
+            ue = self.use_ev[s]
+            while ue is not None and not ue.query():
+                time.sleep(20e-6)
             with torch.cuda.stream(self.copy):
-                if self.use_ev[s] is not None:
-                    self.copy.wait_event(self.use_ev[s])
                 for d, h in zip(dst, host):
                     d.copy_(h, non_blocking=True)
                 ev = torch.cuda.Event()
@@ -79,7 +95,9 @@ class HostPrefetcher:
         else:
             for d, h in zip(dst, host):
                 d.copy_(h)
+        t1 = time.perf_counter()
         self._submit(j + self.L)
+        self.t_submit += time.perf_counter() - t1
         return dst, s
 
     def release(self, slot: int):
@@ -101,5 +119,5 @@ def host_prefetcher(table_rows, batch: int, device, pooling=None, seed: int = 0,
     cuda = torch.device(device).type == "cuda"
     gen = HostSyntheticCriteo(table_rows, batch, num_dense, pooling=pooling, seed=seed, dist=dist,
                               zipf_alpha=zipf_alpha, rank=rank, threads=threads, pin=cuda,
-                              stream=stream, nbuf=lookahead + 1)
+                              stream=stream, nbuf=lookahead + 4)
     return HostPrefetcher(gen, device, start=start, lookahead=lookahead)
