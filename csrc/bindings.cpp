@@ -40,7 +40,8 @@ void gemm(const Tensor& a_in, bool a_col, const Tensor& b_in, bool b_col,
           const c10::optional<Tensor>& bias, bool relu,
           const c10::optional<Tensor>& mask, const c10::optional<Tensor>& out,
           const c10::optional<Tensor>& out32, int64_t splits, const c10::optional<Tensor>& mul,
-          const c10::optional<Tensor>& add, const c10::optional<Tensor>& out2) {
+          const c10::optional<Tensor>& add, const c10::optional<Tensor>& out2, int64_t ldc32,
+          int64_t csum_col) {
   check_dev(a_in, "a"); check_dev(b_in, "b");
   check_2d_rowmajor(a_in, "a"); check_2d_rowmajor(b_in, "b");
   const int64_t Ka = a_col ? a_in.size(0) : a_in.size(1);
@@ -94,9 +95,18 @@ void gemm(const Tensor& a_in, bool a_col, const Tensor& b_in, bool b_col,
   }
   if (out32) {
     TORCH_CHECK(out32->scalar_type() == at::kFloat && out32->is_contiguous(), "gemm: out32 fp32 contiguous");
-    TORCH_CHECK(out32->numel() >= splits * M * N, "gemm: out32 too small");
-    g.C32 = out32->data_ptr<float>(); g.ldc32 = N;
+    // ldc32: row pitch of each [M, ldc32] split slab (>= N; 0 = N)
+    const int64_t ld32 = ldc32 > 0 ? ldc32 : N;
+    TORCH_CHECK(ld32 >= N && ld32 % 4 == 0, "gemm: ldc32 must be >= N and a multiple of 4");
+    TORCH_CHECK(out32->numel() >= splits * M * ld32, "gemm: out32 too small");
+    g.C32 = out32->data_ptr<float>(); g.ldc32 = ld32;
+    if (csum_col >= 0) {
+      TORCH_CHECK(a_col && csum_col >= N && csum_col < ld32,
+                  "gemm: csum_col needs a col-layout A and N <= csum_col < ldc32");
+      g.csum_on = 1; g.csum_col = (int)csum_col;
+    }
   }
+  TORCH_CHECK(csum_col < 0 || out32, "gemm: csum_col needs out32");
   auto check_mn = [&](const c10::optional<Tensor>& t, const char* name) {
     check_2d_rowmajor(*t, name);
     TORCH_CHECK(t->size(0) == M && t->size(1) == N && t->stride(0) % 8 == 0 &&
@@ -937,7 +947,7 @@ void jagged_ids_to_dense(const Tensor& values, const Tensor& offsets, int64_t pa
 TORCH_LIBRARY(tdfo, m) {
   m.def("gemm(Tensor a, bool a_col, Tensor b, bool b_col, Tensor? bias, bool relu, Tensor? mask, "
         "Tensor(a!)? out, Tensor(b!)? out32, int splits, Tensor? mul=None, Tensor? add=None, "
-        "Tensor(c!)? out2=None) -> ()");
+        "Tensor(c!)? out2=None, int ldc32=0, int csum_col=-1) -> ()");
   m.def("radix_sort_sep_hist(int v) -> int",
         [](int64_t v) { return (int64_t)tdfo::radix_sort_sep_hist((int)v); });
   m.def("radix_sort_max_bits(int b) -> int",

@@ -29,6 +29,12 @@ struct GemmArgs {
   const uint16_t* mul; int64_t ldmul;
   const uint16_t* add; int64_t ldadd;
   uint16_t* C2; int64_t ldc2;
+  // csum_on (col-layout A, fp32 C32 output): each split also writes the sum
+  // over its K range of A's column m (= sum_k A[k][m]) into C32 row m, column
+  // csum_col (>= N, so the GEMM tile never writes it). The weight-grad GEMM
+  // uses it for the bias gradient (sum over the batch of dy), which lets the
+  // GEMM's N stay at the 128-aligned input width.
+  int csum_on, csum_col;
   int abl;   // perf-ablation bits (0 in production): 1 skip A loads, 2 skip B loads, 4 skip all in-loop loads
 };
 void gemm_bf16(const GemmArgs& a, hipStream_t s);

@@ -398,9 +398,17 @@ __device__ __forceinline__ void epilogue(const GemmArgs& p, const f32x4_t (&acc)
 // 16 MFMAs of one 64-deep K step for a wave's 64x64 sub-tile (two 32-deep
 // halves). ta/tb: 16-KiB images holding the wave's A rows / B cols at
 // a_r0 / b_c0.
-template <bool A_COL, bool B_COL, int MI = 4>
+// CS (col-layout A only): running column sums of A, as one extra MFMA per
+// fragment pair against an all-ones B fragment -- the sum over the
+// fragment's 32 k of row 16 i + (l & 15) lands in every register of the
+// lane. The two waves of a row pair (cs_par = wc) take alternate fragments,
+// picked with a select so the MFMA stream has no branches. VALU sums of the
+// unpacked bf16 cost ~4x the MFMA time of the waves that carry them
+// (measured: bot/top3 wgrads 13 vs 10 us).
+template <bool A_COL, bool B_COL, int MI = 4, bool CS = false>
 __device__ __forceinline__ void mfma_k64(f32x4_t (&acc)[MI][4], const TDFO_LDS char* ta,
-                                         int a_r0, const TDFO_LDS char* tb, int b_c0, int lane) {
+                                         int a_r0, const TDFO_LDS char* tb, int b_c0, int lane,
+                                         f32x4_t* cs = nullptr, int cs_par = 0) {
 #pragma unroll
   for (int ks = 0; ks < 2; ++ks) {
     bf16x8_t af[MI], bfr[4];
@@ -415,8 +423,35 @@ __device__ __forceinline__ void mfma_k64(f32x4_t (&acc)[MI][4], const TDFO_LDS c
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    if constexpr (A_COL && CS) {
+      const bf16x8_t ones = __builtin_bit_cast(
+          bf16x8_t, (s16x8_t){0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80});
+#pragma unroll
+      for (int h = 0; h < MI / 2; ++h) {
+        const bf16x8_t a = cs_par ? af[2 * h + 1] : af[2 * h];
+        cs[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, a, cs[h], 0, 0, 0);
+      }
+    }
   }
 }
+
+// Store this wave's column sums (fragments 2 h + cs_par) into this split's
+// fp32 slab, column csum_col of rows a_m0 + 16 (2 h + cs_par) + (l & 15).
+template <int MI>
+__device__ __forceinline__ void csum_store(const GemmArgs& p, const f32x4_t (&cs)[MI / 2],
+                                           int a_m0, int lane, int split, int cs_par) {
+  float* c32 = p.C32 + (int64_t)split * p.M * p.ldc32;
+#pragma unroll
+  for (int h = 0; h < MI / 2; ++h) {
+    const int m = a_m0 + (2 * h + cs_par) * 16 + (lane & 15);
+    if (lane < 16 && m < p.M) c32[(int64_t)m * p.ldc32 + p.csum_col] = cs[h][0];
+  }
+}
+
+template <bool B>
+struct BoolC {
+  static constexpr bool value = B;
+};
 
 // ---------------------------------------------------------------------------
 // Small-tile kernel: BMT x 128 x 64 (BMT = 128, or 64 for row-layout A when
@@ -463,17 +498,35 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs p) {
     else       stage_row(p.B, p.ldb, n0, p.N, k0, tb, w, lane);
   };
 
-  if (kt0 < kt1) {
-    stage(0, kt0);
-    __syncthreads();
-    int cur = 0;
-    for (int kt = kt0; kt < kt1; ++kt) {
-      if (kt + 1 < kt1) stage(cur ^ 1, kt + 1);
-      const TDFO_LDS char* ta = smem + cur * ST;
-      mfma_k64<A_COL, B_COL, MI>(acc, ta, wr * (BMT / 2), ta + A_BYTES, wc * 64, lane);
+  // column sums of A (bias gradient) in the first column tile's blocks,
+  // whose waves already hold every A fragment of their rows; the loop is
+  // instantiated with and without them (block-uniform branch outside it)
+  const bool csum = A_COL && p.csum_on && ti.tn == 0;
+  const int cs_par = __builtin_amdgcn_readfirstlane(wc);
+  f32x4_t cs[MI / 2];
+#pragma unroll
+  for (int h = 0; h < MI / 2; ++h) cs[h] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  auto kloop = [&](auto cs_on) {
+    constexpr bool CS = decltype(cs_on)::value;
+    if (kt0 < kt1) {
+      stage(0, kt0);
       __syncthreads();
-      cur ^= 1;
+      int cur = 0;
+      for (int kt = kt0; kt < kt1; ++kt) {
+        if (kt + 1 < kt1) stage(cur ^ 1, kt + 1);
+        const TDFO_LDS char* ta = smem + cur * ST;
+        mfma_k64<A_COL, B_COL, MI, CS>(acc, ta, wr * (BMT / 2), ta + A_BYTES, wc * 64, lane, cs,
+                                       cs_par);
+        __syncthreads();
+        cur ^= 1;
+      }
     }
+  };
+  if (csum) {
+    kloop(BoolC<true>{});
+    csum_store<MI>(p, cs, m0 + wr * (BMT / 2), lane, ti.split, cs_par);
+  } else {
+    kloop(BoolC<false>{});
   }
   epilogue<BMT, 256, MI>(p, acc, smem_raw, m0, n0, wr, wc, lane, tid, ti.split);
 }
@@ -669,17 +722,20 @@ void launch(const GemmArgs& a, hipStream_t s) {
                      g_policy == 21 || g_policy == 22;
   bool big = (g_policy >= 2 && g_policy != 3 && g_policy != 4 && !autop) ||
              (g_policy == 4 && AC) || (autop && small_tiles * a.splits >= 1024);
+  // the A column sums are produced by the 128x128 kernel only
+  const bool small_only = a.csum_on != 0;
+  if (small_only) big = false;
   // policy 20: the 4-wave 128x64-per-wave kernel for every GEMM; 21: auto
   // with it in place of the 8-wave kernel; 22: auto with it for every GEMM
   // that fills >= 128 CUs with 256x128 tiles
-  if (g_policy == 20 || (g_policy == 22 && big_tiles * a.splits >= 128)) {
+  if (!small_only && (g_policy == 20 || (g_policy == 22 && big_tiles * a.splits >= 128))) {
     b.abl = 0;
     dim3 grid(big_tiles * a.splits);
     hipLaunchKernelGGL((gemm_big_kernel<AC, BC, 8>), grid, dim3(256), LSMEM, s, b);
     TDFO_CHECK_HIP(hipGetLastError());
     return;
   }
-  if (g_policy == 21 && small_tiles * a.splits >= 1024) {
+  if (!small_only && g_policy == 21 && small_tiles * a.splits >= 1024) {
     dim3 grid(big_tiles * a.splits);
     hipLaunchKernelGGL((gemm_big_kernel<AC, BC, 8>), grid, dim3(256), LSMEM, s, b);
     TDFO_CHECK_HIP(hipGetLastError());

@@ -188,11 +188,18 @@ class Lin:
         return self.bcol < self.in_k
 
 
+# Row pitch added past in_k when the bias column cannot ride in the K padding:
+# 64 elements keeps every activation / weight row 128-B aligned, so each 128-B
+# K chunk a GEMM stages is one cache line (an 8-element pad made 7 of 8 rows
+# straddle two lines: top1 fwd 28.2 vs 23.5 us, profiles/gemm_step_ab.md).
+WCOL_PAD = int(os.environ.get("TDFO_WCOL_PAD", "64"))
+
+
 def make_lin(name: str, in_real: int, out: int) -> Lin:
     in_k = pad64(in_real)
     if in_real < in_k:
         return Lin(name, in_real, in_k, out, in_real, in_k)
-    return Lin(name, in_real, in_k, out, in_k, in_k + 8)
+    return Lin(name, in_real, in_k, out, in_k, in_k + WCOL_PAD)
 
 
 class DLRMTrainer:
@@ -303,25 +310,37 @@ class DLRMTrainer:
         self.nparts = ops.head_parts(B)
         self.head_part = z(self.nparts * (self.head_k + 2), dt=torch.float32)
         self.loss_sum = z(1, dt=torch.float32)
+        # split-K block target and bias-grad form of the weight grads, measured
+        # per workload on MI355X (scripts/wgrad_sweep.sh, dcn_wgrad_ab.sh):
+        # DLRM-1TB 0.585 ms/step with column sums at 512 blocks vs 0.599 with
+        # the bias column in N at 256; DCN-v2 (256x128 tiles) 2.876 ms with the
+        # bias column at 256 vs 2.897 with column sums, 2.985-2.999 at 512.
+        dcn = cfg.interaction == "dcn"
+        self._wg_target = int(os.environ.get("TDFO_WGRAD_TARGET", 256 if dcn else 512))
+        # TDFO_WGRAD_CSUM=0/1 overrides (A/B)
+        self._csum = os.environ.get("TDFO_WGRAD_CSUM", "0" if dcn else "1") != "0"
         max_slab = 1
-        for L in self.bottom_layers + self.top_layers + self.dcn_u:
-            max_slab = max(max_slab, ops.wgrad_splits(L.out, L.wcols, B) * L.out * L.wcols)
-        if cfg.interaction == "dcn":
-            s_ = ops.wgrad_splits(cfg.dcn_rank, self.top_real, B)
+        if dcn:
+            s_ = ops.wgrad_splits(cfg.dcn_rank, self.top_real, B, self._wg_target)
             max_slab = max(max_slab, s_ * cfg.dcn_rank * self.top_real)
         self.slab = z(max_slab, dt=torch.float32)
-        # One process on a GPU: each MLP layer's split-K weight-grad partials
-        # get their own slab and are summed inside the fused optimizer pass
-        # (no reduce launch per layer). With >1 rank the grads are reduced
-        # first because the all-reduce needs them.
+        # Weight grads of the augmented layers: the GEMM's N is the 64-aligned
+        # input width in_k and the bias column (when it is past in_k) comes
+        # from the same kernel's column sums of dy (csum), so N tiles evenly
+        # (top1: 64 tiles x 8 splits instead of 72 x 4). Each layer's split-K
+        # partials get their own zero-initialised slab [S][out][wcols]: one
+        # process on a GPU sums them inside the fused optimizer pass (no
+        # reduce launch per layer); with >1 rank they are reduced first
+        # because the all-reduce needs the grads.
         self.wslab = {}
         self._segments = []
-        if dev.type == "cuda" and world_size == 1:
-            for L in self.bottom_layers + self.top_layers:
-                S = ops.wgrad_splits(L.out, L.wcols, B)
-                if S > 1:
-                    sl = z(S * L.out * L.wcols, dt=torch.float32)
-                    self.wslab[L.name] = (sl, S)
+        self._opt_sums_slabs = dev.type == "cuda" and world_size == 1
+        for L in self.bottom_layers + self.top_layers + self.dcn_u:
+            S = ops.wgrad_splits(L.out, self._wgrad_n(L), B, self._wg_target)
+            if S > 1:
+                sl = z(S * L.out * L.wcols, dt=torch.float32)
+                self.wslab[L.name] = (sl, S)
+                if self._opt_sums_slabs:
                     self._segments.append((fp.offset(L.name + ".w"), sl, S))
         self.dense_hyper = torch.tensor([cfg.dense_lr, 0.0, 1.0], dtype=torch.float32, device=dev)
         self.emb_hyper = torch.tensor([cfg.emb_lr, 0.0], dtype=torch.float32, device=dev)
@@ -413,12 +432,25 @@ class DLRMTrainer:
             wgrad()
         self._dgrad(L, x, dy, dx, x_is_relu)
 
+    def _wgrad_n(self, L: Lin) -> int:
+        return L.in_k if self._csum else L.wcols
+
     def _wgrad(self, L: Lin, x, dy):
-        if L.name in self.wslab:              # partials only; summed by the optimizer
+        """dW[:, :in_k] = dy^T x[:, :in_k]; db (column bcol) = colsum(dy) from
+        the same GEMM when the bias is not inside K."""
+        n = self._wgrad_n(L)
+        csum = -1 if (L.bias_in_k or not self._csum) else L.bcol
+        g = self.fp.grad(L.name + ".w").view(-1)
+        if L.name in self.wslab:
             sl, S = self.wslab[L.name]
-            ops.gemm(dy, True, x, True, None, False, None, None, sl, S)
+            ops.gemm(dy, True, x[:, :n], True, None, False, None, None, sl, S,
+                     ldc32=L.wcols, csum_col=csum)
+            if not self._opt_sums_slabs:      # else: partials summed by the optimizer
+                n = L.out * L.wcols
+                ops.reduce_rows(sl, S, n, n, g, False, 1.0)
         else:
-            ops.linear_wgrad(dy, x, self.fp.grad(L.name + ".w").view(-1), slab=self.slab)
+            ops.gemm(dy, True, x[:, :n], True, None, False, None, None, g, 1,
+                     ldc32=L.wcols, csum_col=csum)
 
     def _dgrad(self, L: Lin, x, dy, dx, x_is_relu):
         if dx is not None:
@@ -630,12 +662,12 @@ class DLRMTrainer:
             dxo = self.dcn_dx[i + 1]
             # dy = dxo * x0 ; acc (+)= dxo * y (+ dxo at i == 0: x_0's residual)
             ops.cross_bwd(dxo, x0, self.dcn_y[i], self.dcn_dy, acc, i != Lc - 1, i == 0)
-            ops.linear_wgrad(self.dcn_dy, self.dcn_h[i], fp.grad(u.name + ".w").view(-1),
-                             slab=self.slab)
+            self._wgrad(u, self.dcn_h[i], self.dcn_dy)
             Uw = fp.bf16(u.name + ".w")
             ops.gemm(self.dcn_dy, False, Uw[:, :u.in_k], True, None, False, None, self.dcn_dh,
                      None, 1)
             ops.linear_wgrad(self.dcn_dh, self.dcn_x[i][:, :Wd], fp.grad(f"dcn{i}.v").view(-1),
+                             splits=ops.wgrad_splits(cfg.dcn_rank, Wd, self.B, self._wg_target),
                              slab=self.slab)
             # dx_i = dh V + (i > 0 ? dxo : acc)
             ops.gemm(self.dcn_dh, False, fp.bf16(f"dcn{i}.v"), True, None, False, None, None, None,

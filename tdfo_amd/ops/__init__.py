@@ -20,11 +20,16 @@ def _gpu(t: torch.Tensor) -> bool:
 
 
 def gemm(a, a_col, b, b_col, bias=None, relu=False, mask=None, out=None, out32=None, splits=1,
-         mul=None, add=None, out2=None):
+         mul=None, add=None, out2=None, ldc32=0, csum_col=-1):
+    """C = A B (+ epilogue). out32: fp32 split-K slabs [splits][M][ldc32]
+    (ldc32 0 = N); csum_col >= 0 (col-layout A): each slab's column csum_col
+    also gets the sum over that split's K range of A's column m."""
     if _gpu(a):
-        _native().gemm(a, a_col, b, b_col, bias, relu, mask, out, out32, splits, mul, add, out2)
+        _native().gemm(a, a_col, b, b_col, bias, relu, mask, out, out32, splits, mul, add, out2,
+                       ldc32, csum_col)
     else:
-        ref.gemm(a, a_col, b, b_col, bias, relu, mask, out, out32, splits, mul, add, out2)
+        ref.gemm(a, a_col, b, b_col, bias, relu, mask, out, out32, splits, mul, add, out2,
+                 ldc32, csum_col)
 
 
 def gemm_policy(p: int = -1) -> int:
@@ -90,10 +95,12 @@ def linear_dgrad(dy, w, mask=None, out=None):
     return out
 
 
-# split-K block target for weight grads. In-step A/B (XCD-remapped split-K,
+# split-K block target for weight grads (DLRMTrainer passes its own per
+# workload: profiles/gemm_step_ab.md). Round-1 in-step A/B (XCD-remapped split-K,
 # direct fp32 slab stores): DLRM 0.621 ms at 256 vs 0.636-0.641 at 512, 0.646
 # at 1024, 0.670 at 128; DCN-v2 2.902 vs 3.003 (512), 3.200 (128).
-_WGRAD_TARGET = int(__import__("os").environ.get("TDFO_WGRAD_TARGET", "256"))
+_WGRAD_TARGET = int(__import__("os").environ.get("TDFO_WGRAD_TARGET", "512"))
+_WGRAD_MINKT = int(__import__("os").environ.get("TDFO_WGRAD_MINKT", "8"))
 
 
 def wgrad_splits(M: int, N: int, K: int, target_blocks: int = 0) -> int:
@@ -103,7 +110,7 @@ def wgrad_splits(M: int, N: int, K: int, target_blocks: int = 0) -> int:
     target_blocks = target_blocks or _WGRAD_TARGET
     tiles = ((M + 127) // 128) * ((N + 127) // 128)
     kt = K // 64
-    s = max(1, min(max(1, kt // 8), -(-target_blocks // tiles)))
+    s = max(1, min(max(1, kt // _WGRAD_MINKT), -(-target_blocks // tiles)))
     return s
 
 

@@ -20,7 +20,7 @@ def _f(t: torch.Tensor) -> torch.Tensor:
 
 
 def gemm(a, a_col, b, b_col, bias=None, relu=False, mask=None, out=None, out32=None, splits=1,
-         mul=None, add=None, out2=None):
+         mul=None, add=None, out2=None, ldc32=0, csum_col=-1):
     A = _f(a).t() if a_col else _f(a)          # [M, K]
     Bm = _f(b) if b_col else _f(b).t()         # [K, N]
     c = A @ Bm
@@ -39,11 +39,14 @@ def gemm(a, a_col, b, b_col, bias=None, relu=False, mask=None, out=None, out32=N
         out2.copy_(c2.to(out2.dtype))
     if out32 is not None:
         M, N = c.shape
+        ld = ldc32 or N
         # split-K semantics: slice 0 holds the full sum, other slices zero
-        flat = out32.view(-1)
-        flat[: M * N].copy_(c.reshape(-1))
-        if splits > 1:
-            flat[M * N: splits * M * N].zero_()
+        sl = out32.view(-1)[: splits * M * ld].view(splits, M, ld)
+        sl[0, :, :N].copy_(c)
+        sl[1:, :, :N].zero_()
+        if csum_col >= 0:                      # column sums of A (bias grads)
+            sl[0, :, csum_col].copy_(A.sum(1))
+            sl[1:, :, csum_col].zero_()
 
 
 def interaction_fwd(dense, emb, off, stride, F, D, out, ones_col=-1):

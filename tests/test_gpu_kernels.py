@@ -88,6 +88,27 @@ def test_gemm_epilogue_bias_relu_mask(gemm_pol):
     assert rel_err(out, exp) < 1e-2
 
 
+@pytest.mark.parametrize("M,N,K,S", [(1024, 1024, 8192, 8), (128, 256, 8192, 16),
+                                     (200, 64, 640, 1), (512, 320, 4096, 3)])
+def test_gemm_wgrad_pitched_slabs_with_colsum(M, N, K, S, gemm_pol):
+    """Weight-grad GEMM into [S][M][ldc32] slabs with the A column sums (the
+    bias gradient) in column csum_col; the pad columns stay untouched."""
+    torch.manual_seed(3)
+    ld = N + 64
+    dy = bf(torch.randn(K, M, device=DEV))
+    x = bf(torch.randn(K, N + 64, device=DEV))
+    slab = torch.full((S * M * ld,), 7.0, device=DEV)
+    ops.gemm(dy, True, x[:, :N], True, None, False, None, None, slab, S, ldc32=ld, csum_col=N)
+    sl = slab.view(S, M, ld)
+    exp = dy.float().t() @ x[:, :N].float()
+    assert rel_err(sl[:, :, :N].sum(0), exp) < 1e-4
+    assert rel_err(sl[:, :, N].sum(0), dy.float().sum(0)) < 1e-4
+    assert torch.all(sl[:, :, N + 1:] == 7.0)
+    exp_s = torch.full((S * M * ld,), 7.0, device=DEV)
+    ref.gemm(dy, True, x[:, :N], True, None, False, None, None, exp_s, S, ldc32=ld, csum_col=N)
+    assert rel_err(exp_s.view(S, M, ld)[:, :, :N + 1].sum(0), sl[:, :, :N + 1].sum(0)) < 1e-4
+
+
 def test_gemm_strided_out_and_splitk(gemm_pol):
     torch.manual_seed(2)
     M, N, K = 256, 512, 8192
