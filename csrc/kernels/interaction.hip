@@ -61,26 +61,33 @@ __global__ __launch_bounds__(256) void inter_fwd_kernel(
   for (int e = D + P + lane; e < ldo; e += 64) row[e] = e == ones_col ? (uint16_t)0x3f80 : 0;
 
   const int i = lane & 31, h = lane >> 5;
+  constexpr int PC = (D / 8 + 63) / 64;
+  // each wave walks several samples; sample n+1's feature rows are loaded
+  // into a second register set while sample n's MFMAs, LDS packing and
+  // stores run, so the HBM round trip overlaps the previous sample's work
+  auto load = [&](int b, bf16x8_t (&fr)[KS], s16x8_t (&pv)[PC]) {
+    const uint16_t* rp = feat_row(dense, ld_dense, emb, sm, i, F, b);
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      if (rp) fr[s] = *(const bf16x8_t*)(rp + 16 * s + 8 * h);
+      else    fr[s] = __builtin_bit_cast(bf16x8_t, (s16x8_t){0,0,0,0,0,0,0,0});
+    }
+    // dense passthrough chunk, loaded with the feature rows
+    const uint16_t* dp = dense + (int64_t)b * ld_dense;
+#pragma unroll
+    for (int k = 0; k < PC; ++k)
+      if (lane + 64 * k < D / 8) pv[k] = *(const s16x8_t*)(dp + (lane + 64 * k) * 8);
+  };
   const int iters = (B + gridDim.x * WAVES - 1) / (gridDim.x * WAVES);
+  bf16x8_t fr[KS], frn[KS];
+  s16x8_t pv[PC], pvn[PC];
+  int b = blockIdx.x * WAVES + w;
+  if (b < B) load(b, fr, pv);
   for (int it = 0; it < iters; ++it) {
-    const int b = (it * gridDim.x + blockIdx.x) * WAVES + w;
     const bool valid = b < B;
+    const int bn = b + gridDim.x * WAVES;
+    if (it + 1 < iters && bn < B) load(bn, frn, pvn);
     if (valid) {
-      const uint16_t* rp = feat_row(dense, ld_dense, emb, sm, i, F, b);
-      bf16x8_t fr[KS];
-#pragma unroll
-      for (int s = 0; s < KS; ++s) {
-        if (rp) fr[s] = *(const bf16x8_t*)(rp + 16 * s + 8 * h);
-        else    fr[s] = __builtin_bit_cast(bf16x8_t, (s16x8_t){0,0,0,0,0,0,0,0});
-      }
-      // dense passthrough chunk, loaded with the feature rows (one HBM
-      // round trip per sample)
-      const uint16_t* dp = dense + (int64_t)b * ld_dense;
-      constexpr int PC = (D / 8 + 63) / 64;
-      s16x8_t pv[PC];
-#pragma unroll
-      for (int k = 0; k < PC; ++k)
-        if (lane + 64 * k < D / 8) pv[k] = *(const s16x8_t*)(dp + (lane + 64 * k) * 8);
       f32x16_t acc = {};
 #pragma unroll
       for (int s = 0; s < KS; ++s)
@@ -102,6 +109,11 @@ __global__ __launch_bounds__(256) void inter_fwd_kernel(
         *(uint4*)(op + c * 8) = *(const uint4*)(row + c * 8);
     }
     wave_sync();
+#pragma unroll
+    for (int s = 0; s < KS; ++s) fr[s] = frn[s];
+#pragma unroll
+    for (int k = 0; k < PC; ++k) pv[k] = pvn[k];
+    b = bn;
   }
 }
 
@@ -148,29 +160,41 @@ __global__ __launch_bounds__(256) void inter_bwd_kernel(
     if (j >= F) *(uint4*)(xs + c * 16) = make_uint4(0, 0, 0, 0);
   }
 
-  const int iters = (B + gridDim.x * WAVES - 1) / (gridDim.x * WAVES);
-  for (int it = 0; it < iters; ++it) {
-    const int b = (it * gridDim.x + blockIdx.x) * WAVES + w;
-    const bool valid = b < B;
-    if (valid) {
-      // every X chunk load is issued before the first LDS write, so the
-      // sample costs one HBM round trip instead of one per 64-chunk pass
-      // (each wave owns ~1 sample: the kernel is latency-bound otherwise)
-      s16x8_t xv[XC];
+  // each wave walks several samples: sample n+1's X rows and dZ row are
+  // loaded into registers right after sample n's went to LDS, so the HBM
+  // round trip overlaps sample n's MFMAs and gradient stores
+  const int nzc = (D + F * (F - 1) / 2 + 7) / 8;   // dZ chunks read (<= 94 <= 2 x 64)
+  s16x8_t xv[XC];
+  uint4 zv[2];
+  auto load = [&](int b) {
 #pragma unroll
-      for (int k = 0; k < XC; ++k) {
-        const int c = lane + 64 * k;
-        if (c < F * CPR) {
-          const int j = c / CPR, ch = c - j * CPR;
-          const uint16_t* rp = j == 0 ? dense + (int64_t)b * ld_dense
-                                      : emb + slot[j] + (int64_t)b * slot[32 + j];
-          xv[k] = *(const s16x8_t*)(rp + ch * 8);
-        }
+    for (int k = 0; k < XC; ++k) {
+      const int c = lane + 64 * k;
+      if (c < F * CPR) {
+        const int j = c / CPR, ch = c - j * CPR;
+        const uint16_t* rp = j == 0 ? dense + (int64_t)b * ld_dense
+                                    : emb + slot[j] + (int64_t)b * slot[32 + j];
+        xv[k] = *(const s16x8_t*)(rp + ch * 8);
       }
-      const uint16_t* zp = dz + (int64_t)b * ldz;
-      for (int c = lane; c < ldz_al / 8; c += 64) {
-        if (c * 8 + 8 <= ldz) *(uint4*)(zrow + c * 8) = *(const uint4*)(zp + c * 8);
-        else for (int e = c * 8; e < ldz_al; ++e) zrow[e] = e < ldz ? zp[e] : 0;
+    }
+    const uint16_t* zp = dz + (int64_t)b * ldz;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int c = lane + 64 * k;
+      if (c < nzc) zv[k] = *(const uint4*)(zp + c * 8);
+    }
+  };
+  const int iters = (B + gridDim.x * WAVES - 1) / (gridDim.x * WAVES);
+  int b = blockIdx.x * WAVES + w;
+  if (b < B) load(b);
+  for (int it = 0; it < iters; ++it) {
+    const bool valid = b < B;
+    const int bn = b + gridDim.x * WAVES;
+    if (valid) {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int c = lane + 64 * k;
+        if (c < nzc) *(uint4*)(zrow + c * 8) = zv[k];
       }
 #pragma unroll
       for (int k = 0; k < XC; ++k) {
@@ -181,6 +205,7 @@ __global__ __launch_bounds__(256) void inter_bwd_kernel(
         }
       }
     }
+    if (it + 1 < iters && bn < B) load(bn);
     wave_sync();
     if (valid) {
       // A operand: S[i][k], i = lane&31, k = 16ks + 8h + jj
@@ -255,12 +280,23 @@ __global__ __launch_bounds__(256) void inter_bwd_kernel(
       }
     }
     wave_sync();
+    b = bn;
   }
 }
 
-int grid_for(int B) {
-  int waves = (B + WAVES - 1) / WAVES;
-  return waves < 2048 ? waves : 2048;
+// Samples per wave of the software-pipelined walk. Measured on MI355X
+// (B = 8192, F = 27, D = 128; scripts/inter_ab.sh): fwd 15.4 / 15.1 / 16.3 us
+// and bwd 43.3 / 37.8 / 34.4 us at 1 / 2 / 4 samples per wave (round 1's
+// one-sample-per-wave kernels: 20 / 42 us in the step). TDFO_INTER_SPW
+// overrides both.
+int grid_for(int B, int spw_default) {
+  static const int env = [] {
+    const char* e = getenv("TDFO_INTER_SPW");
+    return e ? atoi(e) : 0;
+  }();
+  const int spw = env >= 1 ? env : spw_default;
+  const int waves = (B + WAVES * spw - 1) / (WAVES * spw);
+  return waves > 0 ? waves : 1;
 }
 
 }  // namespace
@@ -270,7 +306,7 @@ void interaction_fwd(const uint16_t* dense, int64_t ld_dense,
                      int B, uint16_t* out, int64_t ldo, int ones_col, hipStream_t s) {
   if (B <= 0) return;
   const size_t smem = (size_t)WAVES * ldo * 2;
-  dim3 grid(grid_for(B));
+  dim3 grid(grid_for(B, 2));
 #define TDFO_IFWD(DD)                                                          \
   hipLaunchKernelGGL(inter_fwd_kernel<DD>, grid, dim3(256), smem, s, dense,    \
                      ld_dense, emb, slots, F, B, out, ldo, ones_col)
@@ -293,7 +329,7 @@ void interaction_bwd(const uint16_t* dz, int64_t ldz, const uint16_t* dense,
   if (B <= 0) return;
   const int ldz_al = (int)((ldz + 7) & ~7LL);
   const size_t smem = SLOT_BYTES + (size_t)WAVES * (32 * D * 2 + ldz_al * 2);
-  dim3 grid(grid_for(B));
+  dim3 grid(grid_for(B, 4));
 #define TDFO_IBWD(DD)                                                          \
   if (smem > 65536)                                                            \
     TDFO_CHECK_HIP(hipFuncSetAttribute((const void*)inter_bwd_kernel<DD>,      \
