@@ -335,6 +335,55 @@ void layernorm_bwd(const Tensor& x, const Tensor& g, int64_t n, const Tensor& ga
                       part.data_ptr<float>(), dgb.data_ptr<float>(), cur_stream());
 }
 
+void seq_prologue_fwd(const Tensor& x, const Tensor& pos, int64_t n, double eps,
+                      const Tensor& gamma, const Tensor& beta, double rate, int64_t seed,
+                      const c10::optional<Tensor>& step, const Tensor& y, const Tensor& mean,
+                      const Tensor& rstd) {
+  check_f32c(x, "x"); check_f32c(pos, "pos"); check_f32c(gamma, "gamma"); check_f32c(beta, "beta");
+  check_f32c(y, "y"); check_f32c(mean, "mean"); check_f32c(rstd, "rstd");
+  TORCH_CHECK(n > 0 && n <= 1024 && x.numel() % n == 0, "seq_prologue: n in (0, 1024] dividing x");
+  const int64_t M = x.numel() / n;
+  TORCH_CHECK(pos.numel() == n && gamma.numel() == n && beta.numel() == n &&
+              y.numel() == x.numel() && mean.numel() >= M && rstd.numel() >= M,
+              "seq_prologue: shapes");
+  const int64_t* sp = nullptr;
+  if (step) {
+    check_dev(*step, "step");
+    TORCH_CHECK(step->scalar_type() == at::kLong && step->numel() >= 1, "step: int64 device scalar");
+    sp = step->data_ptr<int64_t>();
+  }
+  tdfo::seq_prologue_fwd(x.data_ptr<float>(), pos.data_ptr<float>(), M, (int)n, (float)eps,
+                         gamma.data_ptr<float>(), beta.data_ptr<float>(), (float)rate,
+                         (uint32_t)seed, sp, y.data_ptr<float>(), mean.data_ptr<float>(),
+                         rstd.data_ptr<float>(), cur_stream());
+}
+
+void seq_prologue_bwd(const Tensor& x, const Tensor& pos, const Tensor& g, int64_t n,
+                      const Tensor& gamma, const Tensor& mean, const Tensor& rstd, double rate,
+                      int64_t seed, const c10::optional<Tensor>& step, const Tensor& dx,
+                      const Tensor& part, const Tensor& out3) {
+  check_f32c(x, "x"); check_f32c(pos, "pos"); check_f32c(g, "g"); check_f32c(gamma, "gamma");
+  check_f32c(mean, "mean"); check_f32c(rstd, "rstd"); check_f32c(dx, "dx");
+  check_f32c(part, "part"); check_f32c(out3, "out3");
+  TORCH_CHECK(n > 0 && n <= 1024 && x.numel() % n == 0, "seq_prologue: n");
+  const int64_t M = x.numel() / n;
+  TORCH_CHECK(pos.numel() == n && g.numel() == x.numel() && dx.numel() == x.numel() &&
+              gamma.numel() == n && mean.numel() >= M && rstd.numel() >= M &&
+              out3.numel() == 3 * n &&
+              part.numel() >= (int64_t)tdfo::layernorm_parts(M) * 3 * n, "seq_prologue_bwd: shapes");
+  const int64_t* sp = nullptr;
+  if (step) {
+    check_dev(*step, "step");
+    TORCH_CHECK(step->scalar_type() == at::kLong && step->numel() >= 1, "step: int64 device scalar");
+    sp = step->data_ptr<int64_t>();
+  }
+  tdfo::seq_prologue_bwd(x.data_ptr<float>(), pos.data_ptr<float>(), g.data_ptr<float>(), M,
+                         (int)n, gamma.data_ptr<float>(), mean.data_ptr<float>(),
+                         rstd.data_ptr<float>(), (float)rate, (uint32_t)seed, sp,
+                         dx.data_ptr<float>(), part.data_ptr<float>(), out3.data_ptr<float>(),
+                         cur_stream());
+}
+
 // ---------------------------------------------------------- batch gather
 void gather_columns(at::TensorList src, const c10::optional<Tensor>& idx, int64_t row0, int64_t n,
                     at::TensorList dst, at::IntArrayRef dst_stride) {
@@ -862,7 +911,8 @@ void two_tower(const Tensor& X, const Tensor& P, const Tensor& labels, double in
 
 void linear_xent(const Tensor& H, const Tensor& W, const Tensor& bias, const Tensor& labels,
                  double eps, int64_t ignore, const Tensor& dH, const Tensor& lossv,
-                 const c10::optional<Tensor>& dW, const c10::optional<Tensor>& db) {
+                 const c10::optional<Tensor>& dW, const c10::optional<Tensor>& db,
+                 const c10::optional<Tensor>& loss, const c10::optional<Tensor>& loss_acc) {
   check_dev(H, "H");
   TORCH_CHECK(H.scalar_type() == at::kFloat && H.dim() == 2 && H.size(1) == 16 &&
               H.is_contiguous() && aligned16(H.data_ptr()), "linear_xent: H fp32 [N,16]");
@@ -887,6 +937,17 @@ void linear_xent(const Tensor& H, const Tensor& W, const Tensor& bias, const Ten
                 dW->scalar_type() == at::kFloat && aligned16(dW->data_ptr()) &&
                 db->numel() == V && db->scalar_type() == at::kFloat, "linear_xent: dW/db");
     a.dW = dW->data_ptr<float>(); a.db = db->data_ptr<float>();
+  }
+  if (loss) {
+    check_dev(*loss, "loss");
+    TORCH_CHECK(loss->scalar_type() == at::kFloat && loss->numel() >= 1, "linear_xent: loss fp32 [1]");
+    a.loss = loss->data_ptr<float>();
+  }
+  if (loss_acc) {
+    check_dev(*loss_acc, "loss_acc");
+    TORCH_CHECK(loss && loss_acc->scalar_type() == at::kDouble && loss_acc->numel() >= 1,
+                "linear_xent: loss_acc fp64 [1] (with loss)");
+    a.loss_acc = loss_acc->data_ptr<double>();
   }
   Tensor ws = at::empty({(int64_t)tdfo::linear_xent_workspace((int)N, V)},
                         H.options().dtype(at::kByte));
@@ -976,6 +1037,11 @@ TORCH_LIBRARY(tdfo, m) {
         "Tensor(b!) mean, Tensor(c!) rstd) -> ()");
   m.def("layernorm_bwd(Tensor x, Tensor g, int n, Tensor gamma, Tensor mean, Tensor rstd, "
         "Tensor(a!) dx, Tensor(b!) part, Tensor(c!) dgb) -> ()");
+  m.def("seq_prologue_fwd(Tensor x, Tensor pos, int n, float eps, Tensor gamma, Tensor beta, "
+        "float rate, int seed, Tensor? step, Tensor(a!) y, Tensor(b!) mean, Tensor(c!) rstd) -> ()");
+  m.def("seq_prologue_bwd(Tensor x, Tensor pos, Tensor g, int n, Tensor gamma, Tensor mean, "
+        "Tensor rstd, float rate, int seed, Tensor? step, Tensor(a!) dx, Tensor(b!) part, "
+        "Tensor(c!) out3) -> ()");
   m.def("layernorm_parts(int M) -> int", [](int64_t M) { return (int64_t)tdfo::layernorm_parts(M); });
   m.def("gather_columns(Tensor[] src, Tensor? idx, int row0, int n, Tensor(a!)[] dst, int[] dst_stride) -> ()");
   m.def("concat_features(Tensor dense, Tensor emb, int[] off, int[] stride, int F, int D, "
@@ -1034,7 +1100,8 @@ TORCH_LIBRARY(tdfo, m) {
   m.def("colsum(Tensor x, Tensor(a!) out, bool accumulate) -> ()");
   m.def("auc_hist(Tensor logits, Tensor labels, int nb, Tensor(a!) hist) -> ()");
   m.def("linear_xent(Tensor H, Tensor W, Tensor bias, Tensor labels, float eps, int ignore, "
-        "Tensor(a!) dH, Tensor(b!) lossv, Tensor(c!)? dW, Tensor(d!)? db) -> ()");
+        "Tensor(a!) dH, Tensor(b!) lossv, Tensor(c!)? dW, Tensor(d!)? db, Tensor(e!)? loss=None, "
+        "Tensor(f!)? loss_acc=None) -> ()");
   m.def("jagged_to_dense(Tensor values, Tensor offsets, int T, float pad, Tensor(a!) out) -> ()");
   m.def("dense_to_jagged(Tensor dense, Tensor offsets, Tensor(a!) vgrad) -> ()");
   m.def("jagged_ids_to_dense(Tensor values, Tensor offsets, int pad, Tensor(a!) out) -> ()");
@@ -1050,6 +1117,8 @@ TORCH_LIBRARY_IMPL(tdfo, CUDA, m) {
   m.impl("attention_bwd", attention_bwd);
   m.impl("layernorm_fwd", layernorm_fwd);
   m.impl("layernorm_bwd", layernorm_bwd);
+  m.impl("seq_prologue_fwd", seq_prologue_fwd);
+  m.impl("seq_prologue_bwd", seq_prologue_bwd);
   m.impl("gather_columns", gather_columns);
   m.impl("concat_features", concat_features);
   m.impl("batch_load", batch_load);

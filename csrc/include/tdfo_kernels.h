@@ -273,6 +273,8 @@ struct LinearXentArgs {
   float* dH;               // [N, 16] (scaled by 1/n_valid)
   float* lossv;            // [N] per-token loss (0 for ignored)
   float* dW; float* db;    // optional [V, 16], [V]
+  float* loss;             // optional scalar: sum(lossv) / max(1, n_valid)
+  double* loss_acc;        // optional running sum: += loss (device, fp64)
   void* workspace;
 };
 size_t linear_xent_workspace(int N, int64_t V);
@@ -320,6 +322,17 @@ void layernorm_fwd(const float* x, int64_t M, int n, float eps, const float* gam
 void layernorm_bwd(const float* x, const float* g, int64_t M, int n, const float* gamma,
                    const float* mean, const float* rstd, float* dx, float* part,
                    float* dgamma_dbeta, hipStream_t s);
+// Bert4Rec input block y = dropout(LN(x + pos)) (pos [n] broadcast over rows;
+// counter-hash dropout keyed by seed ^ f(step[0]), regenerated in backward).
+// bwd: dx, and [dgamma | dbeta | dpos] (3n) reduced over rows in fixed order;
+// part: layernorm_parts(M) * 3n floats.
+void seq_prologue_fwd(const float* x, const float* pos, int64_t M, int n, float eps,
+                      const float* gamma, const float* beta, float rate, uint32_t seed,
+                      const int64_t* step, float* y, float* mean, float* rstd, hipStream_t s);
+void seq_prologue_bwd(const float* x, const float* pos, const float* g, int64_t M, int n,
+                      const float* gamma, const float* mean, const float* rstd, float rate,
+                      uint32_t seed, const int64_t* step, float* dx, float* part,
+                      float* dgamma_dbeta_dpos, hipStream_t s);
 
 // ------------------------------------------------------ batch gather ----
 // out_c[i * dst_stride_c] = convert(src_c[idx ? idx[i] : row0 + i]) for every

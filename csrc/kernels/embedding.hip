@@ -70,53 +70,115 @@ __global__ __launch_bounds__(256) void emb_fwd_onehot_kernel(EmbFwdArgs a) {
   }
 }
 
+// Multi-hot bags, LDS-staged index gather. A lane group of LPB lanes pools
+// one bag (BPW bags per wave). The bag's ids are staged CH at a time into a
+// per-wave LDS slice with one coalesced load per lane (plus the per-sample
+// weights), then every lane of the group reads them back as broadcast LDS
+// reads and keeps RIF row gathers in flight: the id -> row dependency no
+// longer serialises each row load behind a global index load, and the next
+// chunk's ids are loaded while this chunk's rows are in flight. Groups of a
+// wave with different bag lengths run the wave-uniform maximum trip count,
+// predicated per group.
+#ifndef TDFO_EMB_RIF
+#define TDFO_EMB_RIF 4
+#endif
+__device__ __forceinline__ void emb_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 template <int D, bool OUT_BF16>
 __global__ __launch_bounds__(256) void emb_fwd_kernel(EmbFwdArgs a) {
   constexpr int LPB = (D / 4) < 64 ? (D / 4) : 64;  // lanes per bag
   constexpr int BPW = 64 / LPB;                     // bags per wave
-  const int lane = threadIdx.x & 63;
+  constexpr int NCP = D / (4 * LPB);                // float4 column passes per lane
+  constexpr int CH = 64;                            // ids staged per bag per chunk
+  constexpr int IPL = (CH + LPB - 1) / LPB;         // staging loads per lane
+  constexpr int RIF = TDFO_EMB_RIF;                 // row gathers in flight per lane
+  __shared__ int64_t s_ids[4][BPW][CH];
+  __shared__ float s_w[4][BPW][CH];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int sub = lane / LPB, sl = lane - sub * LPB;
+  int64_t* ids = s_ids[w][sub];
+  float* wts = s_w[w][sub];
   const int64_t nbags = (int64_t)a.T * a.B;
   const int64_t wave0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t j = wave0 * BPW + sub; j < nbags; j += nwaves * BPW) {
-    const int t = (int)(j / a.B);
-    const int b = (int)(j - (int64_t)t * a.B);
-    const int64_t s = a.offsets[j], e = a.offsets[j + 1];
-    const float* wbase = a.W + a.row_offset[t] * D;
-    for (int c = sl * 4; c < D; c += LPB * 4) {
-      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-      int64_t p = s;
-      for (; p + 4 <= e; p += 4) {
-        float4 r[4];
-        float wt[4];
+  const int64_t nw_iters = (nbags + nwaves * BPW - 1) / (nwaves * BPW);
+  for (int64_t it = 0; it < nw_iters; ++it) {
+    const int64_t j = (it * nwaves + wave0) * BPW + sub;
+    const bool active = j < nbags;
+    const int t = active ? (int)(j / a.B) : 0;
+    const int b = active ? (int)(j - (int64_t)t * a.B) : 0;
+    const int64_t s = active ? a.offsets[j] : 0, e = active ? a.offsets[j + 1] : 0;
+    const int len = (int)(e - s);
+    // wave-uniform chunk count (max over the wave's bags)
+    int nch = (len + CH - 1) / CH;
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          r[u] = *(const float4*)(wbase + a.indices[p + u] * D + c);
-          wt[u] = a.psw ? a.psw[p + u] : 1.f;
+    for (int o = LPB; o < 64; o <<= 1) nch = max(nch, __shfl_xor(nch, o));
+    const float* wbase = a.W + (active ? a.row_offset[t] : 0) * D;
+    float4 acc[NCP];
+#pragma unroll
+    for (int cp = 0; cp < NCP; ++cp) acc[cp] = make_float4(0.f, 0.f, 0.f, 0.f);
+    // ids of chunk 0 in registers
+    int64_t nid[IPL];
+    float nwt[IPL];
+    auto fetch = [&](int c) {
+#pragma unroll
+      for (int k = 0; k < IPL; ++k) {
+        const int u = sl + k * LPB;
+        const int64_t p = s + (int64_t)c * CH + u;
+        const bool ok = u < CH && p < e;
+        nid[k] = ok ? a.indices[p] : 0;
+        nwt[k] = ok ? (a.psw ? a.psw[p] : 1.f) : 0.f;
+      }
+    };
+    fetch(0);
+    for (int c = 0; c < nch; ++c) {
+      emb_wave_sync();                       // previous chunk's LDS reads done
+#pragma unroll
+      for (int k = 0; k < IPL; ++k) {
+        const int u = sl + k * LPB;
+        if (u < CH) { ids[u] = nid[k]; wts[u] = nwt[k]; }
+      }
+      emb_wave_sync();
+      if (c + 1 < nch) fetch(c + 1);         // next chunk's ids overlap this chunk's rows
+      const int n = max(0, min(CH, len - c * CH));
+      int nmax = n;
+#pragma unroll
+      for (int o = LPB; o < 64; o <<= 1) nmax = max(nmax, __shfl_xor(nmax, o));
+      for (int u0 = 0; u0 < nmax; u0 += RIF) {
+        float4 r[RIF][NCP];
+        float wt[RIF];
+#pragma unroll
+        for (int v = 0; v < RIF; ++v) {
+          const bool ok = u0 + v < n;
+          const int64_t row = ok ? ids[u0 + v] : 0;
+          wt[v] = ok ? wts[u0 + v] : 0.f;
+#pragma unroll
+          for (int cp = 0; cp < NCP; ++cp)
+            r[v][cp] = ok ? *(const float4*)(wbase + row * D + (cp * LPB + sl) * 4)
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          acc.x += wt[u] * r[u].x; acc.y += wt[u] * r[u].y;
-          acc.z += wt[u] * r[u].z; acc.w += wt[u] * r[u].w;
-        }
+        for (int v = 0; v < RIF; ++v)
+#pragma unroll
+          for (int cp = 0; cp < NCP; ++cp) {
+            acc[cp].x += wt[v] * r[v][cp].x; acc[cp].y += wt[v] * r[v][cp].y;
+            acc[cp].z += wt[v] * r[v][cp].z; acc[cp].w += wt[v] * r[v][cp].w;
+          }
       }
-      for (; p < e; ++p) {
-        const float4 r = *(const float4*)(wbase + a.indices[p] * D + c);
-        const float wt = a.psw ? a.psw[p] : 1.f;
-        acc.x += wt * r.x; acc.y += wt * r.y; acc.z += wt * r.z; acc.w += wt * r.w;
-      }
-      if (a.mean && e > s) {
-        const float inv = 1.f / (float)(e - s);
-        acc.x *= inv; acc.y *= inv; acc.z *= inv; acc.w *= inv;
-      }
-      const int64_t o = (int64_t)b * a.out_stride + a.out_off[t] + c;
-      if (OUT_BF16) {
-        uint2 v = make_uint2(pack2bf(acc.x, acc.y), pack2bf(acc.z, acc.w));
-        *(uint2*)((uint16_t*)a.out + o) = v;
-      } else {
-        *(float4*)((float*)a.out + o) = acc;
-      }
+    }
+    if (!active) continue;
+    const float inv = (a.mean && len > 0) ? 1.f / (float)len : 1.f;
+#pragma unroll
+    for (int cp = 0; cp < NCP; ++cp) {
+      const float4 v = make_float4(acc[cp].x * inv, acc[cp].y * inv, acc[cp].z * inv,
+                                   acc[cp].w * inv);
+      const int64_t o = (int64_t)b * a.out_stride + a.out_off[t] + (cp * LPB + sl) * 4;
+      if (OUT_BF16) *(uint2*)((uint16_t*)a.out + o) = make_uint2(pack2bf(v.x, v.y), pack2bf(v.z, v.w));
+      else          *(float4*)((float*)a.out + o) = v;
     }
   }
 }

@@ -757,6 +757,31 @@ size_t linear_xent_workspace(int N, int64_t V) {
          (size_t)S * (XE + 1) * 4 + (size_t)(xent_blocks(N) - 1) * V * (XE + 1) * 4 + 512;
 }
 
+// Mean loss over the valid tokens in fixed order (one block, fixed reduction
+// tree: deterministic), optionally accumulated into a device fp64 running sum
+// -- replaces the count / sum / clamp / divide / accumulate library ops.
+__global__ __launch_bounds__(1024) void xent_loss_kernel(const float* __restrict__ lossv, int N,
+                                                         const int32_t* __restrict__ count,
+                                                         float* __restrict__ loss,
+                                                         double* __restrict__ acc) {
+  __shared__ float red[16];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  float v = 0.f;
+  for (int i = tid; i < N; i += 1024) v += lossv[i];
+  v = wave_sum(v);
+  if (lane == 0) red[w] = v;
+  __syncthreads();
+  if (w == 0) {
+    float t = lane < 16 ? red[lane] : 0.f;
+    t = wave_sum(t);
+    if (lane == 0) {
+      const float L = t / (float)max(1, *count);
+      loss[0] = L;
+      if (acc) acc[0] += (double)L;
+    }
+  }
+}
+
 void linear_xent(const LinearXentArgs& a, hipStream_t s) {
   if (a.N <= 0) return;
   if (a.V <= 0 || a.V >= (int64_t(1) << 31))
@@ -802,6 +827,9 @@ void linear_xent(const LinearXentArgs& a, hipStream_t s) {
                          a.H, a.W, a.bias, a.labels, a.V, a.eps, idx, count, lse, a.dW, a.db);
     }
   }
+  if (a.loss)
+    hipLaunchKernelGGL(xent_loss_kernel, dim3(1), dim3(1024), 0, s, a.lossv, a.N, count, a.loss,
+                       a.loss_acc);
   TDFO_CHECK_HIP(hipGetLastError());
 }
 

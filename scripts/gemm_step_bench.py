@@ -62,6 +62,29 @@ def calls(tr: DLRMTrainer):
         o = tr.top_in[i + 1][:, :L.out] if i + 1 < n else tr.t_out
         dx = tr.top_grad[i - 1] if i > 0 else tr.dz
         layers.append((L, tr.top_in[i], o, tr.top_grad[i], dx, i > 0))
+    if tr.cfg.interaction == "dcn":
+        fp, Wd, r = tr.fp, tr.top_real, tr.cfg.dcn_rank
+        x0 = tr.dcn_x[0]
+        for i, u in enumerate(tr.dcn_u):
+            V = fp.bf16(f"dcn{i}.v")
+            Uw = fp.bf16(u.name + ".w")
+            h, xi = tr.dcn_h[i], tr.dcn_x[i]
+            fl = 2.0 * B * Wd * r
+            out.append((f"dcn{i}", "V.fwd", fl, lambda xi=xi, V=V, h=h, u=u: ops.linear_fwd(
+                xi[:, :Wd], V, None, relu=False, out=h[:, :u.in_real])))
+            out.append((f"dcn{i}", "U.fwd", fl, lambda h=h, Uw=Uw, u=u, i=i, xi=xi: ops.gemm(
+                h[:, :u.in_k], False, Uw[:, :u.in_k], False,
+                None if u.bias_in_k else fp.param(u.name + ".w")[:, u.bcol], False, None,
+                tr.dcn_y[i], None, 1, mul=x0, add=xi[:, :Wd], out2=tr.dcn_x[i + 1][:, :Wd])))
+            out.append((f"dcn{i}", "U.wgrad", fl, lambda u=u, h=h: tr._wgrad(u, h, tr.dcn_dy)))
+            out.append((f"dcn{i}", "U.dgrad", fl, lambda Uw=Uw, u=u: ops.gemm(
+                tr.dcn_dy, False, Uw[:, :u.in_k], True, None, False, None, tr.dcn_dh, None, 1)))
+            out.append((f"dcn{i}", "V.wgrad", fl, lambda xi=xi, i=i: ops.linear_wgrad(
+                tr.dcn_dh, xi[:, :Wd], fp.grad(f"dcn{i}.v").view(-1),
+                splits=ops.wgrad_splits(r, Wd, B, tr._wg_target), slab=tr.slab)))
+            out.append((f"dcn{i}", "V.dgrad", fl, lambda V=V, i=i: ops.gemm(
+                tr.dcn_dh, False, V, True, None, False, None, None, None, 1,
+                add=tr.dcn_dx[i + 1], out2=tr.dcn_dx[i])))
     for L, x, o, dy, dx, relu_in in layers:
         fl = 2.0 * B * L.out * L.in_k
         out.append((L.name, "fwd", fl, lambda L=L, x=x, o=o: tr._fwd(L, x, o)))

@@ -62,6 +62,8 @@ def build_hip(force: bool = False, debug: bool = False, jobs: int = 8) -> Path:
              "-D__HIP_PLATFORM_AMD__=1", "-munsafe-fp-atomics"]
     if debug:
         flags += ["-g", "-DTDFO_DEBUG=1"]
+    # A/B builds of compile-time kernel knobs (e.g. "-DTDFO_EMB_RIF=8")
+    flags += os.environ.get("TDFO_HIPCC_EXTRA", "").split()
     inc, tlib = _torch_paths()
     tflags = [f"-I{p}" for p in inc] + ["-DUSE_ROCM=1", "-D_GLIBCXX_USE_CXX11_ABI=1",
                                         "-DTORCH_EXTENSION_NAME=tdfo_hip"]

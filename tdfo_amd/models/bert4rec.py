@@ -138,6 +138,39 @@ class _EncoderLayerFn(torch.autograd.Function):
         return (dx, None, None, None, None, None, None, *grads)
 
 
+class _SeqPrologueFn(torch.autograd.Function):
+    """dropout(LN_[T,E](item_emb + pos)) as one HIP kernel each way
+    (layernorm.hip seq_prologue_*): replaces the add, LayerNorm, dropout and
+    their backward library ops, incl. the positional-encoding grad reduction."""
+
+    @staticmethod
+    def forward(ctx, x, pos, gamma, beta, eps, rate, seed, step):
+        x = x.contiguous()
+        n = pos.numel()
+        M = x.numel() // n
+        y = torch.empty_like(x)
+        mean = torch.empty(M, dtype=torch.float32, device=x.device)
+        rstd = torch.empty_like(mean)
+        ops.seq_prologue_fwd(x, pos.contiguous(), n, eps, gamma.contiguous(), beta.contiguous(),
+                             rate, seed, step, y, mean, rstd)
+        ctx.save_for_backward(x, pos, gamma, mean, rstd, step)
+        ctx.cfg = (n, rate, seed)
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        x, pos, gamma, mean, rstd, step = ctx.saved_tensors
+        n, rate, seed = ctx.cfg
+        M = x.numel() // n
+        dx = torch.empty_like(x)
+        part = torch.empty(ops.layernorm_parts(M) * 3 * n, dtype=torch.float32, device=x.device)
+        out3 = torch.empty(3 * n, dtype=torch.float32, device=x.device)
+        ops.seq_prologue_bwd(x, pos.contiguous(), g.contiguous(), n, gamma.contiguous(), mean,
+                             rstd, rate, seed, step, dx, part, out3)
+        return (dx, out3[2 * n:].view_as(pos), out3[:n].view_as(gamma),
+                out3[n:2 * n].view_as(gamma), None, None, None, None)
+
+
 _ENC_OK: Dict[tuple, bool] = {}
 
 
@@ -312,26 +345,35 @@ class ItemEmbedding(nn.Module):
 
 class _LinearXentFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, H, W, b, labels, eps):
+    def forward(ctx, H, W, b, labels, eps, loss_acc, unit_grad):
         N = H.shape[0]
         dH = torch.empty_like(H)
         lossv = torch.empty(N, dtype=torch.float32, device=H.device)
         dW = torch.empty_like(W)
         db = torch.empty_like(b)
-        ops.linear_xent(H, W, b, labels, eps, PAD_ID, dH, lossv, dW, db)
-        nv = (labels != PAD_ID).sum().clamp_min(1).to(torch.float32)
+        loss = torch.empty(1, dtype=torch.float32, device=H.device)
+        # the kernel also reduces the mean loss (and adds it to loss_acc)
+        ops.linear_xent(H, W, b, labels, eps, PAD_ID, dH, lossv, dW, db, loss=loss,
+                        loss_acc=loss_acc)
         ctx.save_for_backward(dH, dW, db)
-        return lossv.sum() / nv
+        ctx.unit_grad = unit_grad
+        return loss[0]
 
     @staticmethod
     def backward(ctx, g):
         dH, dW, db = ctx.saved_tensors
-        return dH * g, dW * g, db * g, None, None
+        if ctx.unit_grad:      # caller's promise: the loss is backward()'s root (g == 1)
+            return dH, dW, db, None, None, None, None
+        return dH * g, dW * g, db * g, None, None, None, None
 
 
-def linear_cross_entropy(H, W, b, labels, eps=0.1):
-    """mean CE(ignore_index=0, label_smoothing=eps) of H @ W^T + b, fused."""
-    return _LinearXentFn.apply(H.contiguous(), W, b, labels.contiguous(), eps)
+def linear_cross_entropy(H, W, b, labels, eps=0.1, loss_acc=None, unit_grad=False):
+    """mean CE(ignore_index=0, label_smoothing=eps) of H @ W^T + b, fused.
+    loss_acc (fp64 [1]): the kernel adds the loss to it. unit_grad: the
+    returned loss is the root of backward() (gradient exactly 1), so the
+    saved gradients are returned without the scaling launches."""
+    return _LinearXentFn.apply(H.contiguous(), W, b, labels.contiguous(), eps, loss_acc,
+                               unit_grad)
 
 
 class Bert4Rec(nn.Module):
@@ -360,7 +402,13 @@ class Bert4Rec(nn.Module):
             mask = KeyPad(seqs.contiguous(), self.rng_step)
         else:
             mask = (seqs != PAD_ID).unsqueeze(1).unsqueeze(1)      # [B, 1, 1, T] key mask
-        x = self.emb_dropout(layer_norm(item_emb + self.positional_encoding, self.layernorm))
+        if _fused(item_emb):
+            rate = self.emb_dropout.p if self.training else 0.0
+            x = _SeqPrologueFn.apply(item_emb, self.positional_encoding, self.layernorm.weight,
+                                     self.layernorm.bias, self.layernorm.eps, rate,
+                                     0x5EED0E3B, self.rng_step)
+        else:
+            x = self.emb_dropout(layer_norm(item_emb + self.positional_encoding, self.layernorm))
         for blk in self.transformer_blocks:
             x = blk(x, mask)
         return x
@@ -443,7 +491,8 @@ class Bert4RecTrainer:
         x = self._embed(seqs)
         h = self.model.encode(x, seqs)
         loss = linear_cross_entropy(h.reshape(-1, self.E), self.model.out.weight,
-                                    self.model.out.bias, labels.reshape(-1), self.eps)
+                                    self.model.out.bias, labels.reshape(-1), self.eps,
+                                    loss_acc=self.loss_sum, unit_grad=True)
         loss.backward()
         return loss
 
@@ -453,8 +502,7 @@ class Bert4RecTrainer:
         self.opt.all_reduce_grads(average=True)
         self.opt.step()
         self.model.rng_step.add_(1)
-        self.loss_sum.add_(loss.detach().double())
-        return loss
+        return loss          # (already added to loss_sum by the fused loss kernel)
 
     def load_batch(self, seqs, labels):
         b = seqs.shape[0]

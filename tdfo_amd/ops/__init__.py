@@ -402,12 +402,21 @@ def two_tower(X, P, labels, inv_n, logits, dX=None, part=None, loss_scale=None, 
         ref.two_tower(X, P, labels, inv_n, logits, dX, part, loss_scale, half)
 
 
-def linear_xent(H, W, bias, labels, eps, ignore, dH, lossv, dW=None, db=None):
-    """Fused Linear(16->V) + label-smoothed CrossEntropy, fwd+bwd (no logits)."""
+def linear_xent(H, W, bias, labels, eps, ignore, dH, lossv, dW=None, db=None, loss=None,
+                loss_acc=None):
+    """Fused Linear(16->V) + label-smoothed CrossEntropy, fwd+bwd (no logits).
+    loss (fp32 [1]): mean loss over the non-ignored tokens; loss_acc (fp64
+    [1]): += that loss (device running sum)."""
     if _gpu(H):
-        _native().linear_xent(H, W, bias, labels, float(eps), int(ignore), dH, lossv, dW, db)
+        _native().linear_xent(H, W, bias, labels, float(eps), int(ignore), dH, lossv, dW, db,
+                              loss, loss_acc)
     else:
         ref.linear_xent(H, W, bias, labels, eps, ignore, dH, lossv, dW, db)
+        if loss is not None:
+            nv = (labels != ignore).sum().clamp_min(1).to(torch.float32)
+            loss.view(-1)[0] = lossv.sum() / nv
+            if loss_acc is not None:
+                loss_acc.view(-1)[0] += loss.view(-1)[0].double()
 
 
 def jagged_to_dense(values, offsets, T, pad, out):
@@ -458,6 +467,25 @@ def layernorm_fwd(x, n, eps, gamma, beta, y, mean, rstd):
         _native().layernorm_fwd(x, int(n), float(eps), gamma, beta, y, mean, rstd)
     else:
         ref.layernorm_fwd(x, n, eps, gamma, beta, y, mean, rstd)
+
+
+def seq_prologue_fwd(x, pos, n, eps, gamma, beta, rate, seed, step, y, mean, rstd):
+    """y = dropout(LN(x + pos)) over rows of n (Bert4Rec input block); the
+    dropout mask is a counter hash of (seed, step[0], row, element)."""
+    if _gpu(x):
+        _native().seq_prologue_fwd(x, pos, int(n), float(eps), gamma, beta, float(rate),
+                                   int(seed) & 0xFFFFFFFF, step, y, mean, rstd)
+    else:
+        ref.seq_prologue_fwd(x, pos, n, eps, gamma, beta, rate, seed, step, y, mean, rstd)
+
+
+def seq_prologue_bwd(x, pos, g, n, gamma, mean, rstd, rate, seed, step, dx, part, out3):
+    """dx and out3 = [dgamma | dbeta | dpos] (3n) of seq_prologue_fwd."""
+    if _gpu(x):
+        _native().seq_prologue_bwd(x, pos, g, int(n), gamma, mean, rstd, float(rate),
+                                   int(seed) & 0xFFFFFFFF, step, dx, part, out3)
+    else:
+        ref.seq_prologue_bwd(x, pos, g, n, gamma, mean, rstd, rate, seed, step, dx, out3)
 
 
 def layernorm_bwd(x, g, n, gamma, mean, rstd, dx, part, dgb):

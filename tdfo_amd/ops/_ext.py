@@ -14,7 +14,9 @@ from pathlib import Path
 
 import torch
 
-_LIB_PATH = Path(__file__).resolve().parent.parent / "lib" / "libtdfo_hip.so"
+# TDFO_LIB_PATH: load another build of the library (same-box A/B runs)
+_LIB_PATH = Path(os.environ.get("TDFO_LIB_PATH") or
+                 Path(__file__).resolve().parent.parent / "lib" / "libtdfo_hip.so")
 _lock = threading.Lock()
 _loaded = False
 _error: Exception | None = None

@@ -642,6 +642,45 @@ def layernorm_bwd(x, g, n, gamma, mean, rstd, dx, dgb):
     dgb[n:].copy_(gv.sum(0))
 
 
+def seq_prologue_mul(M: int, n: int, rate: float, seed: int, step: int, device):
+    """[M, n] dropout multiplier of the fused sequence prologue
+    (csrc/kernels/layernorm.hip::pro_mul)."""
+    if rate <= 0:
+        return torch.ones(M, n, device=device)
+    sd = ((seed & _M32) ^ ((step * 0x632BE5AB) & _M32) ^ 0x51ED270B) & _M32
+    r = _hash3(torch.full((1,), sd, dtype=torch.int64, device=device),
+               torch.arange(M, dtype=torch.int64, device=device).view(M, 1),
+               torch.arange(n, dtype=torch.int64, device=device).view(1, n))
+    keep = (r >> 8).to(torch.float32) * (1.0 / 16777216.0) >= rate
+    return keep.to(torch.float32) / (1.0 - rate)
+
+
+def seq_prologue_fwd(x, pos, n, eps, gamma, beta, rate, seed, step, y, mean, rstd):
+    v = x.reshape(-1, n) + pos.reshape(1, n)
+    M = v.shape[0]
+    mu = v.mean(1)
+    rs = torch.rsqrt(v.var(1, unbiased=False) + eps)
+    o = (v - mu[:, None]) * rs[:, None] * gamma.view(1, n) + beta.view(1, n)
+    st = int(step.reshape(-1)[0]) if step is not None else 0
+    y.view(-1, n).copy_(o * seq_prologue_mul(M, n, rate, seed, st, x.device))
+    mean[:M].copy_(mu)
+    rstd[:M].copy_(rs)
+
+
+def seq_prologue_bwd(x, pos, g, n, gamma, mean, rstd, rate, seed, step, dx, out3):
+    v = x.reshape(-1, n) + pos.reshape(1, n)
+    M = v.shape[0]
+    st = int(step.reshape(-1)[0]) if step is not None else 0
+    gv = g.reshape(-1, n) * seq_prologue_mul(M, n, rate, seed, st, x.device)
+    xh = (v - mean[:M, None]) * rstd[:M, None]
+    gg = gv * gamma.view(1, n)
+    dxv = rstd[:M, None] * (gg - gg.mean(1, keepdim=True) - xh * (gg * xh).mean(1, keepdim=True))
+    dx.view(-1, n).copy_(dxv)
+    out3[:n].copy_((gv * xh).sum(0))
+    out3[n:2 * n].copy_(gv.sum(0))
+    out3[2 * n:].copy_(dxv.sum(0))
+
+
 # ------------------------------------------------------------ encoder layer
 ENC_SITE_A, ENC_SITE_F, ENC_SITE_G, ENC_SITE_BLK = 1, 2, 3, 4
 

@@ -230,3 +230,30 @@ def test_encoder_layer_reference_matches_block():
     got = ref.encoder_layer(x, ids, blk._fused_params(), H, 0.0, 1, 0, 0,
                             blk.input_sublayer.norm.eps)
     assert torch.allclose(got, exp, atol=1e-5, rtol=1e-5)
+
+
+def test_seq_prologue_reference_matches_autograd():
+    """CPU reference of the fused Bert4Rec input block (dropout(LN(x + pos)))
+    vs torch autograd of the unfused ops at rate 0, and mask statistics."""
+    from tdfo_amd.ops import reference as ref
+
+    torch.manual_seed(0)
+    M, n = 64, 320
+    x, pos = torch.randn(M, n), torch.randn(n)
+    gamma, beta = torch.randn(n), torch.randn(n)
+    y, mean, rstd = torch.empty(M, n), torch.empty(M), torch.empty(M)
+    ref.seq_prologue_fwd(x, pos, n, 1e-5, gamma, beta, 0.0, 5, None, y, mean, rstd)
+    xr, pr = x.clone().requires_grad_(True), pos.clone().requires_grad_(True)
+    gr, br = gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True)
+    e = torch.nn.functional.layer_norm(xr + pr, (n,), gr, br, 1e-5)
+    assert torch.allclose(y, e, atol=1e-5)
+    g = torch.randn(M, n)
+    e.backward(g)
+    dx, out3 = torch.empty(M, n), torch.empty(3 * n)
+    ref.seq_prologue_bwd(x, pos, g, n, gamma, mean, rstd, 0.0, 5, None, dx, out3)
+    assert torch.allclose(dx, xr.grad, atol=1e-5)
+    assert torch.allclose(out3[:n], gr.grad, atol=1e-4)
+    assert torch.allclose(out3[n:2 * n], br.grad, atol=1e-4)
+    assert torch.allclose(out3[2 * n:], pr.grad, atol=1e-4)
+    m = ref.seq_prologue_mul(M, n, 0.25, 5, 3, "cpu")
+    assert abs(float((m == 0).float().mean()) - 0.25) < 0.02

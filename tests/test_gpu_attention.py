@@ -101,6 +101,44 @@ def test_layernorm_fwd_bwd(M, n):
     assert torch.allclose(dgb[n:], br.grad, atol=1e-3, rtol=1e-3)
 
 
+@pytest.mark.parametrize("M,n,rate", [(512, 320, 0.0), (512, 320, 0.1), (37, 100, 0.3)])
+def test_seq_prologue_fwd_bwd(M, n, rate):
+    """Fused dropout(LN(x + pos)): kernel vs the fp32 reference (same hash mask)
+    and, at rate 0, vs torch autograd of the unfused ops."""
+    from tdfo_amd.ops import reference as ref
+
+    torch.manual_seed(4)
+    x = torch.randn(M, n, device=DEV) * 2 + 0.5
+    pos = torch.randn(n, device=DEV)
+    gamma, beta = torch.randn(n, device=DEV), torch.randn(n, device=DEV)
+    step = torch.tensor([7], dtype=torch.int64, device=DEV)
+    y, mean, rstd = torch.empty_like(x), torch.empty(M, device=DEV), torch.empty(M, device=DEV)
+    ops.seq_prologue_fwd(x, pos, n, 1e-5, gamma, beta, rate, 1234, step, y, mean, rstd)
+    ey, em, er = torch.empty_like(x), torch.empty(M, device=DEV), torch.empty(M, device=DEV)
+    ref.seq_prologue_fwd(x, pos, n, 1e-5, gamma, beta, rate, 1234, step, ey, em, er)
+    assert torch.allclose(y, ey, atol=1e-4, rtol=1e-4)
+    g = torch.randn_like(x)
+    dx = torch.empty_like(x)
+    part = torch.empty(ops.layernorm_parts(M) * 3 * n, device=DEV)
+    out3 = torch.empty(3 * n, device=DEV)
+    ops.seq_prologue_bwd(x, pos, g, n, gamma, mean, rstd, rate, 1234, step, dx, part, out3)
+    edx, eo3 = torch.empty_like(x), torch.empty(3 * n, device=DEV)
+    ref.seq_prologue_bwd(x, pos, g, n, gamma, em, er, rate, 1234, step, edx, eo3)
+    assert torch.allclose(dx, edx, atol=1e-4, rtol=1e-3)
+    assert torch.allclose(out3, eo3, atol=2e-3, rtol=1e-3)
+    if rate > 0:
+        assert 0.0 < float((y == 0).float().mean()) < 2 * rate
+        return
+    xr, pr = x.clone().requires_grad_(True), pos.clone().requires_grad_(True)
+    gr, br = gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True)
+    e = torch.nn.functional.layer_norm(xr + pr, (n,), gr, br, 1e-5)
+    e.backward(g)
+    assert torch.allclose(dx, xr.grad, atol=1e-4, rtol=1e-3)
+    assert torch.allclose(out3[:n], gr.grad, atol=2e-3, rtol=1e-3)
+    assert torch.allclose(out3[n:2 * n], br.grad, atol=2e-3, rtol=1e-3)
+    assert torch.allclose(out3[2 * n:], pr.grad, atol=2e-3, rtol=1e-3)
+
+
 def test_bert4rec_fused_encoder_matches_torch_path():
     """Whole encoder fwd+bwd: fused HIP path vs the torch reference path (dropout 0)."""
     from tdfo_amd.models import bert4rec as m
