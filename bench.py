@@ -47,6 +47,9 @@ def parse(argv=None):
     ap.add_argument("--dist", default="uniform", choices=["uniform", "zipf"])
     ap.add_argument("--sharding", default="auto",
                     choices=["auto", "table_wise", "row_wise", "column_wise", "data_parallel"])
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="N > 1: exchange each batch's ids inside its own step instead of "
+                         "during the previous step's dense update")
     ap.add_argument("--host-data", action="store_true",
                     help="batches from the C++ host generator through pinned slots and a "
                          "copy-stream H2D prefetcher (instead of a pool of device batches)")
@@ -124,12 +127,13 @@ def main(argv=None):
         ops.gemm_policy(int(os.environ["TDFO_GEMM_POLICY"]))
     rows = {"1tb": CRITEO_1TB_ROWS, "kaggle": CRITEO_KAGGLE_ROWS, "gt1tb": DCN_GT1TB_ROWS,
             "tiny": [1000] * 26}[args.rows]
+    pipe = world_env > 1 and not args.no_pipeline
     if args.model == "dlrm":
-        cfg = DLRMConfig(table_rows=list(rows), sharding=args.sharding,
+        cfg = DLRMConfig(table_rows=list(rows), sharding=args.sharding, pipeline=pipe,
                          overlap=(args.overlap if args.overlap == 'wgrad' else bool(args.overlap)))
     else:
         cfg = DLRMConfig(table_rows=list(rows), interaction="dcn", pooling=list(MLPERF_MULTIHOT),
-                         top=[1024, 1024, 512, 256, 1], sharding=args.sharding,
+                         top=[1024, 1024, 512, 256, 1], sharding=args.sharding, pipeline=pipe,
                          overlap=(args.overlap if args.overlap == 'wgrad' else bool(args.overlap)))
     B = args.batch
     t0 = time.time()
@@ -147,16 +151,30 @@ def main(argv=None):
     setup_s = time.time() - t0
     use_graph = not args.no_graph
 
+    def feed(i):
+        """Hand batch i to the trainer (pipelined: as the batch the next step
+        runs on -- this step loads it after its embedding update)."""
+        if pool is None:                       # host data plane: generation + H2D overlapped
+            batch, slot = pf.next()
+        else:
+            batch, slot = pool[i % len(pool)], None
+        (tr.set_next_batch if tr.pipeline else tr.load_batch)(*batch)
+        return slot
+
     def run(n, start):
         for i in range(n):
-            if pool is None:                   # host data plane: generation + H2D overlapped
-                batch, slot = pf.next()
-                tr.load_batch(*batch)
-                pf.release(slot)
-            else:
-                tr.load_batch(*pool[(start + i) % len(pool)])
+            slot = feed(start + i + 1 if tr.pipeline else start + i)
             tr.step()
+            if slot is not None:               # the step has enqueued its reads of it
+                pf.release(slot)
 
+    if tr.pipeline:
+        if pool is None:
+            b0, s0 = pf.next()
+            tr.prime(*b0)
+            pf.release(s0)
+        else:
+            tr.prime(*pool[0])
     run(args.warmup, 0)
     if use_graph:
         tr.capture_graph(warmup=1)

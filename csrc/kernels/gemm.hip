@@ -687,6 +687,95 @@ __global__ __launch_bounds__(MI == 4 ? 512 : 256, 1) void gemm_big_kernel(GemmAr
   epilogue<LBM, NW * 64, MI>(p, acc, smem_raw, m0, n0, wr, wc, lane, tid, ti.split);
 }
 
+// ---------------------------------------------------------------------------
+// Deep-pipelined 128x128 kernel: 4 waves (2x2 of 64x64), DNS-deep glds ring
+// (DNS x 32 KiB, one block per CU) with DNS-2 K tiles of DMA in flight across
+// each raw barrier (counted vmcnt, never 0 in the steady state). For GEMMs
+// whose grid is ~one 128x128 tile per CU and whose K is long (DCN-v2 cross
+// layers, K = 3456): the 2-stage kernel exposes a whole load round trip per
+// K tile there (V fwd: 54 K tiles in 43 us, ~1900 cycles each, ~32 KiB in
+// flight per CU).
+#ifndef TDFO_GEMM_DNS
+#define TDFO_GEMM_DNS 4
+#endif
+constexpr int DNS = TDFO_GEMM_DNS;
+constexpr int DSMEM = DNS * STAGE_BYTES;
+
+template <bool A_COL, bool B_COL>
+__global__ __launch_bounds__(256, 1) void gemm_deep_kernel(GemmArgs p) {
+  constexpr int MI = 4;
+  constexpr int PPW = 8;                             // glds pieces per wave per K tile
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  TDFO_LDS char* smem = (TDFO_LDS char*)smem_raw;
+  const int tiles_m = (p.M + BM - 1) / BM, tiles_n = (p.N + BN - 1) / BN;
+  const TileIdx ti = tile_of(tiles_m, tiles_n, p.splits);
+  const int m0 = ti.tm * BM, n0 = ti.tn * BN;
+  const int ktiles = p.K / BK;
+  const int per = (ktiles + p.splits - 1) / p.splits;
+  const int kt0 = ti.split * per;
+  const int nk = min(ktiles, kt0 + per) - kt0;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wr = w >> 1, wc = w & 1;
+  f32x4_t acc[MI][4];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  // 32 pieces per K tile (A 16, B 16), 8 per wave
+  auto stage = [&](int buf, int kt) {
+    TDFO_LDS char* ta = smem + buf * STAGE_BYTES;
+    TDFO_LDS char* tb = ta + TILE_BYTES;
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      glds_piece_asm<A_COL>(p.A, p.lda, m0, p.M, k0, ta, w * 4 + i, lane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      glds_piece_asm<B_COL>(p.B, p.ldb, n0, p.N, k0, tb, w * 4 + i, lane);
+  };
+  const bool csum = A_COL && p.csum_on && ti.tn == 0;
+  const int cs_par = __builtin_amdgcn_readfirstlane(wc);
+  f32x4_t cs[MI / 2];
+#pragma unroll
+  for (int h = 0; h < MI / 2; ++h) cs[h] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  auto kloop = [&](auto cs_on) {
+    constexpr bool CS = decltype(cs_on)::value;
+#pragma unroll
+    for (int q = 0; q < DNS - 1; ++q)
+      if (q < nk) stage(q, kt0 + q);
+    for (int t = 0; t < nk; ++t) {
+      // tile t landed for this thread: the younger tiles (up to DNS-2) may
+      // still be in flight
+      const int younger = min(nk - 1 - t, DNS - 2);
+      if (younger >= 3)      asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+      else if (younger == 2) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+      else if (younger == 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else                   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      // every thread's pieces of tile t landed, and every wave finished
+      // reading slot (t-1) % DNS, which the stage below refills
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      if (t + DNS - 1 < nk) stage((t + DNS - 1) % DNS, kt0 + t + DNS - 1);
+      const TDFO_LDS char* ta = smem + (t % DNS) * STAGE_BYTES;
+      mfma_k64<A_COL, B_COL, MI, CS>(acc, ta, wr * 64, ta + TILE_BYTES, wc * 64, lane, cs,
+                                     cs_par);
+      // this wave's fragment reads of slot t % DNS done before the next
+      // barrier (the slot is refilled DNS-1 iterations later)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+  };
+  static_assert(DNS >= 2 && DNS <= 5, "ring depth");
+  if (csum) {
+    kloop(BoolC<true>{});
+    csum_store<MI>(p, cs, m0 + wr * 64, lane, ti.split, cs_par);
+  } else {
+    kloop(BoolC<false>{});
+  }
+  __syncthreads();
+  epilogue<BM, 256, MI>(p, acc, smem_raw, m0, n0, wr, wc, lane, tid, ti.split);
+}
+
 // 0 auto, 1 small tiles only (64-row tiles when 128-row ones underfill),
 // 2 large tiles only, 3 128x128 tiles only, 4 = 1 with 256x128 tiles for
 // the weight-grad (col-A) GEMMs, 5 = auto with 64-row tiles below 512
@@ -708,6 +797,8 @@ void launch(const GemmArgs& a, hipStream_t s) {
                                        hipFuncAttributeMaxDynamicSharedMemorySize, LSMEM));
     TDFO_CHECK_HIP(hipFuncSetAttribute((const void*)gemm_big_kernel<AC, BC, 8>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, LSMEM));
+    TDFO_CHECK_HIP(hipFuncSetAttribute((const void*)gemm_deep_kernel<AC, BC>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, DSMEM));
     attr = true;
   }
   const int tn = (a.N + BN - 1) / BN;
@@ -719,7 +810,7 @@ void launch(const GemmArgs& a, hipStream_t s) {
   if (g_policy == 7) b.abl = 256;                // auto, bf16 outputs through the LDS epilogue
   if (g_policy == 17) b.abl = 512;               // auto, masked dgrads on the direct path
   const bool autop = g_policy == 0 || g_policy == 6 || g_policy == 7 || g_policy == 17 ||
-                     g_policy == 21 || g_policy == 22;
+                     g_policy == 21 || g_policy == 22 || g_policy == 24;
   bool big = (g_policy >= 2 && g_policy != 3 && g_policy != 4 && !autop) ||
              (g_policy == 4 && AC) || (autop && small_tiles * a.splits >= 1024);
   // the A column sums are produced by the 128x128 kernel only
@@ -728,6 +819,24 @@ void launch(const GemmArgs& a, hipStream_t s) {
   // policy 20: the 4-wave 128x64-per-wave kernel for every GEMM; 21: auto
   // with it in place of the 8-wave kernel; 22: auto with it for every GEMM
   // that fills >= 128 CUs with 256x128 tiles
+  // policy 23: the deep-pipelined 128x128 kernel for every GEMM; 24: auto,
+  // with it in place of the 2-stage 128x128 kernel where the grid has at
+  // most 2 tiles per CU and K spans >= 16 tiles per split
+  // 25 (DCN-v2): policy 2 (256x128 everywhere), except the deep kernel for
+  // non-weight-grad GEMMs whose 256x128 grid would leave CUs idle while a
+  // 128x128 grid fills them once, with long K (cross-layer V fwd / U dgrad:
+  // 36 vs 44 us and 39 vs 48 us, profiles/gemm_step_ab.md)
+  const int ktps = (a.K / BK + a.splits - 1) / a.splits;
+  const bool deep25 = g_policy == 25 && !AC && big_tiles * a.splits < 256 &&
+                      small_tiles * a.splits <= 512 && ktps >= 16;
+  if (g_policy == 25 && !deep25 && !small_only) big = true;
+  if (g_policy == 23 || deep25 ||
+      (g_policy == 24 && !big && small_tiles * a.splits <= 512 && ktps >= 16)) {
+    dim3 grid(small_tiles * a.splits);
+    hipLaunchKernelGGL((gemm_deep_kernel<AC, BC>), grid, dim3(256), DSMEM, s, b);
+    TDFO_CHECK_HIP(hipGetLastError());
+    return;
+  }
   if (!small_only && (g_policy == 20 || (g_policy == 22 && big_tiles * a.splits >= 128))) {
     b.abl = 0;
     dim3 grid(big_tiles * a.splits);

@@ -83,6 +83,8 @@ class DLRMConfig:
     sharding: str = "auto"                         # planner strategy
     rw_capacity: float = 1.25                      # row-wise segment capacity (x n/W, +256)
     rw_comm: str = "bf16"                          # row-wise reduce-scatter dtype (bf16 | fp32)
+    pipeline: bool = False                         # W > 1: next batch's id exchange overlaps
+    #   this step's dense update (input-dist pipelining; see DLRMTrainer.prime)
     overlap: object = False                        # side streams (GPU): False | True (wgrads +
     #   embedding work) | "wgrad" (weight grads only)
     #   (measured 0.744 vs 0.728 ms/step on DLRM-1TB: the overlapped kernels
@@ -227,9 +229,10 @@ class DLRMTrainer:
         torch.manual_seed(cfg.seed)
         if self.device.type == "cuda" and not os.environ.get("TDFO_GEMM_POLICY"):
             # GEMM tile policy measured per workload (profiles/gemm_tile_ab.md):
-            # DCN-v2's wide cross layers run best on 256x128 tiles throughout,
-            # DLRM's <= 1024-wide MLPs on 128x128 / 64x128 tiles
-            ops.gemm_policy(2 if cfg.interaction == "dcn" else 0)
+            # DCN-v2's wide cross layers run best on 256x128 tiles (policy 25:
+            # + the deep-pipelined 128x128 kernel for its 512-wide long-K
+            # GEMMs), DLRM's <= 1024-wide MLPs on 128x128 / 64x128 tiles
+            ops.gemm_policy(25 if cfg.interaction == "dcn" else 0)
         # ------------------------------------------------------ embeddings
         optim = EmbOptimConfig(cfg.emb_opt, lr=cfg.emb_lr, eps=cfg.emb_eps)
         tables = cfg.tables()
@@ -369,6 +372,15 @@ class DLRMTrainer:
         self._ws = torch.cuda.Stream(device=dev) if on_gpu else None
         self._es = (torch.cuda.Stream(device=dev)
                     if (on_gpu and world_size == 1 and cfg.overlap != "wgrad") else None)
+        # input-dist pipelining (the role of TorchRec's TrainPipelineSparseDist
+        # behind the reference's DMP, torchrec/train.py:241-247): batch i+1's
+        # ids are bucketed and exchanged right after batch i's embedding
+        # update -- the last reader of the exchanged-id buffers -- so the
+        # exchange overlaps batch i's dense optimizer step and batch i+1
+        # starts at its lookup. Numerics are identical to the unpipelined step.
+        self.pipeline = bool(cfg.pipeline) and world_size > 1 and self._es is None
+        self._next = None
+        self._primed = False
 
     # for tests / checkpoints: (weight [out, in_real], bias [out]) views
     def weight(self, name: str):
@@ -406,6 +418,31 @@ class DLRMTrainer:
         """
         # device-resident batch: one fused launch (ids, labels, dense -> bf16)
         ops.batch_load(dense, self.x0, ids, self.ids, label, self.label)
+
+    # ------------------------------------------------- pipelined input dist
+    def prime(self, dense: torch.Tensor, ids: torch.Tensor, label: torch.Tensor):
+        """Pipelined mode: load the first batch and start its id exchange.
+        Then per step: ``set_next_batch(next batch); step()`` -- the step
+        consumes the batch loaded before it and loads / exchanges the next."""
+        assert self.pipeline, "prime() needs DLRMConfig(pipeline=True) and world_size > 1"
+        self.load_batch(dense, ids, label)
+        if not self.emb.fwd_prep_noop:
+            self.emb.stage_fwd_prep(self.ids)
+        self.emb.stage_fwd_ids_exchange(async_op=True)
+        self._next = (dense, ids, label)
+        self._primed = True
+
+    def set_next_batch(self, dense: torch.Tensor, ids: torch.Tensor, label: torch.Tensor):
+        """Pipelined mode: the batch the current step loads for the next one
+        (device tensors that stay valid until the step has been issued)."""
+        self._next = (dense, ids, label)
+
+    def _m_load_next(self):
+        dense, ids, label = self._next
+        ops.batch_load(dense, self.x0, ids, self.ids, label, self.label)
+
+    def _m_ids_exchange_next(self):
+        self.emb.stage_fwd_ids_exchange(async_op=True)
 
     # ------------------------------------------------------------- layers
     def _fwd(self, L: Lin, x, out, relu=True):
@@ -487,6 +524,30 @@ class DLRMTrainer:
             lookup = ("c", emb.stage_fwd_lookup)
         prep = [] if emb.fwd_prep_noop else [("c", lambda: emb.stage_fwd_prep(self.ids))]
         top_wgrad = [("c", self._s_top_wgrad)] if self._defer_top_wgrad else []
+        if self.pipeline:
+            # this batch's ids were exchanged during the previous step (or by
+            # prime()); the next batch is loaded + exchanged after the
+            # embedding update, overlapping the dense optimizer step
+            return [
+                ("m", emb.ids_exchange_wait),
+                lookup,
+                ("m", emb.stage_fwd_out_exchange),
+                ("c", self._s_bottom_fwd),
+                ("m", self._m_fwd_wait),
+                ("c", self._s_top),
+                ("m", emb.backward_start),
+            ] + top_wgrad + [
+                ("m", self._m_allreduce_top_start),
+                ("c", self._s_bottom_bwd),
+                ("m", self._m_allreduce_start),
+                ("m", emb.backward_wait),
+                ("c", self._s_emb_update),
+                ("m", self._m_load_next),
+            ] + prep + [
+                ("m", self._m_ids_exchange_next),
+                ("m", self._m_allreduce_wait),
+                ("c", self._s_dense_update),
+            ]
         return prep + [
             ("m", emb.stage_fwd_ids_exchange),
             lookup,
@@ -677,6 +738,8 @@ class DLRMTrainer:
 
     def step(self):
         """One training step on the batch in the static buffers."""
+        if self.pipeline and not self._primed:
+            raise RuntimeError("pipelined trainer: call prime(first batch) before step()")
         if self.graph is not None:
             if isinstance(self.graph, list):
                 for kind, item in self.graph:

@@ -432,18 +432,30 @@ class ShardedEmbeddingBags:
             ops.rw_bucketize(ids, self.rw_meta, self.nrw, self.world, self.B, self.rw_cap,
                              self.rw_n, self.rw_send, self.rw_ws, self.rw_overflow)
 
-    def stage_fwd_ids_exchange(self):
+    def stage_fwd_ids_exchange(self, async_op: bool = False):
+        """Id exchange (input dist). async_op: the collectives are left in
+        flight (the pipelined trainer overlaps them with the previous step's
+        dense update) until ``ids_exchange_wait``."""
         W = self.world
+        works = []
         if self.dp_tables and W > 1 and not self.dp_dense:
-            dist.all_gather_into_tensor(self.dp_g_ids, self.dp_ids, group=self.group)
+            works.append(dist.all_gather_into_tensor(self.dp_g_ids, self.dp_ids, group=self.group,
+                                                     async_op=async_op))
         if W > 1 and not self.tw_identity:
-            _a2a(self.tw_recv_ids, self.tw_send_ids, [self.tw_recv_count] * W,
-                 self.tw_send_counts, self.group)
+            works.append(_a2a(self.tw_recv_ids, self.tw_send_ids, [self.tw_recv_count] * W,
+                              self.tw_send_counts, self.group, async_op=async_op))
         if W > 1 and self.cw_tables:
-            _a2a(self.cw_recv_ids, self.cw_send_ids, [self.cw_recv_count] * W,
-                 self.cw_send_counts, self.group)
+            works.append(_a2a(self.cw_recv_ids, self.cw_send_ids, [self.cw_recv_count] * W,
+                              self.cw_send_counts, self.group, async_op=async_op))
         if W > 1 and self.rw_tables:
-            dist.all_to_all_single(self.rw_recv, self.rw_send, group=self.group)
+            works.append(dist.all_to_all_single(self.rw_recv, self.rw_send, group=self.group,
+                                                async_op=async_op))
+        self._ids_works = [w for w in works if w is not None] if async_op else []
+
+    def ids_exchange_wait(self):
+        for w in getattr(self, "_ids_works", None) or ():
+            w.wait()
+        self._ids_works = []
 
     def stage_fwd_lookup(self):
         W, B = self.world, self.B

@@ -19,7 +19,7 @@ B = 256
 STEPS = 3
 
 
-def _worker(rank, world, Bk, strategy, graph, rw_comm, emb_opt="rowwise_adagrad"):
+def _worker(rank, world, Bk, strategy, graph, rw_comm, emb_opt="rowwise_adagrad", pipeline=False):
     from tdfo_amd.data.synthetic import SyntheticCriteo
     from tdfo_amd.models.dlrm import DLRMConfig, DLRMTrainer
     from tdfo_amd.parallel.dist import get_info
@@ -27,7 +27,7 @@ def _worker(rank, world, Bk, strategy, graph, rw_comm, emb_opt="rowwise_adagrad"
     dev = get_info().device if world > 1 else torch.device("cuda", 0)
     cfg = DLRMConfig(embedding_dim=64, table_rows=ROWS, bottom=[128, 64], top=[128, 64, 1],
                      dense_opt="sgd", dense_lr=0.05, emb_lr=0.05, sharding=strategy,
-                     pooling=POOL, rw_comm=rw_comm, emb_opt=emb_opt)
+                     pooling=POOL, rw_comm=rw_comm, emb_opt=emb_opt, pipeline=pipeline)
     tr = DLRMTrainer(cfg, Bk, dev, group=get_info().group, rank=rank, world_size=world)
     g = torch.Generator().manual_seed(5)
     for t, r in enumerate(ROWS):
@@ -46,14 +46,24 @@ def _worker(rank, world, Bk, strategy, graph, rw_comm, emb_opt="rowwise_adagrad"
         batches.append((dense[sl].to(dev), torch.cat(parts).to(dev), label[sl].to(dev)))
     # two eager steps, then (graph) capture -- capture's warm-up replays the
     # last loaded batch, so the step sequence is the same in both modes
+    # pipelined input dist: step i runs on the batch loaded by step i - 1 (or
+    # prime()) and loads / exchanges batch i + 1 -- the same batch sequence
+    def feed(i):
+        if tr.pipeline:
+            tr.set_next_batch(*batches[i + 1])
+        else:
+            tr.load_batch(*batches[i])
+
+    if tr.pipeline:
+        tr.prime(*batches[0])
     for i in range(2):
-        tr.load_batch(*batches[i])
+        feed(i)
         tr.step()
     if graph:
         tr.capture_graph(warmup=0)
         assert tr.graph is not None
     for i in range(2, 2 + STEPS):
-        tr.load_batch(*batches[i])
+        feed(i)
         tr.step()
     torch.cuda.synchronize()
     loss = tr.pop_loss()
@@ -103,3 +113,21 @@ def test_two_ranks_match_one_process(strategy, graph, rw_comm, emb_opt, single):
             ref_w = tabs1[t][2][lo:lo + w.shape[0], c0:c0 + w.shape[1]]
             assert torch.allclose(w, ref_w, atol=tol, rtol=tol), (rank, t,
                                                                    float((w - ref_w).abs().max()))
+
+
+@pytest.mark.parametrize("strategy", ["table_wise", "auto"])
+def test_two_ranks_pipelined_input_dist(strategy, single):
+    """Input-dist pipelining (next batch's ids exchanged during the dense
+    update) on the staged hipGraphs: same result as one process."""
+    multi = run_distributed(_worker, 2, B, strategy, True, "bf16", "rowwise_adagrad", True,
+                            device="cuda", timeout=600)
+    p1, tabs1, loss1 = single("rowwise_adagrad")
+    tol = 3e-3
+    loss = multi[0][2] + multi[1][2]
+    assert abs(loss - loss1) / abs(loss1) < tol, (loss, loss1)
+    for rank in range(2):
+        p, tabs, _ = multi[rank]
+        assert torch.allclose(p, p1, atol=tol, rtol=tol), (rank, float((p - p1).abs().max()))
+        for t, (lo, c0, w) in tabs.items():
+            ref_w = tabs1[t][2][lo:lo + w.shape[0], c0:c0 + w.shape[1]]
+            assert torch.allclose(w, ref_w, atol=tol, rtol=tol), (rank, t)

@@ -97,29 +97,41 @@ def test_sharded_embedding_fwd_bwd(strategy, world, dp_dense):
             assert torch.allclose(w, exp, atol=1e-2), (rank, t)
 
 
-def _dlrm_worker(rank, world, B, steps, strategy, emb_opt="rowwise_adagrad", rw_comm="fp32"):
+def _dlrm_worker(rank, world, B, steps, strategy, emb_opt="rowwise_adagrad", rw_comm="fp32",
+                 pipeline=False):
     from tdfo_amd.data.synthetic import SyntheticCriteo
     from tdfo_amd.models.dlrm import DLRMConfig, DLRMTrainer
     from tdfo_amd.parallel.dist import get_info
 
     cfg = DLRMConfig(embedding_dim=32, table_rows=ROWS, bottom=[64, 32], top=[64, 32, 1],
                      dense_lr=1e-2, emb_lr=0.05, sharding=strategy, pooling=[1, 2, 1, 1, 1],
-                     emb_opt=emb_opt, rw_comm=rw_comm)
+                     emb_opt=emb_opt, rw_comm=rw_comm, pipeline=pipeline)
     tr = DLRMTrainer(cfg, B, "cpu", group=get_info().group, rank=rank, world_size=world)
+    assert tr.pipeline == (pipeline and world > 1)
     g = torch.Generator().manual_seed(5)
     for t, r in enumerate(ROWS):
         tr.emb.set_table_weight(t, torch.randn(r, 32, generator=g) * 0.1)
     data = SyntheticCriteo(ROWS, B * world, pooling=cfg.pooling, device="cpu", seed=9)
-    for _ in range(steps):
-        dense, ids, label = data.next()
+
+    def local(batch):
+        dense, ids, label = batch
         # slice this rank's part of the global batch
         parts, off = [], 0
         for t, Lt in enumerate(cfg.pooling):
             n = B * world * Lt
             parts.append(ids[off:off + n].view(B * world, Lt)[rank * B:(rank + 1) * B].reshape(-1))
             off += n
-        tr.load_batch(dense[rank * B:(rank + 1) * B], torch.cat(parts),
-                      label[rank * B:(rank + 1) * B])
+        return (dense[rank * B:(rank + 1) * B].clone(), torch.cat(parts),
+                label[rank * B:(rank + 1) * B].clone())
+
+    batches = [local(data.next()) for _ in range(steps + 1)]
+    if tr.pipeline:
+        tr.prime(*batches[0])
+    for i in range(steps):
+        if tr.pipeline:
+            tr.set_next_batch(*batches[i + 1])
+        else:
+            tr.load_batch(*batches[i])
         tr.step()
     tabs = {}
     for t in range(len(ROWS)):
@@ -145,3 +157,20 @@ def test_dlrm_data_parallel_matches_single_process(strategy):
         for t, (lo, c0, w) in tabs.items():
             ref = tabs1[t][2][lo:lo + w.shape[0], c0:c0 + w.shape[1]]
             assert torch.allclose(w, ref, atol=2e-4), (rank, t, (w - ref).abs().max())
+
+
+@pytest.mark.parametrize("strategy", ["table_wise", "row_wise", "auto"])
+def test_dlrm_pipelined_input_dist_is_exact(strategy):
+    """Input-dist pipelining (next batch's ids exchanged during this step's
+    dense update) changes only when the exchange runs: parameters and tables
+    after 4 steps equal the unpipelined run bit for bit."""
+    B, steps = 8, 4
+    plain = run_distributed(_dlrm_worker, 2, B, steps, strategy, "rowwise_adagrad", "fp32", False)
+    piped = run_distributed(_dlrm_worker, 2, B, steps, strategy, "rowwise_adagrad", "fp32", True)
+    for rank in range(2):
+        p0, tabs0 = plain[rank]
+        p1, tabs1 = piped[rank]
+        assert torch.equal(p0, p1), (rank, (p0 - p1).abs().max())
+        assert tabs0.keys() == tabs1.keys()
+        for t in tabs0:
+            assert torch.equal(tabs0[t][2], tabs1[t][2]), (rank, t)
