@@ -691,16 +691,20 @@ __global__ __launch_bounds__(256) void emb_combine_kernel(
       if (keys[mid] == last) lo = mid + 1; else hi = mid;
     }
     const int64_t jlast = (lo - 1) / CH;
-    for (int64_t j0 = c + 1; j0 <= jlast; j0 += 8) {
-      float hv[8][EPL];
+    // HQ head partials in flight: a skewed table's runs span up to B/CH
+    // chunks (a 3-row table: ~85 per run at B = 8192), and this walk is the
+    // kernel's latency tail (8 in flight: 15 us per DLRM-1TB step)
+    constexpr int HQ = EPL <= 2 ? 32 : (EPL <= 4 ? 16 : 8);
+    for (int64_t j0 = c + 1; j0 <= jlast; j0 += HQ) {
+      float hv[HQ][EPL];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
+      for (int q = 0; q < HQ; ++q) {
         const int64_t j = min(j0 + q, jlast);
 #pragma unroll
         for (int u = 0; u < EPL; ++u) hv[q][u] = head[j * D + e0c + u];
       }
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
+      for (int q = 0; q < HQ; ++q) {
         if (j0 + q <= jlast && act) {
 #pragma unroll
           for (int u = 0; u < EPL; ++u) acc[u] += hv[q][u];

@@ -381,6 +381,12 @@ class DLRMTrainer:
         self.pipeline = bool(cfg.pipeline) and world_size > 1 and self._es is None
         self._next = None
         self._primed = False
+        # one process: per-stream hipGraphs (capture_graph(streams=True)); the
+        # embedding lookup / sort / update replay on their own stream beside
+        # the MLP graphs, joined by events (set while capturing/replaying)
+        self._mstream = False
+        self._ms_wgrad = False
+        self._ms = None
 
     # for tests / checkpoints: (weight [out, in_real], bias [out]) views
     def weight(self, name: str):
@@ -605,7 +611,7 @@ class DLRMTrainer:
         emb = self.emb
         self._join(self._es)
         self._join(self._ls)
-        if self._ps is not None:
+        if self._ps is not None and not self._mstream:
             self._ps.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(self._ps):
                 emb.stage_bwd_prepare()
@@ -644,7 +650,8 @@ class DLRMTrainer:
             self._dcn_backward(h)
         emb.stage_bwd_local(self.emb_hyper)        # replicated tables' dense grads
         self._join(self._ws)
-        self._join(self._ps)
+        if not self._mstream:
+            self._join(self._ps)
 
     def _s_top_wgrad(self):
         """Top-MLP weight grads, deferred past the interaction backward when the
@@ -740,7 +747,9 @@ class DLRMTrainer:
         """One training step on the batch in the static buffers."""
         if self.pipeline and not self._primed:
             raise RuntimeError("pipelined trainer: call prime(first batch) before step()")
-        if self.graph is not None:
+        if self.graph == "streams":
+            self._ms_step()
+        elif self.graph is not None:
             if isinstance(self.graph, list):
                 for kind, item in self.graph:
                     item.replay() if kind == "c" else item()
@@ -750,10 +759,106 @@ class DLRMTrainer:
             self._forward_backward()
         self.steps += 1
 
-    def capture_graph(self, warmup: int = 2, staged: Optional[bool] = None):
+    # ------------------------------------------------ per-stream graphs
+    # The HIP runtime replays one captured graph's independent branches
+    # mostly in order on its own queue (profiles/dlrm1tb_b8192_graph_kernels:
+    # the embedding lookup and the bottom MLP ran back to back), so a single
+    # process instead captures six graphs, three per stream, and replays them
+    # on two streams joined by events: the memory-bound embedding work
+    # (lookup, sort, fused update) runs on the side stream concurrently with
+    # the latency-bound MLP GEMMs.
+    def _ms_plan(self):
+        emb = self.emb
+
+        def e1():
+            if not emb.fwd_prep_noop:
+                emb.stage_fwd_prep(self.ids)
+            emb.stage_fwd_ids_exchange()
+            emb.stage_fwd_lookup()
+            emb.stage_fwd_out_exchange()
+            emb.forward_wait()
+
+        def e3():
+            emb.backward_start()
+            emb.backward_wait()
+            self._s_emb_update()
+
+        def m3():
+            self._s_bottom_bwd()
+            if not self._ms_wgrad:
+                self._s_dense_update()
+        plan = {"E1": e1, "E2": emb.stage_bwd_prepare, "M1": self._s_bottom_fwd,
+                "M2": self._s_top, "E3": e3, "M3": m3}
+        if self._ms_wgrad:
+            plan["W"] = self._s_top_wgrad
+            plan["M4"] = self._s_dense_update
+        return plan
+
+    def _ms_step(self):
+        g, se, sw, ev = (self._ms["graphs"], self._ms["stream"], self._ms["wstream"],
+                         self._ms["events"])
+        main = torch.cuda.current_stream()
+        ev[0].record(main)
+        se.wait_event(ev[0])                 # this step's batch is loaded
+        with torch.cuda.stream(se):
+            g["E1"].replay()
+            ev[1].record(se)
+            g["E2"].replay()
+        g["M1"].replay()
+        main.wait_event(ev[1])               # pooled embeddings ready
+        g["M2"].replay()
+        ev[2].record(main)
+        se.wait_event(ev[2])                 # embedding gradients ready
+        with torch.cuda.stream(se):
+            g["E3"].replay()
+            ev[3].record(se)
+        if sw is not None:                   # top weight grads on a third stream
+            sw.wait_event(ev[2])
+            with torch.cuda.stream(sw):
+                g["W"].replay()
+                ev[4].record(sw)
+        g["M3"].replay()
+        if sw is not None:
+            main.wait_event(ev[4])
+            g["M4"].replay()
+        main.wait_event(ev[3])               # the next batch may overwrite the ids
+
+    def _capture_streams(self, wgrad_stream: bool = False):
+        assert self.world == 1 and self._es is None and self._ls is None
+        self._mstream = True
+        # top weight grads deferred past the interaction backward, onto their
+        # own stream beside the embedding update and the bottom backward
+        self._ms_wgrad = wgrad_stream and self.cfg.interaction == "dot"
+        self._defer_top_wgrad = self._defer_top_wgrad or self._ms_wgrad
+        plan = self._ms_plan()
+        se = torch.cuda.Stream(device=self.device)
+        sw = torch.cuda.Stream(device=self.device) if self._ms_wgrad else None
+        pool = torch.cuda.graph_pool_handle()
+        graphs = {}
+        main = torch.cuda.current_stream()
+        se.wait_stream(main)
+        if sw is not None:
+            sw.wait_stream(main)
+        for name in plan:
+            gr = torch.cuda.CUDAGraph()
+            # (the MLP graphs capture on torch's own side stream: capture is
+            # not allowed on the default stream; replays run on any stream)
+            st = se if name[0] == "E" else (sw if name == "W" else None)
+            with torch.cuda.graph(gr, pool=pool, stream=st):
+                plan[name]()
+            graphs[name] = gr
+        torch.cuda.synchronize()
+        self._ms = {"graphs": graphs, "stream": se, "wstream": sw,
+                    "events": [torch.cuda.Event() for _ in range(5)]}
+        self.graph = "streams"
+
+    def capture_graph(self, warmup: int = 2, staged: Optional[bool] = None,
+                      streams: Optional[bool] = None):
         """Capture the step into hipGraphs. Single process: one graph for the
-        whole step. Multi-process: one graph per compute stage, with the RCCL
-        exchanges issued eagerly between replays (they overlap the next stage)."""
+        whole step, or (streams=True, default from TDFO_STREAM_GRAPHS) per-
+        stream graphs replayed on two streams. Multi-process: one graph per
+        compute stage, with the RCCL exchanges issued eagerly between replays
+        (they overlap the next stage)."""
         assert self.device.type == "cuda"
         if not self.emb.graph_capturable:
             return
@@ -766,6 +871,12 @@ class DLRMTrainer:
         torch.cuda.synchronize()
         if staged is None:
             staged = self.world > 1
+        if streams is None:
+            streams = os.environ.get("TDFO_STREAM_GRAPHS", "1") in ("1", "2")
+        if (not staged and streams and self.world == 1 and self._es is None
+                and self._ls is None):
+            self._capture_streams(wgrad_stream=os.environ.get("TDFO_STREAM_GRAPHS") == "2")
+            return
         if not staged:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
