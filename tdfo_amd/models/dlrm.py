@@ -875,6 +875,8 @@ class DLRMTrainer:
             streams = os.environ.get("TDFO_STREAM_GRAPHS", "1") in ("1", "2")
         if (not staged and streams and self.world == 1 and self._es is None
                 and self._ls is None):
+            # (in-graph cross-stream event nodes would save the graph
+            # boundaries, but torch-ROCm refuses external events)
             self._capture_streams(wgrad_stream=os.environ.get("TDFO_STREAM_GRAPHS") == "2")
             return
         if not staged:
