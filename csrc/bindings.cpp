@@ -384,6 +384,26 @@ void seq_prologue_bwd(const Tensor& x, const Tensor& pos, const Tensor& g, int64
                          cur_stream());
 }
 
+void rank_metrics(const Tensor& h, const Tensor& W, const Tensor& bias, const Tensor& cand,
+                  at::IntArrayRef ks, const Tensor& out) {
+  check_f32c(h, "h"); check_f32c(W, "W"); check_f32c(bias, "bias"); check_f32c(out, "out");
+  check_dev(cand, "cand");
+  TORCH_CHECK(h.dim() == 2 && W.dim() == 2 && h.size(1) == W.size(1), "rank_metrics: h [B,E], W [V,E]");
+  const int64_t B = h.size(0), E = h.size(1);
+  TORCH_CHECK(cand.scalar_type() == at::kLong && cand.dim() == 2 && cand.size(0) == B &&
+              cand.is_contiguous() && cand.size(1) >= 1, "rank_metrics: cand int64 [B, C]");
+  TORCH_CHECK(bias.numel() == W.size(0), "rank_metrics: bias [V]");
+  TORCH_CHECK(aligned16(h.data_ptr()) && aligned16(W.data_ptr()), "rank_metrics: 16-B aligned rows");
+  const int nk = (int)ks.size();
+  TORCH_CHECK(nk >= 1 && nk <= 8 && out.numel() == 2 * nk + 1, "rank_metrics: 1..8 cutoffs, out [2nk+1]");
+  tdfo::RankKs k{};
+  for (int i = 0; i < nk; ++i) k.k[i] = (int)ks[i];
+  Tensor part = at::empty({(int64_t)tdfo::rank_metrics_parts((int)B) * (2 * nk + 1)}, out.options());
+  tdfo::rank_metrics(h.data_ptr<float>(), W.data_ptr<float>(), bias.data_ptr<float>(),
+                     cand.data_ptr<int64_t>(), (int)B, (int)cand.size(1), (int)E, k, nk,
+                     part.data_ptr<float>(), out.data_ptr<float>(), cur_stream());
+}
+
 // ---------------------------------------------------------- batch gather
 void gather_columns(at::TensorList src, const c10::optional<Tensor>& idx, int64_t row0, int64_t n,
                     at::TensorList dst, at::IntArrayRef dst_stride) {
@@ -1042,6 +1062,7 @@ TORCH_LIBRARY(tdfo, m) {
   m.def("seq_prologue_bwd(Tensor x, Tensor pos, Tensor g, int n, Tensor gamma, Tensor mean, "
         "Tensor rstd, float rate, int seed, Tensor? step, Tensor(a!) dx, Tensor(b!) part, "
         "Tensor(c!) out3) -> ()");
+  m.def("rank_metrics(Tensor h, Tensor W, Tensor bias, Tensor cand, int[] ks, Tensor(a!) out) -> ()");
   m.def("layernorm_parts(int M) -> int", [](int64_t M) { return (int64_t)tdfo::layernorm_parts(M); });
   m.def("gather_columns(Tensor[] src, Tensor? idx, int row0, int n, Tensor(a!)[] dst, int[] dst_stride) -> ()");
   m.def("concat_features(Tensor dense, Tensor emb, int[] off, int[] stride, int F, int D, "
@@ -1118,6 +1139,7 @@ TORCH_LIBRARY_IMPL(tdfo, CUDA, m) {
   m.impl("layernorm_fwd", layernorm_fwd);
   m.impl("layernorm_bwd", layernorm_bwd);
   m.impl("seq_prologue_fwd", seq_prologue_fwd);
+  m.impl("rank_metrics", rank_metrics);
   m.impl("seq_prologue_bwd", seq_prologue_bwd);
   m.impl("gather_columns", gather_columns);
   m.impl("concat_features", concat_features);

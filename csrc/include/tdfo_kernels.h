@@ -313,6 +313,17 @@ void encoder_layer_fwd(const EncArgs& a, hipStream_t s);
 // dbe2 | dW1 | db1 | dW2 | db2]
 void encoder_layer_bwd(const EncArgs& a, float* grad, hipStream_t s);
 
+// ------------------------------------------------------ ranking (eval) ----
+// Bert4Rec-style candidate ranking: per sample b, scores of candidates
+// cand[b, 0..C) = h[b] . W[cand] + bias[cand] (candidate 0 = the positive),
+// rank = #negatives scoring >= the positive; out[0..2nk] = sums over samples
+// of [rank < k_i (i < nk) | (rank < k_i) / log2(rank + 2) | 1].
+struct RankKs { int k[8]; };
+int rank_metrics_parts(int B);
+void rank_metrics(const float* h, const float* W, const float* bias, const int64_t* cand, int B,
+                  int C, int E, const RankKs& ks, int nk, float* part, float* out,
+                  hipStream_t s);
+
 // ------------------------------------------------------- layernorm ----
 // Row LayerNorm over the last n <= 1024 elements (layernorm.hip).
 int layernorm_parts(int64_t M);

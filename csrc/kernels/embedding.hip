@@ -237,7 +237,14 @@ __global__ void emb_keys_kernel(const EmbBwdArgs a, K* __restrict__ keys,
 constexpr int SEG_MAX = 8192;
 constexpr int SEG_THREADS = 1024;
 constexpr int SEG_K = SEG_MAX / SEG_THREADS;        // elements per thread
-constexpr int SEG_BITS = 6;
+// 6-bit digits. 7-bit ones (4 passes for a 26-bit table instead of 5, 64 KiB
+// of counters) measured slower: fused one-hot backward 123.6 vs 109.1 us at
+// 26 x 8192 ids (scripts/bench_segsort.py), the bigger scans cost more than
+// the saved pass.
+#ifndef TDFO_SEG_BITS
+#define TDFO_SEG_BITS 6
+#endif
+constexpr int SEG_BITS = TDFO_SEG_BITS;
 constexpr int SEG_BINS = 1 << SEG_BITS;
 constexpr int SEG_WAVES = SEG_THREADS / 64;
 constexpr int SEG_CNT = SEG_BINS * SEG_K * SEG_WAVES;   // 8192 counters

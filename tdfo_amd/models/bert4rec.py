@@ -559,6 +559,13 @@ class Bert4RecTrainer:
         else:
             seqs_p = seqs
         h = self.model.encode(self._embed(seqs_p), seqs_p)[:B, -1, :]         # [B, E]
+        if h.is_cuda and self.E in (16, 32, 64):
+            # one fused scoring + ranking kernel (ranking.hip): no [B, C] scores
+            out = torch.empty(2 * len(METRICS_K) + 1, dtype=torch.float32, device=h.device)
+            ops.rank_metrics(h.contiguous(), self.model.out.weight.detach(),
+                             self.model.out.bias.detach(), candidates.contiguous(), METRICS_K, out)
+            self.metric_sums += out.double()
+            return
         w = self.model.out.weight[candidates]                                # [B, C, E]
         scores = torch.einsum("bce,be->bc", w, h) + self.model.out.bias[candidates]
         self.metric_sums[:-1] += recall_ndcg_sums(scores).double()

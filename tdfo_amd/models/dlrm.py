@@ -831,6 +831,8 @@ class DLRMTrainer:
         self._ms_wgrad = wgrad_stream and self.cfg.interaction == "dot"
         self._defer_top_wgrad = self._defer_top_wgrad or self._ms_wgrad
         plan = self._ms_plan()
+        # (stream priorities -- MLP graphs high, embedding graphs low -- were
+        # measured at 1.9 ms/step vs 0.556: not used)
         se = torch.cuda.Stream(device=self.device)
         sw = torch.cuda.Stream(device=self.device) if self._ms_wgrad else None
         pool = torch.cuda.graph_pool_handle()

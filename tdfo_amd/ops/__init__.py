@@ -469,6 +469,15 @@ def layernorm_fwd(x, n, eps, gamma, beta, y, mean, rstd):
         ref.layernorm_fwd(x, n, eps, gamma, beta, y, mean, rstd)
 
 
+def rank_metrics(h, W, bias, cand, ks, out):
+    """out[2 len(ks) + 1] = per-batch sums of [Recall@k.. | NDCG@k.. | count]
+    for candidates cand [B, C] (column 0 = positive) scored h . W[c] + b[c]."""
+    if _gpu(h):
+        _native().rank_metrics(h, W, bias, cand, list(ks), out)
+    else:
+        ref.rank_metrics(h, W, bias, cand, ks, out)
+
+
 def seq_prologue_fwd(x, pos, n, eps, gamma, beta, rate, seed, step, y, mean, rstd):
     """y = dropout(LN(x + pos)) over rows of n (Bert4Rec input block); the
     dropout mask is a counter hash of (seed, step[0], row, element)."""

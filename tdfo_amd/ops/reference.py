@@ -642,6 +642,16 @@ def layernorm_bwd(x, g, n, gamma, mean, rstd, dx, dgb):
     dgb[n:].copy_(gv.sum(0))
 
 
+def rank_metrics(h, W, bias, cand, ks, out):
+    wr = W[cand]                                                    # [B, C, E]
+    scores = (wr * h[:, None, :]).sum(-1) + bias[cand]
+    rank = (scores[:, 1:] >= scores[:, :1]).sum(1)
+    rec = [(rank < k).float().sum() for k in ks]
+    g = 1.0 / torch.log2(rank.float() + 2.0)
+    ndcg = [torch.where(rank < k, g, torch.zeros_like(g)).sum() for k in ks]
+    out.copy_(torch.stack(rec + ndcg + [torch.tensor(float(h.shape[0]), device=h.device)]))
+
+
 def seq_prologue_mul(M: int, n: int, rate: float, seed: int, step: int, device):
     """[M, n] dropout multiplier of the fused sequence prologue
     (csrc/kernels/layernorm.hip::pro_mul)."""

@@ -257,3 +257,22 @@ def test_seq_prologue_reference_matches_autograd():
     assert torch.allclose(out3[2 * n:], pr.grad, atol=1e-4)
     m = ref.seq_prologue_mul(M, n, 0.25, 5, 3, "cpu")
     assert abs(float((m == 0).float().mean()) - 0.25) < 0.02
+
+
+def test_rank_metrics_reference_matches_recall_ndcg():
+    """ops.rank_metrics (CPU reference of the fused eval kernel) equals the
+    trainer's scores -> recall_ndcg_sums path, ties included."""
+    from tdfo_amd import ops
+    from tdfo_amd.models.bert4rec import METRICS_K, recall_ndcg_sums
+
+    torch.manual_seed(0)
+    B, C, E, V = 37, 101, 16, 500
+    h, W, b = torch.randn(B, E), torch.randn(V, E), torch.randn(V)
+    cand = torch.randint(0, V, (B, C))
+    cand[:5, 7] = cand[:5, 0]                      # exact ties with the positive
+    out = torch.empty(2 * len(METRICS_K) + 1)
+    ops.rank_metrics(h, W, b, cand, METRICS_K, out)
+    scores = torch.einsum("bce,be->bc", W[cand], h) + b[cand]
+    exp = recall_ndcg_sums(scores)
+    assert torch.allclose(out[:-1], exp, atol=1e-4)
+    assert float(out[-1]) == B

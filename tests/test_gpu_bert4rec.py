@@ -100,3 +100,24 @@ def test_bert4rec_graph_replay_matches_eager():
     torch.cuda.synchronize()
     torch.testing.assert_close(a.opt.flat, b.opt.flat, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(a.item.weight, b.item.weight, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("E,C", [(16, 101), (32, 64), (64, 200)])
+def test_rank_metrics_kernel(E, C):
+    """Fused eval scoring + ranking kernel vs the fp32 reference (ties with the
+    positive rank it behind, as recall_ndcg_sums)."""
+    from tdfo_amd import ops
+    from tdfo_amd.ops import reference as ref
+
+    torch.manual_seed(1)
+    B, V = 1000, 5000
+    h = torch.randn(B, E, device="cuda")
+    W = torch.randn(V, E, device="cuda")
+    b = torch.randn(V, device="cuda")
+    cand = torch.randint(0, V, (B, C), device="cuda")
+    cand[:50, 3] = cand[:50, 0]
+    out = torch.empty(7, device="cuda")
+    ops.rank_metrics(h, W, b, cand, (10, 20, 50), out)
+    exp = torch.empty(7, device="cuda")
+    ref.rank_metrics(h, W, b, cand, (10, 20, 50), exp)
+    assert torch.allclose(out, exp, atol=1e-2), (out, exp)
