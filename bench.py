@@ -47,6 +47,8 @@ def parse(argv=None):
     ap.add_argument("--dist", default="uniform", choices=["uniform", "zipf"])
     ap.add_argument("--sharding", default="auto",
                     choices=["auto", "table_wise", "row_wise", "column_wise", "data_parallel"])
+    ap.add_argument("--dense-comm", default="fp32", choices=["fp32", "bf16"],
+                    help="N > 1: wire format of the dense-gradient all-reduce")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="N > 1: exchange each batch's ids inside its own step instead of "
                          "during the previous step's dense update")
@@ -130,10 +132,12 @@ def main(argv=None):
     pipe = world_env > 1 and not args.no_pipeline
     if args.model == "dlrm":
         cfg = DLRMConfig(table_rows=list(rows), sharding=args.sharding, pipeline=pipe,
+                         dense_comm=args.dense_comm,
                          overlap=(args.overlap if args.overlap == 'wgrad' else bool(args.overlap)))
     else:
         cfg = DLRMConfig(table_rows=list(rows), interaction="dcn", pooling=list(MLPERF_MULTIHOT),
                          top=[1024, 1024, 512, 256, 1], sharding=args.sharding, pipeline=pipe,
+                         dense_comm=args.dense_comm,
                          overlap=(args.overlap if args.overlap == 'wgrad' else bool(args.overlap)))
     B = args.batch
     t0 = time.time()

@@ -349,20 +349,28 @@ class _LinearXentFn(torch.autograd.Function):
         N = H.shape[0]
         dH = torch.empty_like(H)
         lossv = torch.empty(N, dtype=torch.float32, device=H.device)
-        dW = torch.empty_like(W)
-        db = torch.empty_like(b)
+        # unit gradient and W / b used nowhere else in the graph: the kernel
+        # writes their gradients straight into the (zeroed) .grad buffers
+        # instead of autograd accumulating returned tensors into them
+        direct = bool(unit_grad and W.grad is not None and b.grad is not None and
+                      W.grad.is_contiguous() and b.grad.is_contiguous())
+        dW = W.grad if direct else torch.empty_like(W)
+        db = b.grad if direct else torch.empty_like(b)
         loss = torch.empty(1, dtype=torch.float32, device=H.device)
         # the kernel also reduces the mean loss (and adds it to loss_acc)
         ops.linear_xent(H, W, b, labels, eps, PAD_ID, dH, lossv, dW, db, loss=loss,
                         loss_acc=loss_acc)
         ctx.save_for_backward(dH, dW, db)
         ctx.unit_grad = unit_grad
+        ctx.direct = direct
         return loss[0]
 
     @staticmethod
     def backward(ctx, g):
         dH, dW, db = ctx.saved_tensors
         if ctx.unit_grad:      # caller's promise: the loss is backward()'s root (g == 1)
+            if ctx.direct:
+                return dH, None, None, None, None, None, None
             return dH, dW, db, None, None, None, None
         return dH * g, dW * g, db * g, None, None, None, None
 
@@ -370,8 +378,10 @@ class _LinearXentFn(torch.autograd.Function):
 def linear_cross_entropy(H, W, b, labels, eps=0.1, loss_acc=None, unit_grad=False):
     """mean CE(ignore_index=0, label_smoothing=eps) of H @ W^T + b, fused.
     loss_acc (fp64 [1]): the kernel adds the loss to it. unit_grad: the
-    returned loss is the root of backward() (gradient exactly 1), so the
-    saved gradients are returned without the scaling launches."""
+    returned loss is the root of backward() (gradient exactly 1) and W / b
+    feed nothing else, so the saved gradients are returned without the
+    scaling launches -- and when W.grad / b.grad exist (the trainer's flat
+    gradient views, zeroed each step) they are written there directly."""
     return _LinearXentFn.apply(H.contiguous(), W, b, labels.contiguous(), eps, loss_acc,
                                unit_grad)
 

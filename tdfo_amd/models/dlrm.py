@@ -83,6 +83,8 @@ class DLRMConfig:
     sharding: str = "auto"                         # planner strategy
     rw_capacity: float = 1.25                      # row-wise segment capacity (x n/W, +256)
     rw_comm: str = "bf16"                          # row-wise reduce-scatter dtype (bf16 | fp32)
+    dense_comm: str = "fp32"                       # dense-grad all-reduce dtype (fp32 | bf16:
+    #   halves the bytes on xGMI; the sum of W bf16-rounded grads, as DDP's bf16 compress hook)
     pipeline: bool = False                         # W > 1: next batch's id exchange overlaps
     #   this step's dense update (input-dist pipelining; see DLRMTrainer.prime)
     overlap: object = False                        # side streams (GPU): False | True (wgrads +
@@ -215,6 +217,8 @@ class DLRMTrainer:
     def __init__(self, cfg: DLRMConfig, batch_size: int, device, group=None, rank: int = 0,
                  world_size: int = 1, plan: Optional[ShardingPlan] = None):
         self.cfg = cfg
+        if cfg.dense_comm not in ("fp32", "bf16"):
+            raise ValueError(f"dense_comm must be fp32 or bf16, got {cfg.dense_comm!r}")
         self.B = B = int(batch_size)
         self.device = dev = torch.device(device)
         self.group = group
@@ -673,17 +677,26 @@ class DLRMTrainer:
     # cross layers) right after the top backward, overlapping the bottom MLP
     # backward and the embedding update; the small bottom MLP after its
     # backward.
+    def _ar_issue(self, lo: int, hi: int):
+        g = self.fp.g[lo:hi]
+        if self.cfg.dense_comm == "bf16":
+            if getattr(self, "_g16", None) is None:
+                self._g16 = torch.empty(self.fp.g.numel(), dtype=torch.bfloat16,
+                                        device=self.device)
+            b = self._g16[lo:hi]
+            ops.cast_bf16(g, b)
+            return (dist.all_reduce(b, group=self.group, async_op=True), g, b)
+        return (dist.all_reduce(g, group=self.group, async_op=True), None, None)
+
     def _m_allreduce_top_start(self):
         self._ar_top = None
         if self.world > 1:
-            self._ar_top = dist.all_reduce(self.fp.g[self._ar_split:], group=self.group,
-                                           async_op=True)
+            self._ar_top = self._ar_issue(self._ar_split, self.fp.g.numel())
 
     def _m_allreduce_start(self):
         self._ar_work = None
         if self.world > 1:
-            self._ar_work = dist.all_reduce(self.fp.g[:self._ar_split], group=self.group,
-                                            async_op=True)
+            self._ar_work = self._ar_issue(0, self._ar_split)
 
     def _s_emb_update(self):
         self.emb.stage_bwd_update(self.emb_hyper)
@@ -692,7 +705,10 @@ class DLRMTrainer:
         for name in ("_ar_top", "_ar_work"):
             w = getattr(self, name, None)
             if w is not None:
-                w.wait()
+                work, g, b = w
+                work.wait()
+                if b is not None:                  # bf16 wire format -> fp32 grads
+                    g.copy_(b)
                 setattr(self, name, None)
 
     def _s_dense_update(self):
@@ -700,6 +716,17 @@ class DLRMTrainer:
         fp = self.fp
         ops.dense_optimizer(fp.p, fp.g, fp.m, fp.v, fp.p_bf16, self.dense_opt, self.dense_hyper,
                             wd=self.cfg.dense_wd, segments=self._segments)
+
+    def _dense_update_range(self, lo: int, hi: int):
+        """The fused dense optimizer over flat elements [lo, hi) (the same
+        elementwise update as _s_dense_update restricted to a range)."""
+        fp = self.fp
+        segs = [(st - lo, sl, S) for st, sl, S in self._segments if lo <= st < hi]
+        sl = slice(lo, hi)
+        ops.dense_optimizer(fp.p[sl], fp.g[sl], fp.m[sl] if fp.m is not None else None,
+                            fp.v[sl] if fp.v is not None else None,
+                            fp.p_bf16[sl] if fp.p_bf16 is not None else None, self.dense_opt,
+                            self.dense_hyper, wd=self.cfg.dense_wd, segments=segs)
 
     # DCN-v2 cross network: x_{l+1} = x0 * (U (V^T x_l) + b) + x_l. The
     # Hadamard product and the residual are fused into the U-GEMM epilogue
@@ -778,14 +805,24 @@ class DLRMTrainer:
             emb.stage_fwd_out_exchange()
             emb.forward_wait()
 
+        # the top-MLP (+ head, DCN) part of the dense optimizer needs only the
+        # top backward: it runs on the embedding stream after the embedding
+        # update, beside the bottom-MLP backward (TDFO_SPLIT_OPT=0: one pass)
+        split = (os.environ.get("TDFO_SPLIT_OPT", "1") == "1" and not self._ms_wgrad)
+        a, P = self._ar_split, self.fp.p.numel()
+
         def e3():
             emb.backward_start()
             emb.backward_wait()
             self._s_emb_update()
+            if split:
+                self._dense_update_range(a, P)
 
         def m3():
             self._s_bottom_bwd()
-            if not self._ms_wgrad:
+            if split:
+                self._dense_update_range(0, a)
+            elif not self._ms_wgrad:
                 self._s_dense_update()
         plan = {"E1": e1, "E2": emb.stage_bwd_prepare, "M1": self._s_bottom_fwd,
                 "M2": self._s_top, "E3": e3, "M3": m3}

@@ -98,14 +98,14 @@ def test_sharded_embedding_fwd_bwd(strategy, world, dp_dense):
 
 
 def _dlrm_worker(rank, world, B, steps, strategy, emb_opt="rowwise_adagrad", rw_comm="fp32",
-                 pipeline=False):
+                 pipeline=False, dense_comm="fp32"):
     from tdfo_amd.data.synthetic import SyntheticCriteo
     from tdfo_amd.models.dlrm import DLRMConfig, DLRMTrainer
     from tdfo_amd.parallel.dist import get_info
 
     cfg = DLRMConfig(embedding_dim=32, table_rows=ROWS, bottom=[64, 32], top=[64, 32, 1],
                      dense_lr=1e-2, emb_lr=0.05, sharding=strategy, pooling=[1, 2, 1, 1, 1],
-                     emb_opt=emb_opt, rw_comm=rw_comm, pipeline=pipeline)
+                     emb_opt=emb_opt, rw_comm=rw_comm, pipeline=pipeline, dense_comm=dense_comm)
     tr = DLRMTrainer(cfg, B, "cpu", group=get_info().group, rank=rank, world_size=world)
     assert tr.pipeline == (pipeline and world > 1)
     g = torch.Generator().manual_seed(5)
@@ -174,3 +174,24 @@ def test_dlrm_pipelined_input_dist_is_exact(strategy):
         assert tabs0.keys() == tabs1.keys()
         for t in tabs0:
             assert torch.equal(tabs0[t][2], tabs1[t][2]), (rank, t)
+
+
+def test_dlrm_bf16_dense_allreduce_close_to_fp32():
+    """dense_comm="bf16" (bf16 wire format for the dense-grad all-reduce)
+    tracks the fp32 all-reduce run closely; tables are unaffected by design
+    only through the dense path, so both are compared."""
+    B, steps = 8, 3
+    f32 = run_distributed(_dlrm_worker, 2, B, steps, "table_wise", "rowwise_adagrad", "fp32",
+                          False, "fp32")
+    b16 = run_distributed(_dlrm_worker, 2, B, steps, "table_wise", "rowwise_adagrad", "fp32",
+                          False, "bf16")
+    for rank in range(2):
+        p0, _ = f32[rank]
+        p1, _ = b16[rank]
+        assert not torch.equal(p0, p1)                     # the wire format is really bf16
+        d = (p0 - p1).abs()
+        # AdamW (lr 1e-2) normalises each update, so elements whose gradient
+        # is ~0 can move by up to lr per step either way: bound the worst case
+        # by 3 steps x lr and require the bulk to agree closely
+        assert float(d.max()) <= 3e-2 and float(d.mean()) < 1e-3, (float(d.max()), float(d.mean()))
+    assert torch.equal(b16[0][0], b16[1][0])               # replicas stay identical
