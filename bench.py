@@ -162,7 +162,10 @@ def main(argv=None):
             batch, slot = pf.next()
         else:
             batch, slot = pool[i % len(pool)], None
-        (tr.set_next_batch if tr.pipeline else tr.load_batch)(*batch)
+        if tr.pipeline:
+            tr.set_next_batch(*batch)
+        else:
+            tr.load_batch(*batch, on_device=pool is not None)
         return slot
 
     def run(n, start):

@@ -389,6 +389,7 @@ class DLRMTrainer:
         # embedding lookup / sort / update replay on their own stream beside
         # the MLP graphs, joined by events (set while capturing/replaying)
         self._mstream = False
+        self._early = os.environ.get("TDFO_EARLY_LOOKUP", "1") == "1"
         self._ms_wgrad = False
         self._ms = None
 
@@ -420,12 +421,30 @@ class DLRMTrainer:
         h[K] = 0.0
 
     # ------------------------------------------------------------ batches
-    def load_batch(self, dense: torch.Tensor, ids: torch.Tensor, label: torch.Tensor):
+    def load_batch(self, dense: torch.Tensor, ids: torch.Tensor, label: torch.Tensor,
+                   on_device: bool = False):
         """Copy a batch into the static input buffers (non_blocking H2D ok).
 
         dense [B, num_dense] (any float dtype), ids flat int64 in table order
-        (table t: B*L_t ids), label [B] float.
+        (table t: B*L_t ids), label [B] float. on_device: the tensors are
+        device-resident and ready for every stream (e.g. a pre-generated
+        pool); with per-stream graphs the ids are then copied on the
+        embedding stream right behind the previous step's embedding update,
+        so the next lookup overlaps the previous step's bottom-MLP backward.
         """
+        if self.graph == "streams" and self._early and ids.is_cuda \
+                and ids.dtype == torch.int64 and ids.is_contiguous() \
+                and ids.numel() == self.ids.numel():
+            se, ev = self._ms["stream"], self._ms["events"][0]
+            main = torch.cuda.current_stream()
+            if not on_device:
+                se.wait_stream(main)               # e.g. an H2D the caller ordered on main
+            with torch.cuda.stream(se):
+                self.ids.copy_(ids, non_blocking=True)
+                ev.record(se)
+            main.wait_event(ev)
+            ops.batch_load(dense, self.x0, ids[:0], self.ids[:0], label, self.label)
+            return
         # device-resident batch: one fused launch (ids, labels, dense -> bf16)
         ops.batch_load(dense, self.x0, ids, self.ids, label, self.label)
 
@@ -835,8 +854,11 @@ class DLRMTrainer:
         g, se, sw, ev = (self._ms["graphs"], self._ms["stream"], self._ms["wstream"],
                          self._ms["events"])
         main = torch.cuda.current_stream()
-        ev[0].record(main)
-        se.wait_event(ev[0])                 # this step's batch is loaded
+        if not self._early:
+            ev[0].record(main)
+            se.wait_event(ev[0])             # this step's batch is loaded (on main)
+        # (early lookup: this step's ids were copied on se by load_batch, so the
+        # lookup follows the previous step's embedding update on the same stream)
         with torch.cuda.stream(se):
             g["E1"].replay()
             ev[1].record(se)
