@@ -442,7 +442,8 @@ class DLRMTrainer:
             with torch.cuda.stream(se):
                 self.ids.copy_(ids, non_blocking=True)
                 ev.record(se)
-            main.wait_event(ev)
+            if not on_device:
+                main.wait_event(ev)                # dense / labels from the same source
             ops.batch_load(dense, self.x0, ids[:0], self.ids[:0], label, self.label)
             return
         # device-resident batch: one fused launch (ids, labels, dense -> bf16)
@@ -880,7 +881,18 @@ class DLRMTrainer:
         if sw is not None:
             main.wait_event(ev[4])
             g["M4"].replay()
-        main.wait_event(ev[3])               # the next batch may overwrite the ids
+        if not self._early:
+            main.wait_event(ev[3])           # the next batch (loaded on main) rewrites the ids
+        # early lookup: no end-of-step join -- the embedding stream's next work
+        # (ids copy, lookup) is ordered behind this update on that stream, and
+        # the next MLP graphs wait for the next lookup; readers of tables /
+        # params outside step() call sync_streams() first
+
+    def sync_streams(self):
+        """Order the current stream after all side-stream work of issued steps
+        (embedding updates, the top-MLP optimizer part)."""
+        if self._ms is not None:
+            torch.cuda.current_stream().wait_stream(self._ms["stream"])
 
     def _capture_streams(self, wgrad_stream: bool = False):
         assert self.world == 1 and self._es is None and self._ls is None
@@ -972,6 +984,7 @@ class DLRMTrainer:
     def pop_loss(self) -> float:
         """Mean training loss since the last call (one device->host read);
         also raises if a row-wise exchange overflowed meanwhile."""
+        self.sync_streams()
         self.emb.check_overflow()
         v = float(self.loss_sum.item())
         self.loss_sum.zero_()
@@ -981,6 +994,7 @@ class DLRMTrainer:
     @torch.no_grad()
     def predict(self) -> torch.Tensor:
         """Forward only on the static batch; returns logits [B] (fp32)."""
+        self.sync_streams()
         cfg = self.cfg
         self.emb.forward(self.ids)
         self._s_bottom_fwd()
@@ -1005,6 +1019,7 @@ class DLRMTrainer:
 
     def dense_state(self):
         """Replicated training state (dense params, moments, step counters)."""
+        self.sync_streams()
         d = {"p": self.fp.p, "dense_hyper": self.dense_hyper, "emb_hyper": self.emb_hyper}
         if self.fp.m is not None:
             d["m"] = self.fp.m

@@ -91,6 +91,8 @@ def save(tr, dirpath: str, step: int, rank: int, world: int, meta: Optional[Dict
     barrier, the manifest (last, atomically)."""
     d = Path(dirpath)
     d.mkdir(parents=True, exist_ok=True)
+    if hasattr(tr, "sync_streams"):
+        tr.sync_streams()                  # side-stream table updates of issued steps
     index = []
     for p in local_pieces(tr.emb):
         if p["replicated"] and rank != 0:
