@@ -558,6 +558,11 @@ class DLRMTrainer:
             # this batch's ids were exchanged during the previous step (or by
             # prime()); the next batch is loaded + exchanged after the
             # embedding update, overlapping the dense optimizer step
+            # Multi-GPU side stream ("e" compute / "em" comm stages run on the
+            # embedding stream, "j" joins it back): the embedding update and
+            # the next batch's load, bucketize and id exchange run beside the
+            # dense-gradient all-reduce wait and the dense optimizer step.
+            eprep = [("e", k[1]) for k in prep]
             return [
                 ("m", emb.ids_exchange_wait),
                 lookup,
@@ -571,12 +576,13 @@ class DLRMTrainer:
                 ("c", self._s_bottom_bwd),
                 ("m", self._m_allreduce_start),
                 ("m", emb.backward_wait),
-                ("c", self._s_emb_update),
-                ("m", self._m_load_next),
-            ] + prep + [
-                ("m", self._m_ids_exchange_next),
+                ("e", self._s_emb_update),
+                ("em", self._m_load_next),
+            ] + eprep + [
+                ("em", self._m_ids_exchange_next),
                 ("m", self._m_allreduce_wait),
                 ("c", self._s_dense_update),
+                ("j", None),
             ]
         return prep + [
             ("m", emb.stage_fwd_ids_exchange),
@@ -591,14 +597,42 @@ class DLRMTrainer:
             ("c", self._s_bottom_bwd),
             ("m", self._m_allreduce_start),      # bottom bucket
             ("m", emb.backward_wait),
-            ("c", self._s_emb_update),
+            ("e", self._s_emb_update),           # beside the all-reduce wait + dense step
             ("m", self._m_allreduce_wait),
             ("c", self._s_dense_update),
+            ("j", None),
         ]
 
+    # side stream of the multi-process stage lists ("e" / "em" / "j" stages)
+    def _side(self):
+        if self.device.type != "cuda" or self.world == 1:
+            return None
+        if getattr(self, "_sides", None) is None:
+            self._sides = torch.cuda.Stream(device=self.device)
+        return self._sides
+
+    def _run_stage(self, kind, fn, graph=None):
+        """Run (or replay) one stage on its stream; forks the side stream off
+        the current stream at the first side stage after main-stream work."""
+        se = self._side()
+        if kind == "j":
+            if se is not None:
+                torch.cuda.current_stream().wait_stream(se)
+            self._on_side = False
+            return
+        if kind in ("e", "em") and se is not None:
+            if not getattr(self, "_on_side", False):
+                se.wait_stream(torch.cuda.current_stream())
+                self._on_side = True
+            with torch.cuda.stream(se):
+                graph.replay() if graph is not None else fn()
+            return
+        graph.replay() if graph is not None else fn()
+
     def _forward_backward(self):
-        for _, fn in self._stages():
-            fn()
+        self._on_side = False
+        for kind, fn in self._stages():
+            self._run_stage(kind, fn)
 
     def _s_bottom_fwd(self):
         n = len(self.bottom_layers)
@@ -798,8 +832,12 @@ class DLRMTrainer:
             self._ms_step()
         elif self.graph is not None:
             if isinstance(self.graph, list):
+                self._on_side = False
                 for kind, item in self.graph:
-                    item.replay() if kind == "c" else item()
+                    if kind in ("c", "e"):
+                        self._run_stage(kind, None, graph=item)
+                    else:
+                        self._run_stage(kind, item)
             else:
                 self.graph.replay()
         else:
@@ -893,6 +931,8 @@ class DLRMTrainer:
         (embedding updates, the top-MLP optimizer part)."""
         if self._ms is not None:
             torch.cuda.current_stream().wait_stream(self._ms["stream"])
+        if getattr(self, "_sides", None) is not None:
+            torch.cuda.current_stream().wait_stream(self._sides)
 
     def _capture_streams(self, wgrad_stream: bool = False):
         assert self.world == 1 and self._es is None and self._ls is None
@@ -964,20 +1004,29 @@ class DLRMTrainer:
         # span them); each RCCL exchange sits between two graphs
         groups: list = []
         for kind, fn in self._stages():
-            if kind == "c" and groups and groups[-1][0] == "c":
+            if kind in ("c", "e") and groups and groups[-1][0] == kind:
                 groups[-1][1].append(fn)
             else:
                 groups.append((kind, [fn]))
+        self._on_side = False
+        se = self._side()
         for kind, fns in groups:
-            if kind == "c":
+            if kind in ("c", "e"):
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g, pool=pool):
+                # thread_local: a backend's own worker thread (gloo's async
+                # device copies of a collective issued just before) must not
+                # invalidate this thread's capture
+                with torch.cuda.graph(g, pool=pool, stream=se if kind == "e" else None,
+                                      capture_error_mode="thread_local"):
                     for fn in fns:
                         fn()
-                seq.append(("c", g))
+                seq.append((kind, g))
             else:
-                fns[0]()      # dry exchange keeps every rank's collective sequence aligned
-                seq.append(("m", fns[0]))
+                # dry exchange keeps every rank's collective sequence aligned
+                self._run_stage(kind, fns[0])
+                seq.append((kind, fns[0]))
+        if se is not None:
+            torch.cuda.current_stream().wait_stream(se)
         torch.cuda.synchronize()
         self.graph = seq
 
