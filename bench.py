@@ -159,13 +159,14 @@ def main(argv=None):
         """Hand batch i to the trainer (pipelined: as the batch the next step
         runs on -- this step loads it after its embedding update)."""
         if pool is None:                       # host data plane: generation + H2D overlapped
-            batch, slot = pf.next()
+            # the H2D is ordered on every stream that reads the batch
+            batch, slot = pf.next(streams=None if tr.pipeline else tr.input_streams())
         else:
             batch, slot = pool[i % len(pool)], None
         if tr.pipeline:
             tr.set_next_batch(*batch)
         else:
-            tr.load_batch(*batch, on_device=pool is not None)
+            tr.load_batch(*batch, on_device=True)
         return slot
 
     def run(n, start):
@@ -173,7 +174,7 @@ def main(argv=None):
             slot = feed(start + i + 1 if tr.pipeline else start + i)
             tr.step()
             if slot is not None:               # the step has enqueued its reads of it
-                pf.release(slot)
+                pf.release(slot, streams=None if tr.pipeline else tr.input_streams())
 
     if tr.pipeline:
         if pool is None:

@@ -65,10 +65,11 @@ class HostPrefetcher:
             time.sleep(20e-6)       # poll: a spinning hipEventSynchronize steals a core
         self.futs[j] = self.pool.submit(self.gen.batch, j)   # ctypes: GIL released
 
-    def next(self) -> Tuple[Tuple[torch.Tensor, torch.Tensor, torch.Tensor], int]:
+    def next(self, streams=None) -> Tuple[Tuple[torch.Tensor, torch.Tensor, torch.Tensor], int]:
         """Device tensors (dense, ids, label) of the next batch (ordered on the
-        current stream) and their staging slot; call ``release(slot)`` once
-        the consumer has enqueued its reads of them."""
+        current stream, or on every stream of ``streams``) and their staging
+        slot; call ``release(slot)`` once the consumer has enqueued its reads
+        of them."""
         j = self.i
         self.i += 1
         t0 = time.perf_counter()
@@ -82,16 +83,17 @@ class HostPrefetcher:
             # hipMemcpyAsync block the launching thread until the GPU gets
             # there: measured 0.5 ms per step). With S above the depth the
             # launching thread runs ahead, this poll only bites as back-pressure.
-            ue = self.use_ev[s]
-            while ue is not None and not ue.query():
-                time.sleep(20e-6)
+            for ue in (self.use_ev[s] or ()):
+                while not ue.query():
+                    time.sleep(20e-6)
             with torch.cuda.stream(self.copy):
                 for d, h in zip(dst, host):
                     d.copy_(h, non_blocking=True)
                 ev = torch.cuda.Event()
                 ev.record(self.copy)
             self.h2d_ev[j % self.H] = ev
-            torch.cuda.current_stream(self.dev).wait_event(ev)
+            for st in (streams or [torch.cuda.current_stream(self.dev)]):
+                st.wait_event(ev)
         else:
             for d, h in zip(dst, host):
                 d.copy_(h)
@@ -100,11 +102,16 @@ class HostPrefetcher:
         self.t_submit += time.perf_counter() - t1
         return dst, s
 
-    def release(self, slot: int):
+    def release(self, slot: int, streams=None):
+        """``streams``: every stream that reads the slot (default: current);
+        the slot is refilled once each of them has passed this point."""
         if self.cuda:
-            e = torch.cuda.Event()
-            e.record(torch.cuda.current_stream(self.dev))
-            self.use_ev[slot] = e
+            evs = []
+            for st in (streams or [torch.cuda.current_stream(self.dev)]):
+                e = torch.cuda.Event()
+                e.record(st)
+                evs.append(e)
+            self.use_ev[slot] = evs
 
     def close(self):
         self.pool.shutdown(wait=True)

@@ -926,6 +926,14 @@ class DLRMTrainer:
         # the next MLP graphs wait for the next lookup; readers of tables /
         # params outside step() call sync_streams() first
 
+    def input_streams(self):
+        """Streams that read a batch handed to load_batch (a producer orders
+        its device copies on each, then passes on_device=True)."""
+        main = torch.cuda.current_stream()
+        if self.graph == "streams" and self._early:
+            return [main, self._ms["stream"]]
+        return [main]
+
     def sync_streams(self):
         """Order the current stream after all side-stream work of issued steps
         (embedding updates, the top-MLP optimizer part)."""
