@@ -404,6 +404,21 @@ void rank_metrics(const Tensor& h, const Tensor& W, const Tensor& bias, const Te
                      part.data_ptr<float>(), out.data_ptr<float>(), cur_stream());
 }
 
+// A HIP stream whose kernels may only use the CUs set in mask_words (bit i
+// of word w = CU 32 w + i). The embedding side stream uses it so its
+// memory-bound, many-block kernels leave CUs to the latency-bound GEMMs.
+// Returned as the raw handle for torch.cuda.ExternalStream (never destroyed:
+// one per trainer).
+int64_t cu_masked_stream(at::IntArrayRef mask_words) {
+  TORCH_CHECK(!mask_words.empty() && mask_words.size() <= 64, "cu_masked_stream: 1..64 words");
+  std::vector<uint32_t> m(mask_words.size());
+  for (size_t i = 0; i < m.size(); ++i) m[i] = (uint32_t)mask_words[i];
+  hipStream_t st = nullptr;
+  const hipError_t e = hipExtStreamCreateWithCUMask(&st, (uint32_t)m.size(), m.data());
+  TORCH_CHECK(e == hipSuccess, "hipExtStreamCreateWithCUMask: ", hipGetErrorString(e));
+  return (int64_t)(uintptr_t)st;
+}
+
 // ---------------------------------------------------------- batch gather
 void gather_columns(at::TensorList src, const c10::optional<Tensor>& idx, int64_t row0, int64_t n,
                     at::TensorList dst, at::IntArrayRef dst_stride) {
@@ -1063,6 +1078,7 @@ TORCH_LIBRARY(tdfo, m) {
         "Tensor rstd, float rate, int seed, Tensor? step, Tensor(a!) dx, Tensor(b!) part, "
         "Tensor(c!) out3) -> ()");
   m.def("rank_metrics(Tensor h, Tensor W, Tensor bias, Tensor cand, int[] ks, Tensor(a!) out) -> ()");
+  m.def("cu_masked_stream(int[] mask_words) -> int", cu_masked_stream);
   m.def("layernorm_parts(int M) -> int", [](int64_t M) { return (int64_t)tdfo::layernorm_parts(M); });
   m.def("gather_columns(Tensor[] src, Tensor? idx, int row0, int n, Tensor(a!)[] dst, int[] dst_stride) -> ()");
   m.def("concat_features(Tensor dense, Tensor emb, int[] off, int[] stride, int F, int D, "

@@ -942,6 +942,21 @@ class DLRMTrainer:
         if getattr(self, "_sides", None) is not None:
             torch.cuda.current_stream().wait_stream(self._sides)
 
+    def _emb_stream(self):
+        """Embedding side stream; TDFO_EMB_CU_KEEP=k (1..3) restricts it to k
+        of every 4 CUs (hipExtStreamCreateWithCUMask) so its memory-bound,
+        many-block kernels leave CUs to the MLP stream's small GEMMs."""
+        keep = int(os.environ.get("TDFO_EMB_CU_KEEP", "4"))
+        if keep >= 4:
+            return torch.cuda.Stream(device=self.device)
+        nib = (1 << keep) - 1
+        word = 0
+        for q in range(8):
+            word |= nib << (4 * q)
+        ncu = torch.cuda.get_device_properties(self.device).multi_processor_count
+        handle = ops.cu_masked_stream([word] * ((ncu + 31) // 32))
+        return torch.cuda.ExternalStream(handle, device=self.device)
+
     def _capture_streams(self, wgrad_stream: bool = False):
         assert self.world == 1 and self._es is None and self._ls is None
         self._mstream = True
@@ -952,7 +967,7 @@ class DLRMTrainer:
         plan = self._ms_plan()
         # (stream priorities -- MLP graphs high, embedding graphs low -- were
         # measured at 1.9 ms/step vs 0.556: not used)
-        se = torch.cuda.Stream(device=self.device)
+        se = self._emb_stream()
         sw = torch.cuda.Stream(device=self.device) if self._ms_wgrad else None
         pool = torch.cuda.graph_pool_handle()
         graphs = {}

@@ -469,6 +469,12 @@ def layernorm_fwd(x, n, eps, gamma, beta, y, mean, rstd):
         ref.layernorm_fwd(x, n, eps, gamma, beta, y, mean, rstd)
 
 
+def cu_masked_stream(mask_words) -> int:
+    """Raw handle of a new HIP stream restricted to the CUs in mask_words
+    (wrap with torch.cuda.ExternalStream)."""
+    return int(_native().cu_masked_stream(list(mask_words)))
+
+
 def rank_metrics(h, W, bias, cand, ks, out):
     """out[2 len(ks) + 1] = per-batch sums of [Recall@k.. | NDCG@k.. | count]
     for candidates cand [B, C] (column 0 = positive) scored h . W[c] + b[c]."""
