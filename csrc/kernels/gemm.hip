@@ -170,6 +170,11 @@ __device__ __forceinline__ TileIdx tile_of(int tiles_m, int tiles_n, int splits)
 // of 64 scalar writes).
 // Register-direct epilogue preconditions: whole tile in range, every touched
 // operand row 16-B aligned (8 bf16 / 4 fp32 columns).
+template <bool B>
+struct BoolC {
+  static constexpr bool value = B;
+};
+
 __device__ __forceinline__ bool al16(const void* q) { return ((uintptr_t)q & 15) == 0; }
 __device__ __forceinline__ bool direct_ok(const GemmArgs& p, int m0, int n0, int rows) {
   if (p.abl & (224 | 256)) return false;           // ablations / forced LDS path
@@ -292,16 +297,57 @@ __device__ __forceinline__ void epilogue(const GemmArgs& p, const f32x4_t (&acc)
     return;
   }
   float* ctile = (float*)smem_raw;   // [ROWS][128] fp32, 16-B chunks XOR-swizzled
-  __syncthreads();
+  // Epilogue operands (ReLU mask, DCN Hadamard / residual inputs) of the
+  // whole tile are loaded into registers here, before the accumulator LDS
+  // round trip: one memory round trip per block, hidden behind the staging,
+  // instead of one per unrolled pair of store-loop iterations (those loads
+  // were issued two at a time and waited on before each store). Addresses
+  // are clamped into the operand, so the loads are unconditional (no
+  // branch-around-load per element); the store loop drops out-of-range rows.
+  constexpr int IT = ROWS * 16 / NT;
+  // bias first: its loads must not queue behind the prefetch (vmcnt retires
+  // in issue order)
+  float bv[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = n0 + wc * 64 + j * 16 + 4 * (lane >> 4) + r;
+      bv[j][r] = (p.bias && n < p.N) ? p.bias[(int64_t)n * p.bias_stride] : 0.f;
+    }
+  const bool pf = !(p.abl & 1024) && (p.N & 7) == 0 &&
+                  (p.mask || (p.C2 && (p.mul || p.add)));
+  uint4 pk[IT], pm[IT], pa[IT];
+  if (pf) {
+    auto pf_load = [&](const uint16_t* base, int64_t ld, uint4 (&dst)[IT]) {
+#pragma unroll
+      for (int it = 0; it < IT; ++it) {
+        const int c = it * NT + tid;
+        const int m = min(m0 + (c >> 4), p.M - 1);
+        const int n = min(n0 + (c & 15) * 8, p.N - 8);
+        dst[it] = *(const uint4*)(base + (int64_t)m * ld + n);
+      }
+    };
+    if (p.mask) pf_load(p.mask, p.ldm, pk);
+    if (p.C2 && p.mul) pf_load(p.mul, p.ldmul, pm);
+    if (p.C2 && p.add) pf_load(p.add, p.ldadd, pa);
+  }
+  // with loads in flight, barriers that wait only for LDS traffic
+  // (__syncthreads would drain vmcnt first)
+  auto lds_barrier = [&]() {
+    if (pf) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    } else {
+      __syncthreads();
+    }
+  };
+  lds_barrier();
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int cl = wc * 64 + j * 16 + 4 * (lane >> 4);       // first of 4 columns
-    float bias[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int n = n0 + cl + r;
-      bias[r] = (p.bias && n < p.N) ? p.bias[(int64_t)n * p.bias_stride] : 0.f;
-    }
+    const float* bias = bv[j];
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
       const int rl = wr * (MI * 16) + i * 16 + (lane & 15);
@@ -315,11 +361,13 @@ __device__ __forceinline__ void epilogue(const GemmArgs& p, const f32x4_t (&acc)
       *(float4*)(ctile + rl * 128 + chunk * 4) = make_float4(v[0], v[1], v[2], v[3]);
     }
   }
-  __syncthreads();
+  lds_barrier();
   float* c32 = p.C32 ? p.C32 + (int64_t)split * p.M * p.ldc32 : nullptr;
   const bool nfull = (n0 + BN <= p.N) && ((p.N & 7) == 0);
-#pragma unroll 2
-  for (int it = 0; it < ROWS * 16 / NT; ++it) {
+  auto store_loop = [&](auto pf_on) {
+  constexpr bool PF = decltype(pf_on)::value;
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
     const int c = it * NT + tid;           // 8-column group id in the tile
     const int rl = c >> 4, cg = (c & 15) * 8;
     const int m = m0 + rl;
@@ -334,7 +382,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs& p, const f32x4_t (&acc)
     const int n = n0 + cg;
     if (nfull || n + 8 <= p.N) {
       if (p.mask) {
-        const uint4 mk = *(const uint4*)(p.mask + (int64_t)m * p.ldm + n);
+        const uint4 mk = PF ? pk[it] : *(const uint4*)(p.mask + (int64_t)m * p.ldm + n);
         const uint32_t mu[4] = {mk.x, mk.y, mk.z, mk.w};
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -352,7 +400,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs& p, const f32x4_t (&acc)
 #pragma unroll
         for (int q = 0; q < 8; ++q) w2[q] = v[q];
         if (p.mul) {
-          const uint4 mv = *(const uint4*)(p.mul + (int64_t)m * p.ldmul + n);
+          const uint4 mv = PF ? pm[it] : *(const uint4*)(p.mul + (int64_t)m * p.ldmul + n);
           const uint32_t mu[4] = {mv.x, mv.y, mv.z, mv.w};
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
@@ -361,7 +409,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs& p, const f32x4_t (&acc)
           }
         }
         if (p.add) {
-          const uint4 av = *(const uint4*)(p.add + (int64_t)m * p.ldadd + n);
+          const uint4 av = PF ? pa[it] : *(const uint4*)(p.add + (int64_t)m * p.ldadd + n);
           const uint32_t au[4] = {av.x, av.y, av.z, av.w};
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
@@ -393,6 +441,9 @@ __device__ __forceinline__ void epilogue(const GemmArgs& p, const f32x4_t (&acc)
       }
     }
   }
+  };
+  if (pf) store_loop(BoolC<true>{});
+  else    store_loop(BoolC<false>{});
 }
 
 // 16 MFMAs of one 64-deep K step for a wave's 64x64 sub-tile (two 32-deep
@@ -447,11 +498,6 @@ __device__ __forceinline__ void csum_store(const GemmArgs& p, const f32x4_t (&cs
     if (lane < 16 && m < p.M) c32[(int64_t)m * p.ldc32 + p.csum_col] = cs[h][0];
   }
 }
-
-template <bool B>
-struct BoolC {
-  static constexpr bool value = B;
-};
 
 // ---------------------------------------------------------------------------
 // Small-tile kernel: BMT x 128 x 64 (BMT = 128, or 64 for row-layout A when

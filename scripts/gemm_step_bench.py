@@ -81,7 +81,7 @@ def calls(tr: DLRMTrainer):
                 tr.dcn_dy, False, Uw[:, :u.in_k], True, None, False, None, tr.dcn_dh, None, 1)))
             out.append((f"dcn{i}", "V.wgrad", fl, lambda xi=xi, i=i: ops.linear_wgrad(
                 tr.dcn_dh, xi[:, :Wd], fp.grad(f"dcn{i}.v").view(-1),
-                splits=ops.wgrad_splits(r, Wd, B, tr._wg_target), slab=tr.slab)))
+                splits=tr._wg_splits(r, Wd), slab=tr.slab)))
             out.append((f"dcn{i}", "V.dgrad", fl, lambda V=V, i=i: ops.gemm(
                 tr.dcn_dh, False, V, True, None, False, None, None, None, 1,
                 add=tr.dcn_dx[i + 1], out2=tr.dcn_dx[i])))

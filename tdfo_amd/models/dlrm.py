@@ -326,9 +326,16 @@ class DLRMTrainer:
         self._wg_target = int(os.environ.get("TDFO_WGRAD_TARGET", 256 if dcn else 512))
         # TDFO_WGRAD_CSUM=0/1 overrides (A/B)
         self._csum = os.environ.get("TDFO_WGRAD_CSUM", "0" if dcn else "1") != "0"
+        # DCN-v2's weight grads run on the one-block-per-CU 256x128 kernel
+        # (policy 25, no column sums): splits sized for its 256 resident
+        # blocks (U wgrad 65 -> ? us, V 58 -> ? us; TDFO_WGRAD_SLOTS=0: the
+        # 128x128-tile target)
+        self._wg_slots = int(os.environ.get(
+            "TDFO_WGRAD_SLOTS", 256 if (dcn and not self._csum and dev.type == "cuda"
+                                        and ops.gemm_policy(-1) == 25) else 0))
         max_slab = 1
         if dcn:
-            s_ = ops.wgrad_splits(cfg.dcn_rank, self.top_real, B, self._wg_target)
+            s_ = self._wg_splits(cfg.dcn_rank, self.top_real)
             max_slab = max(max_slab, s_ * cfg.dcn_rank * self.top_real)
         self.slab = z(max_slab, dt=torch.float32)
         # Weight grads of the augmented layers: the GEMM's N is the 64-aligned
@@ -343,12 +350,21 @@ class DLRMTrainer:
         self._segments = []
         self._opt_sums_slabs = dev.type == "cuda" and world_size == 1
         for L in self.bottom_layers + self.top_layers + self.dcn_u:
-            S = ops.wgrad_splits(L.out, self._wgrad_n(L), B, self._wg_target)
+            S = self._wg_splits(L.out, self._wgrad_n(L))
             if S > 1:
                 sl = z(S * L.out * L.wcols, dt=torch.float32)
                 self.wslab[L.name] = (sl, S)
                 if self._opt_sums_slabs:
                     self._segments.append((fp.offset(L.name + ".w"), sl, S))
+        # DCN-v2 V weight grads: same treatment (one slab per layer, summed by
+        # the optimizer instead of a reduce launch per layer)
+        if dcn and self._opt_sums_slabs:
+            for i in range(cfg.dcn_layers):
+                S = self._wg_splits(cfg.dcn_rank, self.top_real)
+                if S > 1:
+                    sl = z(S * cfg.dcn_rank * self.top_real, dt=torch.float32)
+                    self.wslab[f"dcn{i}.v"] = (sl, S)
+                    self._segments.append((fp.offset(f"dcn{i}.v"), sl, S))
         self.dense_hyper = torch.tensor([cfg.dense_lr, 0.0, 1.0], dtype=torch.float32, device=dev)
         self.emb_hyper = torch.tensor([cfg.emb_lr, 0.0], dtype=torch.float32, device=dev)
         self.slot_off = [0] + list(self.emb.slot_off)
@@ -389,7 +405,13 @@ class DLRMTrainer:
         # embedding lookup / sort / update replay on their own stream beside
         # the MLP graphs, joined by events (set while capturing/replaying)
         self._mstream = False
-        self._early = os.environ.get("TDFO_EARLY_LOOKUP", "1") == "1"
+        # per workload (profiles/graph_streams.md): DLRM's short embedding
+        # stream gains from the early lookup and the split optimizer; DCN-v2's
+        # 0.4 ms multi-hot update + lookup on that stream does not
+        # (2.69-2.71 vs 2.72 ms/step each)
+        dflt = "0" if cfg.interaction == "dcn" else "1"
+        self._early = os.environ.get("TDFO_EARLY_LOOKUP", dflt) == "1"
+        self._split_opt = os.environ.get("TDFO_SPLIT_OPT", dflt) == "1"
         self._ms_wgrad = False
         self._ms = None
 
@@ -498,6 +520,9 @@ class DLRMTrainer:
         else:
             wgrad()
         self._dgrad(L, x, dy, dx, x_is_relu)
+
+    def _wg_splits(self, M: int, N: int) -> int:
+        return ops.wgrad_splits(M, N, self.B, self._wg_target, slots=self._wg_slots)
 
     def _wgrad_n(self, L: Lin) -> int:
         return L.in_k if self._csum else L.wcols
@@ -815,9 +840,14 @@ class DLRMTrainer:
             Uw = fp.bf16(u.name + ".w")
             ops.gemm(self.dcn_dy, False, Uw[:, :u.in_k], True, None, False, None, self.dcn_dh,
                      None, 1)
-            ops.linear_wgrad(self.dcn_dh, self.dcn_x[i][:, :Wd], fp.grad(f"dcn{i}.v").view(-1),
-                             splits=ops.wgrad_splits(cfg.dcn_rank, Wd, self.B, self._wg_target),
-                             slab=self.slab)
+            if f"dcn{i}.v" in self.wslab:    # partials summed by the optimizer
+                sl, S = self.wslab[f"dcn{i}.v"]
+                ops.gemm(self.dcn_dh, True, self.dcn_x[i][:, :Wd], True, None, False, None, None,
+                         sl, S)
+            else:
+                ops.linear_wgrad(self.dcn_dh, self.dcn_x[i][:, :Wd],
+                                 fp.grad(f"dcn{i}.v").view(-1),
+                                 splits=self._wg_splits(cfg.dcn_rank, Wd), slab=self.slab)
             # dx_i = dh V + (i > 0 ? dxo : acc)
             ops.gemm(self.dcn_dh, False, fp.bf16(f"dcn{i}.v"), True, None, False, None, None, None,
                      1, add=dxo if i > 0 else acc, out2=self.dcn_dx[i])
@@ -866,7 +896,7 @@ class DLRMTrainer:
         # the top-MLP (+ head, DCN) part of the dense optimizer needs only the
         # top backward: it runs on the embedding stream after the embedding
         # update, beside the bottom-MLP backward (TDFO_SPLIT_OPT=0: one pass)
-        split = (os.environ.get("TDFO_SPLIT_OPT", "1") == "1" and not self._ms_wgrad)
+        split = self._split_opt and not self._ms_wgrad
         a, P = self._ar_split, self.fp.p.numel()
 
         def e3():
