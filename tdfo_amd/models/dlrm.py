@@ -405,13 +405,16 @@ class DLRMTrainer:
         # embedding lookup / sort / update replay on their own stream beside
         # the MLP graphs, joined by events (set while capturing/replaying)
         self._mstream = False
-        # per workload (profiles/graph_streams.md): DLRM's short embedding
-        # stream gains from the early lookup and the split optimizer; DCN-v2's
-        # 0.4 ms multi-hot update + lookup on that stream does not
-        # (2.69-2.71 vs 2.72 ms/step each)
-        dflt = "0" if cfg.interaction == "dcn" else "1"
-        self._early = os.environ.get("TDFO_EARLY_LOOKUP", dflt) == "1"
-        self._split_opt = os.environ.get("TDFO_SPLIT_OPT", dflt) == "1"
+        # early lookup (both workloads: DLRM 0.538 vs 0.556, DCN-v2 2.571-2.577
+        # vs 2.592-2.596 ms/step) and where the top-MLP part of the dense
+        # optimizer runs: "1" on the embedding stream after the embedding
+        # update (DLRM, whose update is short: 0.541 vs 0.545 for "main"),
+        # "main" first on the MLP stream beside the embedding update (DCN-v2,
+        # whose multi-hot update is 0.42 ms: 2.589 vs 2.633 for "0"), "0" one
+        # pass after the bottom backward (profiles/graph_streams.md)
+        self._early = os.environ.get("TDFO_EARLY_LOOKUP", "1") == "1"
+        self._split_opt = os.environ.get("TDFO_SPLIT_OPT",
+                                         "main" if cfg.interaction == "dcn" else "1")
         self._ms_wgrad = False
         self._ms = None
 
@@ -896,17 +899,20 @@ class DLRMTrainer:
         # the top-MLP (+ head, DCN) part of the dense optimizer needs only the
         # top backward: it runs on the embedding stream after the embedding
         # update, beside the bottom-MLP backward (TDFO_SPLIT_OPT=0: one pass)
-        split = self._split_opt and not self._ms_wgrad
+        split = self._split_opt in ("1", "main") and not self._ms_wgrad
+        on_main = self._split_opt == "main"
         a, P = self._ar_split, self.fp.p.numel()
 
         def e3():
             emb.backward_start()
             emb.backward_wait()
             self._s_emb_update()
-            if split:
+            if split and not on_main:
                 self._dense_update_range(a, P)
 
         def m3():
+            if split and on_main:
+                self._dense_update_range(a, P)
             self._s_bottom_bwd()
             if split:
                 self._dense_update_range(0, a)
