@@ -473,12 +473,22 @@ void split_features(const Tensor& dx, int64_t F, int64_t D, const Tensor& dense,
                     at::IntArrayRef dstride, bool relu_mask) {
   check_dev(dx, "dx");
   const int64_t B = dense.size(0);
-  TORCH_CHECK(dx.is_contiguous() && dx.numel() == B * F * D && D % 8 == 0, "split: dx [B, F*D]");
+  // packed [B * F * D], or a row-major 2-D view whose rows hold >= F*D columns
+  int64_t ld_dx = F * D;
+  if (dx.dim() == 2) {
+    check_2d_rowmajor(dx, "dx");
+    TORCH_CHECK(dx.size(0) == B && dx.size(1) >= F * D && dx.stride(0) % 8 == 0 &&
+                aligned16(dx.data_ptr()), "split: dx view [B, >= F*D], 16-B aligned rows");
+    ld_dx = dx.stride(0);
+  } else {
+    TORCH_CHECK(dx.is_contiguous() && dx.numel() == B * F * D, "split: dx [B, F*D]");
+  }
+  TORCH_CHECK(D % 8 == 0, "split: D % 8");
   check_2d_rowmajor(d_dense, "d_dense");
   TORCH_CHECK(d_dense.stride(0) % 8 == 0 && dense.stride(0) % 8 == 0, "split alignment");
   auto m = make_slots(doff, dstride, F);
   check_slots_fit(d_emb, m, F, D, B);
-  tdfo::split_features(bf16_ptr(dx), (int)F, (int)D, (int)B, bf16_ptr(dense), dense.stride(0),
+  tdfo::split_features(bf16_ptr(dx), ld_dx, (int)F, (int)D, (int)B, bf16_ptr(dense), dense.stride(0),
                        bf16_mut(d_dense), d_dense.stride(0), bf16_mut(d_emb), m, relu_mask,
                        cur_stream());
 }
@@ -1046,6 +1056,8 @@ TORCH_LIBRARY(tdfo, m) {
         "Tensor(c!)? out2=None, int ldc32=0, int csum_col=-1) -> ()");
   m.def("radix_sort_sep_hist(int v) -> int",
         [](int64_t v) { return (int64_t)tdfo::radix_sort_sep_hist((int)v); });
+  m.def("radix_sort_tiled(int v) -> int",
+        [](int64_t v) { return (int64_t)tdfo::radix_sort_tiled((int)v); });
   m.def("radix_sort_max_bits(int b) -> int",
         [](int64_t v) { return (int64_t)tdfo::radix_sort_max_bits((int)v); });
   m.def("gemm_policy(int p) -> int", [](int64_t p) { return (int64_t)tdfo::gemm_policy((int)p); });

@@ -65,10 +65,12 @@ void concat_features(const uint16_t* dense, int64_t ld_dense, const uint16_t* em
                      const SlotMap& slots, int F, int D, int B, uint16_t* out,
                      hipStream_t s);
 // inverse of concat_features; the dense slot is multiplied by (dense > 0)
-// when relu_mask (ReLU of the bottom MLP's last layer).
-void split_features(const uint16_t* dx, int F, int D, int B, const uint16_t* dense,
-                    int64_t ld_dense, uint16_t* d_dense, int64_t ld_ddense,
-                    uint16_t* d_emb, const SlotMap& dslots, int relu_mask, hipStream_t s);
+// when relu_mask (ReLU of the bottom MLP's last layer). Row b of dx starts at
+// dx + b * ld_dx (F * D when packed).
+void split_features(const uint16_t* dx, int64_t ld_dx, int F, int D, int B,
+                    const uint16_t* dense, int64_t ld_dense, uint16_t* d_dense,
+                    int64_t ld_ddense, uint16_t* d_emb, const SlotMap& dslots, int relu_mask,
+                    hipStream_t s);
 // DCN-v2 cross backward: dy = dout * x0 ;
 // dx0 = (accumulate ? dx0 : 0) + dout * y + (add_dout ? dout : 0)
 void cross_bwd(const uint16_t* dout, const uint16_t* x0, const uint16_t* y, int64_t n,
@@ -81,8 +83,12 @@ void cross_bwd(const uint16_t* dout, const uint16_t* x0, const uint16_t* y, int6
 size_t radix_sort_workspace(int64_t n);
 // digit bits per radix pass (4..10); returns the previous value (b < 4: read only)
 int radix_sort_max_bits(int b);
-// number of digit passes for key_bits (odd: the sorted result lands in (kb, vb))
-int radix_sort_passes(int key_bits);
+// number of digit passes for key_bits at n keys (odd: the sorted result lands
+// in (kb, vb))
+int radix_sort_passes(int key_bits, int64_t n);
+// 0: 1024-item tiles / 10-bit digits, 1: 4096-item tiles / <=8-bit digits
+// from 2^19 keys up (default), 2: always 4096-item tiles; returns the old mode
+int radix_sort_tiled(int v);
 // 1: per-pass hist kernels, 0: next-pass hist counted by the scatter (atomics)
 int radix_sort_sep_hist(int v);
 int radix_sort_pairs_u32(uint32_t* ka, int32_t* va, uint32_t* kb, int32_t* vb, int64_t n,

@@ -26,8 +26,8 @@ __global__ __launch_bounds__(256) void concat_kernel(const uint16_t* __restrict_
   }
 }
 
-__global__ __launch_bounds__(256) void split_kernel(const uint16_t* __restrict__ dx, int F,
-                                                    int D, int B,
+__global__ __launch_bounds__(256) void split_kernel(const uint16_t* __restrict__ dx,
+                                                    int64_t ld_dx, int F, int D, int B,
                                                     const uint16_t* __restrict__ dense,
                                                     int64_t ld_dense,
                                                     uint16_t* __restrict__ d_dense,
@@ -42,7 +42,7 @@ __global__ __launch_bounds__(256) void split_kernel(const uint16_t* __restrict__
     const int64_t bf = i / gpr;
     const int f = (int)(bf % F);
     const int64_t b = bf / F;
-    uint4 v = *(const uint4*)(dx + (b * F + f) * D + g * 8);
+    uint4 v = *(const uint4*)(dx + b * ld_dx + f * D + g * 8);
     if (f == 0) {
       if (relu_mask) {
         const uint4 h = *(const uint4*)(dense + b * ld_dense + g * 8);
@@ -108,11 +108,12 @@ void concat_features(const uint16_t* dense, int64_t ld_dense, const uint16_t* em
   TDFO_CHECK_HIP(hipGetLastError());
 }
 
-void split_features(const uint16_t* dx, int F, int D, int B, const uint16_t* dense,
-                    int64_t ld_dense, uint16_t* d_dense, int64_t ld_ddense, uint16_t* d_emb,
-                    const SlotMap& dslots, int relu_mask, hipStream_t s) {
+void split_features(const uint16_t* dx, int64_t ld_dx, int F, int D, int B,
+                    const uint16_t* dense, int64_t ld_dense, uint16_t* d_dense,
+                    int64_t ld_ddense, uint16_t* d_emb, const SlotMap& dslots, int relu_mask,
+                    hipStream_t s) {
   const int64_t n = (int64_t)B * F * (D / 8);
-  hipLaunchKernelGGL(split_kernel, dim3(grid_of(n)), dim3(256), 0, s, dx, F, D, B, dense,
+  hipLaunchKernelGGL(split_kernel, dim3(grid_of(n)), dim3(256), 0, s, dx, ld_dx, F, D, B, dense,
                      ld_dense, d_dense, ld_ddense, d_emb, dslots, relu_mask);
   TDFO_CHECK_HIP(hipGetLastError());
 }

@@ -76,14 +76,13 @@ def calls(tr: DLRMTrainer):
                 h[:, :u.in_k], False, Uw[:, :u.in_k], False,
                 None if u.bias_in_k else fp.param(u.name + ".w")[:, u.bcol], False, None,
                 tr.dcn_y[i], None, 1, mul=x0, add=xi[:, :Wd], out2=tr.dcn_x[i + 1][:, :Wd])))
-            out.append((f"dcn{i}", "U.wgrad", fl, lambda u=u, h=h: tr._wgrad(u, h, tr.dcn_dy)))
-            out.append((f"dcn{i}", "U.dgrad", fl, lambda Uw=Uw, u=u: ops.gemm(
-                tr.dcn_dy, False, Uw[:, :u.in_k], True, None, False, None, tr.dcn_dh, None, 1)))
-            out.append((f"dcn{i}", "V.wgrad", fl, lambda xi=xi, i=i: ops.linear_wgrad(
-                tr.dcn_dh, xi[:, :Wd], fp.grad(f"dcn{i}.v").view(-1),
-                splits=tr._wg_splits(r, Wd), slab=tr.slab)))
-            out.append((f"dcn{i}", "V.dgrad", fl, lambda V=V, i=i: ops.gemm(
-                tr.dcn_dh, False, V, True, None, False, None, None, None, 1,
+            dy, dh = tr._dcn_bufs(i)
+            out.append((f"dcn{i}", "U.wgrad", fl, lambda u=u, h=h, dy=dy: tr._wgrad(u, h, dy)))
+            out.append((f"dcn{i}", "U.dgrad", fl, lambda Uw=Uw, u=u, dy=dy, dh=dh: ops.gemm(
+                dy, False, Uw[:, :u.in_k], True, None, False, None, dh, None, 1)))
+            out.append((f"dcn{i}", "V.wgrad", fl, lambda i=i: tr._dcn_wgrad_v(i)))
+            out.append((f"dcn{i}", "V.dgrad", fl, lambda V=V, i=i, dh=dh: ops.gemm(
+                dh, False, V, True, None, False, None, None, None, 1,
                 add=tr.dcn_dx[i + 1], out2=tr.dcn_dx[i])))
     for L, x, o, dy, dx, relu_in in layers:
         fl = 2.0 * B * L.out * L.in_k

@@ -279,6 +279,16 @@ class DLRMTrainer:
         if world_size > 1:                            # replicated dense arch
             dist.broadcast(fp.p, src=0, group=group)
         fp.sync_bf16()
+        # Weight grads deferred past the interaction / cross-network backward
+        # (per-layer buffers: no reuse), so the embedding gradients -- which
+        # need only the dgrad chain -- exist earlier: multi-rank, their
+        # all-to-all overlaps the wgrads. On one GPU (TDFO_DEFER_WGRAD=1)
+        # DCN-v2's multi-hot embedding update would run beside its top + cross
+        # wgrads instead of after them: measured 2.606 vs 2.514-2.531 ms/step
+        # (the memory-bound update's many blocks starve the one-block-per-CU
+        # 256x128 wgrad GEMMs: 1.07 ms of them instead of 0.4), so off.
+        dflt = world_size > 1
+        self._defer_top_wgrad = os.environ.get("TDFO_DEFER_WGRAD", "1" if dflt else "0") == "1"
         # ------------------------------------------------------ buffers
         bf = torch.bfloat16
 
@@ -311,8 +321,23 @@ class DLRMTrainer:
             self.dcn_y = [z(B, Wd) for _ in range(Lc)]         # U h + b
             self.dcn_dx = [z(B, Wd) for _ in range(Lc + 1)]
             self.dcn_dx0acc = z(B, Wd)
-            self.dcn_dh = z(B, r)
-            self.dcn_dy = z(B, Wd)
+            # dy = dx_{l+1} * x0 and dh = dy U of each layer: the wgrads'
+            # inputs (one buffer per layer when those are deferred)
+            nb = Lc if self._defer_top_wgrad else 1
+            self.dcn_dhl = [z(B, r) for _ in range(nb)]
+            self.dcn_dyl = [z(B, Wd) for _ in range(nb)]
+        # DCN-v2, one rank: the lookup pools straight into x_0's embedding
+        # columns and the bottom MLP writes its output into x_0's dense slot;
+        # the embedding backward reads its gradients in place from dx_0 (no
+        # concat / split of the 3456-wide rows: 46 + 20 us per step). Not with
+        # deferred wgrads: layer 0's V wgrad would read x_0 while the next
+        # step's early lookup rewrites it.
+        self._x0_alias = False
+        if (cfg.interaction == "dcn" and not self._defer_top_wgrad
+                and os.environ.get("TDFO_DCN_X0_ALIAS", "1") == "1"
+                and self.emb.alias_pooled(self.dcn_x[0], self.dcn_dx[0], D)):
+            self._x0_alias = True
+            self.h_out = self.dcn_x[0][:, :D]
         self.logits = z(B, dt=torch.float32)
         self.nparts = ops.head_parts(B)
         self.head_part = z(self.nparts * (self.head_k + 2), dt=torch.float32)
@@ -375,9 +400,6 @@ class DLRMTrainer:
         # size 1 the embedding lookup/update run beside the bottom MLP. The
         # forks/joins are stream-event edges, so a captured hipGraph keeps the
         # concurrency as parallel branches.
-        # multi-rank: top wgrads after the interaction backward, so the
-        # embedding-grad all-to-all overlaps them (per-layer buffers: no reuse)
-        self._defer_top_wgrad = world_size > 1 and cfg.interaction == "dot"
         # ids-only half of the embedding backward (keys + sort) on its own
         # stream beside the top MLP: it needs no gradient, and its few
         # latency-bound blocks leave the GEMMs most of the machine
@@ -566,6 +588,7 @@ class DLRMTrainer:
 
     def _stages(self):
         emb = self.emb
+        top_wgrad = [("c", self._s_top_wgrad)] if self._defer_top_wgrad else []
         if self._es is not None:
             # one process: embedding work on its own stream, beside the MLPs
             return [
@@ -573,6 +596,7 @@ class DLRMTrainer:
                 ("c", self._s_bottom_fwd),
                 ("c", self._s_top),
                 ("c", self._s_emb_update_side),
+            ] + top_wgrad + [
                 ("c", self._s_bottom_bwd),
                 ("c", self._s_dense_update),
             ]
@@ -581,7 +605,6 @@ class DLRMTrainer:
         else:
             lookup = ("c", emb.stage_fwd_lookup)
         prep = [] if emb.fwd_prep_noop else [("c", lambda: emb.stage_fwd_prep(self.ids))]
-        top_wgrad = [("c", self._s_top_wgrad)] if self._defer_top_wgrad else []
         if self.pipeline:
             # this batch's ids were exchanged during the previous step (or by
             # prime()); the next batch is loaded + exchanged after the
@@ -740,11 +763,15 @@ class DLRMTrainer:
             self._join(self._ps)
 
     def _s_top_wgrad(self):
-        """Top-MLP weight grads, deferred past the interaction backward when the
-        embedding grads go over the network (their all-to-all runs meanwhile)."""
+        """Top-MLP (and DCN cross-layer) weight grads, deferred past the
+        interaction / cross backward: the embedding grads exist without them
+        (their all-to-all, or on one GPU the embedding update, runs meanwhile)."""
         if self._defer_top_wgrad:
             for i in reversed(range(len(self.top_layers))):
                 self._wgrad(self.top_layers[i], self.top_in[i], self.top_grad[i])
+            for i in reversed(range(len(self.dcn_u))):
+                self._dcn_wgrad_u(i)
+                self._dcn_wgrad_v(i)
 
     def _s_bottom_bwd(self):
         for i in reversed(range(len(self.bottom_layers))):
@@ -818,7 +845,8 @@ class DLRMTrainer:
         cfg, fp, D, F = self.cfg, self.fp, self.cfg.embedding_dim, self.F
         Wd = self.top_real
         x0 = self.dcn_x[0]
-        ops.concat_features(h, self.emb.recv, self.slot_off, self.slot_stride, F, D, x0)
+        if not self._x0_alias:
+            ops.concat_features(h, self.emb.recv, self.slot_off, self.slot_stride, F, D, x0)
         for i in range(cfg.dcn_layers):
             u = self.dcn_u[i]
             ops.linear_fwd(self.dcn_x[i][:, :Wd], fp.bf16(f"dcn{i}.v"), None, relu=False,
@@ -831,31 +859,50 @@ class DLRMTrainer:
 
     def _dcn_backward(self, h):
         cfg, fp, D, F = self.cfg, self.fp, self.cfg.embedding_dim, self.F
-        Lc, Wd = cfg.dcn_layers, self.top_real
+        Lc = cfg.dcn_layers
         x0 = self.dcn_x[0]
         acc = self.dcn_dx0acc
         for i in reversed(range(Lc)):
             u = self.dcn_u[i]
             dxo = self.dcn_dx[i + 1]
+            dy, dh = self._dcn_bufs(i)
             # dy = dxo * x0 ; acc (+)= dxo * y (+ dxo at i == 0: x_0's residual)
-            ops.cross_bwd(dxo, x0, self.dcn_y[i], self.dcn_dy, acc, i != Lc - 1, i == 0)
-            self._wgrad(u, self.dcn_h[i], self.dcn_dy)
+            ops.cross_bwd(dxo, x0, self.dcn_y[i], dy, acc, i != Lc - 1, i == 0)
+            if not self._defer_top_wgrad:
+                self._dcn_wgrad_u(i)
             Uw = fp.bf16(u.name + ".w")
-            ops.gemm(self.dcn_dy, False, Uw[:, :u.in_k], True, None, False, None, self.dcn_dh,
-                     None, 1)
-            if f"dcn{i}.v" in self.wslab:    # partials summed by the optimizer
-                sl, S = self.wslab[f"dcn{i}.v"]
-                ops.gemm(self.dcn_dh, True, self.dcn_x[i][:, :Wd], True, None, False, None, None,
-                         sl, S)
-            else:
-                ops.linear_wgrad(self.dcn_dh, self.dcn_x[i][:, :Wd],
-                                 fp.grad(f"dcn{i}.v").view(-1),
-                                 splits=self._wg_splits(cfg.dcn_rank, Wd), slab=self.slab)
+            ops.gemm(dy, False, Uw[:, :u.in_k], True, None, False, None, dh, None, 1)
+            if not self._defer_top_wgrad:
+                self._dcn_wgrad_v(i)
             # dx_i = dh V + (i > 0 ? dxo : acc)
-            ops.gemm(self.dcn_dh, False, fp.bf16(f"dcn{i}.v"), True, None, False, None, None, None,
+            ops.gemm(dh, False, fp.bf16(f"dcn{i}.v"), True, None, False, None, None, None,
                      1, add=dxo if i > 0 else acc, out2=self.dcn_dx[i])
-        ops.split_features(self.dcn_dx[0], F, D, h, self.bot_grad[-1], self.emb.d_recv,
-                           self.slot_off, self.slot_stride, True)
+        if self._x0_alias:      # only the dense slot's ReLU-masked gradient
+            ops.split_features(self.dcn_dx[0], 1, D, h, self.bot_grad[-1], self.emb.d_recv,
+                               self.slot_off, self.slot_stride, True)
+        else:
+            ops.split_features(self.dcn_dx[0], F, D, h, self.bot_grad[-1], self.emb.d_recv,
+                               self.slot_off, self.slot_stride, True)
+
+    def _dcn_bufs(self, i: int):
+        j = i if len(self.dcn_dyl) > 1 else 0
+        return self.dcn_dyl[j], self.dcn_dhl[j]
+
+    def _dcn_wgrad_u(self, i: int):
+        dy, _ = self._dcn_bufs(i)
+        self._wgrad(self.dcn_u[i], self.dcn_h[i], dy)
+
+    def _dcn_wgrad_v(self, i: int):
+        """dV_i = dh_i^T x_i (split-K partials summed by the optimizer on one
+        GPU, reduced here otherwise)."""
+        _, dh = self._dcn_bufs(i)
+        Wd = self.top_real
+        if f"dcn{i}.v" in self.wslab:
+            sl, S = self.wslab[f"dcn{i}.v"]
+            ops.gemm(dh, True, self.dcn_x[i][:, :Wd], True, None, False, None, None, sl, S)
+        else:
+            ops.linear_wgrad(dh, self.dcn_x[i][:, :Wd], self.fp.grad(f"dcn{i}.v").view(-1),
+                             splits=self._wg_splits(self.cfg.dcn_rank, Wd), slab=self.slab)
 
     def step(self):
         """One training step on the batch in the static buffers."""
@@ -911,6 +958,8 @@ class DLRMTrainer:
                 self._dense_update_range(a, P)
 
         def m3():
+            if self._defer_top_wgrad and not self._ms_wgrad:
+                self._s_top_wgrad()          # beside the embedding update (E3)
             if split and on_main:
                 self._dense_update_range(a, P)
             self._s_bottom_bwd()

@@ -69,6 +69,13 @@ def embedding_segsort(v: int = -1) -> int:
     return int(_native().embedding_segsort(v))
 
 
+def radix_sort_tiled(v: int = -1) -> int:
+    """Device-wide radix sort variant: 0 1024-item tiles / 10-bit digits,
+    1 4096-item tiles / <=8-bit digits from 2^19 keys up (default), 2 always
+    4096-item tiles; v < 0 only reads it. Returns the previous one."""
+    return int(_native().radix_sort_tiled(v))
+
+
 def effective_segsort(segsort: int) -> int:
     return int(segsort) if segsort and embedding_segsort() else 0
 

@@ -434,7 +434,7 @@ def concat_features(dense, emb, off, stride, F, D, out):
 
 def split_features(dx, F, D, dense, d_dense, d_emb, doff, dstride, relu_mask):
     B = dense.shape[0]
-    x = dx.reshape(B, F, D)
+    x = dx[:, :F * D].reshape(B, F, D) if dx.dim() == 2 else dx.reshape(B, F, D)
     d0 = x[:, 0].float()
     if relu_mask:
         d0 = d0 * (dense[:, :D].float() > 0)

@@ -173,6 +173,8 @@ class ShardedEmbeddingBags:
         self.tw_v_offsets = offs.to(self.device)
         self.tw_v_row_off = torch.tensor(v_row_off, dtype=torch.int64, device=self.device)
         self.tw_v_out_off = torch.tensor(v_out_off, dtype=torch.int64, device=self.device)
+        self.tw_ld = self.dsum[rank]          # row pitch of the pooled TW output (alias_pooled)
+        self.pooled_aliased = False
         # buffers
         bf = torch.bfloat16
         self.tw_send_ids = torch.empty(self.nnz_local_tw(), dtype=torch.int64, device=self.device)
@@ -349,6 +351,33 @@ class ShardedEmbeddingBags:
         self._pending = None
         self._rw_state = None
 
+    def alias_pooled(self, out: torch.Tensor, d_out: torch.Tensor, col0: int) -> bool:
+        """One rank, table-wise tables only: pool straight into the consumer's
+        row-major [B, ld] buffer ``out`` at columns col0 + t*D (e.g. DCN-v2's
+        x_0 after the dense slot) and read the pooled gradients from ``d_out``
+        in the same layout -- no concat / split pass through recv / d_recv.
+        Returns False (nothing changed) when the layout does not allow it."""
+        D, B = self.D, self.B
+        if not (self.world == 1 and self.tw_identity and self.tw_nv == self.T
+                and not (self.cw_tables or self.dp_tables or self.rw_tables)):
+            return False
+        for t_ in (out, d_out):
+            if not (t_.is_contiguous() and t_.dim() == 2 and t_.shape[0] == B
+                    and t_.shape[1] >= col0 + self.T * D and t_.dtype == self.recv.dtype):
+                return False
+        if out.shape != d_out.shape:
+            return False
+        ld = out.shape[1]
+        self.recv = out.view(-1)
+        self.d_recv = d_out.view(-1)
+        self.tw_ld = ld
+        self.tw_v_out_off = torch.tensor([col0 + i * D for i in range(self.T)], dtype=torch.int64,
+                                         device=self.device)
+        self.slot_off = [col0 + t * D for t in range(self.T)]
+        self.slot_stride = [ld] * self.T
+        self.pooled_aliased = True
+        return True
+
     def nnz_local_tw(self) -> int:
         return sum(self.tw_send_counts)
 
@@ -468,7 +497,7 @@ class ShardedEmbeddingBags:
         if self.tw_nv:
             self.tw_store.forward(self.tw_recv_ids, self.tw_v_offsets, self.tw_v_row_off, self.tw_nv,
                                   B, self.tw_pooled if W > 1 else self.recv, self.tw_v_out_off,
-                                  self.dsum[self.rank], mean=self.mean,
+                                  self.tw_ld, mean=self.mean,
                                   onehot=self.tw_onehot)
         if self.cw_tables and self.cw_nv:
             self.cw_store.forward(self.cw_recv_ids, self.cw_v_offsets, self.cw_v_row_off,
@@ -571,7 +600,7 @@ class ShardedEmbeddingBags:
         if self.tw_nv:
             self.tw_store.backward_prepare(self.tw_recv_ids, self.tw_v_offsets, self.tw_v_row_off,
                                            self.tw_nv, self.B, self.tw_v_out_off,
-                                           self.dsum[self.rank], mean=self.mean,
+                                           self.tw_ld, mean=self.mean,
                                            segsort=self.tw_segsort)
         if self.rw_tables:
             self._rw_prepare()
@@ -592,7 +621,7 @@ class ShardedEmbeddingBags:
         if self.tw_nv:
             self.tw_store.backward_apply(self.tw_recv_ids, self.tw_v_offsets, self.tw_v_row_off,
                                          self.tw_nv, B, grad, self.tw_v_out_off,
-                                         self.dsum[self.rank], hyper, mean=self.mean,
+                                         self.tw_ld, hyper, mean=self.mean,
                                          segsort=self.tw_segsort)
         if self.cw_tables and self.cw_nv:
             self.cw_store.backward_update(self.cw_recv_ids, self.cw_v_offsets, self.cw_v_row_off,

@@ -478,6 +478,47 @@ def test_dlrm_graph_replay_matches_eager(staged):
     assert torch.allclose(a.fp.p, b.fp.p, atol=1e-5)
 
 
+@pytest.mark.parametrize("mean", [False, True])
+def test_embedding_bwd_multihot_large(mean):
+    """DCN-v2-shaped multi-hot backward (variable and empty bags, ~0.7M ids:
+    the per-bag keys kernel + the 4096-item-tile radix sort) matches the fp32
+    reference, and matches the 1024-item-tile sort bit for bit."""
+    T, B, D = 4, 8192, 128
+    rows = [5, 300_000, 1_000, 2_000_000]
+    g = torch.Generator(device="cpu").manual_seed(3)
+    maxlen = [1, 100, 8, 60]
+    lens = torch.cat([torch.randint(0, m + 1, (B,), generator=g) for m in maxlen])
+    offs = torch.zeros(T * B + 1, dtype=torch.long)
+    offs[1:] = lens.cumsum(0)
+    idx = torch.cat([torch.randint(0, rows[t], (int(lens[t * B:(t + 1) * B].sum()),),
+                                   generator=g) for t in range(T)])
+    assert idx.numel() > (1 << 19)
+    ro = torch.zeros(T, dtype=torch.long)
+    ro[1:] = torch.tensor(rows[:-1]).cumsum(0)
+    W = torch.randn(sum(rows), D, generator=g) * 0.1
+    W, ro, idx, offs = (x.to(DEV) for x in (W, ro, idx, offs))
+    goff = torch.tensor([t * D for t in range(T)], device=DEV)
+    grad = torch.randn(B * T * D, device=DEV)
+    hyper = torch.tensor([0.05, 3.0], device=DEV)
+    res = []
+    for tiled in (1, 0):
+        old = ops.radix_sort_tiled(tiled)
+        try:
+            Wn, s1 = W.clone(), torch.zeros(W.shape[0], device=DEV)
+            ops.embedding_bwd(Wn, ro, idx, offs, goff, T, B, grad, T * D,
+                              ops.EMB_ROWWISE_ADAGRAD, hyper, state1=s1, mean=mean)
+            torch.cuda.synchronize()
+        finally:
+            ops.radix_sort_tiled(old)
+        res.append((Wn, s1))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    We, e1 = W.clone(), torch.zeros(W.shape[0], device=DEV)
+    ref.embedding_bwd(We, ro, idx, offs, goff, None, T, B, mean, 20, grad, T * D,
+                      ops.EMB_ROWWISE_ADAGRAD, e1, None, hyper, 1e-8, 0.9, 0.999, 0.0, None)
+    assert (res[0][0] - We).abs().max() < 1e-4 * max(1.0, We.abs().max().item())
+    assert (res[0][1] - e1).abs().max() < 1e-3 * max(1.0, e1.abs().max().item())
+
+
 def test_embedding_bwd_graph_replay_large():
     """Bench-scale fused backward (213k ids, skewed + uniform tables) captured
     in a hipGraph and replayed must match eager execution bit for bit."""
@@ -581,14 +622,19 @@ def test_dcn_step_matches_cpu():
 
 
 @pytest.mark.parametrize("n", [1, 1000, 4096, 4097, 213_000, 1_500_000])
-@pytest.mark.parametrize("dtype,bits", [(torch.int32, 28), (torch.int64, 40)])
-def test_radix_sort_matches_stable_torch_sort(n, dtype, bits):
+@pytest.mark.parametrize("dtype,bits", [(torch.int32, 28), (torch.int64, 40), (torch.int32, 5)])
+@pytest.mark.parametrize("tiled", [0, 2])
+def test_radix_sort_matches_stable_torch_sort(n, dtype, bits, tiled):
     g = torch.Generator(device="cpu").manual_seed(n)
     keys = torch.randint(0, 1 << bits, (n,), generator=g, dtype=torch.int64)
     keys[: n // 3] = keys[: n // 3] % 7          # heavy duplicates
     keys = keys.to(dtype).to(DEV)
     vals = torch.arange(n, dtype=torch.int32, device=DEV)
-    k, v = ops.sort_pairs(keys, vals, bits)
+    old = ops.radix_sort_tiled(tiled)
+    try:
+        k, v = ops.sort_pairs(keys, vals, bits)
+    finally:
+        ops.radix_sort_tiled(old)
     ek, ei = torch.sort(keys, stable=True)
     assert torch.equal(k, ek)
     assert torch.equal(v, ei.to(torch.int32))
