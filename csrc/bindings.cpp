@@ -505,6 +505,49 @@ void cross_bwd(const Tensor& dout, const Tensor& x0, const Tensor& y, const Tens
                   accumulate, add_dout, cur_stream());
 }
 
+// ------------------------------------------------------- fused MLP
+bool mlp3_supported(int64_t k0, int64_t n0, int64_t n1, int64_t n2) {
+  return tdfo::mlp3_fwd_supported((int)k0, (int)n0, (int)n1, (int)n2);
+}
+
+void mlp3_fwd(const Tensor& x, const Tensor& w0, const Tensor& w1, const Tensor& w2,
+              const c10::optional<Tensor>& b0, const c10::optional<Tensor>& b1,
+              const c10::optional<Tensor>& b2, const Tensor& y0, const Tensor& y1,
+              const Tensor& y2) {
+  const Tensor* ws[3] = {&w0, &w1, &w2};
+  const c10::optional<Tensor>* bs[3] = {&b0, &b1, &b2};
+  const Tensor* ys[3] = {&y0, &y1, &y2};
+  check_dev(x, "x");
+  check_2d_rowmajor(x, "x");
+  const int64_t B = x.size(0);
+  tdfo::Mlp3Args a{};
+  a.x = bf16_ptr(x); a.ldx = x.stride(0); a.B = (int)B;
+  a.k[0] = (int)x.size(1);
+  for (int l = 0; l < 3; ++l) {
+    check_dev(*ws[l], "w"); check_2d_rowmajor(*ws[l], "w");
+    check_dev(*ys[l], "y"); check_2d_rowmajor(*ys[l], "y");
+    const int64_t N = ws[l]->size(0), K = ws[l]->size(1);
+    TORCH_CHECK(K == a.k[l], "mlp3_fwd: layer ", l, " input width ", K, " vs ", a.k[l]);
+    TORCH_CHECK(ys[l]->size(0) == B && ys[l]->size(1) == N, "mlp3_fwd: output shape");
+    for (const Tensor* t : {ws[l], ys[l]})
+      TORCH_CHECK(t->stride(0) % 8 == 0 && aligned16(t->data_ptr()), "mlp3_fwd: 16-B aligned rows");
+    a.w[l] = bf16_ptr(*ws[l]); a.ldw[l] = ws[l]->stride(0);
+    a.y[l] = bf16_mut(*ys[l]); a.ldy[l] = ys[l]->stride(0);
+    a.k[l + 1] = (int)N;
+    if (*bs[l]) {
+      const Tensor& b = **bs[l];
+      check_dev(b, "bias");
+      TORCH_CHECK(b.scalar_type() == at::kFloat && b.dim() == 1 && b.numel() == N,
+                  "mlp3_fwd: bias fp32 [N] (any stride)");
+      a.bias[l] = b.data_ptr<float>(); a.bstride[l] = b.stride(0);
+    }
+  }
+  TORCH_CHECK(x.stride(0) % 8 == 0 && aligned16(x.data_ptr()), "mlp3_fwd: x rows 16-B aligned");
+  TORCH_CHECK(tdfo::mlp3_fwd_supported(a.k[0], a.k[1], a.k[2], a.k[3]), "mlp3_fwd: widths ",
+              a.k[0], "/", a.k[1], "/", a.k[2], "/", a.k[3], " unsupported");
+  tdfo::mlp3_fwd(a, cur_stream());
+}
+
 // ------------------------------------------------------------ radix sort
 std::tuple<Tensor, Tensor> sort_pairs(const Tensor& keys, const Tensor& vals, int64_t key_bits) {
   check_dev(keys, "keys"); check_dev(vals, "vals");
@@ -1056,6 +1099,9 @@ TORCH_LIBRARY(tdfo, m) {
         "Tensor(c!)? out2=None, int ldc32=0, int csum_col=-1) -> ()");
   m.def("radix_sort_sep_hist(int v) -> int",
         [](int64_t v) { return (int64_t)tdfo::radix_sort_sep_hist((int)v); });
+  m.def("mlp3_supported(int k0, int n0, int n1, int n2) -> bool", mlp3_supported);
+  m.def("mlp3_fwd(Tensor x, Tensor w0, Tensor w1, Tensor w2, Tensor? b0, Tensor? b1, "
+        "Tensor? b2, Tensor(a!) y0, Tensor(b!) y1, Tensor(c!) y2) -> ()");
   m.def("radix_sort_tiled(int v) -> int",
         [](int64_t v) { return (int64_t)tdfo::radix_sort_tiled((int)v); });
   m.def("radix_sort_max_bits(int b) -> int",
@@ -1160,6 +1206,7 @@ TORCH_LIBRARY(tdfo, m) {
 
 TORCH_LIBRARY_IMPL(tdfo, CUDA, m) {
   m.impl("gemm", gemm);
+  m.impl("mlp3_fwd", mlp3_fwd);
   m.impl("attention_fwd", attention_fwd);
   m.impl("encoder_layer_fwd", encoder_layer_fwd);
   m.impl("encoder_layer_bwd", encoder_layer_bwd);

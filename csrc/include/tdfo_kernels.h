@@ -42,6 +42,21 @@ void gemm_bf16(const GemmArgs& a, hipStream_t s);
 // p < 0 just reads it. Returns the previous policy.
 int gemm_policy(int p);
 
+// ------------------------------------------------- fused bottom MLP ----
+// y_l = relu(y_{l-1} W_l^T + b_l) for three layers in one launch (32 samples
+// per block, activations in LDS). k = {K0, N0, N1, N2}; bias[l] == nullptr:
+// the bias is inside K (augmented input column). Every y_l is written.
+struct Mlp3Args {
+  const uint16_t* x; int64_t ldx;
+  const uint16_t* w[3]; int64_t ldw[3];
+  const float* bias[3]; int64_t bstride[3];
+  uint16_t* y[3]; int64_t ldy[3];
+  int B;
+  int k[4];
+};
+bool mlp3_fwd_supported(int k0, int n0, int n1, int n2);
+void mlp3_fwd(const Mlp3Args& a, hipStream_t s);
+
 // ------------------------------------------------------ interaction ----
 // DLRM dot interaction over F <= 32 features of width D (one of 16/32/64/128).
 // Feature 0 comes from `dense` ([B, ld_dense]); feature f >= 1 from

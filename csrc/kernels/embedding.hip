@@ -102,15 +102,24 @@ __global__ __launch_bounds__(256) void emb_fwd_kernel(EmbFwdArgs a) {
   const int sub = lane / LPB, sl = lane - sub * LPB;
   int64_t* ids = s_ids[w][sub];
   float* wts = s_w[w][sub];
-  const int64_t nbags = (int64_t)a.T * a.B;
   const int64_t wave0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  const int64_t nw_iters = (nbags + nwaves * BPW - 1) / (nwaves * BPW);
+  // work item k = (bag group, table) with the table fastest: a wave's BPW
+  // bags share a table (same pooling), but consecutive waves -- and each
+  // wave's successive items -- cycle through the tables, so a long-bag
+  // table (DCN-v2's 100-id table: 47% of the rows) is spread over every
+  // block instead of filling one contiguous run of blocks in one pass
+  const int64_t groups = (a.B + BPW - 1) / BPW;
+  const int64_t nitems = groups * a.T;
+  const int64_t nw_iters = (nitems + nwaves - 1) / nwaves;
   for (int64_t it = 0; it < nw_iters; ++it) {
-    const int64_t j = (it * nwaves + wave0) * BPW + sub;
-    const bool active = j < nbags;
-    const int t = active ? (int)(j / a.B) : 0;
-    const int b = active ? (int)(j - (int64_t)t * a.B) : 0;
+    const int64_t k = it * nwaves + wave0;
+    const int tk = (int)(k % a.T);
+    const int64_t bb = (k / a.T) * BPW + sub;
+    const bool active = k < nitems && bb < a.B;
+    const int t = active ? tk : 0;
+    const int b = active ? (int)bb : 0;
+    const int64_t j = (int64_t)t * a.B + b;
     const int64_t s = active ? a.offsets[j] : 0, e = active ? a.offsets[j + 1] : 0;
     const int len = (int)(e - s);
     // wave-uniform chunk count (max over the wave's bags)

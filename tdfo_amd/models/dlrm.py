@@ -438,6 +438,19 @@ class DLRMTrainer:
         self._split_opt = os.environ.get("TDFO_SPLIT_OPT",
                                          "main" if cfg.interaction == "dcn" else "1")
         self._ms_wgrad = False
+        self._ms_merge = False
+        # TDFO_FUSED_BOTTOM=1: the bottom MLP forward as one fused kernel
+        # (csrc/kernels/mlp_fused.hip) when its widths are the DLRM / DCN-v2
+        # ones. Off by default: 17.4 vs 19.5 us for the three GEMM launches in
+        # isolation (scripts/bench_mlp3.py; its row-strided weight-fragment
+        # loads bind the TA), but 40 vs ~35 us in the step, where its 512-thread,
+        # 64 KB-LDS blocks wait for CUs behind the concurrent lookup's blocks
+        # (DLRM-1TB 0.538-0.545 vs 0.540-0.541 ms/step, DCN-v2 2.516 vs 2.495)
+        Lb = self.bottom_layers
+        self._fused_bottom = (dev.type == "cuda" and len(Lb) == 3
+                              and os.environ.get("TDFO_FUSED_BOTTOM", "0") == "1"
+                              and ops.mlp3_supported(Lb[0].in_k, Lb[0].out, Lb[1].out, Lb[2].out)
+                              and Lb[1].in_k == Lb[0].out and Lb[2].in_k == Lb[1].out)
         self._ms = None
 
     # for tests / checkpoints: (weight [out, in_real], bias [out]) views
@@ -686,6 +699,15 @@ class DLRMTrainer:
             self._run_stage(kind, fn)
 
     def _s_bottom_fwd(self):
+        if self._fused_bottom:
+            fp = self.fp
+            Ls = self.bottom_layers
+            ops.mlp3_fwd(self.bot_in[0][:, :Ls[0].in_k],
+                         [fp.bf16(L.name + ".w")[:, :L.in_k] for L in Ls],
+                         [None if L.bias_in_k else fp.param(L.name + ".w")[:, L.bcol] for L in Ls],
+                         [self.bot_in[1][:, :Ls[0].out], self.bot_in[2][:, :Ls[1].out],
+                          self.h_out])
+            return
         n = len(self.bottom_layers)
         for i, L in enumerate(self.bottom_layers):
             out = self.bot_in[i + 1][:, :L.out] if i + 1 < n else self.h_out
@@ -967,6 +989,28 @@ class DLRMTrainer:
                 self._dense_update_range(0, a)
             elif not self._ms_wgrad:
                 self._s_dense_update()
+        if self._ms_merge:
+            # bottom fwd + top in one graph (no M1 -> M2 graph boundary, ~13 us
+            # of queue idle): the lookup it waits for was issued right behind
+            # the previous embedding update, which is now the update alone --
+            # the top-MLP optimizer part runs on its own stream (O) beside it
+            # and beside the bottom backward, and the next step's graph waits
+            # for it
+            def m12():
+                self._s_bottom_fwd()
+                self._s_top()
+
+            def e3m():
+                emb.backward_start()
+                emb.backward_wait()
+                self._s_emb_update()
+
+            def m3m():
+                self._s_bottom_bwd()
+                self._dense_update_range(0, a)
+
+            return {"E1": e1, "E2": emb.stage_bwd_prepare, "M12": m12, "E3": e3m,
+                    "O": lambda: self._dense_update_range(a, P), "M3": m3m}
         plan = {"E1": e1, "E2": emb.stage_bwd_prepare, "M1": self._s_bottom_fwd,
                 "M2": self._s_top, "E3": e3, "M3": m3}
         if self._ms_wgrad:
@@ -978,6 +1022,33 @@ class DLRMTrainer:
         g, se, sw, ev = (self._ms["graphs"], self._ms["stream"], self._ms["wstream"],
                          self._ms["events"])
         main = torch.cuda.current_stream()
+        if self._ms_merge:
+            so = self._ms["ostream"]
+            if not self._early:
+                ev[0].record(main)
+                se.wait_event(ev[0])
+            with torch.cuda.stream(se):
+                g["E1"].replay()
+                ev[1].record(se)
+                g["E2"].replay()
+            main.wait_event(ev[1])           # pooled embeddings ready
+            if self._ms["o_pending"]:
+                main.wait_event(ev[5])       # previous step's top-MLP optimizer part
+            g["M12"].replay()
+            ev[2].record(main)
+            se.wait_event(ev[2])
+            with torch.cuda.stream(se):
+                g["E3"].replay()
+                ev[3].record(se)
+            so.wait_event(ev[2])
+            with torch.cuda.stream(so):
+                g["O"].replay()
+                ev[5].record(so)
+            self._ms["o_pending"] = True
+            g["M3"].replay()
+            if not self._early:
+                main.wait_event(ev[3])
+            return
         if not self._early:
             ev[0].record(main)
             se.wait_event(ev[0])             # this step's batch is loaded (on main)
@@ -1024,6 +1095,8 @@ class DLRMTrainer:
         (embedding updates, the top-MLP optimizer part)."""
         if self._ms is not None:
             torch.cuda.current_stream().wait_stream(self._ms["stream"])
+            if self._ms.get("ostream") is not None:
+                torch.cuda.current_stream().wait_stream(self._ms["ostream"])
         if getattr(self, "_sides", None) is not None:
             torch.cuda.current_stream().wait_stream(self._sides)
 
@@ -1049,28 +1122,37 @@ class DLRMTrainer:
         # own stream beside the embedding update and the bottom backward
         self._ms_wgrad = wgrad_stream and self.cfg.interaction == "dot"
         self._defer_top_wgrad = self._defer_top_wgrad or self._ms_wgrad
+        # TDFO_MS_MERGE=1: bottom fwd + top in one graph, top optimizer part on
+        # a third stream. Measured worse (DLRM-1TB 0.57-0.58 vs 0.545 ms/step,
+        # DCN-v2 2.55 vs 2.50; with GPU_MAX_HW_QUEUES=8 1.19 / 3.58): with 4
+        # HW queues the third stream shares the embedding stream's queue, so
+        # the next lookup queues behind the optimizer pass
+        self._ms_merge = (os.environ.get("TDFO_MS_MERGE", "0") == "1" and not self._ms_wgrad
+                          and not self._defer_top_wgrad)
         plan = self._ms_plan()
         # (stream priorities -- MLP graphs high, embedding graphs low -- were
         # measured at 1.9 ms/step vs 0.556: not used)
         se = self._emb_stream()
         sw = torch.cuda.Stream(device=self.device) if self._ms_wgrad else None
+        so = torch.cuda.Stream(device=self.device) if self._ms_merge else None
         pool = torch.cuda.graph_pool_handle()
         graphs = {}
         main = torch.cuda.current_stream()
         se.wait_stream(main)
-        if sw is not None:
-            sw.wait_stream(main)
+        for x in (sw, so):
+            if x is not None:
+                x.wait_stream(main)
         for name in plan:
             gr = torch.cuda.CUDAGraph()
             # (the MLP graphs capture on torch's own side stream: capture is
             # not allowed on the default stream; replays run on any stream)
-            st = se if name[0] == "E" else (sw if name == "W" else None)
+            st = se if name[0] == "E" else (sw if name == "W" else (so if name == "O" else None))
             with torch.cuda.graph(gr, pool=pool, stream=st):
                 plan[name]()
             graphs[name] = gr
         torch.cuda.synchronize()
-        self._ms = {"graphs": graphs, "stream": se, "wstream": sw,
-                    "events": [torch.cuda.Event() for _ in range(5)]}
+        self._ms = {"graphs": graphs, "stream": se, "wstream": sw, "ostream": so,
+                    "o_pending": False, "events": [torch.cuda.Event() for _ in range(6)]}
         self.graph = "streams"
 
     def capture_graph(self, warmup: int = 2, staged: Optional[bool] = None,

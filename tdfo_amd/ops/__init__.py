@@ -32,6 +32,20 @@ def gemm(a, a_col, b, b_col, bias=None, relu=False, mask=None, out=None, out32=N
                  ldc32, csum_col)
 
 
+def mlp3_supported(k0: int, n0: int, n1: int, n2: int) -> bool:
+    """Widths the fused three-layer MLP forward kernel is built for."""
+    return bool(_native().mlp3_supported(k0, n0, n1, n2))
+
+
+def mlp3_fwd(x, ws, bs, ys):
+    """ys[l] = relu(ys[l-1] @ ws[l]^T + bs[l]) for three layers (ys[-1] = x),
+    bf16 activations; bs[l] None: bias inside K. One fused launch on GPU."""
+    if _gpu(x):
+        _native().mlp3_fwd(x, ws[0], ws[1], ws[2], bs[0], bs[1], bs[2], ys[0], ys[1], ys[2])
+    else:
+        ref.mlp3_fwd(x, ws, bs, ys)
+
+
 def gemm_policy(p: int = -1) -> int:
     """GEMM tile-shape policy of the native library: 0 auto, 1 128x128 tiles
     only, 2 256x128 tiles only; p < 0 only reads it. Returns the previous one."""

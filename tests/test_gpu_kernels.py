@@ -830,3 +830,35 @@ def test_embedding_dense_update_matches_reference(opt, D):
     assert torch.allclose(Wg.cpu(), We, atol=1e-5, rtol=1e-5)
     if opt != ops.EMB_ADAM:
         assert torch.equal(Wg.cpu()[::2], W0[::2])
+
+
+@pytest.mark.parametrize("B", [8192, 1000, 31])
+@pytest.mark.parametrize("strided_out", [False, True])
+def test_mlp3_fused_forward(B, strided_out):
+    """Fused bottom MLP (64 -> 512 -> 256 -> 128, ReLU) vs the fp32 reference
+    layer by layer, and vs the per-layer GEMM launches it replaces; the last
+    output may be a column slice of a wider row (DCN-v2's x_0)."""
+    torch.manual_seed(5)
+    ws = [bf(torch.randn(n, k + 64, device=DEV) / k ** 0.5)[:, :k]
+          for n, k in ((512, 64), (256, 512), (128, 256))]
+    bs = [None, torch.randn(256, 72, device=DEV)[:, 3], torch.randn(128, device=DEV) * 0.1]
+    x = bf(torch.randn(B, 80, device=DEV))[:, :64]
+    wide = torch.zeros(B, 3456, dtype=torch.bfloat16, device=DEV)
+    ys = [torch.empty(B, 576, dtype=torch.bfloat16, device=DEV)[:, :512],
+          torch.empty(B, 320, dtype=torch.bfloat16, device=DEV)[:, :256],
+          wide[:, :128] if strided_out else torch.empty(B, 128, dtype=torch.bfloat16, device=DEV)]
+    ops.mlp3_fwd(x, ws, bs, ys)
+    exp = [torch.empty(B, y.shape[1], dtype=torch.bfloat16, device=DEV) for y in ys]
+    ref.mlp3_fwd(x, ws, bs, exp)
+    for y, e in zip(ys, exp):
+        assert rel_err(y, e) < 2e-2
+    # same numbers as the unfused GEMM chain
+    g = [torch.empty_like(e) for e in exp]
+    h = x
+    for w, b, y in zip(ws, bs, g):
+        ops.gemm(h, False, w, False, b, True, None, y, None, 1)
+        h = y
+    for y, e in zip(ys, g):
+        assert rel_err(y, e) < 1e-2
+    if strided_out:
+        assert wide[:, 128:].abs().sum() == 0
