@@ -65,18 +65,21 @@ __global__ __launch_bounds__(256) void inter_fwd_kernel(
   // each wave walks several samples; sample n+1's feature rows are loaded
   // into a second register set while sample n's MFMAs, LDS packing and
   // stores run, so the HBM round trip overlaps the previous sample's work
+  // loads unconditional at clamped addresses, masked after (a predicated load
+  // makes hipcc branch around it and wait for it: no prefetch overlap)
   auto load = [&](int b, bf16x8_t (&fr)[KS], s16x8_t (&pv)[PC]) {
-    const uint16_t* rp = feat_row(dense, ld_dense, emb, sm, i, F, b);
+    const uint16_t* rp = feat_row(dense, ld_dense, emb, sm, i < F ? i : F - 1, F, b);
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      if (rp) fr[s] = *(const bf16x8_t*)(rp + 16 * s + 8 * h);
-      else    fr[s] = __builtin_bit_cast(bf16x8_t, (s16x8_t){0,0,0,0,0,0,0,0});
+      const s16x8_t v = *(const s16x8_t*)(rp + 16 * s + 8 * h);
+      const s16x8_t z = {0, 0, 0, 0, 0, 0, 0, 0};
+      fr[s] = __builtin_bit_cast(bf16x8_t, i < F ? v : z);
     }
     // dense passthrough chunk, loaded with the feature rows
     const uint16_t* dp = dense + (int64_t)b * ld_dense;
 #pragma unroll
     for (int k = 0; k < PC; ++k)
-      if (lane + 64 * k < D / 8) pv[k] = *(const s16x8_t*)(dp + (lane + 64 * k) * 8);
+      pv[k] = *(const s16x8_t*)(dp + min(lane + 64 * k, D / 8 - 1) * 8);
   };
   const int iters = (B + gridDim.x * WAVES - 1) / (gridDim.x * WAVES);
   bf16x8_t fr[KS], frn[KS];
@@ -164,25 +167,37 @@ __global__ __launch_bounds__(256) void inter_bwd_kernel(
   // loaded into registers right after sample n's went to LDS, so the HBM
   // round trip overlaps sample n's MFMAs and gradient stores
   const int nzc = (D + F * (F - 1) / 2 + 7) / 8;   // dZ chunks read (<= 94 <= 2 x 64)
+  // this lane's 16 S entries (row i = lane & 31, k = 16 ks + 8 h + jj) as
+  // dZ-row offsets of the strict lower triangle, and which of them exist
+  const int i = lane & 31;
+  int soff[16];
+  uint32_t smask = 0;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const int k = 16 * (e >> 3) + 8 * h + (e & 7);
+    const bool ok = i < F && k < F && i != k;
+    const int hi = i > k ? i : k, lo = i > k ? k : i;
+    soff[e] = ok ? D + hi * (hi - 1) / 2 + lo : 0;
+    smask |= (ok ? 1u : 0u) << e;
+  }
+  // Every load is issued unconditionally at a clamped address (chunks past
+  // the row re-read its last chunk and are never written to LDS): a
+  // predicated load made hipcc branch around it, wait for it and park the
+  // dZ chunks in scratch -- no prefetch overlap at all.
   s16x8_t xv[XC];
-  uint4 zv[2];
+  uint4 zv0, zv1;
   auto load = [&](int b) {
 #pragma unroll
     for (int k = 0; k < XC; ++k) {
-      const int c = lane + 64 * k;
-      if (c < F * CPR) {
-        const int j = c / CPR, ch = c - j * CPR;
-        const uint16_t* rp = j == 0 ? dense + (int64_t)b * ld_dense
-                                    : emb + slot[j] + (int64_t)b * slot[32 + j];
-        xv[k] = *(const s16x8_t*)(rp + ch * 8);
-      }
+      const int c = min(lane + 64 * k, F * CPR - 1);
+      const int j = c / CPR, ch = c - j * CPR;
+      const uint16_t* rp = j == 0 ? dense + (int64_t)b * ld_dense
+                                  : emb + slot[j] + (int64_t)b * slot[32 + j];
+      xv[k] = *(const s16x8_t*)(rp + ch * 8);
     }
     const uint16_t* zp = dz + (int64_t)b * ldz;
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int c = lane + 64 * k;
-      if (c < nzc) zv[k] = *(const uint4*)(zp + c * 8);
-    }
+    zv0 = *(const uint4*)(zp + min(lane, nzc - 1) * 8);
+    zv1 = *(const uint4*)(zp + min(lane + 64, nzc - 1) * 8);
   };
   const int iters = (B + gridDim.x * WAVES - 1) / (gridDim.x * WAVES);
   int b = blockIdx.x * WAVES + w;
@@ -191,11 +206,8 @@ __global__ __launch_bounds__(256) void inter_bwd_kernel(
     const bool valid = b < B;
     const int bn = b + gridDim.x * WAVES;
     if (valid) {
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int c = lane + 64 * k;
-        if (c < nzc) *(uint4*)(zrow + c * 8) = zv[k];
-      }
+      if (lane < nzc) *(uint4*)(zrow + lane * 8) = zv0;
+      if (lane + 64 < nzc) *(uint4*)(zrow + (lane + 64) * 8) = zv1;
 #pragma unroll
       for (int k = 0; k < XC; ++k) {
         const int c = lane + 64 * k;
@@ -208,21 +220,17 @@ __global__ __launch_bounds__(256) void inter_bwd_kernel(
     if (it + 1 < iters && bn < B) load(bn);
     wave_sync();
     if (valid) {
-      // A operand: S[i][k], i = lane&31, k = 16ks + 8h + jj
-      const int i = lane & 31;
+      // S operand: S[i][k], i = lane&31, k = 16ks + 8h + jj, read from the
+      // dZ row at the per-lane offsets computed once per kernel (loads
+      // unconditional, masked after)
       bf16x8_t sa[2];
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         s16x8_t t;
 #pragma unroll
         for (int jj = 0; jj < 8; ++jj) {
-          const int k = 16 * ks + 8 * h + jj;
-          uint16_t v = 0;
-          if (i < F && k < F && i != k) {
-            const int hi = i > k ? i : k, lo = i > k ? k : i;
-            v = zrow[D + hi * (hi - 1) / 2 + lo];
-          }
-          t[jj] = (short)v;
+          const uint16_t v = zrow[soff[8 * ks + jj]];
+          t[jj] = (short)(((smask >> (8 * ks + jj)) & 1u) ? v : (uint16_t)0);
         }
         sa[ks] = __builtin_bit_cast(bf16x8_t, t);
       }
@@ -246,27 +254,37 @@ __global__ __launch_bounds__(256) void inter_bwd_kernel(
           }
           s16x8_t bb = {v[0][0], v[0][1], v[0][2], v[0][3],
                         v[1][0], v[1][1], v[1][2], v[1][3]};
+          // dX^T = X^T S (S symmetric): the X fragment as A, S as B, so each
+          // lane's accumulators are 4 runs of 4 consecutive d of ONE feature
+          // row i = lane & 31 (8-B LDS writes below instead of 16 scalar ones)
           acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-              sa[ks], __builtin_bit_cast(bf16x8_t, bb), acc, 0, 0, 0);
+              __builtin_bit_cast(bf16x8_t, bb), sa[ks], acc, 0, 0, 0);
         }
         // dX rows -> per-wave bf16 image ys [32][D] (row 0 gets the concat
         // passthrough dZ[:, :D] and the bottom-MLP ReLU mask here)
-        const int d = 32 * nt + (lane & 31);
-        if (D < 32 && d >= D) continue;
+        if (i < F) {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int ii = (r & 3) + 8 * (r >> 2) + 4 * h;
-          if (ii >= F) continue;
-          float val = acc[r];
-          if (ii == 0) {
-            val += bf2f(zrow[d]);
-            if (relu_mask) {
-              const uint16_t xv = *(const uint16_t*)(xs + (((d >> 3) ^ xswz<D>(0)) << 4) + ((d & 7) << 1));
-              if (!(bf2f(xv) > 0.f)) val = 0.f;
+          for (int gq = 0; gq < 4; ++gq) {
+            const int d0 = 32 * nt + 8 * gq + 4 * h;
+            if (D < 32 && d0 >= D) continue;
+            float v[4];
+#pragma unroll
+            for (int q4 = 0; q4 < 4; ++q4) v[q4] = acc[4 * gq + q4];
+            if (i == 0) {
+              const uint2 zp = *(const uint2*)(zrow + d0);
+              v[0] += bf2f((uint16_t)(zp.x & 0xffff)); v[1] += bf2f((uint16_t)(zp.x >> 16));
+              v[2] += bf2f((uint16_t)(zp.y & 0xffff)); v[3] += bf2f((uint16_t)(zp.y >> 16));
+              if (relu_mask) {
+                const uint2 xm = *(const uint2*)(xs + (((d0 >> 3) ^ xswz<D>(0)) << 4) + ((d0 & 7) << 1));
+                if (!(bf2f((uint16_t)(xm.x & 0xffff)) > 0.f)) v[0] = 0.f;
+                if (!(bf2f((uint16_t)(xm.x >> 16)) > 0.f)) v[1] = 0.f;
+                if (!(bf2f((uint16_t)(xm.y & 0xffff)) > 0.f)) v[2] = 0.f;
+                if (!(bf2f((uint16_t)(xm.y >> 16)) > 0.f)) v[3] = 0.f;
+              }
             }
+            *(uint2*)((char*)ys + i * D * 2 + (((d0 >> 3) ^ xswz<D>(i)) << 4) + ((d0 & 7) << 1)) =
+                make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
           }
-          *(uint16_t*)((char*)ys + ii * D * 2 + (((d >> 3) ^ xswz<D>(ii)) << 4) + ((d & 7) << 1)) =
-              f2bf(val);
         }
       }
       // coalesced 16-B stores of the F gradient rows into their slots (the
