@@ -201,73 +201,34 @@ struct BwdCfg {
 
 // keys[p] = row_offset[t] + id, vals[p] = p, goff[p] = offset of p's pooled
 // gradient row, gscale[p] = per-id scale (psw, 1/len for mean) if needed.
-// One wave per 512 consecutive positions (8 per lane, coalesced loads and
-// stores). The wave binary-searches the bag of its first position once, then
-// holds a window of 64 bag offsets (one per lane) and finds each position's
-// bag with a 6-step search over the window through lane shuffles, sliding
-// the window while positions remain past it. (A binary search over all bag
-// offsets per position -- 18 dependent loads per thread -- took 51 us for
-// DCN-v2's 1.75M ids; a thread per bag walking its bag 128 us, from the
-// 100-id bags' serial walks and strided stores.)
+// One thread per position, its bag by binary search over the bag offsets.
+// (Measured alternatives for DCN-v2's 1.75M multi-hot ids: a thread per bag
+// walking its bag 128 us, a wave per 512 positions sliding a 64-bag offset
+// window 52-63 us, this one 51 us; with ~one id per bag the window variant
+// slid ~8 times per wave and slowed TwoTower / Bert4Rec.)
 template <typename K>
-__global__ __launch_bounds__(256) void emb_keys_kernel(const EmbBwdArgs a, K* __restrict__ keys,
-                                int32_t* __restrict__ vals, int64_t* __restrict__ goff,
-                                float* __restrict__ gscale, int32_t* __restrict__ tail_count) {
-  constexpr int PPL = 8, PPW = 64 * PPL;
+__global__ void emb_keys_kernel(const EmbBwdArgs a, K* __restrict__ keys,
+                                        int32_t* __restrict__ vals, int64_t* __restrict__ goff,
+                                        float* __restrict__ gscale, int32_t* __restrict__ tail_count) {
   if (blockIdx.x == 0 && threadIdx.x == 0) *tail_count = 0;  // read by later kernels
-  const int lane = threadIdx.x & 63;
   const int64_t nbags = (int64_t)a.T * a.B;
-  const int64_t p0 = (((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * PPW;
-  if (p0 >= a.nnz) return;
-  const int64_t pend = min(p0 + (int64_t)PPW, a.nnz);
-  int64_t lo = 0, hi = nbags;                   // last bag j with offsets[j] <= p0
-  while (hi - lo > 1) {
-    const int64_t mid = (lo + hi) >> 1;
-    if (a.offsets[mid] <= p0) lo = mid; else hi = mid;
-  }
-  int64_t jw = lo;                              // window: bags jw .. jw+62, end jw+63
-  int64_t bag[PPL];
-  float inv[PPL];
-#pragma unroll
-  for (int k = 0; k < PPL; ++k) { bag[k] = -1; inv[k] = 1.f; }
-  while (true) {
-    const int64_t ol = a.offsets[min(jw + lane, nbags)];
-    const bool last_win = jw + 63 >= nbags;
-    const int64_t oend = __shfl(ol, 63, 64);
-    // (the shuffles stay outside lane-dependent branches: a bpermute reads
-    // nothing from lanes that are inactive)
-#pragma unroll
-    for (int k = 0; k < PPL; ++k) {
-      const int64_t p = p0 + k * 64 + lane;
-      int l = 0, h = 63;                        // last window lane with offset <= p
-#pragma unroll
-      for (int s = 0; s < 6; ++s) {
-        const int mid = (l + h) >> 1;
-        const int64_t v = __shfl(ol, mid, 64);
-        const bool le = jw + mid < nbags && v <= p;
-        l = le ? mid : l;
-        h = le ? h : mid;
-      }
-      const int64_t o0 = __shfl(ol, l, 64), o1 = __shfl(ol, l + 1, 64);
-      if (bag[k] < 0 && (last_win || p < oend)) {
-        bag[k] = jw + l;
-        inv[k] = (a.mean && o1 > o0) ? 1.f / (float)(o1 - o0) : 1.f;
-      }
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < a.nnz;
+       p += (int64_t)gridDim.x * blockDim.x) {
+    int64_t lo = 0, hi = nbags;                 // last bag j with offsets[j] <= p
+    while (hi - lo > 1) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (a.offsets[mid] <= p) lo = mid; else hi = mid;
     }
-    if (last_win || pend - 1 < oend) break;     // wave-uniform
-    jw += 63;
-  }
-#pragma unroll
-  for (int k = 0; k < PPL; ++k) {
-    const int64_t p = p0 + k * 64 + lane;
-    if (p < pend) {
-      const int64_t j = bag[k];
-      const int t = (int)(j / a.B);
-      const int b = (int)(j - (int64_t)t * a.B);
-      keys[p] = (K)(a.row_offset[t] + a.indices[p]);
-      vals[p] = (int32_t)p;
-      goff[p] = (int64_t)b * a.grad_stride + a.grad_off[t];
-      if (gscale) gscale[p] = (a.psw ? a.psw[p] : 1.f) * inv[k];
+    const int64_t j = lo;
+    const int t = (int)(j / a.B);
+    const int b = (int)(j - (int64_t)t * a.B);
+    keys[p] = (K)(a.row_offset[t] + a.indices[p]);
+    vals[p] = (int32_t)p;
+    goff[p] = (int64_t)b * a.grad_stride + a.grad_off[t];
+    if (gscale) {
+      const int64_t s0 = a.offsets[j], s1 = a.offsets[j + 1];
+      const float inv = (a.mean && s1 > s0) ? 1.f / (float)(s1 - s0) : 1.f;
+      gscale[p] = (a.psw ? a.psw[p] : 1.f) * inv;
     }
   }
 }
@@ -933,7 +894,8 @@ void prep_impl(const EmbBwdArgs& a, const WsLayout& L, hipStream_t s) {
     K* k1 = odd ? keys_out : keys_in;
     int32_t* v0 = odd ? vals_in : vals_out;
     int32_t* v1 = odd ? vals_out : vals_in;
-    const int64_t kb = (a.nnz + 4 * 512 - 1) / (4 * 512);   // 4 waves x 512 positions
+    int64_t kb = (a.nnz + 255) / 256;
+    if (kb > 8192) kb = 8192;
     hipLaunchKernelGGL(emb_keys_kernel<K>, dim3(kb), dim3(256), 0, s, a, k0, v0, goff, gscale,
                        tcount);
     TDFO_CHECK_HIP(hipGetLastError());
