@@ -3,7 +3,7 @@
 # headline and secondary benches, then a kernel-trace profile of the step.
 set -u
 export PYTHONUNBUFFERED=1
-O=gpurun_out/refresh; mkdir -p $O
+O=${O:-gpurun_out/refresh}; mkdir -p $O
 timeout -k 10 900 python -u -m pytest -q -x -m gpu --timeout 300 --timeout-method thread tests > $O/gpu_tests.log 2>&1 || { tail -30 $O/gpu_tests.log; exit 1; }
 tail -2 $O/gpu_tests.log
 timeout -k 10 300 python -u bench.py --steps 100 --warmup 10 > $O/bench_1tb.log 2>&1 || exit 1
