@@ -421,6 +421,13 @@ class DLRMTrainer:
         # exchange overlaps batch i's dense optimizer step and batch i+1
         # starts at its lookup. Numerics are identical to the unpipelined step.
         self.pipeline = bool(cfg.pipeline) and world_size > 1 and self._es is None
+        # pipelined mode: also the next batch's lookup + pooled-embedding
+        # all-to-all in this step's tail (TDFO_PIPE_LOOKUP=0: at the start of
+        # the next step, beside its bottom MLP)
+        self._pipe_lookup = self.pipeline and os.environ.get("TDFO_PIPE_LOOKUP", "1") == "1"
+        on_cuda = dev.type == "cuda"
+        self._ev_loaded = torch.cuda.Event() if (on_cuda and self._pipe_lookup) else None
+        self._ev_lookup = torch.cuda.Event() if (on_cuda and self._pipe_lookup) else None
         self._next = None
         self._primed = False
         # one process: per-stream hipGraphs (capture_graph(streams=True)); the
@@ -519,6 +526,10 @@ class DLRMTrainer:
         if not self.emb.fwd_prep_noop:
             self.emb.stage_fwd_prep(self.ids)
         self.emb.stage_fwd_ids_exchange(async_op=True)
+        if self._pipe_lookup:                # its lookup + pooled exchange too
+            self.emb.ids_exchange_wait()
+            self.emb.stage_fwd_lookup()
+            self._m_out_exchange_next()
         self._next = (dense, ids, label)
         self._primed = True
 
@@ -627,6 +638,36 @@ class DLRMTrainer:
             # the next batch's load, bucketize and id exchange run beside the
             # dense-gradient all-reduce wait and the dense optimizer step.
             eprep = [("e", k[1]) for k in prep]
+            if self._pipe_lookup:
+                # ... and the next batch's lookup + pooled-embedding exchange
+                # follow on the side stream in this step's tail (after the
+                # embedding update they must see), so the next step starts
+                # at its bottom MLP with its pooled embeddings in flight or
+                # landed; the main stream only waits for the next batch's
+                # dense inputs ("jw": an event after the load, not the
+                # whole side stream)
+                return [
+                    ("c", self._s_bottom_fwd),
+                    ("m", self._m_fwd_wait),
+                    ("c", self._s_top),
+                    ("m", emb.backward_start),
+                ] + top_wgrad + [
+                    ("m", self._m_allreduce_top_start),
+                    ("c", self._s_bottom_bwd),
+                    ("m", self._m_allreduce_start),
+                    ("m", emb.backward_wait),
+                    ("e", self._s_emb_update),
+                    ("em", self._m_load_next),
+                    ("em", self._m_mark_loaded),
+                ] + eprep + [
+                    ("em", self._m_ids_exchange_next),
+                    ("em", emb.ids_exchange_wait),
+                    ("e", emb.stage_fwd_lookup),
+                    ("em", self._m_out_exchange_next),
+                    ("m", self._m_allreduce_wait),
+                    ("c", self._s_dense_update),
+                    ("jw", None),
+                ]
             return [
                 ("m", emb.ids_exchange_wait),
                 lookup,
@@ -684,6 +725,11 @@ class DLRMTrainer:
                 torch.cuda.current_stream().wait_stream(se)
             self._on_side = False
             return
+        if kind == "jw":                     # main waits for the next batch's load only
+            if se is not None and self._ev_loaded is not None:
+                torch.cuda.current_stream().wait_event(self._ev_loaded)
+            self._on_side = False
+            return
         if kind in ("e", "em") and se is not None:
             if not getattr(self, "_on_side", False):
                 se.wait_stream(torch.cuda.current_stream())
@@ -715,7 +761,20 @@ class DLRMTrainer:
 
     def _m_fwd_wait(self):
         self._join(self._ls)
+        if self._pipe_lookup and self._ev_lookup is not None and self._side() is not None:
+            # the lookup ran on the side stream in the previous step's tail
+            # (tables it wrote straight into recv have no collective to wait on)
+            torch.cuda.current_stream().wait_event(self._ev_lookup)
         self.emb.forward_wait()
+
+    def _m_mark_loaded(self):
+        if self._ev_loaded is not None:
+            self._ev_loaded.record(torch.cuda.current_stream())
+
+    def _m_out_exchange_next(self):
+        self.emb.stage_fwd_out_exchange()
+        if self._ev_lookup is not None:
+            self._ev_lookup.record(torch.cuda.current_stream())
 
     def _s_emb_lookup_side(self):
         """One process: the pooled lookup (random row gathers, memory-bound)
@@ -1018,6 +1077,16 @@ class DLRMTrainer:
             plan["M4"] = self._s_dense_update
         return plan
 
+    def _ms_run(self, name: str):
+        """Replay a main-stream stage graph, or (TDFO_EAGER_STAGES=M1,M3)
+        launch the stage's kernels eagerly: a graph's end costs the queue
+        13-20 us before the next work starts, an eager launch behind a graph
+        ~0.3 us (profiles/r02_s2/notes.md)."""
+        if name in self._ms["eager"]:
+            self._ms["plan"][name]()
+        else:
+            self._ms["graphs"][name].replay()
+
     def _ms_step(self):
         g, se, sw, ev = (self._ms["graphs"], self._ms["stream"], self._ms["wstream"],
                          self._ms["events"])
@@ -1058,7 +1127,7 @@ class DLRMTrainer:
             g["E1"].replay()
             ev[1].record(se)
             g["E2"].replay()
-        g["M1"].replay()
+        self._ms_run("M1")
         main.wait_event(ev[1])               # pooled embeddings ready
         g["M2"].replay()
         ev[2].record(main)
@@ -1071,7 +1140,7 @@ class DLRMTrainer:
             with torch.cuda.stream(sw):
                 g["W"].replay()
                 ev[4].record(sw)
-        g["M3"].replay()
+        self._ms_run("M3")
         if sw is not None:
             main.wait_event(ev[4])
             g["M4"].replay()
@@ -1151,7 +1220,9 @@ class DLRMTrainer:
                 plan[name]()
             graphs[name] = gr
         torch.cuda.synchronize()
-        self._ms = {"graphs": graphs, "stream": se, "wstream": sw, "ostream": so,
+        eager = {x for x in os.environ.get("TDFO_EAGER_STAGES", "").split(",") if x in ("M1", "M3")}
+        self._ms = {"graphs": graphs, "stream": se, "wstream": sw, "ostream": so, "plan": plan,
+                    "eager": eager if not self._ms_merge else set(),
                     "o_pending": False, "events": [torch.cuda.Event() for _ in range(6)]}
         self.graph = "streams"
 

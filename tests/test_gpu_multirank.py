@@ -115,11 +115,16 @@ def test_two_ranks_match_one_process(strategy, graph, rw_comm, emb_opt, single):
                                                                    float((w - ref_w).abs().max()))
 
 
-@pytest.mark.parametrize("strategy", ["table_wise", "auto"])
-def test_two_ranks_pipelined_input_dist(strategy, single):
+@pytest.mark.parametrize("strategy,rw_comm,pipe_lookup", [
+    ("table_wise", "bf16", "1"), ("auto", "bf16", "1"), ("row_wise", "fp32", "1"),
+    ("data_parallel", "bf16", "1"), ("auto", "bf16", "0")])
+def test_two_ranks_pipelined_input_dist(strategy, rw_comm, pipe_lookup, single, monkeypatch):
     """Input-dist pipelining (next batch's ids exchanged during the dense
-    update) on the staged hipGraphs: same result as one process."""
-    multi = run_distributed(_worker, 2, B, strategy, True, "bf16", "rowwise_adagrad", True,
+    update; TDFO_PIPE_LOOKUP=1: also its lookup and pooled-embedding exchange
+    on the side stream in the step's tail) on the staged hipGraphs: same
+    result as one process."""
+    monkeypatch.setenv("TDFO_PIPE_LOOKUP", pipe_lookup)
+    multi = run_distributed(_worker, 2, B, strategy, True, rw_comm, "rowwise_adagrad", True,
                             device="cuda", timeout=600)
     p1, tabs1, loss1 = single("rowwise_adagrad")
     tol = 3e-3

@@ -160,10 +160,14 @@ def test_dlrm_data_parallel_matches_single_process(strategy):
 
 
 @pytest.mark.parametrize("strategy", ["table_wise", "row_wise", "auto"])
-def test_dlrm_pipelined_input_dist_is_exact(strategy):
+@pytest.mark.parametrize("pipe_lookup", ["1", "0"])
+def test_dlrm_pipelined_input_dist_is_exact(strategy, pipe_lookup, monkeypatch):
     """Input-dist pipelining (next batch's ids exchanged during this step's
-    dense update) changes only when the exchange runs: parameters and tables
-    after 4 steps equal the unpipelined run bit for bit."""
+    dense update; with TDFO_PIPE_LOOKUP=1 also its lookup and pooled-embedding
+    exchange, after this step's embedding update) changes only when the
+    exchanges run: parameters and tables after 4 steps equal the unpipelined
+    run bit for bit."""
+    monkeypatch.setenv("TDFO_PIPE_LOOKUP", pipe_lookup)
     B, steps = 8, 4
     plain = run_distributed(_dlrm_worker, 2, B, steps, strategy, "rowwise_adagrad", "fp32", False)
     piped = run_distributed(_dlrm_worker, 2, B, steps, strategy, "rowwise_adagrad", "fp32", True)
