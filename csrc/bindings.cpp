@@ -36,6 +36,30 @@ void check_2d_rowmajor(const Tensor& t, const char* name) {
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 // ------------------------------------------------------------------ gemm
+// GEMM batching (ops.gemm_batch): while on, gemm() validates and records its
+// launch instead of enqueueing it; gemm_batch_end() enqueues the recorded
+// launches in order through tdfo::gemm_group (pairs share one launch). The
+// operand tensors are kept alive until then.
+struct GemmBatch {
+  bool on = false;
+  std::vector<tdfo::GemmArgs> args;
+  std::vector<Tensor> keep;
+};
+thread_local GemmBatch g_gemm_batch;
+
+void gemm_batch_begin() {
+  TORCH_CHECK(!g_gemm_batch.on, "gemm_batch: already open");
+  g_gemm_batch.on = true;
+}
+
+void gemm_batch_end() {
+  GemmBatch& b = g_gemm_batch;
+  b.on = false;
+  if (!b.args.empty()) tdfo::gemm_group(b.args.data(), (int)b.args.size(), cur_stream());
+  b.args.clear();
+  b.keep.clear();
+}
+
 void gemm(const Tensor& a_in, bool a_col, const Tensor& b_in, bool b_col,
           const c10::optional<Tensor>& bias, bool relu,
           const c10::optional<Tensor>& mask, const c10::optional<Tensor>& out,
@@ -120,6 +144,12 @@ void gemm(const Tensor& a_in, bool a_col, const Tensor& b_in, bool b_col,
     g.C2 = bf16_mut(*out2); g.ldc2 = out2->stride(0);
   }
   TORCH_CHECK(!(mul || add) || out2, "gemm: mul/add need out2");
+  if (g_gemm_batch.on) {
+    g_gemm_batch.args.push_back(g);
+    g_gemm_batch.keep.push_back(a);                // may be a zero-padded copy
+    g_gemm_batch.keep.push_back(b);
+    return;
+  }
   tdfo::gemm_bf16(g, cur_stream());
 }
 
@@ -1102,6 +1132,10 @@ TORCH_LIBRARY(tdfo, m) {
   m.def("mlp3_supported(int k0, int n0, int n1, int n2) -> bool", mlp3_supported);
   m.def("mlp3_fwd(Tensor x, Tensor w0, Tensor w1, Tensor w2, Tensor? b0, Tensor? b1, "
         "Tensor? b2, Tensor(a!) y0, Tensor(b!) y1, Tensor(c!) y2) -> ()");
+  m.def("gemm_batch_begin() -> ()", gemm_batch_begin);
+  m.def("gemm_batch_end() -> ()", gemm_batch_end);
+  m.def("gemm_pairing(int v) -> int",
+        [](int64_t v) { return (int64_t)tdfo::gemm_pairing((int)v); });
   m.def("radix_sort_tiled(int v) -> int",
         [](int64_t v) { return (int64_t)tdfo::radix_sort_tiled((int)v); });
   m.def("radix_sort_max_bits(int b) -> int",

@@ -38,6 +38,11 @@ struct GemmArgs {
   int abl;   // perf-ablation bits (0 in production): 1 skip A loads, 2 skip B loads, 4 skip all in-loop loads
 };
 void gemm_bf16(const GemmArgs& a, hipStream_t s);
+// Launch n independent GEMMs in order; consecutive (weight grad, dgrad)
+// pairs on the small-tile kernel share one paired launch (gemm_pairing(0):
+// never). Returns after enqueueing.
+void gemm_group(const GemmArgs* a, int n, hipStream_t s);
+int gemm_pairing(int v);
 // Tile-shape policy for gemm_bf16 (0 auto, 1 128x128 only, 2 256x128 only);
 // p < 0 just reads it. Returns the previous policy.
 int gemm_policy(int p);

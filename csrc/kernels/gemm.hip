@@ -152,9 +152,10 @@ __device__ __forceinline__ bf16x8_t frag_col(const TDFO_LDS char* tile, int c0,
 struct TileIdx {
   int tm, tn, split;
 };
-__device__ __forceinline__ TileIdx tile_of(int tiles_m, int tiles_n, int splits) {
+__device__ __forceinline__ TileIdx tile_of(int tiles_m, int tiles_n, int splits,
+                                           int bid = -1) {
   const int tiles = tiles_m * tiles_n;
-  const int w = xcd_remap(blockIdx.x, tiles * splits);
+  const int w = xcd_remap(bid < 0 ? (int)blockIdx.x : bid, tiles * splits);
   const int split = w / tiles, t = w - split * tiles;
   return {t / tiles_n, t - (t / tiles_n) * tiles_n, split};
 }
@@ -503,17 +504,18 @@ __device__ __forceinline__ void csum_store(const GemmArgs& p, const f32x4_t (&cs
 // Small-tile kernel: BMT x 128 x 64 (BMT = 128, or 64 for row-layout A when
 // the 128-row grid leaves CUs idle), 4 waves (2x2 of (BMT/2)x64), 2-deep glds
 // ring (2 x (BMT + 128) x 64 x 2 B of LDS) -> 2+ blocks per CU.
+// Body of the small-tile kernel for block `bid` of this problem's grid (a
+// paired launch runs two problems' bodies in one grid, gemm_pair_kernel).
 template <int BMT, bool A_COL, bool B_COL>
-__global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs p) {
+__device__ __forceinline__ void gemm_small_body(const GemmArgs& p, int bid, char* smem_raw) {
   static_assert(BMT == 128 || !A_COL, "64-row tiles need a row-layout A");
   constexpr int MI = BMT / 32;                   // 16-row fragments per wave
   constexpr int A_BYTES = BMT * BK * 2;
   constexpr int ST = A_BYTES + TILE_BYTES;
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   TDFO_LDS char* smem = (TDFO_LDS char*)smem_raw;
 
   const int tiles_m = (p.M + BMT - 1) / BMT, tiles_n = (p.N + BN - 1) / BN;
-  const TileIdx ti = tile_of(tiles_m, tiles_n, p.splits);
+  const TileIdx ti = tile_of(tiles_m, tiles_n, p.splits, bid);
   const int m0 = ti.tm * BMT, n0 = ti.tn * BN;
 
   const int ktiles = p.K / BK;
@@ -575,6 +577,24 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs p) {
     kloop(BoolC<false>{});
   }
   epilogue<BMT, 256, MI>(p, acc, smem_raw, m0, n0, wr, wc, lane, tid, ti.split);
+}
+
+template <int BMT, bool A_COL, bool B_COL>
+__global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  gemm_small_body<BMT, A_COL, B_COL>(p, blockIdx.x, smem_raw);
+}
+
+// Two independent small-tile GEMMs in one grid: blocks [0, nb0) run problem
+// 0, the rest problem 1 (e.g. a layer's weight grad and its dgrad, both
+// reading dy). Each small launch pays ~4-6 us of fill / drain / launch in the
+// graph (profiles/gemm_step_ab.md: 5.9 us for a one-K-tile 256-block GEMM);
+// paired, the two problems' blocks also fill each other's idle CUs.
+template <int BM0, bool AC0, bool BC0, int BM1, bool AC1, bool BC1>
+__global__ __launch_bounds__(256, 2) void gemm_pair_kernel(GemmArgs p0, GemmArgs p1, int nb0) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  if ((int)blockIdx.x < nb0) gemm_small_body<BM0, AC0, BC0>(p0, blockIdx.x, smem_raw);
+  else                       gemm_small_body<BM1, AC1, BC1>(p1, blockIdx.x - nb0, smem_raw);
 }
 
 // ---------------------------------------------------------------------------
@@ -832,8 +852,16 @@ __global__ __launch_bounds__(256, 1) void gemm_deep_kernel(GemmArgs p) {
 // DCN-v2 cross layers (1728 tiles) 256x128 is ahead (3.19 vs 3.28 ms/step).
 int g_policy = 0;
 
+// A small-tile launch a problem would get (bmt 0: another kernel).
+struct SmallPlan {
+  int bmt, grid;
+  GemmArgs args;
+};
+
+// plan != nullptr: decide only; fill *plan (bmt 0 if the problem would not
+// run on the small-tile kernel) and launch nothing.
 template <bool AC, bool BC>
-void launch(const GemmArgs& a, hipStream_t s) {
+void launch(const GemmArgs& a, hipStream_t s, SmallPlan* plan = nullptr) {
   static bool attr = false;
   if (!attr) {
     TDFO_CHECK_HIP(hipFuncSetAttribute((const void*)gemm_kernel<128, AC, BC>,
@@ -876,8 +904,27 @@ void launch(const GemmArgs& a, hipStream_t s) {
   const bool deep25 = g_policy == 25 && !AC && big_tiles * a.splits < 256 &&
                       small_tiles * a.splits <= 512 && ktps >= 16;
   if (g_policy == 25 && !deep25 && !small_only) big = true;
-  if (g_policy == 23 || deep25 ||
-      (g_policy == 24 && !big && small_tiles * a.splits <= 512 && ktps >= 16)) {
+  const bool deep = g_policy == 23 || deep25 ||
+                    (g_policy == 24 && !big && small_tiles * a.splits <= 512 && ktps >= 16);
+  const bool w4 = !small_only && (g_policy == 20 || (g_policy == 22 && big_tiles * a.splits >= 128) ||
+                                  (g_policy == 21 && small_tiles * a.splits >= 1024));
+  if (plan) {
+    plan->bmt = 0;
+    plan->args = b;
+    if (deep || w4 || big) return;
+    if constexpr (!AC) {
+      const int thr64 = g_policy == 5 ? 512 : 256;
+      if (small_tiles * a.splits < thr64 && g_policy != 3 && g_policy != 2) {
+        plan->bmt = 64;
+        plan->grid = ((a.M + 63) / 64) * tn * a.splits;
+        return;
+      }
+    }
+    plan->bmt = 128;
+    plan->grid = small_tiles * a.splits;
+    return;
+  }
+  if (deep) {
     dim3 grid(small_tiles * a.splits);
     hipLaunchKernelGGL((gemm_deep_kernel<AC, BC>), grid, dim3(256), DSMEM, s, b);
     TDFO_CHECK_HIP(hipGetLastError());
@@ -931,6 +978,73 @@ void gemm_bf16(const GemmArgs& a, hipStream_t s) {
     if (a.b_col) launch<true, true>(a, s); else launch<true, false>(a, s);
   } else {
     if (a.b_col) launch<false, true>(a, s); else launch<false, false>(a, s);
+  }
+}
+
+namespace {
+SmallPlan small_plan(const GemmArgs& a) {
+  SmallPlan p{};
+  if (a.a_col) {
+    if (a.b_col) launch<true, true>(a, nullptr, &p); else launch<true, false>(a, nullptr, &p);
+  } else {
+    if (a.b_col) launch<false, true>(a, nullptr, &p); else launch<false, false>(a, nullptr, &p);
+  }
+  return p;
+}
+
+// layout code of a problem: 0 row/row, 1 row/col, 3 col/col (col/row unused)
+int layout_of(const GemmArgs& a) { return (a.a_col ? 2 : 0) | (a.b_col ? 1 : 0); }
+
+template <int BM0, bool AC0, bool BC0, int BM1, bool AC1, bool BC1>
+void pair_launch(const SmallPlan& p0, const SmallPlan& p1, hipStream_t s) {
+  auto fn = gemm_pair_kernel<BM0, AC0, BC0, BM1, AC1, BC1>;
+  static bool attr = false;
+  if (!attr) {
+    TDFO_CHECK_HIP(hipFuncSetAttribute((const void*)fn,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, SMEM_BYTES));
+    attr = true;
+  }
+  hipLaunchKernelGGL(fn, dim3(p0.grid + p1.grid), dim3(256), SMEM_BYTES, s, p0.args, p1.args,
+                     p0.grid);
+  TDFO_CHECK_HIP(hipGetLastError());
+}
+
+// The pairs the MLP backward issues: a layer's dgrad (row A, col B; 64- or
+// 128-row tiles) with its weight grad (col A, col B, 128-row tiles).
+bool try_pair(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s) {
+  const SmallPlan p0 = small_plan(a0), p1 = small_plan(a1);
+  if (!p0.bmt || !p1.bmt) return false;
+  const int l0 = layout_of(a0), l1 = layout_of(a1);
+  if (l0 == 3 && p0.bmt == 128 && l1 == 1) {
+    if (p1.bmt == 64) pair_launch<128, true, true, 64, false, true>(p0, p1, s);
+    else              pair_launch<128, true, true, 128, false, true>(p0, p1, s);
+    return true;
+  }
+  if (l1 == 3 && p1.bmt == 128 && l0 == 1) {
+    if (p0.bmt == 64) pair_launch<128, true, true, 64, false, true>(p1, p0, s);
+    else              pair_launch<128, true, true, 128, false, true>(p1, p0, s);
+    return true;
+  }
+  return false;
+}
+}  // namespace
+
+int g_pair = 1;
+
+int gemm_pairing(int v) {
+  const int old = g_pair;
+  if (v >= 0) g_pair = v ? 1 : 0;
+  return old;
+}
+
+void gemm_group(const GemmArgs* a, int n, hipStream_t s) {
+  for (int i = 0; i < n;) {
+    if (g_pair && i + 1 < n && try_pair(a[i], a[i + 1], s)) {
+      i += 2;
+      continue;
+    }
+    gemm_bf16(a[i], s);
+    ++i;
   }
 }
 

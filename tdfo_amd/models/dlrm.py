@@ -446,6 +446,11 @@ class DLRMTrainer:
                                          "main" if cfg.interaction == "dcn" else "1")
         self._ms_wgrad = False
         self._ms_merge = False
+        # (weight grad, dgrad) of a layer as one paired small-tile launch
+        # (TDFO_PAIR_BWD=0: two launches); only where the weight grad issues
+        # nothing but its GEMM (one GPU: slabs summed by the optimizer)
+        self._pair_bwd = (dev.type == "cuda" and self._opt_sums_slabs
+                          and os.environ.get("TDFO_PAIR_BWD", "1") == "1")
         # TDFO_FUSED_BOTTOM=1: the bottom MLP forward as one fused kernel
         # (csrc/kernels/mlp_fused.hip) when its widths are the DLRM / DCN-v2
         # ones. Off by default: 17.4 vs 19.5 us for the three GEMM launches in
@@ -566,9 +571,13 @@ class DLRMTrainer:
             self._ws.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(self._ws):
                 wgrad()
-        else:
+            self._dgrad(L, x, dy, dx, x_is_relu)
+            return
+        # one GPU: the weight grad (split-K slabs summed by the optimizer, no
+        # reduce launch in between) and the dgrad go out as one paired launch
+        with ops.gemm_batch(self._pair_bwd and dx is not None):
             wgrad()
-        self._dgrad(L, x, dy, dx, x_is_relu)
+            self._dgrad(L, x, dy, dx, x_is_relu)
 
     def _wg_splits(self, M: int, N: int) -> int:
         return ops.wgrad_splits(M, N, self.B, self._wg_target, slots=self._wg_slots)

@@ -46,6 +46,33 @@ def mlp3_fwd(x, ws, bs, ys):
         ref.mlp3_fwd(x, ws, bs, ys)
 
 
+class gemm_batch:
+    """Context manager: GEMMs issued inside are recorded and enqueued in
+    order on exit, consecutive (weight grad, dgrad) pairs on the small-tile
+    kernel as ONE launch (the MLP backward). Only ops.gemm calls may be
+    issued inside (other ops would be enqueued ahead of the recorded GEMMs).
+    No-op off the GPU."""
+
+    def __init__(self, enabled: bool = True):
+        self.enabled = enabled
+
+    def __enter__(self):
+        if self.enabled:
+            _native().gemm_batch_begin()
+        return self
+
+    def __exit__(self, *exc):
+        if self.enabled:
+            _native().gemm_batch_end()
+        return False
+
+
+def gemm_pairing(v: int = -1) -> int:
+    """Paired small-tile launches inside gemm_batch: 1 on (default), 0 off;
+    v < 0 only reads it. Returns the previous value."""
+    return int(_native().gemm_pairing(v))
+
+
 def gemm_policy(p: int = -1) -> int:
     """GEMM tile-shape policy of the native library: 0 auto, 1 128x128 tiles
     only, 2 256x128 tiles only; p < 0 only reads it. Returns the previous one."""

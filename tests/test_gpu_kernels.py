@@ -862,3 +862,35 @@ def test_mlp3_fused_forward(B, strided_out):
         assert rel_err(y, e) < 1e-2
     if strided_out:
         assert wide[:, 128:].abs().sum() == 0
+
+
+@pytest.mark.parametrize("M", [8192, 1000])
+@pytest.mark.parametrize("N,K", [(1024, 512), (256, 512), (512, 256)])
+def test_gemm_batch_pairs_wgrad_dgrad(M, N, K):
+    """A layer's weight grad (split-K slabs + column sums) and dgrad (ReLU
+    mask) recorded under ops.gemm_batch go out as one paired launch with the
+    same numbers as two launches, bit for bit."""
+    torch.manual_seed(7)
+    dy = bf(torch.randn(M, N, device=DEV))
+    x = bf(torch.randn(M, K + 64, device=DEV))
+    W = bf(torch.randn(N, K + 64, device=DEV))
+    S = ops.wgrad_splits(N, K, M)
+    res = []
+    for pair in (1, 0):
+        old = ops.gemm_pairing(pair)
+        try:
+            slab = torch.zeros(S * N * (K + 64), device=DEV)
+            dx = torch.zeros(M, K, dtype=torch.bfloat16, device=DEV)
+            with ops.gemm_batch():
+                ops.gemm(dy, True, x[:, :K], True, None, False, None, None, slab, S,
+                         ldc32=K + 64, csum_col=K)
+                ops.gemm(dy, False, W[:, :K], True, None, False, x[:, :K], dx, None, 1)
+            torch.cuda.synchronize()
+        finally:
+            ops.gemm_pairing(old)
+        res.append((slab, dx))
+    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    sl = res[0][0].view(S, N, K + 64).sum(0)
+    assert rel_err(sl[:, :K], dy.float().t() @ x[:, :K].float()) < 1e-3
+    exp = (dy.float() @ W[:, :K].float()) * (x[:, :K].float() > 0)
+    assert rel_err(res[0][1], exp) < 1e-2
