@@ -963,6 +963,8 @@ void head_reduce(const Tensor& part, int64_t nparts, int64_t K, const Tensor& gr
 
 void reduce_rows(const Tensor& inp, int64_t rows, int64_t n, int64_t ld, const Tensor& out,
                  bool accumulate, double scale) {
+  // it would run ahead of the GEMMs a gemm_batch holds back (wrong order)
+  TORCH_CHECK(!g_gemm_batch.on, "reduce_rows inside ops.gemm_batch");
   check_dev(inp, "inp");
   TORCH_CHECK(inp.scalar_type() == at::kFloat && out.scalar_type() == at::kFloat, "fp32");
   TORCH_CHECK(inp.numel() >= (rows - 1) * ld + n && out.numel() >= n, "reduce_rows bounds");

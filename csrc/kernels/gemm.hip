@@ -618,14 +618,13 @@ constexpr int LSMEM = LNSTAGE * LSTAGE;            // 144 KiB >= 256x128 fp32 ep
 // between MFMAs (fragment double buffer) and the 3-deep ring keeps two K
 // tiles of DMA in flight.
 template <bool A_COL, bool B_COL, int MI>
-__global__ __launch_bounds__(MI == 4 ? 512 : 256, 1) void gemm_big_kernel(GemmArgs p) {
+__device__ __forceinline__ void gemm_big_body(const GemmArgs& p, int bid, char* smem_raw) {
   constexpr int NW = MI == 4 ? 8 : 4;               // waves
   constexpr int APW = 32 / NW, BPW = 16 / NW;       // A / B pieces per wave per K tile
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   TDFO_LDS char* smem = (TDFO_LDS char*)smem_raw;
 
   const int tiles_m = (p.M + LBM - 1) / LBM, tiles_n = (p.N + BN - 1) / BN;
-  const TileIdx ti = tile_of(tiles_m, tiles_n, p.splits);
+  const TileIdx ti = tile_of(tiles_m, tiles_n, p.splits, bid);
   const int m0 = ti.tm * LBM, n0 = ti.tn * BN;
 
   const int ktiles = p.K / BK;
@@ -753,6 +752,20 @@ __global__ __launch_bounds__(MI == 4 ? 512 : 256, 1) void gemm_big_kernel(GemmAr
   epilogue<LBM, NW * 64, MI>(p, acc, smem_raw, m0, n0, wr, wc, lane, tid, ti.split);
 }
 
+template <bool A_COL, bool B_COL, int MI>
+__global__ __launch_bounds__(MI == 4 ? 512 : 256, 1) void gemm_big_kernel(GemmArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  gemm_big_body<A_COL, B_COL, MI>(p, blockIdx.x, smem_raw);
+}
+
+// Paired 256x128 launch (DCN-v2's one-block-per-CU kernel): see gemm_pair_kernel.
+template <bool AC0, bool BC0, bool AC1, bool BC1>
+__global__ __launch_bounds__(512, 1) void gemm_big_pair_kernel(GemmArgs p0, GemmArgs p1, int nb0) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  if ((int)blockIdx.x < nb0) gemm_big_body<AC0, BC0, 4>(p0, blockIdx.x, smem_raw);
+  else                       gemm_big_body<AC1, BC1, 4>(p1, blockIdx.x - nb0, smem_raw);
+}
+
 // ---------------------------------------------------------------------------
 // Deep-pipelined 128x128 kernel: 4 waves (2x2 of 64x64), DNS-deep glds ring
 // (DNS x 32 KiB, one block per CU) with DNS-2 K tiles of DMA in flight across
@@ -852,10 +865,12 @@ __global__ __launch_bounds__(256, 1) void gemm_deep_kernel(GemmArgs p) {
 // DCN-v2 cross layers (1728 tiles) 256x128 is ahead (3.19 vs 3.28 ms/step).
 int g_policy = 0;
 
-// A small-tile launch a problem would get (bmt 0: another kernel).
+// The launch a problem would get: bmt 64 / 128 small-tile kernel, 256 the
+// 8-wave 256x128 kernel, 0 another kernel.
 struct SmallPlan {
   int bmt, grid;
   GemmArgs args;
+  int big_grid;   // deep-kernel problems: the 256x128 grid if paired instead (0: n/a)
 };
 
 // plan != nullptr: decide only; fill *plan (bmt 0 if the problem would not
@@ -911,7 +926,13 @@ void launch(const GemmArgs& a, hipStream_t s, SmallPlan* plan = nullptr) {
   if (plan) {
     plan->bmt = 0;
     plan->args = b;
-    if (deep || w4 || big) return;
+    plan->big_grid = (deep && !small_only) ? big_tiles * a.splits : 0;
+    if (deep || w4) return;
+    if (big) {                                    // 256x128, 8 waves
+      plan->bmt = 256;
+      plan->grid = big_tiles * a.splits;
+      return;
+    }
     if constexpr (!AC) {
       const int thr64 = g_policy == 5 ? 512 : 256;
       if (small_tiles * a.splits < thr64 && g_policy != 3 && g_policy != 2) {
@@ -1011,10 +1032,37 @@ void pair_launch(const SmallPlan& p0, const SmallPlan& p1, hipStream_t s) {
 
 // The pairs the MLP backward issues: a layer's dgrad (row A, col B; 64- or
 // 128-row tiles) with its weight grad (col A, col B, 128-row tiles).
+template <bool AC0, bool BC0, bool AC1, bool BC1>
+void big_pair_launch(const SmallPlan& p0, const SmallPlan& p1, hipStream_t s) {
+  auto fn = gemm_big_pair_kernel<AC0, BC0, AC1, BC1>;
+  static bool attr = false;
+  if (!attr) {
+    TDFO_CHECK_HIP(hipFuncSetAttribute((const void*)fn,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, LSMEM));
+    attr = true;
+  }
+  hipLaunchKernelGGL(fn, dim3(p0.grid + p1.grid), dim3(512), LSMEM, s, p0.args, p1.args,
+                     p0.grid);
+  TDFO_CHECK_HIP(hipGetLastError());
+}
+
+int g_pair_deep = 1;   // pair a deep-kernel dgrad on 256x128 tiles with its weight grad
+
 bool try_pair(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s) {
-  const SmallPlan p0 = small_plan(a0), p1 = small_plan(a1);
+  SmallPlan p0 = small_plan(a0), p1 = small_plan(a1);
+  // a dgrad the deep 128x128 kernel would take alone (DCN-v2's U dgrad: the
+  // 256x128 grid leaves CUs idle) runs on 256x128 tiles beside a 256x128
+  // weight grad, whose blocks fill those CUs
+  if (g_pair_deep && p0.bmt == 256 && !p1.bmt && p1.big_grid) { p1.bmt = 256; p1.grid = p1.big_grid; }
+  if (g_pair_deep && p1.bmt == 256 && !p0.bmt && p0.big_grid) { p0.bmt = 256; p0.grid = p0.big_grid; }
   if (!p0.bmt || !p1.bmt) return false;
   const int l0 = layout_of(a0), l1 = layout_of(a1);
+  if ((p0.bmt == 256) != (p1.bmt == 256)) return false;
+  if (p0.bmt == 256) {                            // weight grad + dgrad on 256x128 tiles
+    if (l0 == 3 && l1 == 1) { big_pair_launch<true, true, false, true>(p0, p1, s); return true; }
+    if (l1 == 3 && l0 == 1) { big_pair_launch<true, true, false, true>(p1, p0, s); return true; }
+    return false;
+  }
   if (l0 == 3 && p0.bmt == 128 && l1 == 1) {
     if (p1.bmt == 64) pair_launch<128, true, true, 64, false, true>(p0, p1, s);
     else              pair_launch<128, true, true, 128, false, true>(p0, p1, s);
@@ -1032,8 +1080,12 @@ bool try_pair(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s) {
 int g_pair = 1;
 
 int gemm_pairing(int v) {
-  const int old = g_pair;
-  if (v >= 0) g_pair = v ? 1 : 0;
+  // 0 off, 1 on, 2 on but a deep-kernel dgrad is not moved to 256x128 tiles
+  const int old = g_pair ? (g_pair_deep ? 1 : 2) : 0;
+  if (v >= 0) {
+    g_pair = v ? 1 : 0;
+    g_pair_deep = v == 1 ? 1 : 0;
+  }
   return old;
 }
 

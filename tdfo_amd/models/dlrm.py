@@ -958,15 +958,19 @@ class DLRMTrainer:
             dy, dh = self._dcn_bufs(i)
             # dy = dxo * x0 ; acc (+)= dxo * y (+ dxo at i == 0: x_0's residual)
             ops.cross_bwd(dxo, x0, self.dcn_y[i], dy, acc, i != Lc - 1, i == 0)
-            if not self._defer_top_wgrad:
-                self._dcn_wgrad_u(i)
             Uw = fp.bf16(u.name + ".w")
-            ops.gemm(dy, False, Uw[:, :u.in_k], True, None, False, None, dh, None, 1)
-            if not self._defer_top_wgrad:
-                self._dcn_wgrad_v(i)
-            # dx_i = dh V + (i > 0 ? dxo : acc)
-            ops.gemm(dh, False, fp.bf16(f"dcn{i}.v"), True, None, False, None, None, None,
-                     1, add=dxo if i > 0 else acc, out2=self.dcn_dx[i])
+            # U's weight grad and dgrad (both read dy): one paired launch
+            with ops.gemm_batch(self._pair_bwd and not self._defer_top_wgrad):
+                if not self._defer_top_wgrad:
+                    self._dcn_wgrad_u(i)
+                ops.gemm(dy, False, Uw[:, :u.in_k], True, None, False, None, dh, None, 1)
+            # V's weight grad and dgrad (both read dh): one paired launch
+            with ops.gemm_batch(self._pair_bwd and not self._defer_top_wgrad):
+                if not self._defer_top_wgrad:
+                    self._dcn_wgrad_v(i)
+                # dx_i = dh V + (i > 0 ? dxo : acc)
+                ops.gemm(dh, False, fp.bf16(f"dcn{i}.v"), True, None, False, None, None, None,
+                         1, add=dxo if i > 0 else acc, out2=self.dcn_dx[i])
         if self._x0_alias:      # only the dense slot's ReLU-masked gradient
             ops.split_features(self.dcn_dx[0], 1, D, h, self.bot_grad[-1], self.emb.d_recv,
                                self.slot_off, self.slot_stride, True)

@@ -68,8 +68,10 @@ class gemm_batch:
 
 
 def gemm_pairing(v: int = -1) -> int:
-    """Paired small-tile launches inside gemm_batch: 1 on (default), 0 off;
-    v < 0 only reads it. Returns the previous value."""
+    """Paired launches inside gemm_batch: 1 on (default; a dgrad the deep
+    128x128 kernel would take alone moves to 256x128 tiles beside its 256x128
+    weight grad), 2 on without that move, 0 off; v < 0 only reads it.
+    Returns the previous value."""
     return int(_native().gemm_pairing(v))
 
 

@@ -865,8 +865,9 @@ def test_mlp3_fused_forward(B, strided_out):
 
 
 @pytest.mark.parametrize("M", [8192, 1000])
-@pytest.mark.parametrize("N,K", [(1024, 512), (256, 512), (512, 256)])
-def test_gemm_batch_pairs_wgrad_dgrad(M, N, K):
+@pytest.mark.parametrize("N,K", [(1024, 512), (256, 512), (512, 256), (512, 3456), (3456, 512)])
+@pytest.mark.parametrize("policy", [0, 25])
+def test_gemm_batch_pairs_wgrad_dgrad(M, N, K, policy):
     """A layer's weight grad (split-K slabs + column sums) and dgrad (ReLU
     mask) recorded under ops.gemm_batch go out as one paired launch with the
     same numbers as two launches, bit for bit."""
@@ -876,7 +877,8 @@ def test_gemm_batch_pairs_wgrad_dgrad(M, N, K):
     W = bf(torch.randn(N, K + 64, device=DEV))
     S = ops.wgrad_splits(N, K, M)
     res = []
-    for pair in (1, 0):
+    oldp = ops.gemm_policy(policy)
+    for pair in (1, 2, 0):
         old = ops.gemm_pairing(pair)
         try:
             slab = torch.zeros(S * N * (K + 64), device=DEV)
@@ -889,7 +891,11 @@ def test_gemm_batch_pairs_wgrad_dgrad(M, N, K):
         finally:
             ops.gemm_pairing(old)
         res.append((slab, dx))
-    assert torch.equal(res[0][0], res[1][0]) and torch.equal(res[0][1], res[1][1])
+    ops.gemm_policy(oldp)
+    # same numbers however the two problems were launched (the deep and the
+    # 256x128 kernels reduce K in the same order)
+    for r in res[1:]:
+        assert torch.equal(res[0][0], r[0]) and torch.equal(res[0][1], r[1])
     sl = res[0][0].view(S, N, K + 64).sum(0)
     assert rel_err(sl[:, :K], dy.float().t() @ x[:, :K].float()) < 1e-3
     exp = (dy.float() @ W[:, :K].float()) * (x[:, :K].float() > 0)
