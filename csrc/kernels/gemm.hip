@@ -1031,7 +1031,8 @@ void pair_launch(const SmallPlan& p0, const SmallPlan& p1, hipStream_t s) {
 }
 
 // The pairs the MLP backward issues: a layer's dgrad (row A, col B; 64- or
-// 128-row tiles) with its weight grad (col A, col B, 128-row tiles).
+// 128-row tiles) with its weight grad (col A, col B, 128-row tiles), or two
+// weight grads (the deferred ones of a multi-rank step).
 template <bool AC0, bool BC0, bool AC1, bool BC1>
 void big_pair_launch(const SmallPlan& p0, const SmallPlan& p1, hipStream_t s) {
   auto fn = gemm_big_pair_kernel<AC0, BC0, AC1, BC1>;
@@ -1061,7 +1062,12 @@ bool try_pair(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s) {
   if (p0.bmt == 256) {                            // weight grad + dgrad on 256x128 tiles
     if (l0 == 3 && l1 == 1) { big_pair_launch<true, true, false, true>(p0, p1, s); return true; }
     if (l1 == 3 && l0 == 1) { big_pair_launch<true, true, false, true>(p1, p0, s); return true; }
+    if (l0 == 3 && l1 == 3) { big_pair_launch<true, true, true, true>(p0, p1, s); return true; }
     return false;
+  }
+  if (l0 == 3 && l1 == 3 && p0.bmt == 128 && p1.bmt == 128) {   // two weight grads
+    pair_launch<128, true, true, 128, true, true>(p0, p1, s);
+    return true;
   }
   if (l0 == 3 && p0.bmt == 128 && l1 == 1) {
     if (p1.bmt == 64) pair_launch<128, true, true, 64, false, true>(p0, p1, s);

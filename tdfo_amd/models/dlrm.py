@@ -449,8 +449,7 @@ class DLRMTrainer:
         # (weight grad, dgrad) of a layer as one paired small-tile launch
         # (TDFO_PAIR_BWD=0: two launches); only where the weight grad issues
         # nothing but its GEMM (one GPU: slabs summed by the optimizer)
-        self._pair_bwd = (dev.type == "cuda" and self._opt_sums_slabs
-                          and os.environ.get("TDFO_PAIR_BWD", "1") == "1")
+        self._pair_bwd = dev.type == "cuda" and os.environ.get("TDFO_PAIR_BWD", "1") == "1"
         # TDFO_FUSED_BOTTOM=1: the bottom MLP forward as one fused kernel
         # (csrc/kernels/mlp_fused.hip) when its widths are the DLRM / DCN-v2
         # ones. Off by default: 17.4 vs 19.5 us for the three GEMM launches in
@@ -573,11 +572,13 @@ class DLRMTrainer:
                 wgrad()
             self._dgrad(L, x, dy, dx, x_is_relu)
             return
-        # one GPU: the weight grad (split-K slabs summed by the optimizer, no
-        # reduce launch in between) and the dgrad go out as one paired launch
+        # the weight grad and the dgrad go out as one paired launch (the slab
+        # reduce of more than one rank runs after both)
         with ops.gemm_batch(self._pair_bwd and dx is not None):
-            wgrad()
+            fin = self._wgrad_gemm(L, x, dy)
             self._dgrad(L, x, dy, dx, x_is_relu)
+        if fin is not None:
+            fin()
 
     def _wg_splits(self, M: int, N: int) -> int:
         return ops.wgrad_splits(M, N, self.B, self._wg_target, slots=self._wg_slots)
@@ -588,6 +589,14 @@ class DLRMTrainer:
     def _wgrad(self, L: Lin, x, dy):
         """dW[:, :in_k] = dy^T x[:, :in_k]; db (column bcol) = colsum(dy) from
         the same GEMM when the bias is not inside K."""
+        fin = self._wgrad_gemm(L, x, dy)
+        if fin is not None:
+            fin()
+
+    def _wgrad_gemm(self, L: Lin, x, dy):
+        """The weight-grad GEMM alone; returns the split-K slab reduce still
+        to run (more than one rank: the all-reduce needs the grads) or None
+        (one GPU: the optimizer sums the slabs)."""
         n = self._wgrad_n(L)
         csum = -1 if (L.bias_in_k or not self._csum) else L.bcol
         g = self.fp.grad(L.name + ".w").view(-1)
@@ -596,11 +605,12 @@ class DLRMTrainer:
             ops.gemm(dy, True, x[:, :n], True, None, False, None, None, sl, S,
                      ldc32=L.wcols, csum_col=csum)
             if not self._opt_sums_slabs:      # else: partials summed by the optimizer
-                n = L.out * L.wcols
-                ops.reduce_rows(sl, S, n, n, g, False, 1.0)
+                m = L.out * L.wcols
+                return lambda: ops.reduce_rows(sl, S, m, m, g, False, 1.0)
         else:
             ops.gemm(dy, True, x[:, :n], True, None, False, None, None, g, 1,
                      ldc32=L.wcols, csum_col=csum)
+        return None
 
     def _dgrad(self, L: Lin, x, dy, dx, x_is_relu):
         if dx is not None:
@@ -857,11 +867,20 @@ class DLRMTrainer:
         interaction / cross backward: the embedding grads exist without them
         (their all-to-all, or on one GPU the embedding update, runs meanwhile)."""
         if self._defer_top_wgrad:
-            for i in reversed(range(len(self.top_layers))):
-                self._wgrad(self.top_layers[i], self.top_in[i], self.top_grad[i])
+            # independent GEMMs: issued in pairs (the slab reduces after them)
+            fins = []
+            with ops.gemm_batch(self._pair_bwd):
+                for i in reversed(range(len(self.top_layers))):
+                    fins.append(self._wgrad_gemm(self.top_layers[i], self.top_in[i],
+                                                 self.top_grad[i]))
+                for i in reversed(range(len(self.dcn_u))):
+                    dy, _ = self._dcn_bufs(i)
+                    fins.append(self._wgrad_gemm(self.dcn_u[i], self.dcn_h[i], dy))
+            for f in fins:
+                if f is not None:
+                    f()
             for i in reversed(range(len(self.dcn_u))):
-                self._dcn_wgrad_u(i)
-                self._dcn_wgrad_v(i)
+                self._dcn_wgrad_v(i)          # (one shared slab off one GPU)
 
     def _s_bottom_bwd(self):
         for i in reversed(range(len(self.bottom_layers))):
@@ -960,12 +979,16 @@ class DLRMTrainer:
             ops.cross_bwd(dxo, x0, self.dcn_y[i], dy, acc, i != Lc - 1, i == 0)
             Uw = fp.bf16(u.name + ".w")
             # U's weight grad and dgrad (both read dy): one paired launch
+            fin = None
             with ops.gemm_batch(self._pair_bwd and not self._defer_top_wgrad):
                 if not self._defer_top_wgrad:
-                    self._dcn_wgrad_u(i)
+                    fin = self._wgrad_gemm(u, self.dcn_h[i], dy)
                 ops.gemm(dy, False, Uw[:, :u.in_k], True, None, False, None, dh, None, 1)
+            if fin is not None:
+                fin()
             # V's weight grad and dgrad (both read dh): one paired launch
-            with ops.gemm_batch(self._pair_bwd and not self._defer_top_wgrad):
+            with ops.gemm_batch(self._pair_bwd and not self._defer_top_wgrad
+                                and f"dcn{i}.v" in self.wslab):
                 if not self._defer_top_wgrad:
                     self._dcn_wgrad_v(i)
                 # dx_i = dh V + (i > 0 ? dxo : acc)

@@ -900,3 +900,31 @@ def test_gemm_batch_pairs_wgrad_dgrad(M, N, K, policy):
     assert rel_err(sl[:, :K], dy.float().t() @ x[:, :K].float()) < 1e-3
     exp = (dy.float() @ W[:, :K].float()) * (x[:, :K].float() > 0)
     assert rel_err(res[0][1], exp) < 1e-2
+
+
+@pytest.mark.parametrize("policy", [0, 25])
+def test_gemm_batch_pairs_two_wgrads(policy):
+    """Two independent weight grads (a multi-rank step's deferred ones) share
+    one paired launch, bit-identical to two launches."""
+    torch.manual_seed(9)
+    M = 4096
+    dys = [bf(torch.randn(M, n, device=DEV)) for n in (1024, 512)]
+    xs = [bf(torch.randn(M, k, device=DEV)) for k in (512, 1024)]
+    oldp = ops.gemm_policy(policy)
+    res = []
+    for pair in (1, 0):
+        old = ops.gemm_pairing(pair)
+        try:
+            outs = [torch.zeros(dy.shape[1] * x.shape[1], device=DEV) for dy, x in zip(dys, xs)]
+            with ops.gemm_batch():
+                for dy, x, o in zip(dys, xs, outs):
+                    ops.gemm(dy, True, x, True, None, False, None, None, o, 1)
+            torch.cuda.synchronize()
+        finally:
+            ops.gemm_pairing(old)
+        res.append(outs)
+    ops.gemm_policy(oldp)
+    for a, b in zip(res[0], res[1]):
+        assert torch.equal(a, b)
+    for dy, x, o in zip(dys, xs, res[0]):
+        assert rel_err(o.view(dy.shape[1], x.shape[1]), dy.float().t() @ x.float()) < 1e-3
