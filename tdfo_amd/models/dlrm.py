@@ -348,16 +348,26 @@ class DLRMTrainer:
         # the bias column in N at 256; DCN-v2 (256x128 tiles) 2.876 ms with the
         # bias column at 256 vs 2.897 with column sums, 2.985-2.999 at 512.
         dcn = cfg.interaction == "dcn"
-        self._wg_target = int(os.environ.get("TDFO_WGRAD_TARGET", 256 if dcn else 512))
+        # (weight grad, dgrad) of a layer as one paired launch (TDFO_PAIR_BWD=0:
+        # two launches)
+        pair_bwd = dev.type == "cuda" and os.environ.get("TDFO_PAIR_BWD", "1") == "1"
+        # paired with its dgrad, a DLRM weight grad needs fewer split-K blocks
+        # to fill the machine: 256 (0.477-0.479 ms/step) vs 512 (0.504-0.514),
+        # 384 0.502, 128 0.510; unpaired 512 stays best (above)
+        self._wg_target = int(os.environ.get("TDFO_WGRAD_TARGET",
+                                             256 if (dcn or pair_bwd) else 512))
         # TDFO_WGRAD_CSUM=0/1 overrides (A/B)
         self._csum = os.environ.get("TDFO_WGRAD_CSUM", "0" if dcn else "1") != "0"
         # DCN-v2's weight grads run on the one-block-per-CU 256x128 kernel
         # (policy 25, no column sums): splits sized for its 256 resident
         # blocks (U wgrad 65 -> ? us, V 58 -> ? us; TDFO_WGRAD_SLOTS=0: the
         # 128x128-tile target)
+        # (paired with its dgrad on 256x128 tiles the weight grad gets half the
+        # slots: 2.347-2.359 vs 2.419-2.431 ms/step at 256, 2.381 at 512)
         self._wg_slots = int(os.environ.get(
-            "TDFO_WGRAD_SLOTS", 256 if (dcn and not self._csum and dev.type == "cuda"
-                                        and ops.gemm_policy(-1) == 25) else 0))
+            "TDFO_WGRAD_SLOTS", (128 if pair_bwd else 256)
+            if (dcn and not self._csum and dev.type == "cuda"
+                and ops.gemm_policy(-1) == 25) else 0))
         max_slab = 1
         if dcn:
             s_ = self._wg_splits(cfg.dcn_rank, self.top_real)
@@ -449,7 +459,7 @@ class DLRMTrainer:
         # (weight grad, dgrad) of a layer as one paired small-tile launch
         # (TDFO_PAIR_BWD=0: two launches); only where the weight grad issues
         # nothing but its GEMM (one GPU: slabs summed by the optimizer)
-        self._pair_bwd = dev.type == "cuda" and os.environ.get("TDFO_PAIR_BWD", "1") == "1"
+        self._pair_bwd = pair_bwd
         # TDFO_FUSED_BOTTOM=1: the bottom MLP forward as one fused kernel
         # (csrc/kernels/mlp_fused.hip) when its widths are the DLRM / DCN-v2
         # ones. Off by default: 17.4 vs 19.5 us for the three GEMM launches in
