@@ -535,6 +535,38 @@ void cross_bwd(const Tensor& dout, const Tensor& x0, const Tensor& y, const Tens
                   accumulate, add_dout, cur_stream());
 }
 
+// ------------------------------------------------ cross-stream events
+// Events for the per-stream step's cross-stream edges with a chosen release
+// scope: a default hipEvent record performs a system-scope fence (L2
+// writeback + invalidate); kernels already release to device scope when they
+// end, so same-device consumers only need the ordering.
+#define TDFO_HIP_OK(expr)                                                      \
+  do {                                                                         \
+    hipError_t _e = (expr);                                                    \
+    TORCH_CHECK(_e == hipSuccess, "HIP error ", hipGetErrorString(_e));        \
+  } while (0)
+
+int64_t sync_event_create(int64_t mode) {
+  unsigned flags = hipEventDisableTiming;
+  if (mode == 1) flags |= hipEventReleaseToDevice;
+  if (mode == 2) flags |= hipEventDisableSystemFence;
+  hipEvent_t e;
+  TDFO_HIP_OK(hipEventCreateWithFlags(&e, flags));
+  return reinterpret_cast<int64_t>(e);
+}
+
+void sync_event_record(int64_t e) {
+  TDFO_HIP_OK(hipEventRecord(reinterpret_cast<hipEvent_t>(e), cur_stream()));
+}
+
+void sync_event_wait(int64_t e) {
+  TDFO_HIP_OK(hipStreamWaitEvent(cur_stream(), reinterpret_cast<hipEvent_t>(e), 0));
+}
+
+void sync_event_destroy(int64_t e) {
+  TDFO_HIP_OK(hipEventDestroy(reinterpret_cast<hipEvent_t>(e)));
+}
+
 // ------------------------------------------------------- fused MLP
 bool mlp3_supported(int64_t k0, int64_t n0, int64_t n1, int64_t n2) {
   return tdfo::mlp3_fwd_supported((int)k0, (int)n0, (int)n1, (int)n2);
@@ -1134,6 +1166,10 @@ TORCH_LIBRARY(tdfo, m) {
   m.def("mlp3_supported(int k0, int n0, int n1, int n2) -> bool", mlp3_supported);
   m.def("mlp3_fwd(Tensor x, Tensor w0, Tensor w1, Tensor w2, Tensor? b0, Tensor? b1, "
         "Tensor? b2, Tensor(a!) y0, Tensor(b!) y1, Tensor(c!) y2) -> ()");
+  m.def("sync_event_create(int mode) -> int", sync_event_create);
+  m.def("sync_event_record(int e) -> ()", sync_event_record);
+  m.def("sync_event_wait(int e) -> ()", sync_event_wait);
+  m.def("sync_event_destroy(int e) -> ()", sync_event_destroy);
   m.def("gemm_batch_begin() -> ()", gemm_batch_begin);
   m.def("gemm_batch_end() -> ()", gemm_batch_end);
   m.def("gemm_pairing(int v) -> int",

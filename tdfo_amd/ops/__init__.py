@@ -46,6 +46,35 @@ def mlp3_fwd(x, ws, bs, ys):
         ref.mlp3_fwd(x, ws, bs, ys)
 
 
+class SyncEvent:
+    """A cross-stream event with a chosen release scope (mode 0: default
+    system-scope fence, 1: device-scope release, 2: no system fence).
+    record()/wait() act on the current stream, like torch.cuda.Event."""
+
+    def __init__(self, mode: int = 1):
+        self._h = int(_native().sync_event_create(mode))
+
+    def record(self, stream=None):
+        if stream is not None:
+            with torch.cuda.stream(stream):
+                _native().sync_event_record(self._h)
+        else:
+            _native().sync_event_record(self._h)
+
+    def wait(self, stream=None):
+        if stream is not None:
+            with torch.cuda.stream(stream):
+                _native().sync_event_wait(self._h)
+        else:
+            _native().sync_event_wait(self._h)
+
+    def __del__(self):
+        try:
+            _native().sync_event_destroy(self._h)
+        except Exception:
+            pass
+
+
 class gemm_batch:
     """Context manager: GEMMs issued inside are recorded and enqueued in
     order on exit, consecutive (weight grad, dgrad) pairs on the small-tile
