@@ -518,6 +518,20 @@ class DLRMTrainer:
                 and ids.numel() == self.ids.numel():
             se, ev = self._ms["stream"], self._ms["events"][0]
             main = torch.cuda.current_stream()
+            cs = self._ms.get("cstream")
+            if cs is not None and on_device:
+                # the ids copy on its own stream right behind this step's
+                # sort (E2, the ids' last reader), so the next lookup (E1)
+                # waits on an event that is already signalled instead of
+                # queueing the copy behind the embedding update
+                if self._ms["e2_recorded"]:
+                    cs.wait_event(self._ms["ev_e2"])
+                with torch.cuda.stream(cs):
+                    self.ids.copy_(ids, non_blocking=True)
+                    self._ms["ev_copy"].record(cs)
+                se.wait_event(self._ms["ev_copy"])
+                ops.batch_load(dense, self.x0, ids[:0], self.ids[:0], label, self.label)
+                return
             if not on_device:
                 se.wait_stream(main)               # e.g. an H2D the caller ordered on main
             with torch.cuda.stream(se):
@@ -1173,6 +1187,9 @@ class DLRMTrainer:
             g["E1"].replay()
             ev[1].record(se)
             g["E2"].replay()
+            if self._ms.get("cstream") is not None:
+                self._ms["ev_e2"].record(se)
+                self._ms["e2_recorded"] = True
         self._ms_run("M1")
         main.wait_event(ev[1])               # pooled embeddings ready
         g["M2"].replay()
@@ -1202,7 +1219,8 @@ class DLRMTrainer:
         its device copies on each, then passes on_device=True)."""
         main = torch.cuda.current_stream()
         if self.graph == "streams" and self._early:
-            return [main, self._ms["stream"]]
+            cs = self._ms.get("cstream")
+            return [main, self._ms["stream"]] + ([cs] if cs is not None else [])
         return [main]
 
     def sync_streams(self):
@@ -1210,8 +1228,9 @@ class DLRMTrainer:
         (embedding updates, the top-MLP optimizer part)."""
         if self._ms is not None:
             torch.cuda.current_stream().wait_stream(self._ms["stream"])
-            if self._ms.get("ostream") is not None:
-                torch.cuda.current_stream().wait_stream(self._ms["ostream"])
+            for k in ("ostream", "cstream"):
+                if self._ms.get(k) is not None:
+                    torch.cuda.current_stream().wait_stream(self._ms[k])
         if getattr(self, "_sides", None) is not None:
             torch.cuda.current_stream().wait_stream(self._sides)
 
@@ -1275,7 +1294,11 @@ class DLRMTrainer:
         # device-scope release
         emode = int(os.environ.get("TDFO_EVENT_MODE", "2"))
         mk = (lambda: ops.SyncEvent(emode)) if emode else torch.cuda.Event
+        # TDFO_IDS_STREAM=1: the early lookup's ids copy on its own stream
+        cs = (torch.cuda.Stream(device=self.device)
+              if self._early and os.environ.get("TDFO_IDS_STREAM", "0") == "1" else None)
         self._ms = {"graphs": graphs, "stream": se, "wstream": sw, "ostream": so, "plan": plan,
+                    "cstream": cs, "ev_e2": mk(), "ev_copy": mk(), "e2_recorded": False,
                     "eager": eager if not self._ms_merge else set(),
                     "o_pending": False, "events": [mk() for _ in range(6)]}
         self.graph = "streams"
