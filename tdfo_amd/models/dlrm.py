@@ -452,8 +452,11 @@ class DLRMTrainer:
         # whose multi-hot update is 0.42 ms: 2.589 vs 2.633 for "0"), "0" one
         # pass after the bottom backward (profiles/graph_streams.md)
         self._early = os.environ.get("TDFO_EARLY_LOOKUP", "1") == "1"
+        # (with paired weight-grad launches the MLP stream has slack and the
+        # embedding stream's update -> next lookup chain gates the next step:
+        # DLRM-1TB "0" 0.463-0.466 vs "1" 0.471-0.479, "main" 0.471-0.472)
         self._split_opt = os.environ.get("TDFO_SPLIT_OPT",
-                                         "main" if cfg.interaction == "dcn" else "1")
+                                         "main" if cfg.interaction == "dcn" else "0")
         self._ms_wgrad = False
         self._ms_merge = False
         # (weight grad, dgrad) of a layer as one paired small-tile launch
