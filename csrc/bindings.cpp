@@ -567,6 +567,48 @@ void sync_event_destroy(int64_t e) {
   TDFO_HIP_OK(hipEventDestroy(reinterpret_cast<hipEvent_t>(e)));
 }
 
+// A chain of captured graphs joined by event nodes, instantiated as ONE
+// executable graph: kinds[i] = 0 child graph (handles[i] = hipGraph_t of a
+// keep_graph capture), 1 wait on the event handles[i], 2 record it. Stream
+// capture cannot create these event nodes on this ROCm (the external-flag
+// record is refused, the wait crashes), so they are added explicitly.
+int64_t graph_compose(std::vector<int64_t> kinds, std::vector<int64_t> handles) {
+  TORCH_CHECK(kinds.size() == handles.size() && !kinds.empty(), "graph_compose: bad parts");
+  hipGraph_t g;
+  TDFO_HIP_OK(hipGraphCreate(&g, 0));
+  hipGraphNode_t prev = nullptr;
+  for (size_t i = 0; i < kinds.size(); ++i) {
+    hipGraphNode_t n;
+    const hipGraphNode_t* dep = prev ? &prev : nullptr;
+    const size_t nd = prev ? 1 : 0;
+    if (kinds[i] == 0) {
+      TDFO_HIP_OK(hipGraphAddChildGraphNode(&n, g, dep, nd,
+                                            reinterpret_cast<hipGraph_t>(handles[i])));
+    } else if (kinds[i] == 1) {
+      TDFO_HIP_OK(hipGraphAddEventWaitNode(&n, g, dep, nd,
+                                           reinterpret_cast<hipEvent_t>(handles[i])));
+    } else if (kinds[i] == 2) {
+      TDFO_HIP_OK(hipGraphAddEventRecordNode(&n, g, dep, nd,
+                                             reinterpret_cast<hipEvent_t>(handles[i])));
+    } else {
+      TORCH_CHECK(false, "graph_compose: unknown part kind ", kinds[i]);
+    }
+    prev = n;
+  }
+  hipGraphExec_t ex;
+  TDFO_HIP_OK(hipGraphInstantiate(&ex, g, nullptr, nullptr, 0));
+  TDFO_HIP_OK(hipGraphDestroy(g));
+  return reinterpret_cast<int64_t>(ex);
+}
+
+void graph_exec_launch(int64_t ex) {
+  TDFO_HIP_OK(hipGraphLaunch(reinterpret_cast<hipGraphExec_t>(ex), cur_stream()));
+}
+
+void graph_exec_destroy(int64_t ex) {
+  TDFO_HIP_OK(hipGraphExecDestroy(reinterpret_cast<hipGraphExec_t>(ex)));
+}
+
 // ------------------------------------------------------- fused MLP
 bool mlp3_supported(int64_t k0, int64_t n0, int64_t n1, int64_t n2) {
   return tdfo::mlp3_fwd_supported((int)k0, (int)n0, (int)n1, (int)n2);
@@ -1170,6 +1212,9 @@ TORCH_LIBRARY(tdfo, m) {
   m.def("sync_event_record(int e) -> ()", sync_event_record);
   m.def("sync_event_wait(int e) -> ()", sync_event_wait);
   m.def("sync_event_destroy(int e) -> ()", sync_event_destroy);
+  m.def("graph_compose(int[] kinds, int[] handles) -> int", graph_compose);
+  m.def("graph_exec_launch(int ex) -> ()", graph_exec_launch);
+  m.def("graph_exec_destroy(int ex) -> ()", graph_exec_destroy);
   m.def("gemm_batch_begin() -> ()", gemm_batch_begin);
   m.def("gemm_batch_end() -> ()", gemm_batch_end);
   m.def("gemm_pairing(int v) -> int",

@@ -459,6 +459,8 @@ class DLRMTrainer:
                                          "main" if cfg.interaction == "dcn" else "0")
         self._ms_wgrad = False
         self._ms_merge = False
+        self._ms_one = False
+        self._opt_early = False
         # (weight grad, dgrad) of a layer as one paired small-tile launch
         # (TDFO_PAIR_BWD=0: two launches); only where the weight grad issues
         # nothing but its GEMM (one GPU: slabs summed by the optimizer)
@@ -842,6 +844,12 @@ class DLRMTrainer:
             self._s_emb_update()
 
     def _s_top(self):
+        self._s_top_a()
+        self._s_top_b()
+
+    def _s_top_a(self):
+        """Interaction / cross forward, top MLP forward + backward (all top
+        weight grads exist after it)."""
         cfg, fp, B = self.cfg, self.fp, self.B
         D, F = cfg.embedding_dim, self.F
         emb = self.emb
@@ -878,6 +886,13 @@ class DLRMTrainer:
                 dx = self.dz if cfg.interaction == "dot" else self.dcn_dx[-1]
             self._bwd(L, self.top_in[i], self.top_grad[i], dx, x_is_relu=i > 0,
                       wgrad_now=not self._defer_top_wgrad)
+
+    def _s_top_b(self):
+        """Interaction / cross backward: the embedding gradients."""
+        cfg = self.cfg
+        D, F = cfg.embedding_dim, self.F
+        emb = self.emb
+        h = self.h_out
         if cfg.interaction == "dot":
             ops.interaction_bwd(self.dz, h, emb.recv, self.slot_off, self.slot_stride, F, D,
                                 self.bot_grad[-1], emb.d_recv, self.slot_off, self.slot_stride,
@@ -1092,13 +1107,18 @@ class DLRMTrainer:
         # update, beside the bottom-MLP backward (TDFO_SPLIT_OPT=0: one pass)
         split = self._split_opt in ("1", "main") and not self._ms_wgrad
         on_main = self._split_opt == "main"
+        # "early" (composed graphs, dot interaction): the top part on the
+        # embedding stream as soon as the top backward is done (beside the
+        # interaction backward), before the embedding update
+        early = self._opt_early
+        split = split or early
         a, P = self._ar_split, self.fp.p.numel()
 
         def e3():
             emb.backward_start()
             emb.backward_wait()
             self._s_emb_update()
-            if split and not on_main:
+            if split and not on_main and not early:
                 self._dense_update_range(a, P)
 
         def m3():
@@ -1133,6 +1153,10 @@ class DLRMTrainer:
 
             return {"E1": e1, "E2": emb.stage_bwd_prepare, "M12": m12, "E3": e3m,
                     "O": lambda: self._dense_update_range(a, P), "M3": m3m}
+        if early:
+            return {"E1": e1, "E2": emb.stage_bwd_prepare, "M1": self._s_bottom_fwd,
+                    "M2": self._s_top_a, "M2b": self._s_top_b,
+                    "ET": lambda: self._dense_update_range(a, P), "E3": e3, "M3": m3}
         plan = {"E1": e1, "E2": emb.stage_bwd_prepare, "M1": self._s_bottom_fwd,
                 "M2": self._s_top, "E3": e3, "M3": m3}
         if self._ms_wgrad:
@@ -1187,26 +1211,36 @@ class DLRMTrainer:
         # (early lookup: this step's ids were copied on se by load_batch, so the
         # lookup follows the previous step's embedding update on the same stream)
         with torch.cuda.stream(se):
-            g["E1"].replay()
-            ev[1].record(se)
-            g["E2"].replay()
+            if self._ms_one:
+                g["EA"].replay()             # records ev[1] inside
+            else:
+                g["E1"].replay()
+                ev[1].record(se)
+                g["E2"].replay()
             if self._ms.get("cstream") is not None:
                 self._ms["ev_e2"].record(se)
                 self._ms["e2_recorded"] = True
-        self._ms_run("M1")
-        main.wait_event(ev[1])               # pooled embeddings ready
-        g["M2"].replay()
-        ev[2].record(main)
-        se.wait_event(ev[2])                 # embedding gradients ready
+        if self._ms_one:
+            g["M"].replay()                  # waits for ev[1], records ev[2] inside
+        else:
+            self._ms_run("M1")
+            main.wait_event(ev[1])           # pooled embeddings ready
+            g["M2"].replay()
+            ev[2].record(main)
         with torch.cuda.stream(se):
-            g["E3"].replay()
+            if self._opt_early:
+                g["EB"].replay()             # waits for ev[6] and ev[2] inside
+            else:
+                se.wait_event(ev[2])         # embedding gradients ready
+                g["E3"].replay()
             ev[3].record(se)
         if sw is not None:                   # top weight grads on a third stream
             sw.wait_event(ev[2])
             with torch.cuda.stream(sw):
                 g["W"].replay()
                 ev[4].record(sw)
-        self._ms_run("M3")
+        if not self._ms_one:
+            self._ms_run("M3")
         if sw is not None:
             main.wait_event(ev[4])
             g["M4"].replay()
@@ -1266,6 +1300,22 @@ class DLRMTrainer:
         # the next lookup queues behind the optimizer pass
         self._ms_merge = (os.environ.get("TDFO_MS_MERGE", "0") == "1" and not self._ms_wgrad
                           and not self._defer_top_wgrad)
+        emode = int(os.environ.get("TDFO_EVENT_MODE", "2"))
+        mk = (lambda: ops.SyncEvent(emode)) if emode else torch.cuda.Event
+        # TDFO_MS_ONE=1 (default for DLRM): the MLP stream's three graphs (and
+        # the embedding stream's lookup + sort) composed into one executable
+        # graph each, the cross-stream edges as event nodes inside: the queue
+        # idles ~8-10 us at an event node instead of ~14 us at a graph boundary.
+        # DLRM-1TB 0.457-0.458 vs 0.462-0.466 ms/step, Kaggle 0.461 vs 0.459,
+        # DCN-v2 2.362-2.367 vs 2.335-2.340 (off). TDFO_SPLIT_OPT=early on
+        # top (the top-MLP optimizer part on the embedding stream right after
+        # the top backward): 0.469-0.473
+        self._ms_one = (os.environ.get("TDFO_MS_ONE",
+                                       "1" if self.cfg.interaction == "dot" else "0") == "1"
+                        and emode != 0 and not self._ms_wgrad and not self._ms_merge)
+        self._ms_ev = [mk() for _ in range(8)]
+        self._opt_early = (self._ms_one and self._split_opt == "early"
+                           and self.cfg.interaction == "dot")
         plan = self._ms_plan()
         # (stream priorities -- MLP graphs high, embedding graphs low -- were
         # measured at 1.9 ms/step vs 0.556: not used)
@@ -1280,13 +1330,28 @@ class DLRMTrainer:
             if x is not None:
                 x.wait_stream(main)
         for name in plan:
-            gr = torch.cuda.CUDAGraph()
+            gr = torch.cuda.CUDAGraph(keep_graph=self._ms_one)
             # (the MLP graphs capture on torch's own side stream: capture is
             # not allowed on the default stream; replays run on any stream)
             st = se if name[0] == "E" else (sw if name == "W" else (so if name == "O" else None))
             with torch.cuda.graph(gr, pool=pool, stream=st):
                 plan[name]()
             graphs[name] = gr
+        if self._ms_one:
+            # the MLP stream's three graphs chained by the two cross-stream
+            # event nodes (wait: pooled embeddings; record: embedding grads)
+            # (and the embedding stream's: lookup, record, sort; then, with
+            # the early optimizer part, wait, top optimizer part, wait, update)
+            ev = self._ms_ev
+            top = [("graph", graphs["M2"])]
+            if self._opt_early:
+                top += [("record", ev[6]), ("graph", graphs["M2b"])]
+                graphs["EB"] = ops.ComposedGraph([("wait", ev[6]), ("graph", graphs["ET"]),
+                                                  ("wait", ev[2]), ("graph", graphs["E3"])])
+            graphs["M"] = ops.ComposedGraph([("graph", graphs["M1"]), ("wait", ev[1])] + top
+                                            + [("record", ev[2]), ("graph", graphs["M3"])])
+            graphs["EA"] = ops.ComposedGraph([("graph", graphs["E1"]), ("record", ev[1]),
+                                              ("graph", graphs["E2"])])
         torch.cuda.synchronize()
         eager = {x for x in os.environ.get("TDFO_EAGER_STAGES", "").split(",") if x in ("M1", "M3")}
         # cross-stream edges between the step's graphs: recorded without the
@@ -1295,15 +1360,13 @@ class DLRMTrainer:
         # and no host reads these edges): DLRM-1TB 0.477-0.480 vs 0.485-0.487
         # ms/step, DCN-v2 neutral. TDFO_EVENT_MODE=0: torch events, 1: a
         # device-scope release
-        emode = int(os.environ.get("TDFO_EVENT_MODE", "2"))
-        mk = (lambda: ops.SyncEvent(emode)) if emode else torch.cuda.Event
         # TDFO_IDS_STREAM=1: the early lookup's ids copy on its own stream
         cs = (torch.cuda.Stream(device=self.device)
               if self._early and os.environ.get("TDFO_IDS_STREAM", "0") == "1" else None)
         self._ms = {"graphs": graphs, "stream": se, "wstream": sw, "ostream": so, "plan": plan,
                     "cstream": cs, "ev_e2": mk(), "ev_copy": mk(), "e2_recorded": False,
                     "eager": eager if not self._ms_merge else set(),
-                    "o_pending": False, "events": [mk() for _ in range(6)]}
+                    "o_pending": False, "events": self._ms_ev}
         self.graph = "streams"
 
     def capture_graph(self, warmup: int = 2, staged: Optional[bool] = None,

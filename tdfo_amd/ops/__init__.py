@@ -68,9 +68,44 @@ class SyncEvent:
         else:
             _native().sync_event_wait(self._h)
 
+    @property
+    def handle(self) -> int:
+        return self._h
+
     def __del__(self):
         try:
             _native().sync_event_destroy(self._h)
+        except Exception:
+            pass
+
+
+class ComposedGraph:
+    """Captured graphs chained with cross-stream event nodes and instantiated
+    as one executable graph. parts: ("graph", torch.cuda.CUDAGraph captured
+    with keep_graph=True), ("wait", SyncEvent) or ("record", SyncEvent). The
+    torch graphs (and the memory pool their kernels use) must outlive this."""
+
+    def __init__(self, parts):
+        kinds, handles = [], []
+        self._keep = []
+        for kind, obj in parts:
+            if kind == "graph":
+                kinds.append(0)
+                handles.append(int(obj.raw_cuda_graph()))
+            elif kind in ("wait", "record"):
+                kinds.append(1 if kind == "wait" else 2)
+                handles.append(obj.handle)
+            else:
+                raise ValueError(kind)
+            self._keep.append(obj)
+        self._ex = int(_native().graph_compose(kinds, handles))
+
+    def replay(self):
+        _native().graph_exec_launch(self._ex)
+
+    def __del__(self):
+        try:
+            _native().graph_exec_destroy(self._ex)
         except Exception:
             pass
 

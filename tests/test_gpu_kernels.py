@@ -449,8 +449,16 @@ def test_dlrm_step_matches_cpu():
     assert sum(lg[-5:]) < sum(lg[:5])
 
 
-@pytest.mark.parametrize("staged", [False, True])
-def test_dlrm_graph_replay_matches_eager(staged):
+@pytest.mark.parametrize("staged,one", [(False, "0"), (False, "1"), (False, "early"),
+                                        (True, "0")])
+def test_dlrm_graph_replay_matches_eager(staged, one, monkeypatch):
+    """Graph-replayed steps match eager ones: per-stream graphs (one=1: each
+    stream's step as composed graphs joined by in-graph event nodes; early:
+    plus the top-MLP optimizer part on the embedding stream right after the
+    top backward) and the staged multi-rank capture at one rank."""
+    monkeypatch.setenv("TDFO_MS_ONE", "0" if one == "0" else "1")
+    if one == "early":
+        monkeypatch.setenv("TDFO_SPLIT_OPT", "early")
     from tdfo_amd.data.synthetic import SyntheticCriteo
     from tdfo_amd.models.dlrm import DLRMConfig, DLRMTrainer
 
@@ -464,6 +472,9 @@ def test_dlrm_graph_replay_matches_eager(staged):
     for t in (a, b):
         t.load_batch(*batches[0])
     b.capture_graph(warmup=1, staged=staged)
+    if not staged:
+        assert b.graph == "streams" and ("M" in b._ms["graphs"]) == (one != "0")
+        assert ("EB" in b._ms["graphs"]) == (one == "early")
     if staged:
         # one rank: the prep stage is a no-op and is not captured (no empty graph)
         assert all(kind in ("m", "em", "j") or g is not None for kind, g in b.graph)
