@@ -23,6 +23,7 @@ once into a hipGraph and replayed (no tracing compiler):
 """
 from __future__ import annotations
 
+import contextlib
 import math
 import os
 from dataclasses import dataclass, field
@@ -460,6 +461,8 @@ class DLRMTrainer:
         self._ms_wgrad = False
         self._ms_merge = False
         self._ms_one = False
+        bp = os.environ.get("TDFO_BOTTOM_POLICY", "")
+        self._bot_policy = int(bp) if bp != "" and self.device.type == "cuda" else None
         self._opt_early = False
         # (weight grad, dgrad) of a layer as one paired small-tile launch
         # (TDFO_PAIR_BWD=0: two launches); only where the weight grad issues
@@ -803,9 +806,25 @@ class DLRMTrainer:
                           self.h_out])
             return
         n = len(self.bottom_layers)
-        for i, L in enumerate(self.bottom_layers):
-            out = self.bot_in[i + 1][:, :L.out] if i + 1 < n else self.h_out
-            self._fwd(L, self.bot_in[i], out)
+        with self._bottom_policy():
+            for i, L in enumerate(self.bottom_layers):
+                out = self.bot_in[i + 1][:, :L.out] if i + 1 < n else self.h_out
+                self._fwd(L, self.bot_in[i], out)
+
+    @contextlib.contextmanager
+    def _bottom_policy(self):
+        """GEMM tile policy for the bottom MLP (TDFO_BOTTOM_POLICY): its
+        GEMMs run beside the embedding lookup, whose blocks cannot share a CU
+        with a 144 KiB-LDS 256x128-tile block."""
+        p = self._bot_policy
+        if p is None:
+            yield
+            return
+        old = ops.gemm_policy(p)
+        try:
+            yield
+        finally:
+            ops.gemm_policy(old)
 
     def _m_fwd_wait(self):
         self._join(self._ls)
@@ -925,10 +944,11 @@ class DLRMTrainer:
                 self._dcn_wgrad_v(i)          # (one shared slab off one GPU)
 
     def _s_bottom_bwd(self):
-        for i in reversed(range(len(self.bottom_layers))):
-            L = self.bottom_layers[i]
-            dx = self.bot_grad[i - 1] if i > 0 else None
-            self._bwd(L, self.bot_in[i], self.bot_grad[i], dx, x_is_relu=i > 0)
+        with self._bottom_policy():
+            for i in reversed(range(len(self.bottom_layers))):
+                L = self.bottom_layers[i]
+                dx = self.bot_grad[i - 1] if i > 0 else None
+                self._bwd(L, self.bot_in[i], self.bot_grad[i], dx, x_is_relu=i > 0)
         self._join(self._ws)
 
     # Dense gradients are all-reduced in two buckets of the flat buffer, each
