@@ -11,50 +11,57 @@
 namespace tdfo {
 namespace {
 
+// One float4 of parameters per thread. Every load the element needs is issued
+// before the first wait: p / m / v, and the split-K slabs of its layer 8 at a
+// time at clamped addresses (a predicated load makes hipcc branch around it and
+// wait for each one); the segment is picked with wave-uniform selects over the
+// kernel-argument table (dynamically indexing that table compiles to dependent
+// global loads). Slabs are summed in slab order, as before.
 __global__ __launch_bounds__(256) void dense_opt_kernel(DenseOptArgs a) {
   if (a.found_inf && a.found_inf[0] > 0.f) return;
   const float lr = a.hyper[0], step = a.hyper[1], gs = a.hyper[2];
   const float bc1 = 1.f - powf(a.beta1, step), bc2 = 1.f - powf(a.beta2, step);
+  const bool adam = a.opt == OPT_ADAMW || a.opt == OPT_ADAM;
+  const bool has_m = adam || a.opt != OPT_SGD || a.momentum != 0.f;
   const int64_t n4 = a.n / 4;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4;
        i += stride) {
-    float4 p = ((float4*)a.p)[i];
-    float4 g;
-    int sk = -1;
+    const float4 p = ((const float4*)a.p)[i];
+    float4 m = make_float4(0.f, 0.f, 0.f, 0.f), v = m;
+    if (has_m) m = ((const float4*)a.m)[i];
+    if (adam) v = ((const float4*)a.v)[i];
     const int64_t e = 4 * i;
-    for (int k = 0; k < a.nseg; ++k)
-      if (e >= a.seg_start[k] && e < a.seg_start[k] + a.seg_len[k]) sk = k;
-    if (sk < 0) {
-      g = ((const float4*)a.g)[i];
+    const float* sp = a.g + e;
+    int64_t L = 0;
+    int S = 0;
+    for (int k = 0; k < a.nseg; ++k) {
+      const int64_t st = a.seg_start[k], ln = a.seg_len[k];
+      const bool in = e >= st && e < st + ln;
+      sp = in ? a.seg_ptr[k] + (e - st) : sp;
+      L = in ? ln : L;
+      S = in ? a.seg_splits[k] : S;
+    }
+    float4 g;
+    if (S == 0) {
+      g = *(const float4*)sp;
     } else {
       // split-K weight-grad slabs of one layer, summed in fixed order here
       // instead of by a separate reduce launch
-      const int64_t o = e - a.seg_start[sk], L = a.seg_len[sk];
-      const float* sp = a.seg_ptr[sk];
       g = make_float4(0.f, 0.f, 0.f, 0.f);
-      // slab loads issued 4 at a time (independent), summed in slab order
-      const int S = a.seg_splits[sk];
-      int q = 0;
-      for (; q + 4 <= S; q += 4) {
-        float4 t[4];
+      for (int q = 0; q < S; q += 8) {
+        float4 t[8];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) t[u] = *(const float4*)(sp + (q + u) * L + o);
+        for (int u = 0; u < 8; ++u) t[u] = *(const float4*)(sp + min(q + u, S - 1) * L);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          g.x += t[u].x; g.y += t[u].y; g.z += t[u].z; g.w += t[u].w;
-        }
-      }
-      for (; q < S; ++q) {
-        const float4 t = *(const float4*)(sp + q * L + o);
-        g.x += t.x; g.y += t.y; g.z += t.z; g.w += t.w;
+        for (int u = 0; u < 8; ++u)
+          if (q + u < S) { g.x += t[u].x; g.y += t[u].y; g.z += t[u].z; g.w += t[u].w; }
       }
     }
     float pv[4] = {p.x, p.y, p.z, p.w};
     float gv[4] = {g.x * gs, g.y * gs, g.z * gs, g.w * gs};
-    if (a.opt == OPT_ADAMW || a.opt == OPT_ADAM) {
-      float4 m = ((float4*)a.m)[i], v = ((float4*)a.v)[i];
-      float mv[4] = {m.x, m.y, m.z, m.w}, vv[4] = {v.x, v.y, v.z, v.w};
+    float mv[4] = {m.x, m.y, m.z, m.w}, vv[4] = {v.x, v.y, v.z, v.w};
+    if (adam) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         float gg = gv[u];
@@ -68,8 +75,6 @@ __global__ __launch_bounds__(256) void dense_opt_kernel(DenseOptArgs a) {
       ((float4*)a.v)[i] = make_float4(vv[0], vv[1], vv[2], vv[3]);
     } else if (a.opt == OPT_SGD) {
       if (a.momentum != 0.f) {
-        float4 m = ((float4*)a.m)[i];
-        float mv[4] = {m.x, m.y, m.z, m.w};
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const float gg = gv[u] + a.weight_decay * pv[u];
@@ -82,8 +87,6 @@ __global__ __launch_bounds__(256) void dense_opt_kernel(DenseOptArgs a) {
         for (int u = 0; u < 4; ++u) pv[u] -= lr * (gv[u] + a.weight_decay * pv[u]);
       }
     } else {  // adagrad
-      float4 m = ((float4*)a.m)[i];
-      float mv[4] = {m.x, m.y, m.z, m.w};
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const float gg = gv[u] + a.weight_decay * pv[u];
@@ -125,8 +128,7 @@ int blocks_for(int64_t n, int per_thread) {
 
 void dense_optimizer(const DenseOptArgs& a, hipStream_t s) {
   if (a.n <= 0) return;
-  hipLaunchKernelGGL(dense_opt_kernel, dim3(blocks_for(a.n, 4)), dim3(256), 0,
-                     s, a);
+  hipLaunchKernelGGL(dense_opt_kernel, dim3(blocks_for(a.n, 4)), dim3(256), 0, s, a);
 }
 
 void check_finite(const float* g, int64_t n, float* found_inf, hipStream_t s) {

@@ -33,6 +33,7 @@ import torch.distributed as dist
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..utils.capture import graph_capture
 from .. import ops
 from ..optim.flat import FlatOptimizer
 from ..sparse.tables import EmbOptimConfig, TableBatchedEmbedding, TableConfig
@@ -540,7 +541,7 @@ class Bert4RecTrainer:
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with graph_capture(g):
             self._step_body(self.seqs, self.labels)
         torch.cuda.synchronize()
         self.graph = g

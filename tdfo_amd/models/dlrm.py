@@ -32,6 +32,7 @@ from typing import List, Optional, Sequence
 import torch
 import torch.distributed as dist
 
+from ..utils.capture import graph_capture
 from .. import ops
 from ..sparse.planner import ShardingPlan, plan_sharding
 from ..sparse.sharded import ShardedEmbeddingBags
@@ -1354,7 +1355,7 @@ class DLRMTrainer:
             # (the MLP graphs capture on torch's own side stream: capture is
             # not allowed on the default stream; replays run on any stream)
             st = se if name[0] == "E" else (sw if name == "W" else (so if name == "O" else None))
-            with torch.cuda.graph(gr, pool=pool, stream=st):
+            with graph_capture(gr, pool=pool, stream=st):
                 plan[name]()
             graphs[name] = gr
         if self._ms_one:
@@ -1418,7 +1419,7 @@ class DLRMTrainer:
             return
         if not staged:
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
+            with graph_capture(g):
                 self._forward_backward()
             self.graph = g
             return
@@ -1440,7 +1441,7 @@ class DLRMTrainer:
                 # thread_local: a backend's own worker thread (gloo's async
                 # device copies of a collective issued just before) must not
                 # invalidate this thread's capture
-                with torch.cuda.graph(g, pool=pool, stream=se if kind == "e" else None,
+                with graph_capture(g, pool=pool, stream=se if kind == "e" else None,
                                       capture_error_mode="thread_local"):
                     for fn in fns:
                         fn()

@@ -38,6 +38,7 @@ from typing import Dict, List, Optional
 import torch
 import torch.distributed as dist
 
+from ..utils.capture import graph_capture
 from .. import ops
 from ..sparse.tables import EmbOptimConfig, TableBatchedEmbedding, TableConfig
 
@@ -382,7 +383,7 @@ class TwoTowerTrainer:
                 self._step_local(self.B)
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with graph_capture(g):
             self._step_local(self.B)
         torch.cuda.synchronize()
         for t, v in zip(self._state_tensors(), saved):   # warmup must not train

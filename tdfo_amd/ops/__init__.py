@@ -53,6 +53,7 @@ class SyncEvent:
 
     def __init__(self, mode: int = 1):
         self._h = int(_native().sync_event_create(mode))
+        self._pinned = False     # referenced by a ComposedGraph's event node
 
     def record(self, stream=None):
         if stream is not None:
@@ -73,6 +74,11 @@ class SyncEvent:
         return self._h
 
     def __del__(self):
+        # an event an executable graph's node refers to is never destroyed: a
+        # cyclic garbage collection finalizes objects in any order, and the
+        # HIP runtime aborts when a graph exec outlives its node's event
+        if self._pinned:
+            return
         try:
             _native().sync_event_destroy(self._h)
         except Exception:
@@ -95,6 +101,7 @@ class ComposedGraph:
             elif kind in ("wait", "record"):
                 kinds.append(1 if kind == "wait" else 2)
                 handles.append(obj.handle)
+                obj._pinned = True
             else:
                 raise ValueError(kind)
             self._keep.append(obj)

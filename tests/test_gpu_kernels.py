@@ -731,22 +731,33 @@ def test_head_reduce_and_step_bumps():
     assert float(h1[1]) == 5.0 and float(h2[1]) == 10.0 and float(h1[0]) == pytest.approx(0.1)
 
 
-def test_dense_optimizer_slab_segments():
-    """Split-K weight-grad slabs summed inside the optimizer == reduce then step."""
+@pytest.mark.parametrize("opt", ["adamw", "sgd_momentum", "adagrad"])
+def test_dense_optimizer_slab_segments(opt):
+    """Split-K weight-grad slabs summed inside the optimizer == reduce then step
+    (segments of 1, 3, 9 and 17 slabs: partial and several 8-slab groups)."""
     torch.manual_seed(12)
-    n = 4096
+    n = 8192
     p = torch.randn(n, device=DEV)
     g = torch.randn(n, device=DEV)
-    slab = torch.randn(3 * 1024, device=DEV)
-    hyper = torch.tensor([1e-2, 1.0, 1.0], device=DEV)
-    p1, m1, v1 = p.clone(), torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
-    ops.dense_optimizer(p1, g, m1, v1, None, ops.OPT_ADAMW, hyper, wd=0.01,
-                        segments=[(1024, slab, 3)])
+    segs = [(0, 512, 1), (1024, 1024, 3), (2048, 2048, 9), (5120, 1536, 17)]
+    slabs = [torch.randn(S * ln, device=DEV) for _, ln, S in segs]
+    hyper = torch.tensor([1e-2, 2.0, 1.0], device=DEV)
+    code = {"adamw": ops.OPT_ADAMW, "sgd_momentum": ops.OPT_SGD,
+            "adagrad": ops.OPT_ADAGRAD}[opt]
+    kw = {"momentum": 0.9} if opt == "sgd_momentum" else {}
     g2 = g.clone()
-    g2[1024:2048] = slab.view(3, 1024).sum(0)
-    p2, m2, v2 = p.clone(), torch.zeros(n, device=DEV), torch.zeros(n, device=DEV)
-    ops.dense_optimizer(p2, g2, m2, v2, None, ops.OPT_ADAMW, hyper, wd=0.01)
-    assert torch.allclose(p1, p2, atol=1e-6) and torch.allclose(m1, m2, atol=1e-6)
+    for (st, ln, S), sl in zip(segs, slabs):
+        g2[st:st + ln] = sl.view(S, ln).sum(0)
+    m0, v0 = torch.rand(n, device=DEV), torch.rand(n, device=DEV)
+    res = []
+    for grad, sg in ((g, [(st, sl, S) for (st, _, S), sl in zip(segs, slabs)]), (g2, ())):
+        p1 = p.clone()
+        m1 = m0.clone()
+        v1 = v0.clone() if opt == "adamw" else None
+        ops.dense_optimizer(p1, grad, m1, v1, None, code, hyper, wd=0.01, segments=sg, **kw)
+        res.append((p1, m1))
+    assert torch.allclose(res[0][0], res[1][0], atol=1e-5)
+    assert torch.allclose(res[0][1], res[1][1], atol=1e-4)
 
 
 def test_gather_columns_matches_index_select():
