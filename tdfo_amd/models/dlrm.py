@@ -462,6 +462,7 @@ class DLRMTrainer:
         self._ms_wgrad = False
         self._ms_merge = False
         self._ms_one = False
+        self._ms_one_e = False
         bp = os.environ.get("TDFO_BOTTOM_POLICY", "")
         self._bot_policy = int(bp) if bp != "" and self.device.type == "cuda" else None
         self._opt_early = False
@@ -1232,7 +1233,7 @@ class DLRMTrainer:
         # (early lookup: this step's ids were copied on se by load_batch, so the
         # lookup follows the previous step's embedding update on the same stream)
         with torch.cuda.stream(se):
-            if self._ms_one:
+            if self._ms_one_e:
                 g["EA"].replay()             # records ev[1] inside
             else:
                 g["E1"].replay()
@@ -1331,9 +1332,10 @@ class DLRMTrainer:
         # DCN-v2 2.362-2.367 vs 2.335-2.340 (off). TDFO_SPLIT_OPT=early on
         # top (the top-MLP optimizer part on the embedding stream right after
         # the top backward): 0.469-0.473
-        self._ms_one = (os.environ.get("TDFO_MS_ONE",
-                                       "1" if self.cfg.interaction == "dot" else "0") == "1"
-                        and emode != 0 and not self._ms_wgrad and not self._ms_merge)
+        one = os.environ.get("TDFO_MS_ONE", "1" if self.cfg.interaction == "dot" else "0")
+        self._ms_one = (one in ("1", "2") and emode != 0 and not self._ms_wgrad
+                        and not self._ms_merge)
+        self._ms_one_e = self._ms_one and one == "1"    # "2": the MLP stream only
         self._ms_ev = [mk() for _ in range(8)]
         self._opt_early = (self._ms_one and self._split_opt == "early"
                            and self.cfg.interaction == "dot")
@@ -1371,8 +1373,9 @@ class DLRMTrainer:
                                                   ("wait", ev[2]), ("graph", graphs["E3"])])
             graphs["M"] = ops.ComposedGraph([("graph", graphs["M1"]), ("wait", ev[1])] + top
                                             + [("record", ev[2]), ("graph", graphs["M3"])])
-            graphs["EA"] = ops.ComposedGraph([("graph", graphs["E1"]), ("record", ev[1]),
-                                              ("graph", graphs["E2"])])
+            if self._ms_one_e:
+                graphs["EA"] = ops.ComposedGraph([("graph", graphs["E1"]), ("record", ev[1]),
+                                                  ("graph", graphs["E2"])])
         torch.cuda.synchronize()
         eager = {x for x in os.environ.get("TDFO_EAGER_STAGES", "").split(",") if x in ("M1", "M3")}
         # cross-stream edges between the step's graphs: recorded without the
