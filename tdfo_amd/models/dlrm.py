@@ -1384,9 +1384,12 @@ class DLRMTrainer:
         # and no host reads these edges): DLRM-1TB 0.477-0.480 vs 0.485-0.487
         # ms/step, DCN-v2 neutral. TDFO_EVENT_MODE=0: torch events, 1: a
         # device-scope release
-        # TDFO_IDS_STREAM=1: the early lookup's ids copy on its own stream
-        cs = (torch.cuda.Stream(device=self.device)
-              if self._early and os.environ.get("TDFO_IDS_STREAM", "0") == "1" else None)
+        # TDFO_IDS_STREAM=1 (default with composed graphs): the early lookup's
+        # ids copy on its own stream right behind the sort. With composed
+        # graphs DLRM-1TB 0.455-0.456 vs 0.463-0.466 ms/step, Kaggle 0.462 vs
+        # 0.460; with separate graphs it was neutral (0.482-0.483 vs 0.473-0.482)
+        ids_stream = os.environ.get("TDFO_IDS_STREAM", "1" if self._ms_one else "0") == "1"
+        cs = torch.cuda.Stream(device=self.device) if self._early and ids_stream else None
         self._ms = {"graphs": graphs, "stream": se, "wstream": sw, "ostream": so, "plan": plan,
                     "cstream": cs, "ev_e2": mk(), "ev_copy": mk(), "e2_recorded": False,
                     "eager": eager if not self._ms_merge else set(),

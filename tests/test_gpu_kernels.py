@@ -450,13 +450,17 @@ def test_dlrm_step_matches_cpu():
 
 
 @pytest.mark.parametrize("staged,one", [(False, "0"), (False, "1"), (False, "early"),
-                                        (True, "0")])
+                                        (False, "ids0"), (True, "0")])
 def test_dlrm_graph_replay_matches_eager(staged, one, monkeypatch):
     """Graph-replayed steps match eager ones: per-stream graphs (one=1: each
     stream's step as composed graphs joined by in-graph event nodes; early:
     plus the top-MLP optimizer part on the embedding stream right after the
-    top backward) and the staged multi-rank capture at one rank."""
+    top backward; device-resident batches, whose ids the composed mode copies
+    on a third stream behind the sort, ids0: without it) and the staged
+    multi-rank capture at one rank."""
     monkeypatch.setenv("TDFO_MS_ONE", "0" if one == "0" else "1")
+    # composed graphs copy device-resident ids on their own stream (ids0: not)
+    monkeypatch.setenv("TDFO_IDS_STREAM", "1" if one in ("1", "early") else "0")
     if one == "early":
         monkeypatch.setenv("TDFO_SPLIT_OPT", "early")
     from tdfo_amd.data.synthetic import SyntheticCriteo
@@ -469,12 +473,14 @@ def test_dlrm_graph_replay_matches_eager(staged, one, monkeypatch):
     b = DLRMTrainer(cfg, B, DEV)
     data = SyntheticCriteo(cfg.table_rows, B, device=DEV, seed=4)
     batches = [data.next() for _ in range(6)]
+    torch.cuda.synchronize()          # device-resident batches, ready for every stream
     for t in (a, b):
         t.load_batch(*batches[0])
     b.capture_graph(warmup=1, staged=staged)
     if not staged:
         assert b.graph == "streams" and ("M" in b._ms["graphs"]) == (one != "0")
         assert ("EB" in b._ms["graphs"]) == (one == "early")
+        assert (b._ms["cstream"] is not None) == (one in ("1", "early"))
     if staged:
         # one rank: the prep stage is a no-op and is not captured (no empty graph)
         assert all(kind in ("m", "em", "j") or g is not None for kind, g in b.graph)
@@ -482,7 +488,7 @@ def test_dlrm_graph_replay_matches_eager(staged, one, monkeypatch):
     a.step()  # replicate the capture warmup on the eager trainer
     for x in batches[1:]:
         a.load_batch(*x)
-        b.load_batch(*x)
+        b.load_batch(*x, on_device=not staged)
         a.step()
         b.step()
     torch.cuda.synchronize()
