@@ -141,6 +141,11 @@ def main(argv=None):
                          overlap=(args.overlap if args.overlap == 'wgrad' else bool(args.overlap)))
     B = args.batch
     t0 = time.time()
+    if args.host_data:
+        # the host data plane orders its H2D on every input stream and
+        # releases a slot after all of them: a third (ids) stream ties the
+        # slot to the sort and stalls the prefetch (0.604 vs 0.470 ms/step)
+        os.environ.setdefault("TDFO_IDS_STREAM", "0")
     tr = DLRMTrainer(cfg, B, info.device, group=info.group, rank=info.rank, world_size=world)
     if args.host_data:
         from tdfo_amd.data.prefetch import host_prefetcher
