@@ -855,6 +855,376 @@ __global__ __launch_bounds__(256, 1) void gemm_deep_kernel(GemmArgs p) {
   epilogue<BM, 256, MI>(p, acc, smem_raw, m0, n0, wr, wc, lane, tid, ti.split);
 }
 
+// ---------------------------------------------------------------------------
+// Ping-pong tile kernel (BM x 128 x 64, BM = 256 or 128, 8 waves).
+//
+// The waves form two groups of four (waves 0-3 and 4-7: one wave of each
+// group per SIMD) that own the upper and lower half of the tile's rows. Each
+// wave alternates a READ segment (its fragment ds_reads for the next k-chunk,
+// plus its share of the global->LDS DMA) and an MFMA segment, every segment
+// closed by a workgroup barrier; group 1 starts one barrier late, so on every
+// SIMD one wave issues MFMAs while the other reads LDS and issues DMA -- the
+// MFMA pipe sees one wave's back-to-back MFMAs in every interval
+// (cdna_hip_programming.md §5 "8-phase template": per-phase interleave with
+// the wave groups staggered by a barrier; T3+T4 counted vmcnt, T5 setprio).
+// Operands are staged by inline-asm global_load_lds into an NST-deep LDS ring
+// (counted vmcnt, raw s_barrier: DMA stays in flight across barriers).
+//   BM = 256: waves 64x64 (2x2 per group), 16 MFMAs per segment, 3-slot ring
+//             (144 KiB LDS).
+//   BM = 128: waves 64x32 (1x4 per group), both k32 steps of a K tile per
+//             segment (16 MFMAs), 4-slot ring (128 KiB LDS).
+// Epilogue straight from the accumulators (bias, ReLU, ReLU mask, DCN
+// Hadamard/residual second output, fp32 split-K slabs, bias-grad column sums).
+template <int BMP, int NSTP = (BMP == 256 ? 3 : 4)>
+struct PPGeom {
+  static constexpr int BM = BMP;
+  static constexpr int GROWS = BM / 2;                  // rows per wave group
+  static constexpr int WGM = BM == 256 ? 2 : 1;         // waves along M in a group
+  static constexpr int WGN = 4 / WGM;
+  static constexpr int WROWS = GROWS / WGM;             // 64
+  static constexpr int WCOLS = BN / WGN;                // 64 | 32
+  static constexpr int MI = WROWS / 16;                 // 4
+  static constexpr int NJ = WCOLS / 16;                 // 4 | 2
+  static constexpr int KS = NJ == 4 ? 1 : 2;            // k32 steps per segment
+  static constexpr int SEGS = 2 / KS;                   // READ/MFMA segment pairs per K tile
+  static constexpr int A_BYTES = BM * BK * 2;
+  static constexpr int STAGE = A_BYTES + TILE_BYTES;
+  static constexpr int NST = NSTP;
+  static constexpr int LDS = NST * STAGE;
+  static constexpr int APW = BM / 64;                   // A glds pieces per wave per K tile
+  static constexpr int BPW = 2;
+  static constexpr int PPW = APW + BPW;
+  static constexpr int CSF = MI / WGN;                  // column-sum fragments per wave
+};
+
+__device__ __forceinline__ void pp_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+// s_waitcnt vmcnt(n * PPW), n in 0..3 (wave-uniform)
+template <int PPW>
+__device__ __forceinline__ void pp_wait_vm(int n) {
+  if (n >= 3)      asm volatile("s_waitcnt vmcnt(%0)" :: "i"(3 * PPW) : "memory");
+  else if (n == 2) asm volatile("s_waitcnt vmcnt(%0)" :: "i"(2 * PPW) : "memory");
+  else if (n == 1) asm volatile("s_waitcnt vmcnt(%0)" :: "i"(PPW) : "memory");
+  else             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// Epilogue of a wave's MI x NJ fragments (acc holds C transposed: lane l,
+// register r of fragment (i, j) = C[mw + 16 i + (l & 15)][nw + 16 j + 4 (l >> 4) + r]).
+template <int MI, int NJ>
+__device__ __forceinline__ void pp_epilogue(const GemmArgs& p, const f32x4_t (&acc)[MI][NJ],
+                                            int mw, int nw, int lane, int split) {
+  const int rho = lane & 15, g = lane >> 4;
+  float* c32 = p.C32 ? p.C32 + (int64_t)split * p.M * p.ldc32 : nullptr;
+  const bool plain32 = c32 && !p.C && !p.C2 && !p.bias && !p.relu && !p.mask;
+  const bool full = mw + MI * 16 <= p.M && nw + NJ * 16 <= p.N;
+  if (plain32 && full && (p.ldc32 & 3) == 0) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+        *(f32x4_t*)(c32 + (int64_t)(mw + 16 * i + rho) * p.ldc32 + nw + 16 * j + 4 * g) = acc[i][j];
+    return;
+  }
+  const bool vec = full && (!p.C || (((p.ldc & 7) == 0) && al16(p.C))) &&
+                   (!p.mask || (((p.ldm & 7) == 0) && al16(p.mask))) &&
+                   (!p.C2 || (((p.ldc2 & 7) == 0) && al16(p.C2))) &&
+                   (!p.mul || (((p.ldmul & 7) == 0) && al16(p.mul))) &&
+                   (!p.add || (((p.ldadd & 7) == 0) && al16(p.add))) &&
+                   (!c32 || (((p.ldc32 & 3) == 0) && al16(c32)));
+  if (vec) {
+    // rows i, i+1 paired: after a v_permlane16_swap per value every lane
+    // holds 8 consecutive columns (16 B of bf16) of ONE row (guide T21)
+    float bias[NJ][4];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        bias[j][r] = p.bias ? p.bias[(int64_t)(nw + 16 * j + 4 * g + r) * p.bias_stride] : 0.f;
+    // epilogue operands first (all loads in flight before the first use)
+    uint4 mk[MI / 2][NJ], mv[MI / 2][NJ], av[MI / 2][NJ];
+#pragma unroll
+    for (int i = 0; i < MI; i += 2)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int m = mw + (i + (g & 1)) * 16 + rho;
+        const int n = nw + 16 * j + 8 * (g >> 1);
+        if (p.mask) mk[i / 2][j] = *(const uint4*)(p.mask + (int64_t)m * p.ldm + n);
+        if (p.C2 && p.mul) mv[i / 2][j] = *(const uint4*)(p.mul + (int64_t)m * p.ldmul + n);
+        if (p.C2 && p.add) av[i / 2][j] = *(const uint4*)(p.add + (int64_t)m * p.ldadd + n);
+      }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int n = nw + 16 * j + 8 * (g >> 1);
+#pragma unroll
+      for (int i = 0; i < MI; i += 2) {
+        float v[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float a = acc[i][j][r] + bias[j][r], b = acc[i + 1][j][r] + bias[j][r];
+          if (p.relu) {
+            a = fmaxf(a, 0.f);
+            b = fmaxf(b, 0.f);
+          }
+          const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b),
+                                                           false, false);
+          v[r] = __uint_as_float(sw[0]);
+          v[4 + r] = __uint_as_float(sw[1]);
+        }
+        const int m = mw + (i + (g & 1)) * 16 + rho;
+        if (p.mask) {
+          const uint4 q4 = mk[i / 2][j];
+          const uint32_t mu[4] = {q4.x, q4.y, q4.z, q4.w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            if (!(bf2f((uint16_t)(mu[q] & 0xffff)) > 0.f)) v[2 * q] = 0.f;
+            if (!(bf2f((uint16_t)(mu[q] >> 16)) > 0.f)) v[2 * q + 1] = 0.f;
+          }
+        }
+        if (p.C)
+          *(uint4*)(p.C + (int64_t)m * p.ldc + n) =
+              make_uint4(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]), pack2bf(v[4], v[5]),
+                         pack2bf(v[6], v[7]));
+        if (p.C2) {
+          float w2[8];
+#pragma unroll
+          for (int q = 0; q < 8; ++q) w2[q] = v[q];
+          if (p.mul) {
+            const uint4 q4 = mv[i / 2][j];
+            const uint32_t mu[4] = {q4.x, q4.y, q4.z, q4.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              w2[2 * q] *= bf2f((uint16_t)(mu[q] & 0xffff));
+              w2[2 * q + 1] *= bf2f((uint16_t)(mu[q] >> 16));
+            }
+          }
+          if (p.add) {
+            const uint4 q4 = av[i / 2][j];
+            const uint32_t au[4] = {q4.x, q4.y, q4.z, q4.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              w2[2 * q] += bf2f((uint16_t)(au[q] & 0xffff));
+              w2[2 * q + 1] += bf2f((uint16_t)(au[q] >> 16));
+            }
+          }
+          *(uint4*)(p.C2 + (int64_t)m * p.ldc2 + n) =
+              make_uint4(pack2bf(w2[0], w2[1]), pack2bf(w2[2], w2[3]), pack2bf(w2[4], w2[5]),
+                         pack2bf(w2[6], w2[7]));
+        }
+        if (c32) {
+          float* o = c32 + (int64_t)m * p.ldc32 + n;
+          *(float4*)o = make_float4(v[0], v[1], v[2], v[3]);
+          *(float4*)(o + 4) = make_float4(v[4], v[5], v[6], v[7]);
+        }
+      }
+    }
+    return;
+  }
+  // edge tiles / unaligned operands: element by element
+#pragma unroll
+  for (int j = 0; j < NJ; ++j)
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = mw + 16 * i + rho, n = nw + 16 * j + 4 * g + r;
+        if (m >= p.M || n >= p.N) continue;
+        float x = acc[i][j][r] + (p.bias ? p.bias[(int64_t)n * p.bias_stride] : 0.f);
+        if (p.relu) x = fmaxf(x, 0.f);
+        if (p.mask && !(bf2f(p.mask[(int64_t)m * p.ldm + n]) > 0.f)) x = 0.f;
+        if (p.C) p.C[(int64_t)m * p.ldc + n] = f2bf(x);
+        if (c32) c32[(int64_t)m * p.ldc32 + n] = x;
+        if (p.C2) {
+          float x2 = x;
+          if (p.mul) x2 *= bf2f(p.mul[(int64_t)m * p.ldmul + n]);
+          if (p.add) x2 += bf2f(p.add[(int64_t)m * p.ldadd + n]);
+          p.C2[(int64_t)m * p.ldc2 + n] = f2bf(x2);
+        }
+      }
+}
+
+template <int BMP, int NSTP, bool A_COL, bool B_COL>
+__device__ __forceinline__ void gemm_pp_body(const GemmArgs& p, int bid, char* smem_raw) {
+  using G = PPGeom<BMP, NSTP>;
+  constexpr int MI = G::MI, NJ = G::NJ, KS = G::KS, SEGS = G::SEGS, NST = G::NST;
+  TDFO_LDS char* smem = (TDFO_LDS char*)smem_raw;
+  const int tiles_m = (p.M + G::BM - 1) / G::BM, tiles_n = (p.N + BN - 1) / BN;
+  const TileIdx ti = tile_of(tiles_m, tiles_n, p.splits, bid);
+  const int m0 = ti.tm * G::BM, n0 = ti.tn * BN;
+  const int ktiles = p.K / BK;
+  const int per = (ktiles + p.splits - 1) / p.splits;
+  const int kt0 = ti.split * per;
+  const int nk = max(0, min(ktiles, kt0 + per) - kt0);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = w >> 2, q = w & 3;
+  const int wr = q / G::WGN, wc = q - (q / G::WGN) * G::WGN;
+  const int a_row = grp * G::GROWS + wr * G::WROWS;       // wave's first row in the tile
+  const int a_img = a_row >> 7, a_r0 = a_row & 127;
+  const int b_c0 = wc * G::WCOLS;
+  // A/B knobs (p.abl): 1 DMA issued in the MFMA segment (4: after its
+  // MFMAs) instead of the READ segment; 2 no stagger (both groups in phase)
+  const bool gm = p.abl & 1, gend = p.abl & 4, nopp = p.abl & 2;
+  const bool lag = grp == 1 && !nopp;
+
+  f32x4_t acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  // this wave's share of K tile kt's DMA into ring slot `slot`
+  auto stage = [&](int slot, int kt) {
+    TDFO_LDS char* ta = smem + slot * G::STAGE;
+    TDFO_LDS char* tb = ta + G::A_BYTES;
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int i = 0; i < G::APW; ++i) {
+      const int ii = w * G::APW + i, img = ii >> 4;
+      glds_piece_asm<A_COL>(p.A, p.lda, m0 + img * 128, p.M, k0, ta + img * TILE_BYTES, ii & 15,
+                            lane);
+    }
+#pragma unroll
+    for (int i = 0; i < G::BPW; ++i)
+      glds_piece_asm<B_COL>(p.B, p.ldb, n0, p.N, k0, tb, w * G::BPW + i, lane);
+  };
+  // K tiles issued before the wait for tile T (at the end of the segment
+  // holding half T*SEGS - 1) that are younger than T: tile X is issued in the
+  // READ segment of half (X - NST + 1) * SEGS (the prologue for X < NST)
+  auto younger = [&](int T) {
+    int n = 0;
+#pragma unroll
+    for (int d = 1; d < NST; ++d) {
+      const int X = T + d;
+      const int hx = (X - NST + 1) * SEGS;
+      if (X < nk && (X < NST || hx < T * SEGS - 1 || (hx == T * SEGS - 1 && !(lag && gm)))) ++n;
+    }
+    return n;
+  };
+
+  bf16x8_t af[KS][MI], bfr[KS][NJ];
+  const bool csum = A_COL && p.csum_on && ti.tn == 0;
+  f32x4_t cs[G::CSF];
+#pragma unroll
+  for (int c = 0; c < G::CSF; ++c) cs[c] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  if (nk > 0) {
+#pragma unroll
+    for (int s = 0; s < NST; ++s)
+      if (s < nk) stage(s, kt0 + s);
+    pp_wait_vm<G::PPW>(younger(0));
+    pp_barrier();
+    if (lag) pp_barrier();                            // group 1 runs one segment behind
+    const int H = nk * SEGS;
+    for (int h = 0; h < H; ++h) {
+      const int t = h / SEGS, s = h - t * SEGS;
+      // ---- READ segment: DMA of tile t + NST - 1 (first half of tile t),
+      // then this half's fragments
+      const bool dma = s == 0 && t >= 1 && t + NST - 1 < nk;
+      if (dma && !gm) stage((t + NST - 1) % NST, kt0 + t + NST - 1);
+      {
+        const TDFO_LDS char* ta = smem + (t % NST) * G::STAGE + a_img * TILE_BYTES;
+        const TDFO_LDS char* tb = smem + (t % NST) * G::STAGE + G::A_BYTES;
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) {
+          const int ks = s * KS + kk;
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            bfr[kk][j] = B_COL ? frag_col(tb, b_c0 + 16 * j, ks, lane)
+                               : frag_row(tb, b_c0 + 16 * j, ks, lane);
+#pragma unroll
+          for (int i = 0; i < MI; ++i)
+            af[kk][i] = A_COL ? frag_col(ta, a_r0 + 16 * i, ks, lane)
+                              : frag_row(ta, a_r0 + 16 * i, ks, lane);
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (lag && s == SEGS - 1 && t + 1 < nk) pp_wait_vm<G::PPW>(younger(t + 1));
+      pp_barrier();
+      // ---- MFMA segment
+      if (dma && gm && !gend) stage((t + NST - 1) % NST, kt0 + t + NST - 1);
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[kk][j], af[kk][i], acc[i][j],
+                                                                0, 0, 0);
+        if constexpr (A_COL) {
+          if (csum) {
+            const bf16x8_t ones = __builtin_bit_cast(
+                bf16x8_t, (s16x8_t){0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80,
+                                    0x3F80});
+#pragma unroll
+            for (int c = 0; c < G::CSF; ++c) {
+              bf16x8_t a = af[kk][c * G::WGN];
+#pragma unroll
+              for (int u = 1; u < G::WGN; ++u)
+                if (wc == u) a = af[kk][c * G::WGN + u];
+              cs[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, a, cs[c], 0, 0, 0);
+            }
+          }
+        }
+      }
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (dma && gm && gend) stage((t + NST - 1) % NST, kt0 + t + NST - 1);
+      if (!lag && s == SEGS - 1 && t + 1 < nk) pp_wait_vm<G::PPW>(younger(t + 1));
+      pp_barrier();
+    }
+    if (grp == 0 && !nopp) pp_barrier();
+  }
+  if constexpr (A_COL) {
+    if (csum) {
+      float* c32 = p.C32 + (int64_t)ti.split * p.M * p.ldc32;
+#pragma unroll
+      for (int c = 0; c < G::CSF; ++c) {
+        const int m = m0 + a_row + (c * G::WGN + wc) * 16 + (lane & 15);
+        if (lane < 16 && m < p.M) c32[(int64_t)m * p.ldc32 + p.csum_col] = cs[c][0];
+      }
+    }
+  }
+  pp_epilogue<MI, NJ>(p, acc, m0 + a_row, n0 + b_c0, lane, ti.split);
+}
+
+template <int BMP, int NSTP, int OCC, bool A_COL, bool B_COL>
+__global__ __launch_bounds__(512, OCC) void gemm_pp_kernel(GemmArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  gemm_pp_body<BMP, NSTP, A_COL, B_COL>(p, blockIdx.x, smem_raw);
+}
+
+// Two problems in one ping-pong grid (a layer's weight grad + dgrad): blocks
+// [0, nb0) run problem 0 on BM0-row tiles, the rest problem 1 on BM1-row tiles.
+// (the production configuration: 128-row tiles, 2-slot ring, 2 blocks per CU)
+template <bool AC0, bool BC0, bool AC1, bool BC1>
+__global__ __launch_bounds__(512, 2) void gemm_pp_pair_kernel(GemmArgs p0, GemmArgs p1, int nb0) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  if ((int)blockIdx.x < nb0) gemm_pp_body<128, 2, AC0, BC0>(p0, blockIdx.x, smem_raw);
+  else                       gemm_pp_body<128, 2, AC1, BC1>(p1, blockIdx.x - nb0, smem_raw);
+}
+
+template <int BMP, int NSTP, int OCC, bool AC, bool BC>
+void pp_launch(const GemmArgs& a, hipStream_t s) {
+  using G = PPGeom<BMP, NSTP>;
+  static bool attr = false;
+  if (!attr) {
+    TDFO_CHECK_HIP(hipFuncSetAttribute((const void*)gemm_pp_kernel<BMP, NSTP, OCC, AC, BC>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
+    attr = true;
+  }
+  const int tiles = ((a.M + BMP - 1) / BMP) * ((a.N + BN - 1) / BN) * a.splits;
+  hipLaunchKernelGGL((gemm_pp_kernel<BMP, NSTP, OCC, AC, BC>), dim3(tiles), dim3(512), G::LDS, s,
+                     a);
+  TDFO_CHECK_HIP(hipGetLastError());
+}
+
 // 0 auto, 1 small tiles only (64-row tiles when 128-row ones underfill),
 // 2 large tiles only, 3 128x128 tiles only, 4 = 1 with 256x128 tiles for
 // the weight-grad (col-A) GEMMs, 5 = auto with 64-row tiles below 512
@@ -890,8 +1260,38 @@ void launch(const GemmArgs& a, hipStream_t s, SmallPlan* plan = nullptr) {
                                        hipFuncAttributeMaxDynamicSharedMemorySize, DSMEM));
     attr = true;
   }
+  if (g_policy >= 30 && g_policy < 70 && !plan) {
+    // ping-pong kernel: 30 auto (256-row tiles when they fill the CUs), 31 256, 32 128;
+    // A/B: 40+k 256-row with abl k, 50+k 128-row, 60+k 128-row 2-slot ring at 2 blocks/CU
+    GemmArgs b = a;
+    const int t256 = ((a.M + 255) / 256) * ((a.N + BN - 1) / BN) * a.splits;
+    if (g_policy >= 40) b.abl = g_policy % 10;
+    if (g_policy == 31 || (g_policy == 30 && t256 >= 240) || (g_policy >= 40 && g_policy < 50))
+      pp_launch<256, 3, 1, AC, BC>(b, s);
+    else if (g_policy >= 60)
+      pp_launch<128, 2, 2, AC, BC>(b, s);
+    else
+      pp_launch<128, 4, 1, AC, BC>(b, s);
+    return;
+  }
   const int tn = (a.N + BN - 1) / BN;
   const int small_tiles = ((a.M + BM - 1) / BM) * tn;
+  // auto: the ping-pong kernel (128-row tiles, 2 blocks per CU) for every
+  // weight grad and dgrad and for forwards whose 128-row grid fills the CUs
+  // (scripts/gemm_lab.py, profiles/gemm_lab_r03.md); GEMMs with >= 1024
+  // tiles keep the 256x128 kernel below
+  if (g_policy == 0 && small_tiles * a.splits < 1024 &&
+      (AC || BC || small_tiles * a.splits >= 256)) {
+    if (plan) {
+      plan->bmt = 129;
+      plan->grid = small_tiles * a.splits;
+      plan->args = a;
+      plan->big_grid = 0;
+      return;
+    }
+    pp_launch<128, 2, 2, AC, BC>(a, s);
+    return;
+  }
   const int big_tiles = ((a.M + LBM - 1) / LBM) * tn;
   GemmArgs b = a;
   b.abl = (g_policy >= 8 && g_policy < 16) ? g_policy - 8 : 0;  // perf ablations (9..15), big kernel
@@ -1047,6 +1447,20 @@ void big_pair_launch(const SmallPlan& p0, const SmallPlan& p1, hipStream_t s) {
   TDFO_CHECK_HIP(hipGetLastError());
 }
 
+template <bool AC0, bool BC0, bool AC1, bool BC1>
+void pp_pair_launch(const SmallPlan& p0, const SmallPlan& p1, hipStream_t s) {
+  auto fn = gemm_pp_pair_kernel<AC0, BC0, AC1, BC1>;
+  constexpr int lds = PPGeom<128, 2>::LDS;
+  static bool attr = false;
+  if (!attr) {
+    TDFO_CHECK_HIP(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       lds));
+    attr = true;
+  }
+  hipLaunchKernelGGL(fn, dim3(p0.grid + p1.grid), dim3(512), lds, s, p0.args, p1.args, p0.grid);
+  TDFO_CHECK_HIP(hipGetLastError());
+}
+
 int g_pair_deep = 1;   // pair a deep-kernel dgrad on 256x128 tiles with its weight grad
 
 bool try_pair(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s) {
@@ -1058,6 +1472,13 @@ bool try_pair(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s) {
   if (g_pair_deep && p1.bmt == 256 && !p0.bmt && p0.big_grid) { p0.bmt = 256; p0.grid = p0.big_grid; }
   if (!p0.bmt || !p1.bmt) return false;
   const int l0 = layout_of(a0), l1 = layout_of(a1);
+  if (p0.bmt == 129 || p1.bmt == 129) {           // ping-pong pairs
+    if (p0.bmt != 129 || p1.bmt != 129) return false;
+    if (l0 == 3 && l1 == 1) { pp_pair_launch<true, true, false, true>(p0, p1, s); return true; }
+    if (l1 == 3 && l0 == 1) { pp_pair_launch<true, true, false, true>(p1, p0, s); return true; }
+    if (l0 == 3 && l1 == 3) { pp_pair_launch<true, true, true, true>(p0, p1, s); return true; }
+    return false;
+  }
   if ((p0.bmt == 256) != (p1.bmt == 256)) return false;
   if (p0.bmt == 256) {                            // weight grad + dgrad on 256x128 tiles
     if (l0 == 3 && l1 == 1) { big_pair_launch<true, true, false, true>(p0, p1, s); return true; }

@@ -30,8 +30,9 @@ def rel_err(a, b):
 
 
 # ------------------------------------------------------------------ GEMM
-@pytest.fixture(params=[0, 1, 2, 3, 6, 20, 23, 25], ids=["auto", "tile64or128", "tile256", "tile128",
-                                                     "auto_ldsepi", "tile256w4", "deep128", "dcn"])
+@pytest.fixture(params=[0, 1, 2, 3, 6, 20, 23, 25, 31, 60],
+                ids=["auto", "tile64or128", "tile256", "tile128", "auto_ldsepi", "tile256w4",
+                     "deep128", "dcn", "pp256", "pp128"])
 def gemm_pol(request):
     """Run a GEMM test once per tile kernel (128x128 2-stage / 256x128 3-stage)."""
     old = ops.gemm_policy(request.param)
