@@ -858,6 +858,7 @@ void rw_bucketize(const Tensor& ids, const Tensor& meta, int64_t nrw, int64_t W,
   a.ids = ids.data_ptr<int64_t>(); a.meta = meta.data_ptr<int64_t>();
   a.nrw = (int)nrw; a.W = (int)W; a.B = (int)B; a.cap = cap; a.n = n;
   a.send = send.data_ptr<int64_t>(); a.overflow = overflow.data_ptr<int32_t>();
+  a.need = overflow.numel() >= 2 ? overflow.data_ptr<int32_t>() + 1 : nullptr;   // [flag, need]
   tdfo::rw_bucketize(a, work.data_ptr(), cur_stream());
 }
 

@@ -35,7 +35,6 @@ struct GemmArgs {
   // uses it for the bias gradient (sum over the batch of dy), which lets the
   // GEMM's N stay at the 128-aligned input width.
   int csum_on, csum_col;
-  int abl;   // perf-ablation bits (0 in production): 1 skip A loads, 2 skip B loads, 4 skip all in-loop loads
 };
 void gemm_bf16(const GemmArgs& a, hipStream_t s);
 // Launch n independent GEMMs in order; consecutive (weight grad, dgrad)
@@ -43,8 +42,9 @@ void gemm_bf16(const GemmArgs& a, hipStream_t s);
 // never). Returns after enqueueing.
 void gemm_group(const GemmArgs* a, int n, hipStream_t s);
 int gemm_pairing(int v);
-// Tile-shape policy for gemm_bf16 (0 auto, 1 128x128 only, 2 256x128 only);
-// p < 0 just reads it. Returns the previous policy.
+// Kernel policy for gemm_bf16 (0 auto; 1 2-stage 64/128-row tiles, 2 deep
+// 4-slot ring, 3 ping-pong: forced, for tests / A/B); p < 0 just reads it.
+// Returns the previous policy.
 int gemm_policy(int p);
 
 // ------------------------------------------------- fused bottom MLP ----
@@ -184,13 +184,14 @@ void embedding_dense_update(const EmbBwdArgs& a, int64_t rows, const float* grad
 // (rowwise.hip) Fixed-capacity row-wise exchange. meta (int64, device):
 // [in_base (nrw) | L (nrw) | blk (nrw) | lrow (nrw) | cum (nrw + 1)]:
 // table j's ids start at ids[in_base[j]], L[j] ids per bag, owner(id) =
-// min(id / blk[j], W - 1), owner-local row key = lrow[j] + id - owner*blk[j],
-// cum = prefix of B*L[j]. Buffers are [W][cap + 1] int64; entry =
-// (j*B + b) << 32 | row key; slot cap of segment o holds its count.
+// id mod W, owner-local row key = lrow[j] + id div W (blk[j] = ceil(rows/W)
+// rows per owner), cum = prefix of B*L[j]. Buffers are [W][cap + 1] int64;
+// entry = (j*B + b) << 32 | row key; slot cap of segment o holds its count.
+// need (optional): the largest per-owner count of this batch.
 struct RwBucketArgs {
   const int64_t* ids; const int64_t* meta;
   int nrw, W, B; int64_t cap; int64_t n;      // n = cum[nrw] rw ids
-  int64_t* send; int32_t* overflow;
+  int64_t* send; int32_t* overflow; int32_t* need;
 };
 size_t rw_bucketize_workspace(int64_t n, int W);
 void rw_bucketize(const RwBucketArgs& a, void* ws, hipStream_t s);

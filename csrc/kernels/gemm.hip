@@ -178,11 +178,10 @@ struct BoolC {
 
 __device__ __forceinline__ bool al16(const void* q) { return ((uintptr_t)q & 15) == 0; }
 __device__ __forceinline__ bool direct_ok(const GemmArgs& p, int m0, int n0, int rows) {
-  if (p.abl & (224 | 256)) return false;           // ablations / forced LDS path
   // operand reads (ReLU mask, DCN mul/add) in this layout are 32-B row runs;
   // the LDS path reads them as 256-B rows (measured: DCN-v2 3.16 vs 3.05 ms)
   if (p.mul || p.add) return false;
-  if (p.mask && !(p.abl & 512)) return false;      // abl 512: masked dgrads direct too (A/B)
+  if (p.mask) return false;
   if (m0 + rows > p.M || n0 + 128 > p.N) return false;
   if (p.C && ((p.ldc & 7) || !al16(p.C))) return false;
   if (p.mask && ((p.ldm & 7) || !al16(p.mask))) return false;
@@ -202,7 +201,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs& p, const f32x4_t (&acc)
   // the accumulators -- no LDS round trip, no barrier; 64-B row runs per
   // 4-lane group.
   if (p.C32 && !p.C && !p.C2 && !p.bias && !p.relu && !p.mask && (p.ldc32 & 3) == 0 &&
-      (p.N & 3) == 0 && !(p.abl & 224)) {   // abl 128: force the LDS path (A/B)
+      (p.N & 3) == 0) {
     float* c32 = p.C32 + (int64_t)split * p.M * p.ldc32;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
@@ -316,7 +315,7 @@ __device__ __forceinline__ void epilogue(const GemmArgs& p, const f32x4_t (&acc)
       const int n = n0 + wc * 64 + j * 16 + 4 * (lane >> 4) + r;
       bv[j][r] = (p.bias && n < p.N) ? p.bias[(int64_t)n * p.bias_stride] : 0.f;
     }
-  const bool pf = !(p.abl & 1024) && (p.N & 7) == 0 &&
+  const bool pf = (p.N & 7) == 0 &&
                   (p.mask || (p.C2 && (p.mul || p.add)));
   uint4 pk[IT], pm[IT], pa[IT];
   if (pf) {
@@ -376,10 +375,6 @@ __device__ __forceinline__ void epilogue(const GemmArgs& p, const f32x4_t (&acc)
     const float4 lo = *(const float4*)(ctile + rl * 128 + (((cg >> 2) ^ (rl & 31)) << 2));
     const float4 hi = *(const float4*)(ctile + rl * 128 + ((((cg >> 2) + 1) ^ (rl & 31)) << 2));
     float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-    if (p.abl & 64) {                  // perf ablation: LDS staging only, no global stores
-      asm volatile("" :: "v"(lo.x), "v"(lo.y), "v"(lo.z), "v"(lo.w), "v"(hi.x), "v"(hi.y), "v"(hi.z), "v"(hi.w));
-      continue;
-    }
     const int n = n0 + cg;
     if (nfull || n + 8 <= p.N) {
       if (p.mask) {
@@ -585,187 +580,6 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs p) {
   gemm_small_body<BMT, A_COL, B_COL>(p, blockIdx.x, smem_raw);
 }
 
-// Two independent small-tile GEMMs in one grid: blocks [0, nb0) run problem
-// 0, the rest problem 1 (e.g. a layer's weight grad and its dgrad, both
-// reading dy). Each small launch pays ~4-6 us of fill / drain / launch in the
-// graph (profiles/gemm_step_ab.md: 5.9 us for a one-K-tile 256-block GEMM);
-// paired, the two problems' blocks also fill each other's idle CUs.
-template <int BM0, bool AC0, bool BC0, int BM1, bool AC1, bool BC1>
-__global__ __launch_bounds__(256, 2) void gemm_pair_kernel(GemmArgs p0, GemmArgs p1, int nb0) {
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  if ((int)blockIdx.x < nb0) gemm_small_body<BM0, AC0, BC0>(p0, blockIdx.x, smem_raw);
-  else                       gemm_small_body<BM1, AC1, BC1>(p1, blockIdx.x - nb0, smem_raw);
-}
-
-// ---------------------------------------------------------------------------
-// Large-tile kernel: 256x128x64, 8 waves (4 along M x 2 along N, each 64x64),
-// 3-deep glds ring (3 x 48 KiB = 144 KiB LDS, 1 block per CU, 2 waves per
-// SIMD). Two K tiles stay in flight across each barrier: the wait before the
-// barrier is a counted vmcnt (6 pieces per thread per tile), the barrier is a
-// raw s_barrier (no vmcnt(0) drain, cdna_hip_programming.md "Pipelining
-// across barriers"), and the ring slot being refilled is the one every wave
-// finished reading before that barrier. Twice the FLOP per staged byte of the
-// 128x128 tile, which is what bounds that kernel on these short-K problems.
-constexpr int LBM = 256;
-constexpr int LSTAGE = 3 * TILE_BYTES;             // A (2 images) + B
-constexpr int LNSTAGE = 3;
-constexpr int LSMEM = LNSTAGE * LSTAGE;            // 144 KiB >= 256x128 fp32 epilogue tile
-
-// MI = 4: 8 waves (4 along M x 2 along N), 64x64 per wave, 2 waves per SIMD.
-// MI = 8: 4 waves (2 x 2), 128x64 per wave (32 accumulators), 1 wave per
-// SIMD: 1.33x the FLOP per LDS-read byte of the 64x64 wave tile (12 fragment
-// reads per 32 MFMAs instead of 8 per 16), the wave hides its own reads
-// between MFMAs (fragment double buffer) and the 3-deep ring keeps two K
-// tiles of DMA in flight.
-template <bool A_COL, bool B_COL, int MI>
-__device__ __forceinline__ void gemm_big_body(const GemmArgs& p, int bid, char* smem_raw) {
-  constexpr int NW = MI == 4 ? 8 : 4;               // waves
-  constexpr int APW = 32 / NW, BPW = 16 / NW;       // A / B pieces per wave per K tile
-  TDFO_LDS char* smem = (TDFO_LDS char*)smem_raw;
-
-  const int tiles_m = (p.M + LBM - 1) / LBM, tiles_n = (p.N + BN - 1) / BN;
-  const TileIdx ti = tile_of(tiles_m, tiles_n, p.splits, bid);
-  const int m0 = ti.tm * LBM, n0 = ti.tn * BN;
-
-  const int ktiles = p.K / BK;
-  const int per = (ktiles + p.splits - 1) / p.splits;
-  const int kt0 = ti.split * per;
-  const int nk = min(ktiles, kt0 + per) - kt0;
-
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wr = w >> 1, wc = w & 1;
-
-  f32x4_t acc[MI][4];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-
-  // 48 pieces per K tile (A: 2 images x 16, B: 16) spread over the waves.
-  auto stage = [&](int buf, int kt) {
-    TDFO_LDS char* ta = smem + buf * LSTAGE;
-    TDFO_LDS char* tb = ta + 2 * TILE_BYTES;
-    const int k0 = kt * BK;
-    if (!(p.abl & 1))
-#pragma unroll
-    for (int i = 0; i < APW; ++i) {
-      const int ii = w * APW + i, half = ii >> 4;
-      glds_piece_asm<A_COL>(p.A, p.lda, m0 + half * 128, p.M, k0, ta + half * TILE_BYTES,
-                            ii & 15, lane);
-    }
-    if (!(p.abl & 2))
-#pragma unroll
-    for (int i = 0; i < BPW; ++i)
-      glds_piece_asm<B_COL>(p.B, p.ldb, n0, p.N, k0, tb, w * BPW + i, lane);
-  };
-  auto wait_one_ahead = [&]() {        // all but the youngest K tile's pieces landed
-    if constexpr (NW == 8) asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(12) lgkmcnt(0)" ::: "memory");
-  };
-
-  // Fragment-pipelined main loop: one raw barrier per K tile, in the middle
-  // of it. Iteration t: issue tile t+2's DMA, read tile t's k=32..63
-  // fragments, MFMAs on its k=0..31 fragments (read last iteration) hide that
-  // read, then wait for tile t+1 + barrier, read tile t+1's k=0..31
-  // fragments, and the k=32..63 MFMAs hide those. Ring-slot reuse: slot
-  // (t+2)%3 was last read before iteration t-1's barrier (each wave drains
-  // its LDS reads with lgkmcnt(0) before that barrier).
-  if (nk > 0 && !(p.abl & 16)) {
-    const TDFO_LDS char* tAo = smem + (MI == 4 ? (wr >> 1) : wr) * TILE_BYTES;
-    const TDFO_LDS char* tBo = smem + 2 * TILE_BYTES;
-    const int a_r0 = MI == 4 ? (wr & 1) * 64 : 0, b_c0 = wc * 64;
-    auto frags = [&](int buf, int ks, bf16x8_t (&af)[MI], bf16x8_t (&bfr)[4]) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-        bfr[j] = B_COL ? frag_col(tBo + buf * LSTAGE, b_c0 + j * 16, ks, lane)
-                       : frag_row(tBo + buf * LSTAGE, b_c0 + j * 16, ks, lane);
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-        af[i] = A_COL ? frag_col(tAo + buf * LSTAGE, a_r0 + i * 16, ks, lane)
-                      : frag_row(tAo + buf * LSTAGE, a_r0 + i * 16, ks, lane);
-    };
-    auto mm = [&](const bf16x8_t (&af)[MI], const bf16x8_t (&bfr)[4]) {
-#pragma unroll
-      for (int i = 0; i < MI; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
-    };
-    stage(0, kt0);
-    if (nk > 1) stage(1, kt0 + 1);
-    if (nk > 1) wait_one_ahead();
-    else        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    __builtin_amdgcn_sched_barrier(0);
-    bf16x8_t a0[MI], b0[4], a1[MI], b1[4];
-    frags(0, 0, a0, b0);
-    int cur = 0;
-    // steady state (straight-line body so the compiler's lgkmcnt waits only
-    // cover the reads each MFMA group actually consumes); last tile peeled
-    for (int t = 0; t + 1 < nk; ++t) {
-      __builtin_amdgcn_sched_barrier(0);
-      const bool pre = t + 2 < nk;
-      if (pre) stage(cur == 0 ? 2 : cur - 1, kt0 + t + 2);
-      frags(cur, 1, a1, b1);
-      __builtin_amdgcn_sched_barrier(0);
-      mm(a0, b0);
-      __builtin_amdgcn_sched_barrier(0);
-      if (pre) wait_one_ahead();
-      else     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      cur = cur == 2 ? 0 : cur + 1;
-      frags(cur, 0, a0, b0);
-      __builtin_amdgcn_sched_barrier(0);
-      mm(a1, b1);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    frags(cur, 1, a1, b1);
-    mm(a0, b0);
-    mm(a1, b1);
-  } else if (nk > 0) {
-    stage(0, kt0);
-    if (nk > 1) stage(1, kt0 + 1);
-    int cur = 0;
-    for (int t = 0; t < nk; ++t) {
-      if (t + 1 < nk && !(p.abl & 7)) wait_one_ahead();
-      else            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      if (t + 2 < nk && !(p.abl & 4)) stage(cur == 0 ? 2 : cur - 1, kt0 + t + 2);
-      const TDFO_LDS char* ta = smem + cur * LSTAGE;
-      mfma_k64<A_COL, B_COL, MI>(acc, ta + (MI == 4 ? (wr >> 1) : wr) * TILE_BYTES,
-                                 MI == 4 ? (wr & 1) * 64 : 0, ta + 2 * TILE_BYTES, wc * 64, lane);
-      cur = cur == 2 ? 0 : cur + 1;
-    }
-  }
-  if (p.abl & 32) {                 // perf ablation: keep acc live, skip the epilogue
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) asm volatile("" :: "v"(acc[i][j]));
-    return;
-  }
-  epilogue<LBM, NW * 64, MI>(p, acc, smem_raw, m0, n0, wr, wc, lane, tid, ti.split);
-}
-
-template <bool A_COL, bool B_COL, int MI>
-__global__ __launch_bounds__(MI == 4 ? 512 : 256, 1) void gemm_big_kernel(GemmArgs p) {
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  gemm_big_body<A_COL, B_COL, MI>(p, blockIdx.x, smem_raw);
-}
-
-// Paired 256x128 launch (DCN-v2's one-block-per-CU kernel): see gemm_pair_kernel.
-template <bool AC0, bool BC0, bool AC1, bool BC1>
-__global__ __launch_bounds__(512, 1) void gemm_big_pair_kernel(GemmArgs p0, GemmArgs p1, int nb0) {
-  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  if ((int)blockIdx.x < nb0) gemm_big_body<AC0, BC0, 4>(p0, blockIdx.x, smem_raw);
-  else                       gemm_big_body<AC1, BC1, 4>(p1, blockIdx.x - nb0, smem_raw);
-}
-
 // ---------------------------------------------------------------------------
 // Deep-pipelined 128x128 kernel: 4 waves (2x2 of 64x64), DNS-deep glds ring
 // (DNS x 32 KiB, one block per CU) with DNS-2 K tiles of DMA in flight across
@@ -856,45 +670,46 @@ __global__ __launch_bounds__(256, 1) void gemm_deep_kernel(GemmArgs p) {
 }
 
 // ---------------------------------------------------------------------------
-// Ping-pong tile kernel (BM x 128 x 64, BM = 256 or 128, 8 waves).
+// Ping-pong tile kernel: 128x128x64 tiles, 8 waves, 2 blocks per CU.
 //
 // The waves form two groups of four (waves 0-3 and 4-7: one wave of each
-// group per SIMD) that own the upper and lower half of the tile's rows. Each
-// wave alternates a READ segment (its fragment ds_reads for the next k-chunk,
-// plus its share of the global->LDS DMA) and an MFMA segment, every segment
-// closed by a workgroup barrier; group 1 starts one barrier late, so on every
-// SIMD one wave issues MFMAs while the other reads LDS and issues DMA -- the
-// MFMA pipe sees one wave's back-to-back MFMAs in every interval
-// (cdna_hip_programming.md §5 "8-phase template": per-phase interleave with
-// the wave groups staggered by a barrier; T3+T4 counted vmcnt, T5 setprio).
-// Operands are staged by inline-asm global_load_lds into an NST-deep LDS ring
-// (counted vmcnt, raw s_barrier: DMA stays in flight across barriers).
-//   BM = 256: waves 64x64 (2x2 per group), 16 MFMAs per segment, 3-slot ring
-//             (144 KiB LDS).
-//   BM = 128: waves 64x32 (1x4 per group), both k32 steps of a K tile per
-//             segment (16 MFMAs), 4-slot ring (128 KiB LDS).
+// group per SIMD) owning the upper and lower 64 rows of the tile; each wave
+// computes 64x32 (4x2 v_mfma_f32_16x16x32_bf16 fragments). Every wave
+// alternates a READ segment (its share of the next K tile's global->LDS DMA,
+// then its fragment ds_reads for one K tile) and an MFMA segment (16 MFMAs),
+// each closed by a workgroup barrier; group 1 starts one barrier late, so on
+// every SIMD one wave issues MFMAs while the other reads LDS and issues DMA
+// (cdna_hip_programming.md §5 "8-phase template": groups staggered by a
+// barrier; T3+T4 counted vmcnt, T5 setprio). Operands are staged by
+// inline-asm global_load_lds into a 2-slot LDS ring (counted vmcnt, raw
+// s_barrier: the DMA stays in flight across barriers); 64 KiB of LDS lets
+// two blocks share a CU, so one block's prologue / epilogue overlaps the
+// other's main loop -- which is what beat every one-block-per-CU variant
+// measured (256x128 and 256x256 tiles, 3-4 slot rings, DMA in the MFMA
+// segment, no stagger: profiles/r03/gemm_lab_variants.jsonl).
 // Epilogue straight from the accumulators (bias, ReLU, ReLU mask, DCN
 // Hadamard/residual second output, fp32 split-K slabs, bias-grad column sums).
-template <int BMP, int NSTP = (BMP == 256 ? 3 : 4)>
+template <int BMP, int NSTP, int BNP = 128>
 struct PPGeom {
-  static constexpr int BM = BMP;
+  static constexpr int BM = BMP, BN = BNP;
   static constexpr int GROWS = BM / 2;                  // rows per wave group
-  static constexpr int WGM = BM == 256 ? 2 : 1;         // waves along M in a group
-  static constexpr int WGN = 4 / WGM;
-  static constexpr int WROWS = GROWS / WGM;             // 64
+  static constexpr int WGN = (BN == 256 || BM == 128) ? 4 : 2;   // waves along N in a group
+  static constexpr int WGM = 4 / WGN;
+  static constexpr int WROWS = GROWS / WGM;             // 64 | 128
   static constexpr int WCOLS = BN / WGN;                // 64 | 32
-  static constexpr int MI = WROWS / 16;                 // 4
-  static constexpr int NJ = WCOLS / 16;                 // 4 | 2
-  static constexpr int KS = NJ == 4 ? 1 : 2;            // k32 steps per segment
+  static constexpr int MI = WROWS / 16;
+  static constexpr int NJ = WCOLS / 16;
+  static constexpr int KS = MI * NJ >= 16 ? 1 : 2;      // k32 steps per segment
   static constexpr int SEGS = 2 / KS;                   // READ/MFMA segment pairs per K tile
   static constexpr int A_BYTES = BM * BK * 2;
-  static constexpr int STAGE = A_BYTES + TILE_BYTES;
+  static constexpr int STAGE = A_BYTES + BN * BK * 2;
   static constexpr int NST = NSTP;
   static constexpr int LDS = NST * STAGE;
   static constexpr int APW = BM / 64;                   // A glds pieces per wave per K tile
-  static constexpr int BPW = 2;
+  static constexpr int BPW = BN / 64;
   static constexpr int PPW = APW + BPW;
   static constexpr int CSF = MI / WGN;                  // column-sum fragments per wave
+  static_assert(PPW * (NST - 1) <= 63, "vmcnt range");
 };
 
 __device__ __forceinline__ void pp_barrier() {
@@ -945,21 +760,18 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs& p, const f32x4_t (&a
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         bias[j][r] = p.bias ? p.bias[(int64_t)(nw + 16 * j + 4 * g + r) * p.bias_stride] : 0.f;
-    // epilogue operands first (all loads in flight before the first use)
-    uint4 mk[MI / 2][NJ], mv[MI / 2][NJ], av[MI / 2][NJ];
-#pragma unroll
-    for (int i = 0; i < MI; i += 2)
-#pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        const int m = mw + (i + (g & 1)) * 16 + rho;
-        const int n = nw + 16 * j + 8 * (g >> 1);
-        if (p.mask) mk[i / 2][j] = *(const uint4*)(p.mask + (int64_t)m * p.ldm + n);
-        if (p.C2 && p.mul) mv[i / 2][j] = *(const uint4*)(p.mul + (int64_t)m * p.ldmul + n);
-        if (p.C2 && p.add) av[i / 2][j] = *(const uint4*)(p.add + (int64_t)m * p.ldadd + n);
-      }
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
       const int n = nw + 16 * j + 8 * (g >> 1);
+      // this column fragment's epilogue operands, all in flight before the first use
+      uint4 mk[MI / 2], mv[MI / 2], av[MI / 2];
+#pragma unroll
+      for (int i = 0; i < MI; i += 2) {
+        const int m = mw + (i + (g & 1)) * 16 + rho;
+        if (p.mask) mk[i / 2] = *(const uint4*)(p.mask + (int64_t)m * p.ldm + n);
+        if (p.C2 && p.mul) mv[i / 2] = *(const uint4*)(p.mul + (int64_t)m * p.ldmul + n);
+        if (p.C2 && p.add) av[i / 2] = *(const uint4*)(p.add + (int64_t)m * p.ldadd + n);
+      }
 #pragma unroll
       for (int i = 0; i < MI; i += 2) {
         float v[8];
@@ -977,7 +789,7 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs& p, const f32x4_t (&a
         }
         const int m = mw + (i + (g & 1)) * 16 + rho;
         if (p.mask) {
-          const uint4 q4 = mk[i / 2][j];
+          const uint4 q4 = mk[i / 2];
           const uint32_t mu[4] = {q4.x, q4.y, q4.z, q4.w};
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
@@ -994,7 +806,7 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs& p, const f32x4_t (&a
 #pragma unroll
           for (int q = 0; q < 8; ++q) w2[q] = v[q];
           if (p.mul) {
-            const uint4 q4 = mv[i / 2][j];
+            const uint4 q4 = mv[i / 2];
             const uint32_t mu[4] = {q4.x, q4.y, q4.z, q4.w};
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -1003,7 +815,7 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs& p, const f32x4_t (&a
             }
           }
           if (p.add) {
-            const uint4 q4 = av[i / 2][j];
+            const uint4 q4 = av[i / 2];
             const uint32_t au[4] = {q4.x, q4.y, q4.z, q4.w};
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -1047,9 +859,10 @@ __device__ __forceinline__ void pp_epilogue(const GemmArgs& p, const f32x4_t (&a
       }
 }
 
-template <int BMP, int NSTP, bool A_COL, bool B_COL>
+template <int BMP, int NSTP, int BNP, bool A_COL, bool B_COL>
 __device__ __forceinline__ void gemm_pp_body(const GemmArgs& p, int bid, char* smem_raw) {
-  using G = PPGeom<BMP, NSTP>;
+  using G = PPGeom<BMP, NSTP, BNP>;
+  constexpr int BN = BNP;
   constexpr int MI = G::MI, NJ = G::NJ, KS = G::KS, SEGS = G::SEGS, NST = G::NST;
   TDFO_LDS char* smem = (TDFO_LDS char*)smem_raw;
   const int tiles_m = (p.M + G::BM - 1) / G::BM, tiles_n = (p.N + BN - 1) / BN;
@@ -1066,10 +879,8 @@ __device__ __forceinline__ void gemm_pp_body(const GemmArgs& p, int bid, char* s
   const int a_row = grp * G::GROWS + wr * G::WROWS;       // wave's first row in the tile
   const int a_img = a_row >> 7, a_r0 = a_row & 127;
   const int b_c0 = wc * G::WCOLS;
-  // A/B knobs (p.abl): 1 DMA issued in the MFMA segment (4: after its
-  // MFMAs) instead of the READ segment; 2 no stagger (both groups in phase)
-  const bool gm = p.abl & 1, gend = p.abl & 4, nopp = p.abl & 2;
-  const bool lag = grp == 1 && !nopp;
+  const int b_img = b_c0 >> 7, b_cc = b_c0 & 127;
+  const bool lag = grp == 1;
 
   f32x4_t acc[MI][NJ];
 #pragma unroll
@@ -1089,8 +900,11 @@ __device__ __forceinline__ void gemm_pp_body(const GemmArgs& p, int bid, char* s
                             lane);
     }
 #pragma unroll
-    for (int i = 0; i < G::BPW; ++i)
-      glds_piece_asm<B_COL>(p.B, p.ldb, n0, p.N, k0, tb, w * G::BPW + i, lane);
+    for (int i = 0; i < G::BPW; ++i) {
+      const int ii = w * G::BPW + i, img = ii >> 4;
+      glds_piece_asm<B_COL>(p.B, p.ldb, n0 + img * 128, p.N, k0, tb + img * TILE_BYTES, ii & 15,
+                            lane);
+    }
   };
   // K tiles issued before the wait for tile T (at the end of the segment
   // holding half T*SEGS - 1) that are younger than T: tile X is issued in the
@@ -1100,8 +914,7 @@ __device__ __forceinline__ void gemm_pp_body(const GemmArgs& p, int bid, char* s
 #pragma unroll
     for (int d = 1; d < NST; ++d) {
       const int X = T + d;
-      const int hx = (X - NST + 1) * SEGS;
-      if (X < nk && (X < NST || hx < T * SEGS - 1 || (hx == T * SEGS - 1 && !(lag && gm)))) ++n;
+      if (X < nk && (X < NST || (X - NST + 1) * SEGS <= T * SEGS - 1)) ++n;
     }
     return n;
   };
@@ -1124,18 +937,17 @@ __device__ __forceinline__ void gemm_pp_body(const GemmArgs& p, int bid, char* s
       const int t = h / SEGS, s = h - t * SEGS;
       // ---- READ segment: DMA of tile t + NST - 1 (first half of tile t),
       // then this half's fragments
-      const bool dma = s == 0 && t >= 1 && t + NST - 1 < nk;
-      if (dma && !gm) stage((t + NST - 1) % NST, kt0 + t + NST - 1);
+      if (s == 0 && t >= 1 && t + NST - 1 < nk) stage((t + NST - 1) % NST, kt0 + t + NST - 1);
       {
         const TDFO_LDS char* ta = smem + (t % NST) * G::STAGE + a_img * TILE_BYTES;
-        const TDFO_LDS char* tb = smem + (t % NST) * G::STAGE + G::A_BYTES;
+        const TDFO_LDS char* tb = smem + (t % NST) * G::STAGE + G::A_BYTES + b_img * TILE_BYTES;
 #pragma unroll
         for (int kk = 0; kk < KS; ++kk) {
           const int ks = s * KS + kk;
 #pragma unroll
           for (int j = 0; j < NJ; ++j)
-            bfr[kk][j] = B_COL ? frag_col(tb, b_c0 + 16 * j, ks, lane)
-                               : frag_row(tb, b_c0 + 16 * j, ks, lane);
+            bfr[kk][j] = B_COL ? frag_col(tb, b_cc + 16 * j, ks, lane)
+                               : frag_row(tb, b_cc + 16 * j, ks, lane);
 #pragma unroll
           for (int i = 0; i < MI; ++i)
             af[kk][i] = A_COL ? frag_col(ta, a_r0 + 16 * i, ks, lane)
@@ -1146,7 +958,6 @@ __device__ __forceinline__ void gemm_pp_body(const GemmArgs& p, int bid, char* s
       if (lag && s == SEGS - 1 && t + 1 < nk) pp_wait_vm<G::PPW>(younger(t + 1));
       pp_barrier();
       // ---- MFMA segment
-      if (dma && gm && !gend) stage((t + NST - 1) % NST, kt0 + t + NST - 1);
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -1175,11 +986,10 @@ __device__ __forceinline__ void gemm_pp_body(const GemmArgs& p, int bid, char* s
       }
       __builtin_amdgcn_s_setprio(0);
       __builtin_amdgcn_sched_barrier(0);
-      if (dma && gm && gend) stage((t + NST - 1) % NST, kt0 + t + NST - 1);
       if (!lag && s == SEGS - 1 && t + 1 < nk) pp_wait_vm<G::PPW>(younger(t + 1));
       pp_barrier();
     }
-    if (grp == 0 && !nopp) pp_barrier();
+    if (grp == 0) pp_barrier();
   }
   if constexpr (A_COL) {
     if (csum) {
@@ -1194,197 +1004,148 @@ __device__ __forceinline__ void gemm_pp_body(const GemmArgs& p, int bid, char* s
   pp_epilogue<MI, NJ>(p, acc, m0 + a_row, n0 + b_c0, lane, ti.split);
 }
 
-template <int BMP, int NSTP, int OCC, bool A_COL, bool B_COL>
-__global__ __launch_bounds__(512, OCC) void gemm_pp_kernel(GemmArgs p) {
+using PPG = PPGeom<128, 2, 128>;
+
+template <bool A_COL, bool B_COL>
+__global__ __launch_bounds__(512, 2) void gemm_pp_kernel(GemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  gemm_pp_body<BMP, NSTP, A_COL, B_COL>(p, blockIdx.x, smem_raw);
+  gemm_pp_body<128, 2, 128, A_COL, B_COL>(p, blockIdx.x, smem_raw);
 }
 
-// Two problems in one ping-pong grid (a layer's weight grad + dgrad): blocks
-// [0, nb0) run problem 0 on BM0-row tiles, the rest problem 1 on BM1-row tiles.
-// (the production configuration: 128-row tiles, 2-slot ring, 2 blocks per CU)
+// Two problems in one ping-pong grid (a layer's weight grad + dgrad, or two
+// weight grads): blocks [0, nb0) run problem 0, the rest problem 1.
 template <bool AC0, bool BC0, bool AC1, bool BC1>
 __global__ __launch_bounds__(512, 2) void gemm_pp_pair_kernel(GemmArgs p0, GemmArgs p1, int nb0) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-  if ((int)blockIdx.x < nb0) gemm_pp_body<128, 2, AC0, BC0>(p0, blockIdx.x, smem_raw);
-  else                       gemm_pp_body<128, 2, AC1, BC1>(p1, blockIdx.x - nb0, smem_raw);
+  if ((int)blockIdx.x < nb0) gemm_pp_body<128, 2, 128, AC0, BC0>(p0, blockIdx.x, smem_raw);
+  else                       gemm_pp_body<128, 2, 128, AC1, BC1>(p1, blockIdx.x - nb0, smem_raw);
 }
 
-template <int BMP, int NSTP, int OCC, bool AC, bool BC>
+int pp_grid(const GemmArgs& a) {
+  return ((a.M + 127) / 128) * ((a.N + 127) / 128) * a.splits;
+}
+
+template <bool AC, bool BC>
 void pp_launch(const GemmArgs& a, hipStream_t s) {
-  using G = PPGeom<BMP, NSTP>;
   static bool attr = false;
   if (!attr) {
-    TDFO_CHECK_HIP(hipFuncSetAttribute((const void*)gemm_pp_kernel<BMP, NSTP, OCC, AC, BC>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS));
+    TDFO_CHECK_HIP(hipFuncSetAttribute((const void*)gemm_pp_kernel<AC, BC>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, PPG::LDS));
     attr = true;
   }
-  const int tiles = ((a.M + BMP - 1) / BMP) * ((a.N + BN - 1) / BN) * a.splits;
-  hipLaunchKernelGGL((gemm_pp_kernel<BMP, NSTP, OCC, AC, BC>), dim3(tiles), dim3(512), G::LDS, s,
-                     a);
+  hipLaunchKernelGGL((gemm_pp_kernel<AC, BC>), dim3(pp_grid(a)), dim3(512), PPG::LDS, s, a);
   TDFO_CHECK_HIP(hipGetLastError());
 }
 
-// 0 auto, 1 small tiles only (64-row tiles when 128-row ones underfill),
-// 2 large tiles only, 3 128x128 tiles only, 4 = 1 with 256x128 tiles for
-// the weight-grad (col-A) GEMMs, 5 = auto with 64-row tiles below 512
-// 128x128 tiles (instead of 256). Auto (default) takes the 256x128 kernel only
-// for GEMMs with >= 1024 128x128 tiles: in the graph-replayed DLRM-1TB step
-// (<= 512 tiles per GEMM) 128x128 measured 0.725-0.728 ms/step vs 0.735 with
-// the 256x128 kernel from 256 blocks up (profiles/gemm_tile_ab.md); on the
-// DCN-v2 cross layers (1728 tiles) 256x128 is ahead (3.19 vs 3.28 ms/step).
+template <bool AC0, bool BC0, bool AC1, bool BC1>
+void pp_pair_launch(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s) {
+  auto fn = gemm_pp_pair_kernel<AC0, BC0, AC1, BC1>;
+  static bool attr = false;
+  if (!attr) {
+    TDFO_CHECK_HIP(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       PPG::LDS));
+    attr = true;
+  }
+  const int g0 = pp_grid(a0);
+  hipLaunchKernelGGL(fn, dim3(g0 + pp_grid(a1)), dim3(512), PPG::LDS, s, a0, a1, g0);
+  TDFO_CHECK_HIP(hipGetLastError());
+}
+
+// Kernel choice. Auto (policy 0), measured on the DLRM / DCN-v2 step shapes
+// on random operands (scripts/gemm_lab.py; profiles/r03/gemm_lab_*.jsonl):
+//   * ping-pong 128x128 (2 blocks per CU): every weight grad and dgrad, and
+//     the forwards whose 128x128 grid fills the CUs (DLRM-1TB MLP GEMMs
+//     266.5 vs 285.2 us on the round-2 kernels, 0.455 vs 0.472 ms/step);
+//   * deep-pipelined 128x128 (4-slot ring, one block per CU): non-weight-grad
+//     GEMMs with >= 32 K tiles per split on <= 512 tiles (DCN-v2 V fwd and
+//     U dgrad, K = 3456: 37 vs 45 us and 41 vs 49 us on the ping-pong kernel);
+//   * 2-stage 64x128 tiles: forwards whose 128x128 grid leaves CUs idle
+//     (N <= 256: bot1 / top3 fwd 8.3 vs 9.6 us).
+// Policies 1 / 2 / 3 force the 2-stage, deep or ping-pong kernel (tests, A/B).
 int g_policy = 0;
 
-// The launch a problem would get: bmt 64 / 128 small-tile kernel, 256 the
-// 8-wave 256x128 kernel, 0 another kernel.
-struct SmallPlan {
-  int bmt, grid;
-  GemmArgs args;
-  int big_grid;   // deep-kernel problems: the 256x128 grid if paired instead (0: n/a)
-};
+enum Kern { K_SMALL64 = 64, K_SMALL128 = 128, K_DEEP = 2, K_PP = 3 };
 
-// plan != nullptr: decide only; fill *plan (bmt 0 if the problem would not
-// run on the small-tile kernel) and launch nothing.
 template <bool AC, bool BC>
-void launch(const GemmArgs& a, hipStream_t s, SmallPlan* plan = nullptr) {
+int choose(const GemmArgs& a) {
+  const int t128 = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN) * a.splits;
+  const int ktps = (a.K / BK + a.splits - 1) / a.splits;
+  switch (g_policy) {
+    case 1: return (!AC && t128 < 256) ? K_SMALL64 : K_SMALL128;
+    case 2: return K_DEEP;
+    case 3: return K_PP;
+    default: break;
+  }
+  if (!AC && ktps >= 32 && t128 <= 512) return K_DEEP;
+  if (AC || BC || t128 >= 256) return K_PP;
+  return K_SMALL64;
+}
+
+template <bool AC, bool BC>
+void launch(const GemmArgs& a, int k, hipStream_t s) {
   static bool attr = false;
   if (!attr) {
     TDFO_CHECK_HIP(hipFuncSetAttribute((const void*)gemm_kernel<128, AC, BC>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       SMEM_BYTES));
-    TDFO_CHECK_HIP(hipFuncSetAttribute((const void*)gemm_big_kernel<AC, BC, 4>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, LSMEM));
-    TDFO_CHECK_HIP(hipFuncSetAttribute((const void*)gemm_big_kernel<AC, BC, 8>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, LSMEM));
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, SMEM_BYTES));
     TDFO_CHECK_HIP(hipFuncSetAttribute((const void*)gemm_deep_kernel<AC, BC>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, DSMEM));
     attr = true;
   }
-  if (g_policy >= 30 && g_policy < 70 && !plan) {
-    // ping-pong kernel: 30 auto (256-row tiles when they fill the CUs), 31 256, 32 128;
-    // A/B: 40+k 256-row with abl k, 50+k 128-row, 60+k 128-row 2-slot ring at 2 blocks/CU
-    GemmArgs b = a;
-    const int t256 = ((a.M + 255) / 256) * ((a.N + BN - 1) / BN) * a.splits;
-    if (g_policy >= 40) b.abl = g_policy % 10;
-    if (g_policy == 31 || (g_policy == 30 && t256 >= 240) || (g_policy >= 40 && g_policy < 50))
-      pp_launch<256, 3, 1, AC, BC>(b, s);
-    else if (g_policy >= 60)
-      pp_launch<128, 2, 2, AC, BC>(b, s);
-    else
-      pp_launch<128, 4, 1, AC, BC>(b, s);
-    return;
-  }
   const int tn = (a.N + BN - 1) / BN;
-  const int small_tiles = ((a.M + BM - 1) / BM) * tn;
-  // auto: the ping-pong kernel (128-row tiles, 2 blocks per CU) for every
-  // weight grad and dgrad and for forwards whose 128-row grid fills the CUs
-  // (scripts/gemm_lab.py, profiles/gemm_lab_r03.md); GEMMs with >= 1024
-  // tiles keep the 256x128 kernel below
-  if (g_policy == 0 && small_tiles * a.splits < 1024 &&
-      (AC || BC || small_tiles * a.splits >= 256)) {
-    if (plan) {
-      plan->bmt = 129;
-      plan->grid = small_tiles * a.splits;
-      plan->args = a;
-      plan->big_grid = 0;
+  switch (k) {
+    case K_PP:
+      pp_launch<AC, BC>(a, s);
       return;
-    }
-    pp_launch<128, 2, 2, AC, BC>(a, s);
-    return;
-  }
-  const int big_tiles = ((a.M + LBM - 1) / LBM) * tn;
-  GemmArgs b = a;
-  b.abl = (g_policy >= 8 && g_policy < 16) ? g_policy - 8 : 0;  // perf ablations (9..15), big kernel
-  if (g_policy == 6) b.abl = 128;                // auto, every output through the LDS epilogue
-  if (g_policy == 7) b.abl = 256;                // auto, bf16 outputs through the LDS epilogue
-  if (g_policy == 17) b.abl = 512;               // auto, masked dgrads on the direct path
-  const bool autop = g_policy == 0 || g_policy == 6 || g_policy == 7 || g_policy == 17 ||
-                     g_policy == 21 || g_policy == 22 || g_policy == 24;
-  bool big = (g_policy >= 2 && g_policy != 3 && g_policy != 4 && !autop) ||
-             (g_policy == 4 && AC) || (autop && small_tiles * a.splits >= 1024);
-  // the A column sums are produced by the 128x128 kernel only
-  const bool small_only = a.csum_on != 0;
-  if (small_only) big = false;
-  // policy 20: the 4-wave 128x64-per-wave kernel for every GEMM; 21: auto
-  // with it in place of the 8-wave kernel; 22: auto with it for every GEMM
-  // that fills >= 128 CUs with 256x128 tiles
-  // policy 23: the deep-pipelined 128x128 kernel for every GEMM; 24: auto,
-  // with it in place of the 2-stage 128x128 kernel where the grid has at
-  // most 2 tiles per CU and K spans >= 16 tiles per split
-  // 25 (DCN-v2): policy 2 (256x128 everywhere), except the deep kernel for
-  // non-weight-grad GEMMs whose 256x128 grid would leave CUs idle while a
-  // 128x128 grid fills them once, with long K (cross-layer V fwd / U dgrad:
-  // 36 vs 44 us and 39 vs 48 us, profiles/gemm_step_ab.md)
-  const int ktps = (a.K / BK + a.splits - 1) / a.splits;
-  const bool deep25 = g_policy == 25 && !AC && big_tiles * a.splits < 256 &&
-                      small_tiles * a.splits <= 512 && ktps >= 16;
-  if (g_policy == 25 && !deep25 && !small_only) big = true;
-  const bool deep = g_policy == 23 || deep25 ||
-                    (g_policy == 24 && !big && small_tiles * a.splits <= 512 && ktps >= 16);
-  const bool w4 = !small_only && (g_policy == 20 || (g_policy == 22 && big_tiles * a.splits >= 128) ||
-                                  (g_policy == 21 && small_tiles * a.splits >= 1024));
-  if (plan) {
-    plan->bmt = 0;
-    plan->args = b;
-    plan->big_grid = (deep && !small_only) ? big_tiles * a.splits : 0;
-    if (deep || w4) return;
-    if (big) {                                    // 256x128, 8 waves
-      plan->bmt = 256;
-      plan->grid = big_tiles * a.splits;
-      return;
-    }
-    if constexpr (!AC) {
-      const int thr64 = g_policy == 5 ? 512 : 256;
-      if (small_tiles * a.splits < thr64 && g_policy != 3 && g_policy != 2) {
-        plan->bmt = 64;
-        plan->grid = ((a.M + 63) / 64) * tn * a.splits;
-        return;
+    case K_DEEP:
+      hipLaunchKernelGGL((gemm_deep_kernel<AC, BC>), dim3(((a.M + BM - 1) / BM) * tn * a.splits),
+                         dim3(256), DSMEM, s, a);
+      break;
+    case K_SMALL64:
+      if constexpr (!AC) {
+        hipLaunchKernelGGL((gemm_kernel<64, AC, BC>), dim3(((a.M + 63) / 64) * tn * a.splits),
+                           dim3(256), 2 * (64 * BK * 2 + TILE_BYTES), s, a);
+        break;
       }
-    }
-    plan->bmt = 128;
-    plan->grid = small_tiles * a.splits;
-    return;
-  }
-  if (deep) {
-    dim3 grid(small_tiles * a.splits);
-    hipLaunchKernelGGL((gemm_deep_kernel<AC, BC>), grid, dim3(256), DSMEM, s, b);
-    TDFO_CHECK_HIP(hipGetLastError());
-    return;
-  }
-  if (!small_only && (g_policy == 20 || (g_policy == 22 && big_tiles * a.splits >= 128))) {
-    b.abl = 0;
-    dim3 grid(big_tiles * a.splits);
-    hipLaunchKernelGGL((gemm_big_kernel<AC, BC, 8>), grid, dim3(256), LSMEM, s, b);
-    TDFO_CHECK_HIP(hipGetLastError());
-    return;
-  }
-  if (!small_only && g_policy == 21 && small_tiles * a.splits >= 1024) {
-    dim3 grid(big_tiles * a.splits);
-    hipLaunchKernelGGL((gemm_big_kernel<AC, BC, 8>), grid, dim3(256), LSMEM, s, b);
-    TDFO_CHECK_HIP(hipGetLastError());
-    return;
-  }
-  if (big) {
-    dim3 grid(big_tiles * a.splits);
-    hipLaunchKernelGGL((gemm_big_kernel<AC, BC, 4>), grid, dim3(512), LSMEM, s, b);
-  } else {
-    if constexpr (!AC) {
-      // 64-row tiles when 128-row tiles leave CUs idle (bottom MLP, top3)
-      const int thr64 = g_policy == 5 ? 512 : 256;
-      if (small_tiles * a.splits < thr64 && g_policy != 3 && g_policy != 2) {
-        const int t64 = ((a.M + 63) / 64) * tn;
-        dim3 grid(t64 * a.splits);
-        hipLaunchKernelGGL((gemm_kernel<64, AC, BC>), grid, dim3(256),
-                           2 * (64 * BK * 2 + TILE_BYTES), s, b);
-        TDFO_CHECK_HIP(hipGetLastError());
-        return;
-      }
-    }
-    dim3 grid(small_tiles * a.splits);
-    hipLaunchKernelGGL((gemm_kernel<128, AC, BC>), grid, dim3(256), SMEM_BYTES, s, b);
+      [[fallthrough]];
+    default:
+      hipLaunchKernelGGL((gemm_kernel<128, AC, BC>), dim3(((a.M + BM - 1) / BM) * tn * a.splits),
+                         dim3(256), SMEM_BYTES, s, a);
+      break;
   }
   TDFO_CHECK_HIP(hipGetLastError());
 }
+
+int kernel_of(const GemmArgs& a) {
+  if (a.a_col) return a.b_col ? choose<true, true>(a) : choose<true, false>(a);
+  return a.b_col ? choose<false, true>(a) : choose<false, false>(a);
+}
+
+void launch_any(const GemmArgs& a, hipStream_t s) {
+  const int k = kernel_of(a);
+  if (a.a_col) {
+    if (a.b_col) launch<true, true>(a, k, s); else launch<true, false>(a, k, s);
+  } else {
+    if (a.b_col) launch<false, true>(a, k, s); else launch<false, false>(a, k, s);
+  }
+}
+
+// layout code of a problem: 0 row/row, 1 row/col, 3 col/col (col/row unused)
+int layout_of(const GemmArgs& a) { return (a.a_col ? 2 : 0) | (a.b_col ? 1 : 0); }
+
+// A layer's weight grad + dgrad (both read dy), or two weight grads, both on
+// the ping-pong kernel: one grid (each small launch pays fill / drain, and
+// the two problems' blocks fill each other's idle CUs). Bit-identical to
+// two launches.
+bool try_pair(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s) {
+  if (kernel_of(a0) != K_PP || kernel_of(a1) != K_PP) return false;
+  const int l0 = layout_of(a0), l1 = layout_of(a1);
+  if (l0 == 3 && l1 == 1) { pp_pair_launch<true, true, false, true>(a0, a1, s); return true; }
+  if (l1 == 3 && l0 == 1) { pp_pair_launch<true, true, false, true>(a1, a0, s); return true; }
+  if (l0 == 3 && l1 == 3) { pp_pair_launch<true, true, true, true>(a0, a1, s); return true; }
+  return false;
+}
+
+int g_pair = 1;
 
 }  // namespace
 
@@ -1394,125 +1155,11 @@ int gemm_policy(int p) {
   return old;
 }
 
-void gemm_bf16(const GemmArgs& a, hipStream_t s) {
-  if (a.a_col) {
-    if (a.b_col) launch<true, true>(a, s); else launch<true, false>(a, s);
-  } else {
-    if (a.b_col) launch<false, true>(a, s); else launch<false, false>(a, s);
-  }
-}
-
-namespace {
-SmallPlan small_plan(const GemmArgs& a) {
-  SmallPlan p{};
-  if (a.a_col) {
-    if (a.b_col) launch<true, true>(a, nullptr, &p); else launch<true, false>(a, nullptr, &p);
-  } else {
-    if (a.b_col) launch<false, true>(a, nullptr, &p); else launch<false, false>(a, nullptr, &p);
-  }
-  return p;
-}
-
-// layout code of a problem: 0 row/row, 1 row/col, 3 col/col (col/row unused)
-int layout_of(const GemmArgs& a) { return (a.a_col ? 2 : 0) | (a.b_col ? 1 : 0); }
-
-template <int BM0, bool AC0, bool BC0, int BM1, bool AC1, bool BC1>
-void pair_launch(const SmallPlan& p0, const SmallPlan& p1, hipStream_t s) {
-  auto fn = gemm_pair_kernel<BM0, AC0, BC0, BM1, AC1, BC1>;
-  static bool attr = false;
-  if (!attr) {
-    TDFO_CHECK_HIP(hipFuncSetAttribute((const void*)fn,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, SMEM_BYTES));
-    attr = true;
-  }
-  hipLaunchKernelGGL(fn, dim3(p0.grid + p1.grid), dim3(256), SMEM_BYTES, s, p0.args, p1.args,
-                     p0.grid);
-  TDFO_CHECK_HIP(hipGetLastError());
-}
-
-// The pairs the MLP backward issues: a layer's dgrad (row A, col B; 64- or
-// 128-row tiles) with its weight grad (col A, col B, 128-row tiles), or two
-// weight grads (the deferred ones of a multi-rank step).
-template <bool AC0, bool BC0, bool AC1, bool BC1>
-void big_pair_launch(const SmallPlan& p0, const SmallPlan& p1, hipStream_t s) {
-  auto fn = gemm_big_pair_kernel<AC0, BC0, AC1, BC1>;
-  static bool attr = false;
-  if (!attr) {
-    TDFO_CHECK_HIP(hipFuncSetAttribute((const void*)fn,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, LSMEM));
-    attr = true;
-  }
-  hipLaunchKernelGGL(fn, dim3(p0.grid + p1.grid), dim3(512), LSMEM, s, p0.args, p1.args,
-                     p0.grid);
-  TDFO_CHECK_HIP(hipGetLastError());
-}
-
-template <bool AC0, bool BC0, bool AC1, bool BC1>
-void pp_pair_launch(const SmallPlan& p0, const SmallPlan& p1, hipStream_t s) {
-  auto fn = gemm_pp_pair_kernel<AC0, BC0, AC1, BC1>;
-  constexpr int lds = PPGeom<128, 2>::LDS;
-  static bool attr = false;
-  if (!attr) {
-    TDFO_CHECK_HIP(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       lds));
-    attr = true;
-  }
-  hipLaunchKernelGGL(fn, dim3(p0.grid + p1.grid), dim3(512), lds, s, p0.args, p1.args, p0.grid);
-  TDFO_CHECK_HIP(hipGetLastError());
-}
-
-int g_pair_deep = 1;   // pair a deep-kernel dgrad on 256x128 tiles with its weight grad
-
-bool try_pair(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s) {
-  SmallPlan p0 = small_plan(a0), p1 = small_plan(a1);
-  // a dgrad the deep 128x128 kernel would take alone (DCN-v2's U dgrad: the
-  // 256x128 grid leaves CUs idle) runs on 256x128 tiles beside a 256x128
-  // weight grad, whose blocks fill those CUs
-  if (g_pair_deep && p0.bmt == 256 && !p1.bmt && p1.big_grid) { p1.bmt = 256; p1.grid = p1.big_grid; }
-  if (g_pair_deep && p1.bmt == 256 && !p0.bmt && p0.big_grid) { p0.bmt = 256; p0.grid = p0.big_grid; }
-  if (!p0.bmt || !p1.bmt) return false;
-  const int l0 = layout_of(a0), l1 = layout_of(a1);
-  if (p0.bmt == 129 || p1.bmt == 129) {           // ping-pong pairs
-    if (p0.bmt != 129 || p1.bmt != 129) return false;
-    if (l0 == 3 && l1 == 1) { pp_pair_launch<true, true, false, true>(p0, p1, s); return true; }
-    if (l1 == 3 && l0 == 1) { pp_pair_launch<true, true, false, true>(p1, p0, s); return true; }
-    if (l0 == 3 && l1 == 3) { pp_pair_launch<true, true, true, true>(p0, p1, s); return true; }
-    return false;
-  }
-  if ((p0.bmt == 256) != (p1.bmt == 256)) return false;
-  if (p0.bmt == 256) {                            // weight grad + dgrad on 256x128 tiles
-    if (l0 == 3 && l1 == 1) { big_pair_launch<true, true, false, true>(p0, p1, s); return true; }
-    if (l1 == 3 && l0 == 1) { big_pair_launch<true, true, false, true>(p1, p0, s); return true; }
-    if (l0 == 3 && l1 == 3) { big_pair_launch<true, true, true, true>(p0, p1, s); return true; }
-    return false;
-  }
-  if (l0 == 3 && l1 == 3 && p0.bmt == 128 && p1.bmt == 128) {   // two weight grads
-    pair_launch<128, true, true, 128, true, true>(p0, p1, s);
-    return true;
-  }
-  if (l0 == 3 && p0.bmt == 128 && l1 == 1) {
-    if (p1.bmt == 64) pair_launch<128, true, true, 64, false, true>(p0, p1, s);
-    else              pair_launch<128, true, true, 128, false, true>(p0, p1, s);
-    return true;
-  }
-  if (l1 == 3 && p1.bmt == 128 && l0 == 1) {
-    if (p0.bmt == 64) pair_launch<128, true, true, 64, false, true>(p1, p0, s);
-    else              pair_launch<128, true, true, 128, false, true>(p1, p0, s);
-    return true;
-  }
-  return false;
-}
-}  // namespace
-
-int g_pair = 1;
+void gemm_bf16(const GemmArgs& a, hipStream_t s) { launch_any(a, s); }
 
 int gemm_pairing(int v) {
-  // 0 off, 1 on, 2 on but a deep-kernel dgrad is not moved to 256x128 tiles
-  const int old = g_pair ? (g_pair_deep ? 1 : 2) : 0;
-  if (v >= 0) {
-    g_pair = v ? 1 : 0;
-    g_pair_deep = v == 1 ? 1 : 0;
-  }
+  const int old = g_pair;
+  if (v >= 0) g_pair = v ? 1 : 0;
   return old;
 }
 

@@ -7,7 +7,10 @@
 //   requester  rw_bucketize : ids -> per-owner segments of a [W][cap+1]
 //              int64 send buffer (slot cap holds the count), each entry
 //              packing (bag key j*B+b) << 32 | owner-local row key; stable,
-//              so every segment stays sorted by bag key
+//              so every segment stays sorted by bag key. Rows are dealt
+//              round-robin (owner = id mod W, local row = id div W), so a
+//              hot head of low ids -- Zipf / frequency-ordered data --
+//              spreads over every owner instead of landing on owner 0.
 //   (RCCL)     all_to_all_single of the send buffer (equal splits)
 //   owner      rw_pool      : per (requester, bag key) partial sum of the
 //              rows it owns -> bf16 [W][B][nrw*D] (zeros where a bag has no
@@ -16,8 +19,11 @@
 //              shared sort-based fused embedding backward, fed from the
 //              received entries (embedding.hip: embedding_bwd_prepare_rw)
 //
-// Entries beyond a segment's capacity are dropped and raise a sticky device
-// flag the engine checks on the host (no silent training on partial bags).
+// The scan also records the largest per-owner count ("need"): the engine
+// all-reduces it before the exchange and grows the capacity (re-bucketizing
+// the batch) when a segment would overflow, so no lookup is ever dropped.
+// Entries beyond a segment's capacity (only possible if that check is
+// bypassed) raise a sticky device flag the engine checks on the host.
 #include "tdfo_common.h"
 #include "tdfo_kernels.h"
 
@@ -55,10 +61,8 @@ __device__ __forceinline__ int rw_route(const RwBucketArgs& a, const RwMeta& M, 
   const int64_t L = M.L[j];
   const int64_t b = off / L;
   const int64_t id = a.ids[M.in_base[j] + off];
-  const int64_t blk = M.blk[j];
-  int64_t o = id / blk;
-  if (o > a.W - 1) o = a.W - 1;
-  const uint64_t row = (uint64_t)(M.lrow[j] + (id - o * blk));
+  const int64_t o = id % a.W;
+  const uint64_t row = (uint64_t)(M.lrow[j] + id / a.W);
   const uint64_t key = (uint64_t)j * (uint64_t)a.B + (uint64_t)b;
   packed = (key << 32) | (row & 0xffffffffull);
   return (int)o;
@@ -87,6 +91,7 @@ __global__ __launch_bounds__(RW_THREADS) void rw_hist_kernel(RwBucketArgs a, int
 __global__ __launch_bounds__(1024) void rw_scan_kernel(RwBucketArgs a, int32_t* hist, int nch) {
   __shared__ int32_t wsum[16];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  int32_t most = 0;
   for (int o = 0; o < a.W; ++o) {
     int32_t carry = 0;
     for (int c0 = 0; c0 < nch; c0 += 1024) {
@@ -111,8 +116,10 @@ __global__ __launch_bounds__(1024) void rw_scan_kernel(RwBucketArgs a, int32_t* 
     if (tid == 0) {
       a.send[(int64_t)o * (a.cap + 1) + a.cap] = carry < a.cap ? carry : a.cap;
       if (carry > a.cap) a.overflow[0] = 1;
+      most = carry > most ? carry : most;
     }
   }
+  if (tid == 0 && a.need) a.need[0] = most;
 }
 
 // Stable scatter: chunk order, then tile order, then wave order, then lane

@@ -596,8 +596,8 @@ class Bert4RecTrainer:
             full = torch.zeros(self.V, self.E, dtype=torch.float32, device=self.device)
             part = self.item.engine.get_table_weight(0)
             if part is not None:
-                lo, w = part
-                full[lo: lo + w.shape[0]].copy_(w)
+                rows, w = part
+                full[rows].copy_(w)
             if self.world > 1:
                 dist.all_reduce(full, group=self.group)
             return full

@@ -233,12 +233,6 @@ class DLRMTrainer:
         assert cfg.top[-1] == 1
         assert cfg.interaction != "dcn" or cfg.dcn_rank % 64 == 0, "dcn_rank must be a multiple of 64"
         torch.manual_seed(cfg.seed)
-        if self.device.type == "cuda" and not os.environ.get("TDFO_GEMM_POLICY"):
-            # GEMM tile policy measured per workload (profiles/gemm_tile_ab.md):
-            # DCN-v2's wide cross layers run best on 256x128 tiles (policy 25:
-            # + the deep-pipelined 128x128 kernel for its 512-wide long-K
-            # GEMMs), DLRM's <= 1024-wide MLPs on 128x128 / 64x128 tiles
-            ops.gemm_policy(25 if cfg.interaction == "dcn" else 0)
         # ------------------------------------------------------ embeddings
         optim = EmbOptimConfig(cfg.emb_opt, lr=cfg.emb_lr, eps=cfg.emb_eps)
         tables = cfg.tables()
@@ -1094,11 +1088,23 @@ class DLRMTrainer:
         elif self.graph is not None:
             if isinstance(self.graph, list):
                 self._on_side = False
+                eager = False
                 for kind, item in self.graph:
                     if kind in ("c", "e"):
-                        self._run_stage(kind, None, graph=item)
+                        g, fns = item
+                        if eager:        # a captured buffer was reallocated this step
+                            self._run_stage(kind, lambda fns=fns: [f() for f in fns])
+                        else:
+                            self._run_stage(kind, None, graph=g)
                     else:
                         self._run_stage(kind, item)
+                        # row-wise capacity grown inside an exchange stage: the
+                        # rest of this step runs eagerly, then re-capture
+                        eager = eager or self.emb.layout_version != self._graph_layout
+                if eager:
+                    self.sync_streams()
+                    torch.cuda.synchronize()
+                    self.capture_graph(warmup=0, staged=True)
             else:
                 self.graph.replay()
         else:
@@ -1451,7 +1457,7 @@ class DLRMTrainer:
                                       capture_error_mode="thread_local"):
                     for fn in fns:
                         fn()
-                seq.append((kind, g))
+                seq.append((kind, (g, fns)))
             else:
                 # dry exchange keeps every rank's collective sequence aligned
                 self._run_stage(kind, fns[0])
@@ -1460,6 +1466,7 @@ class DLRMTrainer:
             torch.cuda.current_stream().wait_stream(se)
         torch.cuda.synchronize()
         self.graph = seq
+        self._graph_layout = self.emb.layout_version
 
     def pop_loss(self) -> float:
         """Mean training loss since the last call (one device->host read);

@@ -460,8 +460,8 @@ class TwoTowerTrainer:
             full = torch.zeros(self.rows[t], E, dtype=torch.float32, device=self.device)
             part = self.sharded.get_table_weight(t)
             if part is not None:
-                lo, w = part
-                full[lo: lo + w.shape[0]].copy_(w)
+                rows, w = part
+                full[rows].copy_(w)
             if self.world > 1:
                 dist.all_reduce(full, group=self.group)
             return full.cpu()

@@ -209,8 +209,10 @@ def rw_unpack_meta(meta, nrw):
 
 def rw_bucketize(ids, meta, nrw, W, B, cap, n, send, overflow):
     """Reference of the row-wise bucketize (rowwise.hip): stable per-owner
-    segments of packed (bag key << 32 | owner-local row) entries, the count in
-    slot ``cap`` of each [cap + 1] segment, overflow flagged (sticky)."""
+    segments (owner = id mod W, local row = id div W) of packed (bag key << 32
+    | owner-local row) entries, the count in slot ``cap`` of each [cap + 1]
+    segment, overflow flagged (sticky) in overflow[0], the largest per-owner
+    count in overflow[1] (when it has two elements)."""
     dev = ids.device
     in_base, L, blk, lrow, cum = rw_unpack_meta(meta, nrw)
     q = torch.arange(n, device=dev)
@@ -218,18 +220,22 @@ def rw_bucketize(ids, meta, nrw, W, B, cap, n, send, overflow):
     off = q - cum[j]
     b = off // L[j]
     gid = ids[in_base[j] + off]
-    owner = torch.clamp(gid // blk[j], max=W - 1)
-    row = lrow[j] + gid - owner * blk[j]
+    owner = gid % W
+    row = lrow[j] + gid // W
     packed = ((j * B + b) << 32) | row
     seg = send.view(W, cap + 1)
+    most = 0
     for o in range(W):
         sel = packed[owner == o]
         c = int(sel.numel())
+        most = max(most, c)
         if c > cap:
             overflow.view(-1)[0] = 1
             c = cap
         seg[o, :c] = sel[:c]
         seg[o, cap] = c
+    if overflow.numel() >= 2:
+        overflow.view(-1)[1] = most
 
 
 def _rw_entries(recv, meta, nrw, W, B, cap):

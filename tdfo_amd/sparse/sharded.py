@@ -18,10 +18,13 @@ Design (MI355X-first):
     place through a slot map (no permute kernel in either direction).
     Shapes are static for fixed pooling factors, so the exchange is
     hipGraph-capturable and needs no split exchange.
-  * row-wise (RW) shards: ids are bucketed by owner block, exchanged with
-    data-dependent splits, looked up unpooled by the owner, returned, and
-    pooled at the requester by the same embedding kernel (the received rows
-    act as a table); gradients travel back per id and the owner's fused
+  * row-wise (RW) shards: rows are dealt round-robin over the ranks (owner =
+    id mod W, so a hot head of low ids -- Zipf / frequency-ordered Criteo --
+    is spread over every owner); ids are bucketed by owner into per-owner
+    segments whose capacity is checked (all-reduced max count) before every
+    exchange and grown on demand, so skewed batches never drop a lookup;
+    the owner pools per (requester, bag) and one reduce-scatter returns the
+    partial sums; gradients come back by all-gather and the owner's fused
     sort-based backward merges duplicates across requesters.
   * column-wise (CW) shards: block k of a table (columns [c0, c0 + Dc)) is
     looked up by its rank exactly like a table-wise shard of width Dc, its
@@ -80,9 +83,11 @@ class ShardedEmbeddingBags:
                  batch_size: int, pooling: Sequence[int], device, optim: EmbOptimConfig,
                  group=None, seed: int = 0, mean: bool = False, rw_capacity: float = 1.25,
                  rw_comm: str = "bf16", dp_dense_max_bytes: int = 256 << 20):
-        """``rw_capacity``: per-owner segment capacity of the row-wise exchange
-        as a multiple of the uniform share n/W (+256); exceeding it raises
-        (``check_overflow``) instead of training on partial bags.
+        """``rw_capacity``: initial per-owner segment capacity of the row-wise
+        exchange as a multiple of the uniform share n/W (+256). Before every
+        exchange the largest per-owner count is all-reduced and the capacity
+        grows (buffers reallocated, ``layout_version`` bumped, the batch
+        re-bucketized) when a segment would overflow.
         ``rw_comm``: dtype of the pooled partials' reduce-scatter ("bf16"
         halves the bytes; "fp32" sums exactly as one process would, up to
         fp32 association)."""
@@ -243,13 +248,14 @@ class ShardedEmbeddingBags:
             meta = ([self.in_base[t] for t in self.rw_tables] + Ls + blocks
                     + list(self.rw_store.row_offset_host) + cum)
             self.rw_meta = torch.tensor(meta, dtype=torch.int64, device=self.device)
-            self.rw_cap = cap = self.rw_capacity(n, W, rw_capacity)
-            self.rw_send = torch.zeros(W * (cap + 1), dtype=torch.int64, device=self.device)
-            self.rw_recv = torch.zeros_like(self.rw_send) if W > 1 else self.rw_send
+            self.rw_cap_factor = float(rw_capacity)
             from .. import ops as _ops
             self.rw_ws = torch.empty(_ops.rw_bucketize_workspace(n, W), dtype=torch.uint8,
                                      device=self.device)
-            self.rw_overflow = torch.zeros(1, dtype=torch.int32, device=self.device)
+            # [sticky overflow flag, largest per-owner count of the last bucketize]
+            self.rw_overflow = torch.zeros(2, dtype=torch.int32, device=self.device)
+            self.rw_dynamic = W > 1          # exact capacity check before every exchange
+            self.rw_grows = 0
             self.rw_starts = torch.zeros(W * (self.nrw * B + 1), dtype=torch.int32,
                                          device=self.device)
             bf_ = torch.bfloat16
@@ -263,10 +269,7 @@ class ShardedEmbeddingBags:
                             if W > 1 and cdt == torch.float32 else None)
             self.rw_gbuf = (torch.zeros(W * B * self.rw_width, dtype=bf_, device=self.device)
                             if W > 1 else None)
-            self.rw_bwd_ws = None
-            if self.device.type == "cuda":
-                self.rw_bwd_ws = torch.empty(_ops.embedding_bwd_workspace(W * cap, D),
-                                             dtype=torch.uint8, device=self.device)
+            self._rw_alloc(self.rw_capacity(n, W, rw_capacity))
             self._rw_prepared = False
         # ---- data-parallel (replicated) group: local lookup, gradient
         # all-gather, identical deterministic update on every rank
@@ -350,6 +353,10 @@ class ShardedEmbeddingBags:
                 self.cw_pieces.append((src, self.dsum[r], self.cw_base + j * D + c0, self.cw_width))
         self._pending = None
         self._rw_state = None
+        self._rw_ids = None
+        # bumped whenever a buffer captured into a hipGraph is reallocated
+        # (row-wise capacity growth): the trainer re-captures its graphs
+        self.layout_version = 0
 
     def alias_pooled(self, out: torch.Tensor, d_out: torch.Tensor, col0: int) -> bool:
         """One rank, table-wise tables only: pool straight into the consumer's
@@ -383,21 +390,66 @@ class ShardedEmbeddingBags:
 
     @staticmethod
     def rw_capacity(n: int, W: int, factor: float) -> int:
+        """Initial per-owner capacity: factor x the uniform share n/W plus a
+        slack of up to 256 ids (grown on demand before any exchange)."""
         if W == 1:
             return max(1, n)
-        return max(1, min(n, -(-int(factor * n) // W) + 256))
+        return max(1, min(n, -(-int(factor * n) // W) + min(256, n // (4 * W))))
+
+    def _rw_alloc(self, cap: int):
+        """(Re)allocate the [W][cap + 1] exchange buffers and the owner-side
+        backward workspace for per-owner capacity ``cap``."""
+        W, D = self.world, self.D
+        self.rw_cap = cap
+        self.rw_send = torch.zeros(W * (cap + 1), dtype=torch.int64, device=self.device)
+        self.rw_recv = torch.zeros_like(self.rw_send) if W > 1 else self.rw_send
+        self.rw_bwd_ws = None
+        if self.device.type == "cuda":
+            from .. import ops as _ops
+            self.rw_bwd_ws = torch.empty(_ops.embedding_bwd_workspace(W * cap, D),
+                                         dtype=torch.uint8, device=self.device)
+
+    def _rw_bucketize(self, ids: torch.Tensor):
+        from .. import ops
+        ops.rw_bucketize(ids, self.rw_meta, self.nrw, self.world, self.B, self.rw_cap,
+                         self.rw_n, self.rw_send, self.rw_ws, self.rw_overflow)
+
+    def _rw_check_capacity(self):
+        """All ranks agree on the largest per-owner count of this batch (MAX
+        all-reduce, one host read) and grow the capacity before the exchange
+        if any segment would overflow: the batch is re-bucketized into the
+        larger segments, so no lookup is dropped whatever the id skew."""
+        need = self.rw_overflow[1:2].clone()
+        if self.world > 1:
+            dist.all_reduce(need, op=dist.ReduceOp.MAX, group=self.group)
+        need = int(need.item())
+        if need <= self.rw_cap:
+            return
+        cap = min(self.rw_n, int(need * 1.25) + 256)
+        self._rw_alloc(cap)
+        self.rw_grows += 1
+        self.layout_version += 1
+        self.rw_overflow[:1].zero_()          # this batch's overflow is undone by the re-bucketize
+        self._rw_bucketize(self._rw_ids)
 
     def _rw_region(self, buf):
         base = sum(self.tw_recv_sizes)
         return buf[base: base + self.B * self.rw_width]
 
     def check_overflow(self):
-        """Raise if any row-wise segment overflowed its capacity (host sync)."""
-        if self.rw_tables and int(self.rw_overflow.item()):
+        """Raise on every rank if any rank's row-wise segment overflowed its
+        capacity (only possible with the per-exchange capacity check off):
+        the flag is MAX all-reduced so no rank is left waiting in the next
+        collective while another raises (host sync)."""
+        if not self.rw_tables:
+            return
+        flag = self.rw_overflow[:1].clone()
+        if self.world > 1:
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
+        if int(flag.item()):
             raise RuntimeError(
                 f"row-wise exchange capacity exceeded (cap {self.rw_cap} ids per owner, "
-                f"{self.rw_n} ids per rank): lookups were dropped; raise rw_capacity "
-                f"(skewed ids per owner block)")
+                f"{self.rw_n} ids per rank) with the capacity check off: lookups were dropped")
 
     @property
     def fwd_prep_noop(self) -> bool:
@@ -457,9 +509,8 @@ class ShardedEmbeddingBags:
             if self.world == 1:
                 self.tw_recv_ids = self.tw_send_ids
         if self.rw_tables:
-            from .. import ops
-            ops.rw_bucketize(ids, self.rw_meta, self.nrw, self.world, self.B, self.rw_cap,
-                             self.rw_n, self.rw_send, self.rw_ws, self.rw_overflow)
+            self._rw_ids = ids
+            self._rw_bucketize(ids)
 
     def stage_fwd_ids_exchange(self, async_op: bool = False):
         """Id exchange (input dist). async_op: the collectives are left in
@@ -477,6 +528,8 @@ class ShardedEmbeddingBags:
             works.append(_a2a(self.cw_recv_ids, self.cw_send_ids, [self.cw_recv_count] * W,
                               self.cw_send_counts, self.group, async_op=async_op))
         if W > 1 and self.rw_tables:
+            if self.rw_dynamic:
+                self._rw_check_capacity()
             works.append(dist.all_to_all_single(self.rw_recv, self.rw_send, group=self.group,
                                                 async_op=async_op))
         self._ids_works = [w for w in works if w is not None] if async_op else []
@@ -674,41 +727,46 @@ class ShardedEmbeddingBags:
         return (0, self.D) if self._local_slices(t) is not None else None
 
     def _local_slices(self, t: int):
-        """(store, local_table_index, row_start, row_stop) of table t here, or None."""
+        """(store, local_table_index, rows) of table t here, or None. ``rows``
+        is a slice of the table's global rows: contiguous for whole tables,
+        ``slice(rank, rows, W)`` for a row-wise shard (round-robin rows);
+        local row k of the store holds global row rows.start + k*rows.step."""
+        n = self.tables[t].num_embeddings
         if t in self.cw_blocks:
             cols = [c0 for (r, c0, _) in self.cw_blocks[t] if r == self.rank]
             if not cols:
                 return None
             k = self.cw_owned[self.rank].index((t, cols[0]))
-            return self.cw_store, k, 0, self.tables[t].num_embeddings
+            return self.cw_store, k, slice(0, n, 1)
         if t in self.tw_mine:
-            return self.tw_store, self.tw_mine.index(t), 0, self.tables[t].num_embeddings
+            return self.tw_store, self.tw_mine.index(t), slice(0, n, 1)
         if t in self.dp_tables:
-            j = self.dp_tables.index(t)
-            return self.dp_store, j, 0, self.tables[t].num_embeddings
+            return self.dp_store, self.dp_tables.index(t), slice(0, n, 1)
         if t in self.rw_tables:
-            j = self.rw_tables.index(t)
-            blk = self.rw_block_host[j]
-            lo = min(self.rank * blk, self.tables[t].num_embeddings)
-            hi = min(lo + blk, self.tables[t].num_embeddings)
-            return self.rw_store, j, lo, hi
+            return self.rw_store, self.rw_tables.index(t), slice(min(self.rank, n), n, self.world)
         return None
+
+    @staticmethod
+    def slice_len(sl: slice) -> int:
+        return len(range(sl.start, sl.stop, sl.step))
 
     def set_table_weight(self, t: int, full: torch.Tensor):
         """Copy this rank's part of table ``t`` from the full [rows, D] tensor."""
-        sl = self._local_slices(t)
-        if sl is not None and sl[3] > sl[2]:
-            store, i, lo, hi = sl
+        loc = self._local_slices(t)
+        if loc is not None and self.slice_len(loc[2]) > 0:
+            store, i, sl = loc
             c0, w = self.table_cols(t)
-            store.table_weight(i)[: hi - lo].copy_(full[lo:hi, c0:c0 + w].to(store.weight.device))
+            store.table_weight(i)[: self.slice_len(sl)].copy_(
+                full[sl, c0:c0 + w].to(store.weight.device))
 
     def get_table_weight(self, t: int):
-        """This rank's (row_start, rows view) of table ``t``, or None."""
-        sl = self._local_slices(t)
-        if sl is None:
+        """This rank's (global row slice, rows view) of table ``t``, or None:
+        ``full[rows][:, cols] == view`` (see ``_local_slices``)."""
+        loc = self._local_slices(t)
+        if loc is None:
             return None
-        store, i, lo, hi = sl
-        return lo, store.table_weight(i)[: max(0, hi - lo)]
+        store, i, sl = loc
+        return sl, store.table_weight(i)[: self.slice_len(sl)]
 
     def state_dict(self):
         d = {"tw": self.tw_store.state_dict()}

@@ -42,8 +42,9 @@ import torch
 FORMAT = "tdfo-sharded-v2"
 
 
-def _piece_name(t: int, lo: int, hi: int, c0: int, c1: int) -> str:
-    return f"t{t}.r{lo}-{hi}.c{c0}-{c1}"
+def _piece_name(t: int, lo: int, hi: int, step: int, c0: int, c1: int) -> str:
+    rs = f"r{lo}-{hi}" + (f"s{step}" if step != 1 else "")
+    return f"t{t}.{rs}.c{c0}-{c1}"
 
 
 def _write_rows(path: Path, view: torch.Tensor, chunk_bytes: int):
@@ -60,28 +61,30 @@ def _write_rows(path: Path, view: torch.Tensor, chunk_bytes: int):
 
 def local_pieces(emb) -> List[Dict]:
     """Pieces of the embedding tables this rank owns under its plan: dicts with
-    table, rows [lo, hi), cols [c0, c1), replicated flag, the weight view and
-    the optimizer-state views (``state1`` row-wise [rows] or [rows, cols])."""
+    table, global rows ``lo, lo + step, ... < hi`` (step 1: a contiguous range;
+    W for a round-robin row-wise shard), cols [c0, c1), replicated flag, the
+    weight view (one row per piece row, in that order) and the
+    optimizer-state views (``state1`` row-wise [rows] or [rows, cols])."""
     out = []
     for t in range(emb.T):
-        sl = emb._local_slices(t)
-        if sl is None:
+        loc = emb._local_slices(t)
+        if loc is None:
             continue
-        store, i, lo, hi = sl
-        if hi <= lo:
+        store, i, sl = loc
+        n = len(range(sl.start, sl.stop, sl.step))
+        if n <= 0:
             continue
         c0, w = emb.table_cols(t)
         r0 = store.row_offset_host[i]
-        n = hi - lo
         states = {}
         for name in ("state1", "state2"):
             st = getattr(store, name)
             if st is None:
                 continue
-            states[name] = st[r0: r0 + n] if st.dim() == 1 else st[r0: r0 + n]
-        out.append({"table": t, "lo": lo, "hi": hi, "c0": c0, "c1": c0 + w,
-                    "replicated": t in emb.dp_tables, "weight": store.weight[r0: r0 + n],
-                    "states": states})
+            states[name] = st[r0: r0 + n]
+        out.append({"table": t, "lo": sl.start, "hi": sl.stop, "step": sl.step, "c0": c0,
+                    "c1": c0 + w, "replicated": t in emb.dp_tables,
+                    "weight": store.weight[r0: r0 + n], "states": states})
     return out
 
 
@@ -97,13 +100,13 @@ def save(tr, dirpath: str, step: int, rank: int, world: int, meta: Optional[Dict
     for p in local_pieces(tr.emb):
         if p["replicated"] and rank != 0:
             continue
-        base = _piece_name(p["table"], p["lo"], p["hi"], p["c0"], p["c1"])
+        base = _piece_name(p["table"], p["lo"], p["hi"], p["step"], p["c0"], p["c1"])
         files = {"weight": base + ".w.bin"}
         _write_rows(d / files["weight"], p["weight"], chunk_bytes)
         for name, view in p["states"].items():
             files[name] = base + (".s1.bin" if name == "state1" else ".s2.bin")
             _write_rows(d / files[name], view, chunk_bytes)
-        index.append({k: p[k] for k in ("table", "lo", "hi", "c0", "c1")} |
+        index.append({k: p[k] for k in ("table", "lo", "hi", "step", "c0", "c1")} |
                      {"files": files, "state1_rowwise": bool("state1" in p["states"] and
                                                              p["states"]["state1"].dim() == 1)})
     (d / f"rank_{rank:05d}.json").write_text(json.dumps(index))
@@ -143,11 +146,15 @@ def _saved_pieces(d: Path, man: Dict) -> Dict[int, List[Dict]]:
     return by_table
 
 
+def _rows(sp: Dict) -> range:
+    return range(sp["lo"], sp["hi"], sp.get("step", 1))
+
+
 def _copy_region(dst: torch.Tensor, d: Path, sp: Dict, fname: str, lo: int, hi: int, c0: int,
                  c1: int, rowwise: bool, chunk_bytes: int, accumulate_weight: float = 0.0):
-    """dst[rows lo..hi of the table, cols c0..c1] <- saved piece ``sp`` (the
-    caller passes the intersection). ``rowwise``: dst is a [rows] state; with
-    accumulate_weight > 0 it is accumulated (width-weighted mean)."""
+    """dst[rows lo..hi of the table, cols c0..c1] <- saved contiguous piece
+    ``sp`` (the caller passes the intersection). ``rowwise``: dst is a [rows]
+    state; with accumulate_weight > 0 it is accumulated (width-weighted mean)."""
     rows_s = sp["hi"] - sp["lo"]
     cols_s = sp["c1"] - sp["c0"]
     shape = (rows_s,) if rowwise else (rows_s, cols_s)
@@ -167,6 +174,48 @@ def _copy_region(dst: torch.Tensor, d: Path, sp: Dict, fname: str, lo: int, hi: 
         else:
             dst[r0 - lo: r1 - lo] = src
     del mm
+
+
+def _copy_strided(p: Dict, d: Path, sp: Dict, chunk_bytes: int) -> int:
+    """Local piece ``p`` <- every row it shares with saved piece ``sp`` when
+    either is strided (round-robin row-wise shards): the local rows are
+    walked in chunks, mapped to global ids, and the saved rows they hit are
+    gathered from the memory-mapped files. Returns the elements covered."""
+    pr, srows = _rows(p), _rows(sp)
+    cl, ch = max(p["c0"], sp["c0"]), min(p["c1"], sp["c1"])
+    if cl >= ch or not pr or not srows:
+        return 0
+    n_s, w_s = len(srows), sp["c1"] - sp["c0"]
+    per_row = max(1, (p["c1"] - p["c0"]) * 4)
+    chunk = max(1, chunk_bytes // per_row)
+    covered = 0
+    files = {"weight": (p["weight"], False)}
+    for name, view in p["states"].items():
+        if name not in sp["files"]:
+            raise ValueError(f"checkpoint piece of table {p['table']} lacks {name}")
+        files[name] = (view, view.dim() == 1)
+    mms = {k: np.memmap(d / sp["files"][k], dtype=np.float32, mode="r",
+                        shape=(n_s,) if rw else (n_s, w_s)) for k, (_, rw) in files.items()}
+    sst = sp.get("step", 1)
+    for k0 in range(0, len(pr), chunk):
+        ids = torch.arange(pr.start + k0 * pr.step,
+                           min(pr.stop, pr.start + (k0 + chunk) * pr.step), pr.step)
+        hit = (ids >= sp["lo"]) & (ids < sp["hi"]) & ((ids - sp["lo"]) % sst == 0)
+        if not bool(hit.any()):
+            continue
+        loc = (torch.nonzero(hit).view(-1) + k0).numpy()
+        src = ((ids[hit] - sp["lo"]) // sst).numpy()
+        covered += len(loc) * (ch - cl)
+        for k, (view, rw) in files.items():
+            li = torch.from_numpy(loc).to(view.device)
+            if rw:
+                vals = torch.from_numpy(np.asarray(mms[k][src])).to(view.device)
+                view[li] += ((ch - cl) / (p["c1"] - p["c0"])) * vals
+            else:
+                vals = np.asarray(mms[k][src][:, cl - sp["c0"]: ch - sp["c0"]])
+                view[li, cl - p["c0"]: ch - p["c0"]] = torch.from_numpy(vals).to(view.device)
+    del mms
+    return covered
 
 
 def load(tr, dirpath: str, rank: int, world: int, expect_meta: Optional[Dict] = None,
@@ -199,6 +248,9 @@ def load(tr, dirpath: str, rank: int, world: int, expect_meta: Optional[Dict] = 
             if rowwise:
                 rw_state.zero_()
             for sp in cands:
+                if p["step"] != 1 or sp.get("step", 1) != 1:
+                    covered += _copy_strided(p, d, sp, chunk_bytes)
+                    continue
                 rl, rh = max(lo, sp["lo"]), min(hi, sp["hi"])
                 cl, ch = max(c0, sp["c0"]), min(c1, sp["c1"])
                 if rl >= rh or cl >= ch:
@@ -216,9 +268,10 @@ def load(tr, dirpath: str, rank: int, world: int, expect_meta: Optional[Dict] = 
                     else:
                         _copy_region(view[rl - lo: rh - lo, cl - c0: ch - c0], d, sp,
                                      sp["files"][name], rl, rh, cl, ch, False, chunk_bytes)
-            if covered != (hi - lo) * (c1 - c0):
-                raise ValueError(f"checkpoint does not cover table {t} rows [{lo},{hi}) "
-                                 f"cols [{c0},{c1}) ({covered} of {(hi - lo) * (c1 - c0)})")
+            want = len(_rows(p)) * (c1 - c0)
+            if covered != want:
+                raise ValueError(f"checkpoint does not cover table {t} rows {_rows(p)} "
+                                 f"cols [{c0},{c1}) ({covered} of {want})")
         dense = torch.load(d / "dense.pt", map_location="cpu", weights_only=True)
         tr.load_dense_state(dense)
     return int(man["step"])

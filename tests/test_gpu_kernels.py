@@ -30,11 +30,9 @@ def rel_err(a, b):
 
 
 # ------------------------------------------------------------------ GEMM
-@pytest.fixture(params=[0, 1, 2, 3, 6, 20, 23, 25, 31, 60],
-                ids=["auto", "tile64or128", "tile256", "tile128", "auto_ldsepi", "tile256w4",
-                     "deep128", "dcn", "pp256", "pp128"])
+@pytest.fixture(params=[0, 1, 2, 3], ids=["auto", "twostage", "deep", "pingpong"])
 def gemm_pol(request):
-    """Run a GEMM test once per tile kernel (128x128 2-stage / 256x128 3-stage)."""
+    """Run a GEMM test once per kernel (auto, and each kernel forced)."""
     old = ops.gemm_policy(request.param)
     yield request.param
     ops.gemm_policy(old)
@@ -895,7 +893,7 @@ def test_mlp3_fused_forward(B, strided_out):
 
 @pytest.mark.parametrize("M", [8192, 1000])
 @pytest.mark.parametrize("N,K", [(1024, 512), (256, 512), (512, 256), (512, 3456), (3456, 512)])
-@pytest.mark.parametrize("policy", [0, 25])
+@pytest.mark.parametrize("policy", [0, 3])
 def test_gemm_batch_pairs_wgrad_dgrad(M, N, K, policy):
     """A layer's weight grad (split-K slabs + column sums) and dgrad (ReLU
     mask) recorded under ops.gemm_batch go out as one paired launch with the
@@ -931,7 +929,7 @@ def test_gemm_batch_pairs_wgrad_dgrad(M, N, K, policy):
     assert rel_err(res[0][1], exp) < 1e-2
 
 
-@pytest.mark.parametrize("policy", [0, 25])
+@pytest.mark.parametrize("policy", [0, 3])
 def test_gemm_batch_pairs_two_wgrads(policy):
     """Two independent weight grads (a multi-rank step's deferred ones) share
     one paired launch, bit-identical to two launches."""

@@ -19,7 +19,11 @@ B = 256
 STEPS = 3
 
 
-def _worker(rank, world, Bk, strategy, graph, rw_comm, emb_opt="rowwise_adagrad", pipeline=False):
+def _worker(rank, world, Bk, strategy, graph, rw_comm, emb_opt="rowwise_adagrad", pipeline=False,
+            dist="uniform", alpha=1.05, rw_capacity=1.25):
+    """dist="zipf": the two eager steps see uniform ids, the graph-replayed
+    ones power-law ids -- the row-wise capacity then has to grow after the
+    capture (eager rest of that step, re-capture)."""
     from tdfo_amd.data.synthetic import SyntheticCriteo
     from tdfo_amd.models.dlrm import DLRMConfig, DLRMTrainer
     from tdfo_amd.parallel.dist import get_info
@@ -27,15 +31,18 @@ def _worker(rank, world, Bk, strategy, graph, rw_comm, emb_opt="rowwise_adagrad"
     dev = get_info().device if world > 1 else torch.device("cuda", 0)
     cfg = DLRMConfig(embedding_dim=64, table_rows=ROWS, bottom=[128, 64], top=[128, 64, 1],
                      dense_opt="sgd", dense_lr=0.05, emb_lr=0.05, sharding=strategy,
-                     pooling=POOL, rw_comm=rw_comm, emb_opt=emb_opt, pipeline=pipeline)
+                     pooling=POOL, rw_comm=rw_comm, emb_opt=emb_opt, pipeline=pipeline,
+                     rw_capacity=rw_capacity)
     tr = DLRMTrainer(cfg, Bk, dev, group=get_info().group, rank=rank, world_size=world)
     g = torch.Generator().manual_seed(5)
     for t, r in enumerate(ROWS):
         tr.emb.set_table_weight(t, torch.randn(r, 64, generator=g) * 0.1)
     data = SyntheticCriteo(ROWS, B * 2, pooling=POOL, device="cpu", seed=9)
+    skew = SyntheticCriteo(ROWS, B * 2, pooling=POOL, device="cpu", seed=9, stream=1, dist=dist,
+                           zipf_alpha=alpha)
     batches = []
-    for _ in range(STEPS + 3):
-        dense, ids, label = data.next()
+    for i in range(STEPS + 3):
+        dense, ids, label = (data if i < 2 else skew).next()
         parts, off = [], 0
         for t, Lt in enumerate(POOL):
             n = B * 2 * Lt
@@ -71,8 +78,10 @@ def _worker(rank, world, Bk, strategy, graph, rw_comm, emb_opt="rowwise_adagrad"
     for t in range(len(ROWS)):
         r = tr.emb.get_table_weight(t)
         if r is not None:
-            tabs[t] = (r[0], tr.emb.table_cols(t)[0], r[1].detach().cpu().clone())
-    return tr.fp.p.detach().cpu().clone(), tabs, loss
+            tabs[t] = ((r[0].start, r[0].stop, r[0].step), tr.emb.table_cols(t)[0],
+                       r[1].detach().cpu().clone())
+    grows = tr.emb.rw_grows if tr.emb.rw_tables else 0
+    return tr.fp.p.detach().cpu().clone(), tabs, loss, grows
 
 
 @pytest.fixture(scope="module")
@@ -80,12 +89,51 @@ def single():
     """One process stepping the 2x batch (table-wise at world 1)."""
     cache = {}
 
-    def get(emb_opt: str):
-        if emb_opt not in cache:
-            cache[emb_opt] = run_distributed(_worker, 1, 2 * B, "table_wise", True, "fp32", emb_opt,
-                                             device="cuda")[0]
-        return cache[emb_opt]
+    def get(emb_opt: str, dist: str = "uniform", alpha: float = 1.05):
+        key = (emb_opt, dist, alpha)
+        if key not in cache:
+            cache[key] = run_distributed(_worker, 1, 2 * B, "table_wise", True, "fp32", emb_opt,
+                                         False, dist, alpha, device="cuda")[0][:3]
+        return cache[key]
     return get
+
+
+def _check(multi, ref, tol):
+    p1, tabs1, loss1 = ref
+    loss = sum(m[2] for m in multi)
+    assert abs(loss - loss1) / abs(loss1) < tol, (loss, loss1)
+    for rank, m in enumerate(multi):
+        p, tabs = m[0], m[1]
+        assert torch.allclose(p, p1, atol=tol, rtol=tol), (rank, float((p - p1).abs().max()))
+        for t, (lo, c0, w) in tabs.items():
+            ref_w = tabs1[t][2][slice(*lo)][:, c0:c0 + w.shape[1]]
+            assert torch.allclose(w, ref_w, atol=tol, rtol=tol), (rank, t,
+                                                                   float((w - ref_w).abs().max()))
+
+
+@pytest.mark.parametrize("strategy,pipeline", [("table_wise", True), ("row_wise", True),
+                                               ("auto", True), ("auto", False)])
+def test_four_ranks_match_one_process(strategy, pipeline, single):
+    """The W >= 3 paths together on the real kernels: 4 ranks sharing cuda:0
+    (uneven table-wise plans, the radix-sorted owner backward, W-run
+    layouts, row-wise at W = 4), staged hipGraphs, pipelined input dist."""
+    multi = run_distributed(_worker, 4, B // 2, strategy, True, "fp32", "rowwise_adagrad", pipeline,
+                            device="cuda", timeout=600)
+    _check(multi, single("rowwise_adagrad"), 3e-3)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("alpha", [1.05, 1.2])
+def test_zipf_row_wise_grows_capacity_after_capture(world, alpha, single):
+    """Power-law ids after the capture (initial capacity 0.3 x n/W): the
+    capacity check grows the row-wise segments inside the exchange stage, the
+    rest of that step runs eagerly and the stages are re-captured; the result
+    equals one process and no lookup is dropped (pop_loss raises otherwise)."""
+    multi = run_distributed(_worker, world, 2 * B // world, "row_wise", True, "fp32",
+                            "rowwise_adagrad", False, "zipf", alpha, 0.3, device="cuda",
+                            timeout=600)
+    assert all(m[3] > 0 for m in multi)
+    _check(multi, single("rowwise_adagrad", "zipf", alpha), 3e-3)
 
 
 # Column-wise keeps one row-wise Adagrad state per column block (as TorchRec CW
@@ -107,10 +155,10 @@ def test_two_ranks_match_one_process(strategy, graph, rw_comm, emb_opt, single):
     loss = multi[0][2] + multi[1][2]
     assert abs(loss - loss1) / abs(loss1) < tol, (loss, loss1)
     for rank in range(2):
-        p, tabs, _ = multi[rank]
+        p, tabs = multi[rank][0], multi[rank][1]
         assert torch.allclose(p, p1, atol=tol, rtol=tol), (rank, float((p - p1).abs().max()))
         for t, (lo, c0, w) in tabs.items():
-            ref_w = tabs1[t][2][lo:lo + w.shape[0], c0:c0 + w.shape[1]]
+            ref_w = tabs1[t][2][slice(*lo)][:, c0:c0 + w.shape[1]]
             assert torch.allclose(w, ref_w, atol=tol, rtol=tol), (rank, t,
                                                                    float((w - ref_w).abs().max()))
 
@@ -131,8 +179,8 @@ def test_two_ranks_pipelined_input_dist(strategy, rw_comm, pipe_lookup, single, 
     loss = multi[0][2] + multi[1][2]
     assert abs(loss - loss1) / abs(loss1) < tol, (loss, loss1)
     for rank in range(2):
-        p, tabs, _ = multi[rank]
+        p, tabs = multi[rank][0], multi[rank][1]
         assert torch.allclose(p, p1, atol=tol, rtol=tol), (rank, float((p - p1).abs().max()))
         for t, (lo, c0, w) in tabs.items():
-            ref_w = tabs1[t][2][lo:lo + w.shape[0], c0:c0 + w.shape[1]]
+            ref_w = tabs1[t][2][slice(*lo)][:, c0:c0 + w.shape[1]]
             assert torch.allclose(w, ref_w, atol=tol, rtol=tol), (rank, t)

@@ -89,7 +89,7 @@ def _ckpt_worker(rank, world, path, strategy, action, chunk_bytes):
                                  chunk_bytes=chunk_bytes) == 3
     out = {"dense": {k: v.clone() for k, v in tr.dense_state().items()}, "pieces": []}
     for p in sharded_ckpt.local_pieces(tr.emb):
-        out["pieces"].append((p["table"], p["lo"], p["c0"], p["weight"].clone(),
+        out["pieces"].append((p["table"], p["lo"], p["step"], p["c0"], p["weight"].clone(),
                               p["states"]["state1"].clone()))
     return out
 
@@ -98,10 +98,11 @@ def _assemble(res, rows, D=16):
     full = {t: torch.full((r, D), float("nan")) for t, r in enumerate(rows)}
     st = {t: torch.full((r, D), float("nan")) for t, r in enumerate(rows)}
     for r in res:
-        for t, lo, c0, w, s1 in r["pieces"]:
-            full[t][lo:lo + w.shape[0], c0:c0 + w.shape[1]] = w
-            st[t][lo:lo + w.shape[0], c0:c0 + w.shape[1]] = (s1[:, None] if s1.dim() == 1
-                                                             else s1)
+        for t, lo, step, c0, w, s1 in r["pieces"]:
+            # (round-robin row-wise shards: rows lo, lo + step, ...)
+            full[t][lo::step][: w.shape[0], c0:c0 + w.shape[1]] = w
+            st[t][lo::step][: w.shape[0], c0:c0 + w.shape[1]] = (s1[:, None] if s1.dim() == 1
+                                                                 else s1)
     return full, st
 
 

@@ -57,7 +57,7 @@ def _emb_worker(rank, world, strategy, B, L, dp_dense_max_bytes=256 << 20):
     for t in range(len(ROWS)):
         r = emb.get_table_weight(t)
         if r is not None:
-            shards[t] = (r[0], emb.table_cols(t)[0], r[1].clone())
+            shards[t] = ((r[0].start, r[0].stop, r[0].step), emb.table_cols(t)[0], r[1].clone())
     return feats, d_recv, shards, [list(emb.slot_off), list(emb.slot_stride)]
 
 
@@ -93,25 +93,27 @@ def test_sharded_embedding_fwd_bwd(strategy, world, dp_dense):
                     new[t][i] -= 0.5 * gb[b]
     for rank in range(world):
         for t, (lo, c0, w) in res[rank][2].items():
-            exp = new[t][lo:lo + w.shape[0], c0:c0 + w.shape[1]]
+            exp = new[t][slice(*lo)][:, c0:c0 + w.shape[1]]
             assert torch.allclose(w, exp, atol=1e-2), (rank, t)
 
 
 def _dlrm_worker(rank, world, B, steps, strategy, emb_opt="rowwise_adagrad", rw_comm="fp32",
-                 pipeline=False, dense_comm="fp32"):
+                 pipeline=False, dense_comm="fp32", dist="uniform", alpha=1.05, rw_capacity=1.25):
     from tdfo_amd.data.synthetic import SyntheticCriteo
     from tdfo_amd.models.dlrm import DLRMConfig, DLRMTrainer
     from tdfo_amd.parallel.dist import get_info
 
     cfg = DLRMConfig(embedding_dim=32, table_rows=ROWS, bottom=[64, 32], top=[64, 32, 1],
                      dense_lr=1e-2, emb_lr=0.05, sharding=strategy, pooling=[1, 2, 1, 1, 1],
-                     emb_opt=emb_opt, rw_comm=rw_comm, pipeline=pipeline, dense_comm=dense_comm)
+                     emb_opt=emb_opt, rw_comm=rw_comm, pipeline=pipeline, dense_comm=dense_comm,
+                     rw_capacity=rw_capacity)
     tr = DLRMTrainer(cfg, B, "cpu", group=get_info().group, rank=rank, world_size=world)
     assert tr.pipeline == (pipeline and world > 1)
     g = torch.Generator().manual_seed(5)
     for t, r in enumerate(ROWS):
         tr.emb.set_table_weight(t, torch.randn(r, 32, generator=g) * 0.1)
-    data = SyntheticCriteo(ROWS, B * world, pooling=cfg.pooling, device="cpu", seed=9)
+    data = SyntheticCriteo(ROWS, B * world, pooling=cfg.pooling, device="cpu", seed=9, dist=dist,
+                           zipf_alpha=alpha)
 
     def local(batch):
         dense, ids, label = batch
@@ -137,8 +139,10 @@ def _dlrm_worker(rank, world, B, steps, strategy, emb_opt="rowwise_adagrad", rw_
     for t in range(len(ROWS)):
         r = tr.emb.get_table_weight(t)
         if r is not None:
-            tabs[t] = (r[0], tr.emb.table_cols(t)[0], r[1].clone())
-    return tr.fp.p.clone(), tabs
+            tabs[t] = ((r[0].start, r[0].stop, r[0].step), tr.emb.table_cols(t)[0], r[1].clone())
+    grows = tr.emb.rw_grows if tr.emb.rw_tables else 0
+    tr.pop_loss()                               # raises on every rank if a lookup was dropped
+    return tr.fp.p.clone(), tabs, grows
 
 
 @pytest.mark.parametrize("strategy", ["table_wise", "row_wise", "data_parallel", "column_wise",
@@ -150,12 +154,12 @@ def test_dlrm_data_parallel_matches_single_process(strategy):
     opt = "adagrad" if strategy == "column_wise" else "rowwise_adagrad"
     multi = run_distributed(_dlrm_worker, 2, B, steps, strategy, opt)
     single = run_distributed(_dlrm_worker, 1, 2 * B, steps, "table_wise", opt)[0]
-    p1, tabs1 = single
+    p1, tabs1, _ = single
     for rank in range(2):
-        p, tabs = multi[rank]
+        p, tabs, _ = multi[rank]
         assert torch.allclose(p, p1, atol=2e-4), (rank, (p - p1).abs().max())
         for t, (lo, c0, w) in tabs.items():
-            ref = tabs1[t][2][lo:lo + w.shape[0], c0:c0 + w.shape[1]]
+            ref = tabs1[t][2][slice(*lo)][:, c0:c0 + w.shape[1]]
             assert torch.allclose(w, ref, atol=2e-4), (rank, t, (w - ref).abs().max())
 
 
@@ -172,8 +176,8 @@ def test_dlrm_pipelined_input_dist_is_exact(strategy, pipe_lookup, monkeypatch):
     plain = run_distributed(_dlrm_worker, 2, B, steps, strategy, "rowwise_adagrad", "fp32", False)
     piped = run_distributed(_dlrm_worker, 2, B, steps, strategy, "rowwise_adagrad", "fp32", True)
     for rank in range(2):
-        p0, tabs0 = plain[rank]
-        p1, tabs1 = piped[rank]
+        p0, tabs0, _ = plain[rank]
+        p1, tabs1, _ = piped[rank]
         assert torch.equal(p0, p1), (rank, (p0 - p1).abs().max())
         assert tabs0.keys() == tabs1.keys()
         for t in tabs0:
@@ -190,8 +194,8 @@ def test_dlrm_bf16_dense_allreduce_close_to_fp32():
     b16 = run_distributed(_dlrm_worker, 2, B, steps, "table_wise", "rowwise_adagrad", "fp32",
                           False, "bf16")
     for rank in range(2):
-        p0, _ = f32[rank]
-        p1, _ = b16[rank]
+        p0 = f32[rank][0]
+        p1 = b16[rank][0]
         assert not torch.equal(p0, p1)                     # the wire format is really bf16
         d = (p0 - p1).abs()
         # AdamW (lr 1e-2) normalises each update, so elements whose gradient
@@ -199,3 +203,27 @@ def test_dlrm_bf16_dense_allreduce_close_to_fp32():
         # by 3 steps x lr and require the bulk to agree closely
         assert float(d.max()) <= 3e-2 and float(d.mean()) < 1e-3, (float(d.max()), float(d.mean()))
     assert torch.equal(b16[0][0], b16[1][0])               # replicas stay identical
+
+
+@pytest.mark.parametrize("strategy,world", [("row_wise", 2), ("row_wise", 3), ("auto", 2)])
+@pytest.mark.parametrize("alpha", [1.05, 1.2])
+def test_dlrm_zipf_ids_match_single_process(strategy, world, alpha):
+    """Power-law ids (the hot head at the low ids, as in frequency-ordered
+    Criteo): the row-wise exchange deals rows round-robin and grows its
+    per-owner capacity before any segment would overflow (started here at a
+    deliberately small 0.3 x n/W), so training equals one process exactly
+    and no lookup is dropped (pop_loss raises on every rank otherwise)."""
+    B, steps = 8, 3
+    multi = run_distributed(_dlrm_worker, world, B, steps, strategy, "rowwise_adagrad", "fp32",
+                            False, "fp32", "zipf", alpha, 0.3)
+    single = run_distributed(_dlrm_worker, 1, world * B, steps, "table_wise", "rowwise_adagrad",
+                             "fp32", False, "fp32", "zipf", alpha)[0]
+    p1, tabs1, _ = single
+    if strategy == "row_wise":
+        assert all(m[2] > 0 for m in multi)      # the capacity really had to grow
+    for rank in range(world):
+        p, tabs, _ = multi[rank]
+        assert torch.allclose(p, p1, atol=2e-4), (rank, (p - p1).abs().max())
+        for t, (lo, c0, w) in tabs.items():
+            ref = tabs1[t][2][slice(*lo)][:, c0:c0 + w.shape[1]]
+            assert torch.allclose(w, ref, atol=2e-4), (rank, t, (w - ref).abs().max())
