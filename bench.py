@@ -41,9 +41,12 @@ def parse(argv=None):
     ap.add_argument("--rows", default="1tb", choices=["1tb", "kaggle", "tiny", "gt1tb"])
     ap.add_argument("--model", default="dlrm", choices=["dlrm", "dcnv2"])
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--overlap", nargs="?", const="all", default="",
-                    help="side streams: 'all' (wgrads + embedding work) or 'wgrad'")
-    ap.add_argument("--pool", type=int, default=8, help="pre-generated device batches")
+    ap.add_argument("--data", default="fresh", choices=["fresh", "pool", "host"],
+                    help="fresh: a new batch every step from the one-launch device generator "
+                         "on a side stream (default); pool: cycle --pool pre-generated device "
+                         "batches; host: the C++ host generator through pinned slots and a "
+                         "copy-stream H2D prefetcher")
+    ap.add_argument("--pool", type=int, default=8, help="--data pool: batches in the pool")
     ap.add_argument("--dist", default="uniform", choices=["uniform", "zipf"])
     ap.add_argument("--sharding", default="auto",
                     choices=["auto", "table_wise", "row_wise", "column_wise", "data_parallel"])
@@ -52,10 +55,11 @@ def parse(argv=None):
     ap.add_argument("--no-pipeline", action="store_true",
                     help="N > 1: exchange each batch's ids inside its own step instead of "
                          "during the previous step's dense update")
-    ap.add_argument("--host-data", action="store_true",
-                    help="batches from the C++ host generator through pinned slots and a "
-                         "copy-stream H2D prefetcher (instead of a pool of device batches)")
-    return ap.parse_args(argv)
+    ap.add_argument("--host-data", action="store_true", help="same as --data host")
+    args = ap.parse_args(argv)
+    if args.host_data:
+        args.data = "host"
+    return args
 
 
 # Stock PyTorch-ROCm eager DLRM (nn.EmbeddingBag + nn.Linear, bf16 autocast,
@@ -132,26 +136,28 @@ def main(argv=None):
     pipe = world_env > 1 and not args.no_pipeline
     if args.model == "dlrm":
         cfg = DLRMConfig(table_rows=list(rows), sharding=args.sharding, pipeline=pipe,
-                         dense_comm=args.dense_comm,
-                         overlap=(args.overlap if args.overlap == 'wgrad' else bool(args.overlap)))
+                         dense_comm=args.dense_comm)
     else:
         cfg = DLRMConfig(table_rows=list(rows), interaction="dcn", pooling=list(MLPERF_MULTIHOT),
                          top=[1024, 1024, 512, 256, 1], sharding=args.sharding, pipeline=pipe,
-                         dense_comm=args.dense_comm,
-                         overlap=(args.overlap if args.overlap == 'wgrad' else bool(args.overlap)))
+                         dense_comm=args.dense_comm)
     B = args.batch
     t0 = time.time()
-    if args.host_data:
-        # the host data plane orders its H2D on every input stream and
+    if args.data in ("host", "fresh"):
+        # a streamed data source orders its batch on every input stream and
         # releases a slot after all of them: a third (ids) stream ties the
         # slot to the sort and stalls the prefetch (0.604 vs 0.470 ms/step)
-        os.environ.setdefault("TDFO_IDS_STREAM", "0")
+        cfg.ids_stream = False
     tr = DLRMTrainer(cfg, B, info.device, group=info.group, rank=info.rank, world_size=world)
-    if args.host_data:
+    pool = pf = None
+    if args.data == "host":
         from tdfo_amd.data.prefetch import host_prefetcher
         pf = host_prefetcher(cfg.table_rows, B, info.device, pooling=cfg.pooling_factors(),
                              seed=1, rank=info.rank, dist=args.dist, threads=8)
-        pool = None
+    elif args.data == "fresh":
+        from tdfo_amd.data.synthetic import DeviceSyntheticStream
+        pf = DeviceSyntheticStream(cfg.table_rows, B, info.device, pooling=cfg.pooling_factors(),
+                                   seed=1, rank=info.rank, dist=args.dist)
     else:
         data = SyntheticCriteo(cfg.table_rows, B, pooling=cfg.pooling_factors(),
                                device=info.device, seed=1, rank=info.rank, dist=args.dist)
@@ -163,8 +169,8 @@ def main(argv=None):
     def feed(i):
         """Hand batch i to the trainer (pipelined: as the batch the next step
         runs on -- this step loads it after its embedding update)."""
-        if pool is None:                       # host data plane: generation + H2D overlapped
-            # the H2D is ordered on every stream that reads the batch
+        if pool is None:                       # streamed: generation (+ H2D) overlapped
+            # the batch is ordered on every stream that reads it
             batch, slot = pf.next(streams=None if tr.pipeline else tr.input_streams())
         else:
             batch, slot = pool[i % len(pool)], None
@@ -216,8 +222,13 @@ def main(argv=None):
                           "dense_tflops": round(cfg.dense_flops_per_example() * value / 1e12, 1),
                           "sol": {k: round(v, 4) for k, v in sol.items()}}),
               file=sys.stderr)
+        mname = "DLRM" if args.model == "dlrm" else "DCN-v2"
+        rname = {"1tb": "1TB", "kaggle": "Kaggle", "gt1tb": "gt1TB", "tiny": "tiny"}[args.rows]
+        src = {"fresh": "a fresh batch per step from the on-device generator (side stream)",
+               "pool": f"a pool of {args.pool} pre-generated device batches, cycled",
+               "host": "C++ host generator + pinned copy-stream H2D"}[args.data]
         print(json.dumps({
-            "metric": "examples/sec (whole node) DLRM on Criteo-1TB-shaped synthetic",
+            "metric": f"examples/sec (whole node) {mname} on Criteo-{rname}-shaped synthetic",
             "value": round(value, 1), "unit": "examples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
             "higher_is_better": True, "scaling": "weak",
@@ -227,10 +238,9 @@ def main(argv=None):
             "sol_ms": round(sol["sol_ms"], 4),
             "frac_of_sol": round(sol["sol_ms"] / ms, 3),
             "dtype": "bf16",
-            "data": f"synthetic (Criteo-{args.rows}-shaped, {args.dist} ids, random-init embeddings"
-                    + (", C++ host generator + pinned copy-stream H2D)" if args.host_data
-                       else ", pre-generated device batches)"),
-            "config": {"model": "DLRM" if args.model == "dlrm" else "DCN-v2",
+            "data": f"synthetic (Criteo-{args.rows}-shaped, {args.dist} ids, random-init "
+                    f"embeddings, {src})",
+            "config": {"model": mname,
                        "global_batch": B * world, "seq_len": None,
                        "parallelism": parallelism(tr.plan, world),
                        "tables": f"criteo-{args.rows}", "embedding_dim": cfg.embedding_dim,

@@ -439,15 +439,6 @@ void rank_metrics(const Tensor& h, const Tensor& W, const Tensor& bias, const Te
 // memory-bound, many-block kernels leave CUs to the latency-bound GEMMs.
 // Returned as the raw handle for torch.cuda.ExternalStream (never destroyed:
 // one per trainer).
-int64_t cu_masked_stream(at::IntArrayRef mask_words) {
-  TORCH_CHECK(!mask_words.empty() && mask_words.size() <= 64, "cu_masked_stream: 1..64 words");
-  std::vector<uint32_t> m(mask_words.size());
-  for (size_t i = 0; i < m.size(); ++i) m[i] = (uint32_t)mask_words[i];
-  hipStream_t st = nullptr;
-  const hipError_t e = hipExtStreamCreateWithCUMask(&st, (uint32_t)m.size(), m.data());
-  TORCH_CHECK(e == hipSuccess, "hipExtStreamCreateWithCUMask: ", hipGetErrorString(e));
-  return (int64_t)(uintptr_t)st;
-}
 
 // ---------------------------------------------------------- batch gather
 void gather_columns(at::TensorList src, const c10::optional<Tensor>& idx, int64_t row0, int64_t n,
@@ -610,47 +601,7 @@ void graph_exec_destroy(int64_t ex) {
 }
 
 // ------------------------------------------------------- fused MLP
-bool mlp3_supported(int64_t k0, int64_t n0, int64_t n1, int64_t n2) {
-  return tdfo::mlp3_fwd_supported((int)k0, (int)n0, (int)n1, (int)n2);
-}
 
-void mlp3_fwd(const Tensor& x, const Tensor& w0, const Tensor& w1, const Tensor& w2,
-              const c10::optional<Tensor>& b0, const c10::optional<Tensor>& b1,
-              const c10::optional<Tensor>& b2, const Tensor& y0, const Tensor& y1,
-              const Tensor& y2) {
-  const Tensor* ws[3] = {&w0, &w1, &w2};
-  const c10::optional<Tensor>* bs[3] = {&b0, &b1, &b2};
-  const Tensor* ys[3] = {&y0, &y1, &y2};
-  check_dev(x, "x");
-  check_2d_rowmajor(x, "x");
-  const int64_t B = x.size(0);
-  tdfo::Mlp3Args a{};
-  a.x = bf16_ptr(x); a.ldx = x.stride(0); a.B = (int)B;
-  a.k[0] = (int)x.size(1);
-  for (int l = 0; l < 3; ++l) {
-    check_dev(*ws[l], "w"); check_2d_rowmajor(*ws[l], "w");
-    check_dev(*ys[l], "y"); check_2d_rowmajor(*ys[l], "y");
-    const int64_t N = ws[l]->size(0), K = ws[l]->size(1);
-    TORCH_CHECK(K == a.k[l], "mlp3_fwd: layer ", l, " input width ", K, " vs ", a.k[l]);
-    TORCH_CHECK(ys[l]->size(0) == B && ys[l]->size(1) == N, "mlp3_fwd: output shape");
-    for (const Tensor* t : {ws[l], ys[l]})
-      TORCH_CHECK(t->stride(0) % 8 == 0 && aligned16(t->data_ptr()), "mlp3_fwd: 16-B aligned rows");
-    a.w[l] = bf16_ptr(*ws[l]); a.ldw[l] = ws[l]->stride(0);
-    a.y[l] = bf16_mut(*ys[l]); a.ldy[l] = ys[l]->stride(0);
-    a.k[l + 1] = (int)N;
-    if (*bs[l]) {
-      const Tensor& b = **bs[l];
-      check_dev(b, "bias");
-      TORCH_CHECK(b.scalar_type() == at::kFloat && b.dim() == 1 && b.numel() == N,
-                  "mlp3_fwd: bias fp32 [N] (any stride)");
-      a.bias[l] = b.data_ptr<float>(); a.bstride[l] = b.stride(0);
-    }
-  }
-  TORCH_CHECK(x.stride(0) % 8 == 0 && aligned16(x.data_ptr()), "mlp3_fwd: x rows 16-B aligned");
-  TORCH_CHECK(tdfo::mlp3_fwd_supported(a.k[0], a.k[1], a.k[2], a.k[3]), "mlp3_fwd: widths ",
-              a.k[0], "/", a.k[1], "/", a.k[2], "/", a.k[3], " unsupported");
-  tdfo::mlp3_fwd(a, cur_stream());
-}
 
 // ------------------------------------------------------------ radix sort
 std::tuple<Tensor, Tensor> sort_pairs(const Tensor& keys, const Tensor& vals, int64_t key_bits) {
@@ -1001,6 +952,37 @@ void batch_load(const Tensor& dense, const Tensor& x0, const Tensor& ids, const 
                    cur_stream());
 }
 
+// ------------------------------------------------------- synthetic data
+void synth_criteo(int64_t seed, int64_t rank, int64_t batch_index, int64_t B,
+                  const Tensor& rows, const Tensor& pooling, const Tensor& base, int64_t dist,
+                  double alpha, const Tensor& w_dense, const Tensor& table_bias,
+                  const Tensor& dense, const Tensor& ids, const Tensor& label) {
+  check_dev(dense, "dense");
+  const int64_t T = rows.numel();
+  TORCH_CHECK(rows.scalar_type() == at::kLong && base.scalar_type() == at::kLong &&
+              pooling.scalar_type() == at::kInt && pooling.numel() == T && base.numel() == T &&
+              rows.is_contiguous() && base.is_contiguous() && pooling.is_contiguous(),
+              "synth_criteo: rows/base int64[T], pooling int32[T]");
+  TORCH_CHECK(dense.scalar_type() == at::kFloat && dense.is_contiguous() && dense.dim() == 2 &&
+              dense.size(0) == B, "synth_criteo: dense fp32 [B, nd]");
+  TORCH_CHECK(w_dense.scalar_type() == at::kFloat && w_dense.numel() == dense.size(1) &&
+              table_bias.scalar_type() == at::kFloat && table_bias.numel() == T * 64 &&
+              w_dense.is_contiguous() && table_bias.is_contiguous(), "synth_criteo: teacher");
+  TORCH_CHECK(ids.scalar_type() == at::kLong && ids.is_contiguous() &&
+              label.scalar_type() == at::kFloat && label.numel() == B, "synth_criteo: outputs");
+  for (const Tensor* t : {&rows, &pooling, &base, &w_dense, &table_bias, &ids, &label})
+    TORCH_CHECK(t->device() == dense.device(), "synth_criteo: one device");
+  tdfo::SynthArgs a{};
+  a.seed = (uint64_t)seed; a.rank = (int)rank; a.batch_index = batch_index;
+  a.B = (int)B; a.num_dense = (int)dense.size(1); a.T = (int)T;
+  a.rows = rows.data_ptr<int64_t>(); a.pooling = pooling.data_ptr<int32_t>();
+  a.base = base.data_ptr<int64_t>(); a.dist = (int)dist; a.alpha = alpha;
+  a.w_dense = w_dense.data_ptr<float>(); a.table_bias = table_bias.data_ptr<float>();
+  a.dense = dense.data_ptr<float>(); a.ids = ids.data_ptr<int64_t>();
+  a.label = label.data_ptr<float>();
+  tdfo::synth_criteo(a, cur_stream());
+}
+
 // ------------------------------------------------------------ loss etc.
 void head_bce(const Tensor& H, const Tensor& w, const Tensor& b, const Tensor& label,
               double inv_n, bool relu_mask, const Tensor& logits, const Tensor& dH,
@@ -1206,9 +1188,6 @@ TORCH_LIBRARY(tdfo, m) {
         "Tensor(c!)? out2=None, int ldc32=0, int csum_col=-1) -> ()");
   m.def("radix_sort_sep_hist(int v) -> int",
         [](int64_t v) { return (int64_t)tdfo::radix_sort_sep_hist((int)v); });
-  m.def("mlp3_supported(int k0, int n0, int n1, int n2) -> bool", mlp3_supported);
-  m.def("mlp3_fwd(Tensor x, Tensor w0, Tensor w1, Tensor w2, Tensor? b0, Tensor? b1, "
-        "Tensor? b2, Tensor(a!) y0, Tensor(b!) y1, Tensor(c!) y2) -> ()");
   m.def("sync_event_create(int mode) -> int", sync_event_create);
   m.def("sync_event_record(int e) -> ()", sync_event_record);
   m.def("sync_event_wait(int e) -> ()", sync_event_wait);
@@ -1254,7 +1233,6 @@ TORCH_LIBRARY(tdfo, m) {
         "Tensor rstd, float rate, int seed, Tensor? step, Tensor(a!) dx, Tensor(b!) part, "
         "Tensor(c!) out3) -> ()");
   m.def("rank_metrics(Tensor h, Tensor W, Tensor bias, Tensor cand, int[] ks, Tensor(a!) out) -> ()");
-  m.def("cu_masked_stream(int[] mask_words) -> int", cu_masked_stream);
   m.def("layernorm_parts(int M) -> int", [](int64_t M) { return (int64_t)tdfo::layernorm_parts(M); });
   m.def("gather_columns(Tensor[] src, Tensor? idx, int row0, int n, Tensor(a!)[] dst, int[] dst_stride) -> ()");
   m.def("concat_features(Tensor dense, Tensor emb, int[] off, int[] stride, int F, int D, "
@@ -1303,6 +1281,9 @@ TORCH_LIBRARY(tdfo, m) {
   m.def("check_finite(Tensor g, Tensor(a!) found) -> ()");
   m.def("sort_pairs(Tensor keys, Tensor vals, int key_bits) -> (Tensor, Tensor)");
   m.def("cast_bf16(Tensor x, Tensor(a!) y) -> ()");
+  m.def("synth_criteo(int seed, int rank, int batch_index, int B, Tensor rows, Tensor pooling, "
+        "Tensor base, int dist, float alpha, Tensor w_dense, Tensor table_bias, Tensor(a!) dense, "
+        "Tensor(b!) ids, Tensor(c!) label) -> ()");
   m.def("batch_load(Tensor dense, Tensor(a!) x0, Tensor ids, Tensor(b!) ids_dst, Tensor label, "
         "Tensor(c!) label_dst) -> ()");
   m.def("head_bce(Tensor H, Tensor w, Tensor b, Tensor label, float inv_n, bool relu_mask, "
@@ -1324,7 +1305,6 @@ TORCH_LIBRARY(tdfo, m) {
 
 TORCH_LIBRARY_IMPL(tdfo, CUDA, m) {
   m.impl("gemm", gemm);
-  m.impl("mlp3_fwd", mlp3_fwd);
   m.impl("attention_fwd", attention_fwd);
   m.impl("encoder_layer_fwd", encoder_layer_fwd);
   m.impl("encoder_layer_bwd", encoder_layer_bwd);
@@ -1337,6 +1317,7 @@ TORCH_LIBRARY_IMPL(tdfo, CUDA, m) {
   m.impl("gather_columns", gather_columns);
   m.impl("concat_features", concat_features);
   m.impl("batch_load", batch_load);
+  m.impl("synth_criteo", synth_criteo);
   m.impl("split_features", split_features);
   m.impl("cross_bwd", cross_bwd);
   m.impl("interaction_fwd", interaction_fwd);

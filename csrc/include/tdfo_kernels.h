@@ -47,21 +47,6 @@ int gemm_pairing(int v);
 // Returns the previous policy.
 int gemm_policy(int p);
 
-// ------------------------------------------------- fused bottom MLP ----
-// y_l = relu(y_{l-1} W_l^T + b_l) for three layers in one launch (32 samples
-// per block, activations in LDS). k = {K0, N0, N1, N2}; bias[l] == nullptr:
-// the bias is inside K (augmented input column). Every y_l is written.
-struct Mlp3Args {
-  const uint16_t* x; int64_t ldx;
-  const uint16_t* w[3]; int64_t ldw[3];
-  const float* bias[3]; int64_t bstride[3];
-  uint16_t* y[3]; int64_t ldy[3];
-  int B;
-  int k[4];
-};
-bool mlp3_fwd_supported(int k0, int n0, int n1, int n2);
-void mlp3_fwd(const Mlp3Args& a, hipStream_t s);
-
 // ------------------------------------------------------ interaction ----
 // DLRM dot interaction over F <= 32 features of width D (one of 16/32/64/128).
 // Feature 0 comes from `dense` ([B, ld_dense]); feature f >= 1 from
@@ -179,6 +164,22 @@ void embedding_bwd_apply(const EmbBwdArgs& a, hipStream_t s);
 // Dense optimizer step over rows [0, rows) of W from a dense fp32 gradient
 // [rows, D] (a.opt, a.state1/2, a.hyper, eps/betas/wd as for the backward).
 void embedding_dense_update(const EmbBwdArgs& a, int64_t rows, const float* grad, hipStream_t s);
+
+// --------------------------------------------------- synthetic data ----
+// (synthetic.hip) One fresh synthetic Criteo batch (device twin of
+// csrc/data/synthetic.cpp): dense [B, num_dense] fp32, ids table-major (table
+// t at base[t], B * pooling[t] ids; dist 0 uniform, 1 Zipf(alpha)), label [B].
+// rows / base int64[T], pooling int32[T], w_dense [num_dense], table_bias
+// [T, 64] all device-resident.
+struct SynthArgs {
+  uint64_t seed; int rank; int64_t batch_index;
+  int B, num_dense, T;
+  const int64_t* rows; const int* pooling; const int64_t* base;
+  int dist; double alpha;
+  const float* w_dense; const float* table_bias;
+  float* dense; int64_t* ids; float* label;
+};
+void synth_criteo(const SynthArgs& a, hipStream_t s);
 
 // --------------------------------------------------- row-wise shards ----
 // (rowwise.hip) Fixed-capacity row-wise exchange. meta (int64, device):

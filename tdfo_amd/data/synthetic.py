@@ -4,10 +4,13 @@ data / random-init embeddings").
 Dense features are log-normal-ish like log(1 + count) Criteo integers, ids
 are uniform (default) or Zipf-skewed per table, labels follow a fixed random
 logistic "teacher" over the dense features and a hash of the ids so the
-loss is learnable. ``SyntheticCriteo`` generates on the device (no host round
-trip); ``HostSyntheticCriteo`` is the multi-threaded C++ twin
+loss is learnable. ``SyntheticCriteo`` generates with torch ops (any device);
+``HostSyntheticCriteo`` is the multi-threaded C++ generator
 (csrc/data/synthetic.cpp, counter-based so every batch is reproducible
-independently) used for CPU runs and host-pipeline benchmarks.
+independently) used for CPU runs and host-pipeline benchmarks;
+``DeviceSyntheticStream`` is its one-launch HIP twin
+(csrc/kernels/synthetic.hip) that draws a fresh batch per training step on a
+side stream (the benchmark's default data source).
 """
 from __future__ import annotations
 
@@ -108,3 +111,75 @@ class HostSyntheticCriteo:
         out = self.batch(self.index)
         self.index += 1
         return out
+
+
+class DeviceSyntheticStream:
+    """Fresh synthetic batches generated on the GPU, one launch per batch, on
+    a side stream, into ``slots`` rotating device buffer sets; batch ``i`` is
+    the same pure function of (seed, rank, i) as ``HostSyntheticCriteo``'s
+    (bit-identical ids for uniform draws). Same contract as
+    ``prefetch.HostPrefetcher``: ``next(streams)`` -> ((dense, ids, label),
+    slot), ordered on every consumer stream; ``release(slot, streams)`` once
+    the consumer has enqueued its reads -- the slot is regenerated only after
+    they ran (device-side event waits on the generator stream)."""
+
+    def __init__(self, table_rows: Sequence[int], batch_size: int, device, num_dense: int = 13,
+                 pooling: Optional[Sequence[int]] = None, seed: int = 0, dist: str = "uniform",
+                 zipf_alpha: float = 1.05, rank: int = 0, stream: int = 0, slots: int = 3,
+                 start: int = 0):
+        from .. import ops
+        self.ops = ops
+        self.dev = torch.device(device)
+        assert self.dev.type == "cuda", "DeviceSyntheticStream runs on the GPU"
+        T = len(table_rows)
+        L = list(pooling) if pooling is not None else [1] * T
+        self.B, self.T = int(batch_size), T
+        self.rows = torch.tensor([int(r) for r in table_rows], dtype=torch.int64, device=self.dev)
+        self.pool_ = torch.tensor(L, dtype=torch.int32, device=self.dev)
+        base, acc = [], 0
+        for x in L:
+            base.append(acc)
+            acc += self.B * int(x)
+        self.base = torch.tensor(base, dtype=torch.int64, device=self.dev)
+        self.nnz = acc
+        self.seed = int(seed) + int(stream) * 1_000_003
+        self.rank, self.dist, self.alpha = int(rank), (1 if dist == "zipf" else 0), zipf_alpha
+        g = torch.Generator(device="cpu")
+        g.manual_seed(seed)   # the teacher of SyntheticCriteo / HostSyntheticCriteo
+        self.w_dense = (torch.randn(num_dense, generator=g) / num_dense ** 0.5).to(self.dev)
+        self.table_bias = (torch.randn(T, 64, generator=g) * 0.5).contiguous().to(self.dev)
+        self.S = int(slots)
+        self.bufs = [(torch.empty(self.B, num_dense, device=self.dev),
+                      torch.empty(self.nnz, dtype=torch.int64, device=self.dev),
+                      torch.empty(self.B, device=self.dev)) for _ in range(self.S)]
+        self.gs = torch.cuda.Stream(device=self.dev)
+        self.use_ev = [None] * self.S
+        self.i = int(start)
+
+    def generate(self, index: int, out):
+        dense, ids, label = out
+        self.ops.synth_criteo(self.seed, self.rank, index, self.B, self.rows, self.pool_,
+                              self.base, self.dist, self.alpha, self.w_dense, self.table_bias,
+                              dense, ids, label)
+
+    def next(self, streams=None):
+        j = self.i
+        self.i += 1
+        s = j % self.S
+        with torch.cuda.stream(self.gs):
+            for ue in (self.use_ev[s] or ()):
+                self.gs.wait_event(ue)          # the slot's previous batch has been consumed
+            self.generate(j, self.bufs[s])
+            ev = torch.cuda.Event()
+            ev.record(self.gs)
+        for st in (streams or [torch.cuda.current_stream(self.dev)]):
+            st.wait_event(ev)
+        return self.bufs[s], s
+
+    def release(self, slot: int, streams=None):
+        evs = []
+        for st in (streams or [torch.cuda.current_stream(self.dev)]):
+            e = torch.cuda.Event()
+            e.record(st)
+            evs.append(e)
+        self.use_ev[slot] = evs

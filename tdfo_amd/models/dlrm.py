@@ -23,9 +23,7 @@ once into a hipGraph and replayed (no tracing compiler):
 """
 from __future__ import annotations
 
-import contextlib
 import math
-import os
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
 
@@ -34,6 +32,7 @@ import torch.distributed as dist
 
 from ..utils.capture import graph_capture
 from .. import ops
+from .dlrm_streams import StreamGraphsMixin
 from ..sparse.planner import ShardingPlan, plan_sharding
 from ..sparse.sharded import ShardedEmbeddingBags
 from ..sparse.tables import EmbOptimConfig, TableConfig
@@ -83,16 +82,25 @@ class DLRMConfig:
     emb_lr: float = 0.01
     emb_eps: float = 1e-8
     sharding: str = "auto"                         # planner strategy
-    rw_capacity: float = 1.25                      # row-wise segment capacity (x n/W, +256)
+    rw_capacity: float = 1.25                      # initial row-wise segment capacity (x n/W);
+    #   grown on demand before any exchange would overflow
     rw_comm: str = "bf16"                          # row-wise reduce-scatter dtype (bf16 | fp32)
     dense_comm: str = "fp32"                       # dense-grad all-reduce dtype (fp32 | bf16:
     #   halves the bytes on xGMI; the sum of W bf16-rounded grads, as DDP's bf16 compress hook)
     pipeline: bool = False                         # W > 1: next batch's id exchange overlaps
     #   this step's dense update (input-dist pipelining; see DLRMTrainer.prime)
-    overlap: object = False                        # side streams (GPU): False | True (wgrads +
-    #   embedding work) | "wgrad" (weight grads only)
-    #   (measured 0.744 vs 0.728 ms/step on DLRM-1TB: the overlapped kernels
-    #   slow each other more than the concurrency saves; kept as an option)
+    pipeline_lookup: bool = True                   # pipelined: also the next batch's lookup +
+    #   pooled exchange in this step's tail (on the side stream)
+    defer_wgrad: Optional[bool] = None             # top / cross weight grads after the
+    #   interaction / cross backward (None: when W > 1, so the embedding-grad exchange
+    #   overlaps them; on one GPU the DCN-v2 update starved them: 2.606 vs 2.52 ms/step)
+    opt_placement: Optional[str] = None            # one GPU: "one_pass" (dense optimizer after
+    #   the bottom backward; DLRM default) | "split_main" (top part first, beside the
+    #   embedding update; DCN-v2 default)
+    composed_graphs: Optional[bool] = None         # one GPU: chain each stream's graphs with
+    #   in-graph event nodes (None: DLRM yes, DCN-v2 no)
+    ids_stream: Optional[bool] = None              # one GPU, composed graphs: copy the next
+    #   ids on a third stream behind the sort (None: with composed graphs)
     seed: int = 0
 
     @property
@@ -198,7 +206,7 @@ class Lin:
 # 64 elements keeps every activation / weight row 128-B aligned, so each 128-B
 # K chunk a GEMM stages is one cache line (an 8-element pad made 7 of 8 rows
 # straddle two lines: top1 fwd 28.2 vs 23.5 us, profiles/gemm_step_ab.md).
-WCOL_PAD = int(os.environ.get("TDFO_WCOL_PAD", "64"))
+WCOL_PAD = 64
 
 
 def make_lin(name: str, in_real: int, out: int) -> Lin:
@@ -208,12 +216,17 @@ def make_lin(name: str, in_real: int, out: int) -> Lin:
     return Lin(name, in_real, in_k, out, in_k, in_k + WCOL_PAD)
 
 
-class DLRMTrainer:
+
+
+class DLRMTrainer(StreamGraphsMixin):
     """Explicit-step DLRM/DCN-v2 trainer over a sharded embedding engine.
 
     ``batch_size`` is per rank (weak scaling). Works on CPU (torch reference
-    ops, gloo) and on MI355X (HIP kernels, RCCL); the step can be captured in
-    hipGraphs (whole step single-process, per compute stage multi-process).
+    ops, gloo) and on MI355X (HIP kernels, RCCL). The step is a fixed list of
+    compute stages and communication stages (``_stages``); it runs eagerly,
+    or captured: one process as per-stream hipGraphs (dlrm_streams.py) or one
+    whole-step graph, several processes as one graph per run of compute
+    stages with the RCCL exchanges issued eagerly between replays.
     """
 
     def __init__(self, cfg: DLRMConfig, batch_size: int, device, group=None, rank: int = 0,
@@ -221,6 +234,11 @@ class DLRMTrainer:
         self.cfg = cfg
         if cfg.dense_comm not in ("fp32", "bf16"):
             raise ValueError(f"dense_comm must be fp32 or bf16, got {cfg.dense_comm!r}")
+        if cfg.opt_placement not in (None, "one_pass", "split_main"):
+            raise ValueError(f"opt_placement must be one_pass or split_main, "
+                             f"got {cfg.opt_placement!r}")
+        if cfg.opt_placement is None:
+            cfg.opt_placement = "split_main" if cfg.interaction == "dcn" else "one_pass"
         self.B = B = int(batch_size)
         self.device = dev = torch.device(device)
         self.group = group
@@ -275,16 +293,8 @@ class DLRMTrainer:
         if world_size > 1:                            # replicated dense arch
             dist.broadcast(fp.p, src=0, group=group)
         fp.sync_bf16()
-        # Weight grads deferred past the interaction / cross-network backward
-        # (per-layer buffers: no reuse), so the embedding gradients -- which
-        # need only the dgrad chain -- exist earlier: multi-rank, their
-        # all-to-all overlaps the wgrads. On one GPU (TDFO_DEFER_WGRAD=1)
-        # DCN-v2's multi-hot embedding update would run beside its top + cross
-        # wgrads instead of after them: measured 2.606 vs 2.514-2.531 ms/step
-        # (the memory-bound update's many blocks starve the one-block-per-CU
-        # 256x128 wgrad GEMMs: 1.07 ms of them instead of 0.4), so off.
-        dflt = world_size > 1
-        self._defer_top_wgrad = os.environ.get("TDFO_DEFER_WGRAD", "1" if dflt else "0") == "1"
+        self._defer_top_wgrad = (world_size > 1 if cfg.defer_wgrad is None
+                                 else bool(cfg.defer_wgrad))
         # ------------------------------------------------------ buffers
         bf = torch.bfloat16
 
@@ -330,7 +340,6 @@ class DLRMTrainer:
         # step's early lookup rewrites it.
         self._x0_alias = False
         if (cfg.interaction == "dcn" and not self._defer_top_wgrad
-                and os.environ.get("TDFO_DCN_X0_ALIAS", "1") == "1"
                 and self.emb.alias_pooled(self.dcn_x[0], self.dcn_dx[0], D)):
             self._x0_alias = True
             self.h_out = self.dcn_x[0][:, :D]
@@ -338,58 +347,31 @@ class DLRMTrainer:
         self.nparts = ops.head_parts(B)
         self.head_part = z(self.nparts * (self.head_k + 2), dt=torch.float32)
         self.loss_sum = z(1, dt=torch.float32)
-        # split-K block target and bias-grad form of the weight grads, measured
-        # per workload on MI355X (scripts/wgrad_sweep.sh, dcn_wgrad_ab.sh):
-        # DLRM-1TB 0.585 ms/step with column sums at 512 blocks vs 0.599 with
-        # the bias column in N at 256; DCN-v2 (256x128 tiles) 2.876 ms with the
-        # bias column at 256 vs 2.897 with column sums, 2.985-2.999 at 512.
-        dcn = cfg.interaction == "dcn"
-        # (weight grad, dgrad) of a layer as one paired launch (TDFO_PAIR_BWD=0:
-        # two launches)
-        pair_bwd = dev.type == "cuda" and os.environ.get("TDFO_PAIR_BWD", "1") == "1"
-        # paired with its dgrad, a DLRM weight grad needs fewer split-K blocks
-        # to fill the machine: 256 (0.477-0.479 ms/step) vs 512 (0.504-0.514),
-        # 384 0.502, 128 0.510; unpaired 512 stays best (above)
-        self._wg_target = int(os.environ.get("TDFO_WGRAD_TARGET",
-                                             256 if (dcn or pair_bwd) else 512))
-        # TDFO_WGRAD_CSUM=0/1 overrides (A/B)
-        self._csum = os.environ.get("TDFO_WGRAD_CSUM", "0" if dcn else "1") != "0"
-        # DCN-v2's weight grads run on the one-block-per-CU 256x128 kernel
-        # (policy 25, no column sums): splits sized for its 256 resident
-        # blocks (U wgrad 65 -> ? us, V 58 -> ? us; TDFO_WGRAD_SLOTS=0: the
-        # 128x128-tile target)
-        # (paired with its dgrad on 256x128 tiles the weight grad gets half the
-        # slots: 2.347-2.359 vs 2.419-2.431 ms/step at 256, 2.381 at 512)
-        self._wg_slots = int(os.environ.get(
-            "TDFO_WGRAD_SLOTS", (128 if pair_bwd else 256)
-            if (dcn and not self._csum and dev.type == "cuda"
-                and ops.gemm_policy(-1) == 25) else 0))
-        max_slab = 1
-        if dcn:
-            s_ = self._wg_splits(cfg.dcn_rank, self.top_real)
-            max_slab = max(max_slab, s_ * cfg.dcn_rank * self.top_real)
-        self.slab = z(max_slab, dt=torch.float32)
-        # Weight grads of the augmented layers: the GEMM's N is the 64-aligned
-        # input width in_k and the bias column (when it is past in_k) comes
-        # from the same kernel's column sums of dy (csum), so N tiles evenly
-        # (top1: 64 tiles x 8 splits instead of 72 x 4). Each layer's split-K
+        # Weight grads: split-K over the batch into ~256 blocks (each paired
+        # with its layer's dgrad in one ping-pong launch: 0.477 vs 0.504 ms/step
+        # at 512 unpaired); the bias gradient comes from the same GEMM's column
+        # sums of dy (N stays the 64-aligned input width). Each layer's
         # partials get their own zero-initialised slab [S][out][wcols]: one
-        # process on a GPU sums them inside the fused optimizer pass (no
-        # reduce launch per layer); with >1 rank they are reduced first
-        # because the all-reduce needs the grads.
+        # process sums them inside the fused optimizer pass (no reduce launch
+        # per layer); with >1 rank they are reduced first because the
+        # all-reduce needs the grads.
+        self._pair_bwd = dev.type == "cuda"
         self.wslab = {}
         self._segments = []
         self._opt_sums_slabs = dev.type == "cuda" and world_size == 1
+        max_slab = 1
+        if cfg.interaction == "dcn":
+            max_slab = self._wg_splits(cfg.dcn_rank, self.top_real) * cfg.dcn_rank * self.top_real
+        self.slab = z(max_slab, dt=torch.float32)
         for L in self.bottom_layers + self.top_layers + self.dcn_u:
-            S = self._wg_splits(L.out, self._wgrad_n(L))
+            S = self._wg_splits(L.out, L.in_k)
             if S > 1:
                 sl = z(S * L.out * L.wcols, dt=torch.float32)
                 self.wslab[L.name] = (sl, S)
                 if self._opt_sums_slabs:
                     self._segments.append((fp.offset(L.name + ".w"), sl, S))
-        # DCN-v2 V weight grads: same treatment (one slab per layer, summed by
-        # the optimizer instead of a reduce launch per layer)
-        if dcn and self._opt_sums_slabs:
+        # DCN-v2 V weight grads: same treatment
+        if cfg.interaction == "dcn" and self._opt_sums_slabs:
             for i in range(cfg.dcn_layers):
                 S = self._wg_splits(cfg.dcn_rank, self.top_real)
                 if S > 1:
@@ -402,81 +384,26 @@ class DLRMTrainer:
         self.slot_stride = [0] + list(self.emb.slot_stride)
         self.graph = None
         self.steps = 0
-        # Side streams (GPU only): wgrads run beside the dgrad chain; at world
-        # size 1 the embedding lookup/update run beside the bottom MLP. The
-        # forks/joins are stream-event edges, so a captured hipGraph keeps the
-        # concurrency as parallel branches.
         # ids-only half of the embedding backward (keys + sort) on its own
         # stream beside the top MLP: it needs no gradient, and its few
         # latency-bound blocks leave the GEMMs most of the machine
         self._ps = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
-        # one process, opt-in (TDFO_EMB_LOOKUP_SIDE=1): lookup beside the bottom
-        # MLP. Measured neutral-to-worse (DLRM 0.636 vs 0.633 ms, DCN-v2 2.999
-        # vs 3.003): the bottom MLP is too short to hide a 48 us gather.
-        self._ls = (torch.cuda.Stream(device=dev)
-                    if dev.type == "cuda" and world_size == 1 and
-                    os.environ.get("TDFO_EMB_LOOKUP_SIDE", "0") == "1" else None)
-        on_gpu = dev.type == "cuda" and bool(cfg.overlap)
-        self._ws = torch.cuda.Stream(device=dev) if on_gpu else None
-        self._es = (torch.cuda.Stream(device=dev)
-                    if (on_gpu and world_size == 1 and cfg.overlap != "wgrad") else None)
         # input-dist pipelining (the role of TorchRec's TrainPipelineSparseDist
         # behind the reference's DMP, torchrec/train.py:241-247): batch i+1's
         # ids are bucketed and exchanged right after batch i's embedding
         # update -- the last reader of the exchanged-id buffers -- so the
         # exchange overlaps batch i's dense optimizer step and batch i+1
         # starts at its lookup. Numerics are identical to the unpipelined step.
-        self.pipeline = bool(cfg.pipeline) and world_size > 1 and self._es is None
-        # pipelined mode: also the next batch's lookup + pooled-embedding
-        # all-to-all in this step's tail (TDFO_PIPE_LOOKUP=0: at the start of
-        # the next step, beside its bottom MLP)
-        self._pipe_lookup = self.pipeline and os.environ.get("TDFO_PIPE_LOOKUP", "1") == "1"
+        self.pipeline = bool(cfg.pipeline) and world_size > 1
+        self._pipe_lookup = self.pipeline and bool(cfg.pipeline_lookup)
         on_cuda = dev.type == "cuda"
         self._ev_loaded = torch.cuda.Event() if (on_cuda and self._pipe_lookup) else None
         self._ev_lookup = torch.cuda.Event() if (on_cuda and self._pipe_lookup) else None
         self._next = None
         self._primed = False
-        # one process: per-stream hipGraphs (capture_graph(streams=True)); the
-        # embedding lookup / sort / update replay on their own stream beside
-        # the MLP graphs, joined by events (set while capturing/replaying)
-        self._mstream = False
-        # early lookup (both workloads: DLRM 0.538 vs 0.556, DCN-v2 2.571-2.577
-        # vs 2.592-2.596 ms/step) and where the top-MLP part of the dense
-        # optimizer runs: "1" on the embedding stream after the embedding
-        # update (DLRM, whose update is short: 0.541 vs 0.545 for "main"),
-        # "main" first on the MLP stream beside the embedding update (DCN-v2,
-        # whose multi-hot update is 0.42 ms: 2.589 vs 2.633 for "0"), "0" one
-        # pass after the bottom backward (profiles/graph_streams.md)
-        self._early = os.environ.get("TDFO_EARLY_LOOKUP", "1") == "1"
-        # (with paired weight-grad launches the MLP stream has slack and the
-        # embedding stream's update -> next lookup chain gates the next step:
-        # DLRM-1TB "0" 0.463-0.466 vs "1" 0.471-0.479, "main" 0.471-0.472)
-        self._split_opt = os.environ.get("TDFO_SPLIT_OPT",
-                                         "main" if cfg.interaction == "dcn" else "0")
-        self._ms_wgrad = False
-        self._ms_merge = False
-        self._ms_one = False
-        self._ms_one_e = False
-        bp = os.environ.get("TDFO_BOTTOM_POLICY", "")
-        self._bot_policy = int(bp) if bp != "" and self.device.type == "cuda" else None
-        self._opt_early = False
-        # (weight grad, dgrad) of a layer as one paired small-tile launch
-        # (TDFO_PAIR_BWD=0: two launches); only where the weight grad issues
-        # nothing but its GEMM (one GPU: slabs summed by the optimizer)
-        self._pair_bwd = pair_bwd
-        # TDFO_FUSED_BOTTOM=1: the bottom MLP forward as one fused kernel
-        # (csrc/kernels/mlp_fused.hip) when its widths are the DLRM / DCN-v2
-        # ones. Off by default: 17.4 vs 19.5 us for the three GEMM launches in
-        # isolation (scripts/bench_mlp3.py; its row-strided weight-fragment
-        # loads bind the TA), but 40 vs ~35 us in the step, where its 512-thread,
-        # 64 KB-LDS blocks wait for CUs behind the concurrent lookup's blocks
-        # (DLRM-1TB 0.538-0.545 vs 0.540-0.541 ms/step, DCN-v2 2.516 vs 2.495)
-        Lb = self.bottom_layers
-        self._fused_bottom = (dev.type == "cuda" and len(Lb) == 3
-                              and os.environ.get("TDFO_FUSED_BOTTOM", "0") == "1"
-                              and ops.mlp3_supported(Lb[0].in_k, Lb[0].out, Lb[1].out, Lb[2].out)
-                              and Lb[1].in_k == Lb[0].out and Lb[2].in_k == Lb[1].out)
+        self._mstream = False            # per-stream graphs (one process)
         self._ms = None
+        self._graph_layout = 0
 
     # for tests / checkpoints: (weight [out, in_real], bias [out]) views
     def weight(self, name: str):
@@ -512,37 +439,12 @@ class DLRMTrainer:
 
         dense [B, num_dense] (any float dtype), ids flat int64 in table order
         (table t: B*L_t ids), label [B] float. on_device: the tensors are
-        device-resident and ready for every stream (e.g. a pre-generated
-        pool); with per-stream graphs the ids are then copied on the
-        embedding stream right behind the previous step's embedding update,
-        so the next lookup overlaps the previous step's bottom-MLP backward.
+        device-resident and ready for every stream (``input_streams()``);
+        with per-stream graphs the ids are then copied on the embedding side
+        right behind the previous step's embedding update, so the next lookup
+        overlaps the previous step's bottom-MLP backward.
         """
-        if self.graph == "streams" and self._early and ids.is_cuda \
-                and ids.dtype == torch.int64 and ids.is_contiguous() \
-                and ids.numel() == self.ids.numel():
-            se, ev = self._ms["stream"], self._ms["events"][0]
-            main = torch.cuda.current_stream()
-            cs = self._ms.get("cstream")
-            if cs is not None and on_device:
-                # the ids copy on its own stream right behind this step's
-                # sort (E2, the ids' last reader), so the next lookup (E1)
-                # waits on an event that is already signalled instead of
-                # queueing the copy behind the embedding update
-                if self._ms["e2_recorded"]:
-                    cs.wait_event(self._ms["ev_e2"])
-                with torch.cuda.stream(cs):
-                    self.ids.copy_(ids, non_blocking=True)
-                    self._ms["ev_copy"].record(cs)
-                se.wait_event(self._ms["ev_copy"])
-                ops.batch_load(dense, self.x0, ids[:0], self.ids[:0], label, self.label)
-                return
-            if not on_device:
-                se.wait_stream(main)               # e.g. an H2D the caller ordered on main
-            with torch.cuda.stream(se):
-                self.ids.copy_(ids, non_blocking=True)
-                ev.record(se)
-            if not on_device:
-                main.wait_event(ev)                # dense / labels from the same source
+        if self.graph == "streams" and self._ms_load_ids(ids, on_device):
             ops.batch_load(dense, self.x0, ids[:0], self.ids[:0], label, self.label)
             return
         # device-resident batch: one fused launch (ids, labels, dense -> bf16)
@@ -586,18 +488,7 @@ class DLRMTrainer:
     def _bwd(self, L: Lin, x, dy, dx, x_is_relu, wgrad_now: bool = True):
         """weight+bias grad (augmented wgrad) and dgrad into dx (masked by x>0).
         wgrad_now=False leaves the weight grad to a later `_wgrad` call."""
-        fp = self.fp
         if not wgrad_now:
-            self._dgrad(L, x, dy, dx, x_is_relu)
-            return
-
-        def wgrad():
-            self._wgrad(L, x, dy)
-
-        if self._ws is not None:
-            self._ws.wait_stream(torch.cuda.current_stream())
-            with torch.cuda.stream(self._ws):
-                wgrad()
             self._dgrad(L, x, dy, dx, x_is_relu)
             return
         # the weight grad and the dgrad go out as one paired launch (the slab
@@ -609,10 +500,7 @@ class DLRMTrainer:
             fin()
 
     def _wg_splits(self, M: int, N: int) -> int:
-        return ops.wgrad_splits(M, N, self.B, self._wg_target, slots=self._wg_slots)
-
-    def _wgrad_n(self, L: Lin) -> int:
-        return L.in_k if self._csum else L.wcols
+        return ops.wgrad_splits(M, N, self.B, 256)
 
     def _wgrad(self, L: Lin, x, dy):
         """dW[:, :in_k] = dy^T x[:, :in_k]; db (column bcol) = colsum(dy) from
@@ -625,18 +513,17 @@ class DLRMTrainer:
         """The weight-grad GEMM alone; returns the split-K slab reduce still
         to run (more than one rank: the all-reduce needs the grads) or None
         (one GPU: the optimizer sums the slabs)."""
-        n = self._wgrad_n(L)
-        csum = -1 if (L.bias_in_k or not self._csum) else L.bcol
+        csum = -1 if L.bias_in_k else L.bcol
         g = self.fp.grad(L.name + ".w").view(-1)
         if L.name in self.wslab:
             sl, S = self.wslab[L.name]
-            ops.gemm(dy, True, x[:, :n], True, None, False, None, None, sl, S,
+            ops.gemm(dy, True, x[:, :L.in_k], True, None, False, None, None, sl, S,
                      ldc32=L.wcols, csum_col=csum)
             if not self._opt_sums_slabs:      # else: partials summed by the optimizer
                 m = L.out * L.wcols
                 return lambda: ops.reduce_rows(sl, S, m, m, g, False, 1.0)
         else:
-            ops.gemm(dy, True, x[:, :n], True, None, False, None, None, g, 1,
+            ops.gemm(dy, True, x[:, :L.in_k], True, None, False, None, None, g, 1,
                      ldc32=L.wcols, csum_col=csum)
         return None
 
@@ -650,40 +537,20 @@ class DLRMTrainer:
                      x[:, :n] if x_is_relu else None, dx[:, :n], None, 1)
 
     # ---------------------------------------------------------- stages
-    # The step is a fixed sequence of compute stages ("c", hipGraph-capturable)
-    # and communication stages ("m", RCCL collectives issued eagerly so they
-    # overlap with the next compute stage on their own stream).
-    def _join(self, s):
-        if s is not None:
-            torch.cuda.current_stream().wait_stream(s)
-
+    # The step is a fixed sequence of compute stages ("c": main stream, "e":
+    # side stream; hipGraph-capturable) and communication stages ("m" / "em":
+    # RCCL collectives issued eagerly on the main / side stream, so they
+    # overlap the next compute stage); "j" joins the side stream back, "jw"
+    # waits only for the next batch's load on it.
     def _stages(self):
         emb = self.emb
         top_wgrad = [("c", self._s_top_wgrad)] if self._defer_top_wgrad else []
-        if self._es is not None:
-            # one process: embedding work on its own stream, beside the MLPs
-            return [
-                ("c", self._s_emb_fwd_side),
-                ("c", self._s_bottom_fwd),
-                ("c", self._s_top),
-                ("c", self._s_emb_update_side),
-            ] + top_wgrad + [
-                ("c", self._s_bottom_bwd),
-                ("c", self._s_dense_update),
-            ]
-        if self.world == 1 and self._ls is not None:
-            lookup = ("c", self._s_emb_lookup_side)
-        else:
-            lookup = ("c", emb.stage_fwd_lookup)
         prep = [] if emb.fwd_prep_noop else [("c", lambda: emb.stage_fwd_prep(self.ids))]
         if self.pipeline:
             # this batch's ids were exchanged during the previous step (or by
-            # prime()); the next batch is loaded + exchanged after the
-            # embedding update, overlapping the dense optimizer step
-            # Multi-GPU side stream ("e" compute / "em" comm stages run on the
-            # embedding stream, "j" joins it back): the embedding update and
-            # the next batch's load, bucketize and id exchange run beside the
-            # dense-gradient all-reduce wait and the dense optimizer step.
+            # prime()); on the side stream the embedding update and the next
+            # batch's load, bucketize and id exchange run beside the
+            # dense-gradient all-reduce wait and the dense optimizer step
             eprep = [("e", k[1]) for k in prep]
             if self._pipe_lookup:
                 # ... and the next batch's lookup + pooled-embedding exchange
@@ -691,8 +558,7 @@ class DLRMTrainer:
                 # embedding update they must see), so the next step starts
                 # at its bottom MLP with its pooled embeddings in flight or
                 # landed; the main stream only waits for the next batch's
-                # dense inputs ("jw": an event after the load, not the
-                # whole side stream)
+                # dense inputs ("jw")
                 return [
                     ("c", self._s_bottom_fwd),
                     ("m", self._m_fwd_wait),
@@ -717,7 +583,7 @@ class DLRMTrainer:
                 ]
             return [
                 ("m", emb.ids_exchange_wait),
-                lookup,
+                ("c", emb.stage_fwd_lookup),
                 ("m", emb.stage_fwd_out_exchange),
                 ("c", self._s_bottom_fwd),
                 ("m", self._m_fwd_wait),
@@ -738,7 +604,7 @@ class DLRMTrainer:
             ]
         return prep + [
             ("m", emb.stage_fwd_ids_exchange),
-            lookup,
+            ("c", emb.stage_fwd_lookup),
             ("m", emb.stage_fwd_out_exchange),
             ("c", self._s_bottom_fwd),
             ("m", self._m_fwd_wait),
@@ -792,38 +658,12 @@ class DLRMTrainer:
             self._run_stage(kind, fn)
 
     def _s_bottom_fwd(self):
-        if self._fused_bottom:
-            fp = self.fp
-            Ls = self.bottom_layers
-            ops.mlp3_fwd(self.bot_in[0][:, :Ls[0].in_k],
-                         [fp.bf16(L.name + ".w")[:, :L.in_k] for L in Ls],
-                         [None if L.bias_in_k else fp.param(L.name + ".w")[:, L.bcol] for L in Ls],
-                         [self.bot_in[1][:, :Ls[0].out], self.bot_in[2][:, :Ls[1].out],
-                          self.h_out])
-            return
         n = len(self.bottom_layers)
-        with self._bottom_policy():
-            for i, L in enumerate(self.bottom_layers):
-                out = self.bot_in[i + 1][:, :L.out] if i + 1 < n else self.h_out
-                self._fwd(L, self.bot_in[i], out)
-
-    @contextlib.contextmanager
-    def _bottom_policy(self):
-        """GEMM tile policy for the bottom MLP (TDFO_BOTTOM_POLICY): its
-        GEMMs run beside the embedding lookup, whose blocks cannot share a CU
-        with a 144 KiB-LDS 256x128-tile block."""
-        p = self._bot_policy
-        if p is None:
-            yield
-            return
-        old = ops.gemm_policy(p)
-        try:
-            yield
-        finally:
-            ops.gemm_policy(old)
+        for i, L in enumerate(self.bottom_layers):
+            out = self.bot_in[i + 1][:, :L.out] if i + 1 < n else self.h_out
+            self._fwd(L, self.bot_in[i], out)
 
     def _m_fwd_wait(self):
-        self._join(self._ls)
         if self._pipe_lookup and self._ev_lookup is not None and self._side() is not None:
             # the lookup ran on the side stream in the previous step's tail
             # (tables it wrote straight into recv have no collective to wait on)
@@ -839,25 +679,6 @@ class DLRMTrainer:
         if self._ev_lookup is not None:
             self._ev_lookup.record(torch.cuda.current_stream())
 
-    def _s_emb_lookup_side(self):
-        """One process: the pooled lookup (random row gathers, memory-bound)
-        on its own stream beside the bottom MLP; joined at the top stage."""
-        self._ls.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(self._ls):
-            self.emb.stage_fwd_lookup()
-
-    def _s_emb_fwd_side(self):
-        self._es.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(self._es):
-            self.emb.stage_fwd_prep(self.ids)
-            self.emb.stage_fwd_lookup()
-
-    def _s_emb_update_side(self):
-        self._es.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(self._es):
-            self.emb.backward_start()
-            self._s_emb_update()
-
     def _s_top(self):
         self._s_top_a()
         self._s_top_b()
@@ -868,8 +689,6 @@ class DLRMTrainer:
         cfg, fp, B = self.cfg, self.fp, self.B
         D, F = cfg.embedding_dim, self.F
         emb = self.emb
-        self._join(self._es)
-        self._join(self._ls)
         if self._ps is not None and not self._mstream:
             self._ps.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(self._ps):
@@ -915,9 +734,8 @@ class DLRMTrainer:
         else:
             self._dcn_backward(h)
         emb.stage_bwd_local(self.emb_hyper)        # replicated tables' dense grads
-        self._join(self._ws)
-        if not self._mstream:
-            self._join(self._ps)
+        if not self._mstream and self._ps is not None:
+            torch.cuda.current_stream().wait_stream(self._ps)
 
     def _s_top_wgrad(self):
         """Top-MLP (and DCN cross-layer) weight grads, deferred past the
@@ -940,12 +758,10 @@ class DLRMTrainer:
                 self._dcn_wgrad_v(i)          # (one shared slab off one GPU)
 
     def _s_bottom_bwd(self):
-        with self._bottom_policy():
-            for i in reversed(range(len(self.bottom_layers))):
-                L = self.bottom_layers[i]
-                dx = self.bot_grad[i - 1] if i > 0 else None
-                self._bwd(L, self.bot_in[i], self.bot_grad[i], dx, x_is_relu=i > 0)
-        self._join(self._ws)
+        for i in reversed(range(len(self.bottom_layers))):
+            L = self.bottom_layers[i]
+            dx = self.bot_grad[i - 1] if i > 0 else None
+            self._bwd(L, self.bot_in[i], self.bot_grad[i], dx, x_is_relu=i > 0)
 
     # Dense gradients are all-reduced in two buckets of the flat buffer, each
     # issued as soon as its grads exist (the role of the DDP reducer,
@@ -988,7 +804,6 @@ class DLRMTrainer:
                 setattr(self, name, None)
 
     def _s_dense_update(self):
-        self._join(self._es)
         fp = self.fp
         ops.dense_optimizer(fp.p, fp.g, fp.m, fp.v, fp.p_bf16, self.dense_opt, self.dense_hyper,
                             wd=self.cfg.dense_wd, segments=self._segments)
@@ -1063,10 +878,6 @@ class DLRMTrainer:
         j = i if len(self.dcn_dyl) > 1 else 0
         return self.dcn_dyl[j], self.dcn_dhl[j]
 
-    def _dcn_wgrad_u(self, i: int):
-        dy, _ = self._dcn_bufs(i)
-        self._wgrad(self.dcn_u[i], self.dcn_h[i], dy)
-
     def _dcn_wgrad_v(self, i: int):
         """dV_i = dh_i^T x_i (split-K partials summed by the optimizer on one
         GPU, reduced here otherwise)."""
@@ -1079,336 +890,48 @@ class DLRMTrainer:
             ops.linear_wgrad(dh, self.dcn_x[i][:, :Wd], self.fp.grad(f"dcn{i}.v").view(-1),
                              splits=self._wg_splits(self.cfg.dcn_rank, Wd), slab=self.slab)
 
+    # ------------------------------------------------------------- step
     def step(self):
         """One training step on the batch in the static buffers."""
         if self.pipeline and not self._primed:
             raise RuntimeError("pipelined trainer: call prime(first batch) before step()")
         if self.graph == "streams":
             self._ms_step()
+        elif isinstance(self.graph, list):
+            self._staged_step()
         elif self.graph is not None:
-            if isinstance(self.graph, list):
-                self._on_side = False
-                eager = False
-                for kind, item in self.graph:
-                    if kind in ("c", "e"):
-                        g, fns = item
-                        if eager:        # a captured buffer was reallocated this step
-                            self._run_stage(kind, lambda fns=fns: [f() for f in fns])
-                        else:
-                            self._run_stage(kind, None, graph=g)
-                    else:
-                        self._run_stage(kind, item)
-                        # row-wise capacity grown inside an exchange stage: the
-                        # rest of this step runs eagerly, then re-capture
-                        eager = eager or self.emb.layout_version != self._graph_layout
-                if eager:
-                    self.sync_streams()
-                    torch.cuda.synchronize()
-                    self.capture_graph(warmup=0, staged=True)
-            else:
-                self.graph.replay()
+            self.graph.replay()
         else:
             self._forward_backward()
         self.steps += 1
 
-    # ------------------------------------------------ per-stream graphs
-    # The HIP runtime replays one captured graph's independent branches
-    # mostly in order on its own queue (profiles/dlrm1tb_b8192_graph_kernels:
-    # the embedding lookup and the bottom MLP ran back to back), so a single
-    # process instead captures six graphs, three per stream, and replays them
-    # on two streams joined by events: the memory-bound embedding work
-    # (lookup, sort, fused update) runs on the side stream concurrently with
-    # the latency-bound MLP GEMMs.
-    def _ms_plan(self):
-        emb = self.emb
-
-        def e1():
-            if not emb.fwd_prep_noop:
-                emb.stage_fwd_prep(self.ids)
-            emb.stage_fwd_ids_exchange()
-            emb.stage_fwd_lookup()
-            emb.stage_fwd_out_exchange()
-            emb.forward_wait()
-
-        # the top-MLP (+ head, DCN) part of the dense optimizer needs only the
-        # top backward: it runs on the embedding stream after the embedding
-        # update, beside the bottom-MLP backward (TDFO_SPLIT_OPT=0: one pass)
-        split = self._split_opt in ("1", "main") and not self._ms_wgrad
-        on_main = self._split_opt == "main"
-        # "early" (composed graphs, dot interaction): the top part on the
-        # embedding stream as soon as the top backward is done (beside the
-        # interaction backward), before the embedding update
-        early = self._opt_early
-        split = split or early
-        a, P = self._ar_split, self.fp.p.numel()
-
-        def e3():
-            emb.backward_start()
-            emb.backward_wait()
-            self._s_emb_update()
-            if split and not on_main and not early:
-                self._dense_update_range(a, P)
-
-        def m3():
-            if self._defer_top_wgrad and not self._ms_wgrad:
-                self._s_top_wgrad()          # beside the embedding update (E3)
-            if split and on_main:
-                self._dense_update_range(a, P)
-            self._s_bottom_bwd()
-            if split:
-                self._dense_update_range(0, a)
-            elif not self._ms_wgrad:
-                self._s_dense_update()
-        if self._ms_merge:
-            # bottom fwd + top in one graph (no M1 -> M2 graph boundary, ~13 us
-            # of queue idle): the lookup it waits for was issued right behind
-            # the previous embedding update, which is now the update alone --
-            # the top-MLP optimizer part runs on its own stream (O) beside it
-            # and beside the bottom backward, and the next step's graph waits
-            # for it
-            def m12():
-                self._s_bottom_fwd()
-                self._s_top()
-
-            def e3m():
-                emb.backward_start()
-                emb.backward_wait()
-                self._s_emb_update()
-
-            def m3m():
-                self._s_bottom_bwd()
-                self._dense_update_range(0, a)
-
-            return {"E1": e1, "E2": emb.stage_bwd_prepare, "M12": m12, "E3": e3m,
-                    "O": lambda: self._dense_update_range(a, P), "M3": m3m}
-        if early:
-            return {"E1": e1, "E2": emb.stage_bwd_prepare, "M1": self._s_bottom_fwd,
-                    "M2": self._s_top_a, "M2b": self._s_top_b,
-                    "ET": lambda: self._dense_update_range(a, P), "E3": e3, "M3": m3}
-        plan = {"E1": e1, "E2": emb.stage_bwd_prepare, "M1": self._s_bottom_fwd,
-                "M2": self._s_top, "E3": e3, "M3": m3}
-        if self._ms_wgrad:
-            plan["W"] = self._s_top_wgrad
-            plan["M4"] = self._s_dense_update
-        return plan
-
-    def _ms_run(self, name: str):
-        """Replay a main-stream stage graph, or (TDFO_EAGER_STAGES=M1,M3)
-        launch the stage's kernels eagerly: a graph's end costs the queue
-        13-20 us before the next work starts, an eager launch behind a graph
-        ~0.3 us (profiles/r02_s2/notes.md)."""
-        if name in self._ms["eager"]:
-            self._ms["plan"][name]()
-        else:
-            self._ms["graphs"][name].replay()
-
-    def _ms_step(self):
-        g, se, sw, ev = (self._ms["graphs"], self._ms["stream"], self._ms["wstream"],
-                         self._ms["events"])
-        main = torch.cuda.current_stream()
-        if self._ms_merge:
-            so = self._ms["ostream"]
-            if not self._early:
-                ev[0].record(main)
-                se.wait_event(ev[0])
-            with torch.cuda.stream(se):
-                g["E1"].replay()
-                ev[1].record(se)
-                g["E2"].replay()
-            main.wait_event(ev[1])           # pooled embeddings ready
-            if self._ms["o_pending"]:
-                main.wait_event(ev[5])       # previous step's top-MLP optimizer part
-            g["M12"].replay()
-            ev[2].record(main)
-            se.wait_event(ev[2])
-            with torch.cuda.stream(se):
-                g["E3"].replay()
-                ev[3].record(se)
-            so.wait_event(ev[2])
-            with torch.cuda.stream(so):
-                g["O"].replay()
-                ev[5].record(so)
-            self._ms["o_pending"] = True
-            g["M3"].replay()
-            if not self._early:
-                main.wait_event(ev[3])
-            return
-        if not self._early:
-            ev[0].record(main)
-            se.wait_event(ev[0])             # this step's batch is loaded (on main)
-        # (early lookup: this step's ids were copied on se by load_batch, so the
-        # lookup follows the previous step's embedding update on the same stream)
-        with torch.cuda.stream(se):
-            if self._ms_one_e:
-                g["EA"].replay()             # records ev[1] inside
+    def _staged_step(self):
+        self._on_side = False
+        eager = False
+        for kind, item in self.graph:
+            if kind in ("c", "e"):
+                g, fns = item
+                if eager:        # a captured buffer was reallocated this step
+                    self._run_stage(kind, lambda fns=fns: [f() for f in fns])
+                else:
+                    self._run_stage(kind, None, graph=g)
             else:
-                g["E1"].replay()
-                ev[1].record(se)
-                g["E2"].replay()
-            if self._ms.get("cstream") is not None:
-                self._ms["ev_e2"].record(se)
-                self._ms["e2_recorded"] = True
-        if self._ms_one:
-            g["M"].replay()                  # waits for ev[1], records ev[2] inside
-        else:
-            self._ms_run("M1")
-            main.wait_event(ev[1])           # pooled embeddings ready
-            g["M2"].replay()
-            ev[2].record(main)
-        with torch.cuda.stream(se):
-            if self._opt_early:
-                g["EB"].replay()             # waits for ev[6] and ev[2] inside
-            else:
-                se.wait_event(ev[2])         # embedding gradients ready
-                g["E3"].replay()
-            ev[3].record(se)
-        if sw is not None:                   # top weight grads on a third stream
-            sw.wait_event(ev[2])
-            with torch.cuda.stream(sw):
-                g["W"].replay()
-                ev[4].record(sw)
-        if not self._ms_one:
-            self._ms_run("M3")
-        if sw is not None:
-            main.wait_event(ev[4])
-            g["M4"].replay()
-        if not self._early:
-            main.wait_event(ev[3])           # the next batch (loaded on main) rewrites the ids
-        # early lookup: no end-of-step join -- the embedding stream's next work
-        # (ids copy, lookup) is ordered behind this update on that stream, and
-        # the next MLP graphs wait for the next lookup; readers of tables /
-        # params outside step() call sync_streams() first
-
-    def input_streams(self):
-        """Streams that read a batch handed to load_batch (a producer orders
-        its device copies on each, then passes on_device=True)."""
-        main = torch.cuda.current_stream()
-        if self.graph == "streams" and self._early:
-            cs = self._ms.get("cstream")
-            return [main, self._ms["stream"]] + ([cs] if cs is not None else [])
-        return [main]
-
-    def sync_streams(self):
-        """Order the current stream after all side-stream work of issued steps
-        (embedding updates, the top-MLP optimizer part)."""
-        if self._ms is not None:
-            torch.cuda.current_stream().wait_stream(self._ms["stream"])
-            for k in ("ostream", "cstream"):
-                if self._ms.get(k) is not None:
-                    torch.cuda.current_stream().wait_stream(self._ms[k])
-        if getattr(self, "_sides", None) is not None:
-            torch.cuda.current_stream().wait_stream(self._sides)
-
-    def _emb_stream(self):
-        """Embedding side stream; TDFO_EMB_CU_KEEP=k (1..3) restricts it to k
-        of every 4 CUs (hipExtStreamCreateWithCUMask) so its memory-bound,
-        many-block kernels leave CUs to the MLP stream's small GEMMs."""
-        keep = int(os.environ.get("TDFO_EMB_CU_KEEP", "4"))
-        if keep >= 4:
-            return torch.cuda.Stream(device=self.device)
-        nib = (1 << keep) - 1
-        word = 0
-        for q in range(8):
-            word |= nib << (4 * q)
-        ncu = torch.cuda.get_device_properties(self.device).multi_processor_count
-        handle = ops.cu_masked_stream([word] * ((ncu + 31) // 32))
-        return torch.cuda.ExternalStream(handle, device=self.device)
-
-    def _capture_streams(self, wgrad_stream: bool = False):
-        assert self.world == 1 and self._es is None and self._ls is None
-        self._mstream = True
-        # top weight grads deferred past the interaction backward, onto their
-        # own stream beside the embedding update and the bottom backward
-        self._ms_wgrad = wgrad_stream and self.cfg.interaction == "dot"
-        self._defer_top_wgrad = self._defer_top_wgrad or self._ms_wgrad
-        # TDFO_MS_MERGE=1: bottom fwd + top in one graph, top optimizer part on
-        # a third stream. Measured worse (DLRM-1TB 0.57-0.58 vs 0.545 ms/step,
-        # DCN-v2 2.55 vs 2.50; with GPU_MAX_HW_QUEUES=8 1.19 / 3.58): with 4
-        # HW queues the third stream shares the embedding stream's queue, so
-        # the next lookup queues behind the optimizer pass
-        self._ms_merge = (os.environ.get("TDFO_MS_MERGE", "0") == "1" and not self._ms_wgrad
-                          and not self._defer_top_wgrad)
-        emode = int(os.environ.get("TDFO_EVENT_MODE", "2"))
-        mk = (lambda: ops.SyncEvent(emode)) if emode else torch.cuda.Event
-        # TDFO_MS_ONE=1 (default for DLRM): the MLP stream's three graphs (and
-        # the embedding stream's lookup + sort) composed into one executable
-        # graph each, the cross-stream edges as event nodes inside: the queue
-        # idles ~8-10 us at an event node instead of ~14 us at a graph boundary.
-        # DLRM-1TB 0.457-0.458 vs 0.462-0.466 ms/step, Kaggle 0.461 vs 0.459,
-        # DCN-v2 2.362-2.367 vs 2.335-2.340 (off). TDFO_SPLIT_OPT=early on
-        # top (the top-MLP optimizer part on the embedding stream right after
-        # the top backward): 0.469-0.473
-        one = os.environ.get("TDFO_MS_ONE", "1" if self.cfg.interaction == "dot" else "0")
-        self._ms_one = (one in ("1", "2") and emode != 0 and not self._ms_wgrad
-                        and not self._ms_merge)
-        self._ms_one_e = self._ms_one and one == "1"    # "2": the MLP stream only
-        self._ms_ev = [mk() for _ in range(8)]
-        self._opt_early = (self._ms_one and self._split_opt == "early"
-                           and self.cfg.interaction == "dot")
-        plan = self._ms_plan()
-        # (stream priorities -- MLP graphs high, embedding graphs low -- were
-        # measured at 1.9 ms/step vs 0.556: not used)
-        se = self._emb_stream()
-        sw = torch.cuda.Stream(device=self.device) if self._ms_wgrad else None
-        so = torch.cuda.Stream(device=self.device) if self._ms_merge else None
-        pool = torch.cuda.graph_pool_handle()
-        graphs = {}
-        main = torch.cuda.current_stream()
-        se.wait_stream(main)
-        for x in (sw, so):
-            if x is not None:
-                x.wait_stream(main)
-        for name in plan:
-            gr = torch.cuda.CUDAGraph(keep_graph=self._ms_one)
-            # (the MLP graphs capture on torch's own side stream: capture is
-            # not allowed on the default stream; replays run on any stream)
-            st = se if name[0] == "E" else (sw if name == "W" else (so if name == "O" else None))
-            with graph_capture(gr, pool=pool, stream=st):
-                plan[name]()
-            graphs[name] = gr
-        if self._ms_one:
-            # the MLP stream's three graphs chained by the two cross-stream
-            # event nodes (wait: pooled embeddings; record: embedding grads)
-            # (and the embedding stream's: lookup, record, sort; then, with
-            # the early optimizer part, wait, top optimizer part, wait, update)
-            ev = self._ms_ev
-            top = [("graph", graphs["M2"])]
-            if self._opt_early:
-                top += [("record", ev[6]), ("graph", graphs["M2b"])]
-                graphs["EB"] = ops.ComposedGraph([("wait", ev[6]), ("graph", graphs["ET"]),
-                                                  ("wait", ev[2]), ("graph", graphs["E3"])])
-            graphs["M"] = ops.ComposedGraph([("graph", graphs["M1"]), ("wait", ev[1])] + top
-                                            + [("record", ev[2]), ("graph", graphs["M3"])])
-            if self._ms_one_e:
-                graphs["EA"] = ops.ComposedGraph([("graph", graphs["E1"]), ("record", ev[1]),
-                                                  ("graph", graphs["E2"])])
-        torch.cuda.synchronize()
-        eager = {x for x in os.environ.get("TDFO_EAGER_STAGES", "").split(",") if x in ("M1", "M3")}
-        # cross-stream edges between the step's graphs: recorded without the
-        # system-scope fence a default event record adds (L2 writeback +
-        # invalidate; the producing kernels already release to device scope,
-        # and no host reads these edges): DLRM-1TB 0.477-0.480 vs 0.485-0.487
-        # ms/step, DCN-v2 neutral. TDFO_EVENT_MODE=0: torch events, 1: a
-        # device-scope release
-        # TDFO_IDS_STREAM=1 (default with composed graphs): the early lookup's
-        # ids copy on its own stream right behind the sort. With composed
-        # graphs DLRM-1TB 0.455-0.456 vs 0.463-0.466 ms/step, Kaggle 0.462 vs
-        # 0.460; with separate graphs it was neutral (0.482-0.483 vs 0.473-0.482)
-        ids_stream = os.environ.get("TDFO_IDS_STREAM", "1" if self._ms_one else "0") == "1"
-        cs = torch.cuda.Stream(device=self.device) if self._early and ids_stream else None
-        self._ms = {"graphs": graphs, "stream": se, "wstream": sw, "ostream": so, "plan": plan,
-                    "cstream": cs, "ev_e2": mk(), "ev_copy": mk(), "e2_recorded": False,
-                    "eager": eager if not self._ms_merge else set(),
-                    "o_pending": False, "events": self._ms_ev}
-        self.graph = "streams"
+                self._run_stage(kind, item)
+                # row-wise capacity grown inside an exchange stage: the rest
+                # of this step runs eagerly, then the stages are re-captured
+                eager = eager or self.emb.layout_version != self._graph_layout
+        if eager:
+            self.sync_streams()
+            torch.cuda.synchronize()
+            self.capture_graph(warmup=0, staged=True)
 
     def capture_graph(self, warmup: int = 2, staged: Optional[bool] = None,
-                      streams: Optional[bool] = None):
-        """Capture the step into hipGraphs. Single process: one graph for the
-        whole step, or (streams=True, default from TDFO_STREAM_GRAPHS) per-
-        stream graphs replayed on two streams. Multi-process: one graph per
-        compute stage, with the RCCL exchanges issued eagerly between replays
-        (they overlap the next stage)."""
+                      streams: bool = True):
+        """Capture the step into hipGraphs. One process: per-stream graphs
+        (``streams``, default) or one graph for the whole step. Several
+        processes (or ``staged``): one graph per run of compute stages, with
+        the RCCL exchanges issued eagerly between replays (they overlap the
+        next stage). ``warmup`` eager steps run first (they train)."""
         assert self.device.type == "cuda"
         if not self.emb.graph_capturable:
             return
@@ -1421,15 +944,10 @@ class DLRMTrainer:
         torch.cuda.synchronize()
         if staged is None:
             staged = self.world > 1
-        if streams is None:
-            streams = os.environ.get("TDFO_STREAM_GRAPHS", "1") in ("1", "2")
-        if (not staged and streams and self.world == 1 and self._es is None
-                and self._ls is None):
-            # (in-graph cross-stream event nodes would save the graph
-            # boundaries, but torch-ROCm refuses external events)
-            self._capture_streams(wgrad_stream=os.environ.get("TDFO_STREAM_GRAPHS") == "2")
-            return
-        if not staged:
+        if not staged and self.world == 1:
+            if streams:
+                self._capture_streams()
+                return
             g = torch.cuda.CUDAGraph()
             with graph_capture(g):
                 self._forward_backward()
@@ -1454,7 +972,7 @@ class DLRMTrainer:
                 # device copies of a collective issued just before) must not
                 # invalidate this thread's capture
                 with graph_capture(g, pool=pool, stream=se if kind == "e" else None,
-                                      capture_error_mode="thread_local"):
+                                   capture_error_mode="thread_local"):
                     for fn in fns:
                         fn()
                 seq.append((kind, (g, fns)))
@@ -1470,7 +988,7 @@ class DLRMTrainer:
 
     def pop_loss(self) -> float:
         """Mean training loss since the last call (one device->host read);
-        also raises if a row-wise exchange overflowed meanwhile."""
+        also raises (on every rank) if a row-wise exchange dropped lookups."""
         self.sync_streams()
         self.emb.check_overflow()
         v = float(self.loss_sum.item())

@@ -1,0 +1,194 @@
+"""One-process DLRM / DCN-v2 step as per-stream hipGraphs (mixin of
+``DLRMTrainer``).
+
+The HIP runtime replays one captured graph's independent branches mostly in
+order on its own queue (the embedding lookup and the bottom MLP ran back to
+back in a single whole-step graph), so one process instead captures the step
+as graphs per stream and replays them on two streams joined by events: the
+memory-bound embedding work (lookup, ids-only sort, fused update) runs on the
+embedding stream concurrently with the MLP stream's GEMMs.
+
+  embedding stream: E1 lookup -> (record ev1) -> E2 sort ......... E3 update
+  MLP stream:       M1 bottom fwd -> (wait ev1) -> M2 top fwd+bwd -> (record
+                    ev2) -> M3 bottom bwd + dense optimizer
+                    (E3 waits for ev2: the embedding gradients)
+
+With ``composed_graphs`` each stream's graphs are chained natively into one
+executable graph with in-graph event nodes (``ops.ComposedGraph``;
+``graph_compose`` in csrc/bindings.cpp): the queue idles ~8-10 us at an event
+node instead of ~14 us at each graph boundary (DLRM-1TB 0.457 vs 0.463 ms/step;
+DCN-v2 is faster without: 2.335 vs 2.362). The early lookup copies the next
+batch's ids on the embedding stream (or, ``ids_stream``, on a third stream
+right behind the sort), so the next lookup overlaps this step's bottom-MLP
+backward; readers of tables / params outside ``step()`` call
+``sync_streams()`` first.
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import ops
+from ..utils.capture import graph_capture
+
+
+class StreamGraphsMixin:
+    """Per-stream graph capture / replay for one process (``capture_graph``
+    with ``streams=True``, the default at world size 1)."""
+
+    def _ms_plan(self):
+        emb = self.emb
+
+        def e1():
+            if not emb.fwd_prep_noop:
+                emb.stage_fwd_prep(self.ids)
+            emb.stage_fwd_ids_exchange()
+            emb.stage_fwd_lookup()
+            emb.stage_fwd_out_exchange()
+            emb.forward_wait()
+
+        # "split_main" (DCN-v2): the top-MLP (+ head, cross layers) part of the
+        # dense optimizer first on the MLP stream, beside the long multi-hot
+        # embedding update (2.35 vs 2.40 ms/step); "one_pass" (DLRM): the
+        # whole optimizer after the bottom backward (0.463 vs 0.471-0.479)
+        split = self.cfg.opt_placement == "split_main"
+        a, P = self._ar_split, self.fp.p.numel()
+
+        def e3():
+            emb.backward_start()
+            emb.backward_wait()
+            self._s_emb_update()
+
+        def m3():
+            if self._defer_top_wgrad:
+                self._s_top_wgrad()          # beside the embedding update (E3)
+            if split:
+                self._dense_update_range(a, P)
+            self._s_bottom_bwd()
+            if split:
+                self._dense_update_range(0, a)
+            else:
+                self._s_dense_update()
+
+        return {"E1": e1, "E2": emb.stage_bwd_prepare, "M1": self._s_bottom_fwd,
+                "M2": self._s_top, "E3": e3, "M3": m3}
+
+    def _capture_streams(self):
+        assert self.world == 1
+        self._mstream = True
+        composed = self.cfg.composed_graphs
+        if composed is None:
+            composed = self.cfg.interaction == "dot"
+        # cross-stream edges recorded without the system-scope fence a default
+        # event record adds (the producing kernels already release to device
+        # scope and no host reads these edges): DLRM-1TB 0.477-0.480 vs
+        # 0.485-0.487 ms/step with torch events
+        ev = [ops.SyncEvent(2) for _ in range(4)]
+        plan = self._ms_plan()
+        se = torch.cuda.Stream(device=self.device)
+        pool = torch.cuda.graph_pool_handle()
+        graphs = {}
+        se.wait_stream(torch.cuda.current_stream())
+        for name in plan:
+            gr = torch.cuda.CUDAGraph(keep_graph=composed)
+            # (the MLP graphs capture on torch's own side stream: capture is
+            # not allowed on the default stream; replays run on any stream)
+            with graph_capture(gr, pool=pool, stream=se if name[0] == "E" else None):
+                plan[name]()
+            graphs[name] = gr
+        if composed:
+            graphs["M"] = ops.ComposedGraph([("graph", graphs["M1"]), ("wait", ev[1]),
+                                             ("graph", graphs["M2"]), ("record", ev[2]),
+                                             ("graph", graphs["M3"])])
+            graphs["EA"] = ops.ComposedGraph([("graph", graphs["E1"]), ("record", ev[1]),
+                                              ("graph", graphs["E2"])])
+        torch.cuda.synchronize()
+        ids_stream = self.cfg.ids_stream
+        if ids_stream is None:
+            ids_stream = composed
+        cs = torch.cuda.Stream(device=self.device) if ids_stream else None
+        self._ms = {"graphs": graphs, "stream": se, "plan": plan, "composed": composed,
+                    "cstream": cs, "ev_e2": ops.SyncEvent(2), "ev_copy": ops.SyncEvent(2),
+                    "e2_recorded": False, "events": ev}
+        self.graph = "streams"
+
+    def _ms_load_ids(self, ids: torch.Tensor, on_device: bool) -> bool:
+        """Per-stream mode: copy this step's ids on the embedding side (the
+        lookup follows the previous step's embedding update on that stream).
+        Returns False when the caller must use the plain fused load."""
+        if not (ids.is_cuda and ids.dtype == torch.int64 and ids.is_contiguous()
+                and ids.numel() == self.ids.numel()):
+            return False
+        se, ev = self._ms["stream"], self._ms["events"][0]
+        main = torch.cuda.current_stream()
+        cs = self._ms.get("cstream")
+        if cs is not None and on_device:
+            # the ids copy on its own stream right behind this step's sort (E2,
+            # the ids' last reader): the next lookup waits on an event that is
+            # already signalled instead of queueing the copy behind the update
+            if self._ms["e2_recorded"]:
+                cs.wait_event(self._ms["ev_e2"])
+            with torch.cuda.stream(cs):
+                self.ids.copy_(ids, non_blocking=True)
+                self._ms["ev_copy"].record(cs)
+            se.wait_event(self._ms["ev_copy"])
+            return True
+        if not on_device:
+            se.wait_stream(main)               # e.g. an H2D the caller ordered on main
+        with torch.cuda.stream(se):
+            self.ids.copy_(ids, non_blocking=True)
+            ev.record(se)
+        if not on_device:
+            main.wait_event(ev)                # dense / labels from the same source
+        return True
+
+    def _ms_step(self):
+        g, se, ev = self._ms["graphs"], self._ms["stream"], self._ms["events"]
+        main = torch.cuda.current_stream()
+        composed = self._ms["composed"]
+        # (this step's ids were copied on the embedding side by load_batch, so
+        # the lookup follows the previous step's embedding update there)
+        with torch.cuda.stream(se):
+            if composed:
+                g["EA"].replay()             # records ev[1] inside
+            else:
+                g["E1"].replay()
+                ev[1].record(se)
+                g["E2"].replay()
+            if self._ms.get("cstream") is not None:
+                self._ms["ev_e2"].record(se)
+                self._ms["e2_recorded"] = True
+        if composed:
+            g["M"].replay()                  # waits for ev[1], records ev[2] inside
+        else:
+            g["M1"].replay()
+            main.wait_event(ev[1])           # pooled embeddings ready
+            g["M2"].replay()
+            ev[2].record(main)
+        with torch.cuda.stream(se):
+            se.wait_event(ev[2])             # embedding gradients ready
+            g["E3"].replay()
+            ev[3].record(se)
+        if not composed:
+            g["M3"].replay()
+        # no end-of-step join: the embedding stream's next work (ids copy,
+        # lookup) is ordered behind this update on that stream, and the next
+        # MLP graphs wait for the next lookup
+
+    def input_streams(self):
+        """Streams that read a batch handed to load_batch (a producer orders
+        its device copies on each, then passes on_device=True)."""
+        main = torch.cuda.current_stream()
+        if self.graph == "streams":
+            cs = self._ms.get("cstream")
+            return [main, self._ms["stream"]] + ([cs] if cs is not None else [])
+        return [main]
+
+    def sync_streams(self):
+        """Order the current stream after all side-stream work of issued steps
+        (embedding updates)."""
+        if self._ms is not None:
+            torch.cuda.current_stream().wait_stream(self._ms["stream"])
+            if self._ms.get("cstream") is not None:
+                torch.cuda.current_stream().wait_stream(self._ms["cstream"])
+        if getattr(self, "_sides", None) is not None:
+            torch.cuda.current_stream().wait_stream(self._sides)

@@ -32,20 +32,6 @@ def gemm(a, a_col, b, b_col, bias=None, relu=False, mask=None, out=None, out32=N
                  ldc32, csum_col)
 
 
-def mlp3_supported(k0: int, n0: int, n1: int, n2: int) -> bool:
-    """Widths the fused three-layer MLP forward kernel is built for."""
-    return bool(_native().mlp3_supported(k0, n0, n1, n2))
-
-
-def mlp3_fwd(x, ws, bs, ys):
-    """ys[l] = relu(ys[l-1] @ ws[l]^T + bs[l]) for three layers (ys[-1] = x),
-    bf16 activations; bs[l] None: bias inside K. One fused launch on GPU."""
-    if _gpu(x):
-        _native().mlp3_fwd(x, ws[0], ws[1], ws[2], bs[0], bs[1], bs[2], ys[0], ys[1], ys[2])
-    else:
-        ref.mlp3_fwd(x, ws, bs, ys)
-
-
 class SyncEvent:
     """A cross-stream event with a chosen release scope (mode 0: default
     system-scope fence, 1: device-scope release, 2: no system fence).
@@ -220,38 +206,20 @@ def linear_dgrad(dy, w, mask=None, out=None):
 # workload: profiles/gemm_step_ab.md). Round-1 in-step A/B (XCD-remapped split-K,
 # direct fp32 slab stores): DLRM 0.621 ms at 256 vs 0.636-0.641 at 512, 0.646
 # at 1024, 0.670 at 128; DCN-v2 2.902 vs 3.003 (512), 3.200 (128).
-_WGRAD_TARGET = int(__import__("os").environ.get("TDFO_WGRAD_TARGET", "512"))
-_WGRAD_MINKT = int(__import__("os").environ.get("TDFO_WGRAD_MINKT", "8"))
+_WGRAD_TARGET = 512
+_WGRAD_MINKT = 8
 
 
-def wgrad_splits(M: int, N: int, K: int, target_blocks: int = 0, slots: int = 0) -> int:
-    """Split-K count for a weight-grad GEMM (K = batch): ~target_blocks blocks,
-    but every split keeps >= 8 K tiles (measured on MI355X: bot/top3 wgrads run
-    18.8 us at 16 splits vs 22.7 us at 64; top1 is best at 8).
-
-    slots > 0: the GEMM runs on the 256x128 one-block-per-CU kernel (DCN-v2,
-    policy 25), with `slots` resident blocks. A 128x128-tile target then
-    leaves CUs idle (U wgrad: 70 tiles x 2 splits = 140 blocks), so the split
-    minimises (block rounds x K tiles per split) + the fp32 slab traffic each
-    extra split adds (written here, read by the optimizer / reduce; priced in
-    K-tile times of ~0.6 us at ~5 TB/s).
-    """
+def wgrad_splits(M: int, N: int, K: int, target_blocks: int = 0) -> int:
+    """Split-K count for a weight-grad GEMM (K = batch): ~target_blocks blocks
+    of 128x128 tiles, but every split keeps >= 8 K tiles (measured on
+    MI355X: bot/top3 wgrads run 18.8 us at 16 splits vs 22.7 us at 64; top1
+    is best at 8)."""
     kt = K // 64
     smax = max(1, kt // _WGRAD_MINKT)
-    if slots > 0:
-        tiles = ((M + 255) // 256) * ((N + 127) // 128)
-        pen = M * N * 8 / 5e12 / 0.6e-6
-        best, best_s = None, 1
-        for s in range(1, smax + 1):
-            cost = -(-tiles * s // slots) * -(-kt // s) + pen * (s - 1)
-            if best is None or cost < best:
-                best, best_s = cost, s
-        return best_s
     target_blocks = target_blocks or _WGRAD_TARGET
     tiles = ((M + 127) // 128) * ((N + 127) // 128)
-    s = max(1, min(smax, -(-target_blocks // tiles)))
-    return s
-
+    return max(1, min(smax, -(-target_blocks // tiles)))
 
 def linear_wgrad(dy, x, out, slab=None, splits=None, accumulate=False):
     """out[N,K] (fp32) = dy^T @ x with dy [M,N], x [M,K]; split-K over M."""
@@ -473,6 +441,17 @@ def cast_bf16(x, y):
         ref.cast_bf16(x, y)
 
 
+def synth_criteo(seed, rank, batch_index, B, rows, pooling, base, dist, alpha, w_dense,
+                 table_bias, dense, ids, label):
+    """One fresh synthetic Criteo batch on the device (csrc/kernels/synthetic.hip),
+    the twin of the C++ host generator; GPU only."""
+    n = int(sum(int(B) * int(x) for x in pooling.tolist())) if not pooling.is_cuda else None
+    if n is not None and ids.numel() != n:
+        raise ValueError(f"synth_criteo: ids has {ids.numel()} entries, batch needs {n}")
+    _native().synth_criteo(int(seed), int(rank), int(batch_index), int(B), rows, pooling, base,
+                           int(dist), float(alpha), w_dense, table_bias, dense, ids, label)
+
+
 def batch_load(dense, x0, ids, ids_dst, label, label_dst):
     """x0[:, :nd] = bf16(dense), ids_dst = ids, label_dst = label (one launch on GPU)."""
     # the fused kernel needs fp32 row-major dense, int64 ids at a 16-B aligned
@@ -606,12 +585,6 @@ def layernorm_fwd(x, n, eps, gamma, beta, y, mean, rstd):
         _native().layernorm_fwd(x, int(n), float(eps), gamma, beta, y, mean, rstd)
     else:
         ref.layernorm_fwd(x, n, eps, gamma, beta, y, mean, rstd)
-
-
-def cu_masked_stream(mask_words) -> int:
-    """Raw handle of a new HIP stream restricted to the CUs in mask_words
-    (wrap with torch.cuda.ExternalStream)."""
-    return int(_native().cu_masked_stream(list(mask_words)))
 
 
 def rank_metrics(h, W, bias, cand, ks, out):

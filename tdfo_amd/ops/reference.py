@@ -733,13 +733,3 @@ def encoder_layer(x, ids, params, H, rate, seed, step, pad_id=0, eps=1e-5):
     return x2 * m(ENC_SITE_BLK, E)
 
 
-def mlp3_fwd(x, ws, bs, ys):
-    """Three ReLU layers, fp32 accumulation, each output rounded to the output
-    dtype and fed to the next layer (the fused kernel's LDS images)."""
-    h = x
-    for w, b, y in zip(ws, bs, ys):
-        v = h.float() @ w.float().t()
-        if b is not None:
-            v = v + b.float()
-        y.copy_(v.clamp_min(0).to(y.dtype))
-        h = y

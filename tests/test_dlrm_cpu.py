@@ -123,21 +123,20 @@ def test_profiling_helpers_cpu():
 
 
 @pytest.mark.parametrize("interaction", ["dot", "dcn"])
-def test_deferred_wgrads_bitwise_equal(interaction, monkeypatch):
+def test_deferred_wgrads_bitwise_equal(interaction):
     """Weight grads deferred past the cross / interaction backward
-    (TDFO_DEFER_WGRAD, default on for DCN-v2) change only the issue order:
-    parameters after a few steps are bit-identical."""
+    (DLRMConfig.defer_wgrad, default on with more than one rank) change only
+    the issue order: parameters after a few steps are bit-identical."""
     from tdfo_amd.data.synthetic import SyntheticCriteo
     from tdfo_amd.models.dlrm import DLRMConfig, DLRMTrainer
 
-    cfg = DLRMConfig(embedding_dim=32, table_rows=[100, 20, 300], bottom=[64, 32],
-                     top=[64, 32, 1], interaction=interaction, dcn_layers=2, dcn_rank=64,
-                     pooling=[2, 1, 3], dense_lr=1e-2, emb_lr=0.05)
     res = []
-    for flag in ("0", "1"):
-        monkeypatch.setenv("TDFO_DEFER_WGRAD", flag)
+    for flag in (False, True):
+        cfg = DLRMConfig(embedding_dim=32, table_rows=[100, 20, 300], bottom=[64, 32],
+                         top=[64, 32, 1], interaction=interaction, dcn_layers=2, dcn_rank=64,
+                         pooling=[2, 1, 3], dense_lr=1e-2, emb_lr=0.05, defer_wgrad=flag)
         tr = DLRMTrainer(cfg, 64, "cpu")
-        assert tr._defer_top_wgrad == (flag == "1")
+        assert tr._defer_top_wgrad == flag
         data = SyntheticCriteo(cfg.table_rows, 64, pooling=cfg.pooling, device="cpu", seed=5)
         for _ in range(3):
             tr.load_batch(*data.next())

@@ -448,25 +448,19 @@ def test_dlrm_step_matches_cpu():
     assert sum(lg[-5:]) < sum(lg[:5])
 
 
-@pytest.mark.parametrize("staged,one", [(False, "0"), (False, "1"), (False, "early"),
-                                        (False, "ids0"), (True, "0")])
-def test_dlrm_graph_replay_matches_eager(staged, one, monkeypatch):
+@pytest.mark.parametrize("staged,one", [(False, "0"), (False, "1"), (False, "ids0"),
+                                        (True, "0")])
+def test_dlrm_graph_replay_matches_eager(staged, one):
     """Graph-replayed steps match eager ones: per-stream graphs (one=1: each
-    stream's step as composed graphs joined by in-graph event nodes; early:
-    plus the top-MLP optimizer part on the embedding stream right after the
-    top backward; device-resident batches, whose ids the composed mode copies
-    on a third stream behind the sort, ids0: without it) and the staged
-    multi-rank capture at one rank."""
-    monkeypatch.setenv("TDFO_MS_ONE", "0" if one == "0" else "1")
-    # composed graphs copy device-resident ids on their own stream (ids0: not)
-    monkeypatch.setenv("TDFO_IDS_STREAM", "1" if one in ("1", "early") else "0")
-    if one == "early":
-        monkeypatch.setenv("TDFO_SPLIT_OPT", "early")
+    stream's step as composed graphs joined by in-graph event nodes, with
+    device-resident batches whose ids are copied on a third stream behind the
+    sort; ids0: without that stream) and the staged multi-rank capture at one
+    rank."""
     from tdfo_amd.data.synthetic import SyntheticCriteo
     from tdfo_amd.models.dlrm import DLRMConfig, DLRMTrainer
 
     cfg = DLRMConfig(embedding_dim=128, table_rows=[1000, 20, 5000], bottom=[128],
-                     top=[256, 1])
+                     top=[256, 1], composed_graphs=one != "0", ids_stream=one == "1")
     B = 512
     a = DLRMTrainer(cfg, B, DEV)
     b = DLRMTrainer(cfg, B, DEV)
@@ -478,11 +472,10 @@ def test_dlrm_graph_replay_matches_eager(staged, one, monkeypatch):
     b.capture_graph(warmup=1, staged=staged)
     if not staged:
         assert b.graph == "streams" and ("M" in b._ms["graphs"]) == (one != "0")
-        assert ("EB" in b._ms["graphs"]) == (one == "early")
-        assert (b._ms["cstream"] is not None) == (one in ("1", "early"))
+        assert (b._ms["cstream"] is not None) == (one == "1")
     if staged:
         # one rank: the prep stage is a no-op and is not captured (no empty graph)
-        assert all(kind in ("m", "em", "j") or g is not None for kind, g in b.graph)
+        assert all(kind in ("m", "em", "j") or g[0] is not None for kind, g in b.graph)
         assert not b.emb.fwd_prep_noop or len(b._stages()) == 15
     a.step()  # replicate the capture warmup on the eager trainer
     for x in batches[1:]:
@@ -857,38 +850,6 @@ def test_embedding_dense_update_matches_reference(opt, D):
     assert torch.allclose(Wg.cpu(), We, atol=1e-5, rtol=1e-5)
     if opt != ops.EMB_ADAM:
         assert torch.equal(Wg.cpu()[::2], W0[::2])
-
-
-@pytest.mark.parametrize("B", [8192, 1000, 31])
-@pytest.mark.parametrize("strided_out", [False, True])
-def test_mlp3_fused_forward(B, strided_out):
-    """Fused bottom MLP (64 -> 512 -> 256 -> 128, ReLU) vs the fp32 reference
-    layer by layer, and vs the per-layer GEMM launches it replaces; the last
-    output may be a column slice of a wider row (DCN-v2's x_0)."""
-    torch.manual_seed(5)
-    ws = [bf(torch.randn(n, k + 64, device=DEV) / k ** 0.5)[:, :k]
-          for n, k in ((512, 64), (256, 512), (128, 256))]
-    bs = [None, torch.randn(256, 72, device=DEV)[:, 3], torch.randn(128, device=DEV) * 0.1]
-    x = bf(torch.randn(B, 80, device=DEV))[:, :64]
-    wide = torch.zeros(B, 3456, dtype=torch.bfloat16, device=DEV)
-    ys = [torch.empty(B, 576, dtype=torch.bfloat16, device=DEV)[:, :512],
-          torch.empty(B, 320, dtype=torch.bfloat16, device=DEV)[:, :256],
-          wide[:, :128] if strided_out else torch.empty(B, 128, dtype=torch.bfloat16, device=DEV)]
-    ops.mlp3_fwd(x, ws, bs, ys)
-    exp = [torch.empty(B, y.shape[1], dtype=torch.bfloat16, device=DEV) for y in ys]
-    ref.mlp3_fwd(x, ws, bs, exp)
-    for y, e in zip(ys, exp):
-        assert rel_err(y, e) < 2e-2
-    # same numbers as the unfused GEMM chain
-    g = [torch.empty_like(e) for e in exp]
-    h = x
-    for w, b, y in zip(ws, bs, g):
-        ops.gemm(h, False, w, False, b, True, None, y, None, 1)
-        h = y
-    for y, e in zip(ys, g):
-        assert rel_err(y, e) < 1e-2
-    if strided_out:
-        assert wide[:, 128:].abs().sum() == 0
 
 
 @pytest.mark.parametrize("M", [8192, 1000])

@@ -20,7 +20,7 @@ STEPS = 3
 
 
 def _worker(rank, world, Bk, strategy, graph, rw_comm, emb_opt="rowwise_adagrad", pipeline=False,
-            dist="uniform", alpha=1.05, rw_capacity=1.25):
+            dist="uniform", alpha=1.05, rw_capacity=1.25, pipe_lookup=True):
     """dist="zipf": the two eager steps see uniform ids, the graph-replayed
     ones power-law ids -- the row-wise capacity then has to grow after the
     capture (eager rest of that step, re-capture)."""
@@ -32,7 +32,7 @@ def _worker(rank, world, Bk, strategy, graph, rw_comm, emb_opt="rowwise_adagrad"
     cfg = DLRMConfig(embedding_dim=64, table_rows=ROWS, bottom=[128, 64], top=[128, 64, 1],
                      dense_opt="sgd", dense_lr=0.05, emb_lr=0.05, sharding=strategy,
                      pooling=POOL, rw_comm=rw_comm, emb_opt=emb_opt, pipeline=pipeline,
-                     rw_capacity=rw_capacity)
+                     rw_capacity=rw_capacity, pipeline_lookup=pipe_lookup)
     tr = DLRMTrainer(cfg, Bk, dev, group=get_info().group, rank=rank, world_size=world)
     g = torch.Generator().manual_seed(5)
     for t, r in enumerate(ROWS):
@@ -166,14 +166,14 @@ def test_two_ranks_match_one_process(strategy, graph, rw_comm, emb_opt, single):
 @pytest.mark.parametrize("strategy,rw_comm,pipe_lookup", [
     ("table_wise", "bf16", "1"), ("auto", "bf16", "1"), ("row_wise", "fp32", "1"),
     ("data_parallel", "bf16", "1"), ("auto", "bf16", "0")])
-def test_two_ranks_pipelined_input_dist(strategy, rw_comm, pipe_lookup, single, monkeypatch):
+def test_two_ranks_pipelined_input_dist(strategy, rw_comm, pipe_lookup, single):
     """Input-dist pipelining (next batch's ids exchanged during the dense
-    update; TDFO_PIPE_LOOKUP=1: also its lookup and pooled-embedding exchange
+    update; pipeline_lookup: also its lookup and pooled-embedding exchange
     on the side stream in the step's tail) on the staged hipGraphs: same
     result as one process."""
-    monkeypatch.setenv("TDFO_PIPE_LOOKUP", pipe_lookup)
     multi = run_distributed(_worker, 2, B, strategy, True, rw_comm, "rowwise_adagrad", True,
-                            device="cuda", timeout=600)
+                            "uniform", 1.05, 1.25, pipe_lookup == "1", device="cuda",
+                            timeout=600)
     p1, tabs1, loss1 = single("rowwise_adagrad")
     tol = 3e-3
     loss = multi[0][2] + multi[1][2]

@@ -98,7 +98,8 @@ def test_sharded_embedding_fwd_bwd(strategy, world, dp_dense):
 
 
 def _dlrm_worker(rank, world, B, steps, strategy, emb_opt="rowwise_adagrad", rw_comm="fp32",
-                 pipeline=False, dense_comm="fp32", dist="uniform", alpha=1.05, rw_capacity=1.25):
+                 pipeline=False, dense_comm="fp32", dist="uniform", alpha=1.05, rw_capacity=1.25,
+                 pipe_lookup=True):
     from tdfo_amd.data.synthetic import SyntheticCriteo
     from tdfo_amd.models.dlrm import DLRMConfig, DLRMTrainer
     from tdfo_amd.parallel.dist import get_info
@@ -106,7 +107,7 @@ def _dlrm_worker(rank, world, B, steps, strategy, emb_opt="rowwise_adagrad", rw_
     cfg = DLRMConfig(embedding_dim=32, table_rows=ROWS, bottom=[64, 32], top=[64, 32, 1],
                      dense_lr=1e-2, emb_lr=0.05, sharding=strategy, pooling=[1, 2, 1, 1, 1],
                      emb_opt=emb_opt, rw_comm=rw_comm, pipeline=pipeline, dense_comm=dense_comm,
-                     rw_capacity=rw_capacity)
+                     rw_capacity=rw_capacity, pipeline_lookup=pipe_lookup)
     tr = DLRMTrainer(cfg, B, "cpu", group=get_info().group, rank=rank, world_size=world)
     assert tr.pipeline == (pipeline and world > 1)
     g = torch.Generator().manual_seed(5)
@@ -165,16 +166,16 @@ def test_dlrm_data_parallel_matches_single_process(strategy):
 
 @pytest.mark.parametrize("strategy", ["table_wise", "row_wise", "auto"])
 @pytest.mark.parametrize("pipe_lookup", ["1", "0"])
-def test_dlrm_pipelined_input_dist_is_exact(strategy, pipe_lookup, monkeypatch):
+def test_dlrm_pipelined_input_dist_is_exact(strategy, pipe_lookup):
     """Input-dist pipelining (next batch's ids exchanged during this step's
-    dense update; with TDFO_PIPE_LOOKUP=1 also its lookup and pooled-embedding
+    dense update; with pipeline_lookup also its lookup and pooled-embedding
     exchange, after this step's embedding update) changes only when the
     exchanges run: parameters and tables after 4 steps equal the unpipelined
     run bit for bit."""
-    monkeypatch.setenv("TDFO_PIPE_LOOKUP", pipe_lookup)
     B, steps = 8, 4
     plain = run_distributed(_dlrm_worker, 2, B, steps, strategy, "rowwise_adagrad", "fp32", False)
-    piped = run_distributed(_dlrm_worker, 2, B, steps, strategy, "rowwise_adagrad", "fp32", True)
+    piped = run_distributed(_dlrm_worker, 2, B, steps, strategy, "rowwise_adagrad", "fp32", True,
+                            "fp32", "uniform", 1.05, 1.25, pipe_lookup == "1")
     for rank in range(2):
         p0, tabs0, _ = plain[rank]
         p1, tabs1, _ = piped[rank]
