@@ -49,13 +49,19 @@ def parse(argv=None):
     ap.add_argument("--pool", type=int, default=8, help="--data pool: batches in the pool")
     ap.add_argument("--dist", default="uniform", choices=["uniform", "zipf"])
     ap.add_argument("--sharding", default="auto",
-                    choices=["auto", "table_wise", "row_wise", "column_wise", "data_parallel"])
+                    choices=["auto", "table_wise", "row_wise", "column_wise", "data_parallel",
+                             "replicated"])
     ap.add_argument("--dense-comm", default="fp32", choices=["fp32", "bf16"],
                     help="N > 1: wire format of the dense-gradient all-reduce")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="N > 1: exchange each batch's ids inside its own step instead of "
                          "during the previous step's dense update")
     ap.add_argument("--host-data", action="store_true", help="same as --data host")
+    ap.add_argument("--emulate-world", type=int, default=0, metavar="W",
+                    help="one GPU runs rank 0 of the W-rank job: the real W-rank plan, layouts "
+                         "and kernels, each collective replaced by device copies of the same "
+                         "byte count (parallel/comm.py LoopbackComm); reports device ms/step, "
+                         "host issue us/step and the collective volume (not the headline)")
     args = ap.parse_args(argv)
     if args.host_data:
         args.data = "host"
@@ -124,8 +130,16 @@ def main(argv=None):
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     if world_env != args.gpus:
         raise SystemExit(f"error: --gpus {args.gpus} but WORLD_SIZE={world_env}")
+    if args.emulate_world and args.gpus != 1:
+        raise SystemExit("error: --emulate-world runs in one process (--gpus 1)")
     info = init_distributed("cuda")
     world = info.world_size
+    group = info.group
+    if args.emulate_world > 1:
+        from tdfo_amd.parallel.comm import LoopbackComm
+        world = args.emulate_world
+        group = LoopbackComm(world, 0, info.device)
+        world_env = world
     if not _ext.load():
         raise RuntimeError("native HIP library failed to load")
     if os.environ.get("TDFO_GEMM_POLICY"):      # override the trainer's per-model choice
@@ -148,67 +162,38 @@ def main(argv=None):
         # releases a slot after all of them: a third (ids) stream ties the
         # slot to the sort and stalls the prefetch (0.604 vs 0.470 ms/step)
         cfg.ids_stream = False
-    tr = DLRMTrainer(cfg, B, info.device, group=info.group, rank=info.rank, world_size=world)
-    pool = pf = None
-    if args.data == "host":
-        from tdfo_amd.data.prefetch import host_prefetcher
-        pf = host_prefetcher(cfg.table_rows, B, info.device, pooling=cfg.pooling_factors(),
-                             seed=1, rank=info.rank, dist=args.dist, threads=8)
-    elif args.data == "fresh":
-        from tdfo_amd.data.synthetic import DeviceSyntheticStream
-        pf = DeviceSyntheticStream(cfg.table_rows, B, info.device, pooling=cfg.pooling_factors(),
-                                   seed=1, rank=info.rank, dist=args.dist)
-    else:
+    tr = DLRMTrainer(cfg, B, info.device, group=group, rank=info.rank, world_size=world)
+    from tdfo_amd.train.loop import PoolBatches, StepLoop, make_source
+    if args.data == "pool":
         data = SyntheticCriteo(cfg.table_rows, B, pooling=cfg.pooling_factors(),
                                device=info.device, seed=1, rank=info.rank, dist=args.dist)
-        pool = [data.next() for _ in range(args.pool)]
+        src = PoolBatches([data.next() for _ in range(args.pool)])
+    else:
+        src = make_source(cfg.table_rows, B, info.device, cfg.pooling_factors(), 1, info.rank,
+                          dist=args.dist, kind=args.data)
+    loop = StepLoop(tr, src)
     torch.cuda.synchronize()
     setup_s = time.time() - t0
     use_graph = not args.no_graph
 
-    def feed(i):
-        """Hand batch i to the trainer (pipelined: as the batch the next step
-        runs on -- this step loads it after its embedding update)."""
-        if pool is None:                       # streamed: generation (+ H2D) overlapped
-            # the batch is ordered on every stream that reads it
-            batch, slot = pf.next(streams=None if tr.pipeline else tr.input_streams())
-        else:
-            batch, slot = pool[i % len(pool)], None
-        if tr.pipeline:
-            tr.set_next_batch(*batch)
-        else:
-            tr.load_batch(*batch, on_device=True)
-        return slot
-
-    def run(n, start):
-        for i in range(n):
-            slot = feed(start + i + 1 if tr.pipeline else start + i)
-            tr.step()
-            if slot is not None:               # the step has enqueued its reads of it
-                pf.release(slot, streams=None if tr.pipeline else tr.input_streams())
-
-    if tr.pipeline:
-        if pool is None:
-            b0, s0 = pf.next()
-            tr.prime(*b0)
-            pf.release(s0)
-        else:
-            tr.prime(*pool[0])
-    run(args.warmup, 0)
+    loop.run(args.warmup)
     if use_graph:
         tr.capture_graph(warmup=1)
     torch.cuda.synchronize()
     tr.pop_loss()
-    if world > 1:
+    if info.world_size > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
+    if tr.comm is not None:
+        tr.comm.reset_stats()
     t = time.perf_counter()
-    run(args.steps, args.warmup)
+    loop.run(args.steps)
+    host_s = time.perf_counter() - t          # issue time (the device runs behind)
     torch.cuda.synchronize()
-    if world > 1:
+    if info.world_size > 1:
         torch.distributed.barrier()
     el = time.perf_counter() - t
-    if world > 1:
+    if info.world_size > 1:
         x = torch.tensor([el], dtype=torch.float64, device=info.device)
         torch.distributed.all_reduce(x, op=torch.distributed.ReduceOp.MAX)
         el = float(x.item())
@@ -216,9 +201,28 @@ def main(argv=None):
     ms = el / args.steps * 1e3
     value = B * world * args.steps / el
     sol = cfg.sol(B, world)
+    comm = ({k: {"calls_per_step": round(c / args.steps, 2),
+                 "MB_per_step": round(b / args.steps / 1e6, 3)}
+             for k, (c, b) in sorted(tr.comm.stats.items())} if tr.comm is not None else {})
+    if args.emulate_world > 1:
+        print(json.dumps({
+            "metric": f"emulated rank-0 step of the {world}-rank job (loopback collectives)",
+            "value": round(ms, 4), "unit": "ms/step", "higher_is_better": False,
+            "emulated_world": world, "steps": args.steps, "warmup": args.warmup,
+            "host_issue_us_per_step": round(host_s / args.steps * 1e6, 1),
+            "sol_ms_compute": round(cfg.sol(B, 1)["sol_ms"], 4),
+            "sol_comm_ms": round(sol["comm_ms"], 4), "comm": comm,
+            "plan": tr.plan.summary(), "graph": use_graph, "pipeline": tr.pipeline,
+            "data": args.data, "config": {"model": "DLRM" if args.model == "dlrm" else "DCN-v2",
+                                          "tables": f"criteo-{args.rows}", "per_gpu_batch": B}}),
+              flush=True)
+        reset()
+        return
     if info.rank == 0:
         print(json.dumps({"plan": tr.plan.summary(), "setup_s": round(setup_s, 1),
                           "train_loss": round(loss, 4), "graph": use_graph,
+                          "host_issue_us_per_step": round(host_s / args.steps * 1e6, 1),
+                          "comm": comm,
                           "dense_tflops": round(cfg.dense_flops_per_example() * value / 1e12, 1),
                           "sol": {k: round(v, 4) for k, v in sol.items()}}),
               file=sys.stderr)

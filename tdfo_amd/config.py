@@ -25,6 +25,7 @@ except ModuleNotFoundError:  # pragma: no cover - py3.10
 @dataclass
 class ShardingConfig:
     strategy: str = "auto"            # auto | table_wise | row_wise | column_wise | data_parallel
+    #                                   | replicated
     hbm_gb: float = 288.0
     reserve_frac: float = 0.15
     dp_max_mb: float = 0.0

@@ -6,8 +6,9 @@ The role of the reference's ``prefetch_to_device(size=2)``
 (csrc/data/synthetic.cpp, or any host batch source with the same
 ``batch(i)`` contract) fills pinned host slots on a background thread,
 ``lookahead`` batches ahead; each batch is copied host -> device on a
-dedicated copy stream into one of two device staging slots, and the compute
-stream only waits on that copy's event. The trainer's ``load_batch`` then
+dedicated copy stream into one of ``stages`` rotating device staging slots
+(default 6: deep enough that the host polling loop never has to block), and
+the compute stream only waits on that copy's event. The trainer's ``load_batch`` then
 moves staging -> its static (graph-captured) inputs with one fused kernel,
 so the H2D of batch i+1 overlaps step i.
 

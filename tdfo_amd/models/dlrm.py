@@ -28,11 +28,11 @@ from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
 
 import torch
-import torch.distributed as dist
 
 from ..utils.capture import graph_capture
 from .. import ops
 from .dlrm_streams import StreamGraphsMixin
+from ..parallel.comm import as_comm
 from ..sparse.planner import ShardingPlan, plan_sharding
 from ..sparse.sharded import ShardedEmbeddingBags
 from ..sparse.tables import EmbOptimConfig, TableConfig
@@ -242,6 +242,7 @@ class DLRMTrainer(StreamGraphsMixin):
         self.B = B = int(batch_size)
         self.device = dev = torch.device(device)
         self.group = group
+        self.comm = as_comm(group) if world_size > 1 else None
         self.rank = rank
         self.world = world_size
         D = cfg.embedding_dim
@@ -257,7 +258,7 @@ class DLRMTrainer(StreamGraphsMixin):
         self.plan = plan or plan_sharding(tables, world_size, optim, batch_per_rank=B,
                                           pooling=cfg.pooling_factors(), strategy=cfg.sharding)
         self.emb = ShardedEmbeddingBags(tables, self.plan, rank, B, cfg.pooling_factors(), dev,
-                                        optim, group=group, seed=cfg.seed,
+                                        optim, group=self.comm, seed=cfg.seed,
                                         rw_capacity=cfg.rw_capacity, rw_comm=cfg.rw_comm)
         # ------------------------------------------------------ dense params
         fp = FlatParams()
@@ -291,7 +292,7 @@ class DLRMTrainer(StreamGraphsMixin):
         self._ar_split = fp.offset(self.top_layers[0].name + ".w")
         self._init_dense()
         if world_size > 1:                            # replicated dense arch
-            dist.broadcast(fp.p, src=0, group=group)
+            self.comm.broadcast(fp.p, src=0)
         fp.sync_bf16()
         self._defer_top_wgrad = (world_size > 1 if cfg.defer_wgrad is None
                                  else bool(cfg.defer_wgrad))
@@ -777,8 +778,8 @@ class DLRMTrainer(StreamGraphsMixin):
                                         device=self.device)
             b = self._g16[lo:hi]
             ops.cast_bf16(g, b)
-            return (dist.all_reduce(b, group=self.group, async_op=True), g, b)
-        return (dist.all_reduce(g, group=self.group, async_op=True), None, None)
+            return (self.comm.all_reduce(b, async_op=True), g, b)
+        return (self.comm.all_reduce(g, async_op=True), None, None)
 
     def _m_allreduce_top_start(self):
         self._ar_top = None
@@ -994,6 +995,16 @@ class DLRMTrainer(StreamGraphsMixin):
         v = float(self.loss_sum.item())
         self.loss_sum.zero_()
         return v
+
+    def drain(self):
+        """Pipelined trainer: wait (device-side) for the next batch's in-flight
+        id / pooled-embedding exchanges and the side stream, so the static
+        buffers can be reused (eval); ``prime`` restarts the pipeline."""
+        if self.pipeline:
+            self.emb.ids_exchange_wait()
+            if self.emb._pending is not None:
+                self.emb.forward_wait()
+        self.sync_streams()
 
     # ------------------------------------------------------------ eval
     @torch.no_grad()

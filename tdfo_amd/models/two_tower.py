@@ -134,8 +134,11 @@ class TwoTowerTrainer:
             plan = plan_sharding(tabs, world_size, emb_opt, batch_per_rank=self.B,
                                  pooling=[1] * len(rows), strategy=emb_sharding)
             self.plan = plan
+            # fp32 pooled rows and gradients end to end: the towers are an
+            # fp32 model (the reference's TF PS variables return fp32 rows)
             self.sharded = ShardedEmbeddingBags(tabs, plan, rank, self.B, [1] * len(rows), dev,
-                                                emb_opt, group=group, seed=cfg.seed)
+                                                emb_opt, group=group, seed=cfg.seed,
+                                                recv_dtype="fp32")
             # same initial tables as the replicated path (seeded full tables)
             for t in range(len(rows)):
                 self.sharded.set_table_weight(t, init_store.table_weight(t))
@@ -389,6 +392,36 @@ class TwoTowerTrainer:
         for t, v in zip(self._state_tensors(), saved):   # warmup must not train
             t.copy_(v)
         self.graph = g
+
+    def capture_execution(self, cols: Dict[str, torch.Tensor], k: int):
+        """``steps_per_execution = k`` (the reference's Keras
+        ``steps_per_execution``, tensorflow2/train.py:14-18): one hipGraph
+        holds k consecutive (HBM gather + training step) pairs reading their
+        rows from a static index buffer, so one index copy and one replay
+        issue k steps. Needs the one-step graph to exist (its capture ran the
+        warmup that sizes every workspace)."""
+        assert self.graph is not None and k > 1
+        B = self.B
+        self._exec_idx = torch.zeros(k * B, dtype=torch.int64, device=self.device)
+        self._exec_cols = cols
+        g = torch.cuda.CUDAGraph()
+        with graph_capture(g):
+            for j in range(k):
+                self.load_columns(cols, self._exec_idx[j * B:(j + 1) * B], 0, B)
+                self._step_local(B)
+        torch.cuda.synchronize()
+        self._exec_graph, self._exec_k = g, k
+
+    def run_execution(self, idxs: List[torch.Tensor]):
+        """Run len(idxs) == k full steps (rows idxs[j] of the columns given to
+        ``capture_execution``) with one replay."""
+        k, B = self._exec_k, self.B
+        assert len(idxs) == k and all(int(i.numel()) == B for i in idxs)
+        for j, ix in enumerate(idxs):
+            self._exec_idx[j * B:(j + 1) * B].copy_(ix, non_blocking=True)
+        self._exec_graph.replay()
+        self._cur_b = B
+        self.n_seen += k * B
 
     def _state_tensors(self):
         ts = [self.P, self.M, self.V, self.hyper, self.emb_hyper, self.emb.weight, self.loss_sum,

@@ -1,0 +1,260 @@
+"""Collective layer of the sharded engine and the DLRM trainer.
+
+Every exchange the north-star step makes goes through a ``Comm``: the
+pooled-embedding / id all-to-alls, the row-wise reduce-scatter and
+all-gathers, the bucketed dense-gradient all-reduce and the capacity MAX
+all-reduce (the reference's equivalents: TorchRec DMP's input/output dists
+and the DDP reducer, torchrec/train.py:241-260; TF PS pulls/pushes,
+tensorflow2/train_ps.py:55-61).
+
+Two implementations:
+
+* ``ProcessGroupComm``: a torch.distributed group -- RCCL over xGMI on
+  MI355X (the "nccl" backend), gloo on CPU. Collectives run on the process
+  group's own stream; ``async_op`` handles make the caller's current stream
+  wait device-side (never the host).
+* ``LoopbackComm``: rank ``rank`` of a ``world``-rank job emulated in one
+  process (``bench.py --emulate-world 8``): the real W-rank plan, layouts and
+  kernels run, and each collective becomes device copies of the same byte
+  count on a dedicated comm stream, with the data of this rank's own
+  segment replicated into every peer's slot (so exchanged ids stay valid row
+  ids of the tables this rank owns). Device time per step then shows every
+  W-dependent kernel cost and the host time per step the full issue cost of
+  the multi-rank step, without needing W GPUs.
+
+Both count calls and bytes per kind (``stats``), so a step's collective
+volume is reported next to its time.
+"""
+from __future__ import annotations
+
+from collections import defaultdict
+from typing import List, Optional, Sequence
+
+import torch
+import torch.distributed as dist
+
+
+class _Done:
+    def wait(self):
+        return None
+
+
+class _EventWork:
+    """Handle of a collective enqueued on a comm stream: ``wait`` orders the
+    caller's current stream after it (device-side)."""
+
+    def __init__(self, ev):
+        self.ev = ev
+
+    def wait(self):
+        torch.cuda.current_stream().wait_event(self.ev)
+
+
+def _splits(n: int, W: int, splits: Optional[Sequence[int]]) -> List[int]:
+    if splits is None:
+        assert n % W == 0, f"equal-split exchange of {n} elements over {W} ranks"
+        return [n // W] * W
+    s = [int(x) for x in splits]
+    assert len(s) == W and sum(s) == n, (s, n, W)
+    return s
+
+
+class Comm:
+    """Collective interface (subclasses implement the ``_``-prefixed ops)."""
+
+    world: int = 1
+    rank: int = 0
+
+    def __init__(self):
+        self.stats = defaultdict(lambda: [0, 0])     # kind -> [calls, bytes moved by this rank]
+
+    def _count(self, kind: str, t: torch.Tensor):
+        s = self.stats[kind]
+        s[0] += 1
+        s[1] += t.numel() * t.element_size()
+
+    def reset_stats(self):
+        self.stats.clear()
+
+    # -- public API (counting wrappers)
+    def all_to_all(self, out, inp, out_splits=None, in_splits=None, async_op=False):
+        """out[slot r] = what rank r sends here; inp[slot r] goes to rank r."""
+        self._count("all_to_all", inp)
+        return self._all_to_all(out, inp, out_splits, in_splits, async_op)
+
+    def all_gather(self, out, inp, async_op=False):
+        """out = concat over ranks of inp (rank-major)."""
+        self._count("all_gather", out)
+        return self._all_gather(out, inp, async_op)
+
+    def reduce_scatter(self, out, inp, async_op=False):
+        """out = sum over ranks of their inp chunk [rank] (equal chunks)."""
+        self._count("reduce_scatter", inp)
+        return self._reduce_scatter(out, inp, async_op)
+
+    def all_reduce(self, t, op: str = "sum", async_op=False):
+        self._count("all_reduce_" + op, t)
+        return self._all_reduce(t, op, async_op)
+
+    def broadcast(self, t, src: int = 0):
+        self._count("broadcast", t)
+        return self._broadcast(t, src)
+
+    def barrier(self):
+        return None
+
+
+class ProcessGroupComm(Comm):
+    """torch.distributed group (RCCL on MI355X, gloo on CPU)."""
+
+    def __init__(self, group=None):
+        super().__init__()
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.backend = dist.get_backend(group) if dist.is_initialized() else None
+
+    def _all_to_all(self, out, inp, out_splits, in_splits, async_op):
+        if out_splits is None and in_splits is None and not (inp.is_cuda and self.backend == "gloo"):
+            return dist.all_to_all_single(out, inp, group=self.group, async_op=async_op)
+        # explicit splits: gloo's equal-split device all-to-all mangles bf16
+        # (measured on the shared-GPU rehearsal); the split-size form is exact
+        os_ = _splits(out.numel(), self.world, out_splits)
+        is_ = _splits(inp.numel(), self.world, in_splits)
+        return dist.all_to_all_single(out, inp, output_split_sizes=os_, input_split_sizes=is_,
+                                      group=self.group, async_op=async_op)
+
+    def _all_gather(self, out, inp, async_op):
+        return dist.all_gather_into_tensor(out, inp, group=self.group, async_op=async_op)
+
+    def _reduce_scatter(self, out, inp, async_op):
+        if inp.is_cuda and self.backend == "gloo":
+            # gloo has no device reduce-scatter (shared-GPU rehearsal backend):
+            # an all-to-all of the chunks + an in-order sum
+            W = self.world
+            tmp = torch.empty_like(inp)
+            n = inp.numel() // W
+            self._all_to_all(tmp, inp, [n] * W, [n] * W, False)
+            out.copy_(tmp.view(W, -1).float().sum(0))
+            return _Done()
+        return dist.reduce_scatter_tensor(out, inp, group=self.group, async_op=async_op)
+
+    def _all_reduce(self, t, op, async_op):
+        rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
+        return dist.all_reduce(t, op=rop, group=self.group, async_op=async_op)
+
+    def _broadcast(self, t, src):
+        return dist.broadcast(t, src=src, group=self.group)
+
+    def barrier(self):
+        if self.world > 1:
+            dist.barrier(group=self.group)
+
+
+class LoopbackComm(Comm):
+    """Rank ``rank`` of a ``world``-rank job in one process (see module doc).
+
+    Data semantics: every peer is taken to send what this rank sends to
+    itself (all-to-all), to hold this rank's tensor (all-gather), and to
+    contribute nothing to a reduction (all-reduce / reduce-scatter keep this
+    rank's values) -- so the numbers stay finite and exchanged ids stay in
+    range. Byte counts per call equal the real collective's."""
+
+    def __init__(self, world: int, rank: int = 0, device=None):
+        super().__init__()
+        assert 0 <= rank < world
+        self.world, self.rank = int(world), int(rank)
+        self.device = torch.device(device) if device is not None else None
+        self._stream = None
+        self._scratch = None
+
+    def _begin(self, t):
+        if not t.is_cuda:
+            return None
+        if self._stream is None:
+            self._stream = torch.cuda.Stream(device=t.device)
+        s = self._stream
+        s.wait_stream(torch.cuda.current_stream(t.device))
+        return s
+
+    def _end(self, s, async_op):
+        if s is None:
+            return _Done()
+        ev = torch.cuda.Event()
+        ev.record(s)
+        w = _EventWork(ev)
+        if not async_op:
+            w.wait()
+            return None
+        return w
+
+    def _all_to_all(self, out, inp, out_splits, in_splits, async_op):
+        W, r = self.world, self.rank
+        os_ = _splits(out.numel(), W, out_splits)
+        is_ = _splits(inp.numel(), W, in_splits)
+        src0 = sum(is_[:r])
+        own = inp.view(-1)[src0: src0 + is_[r]]
+        o = out.view(-1)
+        s = self._begin(inp)
+        with torch.cuda.stream(s) if s is not None else _nullctx():
+            if all(n == own.numel() for n in os_):          # one broadcast copy
+                o.view(W, -1).copy_(own.view(1, -1).expand(W, -1))
+                return self._end(s, async_op)
+            off = 0
+            for n in os_:
+                k = 0
+                while k < n and own.numel():                 # tile this rank's own segment
+                    m = min(own.numel(), n - k)
+                    o[off + k: off + k + m].copy_(own[:m])
+                    k += m
+                off += n
+        return self._end(s, async_op)
+
+    def _all_gather(self, out, inp, async_op):
+        s = self._begin(inp)
+        with torch.cuda.stream(s) if s is not None else _nullctx():
+            out.view(self.world, -1).copy_(inp.view(1, -1).expand(self.world, -1))
+        return self._end(s, async_op)
+
+    def _reduce_scatter(self, out, inp, async_op):
+        n = out.numel()
+        s = self._begin(inp)
+        with torch.cuda.stream(s) if s is not None else _nullctx():
+            # reads all W chunks like the real reduction (their sum would
+            # scale the values W-fold; this rank's own chunk is kept)
+            tmp = inp.view(self.world, -1)[:, :n].sum(0, dtype=torch.float32)
+            out.view(-1).copy_(inp.view(-1)[self.rank * n: (self.rank + 1) * n])
+            del tmp
+        return self._end(s, async_op)
+
+    def _all_reduce(self, t, op, async_op):
+        s = self._begin(t)
+        with torch.cuda.stream(s) if s is not None else _nullctx():
+            if t.numel() > 64:
+                # a ring all-reduce reads and writes the buffer ~2x
+                if self._scratch is None or self._scratch.numel() < t.numel() * t.element_size():
+                    self._scratch = torch.empty(t.numel() * t.element_size(), dtype=torch.uint8,
+                                                device=t.device)
+                sc = self._scratch[: t.numel() * t.element_size()].view(t.dtype).view(t.shape)
+                sc.copy_(t)
+                t.copy_(sc)
+        return self._end(s, async_op)
+
+    def _broadcast(self, t, src):
+        return None
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def as_comm(group=None) -> Comm:
+    """A ``Comm`` for ``group``: itself if it is one, else the torch process
+    group wrapped (None: the default group, or a one-rank no-op layer)."""
+    if isinstance(group, Comm):
+        return group
+    return ProcessGroupComm(group)

@@ -44,7 +44,10 @@ class ShardedEmbeddingModule(torch.nn.Module):
                  pooling: Optional[Sequence[int]] = None, optim: Optional[EmbOptimConfig] = None,
                  device="cpu", world_size: int = 1, rank: int = 0, group=None,
                  strategy: str = "auto", plan: Optional[ShardingPlan] = None, seed: int = 0,
-                 mean: bool = False):
+                 mean: bool = False, recv_dtype: str = "fp32"):
+        """``recv_dtype``: "fp32" (default: the fp32 models of the reference,
+        whose TBE returns fp32 rows, torchrec/models.py:158-164) or "bf16"
+        (half the exchange bytes)."""
         super().__init__()
         self.tables = list(tables)
         self.pooling = list(pooling) if pooling is not None else [1] * len(self.tables)
@@ -53,7 +56,8 @@ class ShardedEmbeddingModule(torch.nn.Module):
                                           batch_per_rank=batch_size, pooling=self.pooling,
                                           strategy=strategy)
         self.engine = ShardedEmbeddingBags(self.tables, self.plan, rank, batch_size, self.pooling,
-                                           device, self.optim, group=group, seed=seed, mean=mean)
+                                           device, self.optim, group=group, seed=seed, mean=mean,
+                                           recv_dtype=recv_dtype)
         self.engine._hyper = torch.tensor([self.optim.lr, 0.0], dtype=torch.float32,
                                           device=device)
         # a differentiable anchor so autograd always calls backward

@@ -22,11 +22,22 @@ table) and of TF's MinSizePartitioner for the parameter-server path
 
 Sharding kinds:
   table_wise   whole table on one rank (pooled-embedding all-to-all)
-  row_wise     rows split in contiguous blocks across all ranks (id
-               bucketize + all-to-all of ids, owner-side pooling, bf16
+  row_wise     rows dealt round-robin across all ranks (owner = id mod W;
+               id bucketize + all-to-all of ids, owner-side pooling, bf16
                reduce-scatter of the pooled partials)
   column_wise  D split across ranks; each column block is a table-wise shard
-  data_parallel  replicated (tiny tables; gradient all-reduce)
+  data_parallel  replicated (small tables; dense-gradient all-reduce)
+
+Strategies: "data_parallel" (config 3, the reference's pmap / Mirrored /
+DDP data parallelism, jax-flax/train_dp.py:63, tensorflow2/train_dp.py:71-72)
+replicates every table up to ``dp_replicate_max_bytes`` (256 MB: its dense
+fp32 gradient all-reduce is cheap and its update is the same dense pass on
+every rank) and owner-partitions the larger ones as row-wise shards: an exact
+replica of a big table would make every rank apply the whole global batch's
+update (W x the one-GPU work, plus W x B pooled gradients gathered), while
+the owner-partitioned table gives the same numbers with each rank updating
+only its 1/W of the rows. "replicated" keeps every table whole on every rank
+(the literal pmap layout; per-rank update work grows with W).
 """
 from __future__ import annotations
 
@@ -81,12 +92,15 @@ def plan_sharding(tables: Sequence[TableConfig], world_size: int, optim: EmbOpti
                   hbm_bytes: int = HBM_BYTES, reserve_frac: float = 0.15,
                   strategy: str = "auto", dp_max_bytes: int = 0,
                   row_cost: Optional[Callable[[int], float]] = None,
-                  dp_max_rows: Optional[int] = None) -> ShardingPlan:
+                  dp_max_rows: Optional[int] = None,
+                  dp_replicate_max_bytes: int = 256 << 20) -> ShardingPlan:
     """Deterministic greedy planner.
 
     strategy: "auto" (table-wise with row-wise fallback for tables that fit
     no rank), "table_wise", "row_wise", "column_wise" (tables split evenly by
-    columns), "data_parallel".
+    columns), "data_parallel" (replicated up to dp_replicate_max_bytes,
+    owner-partitioned row-wise above), "replicated" (every table on every
+    rank).
 
     dp_max_rows: "auto" replicates (data_parallel) every table with fewer
     rows than this (default at W > 1: batch_per_rank // 2 -- a replicated
@@ -138,7 +152,7 @@ def plan_sharding(tables: Sequence[TableConfig], world_size: int, optim: EmbOpti
         blocks = [max(0, min(blk, rows - r * blk)) for r in range(W)]
         per_row = _mem_per_row(tables[t].embedding_dim, optim)
         for r in range(W):
-            mem[r] += (blk + (1 if r == 0 else 0)) * per_row   # padded block + scratch row
+            mem[r] += (blk + 1) * per_row   # padded block + scratch row (every rank)
             cost[r] += rcost(t)
         return TableShard(t, "row_wise", list(range(W)), row_blocks=blocks)
 
@@ -164,7 +178,11 @@ def plan_sharding(tables: Sequence[TableConfig], world_size: int, optim: EmbOpti
         if shards[t] is not None:
             continue
         tb = tables[t].num_embeddings * _mem_per_row(tables[t].embedding_dim, optim)
-        if strategy == "data_parallel" or (strategy == "auto" and (
+        if strategy == "data_parallel" and W > 1 and (
+                tables[t].num_embeddings * tables[t].embedding_dim * 4 > dp_replicate_max_bytes):
+            shards[t] = row_wise(t)                 # owner-partitioned big table
+            continue
+        if strategy in ("data_parallel", "replicated") or (strategy == "auto" and (
                 tb <= dp_max_bytes or tables[t].num_embeddings < dp_max_rows)):
             for r in range(W):
                 mem[r] += tb

@@ -38,35 +38,11 @@ from __future__ import annotations
 from typing import List, Optional, Sequence
 
 import torch
-import torch.distributed as dist
 
+from .. import ops
+from ..parallel.comm import as_comm
 from .planner import ShardingPlan
 from .tables import EmbOptimConfig, TableBatchedEmbedding, TableConfig
-
-
-def _a2a(out, inp, out_splits, in_splits, group, async_op=False):
-    return dist.all_to_all_single(out, inp, output_split_sizes=out_splits,
-                                  input_split_sizes=in_splits, group=group, async_op=async_op)
-
-
-class _Done:
-    def wait(self):
-        return None
-
-
-def _reduce_scatter(out, inp, group, async_op=False):
-    """reduce_scatter_tensor; over gloo with device tensors (the shared-GPU
-    rehearsal backend) it is emulated by an all-to-all + an in-order sum."""
-    if inp.is_cuda and dist.get_backend(group) == "gloo":
-        W = dist.get_world_size(group)
-        tmp = torch.empty_like(inp)
-        # explicit splits: gloo's equal-split device all-to-all mangles bf16
-        # (measured on the shared-GPU rehearsal); the split-size form is exact
-        n = inp.numel() // W
-        _a2a(tmp, inp, [n] * W, [n] * W, group)
-        out.copy_(tmp.view(W, -1).float().sum(0))
-        return _Done()
-    return dist.reduce_scatter_tensor(out, inp, group=group, async_op=async_op)
 
 
 class ShardedEmbeddingBags:
@@ -82,7 +58,8 @@ class ShardedEmbeddingBags:
     def __init__(self, tables: Sequence[TableConfig], plan: ShardingPlan, rank: int,
                  batch_size: int, pooling: Sequence[int], device, optim: EmbOptimConfig,
                  group=None, seed: int = 0, mean: bool = False, rw_capacity: float = 1.25,
-                 rw_comm: str = "bf16", dp_dense_max_bytes: int = 256 << 20):
+                 rw_comm: str = "bf16", dp_dense_max_bytes: int = 256 << 20,
+                 recv_dtype: str = "bf16"):
         """``rw_capacity``: initial per-owner segment capacity of the row-wise
         exchange as a multiple of the uniform share n/W (+256). Before every
         exchange the largest per-owner count is all-reduced and the capacity
@@ -90,7 +67,13 @@ class ShardedEmbeddingBags:
         re-bucketized) when a segment would overflow.
         ``rw_comm``: dtype of the pooled partials' reduce-scatter ("bf16"
         halves the bytes; "fp32" sums exactly as one process would, up to
-        fp32 association)."""
+        fp32 association).
+        ``recv_dtype``: dtype of the pooled rows handed to the model and of
+        their gradients, on the wire too ("bf16": the DLRM path; "fp32": fp32
+        models whose embeddings must not be rounded -- the reference's TBE
+        and TF PS return fp32 rows, torchrec/models.py:158-164,
+        tensorflow2/train_ps.py:55-61; row-wise partials are then summed in
+        fp32 as well)."""
         self.tables = list(tables)
         self.T = len(self.tables)
         dims = {t.embedding_dim for t in self.tables}
@@ -103,6 +86,7 @@ class ShardedEmbeddingBags:
         self.L = [int(x) for x in pooling]
         self.device = torch.device(device)
         self.group = group
+        self.comm = as_comm(group) if plan.world_size > 1 else None
         self.mean = mean
         self.optim = optim
         for s in plan.shards:
@@ -181,7 +165,12 @@ class ShardedEmbeddingBags:
         self.tw_ld = self.dsum[rank]          # row pitch of the pooled TW output (alias_pooled)
         self.pooled_aliased = False
         # buffers
-        bf = torch.bfloat16
+        if recv_dtype not in ("bf16", "fp32"):
+            raise ValueError(f"recv_dtype must be bf16 or fp32, got {recv_dtype!r}")
+        bf = torch.bfloat16 if recv_dtype == "bf16" else torch.float32
+        self.recv_dtype = bf
+        if recv_dtype == "fp32":
+            rw_comm = "fp32"
         self.tw_send_ids = torch.empty(self.nnz_local_tw(), dtype=torch.int64, device=self.device)
         self.tw_recv_ids = torch.empty(W * self.tw_recv_count, dtype=torch.int64, device=self.device)
         self.tw_pooled = torch.empty(max(1, W * B * self.dsum[rank]), dtype=bf, device=self.device)
@@ -258,7 +247,7 @@ class ShardedEmbeddingBags:
             self.rw_grows = 0
             self.rw_starts = torch.zeros(W * (self.nrw * B + 1), dtype=torch.int32,
                                          device=self.device)
-            bf_ = torch.bfloat16
+            bf_ = bf
             if rw_comm not in ("bf16", "fp32"):
                 raise ValueError(f"rw_comm must be bf16 or fp32, got {rw_comm}")
             cdt = bf_ if rw_comm == "bf16" else torch.float32
@@ -266,7 +255,7 @@ class ShardedEmbeddingBags:
                             if W > 1 else None)
             # fp32 partials are reduced into an fp32 landing buffer, then cast
             self.rw_rs32 = (torch.zeros(B * self.rw_width, dtype=cdt, device=self.device)
-                            if W > 1 and cdt == torch.float32 else None)
+                            if W > 1 and cdt == torch.float32 and bf != torch.float32 else None)
             self.rw_gbuf = (torch.zeros(W * B * self.rw_width, dtype=bf_, device=self.device)
                             if W > 1 else None)
             self._rw_alloc(self.rw_capacity(n, W, rw_capacity))
@@ -300,8 +289,12 @@ class ShardedEmbeddingBags:
             # rank's fused backward writes a dense fp32 gradient, one
             # all-reduce sums it and every rank takes the same dense step --
             # per-rank work and bytes independent of the batch size and W
+            # (only for optimizers whose zero-gradient update is a no-op: Adam's
+            # moment decay or weight decay would touch rows the batch never saw)
             dp_bytes = self.dp_store.total_rows * D * 4
-            self.dp_dense = W > 1 and dp_bytes <= dp_dense_max_bytes
+            zero_noop = (optim.code in (ops.EMB_SGD, ops.EMB_ADAGRAD, ops.EMB_ROWWISE_ADAGRAD)
+                         and optim.weight_decay == 0.0)
+            self.dp_dense = W > 1 and dp_bytes <= dp_dense_max_bytes and zero_noop
             if self.dp_dense:
                 self.dp_dgrad = torch.zeros(self.dp_store.total_rows, D, dtype=torch.float32,
                                             device=self.device)
@@ -421,7 +414,7 @@ class ShardedEmbeddingBags:
         larger segments, so no lookup is dropped whatever the id skew."""
         need = self.rw_overflow[1:2].clone()
         if self.world > 1:
-            dist.all_reduce(need, op=dist.ReduceOp.MAX, group=self.group)
+            self.comm.all_reduce(need, "max")
         need = int(need.item())
         if need <= self.rw_cap:
             return
@@ -445,7 +438,7 @@ class ShardedEmbeddingBags:
             return
         flag = self.rw_overflow[:1].clone()
         if self.world > 1:
-            dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group)
+            self.comm.all_reduce(flag, "max")
         if int(flag.item()):
             raise RuntimeError(
                 f"row-wise exchange capacity exceeded (cap {self.rw_cap} ids per owner, "
@@ -519,19 +512,19 @@ class ShardedEmbeddingBags:
         W = self.world
         works = []
         if self.dp_tables and W > 1 and not self.dp_dense:
-            works.append(dist.all_gather_into_tensor(self.dp_g_ids, self.dp_ids, group=self.group,
-                                                     async_op=async_op))
+            works.append(self.comm.all_gather(self.dp_g_ids, self.dp_ids, async_op=async_op))
         if W > 1 and not self.tw_identity:
-            works.append(_a2a(self.tw_recv_ids, self.tw_send_ids, [self.tw_recv_count] * W,
-                              self.tw_send_counts, self.group, async_op=async_op))
+            works.append(self.comm.all_to_all(self.tw_recv_ids, self.tw_send_ids,
+                                              [self.tw_recv_count] * W, self.tw_send_counts,
+                                              async_op=async_op))
         if W > 1 and self.cw_tables:
-            works.append(_a2a(self.cw_recv_ids, self.cw_send_ids, [self.cw_recv_count] * W,
-                              self.cw_send_counts, self.group, async_op=async_op))
+            works.append(self.comm.all_to_all(self.cw_recv_ids, self.cw_send_ids,
+                                              [self.cw_recv_count] * W, self.cw_send_counts,
+                                              async_op=async_op))
         if W > 1 and self.rw_tables:
             if self.rw_dynamic:
                 self._rw_check_capacity()
-            works.append(dist.all_to_all_single(self.rw_recv, self.rw_send, group=self.group,
-                                                async_op=async_op))
+            works.append(self.comm.all_to_all(self.rw_recv, self.rw_send, async_op=async_op))
         self._ids_works = [w for w in works if w is not None] if async_op else []
 
     def ids_exchange_wait(self):
@@ -568,13 +561,13 @@ class ShardedEmbeddingBags:
         if W > 1:
             tw_total = sum(self.tw_recv_sizes)
             if tw_total:
-                works.append(_a2a(self.recv[:tw_total],
-                                  self.tw_pooled[: W * B * self.dsum[self.rank]],
-                                  self.tw_recv_sizes, [B * self.dsum[self.rank]] * W, self.group,
-                                  async_op=True))
+                works.append(self.comm.all_to_all(self.recv[:tw_total],
+                                                  self.tw_pooled[: W * B * self.dsum[self.rank]],
+                                                  self.tw_recv_sizes,
+                                                  [B * self.dsum[self.rank]] * W, async_op=True))
             if self.rw_tables:
                 dst = self.rw_rs32 if self.rw_rs32 is not None else self._rw_region(self.recv)
-                works.append(_reduce_scatter(dst, self.rw_pbuf, self.group, async_op=True))
+                works.append(self.comm.reduce_scatter(dst, self.rw_pbuf, async_op=True))
         self._pending = works
 
     def forward_wait(self):
@@ -619,20 +612,20 @@ class ShardedEmbeddingBags:
             self._cw_disassemble(d_recv)
         work = None
         if W > 1:
-            work = _a2a(self.d_pooled[: W * B * self.dsum[self.rank]], d_recv[:tw_total],
-                        [B * self.dsum[self.rank]] * W, self.tw_recv_sizes, self.group,
-                        async_op=True)
+            work = self.comm.all_to_all(self.d_pooled[: W * B * self.dsum[self.rank]],
+                                        d_recv[:tw_total], [B * self.dsum[self.rank]] * W,
+                                        self.tw_recv_sizes, async_op=True)
         self._dp_work = None
         if W > 1 and self.dp_tables and self.dp_dense:
-            self._dp_work = dist.all_reduce(self.dp_dgrad, group=self.group, async_op=True)
+            self._dp_work = self.comm.all_reduce(self.dp_dgrad, async_op=True)
         elif W > 1 and self.dp_tables:
-            self._dp_work = dist.all_gather_into_tensor(
+            self._dp_work = self.comm.all_gather(
                 self.dp_g_grad, d_recv[self.dp_base: self.dp_base + B * self.dp_width],
-                group=self.group, async_op=True)
+                async_op=True)
         self._rw_work = None
         if W > 1 and self.rw_tables:
-            self._rw_work = dist.all_gather_into_tensor(self.rw_gbuf, self._rw_region(d_recv),
-                                                        group=self.group, async_op=True)
+            self._rw_work = self.comm.all_gather(self.rw_gbuf, self._rw_region(d_recv),
+                                                 async_op=True)
         self._bw = (work, d_recv)
 
     def backward_wait(self):

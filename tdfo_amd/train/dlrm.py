@@ -28,7 +28,6 @@ import torch
 
 from .. import ops
 from ..config import Config
-from ..data.synthetic import HostSyntheticCriteo, SyntheticCriteo
 from ..models.dlrm import (CRITEO_1TB_ROWS, CRITEO_KAGGLE_ROWS, DCN_GT1TB_ROWS, MLPERF_MULTIHOT,
                            DLRMConfig, DLRMTrainer)
 from ..parallel.dist import init_distributed
@@ -36,6 +35,7 @@ from ..sparse import tables as _tables
 from ..utils import checkpoint as ckpt
 from ..utils import sharded_ckpt
 from ..utils.profiling import ProfileWindow, StepTimer, trace_range
+from .loop import StepLoop, make_source
 
 TINY_ROWS = [40_000] * 26          # DLRM-tiny: ~1M embedding rows (BASELINE config 1)
 
@@ -59,58 +59,18 @@ def dlrm_config(cfg: Config, strategy: str) -> DLRMConfig:
                       emb_lr=cfg.emb_learning_rate, sharding=strategy, seed=cfg.seed)
 
 
-class _Data:
-    """Per-rank synthetic batch stream; batch i is reproducible after resume.
-
-    CPU: the C++ host generator. GPU: the device generator, or with
-    ``synthetic.host_data`` the C++ generator behind the pinned, copy-stream
-    prefetcher (data/prefetch.py) -- the host data plane a real input
-    pipeline would use."""
-
-    def __init__(self, cfg: Config, dcfg: DLRMConfig, B: int, device, rank: int, seed_off: int,
-                 prefetch: bool = True):
-        self.host = device.type == "cpu"
-        self.pf = None
-        kw = dict(pooling=dcfg.pooling_factors(), seed=cfg.seed, rank=rank,
-                  dist=cfg.synthetic.dist, stream=seed_off)
-        self._args = (cfg, dcfg, B, device, kw)
-        if self.host:
-            self.gen = HostSyntheticCriteo(dcfg.table_rows, B, dcfg.num_dense,
-                                           zipf_alpha=cfg.synthetic.zipf_alpha, threads=4, **kw)
-        elif cfg.synthetic.host_data and prefetch:
-            self.pf = self._prefetcher(0)
-        else:
-            self.gen = SyntheticCriteo(dcfg.table_rows, B, dcfg.num_dense, device=device,
-                                       zipf_alpha=cfg.synthetic.zipf_alpha, **kw)
-        self.device = device
-        self.i = 0
-        self._slot = None
-
-    def _prefetcher(self, start: int):
-        from ..data.prefetch import host_prefetcher
-        cfg, dcfg, B, device, kw = self._args
-        return host_prefetcher(dcfg.table_rows, B, device, num_dense=dcfg.num_dense,
-                               zipf_alpha=cfg.synthetic.zipf_alpha, start=start, **kw)
-
-    def seek(self, i: int):
-        if self.pf is not None:
-            self.pf.close()
-            self.pf = self._prefetcher(i)
-        elif self.host:
-            self.gen.index = i
-        else:                  # device generator: replay the stream
-            for _ in range(i - self.i):
-                self.gen.next()
-        self.i = i
-
-    def next(self):
-        self.i += 1
-        if self.pf is not None:
-            if self._slot is not None:
-                self.pf.release(self._slot)       # previous batch was consumed
-            batch, self._slot = self.pf.next()
-            return batch
-        return self.gen.next()
+def _source(cfg: Config, dcfg: DLRMConfig, B: int, device, rank: int, stream: int,
+            start: int, eval_: bool = False):
+    """Batch source positioned at batch ``start`` (train/loop.py): the C++ host
+    generator on CPU; on a GPU the one-launch device generator (a fresh batch
+    per step on a side stream), or with ``synthetic.host_data`` the C++
+    generator behind the pinned copy-stream prefetcher -- the host data plane
+    a real input pipeline would use. Batch i is reproducible after resume."""
+    kind = "cpu" if device.type == "cpu" else (
+        "host" if cfg.synthetic.host_data and not eval_ else "fresh")
+    return make_source(dcfg.table_rows, B, device, dcfg.pooling_factors(), cfg.seed, rank,
+                       dist=cfg.synthetic.dist, zipf_alpha=cfg.synthetic.zipf_alpha, start=start,
+                       stream=stream, kind=kind, num_dense=dcfg.num_dense)
 
 
 def _log(rank, msg):
@@ -135,13 +95,14 @@ def run(cfg: Config, mode: str = "single", out_dir: str = ".",
     else:
         strategy = cfg.sharding.strategy
     dcfg = dlrm_config(cfg, strategy)
+    # more than one rank: input-dist pipelining, the step bench.py measures
+    dcfg.pipeline = world > 1
     B = cfg.per_device_train_batch_size
     tr = DLRMTrainer(dcfg, B, dev, group=group, rank=rank, world_size=world)
     _log(rank, f"===== model: {cfg.model}, tables: {dcfg.num_tables} "
                f"({sum(dcfg.table_rows):,} rows x {dcfg.embedding_dim}), "
                f"per-device batch {B}, num devices: {world} =====")
     _log(rank, f"===== sharding plan: {json.dumps(tr.plan.summary())} =====")
-    data = _Data(cfg, dcfg, B, dev, rank, 0)
     total_steps = cfg.max_steps or cfg.synthetic.num_batches * cfg.n_epochs
     start = 0
     meta = {"model": cfg.model, "world_size": world, "strategy": strategy,
@@ -155,31 +116,49 @@ def run(cfg: Config, mode: str = "single", out_dir: str = ".",
                 st = ckpt.load_sharded(str(latest), rank, world, expect_meta=meta)
                 tr.load_flat_state(st["tensors"])
                 start = int(st["step"])
-            data.seek(start)
             _log(rank, f"===== resumed from {latest} at step {start} =====")
+    loop = StepLoop(tr, _source(cfg, dcfg, B, dev, rank, 0, start), start)
     metrics_path = cfg.metrics_file
     fault_at = int(os.environ.get("TDFO_FAULT_AT_STEP", "0") or 0)
     fault_rank = int(os.environ.get("TDFO_FAULT_RANK", "0") or 0)
-    use_graph = cfg.hip_graph and dev.type == "cuda" and tr.emb.graph_capturable
+    # jit_xla = false (tensorflow2/train.py:16): eager launches, no hipGraph
+    use_graph = (cfg.hip_graph and cfg.jit_xla is not False and dev.type == "cuda"
+                 and tr.emb.graph_capturable)
+    # steps_per_execution (tensorflow2/train.py:17): steps issued per host
+    # round; logging, checkpoints and the fault hook run between rounds
+    k_exec = max(1, int(cfg.steps_per_execution))
     history: List[Dict] = []
     t0 = time.perf_counter()
     last_t, last_step = t0, start
     step = start
     prof = ProfileWindow(cfg.profile_steps or None)
     timer = StepTimer(enabled=dev.type == "cuda")
+
+    def boundary(s: int) -> int:
+        """Next step count at which the host must look (log / ckpt / fault /
+        graph capture / end), so executions never straddle one."""
+        cands = [total_steps, (s // cfg.log_every + 1) * cfg.log_every]
+        if cfg.ckpt_dir and cfg.ckpt_every:
+            cands.append((s // cfg.ckpt_every + 1) * cfg.ckpt_every)
+        if fault_at and s < fault_at:
+            cands.append(fault_at)
+        if use_graph and tr.graph is None:
+            cands.append(max(s + 1, start + 2))
+        w = prof.win
+        if w is not None:
+            cands += [x for x in (w[0], w[0] + w[1]) if x > s]
+        return min(cands)
+
     while step < total_steps:
+        n = max(1, min(k_exec, boundary(step) - step))
         prof.before_step(step)
-        with trace_range("load_batch"):
-            dense, ids, label = data.next()
-            tr.load_batch(dense.to(dev, non_blocking=True), ids.to(dev, non_blocking=True),
-                          label.to(dev, non_blocking=True))
         timer.start()
         with trace_range("train_step"):
-            tr.step()
-        timer.stop()
-        step += 1
+            loop.run(n)
+        timer.stop(n)
+        step += n
         prof.after_step(step)
-        if use_graph and tr.graph is None and step - start == 2:
+        if use_graph and tr.graph is None and step - start >= 2:
             tr.capture_graph(warmup=0)
         if fault_at and step == fault_at and rank == fault_rank:
             os._exit(17)                               # simulated rank failure
@@ -214,6 +193,7 @@ def run(cfg: Config, mode: str = "single", out_dir: str = ".",
         if cfg.ckpt_dir and cfg.ckpt_every and step % cfg.ckpt_every == 0:
             with trace_range("checkpoint"):
                 save(tr, cfg.ckpt_dir, step, rank, world, meta)
+    loop.close()
     if cfg.ckpt_dir:
         save(tr, cfg.ckpt_dir, step, rank, world, meta)
     return {"history": history, "steps": step, "trainer": tr}
@@ -245,13 +225,16 @@ def evaluate(tr: DLRMTrainer, cfg: Config, dcfg: DLRMConfig, B: int, dev, rank: 
     """Held-out synthetic batches (a different seed): loss + bucketed AUC,
     reduced over ranks. Uses the trainer's static buffers, so the current
     training batch is restored afterwards."""
-    saved = (tr.x0[:, :dcfg.num_dense].clone(), tr.ids.clone(), tr.label.clone())
-    gen = _Data(cfg, dcfg, B, dev, rank, 7, prefetch=False)
+    tr.drain()
+    saved = (tr.x0[:, :dcfg.num_dense].float(), tr.ids.clone(), tr.label.clone())
+    src = _source(cfg, dcfg, B, dev, rank, 7, 0, eval_=True)
     hist = torch.zeros(2 * 199, dtype=torch.int64, device=dev)
     loss = torch.zeros(2, dtype=torch.float64, device=dev)
     for _ in range(batches):
-        d, i, y = gen.next()
-        tr.load_batch(d.to(dev), i.to(dev), y.to(dev))
+        (d, i, y), slot = src.next()
+        tr.load_batch(d, i, y)
+        if slot is not None:
+            src.release(slot)
         lg = tr.predict().float()
         yy = tr.label.float()
         loss[0] += torch.nn.functional.binary_cross_entropy_with_logits(lg, yy, reduction="sum")
@@ -260,5 +243,9 @@ def evaluate(tr: DLRMTrainer, cfg: Config, dcfg: DLRMConfig, B: int, dev, rank: 
     if world > 1:
         torch.distributed.all_reduce(hist, group=group)
         torch.distributed.all_reduce(loss, group=group)
-    tr.load_batch(*saved)
+    if tr.pipeline:              # the next step's batch: reload and re-exchange it
+        tr.drain()
+        tr.prime(*saved)
+    else:
+        tr.load_batch(*saved)
     return {"eval_loss": float(loss[0] / loss[1]), "eval_auc": ops.reference.hist_auc(hist)}

@@ -43,6 +43,19 @@ def _load_split(cfg: Config, which: str) -> Dict:
     return {k: cols[k] for k in keep}
 
 
+def _columns(cfg: Config, which: str, data_dev) -> DeviceColumns:
+    """A split's columns on ``data_dev``. ``streaming`` (parquet): read in
+    bounded chunks straight into the preallocated columns; otherwise the
+    split is read whole on the host first (the reference's in-memory
+    loader)."""
+    pattern = cfg.train_data if which == "train" else cfg.eval_data
+    if cfg.streaming and not (cfg.write_format == "tfrecord" or pattern.endswith(".tfrecord")):
+        keep = ID_COLS + ["avg_rating", "num_pages", "label"]
+        return DeviceColumns.from_parquet_stream(str(cfg.data_dir / "parquet" / pattern),
+                                                 data_dev, keep, _dtypes())
+    return DeviceColumns(_load_split(cfg, which), data_dev, _dtypes())
+
+
 def _dtypes():
     d = dict(TRAIN_DTYPES)
     d.update({k: torch.int64 for k in ID_COLS})
@@ -69,14 +82,12 @@ def run(cfg: Config, mode: str = "single", flavor: str = "flax", out_dir: str = 
     group = info.group if info else None
     out = Path(out_dir)
 
-    train_cols, eval_cols = _load_split(cfg, "train"), _load_split(cfg, "eval")
-    n_train, n_eval = len(train_cols["label"]), len(eval_cols["label"])
+    data_dev = dev if cfg.data_on_device else torch.device("cpu")
+    train, evald = _columns(cfg, "train", data_dev), _columns(cfg, "eval", data_dev)
+    n_train, n_eval = len(train), len(evald)
     _log(f"===== train size: {n_train:,}, eval size: {n_eval:,} =====", rank)
     if mode != "single":
         _log(f"===== num devices: {world} =====\n", rank)
-    data_dev = dev if cfg.data_on_device else torch.device("cpu")
-    train = DeviceColumns(train_cols, data_dev, _dtypes())
-    evald = DeviceColumns(eval_cols, data_dev, _dtypes())
 
     B, EB = cfg.per_device_train_batch_size, cfg.per_device_eval_batch_size
     init = cfg.tower_init or ("keras" if flavor == "keras" else "flax")
@@ -106,14 +117,35 @@ def run(cfg: Config, mode: str = "single", flavor: str = "flax", out_dir: str = 
             _log(f"===== restored from backup: resuming at epoch {start_epoch} =====", rank)
     metrics_path = cfg.metrics_file or (str(out / "log" / "metrics.jsonl") if mode == "ps" else "")
     history: List[Dict] = []
-    use_graph = (cfg.hip_graph and dev.type == "cuda" and mode == "single")
+    # jit_xla (tensorflow2/train.py:16, train_dp.py:76): false = eager kernel
+    # launches, no hipGraph (the XLA-compiled step's counterpart)
+    use_graph = (cfg.hip_graph and cfg.jit_xla is not False and dev.type == "cuda"
+                 and mode == "single")
+    k_exec = max(1, int(cfg.steps_per_execution))
     for epoch in range(start_epoch, cfg.n_epochs + 1):
         t0 = time.perf_counter()
         steps = 0
+        pend: List[torch.Tensor] = []          # full batches waiting for a k-step execution
         # HBM-resident columns: one gather launch per batch straight into the
         # trainer's static buffers; host-resident columns: per-column H2D
         for idx, s, n in train.batch_slices(B, shuffle=True, seed=cfg.seed, epoch=epoch,
                                             drop_last=drop_last, rank=rank, world_size=world):
+            if (k_exec > 1 and use_graph and tr.graph is not None and train.device == dev
+                    and idx is not None and n == B
+                    and not (cfg.max_steps and steps + len(pend) + 1 > cfg.max_steps)):
+                if getattr(tr, "_exec_graph", None) is None:
+                    tr.capture_execution(train.cols, k_exec)
+                pend.append(idx)
+                if len(pend) == k_exec:
+                    tr.run_execution(pend)
+                    steps += k_exec
+                    pend = []
+                continue
+            for ix in pend:                    # a partial execution: one step at a time
+                tr.load_columns(train.cols, ix, 0, B)
+                tr.step()
+                steps += 1
+            pend = []
             if train.device == dev:
                 b = tr.load_columns(train.cols, idx, s, n)
             else:
@@ -128,6 +160,10 @@ def run(cfg: Config, mode: str = "single", flavor: str = "flax", out_dir: str = 
                 tr.capture_graph()
             if cfg.max_steps and steps >= cfg.max_steps:
                 break
+        for ix in pend:
+            tr.load_columns(train.cols, ix, 0, B)
+            tr.step()
+            steps += 1
         if dev.type == "cuda":
             torch.cuda.synchronize()
         el = time.perf_counter() - t0

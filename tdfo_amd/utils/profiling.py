@@ -51,11 +51,12 @@ class StepTimer:
             e.record()
             self._open = e
 
-    def stop(self):
+    def stop(self, steps: int = 1):
+        """Close the interval opened by ``start``; it covered ``steps`` steps."""
         if self.enabled and self._open is not None:
             e = torch.cuda.Event(enable_timing=True)
             e.record()
-            self._pairs.append((self._open, e))
+            self._pairs.append((self._open, e, int(steps)))
             self._open = None
 
     def mean_ms(self) -> Optional[float]:
@@ -63,9 +64,10 @@ class StepTimer:
         if not self._pairs:
             return None
         self._pairs[-1][1].synchronize()
-        ms = [a.elapsed_time(b) for a, b in self._pairs]
+        ms = sum(a.elapsed_time(b) for a, b, _ in self._pairs)
+        n = sum(k for _, _, k in self._pairs)
         self._pairs.clear()
-        return sum(ms) / len(ms)
+        return ms / max(1, n)
 
 
 def parse_window(spec: str) -> Optional[Tuple[int, int]]:

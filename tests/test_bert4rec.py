@@ -183,10 +183,18 @@ def test_bert4rec_distributed_matches_single(mode):
         tr.step()
     ref_sd = tr.state_dict()
     outs = run_distributed(_dist_worker, world, mode, steps)
-    tol = 2e-5 if mode == "ddp" else 2e-2
+    tol = 2e-5    # dmp: fp32 pooled rows (ShardedEmbeddingModule recv_dtype="fp32")
     for o in outs:
         for k, v in ref_sd.items():
-            torch.testing.assert_close(o["sd"][k], v, rtol=tol, atol=tol, msg=k)
+            d = (o["sd"][k] - v).abs()
+            if mode == "dmp" and "embedding" in k:
+                # the owner sums a row's gradient contributions in another
+                # order: a row whose fp32 sum cancels to ~0 takes a different
+                # Adam sign step (<= lr) -- allowed for a handful of elements
+                assert (d > tol).float().mean() < 0.01 and d.max() <= 3e-3, (k, d.max())
+            else:
+                torch.testing.assert_close(o["sd"][k], v, rtol=tol, atol=tol,
+                                           msg=lambda m, k=k: f"{k}: {m}")
 
 
 def test_reference_attention_core_matches_model_math():

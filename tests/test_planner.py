@@ -69,3 +69,23 @@ def test_plan_cost_counts_xgmi():
     assert sum(p8.cost) / 8 > sum(p1.cost)
     prw = plan_sharding(cfg.tables(), 8, opt, strategy="row_wise")
     assert max(prw.cost) > max(p8.cost)          # RW moves W x the pooled bytes
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_plan_data_parallel_owner_partitions_big_tables(world):
+    """Config 3 (data_parallel): tables up to 256 MB are replicated, larger
+    ones are owner-partitioned (row-wise), so each rank updates 1/W of their
+    rows and its memory stays far below a full replica; "replicated" keeps
+    every table whole on every rank."""
+    cfg = DLRMConfig()
+    o = EmbOptimConfig("rowwise_adagrad")
+    p = plan_sharding(cfg.tables(), world, o, strategy="data_parallel")
+    for t, r in enumerate(CRITEO_1TB_ROWS):
+        big = r * 128 * 4 > 256 << 20
+        assert p.kind_of(t) == ("row_wise" if big else "data_parallel"), (t, r)
+    assert max(p.mem_bytes) < 100 * GiB / world + 2 * GiB
+    rep = plan_sharding(cfg.tables(), world, o, strategy="replicated")
+    assert all(s.kind == "data_parallel" for s in rep.shards)
+    assert min(rep.mem_bytes) > 90 * GiB
+    one = plan_sharding(cfg.tables(), 1, o, strategy="data_parallel")
+    assert all(s.kind == "data_parallel" for s in one.shards)

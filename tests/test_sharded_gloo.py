@@ -146,13 +146,17 @@ def _dlrm_worker(rank, world, B, steps, strategy, emb_opt="rowwise_adagrad", rw_
     return tr.fp.p.clone(), tabs, grows
 
 
-@pytest.mark.parametrize("strategy", ["table_wise", "row_wise", "data_parallel", "column_wise",
-                                      "auto"])
-def test_dlrm_data_parallel_matches_single_process(strategy):
+@pytest.mark.parametrize("strategy,opt", [
+    ("table_wise", "rowwise_adagrad"), ("row_wise", "rowwise_adagrad"),
+    ("data_parallel", "rowwise_adagrad"), ("data_parallel", "adam"),
+    ("column_wise", "adagrad"), ("auto", "rowwise_adagrad")])
+def test_dlrm_data_parallel_matches_single_process(strategy, opt):
+    """Every sharding kind at W=2 equals one process on the global batch.
+    Row-wise Adagrad keeps one state per row *per column block* under CW (as
+    TorchRec CW shards do), so CW is checked with elementwise Adagrad; Adam on
+    replicated tables must not decay the moments of rows the batch never
+    touched (the dense-gradient path is off for it)."""
     B, steps = 8, 3
-    # row-wise Adagrad keeps one state per row *per column block* under CW
-    # (as TorchRec CW shards do), so CW is checked with elementwise Adagrad
-    opt = "adagrad" if strategy == "column_wise" else "rowwise_adagrad"
     multi = run_distributed(_dlrm_worker, 2, B, steps, strategy, opt)
     single = run_distributed(_dlrm_worker, 1, 2 * B, steps, "table_wise", opt)[0]
     p1, tabs1, _ = single
