@@ -58,6 +58,7 @@ def build_hip(force: bool = False, debug: bool = False, jobs: int = 8) -> Path:
     headers = list((CSRC / "include").glob("*.h"))
     kernels = sorted((CSRC / "kernels").glob("*.hip"))
     bindings = CSRC / "bindings.cpp"
+    comm = sorted((CSRC / "comm").glob("*.cpp"))
     flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", f"-I{CSRC / 'include'}",
              "-D__HIP_PLATFORM_AMD__=1", "-munsafe-fp-atomics"]
     if debug:
@@ -67,7 +68,7 @@ def build_hip(force: bool = False, debug: bool = False, jobs: int = 8) -> Path:
     inc, tlib = _torch_paths()
     tflags = [f"-I{p}" for p in inc] + ["-DUSE_ROCM=1", "-D_GLIBCXX_USE_CXX11_ABI=1",
                                         "-DTORCH_EXTENSION_NAME=tdfo_hip"]
-    key = _digest(headers + kernels + [bindings], " ".join(flags + tflags))
+    key = _digest(headers + kernels + [bindings] + comm, " ".join(flags + tflags))
     stamp = BUILD / "hip.stamp"
     if not force and HIP_LIB.exists() and stamp.exists() and stamp.read_text() == key:
         return HIP_LIB
@@ -75,19 +76,19 @@ def build_hip(force: bool = False, debug: bool = False, jobs: int = 8) -> Path:
     LIBDIR.mkdir(parents=True, exist_ok=True)
 
     def compile_one(src: Path):
-        obj = BUILD / (src.stem + ".o")
+        obj = BUILD / (src.parent.name + "_" + src.stem + ".o")
         extra = tflags if src.suffix == ".cpp" else []
         lang = ["-x", "hip"] if src.suffix == ".cpp" else []
         _run([HIPCC, *flags, *extra, *lang, "-c", str(src), "-o", str(obj)])
         return obj
 
-    srcs = kernels + [bindings]
+    srcs = kernels + [bindings] + comm
     with cf.ThreadPoolExecutor(max_workers=max(1, min(jobs, len(srcs)))) as ex:
         objs = list(ex.map(compile_one, srcs))
     tmp = HIP_LIB.with_suffix(".so.tmp")
     _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(tmp),
           f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
-          f"-Wl,-rpath,{tlib}"])
+          "-lrccl", f"-Wl,-rpath,{tlib}"])
     os.replace(tmp, HIP_LIB)
     stamp.write_text(key)
     return HIP_LIB

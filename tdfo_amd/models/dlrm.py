@@ -101,6 +101,9 @@ class DLRMConfig:
     #   in-graph event nodes (None: DLRM yes, DCN-v2 no)
     ids_stream: Optional[bool] = None              # one GPU, composed graphs: copy the next
     #   ids on a third stream behind the sort (None: with composed graphs)
+    whole_graph: bool = True                       # W > 1, pipelined, capturable comm (native
+    #   RCCL / loopback): the whole step, collectives included, as ONE hipGraph (one launch
+    #   per step) instead of graphs between eagerly issued exchanges
     seed: int = 0
 
     @property
@@ -404,6 +407,8 @@ class DLRMTrainer(StreamGraphsMixin):
         self._primed = False
         self._mstream = False            # per-stream graphs (one process)
         self._ms = None
+        self._whole_capture = False      # capturing the whole multi-rank step
+        self._stg = None                 # whole-step graph: next-batch staging buffers
         self._graph_layout = 0
 
     # for tests / checkpoints: (weight [out, in_real], bias [out]) views
@@ -467,13 +472,27 @@ class DLRMTrainer(StreamGraphsMixin):
             self._m_out_exchange_next()
         self._next = (dense, ids, label)
         self._primed = True
+        self._inflight = True
 
     def set_next_batch(self, dense: torch.Tensor, ids: torch.Tensor, label: torch.Tensor):
         """Pipelined mode: the batch the current step loads for the next one
-        (device tensors that stay valid until the step has been issued)."""
+        (device tensors that stay valid until the step has been issued).
+        Whole-step graph: copied now into the static staging buffers the
+        graph's tail loads from (one launch; the previous replay, the last
+        reader of the staging, precedes it on this stream)."""
+        if self.graph == "whole":
+            sx, si, sl = self._stg
+            ops.batch_load(dense, sx, ids, si, label, sl)
+            return
         self._next = (dense, ids, label)
 
     def _m_load_next(self):
+        if self._whole_capture:
+            sx, si, sl = self._stg
+            self.x0.copy_(sx)
+            self.ids.copy_(si)
+            self.label.copy_(sl)
+            return
         dense, ids, label = self._next
         ops.batch_load(dense, self.x0, ids, self.ids, label, self.label)
 
@@ -665,6 +684,11 @@ class DLRMTrainer(StreamGraphsMixin):
             self._fwd(L, self.bot_in[i], out)
 
     def _m_fwd_wait(self):
+        if self._whole_capture:
+            # the previous replay completed this batch's exchanges (a graph
+            # ends joined); only the post-exchange assembly runs here
+            self.emb.forward_wait()
+            return
         if self._pipe_lookup and self._ev_lookup is not None and self._side() is not None:
             # the lookup ran on the side stream in the previous step's tail
             # (tables it wrote straight into recv have no collective to wait on)
@@ -672,12 +696,12 @@ class DLRMTrainer(StreamGraphsMixin):
         self.emb.forward_wait()
 
     def _m_mark_loaded(self):
-        if self._ev_loaded is not None:
+        if self._ev_loaded is not None and not self._whole_capture:
             self._ev_loaded.record(torch.cuda.current_stream())
 
     def _m_out_exchange_next(self):
         self.emb.stage_fwd_out_exchange()
-        if self._ev_lookup is not None:
+        if self._ev_lookup is not None and not self._whole_capture:
             self._ev_lookup.record(torch.cuda.current_stream())
 
     def _s_top(self):
@@ -898,6 +922,8 @@ class DLRMTrainer(StreamGraphsMixin):
             raise RuntimeError("pipelined trainer: call prime(first batch) before step()")
         if self.graph == "streams":
             self._ms_step()
+        elif self.graph == "whole":
+            self._whole_step()
         elif isinstance(self.graph, list):
             self._staged_step()
         elif self.graph is not None:
@@ -945,6 +971,9 @@ class DLRMTrainer(StreamGraphsMixin):
         torch.cuda.synchronize()
         if staged is None:
             staged = self.world > 1
+            if self._whole_ok():
+                self._capture_whole()
+                return
         if not staged and self.world == 1:
             if streams:
                 self._capture_streams()
@@ -986,6 +1015,78 @@ class DLRMTrainer(StreamGraphsMixin):
         torch.cuda.synchronize()
         self.graph = seq
         self._graph_layout = self.emb.layout_version
+
+    # ------------------------------------------- whole-step graph (W > 1)
+    def _whole_ok(self) -> bool:
+        """The multi-rank step can be one graph: pipelined with the lookup in
+        the tail, every exchange enqueue-only (native RCCL or loopback), and
+        no host read inside the step (the row-wise capacity check is one)."""
+        return (self.world > 1 and self.cfg.whole_graph and self._pipe_lookup
+                and getattr(self.comm, "capturable", False)
+                and not (self.emb.rw_tables and self.emb.rw_dynamic))
+
+    def _drain_inflight(self):
+        """Order the current stream after every exchange left in flight by
+        eager stages (prime(), eager steps): nothing crosses a graph edge."""
+        self.emb.ids_exchange_wait()
+        if self.emb._pending:
+            self.emb.forward_wait()
+        se = self._side()
+        if se is not None:
+            torch.cuda.current_stream().wait_stream(se)
+        self._inflight = False
+
+    def _whole_stages(self):
+        stages = self._stages()
+        assert stages[-1][0] == "jw"
+        # the tail joins the next batch's pooled exchange and the side stream
+        # (a replay ends with everything it started complete)
+        return stages[:-1] + [("m", self._whole_tail), ("j", None)]
+
+    def _whole_tail(self):
+        for w in self.emb._pending or ():
+            w.wait()
+        self.emb._pending = None
+
+    def _capture_whole(self):
+        """W > 1: the pipelined step -- compute on two streams, every RCCL
+        exchange (comm stream), the next batch's load from static staging --
+        captured as ONE hipGraph: one launch per step instead of ~20 Python
+        stage issues, ~6 c10d collectives and their event waits
+        (host 683 us/step at emulated W=8, profiles/r03/emu/w8.log). The
+        cross-step overlap of the next lookup with the next bottom MLP is
+        given up (a replay ends joined)."""
+        sx = self.x0.clone()
+        self._stg = (sx, self.ids.clone(), self.label.clone())
+        self._drain_inflight()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        self._whole_capture = True
+        self._on_side = False
+        try:
+            with graph_capture(g, pool=torch.cuda.graph_pool_handle(),
+                               capture_error_mode="thread_local"):
+                for kind, fn in self._whole_stages():
+                    self._run_stage(kind, fn)
+        finally:
+            self._whole_capture = False
+        # the captured tail's exchange handles are not real in-flight work
+        self.emb._ids_works = []
+        self.emb._pending = None
+        torch.cuda.synchronize()
+        # the capture ran nothing: the batch set before it (self._next) is the
+        # one the first replay must load
+        if self._next is not None:
+            d, i, l = self._next
+            ops.batch_load(d, sx, i, self._stg[1], l, self._stg[2])
+        self._whole = g
+        self.graph = "whole"
+        self._graph_layout = self.emb.layout_version
+
+    def _whole_step(self):
+        if getattr(self, "_inflight", False):
+            self._drain_inflight()
+        self._whole.replay()
 
     def pop_loss(self) -> float:
         """Mean training loss since the last call (one device->host read);

@@ -7,12 +7,16 @@ all-reduce (the reference's equivalents: TorchRec DMP's input/output dists
 and the DDP reducer, torchrec/train.py:241-260; TF PS pulls/pushes,
 tensorflow2/train_ps.py:55-61).
 
-Two implementations:
+Three implementations:
 
-* ``ProcessGroupComm``: a torch.distributed group -- RCCL over xGMI on
-  MI355X (the "nccl" backend), gloo on CPU. Collectives run on the process
-  group's own stream; ``async_op`` handles make the caller's current stream
-  wait device-side (never the host).
+* ``RcclComm`` (default for an RCCL group): the native layer
+  ``csrc/comm/rccl_comm.cpp`` -- a communicator of its own, every collective
+  enqueued from C++ (no c10d work objects), so the whole multi-rank step
+  captures into one hipGraph (``capturable``);
+* ``ProcessGroupComm``: a torch.distributed group -- gloo on CPU and in the
+  shared-GPU rehearsal, or RCCL through c10d with ``TDFO_COMM=torch``.
+  Collectives run on the process group's own stream; ``async_op`` handles
+  make the caller's current stream wait device-side (never the host).
 * ``LoopbackComm``: rank ``rank`` of a ``world``-rank job emulated in one
   process (``bench.py --emulate-world 8``): the real W-rank plan, layouts and
   kernels run, and each collective becomes device copies of the same byte
@@ -22,11 +26,12 @@ Two implementations:
   W-dependent kernel cost and the host time per step the full issue cost of
   the multi-rank step, without needing W GPUs.
 
-Both count calls and bytes per kind (``stats``), so a step's collective
+All count calls and bytes per kind (``stats``), so a step's collective
 volume is reported next to its time.
 """
 from __future__ import annotations
 
+import os
 from collections import defaultdict
 from typing import List, Optional, Sequence
 
@@ -64,6 +69,9 @@ class Comm:
 
     world: int = 1
     rank: int = 0
+    # every op only enqueues device work (no host wait, no host-side
+    # transport): a step issuing them can be captured into one hipGraph
+    capturable: bool = False
 
     def __init__(self):
         self.stats = defaultdict(lambda: [0, 0])     # kind -> [calls, bytes moved by this rank]
@@ -151,6 +159,105 @@ class ProcessGroupComm(Comm):
             dist.barrier(group=self.group)
 
 
+class _RcclWork:
+    __slots__ = ("h", "tok")
+
+    def __init__(self, h: int, tok: int):
+        self.h, self.tok = h, tok
+
+    def wait(self):
+        torch.ops.tdfo.rccl_wait(self.h, self.tok)
+
+
+class RcclComm(Comm):
+    """The native collective layer (``csrc/comm/rccl_comm.cpp``): an RCCL
+    communicator of its own over the ranks of ``group``, every op issued from
+    C++ on the caller's stream (sync) or forked onto the communicator's stream
+    (async, joined by ``wait``) -- nothing blocks the host, so a whole
+    multi-rank step, collectives included, captures into one hipGraph
+    (``capturable``). The torch process group only carries the unique id."""
+
+    capturable = True
+
+    def __init__(self, group=None, device=None):
+        super().__init__()
+        from .. import ops  # noqa: F401  (loads the native library)
+        from ..ops import _ext
+        if not _ext.load():
+            raise RuntimeError("RcclComm needs the native HIP library (tdfo_amd/lib/libtdfo_hip.so)")
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        dev = torch.device(device) if device is not None else torch.device(
+            "cuda", torch.cuda.current_device())
+        self.device = dev
+        self._side = None
+        uid = torch.ops.tdfo.rccl_unique_id() if self.rank == 0 else torch.zeros(128, dtype=torch.uint8)
+        if self.world > 1:
+            backend = dist.get_backend(group)
+            t = uid.to(dev) if backend == "nccl" else uid
+            src = dist.get_global_rank(group, 0) if group is not None else 0
+            dist.broadcast(t, src=src, group=group)
+            uid = t.cpu()
+        with torch.cuda.device(dev):
+            self.h = int(torch.ops.tdfo.rccl_init(uid, self.world, self.rank))
+
+    # async_op: fork the collective onto the comm stream with torch streams /
+    # events (the C++ fork with events of its own crashes hipStreamEndCapture
+    # on this ROCm; torch's wait_stream fork is capture-safe), or in C++
+    # (TDFO_RCCL_FORK=native: ~20 us less host time per eager collective)
+    _native_fork = os.environ.get("TDFO_RCCL_FORK", "torch") == "native"
+
+    def _run(self, fn, async_op: bool):
+        if not async_op:
+            fn(False)
+            return None
+        if self._native_fork:
+            return _RcclWork(self.h, int(fn(True)))
+        cur = torch.cuda.current_stream(self.device)
+        if self._side is None:
+            self._side = torch.cuda.Stream(device=self.device)
+        s = self._side
+        s.wait_stream(cur)
+        with torch.cuda.stream(s):
+            fn(False)
+        ev = torch.cuda.Event()
+        ev.record(s)
+        return _EventWork(ev)
+
+    def _all_to_all(self, out, inp, out_splits, in_splits, async_op):
+        os_ = [] if out_splits is None else [int(x) for x in out_splits]
+        is_ = [] if in_splits is None else [int(x) for x in in_splits]
+        o, i = out.view(-1), inp.reshape(-1)
+        return self._run(lambda a: torch.ops.tdfo.rccl_all_to_all(self.h, o, i, os_, is_, a),
+                         async_op)
+
+    def _all_gather(self, out, inp, async_op):
+        o, i = out.view(-1), inp.reshape(-1)
+        return self._run(lambda a: torch.ops.tdfo.rccl_all_gather(self.h, o, i, a), async_op)
+
+    def _reduce_scatter(self, out, inp, async_op):
+        o, i = out.view(-1), inp.reshape(-1)
+        return self._run(lambda a: torch.ops.tdfo.rccl_reduce_scatter(self.h, o, i, a), async_op)
+
+    def _all_reduce(self, t, op, async_op):
+        code = {"sum": 0, "max": 1, "min": 2}[op]
+        v = t.view(-1)
+        return self._run(lambda a: torch.ops.tdfo.rccl_all_reduce(self.h, v, code, a), async_op)
+
+    def _broadcast(self, t, src):
+        torch.ops.tdfo.rccl_broadcast(self.h, t.view(-1), int(src))
+
+    def barrier(self):
+        if self.world > 1:
+            dist.barrier(group=self.group)
+
+    def close(self):
+        if getattr(self, "h", None) is not None:
+            torch.ops.tdfo.rccl_destroy(self.h)
+            self.h = None
+
+
 class LoopbackComm(Comm):
     """Rank ``rank`` of a ``world``-rank job in one process (see module doc).
 
@@ -163,6 +270,7 @@ class LoopbackComm(Comm):
     def __init__(self, world: int, rank: int = 0, device=None):
         super().__init__()
         assert 0 <= rank < world
+        self.capturable = device is not None and torch.device(device).type == "cuda"
         self.world, self.rank = int(world), int(rank)
         self.device = torch.device(device) if device is not None else None
         self._stream = None
@@ -252,9 +360,28 @@ class _nullctx:
         return False
 
 
+_NATIVE: dict = {}
+
+
 def as_comm(group=None) -> Comm:
-    """A ``Comm`` for ``group``: itself if it is one, else the torch process
-    group wrapped (None: the default group, or a one-rank no-op layer)."""
+    """A ``Comm`` for ``group``: itself if it is one; for an RCCL ("nccl")
+    group the native ``RcclComm`` (one communicator per group, cached;
+    ``TDFO_COMM=torch`` keeps the c10d path); else the torch process group
+    wrapped (gloo, or None outside torch.distributed: a one-rank no-op)."""
     if isinstance(group, Comm):
         return group
+    if (dist.is_initialized() and dist.get_backend(group) == "nccl"
+            and os.environ.get("TDFO_COMM", "native") != "torch"):
+        key = id(group) if group is not None else None
+        c = _NATIVE.get(key)
+        if c is None:
+            c = _NATIVE[key] = RcclComm(group)
+        return c
     return ProcessGroupComm(group)
+
+
+def release_native():
+    """Destroy the cached native communicators (before the process group)."""
+    for c in _NATIVE.values():
+        c.close()
+    _NATIVE.clear()

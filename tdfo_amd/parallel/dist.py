@@ -91,6 +91,8 @@ def get_info() -> DistInfo:
 def reset():
     """Tear down (tests / end of training)."""
     global _INFO
+    from .comm import release_native
+    release_native()
     if dist.is_initialized():
         dist.destroy_process_group()
     _INFO = None

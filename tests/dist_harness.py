@@ -42,6 +42,19 @@ def _worker(rank, world, port, fn, args, q, device="cpu"):
         import torch
         torch.set_num_threads(1)
         from tdfo_amd.parallel import dist as tdist
+        if device == "cuda_rccl":
+            # one rank per GPU over RCCL (a one-rank group on a one-GPU box)
+            import datetime
+
+            import torch.distributed as dist
+            torch.cuda.set_device(rank)
+            dist.init_process_group("nccl", rank=rank, world_size=world,
+                                    timeout=datetime.timedelta(seconds=120),
+                                    device_id=torch.device("cuda", rank))
+            out = fn(rank, world, *args)
+            q.put((rank, "ok", _to_bytes(out)))
+            tdist.reset()
+            return
         tdist.init_distributed(device, "gloo", timeout_s=120)
         out = fn(rank, world, *args)
         q.put((rank, "ok", _to_bytes(out)))
@@ -51,7 +64,8 @@ def _worker(rank, world, port, fn, args, q, device="cpu"):
 
 
 def run_distributed(fn, world, *args, timeout=300, device="cpu"):
-    """``device="cuda"``: ranks share cuda:0 over gloo (fresh spawned processes)."""
+    """``device="cuda"``: ranks share cuda:0 over gloo (fresh spawned processes);
+    ``"cuda_rccl"``: rank r on cuda:r over RCCL (world <= visible GPUs)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
