@@ -65,6 +65,12 @@ def parse(argv=None):
                          "and kernels, each collective replaced by device copies of the same "
                          "byte count (parallel/comm.py LoopbackComm); reports device ms/step, "
                          "host issue us/step and the collective volume (not the headline)")
+    ap.add_argument("--emulate-link-gbps", type=float, default=300.0,
+                    help="--emulate-world: modelled per-rank xGMI injection bandwidth (GB/s); "
+                         "each emulated collective also holds the comm stream for its link "
+                         "bytes / this (0: local copies only)")
+    ap.add_argument("--emulate-latency-us", type=float, default=10.0,
+                    help="--emulate-world: modelled fixed cost per collective (us)")
     args = ap.parse_args(argv)
     if args.host_data:
         args.data = "host"
@@ -141,7 +147,8 @@ def main(argv=None):
     if args.emulate_world > 1:
         from tdfo_amd.parallel.comm import LoopbackComm
         world = args.emulate_world
-        group = LoopbackComm(world, 0, info.device)
+        group = LoopbackComm(world, 0, info.device, link_gbps=args.emulate_link_gbps,
+                             latency_us=args.emulate_latency_us)
         world_env = world
     if not _ext.load():
         raise RuntimeError("native HIP library failed to load")
@@ -183,16 +190,23 @@ def main(argv=None):
     # two replays of the fresh graph (its first launches upload it)
     post = 2 if use_graph and args.warmup >= 4 else 0
     loop.run(args.warmup - (1 + post if use_graph else 0))
+    # one eager step's collectives (a whole-step graph issues none from the host)
+    step_stats = None
+    if tr.comm is not None:
+        tr.comm.reset_stats()
+        if hasattr(tr.comm, "modelled_us"):
+            tr.comm.modelled_us = 0.0
+        loop.run(1)
+        step_stats = ({k: tuple(v) for k, v in tr.comm.stats.items()},
+                      getattr(tr.comm, "modelled_us", 0.0))
     if use_graph:
-        tr.capture_graph(warmup=1)
+        tr.capture_graph(warmup=0 if step_stats is not None else 1)
         loop.run(post)
     torch.cuda.synchronize()
     tr.pop_loss()
     if info.world_size > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
-    if tr.comm is not None:
-        tr.comm.reset_stats()
     t = time.perf_counter()
     loop.run(args.steps)
     host_s = time.perf_counter() - t          # issue time (the device runs behind)
@@ -208,9 +222,8 @@ def main(argv=None):
     ms = el / args.steps * 1e3
     value = B * world * args.steps / el
     sol = cfg.sol(B, world)
-    comm = ({k: {"calls_per_step": round(c / args.steps, 2),
-                 "MB_per_step": round(b / args.steps / 1e6, 3)}
-             for k, (c, b) in sorted(tr.comm.stats.items())} if tr.comm is not None else {})
+    comm = ({k: {"calls_per_step": round(c, 2), "MB_per_step": round(b / 1e6, 3)}
+             for k, (c, b) in sorted(step_stats[0].items())} if step_stats is not None else {})
     if args.emulate_world > 1:
         print(json.dumps({
             "metric": f"emulated rank-0 step of the {world}-rank job (loopback collectives)",
@@ -219,6 +232,9 @@ def main(argv=None):
             "host_issue_us_per_step": round(host_s / args.steps * 1e6, 1),
             "sol_ms_compute": round(cfg.sol(B, 1)["sol_ms"], 4),
             "sol_comm_ms": round(sol["comm_ms"], 4), "comm": comm,
+            "comm_model": {"link_gbps": args.emulate_link_gbps,
+                           "latency_us": args.emulate_latency_us,
+                           "modelled_us_per_step": round(step_stats[1], 1)},
             "plan": tr.plan.summary(), "graph": tr.graph if isinstance(tr.graph, str) else
             ("staged" if tr.graph else None), "pipeline": tr.pipeline,
             "data": args.data, "config": {"model": "DLRM" if args.model == "dlrm" else "DCN-v2",

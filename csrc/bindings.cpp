@@ -1189,6 +1189,15 @@ TORCH_LIBRARY(tdfo, m) {
   m.def("radix_sort_sep_hist(int v) -> int",
         [](int64_t v) { return (int64_t)tdfo::radix_sort_sep_hist((int)v); });
   m.def("sync_event_create(int mode) -> int", sync_event_create);
+  m.def("spin_us(float us) -> ()", [](double us) {
+    static const double ticks_per_us = [] {
+      int dev = 0, khz = 0;
+      TDFO_HIP_OK(hipGetDevice(&dev));
+      TDFO_HIP_OK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
+      return khz > 0 ? khz / 1000.0 : 100.0;
+    }();
+    tdfo::spin_ticks(us > 0 ? (uint64_t)(us * ticks_per_us) : 0, cur_stream());
+  });
   m.def("sync_event_record(int e) -> ()", sync_event_record);
   m.def("sync_event_wait(int e) -> ()", sync_event_wait);
   m.def("sync_event_destroy(int e) -> ()", sync_event_destroy);

@@ -206,6 +206,21 @@ void gather_columns(const GatherColsArgs& a, hipStream_t s) {
   TDFO_CHECK_HIP(hipGetLastError());
 }
 
+// One wave that occupies its stream for `ticks` of the 100 MHz constant
+// clock, sleeping between reads (modelled link time of an emulated
+// collective, parallel/comm.py LoopbackComm). Every wave exits once the
+// clock has advanced by `ticks`.
+__global__ __launch_bounds__(64) void spin_kernel(uint64_t ticks) {
+  const uint64_t t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+
+void spin_ticks(uint64_t ticks, hipStream_t s) {
+  if (ticks == 0) return;
+  hipLaunchKernelGGL(spin_kernel, dim3(1), dim3(64), 0, s, ticks);
+  TDFO_CHECK_HIP(hipGetLastError());
+}
+
 void batch_load(const float* dense, int nd, int64_t ld_dense, uint16_t* x0, int64_t ldx,
                 const int64_t* ids, int64_t* ids_dst, int64_t n, const float* label,
                 float* label_dst, int B, hipStream_t s) {

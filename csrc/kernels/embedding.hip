@@ -264,7 +264,8 @@ constexpr int SEG_CNT = SEG_BINS * SEG_K * SEG_WAVES;   // 8192 counters
 template <typename K, bool SORTED_G>
 __global__ __launch_bounds__(SEG_THREADS) void emb_segsort_kernel(
     const EmbBwdArgs a, K* __restrict__ keys_out, int32_t* __restrict__ vals_out,
-    int64_t* __restrict__ goff, float* __restrict__ gscale, int32_t* __restrict__ tail_count) {
+    int64_t* __restrict__ goff, float* __restrict__ gscale, int32_t* __restrict__ tail_count,
+    int32_t* __restrict__ pos) {
   __shared__ uint32_t skey[SEG_MAX];
   __shared__ uint32_t sval[SEG_MAX];
   __shared__ uint32_t cnt[SEG_CNT];
@@ -364,6 +365,7 @@ __global__ __launch_bounds__(SEG_THREADS) void emb_segsort_kernel(
     if (i < n) {
       keys_out[s0 + i] = kb + (K)key[k];
       vals_out[s0 + i] = (int32_t)(s0 + val[k]);
+      if (pos) pos[s0 + i] = i;            // its index in its own run (merge below)
       if (SORTED_G) {     // gradient-row offset (and scale) already in sorted order
         goff[s0 + i] = (int64_t)val[k] * a.grad_stride + go;
         if (gscale) gscale[s0 + i] = a.psw ? a.psw[s0 + val[k]] : 1.f;
@@ -374,59 +376,61 @@ __global__ __launch_bounds__(SEG_THREADS) void emb_segsort_kernel(
 
 // Multi-source one-hot (world > 1): a physical table's ids arrive as R runs
 // (one per source rank, virtual table v = run * Tp + table), each sorted by
-// emb_segsort_kernel. One block per run places every element at its final
-// position: its index in its own run plus, for every other run, the number
-// of keys that sort before it there (ties: earlier runs first = the stable
-// order of the positions). Each thread owns 8 consecutive keys, binary-
-// searches the first and walks forward for the rest.
+// emb_segsort_kernel. An element's final position in its table is its index
+// in its own run plus, for every other run, the number of keys that sort
+// before it there (ties: earlier runs first = the stable order of the
+// positions). One block per (run, other run) pair -- Tp x R x (R-1) blocks,
+// so the R-1 rank computations of a run run concurrently instead of one
+// after another in one block (207 -> see profiles/embedding_bwd_segsort_vs_radix
+// for the serial form at R = 8) -- loads the other run into LDS; each thread
+// owns 8 consecutive keys, binary-searches the first, walks forward for the
+// rest and adds its counts to pos[] (7 atomic adds per element at R = 8, on
+// distinct addresses per block). emb_runscatter_kernel then places keys and
+// values.
 template <typename K>
-__global__ __launch_bounds__(SEG_THREADS) void emb_runmerge_kernel(
-    int Tp, int R, int B, const K* __restrict__ kin, const int32_t* __restrict__ vin,
-    K* __restrict__ kout, int32_t* __restrict__ vout) {
+__global__ __launch_bounds__(SEG_THREADS) void emb_runrank_kernel(
+    int Tp, int R, int B, const K* __restrict__ kin, int32_t* __restrict__ pos) {
   __shared__ K other[SEG_MAX];
-  const int v = blockIdx.x, tid = threadIdx.x;
+  const int pair = blockIdx.x, tid = threadIdx.x;
+  const int v = pair / (R - 1), j = pair - v * (R - 1);
   const int run = v / Tp, p = v - run * Tp;
+  const int r = j < run ? j : j + 1;
   const int64_t src = (int64_t)v * B;
+  const int64_t o = (int64_t)(r * Tp + p) * B;
+  for (int i = tid; i < B; i += SEG_THREADS) other[i] = kin[o + i];
+  __syncthreads();
+  const bool le = r < run;                 // earlier run: equal keys go first
   const int i0 = tid * SEG_K;
+  if (i0 >= B) return;
   K key[SEG_K];
-  int64_t pos[SEG_K];
+#pragma unroll
+  for (int k = 0; k < SEG_K; ++k) key[k] = i0 + k < B ? kin[src + i0 + k] : key[0];
+  int lo = 0, hi = B;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    const bool before = le ? other[mid] <= key[0] : other[mid] < key[0];
+    if (before) lo = mid + 1; else hi = mid;
+  }
 #pragma unroll
   for (int k = 0; k < SEG_K; ++k) {
-    const int i = i0 + k;
-    key[k] = i < B ? kin[src + i] : (K)0;
-    pos[k] = i;
+    if (i0 + k >= B) break;
+    while (lo < B && (le ? other[lo] <= key[k] : other[lo] < key[k])) ++lo;
+    atomicAdd(&pos[src + i0 + k], lo);
   }
-  for (int r = 0; r < R; ++r) {
-    if (r == run) continue;
-    const int64_t o = (int64_t)(r * Tp + p) * B;
-    __syncthreads();
-    for (int i = tid; i < B; i += SEG_THREADS) other[i] = kin[o + i];
-    __syncthreads();
-    const bool le = r < run;               // earlier run: equal keys go first
-    // first key: count of other[] before key[0] (binary search)
-    int lo = 0, hi = B;
-    if (i0 < B) {
-      while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        const bool before = le ? other[mid] <= key[0] : other[mid] < key[0];
-        if (before) lo = mid + 1; else hi = mid;
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < SEG_K; ++k) {
-      if (i0 + k >= B) break;
-      while (lo < B && (le ? other[lo] <= key[k] : other[lo] < key[k])) ++lo;
-      pos[k] += lo;
-    }
-  }
-  const int64_t base = (int64_t)p * R * B;
-#pragma unroll
-  for (int k = 0; k < SEG_K; ++k) {
-    const int i = i0 + k;
-    if (i < B) {
-      kout[base + pos[k]] = key[k];
-      vout[base + pos[k]] = vin[src + i];
-    }
+}
+
+template <typename K>
+__global__ __launch_bounds__(256) void emb_runscatter_kernel(
+    int Tp, int R, int B, const K* __restrict__ kin, const int32_t* __restrict__ vin,
+    const int32_t* __restrict__ pos, K* __restrict__ kout, int32_t* __restrict__ vout) {
+  const int64_t n = (int64_t)Tp * R * B;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+       e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t v = e / B;
+    const int p = (int)(v % Tp);
+    const int64_t d = (int64_t)p * R * B + pos[e];
+    kout[d] = kin[e];
+    vout[d] = vin[e];
   }
 }
 
@@ -829,7 +833,8 @@ void dense_update_dispatch(const EmbBwdArgs& a, int64_t rows, const float* g, hi
 int g_emb_segsort = 1;   // one-hot batches: per-table LDS sort (0: device-wide radix sort)
 
 struct WsLayout {
-  size_t keys_in, keys_out, vals_in, vals_out, goff, gscale, head, tail, tlist, tcount, sortws;
+  size_t keys_in, keys_out, vals_in, vals_out, goff, gscale, head, tail, tlist, tcount, sortws,
+      pos;
   size_t total;
 };
 
@@ -852,6 +857,7 @@ WsLayout ws_layout(int64_t nnz, int D) {
   L.tlist = o;    o += al((size_t)nch * 4);
   L.tcount = o;   o += al(16);
   L.sortws = o;   o += al(radix_sort_workspace(nnz));
+  L.pos = o;      o += al(nnz * 4);
   L.total = o;
   return L;
 }
@@ -879,13 +885,20 @@ void prep_impl(const EmbBwdArgs& a, const WsLayout& L, hipStream_t s) {
   if (onehot_path(a)) {
     if (R == 1) {
       hipLaunchKernelGGL((emb_segsort_kernel<K, true>), dim3(a.T), dim3(SEG_THREADS), 0, s, a,
-                         keys_out, vals_out, goff, gscale, tcount);
+                         keys_out, vals_out, goff, gscale, tcount, (int32_t*)nullptr);
     } else {
+      int32_t* pos = (int32_t*)(ws + L.pos);
       hipLaunchKernelGGL((emb_segsort_kernel<K, false>), dim3(a.T), dim3(SEG_THREADS), 0, s, a, keys_in,
-                         vals_in, goff, gscale, tcount);
+                         vals_in, goff, gscale, tcount, pos);
       TDFO_CHECK_HIP(hipGetLastError());
-      hipLaunchKernelGGL(emb_runmerge_kernel<K>, dim3(a.T), dim3(SEG_THREADS), 0, s, a.T / R, R,
-                         a.B, keys_in, vals_in, keys_out, vals_out);
+      const int Tp = a.T / R;
+      hipLaunchKernelGGL(emb_runrank_kernel<K>, dim3(a.T * (R - 1)), dim3(SEG_THREADS), 0, s, Tp,
+                         R, a.B, keys_in, pos);
+      TDFO_CHECK_HIP(hipGetLastError());
+      int64_t sb = (a.nnz + 255) / 256;
+      if (sb > 4096) sb = 4096;
+      hipLaunchKernelGGL(emb_runscatter_kernel<K>, dim3(sb), dim3(256), 0, s, Tp, R, a.B,
+                         keys_in, vals_in, pos, keys_out, vals_out);
     }
   } else {
     // generate where an even/odd number of passes leaves the result in *_out

@@ -60,6 +60,14 @@ DENSE_OPTS = {"adamw": ops.OPT_ADAMW, "adam": ops.OPT_ADAM, "sgd": ops.OPT_SGD,
               "adagrad": ops.OPT_ADAGRAD}
 
 
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
 def pad64(n: int) -> int:
     return -(-n // 64) * 64
 
@@ -408,6 +416,7 @@ class DLRMTrainer(StreamGraphsMixin):
         self._mstream = False            # per-stream graphs (one process)
         self._ms = None
         self._whole_capture = False      # capturing the whole multi-rank step
+        self._cap_origin = None          # ... and the origin stream of that capture
         self._stg = None                 # whole-step graph: next-batch staging buffers
         self._graph_layout = 0
 
@@ -641,6 +650,20 @@ class DLRMTrainer(StreamGraphsMixin):
             ("j", None),
         ]
 
+    def _wait(self, dst, src):
+        """``dst`` waits for the work issued on ``src``. While the whole step
+        is being captured, a wait between two non-origin streams is routed
+        through the capture's origin (origin waits ``src``, ``dst`` waits
+        origin): HIP's hipStreamEndCapture segfaults on this ROCm when a
+        stream forked into a capture is itself the source of another fork
+        (scripts/rccl_capture_probe.py, nested_* modes)."""
+        o = self._cap_origin
+        if o is None or dst == o or src == o:
+            dst.wait_stream(src)
+        else:
+            o.wait_stream(src)
+            dst.wait_stream(o)
+
     # side stream of the multi-process stage lists ("e" / "em" / "j" stages)
     def _side(self):
         if self.device.type != "cuda" or self.world == 1:
@@ -655,7 +678,7 @@ class DLRMTrainer(StreamGraphsMixin):
         se = self._side()
         if kind == "j":
             if se is not None:
-                torch.cuda.current_stream().wait_stream(se)
+                self._wait(torch.cuda.current_stream(), se)
             self._on_side = False
             return
         if kind == "jw":                     # main waits for the next batch's load only
@@ -665,7 +688,7 @@ class DLRMTrainer(StreamGraphsMixin):
             return
         if kind in ("e", "em") and se is not None:
             if not getattr(self, "_on_side", False):
-                se.wait_stream(torch.cuda.current_stream())
+                self._wait(se, torch.cuda.current_stream())
                 self._on_side = True
             with torch.cuda.stream(se):
                 graph.replay() if graph is not None else fn()
@@ -715,7 +738,7 @@ class DLRMTrainer(StreamGraphsMixin):
         D, F = cfg.embedding_dim, self.F
         emb = self.emb
         if self._ps is not None and not self._mstream:
-            self._ps.wait_stream(torch.cuda.current_stream())
+            self._wait(self._ps, torch.cuda.current_stream())
             with torch.cuda.stream(self._ps):
                 emb.stage_bwd_prepare()
         h = self.h_out
@@ -760,7 +783,7 @@ class DLRMTrainer(StreamGraphsMixin):
             self._dcn_backward(h)
         emb.stage_bwd_local(self.emb_hyper)        # replicated tables' dense grads
         if not self._mstream and self._ps is not None:
-            torch.cuda.current_stream().wait_stream(self._ps)
+            self._wait(torch.cuda.current_stream(), self._ps)
 
     def _s_top_wgrad(self):
         """Top-MLP (and DCN cross-layer) weight grads, deferred past the
@@ -1063,13 +1086,24 @@ class DLRMTrainer(StreamGraphsMixin):
         g = torch.cuda.CUDAGraph()
         self._whole_capture = True
         self._on_side = False
+        # the capture's origin is the comm stream (RCCL under capture must be
+        # enqueued on the origin: RcclComm.capture_origin); the compute runs
+        # on a stream forked from it and joins back at the end
+        origin = torch.cuda.Stream(device=self.device)
+        ms = torch.cuda.Stream(device=self.device)
+        route = getattr(self.comm, "capture_origin", None)
+        self._cap_origin = origin
         try:
-            with graph_capture(g, pool=torch.cuda.graph_pool_handle(),
+            with graph_capture(g, pool=torch.cuda.graph_pool_handle(), stream=origin,
                                capture_error_mode="thread_local"):
-                for kind, fn in self._whole_stages():
-                    self._run_stage(kind, fn)
+                ms.wait_stream(origin)
+                with torch.cuda.stream(ms), (route(origin) if route else _nullctx()):
+                    for kind, fn in self._whole_stages():
+                        self._run_stage(kind, fn)
+                origin.wait_stream(ms)
         finally:
             self._whole_capture = False
+            self._cap_origin = None
         # the captured tail's exchange handles are not real in-flight work
         self.emb._ids_works = []
         self.emb._pending = None

@@ -452,6 +452,12 @@ def synth_criteo(seed, rank, batch_index, B, rows, pooling, base, dist, alpha, w
                            int(dist), float(alpha), w_dense, table_bias, dense, ids, label)
 
 
+def spin_us(us: float):
+    """Occupy the current stream for ``us`` microseconds (one sleeping wave):
+    the modelled link time of an emulated collective."""
+    _native().spin_us(float(us))
+
+
 def batch_load(dense, x0, ids, ids_dst, label, label_dst):
     """x0[:, :nd] = bf16(dense), ids_dst = ids, label_dst = label (one launch on GPU)."""
     # the fused kernel needs fp32 row-major dense, int64 ids at a 16-B aligned

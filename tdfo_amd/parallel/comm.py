@@ -191,7 +191,7 @@ class RcclComm(Comm):
         dev = torch.device(device) if device is not None else torch.device(
             "cuda", torch.cuda.current_device())
         self.device = dev
-        self._side = None
+        self._origin = None
         uid = torch.ops.tdfo.rccl_unique_id() if self.rank == 0 else torch.zeros(128, dtype=torch.uint8)
         if self.world > 1:
             backend = dist.get_backend(group)
@@ -202,27 +202,50 @@ class RcclComm(Comm):
         with torch.cuda.device(dev):
             self.h = int(torch.ops.tdfo.rccl_init(uid, self.world, self.rank))
 
-    # async_op: fork the collective onto the comm stream with torch streams /
-    # events (the C++ fork with events of its own crashes hipStreamEndCapture
-    # on this ROCm; torch's wait_stream fork is capture-safe), or in C++
-    # (TDFO_RCCL_FORK=native: ~20 us less host time per eager collective)
-    _native_fork = os.environ.get("TDFO_RCCL_FORK", "torch") == "native"
+    # Under stream capture RCCL must be enqueued on the capture's ORIGIN
+    # stream: a collective on any stream joined into the capture by an event
+    # wait (torch's own async c10d collectives included) crashes
+    # hipStreamEndCapture on this ROCm (scripts/rccl_capture_probe.py). So a
+    # capturing caller names its origin (``capture_origin``) and every
+    # collective goes there -- origin waits on the caller's stream, the
+    # collective runs, the caller's stream waits on it (async: when the handle
+    # is waited). Eagerly, async ops fork onto the communicator's own stream
+    # in C++ (event record + wait, no Python stream objects).
+    def capture_origin(self, stream):
+        """Context: route collectives through ``stream`` (the origin of the
+        capture in progress)."""
+        comm = self
+
+        class _Ctx:
+            def __enter__(self_):
+                comm._origin = stream
+
+            def __exit__(self_, *a):
+                comm._origin = None
+                return False
+
+        return _Ctx()
 
     def _run(self, fn, async_op: bool):
-        if not async_op:
-            fn(False)
-            return None
-        if self._native_fork:
-            return _RcclWork(self.h, int(fn(True)))
+        o = self._origin
+        if o is None:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("RcclComm: collective inside a stream capture without "
+                                   "capture_origin(stream) (RCCL must run on the origin stream)")
+            tok = fn(async_op)
+            return _RcclWork(self.h, int(tok)) if async_op else None
         cur = torch.cuda.current_stream(self.device)
-        if self._side is None:
-            self._side = torch.cuda.Stream(device=self.device)
-        s = self._side
-        s.wait_stream(cur)
-        with torch.cuda.stream(s):
+        if cur == o:
             fn(False)
+            return None if not async_op else _Done()
+        o.wait_stream(cur)
+        with torch.cuda.stream(o):
+            fn(False)
+        if not async_op:
+            cur.wait_stream(o)
+            return None
         ev = torch.cuda.Event()
-        ev.record(s)
+        ev.record(o)
         return _EventWork(ev)
 
     def _all_to_all(self, out, inp, out_splits, in_splits, async_op):
@@ -267,7 +290,8 @@ class LoopbackComm(Comm):
     rank's values) -- so the numbers stay finite and exchanged ids stay in
     range. Byte counts per call equal the real collective's."""
 
-    def __init__(self, world: int, rank: int = 0, device=None):
+    def __init__(self, world: int, rank: int = 0, device=None, link_gbps: float = 0.0,
+                 latency_us: float = 0.0):
         super().__init__()
         assert 0 <= rank < world
         self.capturable = device is not None and torch.device(device).type == "cuda"
@@ -275,19 +299,56 @@ class LoopbackComm(Comm):
         self.device = torch.device(device) if device is not None else None
         self._stream = None
         self._scratch = None
+        # modelled xGMI time (GPU only): after its local copies each collective
+        # holds the comm stream for latency_us + (bytes over the links) /
+        # link_gbps -- this rank's injection bandwidth into the other W-1 --
+        # so the emulated step also shows where the exchanges would sit on
+        # the critical path (0: copies only)
+        self.link_gbps = float(link_gbps)
+        self.latency_us = float(latency_us)
+        self.modelled_us = 0.0
+        self._origin = None
+
+    def _model(self, link_bytes: float):
+        if self._stream is None or (self.link_gbps <= 0 and self.latency_us <= 0):
+            return
+        us = self.latency_us + (link_bytes / (self.link_gbps * 1e3) if self.link_gbps > 0 else 0.0)
+        self.modelled_us += us
+        from .. import ops
+        ops.spin_us(us)
+
+    def capture_origin(self, stream):
+        """Context: during a whole-step capture the emulated collectives run
+        on the capture's origin stream (as RcclComm's must), so no forked
+        stream is the source of another fork (see DLRMTrainer._wait)."""
+        comm = self
+
+        class _Ctx:
+            def __enter__(self_):
+                comm._origin = stream
+
+            def __exit__(self_, *a):
+                comm._origin = None
+                return False
+
+        return _Ctx()
 
     def _begin(self, t):
         if not t.is_cuda:
             return None
         if self._stream is None:
             self._stream = torch.cuda.Stream(device=t.device)
-        s = self._stream
-        s.wait_stream(torch.cuda.current_stream(t.device))
+        s = self._origin if self._origin is not None else self._stream
+        cur = torch.cuda.current_stream(t.device)
+        if cur != s:
+            s.wait_stream(cur)
         return s
 
     def _end(self, s, async_op):
         if s is None:
             return _Done()
+        if s == torch.cuda.current_stream(s.device):     # ran on the caller's stream
+            return _Done() if async_op else None
         ev = torch.cuda.Event()
         ev.record(s)
         w = _EventWork(ev)
@@ -304,24 +365,27 @@ class LoopbackComm(Comm):
         own = inp.view(-1)[src0: src0 + is_[r]]
         o = out.view(-1)
         s = self._begin(inp)
+        es = inp.element_size()
         with torch.cuda.stream(s) if s is not None else _nullctx():
             if all(n == own.numel() for n in os_):          # one broadcast copy
                 o.view(W, -1).copy_(own.view(1, -1).expand(W, -1))
-                return self._end(s, async_op)
-            off = 0
-            for n in os_:
-                k = 0
-                while k < n and own.numel():                 # tile this rank's own segment
-                    m = min(own.numel(), n - k)
-                    o[off + k: off + k + m].copy_(own[:m])
-                    k += m
-                off += n
+            else:
+                off = 0
+                for n in os_:
+                    k = 0
+                    while k < n and own.numel():             # tile this rank's own segment
+                        m = min(own.numel(), n - k)
+                        o[off + k: off + k + m].copy_(own[:m])
+                        k += m
+                    off += n
+            self._model(max(sum(is_) - is_[r], sum(os_) - os_[r]) * es)
         return self._end(s, async_op)
 
     def _all_gather(self, out, inp, async_op):
         s = self._begin(inp)
         with torch.cuda.stream(s) if s is not None else _nullctx():
             out.view(self.world, -1).copy_(inp.view(1, -1).expand(self.world, -1))
+            self._model(out.numel() * out.element_size() * (self.world - 1) / self.world)
         return self._end(s, async_op)
 
     def _reduce_scatter(self, out, inp, async_op):
@@ -333,6 +397,7 @@ class LoopbackComm(Comm):
             tmp = inp.view(self.world, -1)[:, :n].sum(0, dtype=torch.float32)
             out.view(-1).copy_(inp.view(-1)[self.rank * n: (self.rank + 1) * n])
             del tmp
+            self._model(inp.numel() * inp.element_size() * (self.world - 1) / self.world)
         return self._end(s, async_op)
 
     def _all_reduce(self, t, op, async_op):
@@ -346,6 +411,7 @@ class LoopbackComm(Comm):
                 sc = self._scratch[: t.numel() * t.element_size()].view(t.dtype).view(t.shape)
                 sc.copy_(t)
                 t.copy_(sc)
+            self._model(2 * t.numel() * t.element_size() * (self.world - 1) / self.world)
         return self._end(s, async_op)
 
     def _broadcast(self, t, src):

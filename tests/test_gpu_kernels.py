@@ -287,12 +287,12 @@ def test_embedding_bwd_onehot_segsort(B, skew, opt):
     assert (res[0][0] - We).abs().max() < 1e-4 * max(1.0, We.abs().max().item())
 
 
-@pytest.mark.parametrize("R", [2, 8])
-def test_embedding_bwd_onehot_multirun(R):
+@pytest.mark.parametrize("R,B", [(2, 2048), (3, 2048), (8, 2048), (8, 8192)])
+def test_embedding_bwd_onehot_multirun(R, B):
     """World > 1 layout: each physical table's ids arrive as R runs (virtual
     tables v = run * Tp + table sharing the table's rows). Per-run LDS sorts +
     run merge must match the radix-sort path bit for bit."""
-    Tp, B, D = 3, 2048, 128
+    Tp, D = 3, 128
     rows = [50, 9000, 70000]
     g = torch.Generator().manual_seed(11)
     T = R * Tp
