@@ -56,9 +56,9 @@ def parse(argv=None):
     ap.add_argument("--no-pipeline", action="store_true",
                     help="N > 1: exchange each batch's ids inside its own step instead of "
                          "during the previous step's dense update")
-    ap.add_argument("--no-whole-graph", action="store_true",
+    ap.add_argument("--no-stream-graphs", action="store_true",
                     help="N > 1: replay graphs between eagerly issued exchanges instead of the "
-                         "whole step (collectives included) as one hipGraph")
+                         "per-stream step graphs with the collectives inside")
     ap.add_argument("--host-data", action="store_true", help="same as --data host")
     ap.add_argument("--emulate-world", type=int, default=0, metavar="W",
                     help="one GPU runs rank 0 of the W-rank job: the real W-rank plan, layouts "
@@ -160,11 +160,11 @@ def main(argv=None):
     pipe = world_env > 1 and not args.no_pipeline
     if args.model == "dlrm":
         cfg = DLRMConfig(table_rows=list(rows), sharding=args.sharding, pipeline=pipe,
-                         dense_comm=args.dense_comm, whole_graph=not args.no_whole_graph)
+                         dense_comm=args.dense_comm, stream_graphs=not args.no_stream_graphs)
     else:
         cfg = DLRMConfig(table_rows=list(rows), interaction="dcn", pooling=list(MLPERF_MULTIHOT),
                          top=[1024, 1024, 512, 256, 1], sharding=args.sharding, pipeline=pipe,
-                         dense_comm=args.dense_comm, whole_graph=not args.no_whole_graph)
+                         dense_comm=args.dense_comm, stream_graphs=not args.no_stream_graphs)
     B = args.batch
     t0 = time.time()
     if args.data in ("host", "fresh"):
@@ -193,12 +193,19 @@ def main(argv=None):
     # one eager step's collectives (a whole-step graph issues none from the host)
     step_stats = None
     if tr.comm is not None:
-        tr.comm.reset_stats()
-        if hasattr(tr.comm, "modelled_us"):
-            tr.comm.modelled_us = 0.0
+        comms = [tr.comm] + ([tr.dcomm] if tr.dcomm is not tr.comm else [])
+        for c in comms:
+            c.reset_stats()
+            if hasattr(c, "modelled_us"):
+                c.modelled_us = 0.0
         loop.run(1)
-        step_stats = ({k: tuple(v) for k, v in tr.comm.stats.items()},
-                      getattr(tr.comm, "modelled_us", 0.0))
+        agg = {}
+        for c in comms:
+            for k, (n, b) in c.stats.items():
+                a = agg.setdefault(k, [0, 0])
+                a[0] += n
+                a[1] += b
+        step_stats = (agg, sum(getattr(c, "modelled_us", 0.0) for c in comms))
     if use_graph:
         tr.capture_graph(warmup=0 if step_stats is not None else 1)
         loop.run(post)

@@ -1189,6 +1189,14 @@ TORCH_LIBRARY(tdfo, m) {
   m.def("radix_sort_sep_hist(int v) -> int",
         [](int64_t v) { return (int64_t)tdfo::radix_sort_sep_hist((int)v); });
   m.def("sync_event_create(int mode) -> int", sync_event_create);
+  m.def("stamp(Tensor(a!) buf, Tensor(b!) cnt, int seg, int nseg, int which) -> ()",
+        [](const Tensor& buf, const Tensor& cnt, int64_t seg, int64_t nseg, int64_t which) {
+    TORCH_CHECK(buf.is_cuda() && buf.scalar_type() == at::kLong && cnt.is_cuda() &&
+                cnt.scalar_type() == at::kLong && seg >= 0 && seg < cnt.numel() &&
+                seg < nseg && (which == 0 || which == 1), "stamp: int64 GPU buffers");
+    tdfo::stamp(reinterpret_cast<uint64_t*>(buf.data_ptr()), cnt.data_ptr<int64_t>(), (int)seg,
+                (int)nseg, (int)which, buf.numel(), cur_stream());
+  });
   m.def("spin_us(float us) -> ()", [](double us) {
     static const double ticks_per_us = [] {
       int dev = 0, khz = 0;

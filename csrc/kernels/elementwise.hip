@@ -215,6 +215,25 @@ __global__ __launch_bounds__(64) void spin_kernel(uint64_t ticks) {
   while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
 }
 
+// In-graph timestamps for schedule probes (scripts/mr_sched_probe.py): the
+// k-th run of segment `seg` writes the 100 MHz wall clock to
+// buf[(k * nseg + seg) * 2 + which]; its end stamp (which = 1) advances k.
+// One lane, vector stores; a segment's runs are ordered on its stream.
+__global__ void stamp_kernel(uint64_t* buf, int64_t* cnt, int seg, int nseg, int which,
+                             int64_t cap) {
+  if (threadIdx.x != 0) return;
+  const int64_t k = cnt[seg];
+  const int64_t i = (k * nseg + seg) * 2 + which;
+  if (i < cap) buf[i] = (uint64_t)wall_clock64();
+  if (which == 1) cnt[seg] = k + 1;
+}
+
+void stamp(uint64_t* buf, int64_t* cnt, int seg, int nseg, int which, int64_t cap,
+           hipStream_t s) {
+  hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(64), 0, s, buf, cnt, seg, nseg, which, cap);
+  TDFO_CHECK_HIP(hipGetLastError());
+}
+
 void spin_ticks(uint64_t ticks, hipStream_t s) {
   if (ticks == 0) return;
   hipLaunchKernelGGL(spin_kernel, dim3(1), dim3(64), 0, s, ticks);

@@ -32,7 +32,8 @@ import torch
 from ..utils.capture import graph_capture
 from .. import ops
 from .dlrm_streams import StreamGraphsMixin
-from ..parallel.comm import as_comm
+from .dlrm_multirank import MultiRankStreamsMixin
+from ..parallel.comm import as_comm, dense_comm_for
 from ..sparse.planner import ShardingPlan, plan_sharding
 from ..sparse.sharded import ShardedEmbeddingBags
 from ..sparse.tables import EmbOptimConfig, TableConfig
@@ -58,14 +59,6 @@ MLPERF_MULTIHOT = [3, 2, 1, 2, 6, 1, 1, 1, 1, 7, 3, 8, 1, 6, 9, 5, 1, 1, 1, 12, 
 
 DENSE_OPTS = {"adamw": ops.OPT_ADAMW, "adam": ops.OPT_ADAM, "sgd": ops.OPT_SGD,
               "adagrad": ops.OPT_ADAGRAD}
-
-
-class _nullctx:
-    def __enter__(self):
-        return self
-
-    def __exit__(self, *a):
-        return False
 
 
 def pad64(n: int) -> int:
@@ -109,9 +102,10 @@ class DLRMConfig:
     #   in-graph event nodes (None: DLRM yes, DCN-v2 no)
     ids_stream: Optional[bool] = None              # one GPU, composed graphs: copy the next
     #   ids on a third stream behind the sort (None: with composed graphs)
-    whole_graph: bool = True                       # W > 1, pipelined, capturable comm (native
-    #   RCCL / loopback): the whole step, collectives included, as ONE hipGraph (one launch
-    #   per step) instead of graphs between eagerly issued exchanges
+    stream_graphs: bool = True                     # W > 1, pipelined, capturable comm (native
+    #   RCCL / loopback): the step as per-stream hipGraphs with the collectives inside
+    #   (dlrm_multirank.py; 3 launches per step) instead of graphs between eagerly issued
+    #   exchanges
     seed: int = 0
 
     @property
@@ -229,7 +223,7 @@ def make_lin(name: str, in_real: int, out: int) -> Lin:
 
 
 
-class DLRMTrainer(StreamGraphsMixin):
+class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin):
     """Explicit-step DLRM/DCN-v2 trainer over a sharded embedding engine.
 
     ``batch_size`` is per rank (weak scaling). Works on CPU (torch reference
@@ -254,6 +248,10 @@ class DLRMTrainer(StreamGraphsMixin):
         self.device = dev = torch.device(device)
         self.group = group
         self.comm = as_comm(group) if world_size > 1 else None
+        # the dense-gradient all-reduces get a communicator of their own where
+        # collectives are stream-ordered (native RCCL, loopback), so they run
+        # beside the embedding exchanges (dlrm_multirank.py)
+        self.dcomm = dense_comm_for(self.comm) if world_size > 1 else None
         self.rank = rank
         self.world = world_size
         D = cfg.embedding_dim
@@ -271,6 +269,8 @@ class DLRMTrainer(StreamGraphsMixin):
         self.emb = ShardedEmbeddingBags(tables, self.plan, rank, B, cfg.pooling_factors(), dev,
                                         optim, group=self.comm, seed=cfg.seed,
                                         rw_capacity=cfg.rw_capacity, rw_comm=cfg.rw_comm)
+        if self.dcomm is not None:
+            self.emb.dp_comm = self.dcomm         # replicated tables' all-reduce beside it
         # ------------------------------------------------------ dense params
         fp = FlatParams()
         dims = [cfg.num_dense] + cfg.bottom
@@ -415,9 +415,10 @@ class DLRMTrainer(StreamGraphsMixin):
         self._primed = False
         self._mstream = False            # per-stream graphs (one process)
         self._ms = None
-        self._whole_capture = False      # capturing the whole multi-rank step
-        self._cap_origin = None          # ... and the origin stream of that capture
-        self._stg = None                 # whole-step graph: next-batch staging buffers
+        self._whole_capture = False      # capturing the multi-rank stream graphs
+        self._cap_origin = None          # origin of a multi-stream capture (see _wait)
+        self._stg = None                 # multi-rank graphs: next-batch staging buffers
+        self._mr = None
         self._graph_layout = 0
 
     # for tests / checkpoints: (weight [out, in_real], bias [out]) views
@@ -481,7 +482,7 @@ class DLRMTrainer(StreamGraphsMixin):
             self._m_out_exchange_next()
         self._next = (dense, ids, label)
         self._primed = True
-        self._inflight = True
+        self._mr_inflight = True
 
     def set_next_batch(self, dense: torch.Tensor, ids: torch.Tensor, label: torch.Tensor):
         """Pipelined mode: the batch the current step loads for the next one
@@ -489,9 +490,8 @@ class DLRMTrainer(StreamGraphsMixin):
         Whole-step graph: copied now into the static staging buffers the
         graph's tail loads from (one launch; the previous replay, the last
         reader of the staging, precedes it on this stream)."""
-        if self.graph == "whole":
-            sx, si, sl = self._stg
-            ops.batch_load(dense, sx, ids, si, label, sl)
+        if self.graph == "mstreams":
+            self._mr_stage_next(dense, ids, label)
             return
         self._next = (dense, ids, label)
 
@@ -651,12 +651,12 @@ class DLRMTrainer(StreamGraphsMixin):
         ]
 
     def _wait(self, dst, src):
-        """``dst`` waits for the work issued on ``src``. While the whole step
-        is being captured, a wait between two non-origin streams is routed
-        through the capture's origin (origin waits ``src``, ``dst`` waits
-        origin): HIP's hipStreamEndCapture segfaults on this ROCm when a
-        stream forked into a capture is itself the source of another fork
-        (scripts/rccl_capture_probe.py, nested_* modes)."""
+        """``dst`` waits for the work issued on ``src``. Inside a capture
+        that names its origin (``_cap_origin``), a wait between two
+        non-origin streams is routed through the origin (origin waits
+        ``src``, ``dst`` waits origin): hipStreamEndCapture segfaults on this
+        ROCm when a stream forked into a capture is itself the source of
+        another fork (scripts/rccl_capture_probe.py, nested_* modes)."""
         o = self._cap_origin
         if o is None or dst == o or src == o:
             dst.wait_stream(src)
@@ -781,7 +781,8 @@ class DLRMTrainer(StreamGraphsMixin):
                                 True)
         else:
             self._dcn_backward(h)
-        emb.stage_bwd_local(self.emb_hyper)        # replicated tables' dense grads
+        if not self._whole_capture:                # (multi-rank graphs: an EC segment)
+            emb.stage_bwd_local(self.emb_hyper)    # replicated tables' dense grads
         if not self._mstream and self._ps is not None:
             self._wait(torch.cuda.current_stream(), self._ps)
 
@@ -825,8 +826,8 @@ class DLRMTrainer(StreamGraphsMixin):
                                         device=self.device)
             b = self._g16[lo:hi]
             ops.cast_bf16(g, b)
-            return (self.comm.all_reduce(b, async_op=True), g, b)
-        return (self.comm.all_reduce(g, async_op=True), None, None)
+            return (self.dcomm.all_reduce(b, async_op=True), g, b)
+        return (self.dcomm.all_reduce(g, async_op=True), None, None)
 
     def _m_allreduce_top_start(self):
         self._ar_top = None
@@ -945,8 +946,8 @@ class DLRMTrainer(StreamGraphsMixin):
             raise RuntimeError("pipelined trainer: call prime(first batch) before step()")
         if self.graph == "streams":
             self._ms_step()
-        elif self.graph == "whole":
-            self._whole_step()
+        elif self.graph == "mstreams":
+            self._mr_step()
         elif isinstance(self.graph, list):
             self._staged_step()
         elif self.graph is not None:
@@ -994,8 +995,8 @@ class DLRMTrainer(StreamGraphsMixin):
         torch.cuda.synchronize()
         if staged is None:
             staged = self.world > 1
-            if self._whole_ok():
-                self._capture_whole()
+            if self._mr_ok():
+                self._mr_capture()
                 return
         if not staged and self.world == 1:
             if streams:
@@ -1038,89 +1039,6 @@ class DLRMTrainer(StreamGraphsMixin):
         torch.cuda.synchronize()
         self.graph = seq
         self._graph_layout = self.emb.layout_version
-
-    # ------------------------------------------- whole-step graph (W > 1)
-    def _whole_ok(self) -> bool:
-        """The multi-rank step can be one graph: pipelined with the lookup in
-        the tail, every exchange enqueue-only (native RCCL or loopback), and
-        no host read inside the step (the row-wise capacity check is one)."""
-        return (self.world > 1 and self.cfg.whole_graph and self._pipe_lookup
-                and getattr(self.comm, "capturable", False)
-                and not (self.emb.rw_tables and self.emb.rw_dynamic))
-
-    def _drain_inflight(self):
-        """Order the current stream after every exchange left in flight by
-        eager stages (prime(), eager steps): nothing crosses a graph edge."""
-        self.emb.ids_exchange_wait()
-        if self.emb._pending:
-            self.emb.forward_wait()
-        se = self._side()
-        if se is not None:
-            torch.cuda.current_stream().wait_stream(se)
-        self._inflight = False
-
-    def _whole_stages(self):
-        stages = self._stages()
-        assert stages[-1][0] == "jw"
-        # the tail joins the next batch's pooled exchange and the side stream
-        # (a replay ends with everything it started complete)
-        return stages[:-1] + [("m", self._whole_tail), ("j", None)]
-
-    def _whole_tail(self):
-        for w in self.emb._pending or ():
-            w.wait()
-        self.emb._pending = None
-
-    def _capture_whole(self):
-        """W > 1: the pipelined step -- compute on two streams, every RCCL
-        exchange (comm stream), the next batch's load from static staging --
-        captured as ONE hipGraph: one launch per step instead of ~20 Python
-        stage issues, ~6 c10d collectives and their event waits
-        (host 683 us/step at emulated W=8, profiles/r03/emu/w8.log). The
-        cross-step overlap of the next lookup with the next bottom MLP is
-        given up (a replay ends joined)."""
-        sx = self.x0.clone()
-        self._stg = (sx, self.ids.clone(), self.label.clone())
-        self._drain_inflight()
-        torch.cuda.synchronize()
-        g = torch.cuda.CUDAGraph()
-        self._whole_capture = True
-        self._on_side = False
-        # the capture's origin is the comm stream (RCCL under capture must be
-        # enqueued on the origin: RcclComm.capture_origin); the compute runs
-        # on a stream forked from it and joins back at the end
-        origin = torch.cuda.Stream(device=self.device)
-        ms = torch.cuda.Stream(device=self.device)
-        route = getattr(self.comm, "capture_origin", None)
-        self._cap_origin = origin
-        try:
-            with graph_capture(g, pool=torch.cuda.graph_pool_handle(), stream=origin,
-                               capture_error_mode="thread_local"):
-                ms.wait_stream(origin)
-                with torch.cuda.stream(ms), (route(origin) if route else _nullctx()):
-                    for kind, fn in self._whole_stages():
-                        self._run_stage(kind, fn)
-                origin.wait_stream(ms)
-        finally:
-            self._whole_capture = False
-            self._cap_origin = None
-        # the captured tail's exchange handles are not real in-flight work
-        self.emb._ids_works = []
-        self.emb._pending = None
-        torch.cuda.synchronize()
-        # the capture ran nothing: the batch set before it (self._next) is the
-        # one the first replay must load
-        if self._next is not None:
-            d, i, l = self._next
-            ops.batch_load(d, sx, i, self._stg[1], l, self._stg[2])
-        self._whole = g
-        self.graph = "whole"
-        self._graph_layout = self.emb.layout_version
-
-    def _whole_step(self):
-        if getattr(self, "_inflight", False):
-            self._drain_inflight()
-        self._whole.replay()
 
     def pop_loss(self) -> float:
         """Mean training loss since the last call (one device->host read);

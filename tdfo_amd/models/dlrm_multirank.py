@@ -1,0 +1,225 @@
+"""Multi-rank DLRM / DCN-v2 step as per-stream hipGraphs with the RCCL
+collectives inside (mixin of ``DLRMTrainer``; W > 1, pipelined input dist).
+
+Why this shape (all measured on this ROCm, scripts/rccl_capture_probe.py and
+scripts/whole_capture_bisect.py):
+
+* RCCL can only be captured on the capture's ORIGIN stream: a collective on a
+  stream forked into a capture (torch's own async c10d collectives included)
+  makes hipStreamEndCapture segfault, as does any fork whose source is itself
+  a forked stream.
+* One captured graph's independent branches are replayed mostly in order, so
+  a single whole-step graph serialises the embedding work behind the MLP
+  (emulated W=8: 0.95 ms/step vs 0.91 for the staged replay).
+
+So each stream's share of the step is captured as segments with THAT stream
+as origin (no forks at all), and the segments of a stream are chained with
+explicit event record / wait nodes into one executable graph
+(``ops.ComposedGraph``), launched on its own stream -- three launches per
+step instead of ~20 Python stage issues and ~8 c10d calls:
+
+  M  (MLP):      [wait d'] bottom fwd  [wait c5'] top fwd/bwd + interaction bwd
+                 (m2)  bottom bwd, next batch's load from staging (m4)  top
+                 weight grads (m3)
+  D  (dense      [wait c5'] ids-only sort of this batch (e0)  [wait m2]
+      comm):     replicated tables' dense grad + all-reduce (dp)  [wait m4]
+                 bottom-bucket all-reduce  [wait m3] top-bucket all-reduce,
+                 dense optimizer (d)
+  EC (embedding  [wait m2] gradient all-to-all  [wait e0, dp] fused embedding
+      + its      update  [wait m4] bucketize + id all-to-all, lookup + pooled
+      RCCL):     all-to-all (c5)
+
+(primed events: the previous step's records). The embedding exchanges and
+the dense all-reduces use two communicators so they run concurrently (the
+role of TorchRec's input/output dists beside the DDP reducer,
+torchrec/train.py:241-260). A wait node binds to the most recent record
+enqueued before its graph is launched, so the per-step launch order M, D, EC
+makes M's waits see the previous step's records and D's / EC's this step's
+(D's c5 wait: the previous step's, EC has not been launched yet).
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import ops
+from ..utils.capture import graph_capture
+
+
+class MultiRankStreamsMixin:
+    """Per-stream graph capture / replay for W > 1 (``capture_graph`` picks it
+    when ``_mr_ok()``)."""
+
+    def _mr_ok(self) -> bool:
+        """Pipelined with the lookup in the tail, every exchange enqueue-only
+        (native RCCL or loopback), and no host read inside the step (the
+        row-wise capacity check is one)."""
+        return (self.world > 1 and self.cfg.stream_graphs and self._pipe_lookup
+                and getattr(self.comm, "capturable", False)
+                and getattr(self.dcomm, "capturable", False)
+                and not (self.emb.rw_tables and self.emb.rw_dynamic))
+
+    def _mr_drain(self):
+        """Complete every exchange left in flight by eager stages (prime(),
+        eager steps): nothing crosses into the graphs."""
+        self.emb.ids_exchange_wait()
+        if self.emb._pending:
+            self.emb.forward_wait()
+        se = self._side()
+        if se is not None:
+            torch.cuda.current_stream().wait_stream(se)
+        self._mr_inflight = False
+
+    def _mr_segments(self):
+        emb = self.emb
+        hyper = self.emb_hyper
+
+        def m2():
+            emb.forward_wait()                  # post-exchange assembly only
+            self._s_top()
+
+        def dp_a():                             # replicated tables: dense grad + all-reduce
+            emb.stage_bwd_local(hyper)
+            emb.backward_start(exchange=False)
+
+        def ec_upd():
+            emb.backward_wait()                 # (handles of stream-ordered enqueues)
+            self._s_emb_update()
+
+        def ec_b1():
+            if not emb.fwd_prep_noop:
+                emb.stage_fwd_prep(self.ids)
+            emb.stage_fwd_ids_exchange()
+
+        def ec_b2():
+            emb.stage_fwd_lookup()
+            emb.stage_fwd_out_exchange()
+
+        def d_b():
+            self._m_allreduce_top_start()
+            self._m_allreduce_wait()
+            self._s_dense_update()
+
+        def m4():
+            self._s_bottom_bwd()
+            self._m_load_next()                 # x0 / labels / ids free: next batch in
+
+        def ec_b():
+            ec_b1()
+            ec_b2()
+
+        return {"M1": self._s_bottom_fwd, "M2": m2, "M4": m4,
+                "M3": self._s_top_wgrad if self._defer_top_wgrad else None,
+                "D0": emb.stage_bwd_prepare, "Dp": dp_a, "Da": self._m_allreduce_start,
+                "Db": d_b, "EC1": lambda: emb.backward_start(dp=False), "ECu": ec_upd,
+                "ECb": ec_b}
+
+    def _mr_capture(self):
+        assert self.device.type == "cuda"
+        dev = self.device
+        self._stg = (self.x0.clone(), self.ids.clone(), self.label.clone())
+        self._mr_drain()
+        torch.cuda.synchronize()
+        streams = {k: torch.cuda.Stream(device=dev) for k in ("M", "D", "EC")}
+        ev = {k: ops.SyncEvent(2) for k in ("d", "c5", "m2", "m3", "m4", "e0", "dp")}
+        seg = self._mr_segments()
+        home = lambda name: "EC" if name.startswith("EC") else name[0]  # noqa: E731
+        pool = torch.cuda.graph_pool_handle()
+        graphs = {}
+        self._whole_capture = True       # staging load, no _ps fork, no event records
+        was_mstream = self._mstream
+        self._mstream = True             # the ids-only sort is its own segment (D0)
+        try:
+            for name, fn in seg.items():
+                if fn is None:
+                    continue
+                st = streams[home(name)]
+                g = torch.cuda.CUDAGraph(keep_graph=True)
+                routes = [c.capture_origin(st) for c in {id(self.comm): self.comm,
+                                                          id(self.dcomm): self.dcomm}.values()
+                          if hasattr(c, "capture_origin")]
+                with graph_capture(g, pool=pool, stream=st, capture_error_mode="thread_local"):
+                    for r in routes:
+                        r.__enter__()
+                    try:
+                        fn()
+                    finally:
+                        for r in routes:
+                            r.__exit__(None, None, None)
+                graphs[name] = g
+        finally:
+            self._whole_capture = False
+            self._mstream = was_mstream
+        # the captured exchanges' handles are not real in-flight work
+        self.emb._ids_works = []
+        self.emb._pending = None
+        self._ar_top = self._ar_work = None
+        torch.cuda.synchronize()
+
+        def chain(parts):
+            return ops.ComposedGraph([(k, graphs[v] if k == "graph" else ev[v])
+                                      for k, v in parts if k != "graph" or v in graphs])
+
+        # M: the bottom backward before the top weight grads, so the next
+        # batch may load (x0 free) and the bottom bucket reduce sooner
+        # (every segment boundary costs ~8 us of queue idle and every
+        # cross-stream wait ~15-23 us: scripts/mr_sched_probe.py)
+        composed = {
+            # M: the bottom backward (+ the next batch's load into x0 / ids /
+            # labels, all of whose readers have run) before the top weight
+            # grads, so the embedding side and the bottom bucket go sooner
+            "M": chain([("wait", "d"), ("graph", "M1"), ("wait", "c5"), ("graph", "M2"),
+                        ("record", "m2"), ("graph", "M4"), ("record", "m4"), ("graph", "M3"),
+                        ("record", "m3")]),
+            # D: the ids-only sort of this batch (its ids arrived with the
+            # previous step's exchanges), the replicated tables' dense grad +
+            # all-reduce, the two dense buckets and the dense optimizer
+            "D": chain([("wait", "c5"), ("graph", "D0"), ("record", "e0"), ("wait", "m2"),
+                        ("graph", "Dp"), ("record", "dp"), ("wait", "m4"), ("graph", "Da"),
+                        ("wait", "m3"), ("graph", "Db"), ("record", "d")]),
+            # EC: gradient all-to-all, fused embedding update, then the next
+            # batch's bucketize, id all-to-all, lookup and pooled all-to-all
+            "EC": chain([("wait", "m2"), ("graph", "EC1"), ("wait", "e0"), ("wait", "dp"),
+                         ("graph", "ECu"), ("wait", "m4"), ("graph", "ECb"), ("record", "c5")]),
+        }
+        self._mr = {"streams": streams, "events": ev, "graphs": graphs, "composed": composed,
+                    "launched": False}
+        # the capture ran nothing: the batch handed in before it is the one
+        # the first replay loads
+        if self._next is not None:
+            d, i, l = self._next
+            sx, si, sl = self._stg
+            ops.batch_load(d, sx, i, si, l, sl)
+        torch.cuda.synchronize()
+        self.graph = "mstreams"
+        self._graph_layout = self.emb.layout_version
+
+    def _mr_stage_next(self, dense, ids, label):
+        """Copy the next batch into the staging buffers on the current stream,
+        after the previous step's graph has read them (its m4 record)."""
+        cur = torch.cuda.current_stream()
+        if self._mr["launched"]:
+            self._mr["events"]["m4"].wait(cur)
+        sx, si, sl = self._stg
+        ops.batch_load(dense, sx, ids, si, label, sl)
+
+    def _mr_step(self):
+        if getattr(self, "_mr_inflight", False):
+            self._mr_drain()
+        mr = self._mr
+        s, g = mr["streams"], mr["composed"]
+        cur = torch.cuda.current_stream()
+        # M loads the staging this thread just wrote on the current stream;
+        # on the first replay every stream starts behind the eager steps
+        for k in (("M", "D", "EC") if not mr["launched"] else ("M",)):
+            s[k].wait_stream(cur)
+        # launch order M, D, EC: a wait node binds to the latest record
+        # enqueued before its graph's launch (see the module docstring)
+        for k in ("M", "D", "EC"):
+            with torch.cuda.stream(s[k]):
+                g[k].replay()
+        mr["launched"] = True
+
+    def _mr_sync(self):
+        cur = torch.cuda.current_stream()
+        for st in self._mr["streams"].values():
+            cur.wait_stream(st)

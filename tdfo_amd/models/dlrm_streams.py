@@ -192,3 +192,5 @@ class StreamGraphsMixin:
                 torch.cuda.current_stream().wait_stream(self._ms["cstream"])
         if getattr(self, "_sides", None) is not None:
             torch.cuda.current_stream().wait_stream(self._sides)
+        if getattr(self, "_mr", None) is not None:
+            self._mr_sync()

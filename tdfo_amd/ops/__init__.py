@@ -452,6 +452,11 @@ def synth_criteo(seed, rank, batch_index, B, rows, pooling, base, dist, alpha, w
                            int(dist), float(alpha), w_dense, table_bias, dense, ids, label)
 
 
+def stamp(buf, cnt, seg: int, nseg: int, which: int):
+    """Device timestamp of segment ``seg``'s current run (see stamp_kernel)."""
+    _native().stamp(buf, cnt, int(seg), int(nseg), int(which))
+
+
 def spin_us(us: float):
     """Occupy the current stream for ``us`` microseconds (one sleeping wave):
     the modelled link time of an emulated collective."""

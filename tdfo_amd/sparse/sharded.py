@@ -87,6 +87,7 @@ class ShardedEmbeddingBags:
         self.device = torch.device(device)
         self.group = group
         self.comm = as_comm(group) if plan.world_size > 1 else None
+        self.dp_comm = None        # the replicated tables' reduction (default: comm)
         self.mean = mean
         self.optim = optim
         for s in plan.shards:
@@ -295,6 +296,11 @@ class ShardedEmbeddingBags:
             zero_noop = (optim.code in (ops.EMB_SGD, ops.EMB_ADAGRAD, ops.EMB_ROWWISE_ADAGRAD)
                          and optim.weight_decay == 0.0)
             self.dp_dense = W > 1 and dp_bytes <= dp_dense_max_bytes and zero_noop
+            # one id per bag: the dense-gradient backward sorts each table's
+            # ids in LDS (passes for its largest id only: 2 for these small
+            # tables) instead of the device-wide radix sort
+            self.dp_segsort = 1 if (all(self.L[t] == 1 for t in dpt) and B <= 8192
+                                    and not mean) else 0
             if self.dp_dense:
                 self.dp_dgrad = torch.zeros(self.dp_store.total_rows, D, dtype=torch.float32,
                                             device=self.device)
@@ -594,7 +600,7 @@ class ShardedEmbeddingBags:
             ops.embedding_bwd(st.weight, st.row_offset, self.dp_ids, self.dp_offsets,
                               self.dp_out_off, len(self.dp_tables), self.B, d_recv,
                               self.dp_width, ops.EMB_DENSE_GRAD, hyper, key_bits=st.key_bits,
-                              mean=self.mean, dense_grad=self.dp_dgrad)
+                              mean=self.mean, dense_grad=self.dp_dgrad, segsort=self.dp_segsort)
 
     def backward(self, hyper: torch.Tensor, d_recv: Optional[torch.Tensor] = None):
         """The whole backward in one call (tests / eager use)."""
@@ -602,10 +608,23 @@ class ShardedEmbeddingBags:
         self.backward_start(d_recv)
         self.backward_finish(hyper)
 
-    def backward_start(self, d_recv: Optional[torch.Tensor] = None):
+    def backward_start(self, d_recv: Optional[torch.Tensor] = None, exchange: bool = True,
+                       dp: bool = True):
         """Start the gradient exchange (async on GPU). ``d_recv`` defaults to
-        ``self.d_recv`` (same layout as ``self.recv``)."""
+        ``self.d_recv`` (same layout as ``self.recv``). ``exchange`` /
+        ``dp``: only the sharded tables' exchanges (table/column-wise
+        all-to-all, row-wise all-gather) / only the replicated tables'
+        reduction, so the latter can wait for their dense gradient
+        (``stage_bwd_local``) on another stream while the former is in
+        flight; ``backward_wait`` waits for both."""
         d_recv = self.d_recv if d_recv is None else d_recv
+        W, B = self.world, self.B
+        if exchange:
+            self._backward_exchange(d_recv)
+        if dp:
+            self._backward_dp(d_recv)
+
+    def _backward_exchange(self, d_recv):
         W, B = self.world, self.B
         tw_total = sum(self.tw_recv_sizes)
         if self.cw_tables:
@@ -615,18 +634,22 @@ class ShardedEmbeddingBags:
             work = self.comm.all_to_all(self.d_pooled[: W * B * self.dsum[self.rank]],
                                         d_recv[:tw_total], [B * self.dsum[self.rank]] * W,
                                         self.tw_recv_sizes, async_op=True)
-        self._dp_work = None
-        if W > 1 and self.dp_tables and self.dp_dense:
-            self._dp_work = self.comm.all_reduce(self.dp_dgrad, async_op=True)
-        elif W > 1 and self.dp_tables:
-            self._dp_work = self.comm.all_gather(
-                self.dp_g_grad, d_recv[self.dp_base: self.dp_base + B * self.dp_width],
-                async_op=True)
         self._rw_work = None
         if W > 1 and self.rw_tables:
             self._rw_work = self.comm.all_gather(self.rw_gbuf, self._rw_region(d_recv),
                                                  async_op=True)
         self._bw = (work, d_recv)
+
+    def _backward_dp(self, d_recv):
+        W, B = self.world, self.B
+        self._dp_work = None
+        comm = self.dp_comm or self.comm
+        if W > 1 and self.dp_tables and self.dp_dense:
+            self._dp_work = comm.all_reduce(self.dp_dgrad, async_op=True)
+        elif W > 1 and self.dp_tables:
+            self._dp_work = comm.all_gather(
+                self.dp_g_grad, d_recv[self.dp_base: self.dp_base + B * self.dp_width],
+                async_op=True)
 
     def backward_wait(self):
         work, d_recv = self._bw

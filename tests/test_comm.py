@@ -60,6 +60,7 @@ def test_emulated_rank0_of_eight_trains(strategy, pipeline):
     if pipeline:
         tr.prime(*data.next())
     comm.reset_stats()
+    tr.dcomm.reset_stats()
     steps = 3
     for _ in range(steps):
         if pipeline:
@@ -70,6 +71,8 @@ def test_emulated_rank0_of_eight_trains(strategy, pipeline):
     loss = tr.pop_loss() / (steps * B)
     assert math.isfinite(loss)
     st = comm.stats
-    assert st["all_reduce_sum"][0] >= 2 * steps         # the two dense-gradient buckets
+    # the two dense-gradient buckets go through the dense twin communicator
+    assert tr.dcomm is not comm and isinstance(tr.dcomm, LoopbackComm)
+    assert tr.dcomm.stats["all_reduce_sum"][0] >= 2 * steps
     if strategy in ("table_wise", "auto"):
         assert st["all_to_all"][0] >= 3 * steps          # ids, pooled rows, pooled grads

@@ -4,10 +4,11 @@ whole-step multi-rank hipGraph it enables.
 * RcclComm on a one-rank RCCL communicator (the box has one GPU; RCCL
   refuses two ranks on one device): every op against its definition, eager
   and captured into a hipGraph, sync and async (comm-stream fork / join).
-* The W > 1 DLRM step captured as ONE graph (``DLRMConfig.whole_graph``)
-  with loopback collectives (rank 0 of a W-rank job, ``LoopbackComm``) is
-  bit-identical to the staged replay (graphs between eagerly issued
-  exchanges) over the same batches.
+* The W > 1 DLRM step as per-stream graphs with the collectives inside
+  (``DLRMConfig.stream_graphs``, models/dlrm_multirank.py) with loopback
+  collectives (rank 0 of a W-rank job, ``LoopbackComm``) is bit-identical to
+  the staged replay (graphs between eagerly issued exchanges) over the same
+  batches.
 """
 import os
 
@@ -103,7 +104,7 @@ def _trainer(whole: bool, W: int, strategy: str):
     rows = [5000, 7, 30000, 1000, 3, 800, 64, 129]
     cfg = DLRMConfig(embedding_dim=64, table_rows=rows, bottom=[128, 64], top=[128, 64, 1],
                      sharding=strategy, pipeline=True, pooling=[1, 2, 1, 3, 1, 1, 1, 1],
-                     whole_graph=whole, seed=3)
+                     stream_graphs=whole, seed=3)
     dev = torch.device("cuda", 0)
     comm = LoopbackComm(W, 0, dev)
     tr = DLRMTrainer(cfg, 256, dev, group=comm, rank=0, world_size=W)
@@ -111,7 +112,7 @@ def _trainer(whole: bool, W: int, strategy: str):
 
 
 @pytest.mark.parametrize("strategy", ["table_wise", "auto", "column_wise", "data_parallel"])
-def test_whole_step_graph_matches_staged(strategy):
+def test_stream_graphs_match_staged(strategy):
     from tdfo_amd.data.synthetic import SyntheticCriteo
 
     W = 4
@@ -125,7 +126,7 @@ def test_whole_step_graph_matches_staged(strategy):
             tr.set_next_batch(*batches[i + 1])
             tr.step()
         tr.capture_graph(warmup=0)
-        assert (tr.graph == "whole") == whole, tr.graph
+        assert (tr.graph == "mstreams") == whole, tr.graph
         for i in range(2, 8):
             tr.set_next_batch(*batches[i + 1])
             tr.step()
@@ -147,9 +148,9 @@ def test_whole_step_graph_matches_staged(strategy):
             assert torch.equal(a, b)
 
 
-def test_whole_step_graph_host_cost():
-    """One launch per step: the host issues a step of the emulated W=8 job in
-    a small fraction of the staged path's time."""
+def test_stream_graphs_host_cost():
+    """Three graph launches per step: the host issues a step of the emulated
+    W=8 job in a small fraction of the staged path's time."""
     import time
 
     from tdfo_amd.data.synthetic import SyntheticCriteo
