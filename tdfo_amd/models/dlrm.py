@@ -24,6 +24,7 @@ once into a hipGraph and replayed (no tracing compiler):
 from __future__ import annotations
 
 import math
+import warnings
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
 
@@ -996,8 +997,15 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin):
         if staged is None:
             staged = self.world > 1
             if self._mr_ok():
-                self._mr_capture()
-                return
+                try:
+                    self._mr_capture()
+                    return
+                except Exception as e:  # deterministic on every rank: all fall back alike
+                    warnings.warn(f"multi-rank stream graphs unavailable ({e!r}); "
+                                  "replaying staged graphs")
+                    self._mr = None
+                    self._whole_capture = False
+                    torch.cuda.synchronize()
         if not staged and self.world == 1:
             if streams:
                 self._capture_streams()

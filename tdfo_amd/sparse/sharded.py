@@ -299,8 +299,8 @@ class ShardedEmbeddingBags:
             # one id per bag: the dense-gradient backward sorts each table's
             # ids in LDS (passes for its largest id only: 2 for these small
             # tables) instead of the device-wide radix sort
-            self.dp_segsort = 1 if (all(self.L[t] == 1 for t in dpt) and B <= 8192
-                                    and not mean) else 0
+            self.dp_onehot = all(self.L[t] == 1 for t in dpt)      # lookup skips offsets
+            self.dp_segsort = 1 if (self.dp_onehot and B <= 8192 and not mean) else 0
             if self.dp_dense:
                 self.dp_dgrad = torch.zeros(self.dp_store.total_rows, D, dtype=torch.float32,
                                             device=self.device)
@@ -543,7 +543,7 @@ class ShardedEmbeddingBags:
         if self.dp_tables:
             self.dp_store.forward(self.dp_ids, self.dp_offsets, self.dp_store.row_offset,
                                   len(self.dp_tables), B, self.recv, self.dp_out_off,
-                                  self.dp_width, mean=self.mean)
+                                  self.dp_width, mean=self.mean, onehot=self.dp_onehot)
             if W > 1 and not self.dp_dense:
                 torch.index_select(self.dp_g_ids, 0, self.dp_g_perm, out=self.dp_g_ids_t)
         if self.tw_nv:
