@@ -11,6 +11,8 @@
 // Backward, one wave per sample: dX = S X with S the symmetric matrix built
 // from dZ. S comes from an LDS copy of the dZ row; X is staged in LDS and
 // read as the MFMA B operand with ds_read_b64_tr_b16 (k = feature index).
+// All column tiles' MFMAs issue back to back before their epilogue, which
+// reads nothing from LDS (37 -> see profiles for the in-step time).
 // The concat passthrough (dZ[:, :D]) and the bottom-MLP ReLU mask are fused
 // into the dense-slot store, and embedding-slot gradients are written
 // directly in the layout the embedding backward / all-to-all consumes.
@@ -24,7 +26,7 @@ namespace tdfo {
 namespace {
 
 constexpr int WAVES = 4;
-constexpr int SLOT_BYTES = 64 * 8;   // backward: SlotMap copy at the LDS base
+constexpr int SLOT_BYTES = 128 * 8;  // backward: both SlotMaps' copies at the LDS base
 
 __device__ __forceinline__ const uint16_t* feat_row(const uint16_t* dense,
                                                     int64_t ld_dense,
@@ -139,10 +141,17 @@ __global__ __launch_bounds__(256) void inter_bwd_kernel(
   const int ldz_al = (int)((ldz + 7) & ~7LL);
   // slot offsets / strides in LDS: the unrolled chunk loads below index them
   // per lane, which on the kernel-argument struct would go through scratch
+  // (and the gradient slots' too: read per lane in the store loop, the
+  // kernel-argument copy costs a vector load + vmcnt(0) per row, which also
+  // drained the next sample's prefetch every iteration)
   int64_t* slot = (int64_t*)smem_raw;   // [0, 32): off, [32, 64): stride
+  int64_t* dslot = slot + 64;           // the same for the gradient slots
   if (threadIdx.x == 0) {
 #pragma unroll
-    for (int q = 0; q < 32; ++q) { slot[q] = sm.off[q]; slot[32 + q] = sm.stride[q]; }
+    for (int q = 0; q < 32; ++q) {
+      slot[q] = sm.off[q]; slot[32 + q] = sm.stride[q];
+      dslot[q] = dsm.off[q]; dslot[32 + q] = dsm.stride[q];
+    }
   }
   __syncthreads();
   char* base = smem_raw + SLOT_BYTES + w * (XB + ldz_al * 2);
@@ -217,7 +226,13 @@ __global__ __launch_bounds__(256) void inter_bwd_kernel(
         }
       }
     }
-    if (it + 1 < iters && bn < B) load(bn);
+    // this sample's dZ chunk and X chunk 0 (lanes < D / 8: the dense slot)
+    // outlive the prefetch below: the epilogue's passthrough / ReLU mask
+    const uint4 zv0s = zv0;
+    const uint4 xv0s = __builtin_bit_cast(uint4, xv[0]);
+    // unconditional (clamped) prefetch: a conditional one makes hipcc copy
+    // the loaded registers at the join and wait for them right away
+    load(bn < B ? bn : B - 1);
     wave_sync();
     if (valid) {
       // S operand: S[i][k], i = lane&31, k = 16ks + 8h + jj, read from the
@@ -238,63 +253,95 @@ __global__ __launch_bounds__(256) void inter_bwd_kernel(
       // D = 16: one 32-wide column tile whose upper half reads past the row
       // (finite LDS data, never stored)
       constexpr int NT = D >= 32 ? D / 32 : 1;
+      // column tiles in batches of up to 4: every batch's MFMAs issue back to
+      // back (their transposing reads ahead of them), then its epilogue --
+      // no MFMA result is read right after its own MFMA and no LDS round
+      // trip sits between them (the dense slot's passthrough and ReLU mask
+      // come from registers: lane c of zv0s / xv0s holds chunk c of the dZ
+      // row / of X row 0, broadcast with readlane)
+      constexpr int NB = NT < 4 ? NT : 4;
 #pragma unroll
-      for (int nt = 0; nt < NT; ++nt) {
-        f32x16_t acc = {};
+      for (int nb = 0; nb < NT; nb += NB) {
+        f32x16_t acc[NB];
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          s16x4_t v[2];
+        for (int t = 0; t < NB; ++t) {
+          const int nt = nb + t;
+          acc[t] = f32x16_t{};
 #pragma unroll
-          for (int hf = 0; hf < 2; ++hf) {
-            const int j = 16 * ks + 8 * (g >> 1) + 4 * hf + q;
-            const int d = 32 * nt + 16 * (g & 1) + 4 * pp;
-            const int off = j * D * 2 + (((d >> 3) ^ xswz<D>(j)) << 4) + ((d & 7) << 1);
-            v[hf] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((TDFO_LDS s16x4_t*)(
-                (TDFO_LDS char*)xs + off));
+          for (int ks = 0; ks < 2; ++ks) {
+            s16x4_t v[2];
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf) {
+              const int j = 16 * ks + 8 * (g >> 1) + 4 * hf + q;
+              const int d = 32 * nt + 16 * (g & 1) + 4 * pp;
+              const int off = j * D * 2 + (((d >> 3) ^ xswz<D>(j)) << 4) + ((d & 7) << 1);
+              v[hf] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((TDFO_LDS s16x4_t*)(
+                  (TDFO_LDS char*)xs + off));
+            }
+            s16x8_t bb = {v[0][0], v[0][1], v[0][2], v[0][3],
+                          v[1][0], v[1][1], v[1][2], v[1][3]};
+            // dX^T = X^T S (S symmetric): the X fragment as A, S as B, so each
+            // lane's accumulators are 4 runs of 4 consecutive d of ONE feature
+            // row i = lane & 31 (8-B LDS writes below instead of 16 scalar ones)
+            acc[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                __builtin_bit_cast(bf16x8_t, bb), sa[ks], acc[t], 0, 0, 0);
           }
-          s16x8_t bb = {v[0][0], v[0][1], v[0][2], v[0][3],
-                        v[1][0], v[1][1], v[1][2], v[1][3]};
-          // dX^T = X^T S (S symmetric): the X fragment as A, S as B, so each
-          // lane's accumulators are 4 runs of 4 consecutive d of ONE feature
-          // row i = lane & 31 (8-B LDS writes below instead of 16 scalar ones)
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-              __builtin_bit_cast(bf16x8_t, bb), sa[ks], acc, 0, 0, 0);
         }
-        // dX rows -> per-wave bf16 image ys [32][D] (row 0 gets the concat
-        // passthrough dZ[:, :D] and the bottom-MLP ReLU mask here)
-        if (i < F) {
+#pragma unroll
+        for (int t = 0; t < NB; ++t) {
+          const int nt = nb + t;
+          // dX rows -> per-wave bf16 image ys [32][D] (row 0 gets the concat
+          // passthrough dZ[:, :D] and the bottom-MLP ReLU mask here)
 #pragma unroll
           for (int gq = 0; gq < 4; ++gq) {
             const int d0 = 32 * nt + 8 * gq + 4 * h;
             if (D < 32 && d0 >= D) continue;
             float v[4];
 #pragma unroll
-            for (int q4 = 0; q4 < 4; ++q4) v[q4] = acc[4 * gq + q4];
+            for (int q4 = 0; q4 < 4; ++q4) v[q4] = acc[t][4 * gq + q4];
+            // chunk (d0 >> 3) of the dZ row and of X row 0 (wave-uniform reads)
+            const int ch = (32 * nt + 8 * gq) >> 3;
+            const uint32_t z0 = __builtin_amdgcn_readlane(zv0s.x, ch);
+            const uint32_t z1 = __builtin_amdgcn_readlane(zv0s.y, ch);
+            const uint32_t z2 = __builtin_amdgcn_readlane(zv0s.z, ch);
+            const uint32_t z3 = __builtin_amdgcn_readlane(zv0s.w, ch);
+            const uint32_t x0 = __builtin_amdgcn_readlane(xv0s.x, ch);
+            const uint32_t x1 = __builtin_amdgcn_readlane(xv0s.y, ch);
+            const uint32_t x2 = __builtin_amdgcn_readlane(xv0s.z, ch);
+            const uint32_t x3 = __builtin_amdgcn_readlane(xv0s.w, ch);
             if (i == 0) {
-              const uint2 zp = *(const uint2*)(zrow + d0);
-              v[0] += bf2f((uint16_t)(zp.x & 0xffff)); v[1] += bf2f((uint16_t)(zp.x >> 16));
-              v[2] += bf2f((uint16_t)(zp.y & 0xffff)); v[3] += bf2f((uint16_t)(zp.y >> 16));
+              const uint32_t za = h ? z2 : z0, zb = h ? z3 : z1;
+              v[0] += bf2f((uint16_t)(za & 0xffff)); v[1] += bf2f((uint16_t)(za >> 16));
+              v[2] += bf2f((uint16_t)(zb & 0xffff)); v[3] += bf2f((uint16_t)(zb >> 16));
               if (relu_mask) {
-                const uint2 xm = *(const uint2*)(xs + (((d0 >> 3) ^ xswz<D>(0)) << 4) + ((d0 & 7) << 1));
-                if (!(bf2f((uint16_t)(xm.x & 0xffff)) > 0.f)) v[0] = 0.f;
-                if (!(bf2f((uint16_t)(xm.x >> 16)) > 0.f)) v[1] = 0.f;
-                if (!(bf2f((uint16_t)(xm.y & 0xffff)) > 0.f)) v[2] = 0.f;
-                if (!(bf2f((uint16_t)(xm.y >> 16)) > 0.f)) v[3] = 0.f;
+                const uint32_t xa = h ? x2 : x0, xb = h ? x3 : x1;
+                if (!(bf2f((uint16_t)(xa & 0xffff)) > 0.f)) v[0] = 0.f;
+                if (!(bf2f((uint16_t)(xa >> 16)) > 0.f)) v[1] = 0.f;
+                if (!(bf2f((uint16_t)(xb & 0xffff)) > 0.f)) v[2] = 0.f;
+                if (!(bf2f((uint16_t)(xb >> 16)) > 0.f)) v[3] = 0.f;
               }
             }
-            *(uint2*)((char*)ys + i * D * 2 + (((d0 >> 3) ^ xswz<D>(i)) << 4) + ((d0 & 7) << 1)) =
-                make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+            if (i < F)
+              *(uint2*)((char*)ys + i * D * 2 + (((d0 >> 3) ^ xswz<D>(i)) << 4) + ((d0 & 7) << 1)) =
+                  make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
           }
         }
       }
       // coalesced 16-B stores of the F gradient rows into their slots (the
       // wave's own LDS image: in-wave LDS order, no barrier needed)
-      for (int c = lane; c < F * CPR; c += 64) {
-        const int j = c / CPR, ch = c - j * CPR;
-        const uint4 v = *(const uint4*)((const char*)ys + j * D * 2 + ((ch ^ xswz<D>(j)) << 4));
-        uint16_t* dst = j == 0 ? d_dense + (int64_t)b * ld_ddense
-                               : d_emb + dsm.off[j] + (int64_t)b * dsm.stride[j];
-        *(uint4*)(dst + ch * 8) = v;
+      // (a fixed, unrolled count of predicated stores: hipcc can then count
+      // them and wait for the next sample's prefetched rows at the loop top
+      // with vmcnt(stores) instead of draining the stores with vmcnt(0))
+#pragma unroll
+      for (int k = 0; k < XC; ++k) {
+        const int c = lane + 64 * k;
+        if (c < F * CPR) {
+          const int j = c / CPR, ch = c - j * CPR;
+          const uint4 v = *(const uint4*)((const char*)ys + j * D * 2 + ((ch ^ xswz<D>(j)) << 4));
+          uint16_t* dst = j == 0 ? d_dense + (int64_t)b * ld_ddense
+                                 : d_emb + dslot[j] + (int64_t)b * dslot[32 + j];
+          *(uint4*)(dst + ch * 8) = v;
+        }
       }
     }
     wave_sync();

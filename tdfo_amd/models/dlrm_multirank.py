@@ -72,18 +72,21 @@ class MultiRankStreamsMixin:
     def _mr_segments(self):
         emb = self.emb
         hyper = self.emb_hyper
+        dp_dense = bool(emb.dp_tables) and emb.dp_dense
 
         def m2():
             emb.forward_wait()                  # post-exchange assembly only
             self._s_top()
 
-        def dp_a():                             # replicated tables: dense grad + all-reduce
-            emb.stage_bwd_local(hyper)
+        def dp_a():                             # replicated tables: dense grad, all-reduce,
+            emb.stage_bwd_local(hyper)          # update (all on D, beside the exchange)
             emb.backward_start(exchange=False)
+            if dp_dense:
+                emb.stage_bwd_update(hyper, sharded=False)
 
         def ec_upd():
             emb.backward_wait()                 # (handles of stream-ordered enqueues)
-            self._s_emb_update()
+            emb.stage_bwd_update(hyper, dp=not dp_dense)
 
         def ec_b1():
             if not emb.fwd_prep_noop:

@@ -682,21 +682,23 @@ class ShardedEmbeddingBags:
                                      self.rw_dummy, self.rw_bwd_ws)
         self._rw_prepared = True
 
-    def stage_bwd_update(self, hyper: torch.Tensor):
-        """Fused sort-based backward + optimizer on this rank's table-wise shards."""
+    def stage_bwd_update(self, hyper: torch.Tensor, sharded: bool = True, dp: bool = True):
+        """Fused sort-based backward + optimizer on this rank's shards
+        (``sharded``: table/column/row-wise; ``dp``: the replicated tables,
+        whose update the multi-rank stream graphs run beside the others)."""
         d_recv = self._bw[1] if getattr(self, "_bw", None) else self.d_recv
         W, B = self.world, self.B
         grad = self.d_pooled if W > 1 else d_recv
-        if self.tw_nv:
+        if self.tw_nv and sharded:
             self.tw_store.backward_apply(self.tw_recv_ids, self.tw_v_offsets, self.tw_v_row_off,
                                          self.tw_nv, B, grad, self.tw_v_out_off,
                                          self.tw_ld, hyper, mean=self.mean,
                                          segsort=self.tw_segsort)
-        if self.cw_tables and self.cw_nv:
+        if self.cw_tables and self.cw_nv and sharded:
             self.cw_store.backward_update(self.cw_recv_ids, self.cw_v_offsets, self.cw_v_row_off,
                                           self.cw_nv, B, grad, self.cw_v_out_off,
                                           self.dsum[self.rank], hyper, mean=self.mean)
-        if self.dp_tables:
+        if self.dp_tables and dp:
             ndp = len(self.dp_tables)
             if W > 1 and self.dp_dense:
                 from .. import ops
@@ -713,7 +715,7 @@ class ShardedEmbeddingBags:
                 self.dp_store.backward_update(self.dp_ids, self.dp_offsets, self.dp_store.row_offset,
                                               ndp, B, d_recv, self.dp_out_off, self.dp_width, hyper,
                                               mean=self.mean)
-        if self.rw_tables:
+        if self.rw_tables and sharded:
             from .. import ops
             if not self._rw_prepared:
                 self._rw_prepare()
