@@ -25,7 +25,6 @@
 //
 // The library is the RCCL torch itself links (torch/lib/librccl.so, found via
 // this library's rpath), so there is one RCCL in the process.
-#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -138,17 +137,9 @@ int64_t rccl_init(const Tensor& id, int64_t world, int64_t rank) {
   ncclUniqueId uid;
   std::memcpy(uid.internal, id.contiguous().data_ptr(), NCCL_UNIQUE_ID_BYTES);
   TDFO_NCCL_OK(ncclCommInitRank(&c->comm, (int)world, uid, (int)rank));
-  // highest priority: the exchanges gate the compute that waits on them
-  int lo = 0, hi = 0;
-  TDFO_HIPC_OK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-  const char* pe = getenv("TDFO_RCCL_PRIO");
-  const int mode = pe ? atoi(pe) : 1;
-  if (mode == 1)
-    TDFO_HIPC_OK(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, hi));
-  else if (mode == 2)
-    TDFO_HIPC_OK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-  else
-    TDFO_HIPC_OK(hipStreamCreate(&c->stream));
+  // default priority: high-priority streams slowed the multi-stream step
+  // ~3x (models/dlrm_multirank.py)
+  TDFO_HIPC_OK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   for (int k = 0; k < kSlots; ++k) {
     TDFO_HIPC_OK(hipEventCreateWithFlags(&c->fork[k], hipEventDisableTiming));
     TDFO_HIPC_OK(hipEventCreateWithFlags(&c->done[k], hipEventDisableTiming));

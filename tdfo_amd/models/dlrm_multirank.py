@@ -19,14 +19,14 @@ explicit event record / wait nodes into one executable graph
 step instead of ~20 Python stage issues and ~8 c10d calls:
 
   M  (MLP):      [wait d'] bottom fwd  [wait c5'] top fwd/bwd + interaction bwd
-                 (m2)  bottom bwd, next batch's load from staging (m4)  top
-                 weight grads (m3)
+                 (m2)  bottom bwd, next batch's load from staging + bucketize
+                 of its sharded tables' ids (m4)  top weight grads (m3)
   D  (dense      [wait c5'] ids-only sort of this batch (e0)  [wait m2]
-      comm):     replicated tables' dense grad + all-reduce (dp)  [wait m4]
-                 bottom-bucket all-reduce  [wait m3] top-bucket all-reduce,
-                 dense optimizer (d)
+      comm):     replicated tables' dense grad + all-reduce + update (dp)
+                 [wait m4] bottom-bucket all-reduce, next batch's replicated
+                 ids (dpp)  [wait m3] top-bucket all-reduce, dense optimizer (d)
   EC (embedding  [wait m2] gradient all-to-all  [wait e0, dp] fused embedding
-      + its      update  [wait m4] bucketize + id all-to-all, lookup + pooled
+      + its      update  [wait m4, dpp] id all-to-all, lookup + pooled
       RCCL):     all-to-all (c5)
 
 (primed events: the previous step's records). The embedding exchanges and
@@ -89,8 +89,6 @@ class MultiRankStreamsMixin:
             emb.stage_bwd_update(hyper, dp=not dp_dense)
 
         def ec_b1():
-            if not emb.fwd_prep_noop:
-                emb.stage_fwd_prep(self.ids)
             emb.stage_fwd_ids_exchange()
 
         def ec_b2():
@@ -105,6 +103,12 @@ class MultiRankStreamsMixin:
         def m4():
             self._s_bottom_bwd()
             self._m_load_next()                 # x0 / labels / ids free: next batch in
+            # ... and its sharded tables' ids bucketed for the id exchange
+            # (their send buffers' last reader was the previous exchange)
+            emb.stage_fwd_prep(self.ids, dp=False)
+
+        def d_prep():                           # the replicated tables' ids, once their
+            emb.stage_fwd_prep(self.ids, sharded=False)   # dense grad (Dp) has read them
 
         def ec_b():
             ec_b1()
@@ -112,7 +116,8 @@ class MultiRankStreamsMixin:
 
         return {"M1": self._s_bottom_fwd, "M2": m2, "M4": m4,
                 "M3": self._s_top_wgrad if self._defer_top_wgrad else None,
-                "D0": emb.stage_bwd_prepare, "Dp": dp_a, "Da": self._m_allreduce_start,
+                "D0": emb.stage_bwd_prepare, "Dp": dp_a,
+                "Da": lambda: (self._m_allreduce_start(), d_prep()),
                 "Db": d_b, "EC1": lambda: emb.backward_start(dp=False), "ECu": ec_upd,
                 "ECb": ec_b}
 
@@ -122,8 +127,10 @@ class MultiRankStreamsMixin:
         self._stg = (self.x0.clone(), self.ids.clone(), self.label.clone())
         self._mr_drain()
         torch.cuda.synchronize()
+        # (default priority: a high-priority M and/or EC stream ran the
+        # emulated W=8 step at 1.93-2.26 vs 0.63-0.64 ms)
         streams = {k: torch.cuda.Stream(device=dev) for k in ("M", "D", "EC")}
-        ev = {k: ops.SyncEvent(2) for k in ("d", "c5", "m2", "m3", "m4", "e0", "dp")}
+        ev = {k: ops.SyncEvent(2) for k in ("d", "c5", "m2", "m3", "m4", "e0", "dp", "dpp")}
         seg = self._mr_segments()
         home = lambda name: "EC" if name.startswith("EC") else name[0]  # noqa: E731
         pool = torch.cuda.graph_pool_handle()
@@ -178,11 +185,12 @@ class MultiRankStreamsMixin:
             # all-reduce, the two dense buckets and the dense optimizer
             "D": chain([("wait", "c5"), ("graph", "D0"), ("record", "e0"), ("wait", "m2"),
                         ("graph", "Dp"), ("record", "dp"), ("wait", "m4"), ("graph", "Da"),
-                        ("wait", "m3"), ("graph", "Db"), ("record", "d")]),
+                        ("record", "dpp"), ("wait", "m3"), ("graph", "Db"), ("record", "d")]),
             # EC: gradient all-to-all, fused embedding update, then the next
             # batch's bucketize, id all-to-all, lookup and pooled all-to-all
             "EC": chain([("wait", "m2"), ("graph", "EC1"), ("wait", "e0"), ("wait", "dp"),
-                         ("graph", "ECu"), ("wait", "m4"), ("graph", "ECb"), ("record", "c5")]),
+                         ("graph", "ECu"), ("wait", "m4"), ("wait", "dpp"), ("graph", "ECb"),
+                         ("record", "c5")]),
         }
         self._mr = {"streams": streams, "events": ev, "graphs": graphs, "composed": composed,
                     "launched": False}

@@ -493,13 +493,19 @@ class ShardedEmbeddingBags:
         for a, b in self._cw_views(buf):
             a.copy_(b)
 
-    def stage_fwd_prep(self, ids: torch.Tensor):
+    def stage_fwd_prep(self, ids: torch.Tensor, sharded: bool = True, dp: bool = True):
+        """Bucket a batch's ids for the exchanges (``sharded``: table/column/
+        row-wise send buffers) and the replicated tables' local lookup
+        (``dp``); the multi-rank stream graphs run the two halves where their
+        buffers' previous readers are ordered (models/dlrm_multirank.py)."""
+        if self.dp_tables and dp:
+            torch.index_select(ids, 0, self.dp_in_idx, out=self.dp_ids)
+        if not sharded:
+            return
         if self.cw_tables:
             torch.index_select(ids, 0, self.cw_perm, out=self.cw_send_ids)
             if self.world == 1:
                 self.cw_recv_ids = self.cw_send_ids
-        if self.dp_tables:
-            torch.index_select(ids, 0, self.dp_in_idx, out=self.dp_ids)
         if self.tw_identity:
             self.tw_send_ids = ids
             self.tw_recv_ids = ids
