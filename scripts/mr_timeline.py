@@ -1,0 +1,50 @@
+#!/usr/bin/env python
+"""Per-segment device timeline of the multi-rank stream graphs (emulated
+rank 0 of W, modelled links): stamps around every captured segment, printed
+per step in us from the step's M1 start."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    from tdfo_amd.models.dlrm import CRITEO_1TB_ROWS, DLRMConfig, DLRMTrainer
+    from tdfo_amd.parallel.comm import LoopbackComm
+    from tdfo_amd.train.loop import StepLoop, make_source
+    from tdfo_amd.ops import _ext
+    assert _ext.load()
+    dev = torch.device("cuda", 0)
+    W = int(os.environ.get("W", 8))
+    gbps = float(os.environ.get("GBPS", 300))
+    cfg = DLRMConfig(table_rows=list(CRITEO_1TB_ROWS), pipeline=True)
+    cfg.ids_stream = False
+    tr = DLRMTrainer(cfg, 8192, dev, group=LoopbackComm(W, 0, dev, gbps, 10.0), rank=0,
+                     world_size=W)
+    steps = 12
+    nseg = 16
+    buf = torch.zeros((steps + 4) * nseg * 2, dtype=torch.int64, device=dev)
+    cnt = torch.zeros(nseg, dtype=torch.int64, device=dev)
+    tr._mr_stamp = (buf, cnt)
+    src = make_source(cfg.table_rows, 8192, dev, cfg.pooling_factors(), 1, 0, kind="fresh")
+    loop = StepLoop(tr, src)
+    loop.run(4)
+    tr.capture_graph(warmup=0)
+    torch.cuda.synchronize()
+    loop.run(steps)
+    torch.cuda.synchronize()
+    names = tr._mr["names"]
+    n = len(names)
+    b = buf[: steps * n * 2].view(steps, n, 2).cpu()
+    for s in range(2, steps):
+        t0 = int(b[s, names.index("M1"), 0])
+        row = [f"{nm}:{(int(b[s, i, 0]) - t0) / 100:.0f}-{(int(b[s, i, 1]) - t0) / 100:.0f}"
+               for i, nm in enumerate(names)]
+        nxt = (int(b[s + 1, names.index("M1"), 0]) - t0) / 100 if s + 1 < steps else float("nan")
+        print(f"step {s} (period {nxt:.0f} us): " + "  ".join(row), flush=True)
+
+
+if __name__ == "__main__":
+    main()

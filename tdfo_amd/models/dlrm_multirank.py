@@ -92,7 +92,9 @@ class MultiRankStreamsMixin:
             emb.stage_fwd_ids_exchange()
 
         def ec_b2():
-            emb.stage_fwd_lookup()
+            # (replicated tables with a dense update: looked up on D, right
+            # after their update and their ids, see d_prep)
+            emb.stage_fwd_lookup(dp=not dp_dense)
             emb.stage_fwd_out_exchange()
 
         def d_b():
@@ -109,6 +111,8 @@ class MultiRankStreamsMixin:
 
         def d_prep():                           # the replicated tables' ids, once their
             emb.stage_fwd_prep(self.ids, sharded=False)   # dense grad (Dp) has read them
+            if dp_dense:                        # ... and their lookup (updated in Dp)
+                emb.stage_fwd_lookup(sharded=False)
 
         def ec_b():
             ec_b1()
@@ -118,8 +122,8 @@ class MultiRankStreamsMixin:
                 "M3": self._s_top_wgrad if self._defer_top_wgrad else None,
                 "D0": emb.stage_bwd_prepare, "Dp": dp_a,
                 "Da": lambda: (self._m_allreduce_start(), d_prep()),
-                "Db": d_b, "EC1": lambda: emb.backward_start(dp=False), "ECu": ec_upd,
-                "ECb": ec_b}
+                "Db": d_b, "EC1": lambda: emb.backward_start(dp=False),
+                "ECub": lambda: (ec_upd(), ec_b())}
 
     def _mr_capture(self):
         assert self.device.type == "cuda"
@@ -132,12 +136,17 @@ class MultiRankStreamsMixin:
         streams = {k: torch.cuda.Stream(device=dev) for k in ("M", "D", "EC")}
         ev = {k: ops.SyncEvent(2) for k in ("d", "c5", "m2", "m3", "m4", "e0", "dp", "dpp")}
         seg = self._mr_segments()
+        dp_dense = bool(self.emb.dp_tables) and self.emb.dp_dense
         home = lambda name: "EC" if name.startswith("EC") else name[0]  # noqa: E731
         pool = torch.cuda.graph_pool_handle()
         graphs = {}
         self._whole_capture = True       # staging load, no _ps fork, no event records
         was_mstream = self._mstream
         self._mstream = True             # the ids-only sort is its own segment (D0)
+        # diagnostics (scripts/mr_timeline.py): device timestamps around
+        # every segment of every replay
+        stamp = getattr(self, "_mr_stamp", None)
+        names = [n for n, f in seg.items() if f is not None]
         try:
             for name, fn in seg.items():
                 if fn is None:
@@ -151,7 +160,11 @@ class MultiRankStreamsMixin:
                     for r in routes:
                         r.__enter__()
                     try:
+                        if stamp is not None:
+                            ops.stamp(stamp[0], stamp[1], names.index(name), len(names), 0)
                         fn()
+                        if stamp is not None:
+                            ops.stamp(stamp[0], stamp[1], names.index(name), len(names), 1)
                     finally:
                         for r in routes:
                             r.__exit__(None, None, None)
@@ -188,12 +201,19 @@ class MultiRankStreamsMixin:
                         ("record", "dpp"), ("wait", "m3"), ("graph", "Db"), ("record", "d")]),
             # EC: gradient all-to-all, fused embedding update, then the next
             # batch's bucketize, id all-to-all, lookup and pooled all-to-all
-            "EC": chain([("wait", "m2"), ("graph", "EC1"), ("wait", "e0"), ("wait", "dp"),
-                         ("graph", "ECu"), ("wait", "m4"), ("wait", "dpp"), ("graph", "ECb"),
-                         ("record", "c5")]),
+            # (the m4 wait sits before the update, not between it and the
+            # exchange: it is long satisfied there, and a segment boundary
+            # costs ~14 us of queue idle, scripts/mr_timeline.py; with a
+            # dense replicated-table update D also looks those tables up, so
+            # EC waits for none of D's replicated-table work)
+            "EC": (chain([("wait", "m2"), ("graph", "EC1"), ("wait", "e0"), ("wait", "m4"),
+                          ("graph", "ECub"), ("record", "c5")]) if dp_dense else
+                   chain([("wait", "m2"), ("graph", "EC1"), ("wait", "e0"), ("wait", "dp"),
+                          ("wait", "m4"), ("wait", "dpp"), ("graph", "ECub"),
+                          ("record", "c5")])),
         }
         self._mr = {"streams": streams, "events": ev, "graphs": graphs, "composed": composed,
-                    "launched": False}
+                    "launched": False, "names": names}
         # the capture ran nothing: the batch handed in before it is the one
         # the first replay loads
         if self._next is not None:

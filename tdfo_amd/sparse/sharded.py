@@ -544,14 +544,18 @@ class ShardedEmbeddingBags:
             w.wait()
         self._ids_works = []
 
-    def stage_fwd_lookup(self):
+    def stage_fwd_lookup(self, sharded: bool = True, dp: bool = True):
+        """Pooled lookup of the exchanged ids (``sharded``) and of the
+        replicated tables' local ids (``dp``)."""
         W, B = self.world, self.B
-        if self.dp_tables:
+        if self.dp_tables and dp:
             self.dp_store.forward(self.dp_ids, self.dp_offsets, self.dp_store.row_offset,
                                   len(self.dp_tables), B, self.recv, self.dp_out_off,
                                   self.dp_width, mean=self.mean, onehot=self.dp_onehot)
             if W > 1 and not self.dp_dense:
                 torch.index_select(self.dp_g_ids, 0, self.dp_g_perm, out=self.dp_g_ids_t)
+        if not sharded:
+            return
         if self.tw_nv:
             self.tw_store.forward(self.tw_recv_ids, self.tw_v_offsets, self.tw_v_row_off, self.tw_nv,
                                   B, self.tw_pooled if W > 1 else self.recv, self.tw_v_out_off,
