@@ -554,6 +554,13 @@ void sync_event_wait(int64_t e) {
   TDFO_HIP_OK(hipStreamWaitEvent(cur_stream(), reinterpret_cast<hipEvent_t>(e), 0));
 }
 
+bool sync_event_query(int64_t e) {
+  const hipError_t r = hipEventQuery(reinterpret_cast<hipEvent_t>(e));
+  if (r == hipErrorNotReady) return false;
+  TDFO_HIP_OK(r);
+  return true;
+}
+
 void sync_event_destroy(int64_t e) {
   TDFO_HIP_OK(hipEventDestroy(reinterpret_cast<hipEvent_t>(e)));
 }
@@ -1209,6 +1216,7 @@ TORCH_LIBRARY(tdfo, m) {
   m.def("sync_event_record(int e) -> ()", sync_event_record);
   m.def("sync_event_wait(int e) -> ()", sync_event_wait);
   m.def("sync_event_destroy(int e) -> ()", sync_event_destroy);
+  m.def("sync_event_query(int e) -> bool", sync_event_query);
   m.def("graph_compose(int[] kinds, int[] handles) -> int", graph_compose);
   m.def("graph_exec_launch(int ex) -> ()", graph_exec_launch);
   m.def("graph_exec_destroy(int ex) -> ()", graph_exec_destroy);

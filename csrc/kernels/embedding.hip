@@ -708,12 +708,21 @@ __global__ __launch_bounds__(256) void emb_combine_kernel(
     float acc[EPL];
 #pragma unroll
     for (int u = 0; u < EPL; ++u) acc[u] = act ? tail[c * D + e0 + u] : 0.f;
-    int64_t lo = endc, hi = a.nnz;
-    while (lo < hi) {
-      const int64_t mid = (lo + hi) >> 1;
-      if (keys[mid] == last) lo = mid + 1; else hi = mid;
+    // Last chunk of the run: the chunks it covers are exactly the ones after
+    // c whose FIRST key is `last` (sorted keys: a prefix of c+1, c+2, ...), so
+    // each lane probes one chunk's first key and a ballot counts the prefix --
+    // one dependent load per 64 chunks instead of a ~18-step binary search
+    // over every key after the chunk (that chain was most of this kernel's
+    // 16 us in the DLRM-1TB step).
+    const int64_t nch = (a.nnz + CH - 1) / CH;
+    int64_t jlast = c;
+    for (int64_t jb = c + 1; jb < nch; jb += 64) {
+      const int64_t j = jb + lane;
+      const K kj = keys[min(j, nch - 1) * CH];
+      const int cnt = __popcll(__ballot(j < nch && kj == last));
+      jlast += cnt;
+      if (cnt < 64) break;
     }
-    const int64_t jlast = (lo - 1) / CH;
     // HQ head partials in flight: a skewed table's runs span up to B/CH
     // chunks (a 3-row table: ~85 per run at B = 8192), and this walk is the
     // kernel's latency tail (8 in flight: 15 us per DLRM-1TB step)

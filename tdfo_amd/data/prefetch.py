@@ -41,6 +41,8 @@ class HostPrefetcher:
         self.H = gen.nbuf
         self.S = int(stages)
         self.copy = torch.cuda.Stream(self.dev) if self.cuda else None
+        from .. import ops
+        self.ops = ops
         d0, i0, l0 = gen._bufs[0]
         self.stage = [(torch.empty(d0.shape, dtype=d0.dtype, device=self.dev),
                        torch.empty(i0.shape, dtype=i0.dtype, device=self.dev),
@@ -90,7 +92,9 @@ class HostPrefetcher:
             with torch.cuda.stream(self.copy):
                 for d, h in zip(dst, host):
                     d.copy_(h, non_blocking=True)
-                ev = torch.cuda.Event()
+                # (events without the system-scope fence: see
+                # DeviceSyntheticStream; the host only polls their completion)
+                ev = self.ops.SyncEvent(2)
                 ev.record(self.copy)
             self.h2d_ev[j % self.H] = ev
             for st in (streams or [torch.cuda.current_stream(self.dev)]):
@@ -109,7 +113,7 @@ class HostPrefetcher:
         if self.cuda:
             evs = []
             for st in (streams or [torch.cuda.current_stream(self.dev)]):
-                e = torch.cuda.Event()
+                e = self.ops.SyncEvent(2)
                 e.record(st)
                 evs.append(e)
             self.use_ev[slot] = evs

@@ -55,6 +55,10 @@ class SyncEvent:
         else:
             _native().sync_event_wait(self._h)
 
+    def query(self) -> bool:
+        """True once the work before the latest record has completed."""
+        return bool(_native().sync_event_query(self._h))
+
     @property
     def handle(self) -> int:
         return self._h
