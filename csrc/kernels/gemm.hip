@@ -581,6 +581,142 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmArgs p) {
 }
 
 // ---------------------------------------------------------------------------
+// Large-tile kernel: 256x128x64, 8 waves (4 along M x 2 along N, each 64x64),
+// 3-deep glds ring (3 x 48 KiB = 144 KiB LDS, 1 block per CU, 2 waves per
+// SIMD). Two K tiles stay in flight across each barrier: the wait before the
+// barrier is a counted vmcnt (6 pieces per thread per tile), the barrier is a
+// raw s_barrier (no vmcnt(0) drain, cdna_hip_programming.md "Pipelining
+// across barriers"), and the ring slot being refilled is the one every wave
+// finished reading before that barrier. Twice the FLOP per staged byte of the
+// 128x128 tile: DCN-v2's 3456-wide GEMMs (>= 1024 128x128 tiles) and its
+// weight grads run on it (profiles/r03/dcn_policy_ab.log).
+constexpr int LBM = 256;
+constexpr int LSTAGE = 3 * TILE_BYTES;             // A (2 images) + B
+constexpr int LSMEM = 3 * LSTAGE;                  // 144 KiB >= 256x128 fp32 epilogue tile
+
+template <bool A_COL, bool B_COL>
+__device__ __forceinline__ void gemm_big_body(const GemmArgs& p, int bid, char* smem_raw) {
+  constexpr int MI = 4, NW = 8;
+  constexpr int APW = 32 / NW, BPW = 16 / NW;       // A / B pieces per wave per K tile
+  TDFO_LDS char* smem = (TDFO_LDS char*)smem_raw;
+
+  const int tiles_m = (p.M + LBM - 1) / LBM, tiles_n = (p.N + BN - 1) / BN;
+  const TileIdx ti = tile_of(tiles_m, tiles_n, p.splits, bid);
+  const int m0 = ti.tm * LBM, n0 = ti.tn * BN;
+
+  const int ktiles = p.K / BK;
+  const int per = (ktiles + p.splits - 1) / p.splits;
+  const int kt0 = ti.split * per;
+  const int nk = min(ktiles, kt0 + per) - kt0;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wr = w >> 1, wc = w & 1;
+
+  f32x4_t acc[MI][4];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  // 48 pieces per K tile (A: 2 images x 16, B: 16) spread over the waves.
+  auto stage = [&](int buf, int kt) {
+    TDFO_LDS char* ta = smem + buf * LSTAGE;
+    TDFO_LDS char* tb = ta + 2 * TILE_BYTES;
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int i = 0; i < APW; ++i) {
+      const int ii = w * APW + i, half = ii >> 4;
+      glds_piece_asm<A_COL>(p.A, p.lda, m0 + half * 128, p.M, k0, ta + half * TILE_BYTES,
+                            ii & 15, lane);
+    }
+#pragma unroll
+    for (int i = 0; i < BPW; ++i)
+      glds_piece_asm<B_COL>(p.B, p.ldb, n0, p.N, k0, tb, w * BPW + i, lane);
+  };
+  // all but the youngest K tile's pieces landed
+  auto wait_one_ahead = [&]() { asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory"); };
+
+  // Fragment-pipelined main loop: one raw barrier per K tile, in the middle
+  // of it. Iteration t: issue tile t+2's DMA, read tile t's k=32..63
+  // fragments, MFMAs on its k=0..31 fragments (read last iteration) hide that
+  // read, then wait for tile t+1 + barrier, read tile t+1's k=0..31
+  // fragments, and the k=32..63 MFMAs hide those. Ring-slot reuse: slot
+  // (t+2)%3 was last read before iteration t-1's barrier (each wave drains
+  // its LDS reads with lgkmcnt(0) before that barrier).
+  if (nk > 0) {
+    const TDFO_LDS char* tAo = smem + (wr >> 1) * TILE_BYTES;
+    const TDFO_LDS char* tBo = smem + 2 * TILE_BYTES;
+    const int a_r0 = (wr & 1) * 64, b_c0 = wc * 64;
+    auto frags = [&](int buf, int ks, bf16x8_t (&af)[MI], bf16x8_t (&bfr)[4]) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        bfr[j] = B_COL ? frag_col(tBo + buf * LSTAGE, b_c0 + j * 16, ks, lane)
+                       : frag_row(tBo + buf * LSTAGE, b_c0 + j * 16, ks, lane);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+        af[i] = A_COL ? frag_col(tAo + buf * LSTAGE, a_r0 + i * 16, ks, lane)
+                      : frag_row(tAo + buf * LSTAGE, a_r0 + i * 16, ks, lane);
+    };
+    auto mm = [&](const bf16x8_t (&af)[MI], const bf16x8_t (&bfr)[4]) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    };
+    stage(0, kt0);
+    if (nk > 1) stage(1, kt0 + 1);
+    if (nk > 1) wait_one_ahead();
+    else        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    bf16x8_t a0[MI], b0[4], a1[MI], b1[4];
+    frags(0, 0, a0, b0);
+    int cur = 0;
+    // steady state (straight-line body so the compiler's lgkmcnt waits only
+    // cover the reads each MFMA group actually consumes); last tile peeled
+    for (int t = 0; t + 1 < nk; ++t) {
+      __builtin_amdgcn_sched_barrier(0);
+      const bool pre = t + 2 < nk;
+      if (pre) stage(cur == 0 ? 2 : cur - 1, kt0 + t + 2);
+      frags(cur, 1, a1, b1);
+      __builtin_amdgcn_sched_barrier(0);
+      mm(a0, b0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (pre) wait_one_ahead();
+      else     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      cur = cur == 2 ? 0 : cur + 1;
+      frags(cur, 0, a0, b0);
+      __builtin_amdgcn_sched_barrier(0);
+      mm(a1, b1);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    frags(cur, 1, a1, b1);
+    mm(a0, b0);
+    mm(a1, b1);
+  }
+  epilogue<LBM, NW * 64, MI>(p, acc, smem_raw, m0, n0, wr, wc, lane, tid, ti.split);
+}
+
+template <bool A_COL, bool B_COL>
+__global__ __launch_bounds__(512, 1) void gemm_big_kernel(GemmArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  gemm_big_body<A_COL, B_COL>(p, blockIdx.x, smem_raw);
+}
+
+// Two problems in one 256x128 grid (see gemm_pp_pair_kernel).
+template <bool AC0, bool BC0, bool AC1, bool BC1>
+__global__ __launch_bounds__(512, 1) void gemm_big_pair_kernel(GemmArgs p0, GemmArgs p1, int nb0) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  if ((int)blockIdx.x < nb0) gemm_big_body<AC0, BC0>(p0, blockIdx.x, smem_raw);
+  else                       gemm_big_body<AC1, BC1>(p1, blockIdx.x - nb0, smem_raw);
+}
+
+// ---------------------------------------------------------------------------
 // Deep-pipelined 128x128 kernel: 4 waves (2x2 of 64x64), DNS-deep glds ring
 // (DNS x 32 KiB, one block per CU) with DNS-2 K tiles of DMA in flight across
 // each raw barrier (counted vmcnt, never 0 in the steady state). For GEMMs
@@ -1061,22 +1197,39 @@ void pp_pair_launch(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s) {
 //     U dgrad, K = 3456: 37 vs 45 us and 41 vs 49 us on the ping-pong kernel);
 //   * 2-stage 64x128 tiles: forwards whose 128x128 grid leaves CUs idle
 //     (N <= 256: bot1 / top3 fwd 8.3 vs 9.6 us).
-// Policies 1 / 2 / 3 force the 2-stage, deep or ping-pong kernel (tests, A/B).
+//   * 256x128 tiles (8 waves, one block per CU) for GEMMs of >= 1024 128x128
+//     tiles (DCN-v2's 3456-wide U fwd, V dgrad and top-0 dgrad), and, under
+//     policy 5 (DCN-v2's default, DLRMConfig.gemm_big), for every GEMM
+//     without bias column sums except the deep kernel's.
+// Policies 1 / 2 / 3 / 4 force the 2-stage, deep, ping-pong or 256x128
+// kernel (256x128: not for column-sum weight grads) (tests, A/B).
 int g_policy = 0;
 
-enum Kern { K_SMALL64 = 64, K_SMALL128 = 128, K_DEEP = 2, K_PP = 3 };
+enum Kern { K_SMALL64 = 64, K_SMALL128 = 128, K_DEEP = 2, K_PP = 3, K_BIG = 4 };
 
 template <bool AC, bool BC>
 int choose(const GemmArgs& a) {
   const int t128 = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN) * a.splits;
   const int ktps = (a.K / BK + a.splits - 1) / a.splits;
+  const bool big_ok = !a.csum_on && a.K % BK == 0;
   switch (g_policy) {
     case 1: return (!AC && t128 < 256) ? K_SMALL64 : K_SMALL128;
     case 2: return K_DEEP;
     case 3: return K_PP;
+    case 4: return big_ok ? K_BIG : K_PP;
     default: break;
   }
-  if (!AC && ktps >= 32 && t128 <= 512) return K_DEEP;
+  if (g_policy == 5) {
+    // DCN-v2: the deep kernel where a 256x128 grid would leave CUs idle while
+    // a 128x128 one fills them about once, with long K (cross-layer V fwd /
+    // U dgrad); 256x128 tiles for everything else without column sums
+    const int t256 = ((a.M + LBM - 1) / LBM) * ((a.N + BN - 1) / BN) * a.splits;
+    if (!AC && t256 < 256 && t128 <= 512 && ktps >= 16) return K_DEEP;
+    if (big_ok) return K_BIG;
+  } else {
+    if (!AC && ktps >= 32 && t128 <= 512) return K_DEEP;
+    if (big_ok && t128 >= 1024) return K_BIG;
+  }
   if (AC || BC || t128 >= 256) return K_PP;
   return K_SMALL64;
 }
@@ -1089,6 +1242,8 @@ void launch(const GemmArgs& a, int k, hipStream_t s) {
                                        hipFuncAttributeMaxDynamicSharedMemorySize, SMEM_BYTES));
     TDFO_CHECK_HIP(hipFuncSetAttribute((const void*)gemm_deep_kernel<AC, BC>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, DSMEM));
+    TDFO_CHECK_HIP(hipFuncSetAttribute((const void*)gemm_big_kernel<AC, BC>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, LSMEM));
     attr = true;
   }
   const int tn = (a.N + BN - 1) / BN;
@@ -1096,6 +1251,10 @@ void launch(const GemmArgs& a, int k, hipStream_t s) {
     case K_PP:
       pp_launch<AC, BC>(a, s);
       return;
+    case K_BIG:
+      hipLaunchKernelGGL((gemm_big_kernel<AC, BC>), dim3(((a.M + LBM - 1) / LBM) * tn * a.splits),
+                         dim3(512), LSMEM, s, a);
+      break;
     case K_DEEP:
       hipLaunchKernelGGL((gemm_deep_kernel<AC, BC>), dim3(((a.M + BM - 1) / BM) * tn * a.splits),
                          dim3(256), DSMEM, s, a);
@@ -1136,9 +1295,38 @@ int layout_of(const GemmArgs& a) { return (a.a_col ? 2 : 0) | (a.b_col ? 1 : 0);
 // the ping-pong kernel: one grid (each small launch pays fill / drain, and
 // the two problems' blocks fill each other's idle CUs). Bit-identical to
 // two launches.
+int big_grid(const GemmArgs& a) {
+  return ((a.M + LBM - 1) / LBM) * ((a.N + BN - 1) / BN) * a.splits;
+}
+
+template <bool AC0, bool BC0, bool AC1, bool BC1>
+void big_pair_launch(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s) {
+  auto fn = gemm_big_pair_kernel<AC0, BC0, AC1, BC1>;
+  static bool attr = false;
+  if (!attr) {
+    TDFO_CHECK_HIP(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       LSMEM));
+    attr = true;
+  }
+  const int g0 = big_grid(a0);
+  hipLaunchKernelGGL(fn, dim3(g0 + big_grid(a1)), dim3(512), LSMEM, s, a0, a1, g0);
+  TDFO_CHECK_HIP(hipGetLastError());
+}
+
 bool try_pair(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s) {
-  if (kernel_of(a0) != K_PP || kernel_of(a1) != K_PP) return false;
+  const int k0 = kernel_of(a0), k1 = kernel_of(a1);
   const int l0 = layout_of(a0), l1 = layout_of(a1);
+  // 256x128 pairs: a weight grad on that kernel takes its layer's dgrad
+  // along onto it (also a deep-kernel one: one grid instead of two)
+  const bool b0 = k0 == K_BIG || (k1 == K_BIG && k0 == K_DEEP && !a0.csum_on);
+  const bool b1 = k1 == K_BIG || (k0 == K_BIG && k1 == K_DEEP && !a1.csum_on);
+  if (b0 && b1) {
+    if (l0 == 3 && l1 == 1) { big_pair_launch<true, true, false, true>(a0, a1, s); return true; }
+    if (l1 == 3 && l0 == 1) { big_pair_launch<true, true, false, true>(a1, a0, s); return true; }
+    if (l0 == 3 && l1 == 3) { big_pair_launch<true, true, true, true>(a0, a1, s); return true; }
+    return false;
+  }
+  if (k0 != K_PP || k1 != K_PP) return false;
   if (l0 == 3 && l1 == 1) { pp_pair_launch<true, true, false, true>(a0, a1, s); return true; }
   if (l1 == 3 && l0 == 1) { pp_pair_launch<true, true, false, true>(a1, a0, s); return true; }
   if (l0 == 3 && l1 == 3) { pp_pair_launch<true, true, true, true>(a0, a1, s); return true; }

@@ -24,6 +24,7 @@ once into a hipGraph and replayed (no tracing compiler):
 from __future__ import annotations
 
 import math
+import os
 import warnings
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
@@ -369,6 +370,19 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin):
         # per layer); with >1 rank they are reduced first because the
         # all-reduce needs the grads.
         self._pair_bwd = dev.type == "cuda"
+        dcn = cfg.interaction == "dcn"
+        if dev.type == "cuda" and not os.environ.get("TDFO_GEMM_POLICY"):
+            # GEMM tile policy per workload: DCN-v2's 3456-wide cross / top
+            # GEMMs on 256x128 tiles, paired wgrad + dgrad on that kernel
+            # (2.42 vs 2.51-2.52 ms/step on the 128x128 ping-pong dispatch,
+            # same box, profiles/r03/s3/dcn_policy.md); DLRM's <= 1024-wide
+            # MLPs on the ping-pong / 64-row kernels
+            ops.gemm_policy(5 if dcn else 0)
+        # DCN-v2 on 256x128 tiles: bias grads from the ones column inside the
+        # wgrad's N (that kernel has no column-sum epilogue), splits sized for
+        # its resident blocks (half of them beside the paired dgrad)
+        self._csum = not (dcn and dev.type == "cuda" and ops.gemm_policy(-1) in (4, 5))
+        self._wg_slots = (128 if self._pair_bwd else 256) if not self._csum else 0
         self.wslab = {}
         self._segments = []
         self._opt_sums_slabs = dev.type == "cuda" and world_size == 1
@@ -377,7 +391,7 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin):
             max_slab = self._wg_splits(cfg.dcn_rank, self.top_real) * cfg.dcn_rank * self.top_real
         self.slab = z(max_slab, dt=torch.float32)
         for L in self.bottom_layers + self.top_layers + self.dcn_u:
-            S = self._wg_splits(L.out, L.in_k)
+            S = self._wg_splits(L.out, self._wgrad_n(L))
             if S > 1:
                 sl = z(S * L.out * L.wcols, dt=torch.float32)
                 self.wslab[L.name] = (sl, S)
@@ -530,7 +544,10 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin):
             fin()
 
     def _wg_splits(self, M: int, N: int) -> int:
-        return ops.wgrad_splits(M, N, self.B, 256)
+        return ops.wgrad_splits(M, N, self.B, 256, slots=self._wg_slots)
+
+    def _wgrad_n(self, L: Lin) -> int:
+        return L.in_k if self._csum else L.wcols
 
     def _wgrad(self, L: Lin, x, dy):
         """dW[:, :in_k] = dy^T x[:, :in_k]; db (column bcol) = colsum(dy) from
@@ -543,17 +560,18 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin):
         """The weight-grad GEMM alone; returns the split-K slab reduce still
         to run (more than one rank: the all-reduce needs the grads) or None
         (one GPU: the optimizer sums the slabs)."""
-        csum = -1 if L.bias_in_k else L.bcol
+        csum = -1 if (L.bias_in_k or not self._csum) else L.bcol
+        n = self._wgrad_n(L)
         g = self.fp.grad(L.name + ".w").view(-1)
         if L.name in self.wslab:
             sl, S = self.wslab[L.name]
-            ops.gemm(dy, True, x[:, :L.in_k], True, None, False, None, None, sl, S,
+            ops.gemm(dy, True, x[:, :n], True, None, False, None, None, sl, S,
                      ldc32=L.wcols, csum_col=csum)
             if not self._opt_sums_slabs:      # else: partials summed by the optimizer
                 m = L.out * L.wcols
                 return lambda: ops.reduce_rows(sl, S, m, m, g, False, 1.0)
         else:
-            ops.gemm(dy, True, x[:, :L.in_k], True, None, False, None, None, g, 1,
+            ops.gemm(dy, True, x[:, :n], True, None, False, None, None, g, 1,
                      ldc32=L.wcols, csum_col=csum)
         return None
 

@@ -137,7 +137,9 @@ def gemm_pairing(v: int = -1) -> int:
 
 
 def gemm_policy(p: int = -1) -> int:
-    """GEMM tile-shape policy of the native library: 0 auto, 1 128x128 tiles
+    """GEMM tile-shape policy of the native library (0 auto, 1-4 one kernel
+    forced: 2-stage, deep, ping-pong, 256x128; 5 DCN-v2: 256x128 tiles for
+    every GEMM without column sums except the long-K deep ones) -- was: 0 auto, 1 128x128 tiles
     only, 2 256x128 tiles only; p < 0 only reads it. Returns the previous one."""
     return int(_native().gemm_policy(p))
 
@@ -214,13 +216,29 @@ _WGRAD_TARGET = 512
 _WGRAD_MINKT = 8
 
 
-def wgrad_splits(M: int, N: int, K: int, target_blocks: int = 0) -> int:
+def wgrad_splits(M: int, N: int, K: int, target_blocks: int = 0, slots: int = 0) -> int:
     """Split-K count for a weight-grad GEMM (K = batch): ~target_blocks blocks
     of 128x128 tiles, but every split keeps >= 8 K tiles (measured on
     MI355X: bot/top3 wgrads run 18.8 us at 16 splits vs 22.7 us at 64; top1
-    is best at 8)."""
+    is best at 8).
+
+    slots > 0: the GEMM runs on the 256x128 one-block-per-CU kernel (DCN-v2,
+    GEMM policy 5) with `slots` resident blocks. A 128x128-tile target then
+    leaves CUs idle (U wgrad: 70 tiles x 2 splits = 140 blocks), so the split
+    minimises (block rounds x K tiles per split) + the fp32 slab traffic each
+    extra split adds (written here, read by the optimizer / reduce; priced in
+    K-tile times of ~0.6 us at ~5 TB/s)."""
     kt = K // 64
     smax = max(1, kt // _WGRAD_MINKT)
+    if slots > 0:
+        tiles = ((M + 255) // 256) * ((N + 127) // 128)
+        pen = M * N * 8 / 5e12 / 0.6e-6
+        best, best_s = None, 1
+        for s in range(1, smax + 1):
+            cost = -(-tiles * s // slots) * -(-kt // s) + pen * (s - 1)
+            if best is None or cost < best:
+                best, best_s = cost, s
+        return best_s
     target_blocks = target_blocks or _WGRAD_TARGET
     tiles = ((M + 127) // 128) * ((N + 127) // 128)
     return max(1, min(smax, -(-target_blocks // tiles)))
