@@ -1204,6 +1204,19 @@ TORCH_LIBRARY(tdfo, m) {
     tdfo::stamp(reinterpret_cast<uint64_t*>(buf.data_ptr()), cnt.data_ptr<int64_t>(), (int)seg,
                 (int)nseg, (int)which, buf.numel(), cur_stream());
   });
+  m.def("bump(Tensor[] counters) -> ()", [](const std::vector<Tensor>& ts) {
+    TORCH_CHECK(ts.size() <= 8, "bump: at most 8 counters");
+    tdfo::BumpArgs a{};
+    for (const auto& t : ts) {
+      TORCH_CHECK(t.is_cuda() && t.numel() >= 1 &&
+                  (t.scalar_type() == at::kFloat || t.scalar_type() == at::kLong),
+                  "bump: float32 / int64 GPU counters");
+      a.p[a.n] = t.data_ptr();
+      a.is_i64[a.n] = t.scalar_type() == at::kLong;
+      ++a.n;
+    }
+    tdfo::bump(a, cur_stream());
+  });
   m.def("spin_us(float us) -> ()", [](double us) {
     static const double ticks_per_us = [] {
       int dev = 0, khz = 0;

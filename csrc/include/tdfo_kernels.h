@@ -240,6 +240,12 @@ void batch_load(const float* dense, int nd, int64_t ld_dense, uint16_t* x0, int6
                 const int64_t* ids, int64_t* ids_dst, int64_t n, const float* label,
                 float* label_dst, int B, hipStream_t s);
 void spin_ticks(uint64_t ticks, hipStream_t s);
+struct BumpArgs {
+  void* p[8];
+  int is_i64[8];
+  int n;
+};
+void bump(const BumpArgs& a, hipStream_t s);
 void stamp(uint64_t* buf, int64_t* cnt, int seg, int nseg, int which, int64_t cap,
            hipStream_t s);
 

@@ -234,6 +234,21 @@ void stamp(uint64_t* buf, int64_t* cnt, int seg, int nseg, int which, int64_t ca
   TDFO_CHECK_HIP(hipGetLastError());
 }
 
+// Step counters (optimizer step numbers, dropout RNG step) bumped by one
+// launch instead of one library add kernel each.
+__global__ void bump_kernel(BumpArgs a) {
+  const int i = threadIdx.x;
+  if (i >= a.n) return;
+  if (a.is_i64[i]) *(int64_t*)a.p[i] += 1;
+  else             *(float*)a.p[i] += 1.f;
+}
+
+void bump(const BumpArgs& a, hipStream_t s) {
+  if (a.n <= 0) return;
+  hipLaunchKernelGGL(bump_kernel, dim3(1), dim3(64), 0, s, a);
+  TDFO_CHECK_HIP(hipGetLastError());
+}
+
 void spin_ticks(uint64_t ticks, hipStream_t s) {
   if (ticks == 0) return;
   hipLaunchKernelGGL(spin_kernel, dim3(1), dim3(64), 0, s, ticks);

@@ -305,6 +305,7 @@ class ItemEmbedding(nn.Module):
         self.N = n_tokens
         self.group, self.world = group, world
         self.hyper = torch.tensor([optim.lr, 0.0], dtype=torch.float32, device=device)
+        self.step_bumped_by_caller = False
         self.offsets = torch.arange(n_tokens * world + 1, dtype=torch.int64, device=device)
         self.zero = torch.zeros(1, dtype=torch.int64, device=device)
         self.out = torch.zeros(n_tokens, dim, dtype=torch.float32, device=device)
@@ -329,7 +330,8 @@ class ItemEmbedding(nn.Module):
     def _update(self, grad):
         ids = self._ids
         n = ids.numel()
-        self.hyper[1:2].add_(1.0)
+        if not self.step_bumped_by_caller:
+            self.hyper[1:2].add_(1.0)
         if self.world > 1:
             dist.all_gather_into_tensor(self.g_ids[: self.world * n], ids, group=self.group)
             dist.all_gather_into_tensor(self.g_grad[: self.world * n], grad, group=self.group)
@@ -487,6 +489,13 @@ class Bert4RecTrainer:
         self.metric_sums = torch.zeros(len(METRIC_NAMES) + 1, dtype=torch.float64, device=dev)
         self.graph = None
         self._static_loss = None
+        # the step's counters (dense / embedding optimizer step numbers, the
+        # dropout RNG step) bumped by one launch at the start of the step
+        # (three library add kernels before)
+        self.opt.step_bumped_by_caller = True
+        self.item.step_bumped_by_caller = True
+        eh = self.item.engine._hyper if mode == "dmp" else self.item.hyper
+        self._counters = [self.opt.hyper[1:2], eh[1:2], self.model.rng_step]
 
     # ------------------------------------------------------------ train
     def _embed(self, seqs):
@@ -508,11 +517,11 @@ class Bert4RecTrainer:
         return loss
 
     def _step_body(self, seqs, labels):
+        ops.bump(self._counters)
         self.opt.grad.zero_()
         loss = self._fwd_bwd(seqs, labels)
         self.opt.all_reduce_grads(average=True)
         self.opt.step()
-        self.model.rng_step.add_(1)
         return loss          # (already added to loss_sum by the fused loss kernel)
 
     def load_batch(self, seqs, labels):

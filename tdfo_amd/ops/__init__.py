@@ -479,6 +479,17 @@ def stamp(buf, cnt, seg: int, nseg: int, which: int):
     _native().stamp(buf, cnt, int(seg), int(nseg), int(which))
 
 
+def bump(counters):
+    """counters[i].view(-1)[0] += 1 for each float32 / int64 tensor (one launch
+    on the GPU)."""
+    counters = list(counters)
+    if counters and _gpu(counters[0]):
+        _native().bump(counters)
+    else:
+        for t in counters:
+            t.view(-1)[:1].add_(1)
+
+
 def spin_us(us: float):
     """Occupy the current stream for ``us`` microseconds (one sleeping wave):
     the modelled link time of an emulated collective."""

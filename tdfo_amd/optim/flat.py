@@ -62,6 +62,8 @@ class FlatOptimizer:
         self.v = torch.zeros_like(self.flat) if self.opt in (ops.OPT_ADAMW, ops.OPT_ADAM) else None
         self.shadow = torch.zeros(self.numel, dtype=torch.bfloat16, device=dev) if bf16_shadow else None
         self.hyper = torch.tensor([lr, 0.0, 1.0], dtype=torch.float32, device=dev)
+        self._inv_set = 1.0                  # hyper[2] as last written
+        self.step_bumped_by_caller = False   # the caller bumps hyper[1] (ops.bump)
         self.dynamic_scale = dynamic_scale
         self.found_inf = torch.zeros(1, dtype=torch.float32, device=dev) if dynamic_scale else None
         self.scale = 2.0 ** 15 if dynamic_scale else 1.0
@@ -98,11 +100,14 @@ class FlatOptimizer:
     def step(self, grad_scale: Optional[float] = None):
         self._gather_stray_grads()
         inv = 1.0 / self.scale if self.dynamic_scale else (grad_scale or 1.0)
-        self.hyper[2:3].fill_(inv)
+        if inv != self._inv_set:        # (a constant unscale factor is written once)
+            self.hyper[2:3].fill_(inv)
+            self._inv_set = None if self.dynamic_scale else inv
         if self.dynamic_scale:
             self.found_inf.zero_()
             ops.check_finite(self.grad, self.found_inf)
-        self.hyper[1:2].add_(1.0)
+        if not self.step_bumped_by_caller:  # (else: the caller's one-launch ops.bump)
+            self.hyper[1:2].add_(1.0)
         ops.dense_optimizer(self.flat, self.grad, self.m, self.v, self.shadow, self.opt,
                             self.hyper, self.beta1, self.beta2, self.eps, self.wd, self.momentum,
                             self.found_inf)

@@ -55,6 +55,7 @@ class ShardedEmbeddingModule(torch.nn.Module):
         self.plan = plan or plan_sharding(self.tables, world_size, self.optim,
                                           batch_per_rank=batch_size, pooling=self.pooling,
                                           strategy=strategy)
+        self.step_bumped_by_caller = False     # the owner bumps the step counter
         self.engine = ShardedEmbeddingBags(self.tables, self.plan, rank, batch_size, self.pooling,
                                            device, self.optim, group=group, seed=seed, mean=mean,
                                            recv_dtype=recv_dtype)
@@ -72,7 +73,8 @@ class ShardedEmbeddingModule(torch.nn.Module):
         """ids: flat int64, table-major, table t has B*L_t ids. Returns
         per-table pooled rows [B, D] (fp32 views over the receive buffer)."""
         if self.training and torch.is_grad_enabled():
-            self.engine._hyper[1:2].add_(1.0)
+            if not self.step_bumped_by_caller:
+                self.engine._hyper[1:2].add_(1.0)
             recv = _EmbFn.apply(ids, self._anchor, self.engine)
         else:
             recv = self.engine.forward(ids).clone()
