@@ -12,9 +12,9 @@
 // from dZ. S comes from an LDS copy of the dZ row; X is staged in LDS and
 // read as the MFMA B operand with ds_read_b64_tr_b16 (k = feature index).
 // All column tiles' MFMAs issue back to back before their epilogue, which
-// reads nothing from LDS (37 -> see profiles for the in-step time).
-// The concat passthrough (dZ[:, :D]) and the bottom-MLP ReLU mask are fused
-// into the dense-slot store, and embedding-slot gradients are written
+// reads nothing from LDS. The concat passthrough (dZ[:, :D]) and the
+// bottom-MLP ReLU mask are fused into the dense-slot store (by the lanes that
+// hold those dZ / X chunks), and embedding-slot gradients are written
 // directly in the layout the embedding backward / all-to-all consumes.
 //
 // Feature rows are addressed through a SlotMap so the kernels read the
@@ -128,6 +128,19 @@ __device__ __forceinline__ int xswz(int j) {
   return (D >= 128) ? ((j & 3) << 2) : 0;
 }
 
+// swizzle of the dX image: the epilogue writes one 8-B piece of each of the
+// 32 rows per instruction, all at the same column; rows 256 B apart share
+// banks, so X's 4-way swizzle left those writes 8-way bank-conflicted (PMC:
+// conflicts = 53 % of LDS-active cycles). XOR-ing the chunk with the row
+// spreads the 32 rows over every chunk position. Only where all column
+// tiles' MFMAs (hence every X tr read) precede the epilogue (<= 4 tiles):
+// with more, dX tile nt overwrites X columns a later tile still reads, which
+// is safe only when both images share one layout.
+template <int D>
+__device__ __forceinline__ int yswz(int j) {
+  return (D >= 64 && D <= 128) ? (j & (D / 8 - 1)) : xswz<D>(j);
+}
+
 template <int D>
 __global__ __launch_bounds__(256) void inter_bwd_kernel(
     const uint16_t* __restrict__ dz, int64_t ldz,
@@ -154,7 +167,7 @@ __global__ __launch_bounds__(256) void inter_bwd_kernel(
     }
   }
   __syncthreads();
-  char* base = smem_raw + SLOT_BYTES + w * (XB + ldz_al * 2);
+  char* base = smem_raw + SLOT_BYTES + w * (XB + ldz_al * 2 + D * 4);
   char* xs = base;
   // dX image [32][D] aliases the X image (same chunk swizzle): column tile nt
   // is written only after its MFMAs consumed X's same columns, and the
@@ -162,6 +175,10 @@ __global__ __launch_bounds__(256) void inter_bwd_kernel(
   // overwrites it
   uint16_t* ys = (uint16_t*)base;
   uint16_t* zrow = (uint16_t*)(base + XB);
+  // fp32 dX row 0 (the dense slot): its passthrough and ReLU mask are
+  // applied in the store loop by the CPR lanes that hold that row's dZ / X
+  // chunks in registers, instead of by every lane of every epilogue step
+  float* drow = (float*)(base + XB + ldz_al * 2);
   constexpr int CPR = D / 8;  // 16-B chunks per X row
   constexpr int XC = (32 * CPR + 63) / 64;  // X chunks per lane (F <= 32)
   const int h = lane >> 5;
@@ -290,8 +307,8 @@ __global__ __launch_bounds__(256) void inter_bwd_kernel(
 #pragma unroll
         for (int t = 0; t < NB; ++t) {
           const int nt = nb + t;
-          // dX rows -> per-wave bf16 image ys [32][D] (row 0 gets the concat
-          // passthrough dZ[:, :D] and the bottom-MLP ReLU mask here)
+          // dX rows -> per-wave bf16 image ys [32][D]; row 0 (the dense
+          // slot) -> fp32 drow, finished in the store loop
 #pragma unroll
           for (int gq = 0; gq < 4; ++gq) {
             const int d0 = 32 * nt + 8 * gq + 4 * h;
@@ -299,31 +316,12 @@ __global__ __launch_bounds__(256) void inter_bwd_kernel(
             float v[4];
 #pragma unroll
             for (int q4 = 0; q4 < 4; ++q4) v[q4] = acc[t][4 * gq + q4];
-            // chunk (d0 >> 3) of the dZ row and of X row 0 (wave-uniform reads)
-            const int ch = (32 * nt + 8 * gq) >> 3;
-            const uint32_t z0 = __builtin_amdgcn_readlane(zv0s.x, ch);
-            const uint32_t z1 = __builtin_amdgcn_readlane(zv0s.y, ch);
-            const uint32_t z2 = __builtin_amdgcn_readlane(zv0s.z, ch);
-            const uint32_t z3 = __builtin_amdgcn_readlane(zv0s.w, ch);
-            const uint32_t x0 = __builtin_amdgcn_readlane(xv0s.x, ch);
-            const uint32_t x1 = __builtin_amdgcn_readlane(xv0s.y, ch);
-            const uint32_t x2 = __builtin_amdgcn_readlane(xv0s.z, ch);
-            const uint32_t x3 = __builtin_amdgcn_readlane(xv0s.w, ch);
             if (i == 0) {
-              const uint32_t za = h ? z2 : z0, zb = h ? z3 : z1;
-              v[0] += bf2f((uint16_t)(za & 0xffff)); v[1] += bf2f((uint16_t)(za >> 16));
-              v[2] += bf2f((uint16_t)(zb & 0xffff)); v[3] += bf2f((uint16_t)(zb >> 16));
-              if (relu_mask) {
-                const uint32_t xa = h ? x2 : x0, xb = h ? x3 : x1;
-                if (!(bf2f((uint16_t)(xa & 0xffff)) > 0.f)) v[0] = 0.f;
-                if (!(bf2f((uint16_t)(xa >> 16)) > 0.f)) v[1] = 0.f;
-                if (!(bf2f((uint16_t)(xb & 0xffff)) > 0.f)) v[2] = 0.f;
-                if (!(bf2f((uint16_t)(xb >> 16)) > 0.f)) v[3] = 0.f;
-              }
-            }
-            if (i < F)
-              *(uint2*)((char*)ys + i * D * 2 + (((d0 >> 3) ^ xswz<D>(i)) << 4) + ((d0 & 7) << 1)) =
+              *(float4*)(drow + d0) = make_float4(v[0], v[1], v[2], v[3]);
+            } else if (i < F) {
+              *(uint2*)((char*)ys + i * D * 2 + (((d0 >> 3) ^ yswz<D>(i)) << 4) + ((d0 & 7) << 1)) =
                   make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+            }
           }
         }
       }
@@ -337,7 +335,28 @@ __global__ __launch_bounds__(256) void inter_bwd_kernel(
         const int c = lane + 64 * k;
         if (c < F * CPR) {
           const int j = c / CPR, ch = c - j * CPR;
-          const uint4 v = *(const uint4*)((const char*)ys + j * D * 2 + ((ch ^ xswz<D>(j)) << 4));
+          uint4 v;
+          if (k == 0 && c < CPR) {
+            // dense slot chunk ch = lane: dX (fp32) + the concat passthrough
+            // dZ[:, :D], times the bottom-MLP ReLU mask -- this lane holds
+            // chunk ch of the dZ row (zv0s) and of X row 0 (xv0s)
+            const float4 f0 = *(const float4*)(drow + 8 * ch);
+            const float4 f1 = *(const float4*)(drow + 8 * ch + 4);
+            float f[8] = {f0.x, f0.y, f0.z, f0.w, f1.x, f1.y, f1.z, f1.w};
+            const uint32_t zw[4] = {zv0s.x, zv0s.y, zv0s.z, zv0s.w};
+            const uint32_t xw[4] = {xv0s.x, xv0s.y, xv0s.z, xv0s.w};
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+              const uint16_t zq = (uint16_t)(zw[q >> 1] >> (16 * (q & 1)));
+              const uint16_t xq = (uint16_t)(xw[q >> 1] >> (16 * (q & 1)));
+              f[q] += bf2f(zq);
+              if (relu_mask && !(bf2f(xq) > 0.f)) f[q] = 0.f;
+            }
+            v = make_uint4(pack2bf(f[0], f[1]), pack2bf(f[2], f[3]), pack2bf(f[4], f[5]),
+                           pack2bf(f[6], f[7]));
+          } else {
+            v = *(const uint4*)((const char*)ys + j * D * 2 + ((ch ^ yswz<D>(j)) << 4));
+          }
           uint16_t* dst = j == 0 ? d_dense + (int64_t)b * ld_ddense
                                  : d_emb + dslot[j] + (int64_t)b * dslot[32 + j];
           *(uint4*)(dst + ch * 8) = v;
@@ -393,7 +412,7 @@ void interaction_bwd(const uint16_t* dz, int64_t ldz, const uint16_t* dense,
                      const SlotMap& dslots, int relu_mask, hipStream_t s) {
   if (B <= 0) return;
   const int ldz_al = (int)((ldz + 7) & ~7LL);
-  const size_t smem = SLOT_BYTES + (size_t)WAVES * (32 * D * 2 + ldz_al * 2);
+  const size_t smem = SLOT_BYTES + (size_t)WAVES * (32 * D * 2 + ldz_al * 2 + D * 4);
   dim3 grid(grid_for(B, 4));
 #define TDFO_IBWD(DD)                                                          \
   if (smem > 65536)                                                            \
