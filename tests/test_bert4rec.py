@@ -284,3 +284,19 @@ def test_rank_metrics_reference_matches_recall_ndcg():
     exp = recall_ndcg_sums(scores)
     assert torch.allclose(out[:-1], exp, atol=1e-4)
     assert float(out[-1]) == B
+
+
+def test_bert4rec_step_counters_bumped_once_per_step():
+    """The trainer bumps the dense / embedding optimizer step numbers and the
+    dropout RNG step with one ops.bump per step (the optimizers skip their own)."""
+    tr = Bert4RecTrainer(n_items=30, max_len=6, embed_dim=16, n_heads=2, n_layers=1,
+                         batch_size=4, device="cpu")
+    g = torch.Generator().manual_seed(0)
+    for i in range(3):
+        seqs = torch.randint(1, 31, (4, 6), generator=g)
+        labels = torch.where(torch.rand(4, 6, generator=g) < 0.5, seqs, torch.zeros_like(seqs))
+        tr.load_batch(seqs, labels)
+        tr.step()
+        assert float(tr.opt.hyper[1]) == i + 1
+        assert float(tr.item.hyper[1]) == i + 1
+        assert int(tr.model.rng_step) == i + 1

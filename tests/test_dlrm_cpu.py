@@ -144,3 +144,27 @@ def test_deferred_wgrads_bitwise_equal(interaction):
         res.append((tr.fp.p.clone(), tr.emb.tw_store.weight.clone()))
     assert torch.equal(res[0][0], res[1][0])
     assert torch.equal(res[0][1], res[1][1])
+
+
+def test_bump_counters_cpu():
+    """ops.bump adds one to the first element of each float / int64 counter."""
+    h = torch.tensor([0.5, 3.0, 1.0])
+    r = torch.zeros(1, dtype=torch.int64)
+    ops.bump([h[1:2], r])
+    ops.bump([h[1:2], r])
+    assert h.tolist() == [0.5, 5.0, 1.0] and int(r) == 2
+
+
+def test_wgrad_splits_slot_sizing():
+    """128x128-tile target: ~target blocks, >= 8 K tiles per split. Slot
+    sizing (256x128 kernel, DCN-v2): the split count that minimises block
+    rounds x K tiles plus the slab-traffic penalty, never more K splits than
+    the K tiles allow."""
+    assert ops.wgrad_splits(1024, 1024, 8192, 256) == 4
+    assert ops.wgrad_splits(256, 512, 8192, 256) == 16
+    assert ops.wgrad_splits(64, 64, 512, 256) == 1          # K = 8 tiles: no split
+    for M, N in [(512, 3456), (3456, 576), (1024, 3520)]:
+        s = ops.wgrad_splits(M, N, 8192, 256, slots=128)
+        assert 1 <= s <= 8192 // 64 // 8
+        tiles = -(-M // 256) * -(-N // 128)
+        assert tiles * s <= 4 * 128 or s == 1               # a few rounds of the resident blocks
