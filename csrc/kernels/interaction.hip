@@ -167,7 +167,7 @@ __global__ __launch_bounds__(256) void inter_bwd_kernel(
     }
   }
   __syncthreads();
-  char* base = smem_raw + SLOT_BYTES + w * (XB + ldz_al * 2 + D * 4);
+  char* base = smem_raw + SLOT_BYTES + w * (XB + ldz_al * 2 + 16 + D * 4);
   char* xs = base;
   // dX image [32][D] aliases the X image (same chunk swizzle): column tile nt
   // is written only after its MFMAs consumed X's same columns, and the
@@ -178,7 +178,7 @@ __global__ __launch_bounds__(256) void inter_bwd_kernel(
   // fp32 dX row 0 (the dense slot): its passthrough and ReLU mask are
   // applied in the store loop by the CPR lanes that hold that row's dZ / X
   // chunks in registers, instead of by every lane of every epilogue step
-  float* drow = (float*)(base + XB + ldz_al * 2);
+  float* drow = (float*)(base + XB + ldz_al * 2 + 16);
   constexpr int CPR = D / 8;  // 16-B chunks per X row
   constexpr int XC = (32 * CPR + 63) / 64;  // X chunks per lane (F <= 32)
   const int h = lane >> 5;
@@ -196,15 +196,16 @@ __global__ __launch_bounds__(256) void inter_bwd_kernel(
   // this lane's 16 S entries (row i = lane & 31, k = 16 ks + 8 h + jj) as
   // dZ-row offsets of the strict lower triangle, and which of them exist
   const int i = lane & 31;
+  // (entries outside the triangle read a zero kept past the dZ row: no
+  // per-entry select when S is assembled)
+  if (lane == 0) *(uint4*)(zrow + ldz_al) = make_uint4(0, 0, 0, 0);
   int soff[16];
-  uint32_t smask = 0;
 #pragma unroll
   for (int e = 0; e < 16; ++e) {
     const int k = 16 * (e >> 3) + 8 * h + (e & 7);
     const bool ok = i < F && k < F && i != k;
     const int hi = i > k ? i : k, lo = i > k ? k : i;
-    soff[e] = ok ? D + hi * (hi - 1) / 2 + lo : 0;
-    smask |= (ok ? 1u : 0u) << e;
+    soff[e] = ok ? D + hi * (hi - 1) / 2 + lo : ldz_al;
   }
   // Every load is issued unconditionally at a clamped address (chunks past
   // the row re-read its last chunk and are never written to LDS): a
@@ -253,16 +254,14 @@ __global__ __launch_bounds__(256) void inter_bwd_kernel(
     wave_sync();
     if (valid) {
       // S operand: S[i][k], i = lane&31, k = 16ks + 8h + jj, read from the
-      // dZ row at the per-lane offsets computed once per kernel (loads
-      // unconditional, masked after)
+      // dZ row at the per-lane offsets computed once per kernel
       bf16x8_t sa[2];
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         s16x8_t t;
 #pragma unroll
         for (int jj = 0; jj < 8; ++jj) {
-          const uint16_t v = zrow[soff[8 * ks + jj]];
-          t[jj] = (short)(((smask >> (8 * ks + jj)) & 1u) ? v : (uint16_t)0);
+          t[jj] = (short)zrow[soff[8 * ks + jj]];
         }
         sa[ks] = __builtin_bit_cast(bf16x8_t, t);
       }
@@ -412,7 +411,7 @@ void interaction_bwd(const uint16_t* dz, int64_t ldz, const uint16_t* dense,
                      const SlotMap& dslots, int relu_mask, hipStream_t s) {
   if (B <= 0) return;
   const int ldz_al = (int)((ldz + 7) & ~7LL);
-  const size_t smem = SLOT_BYTES + (size_t)WAVES * (32 * D * 2 + ldz_al * 2 + D * 4);
+  const size_t smem = SLOT_BYTES + (size_t)WAVES * (32 * D * 2 + ldz_al * 2 + 16 + D * 4);
   dim3 grid(grid_for(B, 4));
 #define TDFO_IBWD(DD)                                                          \
   if (smem > 65536)                                                            \

@@ -88,12 +88,20 @@ class StreamGraphsMixin:
         pool = torch.cuda.graph_pool_handle()
         graphs = {}
         se.wait_stream(torch.cuda.current_stream())
+        # diagnostics (scripts/w1_timeline.py): device timestamps around each
+        # captured segment
+        stamp = getattr(self, "_ms_stamp", None)
+        names = list(plan)
         for name in plan:
             gr = torch.cuda.CUDAGraph(keep_graph=composed)
             # (the MLP graphs capture on torch's own side stream: capture is
             # not allowed on the default stream; replays run on any stream)
             with graph_capture(gr, pool=pool, stream=se if name[0] == "E" else None):
+                if stamp is not None:
+                    ops.stamp(stamp[0], stamp[1], names.index(name), len(names), 0)
                 plan[name]()
+                if stamp is not None:
+                    ops.stamp(stamp[0], stamp[1], names.index(name), len(names), 1)
             graphs[name] = gr
         if composed:
             graphs["M"] = ops.ComposedGraph([("graph", graphs["M1"]), ("wait", ev[1]),
@@ -107,6 +115,7 @@ class StreamGraphsMixin:
             ids_stream = composed
         cs = torch.cuda.Stream(device=self.device) if ids_stream else None
         self._ms = {"graphs": graphs, "stream": se, "plan": plan, "composed": composed,
+                    "names": names,
                     "cstream": cs, "ev_e2": ops.SyncEvent(2), "ev_copy": ops.SyncEvent(2),
                     "e2_recorded": False, "events": ev}
         self.graph = "streams"
