@@ -12,18 +12,29 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def main():
+    import json
     from tdfo_amd.models.dlrm import CRITEO_1TB_ROWS, DLRMConfig, DLRMTrainer
     from tdfo_amd.ops import _ext
     from tdfo_amd.train.loop import StepLoop, make_source
     assert _ext.load()
     dev = torch.device("cuda", 0)
-    cfg = DLRMConfig(table_rows=list(CRITEO_1TB_ROWS))
+    kind = sys.argv[1] if len(sys.argv) > 1 else "fresh"        # fresh | pool
+    over = json.loads(sys.argv[2]) if len(sys.argv) > 2 else {}  # DLRMConfig overrides
+    cfg = DLRMConfig(table_rows=list(CRITEO_1TB_ROWS), **over)
     tr = DLRMTrainer(cfg, 8192, dev)
+    print(f"data={kind} cfg={over}")
     steps, nseg = 40, 8
     buf = torch.zeros((steps + 8) * nseg * 2, dtype=torch.int64, device=dev)
     cnt = torch.zeros(nseg, dtype=torch.int64, device=dev)
     tr._ms_stamp = (buf, cnt)
-    src = make_source(cfg.table_rows, 8192, dev, cfg.pooling_factors(), 1, 0, kind="fresh")
+    if kind == "pool":
+        from tdfo_amd.data.synthetic import SyntheticCriteo
+        from tdfo_amd.train.loop import PoolBatches
+        data = SyntheticCriteo(cfg.table_rows, 8192, pooling=cfg.pooling_factors(), device=dev,
+                               seed=1)
+        src = PoolBatches([data.next() for _ in range(8)])
+    else:
+        src = make_source(cfg.table_rows, 8192, dev, cfg.pooling_factors(), 1, 0, kind="fresh")
     loop = StepLoop(tr, src)
     loop.run(9)
     tr.capture_graph(warmup=1)

@@ -429,6 +429,7 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin):
         self._next = None
         self._primed = False
         self._mstream = False            # per-stream graphs (one process)
+        self._bstg = None                # staged dense / labels (per-stream graphs)
         self._ms = None
         self._whole_capture = False      # capturing the multi-rank stream graphs
         self._cap_origin = None          # origin of a multi-stream capture (see _wait)
@@ -475,9 +476,20 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin):
         right behind the previous step's embedding update, so the next lookup
         overlaps the previous step's bottom-MLP backward.
         """
-        if self.graph == "streams" and self._ms_load_ids(ids, on_device):
-            ops.batch_load(dense, self.x0, ids[:0], self.ids[:0], label, self.label)
-            return
+        if self.graph == "streams":
+            stg = self._bstg
+            if self._ms_load_ids(ids, on_device, dense, label):
+                if stg is None:
+                    ops.batch_load(dense, self.x0, ids[:0], self.ids[:0], label, self.label)
+                elif not on_device:              # (staged graphs: M1 loads from the staging)
+                    stg[0].copy_(dense, non_blocking=True)
+                    stg[1].copy_(label.reshape(-1), non_blocking=True)
+                return
+            if stg is not None:
+                stg[0].copy_(dense, non_blocking=True)
+                stg[1].copy_(label.reshape(-1), non_blocking=True)
+                self.ids.copy_(ids)
+                return
         # device-resident batch: one fused launch (ids, labels, dense -> bf16)
         ops.batch_load(dense, self.x0, ids, self.ids, label, self.label)
 

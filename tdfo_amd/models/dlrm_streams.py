@@ -69,7 +69,13 @@ class StreamGraphsMixin:
             else:
                 self._s_dense_update()
 
-        return {"E1": e1, "E2": emb.stage_bwd_prepare, "M1": self._s_bottom_fwd,
+        def m1():
+            if self._bstg is not None:       # this step's dense / labels from the staging
+                ops.batch_load(self._bstg[0], self.x0, self.ids[:0], self.ids[:0], self._bstg[1],
+                               self.label)
+            self._s_bottom_fwd()
+
+        return {"E1": e1, "E2": emb.stage_bwd_prepare, "M1": m1,
                 "M2": self._s_top, "E3": e3, "M3": m3}
 
     def _capture_streams(self):
@@ -83,6 +89,20 @@ class StreamGraphsMixin:
         # scope and no host reads these edges): DLRM-1TB 0.477-0.480 vs
         # 0.485-0.487 ms/step with torch events
         ev = [ops.SyncEvent(2) for _ in range(4)]
+        ids_stream = self.cfg.ids_stream
+        if ids_stream is None:
+            ids_stream = composed
+        # Staged batches (composed graphs + ids stream): a device batch is
+        # copied (ids, dense, labels) on the ids stream into fixed buffers, and
+        # the MLP graph converts dense / labels itself behind an in-graph wait
+        # -- no eager launch and graph boundary on the MLP stream between
+        # steps (that boundary idled it ~23-31 us per step,
+        # profiles/r03/s3/w1_timeline/)
+        self._bstg = None
+        if composed and ids_stream:
+            self._bstg = (torch.zeros(self.B, self.cfg.num_dense, device=self.device),
+                          torch.zeros(self.B, device=self.device))
+        ev_copy = ops.SyncEvent(2)
         plan = self._ms_plan()
         se = torch.cuda.Stream(device=self.device)
         pool = torch.cuda.graph_pool_handle()
@@ -104,26 +124,25 @@ class StreamGraphsMixin:
                     ops.stamp(stamp[0], stamp[1], names.index(name), len(names), 1)
             graphs[name] = gr
         if composed:
-            graphs["M"] = ops.ComposedGraph([("graph", graphs["M1"]), ("wait", ev[1]),
-                                             ("graph", graphs["M2"]), ("record", ev[2]),
-                                             ("graph", graphs["M3"])])
+            head = [("wait", ev_copy)] if self._bstg is not None else []
+            graphs["M"] = ops.ComposedGraph(head + [("graph", graphs["M1"]), ("wait", ev[1]),
+                                                    ("graph", graphs["M2"]), ("record", ev[2]),
+                                                    ("graph", graphs["M3"])])
             graphs["EA"] = ops.ComposedGraph([("graph", graphs["E1"]), ("record", ev[1]),
                                               ("graph", graphs["E2"])])
         torch.cuda.synchronize()
-        ids_stream = self.cfg.ids_stream
-        if ids_stream is None:
-            ids_stream = composed
         cs = torch.cuda.Stream(device=self.device) if ids_stream else None
         self._ms = {"graphs": graphs, "stream": se, "plan": plan, "composed": composed,
                     "names": names,
-                    "cstream": cs, "ev_e2": ops.SyncEvent(2), "ev_copy": ops.SyncEvent(2),
+                    "cstream": cs, "ev_e2": ops.SyncEvent(2), "ev_copy": ev_copy,
                     "e2_recorded": False, "events": ev}
         self.graph = "streams"
 
-    def _ms_load_ids(self, ids: torch.Tensor, on_device: bool) -> bool:
+    def _ms_load_ids(self, ids: torch.Tensor, on_device: bool, dense=None, label=None) -> bool:
         """Per-stream mode: copy this step's ids on the embedding side (the
-        lookup follows the previous step's embedding update on that stream).
-        Returns False when the caller must use the plain fused load."""
+        lookup follows the previous step's embedding update on that stream),
+        and with staged batches its dense features / labels too. Returns
+        False when the caller must use the plain fused load."""
         if not (ids.is_cuda and ids.dtype == torch.int64 and ids.is_contiguous()
                 and ids.numel() == self.ids.numel()):
             return False
@@ -136,8 +155,16 @@ class StreamGraphsMixin:
             # already signalled instead of queueing the copy behind the update
             if self._ms["e2_recorded"]:
                 cs.wait_event(self._ms["ev_e2"])
+            stg = self._bstg
+            if stg is not None:
+                # the previous step's MLP graph read the staging in M1, before
+                # its ev[2] record (a wait on a never-recorded event is a no-op)
+                cs.wait_event(self._ms["events"][2])
             with torch.cuda.stream(cs):
                 self.ids.copy_(ids, non_blocking=True)
+                if stg is not None:
+                    stg[0].copy_(dense, non_blocking=True)
+                    stg[1].copy_(label.reshape(-1), non_blocking=True)
                 self._ms["ev_copy"].record(cs)
             se.wait_event(self._ms["ev_copy"])
             return True
