@@ -24,7 +24,6 @@ def run(over, model, steps=50, warmup=10):
         kw.update(interaction="dcn", pooling=list(MLPERF_MULTIHOT), top=[1024, 1024, 512, 256, 1])
     kw.update(over)
     cfg = DLRMConfig(**kw)
-    cfg.ids_stream = False
     tr = DLRMTrainer(cfg, 8192, dev)
     src = make_source(cfg.table_rows, 8192, dev, cfg.pooling_factors(), 1, 0, kind="fresh")
     loop = StepLoop(tr, src)
