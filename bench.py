@@ -61,16 +61,27 @@ def parse(argv=None):
                          "per-stream step graphs with the collectives inside")
     ap.add_argument("--host-data", action="store_true", help="same as --data host")
     ap.add_argument("--emulate-world", type=int, default=0, metavar="W",
-                    help="one GPU runs rank 0 of the W-rank job: the real W-rank plan, layouts "
+                    help="one GPU runs one rank of the W-rank job: the real W-rank plan, layouts "
                          "and kernels, each collective replaced by device copies of the same "
                          "byte count (parallel/comm.py LoopbackComm); reports device ms/step, "
                          "host issue us/step and the collective volume (not the headline)")
-    ap.add_argument("--emulate-link-gbps", type=float, default=300.0,
+    ap.add_argument("--emulate-rank", default="0", metavar="K|max",
+                    help="--emulate-world: the rank to emulate, or 'max': every rank of the "
+                         "plan in turn, reporting the slowest (a synchronous step runs at the "
+                         "pace of its slowest rank)")
+    ap.add_argument("--emulate-link-gbps", type=float, default=None,
                     help="--emulate-world: modelled per-rank xGMI injection bandwidth (GB/s); "
                          "each emulated collective also holds the comm stream for its link "
-                         "bytes / this (0: local copies only)")
+                         "bytes / this. Default: the planner's / SOL's link model, "
+                         "min(W-1, 7) x 153 GB/s (one point-to-point link per peer); 0: local "
+                         "copies only")
     ap.add_argument("--emulate-latency-us", type=float, default=10.0,
                     help="--emulate-world: modelled fixed cost per collective (us)")
+    ap.add_argument("--watchdog-s", type=float, default=float(os.environ.get("TDFO_WATCHDOG_S",
+                                                                          180)),
+                    help="hang guard: a step whose heartbeat has not landed after this many "
+                         "seconds (or a host that stops issuing steps) ends the rank with exit "
+                         "code 3 and a diagnostic on stderr; 0 disables it")
     args = ap.parse_args(argv)
     if args.host_data:
         args.data = "host"
@@ -125,63 +136,38 @@ def self_launch(args, argv) -> int:
     return subprocess.call(cmd)
 
 
-def main(argv=None):
-    argv = list(sys.argv[1:] if argv is None else argv)
-    args = parse(argv)
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        sys.exit(self_launch(args, argv))
-    from tdfo_amd.parallel.dist import init_distributed, reset
-    from tdfo_amd.models.dlrm import (CRITEO_1TB_ROWS, CRITEO_KAGGLE_ROWS, DCN_GT1TB_ROWS,
-                                      MLPERF_MULTIHOT, DLRMConfig, DLRMTrainer)
-    from tdfo_amd.data.synthetic import SyntheticCriteo
-    from tdfo_amd.ops import _ext
-
-    world_env = int(os.environ.get("WORLD_SIZE", "1"))
-    if world_env != args.gpus:
-        raise SystemExit(f"error: --gpus {args.gpus} but WORLD_SIZE={world_env}")
-    if args.emulate_world and args.gpus != 1:
-        raise SystemExit("error: --emulate-world runs in one process (--gpus 1)")
-    info = init_distributed("cuda")
-    world = info.world_size
-    group = info.group
-    if args.emulate_world > 1:
-        from tdfo_amd.parallel.comm import LoopbackComm
-        world = args.emulate_world
-        group = LoopbackComm(world, 0, info.device, link_gbps=args.emulate_link_gbps,
-                             latency_us=args.emulate_latency_us)
-        world_env = world
-    if not _ext.load():
-        raise RuntimeError("native HIP library failed to load")
-    if os.environ.get("TDFO_GEMM_POLICY"):      # override the trainer's per-model choice
-        from tdfo_amd import ops
-        ops.gemm_policy(int(os.environ["TDFO_GEMM_POLICY"]))
-    rows = {"1tb": CRITEO_1TB_ROWS, "kaggle": CRITEO_KAGGLE_ROWS, "gt1tb": DCN_GT1TB_ROWS,
-            "tiny": [1000] * 26}[args.rows]
-    pipe = world_env > 1 and not args.no_pipeline
+def _cfg(args, rows, pipe):
+    from tdfo_amd.models.dlrm import MLPERF_MULTIHOT, DLRMConfig
     if args.model == "dlrm":
-        cfg = DLRMConfig(table_rows=list(rows), sharding=args.sharding, pipeline=pipe,
-                         dense_comm=args.dense_comm, stream_graphs=not args.no_stream_graphs)
-    else:
-        cfg = DLRMConfig(table_rows=list(rows), interaction="dcn", pooling=list(MLPERF_MULTIHOT),
-                         top=[1024, 1024, 512, 256, 1], sharding=args.sharding, pipeline=pipe,
-                         dense_comm=args.dense_comm, stream_graphs=not args.no_stream_graphs)
+        return DLRMConfig(table_rows=list(rows), sharding=args.sharding, pipeline=pipe,
+                          dense_comm=args.dense_comm, stream_graphs=not args.no_stream_graphs)
+    return DLRMConfig(table_rows=list(rows), interaction="dcn", pooling=list(MLPERF_MULTIHOT),
+                      top=[1024, 1024, 512, 256, 1], sharding=args.sharding, pipeline=pipe,
+                      dense_comm=args.dense_comm, stream_graphs=not args.no_stream_graphs)
+
+
+def measure(args, info, cfg, world: int, group, rank: int) -> dict:
+    """Build the trainer of ``rank``, run the warm-up (eager steps, capture,
+    first replays), then time ``args.steps`` steps between barriers + device
+    synchronisations. Returns the measurement and the live trainer."""
+    from tdfo_amd.models.dlrm import DLRMTrainer
+    from tdfo_amd.data.synthetic import SyntheticCriteo
+    from tdfo_amd.train.loop import PoolBatches, StepLoop, make_source
+    from tdfo_amd.utils.watchdog import StepWatchdog
+
     B = args.batch
     t0 = time.time()
-    if args.data in ("host", "fresh"):
-        # a streamed data source orders its batch on every input stream and
-        # releases a slot after all of them: a third (ids) stream ties the
-        # slot to the sort and stalls the prefetch (0.604 vs 0.470 ms/step)
-        cfg.ids_stream = False
-    tr = DLRMTrainer(cfg, B, info.device, group=group, rank=info.rank, world_size=world)
-    from tdfo_amd.train.loop import PoolBatches, StepLoop, make_source
+    tr = DLRMTrainer(cfg, B, info.device, group=group, rank=rank, world_size=world)
     if args.data == "pool":
         data = SyntheticCriteo(cfg.table_rows, B, pooling=cfg.pooling_factors(),
-                               device=info.device, seed=1, rank=info.rank, dist=args.dist)
+                               device=info.device, seed=1, rank=rank, dist=args.dist)
         src = PoolBatches([data.next() for _ in range(args.pool)])
     else:
-        src = make_source(cfg.table_rows, B, info.device, cfg.pooling_factors(), 1, info.rank,
+        src = make_source(cfg.table_rows, B, info.device, cfg.pooling_factors(), 1, rank,
                           dist=args.dist, kind=args.data)
-    loop = StepLoop(tr, src)
+    wd = (StepWatchdog(info.device, args.watchdog_s, rank=info.rank, describe=tr.progress)
+          if args.watchdog_s > 0 else None)
+    loop = StepLoop(tr, src, watchdog=wd)
     torch.cuda.synchronize()
     setup_s = time.time() - t0
     use_graph = not args.no_graph
@@ -214,6 +200,9 @@ def main(argv=None):
     if info.world_size > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
+    mb = tr.emb._rw_mbox
+    wait0 = mb.wait_s if mb is not None else 0.0
+    grows0 = tr.emb.rw_grows if tr.emb.rw_tables else 0
     t = time.perf_counter()
     loop.run(args.steps)
     host_s = time.perf_counter() - t          # issue time (the device runs behind)
@@ -221,44 +210,150 @@ def main(argv=None):
     if info.world_size > 1:
         torch.distributed.barrier()
     el = time.perf_counter() - t
+    if wd is not None:
+        wd.close()
     if info.world_size > 1:
         x = torch.tensor([el], dtype=torch.float64, device=info.device)
         torch.distributed.all_reduce(x, op=torch.distributed.ReduceOp.MAX)
         el = float(x.item())
+    wait_s = (mb.wait_s if mb is not None else 0.0) - wait0
     loss = tr.pop_loss() / max(1, args.steps * B)
+    comm = ({k: {"calls_per_step": round(c, 2), "MB_per_step": round(b / 1e6, 3)}
+             for k, (c, b) in sorted(step_stats[0].items())} if step_stats is not None else {})
+    return {"tr": tr, "loop": loop, "el": el, "host_s": host_s, "wait_s": wait_s,
+            "loss": loss, "setup_s": setup_s, "comm": comm,
+            "modelled_us": step_stats[1] if step_stats is not None else 0.0,
+            "rw_grows_timed": (tr.emb.rw_grows if tr.emb.rw_tables else 0) - grows0}
+
+
+def _graph_name(tr):
+    return tr.graph if isinstance(tr.graph, str) else ("staged" if tr.graph else None)
+
+
+def emulate(args, info, rows):
+    """--emulate-world: one (or, with --emulate-rank max, every) rank of the
+    W-rank job on this GPU over loopback collectives."""
+    import gc
+
+    from tdfo_amd.parallel.comm import LoopbackComm
+    from tdfo_amd.sparse.planner import LINK_GBS
+
+    W = args.emulate_world
+    link = (args.emulate_link_gbps if args.emulate_link_gbps is not None
+            else min(W - 1, 7) * LINK_GBS)
+    ranks = list(range(W)) if args.emulate_rank == "max" else [int(args.emulate_rank)]
+    cfg = _cfg(args, rows, not args.no_pipeline)
+    if args.data in ("host", "fresh"):
+        cfg.ids_stream = False
+    per = []
+    comm0 = plan_summary = None
+    for k in ranks:
+        group = LoopbackComm(W, k, info.device, link_gbps=link, latency_us=args.emulate_latency_us)
+        r = measure(args, info, cfg, W, group, k)
+        tr = r["tr"]
+        ms = r["el"] / args.steps * 1e3
+        rec = {"rank": k, "ms_per_step": round(ms, 4),
+               "host_issue_us_per_step": round((r["host_s"] - r["wait_s"]) / args.steps * 1e6, 1),
+               "host_wait_us_per_step": round(r["wait_s"] / args.steps * 1e6, 1),
+               "graph": _graph_name(tr), "plan_cost": round(tr.plan.cost[k], 1),
+               "mem_GiB": round(tr.plan.mem_bytes[k] / 2**30, 1), "setup_s": round(r["setup_s"], 1)}
+        if tr.emb.rw_tables:
+            rec.update(rw_cap=tr.emb.rw_cap, rw_grows=tr.emb.rw_grows,
+                       rw_grows_timed=r["rw_grows_timed"])
+        print(json.dumps(rec), file=sys.stderr, flush=True)
+        if plan_summary is None:
+            plan_summary, comm0 = tr.plan.summary(), r["comm"]
+        per.append((rec, r))
+        if len(ranks) > 1:
+            r["loop"].close()
+            del tr, r, group
+            per[-1] = (rec, None)
+            gc.collect()
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+    rec = max((p[0] for p in per), key=lambda x: x["ms_per_step"])
+    ms = rec["ms_per_step"]
+    print(json.dumps({
+        "metric": (f"emulated step of the {W}-rank job, slowest of ranks {ranks} "
+                   "(loopback collectives)" if len(ranks) > 1 else
+                   f"emulated rank-{ranks[0]} step of the {W}-rank job (loopback collectives)"),
+        "value": ms, "unit": "ms/step", "higher_is_better": False,
+        "emulated_world": W, "emulated_rank": rec["rank"], "steps": args.steps,
+        "warmup": args.warmup, "per_rank_ms": {p[0]["rank"]: p[0]["ms_per_step"] for p in per},
+        "host_issue_us_per_step": rec["host_issue_us_per_step"],
+        "host_wait_us_per_step": rec["host_wait_us_per_step"],
+        "examples_per_sec_whole_job_model": round(args.batch * W / (ms / 1e3), 1),
+        "sol_ms_compute": round(cfg.sol(args.batch, 1)["sol_ms"], 4),
+        "sol_comm_ms": round(cfg.sol(args.batch, W)["comm_ms"], 4),
+        "comm": comm0,
+        "comm_model": {"link_gbps": link, "latency_us": args.emulate_latency_us},
+        "plan": plan_summary, "graph": rec["graph"], "pipeline": not args.no_pipeline,
+        "dist": args.dist, "data": args.data,
+        "config": {"model": "DLRM" if args.model == "dlrm" else "DCN-v2",
+                   "tables": f"criteo-{args.rows}", "per_gpu_batch": args.batch,
+                   "sharding": args.sharding}}), flush=True)
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args, argv))
+    from tdfo_amd.parallel.dist import init_distributed, reset
+    from tdfo_amd.models.dlrm import CRITEO_1TB_ROWS, CRITEO_KAGGLE_ROWS, DCN_GT1TB_ROWS
+    from tdfo_amd.ops import _ext
+
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env != args.gpus:
+        raise SystemExit(f"error: --gpus {args.gpus} but WORLD_SIZE={world_env}")
+    if args.emulate_world and args.gpus != 1:
+        raise SystemExit("error: --emulate-world runs in one process (--gpus 1)")
+    info = init_distributed("cuda")
+    if not _ext.load():
+        raise RuntimeError("native HIP library failed to load")
+    if os.environ.get("TDFO_GEMM_POLICY"):      # override the trainer's per-model choice
+        from tdfo_amd import ops
+        ops.gemm_policy(int(os.environ["TDFO_GEMM_POLICY"]))
+    rows = {"1tb": CRITEO_1TB_ROWS, "kaggle": CRITEO_KAGGLE_ROWS, "gt1tb": DCN_GT1TB_ROWS,
+            "tiny": [1000] * 26}[args.rows]
+    if args.emulate_world > 1:
+        emulate(args, info, rows)
+        reset()
+        return
+    world = info.world_size
+    cfg = _cfg(args, rows, world > 1 and not args.no_pipeline)
+    if args.data in ("host", "fresh"):
+        # a streamed data source orders its batch on every input stream and
+        # releases a slot after all of them: a third (ids) stream ties the
+        # slot to the sort and stalls the prefetch (0.604 vs 0.470 ms/step)
+        cfg.ids_stream = False
+    B = args.batch
+    r = measure(args, info, cfg, world, info.group, info.rank)
+    tr, el = r["tr"], r["el"]
     ms = el / args.steps * 1e3
     value = B * world * args.steps / el
     sol = cfg.sol(B, world)
-    comm = ({k: {"calls_per_step": round(c, 2), "MB_per_step": round(b / 1e6, 3)}
-             for k, (c, b) in sorted(step_stats[0].items())} if step_stats is not None else {})
-    if args.emulate_world > 1:
-        print(json.dumps({
-            "metric": f"emulated rank-0 step of the {world}-rank job (loopback collectives)",
-            "value": round(ms, 4), "unit": "ms/step", "higher_is_better": False,
-            "emulated_world": world, "steps": args.steps, "warmup": args.warmup,
-            "host_issue_us_per_step": round(host_s / args.steps * 1e6, 1),
-            "sol_ms_compute": round(cfg.sol(B, 1)["sol_ms"], 4),
-            "sol_comm_ms": round(sol["comm_ms"], 4), "comm": comm,
-            "comm_model": {"link_gbps": args.emulate_link_gbps,
-                           "latency_us": args.emulate_latency_us,
-                           "modelled_us_per_step": round(step_stats[1], 1)},
-            "plan": tr.plan.summary(), "graph": tr.graph if isinstance(tr.graph, str) else
-            ("staged" if tr.graph else None), "pipeline": tr.pipeline,
-            "data": args.data, "config": {"model": "DLRM" if args.model == "dlrm" else "DCN-v2",
-                                          "tables": f"criteo-{args.rows}", "per_gpu_batch": B}}),
-              flush=True)
-        reset()
-        return
+    consistent, per = True, {}
+    if world > 1:
+        # replicas must agree bit for bit before a throughput is reported
+        from tdfo_amd.parallel.replicas import check_replicas
+        inject = os.environ.get("TDFO_INJECT_DIVERGENCE")
+        state = tr.replicated_state()
+        if inject is not None and int(inject) == info.rank:
+            state["dense.p"].view(-1)[0] += 1e-3          # test hook: one diverged replica
+        consistent, per = check_replicas(state, info.group)
     if info.rank == 0:
-        print(json.dumps({"plan": tr.plan.summary(), "setup_s": round(setup_s, 1),
-                          "train_loss": round(loss, 4),
-                          "graph": tr.graph if isinstance(tr.graph, str) else
-                          ("staged" if tr.graph else None),
-                          "host_issue_us_per_step": round(host_s / args.steps * 1e6, 1),
-                          "comm": comm,
+        print(json.dumps({"plan": tr.plan.summary(), "setup_s": round(r["setup_s"], 1),
+                          "train_loss": round(r["loss"], 4), "graph": _graph_name(tr),
+                          "host_issue_us_per_step": round((r["host_s"] - r["wait_s"])
+                                                          / args.steps * 1e6, 1),
+                          "host_wait_us_per_step": round(r["wait_s"] / args.steps * 1e6, 1),
+                          "comm": r["comm"],
+                          "ranks_consistent": consistent if world > 1 else None,
+                          "replica_check": per if not consistent else None,
                           "dense_tflops": round(cfg.dense_flops_per_example() * value / 1e12, 1),
                           "sol": {k: round(v, 4) for k, v in sol.items()}}),
-              file=sys.stderr)
+              file=sys.stderr, flush=True)
         mname = "DLRM" if args.model == "dlrm" else "DCN-v2"
         rname = {"1tb": "1TB", "kaggle": "Kaggle", "gt1tb": "gt1TB", "tiny": "tiny"}[args.rows]
         src = {"fresh": "a fresh batch per step from the on-device generator (side stream)",
@@ -282,7 +377,12 @@ def main(argv=None):
                        "parallelism": parallelism(tr.plan, world),
                        "tables": f"criteo-{args.rows}", "embedding_dim": cfg.embedding_dim,
                        "per_gpu_batch": B}}), flush=True)
+    r["loop"].close()
     reset()
+    if not consistent:
+        print(f"error: rank {info.rank}: replicated state differs across ranks ({per})",
+              file=sys.stderr, flush=True)
+        sys.exit(4)
 
 
 if __name__ == "__main__":

@@ -5,6 +5,7 @@
 // allocation. Shapes, dtypes, strides and alignment are validated on the host
 // before any launch (a mis-shaped launch can fault the GPU).
 #include <cmath>
+#include <cstring>
 
 #include <ATen/ATen.h>
 #include <ATen/hip/HIPContext.h>
@@ -565,6 +566,32 @@ void sync_event_destroy(int64_t e) {
   TDFO_HIP_OK(hipEventDestroy(reinterpret_cast<hipEvent_t>(e)));
 }
 
+// ------------------------------------------------------- host mailbox
+// Words of hipHostMalloc'd coherent + mapped memory wrapped as a CPU int64
+// tensor (freed with it); the device writes them through their mapping
+// (host_publish) and the host polls them (parallel/mailbox.py).
+Tensor host_mailbox_alloc(int64_t n) {
+  TORCH_CHECK(n >= 1 && n <= 4096, "host_mailbox_alloc: 1..4096 words");
+  void* p = nullptr;
+  TDFO_HIP_OK(hipHostMalloc(&p, (size_t)n * 8, hipHostMallocCoherent | hipHostMallocMapped));
+  std::memset(p, 0, (size_t)n * 8);
+  return at::from_blob(p, {n}, [](void* q) { (void)hipHostFree(q); },
+                       at::TensorOptions().dtype(at::kLong));
+}
+
+void host_publish(const Tensor& value, const Tensor& seq, const Tensor& host, int64_t slot) {
+  TORCH_CHECK(value.is_cuda() && value.scalar_type() == at::kInt && value.numel() >= 1,
+              "host_publish: int32 GPU value");
+  TORCH_CHECK(seq.is_cuda() && seq.scalar_type() == at::kInt && seq.numel() >= 1,
+              "host_publish: int32 GPU sequence counter");
+  TORCH_CHECK(!host.is_cuda() && host.scalar_type() == at::kLong && slot >= 0 &&
+              slot < host.numel(), "host_publish: host mailbox word out of range");
+  void* dptr = nullptr;
+  TDFO_HIP_OK(hipHostGetDevicePointer(&dptr, host.data_ptr<int64_t>() + slot, 0));
+  tdfo::host_publish(value.data_ptr<int32_t>(), seq.data_ptr<int32_t>(),
+                     reinterpret_cast<uint64_t*>(dptr), cur_stream());
+}
+
 // A chain of captured graphs joined by event nodes, instantiated as ONE
 // executable graph: kinds[i] = 0 child graph (handles[i] = hipGraph_t of a
 // keep_graph capture), 1 wait on the event handles[i], 2 record it. Stream
@@ -1036,6 +1063,28 @@ void reduce_rows(const Tensor& inp, int64_t rows, int64_t n, int64_t ld, const T
                     (float)scale, cur_stream());
 }
 
+void slab_reduce(const std::vector<Tensor>& ins, const std::vector<int64_t>& splits,
+                 const std::vector<Tensor>& outs) {
+  TORCH_CHECK(!g_gemm_batch.on, "slab_reduce inside ops.gemm_batch");
+  TORCH_CHECK(ins.size() == splits.size() && ins.size() == outs.size() &&
+              (int)ins.size() <= tdfo::SLAB_MAX_SEGS, "slab_reduce: 1..16 matching segments");
+  tdfo::SlabReduceArgs a{};
+  a.nseg = (int)ins.size();
+  a.start[0] = 0;
+  for (int k = 0; k < a.nseg; ++k) {
+    const Tensor &in = ins[k], &out = outs[k];
+    check_dev(in, "slab"); check_dev(out, "out");
+    TORCH_CHECK(in.scalar_type() == at::kFloat && out.scalar_type() == at::kFloat &&
+                in.is_contiguous() && out.is_contiguous(), "slab_reduce: contiguous fp32");
+    const int64_t n = out.numel(), S = splits[k];
+    TORCH_CHECK(S >= 1 && n % 4 == 0 && in.numel() >= S * n && aligned16(in.data_ptr()) &&
+                aligned16(out.data_ptr()), "slab_reduce: S >= 1, n % 4, bounds, 16-B alignment");
+    a.seg[k] = {in.data_ptr<float>(), out.data_ptr<float>(), n, (int)S};
+    a.start[k + 1] = a.start[k] + n / 4;
+  }
+  tdfo::slab_reduce(a, cur_stream());
+}
+
 void colsum(const Tensor& x, const Tensor& out, bool accumulate) {
   check_dev(x, "x"); check_2d_rowmajor(x, "x");
   const int64_t M = x.size(0), N = x.size(1);
@@ -1226,6 +1275,8 @@ TORCH_LIBRARY(tdfo, m) {
     }();
     tdfo::spin_ticks(us > 0 ? (uint64_t)(us * ticks_per_us) : 0, cur_stream());
   });
+  m.def("host_mailbox_alloc(int n) -> Tensor", host_mailbox_alloc);
+  m.def("host_publish(Tensor value, Tensor(a!) seq, Tensor host, int slot) -> ()", host_publish);
   m.def("sync_event_record(int e) -> ()", sync_event_record);
   m.def("sync_event_wait(int e) -> ()", sync_event_wait);
   m.def("sync_event_destroy(int e) -> ()", sync_event_destroy);
@@ -1330,6 +1381,7 @@ TORCH_LIBRARY(tdfo, m) {
         "Tensor(c!)[] bumps) -> ()");
   m.def("reduce_rows(Tensor inp, int rows, int n, int ld, Tensor(a!) out, bool accumulate, float scale) -> ()");
   m.def("colsum(Tensor x, Tensor(a!) out, bool accumulate) -> ()");
+  m.def("slab_reduce(Tensor[] slabs, int[] splits, Tensor(a!)[] outs) -> ()");
   m.def("auc_hist(Tensor logits, Tensor labels, int nb, Tensor(a!) hist) -> ()");
   m.def("linear_xent(Tensor H, Tensor W, Tensor bias, Tensor labels, float eps, int ignore, "
         "Tensor(a!) dH, Tensor(b!) lossv, Tensor(c!)? dW, Tensor(d!)? db, Tensor(e!)? loss=None, "
@@ -1373,6 +1425,7 @@ TORCH_LIBRARY_IMPL(tdfo, CUDA, m) {
   m.impl("check_finite", check_finite);
   m.impl("sort_pairs", sort_pairs);
   m.impl("cast_bf16", cast_bf16);
+  m.impl("slab_reduce", slab_reduce);
   m.impl("head_bce", head_bce);
   m.impl("reduce_rows", reduce_rows);
   m.impl("head_reduce", head_reduce);

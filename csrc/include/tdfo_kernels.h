@@ -248,6 +248,8 @@ struct BumpArgs {
 void bump(const BumpArgs& a, hipStream_t s);
 void stamp(uint64_t* buf, int64_t* cnt, int seg, int nseg, int which, int64_t cap,
            hipStream_t s);
+// host mailbox: host_word[slot] = (++seq[slot]) << 32 | (uint32) value[0]
+void host_publish(const int32_t* value, int32_t* seq, uint64_t* host_word, hipStream_t s);
 
 // ---------------------------------------------------- loss / reduce ----
 // Fused last layer (K -> 1) + sigmoid BCE-with-logits + backward:
@@ -267,6 +269,12 @@ void head_reduce(const float* part, int nparts, int K, float* grad, float* loss_
 // out[j] (=|+=) sum_r in[r*ld + j], j < n, fixed order (deterministic).
 void reduce_rows(const float* in, int rows, int64_t n, int64_t ld, float* out,
                  int accumulate, float scale, hipStream_t s);
+// several fp32 split-K slab sets reduced in one launch: seg k sums S slabs of
+// n floats (n % 4 == 0, 16-B aligned) into out; start[] = prefix of n / 4
+struct SlabSeg { const float* in; float* out; int64_t n; int S; };
+constexpr int SLAB_MAX_SEGS = 16;
+struct SlabReduceArgs { SlabSeg seg[SLAB_MAX_SEGS]; int64_t start[SLAB_MAX_SEGS + 1]; int nseg; };
+void slab_reduce(const SlabReduceArgs& a, hipStream_t s);
 // out[n] = sum_m x[m, n] (bf16 in). part must hold parts(M)*N floats.
 void colsum_bf16(const uint16_t* x, int M, int N, int64_t ldx, float* part,
                  int nparts, float* out, int accumulate, hipStream_t s);

@@ -234,6 +234,25 @@ void stamp(uint64_t* buf, int64_t* cnt, int seg, int nseg, int which, int64_t ca
   TDFO_CHECK_HIP(hipGetLastError());
 }
 
+// Host mailbox (parallel/mailbox.py): one lane bumps the slot's device
+// sequence number and stores (seq << 32 | value) into host-mapped coherent
+// memory with ONE 64-bit system-scope vector store -- no fence, no L2
+// writeback (a system-scope event release idles every queue ~24 us). The host
+// polls the word until the sequence number it expects appears, so a late or
+// reordered store can only delay it, never hand it a stale value.
+__global__ void host_publish_kernel(const int32_t* value, int32_t* seq, uint64_t* host_word) {
+  if (threadIdx.x != 0) return;
+  const uint32_t s = (uint32_t)seq[0] + 1u;
+  seq[0] = (int32_t)s;
+  const uint64_t w = ((uint64_t)s << 32) | (uint64_t)(uint32_t)value[0];
+  __hip_atomic_store(host_word, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+void host_publish(const int32_t* value, int32_t* seq, uint64_t* host_word, hipStream_t s) {
+  hipLaunchKernelGGL(host_publish_kernel, dim3(1), dim3(64), 0, s, value, seq, host_word);
+  TDFO_CHECK_HIP(hipGetLastError());
+}
+
 // Step counters (optimizer step numbers, dropout RNG step) bumped by one
 // launch instead of one library add kernel each.
 __global__ void bump_kernel(BumpArgs a) {

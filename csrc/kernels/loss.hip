@@ -241,6 +241,37 @@ void reduce_rows(const float* in, int rows, int64_t n, int64_t ld, float* out,
   }
 }
 
+// Split-K weight-grad slabs of several layers summed in ONE launch (the
+// multi-rank step's per-bucket reduce before the dense all-reduce; one
+// reduce_rows launch per layer cost ~6.7 us each, profiles/r03/mstreams):
+// out[j] = sum_{r = 0..S-1} in[r * n + j] in split order (deterministic),
+// 16 B per thread, grid-stride over the segments' concatenated float4 work.
+__global__ __launch_bounds__(256) void slab_reduce_kernel(SlabReduceArgs a) {
+  const int64_t total = a.start[a.nseg];
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < total;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    int k = 0;
+    while (k + 1 < a.nseg && q >= a.start[k + 1]) ++k;
+    const SlabSeg& g = a.seg[k];
+    const int64_t j = (q - a.start[k]) * 4;
+    float4 acc = *(const float4*)(g.in + j);
+    for (int r = 1; r < g.S; ++r) {
+      const float4 v = *(const float4*)(g.in + (int64_t)r * g.n + j);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    *(float4*)(g.out + j) = acc;
+  }
+}
+
+void slab_reduce(const SlabReduceArgs& a, hipStream_t s) {
+  const int64_t total = a.start[a.nseg];
+  if (total <= 0) return;
+  int64_t blocks = (total + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(slab_reduce_kernel, dim3(blocks), dim3(256), 0, s, a);
+  TDFO_CHECK_HIP(hipGetLastError());
+}
+
 int colsum_parts(int M) { return COLSUM_CHUNKS; }
 
 void head_reduce(const float* part, int nparts, int K, float* grad, float* loss_acc,

@@ -379,12 +379,17 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
             # same box, profiles/r03/s3/dcn_policy.md); DLRM's <= 1024-wide
             # MLPs on the ping-pong / 64-row kernels
             ops.gemm_policy(5 if dcn else 0)
+        # the tile policy is process-global in the native library: each
+        # trainer re-applies its own before it issues or captures GEMMs, so
+        # trainers of different models can share a process
+        self._gemm_pol = ops.gemm_policy(-1) if dev.type == "cuda" else None
         # DCN-v2 on 256x128 tiles: bias grads from the ones column inside the
         # wgrad's N (that kernel has no column-sum epilogue), splits sized for
         # its resident blocks (half of them beside the paired dgrad)
         self._csum = not (dcn and dev.type == "cuda" and ops.gemm_policy(-1) in (4, 5))
         self._wg_slots = (128 if self._pair_bwd else 256) if not self._csum else 0
         self.wslab = {}
+        self._slab_sums = []          # (flat offset, slab, S, grad view) summed by _reduce_slabs
         self._segments = []
         self._opt_sums_slabs = dev.type == "cuda" and world_size == 1
         max_slab = 1
@@ -398,14 +403,22 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
                 self.wslab[L.name] = (sl, S)
                 if self._opt_sums_slabs:
                     self._segments.append((fp.offset(L.name + ".w"), sl, S))
-        # DCN-v2 V weight grads: same treatment
-        if cfg.interaction == "dcn" and self._opt_sums_slabs:
+                else:
+                    self._slab_sums.append((fp.offset(L.name + ".w"), sl, S,
+                                            fp.grad(L.name + ".w").view(-1)))
+        # DCN-v2 V weight grads: same treatment (per-layer slabs also with
+        # more than one rank, where their sums are batched per bucket)
+        if cfg.interaction == "dcn" and dev.type == "cuda":
             for i in range(cfg.dcn_layers):
                 S = self._wg_splits(cfg.dcn_rank, self.top_real)
                 if S > 1:
                     sl = z(S * cfg.dcn_rank * self.top_real, dt=torch.float32)
                     self.wslab[f"dcn{i}.v"] = (sl, S)
-                    self._segments.append((fp.offset(f"dcn{i}.v"), sl, S))
+                    if self._opt_sums_slabs:
+                        self._segments.append((fp.offset(f"dcn{i}.v"), sl, S))
+                    else:
+                        self._slab_sums.append((fp.offset(f"dcn{i}.v"), sl, S,
+                                                fp.grad(f"dcn{i}.v").view(-1)))
         self.dense_hyper = torch.tensor([cfg.dense_lr, 0.0, 1.0], dtype=torch.float32, device=dev)
         self.emb_hyper = torch.tensor([cfg.emb_lr, 0.0], dtype=torch.float32, device=dev)
         self.slot_off = [0] + list(self.emb.slot_off)
@@ -424,6 +437,11 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
         # starts at its lookup. Numerics are identical to the unpipelined step.
         self.pipeline = bool(cfg.pipeline) and world_size > 1
         self._pipe_lookup = self.pipeline and bool(cfg.pipeline_lookup)
+        # pipelined row-wise exchanges check their capacity one step late
+        # (ShardedEmbeddingBags.rw_publish_need / rw_resolve_need): no host
+        # read inside the step, so the row-wise plans (configs 3 and 5) run on
+        # the per-stream graphs too
+        self._rw_lagged = self.pipeline and bool(self.emb.rw_tables) and self.emb.rw_dynamic
         on_cuda = dev.type == "cuda"
         self._ev_loaded = torch.cuda.Event() if (on_cuda and self._pipe_lookup) else None
         self._ev_lookup = torch.cuda.Event() if (on_cuda and self._pipe_lookup) else None
@@ -501,6 +519,7 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
         consumes the batch loaded before it and loads / exchanges the next."""
         assert self.pipeline, "prime() needs DLRMConfig(pipeline=True) and world_size > 1"
         self.load_batch(dense, ids, label)
+        self.emb._rw_lag_pending = False       # (this exchange checks its capacity itself)
         if not self.emb.fwd_prep_noop:
             self.emb.stage_fwd_prep(self.ids)
         self.emb.stage_fwd_ids_exchange(async_op=True)
@@ -534,7 +553,16 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
         ops.batch_load(dense, self.x0, ids, self.ids, label, self.label)
 
     def _m_ids_exchange_next(self):
-        self.emb.stage_fwd_ids_exchange(async_op=True)
+        self.emb.stage_fwd_ids_exchange(async_op=True, lagged=self._rw_lagged)
+
+    def _rw_resolve(self):
+        """Lagged row-wise capacity check of the batch the coming step
+        consumes (exchanged in the previous step's tail): on growth its
+        row-wise exchange is redone into the larger segments here, every
+        stream idle, and the graphs are re-captured (layout_version)."""
+        if self._rw_lagged and self.emb.rw_resolve_need():
+            self.sync_streams()
+            self.emb.rw_redo()
 
     # ------------------------------------------------------------- layers
     def _fwd(self, L: Lin, x, out, relu=True):
@@ -549,12 +577,10 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
             self._dgrad(L, x, dy, dx, x_is_relu)
             return
         # the weight grad and the dgrad go out as one paired launch (the slab
-        # reduce of more than one rank runs after both)
+        # sum of more than one rank is batched per all-reduce bucket)
         with ops.gemm_batch(self._pair_bwd and dx is not None):
-            fin = self._wgrad_gemm(L, x, dy)
+            self._wgrad_gemm(L, x, dy)
             self._dgrad(L, x, dy, dx, x_is_relu)
-        if fin is not None:
-            fin()
 
     def _wg_splits(self, M: int, N: int) -> int:
         return ops.wgrad_splits(M, N, self.B, 256, slots=self._wg_slots)
@@ -565,14 +591,14 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
     def _wgrad(self, L: Lin, x, dy):
         """dW[:, :in_k] = dy^T x[:, :in_k]; db (column bcol) = colsum(dy) from
         the same GEMM when the bias is not inside K."""
-        fin = self._wgrad_gemm(L, x, dy)
-        if fin is not None:
-            fin()
+        self._wgrad_gemm(L, x, dy)
 
     def _wgrad_gemm(self, L: Lin, x, dy):
-        """The weight-grad GEMM alone; returns the split-K slab reduce still
-        to run (more than one rank: the all-reduce needs the grads) or None
-        (one GPU: the optimizer sums the slabs)."""
+        """The weight-grad GEMM alone. Its split-K slabs are summed by the
+        fused optimizer on one GPU; with more than one rank the all-reduce
+        needs the grads, so the slabs of every layer of an all-reduce bucket
+        are summed in ONE launch right before that all-reduce
+        (``_reduce_slabs``)."""
         csum = -1 if (L.bias_in_k or not self._csum) else L.bcol
         n = self._wgrad_n(L)
         g = self.fp.grad(L.name + ".w").view(-1)
@@ -580,9 +606,6 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
             sl, S = self.wslab[L.name]
             ops.gemm(dy, True, x[:, :n], True, None, False, None, None, sl, S,
                      ldc32=L.wcols, csum_col=csum)
-            if not self._opt_sums_slabs:      # else: partials summed by the optimizer
-                m = L.out * L.wcols
-                return lambda: ops.reduce_rows(sl, S, m, m, g, False, 1.0)
         else:
             ops.gemm(dy, True, x[:, :n], True, None, False, None, None, g, 1,
                      ldc32=L.wcols, csum_col=csum)
@@ -823,20 +846,15 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
         interaction / cross backward: the embedding grads exist without them
         (their all-to-all, or on one GPU the embedding update, runs meanwhile)."""
         if self._defer_top_wgrad:
-            # independent GEMMs: issued in pairs (the slab reduces after them)
-            fins = []
+            # independent GEMMs: issued in pairs
             with ops.gemm_batch(self._pair_bwd):
                 for i in reversed(range(len(self.top_layers))):
-                    fins.append(self._wgrad_gemm(self.top_layers[i], self.top_in[i],
-                                                 self.top_grad[i]))
+                    self._wgrad_gemm(self.top_layers[i], self.top_in[i], self.top_grad[i])
                 for i in reversed(range(len(self.dcn_u))):
                     dy, _ = self._dcn_bufs(i)
-                    fins.append(self._wgrad_gemm(self.dcn_u[i], self.dcn_h[i], dy))
-            for f in fins:
-                if f is not None:
-                    f()
+                    self._wgrad_gemm(self.dcn_u[i], self.dcn_h[i], dy)
             for i in reversed(range(len(self.dcn_u))):
-                self._dcn_wgrad_v(i)          # (one shared slab off one GPU)
+                self._dcn_wgrad_v(i)
 
     def _s_bottom_bwd(self):
         for i in reversed(range(len(self.bottom_layers))):
@@ -850,7 +868,16 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
     # cross layers) right after the top backward, overlapping the bottom MLP
     # backward and the embedding update; the small bottom MLP after its
     # backward.
+    def _reduce_slabs(self, lo: int, hi: int):
+        """Sum the split-K slabs of the weight grads in flat range [lo, hi)
+        into ``fp.g`` (one launch for all of them; the layers are the same
+        every step, so staged graphs and eager stages issue the same work)."""
+        mine = [(sl, S, g) for off, sl, S, g in self._slab_sums if lo <= off < hi]
+        if mine:
+            ops.slab_reduce(mine)
+
     def _ar_issue(self, lo: int, hi: int):
+        self._reduce_slabs(lo, hi)
         g = self.fp.g[lo:hi]
         if self.cfg.dense_comm == "bf16":
             if getattr(self, "_g16", None) is None:
@@ -885,6 +912,8 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
                 setattr(self, name, None)
 
     def _s_dense_update(self):
+        if self.world == 1:
+            self._reduce_slabs(0, self.fp.g.numel())
         fp = self.fp
         ops.dense_optimizer(fp.p, fp.g, fp.m, fp.v, fp.p_bf16, self.dense_opt, self.dense_hyper,
                             wd=self.cfg.dense_wd, segments=self._segments)
@@ -893,6 +922,8 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
         """The fused dense optimizer over flat elements [lo, hi) (the same
         elementwise update as _s_dense_update restricted to a range)."""
         fp = self.fp
+        if self.world == 1:
+            self._reduce_slabs(lo, hi)
         segs = [(st - lo, sl, S) for st, sl, S in self._segments if lo <= st < hi]
         sl = slice(lo, hi)
         ops.dense_optimizer(fp.p[sl], fp.g[sl], fp.m[sl] if fp.m is not None else None,
@@ -905,9 +936,16 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
         """One training step on the batch in the static buffers."""
         if self.pipeline and not self._primed:
             raise RuntimeError("pipelined trainer: call prime(first batch) before step()")
+        self._rw_resolve()
+        self._use_gemm_policy()
         if self.graph == "streams":
             self._ms_step()
         elif self.graph == "mstreams":
+            if self.emb.layout_version != self._graph_layout:
+                # a captured buffer was reallocated (row-wise capacity grown
+                # here, or by an eager forward such as predict()): re-capture
+                # before replaying, keeping the staged next batch
+                self._mr_recapture()
             self._mr_step()
         elif isinstance(self.graph, list):
             self._staged_step()
@@ -917,9 +955,17 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
             self._forward_backward()
         self.steps += 1
 
+    def _use_gemm_policy(self):
+        if self._gemm_pol is not None and ops.gemm_policy(-1) != self._gemm_pol:
+            ops.gemm_policy(self._gemm_pol)
+
     def _staged_step(self):
         self._on_side = False
-        eager = False
+        # a captured buffer reallocated before this step (lagged row-wise
+        # growth, or an eager forward such as predict() growing the capacity)
+        # or inside one of its exchange stages: the compute stages run eagerly
+        # until the end of the step, then the stages are re-captured
+        eager = self.emb.layout_version != self._graph_layout
         for kind, item in self.graph:
             if kind in ("c", "e"):
                 g, fns = item
@@ -947,10 +993,12 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
         assert self.device.type == "cuda"
         if not self.emb.graph_capturable:
             return
+        self._use_gemm_policy()
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(warmup):
+                self._rw_resolve()
                 self._forward_backward()
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
@@ -1011,6 +1059,7 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
     def pop_loss(self) -> float:
         """Mean training loss since the last call (one device->host read);
         also raises (on every rank) if a row-wise exchange dropped lookups."""
+        self._rw_resolve()
         self.sync_streams()
         self.emb.check_overflow()
         v = float(self.loss_sum.item())
@@ -1022,6 +1071,7 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
         id / pooled-embedding exchanges and the side stream, so the static
         buffers can be reused (eval); ``prime`` restarts the pipeline."""
         if self.pipeline:
+            self._rw_resolve()
             self.emb.ids_exchange_wait()
             if self.emb._pending is not None:
                 self.emb.forward_wait()
@@ -1032,6 +1082,7 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
     def predict(self) -> torch.Tensor:
         """Forward only on the static batch; returns logits [B] (fp32)."""
         self.sync_streams()
+        self._use_gemm_policy()
         cfg = self.cfg
         self.emb.forward(self.ids)
         self._s_bottom_fwd()
@@ -1063,6 +1114,40 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
         if self.fp.v is not None:
             d["v"] = self.fp.v
         return d
+
+    def replicated_state(self):
+        """name -> tensor of the training state every rank holds an identical
+        copy of: dense parameters, their moments, the step counters and the
+        replicated (data-parallel) embedding tables with their optimizer
+        state (parallel/replicas.py checks them across ranks)."""
+        d = {f"dense.{k}": v for k, v in self.dense_state().items()}
+        if self.emb.dp_tables:
+            for k, v in self.emb.dp_store.state_dict().items():
+                if isinstance(v, torch.Tensor):
+                    d[f"emb.dp.{k}"] = v
+        return d
+
+    def heartbeat_stream(self):
+        """The stream whose work ends an issued step (None: the current one):
+        the M stream of the multi-rank step graphs, which waits every other
+        stream's previous step before it can finish the next."""
+        if self.graph == "mstreams" and self._mr is not None:
+            return self._mr["streams"]["M"]
+        return None
+
+    def progress(self) -> dict:
+        """Host-side view of the step pipeline (hang diagnostics)."""
+        r = {"rank": self.rank, "world": self.world, "steps_issued": self.steps,
+             "graph": self.graph if isinstance(self.graph, (str, type(None))) else "staged",
+             "pipeline": self.pipeline, "layout_version": self.emb.layout_version}
+        if self.emb.rw_tables:
+            r["rw_cap"] = self.emb.rw_cap
+            r["rw_grows"] = self.emb.rw_grows
+        if self._mr is not None:
+            # each per-stream event: has the work before its latest record
+            # completed (which stream is stuck)
+            r["stream_events_done"] = {k: ev.query() for k, ev in self._mr["events"].items()}
+        return r
 
     def load_dense_state(self, d):
         for k, v in self.dense_state().items():

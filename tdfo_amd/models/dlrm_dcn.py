@@ -44,13 +44,10 @@ class DCNMixin:
             ops.cross_bwd(dxo, x0, self.dcn_y[i], dy, acc, i != Lc - 1, i == 0)
             Uw = fp.bf16(u.name + ".w")
             # U's weight grad and dgrad (both read dy): one paired launch
-            fin = None
             with ops.gemm_batch(self._pair_bwd and not self._defer_top_wgrad):
                 if not self._defer_top_wgrad:
-                    fin = self._wgrad_gemm(u, self.dcn_h[i], dy)
+                    self._wgrad_gemm(u, self.dcn_h[i], dy)
                 ops.gemm(dy, False, Uw[:, :u.in_k], True, None, False, None, dh, None, 1)
-            if fin is not None:
-                fin()
             # V's weight grad and dgrad (both read dh): one paired launch
             with ops.gemm_batch(self._pair_bwd and not self._defer_top_wgrad
                                 and f"dcn{i}.v" in self.wslab):
@@ -72,7 +69,7 @@ class DCNMixin:
 
     def _dcn_wgrad_v(self, i: int):
         """dV_i = dh_i^T x_i (split-K partials summed by the optimizer on one
-        GPU, reduced here otherwise)."""
+        GPU, with their all-reduce bucket otherwise: DLRMTrainer._reduce_slabs)."""
         _, dh = self._dcn_bufs(i)
         Wd = self.top_real
         if f"dcn{i}.v" in self.wslab:

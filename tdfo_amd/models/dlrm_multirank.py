@@ -50,13 +50,14 @@ class MultiRankStreamsMixin:
     when ``_mr_ok()``)."""
 
     def _mr_ok(self) -> bool:
-        """Pipelined with the lookup in the tail, every exchange enqueue-only
-        (native RCCL or loopback), and no host read inside the step (the
-        row-wise capacity check is one)."""
+        """Pipelined with the lookup in the tail and every exchange
+        enqueue-only (native RCCL or loopback). Row-wise tables qualify: their
+        capacity check is lagged (no host read inside the step; the host reads
+        the need the previous replay published when it issues the next)."""
         return (self.world > 1 and self.cfg.stream_graphs and self._pipe_lookup
                 and getattr(self.comm, "capturable", False)
                 and getattr(self.dcomm, "capturable", False)
-                and not (self.emb.rw_tables and self.emb.rw_dynamic))
+                and (not (self.emb.rw_tables and self.emb.rw_dynamic) or self._rw_lagged))
 
     def _mr_drain(self):
         """Complete every exchange left in flight by eager stages (prime(),
@@ -89,7 +90,8 @@ class MultiRankStreamsMixin:
             emb.stage_bwd_update(hyper, dp=not dp_dense)
 
         def ec_b1():
-            emb.stage_fwd_ids_exchange()
+            # (row-wise need published on D, right after the bucketize)
+            emb.stage_fwd_ids_exchange(lagged=self._rw_lagged, publish=False)
 
         def ec_b2():
             # (replicated tables with a dense update: looked up on D, right
@@ -118,17 +120,29 @@ class MultiRankStreamsMixin:
             ec_b1()
             ec_b2()
 
+        def d_a():
+            # the next batch's all-reduced row-wise need to the host mailbox
+            # first (the host reads it when it issues the next step), then the
+            # bottom bucket and the replicated tables' ids
+            if self._rw_lagged:
+                emb.rw_publish_need(self.dcomm)
+            self._m_allreduce_start()
+            d_prep()
+
         return {"M1": self._s_bottom_fwd, "M2": m2, "M4": m4,
                 "M3": self._s_top_wgrad if self._defer_top_wgrad else None,
                 "D0": emb.stage_bwd_prepare, "Dp": dp_a,
-                "Da": lambda: (self._m_allreduce_start(), d_prep()),
+                "Da": d_a,
                 "Db": d_b, "EC1": lambda: emb.backward_start(dp=False),
                 "ECub": lambda: (ec_upd(), ec_b())}
 
-    def _mr_capture(self):
+    def _mr_capture(self, restage: bool = True):
+        """``restage`` False (re-capture between steps): keep the staging
+        buffers and the next batch already staged in them."""
         assert self.device.type == "cuda"
         dev = self.device
-        self._stg = (self.x0.clone(), self.ids.clone(), self.label.clone())
+        if restage or self._stg is None:
+            self._stg = (self.x0.clone(), self.ids.clone(), self.label.clone())
         self._mr_drain()
         torch.cuda.synchronize()
         # (default priority: a high-priority M and/or EC stream ran the
@@ -216,7 +230,7 @@ class MultiRankStreamsMixin:
                     "launched": False, "names": names}
         # the capture ran nothing: the batch handed in before it is the one
         # the first replay loads
-        if self._next is not None:
+        if restage and self._next is not None:
             d, i, l = self._next
             sx, si, sl = self._stg
             ops.batch_load(d, sx, i, si, l, sl)
@@ -248,7 +262,16 @@ class MultiRankStreamsMixin:
         for k in ("M", "D", "EC"):
             with torch.cuda.stream(s[k]):
                 g[k].replay()
+        if self._rw_lagged:
+            self.emb.rw_note_replay()           # D published the next batch's need
         mr["launched"] = True
+
+    def _mr_recapture(self):
+        """Re-capture between two steps (a captured buffer was reallocated),
+        keeping the next batch the caller already staged."""
+        self.sync_streams()
+        torch.cuda.synchronize()
+        self._mr_capture(restage=False)
 
     def _mr_sync(self):
         cur = torch.cuda.current_stream()

@@ -137,10 +137,10 @@ def gemm_pairing(v: int = -1) -> int:
 
 
 def gemm_policy(p: int = -1) -> int:
-    """GEMM tile-shape policy of the native library (0 auto, 1-4 one kernel
-    forced: 2-stage, deep, ping-pong, 256x128; 5 DCN-v2: 256x128 tiles for
-    every GEMM without column sums except the long-K deep ones) -- was: 0 auto, 1 128x128 tiles
-    only, 2 256x128 tiles only; p < 0 only reads it. Returns the previous one."""
+    """GEMM tile-shape policy of the native library (process-global): 0 auto,
+    1-4 one kernel forced (2-stage, deep, ping-pong, 256x128), 5 DCN-v2
+    (256x128 tiles for every GEMM without column sums except the long-K deep
+    ones). p < 0 only reads it. Returns the previous one."""
     return int(_native().gemm_policy(p))
 
 
@@ -431,6 +431,22 @@ def reduce_rows(inp, rows, n, ld, out, accumulate=False, scale=1.0):
         _native().reduce_rows(inp, rows, n, ld, out, accumulate, scale)
     else:
         ref.reduce_rows(inp, rows, n, ld, out, accumulate, scale)
+
+
+def slab_reduce(segs):
+    """segs: [(slabs, S, out)]: out = sum of the S consecutive out-sized fp32
+    slabs in ``slabs`` (split order), every segment in one launch."""
+    if not segs:
+        return
+    if _gpu(segs[0][0]):
+        for i in range(0, len(segs), 16):
+            part = segs[i:i + 16]
+            _native().slab_reduce([x[0] for x in part], [int(x[1]) for x in part],
+                                  [x[2] for x in part])
+    else:
+        for sl, S, out in segs:
+            n = out.numel()
+            out.view(-1).copy_(sl.view(-1)[:S * n].view(S, n).sum(0))
 
 
 def head_reduce(part, nparts, K, grad, loss_acc, bumps=()):

@@ -444,16 +444,28 @@ class _nullctx:
 
 
 _NATIVE: dict = {}
+_TWINS: dict = {}
 
 
 def dense_comm_for(comm: Comm) -> Comm:
     """A second communicator over the same ranks for the dense-gradient
     all-reduces, where collectives are stream-ordered enqueues (native RCCL:
-    a new communicator, created collectively here; loopback: a twin), so
-    they run concurrently with the embedding exchanges on their own stream.
-    Other layers (c10d / gloo) share ``comm``."""
+    a new communicator, created collectively here the first time and cached
+    per communicator, so trainers built one after another share it; loopback:
+    a twin), so they run concurrently with the embedding exchanges on their
+    own stream. Other layers (c10d / gloo) share ``comm``.
+
+    Two communicators are deadlock-free here because their collectives are
+    issued in one fixed order on every rank: each communicator's collectives
+    sit on one stream (embedding exchanges on EC, dense all-reduces on D),
+    inside graphs every rank captured from the same code and launches in the
+    same order (models/dlrm_multirank.py); the staged / eager paths issue both
+    from one host thread in the same stage order on every rank."""
     if isinstance(comm, RcclComm):
-        return RcclComm(comm.group, comm.device)
+        twin = _TWINS.get(id(comm))
+        if twin is None or twin.h is None:
+            twin = _TWINS[id(comm)] = RcclComm(comm.group, comm.device)
+        return twin
     if isinstance(comm, LoopbackComm):
         return LoopbackComm(comm.world, comm.rank, comm.device, comm.link_gbps, comm.latency_us)
     return comm
@@ -477,8 +489,9 @@ def as_comm(group=None) -> Comm:
 
 
 def release_native():
-    """Destroy the cached native communicators (before the process group;
-    ``dense_comm_for`` twins live until the process exits)."""
-    for c in _NATIVE.values():
+    """Destroy the cached native communicators and their ``dense_comm_for``
+    twins (before the process group)."""
+    for c in list(_TWINS.values()) + list(_NATIVE.values()):
         c.close()
+    _TWINS.clear()
     _NATIVE.clear()

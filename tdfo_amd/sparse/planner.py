@@ -57,7 +57,8 @@ class TableShard:
     table: int
     kind: str                      # table_wise | row_wise | column_wise | data_parallel
     ranks: List[int]
-    row_blocks: List[int] = field(default_factory=list)   # row_wise: rows per rank
+    row_blocks: List[int] = field(default_factory=list)   # row_wise: rows held per rank
+    #   (round-robin ownership: rank r holds rows r, r + W, r + 2W, ...)
     col_blocks: List[int] = field(default_factory=list)   # column_wise: cols per rank
 
 
@@ -148,8 +149,11 @@ def plan_sharding(tables: Sequence[TableConfig], world_size: int, optim: EmbOpti
 
     def row_wise(t: int):
         rows = tables[t].num_embeddings
-        blk = -(-rows // W)                  # owner(id) = id // blk
-        blocks = [max(0, min(blk, rows - r * blk)) for r in range(W)]
+        # rows dealt round-robin: owner(id) = id mod W, local row id div W, so
+        # rank r holds ceil((rows - r) / W) rows (row_blocks, also written to
+        # checkpoint manifests); every rank allocates the largest share
+        blk = -(-rows // W)
+        blocks = [len(range(r, rows, W)) for r in range(W)]
         per_row = _mem_per_row(tables[t].embedding_dim, optim)
         for r in range(W):
             mem[r] += (blk + 1) * per_row   # padded block + scratch row (every rank)

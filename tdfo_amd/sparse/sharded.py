@@ -246,6 +246,7 @@ class ShardedEmbeddingBags:
             self.rw_overflow = torch.zeros(2, dtype=torch.int32, device=self.device)
             self.rw_dynamic = W > 1          # exact capacity check before every exchange
             self.rw_grows = 0
+            self.rw_lag_reads = 0
             self.rw_starts = torch.zeros(W * (self.nrw * B + 1), dtype=torch.int32,
                                          device=self.device)
             bf_ = bf
@@ -356,6 +357,8 @@ class ShardedEmbeddingBags:
         # bumped whenever a buffer captured into a hipGraph is reallocated
         # (row-wise capacity growth): the trainer re-captures its graphs
         self.layout_version = 0
+        self._rw_mbox = None
+        self._rw_lag_pending = False
 
     def alias_pooled(self, out: torch.Tensor, d_out: torch.Tensor, col0: int) -> bool:
         """One rank, table-wise tables only: pool straight into the consumer's
@@ -424,12 +427,90 @@ class ShardedEmbeddingBags:
         need = int(need.item())
         if need <= self.rw_cap:
             return
+        self._rw_grow(need)
+        self._rw_bucketize(self._rw_ids)
+
+    def _rw_grow(self, need: int):
         cap = min(self.rw_n, int(need * 1.25) + 256)
         self._rw_alloc(cap)
         self.rw_grows += 1
         self.layout_version += 1
         self.rw_overflow[:1].zero_()          # this batch's overflow is undone by the re-bucketize
+
+    # -- lagged capacity check (pipelined trainers: the batch bucketized and
+    # exchanged in step i's tail is consumed by step i+1). Step i publishes the
+    # all-reduced per-owner need to a host mailbox (no host wait, capturable);
+    # the host reads it when it issues step i+1 -- the device produced it long
+    # before -- and only if a segment overflowed does it grow the capacity and
+    # redo that batch's row-wise exchange (``rw_redo``) before step i+1 runs.
+    # Every rank reads the same MAX, so all take the same branch.
+    def _rw_mailbox(self):
+        if self._rw_mbox is None:
+            from ..parallel.mailbox import HostMailbox
+            self._rw_mbox = HostMailbox(1, self.device)
+        return self._rw_mbox
+
+    def rw_publish_need(self, comm=None):
+        """All ranks' largest per-owner count of the batch bucketized last
+        (in-place MAX all-reduce on ``comm``, default the exchange comm) to the
+        host mailbox. Under stream capture the replays publish; the trainer
+        counts them (``rw_note_replay``)."""
+        if not (self.rw_tables and self.rw_dynamic):
+            return
+        need = self.rw_overflow[1:2]
+        if self.world > 1:
+            (comm or self.comm).all_reduce(need, "max")
+        self._rw_mailbox().publish(need)
+        if self.device.type != "cuda" or not torch.cuda.is_current_stream_capturing():
+            self._rw_lag_pending = True
+
+    def rw_note_replay(self):
+        """A graph holding one ``rw_publish_need`` was launched."""
+        self._rw_mailbox().note_launch()
+        self._rw_lag_pending = True
+
+    def rw_resolve_need(self) -> bool:
+        """Read the latest published need; if a segment overflowed, wait for
+        the device, grow the capacity and return True -- the caller then redoes
+        the row-wise exchange of that batch (``rw_redo``) before consuming it
+        and re-captures its graphs (``layout_version`` changed)."""
+        if not self._rw_lag_pending:
+            return False
+        self._rw_lag_pending = False
+        need = self._rw_mailbox().read()
+        self.rw_lag_reads += 1
+        if need <= self.rw_cap:
+            return False
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)    # in-flight kernels hold the old buffers
+        self._rw_grow(need)
+        return True
+
+    def rw_redo(self):
+        """The row-wise part of the forward exchange of the batch bucketized
+        last (its ids are still in the buffer ``stage_fwd_prep`` saw), into the
+        grown segments: bucketize, id all-to-all, owner pooling, reduce-scatter
+        into this batch's row-wise slots of ``recv``. Synchronous."""
+        from .. import ops
+        W = self.world
+        # the first exchange's collectives may still be in flight (async
+        # handles, e.g. gloo's worker threads): they must land before the
+        # redo overwrites their outputs ("forward_wait" then only assembles)
+        self.ids_exchange_wait()
+        for w in self._pending or ():
+            w.wait()
+        self._pending = None
         self._rw_bucketize(self._rw_ids)
+        if W > 1:
+            self.comm.all_to_all(self.rw_recv, self.rw_send)
+        out = self.rw_pbuf if W > 1 else self._rw_region(self.recv)
+        ops.rw_pool(self.rw_store.weight, self.rw_recv, self.rw_meta, self.nrw, W, self.B,
+                    self.rw_cap, self.mean, self.rw_starts, out, self.rw_width)
+        if W > 1:
+            dst = self.rw_rs32 if self.rw_rs32 is not None else self._rw_region(self.recv)
+            self.comm.reduce_scatter(dst, self.rw_pbuf)
+            if self.rw_rs32 is not None:
+                ops.cast_bf16(self.rw_rs32, self._rw_region(self.recv))
 
     def _rw_region(self, buf):
         base = sum(self.tw_recv_sizes)
@@ -517,10 +598,15 @@ class ShardedEmbeddingBags:
             self._rw_ids = ids
             self._rw_bucketize(ids)
 
-    def stage_fwd_ids_exchange(self, async_op: bool = False):
+    def stage_fwd_ids_exchange(self, async_op: bool = False, lagged: bool = False,
+                               publish: bool = True):
         """Id exchange (input dist). async_op: the collectives are left in
         flight (the pipelined trainer overlaps them with the previous step's
-        dense update) until ``ids_exchange_wait``."""
+        dense update) until ``ids_exchange_wait``. lagged: the row-wise
+        capacity is checked one step later (``rw_publish_need`` here unless
+        ``publish`` is False -- the caller publishes elsewhere -- and
+        ``rw_resolve_need`` before the batch is consumed) instead of by a host
+        read before the exchange."""
         W = self.world
         works = []
         if self.dp_tables and W > 1 and not self.dp_dense:
@@ -534,8 +620,10 @@ class ShardedEmbeddingBags:
                                               [self.cw_recv_count] * W, self.cw_send_counts,
                                               async_op=async_op))
         if W > 1 and self.rw_tables:
-            if self.rw_dynamic:
+            if self.rw_dynamic and not lagged:
                 self._rw_check_capacity()
+            elif self.rw_dynamic and publish:
+                self.rw_publish_need()
             works.append(self.comm.all_to_all(self.rw_recv, self.rw_send, async_op=async_op))
         self._ids_works = [w for w in works if w is not None] if async_op else []
 

@@ -89,11 +89,16 @@ class StepLoop:
     """Drive ``trainer`` (a ``DLRMTrainer``) from ``source``, which must be
     positioned at batch ``start`` (the step about to run)."""
 
-    def __init__(self, trainer, source, start: int = 0):
+    def __init__(self, trainer, source, start: int = 0, watchdog=None, beat_every: int = 8):
+        """``watchdog``: a ``utils.watchdog.StepWatchdog`` -- every
+        ``beat_every`` steps (and at the end of each ``run``) a heartbeat is
+        enqueued behind the step, and the host must keep issuing steps."""
         self.tr = trainer
         self.src = source
         self.step_index = int(start)
         self._primed = False
+        self.wd = watchdog
+        self.beat_every = max(1, int(beat_every))
 
     def _streams(self):
         return None if self.tr.pipeline else self.tr.input_streams()
@@ -120,7 +125,18 @@ class StepLoop:
         if tr.pipeline and not self._primed:
             self.prime()
         on_dev = tr.device.type == "cuda"
-        for _ in range(n):
+        wd = self.wd
+        if wd is None:
+            self._run(n, on_dev)
+            return
+        with wd.active():
+            self._run(n, on_dev)
+            if n:
+                wd.beat(tr.heartbeat_stream(), self.step_index)
+
+    def _run(self, n: int, on_dev: bool):
+        tr, wd = self.tr, self.wd
+        for k in range(n):
             batch, slot = self._next()
             if tr.pipeline:
                 tr.set_next_batch(*batch)
@@ -130,6 +146,8 @@ class StepLoop:
             tr.step()
             self._release(slot)
             self.step_index += 1
+            if wd is not None and (self.step_index % self.beat_every == 0) and k + 1 < n:
+                wd.beat(tr.heartbeat_stream(), self.step_index)
 
     def close(self):
         if hasattr(self.src, "close"):

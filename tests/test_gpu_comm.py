@@ -111,8 +111,14 @@ def _trainer(whole: bool, W: int, strategy: str):
     return tr, rows, cfg
 
 
-@pytest.mark.parametrize("strategy", ["table_wise", "auto", "column_wise", "data_parallel"])
-def test_stream_graphs_match_staged(strategy):
+@pytest.mark.parametrize("strategy,skew", [("table_wise", False), ("auto", False),
+                                           ("column_wise", False), ("data_parallel", False),
+                                           ("row_wise", False), ("row_wise", True)])
+def test_stream_graphs_match_staged(strategy, skew):
+    """Row-wise tables run on the stream graphs with the lagged capacity
+    check; ``skew``: the batches after the capture carry only ids that are
+    multiples of W (one owner gets every row-wise id), so the capacity grows
+    between two replays (redo of that batch's exchange, re-capture)."""
     from tdfo_amd.data.synthetic import SyntheticCriteo
 
     W = 4
@@ -121,6 +127,8 @@ def test_stream_graphs_match_staged(strategy):
         tr, rows, cfg = _trainer(whole, W, strategy)
         data = SyntheticCriteo(rows, 256, pooling=cfg.pooling_factors(), device="cuda:0", seed=9)
         batches = [data.next() for _ in range(9)]
+        if skew:
+            batches = batches[:3] + [(d, i - i % W, y) for d, i, y in batches[3:]]
         tr.prime(*batches[0])
         for i in range(2):
             tr.set_next_batch(*batches[i + 1])
@@ -131,6 +139,10 @@ def test_stream_graphs_match_staged(strategy):
             tr.set_next_batch(*batches[i + 1])
             tr.step()
         torch.cuda.synchronize()
+        assert (tr.graph == "mstreams") == whole, tr.graph      # (still, after any growth)
+        if strategy == "row_wise":
+            assert tr.emb.rw_lag_reads >= 6
+            assert (tr.emb.rw_grows > 0) == skew, tr.emb.rw_grows
         loss = tr.pop_loss()
         tr.drain()
         torch.cuda.synchronize()

@@ -89,3 +89,16 @@ def test_plan_data_parallel_owner_partitions_big_tables(world):
     assert min(rep.mem_bytes) > 90 * GiB
     one = plan_sharding(cfg.tables(), 1, o, strategy="data_parallel")
     assert all(s.kind == "data_parallel" for s in one.shards)
+
+
+def test_row_wise_row_blocks_are_round_robin_shares():
+    """Row-wise ownership is id mod W: rank r holds ceil((rows - r) / W) rows,
+    and the recorded row_blocks (checkpoint manifests) say so."""
+    from tdfo_amd.sparse.planner import plan_sharding
+    from tdfo_amd.sparse.tables import EmbOptimConfig, TableConfig
+
+    tabs = [TableConfig("a", 10, 16, ["a"]), TableConfig("b", 3, 16, ["b"])]
+    p = plan_sharding(tabs, 4, EmbOptimConfig("rowwise_adagrad"), strategy="row_wise")
+    assert p.shards[0].row_blocks == [3, 3, 2, 2]
+    assert p.shards[1].row_blocks == [1, 1, 1, 0]
+    assert all(sum(s.row_blocks) == t.num_embeddings for s, t in zip(p.shards, tabs))

@@ -99,7 +99,9 @@ def test_sharded_embedding_fwd_bwd(strategy, world, dp_dense):
 
 def _dlrm_worker(rank, world, B, steps, strategy, emb_opt="rowwise_adagrad", rw_comm="fp32",
                  pipeline=False, dense_comm="fp32", dist="uniform", alpha=1.05, rw_capacity=1.25,
-                 pipe_lookup=True):
+                 pipe_lookup=True, skew_from=None):
+    """skew_from: batches from this index on carry only even ids (every
+    row-wise id of a 2-rank job then goes to owner 0)."""
     from tdfo_amd.data.synthetic import SyntheticCriteo
     from tdfo_amd.models.dlrm import DLRMConfig, DLRMTrainer
     from tdfo_amd.parallel.dist import get_info
@@ -128,6 +130,8 @@ def _dlrm_worker(rank, world, B, steps, strategy, emb_opt="rowwise_adagrad", rw_
                 label[rank * B:(rank + 1) * B].clone())
 
     batches = [local(data.next()) for _ in range(steps + 1)]
+    if skew_from is not None:
+        batches = [(d, i - i % 2 if k >= skew_from else i, y) for k, (d, i, y) in enumerate(batches)]
     if tr.pipeline:
         tr.prime(*batches[0])
     for i in range(steps):
@@ -143,6 +147,8 @@ def _dlrm_worker(rank, world, B, steps, strategy, emb_opt="rowwise_adagrad", rw_
             tabs[t] = ((r[0].start, r[0].stop, r[0].step), tr.emb.table_cols(t)[0], r[1].clone())
     grows = tr.emb.rw_grows if tr.emb.rw_tables else 0
     tr.pop_loss()                               # raises on every rank if a lookup was dropped
+    if skew_from is not None:
+        return tr.fp.p.clone(), tabs, grows, tr.emb.rw_lag_reads if tr.emb.rw_tables else 0
     return tr.fp.p.clone(), tabs, grows
 
 
@@ -232,3 +238,31 @@ def test_dlrm_zipf_ids_match_single_process(strategy, world, alpha):
         for t, (lo, c0, w) in tabs.items():
             ref = tabs1[t][2][slice(*lo)][:, c0:c0 + w.shape[1]]
             assert torch.allclose(w, ref, atol=2e-4), (rank, t, (w - ref).abs().max())
+
+
+def test_dlrm_lagged_rw_growth_is_exact():
+    """Pipelined row-wise exchanges check their capacity one step late (the
+    need is published in step i's tail and read when step i+1 is issued):
+    when the ids turn skewed after the prime (every id even -> one owner), the
+    lagged check grows the capacity and redoes that batch's exchange before it
+    is consumed -- parameters and tables equal the unpipelined run (capacity
+    checked by a host read before every exchange) bit for bit, and one
+    process up to fp32 association."""
+    B, steps = 64, 5
+    plain = run_distributed(_dlrm_worker, 2, B, steps, "row_wise", "rowwise_adagrad", "fp32", False,
+                            "fp32", "uniform", 1.05, 1.25, True, 2)
+    lag = run_distributed(_dlrm_worker, 2, B, steps, "row_wise", "rowwise_adagrad", "fp32", True,
+                          "fp32", "uniform", 1.05, 1.25, True, 2)
+    single = run_distributed(_dlrm_worker, 1, 2 * B, steps, "table_wise", "rowwise_adagrad", "fp32",
+                             False, "fp32", "uniform", 1.05, 1.25, True, 2)[0]
+    for rank in range(2):
+        p0, tabs0, g0, _ = plain[rank]
+        p1, tabs1, g1, reads = lag[rank]
+        assert g0 > 0 and g1 > 0 and reads >= steps - 1, (g0, g1, reads)
+        assert torch.equal(p0, p1), (rank, (p0 - p1).abs().max())
+        for t in tabs0:
+            assert torch.equal(tabs0[t][2], tabs1[t][2]), (rank, t)
+        assert torch.allclose(p1, single[0], atol=2e-4)
+        for t, (lo, c0, w) in tabs1.items():
+            ref = single[1][t][2][slice(*lo)][:, c0:c0 + w.shape[1]]
+            assert torch.allclose(w, ref, atol=2e-4), (rank, t)
