@@ -51,6 +51,13 @@ def parse(argv=None):
     ap.add_argument("--sharding", default="auto",
                     choices=["auto", "table_wise", "row_wise", "column_wise", "data_parallel",
                              "replicated"])
+    ap.add_argument("--opt-placement", default=None,
+                    choices=["one_pass", "split_main", "split_emb"],
+                    help="one GPU: where the dense optimizer runs in the per-stream step "
+                         "(DLRMConfig.opt_placement; default: the model's)")
+    ap.add_argument("--defer-wgrad", default=None, choices=["0", "1"],
+                    help="top / cross weight grads after the interaction / cross backward "
+                         "(DLRMConfig.defer_wgrad; default: when N > 1)")
     ap.add_argument("--dense-comm", default="fp32", choices=["fp32", "bf16"],
                     help="N > 1: wire format of the dense-gradient all-reduce")
     ap.add_argument("--no-pipeline", action="store_true",
@@ -65,10 +72,10 @@ def parse(argv=None):
                          "and kernels, each collective replaced by device copies of the same "
                          "byte count (parallel/comm.py LoopbackComm); reports device ms/step, "
                          "host issue us/step and the collective volume (not the headline)")
-    ap.add_argument("--emulate-rank", default="0", metavar="K|max",
-                    help="--emulate-world: the rank to emulate, or 'max': every rank of the "
-                         "plan in turn, reporting the slowest (a synchronous step runs at the "
-                         "pace of its slowest rank)")
+    ap.add_argument("--emulate-rank", default="0", metavar="K[,K...]|max",
+                    help="--emulate-world: the rank(s) to emulate, in turn, or 'max': every "
+                         "rank of the plan; the slowest is reported (a synchronous step runs "
+                         "at the pace of its slowest rank)")
     ap.add_argument("--emulate-link-gbps", type=float, default=None,
                     help="--emulate-world: modelled per-rank xGMI injection bandwidth (GB/s); "
                          "each emulated collective also holds the comm stream for its link "
@@ -138,12 +145,14 @@ def self_launch(args, argv) -> int:
 
 def _cfg(args, rows, pipe):
     from tdfo_amd.models.dlrm import MLPERF_MULTIHOT, DLRMConfig
+    kw = dict(table_rows=list(rows), sharding=args.sharding, pipeline=pipe,
+              dense_comm=args.dense_comm, stream_graphs=not args.no_stream_graphs,
+              opt_placement=args.opt_placement,
+              defer_wgrad=None if args.defer_wgrad is None else args.defer_wgrad == "1")
     if args.model == "dlrm":
-        return DLRMConfig(table_rows=list(rows), sharding=args.sharding, pipeline=pipe,
-                          dense_comm=args.dense_comm, stream_graphs=not args.no_stream_graphs)
-    return DLRMConfig(table_rows=list(rows), interaction="dcn", pooling=list(MLPERF_MULTIHOT),
-                      top=[1024, 1024, 512, 256, 1], sharding=args.sharding, pipeline=pipe,
-                      dense_comm=args.dense_comm, stream_graphs=not args.no_stream_graphs)
+        return DLRMConfig(**kw)
+    return DLRMConfig(interaction="dcn", pooling=list(MLPERF_MULTIHOT),
+                      top=[1024, 1024, 512, 256, 1], **kw)
 
 
 def measure(args, info, cfg, world: int, group, rank: int) -> dict:
@@ -241,7 +250,8 @@ def emulate(args, info, rows):
     W = args.emulate_world
     link = (args.emulate_link_gbps if args.emulate_link_gbps is not None
             else min(W - 1, 7) * LINK_GBS)
-    ranks = list(range(W)) if args.emulate_rank == "max" else [int(args.emulate_rank)]
+    ranks = (list(range(W)) if args.emulate_rank == "max" else
+             [int(x) for x in args.emulate_rank.split(",")])
     cfg = _cfg(args, rows, not args.no_pipeline)
     if args.data in ("host", "fresh"):
         cfg.ids_stream = False

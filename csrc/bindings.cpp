@@ -1063,6 +1063,32 @@ void reduce_rows(const Tensor& inp, int64_t rows, int64_t n, int64_t ld, const T
                     (float)scale, cur_stream());
 }
 
+void seg_copy(const Tensor& src, const Tensor& dst, const Tensor& chunks, int64_t src_n,
+              int64_t dst_n) {
+  check_dev(src, "src"); check_dev(dst, "dst"); check_dev(chunks, "chunks");
+  TORCH_CHECK(src.scalar_type() == at::kLong && dst.scalar_type() == at::kLong &&
+              chunks.scalar_type() == at::kLong && src.is_contiguous() && dst.is_contiguous() &&
+              chunks.is_contiguous() && chunks.dim() == 2 && chunks.size(1) == 3,
+              "seg_copy: contiguous int64 src / dst and int64 [n, 3] chunks");
+  // the chunk table was bounds-checked on the host against (src_n, dst_n)
+  TORCH_CHECK(src.numel() >= src_n && dst.numel() >= dst_n, "seg_copy: buffers smaller than "
+              "the extents the segment map was built for");
+  tdfo::seg_copy(src.data_ptr<int64_t>(), dst.data_ptr<int64_t>(), chunks.data_ptr<int64_t>(),
+                 (int)chunks.size(0), cur_stream());
+}
+
+void piece_copy(const Tensor& buf, const Tensor& pieces, int64_t B, int64_t w, int64_t extent) {
+  check_dev(buf, "buf"); check_dev(pieces, "pieces");
+  TORCH_CHECK(buf.scalar_type() == at::kBFloat16 && buf.is_contiguous() &&
+              pieces.scalar_type() == at::kLong && pieces.is_contiguous() && pieces.dim() == 2 &&
+              pieces.size(1) == 4 && w % 8 == 0 && aligned16(buf.data_ptr()),
+              "piece_copy: contiguous bf16 buffer, int64 [n, 4] pieces, w % 8 == 0");
+  // the piece table was bounds- and alignment-checked on the host against extent
+  TORCH_CHECK(buf.numel() >= extent, "piece_copy: buffer smaller than its piece table's extent");
+  tdfo::piece_copy_bf16(reinterpret_cast<uint16_t*>(buf.data_ptr()), pieces.data_ptr<int64_t>(),
+                        (int)pieces.size(0), (int)B, (int)w, cur_stream());
+}
+
 void slab_reduce(const std::vector<Tensor>& ins, const std::vector<int64_t>& splits,
                  const std::vector<Tensor>& outs) {
   TORCH_CHECK(!g_gemm_batch.on, "slab_reduce inside ops.gemm_batch");
@@ -1382,6 +1408,8 @@ TORCH_LIBRARY(tdfo, m) {
   m.def("reduce_rows(Tensor inp, int rows, int n, int ld, Tensor(a!) out, bool accumulate, float scale) -> ()");
   m.def("colsum(Tensor x, Tensor(a!) out, bool accumulate) -> ()");
   m.def("slab_reduce(Tensor[] slabs, int[] splits, Tensor(a!)[] outs) -> ()");
+  m.def("seg_copy(Tensor src, Tensor(a!) dst, Tensor chunks, int src_n, int dst_n) -> ()");
+  m.def("piece_copy(Tensor(a!) buf, Tensor pieces, int B, int w, int extent) -> ()");
   m.def("auc_hist(Tensor logits, Tensor labels, int nb, Tensor(a!) hist) -> ()");
   m.def("linear_xent(Tensor H, Tensor W, Tensor bias, Tensor labels, float eps, int ignore, "
         "Tensor(a!) dH, Tensor(b!) lossv, Tensor(c!)? dW, Tensor(d!)? db, Tensor(e!)? loss=None, "
@@ -1426,6 +1454,8 @@ TORCH_LIBRARY_IMPL(tdfo, CUDA, m) {
   m.impl("sort_pairs", sort_pairs);
   m.impl("cast_bf16", cast_bf16);
   m.impl("slab_reduce", slab_reduce);
+  m.impl("seg_copy", seg_copy);
+  m.impl("piece_copy", piece_copy);
   m.impl("head_bce", head_bce);
   m.impl("reduce_rows", reduce_rows);
   m.impl("head_reduce", head_reduce);

@@ -248,6 +248,14 @@ struct BumpArgs {
 void bump(const BumpArgs& a, hipStream_t s);
 void stamp(uint64_t* buf, int64_t* cnt, int seg, int nseg, int which, int64_t cap,
            hipStream_t s);
+// dst[chunk.dst_off + i] = src[chunk.src_off + i], i < chunk.len, for every
+// chunk of the device table chunks[nchunks][3] (one block per chunk)
+void seg_copy(const int64_t* src, int64_t* dst, const int64_t* chunks, int nchunks,
+              hipStream_t s);
+// pieces[p] = (src_off, src_ld, dst_off, dst_ld) (device, elements): B rows x w
+// bf16 (w % 8 == 0, 16-B aligned rows) copied within buf, all pieces in one launch
+void piece_copy_bf16(uint16_t* buf, const int64_t* pieces, int npieces, int B, int w,
+                     hipStream_t s);
 // host mailbox: host_word[slot] = (++seq[slot]) << 32 | (uint32) value[0]
 void host_publish(const int32_t* value, int32_t* seq, uint64_t* host_word, hipStream_t s);
 

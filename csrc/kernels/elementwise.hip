@@ -234,6 +234,55 @@ void stamp(uint64_t* buf, int64_t* cnt, int seg, int nseg, int which, int64_t ca
   TDFO_CHECK_HIP(hipGetLastError());
 }
 
+// Static segment permutation of an int64 buffer (the sharded engine's id
+// layouts: table-wise / column-wise send order, replicated tables' ids, the
+// all-gathered ids rank-major -> table-major): block b copies chunk b,
+// chunks[b] = (src_off, dst_off, len <= SEG_CHUNK), built once on the host.
+// Replaces a torch index_select (and its int64 index array read).
+__global__ __launch_bounds__(256) void seg_copy_kernel(const int64_t* __restrict__ src,
+                                                       int64_t* __restrict__ dst,
+                                                       const int64_t* __restrict__ chunks) {
+  const int64_t so = chunks[3 * blockIdx.x], d0 = chunks[3 * blockIdx.x + 1];
+  const int64_t len = chunks[3 * blockIdx.x + 2];
+  for (int64_t i = threadIdx.x; i < len; i += 256) dst[d0 + i] = src[so + i];
+}
+
+// Column-wise shards' row assembly: piece p moves a B x w bf16 block between
+// two strided views of one buffer (dst row b = buf + dst_off + b * dst_ld,
+// src likewise), 16 B per thread; every piece in one launch.
+__global__ __launch_bounds__(256) void piece_copy_kernel(uint16_t* buf, const int64_t* pieces,
+                                                         int npieces, int B, int w) {
+  const int g8 = w / 8;
+  const int64_t total = (int64_t)npieces * B * g8;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int g = (int)(i % g8);
+    const int64_t pb = i / g8;
+    const int p = (int)(pb / B);
+    const int64_t b = pb - (int64_t)p * B;
+    const int64_t* q = pieces + 4 * p;            // src_off, src_ld, dst_off, dst_ld
+    *(uint4*)(buf + q[2] + b * q[3] + g * 8) = *(const uint4*)(buf + q[0] + b * q[1] + g * 8);
+  }
+}
+
+void piece_copy_bf16(uint16_t* buf, const int64_t* pieces, int npieces, int B, int w,
+                     hipStream_t s) {
+  const int64_t total = (int64_t)npieces * B * (w / 8);
+  if (total <= 0) return;
+  int64_t blocks = (total + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(piece_copy_kernel, dim3(blocks), dim3(256), 0, s, buf, pieces, npieces, B,
+                     w);
+  TDFO_CHECK_HIP(hipGetLastError());
+}
+
+void seg_copy(const int64_t* src, int64_t* dst, const int64_t* chunks, int nchunks,
+              hipStream_t s) {
+  if (nchunks <= 0) return;
+  hipLaunchKernelGGL(seg_copy_kernel, dim3(nchunks), dim3(256), 0, s, src, dst, chunks);
+  TDFO_CHECK_HIP(hipGetLastError());
+}
+
 // Host mailbox (parallel/mailbox.py): one lane bumps the slot's device
 // sequence number and stores (seq << 32 | value) into host-mapped coherent
 // memory with ONE 64-bit system-scope vector store -- no fence, no L2

@@ -97,10 +97,13 @@ class DLRMConfig:
     #   pooled exchange in this step's tail (on the side stream)
     defer_wgrad: Optional[bool] = None             # top / cross weight grads after the
     #   interaction / cross backward (None: when W > 1, so the embedding-grad exchange
-    #   overlaps them; on one GPU the DCN-v2 update starved them: 2.606 vs 2.52 ms/step)
+    #   overlaps them; on one GPU the DCN-v2 update starved them: 2.606 vs 2.52 ms/step;
+    #   with opt_placement="split_emb" the top optimizer part waits for them in-graph)
     opt_placement: Optional[str] = None            # one GPU: "one_pass" (dense optimizer after
     #   the bottom backward; DLRM default) | "split_main" (top part first, beside the
-    #   embedding update; DCN-v2 default)
+    #   embedding update; DCN-v2 default) | "split_emb" (bottom part after the bottom
+    #   backward on the MLP stream, top part on the embedding stream right after the
+    #   embedding update, ahead of the next lookup the next top forward waits for)
     composed_graphs: Optional[bool] = None         # one GPU: chain each stream's graphs with
     #   in-graph event nodes (None: DLRM yes, DCN-v2 no)
     ids_stream: Optional[bool] = None              # one GPU, composed graphs: copy the next
@@ -242,8 +245,8 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
         self.cfg = cfg
         if cfg.dense_comm not in ("fp32", "bf16"):
             raise ValueError(f"dense_comm must be fp32 or bf16, got {cfg.dense_comm!r}")
-        if cfg.opt_placement not in (None, "one_pass", "split_main"):
-            raise ValueError(f"opt_placement must be one_pass or split_main, "
+        if cfg.opt_placement not in (None, "one_pass", "split_main", "split_emb"):
+            raise ValueError(f"opt_placement must be one_pass, split_main or split_emb, "
                              f"got {cfg.opt_placement!r}")
         if cfg.opt_placement is None:
             cfg.opt_placement = "split_main" if cfg.interaction == "dcn" else "one_pass"

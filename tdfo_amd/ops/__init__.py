@@ -433,6 +433,87 @@ def reduce_rows(inp, rows, n, ld, out, accumulate=False, scale=1.0):
         ref.reduce_rows(inp, rows, n, ld, out, accumulate, scale)
 
 
+class SegmentMap:
+    """A static permutation of an int64 buffer made of contiguous pieces
+    ``(src_off, dst_off, length)``: ``apply(src, dst)`` copies every piece in
+    one native launch on the GPU (seg_copy_kernel: one block per <= 4096-id
+    chunk, offsets from a device table built here once), or one index_select
+    on the CPU."""
+
+    CHUNK = 4096
+
+    def __init__(self, pieces, device):
+        self.device = torch.device(device)
+        pieces = [(int(a), int(b), int(n)) for a, b, n in pieces if int(n) > 0]
+        self.src_n = max([a + n for a, _, n in pieces], default=0)
+        self.dst_n = max([b + n for _, b, n in pieces], default=0)
+        self.n = sum(n for _, _, n in pieces)
+        if self.device.type == "cuda":
+            ch = []
+            for a, b, n in pieces:
+                for o in range(0, n, self.CHUNK):
+                    ch.append((a + o, b + o, min(self.CHUNK, n - o)))
+            self.chunks = torch.tensor(ch if ch else [[0, 0, 0]], dtype=torch.int64,
+                                       device=self.device).view(-1, 3)
+            self.nchunks = len(ch)
+        else:
+            idx = torch.zeros(self.dst_n, dtype=torch.int64)
+            for a, b, n in pieces:
+                idx[b:b + n] = torch.arange(a, a + n)
+            self.index = idx
+
+    def apply(self, src: torch.Tensor, dst: torch.Tensor):
+        if src.is_cuda:
+            if self.nchunks:
+                _native().seg_copy(src, dst, self.chunks, self.src_n, self.dst_n)
+        else:
+            torch.index_select(src, 0, self.index, out=dst[:self.dst_n])
+
+    @staticmethod
+    def from_index(index: torch.Tensor, device):
+        """The pieces of a gather index that is a union of contiguous runs."""
+        ix = index.to("cpu", torch.int64).view(-1)
+        pieces, start = [], 0
+        for i in range(1, ix.numel() + 1):
+            if i == ix.numel() or int(ix[i]) != int(ix[i - 1]) + 1:
+                pieces.append((int(ix[start]), start, i - start))
+                start = i
+        return SegmentMap(pieces, device)
+
+
+class PieceCopy:
+    """Static B x w block copies between strided views of one bf16 buffer,
+    pieces ``(src_off, src_ld, dst_off, dst_ld)`` in elements: one native
+    launch for all of them on the GPU (piece_copy_kernel), strided torch
+    copies on the CPU. ``reverse()`` swaps source and destination."""
+
+    def __init__(self, pieces, B: int, w: int, device):
+        self.pieces = [tuple(int(v) for v in p) for p in pieces]
+        self.B, self.w = int(B), int(w)
+        self.device = torch.device(device)
+        self.extent = max([max(a + (self.B - 1) * la, c + (self.B - 1) * lc) + self.w
+                           for a, la, c, lc in self.pieces], default=0)
+        if self.device.type == "cuda" and self.pieces:
+            ok = self.w % 8 == 0 and all(v % 8 == 0 for p in self.pieces for v in p)
+            if not ok:
+                raise ValueError("PieceCopy: offsets, strides and width must be multiples of 8")
+            self.table = torch.tensor(self.pieces, dtype=torch.int64, device=self.device)
+
+    def reverse(self) -> "PieceCopy":
+        return PieceCopy([(c, lc, a, la) for a, la, c, lc in self.pieces], self.B, self.w,
+                         self.device)
+
+    def apply(self, buf: torch.Tensor):
+        if not self.pieces:
+            return
+        if buf.is_cuda:
+            _native().piece_copy(buf, self.table, self.B, self.w, self.extent)
+            return
+        for a, la, c, lc in self.pieces:
+            buf.as_strided((self.B, self.w), (lc, 1), c).copy_(
+                buf.as_strided((self.B, self.w), (la, 1), a))
+
+
 def slab_reduce(segs):
     """segs: [(slabs, S, out)]: out = sum of the S consecutive out-sized fp32
     slabs in ``slabs`` (split order), every segment in one launch."""

@@ -139,6 +139,9 @@ class ShardedEmbeddingBags:
         self.tw_identity = bool(W == 1 and torch.equal(perm, torch.arange(perm.numel()))
                                 and len(order) == self.T)
         self.tw_perm = perm.to(self.device)
+        # the id permutes are static runs of the input: one native launch each
+        # (ops.SegmentMap) instead of an index_select
+        self.tw_map = ops.SegmentMap(self._runs(order), self.device)
         # owner-side virtual tables v = (src s, local table i)
         nv = W * len(mine)
         lens = []
@@ -189,6 +192,7 @@ class ShardedEmbeddingBags:
             self.cw_recv_count = sum(B * self.L[t] for t, _ in cmine)
             self.cw_perm = torch.cat([torch.arange(self.in_base[t], self.in_base[t] + B * self.L[t])
                                       for t in corder]).to(self.device)
+            self.cw_map = ops.SegmentMap(self._runs(corder), self.device)
             self.cw_send_ids = torch.empty(sum(self.cw_send_counts), dtype=torch.int64,
                                            device=self.device)
             self.cw_recv_ids = torch.empty(W * self.cw_recv_count, dtype=torch.int64,
@@ -275,6 +279,7 @@ class ShardedEmbeddingBags:
                              for t in dpt], seed=seed * 1000 + 777)        # same on all ranks
             self.dp_in_idx = torch.cat([torch.arange(self.in_base[t], self.in_base[t] + B * self.L[t])
                                         for t in dpt]).to(self.device)
+            self.dp_in_map = ops.SegmentMap(self._runs(dpt), self.device)
             self.dp_nid = int(self.dp_in_idx.numel())
 
             def bag_offsets(nb):
@@ -314,14 +319,17 @@ class ShardedEmbeddingBags:
                 self.dp_g_goff = torch.tensor([j * D for j in range(len(dpt))], dtype=torch.int64,
                                               device=self.device)
                 # gathered (rank-major) ids -> table-major over W*B bags
-                src = []
-                base = 0
+                src, pieces = [], []
+                base = dst = 0
                 for t in dpt:
                     n_t = B * self.L[t]
                     for r in range(W):
                         src.append(torch.arange(r * self.dp_nid + base, r * self.dp_nid + base + n_t))
+                        pieces.append((r * self.dp_nid + base, dst, n_t))
+                        dst += n_t
                     base += n_t
                 self.dp_g_perm = torch.cat(src).to(self.device)
+                self.dp_g_map = ops.SegmentMap(pieces, self.device)
                 self.dp_g_ids_t = torch.zeros_like(self.dp_g_ids)
         self.cw_base = self.dp_base + B * self.dp_width
         self.cw_width = len(self.cw_tables) * D
@@ -351,6 +359,11 @@ class ShardedEmbeddingBags:
                 k = self.cw_owned[r].index((t, c0))
                 src = self.tw_recv_base[r] + len(self.tw_tables[r]) * D + k * Dc
                 self.cw_pieces.append((src, self.dsum[r], self.cw_base + j * D + c0, self.cw_width))
+        if self.cw_tables:
+            # the pooled pieces -> D-wide rows (and back for the gradients):
+            # one native launch each way
+            self._cw_copy = ops.PieceCopy(self.cw_pieces, B, Dc, self.device)
+            self._cw_copy_rev = self._cw_copy.reverse()
         self._pending = None
         self._rw_state = None
         self._rw_ids = None
@@ -359,6 +372,16 @@ class ShardedEmbeddingBags:
         self.layout_version = 0
         self._rw_mbox = None
         self._rw_lag_pending = False
+
+    def _runs(self, tables):
+        """(src, dst, length) pieces laying the given tables' id runs of the
+        input back to back, in that order."""
+        out, dst = [], 0
+        for t in tables:
+            n = self.B * self.L[t]
+            out.append((self.in_base[t], dst, n))
+            dst += n
+        return out
 
     def alias_pooled(self, out: torch.Tensor, d_out: torch.Tensor, col0: int) -> bool:
         """One rank, table-wise tables only: pool straight into the consumer's
@@ -561,18 +584,11 @@ class ShardedEmbeddingBags:
         return True
 
     # -- stages (compute stages are hipGraph-capturable; exchanges are RCCL)
-    def _cw_views(self, buf):
-        B, Dc = self.B, self.Dc
-        for src, sst, dst, dstr in self.cw_pieces:
-            yield (buf.as_strided((B, Dc), (sst, 1), src), buf.as_strided((B, Dc), (dstr, 1), dst))
-
     def _cw_assemble(self, buf):
-        for a, b in self._cw_views(buf):
-            b.copy_(a)
+        self._cw_copy.apply(buf)
 
     def _cw_disassemble(self, buf):
-        for a, b in self._cw_views(buf):
-            a.copy_(b)
+        self._cw_copy_rev.apply(buf)
 
     def stage_fwd_prep(self, ids: torch.Tensor, sharded: bool = True, dp: bool = True):
         """Bucket a batch's ids for the exchanges (``sharded``: table/column/
@@ -580,18 +596,18 @@ class ShardedEmbeddingBags:
         (``dp``); the multi-rank stream graphs run the two halves where their
         buffers' previous readers are ordered (models/dlrm_multirank.py)."""
         if self.dp_tables and dp:
-            torch.index_select(ids, 0, self.dp_in_idx, out=self.dp_ids)
+            self.dp_in_map.apply(ids, self.dp_ids)
         if not sharded:
             return
         if self.cw_tables:
-            torch.index_select(ids, 0, self.cw_perm, out=self.cw_send_ids)
+            self.cw_map.apply(ids, self.cw_send_ids)
             if self.world == 1:
                 self.cw_recv_ids = self.cw_send_ids
         if self.tw_identity:
             self.tw_send_ids = ids
             self.tw_recv_ids = ids
         else:
-            torch.index_select(ids, 0, self.tw_perm, out=self.tw_send_ids)
+            self.tw_map.apply(ids, self.tw_send_ids)
             if self.world == 1:
                 self.tw_recv_ids = self.tw_send_ids
         if self.rw_tables:
@@ -641,7 +657,7 @@ class ShardedEmbeddingBags:
                                   len(self.dp_tables), B, self.recv, self.dp_out_off,
                                   self.dp_width, mean=self.mean, onehot=self.dp_onehot)
             if W > 1 and not self.dp_dense:
-                torch.index_select(self.dp_g_ids, 0, self.dp_g_perm, out=self.dp_g_ids_t)
+                self.dp_g_map.apply(self.dp_g_ids, self.dp_g_ids_t)
         if not sharded:
             return
         if self.tw_nv:

@@ -449,21 +449,29 @@ def test_dlrm_step_matches_cpu():
 
 
 @pytest.mark.parametrize("staged,one", [(False, "0"), (False, "1"), (False, "ids0"),
-                                        (True, "0")])
+                                        (True, "0"), (False, "emb"), (False, "embdefer")])
 def test_dlrm_graph_replay_matches_eager(staged, one):
     """Graph-replayed steps match eager ones: per-stream graphs (one=1: each
     stream's step as composed graphs joined by in-graph event nodes, with
     device-resident batches whose ids are copied on a third stream behind the
-    sort; ids0: without that stream) and the staged multi-rank capture at one
+    sort; ids0: without that stream; emb: as 1, with the top part of the dense
+    optimizer on the embedding stream behind the embedding update; embdefer:
+    and the top weight grads after the interaction backward, the top optimizer
+    part waiting for them in-graph) and the staged multi-rank capture at one
     rank."""
+    import dataclasses
+
     from tdfo_amd.data.synthetic import SyntheticCriteo
     from tdfo_amd.models.dlrm import DLRMConfig, DLRMTrainer
 
     cfg = DLRMConfig(embedding_dim=128, table_rows=[1000, 20, 5000], bottom=[128],
-                     top=[256, 1], composed_graphs=one != "0", ids_stream=one == "1")
+                     top=[256, 1], composed_graphs=one != "0",
+                     ids_stream=one in ("1", "emb", "embdefer"))
     B = 512
     a = DLRMTrainer(cfg, B, DEV)
-    b = DLRMTrainer(cfg, B, DEV)
+    cfg_b = dataclasses.replace(cfg, opt_placement="split_emb" if one.startswith("emb") else None,
+                                defer_wgrad=True if one == "embdefer" else None)
+    b = DLRMTrainer(cfg_b, B, DEV)
     data = SyntheticCriteo(cfg.table_rows, B, device=DEV, seed=4)
     batches = [data.next() for _ in range(6)]
     torch.cuda.synchronize()          # device-resident batches, ready for every stream
@@ -472,7 +480,8 @@ def test_dlrm_graph_replay_matches_eager(staged, one):
     b.capture_graph(warmup=1, staged=staged)
     if not staged:
         assert b.graph == "streams" and ("M" in b._ms["graphs"]) == (one != "0")
-        assert (b._ms["cstream"] is not None) == (one == "1")
+        assert (b._ms["cstream"] is not None) == (one in ("1", "emb", "embdefer"))
+        assert ("EB" in b._ms["graphs"]) == (one == "embdefer")
     if staged:
         # one rank: the prep stage is a no-op and is not captured (no empty graph)
         assert all(kind in ("m", "em", "j") or g[0] is not None for kind, g in b.graph)
@@ -484,7 +493,10 @@ def test_dlrm_graph_replay_matches_eager(staged, one):
         a.step()
         b.step()
     torch.cuda.synchronize()
+    b.sync_streams()
+    torch.cuda.synchronize()
     assert torch.allclose(a.fp.p, b.fp.p, atol=1e-5)
+    assert torch.allclose(a.emb.tw_store.weight, b.emb.tw_store.weight, atol=1e-5)
 
 
 @pytest.mark.parametrize("mean", [False, True])
