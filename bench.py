@@ -41,18 +41,20 @@ def parse(argv=None):
     ap.add_argument("--rows", default="1tb", choices=["1tb", "kaggle", "tiny", "gt1tb"])
     ap.add_argument("--model", default="dlrm", choices=["dlrm", "dcnv2"])
     ap.add_argument("--no-graph", action="store_true")
-    ap.add_argument("--data", default="fresh", choices=["fresh", "pool", "host"],
+    ap.add_argument("--data", default="fresh", choices=["fresh", "instep", "pool", "host"],
                     help="fresh: a new batch every step from the one-launch device generator "
-                         "on a side stream (default); pool: cycle --pool pre-generated device "
-                         "batches; host: the C++ host generator through pinned slots and a "
-                         "copy-stream H2D prefetcher")
+                         "on a side stream (default); instep (one GPU): the same batches "
+                         "generated inside the step graphs (ids on the embedding stream, dense "
+                         "features / labels on the MLP stream); pool: cycle --pool "
+                         "pre-generated device batches; host: the C++ host generator through "
+                         "pinned slots and a copy-stream H2D prefetcher")
     ap.add_argument("--pool", type=int, default=8, help="--data pool: batches in the pool")
     ap.add_argument("--dist", default="uniform", choices=["uniform", "zipf"])
     ap.add_argument("--sharding", default="auto",
                     choices=["auto", "table_wise", "row_wise", "column_wise", "data_parallel",
                              "replicated"])
     ap.add_argument("--opt-placement", default=None,
-                    choices=["one_pass", "split_main", "split_emb"],
+                    choices=["one_pass", "split_main"],
                     help="one GPU: where the dense optimizer runs in the per-stream step "
                          "(DLRMConfig.opt_placement; default: the model's)")
     ap.add_argument("--defer-wgrad", default=None, choices=["0", "1"],
@@ -253,7 +255,7 @@ def emulate(args, info, rows):
     ranks = (list(range(W)) if args.emulate_rank == "max" else
              [int(x) for x in args.emulate_rank.split(",")])
     cfg = _cfg(args, rows, not args.no_pipeline)
-    if args.data in ("host", "fresh"):
+    if args.data in ("host", "fresh", "instep"):
         cfg.ids_stream = False
     per = []
     comm0 = plan_summary = None
@@ -332,7 +334,7 @@ def main(argv=None):
         return
     world = info.world_size
     cfg = _cfg(args, rows, world > 1 and not args.no_pipeline)
-    if args.data in ("host", "fresh"):
+    if args.data in ("host", "fresh", "instep"):
         # a streamed data source orders its batch on every input stream and
         # releases a slot after all of them: a third (ids) stream ties the
         # slot to the sort and stalls the prefetch (0.604 vs 0.470 ms/step)
@@ -367,6 +369,7 @@ def main(argv=None):
         mname = "DLRM" if args.model == "dlrm" else "DCN-v2"
         rname = {"1tb": "1TB", "kaggle": "Kaggle", "gt1tb": "gt1TB", "tiny": "tiny"}[args.rows]
         src = {"fresh": "a fresh batch per step from the on-device generator (side stream)",
+               "instep": "a fresh batch per step generated inside the step graphs",
                "pool": f"a pool of {args.pool} pre-generated device batches, cycled",
                "host": "C++ host generator + pinned copy-stream H2D"}[args.data]
         print(json.dumps({

@@ -1017,6 +1017,65 @@ void synth_criteo(int64_t seed, int64_t rank, int64_t batch_index, int64_t B,
   tdfo::synth_criteo(a, cur_stream());
 }
 
+// In-step generation: the batch index is index_base + counter[0] (a float
+// step counter on the device), read by the kernel -> a fresh batch per replay.
+static tdfo::SynthArgs synth_in_step_args(int64_t seed, int64_t rank, int64_t index_base,
+                                          int64_t B, const Tensor& rows, const Tensor& pooling,
+                                          const Tensor& base, int64_t dist, double alpha,
+                                          const Tensor& counter) {
+  const int64_t T = rows.numel();
+  check_dev(rows, "rows"); check_dev(counter, "counter");
+  TORCH_CHECK(rows.scalar_type() == at::kLong && base.scalar_type() == at::kLong &&
+              pooling.scalar_type() == at::kInt && pooling.numel() == T && base.numel() == T &&
+              rows.is_contiguous() && base.is_contiguous() && pooling.is_contiguous() &&
+              base.device() == rows.device() && pooling.device() == rows.device(),
+              "synth in-step: rows/base int64[T], pooling int32[T] on one device");
+  TORCH_CHECK(counter.scalar_type() == at::kFloat && counter.numel() >= 1 &&
+              counter.device() == rows.device(), "synth in-step: float step counter");
+  tdfo::SynthArgs a{};
+  a.seed = (uint64_t)seed; a.rank = (int)rank; a.batch_index = index_base;
+  a.B = (int)B; a.T = (int)T;
+  a.rows = rows.data_ptr<int64_t>(); a.pooling = pooling.data_ptr<int32_t>();
+  a.base = base.data_ptr<int64_t>(); a.dist = (int)dist; a.alpha = alpha;
+  a.index_ptr = counter.data_ptr<float>();
+  return a;
+}
+
+void synth_ids(int64_t seed, int64_t rank, int64_t index_base, int64_t B, const Tensor& rows,
+               const Tensor& pooling, const Tensor& base, int64_t dist, double alpha,
+               const Tensor& counter, int64_t nnz, const Tensor& ids) {
+  tdfo::SynthArgs a = synth_in_step_args(seed, rank, index_base, B, rows, pooling, base, dist,
+                                         alpha, counter);
+  check_dev(ids, "ids");
+  // nnz = sum_t B * pooling[t] (the host knows it; pooling lives on the device)
+  TORCH_CHECK(ids.scalar_type() == at::kLong && ids.is_contiguous() && ids.numel() == nnz &&
+              ids.device() == rows.device(), "synth_ids: ids int64 [nnz]");
+  a.ids = ids.data_ptr<int64_t>();
+  tdfo::synth_ids(a, cur_stream());
+}
+
+void synth_dense(int64_t seed, int64_t rank, int64_t index_base, int64_t B, const Tensor& rows,
+                 const Tensor& pooling, const Tensor& base, int64_t dist, double alpha,
+                 const Tensor& counter, const Tensor& w_dense, const Tensor& table_bias,
+                 const Tensor& x0, const Tensor& label) {
+  tdfo::SynthArgs a = synth_in_step_args(seed, rank, index_base, B, rows, pooling, base, dist,
+                                         alpha, counter);
+  check_dev(x0, "x0"); check_dev(label, "label");
+  TORCH_CHECK(x0.scalar_type() == at::kBFloat16 && x0.dim() == 2 && x0.size(0) == B &&
+              x0.stride(1) == 1 && x0.size(1) >= w_dense.numel(), "synth_dense: x0 bf16 [B, >= nd]");
+  TORCH_CHECK(w_dense.scalar_type() == at::kFloat && w_dense.is_contiguous() &&
+              table_bias.scalar_type() == at::kFloat && table_bias.numel() == rows.numel() * 64 &&
+              table_bias.is_contiguous() && label.scalar_type() == at::kFloat &&
+              label.numel() == B && label.is_contiguous(), "synth_dense: teacher / label");
+  for (const Tensor* t : {&w_dense, &table_bias, &x0, &label})
+    TORCH_CHECK(t->device() == rows.device(), "synth_dense: one device");
+  a.num_dense = (int)w_dense.numel();
+  a.w_dense = w_dense.data_ptr<float>(); a.table_bias = table_bias.data_ptr<float>();
+  a.x0 = reinterpret_cast<uint16_t*>(x0.data_ptr()); a.ldx = x0.stride(0);
+  a.label = label.data_ptr<float>();
+  tdfo::synth_dense(a, cur_stream());
+}
+
 // ------------------------------------------------------------ loss etc.
 void head_bce(const Tensor& H, const Tensor& w, const Tensor& b, const Tensor& label,
               double inv_n, bool relu_mask, const Tensor& logits, const Tensor& dH,
@@ -1399,6 +1458,11 @@ TORCH_LIBRARY(tdfo, m) {
   m.def("synth_criteo(int seed, int rank, int batch_index, int B, Tensor rows, Tensor pooling, "
         "Tensor base, int dist, float alpha, Tensor w_dense, Tensor table_bias, Tensor(a!) dense, "
         "Tensor(b!) ids, Tensor(c!) label) -> ()");
+  m.def("synth_ids(int seed, int rank, int index_base, int B, Tensor rows, Tensor pooling, "
+        "Tensor base, int dist, float alpha, Tensor counter, int nnz, Tensor(a!) ids) -> ()");
+  m.def("synth_dense(int seed, int rank, int index_base, int B, Tensor rows, Tensor pooling, "
+        "Tensor base, int dist, float alpha, Tensor counter, Tensor w_dense, Tensor table_bias, "
+        "Tensor(a!) x0, Tensor(b!) label) -> ()");
   m.def("batch_load(Tensor dense, Tensor(a!) x0, Tensor ids, Tensor(b!) ids_dst, Tensor label, "
         "Tensor(c!) label_dst) -> ()");
   m.def("head_bce(Tensor H, Tensor w, Tensor b, Tensor label, float inv_n, bool relu_mask, "
@@ -1454,6 +1518,8 @@ TORCH_LIBRARY_IMPL(tdfo, CUDA, m) {
   m.impl("sort_pairs", sort_pairs);
   m.impl("cast_bf16", cast_bf16);
   m.impl("slab_reduce", slab_reduce);
+  m.impl("synth_ids", synth_ids);
+  m.impl("synth_dense", synth_dense);
   m.impl("seg_copy", seg_copy);
   m.impl("piece_copy", piece_copy);
   m.impl("head_bce", head_bce);

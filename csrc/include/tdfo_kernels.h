@@ -178,8 +178,17 @@ struct SynthArgs {
   int dist; double alpha;
   const float* w_dense; const float* table_bias;
   float* dense; int64_t* ids; float* label;
+  // in-step generation (synth_ids / synth_dense): batch index = batch_index +
+  // (int64) index_ptr[0] read on the device (a step counter), so a captured
+  // graph draws a fresh batch every replay; synth_dense writes bf16 features
+  // into x0 (row pitch ldx) instead of fp32 `dense`
+  const float* index_ptr; uint16_t* x0; int64_t ldx;
 };
 void synth_criteo(const SynthArgs& a, hipStream_t s);
+// the ids of synth_criteo's batch only (one thread per (table, sample))
+void synth_ids(const SynthArgs& a, hipStream_t s);
+// its dense features (-> bf16 x0) and labels only (one thread per sample)
+void synth_dense(const SynthArgs& a, hipStream_t s);
 
 // --------------------------------------------------- row-wise shards ----
 // (rowwise.hip) Fixed-capacity row-wise exchange. meta (int64, device):

@@ -97,7 +97,90 @@ __global__ __launch_bounds__(256) void synth_criteo_kernel(SynthArgs a) {
   }
 }
 
+__device__ __forceinline__ int64_t batch_of(const SynthArgs& a) {
+  return a.index_ptr ? a.batch_index + (int64_t)a.index_ptr[0] : a.batch_index;
+}
+
+__device__ __forceinline__ uint64_t sample_key(const SynthArgs& a, int64_t bi, int b) {
+  const uint64_t key = mix64(a.seed * 0x100000001B3ull ^ mix64((uint64_t)a.rank << 40 ^ (uint64_t)bi));
+  return mix64(key ^ (uint64_t)b * 0xD6E8FEB86659FD93ull);
+}
+
+// id l of table t for the sample with key rk (synth_criteo's formula)
+__device__ __forceinline__ int64_t draw_id(const SynthArgs& a, uint64_t rk, int t, int l) {
+  const uint64_t r = (uint64_t)a.rows[t];
+  const uint64_t tk = (uint64_t)(t + 1) << 32;
+  const uint64_t h = mix64(rk ^ tk ^ (uint64_t)(l + 1000));
+  if (a.dist == 1 && r > 1) {
+    const double x = pow((pow((double)r, 1 - a.alpha) - 1) * u01(h) + 1, 1 / (1 - a.alpha));
+    int64_t id = (int64_t)x - 1;
+    return id < 0 ? 0 : (id > (int64_t)r - 1 ? (int64_t)r - 1 : id);
+  }
+  return (int64_t)__umul64hi(h, r);
+}
+
+// ids only: thread (t, b) writes sample b's L_t ids of table t -- the same
+// values synth_criteo writes, with 26x its parallelism (it runs on the
+// embedding stream right before the lookup, on the step's critical chain)
+__global__ __launch_bounds__(256) void synth_ids_kernel(SynthArgs a) {
+  const int64_t bi = batch_of(a);
+  const int64_t n = (int64_t)a.T * a.B;
+  for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n;
+       q += (int64_t)gridDim.x * blockDim.x) {
+    const int t = (int)(q / a.B), b = (int)(q - (int64_t)t * a.B);
+    const uint64_t rk = sample_key(a, bi, b);
+    const int L = a.pooling[t];
+    int64_t* out = a.ids + a.base[t] + (int64_t)b * L;
+    for (int l = 0; l < L; ++l) out[l] = draw_id(a, rk, t, l);
+  }
+}
+
+// dense features (bf16 into x0) and labels: one thread per sample; the
+// teacher score is summed in synth_criteo's order (dense part, then table
+// groups g = 0..3 over t = g, g + 4, ...) so the labels are identical
+__global__ __launch_bounds__(256) void synth_dense_kernel(SynthArgs a) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= a.B) return;
+  const int64_t bi = batch_of(a);
+  const uint64_t rk = sample_key(a, bi, b);
+  const double bias_w = 3.0 / sqrt((double)a.T);
+  double part[TG];
+  double sc = 0.0;
+  for (int j = 0; j < a.num_dense; ++j) {
+    const float x = fast_ln(1.f + (float)(u01(mix64(rk + j)) * 100.0));
+    a.x0[(int64_t)b * a.ldx + j] = f2bf(x);
+    sc += (x - 3.6) * a.w_dense[j] * 2.0;
+  }
+  for (int g = 0; g < TG; ++g) {
+    double pg = g == 0 ? sc : 0.0;
+    for (int t = g; t < a.T; t += TG) {
+      const int64_t id = draw_id(a, rk, t, 0);
+      pg += a.table_bias[t * 64 + (id & 63)] * bias_w;
+    }
+    part[g] = pg;
+  }
+  double s = -1.1;
+  for (int q = 0; q < TG; ++q) s += part[q];
+  const double p = 1.0 / (1.0 + exp(-s));
+  a.label[b] = u01(mix64(rk ^ 0xABCDEFull)) < p ? 1.f : 0.f;
+}
+
 }  // namespace
+
+void synth_ids(const SynthArgs& a, hipStream_t s) {
+  const int64_t n = (int64_t)a.T * a.B;
+  if (n <= 0) return;
+  int64_t blocks = (n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(synth_ids_kernel, dim3(blocks), dim3(256), 0, s, a);
+  TDFO_CHECK_HIP(hipGetLastError());
+}
+
+void synth_dense(const SynthArgs& a, hipStream_t s) {
+  if (a.B <= 0) return;
+  hipLaunchKernelGGL(synth_dense_kernel, dim3((a.B + 255) / 256), dim3(256), 0, s, a);
+  TDFO_CHECK_HIP(hipGetLastError());
+}
 
 void synth_criteo(const SynthArgs& a, hipStream_t s) {
   if (a.B <= 0) return;

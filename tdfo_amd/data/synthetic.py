@@ -193,3 +193,52 @@ class DeviceSyntheticStream:
         for e, st in zip(pool, sts):
             e.record(st)
         self.use_ev[slot] = pool[:len(sts)]
+
+
+class InStepSynthetic:
+    """``DeviceSyntheticStream``'s batch sequence generated INSIDE the
+    trainer's step (one-GPU DLRM / DCN-v2, ``DLRMTrainer.attach_in_step_source``):
+    the ids kernel runs on the embedding stream right before the lookup and
+    writes the trainer's id buffer, the dense/label kernel runs on the MLP
+    stream at the start of the bottom forward and writes x0 (bf16) and the
+    labels -- no side-stream generation, no copies and no cross-stream event
+    waits per step (each costs ~10-23 us of queue idle on this ROCm,
+    profiles/r04/prof_dlrm/step_lanes.txt). The batch index is read on the
+    device from the trainer's step counter, so every graph replay draws the
+    next batch; batch i equals ``DeviceSyntheticStream``'s batch i bit for bit."""
+
+    in_step = True
+
+    def __init__(self, table_rows: Sequence[int], batch_size: int, device, num_dense: int = 13,
+                 pooling: Optional[Sequence[int]] = None, seed: int = 0, dist: str = "uniform",
+                 zipf_alpha: float = 1.05, rank: int = 0, stream: int = 0, start: int = 0):
+        self.g = DeviceSyntheticStream(table_rows, batch_size, device, num_dense=num_dense,
+                                       pooling=pooling, seed=seed, dist=dist,
+                                       zipf_alpha=zipf_alpha, rank=rank, stream=stream, slots=1,
+                                       start=start)
+        self.start = int(start)
+        self.counter = None
+        self.base = None
+
+    def bind(self, counter: torch.Tensor):
+        """``counter``: the trainer's float step counter (bumped once per
+        step, after both generators of the step have read it)."""
+        self.counter = counter
+        self.base = self.start - int(round(float(counter.reshape(-1)[0].item())))
+
+    def gen_ids(self, ids: torch.Tensor):
+        g = self.g
+        g.ops._native().synth_ids(g.seed, g.rank, self.base, g.B, g.rows, g.pool_, g.base,
+                                  g.dist, float(g.alpha), self.counter, g.nnz, ids)
+
+    def gen_dense(self, x0: torch.Tensor, label: torch.Tensor):
+        g = self.g
+        g.ops._native().synth_dense(g.seed, g.rank, self.base, g.B, g.rows, g.pool_, g.base,
+                                    g.dist, float(g.alpha), self.counter, g.w_dense,
+                                    g.table_bias, x0, label)
+
+    def next(self, streams=None):
+        raise RuntimeError("InStepSynthetic batches are generated inside the trainer's step")
+
+    def release(self, slot, streams=None):
+        return None

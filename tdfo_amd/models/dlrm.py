@@ -97,13 +97,13 @@ class DLRMConfig:
     #   pooled exchange in this step's tail (on the side stream)
     defer_wgrad: Optional[bool] = None             # top / cross weight grads after the
     #   interaction / cross backward (None: when W > 1, so the embedding-grad exchange
-    #   overlaps them; on one GPU the DCN-v2 update starved them: 2.606 vs 2.52 ms/step;
-    #   with opt_placement="split_emb" the top optimizer part waits for them in-graph)
+    #   overlaps them; on one GPU the DCN-v2 update starved them: 2.606 vs 2.52 ms/step,
+    #   and DLRM-1TB runs 0.488 vs 0.440, profiles/r04/notes.md)
     opt_placement: Optional[str] = None            # one GPU: "one_pass" (dense optimizer after
     #   the bottom backward; DLRM default) | "split_main" (top part first, beside the
-    #   embedding update; DCN-v2 default) | "split_emb" (bottom part after the bottom
-    #   backward on the MLP stream, top part on the embedding stream right after the
-    #   embedding update, ahead of the next lookup the next top forward waits for)
+    #   embedding update; DCN-v2 default). (Rejected, round 4: the top part on the
+    #   embedding stream behind the update, with or without deferred top weight grads:
+    #   DLRM-1TB 0.458 / 0.478 vs 0.440 ms/step, profiles/r04/notes.md)
     composed_graphs: Optional[bool] = None         # one GPU: chain each stream's graphs with
     #   in-graph event nodes (None: DLRM yes, DCN-v2 no)
     ids_stream: Optional[bool] = None              # one GPU, composed graphs: copy the next
@@ -245,8 +245,8 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
         self.cfg = cfg
         if cfg.dense_comm not in ("fp32", "bf16"):
             raise ValueError(f"dense_comm must be fp32 or bf16, got {cfg.dense_comm!r}")
-        if cfg.opt_placement not in (None, "one_pass", "split_main", "split_emb"):
-            raise ValueError(f"opt_placement must be one_pass, split_main or split_emb, "
+        if cfg.opt_placement not in (None, "one_pass", "split_main"):
+            raise ValueError(f"opt_placement must be one_pass or split_main, "
                              f"got {cfg.opt_placement!r}")
         if cfg.opt_placement is None:
             cfg.opt_placement = "split_main" if cfg.interaction == "dcn" else "one_pass"
@@ -458,6 +458,7 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
         self._stg = None                 # multi-rank graphs: next-batch staging buffers
         self._mr = None
         self._graph_layout = 0
+        self._insrc = None               # in-step batch generator (attach_in_step_source)
 
     # for tests / checkpoints: (weight [out, in_real], bias [out]) views
     def weight(self, name: str):
@@ -514,6 +515,27 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
                 return
         # device-resident batch: one fused launch (ids, labels, dense -> bf16)
         ops.batch_load(dense, self.x0, ids, self.ids, label, self.label)
+
+    def attach_in_step_source(self, src):
+        """One GPU: every step draws its own batch inside its graphs
+        (``data.synthetic.InStepSynthetic``): the ids on the embedding
+        stream right before the lookup, dense features / labels on the MLP
+        stream at the start of the bottom forward, the batch index read from
+        the step counter on the device. Attach before capturing graphs."""
+        if self.world != 1 or self.pipeline:
+            raise ValueError("in-step batch generation is for the one-GPU step")
+        if self.graph is not None:
+            raise RuntimeError("attach the in-step source before capture_graph()")
+        self._insrc = src
+        src.bind(self.dense_hyper[1:2])
+
+    def _s_gen_ids(self):
+        if self._insrc is not None:
+            self._insrc.gen_ids(self.ids)
+
+    def _s_gen_dense(self):
+        if self._insrc is not None:
+            self._insrc.gen_dense(self.x0, self.label)
 
     # ------------------------------------------------- pipelined input dist
     def prime(self, dense: torch.Tensor, ids: torch.Tensor, label: torch.Tensor):
@@ -689,7 +711,8 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
                 ("c", self._s_dense_update),
                 ("j", None),
             ]
-        return prep + [
+        gen = [("c", lambda: (self._s_gen_ids(), self._s_gen_dense()))] if self._insrc else []
+        return gen + prep + [
             ("m", emb.stage_fwd_ids_exchange),
             ("c", emb.stage_fwd_lookup),
             ("m", emb.stage_fwd_out_exchange),

@@ -39,6 +39,7 @@ class StreamGraphsMixin:
         emb = self.emb
 
         def e1():
+            self._s_gen_ids()                # (in-step batches: this step's ids)
             if not emb.fwd_prep_noop:
                 emb.stage_fwd_prep(self.ids)
             emb.stage_fwd_ids_exchange()
@@ -51,58 +52,33 @@ class StreamGraphsMixin:
         # embedding update (2.35 vs 2.40 ms/step); "one_pass" (DLRM): the
         # whole optimizer after the bottom backward (0.463 vs 0.471-0.479)
         split = self.cfg.opt_placement == "split_main"
-        # "split_emb": the top part of the optimizer (every top / head / cross
-        # parameter: its grads exist when the MLP graph records ev[2]) behind
-        # the embedding update on the embedding stream. The next step's top
-        # forward waits for the next lookup (ev[1]), which follows it there;
-        # the next bottom forward needs only the bottom part, updated on the
-        # MLP stream right after the bottom backward.
-        emb_top = self.cfg.opt_placement == "split_emb"
         a, P = self._ar_split, self.fp.p.numel()
-        # "split_emb" with deferred top weight grads: the MLP graph records
-        # ev_wg after them (M3 -> ev_wg -> M3b: bottom backward + bottom part
-        # of the optimizer) and the embedding stream runs the update, waits
-        # ev_wg, then the top part (E3 -> wait ev_wg -> E3b). The top backward
-        # then holds only the dgrad chain, so the embedding gradients -- and
-        # the update -- come ~100 us sooner in the DLRM-1TB step.
-        wg_split = emb_top and self._defer_top_wgrad
 
         def e3():
             emb.backward_start()
             emb.backward_wait()
             self._s_emb_update()
-            if emb_top and not wg_split:
-                self._dense_update_range(a, P)
 
         def m3():
             if self._defer_top_wgrad:
                 self._s_top_wgrad()          # beside the embedding update (E3)
-            if wg_split:
-                return                       # (M3b)
             if split:
                 self._dense_update_range(a, P)
             self._s_bottom_bwd()
-            if split or emb_top:
+            if split:
                 self._dense_update_range(0, a)
             else:
                 self._s_dense_update()
 
-        def m3b():
-            self._s_bottom_bwd()
-            self._dense_update_range(0, a)
-
         def m1():
+            self._s_gen_dense()              # (in-step batches: dense features / labels)
             if self._bstg is not None:       # this step's dense / labels from the staging
                 ops.batch_load(self._bstg[0], self.x0, self.ids[:0], self.ids[:0], self._bstg[1],
                                self.label)
             self._s_bottom_fwd()
 
-        plan = {"E1": e1, "E2": emb.stage_bwd_prepare, "M1": m1,
+        return {"E1": e1, "E2": emb.stage_bwd_prepare, "M1": m1,
                 "M2": self._s_top, "E3": e3, "M3": m3}
-        if wg_split:
-            plan["M3b"] = m3b
-            plan["E3b"] = lambda: self._dense_update_range(a, P)
-        return plan
 
     def _capture_streams(self):
         assert self.world == 1
@@ -125,15 +101,11 @@ class StreamGraphsMixin:
         # steps (that boundary idled it ~23-31 us per step,
         # profiles/r03/s3/w1_timeline/)
         self._bstg = None
-        if composed and ids_stream:
+        if composed and ids_stream and self._insrc is None:
             self._bstg = (torch.zeros(self.B, self.cfg.num_dense, device=self.device),
                           torch.zeros(self.B, device=self.device))
         ev_copy = ops.SyncEvent(2)
-        ev_wg = ops.SyncEvent(2)
         plan = self._ms_plan()
-        if "M3b" in plan and not composed:
-            raise ValueError("deferred top weight grads with opt_placement='split_emb' need "
-                             "composed_graphs (in-graph event nodes)")
         se = torch.cuda.Stream(device=self.device)
         pool = torch.cuda.graph_pool_handle()
         graphs = {}
@@ -155,18 +127,14 @@ class StreamGraphsMixin:
             graphs[name] = gr
         if composed:
             head = [("wait", ev_copy)] if self._bstg is not None else []
-            tail = ([("record", ev_wg), ("graph", graphs["M3b"])] if "M3b" in graphs else [])
             graphs["M"] = ops.ComposedGraph(head + [("graph", graphs["M1"]), ("wait", ev[1]),
                                                     ("graph", graphs["M2"]), ("record", ev[2]),
-                                                    ("graph", graphs["M3"])] + tail)
-            if "E3b" in graphs:
-                # launched after M, so its wait binds to this step's ev_wg
-                graphs["EB"] = ops.ComposedGraph([("graph", graphs["E3"]), ("wait", ev_wg),
-                                                  ("graph", graphs["E3b"])])
+                                                    ("graph", graphs["M3"])])
             graphs["EA"] = ops.ComposedGraph([("graph", graphs["E1"]), ("record", ev[1]),
                                               ("graph", graphs["E2"])])
         torch.cuda.synchronize()
-        cs = torch.cuda.Stream(device=self.device) if ids_stream else None
+        cs = (torch.cuda.Stream(device=self.device) if ids_stream and self._insrc is None
+              else None)
         self._ms = {"graphs": graphs, "stream": se, "plan": plan, "composed": composed,
                     "names": names,
                     "cstream": cs, "ev_e2": ops.SyncEvent(2), "ev_copy": ev_copy,
@@ -237,7 +205,7 @@ class StreamGraphsMixin:
             ev[2].record(main)
         with torch.cuda.stream(se):
             se.wait_event(ev[2])             # embedding gradients ready
-            (g["EB"] if "EB" in g else g["E3"]).replay()
+            g["E3"].replay()
             ev[3].record(se)
         if not composed:
             g["M3"].replay()

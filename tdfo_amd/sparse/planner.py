@@ -30,9 +30,10 @@ Sharding kinds:
 
 Strategies: "data_parallel" (config 3, the reference's pmap / Mirrored /
 DDP data parallelism, jax-flax/train_dp.py:63, tensorflow2/train_dp.py:71-72)
-replicates every table up to ``dp_replicate_max_bytes`` (256 MB: its dense
-fp32 gradient all-reduce is cheap and its update is the same dense pass on
-every rank) and owner-partitions the larger ones as row-wise shards: an exact
+replicates the smallest tables while their fp32 weights total at most
+``dp_replicate_max_bytes`` (256 MB: one dense fp32 gradient all-reduce trains
+all of them and their update is the same dense pass on every rank) and
+owner-partitions the larger ones as row-wise shards: an exact
 replica of a big table would make every rank apply the whole global batch's
 update (W x the one-GPU work, plus W x B pooled gradients gathered), while
 the owner-partitioned table gives the same numbers with each rank updating
@@ -178,12 +179,27 @@ def plan_sharding(tables: Sequence[TableConfig], world_size: int, optim: EmbOpti
         for t in order:
             if tables[t].num_embeddings * _mem_per_row(tables[t].embedding_dim, optim) > cap:
                 shards[t] = row_wise(t)
+    # "data_parallel": the smallest tables are replicated while their fp32
+    # weights add up to at most dp_replicate_max_bytes -- the replicated set
+    # then trains by ONE dense fp32 gradient all-reduce per step (the
+    # reference's DP all-reduce, jax-flax/train_dp.py:63) -- and the rest are
+    # owner-partitioned row-wise (an exact replica of a big table would make
+    # every rank apply the whole global batch's update)
+    replicate = set()
+    if strategy == "data_parallel" and W > 1:
+        cum = 0
+        for t in sorted(range(T), key=lambda t: (tables[t].num_embeddings *
+                                                  tables[t].embedding_dim, t)):
+            nb = tables[t].num_embeddings * tables[t].embedding_dim * 4
+            if cum + nb > dp_replicate_max_bytes:
+                break
+            cum += nb
+            replicate.add(t)
     for t in order:
         if shards[t] is not None:
             continue
         tb = tables[t].num_embeddings * _mem_per_row(tables[t].embedding_dim, optim)
-        if strategy == "data_parallel" and W > 1 and (
-                tables[t].num_embeddings * tables[t].embedding_dim * 4 > dp_replicate_max_bytes):
+        if strategy == "data_parallel" and W > 1 and t not in replicate:
             shards[t] = row_wise(t)                 # owner-partitioned big table
             continue
         if strategy in ("data_parallel", "replicated") or (strategy == "auto" and (

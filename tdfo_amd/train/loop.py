@@ -58,14 +58,20 @@ def make_source(table_rows: Sequence[int], batch: int, device, pooling: Optional
                 seed: int, rank: int, dist: str = "uniform", zipf_alpha: float = 1.05,
                 start: int = 0, stream: int = 0, kind: str = "auto", num_dense: int = 13,
                 threads: int = 8):
-    """The batch source for ``kind``: "fresh" (device generator), "host"
-    (host generator + prefetcher), "cpu" (host generator, synchronous) or
-    "auto" (fresh on a GPU, cpu otherwise). Batch ``i`` is the same pure
-    function of (seed, stream, rank, i) for every kind (uniform ids)."""
+    """The batch source for ``kind``: "fresh" (device generator), "instep"
+    (the same generator inside the trainer's step; one GPU), "host" (host
+    generator + prefetcher), "cpu" (host generator, synchronous) or "auto"
+    (fresh on a GPU, cpu otherwise). Batch ``i`` is the same pure function of
+    (seed, stream, rank, i) for every kind (uniform ids)."""
     import torch
     dev = torch.device(device)
     if kind == "auto":
         kind = "fresh" if dev.type == "cuda" else "cpu"
+    if kind == "instep":
+        from ..data.synthetic import InStepSynthetic
+        return InStepSynthetic(table_rows, batch, dev, num_dense=num_dense, pooling=pooling,
+                               seed=seed, dist=dist, zipf_alpha=zipf_alpha, rank=rank,
+                               stream=stream, start=start)
     if kind == "fresh":
         from ..data.synthetic import DeviceSyntheticStream
         return DeviceSyntheticStream(table_rows, batch, dev, num_dense=num_dense, pooling=pooling,
@@ -99,6 +105,9 @@ class StepLoop:
         self._primed = False
         self.wd = watchdog
         self.beat_every = max(1, int(beat_every))
+        self.in_step = bool(getattr(source, "in_step", False))
+        if self.in_step:
+            trainer.attach_in_step_source(source)
 
     def _streams(self):
         return None if self.tr.pipeline else self.tr.input_streams()
@@ -137,6 +146,12 @@ class StepLoop:
     def _run(self, n: int, on_dev: bool):
         tr, wd = self.tr, self.wd
         for k in range(n):
+            if self.in_step:                   # the step draws its own batch
+                tr.step()
+                self.step_index += 1
+                if wd is not None and (self.step_index % self.beat_every == 0) and k + 1 < n:
+                    wd.beat(tr.heartbeat_stream(), self.step_index)
+                continue
             batch, slot = self._next()
             if tr.pipeline:
                 tr.set_next_batch(*batch)

@@ -1,0 +1,68 @@
+"""In-step synthetic batches (data.synthetic.InStepSynthetic; csrc/kernels/
+synthetic.hip synth_ids / synth_dense): the ids, bf16 dense features and
+labels the step draws from its device step counter equal the side-stream
+generator's batch of the same index bit for bit, and a trainer whose per-stream
+graphs generate their own batches trains exactly like one fed the same
+batches through load_batch."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = torch.device("cuda", 0)
+ROWS = [1000, 20, 5000, 3]
+
+
+@pytest.mark.parametrize("dist,pooling", [("uniform", None), ("zipf", [2, 1, 3, 1])])
+def test_in_step_batches_equal_device_stream(dist, pooling):
+    from tdfo_amd import ops
+    from tdfo_amd.data.synthetic import DeviceSyntheticStream, InStepSynthetic
+
+    B, nd = 300, 13
+    ref = DeviceSyntheticStream(ROWS, B, DEV, pooling=pooling, seed=5, dist=dist, start=7)
+    ins = InStepSynthetic(ROWS, B, DEV, pooling=pooling, seed=5, dist=dist, start=7)
+    counter = torch.tensor([3.0], device=DEV)
+    ins.bind(counter)
+    x0 = torch.zeros(B, 64, dtype=torch.bfloat16, device=DEV)
+    x0[:, nd] = 1.0
+    ids = torch.empty(ref.nnz, dtype=torch.int64, device=DEV)
+    label = torch.empty(B, device=DEV)
+    for k in range(3):
+        (d, i, y), slot = ref.next()
+        ins.gen_ids(ids)
+        ins.gen_dense(x0, label)
+        torch.cuda.synchronize()
+        assert torch.equal(ids, i), k
+        assert torch.equal(label, y), k
+        # the same bf16 conversion batch_load applies
+        xr = torch.zeros_like(x0)
+        xr[:, nd] = 1.0
+        ops.batch_load(d, xr, i[:0], i[:0], y, torch.empty_like(y))
+        assert torch.equal(x0, xr), k
+        ref.release(slot)
+        counter += 1.0
+
+
+def test_trainer_in_step_matches_loaded_batches():
+    from tdfo_amd.data.synthetic import DeviceSyntheticStream, InStepSynthetic
+    from tdfo_amd.models.dlrm import DLRMConfig, DLRMTrainer
+    from tdfo_amd.train.loop import StepLoop
+
+    cfg = DLRMConfig(embedding_dim=128, table_rows=ROWS, bottom=[128], top=[256, 1], ids_stream=False)
+    B = 512
+    a = DLRMTrainer(cfg, B, DEV)
+    b = DLRMTrainer(cfg, B, DEV)
+    la = StepLoop(a, DeviceSyntheticStream(ROWS, B, DEV, seed=2))
+    lb = StepLoop(b, InStepSynthetic(ROWS, B, DEV, seed=2))
+    for lp in (la, lb):
+        lp.run(2)
+        lp.tr.capture_graph(warmup=0)
+        assert lp.tr.graph == "streams"
+        lp.run(6)
+    torch.cuda.synchronize()
+    for t in (a, b):
+        t.sync_streams()
+    torch.cuda.synchronize()
+    assert torch.equal(a.fp.p, b.fp.p)
+    assert torch.equal(a.emb.tw_store.weight, b.emb.tw_store.weight)
+    assert a.pop_loss() == b.pop_loss()

@@ -73,16 +73,26 @@ def test_plan_cost_counts_xgmi():
 
 @pytest.mark.parametrize("world", [2, 8])
 def test_plan_data_parallel_owner_partitions_big_tables(world):
-    """Config 3 (data_parallel): tables up to 256 MB are replicated, larger
+    """Config 3 (data_parallel): the smallest tables are replicated while they
+    total at most 256 MB (one dense-gradient all-reduce trains them), larger
     ones are owner-partitioned (row-wise), so each rank updates 1/W of their
     rows and its memory stays far below a full replica; "replicated" keeps
     every table whole on every rank."""
     cfg = DLRMConfig()
     o = EmbOptimConfig("rowwise_adagrad")
     p = plan_sharding(cfg.tables(), world, o, strategy="data_parallel")
+    order = sorted(range(len(CRITEO_1TB_ROWS)), key=lambda t: (CRITEO_1TB_ROWS[t], t))
+    cum, rep_set = 0, set()
+    for t in order:
+        if cum + CRITEO_1TB_ROWS[t] * 128 * 4 > 256 << 20:
+            break
+        cum += CRITEO_1TB_ROWS[t] * 128 * 4
+        rep_set.add(t)
+    assert 403346 not in [CRITEO_1TB_ROWS[t] for t in rep_set]     # 206 MB: over the budget
     for t, r in enumerate(CRITEO_1TB_ROWS):
-        big = r * 128 * 4 > 256 << 20
-        assert p.kind_of(t) == ("row_wise" if big else "data_parallel"), (t, r)
+        assert p.kind_of(t) == ("data_parallel" if t in rep_set else "row_wise"), (t, r)
+    dp_bytes = sum(CRITEO_1TB_ROWS[t] * 128 * 4 for t in rep_set)
+    assert dp_bytes <= 256 << 20
     assert max(p.mem_bytes) < 100 * GiB / world + 2 * GiB
     rep = plan_sharding(cfg.tables(), world, o, strategy="replicated")
     assert all(s.kind == "data_parallel" for s in rep.shards)
