@@ -59,12 +59,20 @@ class StreamGraphsMixin:
             emb.backward_wait()
             self._s_emb_update()
 
+        early = self.cfg.bottom_bwd_first and not self._defer_top_wgrad
+
+        def m2():
+            self._s_top()
+            if early:                        # before ev[2]: E3 starts after it
+                self._s_bottom_bwd()
+
         def m3():
             if self._defer_top_wgrad:
                 self._s_top_wgrad()          # beside the embedding update (E3)
             if split:
                 self._dense_update_range(a, P)
-            self._s_bottom_bwd()
+            if not early:
+                self._s_bottom_bwd()
             if split:
                 self._dense_update_range(0, a)
             else:
@@ -78,7 +86,7 @@ class StreamGraphsMixin:
             self._s_bottom_fwd()
 
         return {"E1": e1, "E2": emb.stage_bwd_prepare, "M1": m1,
-                "M2": self._s_top, "E3": e3, "M3": m3}
+                "M2": m2, "E3": e3, "M3": m3}
 
     def _capture_streams(self):
         assert self.world == 1

@@ -2,8 +2,9 @@
 
 Entry points (recipes/dlrm):
   train.py     single process (CPU: DLRM-tiny, config 1; one GPU: config 2)
-  train_dp.py  one process per GPU, replicated tables (``data_parallel``
-               sharding: local lookups, row-gradient all-gather) + dense
+  train_dp.py  one process per GPU, ``data_parallel`` sharding (the small
+               tables replicated and trained by one dense-gradient
+               all-reduce, the large ones owner-partitioned row-wise) + dense
                all-reduce over RCCL (config 3)
   train_ps.py  the parameter-server entry point of the reference collapsed
                into the sharded engine: table-wise / row-wise shards with
@@ -13,7 +14,11 @@ Training loop services: JSONL metrics + stdout log lines,
 examples/s throughput, held-out synthetic eval (loss + bucketed ROC-AUC),
 non-finite loss detection (halt with a clear error), sharded checkpoints
 (one file per rank + manifest, atomically completed) and resume, and a
-fault-injection hook (``TDFO_FAULT_AT_STEP``) used by the recovery tests.
+fault-injection hook (``TDFO_FAULT_AT_STEP``) used by the recovery tests;
+on a GPU a step watchdog (utils/watchdog.py, ``TDFO_WATCHDOG_S``, default
+600 s) ends a hung rank with a diagnostic, and a multi-rank run checks at
+the end that every rank's replicated state is bit-identical
+(parallel/replicas.py) and raises otherwise.
 """
 from __future__ import annotations
 
@@ -117,7 +122,11 @@ def run(cfg: Config, mode: str = "single", out_dir: str = ".",
                 tr.load_flat_state(st["tensors"])
                 start = int(st["step"])
             _log(rank, f"===== resumed from {latest} at step {start} =====")
-    loop = StepLoop(tr, _source(cfg, dcfg, B, dev, rank, 0, start), start)
+    wd = None
+    if dev.type == "cuda" and float(os.environ.get("TDFO_WATCHDOG_S", "600") or 0) > 0:
+        from ..utils.watchdog import StepWatchdog
+        wd = StepWatchdog(dev, 600.0, rank=rank, describe=tr.progress)
+    loop = StepLoop(tr, _source(cfg, dcfg, B, dev, rank, 0, start), start, watchdog=wd)
     metrics_path = cfg.metrics_file
     fault_at = int(os.environ.get("TDFO_FAULT_AT_STEP", "0") or 0)
     fault_rank = int(os.environ.get("TDFO_FAULT_RANK", "0") or 0)
@@ -194,6 +203,14 @@ def run(cfg: Config, mode: str = "single", out_dir: str = ".",
             with trace_range("checkpoint"):
                 save(tr, cfg.ckpt_dir, step, rank, world, meta)
     loop.close()
+    if wd is not None:
+        wd.close()
+    if world > 1:
+        from ..parallel.replicas import check_replicas
+        ok, per = check_replicas(tr.replicated_state(), group)
+        _log(rank, f"===== replicated state consistent across ranks: {ok} =====")
+        if not ok:
+            raise RuntimeError(f"rank {rank}: replicated state differs across ranks: {per}")
     if cfg.ckpt_dir:
         save(tr, cfg.ckpt_dir, step, rank, world, meta)
     return {"history": history, "steps": step, "trainer": tr}
