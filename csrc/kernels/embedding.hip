@@ -21,6 +21,7 @@
 //   combine: the chunk where a crossing run starts adds the following chunks'
 //            head partials in order and applies the optimizer once.
 // Every unique row is updated exactly once per step, in a fixed order.
+#include <cstdlib>
 #include <type_traits>
 
 #include "tdfo_common.h"
@@ -610,10 +611,13 @@ __global__ __launch_bounds__(256) void emb_chunk_kernel(
   constexpr int EPL = BwdCfg<D>::EPL, CH = BwdCfg<D>::CH;
   constexpr bool NEED_W = OPT != EMB_DENSE_GRAD;
   const int lane = threadIdx.x & 63;
-  const int64_t c = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int64_t start = c * CH;
-  if (start >= a.nnz || skip_step(a)) return;
+  if (skip_step(a)) return;
   const OptScalars o = opt_scalars(a);
+  const int64_t nch = (a.nnz + CH - 1) / CH;
+  const int64_t nwv = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  // one wave per chunk; a capped grid (chunk_grid_cap) walks the chunks
+  for (int64_t c = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; c < nch; c += nwv) {
+  const int64_t start = c * CH;
   const int64_t end = min(start + (int64_t)CH, a.nnz);
   const int len = (int)(end - start);
   const int li = lane < len ? lane : len - 1;     // lanes >= len duplicate the last entry
@@ -681,6 +685,7 @@ __global__ __launch_bounds__(256) void emb_chunk_kernel(
       const int slot = atomicAdd(tail_count, 1);
       if (slot < (int)((a.nnz + CH - 1) / CH)) tail_list[slot] = (int32_t)c;
     }
+  }
   }
 }
 
@@ -841,6 +846,17 @@ void dense_update_dispatch(const EmbBwdArgs& a, int64_t rows, const float* g, hi
 
 int g_emb_segsort = 1;   // one-hot batches: per-table LDS sort (0: device-wide radix sort)
 
+// A/B knob: cap on the fused update's grid (blocks of 4 chunk waves; 0 = one
+// wave per chunk), so a long multi-hot update leaves CUs to GEMMs beside it
+// (TDFO_EMB_CHUNK_GRID)
+int64_t chunk_grid_cap() {
+  static const int64_t v = [] {
+    const char* e = getenv("TDFO_EMB_CHUNK_GRID");
+    return e ? (int64_t)atoll(e) : (int64_t)0;
+  }();
+  return v;
+}
+
 struct WsLayout {
   size_t keys_in, keys_out, vals_in, vals_out, goff, gscale, head, tail, tlist, tcount, sortws,
       pos;
@@ -944,7 +960,8 @@ void apply_impl(const EmbBwdArgs& a0, const WsLayout& L, hipStream_t s) {
   int32_t* tcount = (int32_t*)(ws + L.tcount);
   constexpr int CH = BwdCfg<D>::CH;
   const int64_t nch = (a.nnz + CH - 1) / CH;
-  const int64_t blocks = (nch + 3) / 4;
+  int64_t blocks = (nch + 3) / 4;
+  if (chunk_grid_cap() > 0 && blocks > chunk_grid_cap()) blocks = chunk_grid_cap();
   if (a.grad_bf16)
     hipLaunchKernelGGL((emb_chunk_kernel<D, K, true, OPT>), dim3(blocks), dim3(256), 0, s, a,
                        keys_out, vals_out, goff, gscale, head, tail, tlist, tcount);
