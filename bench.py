@@ -60,9 +60,6 @@ def parse(argv=None):
     ap.add_argument("--defer-wgrad", default=None, choices=["0", "1"],
                     help="top / cross weight grads after the interaction / cross backward "
                          "(DLRMConfig.defer_wgrad; default: when N > 1)")
-    ap.add_argument("--bottom-bwd-first", action="store_true",
-                    help="one GPU: bottom-MLP backward before the embedding update starts "
-                         "(DLRMConfig.bottom_bwd_first)")
     ap.add_argument("--dense-comm", default="fp32", choices=["fp32", "bf16"],
                     help="N > 1: wire format of the dense-gradient all-reduce")
     ap.add_argument("--no-pipeline", action="store_true",
@@ -78,7 +75,8 @@ def parse(argv=None):
                          "byte count (parallel/comm.py LoopbackComm); reports device ms/step, "
                          "host issue us/step and the collective volume (not the headline)")
     ap.add_argument("--emulate-rank", default="0", metavar="K[,K...]|max",
-                    help="--emulate-world: the rank(s) to emulate, in turn, or 'max': every "
+                    help="--emulate-world: the rank(s) to emulate, each in its own child "
+                         "process (TDFO_EMU_INPROC=1: in turn in this one), or 'max': every "
                          "rank of the plan; the slowest is reported (a synchronous step runs "
                          "at the pace of its slowest rank)")
     ap.add_argument("--emulate-link-gbps", type=float, default=None,
@@ -153,8 +151,7 @@ def _cfg(args, rows, pipe):
     kw = dict(table_rows=list(rows), sharding=args.sharding, pipeline=pipe,
               dense_comm=args.dense_comm, stream_graphs=not args.no_stream_graphs,
               opt_placement=args.opt_placement,
-              defer_wgrad=None if args.defer_wgrad is None else args.defer_wgrad == "1",
-              bottom_bwd_first=args.bottom_bwd_first)
+              defer_wgrad=None if args.defer_wgrad is None else args.defer_wgrad == "1")
     if args.model == "dlrm":
         return DLRMConfig(**kw)
     return DLRMConfig(interaction="dcn", pooling=list(MLPERF_MULTIHOT),
@@ -310,11 +307,40 @@ def emulate(args, info, rows):
                    "sharding": args.sharding}}), flush=True)
 
 
+def emulate_ranks_isolated(args, argv) -> int:
+    """--emulate-rank with several ranks: each rank in a fresh child process
+    (started before this process touches the GPU), so no rank runs on memory
+    another trainer freed -- in one process the 4th trainer of a sequence ran
+    up to 1.35x slower whichever rank it was (profiles/r04/notes.md). Prints
+    the slowest rank's line with every rank's ms/step."""
+    W = args.emulate_world
+    ranks = (list(range(W)) if args.emulate_rank == "max" else
+             [int(x) for x in args.emulate_rank.split(",")])
+    per = []
+    for k in ranks:
+        cmd = [sys.executable, os.path.abspath(__file__), *argv, "--emulate-rank", str(k)]
+        p = subprocess.run(cmd, stdout=subprocess.PIPE, text=True)
+        lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+        if p.returncode != 0 or not lines:
+            print(f"error: emulated rank {k} exited {p.returncode}", file=sys.stderr)
+            return p.returncode or 1
+        per.append(json.loads(lines[-1]))
+    top = max(per, key=lambda x: x["value"])
+    top["metric"] = (f"emulated step of the {W}-rank job, slowest of ranks {ranks} "
+                     "(loopback collectives, one process per rank)")
+    top["per_rank_ms"] = {x["emulated_rank"]: x["value"] for x in per}
+    print(json.dumps(top), flush=True)
+    return 0
+
+
 def main(argv=None):
     argv = list(sys.argv[1:] if argv is None else argv)
     args = parse(argv)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(self_launch(args, argv))
+    if (args.emulate_world > 1 and (args.emulate_rank == "max" or "," in args.emulate_rank)
+            and os.environ.get("TDFO_EMU_INPROC") != "1"):
+        sys.exit(emulate_ranks_isolated(args, argv))
     from tdfo_amd.parallel.dist import init_distributed, reset
     from tdfo_amd.models.dlrm import CRITEO_1TB_ROWS, CRITEO_KAGGLE_ROWS, DCN_GT1TB_ROWS
     from tdfo_amd.ops import _ext

@@ -800,7 +800,7 @@ void embedding_bwd_apply(const Tensor& W, const Tensor& row_offset, const Tensor
 void embedding_dense_update(const Tensor& W, const Tensor& grad, int64_t rows, int64_t opt,
                             const c10::optional<Tensor>& state1, const c10::optional<Tensor>& state2,
                             const Tensor& hyper, double eps, double beta1, double beta2,
-                            double weight_decay) {
+                            double weight_decay, bool clear_grad) {
   check_dev(W, "W");
   TORCH_CHECK(W.scalar_type() == at::kFloat && W.is_contiguous() && W.dim() == 2, "W fp32 2-D");
   const int64_t D = W.size(1);
@@ -814,7 +814,9 @@ void embedding_dense_update(const Tensor& W, const Tensor& grad, int64_t rows, i
   a.W = W.data_ptr<float>(); a.D = (int)D;
   emb_bwd_opt_args(a, W, grad, opt, state1, state2, hyper, eps, beta1, beta2, weight_decay,
                    c10::nullopt);
-  tdfo::embedding_dense_update(a, rows, grad.data_ptr<float>(), cur_stream());
+  tdfo::embedding_dense_update(a, rows, grad.data_ptr<float>(),
+                               clear_grad ? const_cast<float*>(grad.data_ptr<float>()) : nullptr,
+                               cur_stream());
 }
 
 // ------------------------------------------------------- row-wise shards
@@ -1436,9 +1438,9 @@ TORCH_LIBRARY(tdfo, m) {
         "int grad_stride, int opt, Tensor(b!)? state1, Tensor(c!)? state2, Tensor hyper, "
         "float eps, float beta1, float beta2, float weight_decay, Tensor(d!)? dense_grad, "
         "int segsort, Tensor(e!) workspace) -> ()");
-  m.def("embedding_dense_update(Tensor(a!) W, Tensor grad, int rows, int opt, Tensor(b!)? state1, "
+  m.def("embedding_dense_update(Tensor(a!) W, Tensor(d!) grad, int rows, int opt, Tensor(b!)? state1, "
         "Tensor(c!)? state2, Tensor hyper, float eps, float beta1, float beta2, "
-        "float weight_decay) -> ()");
+        "float weight_decay, bool clear_grad) -> ()");
   m.def("rw_bucketize_workspace(int n, int W) -> int", rw_bucketize_workspace);
   m.def("rw_bucketize(Tensor ids, Tensor meta, int nrw, int W, int B, int cap, int n, "
         "Tensor(a!) send, Tensor(b!) workspace, Tensor(c!) overflow) -> ()");

@@ -163,7 +163,9 @@ void embedding_bwd_apply(const EmbBwdArgs& a, hipStream_t s);
 
 // Dense optimizer step over rows [0, rows) of W from a dense fp32 gradient
 // [rows, D] (a.opt, a.state1/2, a.hyper, eps/betas/wd as for the backward).
-void embedding_dense_update(const EmbBwdArgs& a, int64_t rows, const float* grad, hipStream_t s);
+// clear: null, or grad itself (each row zeroed once read)
+void embedding_dense_update(const EmbBwdArgs& a, int64_t rows, const float* grad, float* clear,
+                            hipStream_t s);
 
 // --------------------------------------------------- synthetic data ----
 // (synthetic.hip) One fresh synthetic Criteo batch (device twin of

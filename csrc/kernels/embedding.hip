@@ -800,10 +800,29 @@ __global__ void emb_rw_keys_kernel(const EmbBwdArgs a, const int64_t* __restrict
 // gradient [rows, D] -- the data-parallel tables' step after their gradient
 // all-reduce. One wave per row; rows with an all-zero gradient are left
 // untouched for SGD / row-wise Adagrad / Adagrad without weight decay, so the
-// result equals the sparse update of the touched rows.
+// result equals the sparse update of the touched rows. ``gclr`` (== g or
+// null): zero each gradient row once read, so the next step's backward
+// accumulates into a clean buffer without a separate fill pass (also on a
+// skipped step).
+template <int D>
+__device__ __forceinline__ void zero_row(float* w) {
+  constexpr int EPL = BwdCfg<D>::EPL;
+  if constexpr (EPL == 2) {
+    *(float2*)w = make_float2(0.f, 0.f);
+  } else if constexpr (EPL == 4) {
+    *(float4*)w = make_float4(0.f, 0.f, 0.f, 0.f);
+  } else if constexpr (EPL == 8) {
+    *(float4*)w = make_float4(0.f, 0.f, 0.f, 0.f);
+    *(float4*)(w + 4) = make_float4(0.f, 0.f, 0.f, 0.f);
+  } else {
+    w[0] = 0.f;
+  }
+}
+
 template <int D, int OPT>
 __global__ __launch_bounds__(256) void emb_dense_update_kernel(EmbBwdArgs a, int64_t rows,
-                                                              const float* __restrict__ g) {
+                                                              const float* __restrict__ g,
+                                                              float* gclr) {
   constexpr int EPL = BwdCfg<D>::EPL;
   const int lane = threadIdx.x & 63;
   const int e0 = elem0<D>(lane);
@@ -811,11 +830,16 @@ __global__ __launch_bounds__(256) void emb_dense_update_kernel(EmbBwdArgs a, int
   const int e0c = act ? e0 : 0;
   const OptScalars o = opt_scalars(a);
   const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  if (skip_step(a)) return;
-  for (int64_t row = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; row < rows;
-       row += nw) {
+  const int64_t row0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (skip_step(a)) {
+    if (gclr && act)
+      for (int64_t row = row0; row < rows; row += nw) zero_row<D>(gclr + row * D + e0);
+    return;
+  }
+  for (int64_t row = row0; row < rows; row += nw) {
     float acc[EPL], wv[EPL];
     load_row<D>(acc, g + row * D + e0c);
+    if (gclr && act) zero_row<D>(gclr + row * D + e0);
     load_row<D>(wv, a.W + row * D + e0c);
     if (!act) {
 #pragma unroll
@@ -827,12 +851,13 @@ __global__ __launch_bounds__(256) void emb_dense_update_kernel(EmbBwdArgs a, int
 }
 
 template <int D>
-void dense_update_dispatch(const EmbBwdArgs& a, int64_t rows, const float* g, hipStream_t s) {
+void dense_update_dispatch(const EmbBwdArgs& a, int64_t rows, const float* g, float* gclr,
+                           hipStream_t s) {
   int64_t blocks = (rows + 3) / 4;
   if (blocks > 16384) blocks = 16384;
   if (blocks < 1) return;
 #define TDFO_DU(OPT) hipLaunchKernelGGL((emb_dense_update_kernel<D, OPT>), dim3(blocks), dim3(256), \
-                                        0, s, a, rows, g)
+                                        0, s, a, rows, g, gclr)
   switch (a.opt) {
     case EMB_SGD: TDFO_DU(EMB_SGD); break;
     case EMB_ROWWISE_ADAGRAD: TDFO_DU(EMB_ROWWISE_ADAGRAD); break;
@@ -1086,14 +1111,15 @@ void embedding_bwd_prepare_rw(const EmbBwdArgs& a, const int64_t* recv, const in
     prep_rw_impl<uint64_t>(a, L, recv, meta, nrw, W, cap, grad_ld, dummy_row, s);
 }
 
-void embedding_dense_update(const EmbBwdArgs& a, int64_t rows, const float* grad, hipStream_t s) {
+void embedding_dense_update(const EmbBwdArgs& a, int64_t rows, const float* grad, float* clear,
+                            hipStream_t s) {
   switch (a.D) {
-    case 16: dense_update_dispatch<16>(a, rows, grad, s); break;
-    case 32: dense_update_dispatch<32>(a, rows, grad, s); break;
-    case 64: dense_update_dispatch<64>(a, rows, grad, s); break;
-    case 128: dense_update_dispatch<128>(a, rows, grad, s); break;
-    case 256: dense_update_dispatch<256>(a, rows, grad, s); break;
-    case 512: dense_update_dispatch<512>(a, rows, grad, s); break;
+    case 16: dense_update_dispatch<16>(a, rows, grad, clear, s); break;
+    case 32: dense_update_dispatch<32>(a, rows, grad, clear, s); break;
+    case 64: dense_update_dispatch<64>(a, rows, grad, clear, s); break;
+    case 128: dense_update_dispatch<128>(a, rows, grad, clear, s); break;
+    case 256: dense_update_dispatch<256>(a, rows, grad, clear, s); break;
+    case 512: dense_update_dispatch<512>(a, rows, grad, clear, s); break;
   }
 }
 

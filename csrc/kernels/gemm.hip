@@ -1207,16 +1207,6 @@ void pp_pair_launch(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s) {
 // kernel (256x128: not for column-sum weight grads) (tests, A/B).
 int g_policy = 0;
 
-// policy 5: the smallest GEMM (in 128x128 tiles x splits) that goes to the
-// 256x128 kernel (TDFO_GEMM_BIG_MIN overrides, for A/B)
-int big_min() {
-  static const int v = [] {
-    const char* e = getenv("TDFO_GEMM_BIG_MIN");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-
 enum Kern { K_SMALL64 = 64, K_SMALL128 = 128, K_DEEP = 2, K_PP = 3, K_BIG = 4 };
 
 template <bool AC, bool BC>
@@ -1234,15 +1224,15 @@ int choose(const GemmArgs& a) {
   if (g_policy == 5) {
     // DCN-v2: the deep kernel where a 256x128 grid would leave CUs idle while
     // a 128x128 one fills them about once, with long K (cross-layer V fwd /
-    // U dgrad); 256x128 tiles for everything else without column sums --
-    // except GEMMs of fewer than big_min() 128x128 tiles (the bottom MLP),
-    // which run beside the memory-bound embedding kernels: a 144-KiB,
-    // 512-thread block waits for a whole free CU there (DCN-v2 step: the
-    // bottom backward pair took 398 us beside the 506-us embedding update,
-    // profiles/r04/prof_dcn/step_lanes.txt)
+    // U dgrad); 256x128 tiles for everything else without column sums, the
+    // bottom MLP included: it runs beside the memory-bound embedding kernels
+    // and its 144-KiB blocks wait there for whole free CUs (a 398-us backward
+    // pair, profiles/r04/prof_dcn/step_lanes.txt), yet sending its GEMMs of
+    // < 300 / 600 tiles to the 128x128 kernels ran the step at 2.64 / 2.66 vs
+    // 2.36 ms (profiles/r04/notes.md)
     const int t256 = ((a.M + LBM - 1) / LBM) * ((a.N + BN - 1) / BN) * a.splits;
     if (!AC && t256 < 256 && t128 <= 512 && ktps >= 16) return K_DEEP;
-    if (big_ok && t128 >= big_min()) return K_BIG;
+    if (big_ok) return K_BIG;
   } else {
     if (!AC && ktps >= 32 && t128 <= 512) return K_DEEP;
     if (big_ok && t128 >= 1024) return K_BIG;

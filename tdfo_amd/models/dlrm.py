@@ -104,9 +104,8 @@ class DLRMConfig:
     #   embedding update; DCN-v2 default). (Rejected, round 4: the top part on the
     #   embedding stream behind the update, with or without deferred top weight grads:
     #   DLRM-1TB 0.458 / 0.478 vs 0.440 ms/step, profiles/r04/notes.md)
-    bottom_bwd_first: bool = False                 # one GPU: the bottom-MLP backward runs
-    #   before the embedding gradients are handed to the update (uncontended), instead of
-    #   beside the update (where the update's blocks fill every CU)
+    #   (Rejected, round 4: the bottom-MLP backward before the embedding update
+    #   starts, uncontended: 0.48 vs 0.44 ms/step, profiles/r04/notes.md)
     composed_graphs: Optional[bool] = None         # one GPU: chain each stream's graphs with
     #   in-graph event nodes (None: DLRM yes, DCN-v2 no)
     ids_stream: Optional[bool] = None              # one GPU, composed graphs: copy the next

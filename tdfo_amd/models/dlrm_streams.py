@@ -59,20 +59,15 @@ class StreamGraphsMixin:
             emb.backward_wait()
             self._s_emb_update()
 
-        early = self.cfg.bottom_bwd_first and not self._defer_top_wgrad
-
         def m2():
             self._s_top()
-            if early:                        # before ev[2]: E3 starts after it
-                self._s_bottom_bwd()
 
         def m3():
             if self._defer_top_wgrad:
                 self._s_top_wgrad()          # beside the embedding update (E3)
             if split:
                 self._dense_update_range(a, P)
-            if not early:
-                self._s_bottom_bwd()
+            self._s_bottom_bwd()
             if split:
                 self._dense_update_range(0, a)
             else:

@@ -334,15 +334,18 @@ def embedding_bwd_apply(W, row_offset, indices, offsets, grad_off, T, B, grad, g
 
 
 def embedding_dense_update(W, grad, rows, opt, hyper, state1=None, state2=None, eps=1e-8,
-                           beta1=0.9, beta2=0.999, weight_decay=0.0):
+                           beta1=0.9, beta2=0.999, weight_decay=0.0, clear_grad=False):
     """Optimizer step over rows [0, rows) of W from a dense fp32 gradient
-    (data-parallel tables after their gradient all-reduce)."""
+    (data-parallel tables after their gradient all-reduce). ``clear_grad``:
+    zero grad rows [0, rows) as they are read (also on a skipped step)."""
     if _gpu(W):
         _native().embedding_dense_update(W, grad, int(rows), int(opt), state1, state2, hyper, eps,
-                                         beta1, beta2, weight_decay)
+                                         beta1, beta2, weight_decay, bool(clear_grad))
     else:
         ref.embedding_dense_update(W, grad, rows, opt, state1, state2, hyper, eps, beta1, beta2,
                                    weight_decay)
+        if clear_grad:
+            grad.view(-1)[: int(rows) * W.shape[1]].zero_()
 
 
 def rw_bucketize_workspace(n: int, W: int) -> int:

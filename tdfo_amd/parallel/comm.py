@@ -309,6 +309,36 @@ class LoopbackComm(Comm):
         self.modelled_us = 0.0
         self._origin = None
         self._idx = {}
+        self._maps = {}
+        self._rs_tmp = None
+
+    def _copy_pieces(self, src, dst, pieces) -> bool:
+        """dst[b:b+n] = src[a:a+n] for (a, b, n) in pieces (flat elements of
+        one dtype) in one native seg_copy launch over an int64 view, cached per
+        piece list, so the emulated exchanges run no torch kernels. False when
+        not applicable (CPU, misaligned, too many pieces)."""
+        if not src.is_cuda or not pieces or len(pieces) > 4096:
+            return False
+        from .. import ops
+        if not ops.native_available():
+            return False
+        es = src.element_size()
+        if dst.element_size() != es or not (src.is_contiguous() and dst.is_contiguous()):
+            return False
+        if (src.numel() * es) % 8 or (dst.numel() * es) % 8 \
+                or (src.storage_offset() * es) % 8 or (dst.storage_offset() * es) % 8:
+            return False
+        if any((v * es) % 8 for p in pieces for v in p):
+            return False
+        key = (tuple(pieces), es, str(src.device))
+        m = self._maps.get(key)
+        if m is None:
+            if len(self._maps) >= 256:
+                self._maps.clear()
+            m = self._maps[key] = ops.SegmentMap([(a * es // 8, b * es // 8, n * es // 8)
+                                                  for a, b, n in pieces], src.device)
+        m.apply(src.reshape(-1).view(torch.int64), dst.reshape(-1).view(torch.int64))
+        return True
 
     def _model(self, link_bytes: float):
         if self._stream is None or (self.link_gbps <= 0 and self.latency_us <= 0):
@@ -369,7 +399,9 @@ class LoopbackComm(Comm):
         es = inp.element_size()
         with torch.cuda.stream(s) if s is not None else _nullctx():
             if all(n == own.numel() for n in os_):          # one broadcast copy
-                o.view(W, -1).copy_(own.view(1, -1).expand(W, -1))
+                n = own.numel()
+                if not self._copy_pieces(inp, o, [(src0, k * n, n) for k in range(W)]):
+                    o.view(W, -1).copy_(own.view(1, -1).expand(W, -1))
             elif inp.is_floating_point():
                 # values (pooled rows / gradients): only their finiteness
                 # matters downstream -- one contiguous copy of as many bytes as
@@ -388,20 +420,28 @@ class LoopbackComm(Comm):
                     if c > 1 and all(x % c == 0 for x in list(os_) + list(is_) + [src0]):
                         u = c
                         break
-                key = (tuple(os_), src0, own.numel(), u, str(o.device))
-                idx = self._idx.get(key)
-                if idx is None:
-                    n_own = own.numel() // u
-                    parts = [torch.arange(n // u, dtype=torch.int64) % n_own for n in os_]
-                    idx = self._idx[key] = (torch.cat(parts) + src0 // u).to(o.device)
-                torch.index_select(inp.reshape(-1, u), 0, idx, out=o.view(-1, u))
+                n_own, pieces, b = own.numel(), [], 0
+                for n in os_:
+                    for k in range(0, n, n_own):
+                        pieces.append((src0, b + k, min(n_own, n - k)))
+                    b += n
+                if not self._copy_pieces(inp, o, pieces):
+                    key = (tuple(os_), src0, own.numel(), u, str(o.device))
+                    idx = self._idx.get(key)
+                    if idx is None:
+                        n_own = own.numel() // u
+                        parts = [torch.arange(n // u, dtype=torch.int64) % n_own for n in os_]
+                        idx = self._idx[key] = (torch.cat(parts) + src0 // u).to(o.device)
+                    torch.index_select(inp.reshape(-1, u), 0, idx, out=o.view(-1, u))
             self._model(max(sum(is_) - is_[r], sum(os_) - os_[r]) * es)
         return self._end(s, async_op)
 
     def _all_gather(self, out, inp, async_op):
         s = self._begin(inp)
         with torch.cuda.stream(s) if s is not None else _nullctx():
-            out.view(self.world, -1).copy_(inp.view(1, -1).expand(self.world, -1))
+            n = inp.numel()
+            if not self._copy_pieces(inp, out, [(0, k * n, n) for k in range(self.world)]):
+                out.view(self.world, -1).copy_(inp.view(1, -1).expand(self.world, -1))
             self._model(out.numel() * out.element_size() * (self.world - 1) / self.world)
         return self._end(s, async_op)
 
@@ -411,9 +451,17 @@ class LoopbackComm(Comm):
         with torch.cuda.stream(s) if s is not None else _nullctx():
             # reads all W chunks like the real reduction (their sum would
             # scale the values W-fold; this rank's own chunk is kept)
-            tmp = inp.view(self.world, -1)[:, :n].sum(0, dtype=torch.float32)
-            out.view(-1).copy_(inp.view(-1)[self.rank * n: (self.rank + 1) * n])
-            del tmp
+            from .. import ops
+            if inp.is_cuda and inp.dtype == torch.float32 and ops.native_available() \
+                    and inp.numel() == self.world * n:
+                if self._rs_tmp is None or self._rs_tmp.numel() < n:
+                    self._rs_tmp = torch.empty(n, dtype=torch.float32, device=inp.device)
+                ops.slab_reduce([(inp, self.world, self._rs_tmp[:n])])
+            else:
+                tmp = inp.view(self.world, -1)[:, :n].sum(0, dtype=torch.float32)
+                del tmp
+            if not self._copy_pieces(inp, out, [(self.rank * n, 0, n)]):
+                out.view(-1).copy_(inp.view(-1)[self.rank * n: (self.rank + 1) * n])
             self._model(inp.numel() * inp.element_size() * (self.world - 1) / self.world)
         return self._end(s, async_op)
 

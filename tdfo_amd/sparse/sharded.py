@@ -310,6 +310,7 @@ class ShardedEmbeddingBags:
             if self.dp_dense:
                 self.dp_dgrad = torch.zeros(self.dp_store.total_rows, D, dtype=torch.float32,
                                             device=self.device)
+                self._dp_clean = True
             elif W > 1:
                 # large replicated tables: all-gather ids + pooled grads, and
                 # every rank applies the identical global-batch sparse update
@@ -710,7 +711,9 @@ class ShardedEmbeddingBags:
             from .. import ops
             d_recv = self.d_recv if d_recv is None else d_recv
             st = self.dp_store
-            self.dp_dgrad.zero_()
+            if not self._dp_clean:             # the dense update zeroes it as it reads
+                self.dp_dgrad.zero_()
+            self._dp_clean = False
             ops.embedding_bwd(st.weight, st.row_offset, self.dp_ids, self.dp_offsets,
                               self.dp_out_off, len(self.dp_tables), self.B, d_recv,
                               self.dp_width, ops.EMB_DENSE_GRAD, hyper, key_bits=st.key_bits,
@@ -820,7 +823,8 @@ class ShardedEmbeddingBags:
                 ops.embedding_dense_update(st.weight, self.dp_dgrad, st.total_rows, o.code, hyper,
                                            state1=st.state1, state2=st.state2, eps=o.eps,
                                            beta1=o.beta1, beta2=o.beta2,
-                                           weight_decay=o.weight_decay)
+                                           weight_decay=o.weight_decay, clear_grad=True)
+                self._dp_clean = True
             elif W > 1:
                 self.dp_store.backward_update(self.dp_g_ids_t, self.dp_g_offsets,
                                               self.dp_store.row_offset, ndp, W * B, self.dp_g_grad,

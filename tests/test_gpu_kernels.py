@@ -449,15 +449,14 @@ def test_dlrm_step_matches_cpu():
 
 
 @pytest.mark.parametrize("staged,one", [(False, "0"), (False, "1"), (False, "ids0"),
-                                        (True, "0"), (False, "defer"), (False, "botfirst")])
+                                        (True, "0"), (False, "defer")])
 def test_dlrm_graph_replay_matches_eager(staged, one):
     """Graph-replayed steps match eager ones: per-stream graphs (one=1: each
     stream's step as composed graphs joined by in-graph event nodes, with
     device-resident batches whose ids are copied on a third stream behind the
     sort; ids0: without that stream; defer: as 1, with the top weight grads
-    after the interaction backward; botfirst: as 1, with the bottom-MLP
-    backward before the embedding-update event) and the staged multi-rank
-    capture at one rank."""
+    after the interaction backward) and the staged multi-rank capture at one
+    rank."""
     import dataclasses
 
     from tdfo_amd.data.synthetic import SyntheticCriteo
@@ -465,11 +464,10 @@ def test_dlrm_graph_replay_matches_eager(staged, one):
 
     cfg = DLRMConfig(embedding_dim=128, table_rows=[1000, 20, 5000], bottom=[128],
                      top=[256, 1], composed_graphs=one != "0",
-                     ids_stream=one in ("1", "defer", "botfirst"))
+                     ids_stream=one in ("1", "defer"))
     B = 512
     a = DLRMTrainer(cfg, B, DEV)
-    cfg_b = dataclasses.replace(cfg, defer_wgrad=True if one == "defer" else None,
-                                bottom_bwd_first=one == "botfirst")
+    cfg_b = dataclasses.replace(cfg, defer_wgrad=True if one == "defer" else None)
     b = DLRMTrainer(cfg_b, B, DEV)
     data = SyntheticCriteo(cfg.table_rows, B, device=DEV, seed=4)
     batches = [data.next() for _ in range(6)]
@@ -479,7 +477,7 @@ def test_dlrm_graph_replay_matches_eager(staged, one):
     b.capture_graph(warmup=1, staged=staged)
     if not staged:
         assert b.graph == "streams" and ("M" in b._ms["graphs"]) == (one != "0")
-        assert (b._ms["cstream"] is not None) == (one in ("1", "defer", "botfirst"))
+        assert (b._ms["cstream"] is not None) == (one in ("1", "defer"))
     if staged:
         # one rank: the prep stage is a no-op and is not captured (no empty graph)
         assert all(kind in ("m", "em", "j") or g[0] is not None for kind, g in b.graph)
