@@ -602,13 +602,13 @@ __device__ __forceinline__ void update_row(const EmbBwdArgs& a, const OptScalars
 // flow between the loads (hipcc keeps all of them in flight); runs are then
 // reduced in registers in sorted order and each run that finishes inside the
 // chunk gets exactly one optimizer update.
-template <int D, typename K, bool GB, int OPT>
+template <int D, typename K, bool GB, int OPT, int CH>
 __global__ __launch_bounds__(256) void emb_chunk_kernel(
     EmbBwdArgs a, const K* __restrict__ keys, const int32_t* __restrict__ vals,
     const int64_t* __restrict__ goff, const float* __restrict__ gscale,
     float* __restrict__ head, float* __restrict__ tail, int32_t* __restrict__ tail_list,
     int32_t* __restrict__ tail_count) {
-  constexpr int EPL = BwdCfg<D>::EPL, CH = BwdCfg<D>::CH;
+  constexpr int EPL = BwdCfg<D>::EPL;
   constexpr bool NEED_W = OPT != EMB_DENSE_GRAD;
   const int lane = threadIdx.x & 63;
   if (skip_step(a)) return;
@@ -692,12 +692,12 @@ __global__ __launch_bounds__(256) void emb_chunk_kernel(
 // Runs crossing chunk edges: the chunk where a run starts adds the head
 // partials of the chunks the run covers (found by binary search), in chunk
 // order with 8 loads in flight, and applies the optimizer once.
-template <int D, typename K, int OPT>
+template <int D, typename K, int OPT, int CH>
 __global__ __launch_bounds__(256) void emb_combine_kernel(
     EmbBwdArgs a, const K* __restrict__ keys, const float* __restrict__ head,
     const float* __restrict__ tail, const int32_t* __restrict__ tail_list,
     const int32_t* __restrict__ tail_count) {
-  constexpr int EPL = BwdCfg<D>::EPL, CH = BwdCfg<D>::CH;
+  constexpr int EPL = BwdCfg<D>::EPL;
   const int lane = threadIdx.x & 63;
   const int nw = (gridDim.x * blockDim.x) >> 6;
   if (skip_step(a)) return;
@@ -892,9 +892,22 @@ inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
 
 int ch_for(int D) { return D <= 128 ? 32 : (D == 256 ? 16 : 8); }
 
+// Lean update (TDFO_EMB_LEAN=1, A/B): half-size chunks, so a wave holds half
+// the rows in registers -- few enough VGPRs that one update wave per SIMD fits
+// beside a 256x128 GEMM block (2 x 196 VGPRs) when the update grid is capped
+// (TDFO_EMB_CHUNK_GRID), instead of the two kernels excluding each other per CU
+bool emb_lean() {
+  static const bool v = [] {
+    const char* e = getenv("TDFO_EMB_LEAN");
+    return e && atoi(e) != 0;
+  }();
+  return v;
+}
+
 WsLayout ws_layout(int64_t nnz, int D) {
   WsLayout L;
-  const int64_t nch = (nnz + ch_for(D) - 1) / ch_for(D);
+  const int ch = ch_for(D) / 2;            // the smaller (lean) chunk: most chunks
+  const int64_t nch = (nnz + ch - 1) / ch;
   size_t o = 0;
   L.keys_in = o;  o += al(nnz * 8);
   L.keys_out = o; o += al(nnz * 8);
@@ -983,22 +996,27 @@ void apply_impl(const EmbBwdArgs& a0, const WsLayout& L, hipStream_t s) {
   float* tail = (float*)(ws + L.tail);
   int32_t* tlist = (int32_t*)(ws + L.tlist);
   int32_t* tcount = (int32_t*)(ws + L.tcount);
-  constexpr int CH = BwdCfg<D>::CH;
-  const int64_t nch = (a.nnz + CH - 1) / CH;
-  int64_t blocks = (nch + 3) / 4;
-  if (chunk_grid_cap() > 0 && blocks > chunk_grid_cap()) blocks = chunk_grid_cap();
-  if (a.grad_bf16)
-    hipLaunchKernelGGL((emb_chunk_kernel<D, K, true, OPT>), dim3(blocks), dim3(256), 0, s, a,
-                       keys_out, vals_out, goff, gscale, head, tail, tlist, tcount);
-  else
-    hipLaunchKernelGGL((emb_chunk_kernel<D, K, false, OPT>), dim3(blocks), dim3(256), 0, s, a,
-                       keys_out, vals_out, goff, gscale, head, tail, tlist, tcount);
-  TDFO_CHECK_HIP(hipGetLastError());
-  int64_t cblocks = (nch + 3) / 4;
-  if (cblocks > 1024) cblocks = 1024;
-  hipLaunchKernelGGL((emb_combine_kernel<D, K, OPT>), dim3(cblocks), dim3(256), 0, s, a,
-                     keys_out, head, tail, tlist, tcount);
-  TDFO_CHECK_HIP(hipGetLastError());
+  auto run = [&](auto ch_c) {
+    constexpr int CH = decltype(ch_c)::value;
+    const int64_t nch = (a.nnz + CH - 1) / CH;
+    int64_t blocks = (nch + 3) / 4;
+    if (chunk_grid_cap() > 0 && blocks > chunk_grid_cap()) blocks = chunk_grid_cap();
+    if (a.grad_bf16)
+      hipLaunchKernelGGL((emb_chunk_kernel<D, K, true, OPT, CH>), dim3(blocks), dim3(256), 0, s, a,
+                         keys_out, vals_out, goff, gscale, head, tail, tlist, tcount);
+    else
+      hipLaunchKernelGGL((emb_chunk_kernel<D, K, false, OPT, CH>), dim3(blocks), dim3(256), 0, s,
+                         a, keys_out, vals_out, goff, gscale, head, tail, tlist, tcount);
+    TDFO_CHECK_HIP(hipGetLastError());
+    int64_t cblocks = (nch + 3) / 4;
+    if (cblocks > 1024) cblocks = 1024;
+    hipLaunchKernelGGL((emb_combine_kernel<D, K, OPT, CH>), dim3(cblocks), dim3(256), 0, s, a,
+                       keys_out, head, tail, tlist, tcount);
+    TDFO_CHECK_HIP(hipGetLastError());
+  };
+  constexpr int CH0 = BwdCfg<D>::CH;
+  if (emb_lean() && CH0 >= 16) run(std::integral_constant<int, CH0 / 2>{});
+  else run(std::integral_constant<int, CH0>{});
 }
 
 template <int D, typename K>
