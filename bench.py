@@ -60,6 +60,11 @@ def parse(argv=None):
     ap.add_argument("--defer-wgrad", default=None, choices=["0", "1"],
                     help="top / cross weight grads after the interaction / cross backward "
                          "(DLRMConfig.defer_wgrad; default: when N > 1)")
+    ap.add_argument("--stream-sync", default="event", choices=["event", "value"],
+                    help="one GPU: cross-stream hand-offs as event nodes or signal-memory value "
+                         "waits (DLRMConfig.stream_sync)")
+    ap.add_argument("--graph-steps", type=int, default=1,
+                    help="one GPU, --stream-sync value, --data instep: steps per graph launch")
     ap.add_argument("--dense-comm", default="fp32", choices=["fp32", "bf16"],
                     help="N > 1: wire format of the dense-gradient all-reduce")
     ap.add_argument("--no-pipeline", action="store_true",
@@ -151,7 +156,8 @@ def _cfg(args, rows, pipe):
     kw = dict(table_rows=list(rows), sharding=args.sharding, pipeline=pipe,
               dense_comm=args.dense_comm, stream_graphs=not args.no_stream_graphs,
               opt_placement=args.opt_placement,
-              defer_wgrad=None if args.defer_wgrad is None else args.defer_wgrad == "1")
+              defer_wgrad=None if args.defer_wgrad is None else args.defer_wgrad == "1",
+              stream_sync=args.stream_sync, graph_steps=args.graph_steps)
     if args.model == "dlrm":
         return DLRMConfig(**kw)
     return DLRMConfig(interaction="dcn", pooling=list(MLPERF_MULTIHOT),
