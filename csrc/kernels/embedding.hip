@@ -80,23 +80,21 @@ __global__ __launch_bounds__(256) void emb_fwd_onehot_kernel(EmbFwdArgs a) {
 // chunk's ids are loaded while this chunk's rows are in flight. Groups of a
 // wave with different bag lengths run the wave-uniform maximum trip count,
 // predicated per group.
-#ifndef TDFO_EMB_RIF
-#define TDFO_EMB_RIF 4
-#endif
 __device__ __forceinline__ void emb_wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <int D, bool OUT_BF16>
+template <int D, bool OUT_BF16, int RIF>
 __global__ __launch_bounds__(256) void emb_fwd_kernel(EmbFwdArgs a) {
   constexpr int LPB = (D / 4) < 64 ? (D / 4) : 64;  // lanes per bag
   constexpr int BPW = 64 / LPB;                     // bags per wave
   constexpr int NCP = D / (4 * LPB);                // float4 column passes per lane
   constexpr int CH = 64;                            // ids staged per bag per chunk
   constexpr int IPL = (CH + LPB - 1) / LPB;         // staging loads per lane
-  constexpr int RIF = TDFO_EMB_RIF;                 // row gathers in flight per lane
+  // RIF: row gathers in flight per lane (a 100-id bag is ~100 / RIF dependent
+  // round trips; TDFO_EMB_RIF picks 4 / 8 / 16 for A/B)
   __shared__ int64_t s_ids[4][BPW][CH];
   __shared__ float s_w[4][BPW][CH];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -1039,9 +1037,18 @@ void bwd_dispatch(const EmbBwdArgs& a, const WsLayout& L, hipStream_t s) {
 
 }  // namespace
 
+int emb_rif() {
+  static const int v = [] {
+    const char* e = getenv("TDFO_EMB_RIF");
+    return e ? atoi(e) : 4;
+  }();
+  return v;
+}
+
 void embedding_bag_fwd(const EmbFwdArgs& a, hipStream_t s) {
   const int64_t nbags = (int64_t)a.T * a.B;
   if (nbags == 0) return;
+  const int rif = emb_rif();
   const int lpb = a.D / 4 < 64 ? a.D / 4 : 64;
   const int64_t waves = (nbags * lpb + 63) / 64;
   int64_t blocks = (waves + 3) / 4;
@@ -1052,9 +1059,19 @@ void embedding_bag_fwd(const EmbFwdArgs& a, hipStream_t s) {
                                        dim3(blocks), dim3(256), 0, s, a);      \
     else hipLaunchKernelGGL((emb_fwd_onehot_kernel<DD, false>), dim3(blocks),  \
                             dim3(256), 0, s, a);                               \
-  } else if (a.out_bf16) hipLaunchKernelGGL((emb_fwd_kernel<DD, true>),        \
+  } else if (rif == 8) {                                                       \
+    if (a.out_bf16) hipLaunchKernelGGL((emb_fwd_kernel<DD, true, 8>), dim3(blocks), \
+                                       dim3(256), 0, s, a);                    \
+    else hipLaunchKernelGGL((emb_fwd_kernel<DD, false, 8>), dim3(blocks),      \
+                            dim3(256), 0, s, a);                               \
+  } else if (rif == 16) {                                                      \
+    if (a.out_bf16) hipLaunchKernelGGL((emb_fwd_kernel<DD, true, 16>), dim3(blocks), \
+                                       dim3(256), 0, s, a);                    \
+    else hipLaunchKernelGGL((emb_fwd_kernel<DD, false, 16>), dim3(blocks),     \
+                            dim3(256), 0, s, a);                               \
+  } else if (a.out_bf16) hipLaunchKernelGGL((emb_fwd_kernel<DD, true, 4>),     \
                                             dim3(blocks), dim3(256), 0, s, a); \
-  else hipLaunchKernelGGL((emb_fwd_kernel<DD, false>), dim3(blocks),           \
+  else hipLaunchKernelGGL((emb_fwd_kernel<DD, false, 4>), dim3(blocks),        \
                           dim3(256), 0, s, a)
   switch (a.D) {
     case 16: TDFO_EF(16); break;
@@ -1065,6 +1082,7 @@ void embedding_bag_fwd(const EmbFwdArgs& a, hipStream_t s) {
     case 512: TDFO_EF(512); break;
   }
 #undef TDFO_EF
+  TDFO_CHECK_HIP(hipGetLastError());
 }
 
 int embedding_segsort(int v) {
