@@ -221,13 +221,31 @@ def measure(args, info, cfg, world: int, group, rank: int) -> dict:
     mb = tr.emb._rw_mbox
     wait0 = mb.wait_s if mb is not None else 0.0
     grows0 = tr.emb.rw_grows if tr.emb.rw_tables else 0
+    curve = int(os.environ.get("TDFO_BENCH_CURVE", "0"))
+    marks = []
     t = time.perf_counter()
-    loop.run(args.steps)
+    if curve > 0:
+        # diagnostics: device time of every `curve` timed steps (events on the
+        # current stream between launches), to stderr
+        for k in range(0, args.steps, curve):
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            marks.append(e)
+            loop.run(min(curve, args.steps - k))
+        e = torch.cuda.Event(enable_timing=True)
+        e.record()
+        marks.append(e)
+    else:
+        loop.run(args.steps)
     host_s = time.perf_counter() - t          # issue time (the device runs behind)
     torch.cuda.synchronize()
     if info.world_size > 1:
         torch.distributed.barrier()
     el = time.perf_counter() - t
+    if marks:
+        ms_w = [round(a.elapsed_time(b) / curve, 4) for a, b in zip(marks, marks[1:])]
+        print(json.dumps({"ms_per_step_windows": ms_w, "window": curve}), file=sys.stderr,
+              flush=True)
     if wd is not None:
         wd.close()
     if info.world_size > 1:

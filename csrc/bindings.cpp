@@ -652,6 +652,9 @@ int64_t graph_compose(std::vector<int64_t> kinds, std::vector<int64_t> handles,
       }
       hipBatchMemOpNodeParams np;
       std::memset(&np, 0, sizeof(np));
+      hipCtx_t ctx = nullptr;
+      (void)hipCtxGetCurrent(&ctx);
+      np.ctx = ctx;
       np.count = 1;
       np.paramArray = &op;
       TDFO_HIP_OK(hipGraphAddBatchMemOpNode(&n, g, dep, nd, &np));

@@ -613,7 +613,7 @@ __global__ __launch_bounds__(256) void emb_chunk_kernel(
   const OptScalars o = opt_scalars(a);
   const int64_t nch = (a.nnz + CH - 1) / CH;
   const int64_t nwv = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  // one wave per chunk; a capped grid (chunk_grid_cap) walks the chunks
+  // one wave per chunk (grid-stride: any grid size walks every chunk)
   for (int64_t c = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; c < nch; c += nwv) {
   const int64_t start = c * CH;
   const int64_t end = min(start + (int64_t)CH, a.nnz);
@@ -869,16 +869,11 @@ void dense_update_dispatch(const EmbBwdArgs& a, int64_t rows, const float* g, fl
 
 int g_emb_segsort = 1;   // one-hot batches: per-table LDS sort (0: device-wide radix sort)
 
-// A/B knob: cap on the fused update's grid (blocks of 4 chunk waves; 0 = one
-// wave per chunk), so a long multi-hot update leaves CUs to GEMMs beside it
-// (TDFO_EMB_CHUNK_GRID)
-int64_t chunk_grid_cap() {
-  static const int64_t v = [] {
-    const char* e = getenv("TDFO_EMB_CHUNK_GRID");
-    return e ? (int64_t)atoll(e) : (int64_t)0;
-  }();
-  return v;
-}
+// (Rejected, round 4: capping the fused update's grid so GEMM blocks get CUs
+// beside it, with the full or a half-chunk 94-VGPR update kernel that fits
+// next to a 256x128 GEMM block: DCN-v2 2.62-2.99 vs 2.37 ms/step, DLRM-1TB
+// 0.465-0.496 vs 0.453-0.458; half chunks alone 2.40-2.42 / 0.454-0.457,
+// profiles/r04/notes.md)
 
 struct WsLayout {
   size_t keys_in, keys_out, vals_in, vals_out, goff, gscale, head, tail, tlist, tcount, sortws,
@@ -890,22 +885,9 @@ inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
 
 int ch_for(int D) { return D <= 128 ? 32 : (D == 256 ? 16 : 8); }
 
-// Lean update (TDFO_EMB_LEAN=1, A/B): half-size chunks, so a wave holds half
-// the rows in registers -- few enough VGPRs that one update wave per SIMD fits
-// beside a 256x128 GEMM block (2 x 196 VGPRs) when the update grid is capped
-// (TDFO_EMB_CHUNK_GRID), instead of the two kernels excluding each other per CU
-bool emb_lean() {
-  static const bool v = [] {
-    const char* e = getenv("TDFO_EMB_LEAN");
-    return e && atoi(e) != 0;
-  }();
-  return v;
-}
-
 WsLayout ws_layout(int64_t nnz, int D) {
   WsLayout L;
-  const int ch = ch_for(D) / 2;            // the smaller (lean) chunk: most chunks
-  const int64_t nch = (nnz + ch - 1) / ch;
+  const int64_t nch = (nnz + ch_for(D) - 1) / ch_for(D);
   size_t o = 0;
   L.keys_in = o;  o += al(nnz * 8);
   L.keys_out = o; o += al(nnz * 8);
@@ -998,7 +980,6 @@ void apply_impl(const EmbBwdArgs& a0, const WsLayout& L, hipStream_t s) {
     constexpr int CH = decltype(ch_c)::value;
     const int64_t nch = (a.nnz + CH - 1) / CH;
     int64_t blocks = (nch + 3) / 4;
-    if (chunk_grid_cap() > 0 && blocks > chunk_grid_cap()) blocks = chunk_grid_cap();
     if (a.grad_bf16)
       hipLaunchKernelGGL((emb_chunk_kernel<D, K, true, OPT, CH>), dim3(blocks), dim3(256), 0, s, a,
                          keys_out, vals_out, goff, gscale, head, tail, tlist, tcount);
@@ -1012,9 +993,7 @@ void apply_impl(const EmbBwdArgs& a0, const WsLayout& L, hipStream_t s) {
                        keys_out, head, tail, tlist, tcount);
     TDFO_CHECK_HIP(hipGetLastError());
   };
-  constexpr int CH0 = BwdCfg<D>::CH;
-  if (emb_lean() && CH0 >= 16) run(std::integral_constant<int, CH0 / 2>{});
-  else run(std::integral_constant<int, CH0>{});
+  run(std::integral_constant<int, BwdCfg<D>::CH>{});
 }
 
 template <int D, typename K>

@@ -1,9 +1,12 @@
 #!/usr/bin/env python
 """Per-segment device timeline of the multi-rank stream graphs (emulated
-rank 0 of W, modelled links): stamps around every captured segment, printed
-per step in us from the step's M1 start."""
+rank RANK of W, modelled links GBPS per rank): stamps around every captured
+segment, printed per step in us from the step's M1 start; with HOST=1 also
+when the host launched each step (host clock mapped onto the device clock by
+a stamp taken right after a synchronize)."""
 import os
 import sys
+import time
 
 import torch
 
@@ -18,23 +21,35 @@ def main():
     assert _ext.load()
     dev = torch.device("cuda", 0)
     W = int(os.environ.get("W", 8))
-    gbps = float(os.environ.get("GBPS", 300))
+    R = int(os.environ.get("RANK_EMU", 0))
+    gbps = float(os.environ.get("GBPS", min(W - 1, 7) * 153.0))
     cfg = DLRMConfig(table_rows=list(CRITEO_1TB_ROWS), pipeline=True)
     cfg.ids_stream = False
-    tr = DLRMTrainer(cfg, 8192, dev, group=LoopbackComm(W, 0, dev, gbps, 10.0), rank=0,
+    tr = DLRMTrainer(cfg, 8192, dev, group=LoopbackComm(W, R, dev, gbps, 10.0), rank=R,
                      world_size=W)
     steps = 12
     nseg = 16
     buf = torch.zeros((steps + 4) * nseg * 2, dtype=torch.int64, device=dev)
     cnt = torch.zeros(nseg, dtype=torch.int64, device=dev)
     tr._mr_stamp = (buf, cnt)
-    src = make_source(cfg.table_rows, 8192, dev, cfg.pooling_factors(), 1, 0, kind="fresh")
+    src = make_source(cfg.table_rows, 8192, dev, cfg.pooling_factors(), 1, R, kind="fresh")
     loop = StepLoop(tr, src)
     loop.run(4)
     tr.capture_graph(warmup=0)
     torch.cuda.synchronize()
-    loop.run(steps)
+    # host -> device clock: a stamp right after a synchronize ~ now
+    from tdfo_amd import ops
+    cal = torch.zeros(4, dtype=torch.int64, device=dev)
+    ccnt = torch.zeros(1, dtype=torch.int64, device=dev)
+    h0 = time.perf_counter()
+    ops.stamp(cal, ccnt, 0, 1, 0)
     torch.cuda.synchronize()
+    host = []
+    for _ in range(steps):
+        host.append(time.perf_counter())
+        loop.run(1)
+    torch.cuda.synchronize()
+    d0 = int(cal[0].item())
     names = tr._mr["names"]
     n = len(names)
     b = buf[: steps * n * 2].view(steps, n, 2).cpu()
@@ -43,7 +58,9 @@ def main():
         row = [f"{nm}:{(int(b[s, i, 0]) - t0) / 100:.0f}-{(int(b[s, i, 1]) - t0) / 100:.0f}"
                for i, nm in enumerate(names)]
         nxt = (int(b[s + 1, names.index("M1"), 0]) - t0) / 100 if s + 1 < steps else float("nan")
-        print(f"step {s} (period {nxt:.0f} us): " + "  ".join(row), flush=True)
+        hl = ((host[s] - h0) * 1e6 - (t0 - d0) / 100) if os.environ.get("HOST") else None
+        hs = f" host launch {hl:+.0f} us vs M1 start" if hl is not None else ""
+        print(f"step {s} (period {nxt:.0f} us){hs}: " + "  ".join(row), flush=True)
 
 
 if __name__ == "__main__":

@@ -57,6 +57,7 @@ def main():
             ops.stamp(buf, cnt, 1, 2, 1)
         torch.cuda.synchronize()
     out["eager_event_us"] = lat(buf)
+    print(json.dumps(out), flush=True)
 
     # eager value flags (consumer enqueued first: it must wait for the write)
     buf, cnt = fresh(dev)
@@ -73,6 +74,7 @@ def main():
             f.write(k)
         torch.cuda.synchronize()
     out["eager_value_us"] = lat(buf)
+    print(json.dumps(out), flush=True)
 
     # graphs: producer [spin, stamps] + signal, consumer wait + [stamps]
     def capture(fn, stream):
@@ -97,6 +99,7 @@ def main():
             C.replay()
         torch.cuda.synchronize()
     out["graph_event_us"] = lat(buf)
+    print(json.dumps(out), flush=True)
 
     # graphs with value nodes, consumer launched first; the consumer resets
     # the flag after its wait (the next producer write follows it)
@@ -105,8 +108,19 @@ def main():
                            ops.stamp(buf2, cnt2, 0, 2, 1)), s1)
     gc2 = capture(lambda: (ops.stamp(buf2, cnt2, 1, 2, 0), ops.stamp(buf2, cnt2, 1, 2, 1)), s2)
     f2 = ops.SignalFlag()
-    P2 = ops.ComposedGraph([("graph", gp2), ("writeval", (f2, 1))])
-    C2 = ops.ComposedGraph([("waitval", (f2, 1)), ("writeval", (f2, 0)), ("graph", gc2)])
+    try:
+        P2 = ops.ComposedGraph([("graph", gp2), ("writeval", (f2, 1))])
+        C2 = ops.ComposedGraph([("waitval", (f2, 1)), ("writeval", (f2, 0)), ("graph", gc2)])
+        out["value_nodes"] = "explicit"
+    except RuntimeError as e:
+        out["memop_node_error"] = str(e)[:200]
+        # the same operations stream-captured into child graphs instead
+        gw = capture(lambda: f2.write(1), s1)
+        gq = capture(lambda: (f2.wait(1), f2.write(0)), s2)
+        P2 = ops.ComposedGraph([("graph", gp2), ("graph", gw)])
+        C2 = ops.ComposedGraph([("graph", gq), ("graph", gc2)])
+        out["value_nodes"] = "captured"
+    print(json.dumps(out), flush=True)
     cnt2.zero_()
     torch.cuda.synchronize()
     for k in range(N):
