@@ -193,6 +193,8 @@ def measure(args, info, cfg, world: int, group, rank: int) -> dict:
     # W untimed warm-up steps in all: eager ones, one inside the capture, and
     # two replays of the fresh graph (its first launches upload it)
     post = 2 if use_graph and args.warmup >= 4 else 0
+    if use_graph and os.environ.get("TDFO_BENCH_POST"):     # diagnostics: more replays
+        post = max(0, min(int(os.environ["TDFO_BENCH_POST"]), args.warmup - 1))
     loop.run(args.warmup - (1 + post if use_graph else 0))
     # one eager step's collectives (a whole-step graph issues none from the host)
     step_stats = None

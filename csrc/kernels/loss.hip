@@ -250,16 +250,34 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(SlabReduceArgs a) {
   const int64_t total = a.start[a.nseg];
   for (int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; q < total;
        q += (int64_t)gridDim.x * blockDim.x) {
-    int k = 0;
-    while (k + 1 < a.nseg && q >= a.start[k + 1]) ++k;
-    const SlabSeg& g = a.seg[k];
-    const int64_t j = (q - a.start[k]) * 4;
-    float4 acc = *(const float4*)(g.in + j);
-    for (int r = 1; r < g.S; ++r) {
-      const float4 v = *(const float4*)(g.in + (int64_t)r * g.n + j);
-      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    // the segment by wave-uniform-ish selects over the kernel-argument table
+    // (a dynamically indexed table compiles to dependent loads)
+    const float* in = a.seg[0].in;
+    float* out = a.seg[0].out;
+    int64_t n = a.seg[0].n, s0 = 0;
+    int S = a.seg[0].S;
+#pragma unroll
+    for (int k = 1; k < SLAB_MAX_SEGS; ++k) {
+      const bool here = k < a.nseg && q >= a.start[k];
+      in = here ? a.seg[k].in : in;
+      out = here ? a.seg[k].out : out;
+      n = here ? a.seg[k].n : n;
+      S = here ? a.seg[k].S : S;
+      s0 = here ? a.start[k] : s0;
     }
-    *(float4*)(g.out + j) = acc;
+    const int64_t j = (q - s0) * 4;
+    float4 acc = *(const float4*)(in + j);
+    // slabs 1.. in order, 8 loads in flight (clamped addresses: no branch
+    // around a load), so an S-way split is not S dependent round trips
+    for (int r0 = 1; r0 < S; r0 += 8) {
+      float4 t[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) t[u] = *(const float4*)(in + (int64_t)min(r0 + u, S - 1) * n + j);
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (r0 + u < S) { acc.x += t[u].x; acc.y += t[u].y; acc.z += t[u].z; acc.w += t[u].w; }
+    }
+    *(float4*)(out + j) = acc;
   }
 }
 

@@ -133,8 +133,31 @@ def main():
     b = buf2.cpu().view(-1, 2, 2)
     out["graph_value_order_ok"] = all(int(b[k, 1, 0]) >= int(b[k, 0, 1]) for k in range(N))
 
-    # back-to-back step-like chain: two producer/consumer pairs per launch
-    out["device_attr_wait_value"] = None
+    # the same operations stream-captured into child graphs
+    buf3, cnt3 = fresh(dev)
+    gp3 = capture(lambda: (ops.spin_us(50.0), ops.stamp(buf3, cnt3, 0, 2, 0),
+                           ops.stamp(buf3, cnt3, 0, 2, 1)), s1)
+    gc3 = capture(lambda: (ops.stamp(buf3, cnt3, 1, 2, 0), ops.stamp(buf3, cnt3, 1, 2, 1)), s2)
+    f3 = ops.SignalFlag()
+    try:
+        gw = capture(lambda: f3.write(1), s1)
+        gq = capture(lambda: (f3.wait(1), f3.write(0)), s2)
+        P3 = ops.ComposedGraph([("graph", gp3), ("graph", gw)])
+        C3 = ops.ComposedGraph([("graph", gq), ("graph", gc3)])
+        cnt3.zero_()
+        torch.cuda.synchronize()
+        for k in range(N):
+            with torch.cuda.stream(s2):
+                C3.replay()
+            with torch.cuda.stream(s1):
+                P3.replay()
+            torch.cuda.synchronize()
+        out["captured_value_us"] = lat(buf3)
+        b = buf3.cpu().view(-1, 2, 2)
+        out["captured_value_order_ok"] = all(int(b[k, 1, 0]) >= int(b[k, 0, 1])
+                                             for k in range(N))
+    except RuntimeError as e:
+        out["captured_value_error"] = str(e)[:200]
     print(json.dumps(out), flush=True)
 
 
