@@ -60,11 +60,9 @@ def parse(argv=None):
     ap.add_argument("--defer-wgrad", default=None, choices=["0", "1"],
                     help="top / cross weight grads after the interaction / cross backward "
                          "(DLRMConfig.defer_wgrad; default: when N > 1)")
-    ap.add_argument("--stream-sync", default="event", choices=["event", "value"],
-                    help="one GPU: cross-stream hand-offs as event nodes or signal-memory value "
-                         "waits (DLRMConfig.stream_sync)")
-    ap.add_argument("--graph-steps", type=int, default=1,
-                    help="one GPU, --stream-sync value, --data instep: steps per graph launch")
+    ap.add_argument("--dp-lookup-stream", default="D", choices=["D", "EC"],
+                    help="N > 1: stream of the replicated tables' next-batch lookup "
+                         "(DLRMConfig.dp_lookup_stream)")
     ap.add_argument("--dense-comm", default="fp32", choices=["fp32", "bf16"],
                     help="N > 1: wire format of the dense-gradient all-reduce")
     ap.add_argument("--no-pipeline", action="store_true",
@@ -157,7 +155,7 @@ def _cfg(args, rows, pipe):
               dense_comm=args.dense_comm, stream_graphs=not args.no_stream_graphs,
               opt_placement=args.opt_placement,
               defer_wgrad=None if args.defer_wgrad is None else args.defer_wgrad == "1",
-              stream_sync=args.stream_sync, graph_steps=args.graph_steps)
+              dp_lookup_stream=args.dp_lookup_stream)
     if args.model == "dlrm":
         return DLRMConfig(**kw)
     return DLRMConfig(interaction="dcn", pooling=list(MLPERF_MULTIHOT),
@@ -229,11 +227,14 @@ def measure(args, info, cfg, world: int, group, rank: int) -> dict:
     if curve > 0:
         # diagnostics: device time of every `curve` timed steps (events on the
         # current stream between launches), to stderr
+        hmarks = []
         for k in range(0, args.steps, curve):
             e = torch.cuda.Event(enable_timing=True)
             e.record()
             marks.append(e)
+            hmarks.append(time.perf_counter())
             loop.run(min(curve, args.steps - k))
+        hmarks.append(time.perf_counter())
         e = torch.cuda.Event(enable_timing=True)
         e.record()
         marks.append(e)
@@ -246,8 +247,9 @@ def measure(args, info, cfg, world: int, group, rank: int) -> dict:
     el = time.perf_counter() - t
     if marks:
         ms_w = [round(a.elapsed_time(b) / curve, 4) for a, b in zip(marks, marks[1:])]
-        print(json.dumps({"ms_per_step_windows": ms_w, "window": curve}), file=sys.stderr,
-              flush=True)
+        host_w = [round((b - a) * 1e3 / curve, 4) for a, b in zip(hmarks, hmarks[1:])]
+        print(json.dumps({"ms_per_step_windows": ms_w, "host_ms_per_step_windows": host_w,
+                          "window": curve}), file=sys.stderr, flush=True)
     if wd is not None:
         wd.close()
     if info.world_size > 1:

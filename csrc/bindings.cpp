@@ -682,6 +682,10 @@ void graph_exec_launch(int64_t ex) {
   TDFO_HIP_OK(hipGraphLaunch(reinterpret_cast<hipGraphExec_t>(ex), cur_stream()));
 }
 
+void graph_exec_upload(int64_t ex) {
+  TDFO_HIP_OK(hipGraphUpload(reinterpret_cast<hipGraphExec_t>(ex), cur_stream()));
+}
+
 void graph_exec_destroy(int64_t ex) {
   TDFO_HIP_OK(hipGraphExecDestroy(reinterpret_cast<hipGraphExec_t>(ex)));
 }
@@ -1427,6 +1431,7 @@ TORCH_LIBRARY(tdfo, m) {
   m.def("stream_write_value(int p, int value) -> ()", stream_write_value);
   m.def("graph_exec_launch(int ex) -> ()", graph_exec_launch);
   m.def("graph_exec_destroy(int ex) -> ()", graph_exec_destroy);
+  m.def("graph_exec_upload(int ex) -> ()", graph_exec_upload);
   m.def("gemm_batch_begin() -> ()", gemm_batch_begin);
   m.def("gemm_batch_end() -> ()", gemm_batch_end);
   m.def("gemm_pairing(int v) -> int",

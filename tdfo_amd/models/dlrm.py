@@ -110,11 +110,9 @@ class DLRMConfig:
     #   in-graph event nodes (None: DLRM yes, DCN-v2 no)
     ids_stream: Optional[bool] = None              # one GPU, composed graphs: copy the next
     #   ids on a third stream behind the sort (None: with composed graphs)
-    stream_sync: str = "event"                     # one GPU: cross-stream hand-offs as event
-    #   record / wait nodes ("event") or signal-memory value writes / waits ("value": each
-    #   stream's whole step is one executable graph, launchable in any order)
-    graph_steps: int = 1                           # one GPU, stream_sync="value", in-step
-    #   batches: steps per executable graph launch (the step's graphs repeated)
+    dp_lookup_stream: str = "D"                    # W > 1 stream graphs, replicated tables with
+    #   a dense update: their next-batch lookup on the dense-comm stream ("D", right
+    #   after their update) or on the embedding stream ("EC", after the sharded lookup)
     stream_graphs: bool = True                     # W > 1, pipelined, capturable comm (native
     #   RCCL / loopback): the step as per-stream hipGraphs with the collectives inside
     #   (dlrm_multirank.py; 3 launches per step) instead of graphs between eagerly issued
@@ -987,19 +985,6 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
         else:
             self._forward_backward()
         self.steps += 1
-
-    def step_many(self, n: int):
-        """Issue ``n`` steps. Value-synced per-stream graphs
-        (``stream_sync="value"``) launch ``graph_steps`` steps per executable
-        graph; otherwise ``n`` calls of ``step()``."""
-        ms = getattr(self, "_ms", None)
-        if self.graph == "streams" and ms is not None and ms.get("value"):
-            self._use_gemm_policy()
-            self._ms_step(int(n))
-            self.steps += int(n)
-            return
-        for _ in range(int(n)):
-            self.step()
 
     def _use_gemm_policy(self):
         if self._gemm_pol is not None and ops.gemm_policy(-1) != self._gemm_pol:

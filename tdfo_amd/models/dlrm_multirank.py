@@ -93,11 +93,18 @@ class MultiRankStreamsMixin:
             # (row-wise need published on D, right after the bucketize)
             emb.stage_fwd_ids_exchange(lagged=self._rw_lagged, publish=False)
 
+        # replicated tables with a dense update: their next-batch ids + lookup
+        # on D right after their update (d_prep), or on EC after the sharded
+        # tables' lookup ("EC": D's chain to the dense optimizer -- the W > 1
+        # step's critical path -- then carries only the bucket reduces)
+        dp_on_ec = dp_dense and self.cfg.dp_lookup_stream == "EC"
+
         def ec_b2():
-            # (replicated tables with a dense update: looked up on D, right
-            # after their update and their ids, see d_prep)
             emb.stage_fwd_lookup(dp=not dp_dense)
             emb.stage_fwd_out_exchange()
+            if dp_on_ec:
+                emb.stage_fwd_prep(self.ids, sharded=False)
+                emb.stage_fwd_lookup(sharded=False)
 
         def d_b():
             self._m_allreduce_top_start()
@@ -112,7 +119,9 @@ class MultiRankStreamsMixin:
             emb.stage_fwd_prep(self.ids, dp=False)
 
         def d_prep():                           # the replicated tables' ids, once their
-            emb.stage_fwd_prep(self.ids, sharded=False)   # dense grad (Dp) has read them
+            if dp_on_ec:                        # dense grad (Dp) has read them
+                return
+            emb.stage_fwd_prep(self.ids, sharded=False)
             if dp_dense:                        # ... and their lookup (updated in Dp)
                 emb.stage_fwd_lookup(sharded=False)
 
@@ -151,6 +160,7 @@ class MultiRankStreamsMixin:
         ev = {k: ops.SyncEvent(2) for k in ("d", "c5", "m2", "m3", "m4", "e0", "dp", "dpp")}
         seg = self._mr_segments()
         dp_dense = bool(self.emb.dp_tables) and self.emb.dp_dense
+        dp_on_ec = dp_dense and self.cfg.dp_lookup_stream == "EC"
         home = lambda name: "EC" if name.startswith("EC") else name[0]  # noqa: E731
         pool = torch.cuda.graph_pool_handle()
         graphs = {}
@@ -220,12 +230,14 @@ class MultiRankStreamsMixin:
             # costs ~14 us of queue idle, scripts/mr_timeline.py; with a
             # dense replicated-table update D also looks those tables up, so
             # EC waits for none of D's replicated-table work)
-            "EC": (chain([("wait", "m2"), ("graph", "EC1"), ("wait", "e0"), ("wait", "m4"),
-                          ("graph", "ECub"), ("record", "c5")]) if dp_dense else
+            "EC": (chain([("wait", "m2"), ("graph", "EC1"), ("wait", "e0"), ("wait", "m4")]
+                         + ([("wait", "dp")] if dp_on_ec else [])
+                         + [("graph", "ECub"), ("record", "c5")]) if dp_dense else
                    chain([("wait", "m2"), ("graph", "EC1"), ("wait", "e0"), ("wait", "dp"),
                           ("wait", "m4"), ("wait", "dpp"), ("graph", "ECub"),
                           ("record", "c5")])),
         }
+        ops.upload_graphs(composed.values())
         self._mr = {"streams": streams, "events": ev, "graphs": graphs, "composed": composed,
                     "launched": False, "names": names}
         # the capture ran nothing: the batch handed in before it is the one

@@ -89,14 +89,6 @@ class StreamGraphsMixin:
         composed = self.cfg.composed_graphs
         if composed is None:
             composed = self.cfg.interaction == "dot"
-        value = self.cfg.stream_sync == "value"
-        nsteps = max(1, int(self.cfg.graph_steps))
-        if value:
-            composed = True
-        elif self.cfg.stream_sync != "event":
-            raise ValueError(f"stream_sync must be 'event' or 'value', not {self.cfg.stream_sync!r}")
-        if nsteps > 1 and not (value and self._insrc is not None):
-            raise ValueError("graph_steps > 1 needs stream_sync='value' and in-step batches")
         # cross-stream edges recorded without the system-scope fence a default
         # event record adds (the producing kernels already release to device
         # scope and no host reads these edges): DLRM-1TB 0.477-0.480 vs
@@ -104,8 +96,7 @@ class StreamGraphsMixin:
         ev = [ops.SyncEvent(2) for _ in range(4)]
         ids_stream = self.cfg.ids_stream
         if ids_stream is None:
-            ids_stream = composed and not value
-        ids_stream = ids_stream and not value     # value mode: the ids copy on the E stream
+            ids_stream = composed
         # Staged batches (composed graphs + ids stream): a device batch is
         # copied (ids, dense, labels) on the ids stream into fixed buffers, and
         # the MLP graph converts dense / labels itself behind an in-graph wait
@@ -137,37 +128,19 @@ class StreamGraphsMixin:
                 if stamp is not None:
                     ops.stamp(stamp[0], stamp[1], names.index(name), len(names), 1)
             graphs[name] = gr
-        flags = None
-        if value:
-            # f1: pooled embeddings ready (E -> M), f2: embedding gradients
-            # ready (M -> E). The waiter resets its flag right after the wait;
-            # the producer's next write is ordered after that reset through the
-            # other flag (E1(k+1) follows E3(k), which waits for M2(k), which
-            # follows M's reset of f1(k); symmetrically for f2), so a flag never
-            # carries two steps' signals and a wait never sees a stale one.
-            flags = (ops.SignalFlag(), ops.SignalFlag())
-            f1, f2 = flags
-            ep = [("graph", graphs["E1"]), ("writeval", (f1, 1)), ("graph", graphs["E2"]),
-                  ("waitval", (f2, 1)), ("writeval", (f2, 0)), ("graph", graphs["E3"])]
-            mp = [("graph", graphs["M1"]), ("waitval", (f1, 1)), ("writeval", (f1, 0)),
-                  ("graph", graphs["M2"]), ("writeval", (f2, 1)), ("graph", graphs["M3"])]
-            graphs["E"] = ops.ComposedGraph(ep)
-            graphs["M"] = ops.ComposedGraph(mp)
-            if nsteps > 1:
-                graphs["EN"] = ops.ComposedGraph(ep * nsteps)
-                graphs["MN"] = ops.ComposedGraph(mp * nsteps)
-        elif composed:
+        if composed:
             head = [("wait", ev_copy)] if self._bstg is not None else []
             graphs["M"] = ops.ComposedGraph(head + [("graph", graphs["M1"]), ("wait", ev[1]),
                                                     ("graph", graphs["M2"]), ("record", ev[2]),
                                                     ("graph", graphs["M3"])])
             graphs["EA"] = ops.ComposedGraph([("graph", graphs["E1"]), ("record", ev[1]),
                                               ("graph", graphs["E2"])])
+        ops.upload_graphs(graphs.values())
         torch.cuda.synchronize()
         cs = (torch.cuda.Stream(device=self.device) if ids_stream and self._insrc is None
               else None)
         self._ms = {"graphs": graphs, "stream": se, "plan": plan, "composed": composed,
-                    "names": names, "value": value, "nsteps": nsteps, "flags": flags,
+                    "names": names,
                     "cstream": cs, "ev_e2": ops.SyncEvent(2), "ev_copy": ev_copy,
                     "e2_recorded": False, "events": ev}
         self.graph = "streams"
@@ -211,22 +184,10 @@ class StreamGraphsMixin:
             main.wait_event(ev)                # dense / labels from the same source
         return True
 
-    def _ms_step(self, n: int = 1):
-        """Issue ``n`` steps (value sync: as n // graph_steps multi-step
-        launches plus single ones; event sync: n must be 1)."""
+    def _ms_step(self):
         g, se, ev = self._ms["graphs"], self._ms["stream"], self._ms["events"]
         main = torch.cuda.current_stream()
         composed = self._ms["composed"]
-        if self._ms["value"]:
-            N = self._ms["nsteps"]
-            for gE, gM, k in (("EN", "MN", n // N if N > 1 else 0),
-                              ("E", "M", n - (n // N) * N if N > 1 else n)):
-                for _ in range(k):
-                    with torch.cuda.stream(se):
-                        g[gE].replay()
-                    g[gM].replay()
-            return
-        assert n == 1
         # (this step's ids were copied on the embedding side by load_batch, so
         # the lookup follows the previous step's embedding update there)
         with torch.cuda.stream(se):

@@ -147,6 +147,26 @@ class ComposedGraph:
             pass
 
 
+def upload_graphs(graphs):
+    """hipGraphUpload every executable graph (torch CUDAGraph or
+    ComposedGraph) on the current stream, so their first launches do not
+    set them up (TDFO_GRAPH_UPLOAD=0: skip; A/B of the first-replays
+    transient, profiles/r04/notes.md)."""
+    import os
+    if os.environ.get("TDFO_GRAPH_UPLOAD", "1") == "0":
+        return
+    for g in graphs:
+        if isinstance(g, ComposedGraph):
+            _native().graph_exec_upload(g._ex)
+        elif isinstance(g, torch.cuda.CUDAGraph):
+            try:                  # (a keep_graph capture has no executable yet)
+                ex = int(g.raw_cuda_graph_exec())
+            except RuntimeError:
+                ex = 0
+            if ex:
+                _native().graph_exec_upload(ex)
+
+
 class gemm_batch:
     """Context manager: GEMMs issued inside are recorded and enqueued in
     order on exit, consecutive (weight grad, dgrad) pairs on the small-tile

@@ -145,23 +145,13 @@ class StepLoop:
 
     def _run(self, n: int, on_dev: bool):
         tr, wd = self.tr, self.wd
-        if self.in_step:                       # the steps draw their own batches
-            k = 0
-            while k < n:
-                c = n - k
-                if wd is not None:             # heartbeats between launches
-                    c = min(c, self.beat_every - self.step_index % self.beat_every)
-                if hasattr(tr, "step_many"):
-                    tr.step_many(c)
-                else:
-                    for _ in range(c):
-                        tr.step()
-                k += c
-                self.step_index += c
-                if wd is not None and (self.step_index % self.beat_every == 0) and k < n:
-                    wd.beat(tr.heartbeat_stream(), self.step_index)
-            return
         for k in range(n):
+            if self.in_step:                   # the step draws its own batch
+                tr.step()
+                self.step_index += 1
+                if wd is not None and (self.step_index % self.beat_every == 0) and k + 1 < n:
+                    wd.beat(tr.heartbeat_stream(), self.step_index)
+                continue
             batch, slot = self._next()
             if tr.pipeline:
                 tr.set_next_batch(*batch)

@@ -97,14 +97,14 @@ def test_rccl_comm_one_rank_ops_eager_and_captured():
     assert res == [True]
 
 
-def _trainer(whole: bool, W: int, strategy: str):
+def _trainer(whole: bool, W: int, strategy: str, dp_lookup: str = "D"):
     from tdfo_amd.models.dlrm import DLRMConfig, DLRMTrainer
     from tdfo_amd.parallel.comm import LoopbackComm
 
     rows = [5000, 7, 30000, 1000, 3, 800, 64, 129]
     cfg = DLRMConfig(embedding_dim=64, table_rows=rows, bottom=[128, 64], top=[128, 64, 1],
                      sharding=strategy, pipeline=True, pooling=[1, 2, 1, 3, 1, 1, 1, 1],
-                     stream_graphs=whole, seed=3)
+                     stream_graphs=whole, seed=3, dp_lookup_stream=dp_lookup)
     dev = torch.device("cuda", 0)
     comm = LoopbackComm(W, 0, dev)
     tr = DLRMTrainer(cfg, 256, dev, group=comm, rank=0, world_size=W)
@@ -113,6 +113,7 @@ def _trainer(whole: bool, W: int, strategy: str):
 
 @pytest.mark.parametrize("strategy,skew", [("table_wise", False), ("auto", False),
                                            ("column_wise", False), ("data_parallel", False),
+                                           ("data_parallel_ec", False),
                                            ("row_wise", False), ("row_wise", True)])
 def test_stream_graphs_match_staged(strategy, skew):
     """Row-wise tables run on the stream graphs with the lagged capacity
@@ -123,8 +124,10 @@ def test_stream_graphs_match_staged(strategy, skew):
 
     W = 4
     out = []
+    dp_lookup = "EC" if strategy.endswith("_ec") else "D"
+    strategy = strategy.replace("_ec", "")
     for whole in (False, True):
-        tr, rows, cfg = _trainer(whole, W, strategy)
+        tr, rows, cfg = _trainer(whole, W, strategy, dp_lookup)
         data = SyntheticCriteo(rows, 256, pooling=cfg.pooling_factors(), device="cuda:0", seed=9)
         batches = [data.next() for _ in range(9)]
         if skew:

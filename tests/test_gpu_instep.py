@@ -67,38 +67,3 @@ def test_trainer_in_step_matches_loaded_batches():
     assert torch.equal(a.emb.tw_store.weight, b.emb.tw_store.weight)
     assert a.pop_loss() == b.pop_loss()
 
-
-@pytest.mark.parametrize("interaction,steps", [("dot", 1), ("dot", 3), ("dcn", 2)])
-def test_value_synced_multistep_graphs_match_event_graphs(interaction, steps):
-    """Per-stream graphs joined by signal-memory value waits, several steps
-    per executable-graph launch (stream_sync="value", graph_steps), train
-    bit-identically to the event-joined one-step graphs on in-step batches."""
-    import dataclasses
-
-    from tdfo_amd.data.synthetic import InStepSynthetic
-    from tdfo_amd.models.dlrm import DLRMConfig, DLRMTrainer
-    from tdfo_amd.train.loop import StepLoop
-
-    kw = dict(embedding_dim=128, table_rows=ROWS, bottom=[128], top=[256, 1])
-    if interaction == "dcn":
-        kw.update(interaction="dcn", pooling=[2, 1, 3, 1], top=[256, 128, 1])
-    cfg = DLRMConfig(**kw)
-    B = 512
-    a = DLRMTrainer(cfg, B, DEV)
-    b = DLRMTrainer(dataclasses.replace(cfg, stream_sync="value", graph_steps=steps), B, DEV)
-    la = StepLoop(a, InStepSynthetic(ROWS, B, DEV, seed=3, pooling=cfg.pooling_factors()))
-    lb = StepLoop(b, InStepSynthetic(ROWS, B, DEV, seed=3, pooling=cfg.pooling_factors()))
-    for lp in (la, lb):
-        lp.run(2)
-        lp.tr.capture_graph(warmup=0)
-        assert lp.tr.graph == "streams"
-        lp.run(7)                          # 7 = 2 x 3 + 1 and 3 x 2 + 1: multi + single
-    torch.cuda.synchronize()
-    for t in (a, b):
-        t.sync_streams()
-    torch.cuda.synchronize()
-    assert b._ms["value"] and b._ms["nsteps"] == steps
-    assert torch.equal(a.fp.p, b.fp.p)
-    assert torch.equal(a.emb.tw_store.weight, b.emb.tw_store.weight)
-    assert a.pop_loss() == b.pop_loss()
-    assert a.steps == b.steps == 9
