@@ -93,18 +93,13 @@ class MultiRankStreamsMixin:
             # (row-wise need published on D, right after the bucketize)
             emb.stage_fwd_ids_exchange(lagged=self._rw_lagged, publish=False)
 
-        # replicated tables with a dense update: their next-batch ids + lookup
-        # on D right after their update (d_prep), or on EC after the sharded
-        # tables' lookup ("EC": D's chain to the dense optimizer -- the W > 1
-        # step's critical path -- then carries only the bucket reduces)
-        dp_on_ec = dp_dense and self.cfg.dp_lookup_stream == "EC"
-
         def ec_b2():
+            # (replicated tables with a dense update: looked up on D, right
+            # after their update and their ids, see d_prep; on EC instead the
+            # emulated W=8 step ran the same and config 3 slower, 0.96 vs
+            # 0.85 ms, profiles/r04/notes.md)
             emb.stage_fwd_lookup(dp=not dp_dense)
             emb.stage_fwd_out_exchange()
-            if dp_on_ec:
-                emb.stage_fwd_prep(self.ids, sharded=False)
-                emb.stage_fwd_lookup(sharded=False)
 
         def d_b():
             self._m_allreduce_top_start()
@@ -118,10 +113,40 @@ class MultiRankStreamsMixin:
             # (their send buffers' last reader was the previous exchange)
             emb.stage_fwd_prep(self.ids, dp=False)
 
+        # wgrad_first: M runs the top weight grads before the bottom backward,
+        # so the top bucket's all-reduce + optimizer (D) overlap the bottom
+        # backward and only the small bottom bucket follows M's last segment;
+        # the next batch's ids / labels load + bucketize move to a segment
+        # right after the top backward (Mi), x0 (read by the bottom backward)
+        # loads at its end
+        wf = self.cfg.mr_wgrad_first and self._defer_top_wgrad
+        a_split, P = self._ar_split, self.fp.p.numel()
+
+        def m_i():
+            self._m_load_next(x0=False)
+            emb.stage_fwd_prep(self.ids, dp=False)
+
+        def m4_wf():
+            self._s_bottom_bwd()
+            self._m_load_next(ids=False)
+
+        def d_q_wf():                           # next batch: row-wise need, replicated ids
+            if self._rw_lagged:
+                emb.rw_publish_need(self.dcomm)
+            d_prep()
+
+        def d_b_wf():                           # top bucket + its optimizer range
+            self._m_allreduce_top_start()
+            self._m_allreduce_wait("_ar_top")
+            self._dense_update_range(a_split, P)
+
+        def d_a_wf():                           # bottom bucket + its optimizer range
+            self._m_allreduce_start()
+            self._m_allreduce_wait("_ar_work")
+            self._dense_update_range(0, a_split)
+
         def d_prep():                           # the replicated tables' ids, once their
-            if dp_on_ec:                        # dense grad (Dp) has read them
-                return
-            emb.stage_fwd_prep(self.ids, sharded=False)
+            emb.stage_fwd_prep(self.ids, sharded=False)   # dense grad (Dp) has read them
             if dp_dense:                        # ... and their lookup (updated in Dp)
                 emb.stage_fwd_lookup(sharded=False)
 
@@ -138,6 +163,11 @@ class MultiRankStreamsMixin:
             self._m_allreduce_start()
             d_prep()
 
+        if wf:
+            return {"M1": self._s_bottom_fwd, "M2": m2, "Mi": m_i, "M3": self._s_top_wgrad,
+                    "M4": m4_wf, "D0": emb.stage_bwd_prepare, "Dp": dp_a, "Dq": d_q_wf,
+                    "Db": d_b_wf, "Da": d_a_wf, "EC1": lambda: emb.backward_start(dp=False),
+                    "ECub": lambda: (ec_upd(), ec_b())}
         return {"M1": self._s_bottom_fwd, "M2": m2, "M4": m4,
                 "M3": self._s_top_wgrad if self._defer_top_wgrad else None,
                 "D0": emb.stage_bwd_prepare, "Dp": dp_a,
@@ -157,10 +187,9 @@ class MultiRankStreamsMixin:
         # (default priority: a high-priority M and/or EC stream ran the
         # emulated W=8 step at 1.93-2.26 vs 0.63-0.64 ms)
         streams = {k: torch.cuda.Stream(device=dev) for k in ("M", "D", "EC")}
-        ev = {k: ops.SyncEvent(2) for k in ("d", "c5", "m2", "m3", "m4", "e0", "dp", "dpp")}
+        ev = {k: ops.SyncEvent(2) for k in ("d", "c5", "m2", "m3", "m4", "e0", "dp", "dpp", "mi")}
         seg = self._mr_segments()
         dp_dense = bool(self.emb.dp_tables) and self.emb.dp_dense
-        dp_on_ec = dp_dense and self.cfg.dp_lookup_stream == "EC"
         home = lambda name: "EC" if name.startswith("EC") else name[0]  # noqa: E731
         pool = torch.cuda.graph_pool_handle()
         graphs = {}
@@ -210,6 +239,7 @@ class MultiRankStreamsMixin:
         # batch may load (x0 free) and the bottom bucket reduce sooner
         # (every segment boundary costs ~8 us of queue idle and every
         # cross-stream wait ~15-23 us: scripts/mr_sched_probe.py)
+        wf = "Mi" in graphs
         composed = {
             # M: the bottom backward (+ the next batch's load into x0 / ids /
             # labels, all of whose readers have run) before the top weight
@@ -230,13 +260,30 @@ class MultiRankStreamsMixin:
             # costs ~14 us of queue idle, scripts/mr_timeline.py; with a
             # dense replicated-table update D also looks those tables up, so
             # EC waits for none of D's replicated-table work)
-            "EC": (chain([("wait", "m2"), ("graph", "EC1"), ("wait", "e0"), ("wait", "m4")]
-                         + ([("wait", "dp")] if dp_on_ec else [])
-                         + [("graph", "ECub"), ("record", "c5")]) if dp_dense else
+            "EC": (chain([("wait", "m2"), ("graph", "EC1"), ("wait", "e0"), ("wait", "m4"),
+                          ("graph", "ECub"), ("record", "c5")]) if dp_dense else
                    chain([("wait", "m2"), ("graph", "EC1"), ("wait", "e0"), ("wait", "dp"),
                           ("wait", "m4"), ("wait", "dpp"), ("graph", "ECub"),
                           ("record", "c5")])),
         }
+        if wf:
+            # wgrad_first (see _mr_segments): top weight grads before the
+            # bottom backward; D reduces + updates the top bucket beside the
+            # bottom backward, then the bottom bucket; EC's next-batch
+            # exchange waits only for the early ids load (mi)
+            composed["M"] = chain([("wait", "d"), ("graph", "M1"), ("wait", "c5"),
+                                   ("graph", "M2"), ("record", "m2"), ("graph", "Mi"),
+                                   ("record", "mi"), ("graph", "M3"), ("record", "m3"),
+                                   ("graph", "M4"), ("record", "m4")])
+            composed["D"] = chain([("wait", "c5"), ("graph", "D0"), ("record", "e0"),
+                                   ("wait", "m2"), ("graph", "Dp"), ("record", "dp"),
+                                   ("wait", "mi"), ("graph", "Dq"), ("record", "dpp"),
+                                   ("wait", "m3"), ("graph", "Db"), ("wait", "m4"),
+                                   ("graph", "Da"), ("record", "d")])
+            composed["EC"] = chain([("wait", "m2"), ("graph", "EC1"), ("wait", "e0"),
+                                    ("wait", "mi")]
+                                   + ([("wait", "dp"), ("wait", "dpp")] if not dp_dense else [])
+                                   + [("graph", "ECub"), ("record", "c5")])
         ops.upload_graphs(composed.values())
         self._mr = {"streams": streams, "events": ev, "graphs": graphs, "composed": composed,
                     "launched": False, "names": names}
