@@ -1209,6 +1209,18 @@ int g_policy = 0;
 
 enum Kern { K_SMALL64 = 64, K_SMALL128 = 128, K_DEEP = 2, K_PP = 3, K_BIG = 4 };
 
+// A/B (TDFO_GEMM_EPI_PP, policy 5): GEMMs with a memory-heavy epilogue on the
+// ping-pong kernel (two blocks per CU: one block's epilogue traffic overlaps
+// the other's MFMAs; a 256x128 block streams its epilogue with the CU's MFMAs
+// idle) -- 1: DCN Hadamard / residual outputs, 2: also ReLU-masked dgrads
+int epi_pp() {
+  static const int v = [] {
+    const char* e = getenv("TDFO_GEMM_EPI_PP");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 template <bool AC, bool BC>
 int choose(const GemmArgs& a) {
   const int t128 = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN) * a.splits;
@@ -1232,6 +1244,8 @@ int choose(const GemmArgs& a) {
     // 2.36 ms (profiles/r04/notes.md)
     const int t256 = ((a.M + LBM - 1) / LBM) * ((a.N + BN - 1) / BN) * a.splits;
     if (!AC && t256 < 256 && t128 <= 512 && ktps >= 16) return K_DEEP;
+    if (epi_pp() >= 1 && (a.mul || a.add)) return K_PP;
+    if (epi_pp() >= 2 && a.mask) return K_PP;
     if (big_ok) return K_BIG;
   } else {
     if (!AC && ktps >= 32 && t128 <= 512) return K_DEEP;
