@@ -20,10 +20,12 @@ STEPS = 3
 
 
 def _worker(rank, world, Bk, strategy, graph, rw_comm, emb_opt="rowwise_adagrad", pipeline=False,
-            dist="uniform", alpha=1.05, rw_capacity=1.25, pipe_lookup=True):
+            dist="uniform", alpha=1.05, rw_capacity=1.25, pipe_lookup=True, predict_skew=False):
     """dist="zipf": the two eager steps see uniform ids, the graph-replayed
     ones power-law ids -- the row-wise capacity then has to grow after the
-    capture (eager rest of that step, re-capture)."""
+    capture (eager rest of that step, re-capture). predict_skew: between two
+    replayed steps a predict() on a batch whose ids all map to one owner grows
+    the row-wise capacity outside any step."""
     from tdfo_amd.data.synthetic import SyntheticCriteo
     from tdfo_amd.models.dlrm import DLRMConfig, DLRMTrainer
     from tdfo_amd.parallel.dist import get_info
@@ -70,6 +72,10 @@ def _worker(rank, world, Bk, strategy, graph, rw_comm, emb_opt="rowwise_adagrad"
         tr.capture_graph(warmup=0)
         assert tr.graph is not None
     for i in range(2, 2 + STEPS):
+        if predict_skew and i == 3:
+            d, ids_, y = batches[i]
+            tr.load_batch(d, ids_ - ids_ % world, y)
+            tr.predict()
         feed(i)
         tr.step()
     torch.cuda.synchronize()
@@ -184,3 +190,14 @@ def test_two_ranks_pipelined_input_dist(strategy, rw_comm, pipe_lookup, single):
         for t, (lo, c0, w) in tabs.items():
             ref_w = tabs1[t][2][slice(*lo)][:, c0:c0 + w.shape[1]]
             assert torch.allclose(w, ref_w, atol=tol, rtol=tol), (rank, t)
+
+
+def test_row_wise_growth_in_predict_between_replays(single):
+    """Row-wise capacity grown by a predict() between two replayed steps
+    (outside any step): the next step runs its stages eagerly against the
+    reallocated exchange buffers and re-captures, instead of replaying graphs
+    that still hold the freed ones -- the result equals one process."""
+    multi = run_distributed(_worker, 2, B, "row_wise", True, "fp32", "rowwise_adagrad", False,
+                            "uniform", 1.05, 1.25, True, True, device="cuda", timeout=600)
+    assert all(m[3] > 0 for m in multi)
+    _check(multi, single("rowwise_adagrad"), 3e-3)
