@@ -17,6 +17,9 @@ from tdfo_amd import ops  # noqa: E402
 # same layer is (M, K, N) and the wgrad (N, K, M)
 SHAPES = [(8192, 512, 64), (8192, 256, 512), (8192, 128, 256), (8192, 1024, 512),
           (8192, 1024, 1024), (8192, 512, 1024), (8192, 256, 512)]
+# DCN-v2 (--model dcnv2, GEMM policy 5): cross-layer V (d=3456 -> r=512) and
+# U (512 -> 3456), top-0 (3456 -> 1024)
+DCN_SHAPES = [(8192, 512, 3456), (8192, 3456, 512), (8192, 1024, 3456)]
 
 
 def timeit(fn, it=20, reps=10):
@@ -42,7 +45,11 @@ def timeit(fn, it=20, reps=10):
 
 def main():
     bf = torch.bfloat16
-    for M, N, K in SHAPES:
+    shapes = SHAPES
+    if "--model" in sys.argv and sys.argv[sys.argv.index("--model") + 1] == "dcnv2":
+        shapes = DCN_SHAPES
+        ops.gemm_policy(5)
+    for M, N, K in shapes:
         x = torch.randn(M, K, device="cuda").to(bf)
         w = torch.randn(N, K, device="cuda").to(bf)
         b = torch.randn(N, device="cuda").to(bf)
@@ -65,7 +72,11 @@ def main():
                           "ours_dgrad_us": round(ours_d, 2), "blas_dgrad_us": round(blas_d, 2),
                           "ours_wgrad_us": round(ours_w, 2), "blas_wgrad_us": round(blas_w, 2),
                           "ours_fwd_tflops": round(tf / ours * 1e6, 1),
-                          "blas_fwd_tflops": round(tf / blas * 1e6, 1)}), flush=True)
+                          "blas_fwd_tflops": round(tf / blas * 1e6, 1),
+                          "ours_dgrad_tflops": round(tf / ours_d * 1e6, 1),
+                          "blas_dgrad_tflops": round(tf / blas_d * 1e6, 1),
+                          "ours_wgrad_tflops": round(tf / ours_w * 1e6, 1),
+                          "blas_wgrad_tflops": round(tf / blas_w * 1e6, 1)}), flush=True)
 
 
 if __name__ == "__main__":
