@@ -110,8 +110,9 @@ class DLRMConfig:
     #   in-graph event nodes (None: DLRM yes, DCN-v2 no)
     ids_stream: Optional[bool] = None              # one GPU, composed graphs: copy the next
     #   ids on a third stream behind the sort (None: with composed graphs)
-    mr_wgrad_first: bool = False                   # W > 1 stream graphs: top weight grads
-    #   before the bottom backward (dlrm_multirank.py _mr_segments)
+    #   (Rejected, round 4, W > 1 stream graphs: the top weight grads before the bottom
+    #   backward so the top bucket reduces beside it -- emulated W=8 0.616-0.621 vs
+    #   0.590-0.594 ms/step, config 3 0.872 vs 0.849, config 5 3.035 vs 3.016)
     stream_graphs: bool = True                     # W > 1, pipelined, capturable comm (native
     #   RCCL / loopback): the step as per-stream hipGraphs with the collectives inside
     #   (dlrm_multirank.py; 3 launches per step) instead of graphs between eagerly issued
@@ -571,21 +572,15 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
             return
         self._next = (dense, ids, label)
 
-    def _m_load_next(self, x0: bool = True, ids: bool = True):
-        """The next batch into the static buffers (multi-rank stream graphs:
-        from the staging copy; ``x0`` / ``ids`` False: without the dense
-        features / without ids + labels)."""
+    def _m_load_next(self):
         if self._whole_capture:
             sx, si, sl = self._stg
-            if x0:
-                self.x0.copy_(sx)
-            if ids:
-                self.ids.copy_(si)
-                self.label.copy_(sl)
+            self.x0.copy_(sx)
+            self.ids.copy_(si)
+            self.label.copy_(sl)
             return
-        assert x0 and ids
-        dense, nids, label = self._next
-        ops.batch_load(dense, self.x0, nids, self.ids, label, self.label)
+        dense, ids, label = self._next
+        ops.batch_load(dense, self.x0, ids, self.ids, label, self.label)
 
     def _m_ids_exchange_next(self):
         self.emb.stage_fwd_ids_exchange(async_op=True, lagged=self._rw_lagged)
@@ -937,8 +932,8 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
     def _s_emb_update(self):
         self.emb.stage_bwd_update(self.emb_hyper)
 
-    def _m_allreduce_wait(self, only: Optional[str] = None):
-        for name in ((only,) if only else ("_ar_top", "_ar_work")):
+    def _m_allreduce_wait(self):
+        for name in ("_ar_top", "_ar_work"):
             w = getattr(self, name, None)
             if w is not None:
                 work, g, b = w

@@ -113,38 +113,6 @@ class MultiRankStreamsMixin:
             # (their send buffers' last reader was the previous exchange)
             emb.stage_fwd_prep(self.ids, dp=False)
 
-        # wgrad_first: M runs the top weight grads before the bottom backward,
-        # so the top bucket's all-reduce + optimizer (D) overlap the bottom
-        # backward and only the small bottom bucket follows M's last segment;
-        # the next batch's ids / labels load + bucketize move to a segment
-        # right after the top backward (Mi), x0 (read by the bottom backward)
-        # loads at its end
-        wf = self.cfg.mr_wgrad_first and self._defer_top_wgrad
-        a_split, P = self._ar_split, self.fp.p.numel()
-
-        def m_i():
-            self._m_load_next(x0=False)
-            emb.stage_fwd_prep(self.ids, dp=False)
-
-        def m4_wf():
-            self._s_bottom_bwd()
-            self._m_load_next(ids=False)
-
-        def d_q_wf():                           # next batch: row-wise need, replicated ids
-            if self._rw_lagged:
-                emb.rw_publish_need(self.dcomm)
-            d_prep()
-
-        def d_b_wf():                           # top bucket + its optimizer range
-            self._m_allreduce_top_start()
-            self._m_allreduce_wait("_ar_top")
-            self._dense_update_range(a_split, P)
-
-        def d_a_wf():                           # bottom bucket + its optimizer range
-            self._m_allreduce_start()
-            self._m_allreduce_wait("_ar_work")
-            self._dense_update_range(0, a_split)
-
         def d_prep():                           # the replicated tables' ids, once their
             emb.stage_fwd_prep(self.ids, sharded=False)   # dense grad (Dp) has read them
             if dp_dense:                        # ... and their lookup (updated in Dp)
@@ -163,11 +131,6 @@ class MultiRankStreamsMixin:
             self._m_allreduce_start()
             d_prep()
 
-        if wf:
-            return {"M1": self._s_bottom_fwd, "M2": m2, "Mi": m_i, "M3": self._s_top_wgrad,
-                    "M4": m4_wf, "D0": emb.stage_bwd_prepare, "Dp": dp_a, "Dq": d_q_wf,
-                    "Db": d_b_wf, "Da": d_a_wf, "EC1": lambda: emb.backward_start(dp=False),
-                    "ECub": lambda: (ec_upd(), ec_b())}
         return {"M1": self._s_bottom_fwd, "M2": m2, "M4": m4,
                 "M3": self._s_top_wgrad if self._defer_top_wgrad else None,
                 "D0": emb.stage_bwd_prepare, "Dp": dp_a,
@@ -187,7 +150,7 @@ class MultiRankStreamsMixin:
         # (default priority: a high-priority M and/or EC stream ran the
         # emulated W=8 step at 1.93-2.26 vs 0.63-0.64 ms)
         streams = {k: torch.cuda.Stream(device=dev) for k in ("M", "D", "EC")}
-        ev = {k: ops.SyncEvent(2) for k in ("d", "c5", "m2", "m3", "m4", "e0", "dp", "dpp", "mi")}
+        ev = {k: ops.SyncEvent(2) for k in ("d", "c5", "m2", "m3", "m4", "e0", "dp", "dpp")}
         seg = self._mr_segments()
         dp_dense = bool(self.emb.dp_tables) and self.emb.dp_dense
         home = lambda name: "EC" if name.startswith("EC") else name[0]  # noqa: E731
@@ -239,7 +202,6 @@ class MultiRankStreamsMixin:
         # batch may load (x0 free) and the bottom bucket reduce sooner
         # (every segment boundary costs ~8 us of queue idle and every
         # cross-stream wait ~15-23 us: scripts/mr_sched_probe.py)
-        wf = "Mi" in graphs
         composed = {
             # M: the bottom backward (+ the next batch's load into x0 / ids /
             # labels, all of whose readers have run) before the top weight
@@ -266,24 +228,6 @@ class MultiRankStreamsMixin:
                           ("wait", "m4"), ("wait", "dpp"), ("graph", "ECub"),
                           ("record", "c5")])),
         }
-        if wf:
-            # wgrad_first (see _mr_segments): top weight grads before the
-            # bottom backward; D reduces + updates the top bucket beside the
-            # bottom backward, then the bottom bucket; EC's next-batch
-            # exchange waits only for the early ids load (mi)
-            composed["M"] = chain([("wait", "d"), ("graph", "M1"), ("wait", "c5"),
-                                   ("graph", "M2"), ("record", "m2"), ("graph", "Mi"),
-                                   ("record", "mi"), ("graph", "M3"), ("record", "m3"),
-                                   ("graph", "M4"), ("record", "m4")])
-            composed["D"] = chain([("wait", "c5"), ("graph", "D0"), ("record", "e0"),
-                                   ("wait", "m2"), ("graph", "Dp"), ("record", "dp"),
-                                   ("wait", "mi"), ("graph", "Dq"), ("record", "dpp"),
-                                   ("wait", "m3"), ("graph", "Db"), ("wait", "m4"),
-                                   ("graph", "Da"), ("record", "d")])
-            composed["EC"] = chain([("wait", "m2"), ("graph", "EC1"), ("wait", "e0"),
-                                    ("wait", "mi")]
-                                   + ([("wait", "dp"), ("wait", "dpp")] if not dp_dense else [])
-                                   + [("graph", "ECub"), ("record", "c5")])
         ops.upload_graphs(composed.values())
         self._mr = {"streams": streams, "events": ev, "graphs": graphs, "composed": composed,
                     "launched": False, "names": names}
