@@ -1209,18 +1209,6 @@ int g_policy = 0;
 
 enum Kern { K_SMALL64 = 64, K_SMALL128 = 128, K_DEEP = 2, K_PP = 3, K_BIG = 4 };
 
-// A/B (TDFO_GEMM_EPI_PP, policy 5): GEMMs with a memory-heavy epilogue on the
-// ping-pong kernel (two blocks per CU: one block's epilogue traffic overlaps
-// the other's MFMAs; a 256x128 block streams its epilogue with the CU's MFMAs
-// idle) -- 1: DCN Hadamard / residual outputs, 2: also ReLU-masked dgrads
-int epi_pp() {
-  static const int v = [] {
-    const char* e = getenv("TDFO_GEMM_EPI_PP");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-
 template <bool AC, bool BC>
 int choose(const GemmArgs& a) {
   const int t128 = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN) * a.splits;
@@ -1241,11 +1229,11 @@ int choose(const GemmArgs& a) {
     // and its 144-KiB blocks wait there for whole free CUs (a 398-us backward
     // pair, profiles/r04/prof_dcn/step_lanes.txt), yet sending its GEMMs of
     // < 300 / 600 tiles to the 128x128 kernels ran the step at 2.64 / 2.66 vs
-    // 2.36 ms (profiles/r04/notes.md)
+    // 2.36 ms (profiles/r04/notes.md); nor do the epilogue-heavy GEMMs (DCN
+    // Hadamard / residual outputs, ReLU-masked dgrads) on the two-block
+    // ping-pong kernel: 2.55-2.62 vs 2.37 ms
     const int t256 = ((a.M + LBM - 1) / LBM) * ((a.N + BN - 1) / BN) * a.splits;
     if (!AC && t256 < 256 && t128 <= 512 && ktps >= 16) return K_DEEP;
-    if (epi_pp() >= 1 && (a.mul || a.add)) return K_PP;
-    if (epi_pp() >= 2 && a.mask) return K_PP;
     if (big_ok) return K_BIG;
   } else {
     if (!AC && ktps >= 32 && t128 <= 512) return K_DEEP;
