@@ -35,10 +35,6 @@ struct GemmArgs {
   // uses it for the bias gradient (sum over the batch of dy), which lets the
   // GEMM's N stay at the 128-aligned input width.
   int csum_on, csum_col;
-  // tile order within a split (set by the launcher): 0 row-major over the
-  // (M, N) tile grid, 1 M-fastest (an XCD's run of tiles then shares B
-  // column blocks instead of A row blocks)
-  int raster;
 };
 void gemm_bf16(const GemmArgs& a, hipStream_t s);
 // Launch n independent GEMMs in order; consecutive (weight grad, dgrad)

@@ -151,15 +151,17 @@ __device__ __forceinline__ bf16x8_t frag_col(const TDFO_LDS char* tile, int c0,
 // and remapped so that each XCD receives a contiguous run of that space: with
 // split-K, one XCD then works on one K-range (its own slices of A and B), so
 // the operands a split re-reads across its tiles stay in that XCD's L2.
+// (Row-major tile order within a split. M-fastest order, or per shape the
+// order with fewer unique operand bytes per XCD, measured the same on every
+// DLRM / DCN-v2 GEMM and step: profiles/r04/notes.md.)
 struct TileIdx {
   int tm, tn, split;
 };
 __device__ __forceinline__ TileIdx tile_of(int tiles_m, int tiles_n, int splits,
-                                           int bid = -1, int mfast = 0) {
+                                           int bid = -1) {
   const int tiles = tiles_m * tiles_n;
   const int w = xcd_remap(bid < 0 ? (int)blockIdx.x : bid, tiles * splits);
   const int split = w / tiles, t = w - split * tiles;
-  if (mfast) return {t - (t / tiles_m) * tiles_m, t / tiles_m, split};
   return {t / tiles_n, t - (t / tiles_n) * tiles_n, split};
 }
 
@@ -513,7 +515,7 @@ __device__ __forceinline__ void gemm_small_body(const GemmArgs& p, int bid, char
   TDFO_LDS char* smem = (TDFO_LDS char*)smem_raw;
 
   const int tiles_m = (p.M + BMT - 1) / BMT, tiles_n = (p.N + BN - 1) / BN;
-  const TileIdx ti = tile_of(tiles_m, tiles_n, p.splits, bid, p.raster);
+  const TileIdx ti = tile_of(tiles_m, tiles_n, p.splits, bid);
   const int m0 = ti.tm * BMT, n0 = ti.tn * BN;
 
   const int ktiles = p.K / BK;
@@ -604,7 +606,7 @@ __device__ __forceinline__ void gemm_big_body(const GemmArgs& p, int bid, char* 
   TDFO_LDS char* smem = (TDFO_LDS char*)smem_raw;
 
   const int tiles_m = (p.M + LBM - 1) / LBM, tiles_n = (p.N + BN - 1) / BN;
-  const TileIdx ti = tile_of(tiles_m, tiles_n, p.splits, bid, p.raster);
+  const TileIdx ti = tile_of(tiles_m, tiles_n, p.splits, bid);
   const int m0 = ti.tm * LBM, n0 = ti.tn * BN;
 
   const int ktiles = p.K / BK;
@@ -740,7 +742,7 @@ __global__ __launch_bounds__(256, 1) void gemm_deep_kernel(GemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   TDFO_LDS char* smem = (TDFO_LDS char*)smem_raw;
   const int tiles_m = (p.M + BM - 1) / BM, tiles_n = (p.N + BN - 1) / BN;
-  const TileIdx ti = tile_of(tiles_m, tiles_n, p.splits, -1, p.raster);
+  const TileIdx ti = tile_of(tiles_m, tiles_n, p.splits);
   const int m0 = ti.tm * BM, n0 = ti.tn * BN;
   const int ktiles = p.K / BK;
   const int per = (ktiles + p.splits - 1) / p.splits;
@@ -1005,7 +1007,7 @@ __device__ __forceinline__ void gemm_pp_body(const GemmArgs& p, int bid, char* s
   constexpr int MI = G::MI, NJ = G::NJ, KS = G::KS, SEGS = G::SEGS, NST = G::NST;
   TDFO_LDS char* smem = (TDFO_LDS char*)smem_raw;
   const int tiles_m = (p.M + G::BM - 1) / G::BM, tiles_n = (p.N + BN - 1) / BN;
-  const TileIdx ti = tile_of(tiles_m, tiles_n, p.splits, bid, p.raster);
+  const TileIdx ti = tile_of(tiles_m, tiles_n, p.splits, bid);
   const int m0 = ti.tm * G::BM, n0 = ti.tn * BN;
   const int ktiles = p.K / BK;
   const int per = (ktiles + p.splits - 1) / p.splits;
@@ -1289,35 +1291,8 @@ int kernel_of(const GemmArgs& a) {
   return a.b_col ? choose<false, true>(a) : choose<false, false>(a);
 }
 
-// Tile order (TDFO_GEMM_RASTER, A/B): 0 row-major; 1 M-fastest for weight
-// grads (col-layout A: each block streams a distinct K x 128 B slice, so in
-// row-major order an XCD's run of tiles re-fetches all of B while sharing one
-// A slice); 2 whichever order gives an XCD's run of tiles the fewer unique
-// operand bytes
-int raster_mode() {
-  static const int v = [] {
-    const char* e = getenv("TDFO_GEMM_RASTER");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-
-int pick_raster(const GemmArgs& a, int bm) {
-  const int mode = raster_mode();
-  if (mode == 0) return 0;
-  if (mode == 1) return a.a_col ? 1 : 0;
-  const int64_t tm = (a.M + bm - 1) / bm, tn = (a.N + BN - 1) / BN;
-  const int64_t run = (tm * tn + 7) / 8;            // tiles per XCD (per split)
-  auto bytes = [&](int64_t rows, int64_t cols) { return rows * bm + cols * (int64_t)BN; };
-  const int64_t r0 = (run + tn - 1) / tn, c0 = std::min(run, tn);     // row-major
-  const int64_t c1 = (run + tm - 1) / tm, r1 = std::min(run, tm);     // M-fastest
-  return bytes(r1, c1) < bytes(r0, c0) ? 1 : 0;
-}
-
-void launch_any(const GemmArgs& a0, hipStream_t s) {
-  GemmArgs a = a0;
+void launch_any(const GemmArgs& a, hipStream_t s) {
   const int k = kernel_of(a);
-  a.raster = pick_raster(a, k == K_BIG ? LBM : (k == K_SMALL64 ? 64 : BM));
   if (a.a_col) {
     if (a.b_col) launch<true, true>(a, k, s); else launch<true, false>(a, k, s);
   } else {
@@ -1350,14 +1325,9 @@ void big_pair_launch(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s) {
   TDFO_CHECK_HIP(hipGetLastError());
 }
 
-bool try_pair(const GemmArgs& a0_in, const GemmArgs& a1_in, hipStream_t s) {
-  const int k0 = kernel_of(a0_in), k1 = kernel_of(a1_in);
-  const int l0 = layout_of(a0_in), l1 = layout_of(a1_in);
-  const bool bigp = (k0 == K_BIG || (k1 == K_BIG && k0 == K_DEEP && !a0_in.csum_on)) &&
-                    (k1 == K_BIG || (k0 == K_BIG && k1 == K_DEEP && !a1_in.csum_on));
-  GemmArgs a0 = a0_in, a1 = a1_in;
-  a0.raster = pick_raster(a0, bigp ? LBM : BM);
-  a1.raster = pick_raster(a1, bigp ? LBM : BM);
+bool try_pair(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s) {
+  const int k0 = kernel_of(a0), k1 = kernel_of(a1);
+  const int l0 = layout_of(a0), l1 = layout_of(a1);
   // 256x128 pairs: a weight grad on that kernel takes its layer's dgrad
   // along onto it (also a deep-kernel one: one grid instead of two)
   const bool b0 = k0 == K_BIG || (k1 == K_BIG && k0 == K_DEEP && !a0.csum_on);
