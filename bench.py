@@ -60,6 +60,9 @@ def parse(argv=None):
     ap.add_argument("--defer-wgrad", default=None, choices=["0", "1"],
                     help="top / cross weight grads after the interaction / cross backward "
                          "(DLRMConfig.defer_wgrad; default: when N > 1)")
+    ap.add_argument("--emb-stream-cus", type=int, default=0,
+                    help="one GPU: embedding stream confined to this many CUs (0: all; "
+                         "DLRMConfig.emb_stream_cus)")
     ap.add_argument("--dense-comm", default="fp32", choices=["fp32", "bf16"],
                     help="N > 1: wire format of the dense-gradient all-reduce")
     ap.add_argument("--no-pipeline", action="store_true",
@@ -151,7 +154,8 @@ def _cfg(args, rows, pipe):
     kw = dict(table_rows=list(rows), sharding=args.sharding, pipeline=pipe,
               dense_comm=args.dense_comm, stream_graphs=not args.no_stream_graphs,
               opt_placement=args.opt_placement,
-              defer_wgrad=None if args.defer_wgrad is None else args.defer_wgrad == "1")
+              defer_wgrad=None if args.defer_wgrad is None else args.defer_wgrad == "1",
+              emb_stream_cus=args.emb_stream_cus)
     if args.model == "dlrm":
         return DLRMConfig(**kw)
     return DLRMConfig(interaction="dcn", pooling=list(MLPERF_MULTIHOT),
