@@ -60,6 +60,10 @@ def parse(argv=None):
     ap.add_argument("--defer-wgrad", default=None, choices=["0", "1"],
                     help="top / cross weight grads after the interaction / cross backward "
                          "(DLRMConfig.defer_wgrad; default: when N > 1)")
+    ap.add_argument("--preheat-ms", type=float, default=0.0,
+                    help="after the warm-up steps, this many ms of MFMA load on every CU "
+                         "before the timed window (the clock ramps under sustained load: "
+                         "profiles/r04/notes.md); reported in the stderr JSON")
     ap.add_argument("--emb-stream-cus", type=int, default=0,
                     help="one GPU: embedding stream confined to this many CUs (0: all; "
                          "DLRMConfig.emb_stream_cus)")
@@ -215,6 +219,9 @@ def measure(args, info, cfg, world: int, group, rank: int) -> dict:
         loop.run(post)
     torch.cuda.synchronize()
     tr.pop_loss()
+    if args.preheat_ms > 0:
+        from tdfo_amd import ops
+        ops.burn_us(args.preheat_ms * 1e3)
     if info.world_size > 1:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -418,7 +425,7 @@ def main(argv=None):
                           "host_issue_us_per_step": round((r["host_s"] - r["wait_s"])
                                                           / args.steps * 1e6, 1),
                           "host_wait_us_per_step": round(r["wait_s"] / args.steps * 1e6, 1),
-                          "comm": r["comm"],
+                          "comm": r["comm"], "preheat_ms": args.preheat_ms,
                           "ranks_consistent": consistent if world > 1 else None,
                           "replica_check": per if not consistent else None,
                           "dense_tflops": round(cfg.dense_flops_per_example() * value / 1e12, 1),

@@ -1431,6 +1431,14 @@ TORCH_LIBRARY(tdfo, m) {
     }();
     tdfo::spin_ticks(us > 0 ? (uint64_t)(us * ticks_per_us) : 0, cur_stream());
   });
+  m.def("burn_us(float us) -> ()", [](double us) {
+    int dev = 0, khz = 0, cus = 0;
+    TDFO_HIP_OK(hipGetDevice(&dev));
+    TDFO_HIP_OK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev));
+    TDFO_HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const double tpu = khz > 0 ? khz / 1000.0 : 100.0;
+    tdfo::burn_ticks(us > 0 ? (uint64_t)(us * tpu) : 0, 2 * cus, cur_stream());
+  });
   m.def("host_mailbox_alloc(int n) -> Tensor", host_mailbox_alloc);
   m.def("host_publish(Tensor value, Tensor(a!) seq, Tensor host, int slot) -> ()", host_publish);
   m.def("sync_event_record(int e) -> ()", sync_event_record);

@@ -250,6 +250,8 @@ void cast_f32_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t s);
 void batch_load(const float* dense, int nd, int64_t ld_dense, uint16_t* x0, int64_t ldx,
                 const int64_t* ids, int64_t* ids_dst, int64_t n, const float* label,
                 float* label_dst, int B, hipStream_t s);
+// MFMA load on `blocks` 256-thread blocks for `ticks` of the 100 MHz clock
+void burn_ticks(uint64_t ticks, int blocks, hipStream_t s);
 void spin_ticks(uint64_t ticks, hipStream_t s);
 struct BumpArgs {
   void* p[8];

@@ -210,6 +210,24 @@ void gather_columns(const GatherColsArgs& a, hipStream_t s) {
 // clock, sleeping between reads (modelled link time of an emulated
 // collective, parallel/comm.py LoopbackComm). Every wave exits once the
 // clock has advanced by `ticks`.
+// Device warm-up load (bench --preheat-ms): every wave issues MFMAs back to
+// back until `ticks` of the 100 MHz wall clock have passed since it started,
+// so the chip is at its sustained clock when a timed window begins. The
+// result is stored only under a condition that never holds (keeps the loop).
+__device__ float g_burn_sink[256];
+
+__global__ __launch_bounds__(256) void burn_kernel(uint64_t ticks) {
+  const uint64_t t0 = wall_clock64();
+  const bf16x8_t one = __builtin_bit_cast(
+      bf16x8_t, (s16x8_t){0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80, 0x3F80});
+  f32x4_t acc = {0.f, 0.f, 0.f, 0.f};
+  while (wall_clock64() - t0 < ticks) {
+#pragma unroll
+    for (int i = 0; i < 32; ++i) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(one, one, acc, 0, 0, 0);
+  }
+  if (acc[0] < -1.f) g_burn_sink[threadIdx.x] = acc[1];
+}
+
 __global__ __launch_bounds__(64) void spin_kernel(uint64_t ticks) {
   const uint64_t t0 = wall_clock64();
   while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
@@ -314,6 +332,12 @@ __global__ void bump_kernel(BumpArgs a) {
 void bump(const BumpArgs& a, hipStream_t s) {
   if (a.n <= 0) return;
   hipLaunchKernelGGL(bump_kernel, dim3(1), dim3(64), 0, s, a);
+  TDFO_CHECK_HIP(hipGetLastError());
+}
+
+void burn_ticks(uint64_t ticks, int blocks, hipStream_t s) {
+  if (ticks == 0 || blocks <= 0) return;
+  hipLaunchKernelGGL(burn_kernel, dim3(blocks), dim3(256), 0, s, ticks);
   TDFO_CHECK_HIP(hipGetLastError());
 }
 

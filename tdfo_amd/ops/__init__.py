@@ -675,6 +675,11 @@ def bump(counters):
             t.view(-1)[:1].add_(1)
 
 
+def burn_us(us: float):
+    """MFMA load on every CU for ``us`` microseconds (device warm-up)."""
+    _native().burn_us(float(us))
+
+
 def spin_us(us: float):
     """Occupy the current stream for ``us`` microseconds (one sleeping wave):
     the modelled link time of an emulated collective."""
