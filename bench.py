@@ -64,9 +64,6 @@ def parse(argv=None):
                     help="after the warm-up steps, this many ms of MFMA load on every CU "
                          "before the timed window (the clock ramps under sustained load: "
                          "profiles/r04/notes.md); reported in the stderr JSON")
-    ap.add_argument("--emb-stream-cus", type=int, default=0,
-                    help="one GPU: embedding stream confined to this many CUs (0: all; "
-                         "DLRMConfig.emb_stream_cus)")
     ap.add_argument("--dense-comm", default="fp32", choices=["fp32", "bf16"],
                     help="N > 1: wire format of the dense-gradient all-reduce")
     ap.add_argument("--no-pipeline", action="store_true",
@@ -158,8 +155,7 @@ def _cfg(args, rows, pipe):
     kw = dict(table_rows=list(rows), sharding=args.sharding, pipeline=pipe,
               dense_comm=args.dense_comm, stream_graphs=not args.no_stream_graphs,
               opt_placement=args.opt_placement,
-              defer_wgrad=None if args.defer_wgrad is None else args.defer_wgrad == "1",
-              emb_stream_cus=args.emb_stream_cus)
+              defer_wgrad=None if args.defer_wgrad is None else args.defer_wgrad == "1")
     if args.model == "dlrm":
         return DLRMConfig(**kw)
     return DLRMConfig(interaction="dcn", pooling=list(MLPERF_MULTIHOT),

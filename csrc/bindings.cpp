@@ -682,19 +682,6 @@ void graph_exec_launch(int64_t ex) {
   TDFO_HIP_OK(hipGraphLaunch(reinterpret_cast<hipGraphExec_t>(ex), cur_stream()));
 }
 
-// A stream whose kernels run only on the CUs set in `words` (32 CUs per word,
-// hipExtStreamCreateWithCUMask): the one-GPU step can confine its
-// memory-bound embedding stream to part of the chip (DLRMConfig.emb_stream_cus).
-int64_t stream_create_cu_mask(std::vector<int64_t> words) {
-  std::vector<uint32_t> m(words.begin(), words.end());
-  TORCH_CHECK(!m.empty(), "stream_create_cu_mask: empty mask");
-  hipStream_t st = nullptr;
-  TDFO_HIP_OK(hipExtStreamCreateWithCUMask(&st, (uint32_t)m.size(), m.data()));
-  return reinterpret_cast<int64_t>(st);
-}
-
-void stream_destroy(int64_t st) { TDFO_HIP_OK(hipStreamDestroy(reinterpret_cast<hipStream_t>(st))); }
-
 void graph_exec_upload(int64_t ex) {
   TDFO_HIP_OK(hipGraphUpload(reinterpret_cast<hipGraphExec_t>(ex), cur_stream()));
 }
@@ -1453,8 +1440,6 @@ TORCH_LIBRARY(tdfo, m) {
   m.def("graph_exec_launch(int ex) -> ()", graph_exec_launch);
   m.def("graph_exec_destroy(int ex) -> ()", graph_exec_destroy);
   m.def("graph_exec_upload(int ex) -> ()", graph_exec_upload);
-  m.def("stream_create_cu_mask(int[] words) -> int", stream_create_cu_mask);
-  m.def("stream_destroy(int st) -> ()", stream_destroy);
   m.def("gemm_batch_begin() -> ()", gemm_batch_begin);
   m.def("gemm_batch_end() -> ()", gemm_batch_end);
   m.def("gemm_pairing(int v) -> int",

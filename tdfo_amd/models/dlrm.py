@@ -113,9 +113,10 @@ class DLRMConfig:
     #   (Rejected, round 4, W > 1 stream graphs: the top weight grads before the bottom
     #   backward so the top bucket reduces beside it -- emulated W=8 0.616-0.621 vs
     #   0.590-0.594 ms/step, config 3 0.872 vs 0.849, config 5 3.035 vs 3.016)
-    emb_stream_cus: int = 0                        # one GPU, per-stream graphs: run the
-    #   embedding stream on this many CUs (a CU-masked HIP stream; 0 = all), leaving the
-    #   rest to the MLP stream's GEMMs beside the memory-bound embedding kernels
+    #   (Rejected, round 4, one GPU: the embedding stream on a CU-masked HIP stream
+    #   (hipExtStreamCreateWithCUMask, 160-224 of 256 CUs) -- DLRM-1TB 2.03-2.23 vs
+    #   0.444 ms/step, DCN-v2 4.57-4.87 vs 2.36: masked queues do not run beside the
+    #   others here)
     stream_graphs: bool = True                     # W > 1, pipelined, capturable comm (native
     #   RCCL / loopback): the step as per-stream hipGraphs with the collectives inside
     #   (dlrm_multirank.py; 3 launches per step) instead of graphs between eagerly issued

@@ -109,12 +109,7 @@ class StreamGraphsMixin:
                           torch.zeros(self.B, device=self.device))
         ev_copy = ops.SyncEvent(2)
         plan = self._ms_plan()
-        self._se_mask = None
-        if self.cfg.emb_stream_cus:
-            self._se_mask = ops.CUMaskedStream(self.device, self.cfg.emb_stream_cus)
-            se = self._se_mask.stream
-        else:
-            se = torch.cuda.Stream(device=self.device)
+        se = torch.cuda.Stream(device=self.device)
         pool = torch.cuda.graph_pool_handle()
         graphs = {}
         se.wait_stream(torch.cuda.current_stream())

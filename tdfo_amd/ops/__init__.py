@@ -147,31 +147,6 @@ class ComposedGraph:
             pass
 
 
-class CUMaskedStream:
-    """A torch stream (``.stream``) whose kernels run only on ``n_cus`` of the
-    device's CUs, spread evenly over the CU mask bits (so over the XCDs).
-    Kept alive by this object (the HIP stream is destroyed with it)."""
-
-    def __init__(self, device, n_cus: int):
-        dev = torch.device(device)
-        total = torch.cuda.get_device_properties(dev).multi_processor_count
-        n = max(1, min(int(n_cus), total))
-        bits = sorted({(j * total) // n for j in range(n)})
-        words = [0] * ((total + 31) // 32)
-        for b in bits:
-            words[b // 32] |= 1 << (b % 32)
-        self.n_cus, self.total = len(bits), total
-        with torch.cuda.device(dev):
-            self._h = int(_native().stream_create_cu_mask(words))
-        self.stream = torch.cuda.ExternalStream(self._h, device=dev)
-
-    def __del__(self):
-        try:
-            _native().stream_destroy(self._h)
-        except Exception:
-            pass
-
-
 def upload_graphs(graphs):
     """hipGraphUpload every executable graph (torch CUDAGraph or
     ComposedGraph) on the current stream, so their first launches do not

@@ -68,32 +68,3 @@ def test_trainer_in_step_matches_loaded_batches():
     assert a.pop_loss() == b.pop_loss()
 
 
-
-def test_cu_masked_embedding_stream_trains_identically():
-    """The embedding stream confined to a subset of the CUs
-    (emb_stream_cus, a CU-masked HIP stream) trains bit-identically: the same
-    kernels, on fewer CUs."""
-    import dataclasses
-
-    from tdfo_amd.data.synthetic import DeviceSyntheticStream
-    from tdfo_amd.models.dlrm import DLRMConfig, DLRMTrainer
-    from tdfo_amd.train.loop import StepLoop
-
-    cfg = DLRMConfig(embedding_dim=128, table_rows=ROWS, bottom=[128], top=[256, 1])
-    B = 512
-    a = DLRMTrainer(cfg, B, DEV)
-    b = DLRMTrainer(dataclasses.replace(cfg, emb_stream_cus=64), B, DEV)
-    loops = [StepLoop(t, DeviceSyntheticStream(ROWS, B, DEV, seed=4)) for t in (a, b)]
-    for lp in loops:
-        lp.run(2)
-        lp.tr.capture_graph(warmup=0)
-        assert lp.tr.graph == "streams"
-        lp.run(6)
-    torch.cuda.synchronize()
-    for t in (a, b):
-        t.sync_streams()
-    torch.cuda.synchronize()
-    assert b._se_mask is not None and b._se_mask.n_cus == 64
-    assert torch.equal(a.fp.p, b.fp.p)
-    assert torch.equal(a.emb.tw_store.weight, b.emb.tw_store.weight)
-    assert a.pop_loss() == b.pop_loss()
