@@ -60,10 +60,11 @@ def parse(argv=None):
     ap.add_argument("--defer-wgrad", default=None, choices=["0", "1"],
                     help="top / cross weight grads after the interaction / cross backward "
                          "(DLRMConfig.defer_wgrad; default: when N > 1)")
-    ap.add_argument("--preheat-ms", type=float, default=0.0,
+    ap.add_argument("--preheat-ms", type=float, default=30.0,
                     help="after the warm-up steps, this many ms of MFMA load on every CU "
-                         "before the timed window (the clock ramps under sustained load: "
-                         "profiles/r04/notes.md); reported in the stderr JSON")
+                         "before the timed window (no training work: the chip's clock ramps "
+                         "under sustained load, and host-launched eager warm-up steps leave "
+                         "it idle; profiles/r04/notes.md); reported in the JSON lines; 0: off")
     ap.add_argument("--dense-comm", default="fp32", choices=["fp32", "bf16"],
                     help="N > 1: wire format of the dense-gradient all-reduce")
     ap.add_argument("--no-pipeline", action="store_true",
@@ -443,6 +444,7 @@ def main(argv=None):
                             and args.batch == 8192 else None),
             "sol_ms": round(sol["sol_ms"], 4),
             "frac_of_sol": round(sol["sol_ms"] / ms, 3),
+            "preheat_ms": args.preheat_ms,
             "dtype": "bf16",
             "data": f"synthetic (Criteo-{args.rows}-shaped, {args.dist} ids, random-init "
                     f"embeddings, {src})",
