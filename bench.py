@@ -65,8 +65,6 @@ def parse(argv=None):
                          "before the timed window (no training work: the chip's clock ramps "
                          "under sustained load, and host-launched eager warm-up steps leave "
                          "it idle; profiles/r04/notes.md); reported in the JSON lines; 0: off")
-    ap.add_argument("--fused-bottom", default=None, choices=["0", "1"],
-                    help="bottom MLP forward as one fused launch (DLRMConfig.fused_bottom)")
     ap.add_argument("--dense-comm", default="fp32", choices=["fp32", "bf16"],
                     help="N > 1: wire format of the dense-gradient all-reduce")
     ap.add_argument("--no-pipeline", action="store_true",
@@ -158,8 +156,7 @@ def _cfg(args, rows, pipe):
     kw = dict(table_rows=list(rows), sharding=args.sharding, pipeline=pipe,
               dense_comm=args.dense_comm, stream_graphs=not args.no_stream_graphs,
               opt_placement=args.opt_placement,
-              defer_wgrad=None if args.defer_wgrad is None else args.defer_wgrad == "1",
-              fused_bottom=None if args.fused_bottom is None else args.fused_bottom == "1")
+              defer_wgrad=None if args.defer_wgrad is None else args.defer_wgrad == "1")
     if args.model == "dlrm":
         return DLRMConfig(**kw)
     return DLRMConfig(interaction="dcn", pooling=list(MLPERF_MULTIHOT),

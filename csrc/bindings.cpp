@@ -682,47 +682,6 @@ void graph_exec_launch(int64_t ex) {
   TDFO_HIP_OK(hipGraphLaunch(reinterpret_cast<hipGraphExec_t>(ex), cur_stream()));
 }
 
-// Fused bottom-MLP forward (mlp_fused.hip): x [B, >=K0]; Ws[l] [N_l, >=K_l]
-// bf16; biases[l] fp32 with stride bstrides[l] (an empty tensor: bias in K);
-// outs[l] [B, >=N_l] bf16.
-void mlp3_fwd(const Tensor& x, std::vector<Tensor> Ws, std::vector<Tensor> biases,
-              std::vector<int64_t> bstrides, std::vector<Tensor> outs, std::vector<int64_t> dims) {
-  TORCH_CHECK(Ws.size() == 3 && biases.size() == 3 && bstrides.size() == 3 && outs.size() == 3 &&
-              dims.size() == 4, "mlp3_fwd: three layers");
-  const int B = (int)x.size(0);
-  const int K0 = (int)dims[0], N0 = (int)dims[1], N1 = (int)dims[2], N2 = (int)dims[3];
-  TORCH_CHECK(tdfo::mlp3_fwd_supported(K0, N0, N1, N2, B), "mlp3_fwd: unsupported shape");
-  const int K[3] = {K0, N0, N1}, N[3] = {N0, N1, N2};
-  check_dev(x, "x");
-  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.dim() == 2 && x.stride(1) == 1 &&
-              x.size(1) >= K0 && x.stride(0) % 8 == 0 && aligned16(x.data_ptr()), "mlp3_fwd: x");
-  tdfo::Mlp3Args a{};
-  a.x = reinterpret_cast<const uint16_t*>(x.data_ptr()); a.ldx = x.stride(0); a.B = B;
-  for (int l = 0; l < 3; ++l) {
-    const Tensor& W = Ws[l];
-    check_dev(W, "W");
-    TORCH_CHECK(W.scalar_type() == at::kBFloat16 && W.dim() == 2 && W.stride(1) == 1 &&
-                W.size(0) == N[l] && W.size(1) >= K[l] && W.stride(0) % 8 == 0 &&
-                aligned16(W.data_ptr()), "mlp3_fwd: W");
-    const Tensor& o = outs[l];
-    check_dev(o, "out");
-    TORCH_CHECK(o.scalar_type() == at::kBFloat16 && o.dim() == 2 && o.stride(1) == 1 &&
-                o.size(0) == B && o.size(1) >= N[l] && o.stride(0) % 4 == 0 &&
-                (reinterpret_cast<uintptr_t>(o.data_ptr()) & 7) == 0, "mlp3_fwd: out");
-    a.W[l] = reinterpret_cast<const uint16_t*>(W.data_ptr()); a.ldw[l] = W.stride(0);
-    a.out[l] = reinterpret_cast<uint16_t*>(o.data_ptr()); a.ldo[l] = o.stride(0);
-    if (biases[l].defined() && biases[l].numel() > 0) {
-      const Tensor& b = biases[l];
-      check_dev(b, "bias");
-      TORCH_CHECK(b.scalar_type() == at::kFloat &&
-                  b.storage_offset() + (N[l] - 1) * bstrides[l] < b.storage().nbytes() / 4,
-                  "mlp3_fwd: bias");
-      a.bias[l] = b.data_ptr<float>(); a.bstride[l] = bstrides[l];
-    }
-  }
-  tdfo::mlp3_fwd(a, K0, N0, N1, N2, cur_stream());
-}
-
 void graph_exec_upload(int64_t ex) {
   TDFO_HIP_OK(hipGraphUpload(reinterpret_cast<hipGraphExec_t>(ex), cur_stream()));
 }
@@ -1481,8 +1440,6 @@ TORCH_LIBRARY(tdfo, m) {
   m.def("graph_exec_launch(int ex) -> ()", graph_exec_launch);
   m.def("graph_exec_destroy(int ex) -> ()", graph_exec_destroy);
   m.def("graph_exec_upload(int ex) -> ()", graph_exec_upload);
-  m.def("mlp3_fwd(Tensor x, Tensor[] Ws, Tensor[] biases, int[] bstrides, Tensor(a!)[] outs, "
-        "int[] dims) -> ()", mlp3_fwd);
   m.def("gemm_batch_begin() -> ()", gemm_batch_begin);
   m.def("gemm_batch_end() -> ()", gemm_batch_end);
   m.def("gemm_pairing(int v) -> int",

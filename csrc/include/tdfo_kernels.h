@@ -38,18 +38,7 @@ struct GemmArgs {
 };
 void gemm_bf16(const GemmArgs& a, hipStream_t s);
 
-// Fused 3-layer bias + ReLU MLP forward (mlp_fused.hip): out[l] = relu(in[l]
-// W[l][:, :K_l]^T + bias[l]), in[0] = x, in[l+1] = out[l]; bias[l] null when
-// it rides in K (augmented input column). Shapes: mlp3_fwd_supported.
-struct Mlp3Args {
-  const uint16_t* x; int64_t ldx;
-  const uint16_t* W[3]; int64_t ldw[3];
-  const float* bias[3]; int64_t bstride[3];
-  uint16_t* out[3]; int64_t ldo[3];
-  int B;
-};
-bool mlp3_fwd_supported(int K0, int N0, int N1, int N2, int B);
-void mlp3_fwd(const Mlp3Args& a, int K0, int N0, int N1, int N2, hipStream_t s);
+
 // Launch n independent GEMMs in order; consecutive (weight grad, dgrad)
 // pairs on the small-tile kernel share one paired launch (gemm_pairing(0):
 // never). Returns after enqueueing.

@@ -1024,17 +1024,6 @@ int emb_rif() {
   return v;
 }
 
-// A/B (TDFO_EMB_FWD_GRID): cap on the lookup grid (grid-stride loops), so the
-// lookup leaves register / wave room on every CU for the MLP kernels that run
-// beside it instead of flooding the chip (0: 8192 blocks)
-int64_t fwd_grid_cap() {
-  static const int64_t v = [] {
-    const char* e = getenv("TDFO_EMB_FWD_GRID");
-    return e ? (int64_t)atoll(e) : (int64_t)0;
-  }();
-  return v;
-}
-
 void embedding_bag_fwd(const EmbFwdArgs& a, hipStream_t s) {
   const int64_t nbags = (int64_t)a.T * a.B;
   if (nbags == 0) return;
@@ -1043,7 +1032,6 @@ void embedding_bag_fwd(const EmbFwdArgs& a, hipStream_t s) {
   const int64_t waves = (nbags * lpb + 63) / 64;
   int64_t blocks = (waves + 3) / 4;
   if (blocks > 8192) blocks = 8192;
-  if (fwd_grid_cap() > 0 && blocks > fwd_grid_cap()) blocks = fwd_grid_cap();
 #define TDFO_EF(DD)                                                            \
   if (a.onehot && !a.mean) {                                                   \
     if (a.out_bf16) hipLaunchKernelGGL((emb_fwd_onehot_kernel<DD, true>),      \

@@ -117,8 +117,10 @@ class DLRMConfig:
     #   (hipExtStreamCreateWithCUMask, 160-224 of 256 CUs) -- DLRM-1TB 2.03-2.23 vs
     #   0.444 ms/step, DCN-v2 4.57-4.87 vs 2.36: masked queues do not run beside the
     #   others here)
-    fused_bottom: Optional[bool] = None            # bottom MLP forward as one fused launch
-    #   (ops.mlp3_fwd, 64 -> 512 -> 256 -> 128 only; None: off)
+    #   (Rejected, round 4: the bottom MLP forward as one fused 3-layer launch with the
+    #   activations in LDS -- 22.6 vs 26.8 us of kernel, but its 55-KB / 177-VGPR blocks
+    #   wait ~47 us for CUs the concurrent lookup fills: DLRM-1TB 0.448-0.450 vs
+    #   0.443-0.444 ms/step, W=8 0.591-0.593 vs 0.588-0.591, DCN-v2 neutral)
     stream_graphs: bool = True                     # W > 1, pipelined, capturable comm (native
     #   RCCL / loopback): the step as per-stream hipGraphs with the collectives inside
     #   (dlrm_multirank.py; 3 launches per step) instead of graphs between eagerly issued
@@ -792,24 +794,7 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
         for kind, fn in self._stages():
             self._run_stage(kind, fn)
 
-    def _bottom_fused_ok(self) -> bool:
-        Ls = self.bottom_layers
-        if not self.cfg.fused_bottom or self.device.type != "cuda" or len(Ls) != 3:
-            return False
-        dims = [Ls[0].in_k, Ls[0].out, Ls[1].out, Ls[2].out]
-        return (ops.mlp3_fwd_supported(dims, self.B) and Ls[0].bias_in_k
-                and Ls[1].in_k == Ls[0].out and Ls[2].in_k == Ls[1].out)
-
     def _s_bottom_fwd(self):
-        if self._bottom_fused_ok():
-            Ls = self.bottom_layers
-            Ws = [self.fp.bf16(L.name + ".w") for L in Ls]
-            biases = [None if L.bias_in_k else self.fp.param(L.name + ".w")[:, L.bcol]
-                      for L in Ls]
-            outs = [self.bot_in[1][:, :Ls[0].out], self.bot_in[2][:, :Ls[1].out], self.h_out]
-            ops.mlp3_fwd(self.x0, Ws, biases, [L.wcols for L in Ls], outs,
-                         [Ls[0].in_k, Ls[0].out, Ls[1].out, Ls[2].out])
-            return
         n = len(self.bottom_layers)
         for i, L in enumerate(self.bottom_layers):
             out = self.bot_in[i + 1][:, :L.out] if i + 1 < n else self.h_out

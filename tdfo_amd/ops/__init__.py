@@ -650,28 +650,6 @@ def bump(counters):
             t.view(-1)[:1].add_(1)
 
 
-def mlp3_fwd_supported(dims, B: int) -> bool:
-    """dims = [K0, N0, N1, N2] of the fused three-layer forward (mlp_fused.hip)."""
-    return list(dims) == [64, 512, 256, 128] and B % 32 == 0
-
-
-def mlp3_fwd(x, Ws, biases, bstrides, outs, dims):
-    """Fused bias + ReLU three-layer forward: outs[l] = relu(in_l W_l[:, :K_l]^T
-    + b_l) with in_0 = x, in_{l+1} = outs[l]; biases[l] None when it rides in
-    K (a 1.0 input column). GPU: one launch; CPU: three reference GEMMs."""
-    K = [dims[0], dims[1], dims[2]]
-    if _gpu(x):
-        empty = torch.empty(0, dtype=torch.float32, device=x.device)
-        _native().mlp3_fwd(x, list(Ws), [b if b is not None else empty for b in biases],
-                           [int(v) for v in bstrides], list(outs), [int(d) for d in dims])
-        return
-    inp = x
-    for l in range(3):
-        ref.gemm(inp[:, :K[l]], False, Ws[l][:, :K[l]], False, biases[l], True, None, outs[l],
-                 None, 1, None, None, None, 0, -1)
-        inp = outs[l]
-
-
 def burn_us(us: float):
     """MFMA load on every CU for ``us`` microseconds (device warm-up)."""
     _native().burn_us(float(us))

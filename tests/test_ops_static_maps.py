@@ -53,24 +53,3 @@ def test_slab_reduce_cpu():
     for sl, S, out in segs:
         assert torch.allclose(out, sl.view(S, -1).sum(0))
 
-
-def test_mlp3_fwd_cpu_is_three_relu_gemms():
-    """CPU reference of the fused three-layer forward: three bias + ReLU
-    GEMMs chained through the output buffers."""
-    g = torch.Generator().manual_seed(0)
-    B = 8
-    x = torch.zeros(B, 64)
-    x[:, :13] = torch.randn(B, 13, generator=g)
-    x[:, 13] = 1.0
-    Ws = [torch.randn(512, 64, generator=g), torch.randn(256, 576, generator=g),
-          torch.randn(128, 320, generator=g)]
-    b1, b2 = torch.randn(256, generator=g), torch.randn(128, generator=g)
-    outs = [torch.empty(B, 512), torch.empty(B, 256), torch.empty(B, 128)]
-    ops.mlp3_fwd(x, Ws, [None, b1, b2], [64, 576, 320], outs, [64, 512, 256, 128])
-    h1 = torch.relu(x @ Ws[0].t())
-    h2 = torch.relu(h1 @ Ws[1][:, :512].t() + b1)
-    h3 = torch.relu(h2 @ Ws[2][:, :256].t() + b2)
-    for o, r in zip(outs, (h1, h2, h3)):
-        assert torch.allclose(o, r, rtol=1e-4, atol=1e-4)
-    assert ops.mlp3_fwd_supported([64, 512, 256, 128], 8192)
-    assert not ops.mlp3_fwd_supported([64, 512, 256, 64], 8192)
