@@ -15,6 +15,7 @@ namespace tdfo {
 namespace {
 
 constexpr int HEAD_SPB = 16;  // samples per block (4 per wave)
+static_assert(HEAD_SPB % 4 == 0, "head: samples split over the 4 waves");
 
 template <int K>
 __global__ __launch_bounds__(256) void head_bce_kernel(
@@ -34,18 +35,29 @@ __global__ __launch_bounds__(256) void head_bce_kernel(
   const float bias = bptr[0];
   float db = 0.f, lsum = 0.f;
   const int s0 = blockIdx.x * HEAD_SPB;
-  for (int si = wv; si < HEAD_SPB; si += 4) {
-    const int s = s0 + si;
-    if (s >= B) break;
-    const uint16_t* hp = H + (int64_t)s * ldh + e0;
-    float hv[EPL];
+  // the wave's HEAD_SPB / 4 samples: every H row and label loaded before the
+  // first use (clamped rows; the loop below stops at B), so the wave pays one
+  // memory round trip instead of one per sample (same per-sample math and
+  // accumulation order as a sample-at-a-time loop)
+  constexpr int SPW = HEAD_SPB / 4;
+  float hv[SPW][EPL], yv[SPW];
 #pragma unroll
-    for (int u = 0; u < EPL; ++u) hv[u] = act ? bf2f(hp[u]) : 0.f;
+  for (int q = 0; q < SPW; ++q) {
+    const int s = min(s0 + wv + 4 * q, B - 1);
+    const uint16_t* hp = H + (int64_t)s * ldh + e0;
+#pragma unroll
+    for (int u = 0; u < EPL; ++u) hv[q][u] = act ? bf2f(hp[u]) : 0.f;
+    yv[q] = label[s];
+  }
+#pragma unroll
+  for (int q = 0; q < SPW; ++q) {
+    const int s = s0 + wv + 4 * q;
+    if (s >= B) break;
     float d = 0.f;
 #pragma unroll
-    for (int u = 0; u < EPL; ++u) d += hv[u] * wr[u];
+    for (int u = 0; u < EPL; ++u) d += hv[q][u] * wr[u];
     const float x = wave_sum(d) + bias;
-    const float y = label[s];
+    const float y = yv[q];
     const float sig = 1.f / (1.f + __expf(-x));
     const float g = (sig - y) * inv_n;
     if (lane == 0) {
@@ -58,9 +70,9 @@ __global__ __launch_bounds__(256) void head_bce_kernel(
 #pragma unroll
       for (int u = 0; u < EPL; ++u) {
         float gh = g * wr[u];
-        if (relu_mask && !(hv[u] > 0.f)) gh = 0.f;
+        if (relu_mask && !(hv[q][u] > 0.f)) gh = 0.f;
         dp[u] = f2bf(gh);
-        dw[u] += g * hv[u];
+        dw[u] += g * hv[q][u];
       }
     }
   }
@@ -126,15 +138,41 @@ __global__ __launch_bounds__(256) void head_reduce_kernel(const float* __restric
   const int c = threadIdx.x % COLS, ph = threadIdx.x / COLS;
   const int j = blockIdx.x * COLS + c;
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  if (j < ld) {
-    int r = ph;
-    for (; r + 3 * PH < nparts; r += 4 * PH) {
-      s0 += part[(int64_t)r * ld + j];
-      s1 += part[(int64_t)(r + PH) * ld + j];
-      s2 += part[(int64_t)(r + 2 * PH) * ld + j];
-      s3 += part[(int64_t)(r + 3 * PH) * ld + j];
+  if (j < ld && nparts > 0) {
+    // The first PRE rows of this thread (r = ph, ph + PH, ...) are loaded
+    // up front at clamped addresses and then added in the loop's order
+    // (groups of four into s0..s3, a partial last group into s0), so the
+    // sums are those of the plain loop below with one round trip for up to
+    // PRE * PH = 512 partial rows (B = 8192) instead of one per group.
+    constexpr int PRE = 32;
+    float v[PRE];
+#pragma unroll
+    for (int q = 0; q < PRE; ++q) {
+      const int r = min(ph + q * PH, nparts - 1);
+      v[q] = part[(int64_t)r * ld + j];
     }
-    for (; r < nparts; r += PH) s0 += part[(int64_t)r * ld + j];
+#pragma unroll
+    for (int g = 0; g < PRE / 4; ++g) {
+      const int r = ph + 4 * g * PH;
+      if (r + 3 * PH < nparts) {
+        s0 += v[4 * g]; s1 += v[4 * g + 1]; s2 += v[4 * g + 2]; s3 += v[4 * g + 3];
+      } else {
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+          if (r + q * PH < nparts) s0 += v[4 * g + q];
+      }
+    }
+    int r = ph + PRE * PH;
+    if (r < nparts) {
+      // (more than PRE * PH rows: every group above was full)
+      for (; r + 3 * PH < nparts; r += 4 * PH) {
+        s0 += part[(int64_t)r * ld + j];
+        s1 += part[(int64_t)(r + PH) * ld + j];
+        s2 += part[(int64_t)(r + 2 * PH) * ld + j];
+        s3 += part[(int64_t)(r + 3 * PH) * ld + j];
+      }
+      for (; r < nparts; r += PH) s0 += part[(int64_t)r * ld + j];
+    }
   }
   red[ph][c] = (s0 + s1) + (s2 + s3);
   __syncthreads();

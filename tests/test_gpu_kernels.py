@@ -737,6 +737,41 @@ def test_head_reduce_and_step_bumps():
     assert float(h1[1]) == 5.0 and float(h2[1]) == 10.0 and float(h1[0]) == pytest.approx(0.1)
 
 
+def _fixed_order_column_sums(p, PH=16):
+    """head_reduce's summation order in fp32: per column, row phase ph sums
+    rows ph, ph + PH, ... into four accumulators (groups of four rows, a
+    partial last group into the first), then the phases are added in order."""
+    n = p.shape[0]
+    out = torch.zeros(p.shape[1], dtype=torch.float32)
+    for ph in range(PH):
+        s = [torch.zeros(p.shape[1], dtype=torch.float32) for _ in range(4)]
+        r = ph
+        while r + 3 * PH < n:
+            for q in range(4):
+                s[q] = s[q] + p[r + q * PH]
+            r += 4 * PH
+        while r < n:
+            s[0] = s[0] + p[r]
+            r += PH
+        out = out + ((s[0] + s[1]) + (s[2] + s[3]))
+    return out
+
+
+@pytest.mark.parametrize("nparts", [37, 512, 600])
+def test_head_reduce_fixed_order(nparts):
+    """The preloaded head_reduce adds the partial rows in the plain loop's
+    order: bit-identical to that order for <= 512 rows and past it."""
+    torch.manual_seed(17)
+    K = 256
+    part = torch.randn(nparts * (K + 2), device=DEV)
+    grad = torch.empty(K + 1, device=DEV)
+    loss = torch.zeros(1, device=DEV)
+    ops.head_reduce(part, nparts, K, grad, loss)
+    want = _fixed_order_column_sums(part.view(nparts, K + 2).cpu())
+    assert torch.equal(grad.cpu(), want[: K + 1])
+    assert torch.equal(loss.cpu(), want[K + 1:])
+
+
 @pytest.mark.parametrize("opt", ["adamw", "sgd_momentum", "adagrad"])
 def test_dense_optimizer_slab_segments(opt):
     """Split-K weight-grad slabs summed inside the optimizer == reduce then step
