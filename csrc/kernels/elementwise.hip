@@ -172,44 +172,26 @@ __global__ __launch_bounds__(256) void gather_columns_kernel(GatherColsArgs a) {
 // fp32 labels and the fp32 dense features cast into the bf16 bottom-MLP input
 // (row stride ldx, first nd columns). Replaces three copies and a cast kernel
 // per step (each small launch costs ~5 us of device time).
-// One thread per batch row (plus one per pair of ids): the row's dense
-// features are loaded together and stored as bf16 pairs (a 4-byte store per
-// two columns, the last column of an odd count alone: column nd of x0 may be
-// the bias ones-column of the augmented layout and is never written).
-// (Before: one thread per element, an int64 divide and a 2-byte store each --
-// 8.6 us in the DLRM step for 0.5 MB, profiles/r04/final/prof_dlrm.)
 __global__ __launch_bounds__(256) void batch_load_kernel(
     const float* __restrict__ dense, int nd, int64_t ld_dense, uint16_t* __restrict__ x0,
     int64_t ldx, const int64_t* __restrict__ ids, int64_t* __restrict__ ids_dst, int64_t n,
-    const float* __restrict__ label, float* __restrict__ label_dst, int B, int pairs) {
-  const int64_t n2 = n / 2, ni = n2 + (n & 1);
-  const int64_t total = ni > B ? ni : (int64_t)B;
+    const float* __restrict__ label, float* __restrict__ label_dst, int B) {
+  const int64_t n2 = n / 2, nden = (int64_t)B * nd;
+  const int64_t total = n2 + (n & 1) + nden + B;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
-    if (i < n2) ((longlong2*)ids_dst)[i] = ((const longlong2*)ids)[i];
-    else if (i < ni) ids_dst[n - 1] = ids[n - 1];
-    if (i < B) {
-      const float* src = dense + i * ld_dense;
-      uint16_t* dst = x0 + i * ldx;
-      label_dst[i] = label[i];
-      if (pairs && nd > 0 && nd <= 16) {
-        // every load in flight before the first store (clamped addresses)
-        float v[16];
-#pragma unroll
-        for (int c = 0; c < 16; ++c) v[c] = src[c < nd ? c : nd - 1];
-#pragma unroll
-        for (int c = 0; c < 16; c += 2) {
-          if (c + 1 < nd) *(uint32_t*)(dst + c) = pack2bf(v[c], v[c + 1]);
-          else if (c < nd) dst[c] = f2bf(v[c]);
-        }
-      } else if (pairs) {
-        int c = 0;
-        for (; c + 1 < nd; c += 2)
-          *(uint32_t*)(dst + c) = pack2bf(src[c], src[c + 1]);
-        if (c < nd) dst[c] = f2bf(src[c]);
-      } else {
-        for (int c = 0; c < nd; ++c) dst[c] = f2bf(src[c]);
-      }
+    if (i < n2) {
+      ((longlong2*)ids_dst)[i] = ((const longlong2*)ids)[i];
+    } else if (i < n2 + (n & 1)) {
+      ids_dst[n - 1] = ids[n - 1];
+    } else if (i < n2 + (n & 1) + nden) {
+      const int64_t e = i - n2 - (n & 1);
+      const int64_t b = e / nd;
+      const int c = (int)(e - b * nd);
+      x0[b * ldx + c] = f2bf(dense[b * ld_dense + c]);
+    } else {
+      const int64_t b = i - n2 - (n & 1) - nden;
+      label_dst[b] = label[b];
     }
   }
 }
@@ -368,14 +350,12 @@ void spin_ticks(uint64_t ticks, hipStream_t s) {
 void batch_load(const float* dense, int nd, int64_t ld_dense, uint16_t* x0, int64_t ldx,
                 const int64_t* ids, int64_t* ids_dst, int64_t n, const float* label,
                 float* label_dst, int B, hipStream_t s) {
-  const int64_t ni = n / 2 + (n & 1);
-  const int64_t total = ni > B ? ni : (int64_t)B;
+  const int64_t total = n / 2 + (n & 1) + (int64_t)B * nd + B;
   if (total <= 0) return;
   int64_t blocks = (total + 255) / 256;
   if (blocks > 2048) blocks = 2048;
-  const int pairs = (ldx % 2 == 0) && (((uintptr_t)x0 & 3) == 0);
   hipLaunchKernelGGL(batch_load_kernel, dim3(blocks), dim3(256), 0, s, dense, nd, ld_dense, x0,
-                     ldx, ids, ids_dst, n, label, label_dst, B, pairs);
+                     ldx, ids, ids_dst, n, label, label_dst, B);
   TDFO_CHECK_HIP(hipGetLastError());
 }
 
