@@ -209,7 +209,10 @@ template <typename K>
 __global__ void emb_keys_kernel(const EmbBwdArgs a, K* __restrict__ keys,
                                         int32_t* __restrict__ vals, int64_t* __restrict__ goff,
                                         float* __restrict__ gscale, int32_t* __restrict__ tail_count) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) *tail_count = 0;  // read by later kernels
+  if (blockIdx.x == 0 && threadIdx.x == 0) {  // read by later kernels
+    tail_count[0] = 0;
+    tail_count[1] = 0;
+  }
   const int64_t nbags = (int64_t)a.T * a.B;
   for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < a.nnz;
        p += (int64_t)gridDim.x * blockDim.x) {
@@ -271,7 +274,10 @@ __global__ __launch_bounds__(SEG_THREADS) void emb_segsort_kernel(
   __shared__ uint32_t wsum[SEG_WAVES];
   __shared__ uint32_t smax[SEG_WAVES];
   const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  if (t == 0 && tid == 0) *tail_count = 0;          // read by later kernels
+  if (t == 0 && tid == 0) {                         // read by later kernels
+    tail_count[0] = 0;
+    tail_count[1] = 0;
+  }
   const int n = a.B;
   const int64_t s0 = (int64_t)t * a.B;
   uint32_t key[SEG_K], val[SEG_K];
@@ -690,11 +696,21 @@ __global__ __launch_bounds__(256) void emb_chunk_kernel(
 // Runs crossing chunk edges: the chunk where a run starts adds the head
 // partials of the chunks the run covers (found by binary search), in chunk
 // order with 8 loads in flight, and applies the optimizer once.
+// Runs longer than COMBINE_LONG chunks (hot rows of skewed ids: a Zipf-1.05
+// DCN-v2 batch has runs of ~1.4 K chunks) are left to
+// emb_combine_long_kernel, which splits the walk over a block's 16 waves: one
+// wave walking them took 140 us of the DCN-v2 step. One-hot batches whose
+// longest possible run (R sources x B ids) fits in COMBINE_LONG chunks never
+// divert and skip that launch (DLRM-1TB at W=1: the 3-row tables' 85-chunk
+// runs stay here; diverting runs over 64 chunks cost it 16 us per step).
+constexpr int COMBINE_LONG = 256;
+constexpr int LONG_WAVES = 16;
+
 template <int D, typename K, int OPT, int CH>
 __global__ __launch_bounds__(256) void emb_combine_kernel(
     EmbBwdArgs a, const K* __restrict__ keys, const float* __restrict__ head,
     const float* __restrict__ tail, const int32_t* __restrict__ tail_list,
-    const int32_t* __restrict__ tail_count) {
+    int32_t* __restrict__ tail_count, int64_t* __restrict__ long_list, int allow_long) {
   constexpr int EPL = BwdCfg<D>::EPL;
   const int lane = threadIdx.x & 63;
   const int nw = (gridDim.x * blockDim.x) >> 6;
@@ -726,6 +742,14 @@ __global__ __launch_bounds__(256) void emb_combine_kernel(
       jlast += cnt;
       if (cnt < 64) break;
     }
+    if (allow_long && jlast - c > COMBINE_LONG) {
+      if (lane == 0) {
+        const int slot = atomicAdd(tail_count + 1, 1);
+        long_list[2 * slot] = c;
+        long_list[2 * slot + 1] = jlast;
+      }
+      continue;
+    }
     // HQ head partials in flight: a skewed table's runs span up to B/CH
     // chunks (a 3-row table: ~85 per run at B = 8192), and this walk is the
     // kernel's latency tail (8 in flight: 15 us per DLRM-1TB step)
@@ -755,6 +779,74 @@ __global__ __launch_bounds__(256) void emb_combine_kernel(
   }
 }
 
+// One block of LONG_WAVES waves per long run (block-stride over the list):
+// wave w sums the head partials of a contiguous 1/LONG_WAVES of the run's
+// chunks in chunk order (HQ loads in flight), and wave 0 adds the run's tail
+// partial and the waves' sums in wave order, then applies the optimizer once.
+// Fixed order throughout: bitwise reproducible.
+template <int D, typename K, int OPT, int CH>
+__global__ __launch_bounds__(64 * LONG_WAVES) void emb_combine_long_kernel(
+    EmbBwdArgs a, const K* __restrict__ keys, const float* __restrict__ head,
+    const float* __restrict__ tail, const int32_t* __restrict__ tail_count,
+    const int64_t* __restrict__ long_list) {
+  constexpr int EPL = BwdCfg<D>::EPL;
+  __shared__ float part[LONG_WAVES][64 * EPL];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (skip_step(a)) return;
+  const int n = tail_count[1];
+  const int e0 = elem0<D>(lane);
+  const bool act = D >= 64 || e0 < D;
+  const int e0c = act ? e0 : 0;
+  const OptScalars o = opt_scalars(a);
+  constexpr int HQ = EPL <= 2 ? 32 : (EPL <= 4 ? 16 : 8);
+  for (int i = blockIdx.x; i < n; i += gridDim.x) {
+    const int64_t c = long_list[2 * i], jlast = long_list[2 * i + 1];
+    const int64_t len = jlast - c;                     // chunks c+1 .. jlast
+    const int64_t j_lo = c + 1 + len * w / LONG_WAVES;
+    const int64_t j_hi = c + 1 + len * (w + 1) / LONG_WAVES;   // exclusive
+    float acc[EPL];
+#pragma unroll
+    for (int u = 0; u < EPL; ++u) acc[u] = 0.f;
+    for (int64_t j0 = j_lo; j0 < j_hi; j0 += HQ) {
+      float hv[HQ][EPL];
+#pragma unroll
+      for (int q = 0; q < HQ; ++q) {
+        const int64_t j = min(j0 + q, j_hi - 1);
+#pragma unroll
+        for (int u = 0; u < EPL; ++u) hv[q][u] = head[j * D + e0c + u];
+      }
+#pragma unroll
+      for (int q = 0; q < HQ; ++q) {
+        if (j0 + q < j_hi) {
+#pragma unroll
+          for (int u = 0; u < EPL; ++u) acc[u] += hv[q][u];
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < EPL; ++u) part[w][lane * EPL + u] = acc[u];
+    __syncthreads();
+    if (w == 0) {
+      float t[EPL];
+#pragma unroll
+      for (int u = 0; u < EPL; ++u) t[u] = act ? tail[c * D + e0 + u] : 0.f;
+      for (int q = 0; q < LONG_WAVES; ++q) {
+#pragma unroll
+        for (int u = 0; u < EPL; ++u) t[u] += part[q][lane * EPL + u];
+      }
+      const int64_t endc = min((c + 1) * CH, a.nnz);
+      const K last = keys[endc - 1];
+      float wv[EPL];
+#pragma unroll
+      for (int u = 0; u < EPL; ++u) wv[u] = 0.f;
+      if constexpr (OPT != EMB_DENSE_GRAD) load_row<D>(wv, a.W + (uint64_t)last * D + e0c);
+      const float st = OPT == EMB_ROWWISE_ADAGRAD ? a.state1[(uint64_t)last] : 0.f;
+      update_row<D, OPT>(a, o, (uint64_t)last, t, wv, st, lane);
+    }
+    __syncthreads();                                   // part[] is reused
+  }
+}
+
 // Row-wise owner backward: entry (r, i) of the received [W][cap+1] exchange
 // buffer (rowwise.hip) -> key = owner-local row, val = position, gradient
 // row offset in the all-gathered [W][B][grad_ld] pooled gradients. Slots past
@@ -767,7 +859,10 @@ __global__ void emb_rw_keys_kernel(const EmbBwdArgs a, const int64_t* __restrict
                                    K* __restrict__ keys, int32_t* __restrict__ vals,
                                    int64_t* __restrict__ goff, float* __restrict__ gscale,
                                    int32_t* __restrict__ tail_count) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) *tail_count = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    tail_count[0] = 0;
+    tail_count[1] = 0;
+  }
   const int64_t* L = meta + nrw;
   for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < a.nnz;
        p += (int64_t)gridDim.x * blockDim.x) {
@@ -877,7 +972,7 @@ int g_emb_segsort = 1;   // one-hot batches: per-table LDS sort (0: device-wide 
 
 struct WsLayout {
   size_t keys_in, keys_out, vals_in, vals_out, goff, gscale, head, tail, tlist, tcount, sortws,
-      pos;
+      pos, llist;
   size_t total;
 };
 
@@ -901,6 +996,7 @@ WsLayout ws_layout(int64_t nnz, int D) {
   L.tcount = o;   o += al(16);
   L.sortws = o;   o += al(radix_sort_workspace(nnz));
   L.pos = o;      o += al(nnz * 4);
+  L.llist = o;    o += al((size_t)(nch / COMBINE_LONG + 1) * 16);   // (c, jlast) per long run
   L.total = o;
   return L;
 }
@@ -989,9 +1085,21 @@ void apply_impl(const EmbBwdArgs& a0, const WsLayout& L, hipStream_t s) {
     TDFO_CHECK_HIP(hipGetLastError());
     int64_t cblocks = (nch + 3) / 4;
     if (cblocks > 1024) cblocks = 1024;
+    int64_t* llist = (int64_t*)(ws + L.llist);
+    // one id per bag (segsort = R sources): no run is longer than R x B ids
+    const bool may_long =
+        !(a.segsort > 0 && (int64_t)a.segsort * a.B <= (int64_t)COMBINE_LONG * CH);
     hipLaunchKernelGGL((emb_combine_kernel<D, K, OPT, CH>), dim3(cblocks), dim3(256), 0, s, a,
-                       keys_out, head, tail, tlist, tcount);
+                       keys_out, head, tail, tlist, tcount, llist, (int)may_long);
     TDFO_CHECK_HIP(hipGetLastError());
+    if (may_long) {
+      // long runs: at most nch / COMBINE_LONG of them
+      int64_t lblocks = nch / COMBINE_LONG + 1;
+      if (lblocks > 256) lblocks = 256;
+      hipLaunchKernelGGL((emb_combine_long_kernel<D, K, OPT, CH>), dim3(lblocks),
+                         dim3(64 * LONG_WAVES), 0, s, a, keys_out, head, tail, tcount, llist);
+      TDFO_CHECK_HIP(hipGetLastError());
+    }
   };
   run(std::integral_constant<int, BwdCfg<D>::CH>{});
 }

@@ -255,6 +255,49 @@ def test_embedding_bwd_fused(opt, skew, D):
         assert (dg - edg).abs().max() < 1e-4 * max(1.0, edg.abs().max().item())
 
 
+@pytest.mark.parametrize("opt", [ops.EMB_SGD, ops.EMB_ROWWISE_ADAGRAD, ops.EMB_ADAM,
+                                 ops.EMB_ADAGRAD, ops.EMB_DENSE_GRAD])
+def test_embedding_bwd_long_runs(opt):
+    """Hot rows whose runs span hundreds of chunks (a 3-row table under a
+    multi-hot batch: ~16 k ids per row, ~500 chunks) take the block-wide
+    combine: equal to the fp32 reference and bitwise reproducible."""
+    T, B, L, D = 2, 8192, 12, 128
+    rows = [3, 5000]
+    W, ro, idx, offs = _emb_case(T, B, rows, D, L, True, seed=5)
+    W, ro, idx, offs = (x.to(DEV) for x in (W, ro, idx, offs))
+    goff = torch.tensor([t * D for t in range(T)], device=DEV)
+    grad = torch.randn(B * T * D, device=DEV) * 0.01
+    hyper = torch.tensor([0.05, 3.0], device=DEV)
+    n1 = W.shape[0] if opt == ops.EMB_ROWWISE_ADAGRAD else W.numel()
+    s1 = torch.rand(n1, device=DEV) if opt in (ops.EMB_ROWWISE_ADAGRAD, ops.EMB_ADAGRAD,
+                                                ops.EMB_ADAM) else None
+    s2 = torch.rand(W.numel(), device=DEV) if opt == ops.EMB_ADAM else None
+    res = []
+    for _ in range(2):
+        Wn = W.clone()
+        a1 = s1.clone() if s1 is not None else None
+        a2 = s2.clone() if s2 is not None else None
+        dg = torch.zeros(W.numel(), device=DEV) if opt == ops.EMB_DENSE_GRAD else None
+        ops.embedding_bwd(Wn, ro, idx, offs, goff, T, B, grad, T * D, opt, hyper, state1=a1,
+                          state2=a2, dense_grad=dg)
+        res.append((Wn, a1, dg))
+    torch.cuda.synchronize()
+    assert torch.equal(res[0][0], res[1][0])
+    if opt == ops.EMB_DENSE_GRAD:
+        assert torch.equal(res[0][2], res[1][2])
+    We = W.clone()
+    e1 = s1.clone() if s1 is not None else None
+    e2 = s2.clone() if s2 is not None else None
+    edg = torch.zeros(W.numel(), device=DEV) if opt == ops.EMB_DENSE_GRAD else None
+    ref.embedding_bwd(We, ro, idx, offs, goff, None, T, B, False, 20, grad, T * D, opt, e1, e2,
+                      hyper, 1e-8, 0.9, 0.999, 0.0, edg)
+    assert (res[0][0] - We).abs().max() < 1e-4 * max(1.0, We.abs().max().item())
+    if edg is not None:
+        assert (res[0][2] - edg).abs().max() < 1e-4 * max(1.0, edg.abs().max().item())
+    if e1 is not None:
+        assert (res[0][1] - e1).abs().max() < 1e-3 * max(1.0, e1.abs().max().item())
+
+
 @pytest.mark.parametrize("B", [700, 8192])
 @pytest.mark.parametrize("skew", [False, True])
 @pytest.mark.parametrize("opt", [ops.EMB_ROWWISE_ADAGRAD, ops.EMB_ADAM])
