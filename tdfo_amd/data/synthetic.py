@@ -185,6 +185,18 @@ class DeviceSyntheticStream:
             st.wait_event(ev)
         return self.bufs[s], s
 
+    @property
+    def copy_stream(self):
+        """The generator's stream: a consumer may copy a batch out of its
+        slot there (in order behind the generation, and before the slot is
+        regenerated)."""
+        return self.gs
+
+    def owns(self, t: torch.Tensor) -> bool:
+        """``t`` is one of this stream's slot buffers (ids, dense or labels)."""
+        p = t.data_ptr()
+        return any(p == b.data_ptr() for bs in self.bufs for b in bs)
+
     def release(self, slot: int, streams=None):
         sts = streams or [torch.cuda.current_stream(self.dev)]
         pool = self.rel_ev[slot]

@@ -472,6 +472,8 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
         self._mr = None
         self._graph_layout = 0
         self._insrc = None               # in-step batch generator (attach_in_step_source)
+        self._src_copy_stream = None     # the batch producer's stream (set_copy_stream)
+        self._src_copy_owner = None
 
     # for tests / checkpoints: (weight [out, in_real], bias [out]) views
     def weight(self, name: str):
@@ -528,6 +530,21 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
                 return
         # device-resident batch: one fused launch (ids, labels, dense -> bf16)
         ops.batch_load(dense, self.x0, ids, self.ids, label, self.label)
+
+    def set_copy_stream(self, stream, owner=None):
+        """One GPU, per-stream graphs: copy each batch's ids into the static
+        buffer on ``stream`` -- the device batch producer's own stream, on a
+        hardware queue the embedding stream does not share -- right behind the
+        previous step's ids-only sort, instead of on the embedding stream
+        between the previous step's update and the next lookup (where the
+        copy and its waits idled that stream ~34 us per step). Set before
+        capture_graph()."""
+        if self.graph is not None:
+            raise RuntimeError("set the copy stream before capture_graph()")
+        self._src_copy_stream = stream
+        # batches of any other producer are copied on the embedding stream
+        # behind the MLP stream (which waited for them)
+        self._src_copy_owner = owner
 
     def attach_in_step_source(self, src):
         """One GPU: every step draws its own batch inside its graphs

@@ -139,9 +139,13 @@ class StreamGraphsMixin:
         torch.cuda.synchronize()
         cs = (torch.cuda.Stream(device=self.device) if ids_stream and self._insrc is None
               else None)
+        src_cs = self._src_copy_stream is not None and self._insrc is None and self._bstg is None
+        if src_cs:
+            cs = self._src_copy_stream
         self._ms = {"graphs": graphs, "stream": se, "plan": plan, "composed": composed,
                     "names": names,
                     "cstream": cs, "ev_e2": ops.SyncEvent(2), "ev_copy": ev_copy,
+                    "src_cs": src_cs,
                     "e2_recorded": False, "events": ev}
         self.graph = "streams"
 
@@ -156,6 +160,13 @@ class StreamGraphsMixin:
         se, ev = self._ms["stream"], self._ms["events"][0]
         main = torch.cuda.current_stream()
         cs = self._ms.get("cstream")
+        if self._ms.get("src_cs"):
+            own = self._src_copy_owner
+            if on_device and (own is None or own.owns(ids)):
+                pass                           # the producer's batch: copy on its stream
+            else:
+                # another producer's batch (ordered on the MLP stream only)
+                cs, on_device = None, False
         if cs is not None and on_device:
             # the ids copy on its own stream right behind this step's sort (E2,
             # the ids' last reader): the next lookup waits on an event that is
@@ -222,6 +233,10 @@ class StreamGraphsMixin:
         its device copies on each, then passes on_device=True)."""
         main = torch.cuda.current_stream()
         if self.graph == "streams":
+            if self._ms.get("src_cs"):
+                # the ids are copied on the producer's own stream (in order
+                # behind the batch there); only the MLP stream reads the rest
+                return [main]
             cs = self._ms.get("cstream")
             return [main, self._ms["stream"]] + ([cs] if cs is not None else [])
         return [main]

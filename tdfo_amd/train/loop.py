@@ -20,6 +20,7 @@ the step has enqueued its reads of them.
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional, Sequence
 
 
@@ -108,6 +109,11 @@ class StepLoop:
         self.in_step = bool(getattr(source, "in_step", False))
         if self.in_step:
             trainer.attach_in_step_source(source)
+        elif (os.environ.get("TDFO_SRC_COPY", "1") != "0"
+              and getattr(source, "copy_stream", None) is not None
+              and hasattr(trainer, "set_copy_stream") and getattr(trainer, "graph", 1) is None
+              and getattr(trainer, "world", 1) == 1 and not getattr(trainer, "pipeline", False)):
+            trainer.set_copy_stream(source.copy_stream, owner=source)
 
     def _streams(self):
         return None if self.tr.pipeline else self.tr.input_streams()

@@ -68,3 +68,34 @@ def test_trainer_in_step_matches_loaded_batches():
     assert a.pop_loss() == b.pop_loss()
 
 
+@pytest.mark.parametrize("interaction", ["dot", "dcn"])
+def test_producer_stream_ids_copy_matches_embedding_stream_copy(interaction, monkeypatch):
+    """StepLoop hands the device generator's stream to the trainer, which then
+    copies each batch's ids there (behind the previous step's sort) instead of
+    on the embedding stream: same training, bit for bit."""
+    from tdfo_amd.data.synthetic import DeviceSyntheticStream
+    from tdfo_amd.models.dlrm import DLRMConfig, DLRMTrainer
+    from tdfo_amd.train.loop import StepLoop
+
+    kw = dict(embedding_dim=128, table_rows=ROWS, bottom=[128], top=[256, 1], ids_stream=False)
+    if interaction == "dcn":
+        kw.update(interaction="dcn", dcn_layers=2, dcn_rank=64, pooling=[2, 1, 3, 1])
+    cfg = DLRMConfig(**kw)
+    B = 512
+    out = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("TDFO_SRC_COPY", flag)
+        t = DLRMTrainer(cfg, B, DEV)
+        src = DeviceSyntheticStream(ROWS, B, DEV, seed=3, pooling=cfg.pooling_factors())
+        lp = StepLoop(t, src)
+        assert (t._src_copy_stream is not None) == (flag == "1")
+        lp.run(2)
+        t.capture_graph(warmup=0)
+        assert t.graph == "streams"
+        lp.run(6)
+        t.sync_streams()
+        torch.cuda.synchronize()
+        out.append((t.fp.p.clone(), t.emb.tw_store.weight.clone(), t.pop_loss()))
+    assert torch.equal(out[0][0], out[1][0])
+    assert torch.equal(out[0][1], out[1][1])
+    assert out[0][2] == out[1][2]
