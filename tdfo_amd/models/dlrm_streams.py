@@ -25,6 +25,8 @@ backward; readers of tables / params outside ``step()`` call
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from .. import ops
@@ -89,6 +91,8 @@ class StreamGraphsMixin:
         composed = self.cfg.composed_graphs
         if composed is None:
             composed = self.cfg.interaction == "dot"
+        if os.environ.get("TDFO_COMPOSED") in ("0", "1"):     # A/B override
+            composed = os.environ["TDFO_COMPOSED"] == "1"
         # cross-stream edges recorded without the system-scope fence a default
         # event record adds (the producing kernels already release to device
         # scope and no host reads these edges): DLRM-1TB 0.477-0.480 vs

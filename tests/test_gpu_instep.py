@@ -82,6 +82,10 @@ def test_producer_stream_ids_copy_matches_embedding_stream_copy(interaction, mon
         kw.update(interaction="dcn", dcn_layers=2, dcn_rank=64, pooling=[2, 1, 3, 1])
     cfg = DLRMConfig(**kw)
     B = 512
+    from tdfo_amd.data.synthetic import SyntheticCriteo
+    gen = SyntheticCriteo(ROWS, B, pooling=cfg.pooling_factors(), device=DEV, seed=9)
+    foreign = [gen.next() for _ in range(2)]
+    torch.cuda.synchronize()
     out = []
     for flag in ("1", "0"):
         monkeypatch.setenv("TDFO_SRC_COPY", flag)
@@ -93,6 +97,11 @@ def test_producer_stream_ids_copy_matches_embedding_stream_copy(interaction, mon
         t.capture_graph(warmup=0)
         assert t.graph == "streams"
         lp.run(6)
+        # then batches of another producer through load_batch (the embedding
+        # stream path, behind the MLP stream)
+        for b in foreign:
+            t.load_batch(*b, on_device=True)
+            t.step()
         t.sync_streams()
         torch.cuda.synchronize()
         out.append((t.fp.p.clone(), t.emb.tw_store.weight.clone(), t.pop_loss()))
