@@ -149,7 +149,8 @@ class StreamGraphsMixin:
         self._ms = {"graphs": graphs, "stream": se, "plan": plan, "composed": composed,
                     "names": names,
                     "cstream": cs, "ev_e2": ops.SyncEvent(2), "ev_copy": ev_copy,
-                    "src_cs": src_cs,
+                    "src_cs": src_cs, "pending_e3": False,
+                    "defer_e3": src_cs and os.environ.get("TDFO_DEFER_E3", "1") != "0",
                     "e2_recorded": False, "events": ev}
         self.graph = "streams"
 
@@ -189,6 +190,7 @@ class StreamGraphsMixin:
                     stg[1].copy_(label.reshape(-1), non_blocking=True)
                 self._ms["ev_copy"].record(cs)
             se.wait_event(self._ms["ev_copy"])
+            self.flush_pending()
             return True
         if not on_device:
             se.wait_stream(main)               # e.g. an H2D the caller ordered on main
@@ -197,9 +199,12 @@ class StreamGraphsMixin:
             ev.record(se)
         if not on_device:
             main.wait_event(ev)                # dense / labels from the same source
+        self.flush_pending()
         return True
 
     def _ms_step(self):
+        if self._ms.get("pending_e3"):
+            self._ms_issue_e3()              # (no load_batch since the last step)
         g, se, ev = self._ms["graphs"], self._ms["stream"], self._ms["events"]
         main = torch.cuda.current_stream()
         composed = self._ms["composed"]
@@ -222,15 +227,33 @@ class StreamGraphsMixin:
             main.wait_event(ev[1])           # pooled embeddings ready
             g["M2"].replay()
             ev[2].record(main)
-        with torch.cuda.stream(se):
-            se.wait_event(ev[2])             # embedding gradients ready
-            g["E3"].replay()
-            ev[3].record(se)
+        if self._ms.get("defer_e3"):
+            # the embedding update is issued by the next load_batch, after the
+            # wait for the next batch's ids copy: that wait then sits before
+            # the update (which waits for the MLP stream anyway), not between
+            # the update and the next lookup (flush_pending() / sync_streams()
+            # / the next step issue it otherwise)
+            self._ms["pending_e3"] = True
+        else:
+            self._ms_issue_e3()
         if not composed:
             g["M3"].replay()
         # no end-of-step join: the embedding stream's next work (ids copy,
         # lookup) is ordered behind this update on that stream, and the next
         # MLP graphs wait for the next lookup
+
+    def _ms_issue_e3(self):
+        g, se, ev = self._ms["graphs"], self._ms["stream"], self._ms["events"]
+        with torch.cuda.stream(se):
+            se.wait_event(ev[2])             # embedding gradients ready
+            g["E3"].replay()
+            ev[3].record(se)
+        self._ms["pending_e3"] = False
+
+    def flush_pending(self):
+        """Issue a deferred embedding update (one-GPU per-stream graphs)."""
+        if self._ms is not None and self._ms.get("pending_e3"):
+            self._ms_issue_e3()
 
     def input_streams(self):
         """Streams that read a batch handed to load_batch (a producer orders
@@ -249,6 +272,7 @@ class StreamGraphsMixin:
         """Order the current stream after all side-stream work of issued steps
         (embedding updates)."""
         if self._ms is not None:
+            self.flush_pending()
             torch.cuda.current_stream().wait_stream(self._ms["stream"])
             if self._ms.get("cstream") is not None:
                 torch.cuda.current_stream().wait_stream(self._ms["cstream"])

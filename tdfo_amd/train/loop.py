@@ -141,11 +141,16 @@ class StepLoop:
             self.prime()
         on_dev = tr.device.type == "cuda"
         wd = self.wd
+        flush = getattr(tr, "flush_pending", None)   # every issued step complete
         if wd is None:
             self._run(n, on_dev)
+            if flush is not None:
+                flush()
             return
         with wd.active():
             self._run(n, on_dev)
+            if flush is not None:
+                flush()
             if n:
                 wd.beat(tr.heartbeat_stream(), self.step_index)
 
