@@ -92,6 +92,9 @@ def parse(argv=None):
                          "copies only")
     ap.add_argument("--emulate-latency-us", type=float, default=10.0,
                     help="--emulate-world: modelled fixed cost per collective (us)")
+    ap.add_argument("--no-preflight", action="store_true",
+                    help="N > 1: skip the collective self-test before the trainer is built "
+                         "(parallel/preflight.py; on a mismatch it switches to c10d + staged)")
     ap.add_argument("--watchdog-s", type=float, default=float(os.environ.get("TDFO_WATCHDOG_S",
                                                                           180)),
                     help="hang guard: a step whose heartbeat has not landed after this many "
@@ -370,6 +373,15 @@ def main(argv=None):
     args = parse(argv)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(self_launch(args, argv))
+    from tdfo_amd.utils import supervise
+    if (int(os.environ.get("WORLD_SIZE", "1")) > 1 and not supervise.is_child()
+            and os.environ.get("TDFO_SUPERVISE", "1") == "1"):
+        # every rank: a GPU-free supervisor runs the rank code as a child; if
+        # any rank's child fails (watchdog exit 3, replica mismatch exit 4,
+        # crash), all ranks rerun once on c10d collectives + staged replay
+        sys.exit(supervise.supervise([sys.executable, os.path.abspath(__file__), *argv],
+                                     attempts=[{}, {"TDFO_COMM": "torch"}],
+                                     fallback_argv=[["--no-stream-graphs"]]))
     if (args.emulate_world > 1 and (args.emulate_rank == "max" or "," in args.emulate_rank)
             and os.environ.get("TDFO_EMU_INPROC") != "1"):
         sys.exit(emulate_ranks_isolated(args, argv))
@@ -395,6 +407,13 @@ def main(argv=None):
         reset()
         return
     world = info.world_size
+    pf = None
+    if world > 1 and not args.no_preflight:
+        from tdfo_amd.parallel.preflight import preflight
+        pf = preflight(info.group, info.device)
+        print(json.dumps({"preflight": pf, "rank": info.rank}), file=sys.stderr, flush=True)
+        if not pf["ok"]:
+            args.no_stream_graphs = True          # c10d collectives, staged replay
     cfg = _cfg(args, rows, world > 1 and not args.no_pipeline)
     if args.data in ("host", "fresh", "instep"):
         # a streamed data source orders its batch on every input stream and
@@ -413,9 +432,23 @@ def main(argv=None):
         from tdfo_amd.parallel.replicas import check_replicas
         inject = os.environ.get("TDFO_INJECT_DIVERGENCE")
         state = tr.replicated_state()
-        if inject is not None and int(inject) == info.rank:
+        att = os.environ.get("TDFO_ATTEMPT", "0")
+        if inject is not None and int(inject) == info.rank and \
+                os.environ.get("TDFO_INJECT_ATTEMPT", att) == att:
             state["dense.p"].view(-1)[0] += 1e-3          # test hook: one diverged replica
         consistent, per = check_replicas(state, info.group)
+    comm_path = None
+    if world > 1:
+        from tdfo_amd.parallel.comm import RcclComm
+        comm_path = ("native" if isinstance(tr.comm, RcclComm) else "c10d") + (
+            "-graphs" if _graph_name(tr) == "mstreams" else "-staged")
+    if not consistent:
+        # no throughput for diverged replicas: nothing goes to stdout
+        r["loop"].close()
+        print(f"error: rank {info.rank}: replicated state differs across ranks ({per})",
+              file=sys.stderr, flush=True)
+        reset()
+        sys.exit(4)
     if info.rank == 0:
         print(json.dumps({"plan": tr.plan.summary(), "setup_s": round(r["setup_s"], 1),
                           "train_loss": round(r["loss"], 4), "graph": _graph_name(tr),
@@ -424,7 +457,7 @@ def main(argv=None):
                           "host_wait_us_per_step": round(r["wait_s"] / args.steps * 1e6, 1),
                           "comm": r["comm"], "preheat_ms": args.preheat_ms,
                           "ranks_consistent": consistent if world > 1 else None,
-                          "replica_check": per if not consistent else None,
+                          "preflight": pf,
                           "dense_tflops": round(cfg.dense_flops_per_example() * value / 1e12, 1),
                           "sol": {k: round(v, 4) for k, v in sol.items()}}),
               file=sys.stderr, flush=True)
@@ -445,6 +478,9 @@ def main(argv=None):
             "sol_ms": round(sol["sol_ms"], 4),
             "frac_of_sol": round(sol["sol_ms"] / ms, 3),
             "preheat_ms": args.preheat_ms,
+            "comm_path": comm_path,
+            "attempt": int(os.environ.get("TDFO_ATTEMPT", "0")),
+            "ranks_consistent": consistent if world > 1 else None,
             "dtype": "bf16",
             "data": f"synthetic (Criteo-{args.rows}-shaped, {args.dist} ids, random-init "
                     f"embeddings, {src})",
@@ -455,10 +491,6 @@ def main(argv=None):
                        "per_gpu_batch": B}}), flush=True)
     r["loop"].close()
     reset()
-    if not consistent:
-        print(f"error: rank {info.rank}: replicated state differs across ranks ({per})",
-              file=sys.stderr, flush=True)
-        sys.exit(4)
 
 
 if __name__ == "__main__":

@@ -16,6 +16,16 @@ run() {
   echo "== $tag rc=$rc"; tail -4 gpurun_out/rehearse_$tag.log
   return $rc
 }
+if [ "${SET:-full}" = "guards" ]; then
+  # pre-flight mismatch on rank 1 -> every rank on c10d + staged, consistent
+  TDFO_PREFLIGHT_INJECT=1 run pf_inject --rows kaggle --steps 3 --warmup 1 --batch 2048 &&
+  grep -q '"comm_path": "c10d-staged"' gpurun_out/rehearse_pf_inject.log &&
+  # attempt 0 diverges (exit 4, no metric line) -> the supervisors rerun once
+  TDFO_INJECT_DIVERGENCE=1 TDFO_INJECT_ATTEMPT=0 run sup_fallback --rows kaggle --steps 3 \
+    --warmup 1 --batch 2048 &&
+  grep -q '"attempt": 1' gpurun_out/rehearse_sup_fallback.log
+  exit $?
+fi
 run tw1tb --steps 5 --warmup 2 --batch 4096 &&
 run kaggle_auto --rows kaggle --steps 5 --warmup 2 --batch 4096 &&
 run dcn_rw --model dcnv2 --rows kaggle --sharding row_wise --steps 3 --warmup 1 --batch 2048 &&

@@ -76,6 +76,15 @@ def init_distributed(device: Optional[str] = None, backend: Optional[str] = None
             kw = {}
             if dev.type == "cuda" and backend == "nccl":
                 kw["device_id"] = dev
+            prefix = os.environ.get("TDFO_STORE_PREFIX")
+            if prefix:
+                # a supervised attempt (utils/supervise.py): a client of the
+                # launcher's (or the supervisor's) store under this attempt's
+                # key prefix, so no key of an earlier attempt is read
+                tcp = dist.TCPStore(os.environ["MASTER_ADDR"], int(os.environ["MASTER_PORT"]),
+                                    world_size=world, is_master=False,
+                                    timeout=datetime.timedelta(seconds=timeout_s))
+                kw["store"] = dist.PrefixStore(prefix, tcp)
             dist.init_process_group(backend=backend, rank=rank, world_size=world,
                                     timeout=datetime.timedelta(seconds=timeout_s), **kw)
         info.backend = backend
