@@ -592,42 +592,15 @@ void host_publish(const Tensor& value, const Tensor& seq, const Tensor& host, in
                      reinterpret_cast<uint64_t*>(dptr), cur_stream());
 }
 
-// Stream-ordered 32-bit flags in signal memory (hipMallocSignalMemory): a
-// wait on a value instead of on "the latest record" of an event, so a waiter
-// graph can be launched before its producer graph and several steps can sit
-// in one executable graph (probe: scripts/probe_wait_value.py).
-int64_t signal_flag_alloc() {
-  void* p = nullptr;
-  TDFO_HIP_OK(hipExtMallocWithFlags(&p, 8, hipMallocSignalMemory));
-  TDFO_HIP_OK(hipMemset(p, 0, 8));
-  TDFO_HIP_OK(hipDeviceSynchronize());
-  return reinterpret_cast<int64_t>(p);
-}
-
-void signal_flag_free(int64_t p) { TDFO_HIP_OK(hipFree(reinterpret_cast<void*>(p))); }
-
-// flags: 0 >=, 1 ==
-void stream_wait_value(int64_t p, int64_t value, int64_t flags) {
-  TDFO_HIP_OK(hipStreamWaitValue32(cur_stream(), reinterpret_cast<void*>(p), (uint32_t)value,
-                                   flags == 1 ? hipStreamWaitValueEq : hipStreamWaitValueGte,
-                                   0xFFFFFFFFu));
-}
-
-void stream_write_value(int64_t p, int64_t value) {
-  TDFO_HIP_OK(hipStreamWriteValue32(cur_stream(), reinterpret_cast<void*>(p), (uint32_t)value, 0));
-}
-
 // A chain of captured graphs joined by event nodes, instantiated as ONE
 // executable graph: kinds[i] = 0 child graph (handles[i] = hipGraph_t of a
-// keep_graph capture), 1 wait on the event handles[i], 2 record it, 3 wait
-// until the signal-memory flag at handles[i] >= values[i], 4 write values[i]
-// to it. Stream capture cannot create these event nodes on this ROCm (the
-// external-flag record is refused, the wait crashes), so they are added
-// explicitly.
-int64_t graph_compose(std::vector<int64_t> kinds, std::vector<int64_t> handles,
-                      std::vector<int64_t> values) {
+// keep_graph capture), 1 wait on the event handles[i], 2 record it. Stream
+// capture cannot create these event nodes on this ROCm (the external-flag
+// record is refused, the wait crashes), so they are added explicitly.
+// (Signal-memory value-wait nodes were measured and rejected: as graph nodes
+// the wait did not hold the consumer, profiles/r04/notes.md.)
+int64_t graph_compose(std::vector<int64_t> kinds, std::vector<int64_t> handles) {
   TORCH_CHECK(kinds.size() == handles.size() && !kinds.empty(), "graph_compose: bad parts");
-  TORCH_CHECK(values.empty() || values.size() == kinds.size(), "graph_compose: bad values");
   hipGraph_t g;
   TDFO_HIP_OK(hipGraphCreate(&g, 0));
   hipGraphNode_t prev = nullptr;
@@ -635,30 +608,7 @@ int64_t graph_compose(std::vector<int64_t> kinds, std::vector<int64_t> handles,
     hipGraphNode_t n;
     const hipGraphNode_t* dep = prev ? &prev : nullptr;
     const size_t nd = prev ? 1 : 0;
-    if (kinds[i] == 3 || kinds[i] == 4) {
-      TORCH_CHECK(!values.empty(), "graph_compose: value nodes need values");
-      hipStreamBatchMemOpParams op;
-      std::memset(&op, 0, sizeof(op));
-      if (kinds[i] == 3) {
-        op.waitValue.operation = hipStreamMemOpWaitValue32;
-        op.waitValue.address = reinterpret_cast<hipDeviceptr_t>(handles[i]);
-        op.waitValue.value = (uint32_t)values[i];
-        op.waitValue.flags = hipStreamWaitValueGte;
-      } else {
-        op.writeValue.operation = hipStreamMemOpWriteValue32;
-        op.writeValue.address = reinterpret_cast<hipDeviceptr_t>(handles[i]);
-        op.writeValue.value = (uint32_t)values[i];
-        op.writeValue.flags = 0;
-      }
-      hipBatchMemOpNodeParams np;
-      std::memset(&np, 0, sizeof(np));
-      hipCtx_t ctx = nullptr;
-      (void)hipCtxGetCurrent(&ctx);
-      np.ctx = ctx;
-      np.count = 1;
-      np.paramArray = &op;
-      TDFO_HIP_OK(hipGraphAddBatchMemOpNode(&n, g, dep, nd, &np));
-    } else if (kinds[i] == 0) {
+    if (kinds[i] == 0) {
       TDFO_HIP_OK(hipGraphAddChildGraphNode(&n, g, dep, nd,
                                             reinterpret_cast<hipGraph_t>(handles[i])));
     } else if (kinds[i] == 1) {
@@ -1432,11 +1382,7 @@ TORCH_LIBRARY(tdfo, m) {
   m.def("sync_event_wait(int e) -> ()", sync_event_wait);
   m.def("sync_event_destroy(int e) -> ()", sync_event_destroy);
   m.def("sync_event_query(int e) -> bool", sync_event_query);
-  m.def("graph_compose(int[] kinds, int[] handles, int[] values=[]) -> int", graph_compose);
-  m.def("signal_flag_alloc() -> int", signal_flag_alloc);
-  m.def("signal_flag_free(int p) -> ()", signal_flag_free);
-  m.def("stream_wait_value(int p, int value, int flags) -> ()", stream_wait_value);
-  m.def("stream_write_value(int p, int value) -> ()", stream_write_value);
+  m.def("graph_compose(int[] kinds, int[] handles) -> int", graph_compose);
   m.def("graph_exec_launch(int ex) -> ()", graph_exec_launch);
   m.def("graph_exec_destroy(int ex) -> ()", graph_exec_destroy);
   m.def("graph_exec_upload(int ex) -> ()", graph_exec_upload);

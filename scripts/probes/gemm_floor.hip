@@ -1,0 +1,245 @@
+// GEMM structure lab (standalone executable, no torch): one parametrised
+// LDS-DMA ring kernel, run in four modes on the DLRM / DCN-v2 shapes so that
+// each tile / wave layout's floors are measured with the SAME loop:
+//   mode 0  full GEMM (bf16 out, checked against a naive fp32 kernel)
+//   mode 1  global->LDS DMA only (no fragment reads, no MFMA): load floor
+//   mode 2  fragment reads + MFMA from a resident LDS image (no DMA): compute floor
+//   mode 3  DMA + fragment reads, no MFMA
+// Build: hipcc -O3 --offload-arch=gfx950 -std=c++17 gemm_floor.hip -o gemm_floor
+// Run:   ./gemm_floor            (prints one JSON line per shape x variant x mode)
+#include "lab_common.h"
+
+
+// BM x BN tile, WM x WN waves (wave tile (BM/WM) x (BN/WN), 16x16x32 MFMA),
+// NST-slot ring, one raw barrier per K tile, fragments of the next k32 step
+// read while this step's MFMAs run.
+template <int BM, int BN, int WM, int WN, int NST, bool AC, bool BC, int MODE>
+__global__ __launch_bounds__(64 * WM * WN, 1) void g3(P p) {
+  constexpr int NW = WM * WN, NT = 64 * NW;
+  constexpr int TM = BM / WM, TN = BN / WN, MI = TM / 16, NJ = TN / 16;
+  constexpr int AI = BM / 128, BI = BN / 128;             // images per operand
+  constexpr int STAGE = (AI + BI) * IMG;
+  constexpr int PIECES = (AI + BI) * 16;
+  static_assert(PIECES % NW == 0, "pieces per wave");
+  constexpr int PPW = PIECES / NW;
+  static_assert(PPW * (NST - 1) <= 63, "vmcnt");
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  LDSP char* smem = (LDSP char*)smem_raw;
+  const int tiles_m = (p.M + BM - 1) / BM, tiles_n = (p.N + BN - 1) / BN;
+  const int t = xcd_remap(blockIdx.x, tiles_m * tiles_n);
+  const int m0 = (t / tiles_n) * BM, n0 = (t % tiles_n) * BN;
+  const int nk = p.K / BK;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w / WN, wn = w % WN;
+  const int ar = wm * TM, bc = wn * TN;                   // wave's first row / col in the tile
+  const int a_img = ar / 128, a_r0 = ar % 128, b_img = bc / 128, b_c0 = bc % 128;
+
+  f32x4_t acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  auto stage = [&](int slot, int kt) {
+    if (MODE == 2) return;
+    LDSP char* st = smem + slot * STAGE;
+    const int k0 = kt * BK;
+#pragma unroll
+    for (int q = 0; q < PPW; ++q) {
+      const int ii = w * PPW + q, img = ii >> 4;
+      if (img < AI)
+        piece<AC>(p.A, p.lda, m0 + img * 128, p.M, k0, st + img * IMG, ii & 15, lane);
+      else
+        piece<BC>(p.B, p.ldb, n0 + (img - AI) * 128, p.N, k0, st + img * IMG, ii & 15, lane);
+    }
+  };
+  auto wait_tile = [&](int younger) {
+    if (MODE == 2) return;
+    if (younger >= 3) vm_wait<3 * PPW>();
+    else if (younger == 2) vm_wait<2 * PPW>();
+    else if (younger == 1) vm_wait<PPW>();
+    else vm_wait<0>();
+  };
+  bf16x8_t af[2][MI], bf[2][NJ];
+  auto read = [&](int slot, int ks, int b) {
+    const LDSP char* st = smem + slot * STAGE;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) bf[b][j] = frag<BC>(st + (AI + b_img) * IMG, b_c0 + 16 * j, ks, lane);
+#pragma unroll
+    for (int i = 0; i < MI; ++i) af[b][i] = frag<AC>(st + a_img * IMG, a_r0 + 16 * i, ks, lane);
+  };
+  auto mm = [&](int b) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        if (MODE == 3) {
+          asm volatile("" ::"v"(af[b][i]), "v"(bf[b][j]));   // keep the reads live
+        } else {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[b][j], af[b][i], acc[i][j], 0, 0, 0);
+        }
+      }
+  };
+  if (MODE == 2) {
+    // resident image: fill slot 0 once (garbage contents are fine for timing)
+  }
+#pragma unroll
+  for (int s = 0; s < NST - 1; ++s)
+    if (s < nk) stage(s, s);
+  for (int kt = 0; kt < nk; ++kt) {
+    wait_tile(min(nk - 1 - kt, NST - 2));
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + NST - 1 < nk) stage((kt + NST - 1) % NST, kt + NST - 1);
+    const int slot = MODE == 2 ? 0 : kt % NST;
+    if (MODE != 1) {
+      read(slot, 0, 0);
+      read(slot, 1, 1);
+      mm(0);
+      mm(1);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  // epilogue: C[row][col] bf16 (acc holds C^T fragments: lane l reg r of (i,j)
+  // = C[16i + (l&15)][16j + 4(l>>4) + r])
+  const int rho = lane & 15, g = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int m = m0 + ar + 16 * i + rho, n = n0 + bc + 16 * j + 4 * g;
+      if (m < p.M && n + 3 < p.N) {
+        __bf16 v0 = (__bf16)acc[i][j][0], v1 = (__bf16)acc[i][j][1], v2 = (__bf16)acc[i][j][2],
+               v3 = (__bf16)acc[i][j][3];
+        uint2 u;
+        u.x = (uint32_t)__builtin_bit_cast(uint16_t, v0) | ((uint32_t)__builtin_bit_cast(uint16_t, v1) << 16);
+        u.y = (uint32_t)__builtin_bit_cast(uint16_t, v2) | ((uint32_t)__builtin_bit_cast(uint16_t, v3) << 16);
+        *(uint2*)(p.C + (int64_t)m * p.ldc + n) = u;
+      }
+    }
+}
+
+template <int BM, int BN, int WM, int WN, int NST, bool AC, bool BC, int MODE>
+float run(const P& p, int reps) {
+  auto fn = g3<BM, BN, WM, WN, NST, AC, BC, MODE>;
+  constexpr int STAGE = (BM / 128 + BN / 128) * IMG;
+  const int lds = NST * STAGE;
+  CK(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
+  const int grid = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  for (int i = 0; i < 3; ++i) hipLaunchKernelGGL(fn, dim3(grid), dim3(64 * WM * WN), lds, 0, p);
+  CK(hipDeviceSynchronize());
+  std::vector<float> ts;
+  for (int r = 0; r < 7; ++r) {
+    CK(hipEventRecord(a));
+    for (int i = 0; i < reps; ++i) hipLaunchKernelGGL(fn, dim3(grid), dim3(64 * WM * WN), lds, 0, p);
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    ts.push_back(ms * 1e3f / reps);
+  }
+  std::sort(ts.begin(), ts.end());
+  return ts[ts.size() / 2];
+}
+
+struct Buf {
+  uint16_t *A, *B, *C;
+  float* R;
+};
+
+template <int BM, int BN, int WM, int WN, int NST, bool AC, bool BC>
+void variant(const char* name, const char* shape, P p, Buf& bf, bool check) {
+  const double flop = 2.0 * p.M * p.N * p.K;
+  float t0 = run<BM, BN, WM, WN, NST, AC, BC, 0>(p, 20);
+  double err = -1;
+  if (check) {
+    CK(hipMemset(p.C, 0, (size_t)p.M * p.ldc * 2));
+    run<BM, BN, WM, WN, NST, AC, BC, 0>(p, 1);
+    std::vector<uint16_t> c((size_t)p.M * p.ldc);
+    std::vector<float> r((size_t)p.M * p.N);
+    CK(hipMemcpy(c.data(), p.C, c.size() * 2, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(r.data(), bf.R, r.size() * 4, hipMemcpyDeviceToHost));
+    double mx = 0, sc = 1e-6;
+    for (int m = 0; m < p.M; ++m)
+      for (int n = 0; n < p.N; ++n) {
+        uint32_t u = (uint32_t)c[(size_t)m * p.ldc + n] << 16;
+        float g;
+        memcpy(&g, &u, 4);
+        mx = std::max(mx, (double)std::fabs(g - r[(size_t)m * p.N + n]));
+        sc = std::max(sc, (double)std::fabs(r[(size_t)m * p.N + n]));
+      }
+    err = mx / sc;
+  }
+  float t1 = run<BM, BN, WM, WN, NST, AC, BC, 1>(p, 20);
+  float t2 = run<BM, BN, WM, WN, NST, AC, BC, 2>(p, 20);
+  float t3 = run<BM, BN, WM, WN, NST, AC, BC, 3>(p, 20);
+  const int tiles = ((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
+  const double bytes_cu = (double)tiles * (BM + BN) * (double)p.K * 2 / 256.0;
+  printf("{\"shape\": \"%s\", \"MNK\": [%d, %d, %d], \"variant\": \"%s\", \"tiles\": %d, "
+         "\"full_us\": %.2f, \"TF\": %.0f, \"load_only_us\": %.2f, \"load_GBs_per_CU\": %.1f, "
+         "\"compute_only_us\": %.2f, \"load_read_us\": %.2f, \"rel_err\": %.2e}\n",
+         shape, p.M, p.N, p.K, name, tiles, t0, flop / t0 / 1e6, t1, bytes_cu / t1 / 1e3, t2, t3,
+         err);
+  fflush(stdout);
+}
+
+int main(int argc, char** argv) {
+  const bool check = argc < 2 || std::string(argv[1]) != "nocheck";
+  const size_t MAXE = (size_t)8192 * 4096;
+  Buf bf;
+  CK(hipMalloc(&bf.A, MAXE * 2));
+  CK(hipMalloc(&bf.B, MAXE * 2));
+  CK(hipMalloc(&bf.C, MAXE * 2));
+  CK(hipMalloc(&bf.R, MAXE * 4));
+  {
+    std::vector<uint16_t> h(MAXE);
+    std::mt19937 rng(1);
+    std::uniform_real_distribution<float> u(-1.f, 1.f);
+    for (auto& x : h) x = f2b(u(rng));
+    CK(hipMemcpy(bf.A, h.data(), MAXE * 2, hipMemcpyHostToDevice));
+    for (auto& x : h) x = f2b(u(rng));
+    CK(hipMemcpy(bf.B, h.data(), MAXE * 2, hipMemcpyHostToDevice));
+  }
+  struct S {
+    const char* name;
+    int M, N, K, ac, bc;
+  };
+  // fwd: A [M][K] row, B = W [N][K] row; dgrad: B = W as [K][N] col;
+  // wgrad: A = dy as [K][M] col, B = x as [K][N] col
+  std::vector<S> shapes = {
+      {"top1.fwd", 8192, 1024, 1024, 0, 0}, {"top0.fwd", 8192, 1024, 512, 0, 0},
+      {"top2.fwd", 8192, 512, 1024, 0, 0},  {"top1.dgrad", 8192, 1024, 1024, 0, 1},
+      {"top1.wgrad", 1024, 1024, 8192, 1, 1}, {"dcnU.fwd", 8192, 3456, 512, 0, 0},
+      {"dcnV.fwd", 8192, 512, 3456, 0, 0},
+  };
+  for (auto& s : shapes) {
+    P p{bf.A, bf.B, bf.C, s.ac ? s.M : s.K, s.bc ? s.N : s.K, s.N, s.M, s.N, s.K};
+    if (check) {
+      hipLaunchKernelGGL(ref_kernel, dim3((s.N + 255) / 256, s.M), dim3(256), 0, 0, p, s.ac, s.bc,
+                         bf.R);
+      CK(hipDeviceSynchronize());
+    }
+#define V(BM, BN, WM, WN, NST)                                                          \
+  do {                                                                                  \
+    const char* nm = #BM "x" #BN "_w" #WM "x" #WN "_s" #NST;                           \
+    if (s.ac && s.bc) variant<BM, BN, WM, WN, NST, true, true>(nm, s.name, p, bf, check); \
+    else if (s.bc) variant<BM, BN, WM, WN, NST, false, true>(nm, s.name, p, bf, check);  \
+    else variant<BM, BN, WM, WN, NST, false, false>(nm, s.name, p, bf, check);          \
+  } while (0)
+    V(128, 128, 2, 2, 2);
+    V(128, 128, 2, 2, 3);
+    V(128, 128, 2, 2, 4);
+    V(128, 128, 2, 2, 5);
+    V(256, 128, 4, 2, 2);
+    V(256, 128, 4, 2, 3);
+    V(256, 128, 2, 2, 3);
+    V(128, 256, 2, 2, 3);
+    V(256, 256, 2, 4, 2);
+  }
+  return 0;
+}

@@ -337,8 +337,10 @@ class ItemEmbedding(nn.Module):
             dist.all_gather_into_tensor(self.g_grad[: self.world * n], grad, group=self.group)
             self.g_grad.mul_(1.0 / self.world)
             ids, grad, n = self.g_ids[: self.world * n], self.g_grad[: self.world * n], self.world * n
+        # one id per position of the single table: the per-table LDS sort
+        # (device-wide radix sort past 8192 ids, embedding.hip onehot_path)
         self.store.backward_update(ids, self.offsets[: n + 1], self.zero, 1, n, grad, self.zero,
-                                   self.D, self.hyper)
+                                   self.D, self.hyper, segsort=1)
 
     def forward(self, ids):
         if self.training and torch.is_grad_enabled():

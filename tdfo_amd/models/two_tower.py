@@ -186,6 +186,7 @@ class TwoTowerTrainer:
             self.g_dX = torch.zeros(world_size * self.B, LDX, dtype=torch.float32, device=dev)
         self.graph = None
         self._cur_b = self.B
+        self._bumped = False
 
     # ------------------------------------------------------------ data in
     def load_batch(self, batch: Dict[str, torch.Tensor], eval_mode: bool = False) -> int:
@@ -290,6 +291,8 @@ class TwoTowerTrainer:
 
     def _bump(self, hyper):
         """Advance an optimizer's step counter (not on a skipped step)."""
+        if self._bumped:
+            return                      # done for both optimizers in one launch
         if self.mp:
             hyper[1:2].add_(1.0 - self.found_inf)
         else:
@@ -306,8 +309,11 @@ class TwoTowerTrainer:
         self._bump(self.emb_hyper)
         offs = self.offsets_full[: self.T * b_total + 1]
         if self.cfg.emb_update == "sparse":
+            # one id per bag, tables contiguous: per-table LDS sorts instead of
+            # the device-wide radix sort (falls back to it past 8192 ids per
+            # table, embedding.hip onehot_path)
             self.emb.backward_update(ids, offs, self.emb.row_offset, self.T, b_total, grad,
-                                     self.out_off, LDX, self.emb_hyper)
+                                     self.out_off, LDX, self.emb_hyper, segsort=1)
         else:
             # raw (still scaled) dense gradient; the dense AdamW unscales by
             # hyper[2] and skips on found_inf
@@ -323,8 +329,15 @@ class TwoTowerTrainer:
     def _step_local(self, b: int):
         self._train_compute(b)
         self._mp_check([self.G[:NPARAM], self.dX[:b, :112]])
-        self._dense_update()
-        self._emb_update(self.ids[: self.T * b], b, self.dX[:b])
+        if not self.mp and self.device.type == "cuda":
+            # both step counters in one native launch (no torch kernels)
+            ops.bump([self.hyper, self.emb_hyper])
+            self._bumped = True
+        try:
+            self._dense_update()
+            self._emb_update(self.ids[: self.T * b], b, self.dX[:b])
+        finally:
+            self._bumped = False
         self._mp_update_scale()
 
     def _step_dp(self, b: int):

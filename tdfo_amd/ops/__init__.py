@@ -75,30 +75,6 @@ class SyncEvent:
             pass
 
 
-class SignalFlag:
-    """A 32-bit flag in signal memory for stream-ordered value waits / writes
-    (hipStreamWaitValue32 / hipStreamWriteValue32 and the matching graph
-    nodes): unlike an event wait, a value wait does not bind to "the latest
-    record", so waiter and producer may be launched in either order."""
-
-    def __init__(self):
-        self.ptr = int(_native().signal_flag_alloc())
-
-    def wait(self, value: int, stream=None, eq: bool = False):
-        with torch.cuda.stream(stream) if stream is not None else _null():
-            _native().stream_wait_value(self.ptr, int(value), 1 if eq else 0)
-
-    def write(self, value: int, stream=None):
-        with torch.cuda.stream(stream) if stream is not None else _null():
-            _native().stream_write_value(self.ptr, int(value))
-
-    def __del__(self):
-        try:
-            _native().signal_flag_free(self.ptr)
-        except Exception:
-            pass
-
-
 class _null:
     def __enter__(self):
         return self
@@ -110,16 +86,13 @@ class _null:
 class ComposedGraph:
     """Captured graphs chained with cross-stream event nodes and instantiated
     as one executable graph. parts: ("graph", torch.cuda.CUDAGraph captured
-    with keep_graph=True), ("wait", SyncEvent), ("record", SyncEvent),
-    ("waitval", (SignalFlag, v)): until the flag >= v, or ("writeval",
-    (SignalFlag, v)). The torch graphs (and the memory pool their kernels use)
-    must outlive this."""
+    with keep_graph=True), ("wait", SyncEvent), ("record", SyncEvent). The
+    torch graphs (and the memory pool their kernels use) must outlive this."""
 
     def __init__(self, parts):
-        kinds, handles, values = [], [], []
+        kinds, handles = [], []
         self._keep = []
         for kind, obj in parts:
-            v = 0
             if kind == "graph":
                 kinds.append(0)
                 handles.append(int(obj.raw_cuda_graph()))
@@ -127,15 +100,10 @@ class ComposedGraph:
                 kinds.append(1 if kind == "wait" else 2)
                 handles.append(obj.handle)
                 obj._pinned = True
-            elif kind in ("waitval", "writeval"):
-                kinds.append(3 if kind == "waitval" else 4)
-                obj, v = obj
-                handles.append(obj.ptr)
             else:
                 raise ValueError(kind)
-            values.append(int(v))
             self._keep.append(obj)
-        self._ex = int(_native().graph_compose(kinds, handles, values))
+        self._ex = int(_native().graph_compose(kinds, handles))
 
     def replay(self):
         _native().graph_exec_launch(self._ex)
