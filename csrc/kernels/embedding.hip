@@ -263,14 +263,17 @@ constexpr int SEG_BINS = 1 << SEG_BITS;
 constexpr int SEG_WAVES = SEG_THREADS / 64;
 constexpr int SEG_CNT = SEG_BINS * SEG_K * SEG_WAVES;   // 8192 counters
 
-template <typename K, bool SORTED_G>
+// SK: elements per thread (tables of <= SK * 1024 ids; 2 for small batches:
+// a quarter of the counters to clear and scan per pass)
+template <typename K, bool SORTED_G, int SK = SEG_K>
 __global__ __launch_bounds__(SEG_THREADS) void emb_segsort_kernel(
     const EmbBwdArgs a, K* __restrict__ keys_out, int32_t* __restrict__ vals_out,
     int64_t* __restrict__ goff, float* __restrict__ gscale, int32_t* __restrict__ tail_count,
     int32_t* __restrict__ pos) {
-  __shared__ uint32_t skey[SEG_MAX];
-  __shared__ uint32_t sval[SEG_MAX];
-  __shared__ uint32_t cnt[SEG_CNT];
+  constexpr int CNT = SEG_BINS * SK * SEG_WAVES;
+  __shared__ uint32_t skey[SK * SEG_THREADS];
+  __shared__ uint32_t sval[SK * SEG_THREADS];
+  __shared__ uint32_t cnt[CNT];
   __shared__ uint32_t wsum[SEG_WAVES];
   __shared__ uint32_t smax[SEG_WAVES];
   const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -280,10 +283,10 @@ __global__ __launch_bounds__(SEG_THREADS) void emb_segsort_kernel(
   }
   const int n = a.B;
   const int64_t s0 = (int64_t)t * a.B;
-  uint32_t key[SEG_K], val[SEG_K];
+  uint32_t key[SK], val[SK];
   uint32_t kmax = 0;
 #pragma unroll
-  for (int k = 0; k < SEG_K; ++k) {
+  for (int k = 0; k < SK; ++k) {
     const int i = k * SEG_THREADS + tid;
     if (i < n) {
       const int64_t p = s0 + i;
@@ -308,12 +311,12 @@ __global__ __launch_bounds__(SEG_THREADS) void emb_segsort_kernel(
   const int bits = bmax ? 32 - __clz(bmax) : 1;
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
   for (int shift = 0; shift < bits; shift += SEG_BITS) {
-    for (int c = tid; c < SEG_CNT; c += SEG_THREADS) cnt[c] = 0;
+    for (int c = tid; c < CNT; c += SEG_THREADS) cnt[c] = 0;
     __syncthreads();
-    uint32_t rank[SEG_K];
-    int dig[SEG_K];
+    uint32_t rank[SK];
+    int dig[SK];
 #pragma unroll
-    for (int k = 0; k < SEG_K; ++k) {
+    for (int k = 0; k < SK; ++k) {
       // invalid slots carry the all-ones key: digit 63 in every pass
       const int d = (int)((key[k] >> shift) & (SEG_BINS - 1));
       uint64_t peers = ~0ull;
@@ -324,16 +327,16 @@ __global__ __launch_bounds__(SEG_THREADS) void emb_segsort_kernel(
       }
       rank[k] = (uint32_t)__popcll(peers & lt);
       dig[k] = d;
-      if ((peers & lt) == 0) cnt[(d * SEG_K + k) * SEG_WAVES + w] = (uint32_t)__popcll(peers);
+      if ((peers & lt) == 0) cnt[(d * SK + k) * SEG_WAVES + w] = (uint32_t)__popcll(peers);
     }
     __syncthreads();
     // exclusive scan of cnt in (digit, slot, wave) order: 8 entries per thread
-    uint32_t loc[SEG_CNT / SEG_THREADS];
+    uint32_t loc[CNT / SEG_THREADS];
     uint32_t run = 0;
 #pragma unroll
-    for (int q = 0; q < SEG_CNT / SEG_THREADS; ++q) {
+    for (int q = 0; q < CNT / SEG_THREADS; ++q) {
       loc[q] = run;
-      run += cnt[tid * (SEG_CNT / SEG_THREADS) + q];
+      run += cnt[tid * (CNT / SEG_THREADS) + q];
     }
     uint32_t incl = run;                             // wave inclusive scan of the totals
     for (int off = 1; off < 64; off <<= 1) {
@@ -345,18 +348,18 @@ __global__ __launch_bounds__(SEG_THREADS) void emb_segsort_kernel(
     uint32_t base = incl - run;
     for (int q = 0; q < w; ++q) base += wsum[q];
 #pragma unroll
-    for (int q = 0; q < SEG_CNT / SEG_THREADS; ++q)
-      cnt[tid * (SEG_CNT / SEG_THREADS) + q] = base + loc[q];
+    for (int q = 0; q < CNT / SEG_THREADS; ++q)
+      cnt[tid * (CNT / SEG_THREADS) + q] = base + loc[q];
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < SEG_K; ++k) {
-      const uint32_t dst = cnt[(dig[k] * SEG_K + k) * SEG_WAVES + w] + rank[k];
+    for (int k = 0; k < SK; ++k) {
+      const uint32_t dst = cnt[(dig[k] * SK + k) * SEG_WAVES + w] + rank[k];
       skey[dst] = key[k];
       sval[dst] = val[k];
     }
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < SEG_K; ++k) {
+    for (int k = 0; k < SK; ++k) {
       key[k] = skey[k * SEG_THREADS + tid];
       val[k] = sval[k * SEG_THREADS + tid];
     }
@@ -365,7 +368,7 @@ __global__ __launch_bounds__(SEG_THREADS) void emb_segsort_kernel(
   const K kb = (K)a.row_offset[t];
   const int64_t go = a.grad_off[t];
 #pragma unroll
-  for (int k = 0; k < SEG_K; ++k) {
+  for (int k = 0; k < SK; ++k) {
     const int i = k * SEG_THREADS + tid;
     if (i < n) {
       keys_out[s0 + i] = kb + (K)key[k];
@@ -535,10 +538,14 @@ __device__ __forceinline__ bool skip_step(const EmbBwdArgs& a) {
 }
 
 // One optimizer update of one row; `wv` = current weights (prefetched).
+// Adam with pre-loaded moments (mpre / vpre: this lane's elements of the
+// row's m and v, issued with the chunk's other loads) or loading them here.
 template <int D, int OPT>
 __device__ __forceinline__ void update_row(const EmbBwdArgs& a, const OptScalars& o,
                                            uint64_t row, const float (&acc_in)[BwdCfg<D>::EPL],
-                                           float (&wv)[BwdCfg<D>::EPL], float st_row, int lane) {
+                                           float (&wv)[BwdCfg<D>::EPL], float st_row, int lane,
+                                           const float* mpre = nullptr,
+                                           const float* vpre = nullptr) {
   constexpr int EPL = BwdCfg<D>::EPL;
   float acc[EPL];
 #pragma unroll
@@ -582,8 +589,9 @@ __device__ __forceinline__ void update_row(const EmbBwdArgs& a, const OptScalars
       float* v = a.state2 + row * D + (act ? e0 : 0);
 #pragma unroll
       for (int u = 0; u < EPL; ++u) {
-        const float mm = a.beta1 * m[u] + (1.f - a.beta1) * acc[u];
-        const float vv = a.beta2 * v[u] + (1.f - a.beta2) * acc[u] * acc[u];
+        const float m0 = mpre ? mpre[u] : m[u], v0 = vpre ? vpre[u] : v[u];
+        const float mm = a.beta1 * m0 + (1.f - a.beta1) * acc[u];
+        const float vv = a.beta2 * v0 + (1.f - a.beta2) * acc[u] * acc[u];
         if (act) { m[u] = mm; v[u] = vv; }
         wv[u] -= o.lr * ((mm / o.bc1) / (sqrtf(vv / o.bc2) + a.eps) + a.weight_decay * wv[u]);
       }
@@ -648,11 +656,22 @@ __global__ __launch_bounds__(256) void emb_chunk_kernel(
 
   GradRaw<D, GB> g[CH];
   float wr[CH][EPL];
+  // Adam on narrow rows (one element per lane): the moments of every row of
+  // the chunk are loaded up front too, not one dependent round trip per
+  // finishing run (TwoTower / Bert4Rec, D = 16: a chunk's 32 updates waited
+  // on 32 serial m / v loads)
+  constexpr bool PRE_MV = OPT == EMB_ADAM && EPL == 1;
+  float mr[PRE_MV ? CH : 1][EPL], vr[PRE_MV ? CH : 1][EPL];
 #pragma unroll
   for (int p = 0; p < CH; ++p) {
     const int64_t go = (int64_t)rdlane((uint64_t)mygoff, p);
     load_grad_raw<D, GB>(g[p], a.grad, go + e0c);
-    if constexpr (NEED_W) load_row<D>(wr[p], a.W + (uint64_t)rdlane(mykey, p) * D + e0c);
+    const uint64_t rowp = (uint64_t)rdlane(mykey, p);
+    if constexpr (NEED_W) load_row<D>(wr[p], a.W + rowp * D + e0c);
+    if constexpr (PRE_MV) {
+      mr[p][0] = a.state1[rowp * D + e0c];
+      vr[p][0] = a.state2[rowp * D + e0c];
+    }
   }
   float acc[EPL];
 #pragma unroll
@@ -668,7 +687,12 @@ __global__ __launch_bounds__(256) void emb_chunk_kernel(
           float wv[EPL];
 #pragma unroll
           for (int u = 0; u < EPL; ++u) wv[u] = NEED_W ? wr[p][u] : 0.f;
-          update_row<D, OPT>(a, o, (uint64_t)rdlane(mykey, p), acc, wv, rdlanef(st_l, p), lane);
+          if constexpr (PRE_MV)
+            update_row<D, OPT>(a, o, (uint64_t)rdlane(mykey, p), acc, wv, rdlanef(st_l, p), lane,
+                               mr[p], vr[p]);
+          else
+            update_row<D, OPT>(a, o, (uint64_t)rdlane(mykey, p), acc, wv, rdlanef(st_l, p),
+                               lane);
         } else if (act) {
 #pragma unroll
           for (int u = 0; u < EPL; ++u) head[c * D + e0 + u] = acc[u];
@@ -1023,8 +1047,12 @@ void prep_impl(const EmbBwdArgs& a, const WsLayout& L, hipStream_t s) {
   const int R = a.segsort;                 // runs per physical table (0: off)
   if (onehot_path(a)) {
     if (R == 1) {
-      hipLaunchKernelGGL((emb_segsort_kernel<K, true>), dim3(a.T), dim3(SEG_THREADS), 0, s, a,
-                         keys_out, vals_out, goff, gscale, tcount, (int32_t*)nullptr);
+      if (a.B <= 2 * SEG_THREADS)
+        hipLaunchKernelGGL((emb_segsort_kernel<K, true, 2>), dim3(a.T), dim3(SEG_THREADS), 0, s, a,
+                           keys_out, vals_out, goff, gscale, tcount, (int32_t*)nullptr);
+      else
+        hipLaunchKernelGGL((emb_segsort_kernel<K, true>), dim3(a.T), dim3(SEG_THREADS), 0, s, a,
+                           keys_out, vals_out, goff, gscale, tcount, (int32_t*)nullptr);
     } else {
       int32_t* pos = (int32_t*)(ws + L.pos);
       hipLaunchKernelGGL((emb_segsort_kernel<K, false>), dim3(a.T), dim3(SEG_THREADS), 0, s, a, keys_in,

@@ -1147,6 +1147,154 @@ __device__ __forceinline__ void gemm_pp_body(const GemmArgs& p, int bid, char* s
 
 using PPG = PPGeom<128, 2, 128>;
 
+// ---------------------------------------------------------------------------
+// Two-group split-K kernel ("p8"): 256x128 tiles, 8 waves in two groups of
+// four (waves 0-3 / 4-7: one of each per SIMD), group 1 one barrier behind
+// group 0, so on every SIMD one wave issues MFMAs while its partner reads
+// fragments and issues LDS-DMA (cdna_hip_programming.md §5, the 8-phase
+// template's staggered groups; T3/T4 counted vmcnt + raw barriers; T5
+// setprio). Unlike that template's 256x256 tile, the block tile is 256x128
+// (DLRM's 8192 x 1024 outputs are 256 such tiles: one per CU) and the two
+// groups split each 64-deep K tile: group g computes its k32 half of every K
+// tile on the WHOLE 256x128 tile (wave tile 128x64, 32 fragments, the
+// cheapest LDS bytes per MFMA), and the two sums are added through LDS at
+// the end. Two phases per K tile per group (one 64-row half of the wave tile
+// x 4 column fragments = 16 MFMAs each); a 3-slot LDS ring (144 KiB) keeps
+// two K tiles of DMA in flight (issued in phase 0, two tiles ahead).
+// Measured (scripts/probes/gemm_pp8.hip vs gemm_floor.hip, random bf16):
+// compute floor 2.1 PF at 8192^3 vs 0.8-0.9 for the one-group loops.
+// Epilogue: pp_epilogue (bias, ReLU, ReLU mask, DCN second output, fp32
+// split-K slabs). No column-sum (bias-grad) support.
+constexpr int P8_NST = 3;
+constexpr int P8_STAGE = 3 * TILE_BYTES;                 // A 256x64 + B 128x64
+constexpr int P8_LDS = P8_NST * P8_STAGE;                // 144 KiB (>= 128 KiB reduction)
+static_assert(P8_LDS >= 128 * 1024, "p8 reduction buffer");
+
+template <bool A_COL, bool B_COL>
+__device__ __forceinline__ void gemm_p8_body(const GemmArgs& p, int bid, char* smem_raw) {
+  constexpr int PPW = 6;                                  // 48 DMA pieces per K tile / 8 waves
+  TDFO_LDS char* smem = (TDFO_LDS char*)smem_raw;
+  const int tiles_m = (p.M + LBM - 1) / LBM, tiles_n = (p.N + BN - 1) / BN;
+  const TileIdx ti = tile_of(tiles_m, tiles_n, p.splits, bid);
+  const int m0 = ti.tm * LBM, n0 = ti.tn * BN;
+  const int ktiles = p.K / BK;
+  const int per = (ktiles + p.splits - 1) / p.splits;
+  const int kt0 = ti.split * per;
+  const int nk = max(0, min(ktiles, kt0 + per) - kt0);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = w >> 2, q = w & 3;
+  const int ar = (q >> 1) * 128, bc = (q & 1) * 64;       // wave tile origin (128 x 64)
+
+  f32x4_t acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  auto stage = [&](int slot, int kt) {
+    TDFO_LDS char* st = smem + slot * P8_STAGE;
+    const int k0 = (kt0 + kt) * BK;
+#pragma unroll
+    for (int u = 0; u < PPW; ++u) {
+      const int ii = w * PPW + u, img = ii >> 4;
+      if (img < 2)
+        glds_piece_asm<A_COL>(p.A, p.lda, m0 + img * 128, p.M, k0, st + img * TILE_BYTES, ii & 15,
+                              lane);
+      else
+        glds_piece_asm<B_COL>(p.B, p.ldb, n0, p.N, k0, st + 2 * TILE_BYTES, ii & 15, lane);
+    }
+  };
+  bf16x8_t af[4], bfr[4];
+  auto rd_a = [&](int slot, int half) {
+    const TDFO_LDS char* img = smem + slot * P8_STAGE + (ar >> 7) * TILE_BYTES;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      af[i] = A_COL ? frag_col(img, half * 64 + i * 16, grp, lane)
+                    : frag_row(img, half * 64 + i * 16, grp, lane);
+  };
+  auto rd_b = [&](int slot) {
+    const TDFO_LDS char* img = smem + slot * P8_STAGE + 2 * TILE_BYTES;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      bfr[j] = B_COL ? frag_col(img, bc + j * 16, grp, lane) : frag_row(img, bc + j * 16, grp, lane);
+  };
+  auto mm = [&](int half) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        acc[half * 4 + i][j] =
+            __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[half * 4 + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  // the wait before tile t's first read: every thread's pieces of tile t
+  // landed, tile t+1's (issued one tile later) may still be in flight
+  auto wait_landed = [&](bool one_ahead) {
+    if (one_ahead) asm volatile("s_waitcnt vmcnt(%0)" ::"i"(PPW) : "memory");
+    else           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+  if (nk > 0) {
+    stage(0, 0);
+    if (nk > 1) stage(1, 1);
+    wait_landed(nk > 1);
+  }
+  pp_barrier();
+  if (grp == 1) pp_barrier();                            // group 1: one interval behind
+  for (int t = 0; t < nk; ++t) {
+    const int slot = t % P8_NST;
+    const bool ahead = t + 2 < nk;
+    // phase 0: B fragments + upper A half; DMA of tile t+2 into the slot
+    // every wave finished reading before this phase's opening barrier
+    rd_b(slot);
+    rd_a(slot, 0);
+    if (ahead) stage((t + 2) % P8_NST, t + 2);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    pp_barrier();
+    mm(0);
+    pp_barrier();
+    // phase 1: lower A half
+    rd_a(slot, 1);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (grp == 1 && t + 1 < nk) wait_landed(ahead);      // tile t+1 (group 1's pieces)
+    pp_barrier();
+    mm(1);
+    if (grp == 0 && t + 1 < nk) wait_landed(ahead);      // tile t+1 (group 0's pieces)
+    pp_barrier();
+  }
+  if (grp == 0) pp_barrier();                            // balance group 1's extra barrier
+  // group 1's sums into LDS (lane-major, conflict-free), group 0 adds them
+  __syncthreads();
+  f32x4_t* red = (f32x4_t*)smem_raw;
+  if (grp == 1) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) red[(q * 32 + i * 4 + j) * 64 + lane] = acc[i][j];
+  }
+  __syncthreads();
+  if (grp == 1) return;
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] += red[(q * 32 + i * 4 + j) * 64 + lane];
+  pp_epilogue<8, 4>(p, acc, m0 + ar, n0 + bc, lane, ti.split);
+}
+
+template <bool A_COL, bool B_COL>
+__global__ __launch_bounds__(512, 1) void gemm_p8_kernel(GemmArgs p) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  gemm_p8_body<A_COL, B_COL>(p, blockIdx.x, smem_raw);
+}
+
+template <bool AC0, bool BC0, bool AC1, bool BC1>
+__global__ __launch_bounds__(512, 1) void gemm_p8_pair_kernel(GemmArgs p0, GemmArgs p1, int nb0) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  if ((int)blockIdx.x < nb0) gemm_p8_body<AC0, BC0>(p0, blockIdx.x, smem_raw);
+  else                       gemm_p8_body<AC1, BC1>(p1, blockIdx.x - nb0, smem_raw);
+}
+
 template <bool A_COL, bool B_COL>
 __global__ __launch_bounds__(512, 2) void gemm_pp_kernel(GemmArgs p) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -1210,7 +1358,7 @@ void pp_pair_launch(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s) {
 // kernel (256x128: not for column-sum weight grads) (tests, A/B).
 int g_policy = 0;
 
-enum Kern { K_SMALL64 = 64, K_SMALL128 = 128, K_DEEP = 2, K_PP = 3, K_BIG = 4 };
+enum Kern { K_SMALL64 = 64, K_SMALL128 = 128, K_DEEP = 2, K_PP = 3, K_BIG = 4, K_P8 = 8 };
 
 template <bool AC, bool BC>
 int choose(const GemmArgs& a) {
@@ -1222,6 +1370,7 @@ int choose(const GemmArgs& a) {
     case 2: return K_DEEP;
     case 3: return K_PP;
     case 4: return big_ok ? K_BIG : K_PP;
+    case 8: return big_ok ? K_P8 : K_PP;
     default: break;
   }
   if (g_policy == 5) {
@@ -1256,6 +1405,8 @@ void launch(const GemmArgs& a, int k, hipStream_t s) {
                                        hipFuncAttributeMaxDynamicSharedMemorySize, DSMEM));
     TDFO_CHECK_HIP(hipFuncSetAttribute((const void*)gemm_big_kernel<AC, BC>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, LSMEM));
+    TDFO_CHECK_HIP(hipFuncSetAttribute((const void*)gemm_p8_kernel<AC, BC>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, P8_LDS));
     attr = true;
   }
   const int tn = (a.N + BN - 1) / BN;
@@ -1266,6 +1417,10 @@ void launch(const GemmArgs& a, int k, hipStream_t s) {
     case K_BIG:
       hipLaunchKernelGGL((gemm_big_kernel<AC, BC>), dim3(((a.M + LBM - 1) / LBM) * tn * a.splits),
                          dim3(512), LSMEM, s, a);
+      break;
+    case K_P8:
+      hipLaunchKernelGGL((gemm_p8_kernel<AC, BC>), dim3(((a.M + LBM - 1) / LBM) * tn * a.splits),
+                         dim3(512), P8_LDS, s, a);
       break;
     case K_DEEP:
       hipLaunchKernelGGL((gemm_deep_kernel<AC, BC>), dim3(((a.M + BM - 1) / BM) * tn * a.splits),
@@ -1325,9 +1480,29 @@ void big_pair_launch(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s) {
   TDFO_CHECK_HIP(hipGetLastError());
 }
 
+template <bool AC0, bool BC0, bool AC1, bool BC1>
+void p8_pair_launch(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s) {
+  auto fn = gemm_p8_pair_kernel<AC0, BC0, AC1, BC1>;
+  static bool attr = false;
+  if (!attr) {
+    TDFO_CHECK_HIP(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       P8_LDS));
+    attr = true;
+  }
+  const int g0 = big_grid(a0);
+  hipLaunchKernelGGL(fn, dim3(g0 + big_grid(a1)), dim3(512), P8_LDS, s, a0, a1, g0);
+  TDFO_CHECK_HIP(hipGetLastError());
+}
+
 bool try_pair(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s) {
   const int k0 = kernel_of(a0), k1 = kernel_of(a1);
   const int l0 = layout_of(a0), l1 = layout_of(a1);
+  if (k0 == K_P8 && k1 == K_P8) {
+    if (l0 == 3 && l1 == 1) { p8_pair_launch<true, true, false, true>(a0, a1, s); return true; }
+    if (l1 == 3 && l0 == 1) { p8_pair_launch<true, true, false, true>(a1, a0, s); return true; }
+    if (l0 == 3 && l1 == 3) { p8_pair_launch<true, true, true, true>(a0, a1, s); return true; }
+    return false;
+  }
   // 256x128 pairs: a weight grad on that kernel takes its layer's dgrad
   // along onto it (also a deep-kernel one: one grid instead of two)
   const bool b0 = k0 == K_BIG || (k1 == K_BIG && k0 == K_DEEP && !a0.csum_on);

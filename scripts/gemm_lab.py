@@ -133,7 +133,7 @@ def main():
         for p in pols:
             ops.gemm_policy(p)
             e = c.check()
-            res[(c.name, c.kind, p)] = {"err": e, "ts": []}
+            res[(c.name, c.kind, c.M, c.N, c.K, p)] = {"err": e, "ts": []}
             if not (e < 2e-2):
                 print(json.dumps({"layer": c.name, "kind": c.kind, "policy": p, "BAD_rel_err": e}),
                       flush=True)
@@ -141,17 +141,17 @@ def main():
         for c in cases:
             for p in pols:
                 ops.gemm_policy(p)
-                res[(c.name, c.kind, p)]["ts"].append(timeit(c.run))
+                res[(c.name, c.kind, c.M, c.N, c.K, p)]["ts"].append(timeit(c.run))
     tot = {p: 0.0 for p in pols}
     for c in cases:
         row = {"layer": c.name, "kind": c.kind, "MNK": [c.M, c.N, c.K], "S": c.S}
         for p in pols:
-            ts = sorted(res[(c.name, c.kind, p)]["ts"])
+            ts = sorted(res[(c.name, c.kind, c.M, c.N, c.K, p)]["ts"])
             t = ts[len(ts) // 2]
             tot[p] += t
             row[f"p{p}_us"] = round(t, 2)
             row[f"p{p}_TF"] = round(c.flop / t / 1e6, 1)
-            row[f"p{p}_err"] = float(f"{res[(c.name, c.kind, p)]['err']:.1e}")
+            row[f"p{p}_err"] = float(f"{res[(c.name, c.kind, c.M, c.N, c.K, p)]['err']:.1e}")
         print(json.dumps(row), flush=True)
     print(json.dumps({"total_us": {f"p{p}": round(v, 1) for p, v in tot.items()}}), flush=True)
 

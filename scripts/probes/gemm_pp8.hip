@@ -23,7 +23,7 @@ __device__ __forceinline__ void bar() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-template <int BN, int KS, bool AC, bool BC, int MODE>
+template <int BN, int KS, int NST, bool AC, bool BC, int MODE, int SPREAD = 0>
 __global__ __launch_bounds__(512, 1) void gpp(P p) {
   constexpr int BM = 256;
   constexpr int AI = 2, BI = BN / 128;
@@ -31,7 +31,7 @@ __global__ __launch_bounds__(512, 1) void gpp(P p) {
   constexpr int PIECES = (AI + BI) * 16;                // 1-KiB DMA pieces per K tile
   constexpr int PPW = PIECES / 8;                       // per wave
   constexpr int NPH = KS == 1 ? 4 : 2;                  // phases per K tile
-  constexpr int LPH = KS == 1 ? 2 : 1;                  // phases that issue the next tile's DMA
+  constexpr int LPH = SPREAD ? NPH : (KS == 1 ? 2 : 1);   // phases that issue the next tile's DMA
   static_assert(PPW % LPH == 0, "pieces per phase");
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   LDSP char* smem = (LDSP char*)smem_raw;
@@ -101,17 +101,21 @@ __global__ __launch_bounds__(512, 1) void gpp(P p) {
     __builtin_amdgcn_s_setprio(0);
   };
 
-  // prologue: tile 0 into slot 0
-  if (nk > 0) {
+  // prologue: tiles 0 .. NST-2 into their slots, wait for tile 0
 #pragma unroll
-    for (int part = 0; part < LPH; ++part) stage_part(0, 0, part);
-  }
-  vm_wait<0>();
+  for (int s0 = 0; s0 < NST - 1; ++s0)
+    if (s0 < nk) {
+#pragma unroll
+      for (int part = 0; part < LPH; ++part) stage_part(s0, s0, part);
+    }
+  if (NST == 3 && nk > 1) vm_wait<PPW>();
+  else vm_wait<0>();
   bar();
   if (grp == 1) bar();                                  // group 1 runs one interval behind
   for (int kt = 0; kt < nk; ++kt) {
-    const int slot = MODE == 2 ? 0 : (kt & 1);
-    const bool more = kt + 1 < nk;
+    const int slot = MODE == 2 ? 0 : kt % NST;
+    const bool more = kt + NST - 1 < nk;            // tile kt+NST-1 to stage
+    const bool ahead = kt + 2 < nk && NST == 3;     // tile kt+2 may stay in flight
 #pragma unroll
     for (int ph = 0; ph < NPH; ++ph) {
       // ---- read interval
@@ -129,13 +133,17 @@ __global__ __launch_bounds__(512, 1) void gpp(P p) {
         if (ph == 0) { rdB(slot, 0); rdA(slot, 0); }
         else rdA(slot, 1);
       }
-      if (ph < LPH && more) stage_part(slot ^ 1, kt + 1, ph);
+      if (ph < LPH && more) stage_part((kt + NST - 1) % NST, kt + NST - 1, ph);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (grp == 1 && ph == NPH - 1 && MODE != 2) vm_wait<0>();  // tile kt+1 landed (group 1's DMA)
+      if (grp == 1 && ph == NPH - 1 && MODE != 2) {       // tile kt+1 landed (group 1's DMA)
+        if (ahead) vm_wait<PPW>(); else vm_wait<0>();
+      }
       bar();
       // ---- MFMA interval
       if (MODE != 1) mma(mq, nq);
-      if (grp == 0 && ph == NPH - 1 && MODE != 2) vm_wait<0>();  // tile kt+1 landed (group 0's DMA)
+      if (grp == 0 && ph == NPH - 1 && MODE != 2) {       // tile kt+1 landed (group 0's DMA)
+        if (ahead) vm_wait<PPW>(); else vm_wait<0>();
+      }
       bar();
     }
   }
@@ -178,11 +186,11 @@ __global__ __launch_bounds__(512, 1) void gpp(P p) {
     }
 }
 
-template <int BN, int KS, bool AC, bool BC, int MODE>
+template <int BN, int KS, int NST, bool AC, bool BC, int MODE, int SPREAD = 0>
 float run(const P& p, int reps) {
-  auto fn = gpp<BN, KS, AC, BC, MODE>;
+  auto fn = gpp<BN, KS, NST, AC, BC, MODE, SPREAD>;
   constexpr int STAGE = (2 + BN / 128) * IMG;
-  const int lds = KS == 2 ? 131072 : 2 * STAGE;
+  const int lds = std::max(KS == 2 ? 131072 : 0, NST * STAGE);
   CK(hipFuncSetAttribute((const void*)fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
   const int grid = ((p.M + 255) / 256) * ((p.N + BN - 1) / BN);
   hipEvent_t a, b;
@@ -204,15 +212,15 @@ float run(const P& p, int reps) {
   return ts[ts.size() / 2];
 }
 
-template <int BN, int KS, bool AC, bool BC>
+template <int BN, int KS, int NST, bool AC, bool BC, int SPREAD = 0>
 void variant(const char* shape, P p, float* R, bool check) {
   const double flop = 2.0 * p.M * p.N * p.K;
   const int reps = p.K >= 4096 && p.M * (double)p.N >= 8192.0 * 4096 ? 5 : 20;
-  float t0 = run<BN, KS, AC, BC, 0>(p, reps);
+  float t0 = run<BN, KS, NST, AC, BC, 0, SPREAD>(p, reps);
   double err = -1;
   if (check) {
     CK(hipMemset(p.C, 0, (size_t)p.M * p.ldc * 2));
-    run<BN, KS, AC, BC, 0>(p, 1);
+    run<BN, KS, NST, AC, BC, 0, SPREAD>(p, 1);
     std::vector<uint16_t> c((size_t)p.M * p.ldc);
     std::vector<float> r((size_t)p.M * p.N);
     CK(hipMemcpy(c.data(), p.C, c.size() * 2, hipMemcpyDeviceToHost));
@@ -228,12 +236,12 @@ void variant(const char* shape, P p, float* R, bool check) {
       }
     err = mx / sc;
   }
-  float t1 = run<BN, KS, AC, BC, 1>(p, reps);
-  float t2 = run<BN, KS, AC, BC, 2>(p, reps);
-  printf("{\"shape\": \"%s\", \"MNK\": [%d, %d, %d], \"variant\": \"pp256x%d_ks%d\", "
+  float t1 = run<BN, KS, NST, AC, BC, 1, SPREAD>(p, reps);
+  float t2 = run<BN, KS, NST, AC, BC, 2, SPREAD>(p, reps);
+  printf("{\"shape\": \"%s\", \"MNK\": [%d, %d, %d], \"variant\": \"pp256x%d_ks%d_s%d_d%d\", "
          "\"full_us\": %.2f, \"TF\": %.0f, \"load_only_us\": %.2f, \"compute_only_us\": %.2f, "
          "\"compute_TF\": %.0f, \"rel_err\": %.2e}\n",
-         shape, p.M, p.N, p.K, BN, KS, t0, flop / t0 / 1e6, t1, t2, flop / t2 / 1e6, err);
+         shape, p.M, p.N, p.K, BN, KS, NST, SPREAD, t0, flop / t0 / 1e6, t1, t2, flop / t2 / 1e6, err);
   fflush(stdout);
 }
 
@@ -274,11 +282,13 @@ int main(int argc, char** argv) {
       CK(hipDeviceSynchronize());
     }
     if (s.bc) {
-      variant<256, 1, false, true>(s.name, p, R, ck);
-      variant<128, 2, false, true>(s.name, p, R, ck);
+      variant<256, 1, 2, false, true, 1>(s.name, p, R, ck);
+      variant<128, 2, 3, false, true, 0>(s.name, p, R, ck);
+      variant<128, 2, 3, false, true, 1>(s.name, p, R, ck);
     } else {
-      variant<256, 1, false, false>(s.name, p, R, ck);
-      variant<128, 2, false, false>(s.name, p, R, ck);
+      variant<256, 1, 2, false, false, 1>(s.name, p, R, ck);
+      variant<128, 2, 3, false, false, 0>(s.name, p, R, ck);
+      variant<128, 2, 3, false, false, 1>(s.name, p, R, ck);
     }
   }
   return 0;

@@ -331,7 +331,7 @@ class TwoTowerTrainer:
         self._mp_check([self.G[:NPARAM], self.dX[:b, :112]])
         if not self.mp and self.device.type == "cuda":
             # both step counters in one native launch (no torch kernels)
-            ops.bump([self.hyper, self.emb_hyper])
+            ops.bump([self.hyper[1:2], self.emb_hyper[1:2]])
             self._bumped = True
         try:
             self._dense_update()

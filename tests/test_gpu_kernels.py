@@ -30,7 +30,8 @@ def rel_err(a, b):
 
 
 # ------------------------------------------------------------------ GEMM
-@pytest.fixture(params=[0, 1, 2, 3, 4], ids=["auto", "twostage", "deep", "pingpong", "big"])
+@pytest.fixture(params=[0, 1, 2, 3, 4, 8],
+                ids=["auto", "twostage", "deep", "pingpong", "big", "p8"])
 def gemm_pol(request):
     """Run a GEMM test once per kernel (auto, and each kernel forced)."""
     old = ops.gemm_policy(request.param)
@@ -940,7 +941,7 @@ def test_embedding_dense_update_matches_reference(opt, D):
 
 @pytest.mark.parametrize("M", [8192, 1000])
 @pytest.mark.parametrize("N,K", [(1024, 512), (256, 512), (512, 256), (512, 3456), (3456, 512)])
-@pytest.mark.parametrize("policy", [0, 3, 5])
+@pytest.mark.parametrize("policy", [0, 3, 5, 8])
 def test_gemm_batch_pairs_wgrad_dgrad(M, N, K, policy):
     """A layer's weight grad (split-K slabs + column sums) and dgrad (ReLU
     mask) recorded under ops.gemm_batch go out as one paired launch with the
