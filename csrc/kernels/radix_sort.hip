@@ -254,6 +254,39 @@ __device__ __forceinline__ int ts_block_scan(int x, int* ws, int* total) {
   return pre;
 }
 
+// Column scan for the tiled passes: one 512-thread block per digit (<= 256
+// digits -> <= 256 blocks), the digit's per-tile counts in registers (<= 8
+// consecutive tiles per thread, loads unconditional at clamped addresses),
+// one block-wide scan; rewrites hist[tile][d] as the exclusive prefix over
+// tiles and writes the digit total. Replaces rs_scan_kernel there: its 8
+// blocks walked 64-deep LDS prefix chains, 17.5 us per pass at 428 tiles
+// (DCN-v2 multi-hot, profiles/r04/prof_dcn/summary.txt).
+constexpr int SC2_R = 8;
+
+__global__ __launch_bounds__(512) void ts_scan_col_kernel(int32_t* __restrict__ hist, int ntiles,
+                                                          int nb, int32_t* __restrict__ tot) {
+  __shared__ int ws[TS_WAVES];
+  const int d = blockIdx.x, t = threadIdx.x;
+  const int per = (ntiles + TS_THREADS - 1) / TS_THREADS;       // <= SC2_R (caller checks)
+  const int t0 = t * per, tl = ntiles - 1;
+  int c[SC2_R];
+#pragma unroll
+  for (int q = 0; q < SC2_R; ++q) c[q] = hist[(int64_t)min(t0 + q, tl) * nb + d];
+#pragma unroll
+  for (int q = 0; q < SC2_R; ++q) c[q] = (q < per && t0 + q < ntiles) ? c[q] : 0;
+  int sum = 0;
+#pragma unroll
+  for (int q = 0; q < SC2_R; ++q) sum += c[q];
+  int total;
+  int run = ts_block_scan(sum, ws, &total);
+  if (t == 0) tot[d] = total;
+#pragma unroll
+  for (int q = 0; q < SC2_R; ++q) {
+    if (q < per && t0 + q < ntiles) hist[(int64_t)(t0 + q) * nb + d] = run;
+    run += c[q];
+  }
+}
+
 template <typename K>
 __global__ __launch_bounds__(512) void ts_scatter_kernel(
     const K* __restrict__ kin, const int32_t* __restrict__ vin, K* __restrict__ kout,
@@ -360,8 +393,12 @@ int tiled_sort_impl(K* ka, int32_t* va, K* kb, int32_t* vb, int64_t n, int key_b
     const int nb = 1 << bits;
     hipLaunchKernelGGL(ts_hist_kernel<K>, dim3(ntiles), dim3(TS_THREADS), 0, s, kin, n, sh, bits,
                        hist);
-    hipLaunchKernelGGL(rs_scan_kernel, dim3((nb + SCAN_DPB - 1) / SCAN_DPB), dim3(1024), 0, s,
-                       hist, ntiles, nb, tot);
+    if (ntiles <= TS_THREADS * SC2_R)
+      hipLaunchKernelGGL(ts_scan_col_kernel, dim3(nb), dim3(TS_THREADS), 0, s, hist, ntiles, nb,
+                         tot);
+    else
+      hipLaunchKernelGGL(rs_scan_kernel, dim3((nb + SCAN_DPB - 1) / SCAN_DPB), dim3(1024), 0, s,
+                         hist, ntiles, nb, tot);
     hipLaunchKernelGGL(ts_scatter_kernel<K>, dim3(ntiles), dim3(TS_THREADS), 0, s, kin, vin, kout,
                        vout, n, sh, bits, hist, tot);
     TDFO_CHECK_HIP(hipGetLastError());

@@ -6,20 +6,24 @@
 //                                                          98 -> 16 -> 16
 //   logit = sum(u * i); loss = BCE-with-logits(logit, label)
 //
-// All dense parameters are 2,400 floats, so the whole step is memory/launch
-// bound, not MFMA bound (E = 16). One launch does forward, loss and the full
-// backward for 128 samples per block: one thread per sample with the weights
-// broadcast from LDS, then the per-sample activations / gradients are staged
-// in LDS and every thread reduces float4 slices of the weight gradient over
-// the block's samples. Block partials go to part[block][TT_PART_LD] and are
-// reduced in a fixed order (tdfo::reduce_rows) -> deterministic, no atomics.
-// Embedding gradients are written per sample (dX) for the sort-based fused
-// sparse optimizer (embedding.hip).
+// Every product is a 16-wide fp32 matmul, run on the exact-f32 matrix cores
+// (v_mfma_f32_16x16x4_f32: a k-ordered fmaf chain, cdna_hip_programming.md
+// §3 'FP32-input MFMA') with one wave per 16 samples, in a transposed
+// layout: every activation / gradient tile is [16 features][16 samples] in
+// the accumulator (lane l: samples l&15, features 4(l>>4)+r in register r),
+// which is exactly the B operand the next layer needs (register r feeds the
+// MFMA of k-step r), so forward, backward and input gradients chain in
+// registers with no data movement; weights are broadcast from LDS. Weight
+// gradients (sums over samples) read the tiles back from a per-wave LDS
+// stage, are reduced over the block's 4 waves in LDS and written as one
+// partial row per 64-sample block (reduced in a fixed order by
+// tdfo::reduce_rows: deterministic, no atomics). Embedding gradients are
+// written per sample (dX) for the sort-based fused sparse optimizer
+// (embedding.hip). (The one-thread-per-sample VALU kernel this replaces
+// took 38.8 us at B = 2048, 16 blocks: profiles/r05/two_tower/.)
 //
 // Parameter layout (flat fp32, Flax kernel convention W[in][out]):
 //   [uW1 16x16 | ub1 16 | uW2 16x16 | ub2 16 | iW1 98x16 | ib1 16 | iW2 16x16 | ib2 16]
-// i.e. 150 "rows" of 16; row r < 17 -> (xu,1) x dh_u, r < 34 -> (a_u,1) x du,
-// r < 133 -> (xi,1) x dh_i, else (a_i,1) x di.
 #include <hip/hip_fp16.h>
 
 #include "tdfo_common.h"
@@ -30,9 +34,14 @@ namespace {
 
 constexpr int E = 16;
 constexpr int NI = 98;          // item tower input width
-constexpr int SPB = 128;        // samples per block
-constexpr int AROWS = 150;      // rows of the parameter matrix
-constexpr int NP = AROWS * E;   // 2400
+constexpr int WS = 16;          // samples per wave
+constexpr int NWV = 4;          // waves per block
+constexpr int SPB = WS * NWV;   // samples per block (= ops.reference.TT_SPB)
+constexpr int NP = 150 * E;     // 2400 parameters
+constexpr int XLD = 116;        // staged sample row (114 used)
+// parameter offsets
+constexpr int O_UW1 = 0, O_UB1 = 256, O_UW2 = 272, O_UB2 = 528, O_IW1 = 544, O_IB1 = 2112,
+              O_IW2 = 2128, O_IB2 = 2384;
 
 __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
 
@@ -46,165 +55,183 @@ __device__ __forceinline__ float rnd(float x) {
   else return x;
 }
 
+__device__ __forceinline__ f32x4_t mfma4(float a, float b, f32x4_t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+template <bool HALF>
+__device__ __forceinline__ f32x4_t rnd4(f32x4_t v) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) v[r] = rnd<HALF>(v[r]);
+  return v;
+}
+
+// per-wave LDS tiles [feature][sample] of the weight-gradient operands
+enum { G_AU, G_DU, G_DHU, G_AI, G_DI, G_DHI, G_N };
+
 template <bool TRAIN, bool HALF>
-__global__ __launch_bounds__(SPB) void two_tower_kernel(TwoTowerArgs a) {
+__global__ __launch_bounds__(64 * NWV) void two_tower_kernel(TwoTowerArgs a) {
   __shared__ float Wl[NP];
-  __shared__ float As[TRAIN ? SPB : 1][AROWS];
-  __shared__ __attribute__((aligned(16))) float Gs[TRAIN ? SPB : 1][4 * E];
-  __shared__ float red[SPB / 64];
-  const int t = threadIdx.x;
-  for (int k = t; k < NP; k += SPB) Wl[k] = rnd<HALF>(a.P[k]);
+  __shared__ float Xs[NWV][WS][XLD];
+  __shared__ float Gs[TRAIN ? NWV : 1][G_N][E][WS];
+  __shared__ float Ps[TRAIN ? NWV : 1][NP];
+  __shared__ float red[NWV];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int j = lane & 15, g = lane >> 4;          // sample column / feature group
+  for (int k = t; k < NP; k += 64 * NWV) Wl[k] = rnd<HALF>(a.P[k]);
+  const int64_t s0 = (int64_t)blockIdx.x * SPB + w * WS;
+  float(*X)[XLD] = Xs[w];
+  for (int idx = lane; idx < WS * 114; idx += 64) {
+    const int r = idx / 114, c = idx - r * 114;
+    const int64_t sr = s0 + r;
+    X[r][c] = sr < a.B ? rnd<HALF>(a.X[sr * a.ldx + c]) : 0.f;
+  }
   __syncthreads();
-  const float* uW1 = Wl;
-  const float* ub1 = Wl + 16 * E;
-  const float* uW2 = Wl + 17 * E;
-  const float* ub2 = Wl + 33 * E;
-  const float* iW1 = Wl + 34 * E;
-  const float* ib1 = Wl + 132 * E;
-  const float* iW2 = Wl + 133 * E;
-  const float* ib2 = Wl + 149 * E;
+  const float* uW1 = Wl + O_UW1;
+  const float* uW2 = Wl + O_UW2;
+  const float* iW1 = Wl + O_IW1;
+  const float* iW2 = Wl + O_IW2;
 
-  const int64_t s = (int64_t)blockIdx.x * SPB + t;
+  // ---- forward: H^T = W1^T X^T + b1 (rows: hidden feature 4g+r, cols: sample j)
+  f32x4_t hu, hi;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    hu[r] = Wl[O_UB1 + 4 * g + r];
+    hi[r] = Wl[O_IB1 + 4 * g + r];
+  }
+#pragma unroll
+  for (int k0 = 0; k0 < E; k0 += 4) hu = mfma4(uW1[(k0 + g) * E + j], X[j][k0 + g], hu);
+#pragma unroll
+  for (int k0 = 0; k0 < 100; k0 += 4) {
+    const int k = k0 + g;
+    hi = mfma4(k < NI ? iW1[k * E + j] : 0.f, k < NI ? X[j][E + k] : 0.f, hi);
+  }
+  hu = rnd4<HALF>(hu);
+  hi = rnd4<HALF>(hi);
+  f32x4_t au, ai, u, iv;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    au[r] = rnd<HALF>(hu[r] * sigm(hu[r]));
+    ai[r] = rnd<HALF>(hi[r] * sigm(hi[r]));
+    u[r] = Wl[O_UB2 + 4 * g + r];
+    iv[r] = Wl[O_IB2 + 4 * g + r];
+  }
+  // fc2: k-step r takes hidden feature 4g+r from lane group g (register r)
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    u = mfma4(uW2[(4 * g + r) * E + j], au[r], u);
+    iv = mfma4(iW2[(4 * g + r) * E + j], ai[r], iv);
+  }
+  u = rnd4<HALF>(u);
+  iv = rnd4<HALF>(iv);
+  float dot = 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) dot = fmaf(u[r], iv[r], dot);
+  dot += __shfl_xor(dot, 16, 64);
+  dot += __shfl_xor(dot, 32, 64);
+  const float logit = rnd<HALF>(dot);
+  const int64_t s = s0 + j;
   const bool valid = s < a.B;
-  const float* xr = a.X + (valid ? s : 0) * a.ldx;
-  float xu[E], xi[NI];
+  if (valid && g == 0) a.logits[s] = logit;
+  if constexpr (TRAIN) {
+    // ---- loss + backward
+    const float y = valid ? a.labels[s] : 0.f;
+    float loss = (valid && g == 0) ? fmaxf(logit, 0.f) - logit * y + log1pf(__expf(-fabsf(logit)))
+                                   : 0.f;
+    const float ls = a.loss_scale ? a.loss_scale[0] : 1.f;
+    const float dl = valid ? rnd<HALF>((sigm(logit) - y) * a.inv_n * ls) : 0.f;
+    f32x4_t du, di;
 #pragma unroll
-  for (int k = 0; k < E; k += 4) {
-    const float4 v = *(const float4*)(xr + k);
-    xu[k] = rnd<HALF>(v.x); xu[k + 1] = rnd<HALF>(v.y);
-    xu[k + 2] = rnd<HALF>(v.z); xu[k + 3] = rnd<HALF>(v.w);
-  }
-#pragma unroll
-  for (int k = 0; k < 96; k += 4) {
-    const float4 v = *(const float4*)(xr + E + k);
-    xi[k] = rnd<HALF>(v.x); xi[k + 1] = rnd<HALF>(v.y);
-    xi[k + 2] = rnd<HALF>(v.z); xi[k + 3] = rnd<HALF>(v.w);
-  }
-  xi[96] = rnd<HALF>(xr[E + 96]);
-  xi[97] = rnd<HALF>(xr[E + 97]);
-
-  // ---- forward
-  float hu[E], au[E], u[E], hi[E], ai[E], iv[E];
-#pragma unroll
-  for (int o = 0; o < E; ++o) { hu[o] = ub1[o]; hi[o] = ib1[o]; }
-#pragma unroll
-  for (int k = 0; k < E; ++k)
-#pragma unroll
-    for (int o = 0; o < E; ++o) hu[o] = fmaf(xu[k], uW1[k * E + o], hu[o]);
-#pragma unroll
-  for (int k = 0; k < NI; ++k)
-#pragma unroll
-    for (int o = 0; o < E; ++o) hi[o] = fmaf(xi[k], iW1[k * E + o], hi[o]);
-#pragma unroll
-  for (int o = 0; o < E; ++o) {
-    hu[o] = rnd<HALF>(hu[o]);
-    hi[o] = rnd<HALF>(hi[o]);
-    au[o] = rnd<HALF>(hu[o] * sigm(hu[o]));
-    ai[o] = rnd<HALF>(hi[o] * sigm(hi[o]));
-    u[o] = ub2[o];
-    iv[o] = ib2[o];
-  }
-#pragma unroll
-  for (int k = 0; k < E; ++k)
-#pragma unroll
-    for (int o = 0; o < E; ++o) {
-      u[o] = fmaf(au[k], uW2[k * E + o], u[o]);
-      iv[o] = fmaf(ai[k], iW2[k * E + o], iv[o]);
+    for (int r = 0; r < 4; ++r) {
+      du[r] = rnd<HALF>(dl * iv[r]);
+      di[r] = rnd<HALF>(dl * u[r]);
     }
-  float logit = 0.f;
+    // dA^T = W2 dY^T (rows: hidden feature, k-step r: output feature 4g+r)
+    f32x4_t dau = {0.f, 0.f, 0.f, 0.f}, dai = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int o = 0; o < E; ++o) {
-    u[o] = rnd<HALF>(u[o]);
-    iv[o] = rnd<HALF>(iv[o]);
-  }
-#pragma unroll
-  for (int o = 0; o < E; ++o) logit = fmaf(u[o], iv[o], logit);
-  logit = rnd<HALF>(logit);
-  if (valid) a.logits[s] = logit;
-  if constexpr (!TRAIN) return;
-
-  // ---- loss + backward
-  const float y = valid ? a.labels[s] : 0.f;
-  float loss = valid ? fmaxf(logit, 0.f) - logit * y + log1pf(__expf(-fabsf(logit))) : 0.f;
-  const float ls = a.loss_scale ? a.loss_scale[0] : 1.f;
-  const float dl = valid ? rnd<HALF>((sigm(logit) - y) * a.inv_n * ls) : 0.f;
-  float du[E], di[E], dhu[E], dhi[E];
-#pragma unroll
-  for (int o = 0; o < E; ++o) { du[o] = rnd<HALF>(dl * iv[o]); di[o] = rnd<HALF>(dl * u[o]); }
-#pragma unroll
-  for (int k = 0; k < E; ++k) {
-    float gu = 0.f, gi = 0.f;
-#pragma unroll
-    for (int o = 0; o < E; ++o) {
-      gu = fmaf(uW2[k * E + o], du[o], gu);
-      gi = fmaf(iW2[k * E + o], di[o], gi);
+    for (int r = 0; r < 4; ++r) {
+      dau = mfma4(uW2[j * E + 4 * g + r], du[r], dau);
+      dai = mfma4(iW2[j * E + 4 * g + r], di[r], dai);
     }
-    const float su = sigm(hu[k]), si = sigm(hi[k]);
-    dhu[k] = rnd<HALF>(gu * su * (1.f + hu[k] * (1.f - su)));
-    dhi[k] = rnd<HALF>(gi * si * (1.f + hi[k] * (1.f - si)));
-  }
-  if (valid) {
-    float* dxr = a.dX + s * a.lddx;
+    f32x4_t dhu, dhi;
 #pragma unroll
-    for (int k = 0; k < E; k += 4) {
-      float g[4];
+    for (int r = 0; r < 4; ++r) {
+      const float su = sigm(hu[r]), si = sigm(hi[r]);
+      dhu[r] = rnd<HALF>(dau[r] * su * (1.f + hu[r] * (1.f - su)));
+      dhi[r] = rnd<HALF>(dai[r] * si * (1.f + hi[r] * (1.f - si)));
+    }
+    // embedding gradients dX^T = W1 dH^T: lane (g, j) holds dX[s][k0 + 4g .. +3]
+    {
+      f32x4_t d = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        float acc = 0.f;
-#pragma unroll
-        for (int o = 0; o < E; ++o) acc = fmaf(uW1[(k + q) * E + o], dhu[o], acc);
-        g[q] = rnd<HALF>(acc);
-      }
-      *(float4*)(dxr + k) = make_float4(g[0], g[1], g[2], g[3]);
+      for (int r = 0; r < 4; ++r) d = mfma4(uW1[j * E + 4 * g + r], dhu[r], d);
+      if (valid)
+        *(float4*)(a.dX + s * a.lddx + 4 * g) =
+            make_float4(rnd<HALF>(d[0]), rnd<HALF>(d[1]), rnd<HALF>(d[2]), rnd<HALF>(d[3]));
     }
 #pragma unroll
-    for (int k = 0; k < 96; k += 4) {
-      float g[4];
+    for (int rb = 0; rb < 6; ++rb) {
+      f32x4_t d = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        float acc = 0.f;
-#pragma unroll
-        for (int o = 0; o < E; ++o) acc = fmaf(iW1[(k + q) * E + o], dhi[o], acc);
-        g[q] = rnd<HALF>(acc);
-      }
-      *(float4*)(dxr + E + k) = make_float4(g[0], g[1], g[2], g[3]);
+      for (int r = 0; r < 4; ++r) d = mfma4(iW1[(rb * E + j) * E + 4 * g + r], dhi[r], d);
+      if (valid)
+        *(float4*)(a.dX + s * a.lddx + E + rb * E + 4 * g) =
+            make_float4(rnd<HALF>(d[0]), rnd<HALF>(d[1]), rnd<HALF>(d[2]), rnd<HALF>(d[3]));
     }
-  }
-  // stage A (inputs of each weight row, 1 for biases) and G (output grads)
-  float* A = As[t];
+    // ---- weight gradients of this wave's 16 samples: dW[k][o] = sum_s A[s][k] dY[s][o]
+    float(*G)[E][WS] = Gs[w];
 #pragma unroll
-  for (int k = 0; k < E; ++k) { A[k] = xu[k]; A[17 + k] = au[k]; A[133 + k] = ai[k]; }
-#pragma unroll
-  for (int k = 0; k < NI; ++k) A[34 + k] = xi[k];
-  const float one = valid ? 1.f : 0.f;
-  A[16] = one; A[33] = one; A[132] = one; A[149] = one;
-  float* G = Gs[t];
-#pragma unroll
-  for (int o = 0; o < E; ++o) { G[o] = dhu[o]; G[E + o] = du[o]; G[2 * E + o] = dhi[o]; G[3 * E + o] = di[o]; }
-  // block loss sum
-  for (int off = 32; off > 0; off >>= 1) loss += __shfl_xor(loss, off);
-  if ((t & 63) == 0) red[t >> 6] = loss;
-  __syncthreads();
-  float* prow = a.part + (int64_t)blockIdx.x * TT_PART_LD;
-  if (t == 0) {
-    float l = 0.f;
-    for (int w = 0; w < SPB / 64; ++w) l += red[w];
-    prow[NP] = l;
-  }
-  // weight gradient: unit = (row r, 4 columns c4)
-  for (int unit = t; unit < AROWS * 4; unit += SPB) {
-    const int r = unit >> 2, c4 = (unit & 3) * 4;
-    const int grp = r < 17 ? 0 : (r < 34 ? 1 : (r < 133 ? 2 : 3));
-    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int q = 0; q < SPB; ++q) {
-      const float av = As[q][r];
-      const float4 g = *(const float4*)(&Gs[q][grp * E + c4]);
-      acc.x = fmaf(av, g.x, acc.x);
-      acc.y = fmaf(av, g.y, acc.y);
-      acc.z = fmaf(av, g.z, acc.z);
-      acc.w = fmaf(av, g.w, acc.w);
+    for (int r = 0; r < 4; ++r) {
+      G[G_AU][4 * g + r][j] = au[r];
+      G[G_DU][4 * g + r][j] = du[r];
+      G[G_DHU][4 * g + r][j] = dhu[r];
+      G[G_AI][4 * g + r][j] = ai[r];
+      G[G_DI][4 * g + r][j] = di[r];
+      G[G_DHI][4 * g + r][j] = dhi[r];
     }
-    *(float4*)(prow + r * E + c4) = acc;
+    __syncthreads();
+    float* P = Ps[w];
+    // k-step m sums samples 4m + g; result row k = 4g + r, column o = j
+    auto wtile = [&](auto act, int dy, int base, int krows) {
+      f32x4_t d = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int m = 0; m < 4; ++m) d = mfma4(act(4 * m + g), G[dy][j][4 * m + g], d);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (4 * g + r < krows) P[base + (4 * g + r) * E + j] = d[r];
+    };
+    wtile([&](int sm) { return X[sm][j]; }, G_DHU, O_UW1, E);
+    wtile([&](int sm) { return G[G_AU][j][sm]; }, G_DU, O_UW2, E);
+    wtile([&](int sm) { return G[G_AI][j][sm]; }, G_DI, O_IW2, E);
+#pragma unroll
+    for (int kb = 0; kb < 7; ++kb)
+      wtile([&](int sm) { return kb * E + j < NI ? X[sm][E + kb * E + j] : 0.f; }, G_DHI,
+            O_IW1 + kb * E * E, NI - kb * E);
+    {   // bias grads: lane (g, j) sums tile g's feature j over the samples
+      const int src = g == 0 ? G_DHU : (g == 1 ? G_DU : (g == 2 ? G_DHI : G_DI));
+      const int dst = g == 0 ? O_UB1 : (g == 1 ? O_UB2 : (g == 2 ? O_IB1 : O_IB2));
+      float b = 0.f;
+#pragma unroll
+      for (int q = 0; q < WS; ++q) b += G[src][j][q];
+      P[dst + j] = b;
+    }
+    const float lw = wave_sum(loss);
+    if (lane == 0) red[w] = lw;
+    __syncthreads();
+    // block partial: fixed wave order
+    float* prow = a.part + (int64_t)blockIdx.x * TT_PART_LD;
+    for (int k = t; k < NP; k += 64 * NWV) {
+      float v = Ps[0][k];
+#pragma unroll
+      for (int q = 1; q < NWV; ++q) v += Ps[q][k];
+      prow[k] = v;
+    }
+    if (t == 0) {
+      float l = 0.f;
+#pragma unroll
+      for (int q = 0; q < NWV; ++q) l += red[q];
+      prow[NP] = l;
+    }
   }
 }
 
@@ -215,14 +242,15 @@ int two_tower_parts(int B) { return (B + SPB - 1) / SPB; }
 void two_tower(const TwoTowerArgs& a, int train, hipStream_t s) {
   if (a.B <= 0) return;
   const int grid = two_tower_parts(a.B);
+  const dim3 blk(64 * NWV);
   if (train && a.half)
-    hipLaunchKernelGGL((two_tower_kernel<true, true>), dim3(grid), dim3(SPB), 0, s, a);
+    hipLaunchKernelGGL((two_tower_kernel<true, true>), dim3(grid), blk, 0, s, a);
   else if (train)
-    hipLaunchKernelGGL((two_tower_kernel<true, false>), dim3(grid), dim3(SPB), 0, s, a);
+    hipLaunchKernelGGL((two_tower_kernel<true, false>), dim3(grid), blk, 0, s, a);
   else if (a.half)
-    hipLaunchKernelGGL((two_tower_kernel<false, true>), dim3(grid), dim3(SPB), 0, s, a);
+    hipLaunchKernelGGL((two_tower_kernel<false, true>), dim3(grid), blk, 0, s, a);
   else
-    hipLaunchKernelGGL((two_tower_kernel<false, false>), dim3(grid), dim3(SPB), 0, s, a);
+    hipLaunchKernelGGL((two_tower_kernel<false, false>), dim3(grid), blk, 0, s, a);
   TDFO_CHECK_HIP(hipGetLastError());
 }
 

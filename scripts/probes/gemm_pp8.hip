@@ -23,6 +23,10 @@ __device__ __forceinline__ void bar() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// SPREAD: 0 DMA issued in the first phase(s) of a tile, 1 spread over all
+// phases, 2 register staging (global_load_dwordx4 of tile t+2 into VGPRs at
+// phase 0 of tile t, ds_write_b128 of them at phase 0 of tile t+1 into the
+// same lane-linear images; cdna_hip_programming.md T14)
 template <int BN, int KS, int NST, bool AC, bool BC, int MODE, int SPREAD = 0>
 __global__ __launch_bounds__(512, 1) void gpp(P p) {
   constexpr int BM = 256;
@@ -31,7 +35,8 @@ __global__ __launch_bounds__(512, 1) void gpp(P p) {
   constexpr int PIECES = (AI + BI) * 16;                // 1-KiB DMA pieces per K tile
   constexpr int PPW = PIECES / 8;                       // per wave
   constexpr int NPH = KS == 1 ? 4 : 2;                  // phases per K tile
-  constexpr int LPH = SPREAD ? NPH : (KS == 1 ? 2 : 1);   // phases that issue the next tile's DMA
+  constexpr int LPH = SPREAD == 1 ? NPH : (KS == 1 ? 2 : 1);   // phases that issue DMA
+  constexpr bool REG = SPREAD == 2;
   static_assert(PPW % LPH == 0, "pieces per phase");
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
   LDSP char* smem = (LDSP char*)smem_raw;
@@ -64,6 +69,41 @@ __global__ __launch_bounds__(512, 1) void gpp(P p) {
         piece<AC>(p.A, p.lda, m0 + img * 128, p.M, k0, st + img * IMG, ii & 15, lane);
       else
         piece<BC>(p.B, p.ldb, n0 + (img - AI) * 128, p.N, k0, st + img * IMG, ii & 15, lane);
+    }
+  };
+
+  typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+  u32x4 stg[REG ? PPW : 1];
+  auto src_of = [&](int kt, int ii) -> const uint16_t* {
+    const int img = ii >> 4, pi = ii & 15, k0 = kt * BK;
+    const bool col = img < AI ? AC : BC;
+    const uint16_t* g = img < AI ? p.A : p.B;
+    const int64_t ld = img < AI ? p.lda : p.ldb;
+    const int x0 = img < AI ? m0 + img * 128 : n0 + (img - AI) * 128;
+    const int xs = img < AI ? p.M : p.N;
+    if (col) {
+      const int kr = pi * 4 + (lane >> 4);
+      const int c = (lane & 15) ^ swz_col(kr);
+      int gc = x0 + c * 8;
+      gc = gc <= xs - 8 ? gc : xs - 8;
+      return g + (int64_t)(k0 + kr) * ld + gc;
+    }
+    const int r = pi * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ (r & 7);
+    int gr = x0 + r;
+    gr = gr < xs ? gr : xs - 1;
+    return g + (int64_t)gr * ld + k0 + c * 8;
+  };
+  auto reg_load = [&](int kt) {
+#pragma unroll
+    for (int u = 0; u < PPW; ++u) stg[u] = *(const u32x4*)src_of(kt, w * PPW + u);
+  };
+  auto reg_write = [&](int slot) {
+    LDSP char* st = smem + slot * STAGE;
+#pragma unroll
+    for (int u = 0; u < PPW; ++u) {
+      const int ii = w * PPW + u;
+      *(LDSP u32x4*)(st + (ii >> 4) * IMG + (ii & 15) * 1024 + lane * 16) = stg[u];
     }
   };
 
@@ -102,14 +142,23 @@ __global__ __launch_bounds__(512, 1) void gpp(P p) {
   };
 
   // prologue: tiles 0 .. NST-2 into their slots, wait for tile 0
-#pragma unroll
-  for (int s0 = 0; s0 < NST - 1; ++s0)
-    if (s0 < nk) {
-#pragma unroll
-      for (int part = 0; part < LPH; ++part) stage_part(s0, s0, part);
+  if (REG) {
+    if (MODE != 2 && nk > 0) {
+      reg_load(0);
+      reg_write(0);
+      if (nk > 1) reg_load(1);
     }
-  if (NST == 3 && nk > 1) vm_wait<PPW>();
-  else vm_wait<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  } else {
+#pragma unroll
+    for (int s0 = 0; s0 < NST - 1; ++s0)
+      if (s0 < nk) {
+#pragma unroll
+        for (int part = 0; part < LPH; ++part) stage_part(s0, s0, part);
+      }
+    if (NST == 3 && nk > 1) vm_wait<PPW>();
+    else vm_wait<0>();
+  }
   bar();
   if (grp == 1) bar();                                  // group 1 runs one interval behind
   for (int kt = 0; kt < nk; ++kt) {
@@ -133,15 +182,22 @@ __global__ __launch_bounds__(512, 1) void gpp(P p) {
         if (ph == 0) { rdB(slot, 0); rdA(slot, 0); }
         else rdA(slot, 1);
       }
-      if (ph < LPH && more) stage_part((kt + NST - 1) % NST, kt + NST - 1, ph);
+      if (REG) {
+        if (ph == 0 && MODE != 2) {
+          if (kt + 1 < nk) reg_write((kt + 1) % NST);     // tile kt+1, loaded one tile ago
+          if (kt + 2 < nk) reg_load(kt + 2);
+        }
+      } else if (ph < LPH && more) {
+        stage_part((kt + NST - 1) % NST, kt + NST - 1, ph);
+      }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (grp == 1 && ph == NPH - 1 && MODE != 2) {       // tile kt+1 landed (group 1's DMA)
+      if (!REG && grp == 1 && ph == NPH - 1 && MODE != 2) {   // tile kt+1 landed (group 1's DMA)
         if (ahead) vm_wait<PPW>(); else vm_wait<0>();
       }
       bar();
       // ---- MFMA interval
       if (MODE != 1) mma(mq, nq);
-      if (grp == 0 && ph == NPH - 1 && MODE != 2) {       // tile kt+1 landed (group 0's DMA)
+      if (!REG && grp == 0 && ph == NPH - 1 && MODE != 2) {   // tile kt+1 landed (group 0's DMA)
         if (ahead) vm_wait<PPW>(); else vm_wait<0>();
       }
       bar();
@@ -282,13 +338,13 @@ int main(int argc, char** argv) {
       CK(hipDeviceSynchronize());
     }
     if (s.bc) {
-      variant<256, 1, 2, false, true, 1>(s.name, p, R, ck);
+      variant<256, 1, 2, false, true, 2>(s.name, p, R, ck);
       variant<128, 2, 3, false, true, 0>(s.name, p, R, ck);
-      variant<128, 2, 3, false, true, 1>(s.name, p, R, ck);
+      variant<128, 2, 2, false, true, 2>(s.name, p, R, ck);
     } else {
-      variant<256, 1, 2, false, false, 1>(s.name, p, R, ck);
+      variant<256, 1, 2, false, false, 2>(s.name, p, R, ck);
       variant<128, 2, 3, false, false, 0>(s.name, p, R, ck);
-      variant<128, 2, 3, false, false, 1>(s.name, p, R, ck);
+      variant<128, 2, 2, false, false, 2>(s.name, p, R, ck);
     }
   }
   return 0;

@@ -957,8 +957,8 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
     def _s_emb_update(self):
         self.emb.stage_bwd_update(self.emb_hyper)
 
-    def _m_allreduce_wait(self):
-        for name in ("_ar_top", "_ar_work"):
+    def _m_allreduce_wait(self, names=("_ar_top", "_ar_work")):
+        for name in names:
             w = getattr(self, name, None)
             if w is not None:
                 work, g, b = w

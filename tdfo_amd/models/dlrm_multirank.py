@@ -18,13 +18,14 @@ explicit event record / wait nodes into one executable graph
 (``ops.ComposedGraph``), launched on its own stream -- three launches per
 step instead of ~20 Python stage issues and ~8 c10d calls:
 
-  M  (MLP):      [wait d'] bottom fwd  [wait c5'] top fwd/bwd + interaction bwd
+  M  (MLP):      [wait dpp'] bottom fwd  [wait c5', d'] top fwd/bwd + interaction bwd
                  (m2)  bottom bwd, next batch's load from staging + bucketize
                  of its sharded tables' ids (m4)  top weight grads (m3)
   D  (dense      [wait c5'] ids-only sort of this batch (e0)  [wait m2]
       comm):     replicated tables' dense grad + all-reduce + update (dp)
                  [wait m4] bottom-bucket all-reduce, next batch's replicated
-                 ids (dpp)  [wait m3] top-bucket all-reduce, dense optimizer (d)
+                 ids, bottom-bucket optimizer (dpp)  [wait m3] top-bucket
+                 all-reduce, top-bucket optimizer (d)
   EC (embedding  [wait m2] gradient all-to-all  [wait e0, dp] fused embedding
       + its      update  [wait m4, dpp] id all-to-all, lookup + pooled
       RCCL):     all-to-all (c5)
@@ -38,6 +39,8 @@ makes M's waits see the previous step's records and D's / EC's this step's
 (D's c5 wait: the previous step's, EC has not been launched yet).
 """
 from __future__ import annotations
+
+import os
 
 import torch
 
@@ -101,10 +104,18 @@ class MultiRankStreamsMixin:
             emb.stage_fwd_lookup(dp=not dp_dense)
             emb.stage_fwd_out_exchange()
 
+        split_opt = os.environ.get("TDFO_MR_SPLIT_OPT", "1") != "0"     # A/B knob
+
         def d_b():
+            # the top bucket (top MLP, DCN cross layers, head): all-reduce,
+            # then the optimizer on its range only
             self._m_allreduce_top_start()
-            self._m_allreduce_wait()
-            self._s_dense_update()
+            if split_opt:
+                self._m_allreduce_wait(("_ar_top",))
+                self._dense_update_range(self._ar_split, self.fp.p.numel())
+            else:
+                self._m_allreduce_wait()
+                self._s_dense_update()
 
         def m4():
             self._s_bottom_bwd()
@@ -130,6 +141,14 @@ class MultiRankStreamsMixin:
                 emb.rw_publish_need(self.dcomm)
             self._m_allreduce_start()
             d_prep()
+            # DDP-style split of the dense optimizer: the bottom bucket is
+            # updated as soon as its all-reduce lands, so the next step's
+            # bottom forward (M1, waiting on dpp) runs while the top bucket
+            # is still being reduced (before: M1 waited for the whole
+            # optimizer behind the top bucket, profiles/r04/prof_w8r1_lanes)
+            if split_opt:
+                self._m_allreduce_wait(("_ar_work",))
+                self._dense_update_range(0, self._ar_split)
 
         return {"M1": self._s_bottom_fwd, "M2": m2, "M4": m4,
                 "M3": self._s_top_wgrad if self._defer_top_wgrad else None,
@@ -139,6 +158,7 @@ class MultiRankStreamsMixin:
                 "ECub": lambda: (ec_upd(), ec_b())}
 
     def _mr_capture(self, restage: bool = True):
+        split_opt = os.environ.get("TDFO_MR_SPLIT_OPT", "1") != "0"
         """``restage`` False (re-capture between steps): keep the staging
         buffers and the next batch already staged in them."""
         assert self.device.type == "cuda"
@@ -206,9 +226,9 @@ class MultiRankStreamsMixin:
             # M: the bottom backward (+ the next batch's load into x0 / ids /
             # labels, all of whose readers have run) before the top weight
             # grads, so the embedding side and the bottom bucket go sooner
-            "M": chain([("wait", "d"), ("graph", "M1"), ("wait", "c5"), ("graph", "M2"),
-                        ("record", "m2"), ("graph", "M4"), ("record", "m4"), ("graph", "M3"),
-                        ("record", "m3")]),
+            "M": chain([("wait", "dpp" if split_opt else "d"), ("graph", "M1"), ("wait", "c5"),
+                        ("wait", "d"), ("graph", "M2"), ("record", "m2"), ("graph", "M4"),
+                        ("record", "m4"), ("graph", "M3"), ("record", "m3")]),
             # D: the ids-only sort of this batch (its ids arrived with the
             # previous step's exchanges), the replicated tables' dense grad +
             # all-reduce, the two dense buckets and the dense optimizer

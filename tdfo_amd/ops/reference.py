@@ -465,7 +465,7 @@ def cross_bwd(dout, x0, y, dy, dx0, accumulate, add_dout=False):
 
 TT_NPARAM = 2400
 TT_PART_LD = 2432
-TT_SPB = 128
+TT_SPB = 64          # samples per kernel block (two_tower.hip SPB)
 
 
 def two_tower_unpack(P):
@@ -494,7 +494,7 @@ def two_tower_forward(X, P):
 
 def two_tower(X, P, labels, inv_n, logits, dX=None, part=None, loss_scale=None, half=False):
     """Oracle of tdfo::two_tower via autograd. part rows follow the kernel:
-    one row per 128-sample block, [dP | loss_sum]. ``half``: the towers run
+    one row per TT_SPB-sample block, [dP | loss_sum]. ``half``: the towers run
     in float16 (autograd through fp16 ops); ``loss_scale`` scales the loss."""
     dt = torch.float16 if half else torch.float32
     if dX is None:
