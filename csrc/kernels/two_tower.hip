@@ -15,9 +15,10 @@
 // MFMA of k-step r), so forward, backward and input gradients chain in
 // registers with no data movement; weights are broadcast from LDS. Weight
 // gradients (sums over samples) read the tiles back from a per-wave LDS
-// stage, are reduced over the block's 4 waves in LDS and written as one
-// partial row per 64-sample block (reduced in a fixed order by
-// tdfo::reduce_rows: deterministic, no atomics). Embedding gradients are
+// stage, are reduced over the block's waves in LDS and written as one
+// partial row per block (reduced in a fixed order by tdfo::reduce_rows:
+// deterministic, no atomics). One wave per block: B = 2048 is 128 blocks
+// (64-sample blocks of 4 waves: 19.7 us, 32 blocks). Embedding gradients are
 // written per sample (dX) for the sort-based fused sparse optimizer
 // (embedding.hip). (The one-thread-per-sample VALU kernel this replaces
 // took 38.8 us at B = 2048, 16 blocks: profiles/r05/two_tower/.)
@@ -35,7 +36,7 @@ namespace {
 constexpr int E = 16;
 constexpr int NI = 98;          // item tower input width
 constexpr int WS = 16;          // samples per wave
-constexpr int NWV = 4;          // waves per block
+constexpr int NWV = 1;          // waves per block
 constexpr int SPB = WS * NWV;   // samples per block (= ops.reference.TT_SPB)
 constexpr int NP = 150 * E;     // 2400 parameters
 constexpr int XLD = 116;        // staged sample row (114 used)

@@ -6,6 +6,8 @@ are out-variants so engines can preallocate buffers and capture hipGraphs.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import reference as ref
@@ -242,6 +244,8 @@ def linear_dgrad(dy, w, mask=None, out=None):
 # at 1024, 0.670 at 128; DCN-v2 2.902 vs 3.003 (512), 3.200 (128).
 _WGRAD_TARGET = 512
 _WGRAD_MINKT = 8
+_WGRAD_FEW_TILES = 4
+_WGRAD_FEW_MINKT = int(os.environ.get("TDFO_WGRAD_FEW_MINKT", "2"))   # A/B knob (8: off)
 
 
 def wgrad_splits(M: int, N: int, K: int, target_blocks: int = 0, slots: int = 0) -> int:
@@ -257,7 +261,14 @@ def wgrad_splits(M: int, N: int, K: int, target_blocks: int = 0, slots: int = 0)
     extra split adds (written here, read by the optimizer / reduce; priced in
     K-tile times of ~0.6 us at ~5 TB/s)."""
     kt = K // 64
-    smax = max(1, kt // _WGRAD_MINKT)
+    minkt = _WGRAD_MINKT
+    if slots <= 0 and ((M + 127) // 128) * ((N + 127) // 128) <= _WGRAD_FEW_TILES:
+        # a handful of output tiles (DLRM's bottom-0 wgrad: 512 x 64, 4 tiles):
+        # the GEMM is one K loop of dependent tile loads per block, latency
+        # bound, so shorter K ranges over more blocks win despite the extra
+        # fp32 slabs the optimizer reads
+        minkt = _WGRAD_FEW_MINKT
+    smax = max(1, kt // minkt)
     if slots > 0:
         tiles = ((M + 255) // 256) * ((N + 127) // 128)
         pen = M * N * 8 / 5e12 / 0.6e-6

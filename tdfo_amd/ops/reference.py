@@ -465,7 +465,7 @@ def cross_bwd(dout, x0, y, dy, dx0, accumulate, add_dout=False):
 
 TT_NPARAM = 2400
 TT_PART_LD = 2432
-TT_SPB = 64          # samples per kernel block (two_tower.hip SPB)
+TT_SPB = 16          # samples per kernel block (two_tower.hip SPB)
 
 
 def two_tower_unpack(P):
