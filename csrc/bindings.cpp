@@ -636,6 +636,14 @@ void graph_exec_upload(int64_t ex) {
   TDFO_HIP_OK(hipGraphUpload(reinterpret_cast<hipGraphExec_t>(ex), cur_stream()));
 }
 
+// Node count of a captured (keep_graph) hipGraph: segments that captured
+// no work are left out of the composed chains.
+int64_t graph_num_nodes(int64_t g) {
+  size_t n = 0;
+  TDFO_HIP_OK(hipGraphGetNodes(reinterpret_cast<hipGraph_t>(g), nullptr, &n));
+  return (int64_t)n;
+}
+
 void graph_exec_destroy(int64_t ex) {
   TDFO_HIP_OK(hipGraphExecDestroy(reinterpret_cast<hipGraphExec_t>(ex)));
 }
@@ -1385,6 +1393,7 @@ TORCH_LIBRARY(tdfo, m) {
   m.def("graph_compose(int[] kinds, int[] handles) -> int", graph_compose);
   m.def("graph_exec_launch(int ex) -> ()", graph_exec_launch);
   m.def("graph_exec_destroy(int ex) -> ()", graph_exec_destroy);
+  m.def("graph_num_nodes(int g) -> int", graph_num_nodes);
   m.def("graph_exec_upload(int ex) -> ()", graph_exec_upload);
   m.def("gemm_batch_begin() -> ()", gemm_batch_begin);
   m.def("gemm_batch_end() -> ()", gemm_batch_end);

@@ -230,13 +230,27 @@ class InStepSynthetic:
                                        start=start)
         self.start = int(start)
         self.counter = None
+        self.counter0 = None
         self.base = None
+
+    # the batch index comes from the trainer's fp32 step counter, which
+    # counts integers exactly only up to 2^24 (StepLoop refuses to run past)
+    COUNTER_LIMIT = 1 << 24
 
     def bind(self, counter: torch.Tensor):
         """``counter``: the trainer's float step counter (bumped once per
         step, after both generators of the step have read it)."""
         self.counter = counter
-        self.base = self.start - int(round(float(counter.reshape(-1)[0].item())))
+        self.counter0 = int(round(float(counter.reshape(-1)[0].item())))
+        self.base = self.start - self.counter0
+
+    def check_steps(self, step_index: int, n: int):
+        """Raise if steps [step_index, step_index + n) would read the fp32
+        counter past its exact-integer range."""
+        if self.counter0 is not None and \
+                self.counter0 + (step_index - self.start) + n > self.COUNTER_LIMIT:
+            raise RuntimeError("InStepSynthetic: the fp32 step counter indexes batches exactly "
+                               f"only up to 2^24 steps; use --data fresh for longer runs")
 
     def gen_ids(self, ids: torch.Tensor):
         g = self.g

@@ -1157,6 +1157,9 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
         return self.t_out.float() @ head[:K] + head[K]
 
     def state_dict(self):
+        # a deferred embedding update (per-stream graphs) is issued and
+        # ordered before the tables are exposed
+        self.sync_streams()
         return {"dense": self.fp.state_dict(), "emb": self.emb.state_dict(),
                 "dense_m": self.fp.m, "dense_v": self.fp.v, "dense_hyper": self.dense_hyper,
                 "emb_hyper": self.emb_hyper}

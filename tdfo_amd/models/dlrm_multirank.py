@@ -41,6 +41,7 @@ makes M's waits see the previous step's records and D's / EC's this step's
 from __future__ import annotations
 
 import os
+import warnings
 
 import torch
 
@@ -51,6 +52,11 @@ from ..utils.capture import graph_capture
 class MultiRankStreamsMixin:
     """Per-stream graph capture / replay for W > 1 (``capture_graph`` picks it
     when ``_mr_ok()``)."""
+
+    # segments that always hold work (bottom / top MLP, the dense buckets'
+    # all-reduces + optimizer); the others may be empty for a plan (e.g. Dp
+    # without replicated tables, D0 / EC1 without sharded ones)
+    _MR_WORK = ("M1", "M2", "M4", "Da", "Db")
 
     def _mr_ok(self) -> bool:
         """Pipelined with the lookup in the tail and every exchange
@@ -192,18 +198,27 @@ class MultiRankStreamsMixin:
                 routes = [c.capture_origin(st) for c in {id(self.comm): self.comm,
                                                           id(self.dcomm): self.dcomm}.values()
                           if hasattr(c, "capture_origin")]
-                with graph_capture(g, pool=pool, stream=st, capture_error_mode="thread_local"):
-                    for r in routes:
-                        r.__enter__()
-                    try:
-                        if stamp is not None:
-                            ops.stamp(stamp[0], stamp[1], names.index(name), len(names), 0)
-                        fn()
-                        if stamp is not None:
-                            ops.stamp(stamp[0], stamp[1], names.index(name), len(names), 1)
-                    finally:
+                with warnings.catch_warnings():
+                    # a plan without replicated (or without sharded) tables
+                    # leaves some segments empty: checked and dropped below
+                    warnings.filterwarnings("ignore", message="The CUDA Graph is empty")
+                    with graph_capture(g, pool=pool, stream=st,
+                                       capture_error_mode="thread_local"):
                         for r in routes:
-                            r.__exit__(None, None, None)
+                            r.__enter__()
+                        try:
+                            if stamp is not None:
+                                ops.stamp(stamp[0], stamp[1], names.index(name), len(names), 0)
+                            fn()
+                            if stamp is not None:
+                                ops.stamp(stamp[0], stamp[1], names.index(name), len(names), 1)
+                        finally:
+                            for r in routes:
+                                r.__exit__(None, None, None)
+                if ops.graph_num_nodes(g) == 0:
+                    if name in self._MR_WORK:
+                        raise RuntimeError(f"multi-rank segment {name} captured no work")
+                    continue                       # not chained (its events still are)
                 graphs[name] = g
         finally:
             self._whole_capture = False

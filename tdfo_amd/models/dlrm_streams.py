@@ -22,6 +22,16 @@ batch's ids on the embedding stream (or, ``ids_stream``, on a third stream
 right behind the sort), so the next lookup overlaps this step's bottom-MLP
 backward; readers of tables / params outside ``step()`` call
 ``sync_streams()`` first.
+
+Reader contract with a producer stream (``set_copy_stream``, the default
+with the device generator): the step's embedding update (E3) is *deferred*
+-- enqueued by the next ``load_batch`` / ``step`` / ``sync_streams()`` /
+``flush_pending()``, after the wait for the next batch's ids copy. So after
+a bare ``step()`` the update is not enqueued at all, and a device-wide
+``torch.cuda.synchronize()`` alone does NOT make the tables current: call
+``sync_streams()`` (or ``flush_pending()``) first. The trainer's own readers
+do (``state_dict``, ``dense_state``, ``predict``, ``pop_loss``, checkpoints),
+and ``StepLoop.run`` flushes at its end.
 """
 from __future__ import annotations
 

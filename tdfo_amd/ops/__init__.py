@@ -117,6 +117,11 @@ class ComposedGraph:
             pass
 
 
+def graph_num_nodes(g: torch.cuda.CUDAGraph) -> int:
+    """Nodes of a graph captured with keep_graph=True (0: it captured no work)."""
+    return int(_native().graph_num_nodes(int(g.raw_cuda_graph())))
+
+
 def upload_graphs(graphs):
     """hipGraphUpload every executable graph (torch CUDAGraph or
     ComposedGraph) on the current stream, so their first launches do not
@@ -244,8 +249,6 @@ def linear_dgrad(dy, w, mask=None, out=None):
 # at 1024, 0.670 at 128; DCN-v2 2.902 vs 3.003 (512), 3.200 (128).
 _WGRAD_TARGET = 512
 _WGRAD_MINKT = 8
-_WGRAD_FEW_TILES = 4
-_WGRAD_FEW_MINKT = int(os.environ.get("TDFO_WGRAD_FEW_MINKT", "2"))   # A/B knob (8: off)
 
 
 def wgrad_splits(M: int, N: int, K: int, target_blocks: int = 0, slots: int = 0) -> int:
@@ -261,14 +264,10 @@ def wgrad_splits(M: int, N: int, K: int, target_blocks: int = 0, slots: int = 0)
     extra split adds (written here, read by the optimizer / reduce; priced in
     K-tile times of ~0.6 us at ~5 TB/s)."""
     kt = K // 64
-    minkt = _WGRAD_MINKT
-    if slots <= 0 and ((M + 127) // 128) * ((N + 127) // 128) <= _WGRAD_FEW_TILES:
-        # a handful of output tiles (DLRM's bottom-0 wgrad: 512 x 64, 4 tiles):
-        # the GEMM is one K loop of dependent tile loads per block, latency
-        # bound, so shorter K ranges over more blocks win despite the extra
-        # fp32 slabs the optimizer reads
-        minkt = _WGRAD_FEW_MINKT
-    smax = max(1, kt // minkt)
+    # (round 5: K ranges down to 2 tiles for the few-tile bottom-0 / bottom-2
+    # weight grads measured slower in the DLRM-1TB step, 0.435-0.436 vs
+    # 0.429-0.431 ms, profiles/r05/notes.md)
+    smax = max(1, kt // _WGRAD_MINKT)
     if slots > 0:
         tiles = ((M + 255) // 256) * ((N + 127) // 128)
         pen = M * N * 8 / 5e12 / 0.6e-6

@@ -156,6 +156,8 @@ class StepLoop:
 
     def _run(self, n: int, on_dev: bool):
         tr, wd = self.tr, self.wd
+        if self.in_step and hasattr(self.src, "check_steps"):
+            self.src.check_steps(self.step_index, n)
         for k in range(n):
             if self.in_step:                   # the step draws its own batch
                 tr.step()
