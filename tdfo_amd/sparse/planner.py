@@ -95,8 +95,9 @@ def plan_sharding(tables: Sequence[TableConfig], world_size: int, optim: EmbOpti
                   strategy: str = "auto", dp_max_bytes: int = 0,
                   row_cost: Optional[Callable[[int], float]] = None,
                   dp_max_rows: Optional[int] = None,
-                  dp_replicate_max_bytes: int = 256 << 20) -> ShardingPlan:
-    """Deterministic greedy planner.
+                  dp_replicate_max_bytes: int = 256 << 20,
+                  balance: float = 1.10) -> ShardingPlan:
+    """Deterministic greedy planner with a balance pass.
 
     strategy: "auto" (table-wise with row-wise fallback for tables that fit
     no rank), "table_wise", "row_wise", "column_wise" (tables split evenly by
@@ -117,7 +118,52 @@ def plan_sharding(tables: Sequence[TableConfig], world_size: int, optim: EmbOpti
     4-row and a 40M-row table cost 85 vs 103 us per 65536 ids, while the
     4-table ranks of the world-8 plan, holding only small tables, are the
     slowest at 188 us vs 140-164 us for the 3-table ranks).
+
+    balance ("auto", W > 1): a multi-hot table can cost more than a whole
+    rank's fair share (DCN-v2's pooling-100 table is ~9 ms of lookups on its
+    owner at W = 8, the other ranks ~1.3 ms), and greedy table-wise placement
+    cannot split it. While the plan's max / min rank cost exceeds
+    ``balance``, the costliest table-wise table of the costliest rank is
+    re-planned row-wise (its ids spread over every rank), one table at a
+    time. Along that sequence the plan with the lowest max rank cost wins
+    (within 1 % of it, the most even one), and only if it beats the greedy
+    plan by >= 2 %: one-hot plans whose imbalance is one table's granularity
+    (DLRM-1TB) stay table-wise, since row-wise adds link traffic on every
+    rank.
     """
+    kw = dict(batch_per_rank=batch_per_rank, pooling=pooling, hbm_bytes=hbm_bytes,
+              reserve_frac=reserve_frac, strategy=strategy, dp_max_bytes=dp_max_bytes,
+              row_cost=row_cost, dp_max_rows=dp_max_rows,
+              dp_replicate_max_bytes=dp_replicate_max_bytes)
+    plan = _plan_once(tables, world_size, optim, frozenset(), **kw)
+    if strategy != "auto" or world_size == 1 or balance is None:
+        return plan
+    pool = list(pooling) if pooling is not None else [1.0] * len(tables)
+    if max(plan.cost) <= balance * min(plan.cost):
+        return plan
+    seq, cur, forced = [], plan, frozenset()
+    for _ in range(len(tables)):
+        hot = max(range(world_size), key=lambda r: (cur.cost[r], -r))
+        tw = [s.table for s in cur.shards if s.kind == "table_wise" and s.ranks == [hot]]
+        if not tw or max(cur.cost) <= 1.001 * min(cur.cost):
+            break
+        forced = forced | {max(tw, key=lambda t: (pool[t] * tables[t].embedding_dim, -t))}
+        try:
+            cur = _plan_once(tables, world_size, optim, forced, **kw)
+        except MemoryError:
+            break
+        seq.append(cur)
+    top = min([max(p.cost) for p in seq], default=max(plan.cost))
+    if top > 0.98 * max(plan.cost):
+        return plan
+    # lowest max rank cost; within 1 % of it, the most even plan
+    near = [p for p in seq if max(p.cost) <= 1.01 * top]
+    return min(near, key=lambda p: max(p.cost) / min(p.cost))
+
+
+def _plan_once(tables, world_size, optim, force_rw, batch_per_rank, pooling, hbm_bytes,
+               reserve_frac, strategy, dp_max_bytes, row_cost, dp_max_rows,
+               dp_replicate_max_bytes) -> ShardingPlan:
     W = world_size
     cap = int(hbm_bytes * (1.0 - reserve_frac))
     T = len(tables)
@@ -177,7 +223,8 @@ def plan_sharding(tables: Sequence[TableConfig], world_size: int, optim: EmbOpti
     # every rank, and the table-wise placement below must see that memory
     if strategy == "auto" and W > 1:
         for t in order:
-            if tables[t].num_embeddings * _mem_per_row(tables[t].embedding_dim, optim) > cap:
+            if t in force_rw or (tables[t].num_embeddings *
+                                 _mem_per_row(tables[t].embedding_dim, optim) > cap):
                 shards[t] = row_wise(t)
     # "data_parallel": the smallest tables are replicated while their fp32
     # weights add up to at most dp_replicate_max_bytes -- the replicated set

@@ -60,6 +60,34 @@ def test_plan_config5_gt1tb_rowwise_fits_8_not_4():
             plan_sharding(cfg.tables(), w, opt, pooling=MLPERF_MULTIHOT)
 
 
+@pytest.mark.parametrize("rows", ["gt1tb", "1tb"])
+def test_plan_balance_pass_spreads_multihot_tables(rows):
+    """DCN-v2's multi-hot tables (pooling up to 100) outweigh a rank's fair
+    share: greedy table-wise placement left the gt1tb plan at 2416-3058 us
+    and the 1TB plan at 1331-9470 us (pooling-100 table on rank 0). The
+    balance pass re-plans the heavy tables row-wise."""
+    table_rows = DCN_GT1TB_ROWS if rows == "gt1tb" else CRITEO_1TB_ROWS
+    cfg = DLRMConfig(table_rows=table_rows, interaction="dcn", pooling=MLPERF_MULTIHOT)
+    opt = EmbOptimConfig("rowwise_adagrad")
+    greedy = plan_sharding(cfg.tables(), 8, opt, pooling=MLPERF_MULTIHOT, balance=None)
+    p = plan_sharding(cfg.tables(), 8, opt, pooling=MLPERF_MULTIHOT)
+    assert max(p.cost) < 0.98 * max(greedy.cost)
+    assert max(p.cost) <= (1.10 if rows == "gt1tb" else 1.15) * min(p.cost)
+    assert p.kind_of(20) == "row_wise"                          # the pooling-100 table
+    assert max(p.mem_bytes) <= 288e9 * 0.85
+    assert p == plan_sharding(cfg.tables(), 8, opt, pooling=MLPERF_MULTIHOT)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_plan_balance_pass_keeps_one_hot_table_wise(world):
+    """DLRM-1TB (pooling 1): converting a table row-wise only adds link time
+    on every rank, so the greedy table-wise plan stands."""
+    cfg = DLRMConfig()
+    opt = EmbOptimConfig("rowwise_adagrad")
+    assert plan_sharding(cfg.tables(), world, opt) == \
+        plan_sharding(cfg.tables(), world, opt, balance=None)
+
+
 def test_plan_cost_counts_xgmi():
     cfg = DLRMConfig()
     opt = EmbOptimConfig("rowwise_adagrad")
