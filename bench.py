@@ -50,6 +50,9 @@ def parse(argv=None):
                          "pinned slots and a copy-stream H2D prefetcher")
     ap.add_argument("--pool", type=int, default=8, help="--data pool: batches in the pool")
     ap.add_argument("--dist", default="uniform", choices=["uniform", "zipf"])
+    ap.add_argument("--rw-exchange", default="auto", choices=["auto", "pooled", "rows"],
+                    help="row-wise exchange (DLRMConfig.rw_exchange): rows = one-hot tables "
+                         "return looked-up rows by all-to-all instead of pooled partials")
     ap.add_argument("--sharding", default="auto",
                     choices=["auto", "table_wise", "row_wise", "column_wise", "data_parallel",
                              "replicated"])
@@ -157,6 +160,7 @@ def self_launch(args, argv) -> int:
 def _cfg(args, rows, pipe):
     from tdfo_amd.models.dlrm import MLPERF_MULTIHOT, DLRMConfig
     kw = dict(table_rows=list(rows), sharding=args.sharding, pipeline=pipe,
+              rw_exchange=args.rw_exchange,
               dense_comm=args.dense_comm, stream_graphs=not args.no_stream_graphs,
               opt_placement=args.opt_placement,
               defer_wgrad=None if args.defer_wgrad is None else args.defer_wgrad == "1")

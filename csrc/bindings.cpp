@@ -887,6 +887,53 @@ void rw_pool(const Tensor& Wt, const Tensor& recv, const Tensor& meta, int64_t n
   tdfo::rw_pool(a, cur_stream());
 }
 
+// one-hot row-wise "rows" exchange (rowwise.hip)
+void check_bf16_buf(const Tensor& t, int64_t n, const char* name) {
+  check_dev(t, name);
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16 && t.is_contiguous() && t.numel() >= n, name,
+              ": bf16 contiguous buffer too small");
+}
+
+void rw_rows_gather(const Tensor& Wt, const Tensor& recv, int64_t W, int64_t cap, const Tensor& out) {
+  check_dev(Wt, "W");
+  TORCH_CHECK(Wt.scalar_type() == at::kFloat && Wt.is_contiguous() && Wt.dim() == 2, "W fp32 2-D");
+  TORCH_CHECK(Wt.size(0) <= (1LL << 32), "rw: owner rows must fit 32-bit row keys");
+  const int64_t D = Wt.size(1);
+  TORCH_CHECK(D == 16 || D == 32 || D == 64 || D == 128 || D == 256, "rw_rows_gather: D unsupported");
+  check_i64(recv, "recv");
+  TORCH_CHECK(recv.numel() == W * (cap + 1), "rw recv buffer must be [W][cap+1]");
+  check_bf16_buf(out, W * (cap + 1) * D, "rw rows out");
+  tdfo::rw_rows_gather(Wt.data_ptr<float>(), (int)D, recv.data_ptr<int64_t>(), (int)W, cap,
+                       bf16_mut(out), cur_stream());
+}
+
+void rw_rows_scatter(const Tensor& send, int64_t W, int64_t cap, int64_t B, int64_t D,
+                     const Tensor& rows, const Tensor& region, int64_t ld, const Tensor& map,
+                     int64_t nrw) {
+  check_i64(send, "send");
+  TORCH_CHECK(send.numel() == W * (cap + 1), "rw send buffer must be [W][cap+1]");
+  TORCH_CHECK(D == 16 || D == 32 || D == 64 || D == 128 || D == 256, "rw_rows_scatter: D unsupported");
+  TORCH_CHECK(ld >= nrw * D && ld % 4 == 0, "rw_rows_scatter: row stride");
+  TORCH_CHECK(B * ld < (1LL << 31), "rw_rows_scatter: region offsets must fit int32");
+  check_bf16_buf(rows, W * (cap + 1) * D, "rw rows");
+  check_bf16_buf(region, B * ld, "rw pooled region");
+  check_dev(map, "rw map");
+  TORCH_CHECK(map.scalar_type() == at::kInt && map.numel() >= W * (cap + 1), "rw map int32 [W][cap+1]");
+  tdfo::rw_rows_scatter(send.data_ptr<int64_t>(), (int)W, cap, (int)B, (int)D, bf16_ptr(rows),
+                        bf16_mut(region), ld, map.data_ptr<int32_t>(), cur_stream());
+}
+
+void rw_grads_gather(const Tensor& map, int64_t W, int64_t cap, int64_t D, const Tensor& dregion,
+                     const Tensor& gsend) {
+  check_dev(map, "rw map");
+  TORCH_CHECK(map.scalar_type() == at::kInt && map.numel() >= W * (cap + 1), "rw map int32 [W][cap+1]");
+  TORCH_CHECK(D == 16 || D == 32 || D == 64 || D == 128 || D == 256, "rw_grads_gather: D unsupported");
+  check_bf16_buf(dregion, D, "rw grad region");
+  check_bf16_buf(gsend, W * (cap + 1) * D, "rw grad send");
+  tdfo::rw_grads_gather(map.data_ptr<int32_t>(), (int)W, cap, (int)D, bf16_ptr(dregion),
+                        bf16_mut(gsend), cur_stream());
+}
+
 tdfo::EmbBwdArgs emb_rw_args(const Tensor& W, int64_t Wsz, int64_t B, int64_t cap, bool mean,
                              int64_t key_bits) {
   check_dev(W, "W");
@@ -904,14 +951,15 @@ tdfo::EmbBwdArgs emb_rw_args(const Tensor& W, int64_t Wsz, int64_t B, int64_t ca
 
 void embedding_bwd_prepare_rw(const Tensor& W, const Tensor& recv, const Tensor& meta, int64_t nrw,
                               int64_t Wsz, int64_t B, int64_t cap, bool mean, int64_t key_bits,
-                              int64_t grad_ld, int64_t dummy_row, const Tensor& work) {
+                              int64_t grad_ld, int64_t dummy_row, const Tensor& work,
+                              int64_t rows) {
   auto a = emb_rw_args(W, Wsz, B, cap, mean, key_bits);
   check_i64(recv, "recv"); rw_meta_check(meta, nrw);
   TORCH_CHECK(recv.numel() == Wsz * (cap + 1), "rw recv buffer must be [W][cap+1]");
   TORCH_CHECK(dummy_row >= 0 && dummy_row < W.size(0), "rw scratch row out of range");
   set_emb_ws(a, work);
   tdfo::embedding_bwd_prepare_rw(a, recv.data_ptr<int64_t>(), meta.data_ptr<int64_t>(), (int)nrw,
-                                 (int)Wsz, cap, grad_ld, dummy_row, cur_stream());
+                                 (int)Wsz, cap, grad_ld, dummy_row, (int)rows, cur_stream());
 }
 
 void embedding_bwd_apply_rw(const Tensor& W, int64_t Wsz, int64_t B, int64_t cap, bool mean,
@@ -1471,7 +1519,12 @@ TORCH_LIBRARY(tdfo, m) {
   m.def("rw_pool(Tensor Wt, Tensor recv, Tensor meta, int nrw, int W, int B, int cap, bool mean, "
         "Tensor(a!) starts, Tensor(b!) out, int out_ld) -> ()");
   m.def("embedding_bwd_prepare_rw(Tensor W, Tensor recv, Tensor meta, int nrw, int Wsz, int B, "
-        "int cap, bool mean, int key_bits, int grad_ld, int dummy_row, Tensor(a!) workspace) -> ()");
+        "int cap, bool mean, int key_bits, int grad_ld, int dummy_row, Tensor(a!) workspace, "
+        "int rows=0) -> ()");
+  m.def("rw_rows_gather(Tensor Wt, Tensor recv, int W, int cap, Tensor(a!) out) -> ()");
+  m.def("rw_rows_scatter(Tensor send, int W, int cap, int B, int D, Tensor rows, Tensor(a!) region, "
+        "int ld, Tensor(b!) map, int nrw) -> ()");
+  m.def("rw_grads_gather(Tensor map, int W, int cap, int D, Tensor dregion, Tensor(a!) gsend) -> ()");
   m.def("embedding_bwd_apply_rw(Tensor(a!) W, int Wsz, int B, int cap, bool mean, int key_bits, "
         "Tensor grad, int opt, Tensor(b!)? state1, Tensor(c!)? state2, Tensor hyper, float eps, "
         "float beta1, float beta2, float weight_decay, Tensor(d!) workspace) -> ()");
@@ -1538,6 +1591,9 @@ TORCH_LIBRARY_IMPL(tdfo, CUDA, m) {
   m.impl("rw_bucketize", rw_bucketize);
   m.impl("rw_pool", rw_pool);
   m.impl("embedding_bwd_prepare_rw", embedding_bwd_prepare_rw);
+  m.impl("rw_rows_gather", rw_rows_gather);
+  m.impl("rw_rows_scatter", rw_rows_scatter);
+  m.impl("rw_grads_gather", rw_grads_gather);
   m.impl("embedding_bwd_apply_rw", embedding_bwd_apply_rw);
   m.impl("dense_optimizer", dense_optimizer);
   m.impl("check_finite", check_finite);

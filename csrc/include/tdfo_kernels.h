@@ -218,14 +218,27 @@ struct RwPoolArgs {
   int32_t* starts; void* out; int out_f32; int64_t out_ld;
 };
 void rw_pool(const RwPoolArgs& a, hipStream_t s);
+// One-hot row-wise tables ("rows" exchange, rowwise.hip): the owner's bf16
+// rows per received entry ([W][cap+1][D]), the requester's scatter of the
+// received rows into its pooled region (row stride ld) plus the slot -> offset
+// map ([W][cap+1] int32, slot cap = count) its backward gathers the gradient
+// rows with.
+void rw_rows_gather(const float* Wt, int D, const int64_t* recv, int W, int64_t cap,
+                    uint16_t* out, hipStream_t s);
+void rw_rows_scatter(const int64_t* send, int W, int64_t cap, int B, int D, const uint16_t* rows,
+                     uint16_t* region, int64_t ld, int32_t* map, hipStream_t s);
+void rw_grads_gather(const int32_t* map, int W, int64_t cap, int D, const uint16_t* dregion,
+                     uint16_t* gsend, hipStream_t s);
 // Backward, owner side: keys/positions/gradient offsets of every received
 // entry into the embedding workspace (entry (r, i) reads its gradient row at
 // grad + (r*B + b)*grad_ld + j*D; empty slots update row `dummy_row`, a
 // scratch row the store keeps past its real rows), then the radix sort.
 // embedding_bwd_apply then runs with a.nnz = W*cap, a.segsort = 0.
+// rows = 1 ("rows" exchange): entry (r, i) reads its gradient row at
+// grad + (r*(cap+1) + i)*grad_ld instead.
 void embedding_bwd_prepare_rw(const EmbBwdArgs& a, const int64_t* recv, const int64_t* meta,
                               int nrw, int W, int64_t cap, int64_t grad_ld, int64_t dummy_row,
-                              hipStream_t s);
+                              int rows, hipStream_t s);
 
 // ------------------------------------------------------------ optim ----
 // Flat fused optimizer over one contiguous fp32 parameter buffer.

@@ -879,7 +879,7 @@ __global__ __launch_bounds__(64 * LONG_WAVES) void emb_combine_long_kernel(
 template <typename K>
 __global__ void emb_rw_keys_kernel(const EmbBwdArgs a, const int64_t* __restrict__ recv,
                                    const int64_t* __restrict__ meta, int nrw, int W,
-                                   int64_t cap, int64_t grad_ld, int64_t dummy_row,
+                                   int64_t cap, int64_t grad_ld, int64_t dummy_row, int rows,
                                    K* __restrict__ keys, int32_t* __restrict__ vals,
                                    int64_t* __restrict__ goff, float* __restrict__ gscale,
                                    int32_t* __restrict__ tail_count) {
@@ -903,7 +903,8 @@ __global__ void emb_rw_keys_kernel(const EmbBwdArgs a, const int64_t* __restrict
       const int j = (int)(bk / a.B);
       const int64_t b = bk - (int64_t)j * a.B;
       key = (K)(v & 0xffffffffull);
-      go = ((int64_t)r * a.B + b) * grad_ld + (int64_t)j * a.D;
+      go = rows ? ((int64_t)r * (cap + 1) + i) * grad_ld
+                : ((int64_t)r * a.B + b) * grad_ld + (int64_t)j * a.D;
       if (a.mean) sc = 1.f / (float)L[j];
     }
     keys[p] = key;
@@ -1225,7 +1226,7 @@ void embedding_bwd_prepare(const EmbBwdArgs& a, hipStream_t s) {
 template <typename K>
 void prep_rw_impl(const EmbBwdArgs& a, const WsLayout& L, const int64_t* recv,
                   const int64_t* meta, int nrw, int W, int64_t cap, int64_t grad_ld,
-                  int64_t dummy_row, hipStream_t s) {
+                  int64_t dummy_row, int rows, hipStream_t s) {
   char* ws = (char*)a.workspace;
   K* keys_in = (K*)(ws + L.keys_in);
   K* keys_out = (K*)(ws + L.keys_out);
@@ -1242,7 +1243,7 @@ void prep_rw_impl(const EmbBwdArgs& a, const WsLayout& L, const int64_t* recv,
   int64_t kb = (a.nnz + 255) / 256;
   if (kb > 8192) kb = 8192;
   hipLaunchKernelGGL(emb_rw_keys_kernel<K>, dim3(kb), dim3(256), 0, s, a, recv, meta, nrw, W,
-                     cap, grad_ld, dummy_row, k0, v0, goff, gscale, tcount);
+                     cap, grad_ld, dummy_row, rows, k0, v0, goff, gscale, tcount);
   TDFO_CHECK_HIP(hipGetLastError());
   if constexpr (sizeof(K) == 4)
     radix_sort_pairs_u32(k0, v0, k1, v1, a.nnz, a.key_bits, ws + L.sortws, s);
@@ -1253,13 +1254,13 @@ void prep_rw_impl(const EmbBwdArgs& a, const WsLayout& L, const int64_t* recv,
 
 void embedding_bwd_prepare_rw(const EmbBwdArgs& a, const int64_t* recv, const int64_t* meta,
                               int nrw, int W, int64_t cap, int64_t grad_ld, int64_t dummy_row,
-                              hipStream_t s) {
+                              int rows, hipStream_t s) {
   if (a.nnz <= 0) return;
   const WsLayout L = ws_layout(a.nnz, a.D);
   if (a.key_bits <= 32)
-    prep_rw_impl<uint32_t>(a, L, recv, meta, nrw, W, cap, grad_ld, dummy_row, s);
+    prep_rw_impl<uint32_t>(a, L, recv, meta, nrw, W, cap, grad_ld, dummy_row, rows, s);
   else
-    prep_rw_impl<uint64_t>(a, L, recv, meta, nrw, W, cap, grad_ld, dummy_row, s);
+    prep_rw_impl<uint64_t>(a, L, recv, meta, nrw, W, cap, grad_ld, dummy_row, rows, s);
 }
 
 void embedding_dense_update(const EmbBwdArgs& a, int64_t rows, const float* grad, float* clear,

@@ -89,6 +89,8 @@ class DLRMConfig:
     rw_capacity: float = 1.25                      # initial row-wise segment capacity (x n/W);
     #   grown on demand before any exchange would overflow
     rw_comm: str = "bf16"                          # row-wise reduce-scatter dtype (bf16 | fp32)
+    rw_exchange: str = "auto"                      # row-wise exchange: pooled | rows | auto
+    #   (rows: one-hot tables return looked-up rows by all-to-all, sparse/sharded.py)
     dense_comm: str = "fp32"                       # dense-grad all-reduce dtype (fp32 | bf16:
     #   halves the bytes on xGMI; the sum of W bf16-rounded grads, as DDP's bf16 compress hook)
     pipeline: bool = False                         # W > 1: next batch's id exchange overlaps
@@ -287,7 +289,8 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
                                           pooling=cfg.pooling_factors(), strategy=cfg.sharding)
         self.emb = ShardedEmbeddingBags(tables, self.plan, rank, B, cfg.pooling_factors(), dev,
                                         optim, group=self.comm, seed=cfg.seed,
-                                        rw_capacity=cfg.rw_capacity, rw_comm=cfg.rw_comm)
+                                        rw_capacity=cfg.rw_capacity, rw_comm=cfg.rw_comm,
+                                        rw_exchange=cfg.rw_exchange)
         if self.dcomm is not None:
             self.emb.dp_comm = self.dcomm         # replicated tables' all-reduce beside it
         # ------------------------------------------------------ dense params

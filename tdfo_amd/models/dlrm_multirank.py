@@ -19,16 +19,22 @@ explicit event record / wait nodes into one executable graph
 step instead of ~20 Python stage issues and ~8 c10d calls:
 
   M  (MLP):      [wait dpp'] bottom fwd  [wait c5', d'] top fwd/bwd + interaction bwd
-                 (m2)  bottom bwd, next batch's load from staging + bucketize
-                 of its sharded tables' ids (m4)  top weight grads (m3)
-  D  (dense      [wait c5'] ids-only sort of this batch (e0)  [wait m2]
-      comm):     replicated tables' dense grad + all-reduce + update (dp)
+                 (m2)  [wait stg] bottom bwd, next batch's load from staging
+                 (m4)  top weight grads (m3)
+  D  (dense      [wait c5'] ids-only sort of this batch (e0)  [wait stg] next
+      comm):     batch's sharded-table ids bucketed from the staging, row-wise
+                 need all-reduced + published to the host (pre)  [wait m2]
+                 replicated tables' dense grad + all-reduce + update (dp)
                  [wait m4] bottom-bucket all-reduce, next batch's replicated
                  ids, bottom-bucket optimizer (dpp)  [wait m3] top-bucket
                  all-reduce, top-bucket optimizer (d)
   EC (embedding  [wait m2] gradient all-to-all  [wait e0, dp] fused embedding
-      + its      update  [wait m4, dpp] id all-to-all, lookup + pooled
+      + its      update  [wait pre, dpp] id all-to-all, lookup + pooled
       RCCL):     all-to-all (c5)
+
+(stg: recorded by the host on the current stream after it staged the next
+batch; TDFO_MR_EARLY_PREP=0 moves the bucketize back into M4 and the publish
+into D's bottom-bucket segment.)
 
 (primed events: the previous step's records). The embedding exchanges and
 the dense all-reduces use two communicators so they run concurrently (the
@@ -47,6 +53,14 @@ import torch
 
 from .. import ops
 from ..utils.capture import graph_capture
+
+
+# A/B knob: TDFO_MR_HEAD_WAIT=1 restores the wait for the current stream at
+# the head of M (the staged batch before the bottom forward)
+_HEAD_WAIT = os.environ.get("TDFO_MR_HEAD_WAIT", "0") == "1"
+# A/B knob: TDFO_MR_EARLY_PREP=0 buckets the next batch's sharded ids in M4
+# (from the loaded ids) and publishes the row-wise need in Da, as before
+_EARLY_PREP = os.environ.get("TDFO_MR_EARLY_PREP", "1") != "0"
 
 
 class MultiRankStreamsMixin:
@@ -123,12 +137,28 @@ class MultiRankStreamsMixin:
                 self._m_allreduce_wait()
                 self._s_dense_update()
 
+        early = _EARLY_PREP and not emb.tw_identity
+
         def m4():
             self._s_bottom_bwd()
             self._m_load_next()                 # x0 / labels / ids free: next batch in
             # ... and its sharded tables' ids bucketed for the id exchange
             # (their send buffers' last reader was the previous exchange)
-            emb.stage_fwd_prep(self.ids, dp=False)
+            if not early:
+                emb.stage_fwd_prep(self.ids, dp=False)
+
+        def d_pre():
+            # early prep: the next batch's sharded-table ids bucketed on D
+            # straight from the host staging, as soon as the previous id
+            # exchange (c5') has released the send buffers, and the row-wise
+            # need published right after -- early in the step instead of
+            # after the bottom backward (M4), so the host, which reads it
+            # before it issues the next step, is not held until mid-step
+            emb.stage_fwd_prep(self._stg[1], dp=False)
+            if emb.rw_tables:
+                emb._rw_ids = self.ids          # a redo re-reads the batch from ids (M4 loads it)
+            if self._rw_lagged:
+                emb.rw_publish_need(self.dcomm)
 
         def d_prep():                           # the replicated tables' ids, once their
             emb.stage_fwd_prep(self.ids, sharded=False)   # dense grad (Dp) has read them
@@ -143,7 +173,7 @@ class MultiRankStreamsMixin:
             # the next batch's all-reduced row-wise need to the host mailbox
             # first (the host reads it when it issues the next step), then the
             # bottom bucket and the replicated tables' ids
-            if self._rw_lagged:
+            if self._rw_lagged and not early:
                 emb.rw_publish_need(self.dcomm)
             self._m_allreduce_start()
             d_prep()
@@ -158,7 +188,7 @@ class MultiRankStreamsMixin:
 
         return {"M1": self._s_bottom_fwd, "M2": m2, "M4": m4,
                 "M3": self._s_top_wgrad if self._defer_top_wgrad else None,
-                "D0": emb.stage_bwd_prepare, "Dp": dp_a,
+                "D0": emb.stage_bwd_prepare, "Dpre": d_pre if early else None, "Dp": dp_a,
                 "Da": d_a,
                 "Db": d_b, "EC1": lambda: emb.backward_start(dp=False),
                 "ECub": lambda: (ec_upd(), ec_b())}
@@ -176,9 +206,11 @@ class MultiRankStreamsMixin:
         # (default priority: a high-priority M and/or EC stream ran the
         # emulated W=8 step at 1.93-2.26 vs 0.63-0.64 ms)
         streams = {k: torch.cuda.Stream(device=dev) for k in ("M", "D", "EC")}
-        ev = {k: ops.SyncEvent(2) for k in ("d", "c5", "m2", "m3", "m4", "e0", "dp", "dpp")}
+        ev = {k: ops.SyncEvent(2) for k in ("d", "c5", "m2", "m3", "m4", "e0", "dp", "dpp",
+                                            "stg", "pre")}
         seg = self._mr_segments()
         dp_dense = bool(self.emb.dp_tables) and self.emb.dp_dense
+        early = _EARLY_PREP and not self.emb.tw_identity       # (as in _mr_segments)
         home = lambda name: "EC" if name.startswith("EC") else name[0]  # noqa: E731
         pool = torch.cuda.graph_pool_handle()
         graphs = {}
@@ -241,15 +273,22 @@ class MultiRankStreamsMixin:
             # M: the bottom backward (+ the next batch's load into x0 / ids /
             # labels, all of whose readers have run) before the top weight
             # grads, so the embedding side and the bottom bucket go sooner
+            # (the host-staged next batch is waited for right before M4, its
+            # only reader: the bottom forward does not wait for the host's
+            # generator launch and staging copy, see _mr_step)
             "M": chain([("wait", "dpp" if split_opt else "d"), ("graph", "M1"), ("wait", "c5"),
-                        ("wait", "d"), ("graph", "M2"), ("record", "m2"), ("graph", "M4"),
-                        ("record", "m4"), ("graph", "M3"), ("record", "m3")]),
+                        ("wait", "d"), ("graph", "M2"), ("record", "m2"), ("wait", "stg"),
+                        ("graph", "M4"), ("record", "m4"), ("graph", "M3"), ("record", "m3")]),
             # D: the ids-only sort of this batch (its ids arrived with the
             # previous step's exchanges), the replicated tables' dense grad +
             # all-reduce, the two dense buckets and the dense optimizer
-            "D": chain([("wait", "c5"), ("graph", "D0"), ("record", "e0"), ("wait", "m2"),
-                        ("graph", "Dp"), ("record", "dp"), ("wait", "m4"), ("graph", "Da"),
-                        ("record", "dpp"), ("wait", "m3"), ("graph", "Db"), ("record", "d")]),
+            # (early prep: the next batch's sharded ids from the staging
+            # right after the sort, Dpre)
+            "D": chain([("wait", "c5"), ("graph", "D0"), ("record", "e0")]
+                       + ([("wait", "stg"), ("graph", "Dpre"), ("record", "pre")] if early else [])
+                       + [("wait", "m2"),
+                          ("graph", "Dp"), ("record", "dp"), ("wait", "m4"), ("graph", "Da"),
+                          ("record", "dpp"), ("wait", "m3"), ("graph", "Db"), ("record", "d")]),
             # EC: gradient all-to-all, fused embedding update, then the next
             # batch's bucketize, id all-to-all, lookup and pooled all-to-all
             # (the m4 wait sits before the update, not between it and the
@@ -257,7 +296,8 @@ class MultiRankStreamsMixin:
             # costs ~14 us of queue idle, scripts/mr_timeline.py; with a
             # dense replicated-table update D also looks those tables up, so
             # EC waits for none of D's replicated-table work)
-            "EC": (chain([("wait", "m2"), ("graph", "EC1"), ("wait", "e0"), ("wait", "m4"),
+            "EC": (chain([("wait", "m2"), ("graph", "EC1"), ("wait", "e0"),
+                          ("wait", "pre" if early else "m4"),
                           ("graph", "ECub"), ("record", "c5")]) if dp_dense else
                    chain([("wait", "m2"), ("graph", "EC1"), ("wait", "e0"), ("wait", "dp"),
                           ("wait", "m4"), ("wait", "dpp"), ("graph", "ECub"),
@@ -265,7 +305,8 @@ class MultiRankStreamsMixin:
         }
         ops.upload_graphs(composed.values())
         self._mr = {"streams": streams, "events": ev, "graphs": graphs, "composed": composed,
-                    "launched": False, "names": names}
+                    "launched": False, "names": names, "full_wait": True,
+                    "early": early}
         # the capture ran nothing: the batch handed in before it is the one
         # the first replay loads
         if restage and self._next is not None:
@@ -282,6 +323,8 @@ class MultiRankStreamsMixin:
         cur = torch.cuda.current_stream()
         if self._mr["launched"]:
             self._mr["events"]["m4"].wait(cur)
+            if self._mr["early"]:
+                self._mr["events"]["pre"].wait(cur)     # D's early prep read it too
         sx, si, sl = self._stg
         ops.batch_load(dense, sx, ids, si, label, sl)
 
@@ -291,10 +334,20 @@ class MultiRankStreamsMixin:
         mr = self._mr
         s, g = mr["streams"], mr["composed"]
         cur = torch.cuda.current_stream()
-        # M loads the staging this thread just wrote on the current stream;
-        # on the first replay every stream starts behind the eager steps
-        for k in (("M", "D", "EC") if not mr["launched"] else ("M",)):
-            s[k].wait_stream(cur)
+        # M4 loads the staging this thread just wrote on the current stream:
+        # an event recorded there, waited for inside M right before M4. Only
+        # after a host-side reader / writer (sync_streams(), e.g. a state
+        # load on the current stream) or on the first replay do the streams
+        # wait for everything on the current stream before the step starts.
+        # (Before: M waited at its head, so the bottom forward waited for the
+        # host's generator launch and staging copy, which the host issues
+        # only after the previous step's mailbox read -- emulated W=8: the
+        # MLP queue idled ~270 us/step, profiles/r05/w8/step_lanes_before.txt)
+        mr["events"]["stg"].record(cur)
+        if mr["full_wait"] or not mr["launched"] or _HEAD_WAIT:
+            for k in (("M", "D", "EC") if not mr["launched"] else ("M",)):
+                s[k].wait_stream(cur)
+            mr["full_wait"] = False
         # launch order M, D, EC: a wait node binds to the latest record
         # enqueued before its graph's launch (see the module docstring)
         for k in ("M", "D", "EC"):
@@ -315,3 +368,4 @@ class MultiRankStreamsMixin:
         cur = torch.cuda.current_stream()
         for st in self._mr["streams"].values():
             cur.wait_stream(st)
+        self._mr["full_wait"] = True          # the caller may write on ``cur`` next

@@ -220,6 +220,11 @@ class StreamGraphsMixin:
         composed = self._ms["composed"]
         # (this step's ids were copied on the embedding side by load_batch, so
         # the lookup follows the previous step's embedding update there)
+        # (Measured, round 5: replaying the next lookup before this update --
+        # inexact, a bound on what an early lookup + stale-bag fix could
+        # gain -- ran DCN-v2 at 2.40-2.42 vs 2.36-2.38 ms/step: the update and
+        # lookup are HBM-bound and slow the GEMMs they overlap about as much
+        # as they save, profiles/r05/notes.md)
         with torch.cuda.stream(se):
             if composed:
                 g["EA"].replay()             # records ev[1] inside

@@ -409,25 +409,53 @@ def rw_pool(Wt, recv, meta, nrw, W, B, cap, mean, starts, out, out_ld):
 
 
 def embedding_bwd_prepare_rw(Wt, recv, meta, nrw, W, B, cap, mean, key_bits, grad_ld, dummy_row,
-                             workspace):
+                             workspace, rows=False):
     """GPU: keys + sort of the received row-wise entries (ids only). CPU: no-op
-    (``embedding_bwd_apply_rw`` does everything)."""
+    (``embedding_bwd_apply_rw`` does everything). ``rows``: the gradients
+    arrive per slot ([W][cap + 1][grad_ld], the "rows" exchange)."""
     if _gpu(Wt):
         _native().embedding_bwd_prepare_rw(Wt, recv, meta, int(nrw), int(W), int(B), int(cap),
                                            bool(mean), int(key_bits), int(grad_ld),
-                                           int(dummy_row), workspace)
+                                           int(dummy_row), workspace, int(bool(rows)))
 
 
 def embedding_bwd_apply_rw(Wt, recv, meta, nrw, W, B, cap, mean, key_bits, grad, grad_ld, opt,
                            hyper, workspace, state1=None, state2=None, eps=1e-8, beta1=0.9,
-                           beta2=0.999, weight_decay=0.0):
+                           beta2=0.999, weight_decay=0.0, rows=False):
     if _gpu(Wt):
         _native().embedding_bwd_apply_rw(Wt, int(W), int(B), int(cap), bool(mean), int(key_bits),
                                          grad, int(opt), state1, state2, hyper, eps, beta1, beta2,
                                          weight_decay, workspace)
     else:
         ref.rw_embedding_bwd(Wt, recv, meta, nrw, W, B, cap, mean, grad, grad_ld, opt, state1,
-                             state2, hyper, eps, beta1, beta2, weight_decay)
+                             state2, hyper, eps, beta1, beta2, weight_decay, rows=rows)
+
+
+def rw_rows_gather(Wt, recv, W, cap, out):
+    """One-hot row-wise "rows" exchange, owner side: bf16 row per received
+    entry into ``out`` [W][cap + 1][D] (csrc/kernels/rowwise.hip)."""
+    if _gpu(Wt):
+        _native().rw_rows_gather(Wt, recv, int(W), int(cap), out)
+    else:
+        ref.rw_rows_gather(Wt, recv, W, cap, out)
+
+
+def rw_rows_scatter(send, W, cap, B, D, rows, region, ld, smap, nrw):
+    """Requester side: received rows into the pooled region (row stride
+    ``ld``) and the slot -> offset map the backward gathers with."""
+    if _gpu(send):
+        _native().rw_rows_scatter(send, int(W), int(cap), int(B), int(D), rows, region, int(ld),
+                                  smap, int(nrw))
+    else:
+        ref.rw_rows_scatter(send, W, cap, B, D, rows, region, ld, smap, nrw)
+
+
+def rw_grads_gather(smap, W, cap, D, dregion, gsend):
+    """Requester side of the backward: each slot's gradient row, [W][cap + 1][D]."""
+    if _gpu(smap):
+        _native().rw_grads_gather(smap, int(W), int(cap), int(D), dregion, gsend)
+    else:
+        ref.rw_grads_gather(smap, W, cap, D, dregion, gsend)
 
 
 def dense_optimizer(p, g, m, v, p_bf16, opt, hyper, beta1=0.9, beta2=0.999, eps=1e-8, wd=0.0,

@@ -238,17 +238,65 @@ def rw_bucketize(ids, meta, nrw, W, B, cap, n, send, overflow):
         overflow.view(-1)[1] = most
 
 
-def _rw_entries(recv, meta, nrw, W, B, cap):
-    """(requester, bag key, row key) of every valid received entry."""
+def _rw_entries(recv, meta, nrw, W, B, cap, slots=False):
+    """(requester, bag key, row key) of every valid received entry (and its
+    slot index in the requester's segment with ``slots``)."""
     seg = recv.view(W, cap + 1)
-    rs, keys, rows = [], [], []
+    rs, keys, rows, idx = [], [], [], []
     for r in range(W):
         c = int(seg[r, cap])
         v = seg[r, :c]
         rs.append(torch.full((c,), r, dtype=torch.int64, device=recv.device))
         keys.append(v >> 32)
         rows.append(v & 0xFFFFFFFF)
+        idx.append(torch.arange(c, device=recv.device))
+    if slots:
+        return torch.cat(rs), torch.cat(keys), torch.cat(rows), torch.cat(idx)
     return torch.cat(rs), torch.cat(keys), torch.cat(rows)
+
+
+def rw_rows_gather(Wt, recv, W, cap, out):
+    """Reference of rw_rows_gather (rowwise.hip): the owner's row per received
+    entry, [W][cap + 1][D] (slots past a segment's count untouched)."""
+    D = Wt.shape[1]
+    seg = recv.view(W, cap + 1)
+    o = out.view(-1)[: W * (cap + 1) * D].view(W, cap + 1, D)
+    for r in range(W):
+        c = min(int(seg[r, cap]), cap)
+        if c:
+            o[r, :c] = Wt[seg[r, :c] & 0xFFFFFFFF].to(out.dtype)
+
+
+def rw_rows_scatter(send, W, cap, B, D, rows, region, ld, smap, nrw):
+    """Reference of rw_rows_scatter: each of this requester's slots (o, i)
+    writes its received row to its bag's column block and its offset to the
+    slot map (count in slot cap)."""
+    seg = send.view(W, cap + 1)
+    R = rows.view(-1)[: W * (cap + 1) * D].view(W, cap + 1, D)
+    m = smap.view(-1)[: W * (cap + 1)].view(W, cap + 1)
+    reg = region.view(-1)
+    ar = torch.arange(D, device=send.device)
+    for o in range(W):
+        c = min(int(seg[o, cap]), cap)
+        m[o, cap] = c
+        if c:
+            k = seg[o, :c] >> 32
+            off = (k % B) * ld + (k // B) * D
+            m[o, :c] = off.to(torch.int32)
+            reg[(off[:, None] + ar).reshape(-1)] = R[o, :c].reshape(-1).to(reg.dtype)
+
+
+def rw_grads_gather(smap, W, cap, D, dregion, gsend):
+    """Reference of rw_grads_gather: gradient rows of the slots in the map."""
+    m = smap.view(-1)[: W * (cap + 1)].view(W, cap + 1)
+    G = gsend.view(-1)[: W * (cap + 1) * D].view(W, cap + 1, D)
+    reg = dregion.reshape(-1)
+    ar = torch.arange(D, device=smap.device)
+    for o in range(W):
+        c = int(m[o, cap])
+        if c:
+            off = m[o, :c].long()
+            G[o, :c] = reg[(off[:, None] + ar).reshape(-1)].view(c, D).to(G.dtype)
 
 
 def rw_pool(Wt, recv, meta, nrw, W, B, cap, mean, out, out_ld):
@@ -266,17 +314,18 @@ def rw_pool(Wt, recv, meta, nrw, W, B, cap, mean, out, out_ld):
 
 
 def rw_embedding_bwd(Wt, recv, meta, nrw, W, B, cap, mean, grad, grad_ld, opt, state1, state2,
-                     hyper, eps, beta1, beta2, weight_decay):
+                     hyper, eps, beta1, beta2, weight_decay, rows=False):
     """Owner-side fused backward of the row-wise exchange: every received
-    entry (r, (j, b), row) takes gradient row grad[(r*B + b)*grad_ld + j*D:]."""
+    entry (r, (j, b), row) takes gradient row grad[(r*B + b)*grad_ld + j*D:]
+    (``rows``: the row of its slot, grad[(r*(cap + 1) + i)*grad_ld:])."""
     D = Wt.shape[1]
     _, L, _, _, _ = rw_unpack_meta(meta, nrw)
-    r, k, row = _rw_entries(recv, meta, nrw, W, B, cap)
+    r, k, row, i = _rw_entries(recv, meta, nrw, W, B, cap, slots=True)
     n = int(row.numel())
     if n == 0:
         return
     j, b = k // B, k % B
-    base = (r * B + b) * grad_ld + j * D
+    base = (r * (cap + 1) + i) * grad_ld if rows else (r * B + b) * grad_ld + j * D
     g = grad.reshape(-1)[(base[:, None] + torch.arange(D, device=Wt.device)).reshape(-1)]
     g = g.float().view(n, D).contiguous()
     psw = (1.0 / L[j].float()) if mean else None

@@ -35,6 +35,8 @@ Design (MI355X-first):
 """
 from __future__ import annotations
 
+import os
+
 from typing import List, Optional, Sequence
 
 import torch
@@ -59,7 +61,7 @@ class ShardedEmbeddingBags:
                  batch_size: int, pooling: Sequence[int], device, optim: EmbOptimConfig,
                  group=None, seed: int = 0, mean: bool = False, rw_capacity: float = 1.25,
                  rw_comm: str = "bf16", dp_dense_max_bytes: int = 256 << 20,
-                 recv_dtype: str = "bf16"):
+                 recv_dtype: str = "bf16", rw_exchange: str = "auto"):
         """``rw_capacity``: initial per-owner segment capacity of the row-wise
         exchange as a multiple of the uniform share n/W (+256). Before every
         exchange the largest per-owner count is all-reduced and the capacity
@@ -68,6 +70,13 @@ class ShardedEmbeddingBags:
         ``rw_comm``: dtype of the pooled partials' reduce-scatter ("bf16"
         halves the bytes; "fp32" sums exactly as one process would, up to
         fp32 association).
+        ``rw_exchange``: "pooled" (the owner pools per requester bag, bf16
+        reduce-scatter forward, all-gather of the pooled gradients backward),
+        "rows" (one id per bag only: each looked-up row travels back in the
+        id exchange's [W][cap + 1] layout and each gradient row to its owner,
+        both by all-to-all -- ~W / 1.25 x fewer bytes, the same values) or
+        "auto" (rows when every row-wise table is one-hot and the pooled rows
+        are bf16).
         ``recv_dtype``: dtype of the pooled rows handed to the model and of
         their gradients, on the wire too ("bf16": the DLRM path; "fp32": fp32
         models whose embeddings must not be rounded -- the reference's TBE
@@ -216,6 +225,7 @@ class ShardedEmbeddingBags:
         # owner and summed by a bf16 reduce-scatter; the backward all-gathers
         # the pooled gradients and runs the fused sort-based update on the
         # received entries. Static shapes: hipGraph-capturable, no host sync.
+        self.rw_rows = False
         self.rw_tables = [s.table for s in plan.shards if s.kind == "row_wise"]
         self.rw_col = {t: j * D for j, t in enumerate(self.rw_tables)}
         self.rw_width = len(self.rw_tables) * D
@@ -243,6 +253,14 @@ class ShardedEmbeddingBags:
                     + list(self.rw_store.row_offset_host) + cum)
             self.rw_meta = torch.tensor(meta, dtype=torch.int64, device=self.device)
             self.rw_cap_factor = float(rw_capacity)
+            if rw_exchange not in ("auto", "pooled", "rows"):
+                raise ValueError(f"rw_exchange must be auto, pooled or rows, got {rw_exchange!r}")
+            onehot_rw = all(l_ == 1 for l_ in Ls)
+            if rw_exchange == "rows" and not (onehot_rw and bf == torch.bfloat16):
+                raise ValueError("rw_exchange='rows' needs one id per bag in every row-wise "
+                                 "table and bf16 pooled rows")
+            self.rw_rows = (W > 1 and onehot_rw and bf == torch.bfloat16
+                            and rw_exchange != "pooled")
             from .. import ops as _ops
             self.rw_ws = torch.empty(_ops.rw_bucketize_workspace(n, W), dtype=torch.uint8,
                                      device=self.device)
@@ -257,13 +275,15 @@ class ShardedEmbeddingBags:
             if rw_comm not in ("bf16", "fp32"):
                 raise ValueError(f"rw_comm must be bf16 or fp32, got {rw_comm}")
             cdt = bf_ if rw_comm == "bf16" else torch.float32
+            pooled_x = W > 1 and not self.rw_rows
             self.rw_pbuf = (torch.zeros(W * B * self.rw_width, dtype=cdt, device=self.device)
-                            if W > 1 else None)
+                            if pooled_x else None)
             # fp32 partials are reduced into an fp32 landing buffer, then cast
             self.rw_rs32 = (torch.zeros(B * self.rw_width, dtype=cdt, device=self.device)
-                            if W > 1 and cdt == torch.float32 and bf != torch.float32 else None)
+                            if pooled_x and cdt == torch.float32 and bf != torch.float32 else None)
             self.rw_gbuf = (torch.zeros(W * B * self.rw_width, dtype=bf_, device=self.device)
-                            if W > 1 else None)
+                            if pooled_x else None)
+            self._rw_scatter_pending = False
             self._rw_alloc(self.rw_capacity(n, W, rw_capacity))
             self._rw_prepared = False
         # ---- data-parallel (replicated) group: local lookup, gradient
@@ -430,6 +450,14 @@ class ShardedEmbeddingBags:
         self.rw_send = torch.zeros(W * (cap + 1), dtype=torch.int64, device=self.device)
         self.rw_recv = torch.zeros_like(self.rw_send) if W > 1 else self.rw_send
         self.rw_bwd_ws = None
+        if getattr(self, "rw_rows", False):
+            # "rows" exchange: owner rows out / requester rows in, requester
+            # gradient rows out / owner gradient rows in, the slot map
+            n = W * (cap + 1)
+            mk = lambda: torch.zeros(n * D, dtype=torch.bfloat16, device=self.device)  # noqa: E731
+            self.rw_rows_out, self.rw_rows_in = mk(), mk()
+            self.rw_gsend, self.rw_grecv = mk(), mk()
+            self.rw_smap = torch.zeros(n, dtype=torch.int32, device=self.device)
         if self.device.type == "cuda":
             from .. import ops as _ops
             self.rw_bwd_ws = torch.empty(_ops.embedding_bwd_workspace(W * cap, D),
@@ -501,6 +529,11 @@ class ShardedEmbeddingBags:
         if not self._rw_lag_pending:
             return False
         self._rw_lag_pending = False
+        if os.environ.get("TDFO_DIAG_SKIP_RW_READ") == "1":
+            # diagnostics only (host never waits for the need: measures what
+            # the lagged read costs; an overflow would then raise at the next
+            # check_overflow instead of being redone)
+            return False
         need = self._rw_mailbox().read()
         self.rw_lag_reads += 1
         if need <= self.rw_cap:
@@ -527,6 +560,11 @@ class ShardedEmbeddingBags:
         self._rw_bucketize(self._rw_ids)
         if W > 1:
             self.comm.all_to_all(self.rw_recv, self.rw_send)
+        if self.rw_rows:
+            ops.rw_rows_gather(self.rw_store.weight, self.rw_recv, W, self.rw_cap, self.rw_rows_out)
+            self.comm.all_to_all(self.rw_rows_in, self.rw_rows_out)
+            self._rw_scatter()
+            return
         out = self.rw_pbuf if W > 1 else self._rw_region(self.recv)
         ops.rw_pool(self.rw_store.weight, self.rw_recv, self.rw_meta, self.nrw, W, self.B,
                     self.rw_cap, self.mean, self.rw_starts, out, self.rw_width)
@@ -535,6 +573,14 @@ class ShardedEmbeddingBags:
             self.comm.reduce_scatter(dst, self.rw_pbuf)
             if self.rw_rs32 is not None:
                 ops.cast_bf16(self.rw_rs32, self._rw_region(self.recv))
+
+    def _rw_scatter(self):
+        """"rows" exchange: the received rows into this batch's row-wise
+        slots of ``recv`` (and the slot map the backward gathers with)."""
+        from .. import ops
+        self._rw_scatter_pending = False
+        ops.rw_rows_scatter(self.rw_send, self.world, self.rw_cap, self.B, self.D, self.rw_rows_in,
+                            self._rw_region(self.recv), self.rw_width, self.rw_smap, self.nrw)
 
     def _rw_region(self, buf):
         base = sum(self.tw_recv_sizes)
@@ -672,6 +718,10 @@ class ShardedEmbeddingBags:
                                   self.cw_v_out_off, self.dsum[self.rank], mean=self.mean)
         if self.rw_tables:
             from .. import ops
+            if self.rw_rows:
+                ops.rw_rows_gather(self.rw_store.weight, self.rw_recv, W, self.rw_cap,
+                                   self.rw_rows_out)
+                return
             out = self.rw_pbuf if W > 1 else self._rw_region(self.recv)
             ops.rw_pool(self.rw_store.weight, self.rw_recv, self.rw_meta, self.nrw, W, B,
                         self.rw_cap, self.mean, self.rw_starts, out, self.rw_width)
@@ -686,7 +736,15 @@ class ShardedEmbeddingBags:
                                                   self.tw_pooled[: W * B * self.dsum[self.rank]],
                                                   self.tw_recv_sizes,
                                                   [B * self.dsum[self.rank]] * W, async_op=True))
-            if self.rw_tables:
+            if self.rw_tables and self.rw_rows:
+                works.append(self.comm.all_to_all(self.rw_rows_in, self.rw_rows_out,
+                                                  async_op=True))
+                # a stream-ordered communicator (native RCCL, loopback): the
+                # scatter follows on the same stream; else after the wait
+                self._rw_scatter_pending = True
+                if getattr(self.comm, "capturable", False):
+                    self._rw_scatter()
+            elif self.rw_tables:
                 dst = self.rw_rs32 if self.rw_rs32 is not None else self._rw_region(self.recv)
                 works.append(self.comm.reduce_scatter(dst, self.rw_pbuf, async_op=True))
         self._pending = works
@@ -695,6 +753,8 @@ class ShardedEmbeddingBags:
         for w in self._pending or ():
             w.wait()
         self._pending = None
+        if self.rw_tables and self.rw_rows and self._rw_scatter_pending:
+            self._rw_scatter()
         if self.cw_tables:
             self._cw_assemble(self.recv)
         if self.rw_tables and self.rw_rs32 is not None:
@@ -752,7 +812,12 @@ class ShardedEmbeddingBags:
                                         d_recv[:tw_total], [B * self.dsum[self.rank]] * W,
                                         self.tw_recv_sizes, async_op=True)
         self._rw_work = None
-        if W > 1 and self.rw_tables:
+        if W > 1 and self.rw_tables and self.rw_rows:
+            from .. import ops
+            ops.rw_grads_gather(self.rw_smap, W, self.rw_cap, self.D, self._rw_region(d_recv),
+                                self.rw_gsend)
+            self._rw_work = self.comm.all_to_all(self.rw_grecv, self.rw_gsend, async_op=True)
+        elif W > 1 and self.rw_tables:
             self._rw_work = self.comm.all_gather(self.rw_gbuf, self._rw_region(d_recv),
                                                  async_op=True)
         self._bw = (work, d_recv)
@@ -795,8 +860,9 @@ class ShardedEmbeddingBags:
         from .. import ops
         st = self.rw_store
         ops.embedding_bwd_prepare_rw(st.weight, self.rw_recv, self.rw_meta, self.nrw, self.world,
-                                     self.B, self.rw_cap, self.mean, st.key_bits, self.rw_width,
-                                     self.rw_dummy, self.rw_bwd_ws)
+                                     self.B, self.rw_cap, self.mean, st.key_bits,
+                                     self.D if self.rw_rows else self.rw_width,
+                                     self.rw_dummy, self.rw_bwd_ws, rows=self.rw_rows)
         self._rw_prepared = True
 
     def stage_bwd_update(self, hyper: torch.Tensor, sharded: bool = True, dp: bool = True):
@@ -838,12 +904,15 @@ class ShardedEmbeddingBags:
             if not self._rw_prepared:
                 self._rw_prepare()
             st, o = self.rw_store, self.optim
-            grad = self.rw_gbuf if W > 1 else self._rw_region(d_recv)
+            if self.rw_rows:
+                grad, gld = self.rw_grecv, self.D
+            else:
+                grad, gld = (self.rw_gbuf if W > 1 else self._rw_region(d_recv)), self.rw_width
             ops.embedding_bwd_apply_rw(st.weight, self.rw_recv, self.rw_meta, self.nrw, W, B,
-                                       self.rw_cap, self.mean, st.key_bits, grad, self.rw_width,
+                                       self.rw_cap, self.mean, st.key_bits, grad, gld,
                                        o.code, hyper, self.rw_bwd_ws, state1=st.state1,
                                        state2=st.state2, eps=o.eps, beta1=o.beta1, beta2=o.beta2,
-                                       weight_decay=o.weight_decay)
+                                       weight_decay=o.weight_decay, rows=self.rw_rows)
             self._rw_prepared = False
 
     def backward_finish(self, hyper: torch.Tensor):

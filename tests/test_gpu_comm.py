@@ -98,12 +98,16 @@ def test_rccl_comm_one_rank_ops_eager_and_captured():
 
 
 def _trainer(whole: bool, W: int, strategy: str):
+    """strategy "row_wise_onehot": row-wise with one id per bag (the "rows"
+    exchange: rows back by all-to-all, scatter on the exchange stream)."""
     from tdfo_amd.models.dlrm import DLRMConfig, DLRMTrainer
     from tdfo_amd.parallel.comm import LoopbackComm
 
     rows = [5000, 7, 30000, 1000, 3, 800, 64, 129]
+    onehot = strategy == "row_wise_onehot"
     cfg = DLRMConfig(embedding_dim=64, table_rows=rows, bottom=[128, 64], top=[128, 64, 1],
-                     sharding=strategy, pipeline=True, pooling=[1, 2, 1, 3, 1, 1, 1, 1],
+                     sharding="row_wise" if onehot else strategy, pipeline=True,
+                     pooling=[1] * 8 if onehot else [1, 2, 1, 3, 1, 1, 1, 1],
                      stream_graphs=whole, seed=3)
     dev = torch.device("cuda", 0)
     comm = LoopbackComm(W, 0, dev)
@@ -113,7 +117,8 @@ def _trainer(whole: bool, W: int, strategy: str):
 
 @pytest.mark.parametrize("strategy,skew", [("table_wise", False), ("auto", False),
                                            ("column_wise", False), ("data_parallel", False),
-                                           ("row_wise", False), ("row_wise", True)])
+                                           ("row_wise", False), ("row_wise", True),
+                                           ("row_wise_onehot", False), ("row_wise_onehot", True)])
 def test_stream_graphs_match_staged(strategy, skew):
     """Row-wise tables run on the stream graphs with the lagged capacity
     check; ``skew``: the batches after the capture carry only ids that are
@@ -140,9 +145,10 @@ def test_stream_graphs_match_staged(strategy, skew):
             tr.step()
         torch.cuda.synchronize()
         assert (tr.graph == "mstreams") == whole, tr.graph      # (still, after any growth)
-        if strategy == "row_wise":
+        if strategy.startswith("row_wise"):
             assert tr.emb.rw_lag_reads >= 6
             assert (tr.emb.rw_grows > 0) == skew, tr.emb.rw_grows
+            assert tr.emb.rw_rows == (strategy == "row_wise_onehot")
         loss = tr.pop_loss()
         tr.drain()
         torch.cuda.synchronize()

@@ -20,7 +20,8 @@ STEPS = 3
 
 
 def _worker(rank, world, Bk, strategy, graph, rw_comm, emb_opt="rowwise_adagrad", pipeline=False,
-            dist="uniform", alpha=1.05, rw_capacity=1.25, pipe_lookup=True, predict_skew=False):
+            dist="uniform", alpha=1.05, rw_capacity=1.25, pipe_lookup=True, predict_skew=False,
+            pool=POOL, rw_exchange="auto"):
     """dist="zipf": the two eager steps see uniform ids, the graph-replayed
     ones power-law ids -- the row-wise capacity then has to grow after the
     capture (eager rest of that step, re-capture). predict_skew: between two
@@ -33,20 +34,20 @@ def _worker(rank, world, Bk, strategy, graph, rw_comm, emb_opt="rowwise_adagrad"
     dev = get_info().device if world > 1 else torch.device("cuda", 0)
     cfg = DLRMConfig(embedding_dim=64, table_rows=ROWS, bottom=[128, 64], top=[128, 64, 1],
                      dense_opt="sgd", dense_lr=0.05, emb_lr=0.05, sharding=strategy,
-                     pooling=POOL, rw_comm=rw_comm, emb_opt=emb_opt, pipeline=pipeline,
-                     rw_capacity=rw_capacity, pipeline_lookup=pipe_lookup)
+                     pooling=list(pool), rw_comm=rw_comm, emb_opt=emb_opt, pipeline=pipeline,
+                     rw_capacity=rw_capacity, pipeline_lookup=pipe_lookup, rw_exchange=rw_exchange)
     tr = DLRMTrainer(cfg, Bk, dev, group=get_info().group, rank=rank, world_size=world)
     g = torch.Generator().manual_seed(5)
     for t, r in enumerate(ROWS):
         tr.emb.set_table_weight(t, torch.randn(r, 64, generator=g) * 0.1)
-    data = SyntheticCriteo(ROWS, B * 2, pooling=POOL, device="cpu", seed=9)
-    skew = SyntheticCriteo(ROWS, B * 2, pooling=POOL, device="cpu", seed=9, stream=1, dist=dist,
-                           zipf_alpha=alpha)
+    data = SyntheticCriteo(ROWS, B * 2, pooling=list(pool), device="cpu", seed=9)
+    skew = SyntheticCriteo(ROWS, B * 2, pooling=list(pool), device="cpu", seed=9, stream=1,
+                           dist=dist, zipf_alpha=alpha)
     batches = []
     for i in range(STEPS + 3):
         dense, ids, label = (data if i < 2 else skew).next()
         parts, off = [], 0
-        for t, Lt in enumerate(POOL):
+        for t, Lt in enumerate(pool):
             n = B * 2 * Lt
             v = ids[off:off + n].view(B * 2, Lt)
             parts.append(v[rank * Bk:(rank + 1) * Bk].reshape(-1))
@@ -87,6 +88,8 @@ def _worker(rank, world, Bk, strategy, graph, rw_comm, emb_opt="rowwise_adagrad"
             tabs[t] = ((r[0].start, r[0].stop, r[0].step), tr.emb.table_cols(t)[0],
                        r[1].detach().cpu().clone())
     grows = tr.emb.rw_grows if tr.emb.rw_tables else 0
+    if rw_exchange != "auto" and tr.emb.rw_tables:
+        assert tr.emb.rw_rows == (rw_exchange == "rows")
     return tr.fp.p.detach().cpu().clone(), tabs, loss, grows
 
 
@@ -201,3 +204,23 @@ def test_row_wise_growth_in_predict_between_replays(single):
                             "uniform", 1.05, 1.25, True, True, device="cuda", timeout=600)
     assert all(m[3] > 0 for m in multi)
     _check(multi, single("rowwise_adagrad"), 3e-3)
+
+
+@pytest.mark.parametrize("world,pipeline,dist", [(2, False, "uniform"), (4, True, "uniform"),
+                                                 (2, False, "zipf")])
+def test_row_wise_rows_exchange_matches_pooled(world, pipeline, dist):
+    """One-hot row-wise tables on the real kernels: the "rows" exchange (the
+    owner's bf16 rows back by all-to-all, gradient rows to the owner) equals
+    the pooled reduce-scatter / all-gather exchange bit for bit -- staged
+    hipGraphs, pipelined input dist, and (zipf) capacity growth after the
+    capture with the eager redo of that step."""
+    pool = [1] * len(ROWS)
+    args = (world, 2 * B // world, "row_wise", True, "fp32", "rowwise_adagrad", pipeline, dist,
+            1.2, 0.3 if dist == "zipf" else 1.25, True, False, pool)
+    pooled = run_distributed(_worker, *args, "pooled", device="cuda", timeout=600)
+    rows = run_distributed(_worker, *args, "rows", device="cuda", timeout=600)
+    for rank in range(world):
+        assert torch.equal(pooled[rank][0], rows[rank][0]), rank
+        assert pooled[rank][2] == rows[rank][2], rank
+        for t in pooled[rank][1]:
+            assert torch.equal(pooled[rank][1][t][2], rows[rank][1][t][2]), (rank, t)

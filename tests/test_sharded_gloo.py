@@ -99,7 +99,7 @@ def test_sharded_embedding_fwd_bwd(strategy, world, dp_dense):
 
 def _dlrm_worker(rank, world, B, steps, strategy, emb_opt="rowwise_adagrad", rw_comm="fp32",
                  pipeline=False, dense_comm="fp32", dist="uniform", alpha=1.05, rw_capacity=1.25,
-                 pipe_lookup=True, skew_from=None):
+                 pipe_lookup=True, skew_from=None, pooling=(1, 2, 1, 1, 1), rw_exchange="auto"):
     """skew_from: batches from this index on carry only even ids (every
     row-wise id of a 2-rank job then goes to owner 0)."""
     from tdfo_amd.data.synthetic import SyntheticCriteo
@@ -107,11 +107,13 @@ def _dlrm_worker(rank, world, B, steps, strategy, emb_opt="rowwise_adagrad", rw_
     from tdfo_amd.parallel.dist import get_info
 
     cfg = DLRMConfig(embedding_dim=32, table_rows=ROWS, bottom=[64, 32], top=[64, 32, 1],
-                     dense_lr=1e-2, emb_lr=0.05, sharding=strategy, pooling=[1, 2, 1, 1, 1],
+                     dense_lr=1e-2, emb_lr=0.05, sharding=strategy, pooling=list(pooling),
                      emb_opt=emb_opt, rw_comm=rw_comm, pipeline=pipeline, dense_comm=dense_comm,
-                     rw_capacity=rw_capacity, pipeline_lookup=pipe_lookup)
+                     rw_capacity=rw_capacity, pipeline_lookup=pipe_lookup, rw_exchange=rw_exchange)
     tr = DLRMTrainer(cfg, B, "cpu", group=get_info().group, rank=rank, world_size=world)
     assert tr.pipeline == (pipeline and world > 1)
+    if tr.emb.rw_tables and rw_exchange != "auto":
+        assert tr.emb.rw_rows == (rw_exchange == "rows" and world > 1)
     g = torch.Generator().manual_seed(5)
     for t, r in enumerate(ROWS):
         tr.emb.set_table_weight(t, torch.randn(r, 32, generator=g) * 0.1)
@@ -266,3 +268,27 @@ def test_dlrm_lagged_rw_growth_is_exact():
         for t, (lo, c0, w) in tabs1.items():
             ref = single[1][t][2][slice(*lo)][:, c0:c0 + w.shape[1]]
             assert torch.allclose(w, ref, atol=2e-4), (rank, t)
+
+
+@pytest.mark.parametrize("world,pipeline,skew", [(2, False, None), (3, False, None),
+                                                 (2, True, None), (2, True, 2)])
+def test_dlrm_rw_rows_exchange_matches_pooled(world, pipeline, skew):
+    """One-hot row-wise tables: returning the looked-up rows (and sending
+    each gradient row to its owner) by all-to-all moves ~W/1.25 x fewer
+    bytes than the pooled reduce-scatter / gradient all-gather and gives the
+    same values -- parameters and tables equal the pooled exchange bit for
+    bit, also across a lagged capacity growth (skew: redo of the batch)."""
+    B, steps = 64, 4
+    args = (world, B, steps, "row_wise", "rowwise_adagrad", "fp32", pipeline, "fp32", "uniform",
+            1.05, 1.25, True, skew, (1, 1, 1, 1, 1))
+    pooled = run_distributed(_dlrm_worker, *args, "pooled")
+    rows = run_distributed(_dlrm_worker, *args, "rows")
+    for rank in range(world):
+        p0, tabs0 = pooled[rank][0], pooled[rank][1]
+        p1, tabs1 = rows[rank][0], rows[rank][1]
+        if skew is not None:
+            assert pooled[rank][2] > 0 and rows[rank][2] > 0      # the capacity grew
+        assert torch.equal(p0, p1), (rank, (p0 - p1).abs().max())
+        assert tabs0.keys() == tabs1.keys()
+        for t in tabs0:
+            assert torch.equal(tabs0[t][2], tabs1[t][2]), (rank, t)
