@@ -53,6 +53,9 @@ def parse(argv=None):
     ap.add_argument("--rw-exchange", default="auto", choices=["auto", "pooled", "rows"],
                     help="row-wise exchange (DLRMConfig.rw_exchange): rows = one-hot tables "
                          "return looked-up rows by all-to-all instead of pooled partials")
+    ap.add_argument("--dp-rule", default="cost", choices=["cost", "budget"],
+                    help="--sharding data_parallel: replicate where the dense all-reduce is "
+                         "cheaper than the row-wise exchange (cost) or smallest-first to 256 MB")
     ap.add_argument("--sharding", default="auto",
                     choices=["auto", "table_wise", "row_wise", "column_wise", "data_parallel",
                              "replicated"])
@@ -160,7 +163,7 @@ def self_launch(args, argv) -> int:
 def _cfg(args, rows, pipe):
     from tdfo_amd.models.dlrm import MLPERF_MULTIHOT, DLRMConfig
     kw = dict(table_rows=list(rows), sharding=args.sharding, pipeline=pipe,
-              rw_exchange=args.rw_exchange,
+              rw_exchange=args.rw_exchange, dp_rule=args.dp_rule,
               dense_comm=args.dense_comm, stream_graphs=not args.no_stream_graphs,
               opt_placement=args.opt_placement,
               defer_wgrad=None if args.defer_wgrad is None else args.defer_wgrad == "1")

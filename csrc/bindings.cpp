@@ -788,10 +788,16 @@ void embedding_bwd_prepare(const Tensor& W, const Tensor& row_offset, const Tens
                            const Tensor& offsets, const Tensor& grad_off,
                            const c10::optional<Tensor>& psw, int64_t T, int64_t B, bool mean,
                            int64_t key_bits, int64_t grad_stride, int64_t segsort,
-                           const Tensor& work) {
+                           const Tensor& work, const c10::optional<Tensor>& bag_len) {
   auto a = emb_bwd_args(W, row_offset, indices, offsets, grad_off, psw, T, B, mean, key_bits,
                         grad_stride, segsort);
   set_emb_ws(a, work);
+  if (bag_len) {
+    check_dev(*bag_len, "bag_len");
+    TORCH_CHECK(bag_len->scalar_type() == at::kInt && bag_len->is_contiguous() &&
+                bag_len->numel() >= T, "bag_len: int32 [T]");
+    a.bag_len = bag_len->data_ptr<int32_t>();
+  }
   tdfo::embedding_bwd_prepare(a, cur_stream());
 }
 
@@ -1504,7 +1510,7 @@ TORCH_LIBRARY(tdfo, m) {
   });
   m.def("embedding_bwd_prepare(Tensor W, Tensor row_offset, Tensor indices, Tensor offsets, "
         "Tensor grad_off, Tensor? psw, int T, int B, bool mean, int key_bits, int grad_stride, "
-        "int segsort, Tensor(a!) workspace) -> ()");
+        "int segsort, Tensor(a!) workspace, Tensor? bag_len=None) -> ()");
   m.def("embedding_bwd_apply(Tensor(a!) W, Tensor row_offset, Tensor indices, Tensor offsets, "
         "Tensor grad_off, Tensor? psw, int T, int B, bool mean, int key_bits, Tensor grad, "
         "int grad_stride, int opt, Tensor(b!)? state1, Tensor(c!)? state2, Tensor hyper, "

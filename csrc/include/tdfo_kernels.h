@@ -149,6 +149,11 @@ struct EmbBwdArgs {
   // (+ a run merge when R > 1) replace the radix sort. 0: not applicable.
   int segsort;
   int goff_sorted;             // internal: grad offsets stored in sorted order
+  // optional: every bag of virtual table v holds exactly bag_len[v] ids
+  // (offsets[v*B + b] = offsets[v*B] + b*bag_len[v]; fixed multi-hot): the
+  // keys pass finds a position's bag by division instead of a binary search
+  // over all T*B bag offsets
+  const int32_t* bag_len;
 };
 size_t embedding_bwd_workspace(int64_t nnz, int D);
 // One-hot batches (nnz == T*B, B <= 8192): per-table LDS sort in one launch

@@ -205,8 +205,10 @@ struct BwdCfg {
 // walking its bag 128 us, a wave per 512 positions sliding a 64-bag offset
 // window 52-63 us, this one 51 us; with ~one id per bag the window variant
 // slid ~8 times per wave and slowed TwoTower / Bert4Rec.)
+constexpr int KEYS_REG_MAXT = 1024;           // fixed-length path: virtual tables in LDS
+
 template <typename K>
-__global__ void emb_keys_kernel(const EmbBwdArgs a, K* __restrict__ keys,
+__global__ __launch_bounds__(256) void emb_keys_kernel(const EmbBwdArgs a, K* __restrict__ keys,
                                         int32_t* __restrict__ vals, int64_t* __restrict__ goff,
                                         float* __restrict__ gscale, int32_t* __restrict__ tail_count) {
   if (blockIdx.x == 0 && threadIdx.x == 0) {  // read by later kernels
@@ -214,14 +216,33 @@ __global__ void emb_keys_kernel(const EmbBwdArgs a, K* __restrict__ keys,
     tail_count[1] = 0;
   }
   const int64_t nbags = (int64_t)a.T * a.B;
+  // fixed bag lengths: the virtual tables' first positions in LDS, a
+  // position's table by a short search there, its bag by division
+  __shared__ int64_t tstart[KEYS_REG_MAXT + 1];
+  const bool reg = a.bag_len != nullptr;
+  if (reg) {
+    for (int v = threadIdx.x; v <= a.T; v += blockDim.x)
+      tstart[v] = v < a.T ? a.offsets[(int64_t)v * a.B] : a.nnz;
+    __syncthreads();
+  }
   for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < a.nnz;
        p += (int64_t)gridDim.x * blockDim.x) {
-    int64_t lo = 0, hi = nbags;                 // last bag j with offsets[j] <= p
-    while (hi - lo > 1) {
-      const int64_t mid = (lo + hi) >> 1;
-      if (a.offsets[mid] <= p) lo = mid; else hi = mid;
+    int64_t j;
+    if (reg) {
+      int lo = 0, hi = a.T;                     // last table v with tstart[v] <= p
+      while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (tstart[mid] <= p) lo = mid; else hi = mid;
+      }
+      j = (int64_t)lo * a.B + (p - tstart[lo]) / a.bag_len[lo];
+    } else {
+      int64_t lo = 0, hi = nbags;               // last bag j with offsets[j] <= p
+      while (hi - lo > 1) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (a.offsets[mid] <= p) lo = mid; else hi = mid;
+      }
+      j = lo;
     }
-    const int64_t j = lo;
     const int t = (int)(j / a.B);
     const int b = (int)(j - (int64_t)t * a.B);
     keys[p] = (K)(a.row_offset[t] + a.indices[p]);
@@ -1077,7 +1098,9 @@ void prep_impl(const EmbBwdArgs& a, const WsLayout& L, hipStream_t s) {
     int32_t* v1 = odd ? vals_out : vals_in;
     int64_t kb = (a.nnz + 255) / 256;
     if (kb > 8192) kb = 8192;
-    hipLaunchKernelGGL(emb_keys_kernel<K>, dim3(kb), dim3(256), 0, s, a, k0, v0, goff, gscale,
+    EmbBwdArgs ak = a;
+    if (ak.T > KEYS_REG_MAXT) ak.bag_len = nullptr;   // (LDS table of starts too small)
+    hipLaunchKernelGGL(emb_keys_kernel<K>, dim3(kb), dim3(256), 0, s, ak, k0, v0, goff, gscale,
                        tcount);
     TDFO_CHECK_HIP(hipGetLastError());
     if constexpr (sizeof(K) == 4)

@@ -23,11 +23,13 @@ def main():
     W = int(os.environ.get("W", 8))
     R = int(os.environ.get("RANK_EMU", 0))
     gbps = float(os.environ.get("GBPS", min(W - 1, 7) * 153.0))
-    cfg = DLRMConfig(table_rows=list(CRITEO_1TB_ROWS), pipeline=True)
+    # SHARDING=data_parallel: config 3's plan (replicated + row-wise tables)
+    cfg = DLRMConfig(table_rows=list(CRITEO_1TB_ROWS), pipeline=True,
+                     sharding=os.environ.get("SHARDING", "auto"))
     cfg.ids_stream = False
     tr = DLRMTrainer(cfg, 8192, dev, group=LoopbackComm(W, R, dev, gbps, 10.0), rank=R,
                      world_size=W)
-    steps = 12
+    steps = int(os.environ.get("STEPS", 12))
     nseg = 16
     buf = torch.zeros((steps + 4) * nseg * 2, dtype=torch.int64, device=dev)
     cnt = torch.zeros(nseg, dtype=torch.int64, device=dev)

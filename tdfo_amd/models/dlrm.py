@@ -90,6 +90,9 @@ class DLRMConfig:
     #   grown on demand before any exchange would overflow
     rw_comm: str = "bf16"                          # row-wise reduce-scatter dtype (bf16 | fp32)
     rw_exchange: str = "auto"                      # row-wise exchange: pooled | rows | auto
+    dp_rule: str = "cost"                          # sharding="data_parallel": which tables to
+    #   replicate (cost: where the dense all-reduce moves fewer bytes than the row-wise
+    #   exchange; budget: smallest first up to 256 MB, sparse/planner.py)
     #   (rows: one-hot tables return looked-up rows by all-to-all, sparse/sharded.py)
     dense_comm: str = "fp32"                       # dense-grad all-reduce dtype (fp32 | bf16:
     #   halves the bytes on xGMI; the sum of W bf16-rounded grads, as DDP's bf16 compress hook)
@@ -286,7 +289,8 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
         optim = EmbOptimConfig(cfg.emb_opt, lr=cfg.emb_lr, eps=cfg.emb_eps)
         tables = cfg.tables()
         self.plan = plan or plan_sharding(tables, world_size, optim, batch_per_rank=B,
-                                          pooling=cfg.pooling_factors(), strategy=cfg.sharding)
+                                          pooling=cfg.pooling_factors(), strategy=cfg.sharding,
+                                          dp_rule=cfg.dp_rule)
         self.emb = ShardedEmbeddingBags(tables, self.plan, rank, B, cfg.pooling_factors(), dev,
                                         optim, group=self.comm, seed=cfg.seed,
                                         rw_capacity=cfg.rw_capacity, rw_comm=cfg.rw_comm,

@@ -61,6 +61,10 @@ _HEAD_WAIT = os.environ.get("TDFO_MR_HEAD_WAIT", "0") == "1"
 # A/B knob: TDFO_MR_EARLY_PREP=0 buckets the next batch's sharded ids in M4
 # (from the loaded ids) and publishes the row-wise need in Da, as before
 _EARLY_PREP = os.environ.get("TDFO_MR_EARLY_PREP", "1") != "0"
+# A/B knob: TDFO_MR_SORT_EC=1 runs the ids-only sort and the early prep on
+# the embedding stream (EC idles until the interaction backward) instead of
+# D (which then only carries the dense side)
+_SORT_EC = os.environ.get("TDFO_MR_SORT_EC", "0") == "1"
 
 
 class MultiRankStreamsMixin:
@@ -147,18 +151,21 @@ class MultiRankStreamsMixin:
             if not early:
                 emb.stage_fwd_prep(self.ids, dp=False)
 
-        def d_pre():
+        sort_ec = _SORT_EC and early and dp_dense
+
+        def pre(comm):
             # early prep: the next batch's sharded-table ids bucketed on D
-            # straight from the host staging, as soon as the previous id
-            # exchange (c5') has released the send buffers, and the row-wise
-            # need published right after -- early in the step instead of
-            # after the bottom backward (M4), so the host, which reads it
-            # before it issues the next step, is not held until mid-step
+            # (or EC) straight from the host staging, as soon as the previous
+            # id exchange (c5') has released the send buffers, and the
+            # row-wise need published right after -- early in the step
+            # instead of after the bottom backward (M4), so the host, which
+            # reads it before it issues the next step, is not held until
+            # mid-step (the need's all-reduce on that stream's communicator)
             emb.stage_fwd_prep(self._stg[1], dp=False)
             if emb.rw_tables:
                 emb._rw_ids = self.ids          # a redo re-reads the batch from ids (M4 loads it)
             if self._rw_lagged:
-                emb.rw_publish_need(self.dcomm)
+                emb.rw_publish_need(comm)
 
         def d_prep():                           # the replicated tables' ids, once their
             emb.stage_fwd_prep(self.ids, sharded=False)   # dense grad (Dp) has read them
@@ -188,7 +195,11 @@ class MultiRankStreamsMixin:
 
         return {"M1": self._s_bottom_fwd, "M2": m2, "M4": m4,
                 "M3": self._s_top_wgrad if self._defer_top_wgrad else None,
-                "D0": emb.stage_bwd_prepare, "Dpre": d_pre if early else None, "Dp": dp_a,
+                "D0": None if sort_ec else emb.stage_bwd_prepare,
+                "Dpre": (lambda: pre(self.dcomm)) if early and not sort_ec else None,
+                "ECs": emb.stage_bwd_prepare if sort_ec else None,
+                "ECpre": (lambda: pre(self.comm)) if sort_ec else None,
+                "Dp": dp_a,
                 "Da": d_a,
                 "Db": d_b, "EC1": lambda: emb.backward_start(dp=False),
                 "ECub": lambda: (ec_upd(), ec_b())}
@@ -211,6 +222,7 @@ class MultiRankStreamsMixin:
         seg = self._mr_segments()
         dp_dense = bool(self.emb.dp_tables) and self.emb.dp_dense
         early = _EARLY_PREP and not self.emb.tw_identity       # (as in _mr_segments)
+        sort_ec = _SORT_EC and early and dp_dense
         home = lambda name: "EC" if name.startswith("EC") else name[0]  # noqa: E731
         pool = torch.cuda.graph_pool_handle()
         graphs = {}
@@ -284,8 +296,10 @@ class MultiRankStreamsMixin:
             # all-reduce, the two dense buckets and the dense optimizer
             # (early prep: the next batch's sharded ids from the staging
             # right after the sort, Dpre)
-            "D": chain([("wait", "c5"), ("graph", "D0"), ("record", "e0")]
-                       + ([("wait", "stg"), ("graph", "Dpre"), ("record", "pre")] if early else [])
+            "D": chain(([] if sort_ec else
+                        [("wait", "c5"), ("graph", "D0"), ("record", "e0")]
+                        + ([("wait", "stg"), ("graph", "Dpre"), ("record", "pre")] if early
+                           else []))
                        + [("wait", "m2"),
                           ("graph", "Dp"), ("record", "dp"), ("wait", "m4"), ("graph", "Da"),
                           ("record", "dpp"), ("wait", "m3"), ("graph", "Db"), ("record", "d")]),
@@ -296,7 +310,12 @@ class MultiRankStreamsMixin:
             # costs ~14 us of queue idle, scripts/mr_timeline.py; with a
             # dense replicated-table update D also looks those tables up, so
             # EC waits for none of D's replicated-table work)
-            "EC": (chain([("wait", "m2"), ("graph", "EC1"), ("wait", "e0"),
+            # (sort_ec: the sort and the early prep first on EC itself,
+            # which otherwise idles until the interaction backward)
+            "EC": (chain([("graph", "ECs"), ("record", "e0"), ("wait", "stg"),
+                          ("graph", "ECpre"), ("record", "pre"), ("wait", "m2"),
+                          ("graph", "EC1"), ("graph", "ECub"), ("record", "c5")]) if sort_ec else
+                   chain([("wait", "m2"), ("graph", "EC1"), ("wait", "e0"),
                           ("wait", "pre" if early else "m4"),
                           ("graph", "ECub"), ("record", "c5")]) if dp_dense else
                    chain([("wait", "m2"), ("graph", "EC1"), ("wait", "e0"), ("wait", "dp"),

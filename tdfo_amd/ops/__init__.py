@@ -349,14 +349,16 @@ def embedding_bwd_workspace(nnz: int, D: int) -> int:
 
 
 def embedding_bwd_prepare(W, row_offset, indices, offsets, grad_off, T, B, grad_stride, workspace,
-                          key_bits=None, mean=False, psw=None, segsort=0):
+                          key_bits=None, mean=False, psw=None, segsort=0, bag_len=None):
     """First half of the fused embedding backward (GPU): keys, sort and
     gradient offsets into ``workspace`` -- needs only the ids, so it can run
-    on a side stream before the gradient exists."""
+    on a side stream before the gradient exists. ``bag_len`` (int32 [T],
+    optional): every bag of virtual table v holds bag_len[v] ids (fixed
+    multi-hot) -- the keys pass then divides instead of searching."""
     if key_bits is None:
         key_bits = key_bits_for(W.shape[0])
     _native().embedding_bwd_prepare(W, row_offset, indices, offsets, grad_off, psw, T, B, mean,
-                                    key_bits, grad_stride, int(segsort), workspace)
+                                    key_bits, grad_stride, int(segsort), workspace, bag_len)
 
 
 def embedding_bwd_apply(W, row_offset, indices, offsets, grad_off, T, B, grad, grad_stride, opt,

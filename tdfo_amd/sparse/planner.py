@@ -30,9 +30,14 @@ Sharding kinds:
 
 Strategies: "data_parallel" (config 3, the reference's pmap / Mirrored /
 DDP data parallelism, jax-flax/train_dp.py:63, tensorflow2/train_dp.py:71-72)
-replicates the smallest tables while their fp32 weights total at most
-``dp_replicate_max_bytes`` (256 MB: one dense fp32 gradient all-reduce trains
-all of them and their update is the same dense pass on every rank) and
+replicates the small tables -- those whose dense fp32 gradient all-reduce
+moves fewer bytes per rank than their row-wise exchange would
+(``dp_rule="cost"``: rows x D x 4 x 2 (W-1)/W against the ids + rows +
+gradient rows of a one-hot table's "rows" exchange, or the pooled
+partials / gradients of a multi-hot one), within ``dp_replicate_max_bytes``
+of fp32 weights in all (256 MB); ``dp_rule="budget"``: the smallest tables
+while they fit that budget -- one dense fp32 gradient all-reduce trains all
+of them and their update is the same dense pass on every rank) and
 owner-partitions the larger ones as row-wise shards: an exact
 replica of a big table would make every rank apply the whole global batch's
 update (W x the one-GPU work, plus W x B pooled gradients gathered), while
@@ -96,7 +101,7 @@ def plan_sharding(tables: Sequence[TableConfig], world_size: int, optim: EmbOpti
                   row_cost: Optional[Callable[[int], float]] = None,
                   dp_max_rows: Optional[int] = None,
                   dp_replicate_max_bytes: int = 256 << 20,
-                  balance: float = 1.10) -> ShardingPlan:
+                  balance: float = 1.10, dp_rule: str = "cost") -> ShardingPlan:
     """Deterministic greedy planner with a balance pass.
 
     strategy: "auto" (table-wise with row-wise fallback for tables that fit
@@ -134,7 +139,7 @@ def plan_sharding(tables: Sequence[TableConfig], world_size: int, optim: EmbOpti
     kw = dict(batch_per_rank=batch_per_rank, pooling=pooling, hbm_bytes=hbm_bytes,
               reserve_frac=reserve_frac, strategy=strategy, dp_max_bytes=dp_max_bytes,
               row_cost=row_cost, dp_max_rows=dp_max_rows,
-              dp_replicate_max_bytes=dp_replicate_max_bytes)
+              dp_replicate_max_bytes=dp_replicate_max_bytes, dp_rule=dp_rule)
     plan = _plan_once(tables, world_size, optim, frozenset(), **kw)
     if strategy != "auto" or world_size == 1 or balance is None:
         return plan
@@ -163,7 +168,7 @@ def plan_sharding(tables: Sequence[TableConfig], world_size: int, optim: EmbOpti
 
 def _plan_once(tables, world_size, optim, force_rw, batch_per_rank, pooling, hbm_bytes,
                reserve_frac, strategy, dp_max_bytes, row_cost, dp_max_rows,
-               dp_replicate_max_bytes) -> ShardingPlan:
+               dp_replicate_max_bytes, dp_rule="cost") -> ShardingPlan:
     W = world_size
     cap = int(hbm_bytes * (1.0 - reserve_frac))
     T = len(tables)
@@ -233,12 +238,26 @@ def _plan_once(tables, world_size, optim, force_rw, batch_per_rank, pooling, hbm
     # owner-partitioned row-wise (an exact replica of a big table would make
     # every rank apply the whole global batch's update)
     replicate = set()
+    if dp_rule not in ("cost", "budget"):
+        raise ValueError(f"dp_rule must be cost or budget, got {dp_rule!r}")
+
+    def ar_cheaper(t: int) -> bool:
+        """dense fp32 gradient all-reduce (ring: 2 (W-1)/W of the table per
+        rank) moves fewer bytes than the table's row-wise exchange"""
+        d, L = tables[t].embedding_dim, pooling[t]
+        ar = 2 * (W - 1) / W * tables[t].num_embeddings * d * 4
+        if L == 1:       # "rows" exchange: ids, rows back, gradient rows out (1.25 x capacity)
+            rw = B * (8 + 2 * 1.25 * d * 2) * (W - 1) / W
+        else:            # pooled partials' reduce-scatter + pooled gradients' all-gather
+            rw = B * L * 8 * (W - 1) / W + 2 * (W - 1) * B * d * 2
+        return ar <= rw
+
     if strategy == "data_parallel" and W > 1:
         cum = 0
         for t in sorted(range(T), key=lambda t: (tables[t].num_embeddings *
                                                   tables[t].embedding_dim, t)):
             nb = tables[t].num_embeddings * tables[t].embedding_dim * 4
-            if cum + nb > dp_replicate_max_bytes:
+            if cum + nb > dp_replicate_max_bytes or (dp_rule == "cost" and not ar_cheaper(t)):
                 break
             cum += nb
             replicate.add(t)

@@ -173,6 +173,9 @@ class ShardedEmbeddingBags:
         if lens:
             offs[1:] = torch.cumsum(torch.tensor(lens, dtype=torch.int64), 0)
         self.tw_v_offsets = offs.to(self.device)
+        # fixed bag length per virtual table (the offsets above are regular)
+        self.tw_v_len = torch.tensor([self.L[t] for s_ in range(W) for t in mine],
+                                     dtype=torch.int32, device=self.device)
         self.tw_v_row_off = torch.tensor(v_row_off, dtype=torch.int64, device=self.device)
         self.tw_v_out_off = torch.tensor(v_out_off, dtype=torch.int64, device=self.device)
         self.tw_ld = self.dsum[rank]          # row pitch of the pooled TW output (alias_pooled)
@@ -852,7 +855,7 @@ class ShardedEmbeddingBags:
             self.tw_store.backward_prepare(self.tw_recv_ids, self.tw_v_offsets, self.tw_v_row_off,
                                            self.tw_nv, self.B, self.tw_v_out_off,
                                            self.tw_ld, mean=self.mean,
-                                           segsort=self.tw_segsort)
+                                           segsort=self.tw_segsort, bag_len=self.tw_v_len)
         if self.rw_tables:
             self._rw_prepare()
 

@@ -169,7 +169,7 @@ class TableBatchedEmbedding:
                           segsort=segsort)
 
     def backward_prepare(self, indices, offsets, row_offset, T, B, grad_off, grad_stride,
-                         mean=False, psw=None, segsort=0):
+                         mean=False, psw=None, segsort=0, bag_len=None):
         """Ids-only half of the backward (keys + sort) into a persistent
         workspace; GPU only (CPU: no-op, backward_apply does everything)."""
         self._prepared = None
@@ -181,7 +181,7 @@ class TableBatchedEmbedding:
         seg = ops.effective_segsort(segsort)       # fixed here for the apply half too
         ops.embedding_bwd_prepare(self.weight, row_offset, indices, offsets, grad_off, T, B,
                                   grad_stride, self._bwd_ws, key_bits=self.key_bits, mean=mean,
-                                  psw=psw, segsort=seg)
+                                  psw=psw, segsort=seg, bag_len=bag_len)
         self._prepared = (indices.data_ptr(), indices.numel(), T, B)
         self._prepared_segsort = seg
 

@@ -388,6 +388,43 @@ def test_embedding_bwd_prepare_apply_matches_fused(segsort):
     assert torch.equal(Wf, Wp) and torch.equal(sf, sp)
 
 
+@pytest.mark.parametrize("mean", [False, True])
+def test_embedding_bwd_fixed_bag_len_keys(mean):
+    """Fixed multi-hot (every bag of table t holds L[t] ids, DCN-v2's MLPerf
+    pooling): the keys pass with ``bag_len`` (bag by division) prepares the
+    same workspace as the bag-offset search -- identical update."""
+    T, B, D = 4, 2048, 128
+    rows = [3, 40000, 900, 1 << 20]
+    L = [1, 7, 3, 100]
+    g = torch.Generator().manual_seed(4)
+    idx = torch.cat([torch.randint(0, rows[t], (B * L[t],), generator=g) for t in range(T)])
+    lens = torch.tensor(L).repeat_interleave(B)
+    offs = torch.zeros(T * B + 1, dtype=torch.long)
+    offs[1:] = lens.cumsum(0)
+    ro = torch.zeros(T, dtype=torch.long)
+    ro[1:] = torch.tensor(rows[:-1]).cumsum(0)
+    W = torch.randn(sum(rows), D, generator=g) * 0.1
+    W, ro, idx, offs = (x.to(DEV) for x in (W, ro, idx, offs))
+    goff = torch.tensor([t * D for t in range(T)], device=DEV)
+    grad = torch.randn(B * T * D, device=DEV)
+    hyper = torch.tensor([0.05, 3.0], device=DEV)
+    s1 = torch.rand(W.shape[0], device=DEV)
+    bl = torch.tensor(L, dtype=torch.int32, device=DEV)
+    out = []
+    for bag_len in (None, bl):
+        Wp, sp = W.clone(), s1.clone()
+        ws = torch.empty(ops.embedding_bwd_workspace(idx.numel(), D), dtype=torch.uint8,
+                         device=DEV)
+        ops.embedding_bwd_prepare(Wp, ro, idx, offs, goff, T, B, T * D, ws, mean=mean,
+                                  bag_len=bag_len)
+        ops.embedding_bwd_apply(Wp, ro, idx, offs, goff, T, B, grad, T * D,
+                                ops.EMB_ROWWISE_ADAGRAD, hyper, ws, state1=sp, mean=mean)
+        torch.cuda.synchronize()
+        out.append((Wp, sp))
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+    assert not torch.equal(out[0][0], W)
+
+
 def test_embedding_bwd_deterministic():
     T, B, D = 2, 4096, 128
     rows = [3, 100000]
