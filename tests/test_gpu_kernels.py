@@ -331,6 +331,32 @@ def test_embedding_bwd_onehot_segsort(B, skew, opt):
     assert (res[0][0] - We).abs().max() < 1e-4 * max(1.0, We.abs().max().item())
 
 
+def test_embedding_dense_grad_replicated_tables():
+    """The replicated tables' backward at W > 1 (dense fp32 gradient, one id
+    per bag, per-table LDS sort): the tiny tables' runs span tens of chunks
+    and take the block-wide walk -- equal to the fp32 reference and bitwise
+    reproducible."""
+    T, B, D = 6, 8192, 128
+    rows = [3, 4, 14, 155, 976, 2208]
+    W, ro, idx, offs = _emb_case(T, B, rows, D, 1, False, seed=11)
+    W, ro, idx, offs = (x.to(DEV) for x in (W, ro, idx, offs))
+    goff = torch.tensor([t * D for t in range(T)], device=DEV)
+    grad = torch.randn(B * T * D, device=DEV) * 0.01
+    hyper = torch.tensor([0.05, 3.0], device=DEV)
+    res = []
+    for _ in range(2):
+        dg = torch.zeros(W.numel(), device=DEV)
+        ops.embedding_bwd(W.clone(), ro, idx, offs, goff, T, B, grad, T * D,
+                          ops.EMB_DENSE_GRAD, hyper, dense_grad=dg, segsort=1)
+        res.append(dg)
+    torch.cuda.synchronize()
+    assert torch.equal(res[0], res[1])
+    edg = torch.zeros(W.numel(), device=DEV)
+    ref.embedding_bwd(W.clone(), ro, idx, offs, goff, None, T, B, False, 20, grad, T * D,
+                      ops.EMB_DENSE_GRAD, None, None, hyper, 1e-8, 0.9, 0.999, 0.0, edg)
+    assert (res[0] - edg).abs().max() < 1e-4 * max(1.0, edg.abs().max().item())
+
+
 @pytest.mark.parametrize("R,B", [(2, 2048), (3, 2048), (8, 2048), (8, 8192)])
 def test_embedding_bwd_onehot_multirun(R, B):
     """World > 1 layout: each physical table's ids arrive as R runs (virtual
