@@ -893,6 +893,55 @@ void rw_pool(const Tensor& Wt, const Tensor& recv, const Tensor& meta, int64_t n
   tdfo::rw_pool(a, cur_stream());
 }
 
+// fused bottom MLP forward (mlp_fused.hip)
+bool bottom_mlp_fwd_ok(int64_t k0, int64_t n0, int64_t n1, int64_t n2) {
+  return tdfo::bottom_mlp_fwd_supported((int)k0, (int)n0, (int)n1, (int)n2);
+}
+
+void bottom_mlp_fwd(const Tensor& x, const Tensor& w0, const Tensor& w1, const Tensor& w2,
+                    const c10::optional<Tensor>& b0, const c10::optional<Tensor>& b1,
+                    const c10::optional<Tensor>& b2, const Tensor& y0, const Tensor& y1,
+                    const Tensor& y2) {
+  const Tensor* ts[7] = {&x, &w0, &w1, &w2, &y0, &y1, &y2};
+  const char* nm[7] = {"x", "w0", "w1", "w2", "y0", "y1", "y2"};
+  for (int i = 0; i < 7; ++i) {
+    check_dev(*ts[i], nm[i]);
+    TORCH_CHECK(ts[i]->scalar_type() == at::kBFloat16 && ts[i]->dim() == 2 &&
+                ts[i]->stride(1) == 1 && ts[i]->stride(0) % 8 == 0 && aligned16(ts[i]->data_ptr()),
+                "bottom_mlp_fwd: ", nm[i], " must be bf16 2-D, unit column stride, 16-B rows");
+  }
+  const int64_t M = x.size(0);
+  TORCH_CHECK(tdfo::bottom_mlp_fwd_supported((int)x.size(1), (int)w0.size(0), (int)w1.size(0),
+                                             (int)w2.size(0)), "bottom_mlp_fwd: unsupported dims");
+  TORCH_CHECK(w0.size(1) >= x.size(1) && w1.size(1) >= w0.size(0) && w2.size(1) >= w1.size(0),
+              "bottom_mlp_fwd: weight K");
+  TORCH_CHECK(y0.size(0) == M && y1.size(0) == M && y2.size(0) == M && y0.size(1) >= w0.size(0) &&
+              y1.size(1) >= w1.size(0) && y2.size(1) >= w2.size(0), "bottom_mlp_fwd: outputs");
+  tdfo::BotMlpArgs a{};
+  a.x = bf16_ptr(x); a.ldx = x.stride(0);
+  a.w0 = bf16_ptr(w0); a.w1 = bf16_ptr(w1); a.w2 = bf16_ptr(w2);
+  a.ldw0 = w0.stride(0); a.ldw1 = w1.stride(0); a.ldw2 = w2.stride(0);
+  const c10::optional<Tensor>* bs[3] = {&b0, &b1, &b2};
+  const int64_t nout[3] = {w0.size(0), w1.size(0), w2.size(0)};
+  const float* bp[3] = {nullptr, nullptr, nullptr};
+  int64_t bst[3] = {0, 0, 0};
+  for (int i = 0; i < 3; ++i) {
+    if (*bs[i]) {
+      const Tensor& b = **bs[i];
+      check_dev(b, "bias");
+      TORCH_CHECK(b.scalar_type() == at::kFloat && b.dim() == 1 && b.size(0) >= nout[i],
+                  "bottom_mlp_fwd: bias fp32 1-D");
+      bp[i] = b.data_ptr<float>();
+      bst[i] = b.stride(0);
+    }
+  }
+  a.b0 = bp[0]; a.b1 = bp[1]; a.b2 = bp[2]; a.bs0 = bst[0]; a.bs1 = bst[1]; a.bs2 = bst[2];
+  a.y0 = bf16_mut(y0); a.y1 = bf16_mut(y1); a.y2 = bf16_mut(y2);
+  a.ldy0 = y0.stride(0); a.ldy1 = y1.stride(0); a.ldy2 = y2.stride(0);
+  a.M = (int)M;
+  tdfo::bottom_mlp_fwd(a, cur_stream());
+}
+
 // one-hot row-wise "rows" exchange (rowwise.hip)
 void check_bf16_buf(const Tensor& t, int64_t n, const char* name) {
   check_dev(t, name);
@@ -1528,6 +1577,9 @@ TORCH_LIBRARY(tdfo, m) {
         "int cap, bool mean, int key_bits, int grad_ld, int dummy_row, Tensor(a!) workspace, "
         "int rows=0) -> ()");
   m.def("rw_rows_gather(Tensor Wt, Tensor recv, int W, int cap, Tensor(a!) out) -> ()");
+  m.def("bottom_mlp_fwd_ok(int k0, int n0, int n1, int n2) -> bool", bottom_mlp_fwd_ok);
+  m.def("bottom_mlp_fwd(Tensor x, Tensor w0, Tensor w1, Tensor w2, Tensor? b0, Tensor? b1, "
+        "Tensor? b2, Tensor(a!) y0, Tensor(b!) y1, Tensor(c!) y2) -> ()");
   m.def("rw_rows_scatter(Tensor send, int W, int cap, int B, int D, Tensor rows, Tensor(a!) region, "
         "int ld, Tensor(b!) map, int nrw) -> ()");
   m.def("rw_grads_gather(Tensor map, int W, int cap, int D, Tensor dregion, Tensor(a!) gsend) -> ()");
@@ -1598,6 +1650,7 @@ TORCH_LIBRARY_IMPL(tdfo, CUDA, m) {
   m.impl("rw_pool", rw_pool);
   m.impl("embedding_bwd_prepare_rw", embedding_bwd_prepare_rw);
   m.impl("rw_rows_gather", rw_rows_gather);
+  m.impl("bottom_mlp_fwd", bottom_mlp_fwd);
   m.impl("rw_rows_scatter", rw_rows_scatter);
   m.impl("rw_grads_gather", rw_grads_gather);
   m.impl("embedding_bwd_apply_rw", embedding_bwd_apply_rw);

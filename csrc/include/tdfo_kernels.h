@@ -199,6 +199,26 @@ void synth_ids(const SynthArgs& a, hipStream_t s);
 // its dense features (-> bf16 x0) and labels only (one thread per sample)
 void synth_dense(const SynthArgs& a, hipStream_t s);
 
+// ------------------------------------------------ fused bottom MLP ----
+// (mlp_fused.hip) The default DLRM bottom stack (K0 = 64 padded input with
+// the bias inside K, 512 -> 256 -> 128, ReLU everywhere) in one launch:
+// y_i = relu(y_{i-1} W_i^T + b_i), bf16 activations written to y0 / y1 / y2
+// (row strides ldy*), weights [N][ldw] bf16 (the first K columns used),
+// biases fp32 with element stride bs* (nullptr: inside K). Bitwise equal to
+// the three per-layer GEMMs.
+struct BotMlpArgs {
+  const uint16_t* x; int64_t ldx;
+  const uint16_t* w0; const uint16_t* w1; const uint16_t* w2;
+  int64_t ldw0, ldw1, ldw2;
+  const float* b0; const float* b1; const float* b2;
+  int64_t bs0, bs1, bs2;
+  uint16_t* y0; uint16_t* y1; uint16_t* y2;
+  int64_t ldy0, ldy1, ldy2;
+  int M;
+};
+bool bottom_mlp_fwd_supported(int k0, int n0, int n1, int n2);
+void bottom_mlp_fwd(const BotMlpArgs& a, hipStream_t s);
+
 // --------------------------------------------------- row-wise shards ----
 // (rowwise.hip) Fixed-capacity row-wise exchange. meta (int64, device):
 // [in_base (nrw) | L (nrw) | blk (nrw) | lrow (nrw) | cum (nrw + 1)]:

@@ -1,0 +1,225 @@
+// Fused DLRM bottom-MLP forward: the three Linear + ReLU layers of the
+// default bottom stack (13 -> 512 -> 256 -> 128, input padded to 64 columns
+// with the bias inside K) for a 32-row tile in ONE launch, the intermediate
+// activations chained through LDS (and still written to HBM: the backward
+// reads them).
+//
+// Why: as three GEMM launches the bottom forward is latency-bound (K of 64,
+// 512 and 256: each block runs 1-8 K-tiles, so fill / drain and the launch
+// boundaries dominate): 8.7 + 12.3 + 8.4 us of the one-GPU DLRM step, on the
+// MLP stream's critical path (the embedding lookup it waits for ends ~30 us
+// earlier, profiles/r05/dlrm/step_lanes.txt).
+//
+// Numerics: every output element is the same MFMA chain as the per-layer
+// GEMMs (gemm.hip): v_mfma_f32_16x16x32_bf16 with the weight fragment as the
+// first operand, fragments read from the same XOR-swizzled [rows][64 k] LDS
+// images (lane l: row r0 + (l & 15), k = 32 ks + 8 (l >> 4) + j), K-tiles in
+// order; then + bias (fp32), ReLU, round-to-nearest-even bf16 -- bitwise the
+// layer-by-layer result (tests/test_gpu_kernels.py).
+//
+// 256 threads = 4 waves; wave w owns output columns [w N/4, (w+1) N/4) of
+// every layer and all 32 rows (2 x 16-row fragments). The weights go straight
+// from L2 into MFMA fragments (eight k-steps in flight per wave, the next
+// layer's first ones issued before the barrier between layers, no barrier in
+// a layer: staging them through LDS K-tile by K-tile measured 20.9 us, its
+// per-tile barriers exposing every load); the activations through LDS
+// (52 KiB):
+//   [0, 32K)       layer-0 output as 8 K-tile images [32][64] (layer 1's A)
+//   [32K, 48K)     layer-1 output as 4 K-tile images (layer 2's A)
+//   [48K, 52K)     the input tile [32][64]
+#include "tdfo_common.h"
+#include "tdfo_kernels.h"
+
+namespace tdfo {
+namespace {
+
+typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
+
+constexpr int TM = 32, K0 = 64, N0 = 512, N1 = 256, N2 = 128;
+constexpr int R_O0 = 0, R_O1 = R_O0 + 32 * 1024, R_X = R_O1 + 16 * 1024;
+constexpr int BOT_LDS = R_X + TM * 128;
+
+// byte offset of 16-B chunk c (k = 8c..8c+7) of row r in a [rows][64 k] image
+__device__ __forceinline__ int swz(int r, int c) { return r * 128 + ((c ^ (r & 7)) << 4); }
+
+__device__ __forceinline__ bf16x8_t frag(const TDFO_LDS char* img, int r0, int ks, int lane) {
+  const int r = r0 + (lane & 15);
+  return *(const TDFO_LDS bf16x8_t*)(img + swz(r, ks * 4 + (lane >> 4)));
+}
+
+// R rows x 64 k of K-tile k0 of a row-major bf16 matrix, rows clamped to
+// [0, nrows): Q = R * 8 / 256 16-B chunks per thread
+template <int R>
+struct Chunks {
+  static constexpr int Q = R * 8 / 256;
+  u32x4 v[Q];
+  __device__ __forceinline__ void load(const uint16_t* g, int64_t ld, int row0, int nrows, int k0,
+                                       int tid) {
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int i = tid + q * 256, r = i >> 3, c = i & 7;
+      int gr = row0 + r;
+      gr = gr < nrows ? gr : nrows - 1;
+      v[q] = *(const u32x4*)(g + (int64_t)gr * ld + k0 + c * 8);
+    }
+  }
+  __device__ __forceinline__ void store(TDFO_LDS char* img, int tid) const {
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int i = tid + q * 256, r = i >> 3, c = i & 7;
+      *(TDFO_LDS u32x4*)(img + swz(r, c)) = v[q];
+    }
+  }
+};
+
+// bias of this lane's four output columns of fragment column j (0 without a
+// separate bias), loaded ahead of the layer's MFMAs so the epilogue does not
+// wait on them
+template <int J>
+__device__ __forceinline__ void load_bias(float (&bv)[J][4], const float* bias, int64_t bs,
+                                          int n0w, int lane) {
+#pragma unroll
+  for (int j = 0; j < J; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      bv[j][r] = bias ? bias[(int64_t)(n0w + 16 * j + 4 * (lane >> 4) + r) * bs] : 0.f;
+}
+
+// acc[i][j] + bias, ReLU, bf16 -> global rows m0.. (row stride ldy) and, if
+// LDS_OUT, the next layer's K-tile images at img (column n -> image n / 64,
+// chunk (n % 64) / 8). A compile-time flag, not an img != nullptr test: an LDS
+// pointer to offset 0 compares equal to the address-space-3 null.
+template <int J, bool LDS_OUT>
+__device__ __forceinline__ void epilogue(const f32x4_t (&acc)[2][J], const float (&bv)[J][4],
+                                         int n0w, int m0, int M, uint16_t* y, int64_t ldy,
+                                         TDFO_LDS char* img, int lane) {
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int n = n0w + 16 * j + 4 * (lane >> 4);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int m = 16 * i + (lane & 15);
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = fmaxf(acc[i][j][r] + bv[j][r], 0.f);
+      const u32x2 pk = {pack2bf(v[0], v[1]), pack2bf(v[2], v[3])};
+      if (m0 + m < M) *(u32x2*)(y + (int64_t)(m0 + m) * ldy + n) = pk;
+      if (LDS_OUT) {
+        const int k = n & 63;
+        *(TDFO_LDS u32x2*)(img + (n >> 6) * (TM * 128) + swz(m, k >> 3) + (k & 7) * 2) = pk;
+      }
+    }
+  }
+}
+
+// Weight fragment straight from global memory (L2-resident: every block
+// reads the same weights): lane l gets W row r0 + (l & 15), k = kb + 8 (l >> 4)
+// + 0..7 -- the fragment frag() reads from an LDS image, so the MFMA inputs
+// are the same.
+__device__ __forceinline__ bf16x8_t gfrag(const uint16_t* W, int64_t ldw, int r0, int kb,
+                                          int lane) {
+  const u32x4 v = *(const u32x4*)(W + (int64_t)(r0 + (lane & 15)) * ldw + kb + 8 * (lane >> 4));
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+// issue the weight fragments of k-steps [S0, S1) (fully unrolled: the array
+// only names registers; a fragment lives from its load to its MFMA)
+template <int J, int S, int S0, int S1>
+__device__ __forceinline__ void wload(bf16x8_t (&b)[S][J], const uint16_t* W, int64_t ldw,
+                                      int n0w, int lane) {
+#pragma unroll
+  for (int s = S0; s < S1 && s < S; ++s)
+#pragma unroll
+    for (int j = 0; j < J; ++j) b[s][j] = gfrag(W, ldw, n0w + 16 * j, 32 * s, lane);
+}
+
+// One layer for this wave: out cols [n0w, n0w + 16 J), A fragments from the
+// K-tile images at img, S k-steps; the caller issued k-steps [0, PD) (before
+// the barrier ahead of this layer), step s issues step s + PD: PD k-steps of
+// weights in flight hide the L2 latency (a shallower ring left the kernel
+// latency-bound at 22.8 us).
+template <int J, int S, int PD>
+__device__ __forceinline__ void mma(f32x4_t (&acc)[2][J], bf16x8_t (&b)[S][J],
+                                    const TDFO_LDS char* img, const uint16_t* W, int64_t ldw,
+                                    int n0w, int lane) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < J; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    if (s + PD < S) {
+#pragma unroll
+      for (int j = 0; j < J; ++j) b[s + PD][j] = gfrag(W, ldw, n0w + 16 * j, 32 * (s + PD), lane);
+    }
+    bf16x8_t af[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) af[i] = frag(img + (s >> 1) * (TM * 128), 16 * i, s & 1, lane);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < J; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b[s][j], af[i], acc[i][j], 0, 0, 0);
+  }
+}
+
+__global__ __launch_bounds__(256) void bottom_mlp_fwd_kernel(BotMlpArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  TDFO_LDS char* sm = (TDFO_LDS char*)smem_raw;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int m0 = blockIdx.x * TM;
+  constexpr int J0 = N0 / 64, S0 = K0 / 32, J1 = N1 / 64, S1 = N0 / 32, J2 = N2 / 64, S2 = N1 / 32;
+  constexpr int PD1 = 8;
+  const int c0 = w * (N0 / 4), c1 = w * (N1 / 4), c2 = w * (N2 / 4);
+  // layer 0's weights and bias in flight with the input tile
+  bf16x8_t b0[S0][J0];
+  wload<J0, S0, 0, S0>(b0, a.w0, a.ldw0, c0, lane);
+  float bv0[J0][4];
+  load_bias<J0>(bv0, a.b0, a.bs0, c0, lane);
+  {
+    Chunks<TM> x;                            // the input tile (one 16-B chunk per thread)
+    x.load(a.x, a.ldx, m0, a.M, 0, tid);
+    x.store(sm + R_X, tid);
+  }
+  __syncthreads();
+  bf16x8_t b1[S1][J1];
+  float bv1[J1][4];
+  {
+    f32x4_t acc[2][J0];
+    mma<J0, S0, S0>(acc, b0, sm + R_X, a.w0, a.ldw0, c0, lane);
+    wload<J1, S1, 0, PD1>(b1, a.w1, a.ldw1, c1, lane);   // next layer's first k-steps
+    load_bias<J1>(bv1, a.b1, a.bs1, c1, lane);
+    epilogue<J0, true>(acc, bv0, c0, m0, a.M, a.y0, a.ldy0, sm + R_O0, lane);
+  }
+  __syncthreads();                          // layer-0 output images complete
+  bf16x8_t b2[S2][J2];
+  float bv2[J2][4];
+  {
+    f32x4_t acc[2][J1];
+    mma<J1, S1, PD1>(acc, b1, sm + R_O0, a.w1, a.ldw1, c1, lane);
+    wload<J2, S2, 0, S2>(b2, a.w2, a.ldw2, c2, lane);   // all of layer 2's weights
+    load_bias<J2>(bv2, a.b2, a.bs2, c2, lane);
+    epilogue<J1, true>(acc, bv1, c1, m0, a.M, a.y1, a.ldy1, sm + R_O1, lane);
+  }
+  __syncthreads();
+  {
+    f32x4_t acc[2][J2];
+    mma<J2, S2, S2>(acc, b2, sm + R_O1, a.w2, a.ldw2, c2, lane);
+    epilogue<J2, false>(acc, bv2, c2, m0, a.M, a.y2, a.ldy2, sm, lane);
+  }
+}
+
+}  // namespace
+
+bool bottom_mlp_fwd_supported(int k0, int n0, int n1, int n2) {
+  return k0 == K0 && n0 == N0 && n1 == N1 && n2 == N2;
+}
+
+void bottom_mlp_fwd(const BotMlpArgs& a, hipStream_t s) {
+  if (a.M <= 0) return;
+  hipLaunchKernelGGL(bottom_mlp_fwd_kernel, dim3((a.M + TM - 1) / TM), dim3(256), BOT_LDS, s, a);
+  TDFO_CHECK_HIP(hipGetLastError());
+}
+
+}  // namespace tdfo

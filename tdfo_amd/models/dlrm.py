@@ -349,6 +349,15 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
         self.x0 = act_in(self.bottom_layers[0])
         self.bot_in = [self.x0] + [act_in(L) for L in self.bottom_layers[1:]]
         self.h_out = z(B, D)
+        # the default bottom stack forward as one fused launch (GPU; bitwise
+        # the per-layer GEMMs; TDFO_FUSED_BOTTOM=0 keeps those)
+        Lb = self.bottom_layers
+        self._fused_bottom = (
+            dev.type == "cuda" and len(Lb) == 3 and D == Lb[2].out
+            and os.environ.get("TDFO_FUSED_BOTTOM", "1") != "0"
+            and Lb[0].in_k == Lb[0].wcols and not Lb[1].bias_in_k and not Lb[2].bias_in_k
+            and Lb[1].in_k == Lb[0].out and Lb[2].in_k == Lb[1].out
+            and ops.bottom_mlp_fwd_ok(Lb[0].in_k, Lb[0].out, Lb[1].out, Lb[2].out))
         self.bot_grad = [z(B, L.out) for L in self.bottom_layers]
         self.top_in = [act_in(L) for L in self.top_layers]
         self.t_out = z(B, self.head_k)
@@ -819,6 +828,15 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
             self._run_stage(kind, fn)
 
     def _s_bottom_fwd(self):
+        if self._fused_bottom:
+            # the default 3-layer stack in one launch (csrc/kernels/mlp_fused.hip)
+            Ls = self.bottom_layers
+            bias = [None if L.bias_in_k else self.fp.param(L.name + ".w")[:, L.bcol] for L in Ls]
+            ops.bottom_mlp_fwd(self.bot_in[0], self.fp.bf16(Ls[0].name + ".w"),
+                               self.fp.bf16(Ls[1].name + ".w"), self.fp.bf16(Ls[2].name + ".w"),
+                               bias[0], bias[1], bias[2], self.bot_in[1], self.bot_in[2],
+                               self.h_out)
+            return
         n = len(self.bottom_layers)
         for i, L in enumerate(self.bottom_layers):
             out = self.bot_in[i + 1][:, :L.out] if i + 1 < n else self.h_out

@@ -143,6 +143,9 @@ class StreamGraphsMixin:
                     ops.stamp(stamp[0], stamp[1], names.index(name), len(names), 1)
             graphs[name] = gr
         if composed:
+            # (the ~20-us idle at every step boundary is the graph launch
+            # boundary itself: dropping this wait measured the same,
+            # 0.429-0.432 vs 0.431-0.434 ms/step, profiles/r05/notes.md)
             head = [("wait", ev_copy)] if self._bstg is not None else []
             graphs["M"] = ops.ComposedGraph(head + [("graph", graphs["M1"]), ("wait", ev[1]),
                                                     ("graph", graphs["M2"]), ("record", ev[2]),

@@ -21,6 +21,19 @@ def _gpu(t: torch.Tensor) -> bool:
     return t.is_cuda
 
 
+def bottom_mlp_fwd_ok(k0: int, n0: int, n1: int, n2: int) -> bool:
+    """The fused bottom-MLP forward covers this stack (csrc/kernels/mlp_fused.hip)."""
+    return bool(native_available() and _native().bottom_mlp_fwd_ok(int(k0), int(n0), int(n1),
+                                                                    int(n2)))
+
+
+def bottom_mlp_fwd(x, w0, w1, w2, b0, b1, b2, y0, y1, y2):
+    """Three Linear + ReLU layers in one launch (GPU only): y0 = relu(x w0^T
+    (+ b0)), y1 = relu(y0 w1^T + b1), y2 = relu(y1 w2^T + b2), the first K
+    columns of each weight; bitwise equal to three ``gemm`` calls."""
+    _native().bottom_mlp_fwd(x, w0, w1, w2, b0, b1, b2, y0, y1, y2)
+
+
 def gemm(a, a_col, b, b_col, bias=None, relu=False, mask=None, out=None, out32=None, splits=1,
          mul=None, add=None, out2=None, ldc32=0, csum_col=-1):
     """C = A B (+ epilogue). out32: fp32 split-K slabs [splits][M][ldc32]

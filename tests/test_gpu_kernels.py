@@ -331,6 +331,32 @@ def test_embedding_bwd_onehot_segsort(B, skew, opt):
     assert (res[0][0] - We).abs().max() < 1e-4 * max(1.0, We.abs().max().item())
 
 
+@pytest.mark.parametrize("B", [8192, 1000])
+def test_fused_bottom_mlp_matches_per_layer_gemms(B):
+    """The fused bottom-MLP forward (one launch, activations chained through
+    LDS) writes bitwise the same three activations as the per-layer GEMMs,
+    including a batch that is not a multiple of the 32-row tile."""
+    from tdfo_amd.models.dlrm import DLRMConfig, DLRMTrainer
+
+    cfg = DLRMConfig(table_rows=[1000, 20, 5000])
+    tr = DLRMTrainer(cfg, B, DEV)
+    assert tr._fused_bottom
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(B, 13, generator=g)
+    tr.x0[:, :13] = x.to(DEV, torch.bfloat16)
+    outs = []
+    for fused in (True, False):
+        tr._fused_bottom = fused
+        for t in (tr.bot_in[1], tr.bot_in[2], tr.h_out):
+            t[:, : t.shape[1] - (64 if t is not tr.h_out else 0)].fill_(7.0)
+        tr._s_bottom_fwd()
+        torch.cuda.synchronize()
+        outs.append([tr.bot_in[1].clone(), tr.bot_in[2].clone(), tr.h_out.clone()])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    assert float(outs[0][2].float().abs().sum()) > 0
+
+
 def test_embedding_dense_grad_replicated_tables():
     """The replicated tables' backward at W > 1 (dense fp32 gradient, one id
     per bag, per-table LDS sort): the tiny tables' runs span tens of chunks
