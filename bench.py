@@ -28,6 +28,29 @@ import subprocess
 import sys
 import time
 
+
+def _one_gpu_run(argv) -> bool:
+    """One process on one GPU, not an emulated rank (peeked before argparse:
+    the runtime mode below must be set before any GPU call)."""
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        return False
+    pre = argparse.ArgumentParser(add_help=False)
+    pre.add_argument("--gpus", type=int, default=1)
+    pre.add_argument("--emulate-world", type=int, default=0)
+    a, _ = pre.parse_known_args(argv)
+    return a.gpus <= 1 and a.emulate_world <= 1
+
+
+# HIP runtime mode for the one-GPU per-stream composed graphs, read when the
+# runtime initialises: graph nodes dispatched at launch instead of from AQL
+# packets captured at instantiation. Measured (same box, x2-3): DLRM-1TB 0.414
+# vs 0.425-0.432 ms/step, DCN-v2 and TwoTower neutral. Not for rank
+# processes: it raises the host's issue cost per step (emulated W=8 340 -> 477
+# us, config 3 234 -> 492 us of a ~0.6-ms step), which multi-rank steps cannot
+# afford (profiles/r05/notes.md). An explicit setting wins.
+if _one_gpu_run(sys.argv[1:]):
+    os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+
 import torch
 
 

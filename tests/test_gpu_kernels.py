@@ -628,6 +628,24 @@ def test_dlrm_graph_replay_matches_eager(staged, one):
     assert torch.allclose(a.emb.tw_store.weight, b.emb.tw_store.weight, atol=1e-5)
 
 
+def test_dlrm_graph_replay_matches_eager_without_packet_capture():
+    """bench.py's one-GPU runtime mode (DEBUG_CLR_GRAPH_PACKET_CAPTURE=0: graph
+    nodes dispatched at launch) replays the composed per-stream graphs to the
+    same result as eager steps. A child process: the mode is read when the
+    HIP runtime initialises."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, DEBUG_CLR_GRAPH_PACKET_CAPTURE="0")
+    code = ("import tests.test_gpu_kernels as t; "
+            "t.test_dlrm_graph_replay_matches_eager(False, '1'); print('ok')")
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, env=env, capture_output=True,
+                       text=True, timeout=110)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-2000:]
+
+
 @pytest.mark.parametrize("mean", [False, True])
 def test_embedding_bwd_multihot_large(mean):
     """DCN-v2-shaped multi-hot backward (variable and empty bags, ~0.7M ids:
