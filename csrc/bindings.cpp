@@ -547,12 +547,18 @@ int64_t sync_event_create(int64_t mode) {
   return reinterpret_cast<int64_t>(e);
 }
 
-void sync_event_record(int64_t e) {
-  TDFO_HIP_OK(hipEventRecord(reinterpret_cast<hipEvent_t>(e), cur_stream()));
+// stream: a raw hipStream_t handle, or -1 for the current stream (the
+// explicit handle spares the host a torch stream-context switch per call)
+hipStream_t stream_or_cur(int64_t stream) {
+  return stream == -1 ? cur_stream() : reinterpret_cast<hipStream_t>(stream);
 }
 
-void sync_event_wait(int64_t e) {
-  TDFO_HIP_OK(hipStreamWaitEvent(cur_stream(), reinterpret_cast<hipEvent_t>(e), 0));
+void sync_event_record(int64_t e, int64_t stream) {
+  TDFO_HIP_OK(hipEventRecord(reinterpret_cast<hipEvent_t>(e), stream_or_cur(stream)));
+}
+
+void sync_event_wait(int64_t e, int64_t stream) {
+  TDFO_HIP_OK(hipStreamWaitEvent(stream_or_cur(stream), reinterpret_cast<hipEvent_t>(e), 0));
 }
 
 bool sync_event_query(int64_t e) {
@@ -628,8 +634,8 @@ int64_t graph_compose(std::vector<int64_t> kinds, std::vector<int64_t> handles) 
   return reinterpret_cast<int64_t>(ex);
 }
 
-void graph_exec_launch(int64_t ex) {
-  TDFO_HIP_OK(hipGraphLaunch(reinterpret_cast<hipGraphExec_t>(ex), cur_stream()));
+void graph_exec_launch(int64_t ex, int64_t stream) {
+  TDFO_HIP_OK(hipGraphLaunch(reinterpret_cast<hipGraphExec_t>(ex), stream_or_cur(stream)));
 }
 
 void graph_exec_upload(int64_t ex) {
@@ -1489,12 +1495,12 @@ TORCH_LIBRARY(tdfo, m) {
   });
   m.def("host_mailbox_alloc(int n) -> Tensor", host_mailbox_alloc);
   m.def("host_publish(Tensor value, Tensor(a!) seq, Tensor host, int slot) -> ()", host_publish);
-  m.def("sync_event_record(int e) -> ()", sync_event_record);
-  m.def("sync_event_wait(int e) -> ()", sync_event_wait);
+  m.def("sync_event_record(int e, int stream=-1) -> ()", sync_event_record);
+  m.def("sync_event_wait(int e, int stream=-1) -> ()", sync_event_wait);
   m.def("sync_event_destroy(int e) -> ()", sync_event_destroy);
   m.def("sync_event_query(int e) -> bool", sync_event_query);
   m.def("graph_compose(int[] kinds, int[] handles) -> int", graph_compose);
-  m.def("graph_exec_launch(int ex) -> ()", graph_exec_launch);
+  m.def("graph_exec_launch(int ex, int stream=-1) -> ()", graph_exec_launch);
   m.def("graph_exec_destroy(int ex) -> ()", graph_exec_destroy);
   m.def("graph_num_nodes(int g) -> int", graph_num_nodes);
   m.def("graph_exec_upload(int ex) -> ()", graph_exec_upload);

@@ -370,8 +370,7 @@ class MultiRankStreamsMixin:
         # launch order M, D, EC: a wait node binds to the latest record
         # enqueued before its graph's launch (see the module docstring)
         for k in ("M", "D", "EC"):
-            with torch.cuda.stream(s[k]):
-                g[k].replay()
+            g[k].replay(s[k])
         if self._rw_lagged:
             self.emb.rw_note_replay()           # D published the next batch's need
         mr["launched"] = True

@@ -152,6 +152,9 @@ class StreamGraphsMixin:
                                                     ("graph", graphs["M3"])])
             graphs["EA"] = ops.ComposedGraph([("graph", graphs["E1"]), ("record", ev[1]),
                                               ("graph", graphs["E2"])])
+            # the update with its wait / record as one launch
+            graphs["EU"] = ops.ComposedGraph([("wait", ev[2]), ("graph", graphs["E3"]),
+                                              ("record", ev[3])])
         ops.upload_graphs(graphs.values())
         torch.cuda.synchronize()
         cs = (torch.cuda.Stream(device=self.device) if ids_stream and self._insrc is None
@@ -201,7 +204,7 @@ class StreamGraphsMixin:
                 if stg is not None:
                     stg[0].copy_(dense, non_blocking=True)
                     stg[1].copy_(label.reshape(-1), non_blocking=True)
-                self._ms["ev_copy"].record(cs)
+            self._ms["ev_copy"].record(cs)
             se.wait_event(self._ms["ev_copy"])
             self.flush_pending()
             return True
@@ -228,16 +231,18 @@ class StreamGraphsMixin:
         # gain -- ran DCN-v2 at 2.40-2.42 vs 2.36-2.38 ms/step: the update and
         # lookup are HBM-bound and slow the GEMMs they overlap about as much
         # as they save, profiles/r05/notes.md)
-        with torch.cuda.stream(se):
-            if composed:
-                g["EA"].replay()             # records ev[1] inside
-            else:
+        if composed:
+            # (streams passed to the launches as raw handles: no host-side
+            # torch stream switches on the step's issue path)
+            g["EA"].replay(se)               # records ev[1] inside
+        else:
+            with torch.cuda.stream(se):
                 g["E1"].replay()
                 ev[1].record(se)
                 g["E2"].replay()
-            if self._ms.get("cstream") is not None:
-                self._ms["ev_e2"].record(se)
-                self._ms["e2_recorded"] = True
+        if self._ms.get("cstream") is not None:
+            self._ms["ev_e2"].record(se)
+            self._ms["e2_recorded"] = True
         if composed:
             g["M"].replay()                  # waits for ev[1], records ev[2] inside
         else:
@@ -262,10 +267,13 @@ class StreamGraphsMixin:
 
     def _ms_issue_e3(self):
         g, se, ev = self._ms["graphs"], self._ms["stream"], self._ms["events"]
-        with torch.cuda.stream(se):
-            se.wait_event(ev[2])             # embedding gradients ready
-            g["E3"].replay()
-            ev[3].record(se)
+        if "EU" in g:
+            g["EU"].replay(se)               # waits ev[2], records ev[3] inside
+        else:
+            with torch.cuda.stream(se):
+                se.wait_event(ev[2])         # embedding gradients ready
+                g["E3"].replay()
+                ev[3].record(se)
         self._ms["pending_e3"] = False
 
     def flush_pending(self):

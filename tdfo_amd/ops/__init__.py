@@ -57,18 +57,12 @@ class SyncEvent:
         self._pinned = False     # referenced by a ComposedGraph's event node
 
     def record(self, stream=None):
-        if stream is not None:
-            with torch.cuda.stream(stream):
-                _native().sync_event_record(self._h)
-        else:
-            _native().sync_event_record(self._h)
+        # (an explicit stream goes down as its raw handle: no torch stream
+        # context switch on the host per call)
+        _native().sync_event_record(self._h, -1 if stream is None else stream.cuda_stream)
 
     def wait(self, stream=None):
-        if stream is not None:
-            with torch.cuda.stream(stream):
-                _native().sync_event_wait(self._h)
-        else:
-            _native().sync_event_wait(self._h)
+        _native().sync_event_wait(self._h, -1 if stream is None else stream.cuda_stream)
 
     def query(self) -> bool:
         """True once the work before the latest record has completed."""
@@ -120,8 +114,9 @@ class ComposedGraph:
             self._keep.append(obj)
         self._ex = int(_native().graph_compose(kinds, handles))
 
-    def replay(self):
-        _native().graph_exec_launch(self._ex)
+    def replay(self, stream=None):
+        """Launch on ``stream`` (default: the current stream)."""
+        _native().graph_exec_launch(self._ex, -1 if stream is None else stream.cuda_stream)
 
     def __del__(self):
         try:
