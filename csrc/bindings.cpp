@@ -561,6 +561,18 @@ void sync_event_wait(int64_t e, int64_t stream) {
   TDFO_HIP_OK(hipStreamWaitEvent(stream_or_cur(stream), reinterpret_cast<hipEvent_t>(e), 0));
 }
 
+// dst <- src (same dtype / size, both contiguous on this device) as one async
+// copy on an explicit stream (no torch stream-context switch on the host)
+void copy_on(const Tensor& dst, const Tensor& src, int64_t stream) {
+  check_dev(dst, "dst");
+  check_dev(src, "src");
+  TORCH_CHECK(dst.scalar_type() == src.scalar_type() && dst.numel() == src.numel() &&
+              dst.is_contiguous() && src.is_contiguous(), "copy_on: same dtype / size, contiguous");
+  if (dst.numel() == 0) return;
+  TDFO_HIP_OK(hipMemcpyAsync(dst.data_ptr(), src.data_ptr(), dst.nbytes(), hipMemcpyDeviceToDevice,
+                             stream_or_cur(stream)));
+}
+
 bool sync_event_query(int64_t e) {
   const hipError_t r = hipEventQuery(reinterpret_cast<hipEvent_t>(e));
   if (r == hipErrorNotReady) return false;
@@ -1496,6 +1508,7 @@ TORCH_LIBRARY(tdfo, m) {
   m.def("host_mailbox_alloc(int n) -> Tensor", host_mailbox_alloc);
   m.def("host_publish(Tensor value, Tensor(a!) seq, Tensor host, int slot) -> ()", host_publish);
   m.def("sync_event_record(int e, int stream=-1) -> ()", sync_event_record);
+  m.def("copy_on(Tensor(a!) dst, Tensor src, int stream=-1) -> ()", copy_on);
   m.def("sync_event_wait(int e, int stream=-1) -> ()", sync_event_wait);
   m.def("sync_event_destroy(int e) -> ()", sync_event_destroy);
   m.def("sync_event_query(int e) -> bool", sync_event_query);

@@ -199,11 +199,15 @@ class StreamGraphsMixin:
                 # the previous step's MLP graph read the staging in M1, before
                 # its ev[2] record (a wait on a never-recorded event is a no-op)
                 cs.wait_event(self._ms["events"][2])
-            with torch.cuda.stream(cs):
-                self.ids.copy_(ids, non_blocking=True)
-                if stg is not None:
-                    stg[0].copy_(dense, non_blocking=True)
-                    stg[1].copy_(label.reshape(-1), non_blocking=True)
+            ops.copy_on(self.ids, ids, cs)
+            if stg is not None:
+                for dst, src in ((stg[0], dense), (stg[1], label.reshape(-1))):
+                    if (src.dtype == dst.dtype and src.is_contiguous()
+                            and src.numel() == dst.numel()):
+                        ops.copy_on(dst, src, cs)
+                    else:                      # (a converting copy)
+                        with torch.cuda.stream(cs):
+                            dst.copy_(src.reshape(dst.shape), non_blocking=True)
             self._ms["ev_copy"].record(cs)
             se.wait_event(self._ms["ev_copy"])
             self.flush_pending()

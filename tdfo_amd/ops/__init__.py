@@ -84,6 +84,12 @@ class SyncEvent:
             pass
 
 
+def copy_on(dst, src, stream=None):
+    """dst <- src (same dtype / size, contiguous, GPU) as one async device
+    copy on ``stream`` (default: the current one), passed as its raw handle."""
+    _native().copy_on(dst, src, -1 if stream is None else stream.cuda_stream)
+
+
 class _null:
     def __enter__(self):
         return self
