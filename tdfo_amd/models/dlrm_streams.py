@@ -118,10 +118,15 @@ class StreamGraphsMixin:
         # steps (that boundary idled it ~23-31 us per step,
         # profiles/r03/s3/w1_timeline/)
         self._bstg = None
+        # (Rejected, round 5: staging on the batch producer's own copy stream
+        # too, so the batch load stays inside the MLP graph instead of an eager
+        # launch between two graph launches -- 0.433 vs 0.411-0.414 ms/step,
+        # profiles/r05/notes.md)
         if composed and ids_stream and self._insrc is None:
             self._bstg = (torch.zeros(self.B, self.cfg.num_dense, device=self.device),
                           torch.zeros(self.B, device=self.device))
         ev_copy = ops.SyncEvent(2)
+        ev_stg = ops.SyncEvent(2)
         plan = self._ms_plan()
         se = torch.cuda.Stream(device=self.device)
         pool = torch.cuda.graph_pool_handle()
@@ -146,7 +151,7 @@ class StreamGraphsMixin:
             # (the ~20-us idle at every step boundary is the graph launch
             # boundary itself: dropping this wait measured the same,
             # 0.429-0.432 vs 0.431-0.434 ms/step, profiles/r05/notes.md)
-            head = [("wait", ev_copy)] if self._bstg is not None else []
+            head = [("wait", ev_stg)] if self._bstg is not None else []
             graphs["M"] = ops.ComposedGraph(head + [("graph", graphs["M1"]), ("wait", ev[1]),
                                                     ("graph", graphs["M2"]), ("record", ev[2]),
                                                     ("graph", graphs["M3"])])
@@ -165,6 +170,7 @@ class StreamGraphsMixin:
         self._ms = {"graphs": graphs, "stream": se, "plan": plan, "composed": composed,
                     "names": names,
                     "cstream": cs, "ev_e2": ops.SyncEvent(2), "ev_copy": ev_copy,
+                    "ev_stg": ev_stg,
                     "src_cs": src_cs, "pending_e3": False,
                     "defer_e3": src_cs and os.environ.get("TDFO_DEFER_E3", "1") != "0",
                     "e2_recorded": False, "events": ev}
@@ -194,13 +200,14 @@ class StreamGraphsMixin:
             # already signalled instead of queueing the copy behind the update
             if self._ms["e2_recorded"]:
                 cs.wait_event(self._ms["ev_e2"])
+            ops.copy_on(self.ids, ids, cs)
+            self._ms["ev_copy"].record(cs)     # the ids: the embedding stream's edge
             stg = self._bstg
             if stg is not None:
                 # the previous step's MLP graph read the staging in M1, before
-                # its ev[2] record (a wait on a never-recorded event is a no-op)
+                # its ev[2] record (a wait on a never-recorded event is a no-op);
+                # after the ids' record, so the next lookup does not wait for it
                 cs.wait_event(self._ms["events"][2])
-            ops.copy_on(self.ids, ids, cs)
-            if stg is not None:
                 for dst, src in ((stg[0], dense), (stg[1], label.reshape(-1))):
                     if (src.dtype == dst.dtype and src.is_contiguous()
                             and src.numel() == dst.numel()):
@@ -208,7 +215,7 @@ class StreamGraphsMixin:
                     else:                      # (a converting copy)
                         with torch.cuda.stream(cs):
                             dst.copy_(src.reshape(dst.shape), non_blocking=True)
-            self._ms["ev_copy"].record(cs)
+                self._ms["ev_stg"].record(cs)  # the MLP graph's head waits for this
             se.wait_event(self._ms["ev_copy"])
             self.flush_pending()
             return True
