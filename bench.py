@@ -41,15 +41,12 @@ def _one_gpu_run(argv) -> bool:
     return a.gpus <= 1 and a.emulate_world <= 1
 
 
-# HIP runtime mode for the one-GPU per-stream composed graphs, read when the
-# runtime initialises: graph nodes dispatched at launch instead of from AQL
-# packets captured at instantiation. Measured (same box, x2-3): DLRM-1TB 0.414
-# vs 0.425-0.432 ms/step, DCN-v2 and TwoTower neutral. Not for rank
-# processes: it raises the host's issue cost per step (emulated W=8 340 -> 477
-# us, config 3 234 -> 492 us of a ~0.6-ms step), which multi-rank steps cannot
-# afford (profiles/r05/notes.md). An explicit setting wins.
-if _one_gpu_run(sys.argv[1:]):
-    os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+# HIP runtime mode for one-GPU runs (utils/guarded.py: measured gain, why
+# not for ranks); set before any GPU call and reported in the JSON line.
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from tdfo_amd.utils.guarded import one_gpu_runtime_mode  # noqa: E402 (no GPU work)
+
+RUNTIME_MODE = one_gpu_runtime_mode(_one_gpu_run(sys.argv[1:]))
 
 import torch
 
@@ -404,6 +401,7 @@ def main(argv=None):
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(self_launch(args, argv))
     from tdfo_amd.utils import supervise
+    from tdfo_amd.utils.supervise import emit_result
     if (int(os.environ.get("WORLD_SIZE", "1")) > 1 and not supervise.is_child()
             and os.environ.get("TDFO_SUPERVISE", "1") == "1"):
         # every rank: a GPU-free supervisor runs the rank code as a child; if
@@ -497,7 +495,7 @@ def main(argv=None):
                "instep": "a fresh batch per step generated inside the step graphs",
                "pool": f"a pool of {args.pool} pre-generated device batches, cycled",
                "host": "C++ host generator + pinned copy-stream H2D"}[args.data]
-        print(json.dumps({
+        emit_result(json.dumps({
             "metric": f"examples/sec (whole node) {mname} on Criteo-{rname}-shaped synthetic",
             "value": round(value, 1), "unit": "examples/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
@@ -508,6 +506,7 @@ def main(argv=None):
             "sol_ms": round(sol["sol_ms"], 4),
             "frac_of_sol": round(sol["sol_ms"] / ms, 3),
             "preheat_ms": args.preheat_ms,
+            "hip_graph_packet_capture": RUNTIME_MODE,
             "comm_path": comm_path,
             "attempt": int(os.environ.get("TDFO_ATTEMPT", "0")),
             "ranks_consistent": consistent if world > 1 else None,
@@ -518,7 +517,7 @@ def main(argv=None):
                        "global_batch": B * world, "seq_len": None,
                        "parallelism": parallelism(tr.plan, world),
                        "tables": f"criteo-{args.rows}", "embedding_dim": cfg.embedding_dim,
-                       "per_gpu_batch": B}}), flush=True)
+                       "per_gpu_batch": B}}))
     r["loop"].close()
     reset()
 

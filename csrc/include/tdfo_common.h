@@ -43,6 +43,28 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
+// Full-wave sum on the DPP path (no LDS round trips): two quad swaps, the
+// half-row and row mirrors leave every lane of a 16-lane row holding the row's
+// sum; row_bcast15 / row_bcast31 fold rows 0..2 into row 3, and lane 63's value
+// is broadcast through an SGPR. ~7 dependent VALU ops instead of 6 ds_bpermute
+// round trips (the embedding update reduces once per unique row, in series).
+// Summation order differs from wave_sum: same math, different rounding.
+template <int CTRL, int ROWS>
+__device__ __forceinline__ float dpp_f(float x) {
+  return __builtin_bit_cast(
+      float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, ROWS, 0xf, false));
+}
+
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v += dpp_f<0xb1, 0xf>(v);    // quad_perm [1,0,3,2]
+  v += dpp_f<0x4e, 0xf>(v);    // quad_perm [2,3,0,1]
+  v += dpp_f<0x141, 0xf>(v);   // row_half_mirror
+  v += dpp_f<0x140, 0xf>(v);   // row_mirror
+  v += dpp_f<0x142, 0xa>(v);   // row_bcast15 into rows 1, 3
+  v += dpp_f<0x143, 0xc>(v);   // row_bcast31 into rows 2, 3
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), 63));
+}
+
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));

@@ -269,6 +269,11 @@ __global__ __launch_bounds__(256) void emb_keys_kernel(const EmbBwdArgs a, K* __
 //   per pass: digit ranks inside a wave by ballot matching (6 ballots per
 //   element), per-(digit, slot, wave) counts, one block-wide exclusive scan
 //   over them in (digit, slot, wave) order, scatter into LDS, re-read.
+//   The counters sit at (slot, wave) * (BINS + 1) + digit: a wave's count
+//   writes and offset reads (one digit per lane) hit distinct banks. In the
+//   digit-major order they were 128 words apart, one bank for every digit of
+//   an instruction (~40-way conflicts on random ids): 43 us per 26 x 8192
+//   table sort (scripts/emb_iso.py, profiles/r06/).
 constexpr int SEG_MAX = 8192;
 constexpr int SEG_THREADS = 1024;
 constexpr int SEG_K = SEG_MAX / SEG_THREADS;        // elements per thread
@@ -284,6 +289,81 @@ constexpr int SEG_BINS = 1 << SEG_BITS;
 constexpr int SEG_WAVES = SEG_THREADS / 64;
 constexpr int SEG_CNT = SEG_BINS * SEG_K * SEG_WAVES;   // 8192 counters
 
+// Stable LSD radix sort of the block's SK * 1024 (key, val) pairs held in
+// registers (element i = k * 1024 + tid in slot k), over the low `bits` bits.
+// Only slots k < skn hold entries (block-uniform); the others keep the
+// all-ones sentinel and are skipped. Ends with the sorted pairs in registers.
+template <int SK>
+__device__ __forceinline__ void seg_lsd_sort(uint32_t (&key)[SK], uint32_t (&val)[SK], int bits,
+                                             int skn, uint32_t* skey, uint32_t* sval,
+                                             uint32_t* cnt, uint32_t* wsum) {
+  constexpr int CNT = SEG_BINS * SK * SEG_WAVES;     // logical counters
+  constexpr int KW = SK * SEG_WAVES;                  // (slot, wave) pairs
+  constexpr int CPAD = KW * (SEG_BINS + 1);           // padded physical size
+  constexpr int PER = CNT / SEG_THREADS;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  for (int shift = 0; shift < bits; shift += SEG_BITS) {
+    for (int c = tid; c < CPAD; c += SEG_THREADS) cnt[c] = 0;
+    __syncthreads();
+    uint32_t rank[SK];
+    int dig[SK];
+#pragma unroll
+    for (int k = 0; k < SK; ++k) {
+      if (k >= skn) break;
+      // invalid slots carry the all-ones key: digit 63 in every pass
+      const int d = (int)((key[k] >> shift) & (SEG_BINS - 1));
+      uint64_t peers = ~0ull;
+#pragma unroll
+      for (int b = 0; b < SEG_BITS; ++b) {
+        const uint64_t bal = __ballot((d >> b) & 1);
+        peers &= ((d >> b) & 1) ? bal : ~bal;
+      }
+      rank[k] = (uint32_t)__popcll(peers & lt);
+      dig[k] = d;
+      if ((peers & lt) == 0) cnt[(k * SEG_WAVES + w) * (SEG_BINS + 1) + d] = (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+    // exclusive scan of cnt in (digit, slot, wave) order: PER logical entries
+    // per thread, i = tid * PER + q -> digit i / KW, pair i % KW
+    auto phys = [&](int i) { return (i % KW) * (SEG_BINS + 1) + i / KW; };
+    uint32_t loc[PER];
+    uint32_t run = 0;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+      loc[q] = run;
+      run += cnt[phys(tid * PER + q)];
+    }
+    uint32_t incl = run;                             // wave inclusive scan of the totals
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t o = (uint32_t)__shfl_up((int)incl, off);
+      if (lane >= off) incl += o;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    uint32_t base = incl - run;
+    for (int q = 0; q < w; ++q) base += wsum[q];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) cnt[phys(tid * PER + q)] = base + loc[q];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < SK; ++k) {
+      if (k >= skn) break;
+      const uint32_t dst = cnt[(k * SEG_WAVES + w) * (SEG_BINS + 1) + dig[k]] + rank[k];
+      skey[dst] = key[k];
+      sval[dst] = val[k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < SK; ++k) {
+      if (k >= skn) break;
+      key[k] = skey[k * SEG_THREADS + tid];
+      val[k] = sval[k * SEG_THREADS + tid];
+    }
+    __syncthreads();
+  }
+}
+
 // SK: elements per thread (tables of <= SK * 1024 ids; 2 for small batches:
 // a quarter of the counters to clear and scan per pass)
 template <typename K, bool SORTED_G, int SK = SEG_K>
@@ -291,10 +371,9 @@ __global__ __launch_bounds__(SEG_THREADS) void emb_segsort_kernel(
     const EmbBwdArgs a, K* __restrict__ keys_out, int32_t* __restrict__ vals_out,
     int64_t* __restrict__ goff, float* __restrict__ gscale, int32_t* __restrict__ tail_count,
     int32_t* __restrict__ pos) {
-  constexpr int CNT = SEG_BINS * SK * SEG_WAVES;
   __shared__ uint32_t skey[SK * SEG_THREADS];
   __shared__ uint32_t sval[SK * SEG_THREADS];
-  __shared__ uint32_t cnt[CNT];
+  __shared__ uint32_t cnt[SK * SEG_WAVES * (SEG_BINS + 1)];
   __shared__ uint32_t wsum[SEG_WAVES];
   __shared__ uint32_t smax[SEG_WAVES];
   const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -330,62 +409,7 @@ __global__ __launch_bounds__(SEG_THREADS) void emb_segsort_kernel(
   uint32_t bmax = 0;
   for (int q = 0; q < SEG_WAVES; ++q) bmax = max(bmax, smax[q]);
   const int bits = bmax ? 32 - __clz(bmax) : 1;
-  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-  for (int shift = 0; shift < bits; shift += SEG_BITS) {
-    for (int c = tid; c < CNT; c += SEG_THREADS) cnt[c] = 0;
-    __syncthreads();
-    uint32_t rank[SK];
-    int dig[SK];
-#pragma unroll
-    for (int k = 0; k < SK; ++k) {
-      // invalid slots carry the all-ones key: digit 63 in every pass
-      const int d = (int)((key[k] >> shift) & (SEG_BINS - 1));
-      uint64_t peers = ~0ull;
-#pragma unroll
-      for (int b = 0; b < SEG_BITS; ++b) {
-        const uint64_t bal = __ballot((d >> b) & 1);
-        peers &= ((d >> b) & 1) ? bal : ~bal;
-      }
-      rank[k] = (uint32_t)__popcll(peers & lt);
-      dig[k] = d;
-      if ((peers & lt) == 0) cnt[(d * SK + k) * SEG_WAVES + w] = (uint32_t)__popcll(peers);
-    }
-    __syncthreads();
-    // exclusive scan of cnt in (digit, slot, wave) order: 8 entries per thread
-    uint32_t loc[CNT / SEG_THREADS];
-    uint32_t run = 0;
-#pragma unroll
-    for (int q = 0; q < CNT / SEG_THREADS; ++q) {
-      loc[q] = run;
-      run += cnt[tid * (CNT / SEG_THREADS) + q];
-    }
-    uint32_t incl = run;                             // wave inclusive scan of the totals
-    for (int off = 1; off < 64; off <<= 1) {
-      const uint32_t o = (uint32_t)__shfl_up((int)incl, off);
-      if (lane >= off) incl += o;
-    }
-    if (lane == 63) wsum[w] = incl;
-    __syncthreads();
-    uint32_t base = incl - run;
-    for (int q = 0; q < w; ++q) base += wsum[q];
-#pragma unroll
-    for (int q = 0; q < CNT / SEG_THREADS; ++q)
-      cnt[tid * (CNT / SEG_THREADS) + q] = base + loc[q];
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < SK; ++k) {
-      const uint32_t dst = cnt[(dig[k] * SK + k) * SEG_WAVES + w] + rank[k];
-      skey[dst] = key[k];
-      sval[dst] = val[k];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < SK; ++k) {
-      key[k] = skey[k * SEG_THREADS + tid];
-      val[k] = sval[k * SEG_THREADS + tid];
-    }
-    __syncthreads();
-  }
+  seg_lsd_sort<SK>(key, val, bits, SK, skey, sval, cnt, wsum);
   const K kb = (K)a.row_offset[t];
   const int64_t go = a.grad_off[t];
 #pragma unroll
@@ -399,6 +423,148 @@ __global__ __launch_bounds__(SEG_THREADS) void emb_segsort_kernel(
         goff[s0 + i] = (int64_t)val[k] * a.grad_stride + go;
         if (gscale) gscale[s0 + i] = a.psw ? a.psw[s0 + val[k]] : 1.f;
       }
+    }
+  }
+}
+
+// One-hot, one run per table, split by value range over NB blocks per table
+// (MSD split + LSD in LDS). The single-block sort above is latency-bound on
+// T CUs: ballot ranking of 8 slots x 5 passes for a 26-bit table, 35 us for
+// 26 x 8192 ids with the rest of the GPU idle. Here every block reads the
+// table's B ids, takes the table's largest id, and keeps the ids of its value
+// range (bucket = floor(id * NB / (max + 1)) in f32: monotone, so equal ids
+// share a bucket and buckets are ordered), compacted in position order; the
+// ids of lower buckets give its output offset. It LSD-sorts (id - its
+// smallest id) over only the bits that span, touching only the slots that
+// hold entries: a uniform table becomes NB sorts of ~B / NB ids (one slot,
+// 4 passes) on NB CUs; a table of a few rows, a few buckets of one id each
+// and no pass at all. Skewed ids degrade to one block holding most of the
+// table, i.e. the single-block sort. Same stable order, so the same bits.
+template <typename K, int NB>
+__global__ __launch_bounds__(SEG_THREADS) void emb_segsort_split_kernel(
+    const EmbBwdArgs a, K* __restrict__ keys_out, int32_t* __restrict__ vals_out,
+    int64_t* __restrict__ goff, float* __restrict__ gscale, int32_t* __restrict__ tail_count) {
+  constexpr int SK = SEG_K;
+  constexpr int KW = SK * SEG_WAVES;
+  __shared__ uint32_t skey[SK * SEG_THREADS];
+  __shared__ uint32_t sval[SK * SEG_THREADS];
+  __shared__ uint32_t cnt[KW * (SEG_BINS + 1)];
+  __shared__ uint32_t wsum[SEG_WAVES];
+  __shared__ uint32_t red[2][SEG_WAVES];
+  __shared__ uint32_t moff[KW];                   // (slot, wave) compaction offsets
+  const int t = blockIdx.x / NB, bk = blockIdx.x - t * NB;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (blockIdx.x == 0 && tid == 0) {              // read by later kernels
+    tail_count[0] = 0;
+    tail_count[1] = 0;
+  }
+  const int n = a.B;
+  const int64_t s0 = (int64_t)t * a.B;
+  const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  uint32_t key[SK], val[SK];
+  uint32_t kmax = 0;
+#pragma unroll
+  for (int k = 0; k < SK; ++k) {
+    const int i = k * SEG_THREADS + tid;
+    key[k] = i < n ? (uint32_t)a.indices[s0 + i] : 0u;
+    if (i < n) kmax = max(kmax, key[k]);
+  }
+  for (int off = 32; off > 0; off >>= 1) kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, off));
+  if (lane == 0) red[0][w] = kmax;
+  __syncthreads();
+  uint32_t tmax = 0;
+  for (int q = 0; q < SEG_WAVES; ++q) tmax = max(tmax, red[0][q]);
+  const float scale = (float)NB / ((float)tmax + 1.f);
+  // own bucket's entries: rank inside the wave, per-(slot, wave) counts, and
+  // the count of lower buckets' entries (this block's output offset)
+  bool mine[SK];
+  uint32_t myrank[SK];
+  uint32_t below = 0;
+#pragma unroll
+  for (int k = 0; k < SK; ++k) {
+    const int i = k * SEG_THREADS + tid;
+    const int b = i < n ? min(NB - 1, (int)((float)key[k] * scale)) : NB;
+    mine[k] = b == bk;
+    const uint64_t m = __ballot(mine[k]);
+    below += (uint32_t)__popcll(__ballot(b < bk));
+    myrank[k] = (uint32_t)__popcll(m & lt);
+    if (lane == 0) moff[k * SEG_WAVES + w] = (uint32_t)__popcll(m);
+  }
+  if (lane == 0) red[1][w] = below;
+  __syncthreads();
+  // exclusive scan of the KW = 128 (slot, wave) counts by waves 0 and 1
+  uint32_t v = 0, incl = 0;
+  if (tid < KW) {
+    v = moff[tid];
+    incl = v;
+    for (int off = 1; off < 64; off <<= 1) {
+      const uint32_t o = (uint32_t)__shfl_up((int)incl, off);
+      if (lane >= off) incl += o;
+    }
+    if (lane == 63) wsum[w] = incl;
+  }
+  uint32_t off = 0;
+  for (int q = 0; q < SEG_WAVES; ++q) off += red[1][q];
+  __syncthreads();
+  const int nb = (int)(wsum[0] + wsum[1]);        // entries in this bucket
+  if (tid < KW) moff[tid] = incl - v + (w == 1 ? wsum[0] : 0u);
+  __syncthreads();
+  if (nb == 0) return;                            // (block-uniform)
+#pragma unroll
+  for (int k = 0; k < SK; ++k) {
+    if (mine[k]) {
+      const uint32_t d = moff[k * SEG_WAVES + w] + myrank[k];
+      skey[d] = key[k];
+      sval[d] = (uint32_t)(k * SEG_THREADS + tid);
+    }
+  }
+  __syncthreads();
+  const int skn = (nb + SEG_THREADS - 1) / SEG_THREADS;
+  uint32_t lo = 0xffffffffu, hi = 0;
+#pragma unroll
+  for (int k = 0; k < SK; ++k) {
+    const int i = k * SEG_THREADS + tid;
+    if (i < nb) {
+      key[k] = skey[i];
+      val[k] = sval[i];
+      lo = min(lo, key[k]);
+      hi = max(hi, key[k]);
+    } else {
+      key[k] = 0xffffffffu;
+      val[k] = 0;
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) {
+    lo = min(lo, (uint32_t)__shfl_xor((int)lo, o));
+    hi = max(hi, (uint32_t)__shfl_xor((int)hi, o));
+  }
+  if (lane == 0) {
+    red[0][w] = lo;
+    red[1][w] = hi;
+  }
+  __syncthreads();
+  uint32_t bmin = 0xffffffffu, bmax = 0;
+  for (int q = 0; q < SEG_WAVES; ++q) {
+    bmin = min(bmin, red[0][q]);
+    bmax = max(bmax, red[1][q]);
+  }
+#pragma unroll
+  for (int k = 0; k < SK; ++k)
+    if (k * SEG_THREADS + tid < nb) key[k] -= bmin;
+  const uint32_t span = bmax - bmin;
+  const int bits = span ? 32 - __clz(span) : 0;   // one id only: already sorted
+  seg_lsd_sort<SK>(key, val, bits, skn, skey, sval, cnt, wsum);
+  const K kb = (K)a.row_offset[t] + (K)bmin;
+  const int64_t go = a.grad_off[t];
+#pragma unroll
+  for (int k = 0; k < SK; ++k) {
+    const int i = k * SEG_THREADS + tid;
+    if (i < nb) {
+      const int64_t p = s0 + off + i;
+      keys_out[p] = kb + (K)key[k];
+      vals_out[p] = (int32_t)(s0 + val[k]);
+      goff[p] = (int64_t)val[k] * a.grad_stride + go;
+      if (gscale) gscale[p] = a.psw ? a.psw[s0 + val[k]] : 1.f;
     }
   }
 }
@@ -590,7 +756,7 @@ __device__ __forceinline__ void update_row(const EmbBwdArgs& a, const OptScalars
         g[u] = acc[u] + a.weight_decay * wv[u];
         sq += act ? g[u] * g[u] : 0.f;
       }
-      sq = wave_sum(sq) * (1.f / (float)D);
+      sq = wave_sum_dpp(sq) * (1.f / (float)D);
       const float stv = st_row + sq;
       if (lane == 0) a.state1[row] = stv;
       const float mult = o.lr / (sqrtf(stv) + a.eps);
@@ -1009,6 +1175,13 @@ void dense_update_dispatch(const EmbBwdArgs& a, int64_t rows, const float* g, fl
 }
 
 int g_emb_segsort = 1;   // one-hot batches: per-table LDS sort (0: device-wide radix sort)
+// one-hot, one run, B > 2048: the value-range split sort (TDFO_SEG_SPLIT=0: one
+// block per table)
+constexpr int SEG_SPLIT = 8;
+const int g_emb_seg_split = [] {
+  const char* e = getenv("TDFO_SEG_SPLIT");
+  return e ? atoi(e) : 1;
+}();
 
 // (Rejected, round 4: capping the fused update's grid so GEMM blocks get CUs
 // beside it, with the full or a half-chunk 94-VGPR update kernel that fits
@@ -1072,6 +1245,9 @@ void prep_impl(const EmbBwdArgs& a, const WsLayout& L, hipStream_t s) {
       if (a.B <= 2 * SEG_THREADS)
         hipLaunchKernelGGL((emb_segsort_kernel<K, true, 2>), dim3(a.T), dim3(SEG_THREADS), 0, s, a,
                            keys_out, vals_out, goff, gscale, tcount, (int32_t*)nullptr);
+      else if (g_emb_seg_split)
+        hipLaunchKernelGGL((emb_segsort_split_kernel<K, SEG_SPLIT>), dim3(a.T * SEG_SPLIT),
+                           dim3(SEG_THREADS), 0, s, a, keys_out, vals_out, goff, gscale, tcount);
       else
         hipLaunchKernelGGL((emb_segsort_kernel<K, true>), dim3(a.T), dim3(SEG_THREADS), 0, s, a,
                            keys_out, vals_out, goff, gscale, tcount, (int32_t*)nullptr);

@@ -4,7 +4,8 @@
 model_parallel=true shards the item table over ranks (DMP); false replicates it (DDP)."""
 import _path  # noqa: F401
 from _bootstrap import config
+from tdfo_amd.utils.guarded import supervised
 from tdfo_amd.train.bert4rec import run
 
 if __name__ == "__main__":
-    run(config(__file__))
+    supervised(lambda: run(config(__file__)))

@@ -5,7 +5,8 @@ larger ones owner-partitioned row-wise (sparse/planner.py "data_parallel"):
   python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 train_dp.py"""
 import _path  # noqa: F401
 from _bootstrap import config
+from tdfo_amd.utils.guarded import supervised
 from tdfo_amd.train.dlrm import run
 
 if __name__ == "__main__":
-    run(config(__file__), mode="dp")
+    supervised(lambda: run(config(__file__), mode="dp"))

@@ -4,7 +4,8 @@ parameter-server entry point collapsed into in-node table/row-wise sharding):
       (TDFO_CONFIG=config_1tb.toml or config_dcnv2.toml)"""
 import _path  # noqa: F401
 from _bootstrap import config
+from tdfo_amd.utils.guarded import supervised
 from tdfo_amd.train.dlrm import run
 
 if __name__ == "__main__":
-    run(config(__file__), mode="ps")
+    supervised(lambda: run(config(__file__), mode="ps"))

@@ -4,7 +4,8 @@ One process per GPU over RCCL:
 (plain `python train_dp.py` runs one rank)."""
 import _path  # noqa: F401
 from _bootstrap import config
+from tdfo_amd.utils.guarded import supervised
 from tdfo_amd.train.two_tower import run
 
 if __name__ == "__main__":
-    run(config(__file__), mode="dp", flavor="flax")
+    supervised(lambda: run(config(__file__), mode="dp", flavor="flax"))

@@ -11,11 +11,17 @@ from pathlib import Path
 
 import _path  # noqa: F401
 from _bootstrap import config
+from tdfo_amd.utils.guarded import supervised
 from tdfo_amd.config import read_cluster
 from tdfo_amd.train.two_tower import run
 
-if __name__ == "__main__":
+
+def main():
     cl = read_cluster(Path(__file__).resolve().parent / "cluster.json")
     print(f"===== cluster.json: {cl['num_workers']} workers, {cl['num_ps']} ps "
           "-> sharded embeddings over the launched ranks =====")
     run(config(__file__), mode="ps", flavor="keras")
+
+
+if __name__ == "__main__":
+    supervised(main)

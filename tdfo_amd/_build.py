@@ -76,10 +76,17 @@ def build_hip(force: bool = False, debug: bool = False, jobs: int = 8) -> Path:
     LIBDIR.mkdir(parents=True, exist_ok=True)
 
     def compile_one(src: Path):
+        # per-object stamp (source + every header + flags): an edit to one
+        # kernel file recompiles that file only
         obj = BUILD / (src.parent.name + "_" + src.stem + ".o")
         extra = tflags if src.suffix == ".cpp" else []
+        ostamp = obj.with_suffix(".stamp")
+        okey = _digest(headers + [src], " ".join(flags + extra))
+        if not force and obj.exists() and ostamp.exists() and ostamp.read_text() == okey:
+            return obj
         lang = ["-x", "hip"] if src.suffix == ".cpp" else []
         _run([HIPCC, *flags, *extra, *lang, "-c", str(src), "-o", str(obj)])
+        ostamp.write_text(okey)
         return obj
 
     srcs = kernels + [bindings] + comm

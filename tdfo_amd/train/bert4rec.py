@@ -30,6 +30,7 @@ from ..data.bert4rec_etl import read_columns
 from ..data.columnar import DeviceColumns
 from ..models.bert4rec import Bert4RecTrainer
 from ..parallel.dist import init_distributed
+from ..utils import guarded
 from ..utils.checkpoint import bert4rec_ckpt_name, save_state_dict
 
 
@@ -44,6 +45,7 @@ def run(cfg: Config, out_dir: str = ".", device: Optional[str] = None) -> List[D
     if device is None:
         device = "cuda" if torch.cuda.is_available() else "cpu"
     info = init_distributed(device)
+    guarded.rank_preflight(info)          # W > 1: collective self-test, c10d on mismatch
     rank, world, dev, group = info.rank, info.world_size, info.device, info.group
     root = cfg.data_dir / "parquet_bert4rec"
     train_cols = read_columns(str(root / cfg.train_data))

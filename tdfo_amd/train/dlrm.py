@@ -38,7 +38,7 @@ from ..models.dlrm import (CRITEO_1TB_ROWS, CRITEO_KAGGLE_ROWS, DCN_GT1TB_ROWS, 
 from ..parallel.dist import init_distributed
 from ..sparse import tables as _tables
 from ..utils import checkpoint as ckpt
-from ..utils import sharded_ckpt
+from ..utils import guarded, sharded_ckpt
 from ..utils.profiling import ProfileWindow, StepTimer, trace_range
 from .loop import StepLoop, make_source
 
@@ -89,6 +89,9 @@ def run(cfg: Config, mode: str = "single", out_dir: str = ".",
         device = "cuda" if torch.cuda.is_available() else "cpu"
     info = init_distributed(device)
     rank, world, dev, group = info.rank, info.world_size, info.device, info.group
+    # W > 1: collective self-test before the trainer exists; a mismatch puts
+    # every rank on c10d collectives + staged replay (utils/guarded.py)
+    pf = guarded.rank_preflight(info)
     if cfg.debug_checks:
         _tables.set_debug_checks(True)
     if mode == "single" and world > 1:
@@ -102,17 +105,23 @@ def run(cfg: Config, mode: str = "single", out_dir: str = ".",
     dcfg = dlrm_config(cfg, strategy)
     # more than one rank: input-dist pipelining, the step bench.py measures
     dcfg.pipeline = world > 1
+    dcfg.stream_graphs = dcfg.stream_graphs and guarded.stream_graphs_allowed()
     B = cfg.per_device_train_batch_size
     tr = DLRMTrainer(dcfg, B, dev, group=group, rank=rank, world_size=world)
     _log(rank, f"===== model: {cfg.model}, tables: {dcfg.num_tables} "
                f"({sum(dcfg.table_rows):,} rows x {dcfg.embedding_dim}), "
                f"per-device batch {B}, num devices: {world} =====")
     _log(rank, f"===== sharding plan: {json.dumps(tr.plan.summary())} =====")
+    if world > 1:
+        _log(rank, f"===== attempt {os.environ.get('TDFO_ATTEMPT', '0')}, collectives: "
+                   f"{'c10d' if os.environ.get('TDFO_COMM') == 'torch' else 'native'}, "
+                   f"stream graphs: {dcfg.stream_graphs}, preflight: "
+                   f"{'ok' if pf is None or pf['ok'] else 'FAILED ' + str(pf['failed'])} =====")
     total_steps = cfg.max_steps or cfg.synthetic.num_batches * cfg.n_epochs
     start = 0
     meta = {"model": cfg.model, "world_size": world, "strategy": strategy,
             "tables": len(dcfg.table_rows), "dim": dcfg.embedding_dim}
-    if cfg.resume and cfg.ckpt_dir:
+    if guarded.resume_requested(cfg.resume) and cfg.ckpt_dir:
         latest = _latest(cfg.ckpt_dir)
         if latest is not None:
             if sharded_ckpt.is_v2(str(latest)):        # streamed, reshardable
@@ -123,13 +132,17 @@ def run(cfg: Config, mode: str = "single", out_dir: str = ".",
                 start = int(st["step"])
             _log(rank, f"===== resumed from {latest} at step {start} =====")
     wd = None
-    if dev.type == "cuda" and float(os.environ.get("TDFO_WATCHDOG_S", "600") or 0) > 0:
+    wd_s = float(os.environ.get("TDFO_WATCHDOG_S", "600") or 0)
+    if dev.type == "cuda" and wd_s > 0:
         from ..utils.watchdog import StepWatchdog
-        wd = StepWatchdog(dev, 600.0, rank=rank, describe=tr.progress)
+        wd = StepWatchdog(dev, wd_s, rank=rank, describe=tr.progress)
     loop = StepLoop(tr, _source(cfg, dcfg, B, dev, rank, 0, start), start, watchdog=wd)
     metrics_path = cfg.metrics_file
     fault_at = int(os.environ.get("TDFO_FAULT_AT_STEP", "0") or 0)
     fault_rank = int(os.environ.get("TDFO_FAULT_RANK", "0") or 0)
+    fa = os.environ.get("TDFO_FAULT_ATTEMPT")       # only in this supervisor attempt
+    if fa is not None and fa != os.environ.get("TDFO_ATTEMPT", "0"):
+        fault_at = 0
     # jit_xla = false (tensorflow2/train.py:16): eager launches, no hipGraph
     use_graph = (cfg.hip_graph and cfg.jit_xla is not False and dev.type == "cuda"
                  and tr.emb.graph_capturable)
@@ -213,7 +226,16 @@ def run(cfg: Config, mode: str = "single", out_dir: str = ".",
             raise RuntimeError(f"rank {rank}: replicated state differs across ranks: {per}")
     if cfg.ckpt_dir:
         save(tr, cfg.ckpt_dir, step, rank, world, meta)
-    return {"history": history, "steps": step, "trainer": tr}
+    return {"history": history, "steps": step, "trainer": tr, "start": start, "preflight": pf,
+            "comm_path": _comm_path(tr, world)}
+
+
+def _comm_path(tr: DLRMTrainer, world: int) -> Optional[str]:
+    if world <= 1:
+        return None
+    from ..parallel.comm import RcclComm
+    return (("native" if isinstance(tr.comm, RcclComm) else "c10d")
+            + ("-graphs" if tr.graph == "mstreams" else "-staged"))
 
 
 def _latest(ckpt_dir: str) -> Optional[Path]:

@@ -28,6 +28,7 @@ from ..data import goodreads as G
 from ..models.two_tower import TwoTowerConfig, TwoTowerTrainer
 from ..parallel.dist import init_distributed
 from ..utils import checkpoint as ckpt
+from ..utils import guarded
 
 TRAIN_DTYPES = {"label": torch.float32, "avg_rating": torch.float32, "num_pages": torch.float32}
 ID_COLS = ["user_id", "item_id", "language", "is_ebook", "format", "publisher", "pub_decade"]
@@ -76,6 +77,8 @@ def run(cfg: Config, mode: str = "single", flavor: str = "flax", out_dir: str = 
     if device is None:
         device = "cuda" if torch.cuda.is_available() else "cpu"
     info = init_distributed(device) if mode in ("dp", "ps") else None
+    if info is not None:
+        guarded.rank_preflight(info)     # W > 1: collective self-test, c10d on mismatch
     rank = info.rank if info else 0
     world = info.world_size if info else 1
     dev = info.device if info else torch.device(device if device != "cuda" else "cuda:0")
@@ -106,9 +109,14 @@ def run(cfg: Config, mode: str = "single", flavor: str = "flax", out_dir: str = 
     drop_last = mode != "single"
     start_epoch = 1
     backup = out / "backup"
+    # ps: BackupAndRestore semantics (restored whenever present); dp at W > 1
+    # keeps the same per-epoch backup/, restored when resume is requested
+    # (the supervisor's fallback attempt, utils/guarded.py)
+    keep_backup = mode == "ps" or (mode == "dp" and world > 1)
     if mode == "ps":
         for d in ("ckpt", "backup", "log"):
             (out / d).mkdir(parents=True, exist_ok=True)
+    if keep_backup and (mode == "ps" or guarded.resume_requested(cfg.resume)):
         man = ckpt.load_manifest(str(backup))
         if man is not None and man["world_size"] == world:
             st = ckpt.load_sharded(str(backup), rank, world)
@@ -200,17 +208,18 @@ def run(cfg: Config, mode: str = "single", flavor: str = "flax", out_dir: str = 
             Path(metrics_path).parent.mkdir(parents=True, exist_ok=True)
             with open(metrics_path, "a") as f:
                 f.write(json.dumps(rec) + "\n")
-        if mode == "ps":
+        if keep_backup:
             state = {k: v for k, v in tr.state_dict().items()}
             bar = (lambda: torch.distributed.barrier()) if world > 1 else None
-            ckpt.save_sharded(str(out / "ckpt" / f"epoch_{epoch}"), rank, world, epoch, state,
-                              {"epoch": epoch}, barrier=bar)
+            if mode == "ps":
+                ckpt.save_sharded(str(out / "ckpt" / f"epoch_{epoch}"), rank, world, epoch,
+                                  state, {"epoch": epoch}, barrier=bar)
             ckpt.save_sharded(str(backup), rank, world, epoch, state, {"epoch": epoch},
                               barrier=bar)
     params = tr.flax_params()
     if rank == 0 and flavor == "flax":
         ckpt.save_flax_params(params, str(out / "model_params.pt"))
-    if mode == "ps" and rank == 0:
+    if keep_backup and rank == 0:
         # training finished: BackupAndRestore deletes its backup on success
         for f in backup.glob("*"):
             f.unlink()

@@ -30,9 +30,24 @@ import os
 import signal
 import subprocess
 import sys
+import tempfile
 from typing import Dict, List, Optional, Sequence
 
 CHILD_ENV = "TDFO_SUPERVISED_CHILD"
+METRIC_ENV = "TDFO_METRIC_OUT"
+
+
+def emit_result(line: str) -> None:
+    """A supervised child's result line: into the supervisor's per-attempt
+    file (printed only if every rank's attempt succeeded), else stdout."""
+    path = os.environ.get(METRIC_ENV)
+    if not path:
+        print(line, flush=True)
+        return
+    tmp = path + ".tmp"
+    with open(tmp, "w") as f:
+        f.write(line + "\n")
+    os.replace(tmp, path)
 
 
 def is_child() -> bool:
@@ -74,9 +89,39 @@ def _exchange(store, tag: str, rank: int, world: int, rc: int) -> List[int]:
     return out
 
 
+def _wait_or_peer_failed(child, store, tag: str, rank: int, world: int, poll_s: float) -> int:
+    """Wait for the child; if another rank's child already failed this
+    attempt (its supervisor posted a non-zero code), end ours instead of
+    leaving it blocked in a collective until its watchdog fires (fail fast,
+    the role of GRPC_FAIL_FAST in tensorflow2/train_ps.py:39)."""
+    import time
+    peers = [r for r in range(world) if r != rank]
+    while True:
+        try:
+            return child.wait(timeout=poll_s)
+        except subprocess.TimeoutExpired:
+            pass
+        for r in peers:
+            key = f"tdfo_sup/{tag}/rc/{r}"
+            try:
+                if store.check([key]) and int(store.get(key)) != 0:
+                    child.terminate()
+                    try:
+                        child.wait(timeout=10)
+                    except subprocess.TimeoutExpired:
+                        child.kill()
+                        child.wait()
+                    print(json.dumps({"supervisor": "peer failed, child ended", "rank": rank,
+                                      "peer": r}), file=sys.stderr, flush=True)
+                    return 128 + signal.SIGTERM
+            except Exception:  # noqa: BLE001 -- a store hiccup: keep waiting
+                time.sleep(poll_s)
+
+
 def supervise(child_argv: Sequence[str], attempts: Sequence[Dict[str, str]],
               fallback_argv: Sequence[Sequence[str]] = (), rank: Optional[int] = None,
-              world: Optional[int] = None, timeout_s: float = 1800.0) -> int:
+              world: Optional[int] = None, timeout_s: float = 1800.0,
+              poll_s: float = 0.5) -> int:
     """Run ``child_argv`` once per attempt until every rank's child exits 0.
 
     attempts[k]: extra environment of attempt k; fallback_argv[k] (k >= 1):
@@ -96,20 +141,27 @@ def supervise(child_argv: Sequence[str], attempts: Sequence[Dict[str, str]],
     run_id = os.environ.get("TORCHELASTIC_RUN_ID", "") + os.environ.get(
         "TORCHELASTIC_RESTART_COUNT", "")
     rc_final = 1
+    metric_files: Dict[int, str] = {}
+    ok_attempt = None
     for k, extra in enumerate(attempts):
         env = dict(os.environ)
         env.update(extra)
         env[CHILD_ENV] = "1"
         env["TDFO_ATTEMPT"] = str(k)
         env["TDFO_STORE_PREFIX"] = f"tdfo/{run_id}/attempt{k}/"
+        # a child's result line (bench.py's metric JSON) goes to this file;
+        # only the attempt every rank completed gets it printed on stdout
+        env[METRIC_ENV] = metric_files[k] = os.path.join(
+            tempfile.gettempdir(), f"tdfo_metric_{os.getpid()}_{k}.json")
         argv = list(child_argv) + (list(fallback_argv[k - 1]) if k >= 1 and
                                    k - 1 < len(fallback_argv) else [])
         child = subprocess.Popen(argv, env=env, preexec_fn=_die_with_parent)
-        rc = child.wait()
+        rc = _wait_or_peer_failed(child, store, f"{run_id}/{k}", rank, world, poll_s)
         child = None
         rcs = _exchange(store, f"{run_id}/{k}", rank, world, rc)
         if all(x == 0 for x in rcs):
             rc_final = 0
+            ok_attempt = k
             break
         rc_final = next(x for x in rcs if x != 0)
         if rc_final == -1000:
@@ -119,6 +171,17 @@ def supervise(child_argv: Sequence[str], attempts: Sequence[Dict[str, str]],
                               "next": ("fallback: " + json.dumps(attempts[k + 1]))
                               if k + 1 < len(attempts) else None}),
                   file=sys.stderr, flush=True)
+    for k, path in metric_files.items():
+        if not os.path.exists(path):
+            continue
+        with open(path) as f:
+            line = f.read().strip()
+        os.unlink(path)
+        if k == ok_attempt:
+            print(line, flush=True)
+        elif line:
+            print(json.dumps({"supervisor": "metric line of a failed attempt discarded",
+                              "attempt": k}), file=sys.stderr, flush=True)
     # keep the store (hosted by rank 0's supervisor when there is no launcher
     # store) alive until every supervisor has read the verdict
     try:
