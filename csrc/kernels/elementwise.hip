@@ -233,7 +233,7 @@ __global__ __launch_bounds__(64) void spin_kernel(uint64_t ticks) {
   while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
 }
 
-// In-graph timestamps for schedule probes (scripts/probes/mr_sched_probe.py): the
+// In-graph timestamps for schedule probes (labs/probes/mr_sched_probe.py): the
 // k-th run of segment `seg` writes the 100 MHz wall clock to
 // buf[(k * nseg + seg) * 2 + which]; its end stamp (which = 1) advances k.
 // One lane, vector stores; a segment's runs are ordered on its stream.

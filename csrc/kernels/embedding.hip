@@ -297,14 +297,15 @@ template <int SK>
 __device__ __forceinline__ void seg_lsd_sort(uint32_t (&key)[SK], uint32_t (&val)[SK], int bits,
                                              int skn, uint32_t* skey, uint32_t* sval,
                                              uint32_t* cnt, uint32_t* wsum) {
-  constexpr int CNT = SEG_BINS * SK * SEG_WAVES;     // logical counters
-  constexpr int KW = SK * SEG_WAVES;                  // (slot, wave) pairs
-  constexpr int CPAD = KW * (SEG_BINS + 1);           // padded physical size
-  constexpr int PER = CNT / SEG_THREADS;
+  constexpr int PER = SEG_BINS * SK * SEG_WAVES / SEG_THREADS;   // (= SK)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  // only the skn used slots' counters are cleared and scanned: logical
+  // order (digit, slot < skn, wave), skn entries per thread
+  const int kwn = skn * SEG_WAVES;
+  const int cpn = kwn * (SEG_BINS + 1);
   for (int shift = 0; shift < bits; shift += SEG_BITS) {
-    for (int c = tid; c < CPAD; c += SEG_THREADS) cnt[c] = 0;
+    for (int c = tid; c < cpn; c += SEG_THREADS) cnt[c] = 0;
     __syncthreads();
     uint32_t rank[SK];
     int dig[SK];
@@ -324,15 +325,16 @@ __device__ __forceinline__ void seg_lsd_sort(uint32_t (&key)[SK], uint32_t (&val
       if ((peers & lt) == 0) cnt[(k * SEG_WAVES + w) * (SEG_BINS + 1) + d] = (uint32_t)__popcll(peers);
     }
     __syncthreads();
-    // exclusive scan of cnt in (digit, slot, wave) order: PER logical entries
-    // per thread, i = tid * PER + q -> digit i / KW, pair i % KW
-    auto phys = [&](int i) { return (i % KW) * (SEG_BINS + 1) + i / KW; };
+    // exclusive scan of cnt in (digit, slot, wave) order: skn logical
+    // entries per thread, i = tid * skn + q -> digit i / kwn, pair i % kwn
+    auto phys = [&](int i) { return (i % kwn) * (SEG_BINS + 1) + i / kwn; };
     uint32_t loc[PER];
     uint32_t run = 0;
 #pragma unroll
     for (int q = 0; q < PER; ++q) {
+      if (q >= skn) break;
       loc[q] = run;
-      run += cnt[phys(tid * PER + q)];
+      run += cnt[phys(tid * skn + q)];
     }
     uint32_t incl = run;                             // wave inclusive scan of the totals
     for (int off = 1; off < 64; off <<= 1) {
@@ -344,7 +346,10 @@ __device__ __forceinline__ void seg_lsd_sort(uint32_t (&key)[SK], uint32_t (&val
     uint32_t base = incl - run;
     for (int q = 0; q < w; ++q) base += wsum[q];
 #pragma unroll
-    for (int q = 0; q < PER; ++q) cnt[phys(tid * PER + q)] = base + loc[q];
+    for (int q = 0; q < PER; ++q) {
+      if (q >= skn) break;
+      cnt[phys(tid * skn + q)] = base + loc[q];
+    }
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < SK; ++k) {
@@ -366,11 +371,42 @@ __device__ __forceinline__ void seg_lsd_sort(uint32_t (&key)[SK], uint32_t (&val
 
 // SK: elements per thread (tables of <= SK * 1024 ids; 2 for small batches:
 // a quarter of the counters to clear and scan per pass)
+// Run metadata for the in-kernel combine (one-hot, one run per table, B a
+// multiple of the update's chunk size CH): for every chunk c of the sorted
+// list, meta[c].x = the chunk where the run holding c's FIRST entry starts
+// (-1: it starts in c) and meta[c].y = the chunk where the run holding c's
+// LAST entry ends (-1: it ends in c); rcnt[c] = 0 (arrival counters). Found
+// by binary searches over the table's sorted keys in LDS.
+__device__ __forceinline__ void seg_run_meta(const uint32_t* skey, int n, int64_t s0, int ch,
+                                             int2* __restrict__ meta, int32_t* __restrict__ rcnt) {
+  const int nch = n / ch;
+  for (int lc = threadIdx.x; lc < nch; lc += blockDim.x) {
+    const int f = lc * ch, e = f + ch - 1;
+    const uint32_t kf = skey[f], ke = skey[e];
+    int lo = 0, hi = f;                  // first index with key == kf (sorted: >= kf)
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (skey[mid] < kf) lo = mid + 1; else hi = mid;
+    }
+    const int rs = lo;
+    lo = e + 1; hi = n;                  // first index past e with key > ke
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (skey[mid] <= ke) lo = mid + 1; else hi = mid;
+    }
+    const int re = lo - 1;
+    const int64_t c = s0 / ch + lc;
+    meta[c] = make_int2(rs < f ? (int)((s0 + rs) / ch) : -1, re > e ? (int)((s0 + re) / ch) : -1);
+    rcnt[c] = 0;
+  }
+}
+
 template <typename K, bool SORTED_G, int SK = SEG_K>
 __global__ __launch_bounds__(SEG_THREADS) void emb_segsort_kernel(
     const EmbBwdArgs a, K* __restrict__ keys_out, int32_t* __restrict__ vals_out,
     int64_t* __restrict__ goff, float* __restrict__ gscale, int32_t* __restrict__ tail_count,
-    int32_t* __restrict__ pos) {
+    int32_t* __restrict__ pos, int2* __restrict__ meta = nullptr,
+    int32_t* __restrict__ rcnt = nullptr, int meta_ch = 0) {
   __shared__ uint32_t skey[SK * SEG_THREADS];
   __shared__ uint32_t sval[SK * SEG_THREADS];
   __shared__ uint32_t cnt[SK * SEG_WAVES * (SEG_BINS + 1)];
@@ -410,6 +446,12 @@ __global__ __launch_bounds__(SEG_THREADS) void emb_segsort_kernel(
   for (int q = 0; q < SEG_WAVES; ++q) bmax = max(bmax, smax[q]);
   const int bits = bmax ? 32 - __clz(bmax) : 1;
   seg_lsd_sort<SK>(key, val, bits, SK, skey, sval, cnt, wsum);
+  if (meta != nullptr) {                 // sorted keys back in LDS for the searches
+#pragma unroll
+    for (int k = 0; k < SK; ++k) skey[k * SEG_THREADS + tid] = key[k];
+    __syncthreads();
+    seg_run_meta(skey, n, s0, meta_ch, meta, rcnt);
+  }
   const K kb = (K)a.row_offset[t];
   const int64_t go = a.grad_off[t];
 #pragma unroll
@@ -733,6 +775,7 @@ __device__ __forceinline__ void update_row(const EmbBwdArgs& a, const OptScalars
                                            float (&wv)[BwdCfg<D>::EPL], float st_row, int lane,
                                            const float* mpre = nullptr,
                                            const float* vpre = nullptr) {
+#pragma clang fp contract(off)     // same bits wherever it is inlined
   constexpr int EPL = BwdCfg<D>::EPL;
   float acc[EPL];
 #pragma unroll
@@ -796,17 +839,105 @@ __device__ __forceinline__ void update_row(const EmbBwdArgs& a, const OptScalars
   }
 }
 
+// Partials handed between waves of ONE launch (the in-kernel combine below),
+// possibly across XCDs, whose L2s are not coherent: written and read with
+// agent-scope atomic read-modify-writes (exchange / add 0), which execute at
+// the device-coherent point, never in a stale L2 line. The producing wave's
+// lane 0 then signals with an agent-scope atomic add after the wave's
+// vmcnt(0) wait, and the wave whose add comes last reads. No wave ever waits
+// for another. (Plain sc1 stores / loads, MI355X_MICROARCH.md hand-off row 1,
+// read stale partials here: the reader's L2 can hold the workspace lines
+// from earlier kernels.) A few KB per step.
+template <int EPL>
+__device__ __forceinline__ void part_store(float* p, const float (&v)[EPL]) {
+  if constexpr (EPL % 2 == 0) {
+#pragma unroll
+    for (int u = 0; u < EPL; u += 2) {
+      const unsigned long long x = (unsigned long long)__float_as_uint(v[u]) |
+                                   ((unsigned long long)__float_as_uint(v[u + 1]) << 32);
+      __hip_atomic_exchange((unsigned long long*)(p + u), x, __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_AGENT);
+    }
+  } else {
+    __hip_atomic_exchange((unsigned int*)p, __float_as_uint(v[0]), __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+template <int EPL>
+__device__ __forceinline__ void part_load(float (&v)[EPL], float* p) {
+  if constexpr (EPL % 2 == 0) {
+#pragma unroll
+    for (int u = 0; u < EPL; u += 2) {
+      const unsigned long long x = __hip_atomic_fetch_add(
+          (unsigned long long*)(p + u), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      v[u] = __uint_as_float((uint32_t)x);
+      v[u + 1] = __uint_as_float((uint32_t)(x >> 32));
+    }
+  } else {
+    v[0] = __uint_as_float(__hip_atomic_fetch_add((unsigned int*)p, 0u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT));
+  }
+}
+
+// A run crossing chunk edges, finished by the last of its chunks to arrive:
+// the tail partial of its first chunk cs, then the head partials of chunks
+// cs+1..ce in chunk order (HQ in flight) -- emb_combine_kernel's order, so the
+// same bits -- and one optimizer update of `row`.
+// emb_combine_kernel calls the same code, and FP contraction is off here and
+// in update_row, so the in-kernel and the separate combine give identical
+// bits (inlined into two kernels with contraction on, the update came out
+// 1 ulp apart on 8 of 13 K rows; a non-inlined call cost the update kernel
+// 224 B of scratch and 20 us).
+template <int D, int OPT>
+__device__ __forceinline__ void run_finish(const EmbBwdArgs& a, const OptScalars& o,
+                                           int64_t cs, int64_t ce,
+                           uint64_t row, float* head, float* tail, int lane) {
+#pragma clang fp contract(off)
+  constexpr int EPL = BwdCfg<D>::EPL;
+  constexpr int HQ = EPL <= 2 ? 32 : (EPL <= 4 ? 16 : 8);
+  const int e0 = elem0<D>(lane);
+  const bool act = D >= 64 || e0 < D;
+  const int e0c = act ? e0 : 0;
+  float acc[EPL];
+  part_load<EPL>(acc, tail + cs * D + e0c);
+#pragma unroll
+  for (int u = 0; u < EPL; ++u) acc[u] = act ? acc[u] : 0.f;
+  for (int64_t j0 = cs + 1; j0 <= ce; j0 += HQ) {
+    float hv[HQ][EPL];
+#pragma unroll
+    for (int q = 0; q < HQ; ++q) part_load<EPL>(hv[q], head + min(j0 + q, ce) * D + e0c);
+#pragma unroll
+    for (int q = 0; q < HQ; ++q) {
+      if (j0 + q <= ce && act) {
+#pragma unroll
+        for (int u = 0; u < EPL; ++u) acc[u] += hv[q][u];
+      }
+    }
+  }
+  float wv[EPL];
+#pragma unroll
+  for (int u = 0; u < EPL; ++u) wv[u] = 0.f;
+  if constexpr (OPT != EMB_DENSE_GRAD) load_row<D>(wv, a.W + row * D + e0c);
+  const float st = OPT == EMB_ROWWISE_ADAGRAD ? a.state1[row] : 0.f;
+  update_row<D, OPT>(a, o, row, acc, wv, st, lane);
+}
+
 // One wave = one chunk of CH sorted entries. Every gradient row of the chunk
 // and every weight row it may update are loaded up front with no control
 // flow between the loads (hipcc keeps all of them in flight); runs are then
 // reduced in registers in sorted order and each run that finishes inside the
-// chunk gets exactly one optimizer update.
+// chunk gets exactly one optimizer update. Runs crossing chunk edges leave
+// head / tail partials: with run metadata (``meta``, from the one-hot sort)
+// the last of a run's chunks to arrive finishes it here; otherwise the
+// chunk where it starts is listed for emb_combine_kernel.
 template <int D, typename K, bool GB, int OPT, int CH>
 __global__ __launch_bounds__(256) void emb_chunk_kernel(
     EmbBwdArgs a, const K* __restrict__ keys, const int32_t* __restrict__ vals,
     const int64_t* __restrict__ goff, const float* __restrict__ gscale,
     float* __restrict__ head, float* __restrict__ tail, int32_t* __restrict__ tail_list,
-    int32_t* __restrict__ tail_count) {
+    int32_t* __restrict__ tail_count, const int2* __restrict__ meta,
+    int32_t* __restrict__ rcnt) {
   constexpr int EPL = BwdCfg<D>::EPL;
   constexpr bool NEED_W = OPT != EMB_DENSE_GRAD;
   const int lane = threadIdx.x & 63;
@@ -827,6 +958,7 @@ __global__ __launch_bounds__(256) void emb_chunk_kernel(
   const float mysc = gscale ? gscale[gi] : 1.f;
   const K prevk = start > 0 ? keys[start - 1] : (K)0;
   const K nextk = end < a.nnz ? keys[end] : (K)0;
+  const int2 md = meta != nullptr ? meta[c] : make_int2(-1, -1);
   const K kup = __shfl_up(mykey, 1, 64);
   const K kdn = __shfl_down(mykey, 1, 64);
   const bool is_start = lane < len && (lane == 0 ? (start == 0 || prevk != mykey) : kup != mykey);
@@ -881,25 +1013,48 @@ __global__ __launch_bounds__(256) void emb_chunk_kernel(
             update_row<D, OPT>(a, o, (uint64_t)rdlane(mykey, p), acc, wv, rdlanef(st_l, p),
                                lane);
         } else if (act) {
-#pragma unroll
-          for (int u = 0; u < EPL; ++u) head[c * D + e0 + u] = acc[u];
+          part_store<EPL>(head + c * D + e0, acc);
         }
 #pragma unroll
         for (int u = 0; u < EPL; ++u) acc[u] = 0.f;
       }
     }
   }
-  if (!((emask >> (len - 1)) & 1ull)) {                       // last run continues
-    const bool started_here = smask != 0;
-    if (act) {
-      float* dst = (started_here ? tail : head) + c * D + e0;
-#pragma unroll
-      for (int u = 0; u < EPL; ++u) dst[u] = acc[u];
-    }
-    if (started_here && lane == 0) {
+  const bool cont = !((emask >> (len - 1)) & 1ull);           // last run continues
+  const bool started_here = smask != 0;
+  if (cont) {
+    if (act) part_store<EPL>((started_here ? tail : head) + c * D + e0, acc);
+    if (meta == nullptr && started_here && lane == 0) {
       const int slot = atomicAdd(tail_count, 1);
       if (slot < (int)((a.nnz + CH - 1) / CH)) tail_list[slot] = (int32_t)c;
     }
+  }
+  if (meta != nullptr) {
+    // arrivals: a head partial of the run that came from before (it ends here,
+    // or covers the whole chunk), a tail partial of the run that starts here
+    // and continues; the run's counter sits at its first chunk
+    const bool sig_h = from_before;
+    const int64_t hcs = md.x, hce = emask ? c : (int64_t)md.y;
+    const bool sig_t = cont && started_here;
+    const int64_t tce = md.y;
+    int last_h = 0, last_t = 0;
+    if (sig_h || sig_t) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");       // this wave's partials landed
+      if (lane == 0) {
+        if (sig_h) last_h = atomicAdd(&rcnt[hcs], 1) == (int)(hce - hcs);
+        if (sig_t) last_t = atomicAdd(&rcnt[c], 1) == (int)(tce - c);
+      }
+      last_h = __builtin_amdgcn_readfirstlane(last_h);
+      last_t = __builtin_amdgcn_readfirstlane(last_t);
+      // the last arrival re-arms its counter (an apply replayed without a
+      // new sort sees zeros again)
+      if (lane == 0 && last_h) __hip_atomic_store(&rcnt[hcs], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (lane == 0 && last_t) __hip_atomic_store(&rcnt[c], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (last_h)
+      run_finish<D, OPT>(a, o, hcs, hce, (uint64_t)rdlane(mykey, 0), head, tail, lane);
+    if (last_t)
+      run_finish<D, OPT>(a, o, c, tce, (uint64_t)rdlane(mykey, len - 1), head, tail, lane);
   }
   }
 }
@@ -919,25 +1074,18 @@ constexpr int LONG_WAVES = 16;
 
 template <int D, typename K, int OPT, int CH>
 __global__ __launch_bounds__(256) void emb_combine_kernel(
-    EmbBwdArgs a, const K* __restrict__ keys, const float* __restrict__ head,
-    const float* __restrict__ tail, const int32_t* __restrict__ tail_list,
+    EmbBwdArgs a, const K* __restrict__ keys, float* __restrict__ head,
+    float* __restrict__ tail, const int32_t* __restrict__ tail_list,
     int32_t* __restrict__ tail_count, int64_t* __restrict__ long_list, int allow_long) {
-  constexpr int EPL = BwdCfg<D>::EPL;
   const int lane = threadIdx.x & 63;
   const int nw = (gridDim.x * blockDim.x) >> 6;
   if (skip_step(a)) return;
   const int n = min(*tail_count, (int)((a.nnz + CH - 1) / CH));
-  const int e0 = elem0<D>(lane);
-  const bool act = D >= 64 || e0 < D;
-  const int e0c = act ? e0 : 0;
   const OptScalars o = opt_scalars(a);
   for (int i = ((blockIdx.x * blockDim.x + threadIdx.x) >> 6); i < n; i += nw) {
     const int64_t c = tail_list[i];
     const int64_t endc = min((c + 1) * CH, a.nnz);
     const K last = keys[endc - 1];
-    float acc[EPL];
-#pragma unroll
-    for (int u = 0; u < EPL; ++u) acc[u] = act ? tail[c * D + e0 + u] : 0.f;
     // Last chunk of the run: the chunks it covers are exactly the ones after
     // c whose FIRST key is `last` (sorted keys: a prefix of c+1, c+2, ...), so
     // each lane probes one chunk's first key and a ballot counts the prefix --
@@ -961,32 +1109,7 @@ __global__ __launch_bounds__(256) void emb_combine_kernel(
       }
       continue;
     }
-    // HQ head partials in flight: a skewed table's runs span up to B/CH
-    // chunks (a 3-row table: ~85 per run at B = 8192), and this walk is the
-    // kernel's latency tail (8 in flight: 15 us per DLRM-1TB step)
-    constexpr int HQ = EPL <= 2 ? 32 : (EPL <= 4 ? 16 : 8);
-    for (int64_t j0 = c + 1; j0 <= jlast; j0 += HQ) {
-      float hv[HQ][EPL];
-#pragma unroll
-      for (int q = 0; q < HQ; ++q) {
-        const int64_t j = min(j0 + q, jlast);
-#pragma unroll
-        for (int u = 0; u < EPL; ++u) hv[q][u] = head[j * D + e0c + u];
-      }
-#pragma unroll
-      for (int q = 0; q < HQ; ++q) {
-        if (j0 + q <= jlast && act) {
-#pragma unroll
-          for (int u = 0; u < EPL; ++u) acc[u] += hv[q][u];
-        }
-      }
-    }
-    float wv[EPL];
-#pragma unroll
-    for (int u = 0; u < EPL; ++u) wv[u] = 0.f;
-    if constexpr (OPT != EMB_DENSE_GRAD) load_row<D>(wv, a.W + (uint64_t)last * D + e0c);
-    const float st = OPT == EMB_ROWWISE_ADAGRAD ? a.state1[(uint64_t)last] : 0.f;
-    update_row<D, OPT>(a, o, (uint64_t)last, acc, wv, st, lane);
+    run_finish<D, OPT>(a, o, c, jlast, (uint64_t)last, head, tail, lane);
   }
 }
 
@@ -1175,12 +1298,17 @@ void dense_update_dispatch(const EmbBwdArgs& a, int64_t rows, const float* g, fl
 }
 
 int g_emb_segsort = 1;   // one-hot batches: per-table LDS sort (0: device-wide radix sort)
-// one-hot, one run, B > 2048: the value-range split sort (TDFO_SEG_SPLIT=0: one
-// block per table)
+// one-hot, one run, B > 2048: the value-range split sort (TDFO_SEG_SPLIT=1).
+// Off by default: isolated it sorts 26 x 8192 ids in 17.7-20 us against
+// 35 us for one block per table, but it keeps 8x the CUs busy (208 CU x
+// ~28 us in the step against 26 x ~56), and the sort runs beside the top-MLP
+// forward GEMMs, off the critical path: DLRM-1TB 0.433-0.436 vs 0.421-0.422
+// ms/step (same box, profiles/r06/). What the step pays for a background
+// kernel is its CU-time and bytes, not its latency.
 constexpr int SEG_SPLIT = 8;
 const int g_emb_seg_split = [] {
   const char* e = getenv("TDFO_SEG_SPLIT");
-  return e ? atoi(e) : 1;
+  return e ? atoi(e) : 0;
 }();
 
 // (Rejected, round 4: capping the fused update's grid so GEMM blocks get CUs
@@ -1191,7 +1319,7 @@ const int g_emb_seg_split = [] {
 
 struct WsLayout {
   size_t keys_in, keys_out, vals_in, vals_out, goff, gscale, head, tail, tlist, tcount, sortws,
-      pos, llist;
+      pos, llist, meta, rcnt;
   size_t total;
 };
 
@@ -1216,6 +1344,8 @@ WsLayout ws_layout(int64_t nnz, int D) {
   L.sortws = o;   o += al(radix_sort_workspace(nnz));
   L.pos = o;      o += al(nnz * 4);
   L.llist = o;    o += al((size_t)(nch / COMBINE_LONG + 1) * 16);   // (c, jlast) per long run
+  L.meta = o;     o += al((size_t)nch * 8);                          // run metadata per chunk
+  L.rcnt = o;     o += al((size_t)nch * 4);                          // arrival counters
   L.total = o;
   return L;
 }
@@ -1227,6 +1357,20 @@ bool onehot_path(const EmbBwdArgs& a) {
   const int R = a.segsort;
   return R > 0 && a.T % R == 0 && a.nnz == (int64_t)a.T * a.B &&
          a.B <= SEG_MAX && !a.mean;
+}
+
+// one run per table, chunks never straddling tables, single-block sort: the
+// sort writes run metadata and the update finishes crossing runs in-kernel
+// (no emb_combine_kernel launch). TDFO_EMB_INKERNEL_COMBINE=0: the combine
+// kernel.
+const int g_emb_inkernel_combine = [] {
+  const char* e = getenv("TDFO_EMB_INKERNEL_COMBINE");
+  return e ? atoi(e) : 1;
+}();
+
+bool meta_path(const EmbBwdArgs& a) {
+  return g_emb_inkernel_combine && onehot_path(a) && a.segsort == 1 &&
+         a.B % ch_for(a.D) == 0 && !(g_emb_seg_split && a.B > 2 * SEG_THREADS);
 }
 
 template <typename K>
@@ -1242,19 +1386,24 @@ void prep_impl(const EmbBwdArgs& a, const WsLayout& L, hipStream_t s) {
   const int R = a.segsort;                 // runs per physical table (0: off)
   if (onehot_path(a)) {
     if (R == 1) {
+      int2* meta = meta_path(a) ? (int2*)(ws + L.meta) : nullptr;
+      int32_t* rcnt = (int32_t*)(ws + L.rcnt);
+      const int ch = ch_for(a.D);
       if (a.B <= 2 * SEG_THREADS)
         hipLaunchKernelGGL((emb_segsort_kernel<K, true, 2>), dim3(a.T), dim3(SEG_THREADS), 0, s, a,
-                           keys_out, vals_out, goff, gscale, tcount, (int32_t*)nullptr);
+                           keys_out, vals_out, goff, gscale, tcount, (int32_t*)nullptr, meta,
+                           rcnt, ch);
       else if (g_emb_seg_split)
         hipLaunchKernelGGL((emb_segsort_split_kernel<K, SEG_SPLIT>), dim3(a.T * SEG_SPLIT),
                            dim3(SEG_THREADS), 0, s, a, keys_out, vals_out, goff, gscale, tcount);
       else
         hipLaunchKernelGGL((emb_segsort_kernel<K, true>), dim3(a.T), dim3(SEG_THREADS), 0, s, a,
-                           keys_out, vals_out, goff, gscale, tcount, (int32_t*)nullptr);
+                           keys_out, vals_out, goff, gscale, tcount, (int32_t*)nullptr, meta,
+                           rcnt, ch);
     } else {
       int32_t* pos = (int32_t*)(ws + L.pos);
       hipLaunchKernelGGL((emb_segsort_kernel<K, false>), dim3(a.T), dim3(SEG_THREADS), 0, s, a, keys_in,
-                         vals_in, goff, gscale, tcount, pos);
+                         vals_in, goff, gscale, tcount, pos, (int2*)nullptr, (int32_t*)nullptr, 0);
       TDFO_CHECK_HIP(hipGetLastError());
       const int Tp = a.T / R;
       hipLaunchKernelGGL(emb_runrank_kernel<K>, dim3(a.T * (R - 1)), dim3(SEG_THREADS), 0, s, Tp,
@@ -1300,17 +1449,21 @@ void apply_impl(const EmbBwdArgs& a0, const WsLayout& L, hipStream_t s) {
   float* tail = (float*)(ws + L.tail);
   int32_t* tlist = (int32_t*)(ws + L.tlist);
   int32_t* tcount = (int32_t*)(ws + L.tcount);
+  const int2* meta = meta_path(a0) ? (const int2*)(ws + L.meta) : nullptr;
+  int32_t* rcnt = (int32_t*)(ws + L.rcnt);
   auto run = [&](auto ch_c) {
     constexpr int CH = decltype(ch_c)::value;
     const int64_t nch = (a.nnz + CH - 1) / CH;
     int64_t blocks = (nch + 3) / 4;
     if (a.grad_bf16)
       hipLaunchKernelGGL((emb_chunk_kernel<D, K, true, OPT, CH>), dim3(blocks), dim3(256), 0, s, a,
-                         keys_out, vals_out, goff, gscale, head, tail, tlist, tcount);
+                         keys_out, vals_out, goff, gscale, head, tail, tlist, tcount, meta, rcnt);
     else
       hipLaunchKernelGGL((emb_chunk_kernel<D, K, false, OPT, CH>), dim3(blocks), dim3(256), 0, s,
-                         a, keys_out, vals_out, goff, gscale, head, tail, tlist, tcount);
+                         a, keys_out, vals_out, goff, gscale, head, tail, tlist, tcount, meta,
+                         rcnt);
     TDFO_CHECK_HIP(hipGetLastError());
+    if (meta != nullptr) return;        // crossing runs finished inside the update
     int64_t cblocks = (nch + 3) / 4;
     if (cblocks > 1024) cblocks = 1024;
     int64_t* llist = (int64_t*)(ws + L.llist);

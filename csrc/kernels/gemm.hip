@@ -1161,7 +1161,7 @@ using PPG = PPGeom<128, 2, 128>;
 // the end. Two phases per K tile per group (one 64-row half of the wave tile
 // x 4 column fragments = 16 MFMAs each); a 3-slot LDS ring (144 KiB) keeps
 // two K tiles of DMA in flight (issued in phase 0, two tiles ahead).
-// Measured (scripts/probes/gemm_pp8.hip vs gemm_floor.hip, random bf16):
+// Measured (labs/probes/gemm_pp8.hip vs gemm_floor.hip, random bf16):
 // compute floor 2.1 PF at 8192^3 vs 0.8-0.9 for the one-group loops.
 // Epilogue: pp_epilogue (bias, ReLU, ReLU mask, DCN second output, fp32
 // split-K slabs). No column-sum (bias-grad) support.
@@ -1341,7 +1341,7 @@ void pp_pair_launch(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s) {
 }
 
 // Kernel choice. Auto (policy 0), measured on the DLRM / DCN-v2 step shapes
-// on random operands (scripts/gemm_lab.py; profiles/r03/gemm_lab_*.jsonl):
+// on random operands (labs/gemm_lab.py; profiles/r03/gemm_lab_*.jsonl):
 //   * ping-pong 128x128 (2 blocks per CU): every weight grad and dgrad, and
 //     the forwards whose 128x128 grid fills the CUs (DLRM-1TB MLP GEMMs
 //     266.5 vs 285.2 us on the round-2 kernels, 0.455 vs 0.472 ms/step);

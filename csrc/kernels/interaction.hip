@@ -368,7 +368,7 @@ __global__ __launch_bounds__(256) void inter_bwd_kernel(
 }
 
 // Samples per wave of the software-pipelined walk. Measured on MI355X
-// (B = 8192, F = 27, D = 128; scripts/inter_ab.sh): fwd 15.4 / 15.1 / 16.3 us
+// (B = 8192, F = 27, D = 128; labs/inter_ab.sh): fwd 15.4 / 15.1 / 16.3 us
 // and bwd 43.3 / 37.8 / 34.4 us at 1 / 2 / 4 samples per wave (round 1's
 // one-sample-per-wave kernels: 20 / 42 us in the step). TDFO_INTER_SPW
 // overrides both.

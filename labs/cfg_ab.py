@@ -3,7 +3,7 @@
 batches, captured graphs): each variant is built, warmed, captured and timed
 in turn, twice over (A B A B), in one process.
 
-usage: python scripts/cfg_ab.py '{"defer_wgrad": true}' '{"defer_wgrad": false}' [--model dcnv2]
+usage: python labs/cfg_ab.py '{"defer_wgrad": true}' '{"defer_wgrad": false}' [--model dcnv2]
 """
 import json
 import os

@@ -6,7 +6,7 @@ against an fp32 torch oracle and timed from hipGraph replays, variants
 interleaved round by round in one process (cdna_hip_programming.md §5.4
 rules 24/25). Prints one JSON line per (shape, variant) plus totals.
 
-Usage: python scripts/gemm_lab.py --policies 0,31,32 [--model dlrm|dcnv2] [--rounds 5]
+Usage: python labs/gemm_lab.py --policies 0,31,32 [--model dlrm|dcnv2] [--rounds 5]
 """
 from __future__ import annotations
 

@@ -1,6 +1,6 @@
 #!/usr/bin/env python
 """Interaction fwd / bwd at the DLRM-1TB shape (B=8192, F=27, D=128), N calls
-each, for rocprofv3 kernel-trace / PMC passes (scripts/inter_pmc.sh)."""
+each, for rocprofv3 kernel-trace / PMC passes (labs/inter_pmc.sh)."""
 import sys
 
 import torch

@@ -1,4 +1,4 @@
-// Shared helpers of the GEMM structure labs (scripts/probes/gemm_*.hip):
+// Shared helpers of the GEMM structure labs (labs/probes/gemm_*.hip):
 // LDS-DMA pieces, swizzled fragment reads (the production layouts of
 // csrc/kernels/gemm.hip), XCD remap, a naive fp32 reference GEMM.
 #pragma once

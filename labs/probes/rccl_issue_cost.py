@@ -7,7 +7,7 @@ W=8 rank-0 sizes, next to a hipGraph replay and an event wait. Combined with
 ``bench.py --emulate-world 8`` (whose loopback collectives are cheaper to
 issue) it prices the real W=8 step's host issue time.
 
-    python scripts/probes/rccl_issue_cost.py [--iters 200]
+    python labs/probes/rccl_issue_cost.py [--iters 200]
 """
 import argparse
 import json

@@ -783,7 +783,7 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
         non-origin streams is routed through the origin (origin waits
         ``src``, ``dst`` waits origin): hipStreamEndCapture segfaults on this
         ROCm when a stream forked into a capture is itself the source of
-        another fork (scripts/probes/rccl_capture_probe.py, nested_* modes)."""
+        another fork (labs/probes/rccl_capture_probe.py, nested_* modes)."""
         o = self._cap_origin
         if o is None or dst == o or src == o:
             dst.wait_stream(src)

@@ -1,8 +1,8 @@
 """Multi-rank DLRM / DCN-v2 step as per-stream hipGraphs with the RCCL
 collectives inside (mixin of ``DLRMTrainer``; W > 1, pipelined input dist).
 
-Why this shape (all measured on this ROCm, scripts/probes/rccl_capture_probe.py and
-scripts/probes/whole_capture_bisect.py):
+Why this shape (all measured on this ROCm, labs/probes/rccl_capture_probe.py and
+labs/probes/whole_capture_bisect.py):
 
 * RCCL can only be captured on the capture's ORIGIN stream: a collective on a
   stream forked into a capture (torch's own async c10d collectives included)
@@ -280,7 +280,7 @@ class MultiRankStreamsMixin:
         # M: the bottom backward before the top weight grads, so the next
         # batch may load (x0 free) and the bottom bucket reduce sooner
         # (every segment boundary costs ~8 us of queue idle and every
-        # cross-stream wait ~15-23 us: scripts/probes/mr_sched_probe.py)
+        # cross-stream wait ~15-23 us: labs/probes/mr_sched_probe.py)
         composed = {
             # M: the bottom backward (+ the next batch's load into x0 / ids /
             # labels, all of whose readers have run) before the top weight

@@ -205,7 +205,7 @@ class RcclComm(Comm):
     # Under stream capture RCCL must be enqueued on the capture's ORIGIN
     # stream: a collective on any stream joined into the capture by an event
     # wait (torch's own async c10d collectives included) crashes
-    # hipStreamEndCapture on this ROCm (scripts/probes/rccl_capture_probe.py). So a
+    # hipStreamEndCapture on this ROCm (labs/probes/rccl_capture_probe.py). So a
     # capturing caller names its origin (``capture_origin``) and every
     # collective goes there -- origin waits on the caller's stream, the
     # collective runs, the caller's stream waits on it (async: when the handle

@@ -36,6 +36,7 @@ Design (MI355X-first):
 from __future__ import annotations
 
 import os
+import sys
 
 from typing import List, Optional, Sequence
 
@@ -46,6 +47,8 @@ from ..parallel.comm import as_comm
 from .planner import ShardingPlan
 from .tables import EmbOptimConfig, TableBatchedEmbedding, TableConfig
 
+
+_WARNED_SKIP_RW_READ = False
 
 class ShardedEmbeddingBags:
     """Pooled embedding features of one width D over a sharding plan.
@@ -534,8 +537,15 @@ class ShardedEmbeddingBags:
         self._rw_lag_pending = False
         if os.environ.get("TDFO_DIAG_SKIP_RW_READ") == "1":
             # diagnostics only (host never waits for the need: measures what
-            # the lagged read costs; an overflow would then raise at the next
-            # check_overflow instead of being redone)
+            # the lagged read costs; an overflow then raises at the next
+            # check_overflow -- pop_loss, every log line -- instead of being
+            # redone): say so once, loudly
+            global _WARNED_SKIP_RW_READ
+            if not _WARNED_SKIP_RW_READ:
+                _WARNED_SKIP_RW_READ = True
+                print("WARNING: TDFO_DIAG_SKIP_RW_READ=1 (diagnostics): row-wise capacity "
+                      "overflows are not redone; a dropped lookup raises at the next "
+                      "check_overflow / pop_loss", file=sys.stderr, flush=True)
             return False
         need = self._rw_mailbox().read()
         self.rw_lag_reads += 1
