@@ -272,14 +272,19 @@ tdfo::EncArgs enc_args(const Tensor& x, const Tensor& ids, const c10::optional<T
                        at::TensorList params, int64_t H, double rate, int64_t seed,
                        int64_t pad_id, double eps, at::TensorList saved) {
   TORCH_CHECK(x.dim() == 3, "encoder_layer: x [B, T, E]");
-  TORCH_CHECK(params.size() == 12 && saved.size() == 4, "encoder_layer: 12 params, 4 saved");
+  const bool sep = params.size() == 16;       // Q / K / V weights and biases apart
+  TORCH_CHECK((params.size() == 12 || sep) && saved.size() == 4,
+              "encoder_layer: 12 (or 16: separate Q/K/V) params, 4 saved");
   const int64_t B = x.size(0), T = x.size(1), E = x.size(2);
-  const int64_t FF = params[8].size(0);
-  const int64_t want[12] = {3 * E * E, 3 * E, E * E, E, E, E, E, E, FF * E, FF, E * FF, E};
-  for (int i = 0; i < 12; ++i) {
+  const int64_t FF = params[params.size() - 4].size(0);
+  const int64_t want12[12] = {3 * E * E, 3 * E, E * E, E, E, E, E, E, FF * E, FF, E * FF, E};
+  const int64_t want16[16] = {E * E, E * E, E * E, E, E, E, E * E, E, E, E, E, E,
+                              FF * E, FF, E * FF, E};
+  for (size_t i = 0; i < params.size(); ++i) {
     check_f32c(params[i], "encoder param");
-    TORCH_CHECK(params[i].numel() == want[i], "encoder_layer: param ", i, " has ",
-                params[i].numel(), " elements, expected ", want[i]);
+    const int64_t want = sep ? want16[i] : want12[i];
+    TORCH_CHECK(params[i].numel() == want, "encoder_layer: param ", i, " has ",
+                params[i].numel(), " elements, expected ", want);
   }
   check_f32c(x, "x");
   check_dev(ids, "ids");
@@ -301,9 +306,16 @@ tdfo::EncArgs enc_args(const Tensor& x, const Tensor& ids, const c10::optional<T
     a.step = step->data_ptr<int64_t>();
   }
   a.x = x.data_ptr<float>(); a.ids = ids.data_ptr<int64_t>();
-  const float** pp[12] = {&a.wqkv, &a.bqkv, &a.wo, &a.bo, &a.g1, &a.be1,
-                          &a.g2, &a.be2, &a.w1, &a.b1, &a.w2, &a.b2};
-  for (int i = 0; i < 12; ++i) *pp[i] = params[i].data_ptr<float>();
+  if (params.size() == 16) {
+    // [wq, wk, wv, bq, bk, bv, wo, bo, g1, be1, g2, be2, w1, b1, w2, b2]
+    const float** pp[16] = {&a.wqkv, &a.wk, &a.wv, &a.bqkv, &a.bk, &a.bv, &a.wo, &a.bo,
+                            &a.g1, &a.be1, &a.g2, &a.be2, &a.w1, &a.b1, &a.w2, &a.b2};
+    for (int i = 0; i < 16; ++i) *pp[i] = params[i].data_ptr<float>();
+  } else {
+    const float** pp[12] = {&a.wqkv, &a.bqkv, &a.wo, &a.bo, &a.g1, &a.be1,
+                            &a.g2, &a.be2, &a.w1, &a.b1, &a.w2, &a.b2};
+    for (int i = 0; i < 12; ++i) *pp[i] = params[i].data_ptr<float>();
+  }
   a.qkv = saved[0].data_ptr<float>(); a.ctx = saved[1].data_ptr<float>();
   a.x1 = saved[2].data_ptr<float>(); a.f = saved[3].data_ptr<float>();
   return a;
@@ -1367,7 +1379,9 @@ void two_tower(const Tensor& X, const Tensor& P, const Tensor& labels, double in
 void linear_xent(const Tensor& H, const Tensor& W, const Tensor& bias, const Tensor& labels,
                  double eps, int64_t ignore, const Tensor& dH, const Tensor& lossv,
                  const c10::optional<Tensor>& dW, const c10::optional<Tensor>& db,
-                 const c10::optional<Tensor>& loss, const c10::optional<Tensor>& loss_acc) {
+                 const c10::optional<Tensor>& loss, const c10::optional<Tensor>& loss_acc,
+                 const std::vector<Tensor>& ostate, const c10::optional<Tensor>& ohyper,
+                 const std::vector<double>& oparams, int64_t okind) {
   check_dev(H, "H");
   TORCH_CHECK(H.scalar_type() == at::kFloat && H.dim() == 2 && H.size(1) == 16 &&
               H.is_contiguous() && aligned16(H.data_ptr()), "linear_xent: H fp32 [N,16]");
@@ -1403,6 +1417,30 @@ void linear_xent(const Tensor& H, const Tensor& W, const Tensor& bias, const Ten
     TORCH_CHECK(loss && loss_acc->scalar_type() == at::kDouble && loss_acc->numel() >= 1,
                 "linear_xent: loss_acc fp64 [1] (with loss)");
     a.loss_acc = loss_acc->data_ptr<double>();
+  }
+  if (okind >= 0) {
+    // fused output-layer step: W / bias updated in place from moments
+    // ostate = [mW, vW, mb, vb]; oparams = [beta1, beta2, eps, weight_decay]
+    TORCH_CHECK(okind == tdfo::OPT_ADAM || okind == tdfo::OPT_ADAMW, "linear_xent: okind");
+    TORCH_CHECK(ostate.size() == 4 && ohyper.has_value() && oparams.size() == 4 &&
+                a.dW != nullptr, "linear_xent: fused step needs [mW, vW, mb, vb], hyper, 4 "
+                "params and dW / db scratch");
+    for (int k = 0; k < 4; ++k) {
+      check_dev(ostate[k], "ostate");
+      TORCH_CHECK(ostate[k].scalar_type() == at::kFloat && ostate[k].is_contiguous() &&
+                  ostate[k].numel() == (k < 2 ? V * 16 : V) && aligned16(ostate[k].data_ptr()),
+                  "linear_xent: moments");
+    }
+    check_dev(*ohyper, "ohyper");
+    TORCH_CHECK(ohyper->scalar_type() == at::kFloat && ohyper->numel() >= 3,
+                "linear_xent: hyper fp32 [lr, step, grad_scale]");
+    TORCH_CHECK(aligned16(bias.data_ptr()), "linear_xent: bias alignment");
+    a.okind = (int)okind;
+    a.mW = ostate[0].data_ptr<float>(); a.vW = ostate[1].data_ptr<float>();
+    a.mb = ostate[2].data_ptr<float>(); a.vb = ostate[3].data_ptr<float>();
+    a.ohyper = ohyper->data_ptr<float>();
+    a.beta1 = (float)oparams[0]; a.beta2 = (float)oparams[1];
+    a.oeps = (float)oparams[2]; a.owd = (float)oparams[3];
   }
   Tensor ws = at::empty({(int64_t)tdfo::linear_xent_workspace((int)N, V)},
                         H.options().dtype(at::kByte));
@@ -1632,8 +1670,9 @@ TORCH_LIBRARY(tdfo, m) {
   m.def("piece_copy(Tensor(a!) buf, Tensor pieces, int B, int w, int extent) -> ()");
   m.def("auc_hist(Tensor logits, Tensor labels, int nb, Tensor(a!) hist) -> ()");
   m.def("linear_xent(Tensor H, Tensor W, Tensor bias, Tensor labels, float eps, int ignore, "
-        "Tensor(a!) dH, Tensor(b!) lossv, Tensor(c!)? dW, Tensor(d!)? db, Tensor(e!)? loss=None, "
-        "Tensor(f!)? loss_acc=None) -> ()");
+        "Tensor(a!) dH, Tensor(b!) lossv, Tensor(c!)? dW, Tensor(d!)? db, Tensor(e!)? loss, "
+        "Tensor(f!)? loss_acc, Tensor(g!)[] ostate, Tensor? ohyper, float[] oparams, "
+        "int okind) -> ()");
   m.def("jagged_to_dense(Tensor values, Tensor offsets, int T, float pad, Tensor(a!) out) -> ()");
   m.def("dense_to_jagged(Tensor dense, Tensor offsets, Tensor(a!) vgrad) -> ()");
   m.def("jagged_ids_to_dense(Tensor values, Tensor offsets, int pad, Tensor(a!) out) -> ()");

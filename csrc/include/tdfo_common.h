@@ -71,6 +71,22 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// One Adam / AdamW element update (torch.optim.Adam's L2 form, or decoupled
+// weight decay), shared by the flat dense optimizer and the kernels that fuse
+// the update into their epilogue (linear_xent's output layer): contraction
+// off, so every caller gives the same bits. g is the gradient already
+// multiplied by the loss-scale unscale factor.
+__device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v, float lr,
+                                          float bc1, float bc2, float b1, float b2, float eps,
+                                          float wd, bool adamw) {
+#pragma clang fp contract(off)
+  if (adamw) p -= lr * wd * p;
+  else g += wd * p;
+  m = b1 * m + (1.f - b1) * g;
+  v = b2 * v + (1.f - b2) * g * g;
+  p -= lr * (m / bc1) / (sqrtf(v / bc2) + eps);
+}
+
 // Bijective XCD-aware remap of a 1-D workgroup id (cdna_hip_programming.md §5,
 // "XCD swizzle must be bijective"): consecutive remapped ids land on one XCD,
 // so tiles that share an operand panel share that XCD's L2.

@@ -382,6 +382,14 @@ struct LinearXentArgs {
   float* loss;             // optional scalar: sum(lossv) / max(1, n_valid)
   double* loss_acc;        // optional running sum: += loss (device, fp64)
   void* workspace;
+  // optional fused optimizer step of the output layer (okind OPT_ADAM /
+  // OPT_ADAMW; -1: none): W and bias updated in place from their gradient
+  // inside the kernels (dW / db then serve as scratch), moments mW/vW [V,16],
+  // mb/vb [V], ohyper = the flat optimizer's [lr, step, grad_scale]
+  int okind = -1;
+  float* mW = nullptr; float* vW = nullptr; float* mb = nullptr; float* vb = nullptr;
+  const float* ohyper = nullptr;
+  float beta1 = 0.9f, beta2 = 0.999f, oeps = 1e-8f, owd = 0.f;
 };
 size_t linear_xent_workspace(int N, int64_t V);
 // 1: f32-input MFMA pass1/wgrad (default), 0: VALU kernels; <0 queries.
@@ -409,6 +417,9 @@ struct EncArgs {
   int B, T, E, H, FF; float rate; int64_t seed; const int64_t* step; int64_t pad_id; float eps;
   const float* x; const int64_t* ids;
   const float *wqkv, *bqkv, *wo, *bo, *g1, *be1, *g2, *be2, *w1, *b1, *w2, *b2;
+  // optional: K / V projection weights and biases as separate tensors (then
+  // wqkv / bqkv point at Q's alone)
+  const float *wk = nullptr, *wv = nullptr, *bk = nullptr, *bv = nullptr;
   float *y, *qkv, *ctx, *x1, *f;
   const float* dy; float* dx; float* part;
 };

@@ -839,44 +839,41 @@ __device__ __forceinline__ void update_row(const EmbBwdArgs& a, const OptScalars
   }
 }
 
-// Partials handed between waves of ONE launch (the in-kernel combine below),
-// possibly across XCDs, whose L2s are not coherent: written and read with
-// agent-scope atomic read-modify-writes (exchange / add 0), which execute at
-// the device-coherent point, never in a stale L2 line. The producing wave's
-// lane 0 then signals with an agent-scope atomic add after the wave's
-// vmcnt(0) wait, and the wave whose add comes last reads. No wave ever waits
-// for another. (Plain sc1 stores / loads, MI355X_MICROARCH.md hand-off row 1,
-// read stale partials here: the reader's L2 can hold the workspace lines
-// from earlier kernels.) A few KB per step.
+// Partials handed between waves of ONE launch (the in-kernel combine below):
+// agent-scope (sc1) stores and loads; the producing wave's lane 0 signals
+// with an agent-scope atomic add after the wave's vmcnt(0) wait, and the wave
+// whose add comes last loads (MI355X_MICROARCH.md, inter-workgroup
+// visibility, hand-off row 1). No wave ever waits for another. (Atomic
+// read-modify-write hand-offs -- exchange / add 0 -- measured 18 us slower per
+// DLRM-1TB step: a 3-row table's run walks 85 partials through them.)
 template <int EPL>
 __device__ __forceinline__ void part_store(float* p, const float (&v)[EPL]) {
   if constexpr (EPL % 2 == 0) {
 #pragma unroll
     for (int u = 0; u < EPL; u += 2) {
-      const unsigned long long x = (unsigned long long)__float_as_uint(v[u]) |
-                                   ((unsigned long long)__float_as_uint(v[u + 1]) << 32);
-      __hip_atomic_exchange((unsigned long long*)(p + u), x, __ATOMIC_RELAXED,
-                            __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t x = (uint64_t)__float_as_uint(v[u]) |
+                         ((uint64_t)__float_as_uint(v[u + 1]) << 32);
+      __hip_atomic_store((uint64_t*)(p + u), x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   } else {
-    __hip_atomic_exchange((unsigned int*)p, __float_as_uint(v[0]), __ATOMIC_RELAXED,
-                          __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store((uint32_t*)p, __float_as_uint(v[0]), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
 template <int EPL>
-__device__ __forceinline__ void part_load(float (&v)[EPL], float* p) {
+__device__ __forceinline__ void part_load(float (&v)[EPL], const float* p) {
   if constexpr (EPL % 2 == 0) {
 #pragma unroll
     for (int u = 0; u < EPL; u += 2) {
-      const unsigned long long x = __hip_atomic_fetch_add(
-          (unsigned long long*)(p + u), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t x =
+          __hip_atomic_load((const uint64_t*)(p + u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       v[u] = __uint_as_float((uint32_t)x);
       v[u + 1] = __uint_as_float((uint32_t)(x >> 32));
     }
   } else {
-    v[0] = __uint_as_float(__hip_atomic_fetch_add((unsigned int*)p, 0u, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT));
+    v[0] = __uint_as_float(
+        __hip_atomic_load((const uint32_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   }
 }
 
@@ -889,13 +886,14 @@ __device__ __forceinline__ void part_load(float (&v)[EPL], float* p) {
 // bits (inlined into two kernels with contraction on, the update came out
 // 1 ulp apart on 8 of 13 K rows; a non-inlined call cost the update kernel
 // 224 B of scratch and 20 us).
-template <int D, int OPT>
+template <int D, int OPT, int HQ_MAX = 32>
 __device__ __forceinline__ void run_finish(const EmbBwdArgs& a, const OptScalars& o,
                                            int64_t cs, int64_t ce,
                            uint64_t row, float* head, float* tail, int lane) {
 #pragma clang fp contract(off)
   constexpr int EPL = BwdCfg<D>::EPL;
-  constexpr int HQ = EPL <= 2 ? 32 : (EPL <= 4 ? 16 : 8);
+  constexpr int HQ0 = EPL <= 2 ? 32 : (EPL <= 4 ? 16 : 8);
+  constexpr int HQ = HQ0 < HQ_MAX ? HQ0 : HQ_MAX;     // (the sum order does not depend on it)
   const int e0 = elem0<D>(lane);
   const bool act = D >= 64 || e0 < D;
   const int e0c = act ? e0 : 0;
@@ -931,7 +929,7 @@ __device__ __forceinline__ void run_finish(const EmbBwdArgs& a, const OptScalars
 // head / tail partials: with run metadata (``meta``, from the one-hot sort)
 // the last of a run's chunks to arrive finishes it here; otherwise the
 // chunk where it starts is listed for emb_combine_kernel.
-template <int D, typename K, bool GB, int OPT, int CH>
+template <int D, typename K, bool GB, int OPT, int CH, bool META = false>
 __global__ __launch_bounds__(256) void emb_chunk_kernel(
     EmbBwdArgs a, const K* __restrict__ keys, const int32_t* __restrict__ vals,
     const int64_t* __restrict__ goff, const float* __restrict__ gscale,
@@ -958,7 +956,7 @@ __global__ __launch_bounds__(256) void emb_chunk_kernel(
   const float mysc = gscale ? gscale[gi] : 1.f;
   const K prevk = start > 0 ? keys[start - 1] : (K)0;
   const K nextk = end < a.nnz ? keys[end] : (K)0;
-  const int2 md = meta != nullptr ? meta[c] : make_int2(-1, -1);
+  const int2 md = META ? meta[c] : make_int2(-1, -1);
   const K kup = __shfl_up(mykey, 1, 64);
   const K kdn = __shfl_down(mykey, 1, 64);
   const bool is_start = lane < len && (lane == 0 ? (start == 0 || prevk != mykey) : kup != mykey);
@@ -1024,12 +1022,12 @@ __global__ __launch_bounds__(256) void emb_chunk_kernel(
   const bool started_here = smask != 0;
   if (cont) {
     if (act) part_store<EPL>((started_here ? tail : head) + c * D + e0, acc);
-    if (meta == nullptr && started_here && lane == 0) {
+    if (!META && started_here && lane == 0) {
       const int slot = atomicAdd(tail_count, 1);
       if (slot < (int)((a.nnz + CH - 1) / CH)) tail_list[slot] = (int32_t)c;
     }
   }
-  if (meta != nullptr) {
+  if constexpr (META) {
     // arrivals: a head partial of the run that came from before (it ends here,
     // or covers the whole chunk), a tail partial of the run that starts here
     // and continues; the run's counter sits at its first chunk
@@ -1361,11 +1359,15 @@ bool onehot_path(const EmbBwdArgs& a) {
 
 // one run per table, chunks never straddling tables, single-block sort: the
 // sort writes run metadata and the update finishes crossing runs in-kernel
-// (no emb_combine_kernel launch). TDFO_EMB_INKERNEL_COMBINE=0: the combine
-// kernel.
+// (no emb_combine_kernel launch; TDFO_EMB_INKERNEL_COMBINE=1). Off by
+// default: isolated it takes the DLRM-1TB update from 57.5 to 43.2 us, but
+// the step runs 0.430-0.434 vs 0.412-0.414 ms with the separate combine
+// (same box, 300 steps; profiles/r06/notes.md): the last-arriving chunk's
+// walk over a tiny table's ~85 partials becomes the update kernel's tail,
+// which the next lookup waits behind.
 const int g_emb_inkernel_combine = [] {
   const char* e = getenv("TDFO_EMB_INKERNEL_COMBINE");
-  return e ? atoi(e) : 1;
+  return e ? atoi(e) : 0;
 }();
 
 bool meta_path(const EmbBwdArgs& a) {
@@ -1455,13 +1457,15 @@ void apply_impl(const EmbBwdArgs& a0, const WsLayout& L, hipStream_t s) {
     constexpr int CH = decltype(ch_c)::value;
     const int64_t nch = (a.nnz + CH - 1) / CH;
     int64_t blocks = (nch + 3) / 4;
-    if (a.grad_bf16)
-      hipLaunchKernelGGL((emb_chunk_kernel<D, K, true, OPT, CH>), dim3(blocks), dim3(256), 0, s, a,
-                         keys_out, vals_out, goff, gscale, head, tail, tlist, tcount, meta, rcnt);
-    else
-      hipLaunchKernelGGL((emb_chunk_kernel<D, K, false, OPT, CH>), dim3(blocks), dim3(256), 0, s,
-                         a, keys_out, vals_out, goff, gscale, head, tail, tlist, tcount, meta,
-                         rcnt);
+#define TDFO_CK(GBV, MV)                                                                   \
+    hipLaunchKernelGGL((emb_chunk_kernel<D, K, GBV, OPT, CH, MV>), dim3(blocks), dim3(256), 0, s, \
+                       a, keys_out, vals_out, goff, gscale, head, tail, tlist, tcount, meta, rcnt)
+    if (meta != nullptr) {
+      if (a.grad_bf16) TDFO_CK(true, true); else TDFO_CK(false, true);
+    } else {
+      if (a.grad_bf16) TDFO_CK(true, false); else TDFO_CK(false, false);
+    }
+#undef TDFO_CK
     TDFO_CHECK_HIP(hipGetLastError());
     if (meta != nullptr) return;        // crossing runs finished inside the update
     int64_t cblocks = (nch + 3) / 4;

@@ -84,11 +84,17 @@ struct WPtr {
 };
 __device__ __forceinline__ WPtr stage_weights(const EncArgs& a, const POff& po, float* w,
                                               int tid) {
-  const float* src[12] = {a.wqkv, a.bqkv, a.wo, a.bo, a.g1, a.be1,
-                          a.g2, a.be2, a.w1, a.b1, a.w2, a.b2};
-  const int off[13] = {po.wqkv, po.bqkv, po.wo, po.bo, po.g1, po.be1, po.g2,
+  // Q / K / V projections from three separate tensors (a.wk != null: the
+  // module's own parameters, no concatenated copy per step) or one [3E, E]
+  const int E = a.E, EE = E * E;
+  const bool sep = a.wk != nullptr;
+  const float* src[16] = {a.wqkv, sep ? a.wk : a.wqkv + EE, sep ? a.wv : a.wqkv + 2 * EE,
+                          a.bqkv, sep ? a.bk : a.bqkv + E, sep ? a.bv : a.bqkv + 2 * E,
+                          a.wo, a.bo, a.g1, a.be1, a.g2, a.be2, a.w1, a.b1, a.w2, a.b2};
+  const int off[17] = {po.wqkv, po.wqkv + EE, po.wqkv + 2 * EE, po.bqkv, po.bqkv + E,
+                       po.bqkv + 2 * E, po.wo, po.bo, po.g1, po.be1, po.g2,
                        po.be2, po.w1, po.b1, po.w2, po.b2, po.P};
-  for (int q = 0; q < 12; ++q)
+  for (int q = 0; q < 16; ++q)
     for (int i = tid; i < off[q + 1] - off[q]; i += ENC_THREADS) w[off[q] + i] = src[q][i];
   return {w + po.wqkv, w + po.bqkv, w + po.wo, w + po.bo, w + po.g1, w + po.be1,
           w + po.g2, w + po.be2, w + po.w1, w + po.b1, w + po.w2, w + po.b2};

@@ -555,13 +555,65 @@ __device__ __forceinline__ void xent_load_tok(XentTok& K, const float* __restric
   }
 }
 
+// Fused output-layer optimizer step (LinearXentArgs.okind >= 0): the rows'
+// final gradient updates W / bias in place (adam_elem, the flat optimizer's
+// own element update) instead of being written to dW / db and re-read by the
+// flat optimizer: one fewer 17 M-element gradient round trip per Bert4Rec
+// step. Only the launch that holds the complete gradient does it (the wgrad
+// kernel when every valid token fits one 128-token block, else the slab sum).
+struct XOpt {
+  float* W; float* bias; float* mW; float* vW; float* mb; float* vb;
+  float lr, bc1, bc2, b1, b2, eps, wd, gs;
+  bool adamw, on;
+};
+
+__device__ __forceinline__ XOpt xopt_of(const LinearXentArgs& a) {
+  XOpt o{};
+  o.on = a.okind >= 0;
+  if (!o.on) return o;
+  o.W = (float*)a.W; o.bias = (float*)a.bias;
+  o.mW = a.mW; o.vW = a.vW; o.mb = a.mb; o.vb = a.vb;
+  o.lr = a.ohyper[0];
+  const float step = a.ohyper[1];
+  o.gs = a.ohyper[2];
+  o.bc1 = 1.f - powf(a.beta1, step);
+  o.bc2 = 1.f - powf(a.beta2, step);
+  o.b1 = a.beta1; o.b2 = a.beta2; o.eps = a.oeps; o.wd = a.owd;
+  o.adamw = a.okind == OPT_ADAMW;
+  return o;
+}
+
+// W[v][c0..c0+3] (p = those weights, already in registers) and, if wb, bias[v]
+__device__ __forceinline__ void xopt_row(const XOpt& o, int64_t v, int c0, f32x4_t p, f32x4_t g,
+                                         bool wb, float gb) {
+  const int64_t i = v * XE + c0;
+  const f32x4_t m4 = *(const f32x4_t*)(o.mW + i), w4 = *(const f32x4_t*)(o.vW + i);
+  float pp[4], mm[4], ww[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    pp[r] = p[r]; mm[r] = m4[r]; ww[r] = w4[r];
+    adam_elem(pp[r], g[r] * o.gs, mm[r], ww[r], o.lr, o.bc1, o.bc2, o.b1, o.b2, o.eps, o.wd,
+              o.adamw);
+  }
+  *(f32x4_t*)(o.W + i) = (f32x4_t){pp[0], pp[1], pp[2], pp[3]};
+  *(f32x4_t*)(o.mW + i) = (f32x4_t){mm[0], mm[1], mm[2], mm[3]};
+  *(f32x4_t*)(o.vW + i) = (f32x4_t){ww[0], ww[1], ww[2], ww[3]};
+  if (wb) {
+    float pb = o.bias[v], mbv = o.mb[v], vbv = o.vb[v];
+    adam_elem(pb, gb * o.gs, mbv, vbv, o.lr, o.bc1, o.bc2, o.b1, o.b2, o.eps, o.wd, o.adamw);
+    o.bias[v] = pb;
+    o.mb[v] = mbv;
+    o.vb[v] = vbv;
+  }
+}
+
 // One 16-row tile for NG token groups: X^T = H W^T (bias as C input), dz in
 // registers, dW^T = H^T dz^T; writes dW rows (float4 per lane) and db.
 template <int NG>
 __device__ __forceinline__ void xent_wgrad_tile(const XentTok* K, f32x4_t wa, float b, int v,
                                                 int64_t V, float off, float hit, float pad_off,
                                                 float scale, float* __restrict__ dW,
-                                                float* __restrict__ db, int g) {
+                                                float* __restrict__ db, int g, const XOpt& xo) {
   f32x4_t dw[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
   float dbs = 0.f;
 #pragma unroll
@@ -587,6 +639,10 @@ __device__ __forceinline__ void xent_wgrad_tile(const XentTok* K, f32x4_t wa, fl
   }
   dbs = (sum4rows(dbs) + pad_off) * scale;
   if (v < V) {
+    if (xo.on) {                           // the complete gradient: step in place
+      xopt_row(xo, v, 4 * g, wa, dw[0] + dw[1], g == 0, dbs);
+      return;
+    }
     *(f32x4_t*)(dW + (int64_t)v * XE + 4 * g) = dw[0] + dw[1];    // dW^T[4g+r][v]
     if (g == 0) db[v] = dbs;
   }
@@ -602,7 +658,7 @@ __device__ __forceinline__ void xent_wgrad_body(const float* __restrict__ W,
                                                 const int32_t* __restrict__ ytok,
                                                 const float* __restrict__ lse, int nv, int tok0,
                                                 float* __restrict__ dW, float* __restrict__ db,
-                                                int t, int g) {
+                                                int t, int g, const XOpt& xo) {
   const float scale = 1.f / (float)max(1, nv);
   const float off = eps / (float)V, hit = 1.f - eps;
   XentTok K[NG];
@@ -627,7 +683,7 @@ __device__ __forceinline__ void xent_wgrad_body(const float* __restrict__ W,
         wa0 = *(const f32x4_t*)(Wt + (i + 2) * 16 * XE + la);
         b0 = bt[(i + 2) * 16 + t];
       }
-      xent_wgrad_tile<NG>(K, wa, b, vb + 16 * i, V, off, hit, pad_off, scale, dW, db, g);
+      xent_wgrad_tile<NG>(K, wa, b, vb + 16 * i, V, off, hit, pad_off, scale, dW, db, g, xo);
     }
     if (i + 1 < nfull) {
       const f32x4_t wa = wa1;
@@ -636,7 +692,8 @@ __device__ __forceinline__ void xent_wgrad_body(const float* __restrict__ W,
         wa1 = *(const f32x4_t*)(Wt + (i + 3) * 16 * XE + la);
         b1 = bt[(i + 3) * 16 + t];
       }
-      xent_wgrad_tile<NG>(K, wa, b, vb + 16 * (i + 1), V, off, hit, pad_off, scale, dW, db, g);
+      xent_wgrad_tile<NG>(K, wa, b, vb + 16 * (i + 1), V, off, hit, pad_off, scale, dW, db, g,
+                          xo);
     }
   }
   const int64_t rt = V / 16;                             // ragged last tile
@@ -644,7 +701,7 @@ __device__ __forceinline__ void xent_wgrad_body(const float* __restrict__ W,
     const int64_t vr = min(rt * 16 + t, V - 1);
     const f32x4_t wa = *(const f32x4_t*)(W + vr * XE + 4 * g);
     xent_wgrad_tile<NG>(K, wa, bias[vr] * LOG2E, (int)(rt * 16) + t, V, off, hit, pad_off, scale,
-                        dW, db, g);
+                        dW, db, g, xo);
   }
 }
 
@@ -660,12 +717,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void xe
                                                              const float* __restrict__ lse,
                                                              float* __restrict__ dW,
                                                              float* __restrict__ db,
-                                                             float* __restrict__ slab) {
+                                                             float* __restrict__ slab,
+                                                             LinearXentArgs xa) {
   const int l = threadIdx.x, t = l & 15, g = l >> 4;
   const int nv = *count;
   const int tb = blockIdx.y, tok0 = tb * 16 * XG;
   const int ng = min(XG, max(0, (nv - tok0 + 15) / 16));
   if (tb > 0 && ng == 0) return;
+  // fused optimizer only when this launch holds the whole gradient (one
+  // 128-token block); else xent_slab_reduce_kernel steps after the sum
+  XOpt xo = xopt_of(xa);
+  xo.on = xo.on && nv <= 16 * XG;
   float* dWo = dW;
   float* dbo = db;
   if (tb > 0) {
@@ -677,13 +739,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void xe
 #define XCASE(n)                                                                            \
     case n:                                                                                 \
       xent_wgrad_body<n>(W, bias, V, eps, tile0, tpw, htok, ytok, lse, nv, tok0, dWo, dbo, \
-                         t, g);                                                             \
+                         t, g, xo);                                                         \
       break;
     XCASE(1) XCASE(2) XCASE(3) XCASE(4) XCASE(5) XCASE(6) XCASE(7) XCASE(8)
 #undef XCASE
     default: {                    // no valid token: dW = db = 0 for this run
       const int64_t r1 = min((tile0 + tpw) * 16, V);
       for (int64_t v = tile0 * 16 + t; v < r1; v += 16) {
+        if (xo.on) {                 // (a zero-gradient step still moves W)
+          xopt_row(xo, v, 4 * g, *(const f32x4_t*)(W + v * XE + 4 * g),
+                   (f32x4_t){0.f, 0.f, 0.f, 0.f}, g == 0, 0.f);
+          continue;
+        }
         *(f32x4_t*)(dWo + v * XE + 4 * g) = (f32x4_t){0.f, 0.f, 0.f, 0.f};
         if (g == 0) dbo[v] = 0.f;
       }
@@ -696,9 +763,11 @@ __global__ __launch_bounds__(256) void xent_slab_reduce_kernel(int64_t V,
                                                                const int32_t* __restrict__ count,
                                                                const float* __restrict__ slab,
                                                                float* __restrict__ dW,
-                                                               float* __restrict__ db) {
+                                                               float* __restrict__ db,
+                                                               LinearXentArgs xa) {
   const int nblk = (*count + 16 * XG - 1) / (16 * XG);
-  if (nblk <= 1) return;
+  if (nblk <= 1) return;           // (the wgrad kernel holds the whole gradient)
+  const XOpt xo = xopt_of(xa);
   const int64_t n4 = V * XE / 4;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4 + V;
        i += (int64_t)gridDim.x * 256) {
@@ -706,12 +775,27 @@ __global__ __launch_bounds__(256) void xent_slab_reduce_kernel(int64_t V,
       f32x4_t a = ((f32x4_t*)dW)[i];
       for (int k = 1; k < nblk; ++k)
         a += ((const f32x4_t*)(slab + (int64_t)(k - 1) * V * (XE + 1)))[i];
-      ((f32x4_t*)dW)[i] = a;
+      if (xo.on) {
+        const int64_t v = i / (XE / 4);
+        const int c0 = (int)(i - v * (XE / 4)) * 4;
+        xopt_row(xo, v, c0, *(const f32x4_t*)(xo.W + v * XE + c0), a, false, 0.f);
+      } else {
+        ((f32x4_t*)dW)[i] = a;
+      }
     } else {
       const int64_t v = i - n4;
       float a = db[v];
       for (int k = 1; k < nblk; ++k) a += slab[(int64_t)(k - 1) * V * (XE + 1) + V * XE + v];
-      db[v] = a;
+      if (xo.on) {
+        float pb = xo.bias[v], mbv = xo.mb[v], vbv = xo.vb[v];
+        adam_elem(pb, a * xo.gs, mbv, vbv, xo.lr, xo.bc1, xo.bc2, xo.b1, xo.b2, xo.eps, xo.wd,
+                  xo.adamw);
+        xo.bias[v] = pb;
+        xo.mb[v] = mbv;
+        xo.vb[v] = vbv;
+      } else {
+        db[v] = a;
+      }
     }
   }
 }
@@ -818,13 +902,26 @@ void linear_xent(const LinearXentArgs& a, hipStream_t s) {
       const int tpw = (int)std::max<int64_t>(1, (tiles + 4095) / 4096);
       hipLaunchKernelGGL(xent_wgrad_mfma_kernel,
                          dim3((unsigned)((tiles + tpw - 1) / tpw), blocks), dim3(64), 0, s, a.W,
-                         a.bias, a.V, a.eps, tpw, htok, ytok, count, lse, a.dW, a.db, slab);
+                         a.bias, a.V, a.eps, tpw, htok, ytok, count, lse, a.dW, a.db, slab, a);
       if (blocks > 1)
         hipLaunchKernelGGL(xent_slab_reduce_kernel, dim3(2048), dim3(256), 0, s, a.V, count,
-                           slab, a.dW, a.db);
+                           slab, a.dW, a.db, a);
     } else {
       hipLaunchKernelGGL(xent_wgrad_kernel, dim3((unsigned)((a.V + 255) / 256)), dim3(256), 0, s,
                          a.H, a.W, a.bias, a.labels, a.V, a.eps, idx, count, lse, a.dW, a.db);
+      if (a.okind >= 0) {           // VALU path: the flat optimizer's kernel on W, bias
+        for (int part = 0; part < 2; ++part) {
+          DenseOptArgs o{};
+          o.p = part ? (float*)a.bias : (float*)a.W;
+          o.g = part ? a.db : a.dW;
+          o.m = part ? a.mb : a.mW;
+          o.v = part ? a.vb : a.vW;
+          o.n = part ? (a.V + 3) / 4 * 4 : a.V * XE;    // (flat buffers are padded)
+          o.opt = a.okind; o.hyper = a.ohyper;
+          o.beta1 = a.beta1; o.beta2 = a.beta2; o.eps = a.oeps; o.weight_decay = a.owd;
+          dense_optimizer(o, s);
+        }
+      }
     }
   }
   if (a.loss)

@@ -63,14 +63,9 @@ __global__ __launch_bounds__(256) void dense_opt_kernel(DenseOptArgs a) {
     float mv[4] = {m.x, m.y, m.z, m.w}, vv[4] = {v.x, v.y, v.z, v.w};
     if (adam) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        float gg = gv[u];
-        if (a.opt == OPT_ADAM) gg += a.weight_decay * pv[u];
-        else pv[u] -= lr * a.weight_decay * pv[u];
-        mv[u] = a.beta1 * mv[u] + (1.f - a.beta1) * gg;
-        vv[u] = a.beta2 * vv[u] + (1.f - a.beta2) * gg * gg;
-        pv[u] -= lr * (mv[u] / bc1) / (sqrtf(vv[u] / bc2) + a.eps);
-      }
+      for (int u = 0; u < 4; ++u)
+        adam_elem(pv[u], gv[u], mv[u], vv[u], lr, bc1, bc2, a.beta1, a.beta2, a.eps,
+                  a.weight_decay, a.opt == OPT_ADAMW);
       ((float4*)a.m)[i] = make_float4(mv[0], mv[1], mv[2], mv[3]);
       ((float4*)a.v)[i] = make_float4(vv[0], vv[1], vv[2], vv[3]);
     } else if (a.opt == OPT_SGD) {

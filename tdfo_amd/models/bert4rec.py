@@ -26,6 +26,7 @@ What is different on MI355X:
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, Optional
 
 import torch
@@ -105,10 +106,11 @@ class _EncoderLayerFn(torch.autograd.Function):
     """Whole pre-norm transformer block as two HIP kernels (encoder.hip)."""
 
     @staticmethod
-    def forward(ctx, x, ids, step, H, rate, seed, eps, *params):
+    def forward(ctx, x, ids, step, H, rate, seed, eps, gdst, *params):
         x = x.contiguous()
         B, T, E = x.shape
-        FF = params[8].shape[0]
+        FF = params[-4].shape[0]
+        ctx.gdst = gdst
         dev = x.device
         saved = [torch.empty(B, T, 3 * E, device=dev), torch.empty(B, T, E, device=dev),
                  torch.empty(B, T, E, device=dev), torch.empty(B, T, FF, device=dev)]
@@ -122,21 +124,29 @@ class _EncoderLayerFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         t = ctx.saved_tensors
-        x, ids, step, params, saved = t[0], t[1], t[2], list(t[3:15]), list(t[15:])
+        npar = len(t) - 7                   # x, ids, step, params..., 4 saved
+        x, ids, step = t[0], t[1], t[2]
+        params, saved = list(t[3:3 + npar]), list(t[3 + npar:])
         H, rate, seed, eps = ctx.cfg
         B, T, E = x.shape
-        FF = params[8].shape[0]
+        FF = params[-4].shape[0]
         P = ops.encoder_param_count(E, FF)
         part = torch.empty(B * P, device=x.device)
         grad = torch.empty(P, device=x.device)
         dx = torch.empty_like(x)
         ops.encoder_layer_bwd(x, ids, step, params, H, rate, seed, PAD_ID, eps, saved,
                               dy.contiguous(), dx, part, grad)
+        if ctx.gdst is not None:
+            # every parameter gradient straight into the flat gradient buffer:
+            # one scatter instead of autograd's cat-backward + 16 adds
+            flat, idx = ctx.gdst
+            flat.index_copy_(0, idx, grad)
+            return (dx, None, None, None, None, None, None, None) + (None,) * len(params)
         grads, o = [], 0
         for p in params:
             grads.append(grad[o:o + p.numel()].view_as(p))
             o += p.numel()
-        return (dx, None, None, None, None, None, None, *grads)
+        return (dx, None, None, None, None, None, None, None, *grads)
 
 
 class _SeqPrologueFn(torch.autograd.Function):
@@ -145,9 +155,10 @@ class _SeqPrologueFn(torch.autograd.Function):
     their backward library ops, incl. the positional-encoding grad reduction."""
 
     @staticmethod
-    def forward(ctx, x, pos, gamma, beta, eps, rate, seed, step):
+    def forward(ctx, x, pos, gamma, beta, eps, rate, seed, step, gdst=None):
         x = x.contiguous()
         n = pos.numel()
+        ctx.gdst = gdst
         M = x.numel() // n
         y = torch.empty_like(x)
         mean = torch.empty(M, dtype=torch.float32, device=x.device)
@@ -168,8 +179,12 @@ class _SeqPrologueFn(torch.autograd.Function):
         out3 = torch.empty(3 * n, dtype=torch.float32, device=x.device)
         ops.seq_prologue_bwd(x, pos.contiguous(), g.contiguous(), n, gamma.contiguous(), mean,
                              rstd, rate, seed, step, dx, part, out3)
+        if ctx.gdst is not None:            # [gamma | beta | pos] -> the flat gradients
+            flat, idx = ctx.gdst
+            flat.index_copy_(0, idx, out3)
+            return (dx, None, None, None, None, None, None, None, None)
         return (dx, out3[2 * n:].view_as(pos), out3[:n].view_as(gamma),
-                out3[n:2 * n].view_as(gamma), None, None, None, None)
+                out3[n:2 * n].view_as(gamma), None, None, None, None, None)
 
 
 _ENC_OK: Dict[tuple, bool] = {}
@@ -258,9 +273,10 @@ class TransformerBlock(nn.Module):
         self.dropout = nn.Dropout(dropout)
 
     def _fused_params(self):
+        # Q / K / V as the module's own tensors (the kernel stages them apart:
+        # no concatenated copy per step)
         att, ff = self.attention, self.feed_forward
-        return [torch.cat([l.weight for l in att.linear_layers], 0),
-                torch.cat([l.bias for l in att.linear_layers], 0),
+        return [l.weight for l in att.linear_layers] + [l.bias for l in att.linear_layers] + [
                 att.output_linear.weight, att.output_linear.bias,
                 self.input_sublayer.norm.weight, self.input_sublayer.norm.bias,
                 self.output_sublayer.norm.weight, self.output_sublayer.norm.bias,
@@ -272,7 +288,8 @@ class TransformerBlock(nn.Module):
                 and _fused_block_ok(x.shape[1], x.shape[2], att.h, self.feed_forward.w_1.out_features)):
             rate = self.dropout.p if self.training else 0.0
             return _EncoderLayerFn.apply(x, mask.ids, mask.step, att.h, rate, att.seed,
-                                         self.input_sublayer.norm.eps, *self._fused_params())
+                                         self.input_sublayer.norm.eps,
+                                         getattr(self, "gdst", None), *self._fused_params())
         x = self.input_sublayer(x, lambda y: self.attention(y, mask))
         x = self.output_sublayer(x, self.feed_forward)
         return self.dropout(x)
@@ -350,7 +367,7 @@ class ItemEmbedding(nn.Module):
 
 class _LinearXentFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, H, W, b, labels, eps, loss_acc, unit_grad):
+    def forward(ctx, H, W, b, labels, eps, loss_acc, unit_grad, step=None):
         N = H.shape[0]
         dH = torch.empty_like(H)
         lossv = torch.empty(N, dtype=torch.float32, device=H.device)
@@ -364,7 +381,7 @@ class _LinearXentFn(torch.autograd.Function):
         loss = torch.empty(1, dtype=torch.float32, device=H.device)
         # the kernel also reduces the mean loss (and adds it to loss_acc)
         ops.linear_xent(H, W, b, labels, eps, PAD_ID, dH, lossv, dW, db, loss=loss,
-                        loss_acc=loss_acc)
+                        loss_acc=loss_acc, step=step if direct else None)
         ctx.save_for_backward(dH, dW, db)
         ctx.unit_grad = unit_grad
         ctx.direct = direct
@@ -375,20 +392,22 @@ class _LinearXentFn(torch.autograd.Function):
         dH, dW, db = ctx.saved_tensors
         if ctx.unit_grad:      # caller's promise: the loss is backward()'s root (g == 1)
             if ctx.direct:
-                return dH, None, None, None, None, None, None
-            return dH, dW, db, None, None, None, None
-        return dH * g, dW * g, db * g, None, None, None, None
+                return dH, None, None, None, None, None, None, None
+            return dH, dW, db, None, None, None, None, None
+        return dH * g, dW * g, db * g, None, None, None, None, None
 
 
-def linear_cross_entropy(H, W, b, labels, eps=0.1, loss_acc=None, unit_grad=False):
+def linear_cross_entropy(H, W, b, labels, eps=0.1, loss_acc=None, unit_grad=False, step=None):
     """mean CE(ignore_index=0, label_smoothing=eps) of H @ W^T + b, fused.
     loss_acc (fp64 [1]): the kernel adds the loss to it. unit_grad: the
     returned loss is the root of backward() (gradient exactly 1) and W / b
     feed nothing else, so the saved gradients are returned without the
     scaling launches -- and when W.grad / b.grad exist (the trainer's flat
-    gradient views, zeroed each step) they are written there directly."""
+    gradient views, zeroed each step) they are written there directly.
+    step: the optimizer step of W / b fused into the kernels (see
+    ops.linear_xent; only with unit_grad and direct gradient buffers)."""
     return _LinearXentFn.apply(H.contiguous(), W, b, labels.contiguous(), eps, loss_acc,
-                               unit_grad)
+                               unit_grad, step)
 
 
 class Bert4Rec(nn.Module):
@@ -421,7 +440,7 @@ class Bert4Rec(nn.Module):
             rate = self.emb_dropout.p if self.training else 0.0
             x = _SeqPrologueFn.apply(item_emb, self.positional_encoding, self.layernorm.weight,
                                      self.layernorm.bias, self.layernorm.eps, rate,
-                                     0x5EED0E3B, self.rng_step)
+                                     0x5EED0E3B, self.rng_step, getattr(self, "gdst", None))
         else:
             x = self.emb_dropout(layer_norm(item_emb + self.positional_encoding, self.layernorm))
         for blk in self.transformer_blocks:
@@ -484,6 +503,26 @@ class Bert4RecTrainer:
                 dist.broadcast(p.data, 0, group=group)
         self.opt = FlatOptimizer(self.model.parameters(), "adam", lr=lr, weight_decay=wd,
                                  group=group if world > 1 else None)
+        # One rank: the output layer's Adam step runs inside the fused
+        # Linear+CE kernels, which hold its complete gradient (no 17 M-element
+        # gradient written and re-read by the flat optimizer, no zero fill);
+        # the flat optimizer steps the rest. More ranks all-reduce the
+        # gradient first. TDFO_XENT_FUSED_STEP=0: the unfused path (A/B).
+        self._xent_step = None
+        if (world == 1 and dev.type == "cuda" and not self.opt.dynamic_scale
+                and os.environ.get("TDFO_XENT_FUSED_STEP", "1") != "0"):
+            out = self.model.out
+            mw, vw = self.opt.moments(out.weight)
+            mb, vb = self.opt.moments(out.bias)
+            self._xent_step = (self.opt.opt, [mw, vw, mb, vb], self.opt.hyper, self.opt.beta1,
+                               self.opt.beta2, self.opt.eps, self.opt.wd)
+            self.opt.exclude([out.weight, out.bias])
+        # Fused encoder kernels write their parameter gradients into the flat
+        # gradient buffer through one index_copy each (maps built once from the
+        # flat views), so autograd accumulates nothing there (the QKV cat's
+        # backward and 35 AccumulateGrad adds per step before)
+        if dev.type == "cuda" and os.environ.get("TDFO_B4R_DIRECT_GRADS", "1") != "0":
+            self._attach_direct_grads()
         self.seqs = torch.zeros(batch_size, max_len, dtype=torch.int64, device=dev)
         self.labels = torch.zeros(batch_size, max_len, dtype=torch.int64, device=dev)
         self.loss_sum = torch.zeros(1, dtype=torch.float64, device=dev)
@@ -498,6 +537,28 @@ class Bert4RecTrainer:
         self.item.step_bumped_by_caller = True
         eh = self.item.engine._hyper if mode == "dmp" else self.item.hyper
         self._counters = [self.opt.hyper[1:2], eh[1:2], self.model.rng_step]
+
+    def _flat_index(self, params) -> torch.Tensor:
+        base = self.opt.grad.data_ptr()
+        idx = []
+        for p in params:
+            off = (p.grad.data_ptr() - base) // 4
+            assert 0 <= off and p.grad.is_contiguous(), "parameter grad is not a flat view"
+            idx.append(torch.arange(off, off + p.numel(), dtype=torch.int64))
+        return torch.cat(idx).to(self.device)
+
+    def _attach_direct_grads(self):
+        m = self.model
+        m.gdst = (self.opt.grad, self._flat_index([m.layernorm.weight, m.layernorm.bias,
+                                                   m.positional_encoding]))
+        for blk in m.transformer_blocks:
+            att, ff = blk.attention, blk.feed_forward
+            order = ([l.weight for l in att.linear_layers] + [l.bias for l in att.linear_layers]
+                     + [att.output_linear.weight, att.output_linear.bias,
+                        blk.input_sublayer.norm.weight, blk.input_sublayer.norm.bias,
+                        blk.output_sublayer.norm.weight, blk.output_sublayer.norm.bias,
+                        ff.w_1.weight, ff.w_1.bias, ff.w_2.weight, ff.w_2.bias])
+            blk.gdst = (self.opt.grad, self._flat_index(order))
 
     # ------------------------------------------------------------ train
     def _embed(self, seqs):
@@ -514,13 +575,13 @@ class Bert4RecTrainer:
         h = self.model.encode(x, seqs)
         loss = linear_cross_entropy(h.reshape(-1, self.E), self.model.out.weight,
                                     self.model.out.bias, labels.reshape(-1), self.eps,
-                                    loss_acc=self.loss_sum, unit_grad=True)
+                                    loss_acc=self.loss_sum, unit_grad=True, step=self._xent_step)
         loss.backward()
         return loss
 
     def _step_body(self, seqs, labels):
         ops.bump(self._counters)
-        self.opt.grad.zero_()
+        self.opt.zero_grads()
         loss = self._fwd_bwd(seqs, labels)
         self.opt.all_reduce_grads(average=True)
         self.opt.step()

@@ -752,13 +752,22 @@ def two_tower(X, P, labels, inv_n, logits, dX=None, part=None, loss_scale=None, 
 
 
 def linear_xent(H, W, bias, labels, eps, ignore, dH, lossv, dW=None, db=None, loss=None,
-                loss_acc=None):
+                loss_acc=None, step=None):
     """Fused Linear(16->V) + label-smoothed CrossEntropy, fwd+bwd (no logits).
     loss (fp32 [1]): mean loss over the non-ignored tokens; loss_acc (fp64
-    [1]): += that loss (device running sum)."""
+    [1]): += that loss (device running sum). step = (opt, [mW, vW, mb, vb],
+    hyper, beta1, beta2, eps, weight_decay): apply the flat optimizer's
+    Adam / AdamW step to W and bias in place inside the kernels (dW / db are
+    then scratch and are not the gradient on return)."""
     if _gpu(H):
-        _native().linear_xent(H, W, bias, labels, float(eps), int(ignore), dH, lossv, dW, db,
-                              loss, loss_acc)
+        if step is None:
+            _native().linear_xent(H, W, bias, labels, float(eps), int(ignore), dH, lossv, dW, db,
+                                  loss, loss_acc, [], None, [], -1)
+        else:
+            opt, st, hyper, b1, b2, oeps, wd = step
+            _native().linear_xent(H, W, bias, labels, float(eps), int(ignore), dH, lossv, dW, db,
+                                  loss, loss_acc, list(st), hyper,
+                                  [float(b1), float(b2), float(oeps), float(wd)], int(opt))
     else:
         ref.linear_xent(H, W, bias, labels, eps, ignore, dH, lossv, dW, db)
         if loss is not None:
@@ -766,6 +775,11 @@ def linear_xent(H, W, bias, labels, eps, ignore, dH, lossv, dW=None, db=None, lo
             loss.view(-1)[0] = lossv.sum() / nv
             if loss_acc is not None:
                 loss_acc.view(-1)[0] += loss.view(-1)[0].double()
+        if step is not None:
+            opt, st, hyper, b1, b2, oeps, wd = step
+            for p, g, m, v in ((W, dW, st[0], st[1]), (bias, db, st[2], st[3])):
+                ref.dense_optimizer(p.view(-1), g.view(-1), m.view(-1), v.view(-1), None, opt,
+                                    hyper, b1, b2, oeps, wd, 0.0, None)
 
 
 def jagged_to_dense(values, offsets, T, pad, out):

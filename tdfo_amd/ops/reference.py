@@ -768,6 +768,8 @@ def enc_site_mul(B: int, T: int, N: int, rate: float, seed: int, step: int, site
 def encoder_layer(x, ids, params, H, rate, seed, step, pad_id=0, eps=1e-5):
     """Differentiable torch reference of the fused pre-norm transformer block
     (same math and dropout masks as csrc/kernels/encoder.hip)."""
+    if len(params) == 16:                 # Q / K / V weights and biases as separate tensors
+        params = ([torch.cat(params[0:3], 0), torch.cat(params[3:6], 0)] + list(params[6:]))
     wqkv, bqkv, wo, bo, g1, be1, g2, be2, w1, b1, w2, b2 = params
     B, T, E = x.shape
     dev = x.device

@@ -68,6 +68,39 @@ class FlatOptimizer:
         self.found_inf = torch.zeros(1, dtype=torch.float32, device=dev) if dynamic_scale else None
         self.scale = 2.0 ** 15 if dynamic_scale else 1.0
         self._good_steps = 0
+        self._ranges = [(0, self.numel)]     # flat ranges step() / zero_grads() cover
+
+    def exclude(self, params) -> None:
+        """Leave ``params`` out of step() and zero_grads(): a kernel that
+        holds their complete gradient applies the same element update in its
+        epilogue (e.g. linear_xent's fused output-layer step)."""
+        ids = {id(p) for p in params}
+        cut = sorted((off, off + -(-n // ALIGN) * ALIGN) for p, off, n in self._views
+                     if id(p) in ids)
+        ranges, lo = [], 0
+        for a, b in cut:
+            if a > lo:
+                ranges.append((lo, a))
+            lo = max(lo, b)
+        if lo < self.numel:
+            ranges.append((lo, self.numel))
+        self._ranges = ranges
+
+    def moments(self, p):
+        """(m, v) views of parameter ``p``'s optimizer state."""
+        for q, off, n in self._views:
+            if q is p:
+                return (self.m[off: off + n].view_as(p) if self.m is not None else None,
+                        self.v[off: off + n].view_as(p) if self.v is not None else None)
+        raise KeyError("not a parameter of this optimizer")
+
+    def zero_grads(self):
+        """Zero the gradients step() will read (excluded ranges untouched)."""
+        if self._ranges == [(0, self.numel)]:
+            self.grad.zero_()
+        else:
+            for lo, hi in self._ranges:
+                self.grad[lo:hi].zero_()
 
     # ------------------------------------------------------------------
     def zero_grad(self):
@@ -108,9 +141,14 @@ class FlatOptimizer:
             ops.check_finite(self.grad, self.found_inf)
         if not self.step_bumped_by_caller:  # (else: the caller's one-launch ops.bump)
             self.hyper[1:2].add_(1.0)
-        ops.dense_optimizer(self.flat, self.grad, self.m, self.v, self.shadow, self.opt,
-                            self.hyper, self.beta1, self.beta2, self.eps, self.wd, self.momentum,
-                            self.found_inf)
+        for lo, hi in self._ranges:
+            sl = slice(lo, hi)
+            ops.dense_optimizer(self.flat[sl], self.grad[sl],
+                                self.m[sl] if self.m is not None else None,
+                                self.v[sl] if self.v is not None else None,
+                                self.shadow[sl] if self.shadow is not None else None, self.opt,
+                                self.hyper, self.beta1, self.beta2, self.eps, self.wd,
+                                self.momentum, self.found_inf)
         if self.dynamic_scale:
             self._update_scale()
 

@@ -46,6 +46,52 @@ def test_linear_xent_kernel_matches_reference(V, N, hs, xent_impl):
         assert err < 2e-4, (name, err)
 
 
+@pytest.mark.parametrize("opt", [ops.OPT_ADAM, ops.OPT_ADAMW])
+@pytest.mark.parametrize("V,N", [(4099, 320), (5003, 1030), (600_001, 320), (100, 64)])
+def test_linear_xent_fused_step_matches_separate_optimizer(V, N, opt, xent_impl):
+    """The output layer's Adam step inside the kernels (one token block: the
+    wgrad epilogue; several: the slab sum; VALU impl: a trailing optimizer
+    launch) equals linear_xent + the flat dense optimizer, bit for bit; N=64
+    with every label ignored checks the zero-gradient step."""
+    torch.manual_seed(V + N)
+    H = torch.randn(N, 16, device=DEV)
+    W = torch.randn(V, 16, device=DEV) * 0.2
+    b = torch.randn(V, device=DEV) * 0.1
+    y = torch.randint(1, V, (N,), device=DEV)
+    y[torch.rand(N, device=DEV) < 0.6] = 0
+    if V == 100:
+        y.zero_()
+    pad = -(-V // 64) * 64                    # flat-buffer padding (optim/flat.py ALIGN)
+    mom = [torch.rand(V * 16, device=DEV), torch.rand(V * 16, device=DEV),
+           torch.rand(pad, device=DEV), torch.rand(pad, device=DEV)]
+    hyper = torch.tensor([1e-3, 7.0, 1.0], device=DEV)
+    prm = (0.9, 0.999, 1e-8, 1e-2)
+    # separate: gradient, then the flat optimizer on W and bias
+    Wa, ba = W.clone(), torch.zeros(pad, device=DEV)
+    ba[:V] = b
+    ma = [m.clone() for m in mom]
+    dH, lv, dW, db = (torch.zeros(N, 16, device=DEV), torch.zeros(N, device=DEV),
+                      torch.zeros(V, 16, device=DEV), torch.zeros(pad, device=DEV))
+    ops.linear_xent(H, Wa, ba[:V], y, 0.1, 0, dH, lv, dW, db[:V])
+    ops.dense_optimizer(Wa.view(-1), dW.view(-1), ma[0], ma[1], None, opt, hyper, *prm)
+    ops.dense_optimizer(ba, db, ma[2], ma[3], None, opt, hyper, *prm)
+    # fused
+    Wb, bb = W.clone(), torch.zeros(pad, device=DEV)
+    bb[:V] = b
+    mb = [m.clone() for m in mom]
+    dH2, lv2 = torch.zeros(N, 16, device=DEV), torch.zeros(N, device=DEV)
+    ops.linear_xent(H, Wb, bb[:V], y, 0.1, 0, dH2, lv2, torch.zeros(V, 16, device=DEV),
+                    torch.zeros(V, device=DEV),
+                    step=(opt, [mb[0], mb[1], mb[2][:V], mb[3][:V]], hyper, *prm))
+    torch.cuda.synchronize()
+    assert torch.equal(dH, dH2) and torch.equal(lv, lv2)
+    assert torch.equal(Wa, Wb)
+    assert torch.equal(ba[:V], bb[:V])
+    for x, z in zip(ma, mb):
+        assert torch.equal(x[:V * 16 if x.numel() == V * 16 else V],
+                           z[:V * 16 if z.numel() == V * 16 else V])
+
+
 def test_linear_xent_all_ignored(xent_impl):
     N, V = 64, 100
     H = torch.randn(N, 16, device=DEV)

@@ -355,6 +355,24 @@ def test_fused_bottom_mlp_matches_per_layer_gemms(B):
     for a, b in zip(*outs):
         assert torch.equal(a, b)
     assert float(outs[0][2].float().abs().sum()) > 0
+    # and against an fp32 torch oracle of the same layers (bf16 operands,
+    # fp32 products, the activations rounded to bf16 between layers)
+    h = tr.bot_in[0].float()
+    for i, L in enumerate(tr.bottom_layers):
+        W = tr.fp.bf16(L.name + ".w")[:, :L.in_k].float()
+        y = (h[:, :L.in_k] @ W.t())[:, :L.out]
+        if not L.bias_in_k:
+            y = y + tr.fp.param(L.name + ".w")[:L.out, L.bcol].float()
+        y = torch.relu(y).to(torch.bfloat16).float()
+        if i + 1 < len(tr.bottom_layers):
+            # the next layer's augmented input (its ones column for an in-K bias)
+            h = tr.bot_in[i + 1].float().clone()
+            h[:, :L.out] = y
+        else:
+            h = y
+    got = outs[0][2].float()[:, : h.shape[1]]
+    rel = float((got - h).abs().max() / h.abs().max())
+    assert rel < 2e-2, rel
 
 
 def test_embedding_dense_grad_replicated_tables():
@@ -789,7 +807,9 @@ def test_dcn_step_matches_cpu():
         assert abs(a - b) < 0.02, (a, b)
 
 
-@pytest.mark.parametrize("n", [1, 1000, 4096, 4097, 213_000, 1_500_000])
+# 3 M keys: 2 tiles per thread in the tiled column scan; 16.8 M: past its
+# 4096-tile limit (the single-thread-per-column scan fallback)
+@pytest.mark.parametrize("n", [1, 1000, 4096, 4097, 213_000, 1_500_000, 3_000_000, 16_800_000])
 @pytest.mark.parametrize("dtype,bits", [(torch.int32, 28), (torch.int64, 40), (torch.int32, 5)])
 @pytest.mark.parametrize("tiled", [0, 2])
 def test_radix_sort_matches_stable_torch_sort(n, dtype, bits, tiled):
