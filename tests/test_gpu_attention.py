@@ -172,6 +172,38 @@ def _enc_params(E, FF, dev, g):
             1 + r(E, sc=0.1), r(E, sc=0.1), r(FF, E), r(FF, sc=0.1), r(E, FF), r(E, sc=0.1)]
 
 
+def test_fused_encoder_layer_separate_qkv_matches_concatenated():
+    """The block with Q / K / V weights and biases as 16 separate tensors
+    (what the Bert4Rec trainer passes: no per-step concatenation) equals the
+    12-tensor form with [W_qkv] / [b_qkv] concatenated, bit for bit."""
+    from tdfo_amd.models import bert4rec as m
+
+    B, T, E, H = 16, 20, 16, 2
+    g = torch.Generator().manual_seed(7)
+    params = _enc_params(E, 4 * E, DEV, g)
+    x = torch.randn(B, T, E, generator=g).to(DEV)
+    ids = torch.randint(1, 50, (B, T), generator=g).to(DEV)
+    step = torch.tensor([3], dtype=torch.int64, device=DEV)
+    dy = torch.randn(B, T, E, generator=g).to(DEV)
+    outs = []
+    for sep in (False, True):
+        xa = x.clone().requires_grad_(True)
+        if sep:
+            ps = (list(params[0].split(E, 0)) + list(params[1].split(E, 0)) + list(params[2:]))
+        else:
+            ps = list(params)
+        pa = [p.clone().contiguous().requires_grad_(True) for p in ps]
+        y = m._EncoderLayerFn.apply(xa, ids, step, H, 0.1, 0x5EED, 1e-5, None, *pa)
+        y.backward(dy)
+        grads = [p.grad for p in pa]
+        if sep:
+            grads = [torch.cat(grads[0:3], 0), torch.cat(grads[3:6], 0)] + grads[6:]
+        outs.append((y.detach(), xa.grad, grads))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    for a, b in zip(outs[0][2], outs[1][2]):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("B,T,E,H,rate", [(16, 20, 16, 2, 0.1), (16, 20, 16, 2, 0.0),
                                           (3, 24, 32, 4, 0.1), (5, 7, 16, 1, 0.2)])
 def test_fused_encoder_layer_matches_reference(B, T, E, H, rate):
@@ -190,7 +222,7 @@ def test_fused_encoder_layer_matches_reference(B, T, E, H, rate):
     seed = 0x5EED + 7919
     xa = x.clone().requires_grad_(True)
     pa = [p.clone().requires_grad_(True) for p in params]
-    y = m._EncoderLayerFn.apply(xa, ids, step, H, rate, seed, 1e-5, *pa)
+    y = m._EncoderLayerFn.apply(xa, ids, step, H, rate, seed, 1e-5, None, *pa)
     xr = x.clone().requires_grad_(True)
     pr = [p.clone().requires_grad_(True) for p in params]
     yr = ref.encoder_layer(xr, ids, pr, H, rate, seed, 5, 0, 1e-5)
