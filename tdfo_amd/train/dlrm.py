@@ -113,8 +113,9 @@ def run(cfg: Config, mode: str = "single", out_dir: str = ".",
                f"per-device batch {B}, num devices: {world} =====")
     _log(rank, f"===== sharding plan: {json.dumps(tr.plan.summary())} =====")
     if world > 1:
+        from ..parallel.comm import RcclComm
         _log(rank, f"===== attempt {os.environ.get('TDFO_ATTEMPT', '0')}, collectives: "
-                   f"{'c10d' if os.environ.get('TDFO_COMM') == 'torch' else 'native'}, "
+                   f"{'native' if isinstance(tr.comm, RcclComm) else 'c10d'}, "
                    f"stream graphs: {dcfg.stream_graphs}, preflight: "
                    f"{'ok' if pf is None or pf['ok'] else 'FAILED ' + str(pf['failed'])} =====")
     total_steps = cfg.max_steps or cfg.synthetic.num_batches * cfg.n_epochs

@@ -95,7 +95,7 @@ def rank_preflight(info) -> Optional[Dict]:
     pf = preflight(info.group, info.device, timeout_s=timeout)
     if not pf["ok"]:
         os.environ["TDFO_STREAM_GRAPHS"] = "0"
-    print(json.dumps({"preflight": pf, "rank": info.rank,
-                      "comm_path": "native" if pf["ok"] else "c10d-staged"}),
+    path = ("native" if pf.get("comm") == "RcclComm" else "c10d") if pf["ok"] else "c10d-staged"
+    print(json.dumps({"preflight": pf, "rank": info.rank, "comm_path": path}),
           file=sys.stderr, flush=True)
     return pf
