@@ -1,0 +1,10 @@
+set -u
+O=gpurun_out/r06/t; rm -rf $O; mkdir -p $O
+timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_kernels.py tests/test_gpu_two_tower.py tests/test_gpu_bert4rec.py -k "embedding or two_tower or bert4rec" > $O/tests.log 2>&1 || { echo "tests rc=$?"; tail -30 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+for k in 1 2; do
+for v in 1 0; do
+TDFO_EMB_SMALL_FUSED=$v timeout -k 10 300 python -u scripts/bench_two_tower.py > $O/tt_${v}_$k.log 2>&1 || { echo "tt rc=$?"; tail -5 $O/tt_${v}_$k.log; exit 1; }
+TDFO_EMB_SMALL_FUSED=$v timeout -k 10 300 python -u scripts/bench_bert4rec.py > $O/b4r_${v}_$k.log 2>&1 || { echo "b4r rc=$?"; tail -5 $O/b4r_${v}_$k.log; exit 1; }
+echo "small_fused=$v $k tt $(tail -n 1 $O/tt_${v}_$k.log | grep -o '"ms_per_step": [0-9.]*') b4r $(tail -n 1 $O/b4r_${v}_$k.log | grep -o '"ms_per_step": [0-9.]*')"
+done; done
