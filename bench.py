@@ -246,7 +246,14 @@ def measure(args, info, cfg, world: int, group, rank: int) -> dict:
         loop.run(post)
     torch.cuda.synchronize()
     tr.pop_loss()
-    if args.preheat_ms > 0:
+    if args.preheat_ms > 0 and os.environ.get("TDFO_PREHEAT_KIND") == "copy":
+        # diagnostics: an HBM-bound pre-heat (1 GiB copies, ~0.8 ms each)
+        a = torch.empty(1 << 28, dtype=torch.float32, device=info.device)
+        b = torch.empty_like(a)
+        for _ in range(max(1, int(args.preheat_ms / 0.8))):
+            b.copy_(a)
+        del a, b
+    elif args.preheat_ms > 0:
         from tdfo_amd import ops
         ops.burn_us(args.preheat_ms * 1e3)
     if info.world_size > 1:

@@ -334,14 +334,24 @@ void encoder_layer_fwd(const Tensor& x, const Tensor& ids, const c10::optional<T
 void encoder_layer_bwd(const Tensor& x, const Tensor& ids, const c10::optional<Tensor>& step,
                        at::TensorList params, int64_t H, double rate, int64_t seed,
                        int64_t pad_id, double eps, at::TensorList saved, const Tensor& dy,
-                       const Tensor& dx, const Tensor& part, const Tensor& grad) {
+                       const Tensor& dx, const Tensor& part, const Tensor& grad,
+                       const c10::optional<Tensor>& gidx) {
   auto a = enc_args(x, ids, step, params, H, rate, seed, pad_id, eps, saved);
   check_f32c(dy, "dy"); check_f32c(dx, "dx"); check_f32c(part, "part"); check_f32c(grad, "grad");
   const int64_t P = tdfo::encoder_param_count(a.E, a.FF);
   TORCH_CHECK(dy.numel() == x.numel() && dx.numel() == x.numel(), "encoder_layer: dy/dx");
   TORCH_CHECK(part.numel() >= (int64_t)a.B * P && grad.numel() >= P, "encoder_layer: part/grad");
   a.dy = dy.data_ptr<float>(); a.dx = dx.data_ptr<float>(); a.part = part.data_ptr<float>();
-  tdfo::encoder_layer_bwd(a, grad.data_ptr<float>(), cur_stream());
+  // gidx: flat-buffer positions of the P gradients, bounds-checked against
+  // grad by the caller when it was built (ops.flat_scatter_index)
+  const int64_t* gi = nullptr;
+  if (gidx) {
+    check_dev(*gidx, "gidx");
+    TORCH_CHECK(gidx->scalar_type() == at::kLong && gidx->is_contiguous() && gidx->numel() == P,
+                "encoder_layer: gidx int64 [P]");
+    gi = gidx->data_ptr<int64_t>();
+  }
+  tdfo::encoder_layer_bwd(a, grad.data_ptr<float>(), cur_stream(), gi);
 }
 
 // ------------------------------------------------------------ layernorm
@@ -404,7 +414,7 @@ void seq_prologue_fwd(const Tensor& x, const Tensor& pos, int64_t n, double eps,
 void seq_prologue_bwd(const Tensor& x, const Tensor& pos, const Tensor& g, int64_t n,
                       const Tensor& gamma, const Tensor& mean, const Tensor& rstd, double rate,
                       int64_t seed, const c10::optional<Tensor>& step, const Tensor& dx,
-                      const Tensor& part, const Tensor& out3) {
+                      const Tensor& part, const Tensor& out3, const c10::optional<Tensor>& gidx) {
   check_f32c(x, "x"); check_f32c(pos, "pos"); check_f32c(g, "g"); check_f32c(gamma, "gamma");
   check_f32c(mean, "mean"); check_f32c(rstd, "rstd"); check_f32c(dx, "dx");
   check_f32c(part, "part"); check_f32c(out3, "out3");
@@ -412,7 +422,7 @@ void seq_prologue_bwd(const Tensor& x, const Tensor& pos, const Tensor& g, int64
   const int64_t M = x.numel() / n;
   TORCH_CHECK(pos.numel() == n && g.numel() == x.numel() && dx.numel() == x.numel() &&
               gamma.numel() == n && mean.numel() >= M && rstd.numel() >= M &&
-              out3.numel() == 3 * n &&
+              (gidx ? out3.numel() >= 3 * n : out3.numel() == 3 * n) &&
               part.numel() >= (int64_t)tdfo::layernorm_parts(M) * 3 * n, "seq_prologue_bwd: shapes");
   const int64_t* sp = nullptr;
   if (step) {
@@ -420,11 +430,18 @@ void seq_prologue_bwd(const Tensor& x, const Tensor& pos, const Tensor& g, int64
     TORCH_CHECK(step->scalar_type() == at::kLong && step->numel() >= 1, "step: int64 device scalar");
     sp = step->data_ptr<int64_t>();
   }
+  const int64_t* gi = nullptr;
+  if (gidx) {        // out3 is then a flat gradient buffer: [dgamma|dbeta|dpos][j] -> out3[gidx[j]]
+    check_dev(*gidx, "gidx");
+    TORCH_CHECK(gidx->scalar_type() == at::kLong && gidx->is_contiguous() &&
+                gidx->numel() == 3 * n, "seq_prologue_bwd: gidx int64 [3n]");
+    gi = gidx->data_ptr<int64_t>();
+  }
   tdfo::seq_prologue_bwd(x.data_ptr<float>(), pos.data_ptr<float>(), g.data_ptr<float>(), M,
                          (int)n, gamma.data_ptr<float>(), mean.data_ptr<float>(),
                          rstd.data_ptr<float>(), (float)rate, (uint32_t)seed, sp,
                          dx.data_ptr<float>(), part.data_ptr<float>(), out3.data_ptr<float>(),
-                         cur_stream());
+                         cur_stream(), gi);
 }
 
 void rank_metrics(const Tensor& h, const Tensor& W, const Tensor& bias, const Tensor& cand,
@@ -1340,7 +1357,7 @@ void auc_hist(const Tensor& logits, const Tensor& labels, int64_t nb, const Tens
 void two_tower(const Tensor& X, const Tensor& P, const Tensor& labels, double inv_n,
                const Tensor& logits, const c10::optional<Tensor>& dX,
                const c10::optional<Tensor>& part, const c10::optional<Tensor>& loss_scale,
-               bool half) {
+               bool half, at::TensorList bumps) {
   check_dev(X, "X"); check_2d_rowmajor(X, "X");
   const int64_t B = X.size(0);
   TORCH_CHECK(X.scalar_type() == at::kFloat && X.size(1) >= 114 && X.stride(0) % 4 == 0 &&
@@ -1372,8 +1389,51 @@ void two_tower(const Tensor& X, const Tensor& P, const Tensor& labels, double in
     a.labels = labels.data_ptr<float>();
     a.dX = d.data_ptr<float>(); a.lddx = d.stride(0);
     a.part = part->data_ptr<float>();
+    TORCH_CHECK(bumps.size() <= 4, "two_tower: at most 4 step counters");
+    a.bumps.n = (int)bumps.size();
+    for (size_t i = 0; i < bumps.size(); ++i) {
+      check_f32c(bumps[i], "bump");
+      TORCH_CHECK(bumps[i].numel() >= 2, "two_tower: counters are [lr, step, ...]");
+      a.bumps.p[i] = bumps[i].data_ptr<float>();
+    }
+  } else {
+    TORCH_CHECK(bumps.size() == 0, "two_tower: bumps are a train-step option");
   }
   tdfo::two_tower(a, train ? 1 : 0, cur_stream());
+}
+
+void reduce_adam(const Tensor& part, int64_t nparts, int64_t n, int64_t ld, const Tensor& grad,
+                 const Tensor& p, const Tensor& m, const Tensor& v, const Tensor& hyper,
+                 double beta1, double beta2, double eps, double wd, bool adamw,
+                 const Tensor& loss_acc, const c10::optional<Tensor>& logits,
+                 const c10::optional<Tensor>& labels, int64_t nb,
+                 const c10::optional<Tensor>& hist) {
+  check_f32c(part, "part"); check_f32c(grad, "grad"); check_f32c(p, "p"); check_f32c(m, "m");
+  check_f32c(v, "v"); check_f32c(hyper, "hyper");
+  check_dev(loss_acc, "loss_acc");
+  TORCH_CHECK(loss_acc.scalar_type() == at::kDouble && loss_acc.numel() >= 1,
+              "reduce_adam: loss_acc fp64");
+  TORCH_CHECK(nparts >= 1 && n >= 1 && ld >= n + 1 && part.numel() >= (nparts - 1) * ld + n + 1 &&
+              grad.numel() >= n + 1 && p.numel() >= n && m.numel() >= n && v.numel() >= n &&
+              hyper.numel() >= 3, "reduce_adam: shapes");
+  tdfo::ReduceAdamArgs a{};
+  a.part = part.data_ptr<float>(); a.nparts = (int)nparts; a.n = (int)n; a.ld = (int)ld;
+  a.grad = grad.data_ptr<float>(); a.p = p.data_ptr<float>(); a.m = m.data_ptr<float>();
+  a.v = v.data_ptr<float>(); a.hyper = hyper.data_ptr<float>();
+  a.beta1 = (float)beta1; a.beta2 = (float)beta2; a.eps = (float)eps; a.wd = (float)wd;
+  a.adamw = adamw ? 1 : 0;
+  a.loss_acc = loss_acc.data_ptr<double>();
+  if (hist) {
+    TORCH_CHECK(logits && labels, "reduce_adam: hist needs logits and labels");
+    check_f32c(*logits, "logits"); check_f32c(*labels, "labels"); check_dev(*hist, "hist");
+    TORCH_CHECK(hist->scalar_type() == at::kLong && hist->is_contiguous() && nb > 0 &&
+                nb <= tdfo::REDUCE_ADAM_MAX_NB && hist->numel() == 2 * nb &&
+                labels->numel() == logits->numel(), "reduce_adam: hist int64 [2 * nb], nb <= 512");
+    a.logits = logits->data_ptr<float>(); a.labels = labels->data_ptr<float>();
+    a.nlog = (int)logits->numel(); a.nb = (int)nb;
+    a.hist = reinterpret_cast<unsigned long long*>(hist->data_ptr<int64_t>());
+  }
+  tdfo::reduce_adam(a, cur_stream());
 }
 
 void linear_xent(const Tensor& H, const Tensor& W, const Tensor& bias, const Tensor& labels,
@@ -1578,7 +1638,7 @@ TORCH_LIBRARY(tdfo, m) {
         "int seed, int pad_id, float eps, Tensor(a!)[] saved, Tensor(b!) y) -> ()");
   m.def("encoder_layer_bwd(Tensor x, Tensor ids, Tensor? step, Tensor[] params, int H, float rate, "
         "int seed, int pad_id, float eps, Tensor[] saved, Tensor dy, Tensor(a!) dx, "
-        "Tensor(b!) part, Tensor(c!) grad) -> ()");
+        "Tensor(b!) part, Tensor(c!) grad, Tensor? gidx) -> ()");
   m.def("attention_fwd(Tensor qkv, Tensor ids, int H, float rate, int seed, Tensor? step, int pad_id, "
         "Tensor(a!) out) -> ()");
   m.def("attention_bwd(Tensor qkv, Tensor ids, Tensor dout, int H, float rate, int seed, Tensor? step, "
@@ -1591,7 +1651,7 @@ TORCH_LIBRARY(tdfo, m) {
         "float rate, int seed, Tensor? step, Tensor(a!) y, Tensor(b!) mean, Tensor(c!) rstd) -> ()");
   m.def("seq_prologue_bwd(Tensor x, Tensor pos, Tensor g, int n, Tensor gamma, Tensor mean, "
         "Tensor rstd, float rate, int seed, Tensor? step, Tensor(a!) dx, Tensor(b!) part, "
-        "Tensor(c!) out3) -> ()");
+        "Tensor(c!) out3, Tensor? gidx) -> ()");
   m.def("rank_metrics(Tensor h, Tensor W, Tensor bias, Tensor cand, int[] ks, Tensor(a!) out) -> ()");
   m.def("layernorm_parts(int M) -> int", [](int64_t M) { return (int64_t)tdfo::layernorm_parts(M); });
   m.def("gather_columns(Tensor[] src, Tensor? idx, int row0, int n, Tensor(a!)[] dst, int[] dst_stride) -> ()");
@@ -1677,7 +1737,12 @@ TORCH_LIBRARY(tdfo, m) {
   m.def("dense_to_jagged(Tensor dense, Tensor offsets, Tensor(a!) vgrad) -> ()");
   m.def("jagged_ids_to_dense(Tensor values, Tensor offsets, int pad, Tensor(a!) out) -> ()");
   m.def("two_tower(Tensor X, Tensor P, Tensor labels, float inv_n, Tensor(a!) logits, "
-        "Tensor(b!)? dX, Tensor(c!)? part, Tensor? loss_scale, bool half) -> ()");
+        "Tensor(b!)? dX, Tensor(c!)? part, Tensor? loss_scale, bool half, "
+        "Tensor(d!)[] bumps) -> ()");
+  m.def("reduce_adam(Tensor part, int nparts, int n, int ld, Tensor(a!) grad, Tensor(b!) p, "
+        "Tensor(c!) m, Tensor(d!) v, Tensor hyper, float beta1, float beta2, float eps, "
+        "float wd, bool adamw, Tensor(e!) loss_acc, Tensor? logits, Tensor? labels, int nb, "
+        "Tensor(f!)? hist) -> ()");
 }
 
 TORCH_LIBRARY_IMPL(tdfo, CUDA, m) {
@@ -1727,6 +1792,7 @@ TORCH_LIBRARY_IMPL(tdfo, CUDA, m) {
   m.impl("colsum", colsum);
   m.impl("auc_hist", auc_hist);
   m.impl("two_tower", two_tower);
+  m.impl("reduce_adam", reduce_adam);
   m.impl("linear_xent", linear_xent);
   m.impl("jagged_to_dense", jagged_to_dense);
   m.impl("dense_to_jagged", dense_to_jagged);

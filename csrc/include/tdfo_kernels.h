@@ -327,9 +327,28 @@ int head_bce_parts(int B);
 struct HeadBumps { float* p[4]; int n; };
 void head_reduce(const float* part, int nparts, int K, float* grad, float* loss_acc,
                  const HeadBumps& bumps, hipStream_t s);
+// grad[j] = sum_r part[r * ld + j] for j < n (head_reduce's / reduce_rows'
+// fixed order) followed by one Adam / AdamW step of p[j] from it (hyper =
+// [lr, step, grad_scale], adam_elem: the flat optimizer's bits); column n is
+// the loss partial: loss_acc[0] += (double)sum. Optionally one more block
+// bins logits[0..nlog) into hist ([2 * nb] int64, auc_hist's buckets).
+// Replaces reduce_rows + the flat optimizer + the loss add + auc_hist of a
+// small model's step (TwoTower).
+constexpr int REDUCE_ADAM_MAX_NB = 512;
+struct ReduceAdamArgs {
+  const float* part; int nparts; int n; int ld;
+  float* grad; float* p; float* m; float* v;
+  const float* hyper; float beta1, beta2, eps, wd; int adamw;
+  double* loss_acc;
+  const float* logits = nullptr; const float* labels = nullptr; int nlog = 0; int nb = 0;
+  unsigned long long* hist = nullptr;
+};
+void reduce_adam(const ReduceAdamArgs& a, hipStream_t s);
 // out[j] (=|+=) sum_r in[r*ld + j], j < n, fixed order (deterministic).
+// idx (optional): out[idx[j]] instead of out[j] (a gather-free scatter into
+// a flat gradient buffer whose layout differs from the packed order)
 void reduce_rows(const float* in, int rows, int64_t n, int64_t ld, float* out,
-                 int accumulate, float scale, hipStream_t s);
+                 int accumulate, float scale, hipStream_t s, const int64_t* idx = nullptr);
 // several fp32 split-K slab sets reduced in one launch: seg k sums S slabs of
 // n floats (n % 4 == 0, 16-B aligned) into out; start[] = prefix of n / 4
 struct SlabSeg { const float* in; float* out; int64_t n; int S; };
@@ -363,6 +382,8 @@ struct TwoTowerArgs {
   float* logits;
   float* dX; int64_t lddx;
   float* part;
+  // optional (train): step counters bumped by block 0 (no bump launch)
+  HeadBumps bumps{};
 };
 int two_tower_parts(int B);
 void two_tower(const TwoTowerArgs& a, int train, hipStream_t s);
@@ -428,7 +449,10 @@ bool encoder_layer_supported(int T, int E, int H, int FF);
 void encoder_layer_fwd(const EncArgs& a, hipStream_t s);
 // grad: [encoder_param_count] = [dWqkv | dbqkv | dWo | dbo | dg1 | dbe1 | dg2 |
 // dbe2 | dW1 | db1 | dW2 | db2]
-void encoder_layer_bwd(const EncArgs& a, float* grad, hipStream_t s);
+// gidx (optional): parameter gradient c goes to grad[gidx[c]] (the trainer's
+// flat gradient buffer) instead of grad[c]
+void encoder_layer_bwd(const EncArgs& a, float* grad, hipStream_t s,
+                       const int64_t* gidx = nullptr);
 
 // ------------------------------------------------------ ranking (eval) ----
 // Bert4Rec-style candidate ranking: per sample b, scores of candidates
@@ -460,7 +484,8 @@ void seq_prologue_fwd(const float* x, const float* pos, int64_t M, int n, float 
 void seq_prologue_bwd(const float* x, const float* pos, const float* g, int64_t M, int n,
                       const float* gamma, const float* mean, const float* rstd, float rate,
                       uint32_t seed, const int64_t* step, float* dx, float* part,
-                      float* dgamma_dbeta_dpos, hipStream_t s);
+                      float* dgamma_dbeta_dpos, hipStream_t s,
+                      const int64_t* idx = nullptr);
 
 // ------------------------------------------------------ batch gather ----
 // out_c[i * dst_stride_c] = convert(src_c[idx ? idx[i] : row0 + i]) for every

@@ -1365,13 +1365,22 @@ bool onehot_path(const EmbBwdArgs& a) {
 // (same box, 300 steps; profiles/r06/notes.md): the last-arriving chunk's
 // walk over a tiny table's ~85 partials becomes the update kernel's tail,
 // which the next lookup waits behind.
+// TDFO_EMB_INKERNEL_COMBINE: 1 always, 0 never, unset: batches of at most
+// IKC_AUTO_MAX ids. Small batches (TwoTower 7 x 2048, Bert4Rec 320 ids) gain
+// from dropping the combine launch (TwoTower 0.0762 -> 0.0735 ms/step,
+// Bert4Rec B=16 0.436 -> 0.433); on DLRM-1TB (213 K ids) the last arrival's
+// walk over a short table's ~85 partials became the update's tail: 0.430 vs
+// 0.413 (profiles/r06/notes.md).
+constexpr int64_t IKC_AUTO_MAX = 65536;
 const int g_emb_inkernel_combine = [] {
   const char* e = getenv("TDFO_EMB_INKERNEL_COMBINE");
-  return e ? atoi(e) : 0;
+  return e ? atoi(e) : -1;
 }();
 
 bool meta_path(const EmbBwdArgs& a) {
-  return g_emb_inkernel_combine && onehot_path(a) && a.segsort == 1 &&
+  const bool on = g_emb_inkernel_combine > 0 ||
+                  (g_emb_inkernel_combine < 0 && (int64_t)a.T * a.B <= IKC_AUTO_MAX);
+  return on && onehot_path(a) && a.segsort == 1 &&
          a.B % ch_for(a.D) == 0 && !(g_emb_seg_split && a.B > 2 * SEG_THREADS);
 }
 

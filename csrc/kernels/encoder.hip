@@ -484,12 +484,13 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_bwd_kernel(EncArgs a) {
 
 // grad[c] = sum_b part[b][c], fixed order
 __global__ __launch_bounds__(256) void enc_reduce_kernel(const float* __restrict__ part, int B,
-                                                         int P, float* __restrict__ grad) {
+                                                         int P, float* __restrict__ grad,
+                                                         const int64_t* __restrict__ gidx) {
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= P) return;
   float s = 0.f;
   for (int b = 0; b < B; ++b) s += part[(int64_t)b * P + c];
-  grad[c] = s;
+  grad[gidx ? gidx[c] : c] = s;
 }
 
 size_t fwd_smem(const EncArgs& a) {
@@ -561,13 +562,13 @@ void encoder_layer_fwd(const EncArgs& a, hipStream_t s) {
   TDFO_CHECK_HIP(hipGetLastError());
 }
 
-void encoder_layer_bwd(const EncArgs& a, float* grad, hipStream_t s) {
+void encoder_layer_bwd(const EncArgs& a, float* grad, hipStream_t s, const int64_t* gidx) {
   check(a);
   if (a.B <= 0) return;
   launch<true>(a, bwd_smem(a), s);
   const int P = poff(a.E, a.FF).P;
   hipLaunchKernelGGL(enc_reduce_kernel, dim3((P + 255) / 256), dim3(256), 0, s, a.part, a.B, P,
-                     grad);
+                     grad, gidx);
   TDFO_CHECK_HIP(hipGetLastError());
 }
 

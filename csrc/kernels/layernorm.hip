@@ -209,7 +209,7 @@ void seq_prologue_fwd(const float* x, const float* pos, int64_t M, int n, float 
 void seq_prologue_bwd(const float* x, const float* pos, const float* g, int64_t M, int n,
                       const float* gamma, const float* mean, const float* rstd, float rate,
                       uint32_t seed, const int64_t* step, float* dx, float* part,
-                      float* dgamma_dbeta_dpos, hipStream_t s) {
+                      float* dgamma_dbeta_dpos, hipStream_t s, const int64_t* idx) {
   if (M <= 0) return;
   const int nb = layernorm_parts(M);
   const dim3 grid(nb), block(64 * LN_WAVES);
@@ -217,7 +217,7 @@ void seq_prologue_bwd(const float* x, const float* pos, const float* g, int64_t 
   TDFO_LN_DISPATCH(ln_bwd_kernel, true, grid, block, 0, s, x, g, M, n, gamma, mean, rstd, dx,
                    part, pa);
   TDFO_CHECK_HIP(hipGetLastError());
-  reduce_rows(part, nb, 3 * n, 3 * n, dgamma_dbeta_dpos, 0, 1.f, s);
+  reduce_rows(part, nb, 3 * n, 3 * n, dgamma_dbeta_dpos, 0, 1.f, s, idx);
 }
 #undef TDFO_LN_DISPATCH
 

@@ -92,7 +92,7 @@ __global__ __launch_bounds__(256) void head_bce_kernel(
 template <int COLS>
 __global__ __launch_bounds__(256) void reduce_rows_kernel(
     const float* __restrict__ in, int rows, int64_t n, int64_t ld,
-    float* __restrict__ out, int accumulate, float scale) {
+    float* __restrict__ out, int accumulate, float scale, const int64_t* __restrict__ idx) {
   constexpr int PH = 256 / COLS;
   __shared__ float red[PH][COLS];
   const int c = threadIdx.x % COLS, ph = threadIdx.x / COLS;
@@ -116,10 +116,53 @@ __global__ __launch_bounds__(256) void reduce_rows_kernel(
 #pragma unroll
       for (int q = 0; q < PH; ++q) t += red[q][c];
       t *= scale;
-      out[j] = accumulate ? out[j] + t : t;
+      const int64_t o = idx ? idx[j] : j;
+      out[o] = accumulate ? out[o] + t : t;
     }
     __syncthreads();
   }
+}
+
+// One thread's share of a fixed-order column sum over nparts partial rows:
+// rows ph, ph + PH, ... in groups of four into s0..s3 (a partial last group
+// into s0), returned as (s0 + s1) + (s2 + s3) -- reduce_rows_kernel's loop,
+// with the first PRE rows loaded up front at clamped addresses and then added
+// in that order, so the sums are the plain loop's with one round trip for up
+// to PRE * PH = 512 partial rows (B = 8192) instead of one per group.
+template <int PH>
+__device__ __forceinline__ float col_phase_sum(const float* __restrict__ part, int nparts,
+                                               int ld, int j, int ph) {
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  constexpr int PRE = 32;
+  float v[PRE];
+#pragma unroll
+  for (int q = 0; q < PRE; ++q) {
+    const int r = min(ph + q * PH, nparts - 1);
+    v[q] = part[(int64_t)r * ld + j];
+  }
+#pragma unroll
+  for (int g = 0; g < PRE / 4; ++g) {
+    const int r = ph + 4 * g * PH;
+    if (r + 3 * PH < nparts) {
+      s0 += v[4 * g]; s1 += v[4 * g + 1]; s2 += v[4 * g + 2]; s3 += v[4 * g + 3];
+    } else {
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        if (r + q * PH < nparts) s0 += v[4 * g + q];
+    }
+  }
+  int r = ph + PRE * PH;
+  if (r < nparts) {
+    // (more than PRE * PH rows: every group above was full)
+    for (; r + 3 * PH < nparts; r += 4 * PH) {
+      s0 += part[(int64_t)r * ld + j];
+      s1 += part[(int64_t)(r + PH) * ld + j];
+      s2 += part[(int64_t)(r + 2 * PH) * ld + j];
+      s3 += part[(int64_t)(r + 3 * PH) * ld + j];
+    }
+    for (; r < nparts; r += PH) s0 += part[(int64_t)r * ld + j];
+  }
+  return (s0 + s1) + (s2 + s3);
 }
 
 // Head epilogue in one launch: grad[j] = sum_r part[r][j] (j <= K) and
@@ -137,44 +180,7 @@ __global__ __launch_bounds__(256) void head_reduce_kernel(const float* __restric
   const int ld = K + 2;
   const int c = threadIdx.x % COLS, ph = threadIdx.x / COLS;
   const int j = blockIdx.x * COLS + c;
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  if (j < ld && nparts > 0) {
-    // The first PRE rows of this thread (r = ph, ph + PH, ...) are loaded
-    // up front at clamped addresses and then added in the loop's order
-    // (groups of four into s0..s3, a partial last group into s0), so the
-    // sums are those of the plain loop below with one round trip for up to
-    // PRE * PH = 512 partial rows (B = 8192) instead of one per group.
-    constexpr int PRE = 32;
-    float v[PRE];
-#pragma unroll
-    for (int q = 0; q < PRE; ++q) {
-      const int r = min(ph + q * PH, nparts - 1);
-      v[q] = part[(int64_t)r * ld + j];
-    }
-#pragma unroll
-    for (int g = 0; g < PRE / 4; ++g) {
-      const int r = ph + 4 * g * PH;
-      if (r + 3 * PH < nparts) {
-        s0 += v[4 * g]; s1 += v[4 * g + 1]; s2 += v[4 * g + 2]; s3 += v[4 * g + 3];
-      } else {
-#pragma unroll
-        for (int q = 0; q < 3; ++q)
-          if (r + q * PH < nparts) s0 += v[4 * g + q];
-      }
-    }
-    int r = ph + PRE * PH;
-    if (r < nparts) {
-      // (more than PRE * PH rows: every group above was full)
-      for (; r + 3 * PH < nparts; r += 4 * PH) {
-        s0 += part[(int64_t)r * ld + j];
-        s1 += part[(int64_t)(r + PH) * ld + j];
-        s2 += part[(int64_t)(r + 2 * PH) * ld + j];
-        s3 += part[(int64_t)(r + 3 * PH) * ld + j];
-      }
-      for (; r < nparts; r += PH) s0 += part[(int64_t)r * ld + j];
-    }
-  }
-  red[ph][c] = (s0 + s1) + (s2 + s3);
+  red[ph][c] = (j < ld && nparts > 0) ? col_phase_sum<PH>(part, nparts, ld, j, ph) : 0.f;
   __syncthreads();
   if (ph == 0 && j < ld) {
     float t = 0.f;
@@ -184,6 +190,55 @@ __global__ __launch_bounds__(256) void head_reduce_kernel(const float* __restric
     else loss_acc[0] += t;
   }
   if (blockIdx.x == 0 && threadIdx.x < bumps.n) bumps.p[threadIdx.x][1] += 1.f;
+}
+
+// reduce_rows + the flat Adam / AdamW + the loss accumulation of a small
+// model's step in one launch (TwoTower: 2,400 parameters from 128 block
+// partials; three dependent ~4.5-us launches before, profiles/r05/two_tower).
+// Same column sums as reduce_rows_kernel<16>, same adam_elem as
+// dense_opt_kernel: bit-identical to the three-launch sequence.
+__global__ __launch_bounds__(256) void reduce_adam_kernel(ReduceAdamArgs a) {
+  constexpr int COLS = 16, PH = 256 / COLS;
+  __shared__ float red[PH][COLS];
+  __shared__ unsigned int lh[2 * REDUCE_ADAM_MAX_NB];
+  if (a.hist != nullptr && blockIdx.x == gridDim.x - 1) {
+    // the AUC block: auc_hist_kernel's binning (LDS counts, then one integer
+    // atomic per non-empty bucket)
+    for (int i = threadIdx.x; i < 2 * a.nb; i += 256) lh[i] = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < a.nlog; i += 256) {
+      const float pr = 1.f / (1.f + __expf(-a.logits[i]));
+      int bkt = (int)(pr * a.nb);
+      bkt = bkt < 0 ? 0 : (bkt >= a.nb ? a.nb - 1 : bkt);
+      atomicAdd(&lh[(a.labels[i] > 0.5f ? a.nb : 0) + bkt], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 2 * a.nb; i += 256)
+      if (lh[i]) atomicAdd(&a.hist[i], (unsigned long long)lh[i]);
+    return;
+  }
+  const int c = threadIdx.x % COLS, ph = threadIdx.x / COLS;
+  const int j = blockIdx.x * COLS + c;
+  red[ph][c] = (j <= a.n && a.nparts > 0) ? col_phase_sum<PH>(a.part, a.nparts, a.ld, j, ph)
+                                          : 0.f;
+  __syncthreads();
+  if (ph == 0 && j <= a.n) {
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < PH; ++q) t += red[q][c];
+    a.grad[j] = t;
+    if (j == a.n) {
+      a.loss_acc[0] += (double)t;
+    } else {
+      const float lr = a.hyper[0], step = a.hyper[1], gs = a.hyper[2];
+      const float bc1 = 1.f - powf(a.beta1, step), bc2 = 1.f - powf(a.beta2, step);
+      float p = a.p[j], m = a.m[j], v = a.v[j];
+      adam_elem(p, t * gs, m, v, lr, bc1, bc2, a.beta1, a.beta2, a.eps, a.wd, a.adamw != 0);
+      a.p[j] = p;
+      a.m[j] = m;
+      a.v[j] = v;
+    }
+  }
 }
 
 constexpr int COLSUM_CHUNKS = 16;
@@ -265,17 +320,17 @@ void head_bce(const uint16_t* H, int64_t ldh, int B, int K, const float* w,
 }
 
 void reduce_rows(const float* in, int rows, int64_t n, int64_t ld, float* out,
-                 int accumulate, float scale, hipStream_t s) {
+                 int accumulate, float scale, hipStream_t s, const int64_t* idx) {
   if (n <= 0) return;
   if (n >= 16384) {
     int64_t blocks = (n + 63) / 64;
     if (blocks > 8192) blocks = 8192;
     hipLaunchKernelGGL(reduce_rows_kernel<64>, dim3(blocks), dim3(256), 0, s, in,
-                       rows, n, ld, out, accumulate, scale);
+                       rows, n, ld, out, accumulate, scale, idx);
   } else {
     int64_t blocks = (n + 15) / 16;
     hipLaunchKernelGGL(reduce_rows_kernel<16>, dim3(blocks), dim3(256), 0, s, in,
-                       rows, n, ld, out, accumulate, scale);
+                       rows, n, ld, out, accumulate, scale, idx);
   }
 }
 
@@ -329,6 +384,13 @@ void slab_reduce(const SlabReduceArgs& a, hipStream_t s) {
 }
 
 int colsum_parts(int M) { return COLSUM_CHUNKS; }
+
+void reduce_adam(const ReduceAdamArgs& a, hipStream_t s) {
+  if (a.n <= 0) return;
+  const int blocks = (a.n + 1 + 15) / 16 + (a.hist != nullptr ? 1 : 0);
+  hipLaunchKernelGGL(reduce_adam_kernel, dim3(blocks), dim3(256), 0, s, a);
+  TDFO_CHECK_HIP(hipGetLastError());
+}
 
 void head_reduce(const float* part, int nparts, int K, float* grad, float* loss_acc,
                  const HeadBumps& bumps, hipStream_t s) {

@@ -21,7 +21,11 @@
 // (64-sample blocks of 4 waves: 19.7 us, 32 blocks). Embedding gradients are
 // written per sample (dX) for the sort-based fused sparse optimizer
 // (embedding.hip). (The one-thread-per-sample VALU kernel this replaces
-// took 38.8 us at B = 2048, 16 blocks: profiles/r05/two_tower/.)
+// took 38.8 us at B = 2048, 16 blocks: profiles/r05/two_tower/.) Optionally
+// the optimizers' step counters are bumped here too (no bump launch), and
+// tdfo::reduce_adam sums the partial rows straight into the AdamW step (and
+// bins the logits for the AUC in a block of its own). Binning the logits here
+// with global atomics cost 7 us: at init every logit lands in one bucket.
 //
 // Parameter layout (flat fp32, Flax kernel convention W[in][out]):
 //   [uW1 16x16 | ub1 16 | uW2 16x16 | ub2 16 | iW1 98x16 | ib1 16 | iW2 16x16 | ib2 16]
@@ -137,6 +141,7 @@ __global__ __launch_bounds__(64 * NWV) void two_tower_kernel(TwoTowerArgs a) {
   if constexpr (TRAIN) {
     // ---- loss + backward
     const float y = valid ? a.labels[s] : 0.f;
+    if (blockIdx.x == 0 && t < a.bumps.n) a.bumps.p[t][1] += 1.f;
     float loss = (valid && g == 0) ? fmaxf(logit, 0.f) - logit * y + log1pf(__expf(-fabsf(logit)))
                                    : 0.f;
     const float ls = a.loss_scale ? a.loss_scale[0] : 1.f;

@@ -132,16 +132,18 @@ class _EncoderLayerFn(torch.autograd.Function):
         FF = params[-4].shape[0]
         P = ops.encoder_param_count(E, FF)
         part = torch.empty(B * P, device=x.device)
-        grad = torch.empty(P, device=x.device)
         dx = torch.empty_like(x)
+        if ctx.gdst is not None:
+            # every parameter gradient straight into the flat gradient buffer
+            # by the kernel's reduction (gidx: flat positions in packed order):
+            # no cat-backward, no AccumulateGrad adds, no scatter launch
+            flat, idx = ctx.gdst
+            ops.encoder_layer_bwd(x, ids, step, params, H, rate, seed, PAD_ID, eps, saved,
+                                  dy.contiguous(), dx, part, flat, gidx=idx)
+            return (dx, None, None, None, None, None, None, None) + (None,) * len(params)
+        grad = torch.empty(P, device=x.device)
         ops.encoder_layer_bwd(x, ids, step, params, H, rate, seed, PAD_ID, eps, saved,
                               dy.contiguous(), dx, part, grad)
-        if ctx.gdst is not None:
-            # every parameter gradient straight into the flat gradient buffer:
-            # one scatter instead of autograd's cat-backward + 16 adds
-            flat, idx = ctx.gdst
-            flat.index_copy_(0, idx, grad)
-            return (dx, None, None, None, None, None, None, None) + (None,) * len(params)
         grads, o = [], 0
         for p in params:
             grads.append(grad[o:o + p.numel()].view_as(p))
@@ -176,13 +178,14 @@ class _SeqPrologueFn(torch.autograd.Function):
         M = x.numel() // n
         dx = torch.empty_like(x)
         part = torch.empty(ops.layernorm_parts(M) * 3 * n, dtype=torch.float32, device=x.device)
+        if ctx.gdst is not None:            # [gamma | beta | pos] -> the flat gradients
+            flat, idx = ctx.gdst
+            ops.seq_prologue_bwd(x, pos.contiguous(), g.contiguous(), n, gamma.contiguous(),
+                                 mean, rstd, rate, seed, step, dx, part, flat, gidx=idx)
+            return (dx, None, None, None, None, None, None, None, None)
         out3 = torch.empty(3 * n, dtype=torch.float32, device=x.device)
         ops.seq_prologue_bwd(x, pos.contiguous(), g.contiguous(), n, gamma.contiguous(), mean,
                              rstd, rate, seed, step, dx, part, out3)
-        if ctx.gdst is not None:            # [gamma | beta | pos] -> the flat gradients
-            flat, idx = ctx.gdst
-            flat.index_copy_(0, idx, out3)
-            return (dx, None, None, None, None, None, None, None, None)
         return (dx, out3[2 * n:].view_as(pos), out3[:n].view_as(gamma),
                 out3[n:2 * n].view_as(gamma), None, None, None, None, None)
 
@@ -325,7 +328,6 @@ class ItemEmbedding(nn.Module):
         self.step_bumped_by_caller = False
         self.offsets = torch.arange(n_tokens * world + 1, dtype=torch.int64, device=device)
         self.zero = torch.zeros(1, dtype=torch.int64, device=device)
-        self.out = torch.zeros(n_tokens, dim, dtype=torch.float32, device=device)
         if world > 1:
             self.g_ids = torch.zeros(world * n_tokens, dtype=torch.int64, device=device)
             self.g_grad = torch.zeros(world * n_tokens, dim, dtype=torch.float32, device=device)
@@ -338,11 +340,13 @@ class ItemEmbedding(nn.Module):
 
     def _lookup(self, ids):
         n = ids.numel()
-        out = self.out[:n]
+        # a fresh output (the caller's autograd saves it): the lookup writes it
+        # directly, no copy of a static buffer
+        out = torch.empty(n, self.D, dtype=torch.float32, device=self.store.weight.device)
         self.store.forward(ids, self.offsets[: n + 1], self.zero, 1, n, out, self.zero, self.D,
                            onehot=True)
         self._ids = ids
-        return out.clone()
+        return out
 
     def _update(self, grad):
         ids = self._ids
@@ -521,6 +525,7 @@ class Bert4RecTrainer:
         # gradient buffer through one index_copy each (maps built once from the
         # flat views), so autograd accumulates nothing there (the QKV cat's
         # backward and 35 AccumulateGrad adds per step before)
+        self._zero_ranges = None
         if dev.type == "cuda" and os.environ.get("TDFO_B4R_DIRECT_GRADS", "1") != "0":
             self._attach_direct_grads()
         self.seqs = torch.zeros(batch_size, max_len, dtype=torch.int64, device=dev)
@@ -539,18 +544,13 @@ class Bert4RecTrainer:
         self._counters = [self.opt.hyper[1:2], eh[1:2], self.model.rng_step]
 
     def _flat_index(self, params) -> torch.Tensor:
-        base = self.opt.grad.data_ptr()
-        idx = []
-        for p in params:
-            off = (p.grad.data_ptr() - base) // 4
-            assert 0 <= off and p.grad.is_contiguous(), "parameter grad is not a flat view"
-            idx.append(torch.arange(off, off + p.numel(), dtype=torch.int64))
-        return torch.cat(idx).to(self.device)
+        return ops.flat_scatter_index(self.opt.grad, [p.grad for p in params])
 
     def _attach_direct_grads(self):
         m = self.model
         m.gdst = (self.opt.grad, self._flat_index([m.layernorm.weight, m.layernorm.bias,
                                                    m.positional_encoding]))
+        idxs = [m.gdst[1]]
         for blk in m.transformer_blocks:
             att, ff = blk.attention, blk.feed_forward
             order = ([l.weight for l in att.linear_layers] + [l.bias for l in att.linear_layers]
@@ -559,6 +559,39 @@ class Bert4RecTrainer:
                         blk.output_sublayer.norm.weight, blk.output_sublayer.norm.bias,
                         ff.w_1.weight, ff.w_1.bias, ff.w_2.weight, ff.w_2.bias])
             blk.gdst = (self.opt.grad, self._flat_index(order))
+            idxs.append(blk.gdst[1])
+        # flat ranges the direct writes do not cover: the only ones a step
+        # must still zero while the fused kernels run (none when the output
+        # layer's step is fused too: no fill launches)
+        cov = torch.ones(self.opt.numel, dtype=torch.bool)    # (alignment gaps: never written)
+        for _, off, n in self.opt._views:
+            cov[off:off + n] = False
+        cov[torch.cat(idxs).cpu()] = True
+        self._zero_ranges = []
+        for lo, hi in self.opt._ranges:
+            c = cov[lo:hi]
+            j = lo
+            while j < hi:
+                if bool(c[j - lo]):
+                    j += 1
+                    continue
+                k = j
+                while k < hi and not bool(c[k - lo]):
+                    k += 1
+                self._zero_ranges.append((j, k))
+                j = k
+
+    def _zero_grads(self):
+        m = self.model
+        ff = m.transformer_blocks[0].feed_forward.w_1.out_features if len(m.transformer_blocks) else 0
+        direct = (self._zero_ranges is not None and USE_FUSED and USE_FUSED_BLOCK and
+                  _fused_block_ok(self.T, self.E, m.transformer_blocks[0].attention.h, ff)
+                  if len(m.transformer_blocks) else False)
+        if not direct:
+            self.opt.zero_grads()
+            return
+        for lo, hi in self._zero_ranges:
+            self.opt.grad[lo:hi].zero_()
 
     # ------------------------------------------------------------ train
     def _embed(self, seqs):
@@ -576,12 +609,17 @@ class Bert4RecTrainer:
         loss = linear_cross_entropy(h.reshape(-1, self.E), self.model.out.weight,
                                     self.model.out.bias, labels.reshape(-1), self.eps,
                                     loss_acc=self.loss_sum, unit_grad=True, step=self._xent_step)
-        loss.backward()
+        # the root gradient from a persistent 1 (implicit backward() fills a
+        # fresh ones tensor every step: one fill launch)
+        one = getattr(self, "_one", None)
+        if one is None or one.shape != loss.shape or one.device != loss.device:
+            one = self._one = torch.ones_like(loss)
+        loss.backward(one)
         return loss
 
     def _step_body(self, seqs, labels):
         ops.bump(self._counters)
-        self.opt.zero_grads()
+        self._zero_grads()
         loss = self._fwd_bwd(seqs, labels)
         self.opt.all_reduce_grads(average=True)
         self.opt.step()

@@ -32,6 +32,7 @@ deterministic sparse update, so replicas stay bit-identical. Sharded
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional
 
@@ -187,6 +188,8 @@ class TwoTowerTrainer:
         self.graph = None
         self._cur_b = self.B
         self._bumped = False
+        # one-GPU fp32 steps: the fused six-launch sequence (_step_local_fused)
+        self.fused_step = os.environ.get("TDFO_TT_FUSED", "1") != "0"
 
     # ------------------------------------------------------------ data in
     def load_batch(self, batch: Dict[str, torch.Tensor], eval_mode: bool = False) -> int:
@@ -326,7 +329,30 @@ class TwoTowerTrainer:
                                 self.hyper, wd=self.cfg.weight_decay,
                                 found_inf=self.found_inf if self.mp else None)
 
+    def _step_local_fused(self, b: int):
+        """The one-GPU fp32 step in six launches: lookup; towers + BCE +
+        backward with both step counters; the partial rows' reduction + AdamW
+        + loss add + AUC histogram (``reduce_adam``); the embedding sort,
+        update and combine. Bit-identical to the unfused sequence
+        (``TDFO_TT_FUSED=0``: + reduce_rows, auc_hist, bump, dense_optimizer
+        and the loss add as launches of their own)."""
+        self._lookup(b)
+        ops.two_tower(self.X[:b], self.P, self.labels[:b], 1.0 / b, self.logits[:b], self.dX[:b],
+                      self.part, bumps=[self.hyper, self.emb_hyper])
+        ops.reduce_adam(self.part, ops.two_tower_parts(b), NPARAM, ops.TT_PART_LD, self.G, self.P,
+                        self.M, self.V, self.hyper, wd=self.cfg.weight_decay, adamw=True,
+                        loss_acc=self.loss_sum, logits=self.logits[:b], labels=self.labels[:b],
+                        nb=self.nbins, hist=self.train_hist)
+        self._bumped = True
+        try:
+            self._emb_update(self.ids[: self.T * b], b, self.dX[:b])
+        finally:
+            self._bumped = False
+
     def _step_local(self, b: int):
+        if not self.mp and self.device.type == "cuda" and self.fused_step:
+            self._step_local_fused(b)
+            return
         self._train_compute(b)
         self._mp_check([self.G[:NPARAM], self.dX[:b, :112]])
         if not self.mp and self.device.type == "cuda":

@@ -209,10 +209,26 @@ def encoder_layer_fwd(x, ids, step, params, H, rate, seed, pad_id, eps, saved, y
 
 
 def encoder_layer_bwd(x, ids, step, params, H, rate, seed, pad_id, eps, saved, dy, dx, part,
-                      grad):
-    """dx and the flat parameter gradient (summed over sequences in order)."""
+                      grad, gidx=None):
+    """dx and the packed parameter gradient (summed over sequences in order);
+    with ``gidx`` (see ``flat_scatter_index``) gradient c lands in
+    grad[gidx[c]] -- a trainer's flat gradient buffer -- instead."""
     _native().encoder_layer_bwd(x, ids, step, list(params), H, rate, seed, pad_id, eps,
-                                list(saved), dy, dx, part, grad)
+                                list(saved), dy, dx, part, grad, gidx)
+
+
+def flat_scatter_index(flat: torch.Tensor, views) -> torch.Tensor:
+    """int64 positions in ``flat`` of every element of ``views`` (contiguous
+    views into ``flat``, in order), on flat's device: the ``gidx`` that makes
+    a kernel write a packed gradient straight into a flat gradient buffer.
+    Bounds-checked here, once, so the kernels can trust it."""
+    base, esz, idx = flat.data_ptr(), flat.element_size(), []
+    for v in views:
+        off = (v.data_ptr() - base) // esz
+        if not (v.is_contiguous() and 0 <= off and off + v.numel() <= flat.numel()):
+            raise ValueError("flat_scatter_index: every view must be a contiguous view of flat")
+        idx.append(torch.arange(off, off + v.numel(), dtype=torch.int64))
+    return torch.cat(idx).to(flat.device)
 
 
 def embedding_segsort(v: int = -1) -> int:
@@ -741,14 +757,39 @@ def two_tower_parts(B: int) -> int:
     return (B + ref.TT_SPB - 1) // ref.TT_SPB
 
 
-def two_tower(X, P, labels, inv_n, logits, dX=None, part=None, loss_scale=None, half=False):
+def two_tower(X, P, labels, inv_n, logits, dX=None, part=None, loss_scale=None, half=False,
+              bumps=()):
     """Fused TwoTower forward (+ BCE + backward when dX/part given).
     ``half``: fp16 compute (mixed precision); ``loss_scale``: device scalar
-    multiplying the loss gradient (dynamic loss scaling)."""
+    multiplying the loss gradient (dynamic loss scaling). ``bumps`` (train):
+    step counters ([lr, step, ...]) advanced by one inside the launch."""
+    bumps = list(bumps)
     if _gpu(X):
-        _native().two_tower(X, P, labels, float(inv_n), logits, dX, part, loss_scale, bool(half))
+        _native().two_tower(X, P, labels, float(inv_n), logits, dX, part, loss_scale, bool(half),
+                            bumps)
     else:
         ref.two_tower(X, P, labels, inv_n, logits, dX, part, loss_scale, half)
+        for b in bumps:
+            b[1:2] += 1.0
+
+
+def reduce_adam(part, nparts, n, ld, grad, p, m, v, hyper, beta1=0.9, beta2=0.999, eps=1e-8,
+                wd=0.0, adamw=True, loss_acc=None, logits=None, labels=None, nb=0, hist=None):
+    """grad[:n + 1] = fixed-order sum of ``nparts`` partial rows (stride ``ld``),
+    one Adam(W) step of p[:n] from grad[:n] and loss_acc (fp64) += grad[n]:
+    ``reduce_rows`` + ``dense_optimizer`` + the loss add in one launch; with
+    ``hist`` also ``auc_hist(logits, labels, nb, hist)`` (a block of its own)."""
+    if _gpu(part):
+        _native().reduce_adam(part, int(nparts), int(n), int(ld), grad, p, m, v, hyper,
+                              float(beta1), float(beta2), float(eps), float(wd), bool(adamw),
+                              loss_acc, logits, labels, int(nb), hist)
+    else:
+        if hist is not None:
+            ref.auc_hist(logits, labels, nb, hist)
+        ref.reduce_rows(part, nparts, n + 1, ld, grad, False, 1.0)
+        loss_acc += grad[n:n + 1].double()
+        ref.dense_optimizer(p[:n], grad[:n], m[:n], v[:n], None, OPT_ADAMW if adamw else OPT_ADAM,
+                            hyper, beta1, beta2, eps, wd, 0.0, None)
 
 
 def linear_xent(H, W, bias, labels, eps, ignore, dH, lossv, dW=None, db=None, loss=None,
@@ -851,11 +892,17 @@ def seq_prologue_fwd(x, pos, n, eps, gamma, beta, rate, seed, step, y, mean, rst
         ref.seq_prologue_fwd(x, pos, n, eps, gamma, beta, rate, seed, step, y, mean, rstd)
 
 
-def seq_prologue_bwd(x, pos, g, n, gamma, mean, rstd, rate, seed, step, dx, part, out3):
-    """dx and out3 = [dgamma | dbeta | dpos] (3n) of seq_prologue_fwd."""
+def seq_prologue_bwd(x, pos, g, n, gamma, mean, rstd, rate, seed, step, dx, part, out3,
+                     gidx=None):
+    """dx and out3 = [dgamma | dbeta | dpos] (3n) of seq_prologue_fwd; with
+    ``gidx`` element j of that goes to out3[gidx[j]] (a flat gradient buffer)."""
     if _gpu(x):
         _native().seq_prologue_bwd(x, pos, g, int(n), gamma, mean, rstd, float(rate),
-                                   int(seed) & 0xFFFFFFFF, step, dx, part, out3)
+                                   int(seed) & 0xFFFFFFFF, step, dx, part, out3, gidx)
+    elif gidx is not None:
+        tmp = torch.empty(3 * n, dtype=torch.float32, device=x.device)
+        ref.seq_prologue_bwd(x, pos, g, n, gamma, mean, rstd, rate, seed, step, dx, tmp)
+        out3.index_copy_(0, gidx, tmp)
     else:
         ref.seq_prologue_bwd(x, pos, g, n, gamma, mean, rstd, rate, seed, step, dx, out3)
 

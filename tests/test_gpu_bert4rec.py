@@ -126,6 +126,33 @@ def test_bert4rec_gpu_matches_cpu():
     torch.testing.assert_close(gpu.item.weight.cpu(), cpu.item.weight, rtol=1e-3, atol=1e-4)
 
 
+@pytest.mark.parametrize("fused_xent", ["1", "0"])
+def test_bert4rec_direct_grads_bit_identical(monkeypatch, fused_xent):
+    """Encoder / prologue gradients written by the kernels' reductions
+    straight into the flat buffer (and no zero fill of what they cover) vs
+    the returned-gradient path: same bits after several steps with dropout."""
+    n, T, B = 3000, 20, 16
+    kw = dict(lr=3e-3, dropout=0.1, seed=5)
+    monkeypatch.setenv("TDFO_XENT_FUSED_STEP", fused_xent)
+    monkeypatch.setenv("TDFO_B4R_DIRECT_GRADS", "1")
+    a = Bert4RecTrainer(n, T, 16, 2, 2, B, device=DEV, **kw)
+    monkeypatch.setenv("TDFO_B4R_DIRECT_GRADS", "0")
+    b = Bert4RecTrainer(n, T, 16, 2, 2, B, device=DEV, **kw)
+    assert a._zero_ranges is not None and b._zero_ranges is None
+    if fused_xent == "1":
+        assert a._zero_ranges == []          # every flat gradient written directly
+    g = torch.Generator().manual_seed(0)
+    for _ in range(6):
+        s, l = _batch(g, B, T, n)
+        for t in (a, b):
+            t.load_batch(s.to(DEV), l.to(DEV))
+            t.step()
+    torch.cuda.synchronize()
+    assert torch.equal(a.opt.flat, b.opt.flat)
+    assert torch.equal(a.item.weight, b.item.weight)
+    assert a.pop_loss() == b.pop_loss()
+
+
 def test_bert4rec_graph_replay_matches_eager():
     n, T, B = 5000, 20, 16
     kw = dict(lr=3e-3, dropout=0.0, seed=3)

@@ -68,6 +68,53 @@ def test_two_tower_trainer_gpu_matches_cpu(emb_update):
     assert abs(lg[0] - lc[0]) < 1e-3 and abs(lg[1] - lc[1]) < 1e-3
 
 
+@pytest.mark.parametrize("emb_update,B", [("sparse", 1000), ("sparse", 2048), ("dense", 512)])
+def test_two_tower_fused_step_bit_identical(emb_update, B):
+    """The six-launch step (AUC + counters inside the tower kernel,
+    reduce_adam) against the separate launches: same bits everywhere."""
+    cfg = TwoTowerConfig(SM, learning_rate=3e-3, emb_update=emb_update, weight_decay=1e-2)
+    a = TwoTowerTrainer(cfg, B, DEV)
+    b = TwoTowerTrainer(cfg, B, DEV)
+    a.fused_step, b.fused_step = True, False
+    for i in range(10):
+        x = {k: v.to(DEV) for k, v in make_batch(B, i).items()}
+        a.load_batch(x)
+        b.load_batch(x)
+        a.step()
+        b.step()
+    torch.cuda.synchronize()
+    for name in ("P", "M", "V", "hyper", "emb_hyper", "loss_sum", "train_hist"):
+        assert torch.equal(getattr(a, name), getattr(b, name)), name
+    assert torch.equal(a.G[:ops.TT_NPARAM + 1], b.G[:ops.TT_NPARAM + 1])
+    assert torch.equal(a.emb.weight, b.emb.weight)
+    assert a.pop_metrics() == b.pop_metrics()
+
+
+def test_reduce_adam_matches_reference():
+    torch.manual_seed(3)
+    n, ld, rows = 2400, 2432, 77
+    part = torch.randn(rows * ld, device=DEV)
+    p, m, v = (torch.randn(n, device=DEV) for _ in range(3))
+    v = v.abs()
+    hyper = torch.tensor([1e-2, 3.0, 0.5], device=DEV)
+    grad = torch.zeros(n + 1, device=DEV)
+    acc = torch.zeros(1, dtype=torch.float64, device=DEV)
+    lg = torch.randn(1000, device=DEV) * 3
+    y = (torch.rand(1000, device=DEV) < 0.3).float()
+    h = torch.zeros(2 * 199, dtype=torch.int64, device=DEV)
+    pc, mc, vc, gc, accc, hc = (t.cpu().clone() for t in (p, m, v, grad, acc, h))
+    ops.reduce_adam(part, rows, n, ld, grad, p, m, v, hyper, wd=0.1, adamw=True, loss_acc=acc,
+                    logits=lg, labels=y, nb=199, hist=h)
+    ops.reduce_adam(part.cpu(), rows, n, ld, gc, pc, mc, vc, hyper.cpu(), wd=0.1, adamw=True,
+                    loss_acc=accc, logits=lg.cpu(), labels=y.cpu(), nb=199, hist=hc)
+    assert torch.equal(h.cpu(), hc)
+    torch.testing.assert_close(grad.cpu(), gc, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(p.cpu(), pc, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(m.cpu(), mc, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(v.cpu(), vc, rtol=1e-5, atol=1e-6)
+    assert abs(float(acc.cpu() - accc)) < 1e-3
+
+
 def test_two_tower_graph_replay_matches_eager():
     cfg = TwoTowerConfig(SM, learning_rate=3e-3)
     B = 1024
