@@ -192,10 +192,18 @@ __global__ __launch_bounds__(256) void emb_fwd_kernel(EmbFwdArgs a) {
 }
 
 // ---------------------------------------------------------- backward ----
+// entries per update wave for narrow rows (D <= 32; A/B builds:
+// TDFO_HIPCC_EXTRA=-DTDFO_EMB_SMALL_CH=32). 16: twice the waves, half the
+// serial per-row chain each -- TwoTower 0.0655 -> 0.0621 ms/step, Bert4Rec
+// B=16 0.430 -> 0.426 (8: 0.0641 / 0.424; profiles/r06/notes.md)
+#ifndef TDFO_EMB_SMALL_CH
+#define TDFO_EMB_SMALL_CH 16
+#endif
 template <int D>
 struct BwdCfg {
   static constexpr int EPL = D >= 64 ? D / 64 : 1;                  // elements per lane
-  static constexpr int CH = EPL <= 2 ? 32 : (EPL == 4 ? 16 : 8);    // entries per wave
+  static constexpr int CH = D <= 32 ? TDFO_EMB_SMALL_CH
+                                    : (EPL <= 2 ? 32 : (EPL == 4 ? 16 : 8));   // entries per wave
 };
 
 // keys[p] = row_offset[t] + id, vals[p] = p, goff[p] = offset of p's pooled
@@ -1323,7 +1331,7 @@ struct WsLayout {
 
 inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
 
-int ch_for(int D) { return D <= 128 ? 32 : (D == 256 ? 16 : 8); }
+int ch_for(int D) { return D <= 32 ? TDFO_EMB_SMALL_CH : (D <= 128 ? 32 : (D == 256 ? 16 : 8)); }
 
 WsLayout ws_layout(int64_t nnz, int D) {
   WsLayout L;
