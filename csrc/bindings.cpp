@@ -1357,7 +1357,8 @@ void auc_hist(const Tensor& logits, const Tensor& labels, int64_t nb, const Tens
 void two_tower(const Tensor& X, const Tensor& P, const Tensor& labels, double inv_n,
                const Tensor& logits, const c10::optional<Tensor>& dX,
                const c10::optional<Tensor>& part, const c10::optional<Tensor>& loss_scale,
-               bool half, at::TensorList bumps) {
+               bool half, at::TensorList bumps, const c10::optional<Tensor>& emb_w,
+               const c10::optional<Tensor>& ids, const c10::optional<Tensor>& row_off) {
   check_dev(X, "X"); check_2d_rowmajor(X, "X");
   const int64_t B = X.size(0);
   TORCH_CHECK(X.scalar_type() == at::kFloat && X.size(1) >= 114 && X.stride(0) % 4 == 0 &&
@@ -1375,6 +1376,20 @@ void two_tower(const Tensor& X, const Tensor& P, const Tensor& labels, double in
     a.loss_scale = loss_scale->data_ptr<float>();
   }
   a.logits = logits.data_ptr<float>();
+  if (emb_w) {
+    // ids / row offsets come from the trainer's own validated buffers (the
+    // same ones the lookup kernel it replaces read)
+    TORCH_CHECK(ids && row_off, "two_tower: emb_w needs ids and row_off");
+    check_f32c(*emb_w, "emb_w"); check_dev(*ids, "ids"); check_dev(*row_off, "row_off");
+    TORCH_CHECK(emb_w->dim() == 2 && emb_w->size(1) == 16 && aligned16(emb_w->data_ptr()) &&
+                ids->scalar_type() == at::kLong && ids->is_contiguous() && ids->numel() >= 7 * B &&
+                row_off->scalar_type() == at::kLong && row_off->is_contiguous() &&
+                row_off->numel() >= 7, "two_tower: emb_w [rows, 16] fp32, ids int64 [7 * B], "
+                "row_off int64 [7]");
+    a.emb_w = emb_w->data_ptr<float>();
+    a.ids = ids->data_ptr<int64_t>();
+    a.row_off = row_off->data_ptr<int64_t>();
+  }
   const bool train = dX.has_value();
   if (train) {
     TORCH_CHECK(part.has_value(), "two_tower: train needs part");
@@ -1738,7 +1753,7 @@ TORCH_LIBRARY(tdfo, m) {
   m.def("jagged_ids_to_dense(Tensor values, Tensor offsets, int pad, Tensor(a!) out) -> ()");
   m.def("two_tower(Tensor X, Tensor P, Tensor labels, float inv_n, Tensor(a!) logits, "
         "Tensor(b!)? dX, Tensor(c!)? part, Tensor? loss_scale, bool half, "
-        "Tensor(d!)[] bumps) -> ()");
+        "Tensor(d!)[] bumps, Tensor? emb_w, Tensor? ids, Tensor? row_off) -> ()");
   m.def("reduce_adam(Tensor part, int nparts, int n, int ld, Tensor(a!) grad, Tensor(b!) p, "
         "Tensor(c!) m, Tensor(d!) v, Tensor hyper, float beta1, float beta2, float eps, "
         "float wd, bool adamw, Tensor(e!) loss_acc, Tensor? logits, Tensor? labels, int nb, "

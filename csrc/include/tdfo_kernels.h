@@ -384,6 +384,11 @@ struct TwoTowerArgs {
   float* part;
   // optional (train): step counters bumped by block 0 (no bump launch)
   HeadBumps bumps{};
+  // optional: the 7 embedding rows of every sample gathered here from the
+  // table (emb_w [rows, 16] fp32, ids table-major ids[t * B + s], row_off[t])
+  // instead of read from X[:, :112] -- the lookup launch folded in; X then
+  // supplies only the two dense features (columns 112, 113)
+  const float* emb_w = nullptr; const int64_t* ids = nullptr; const int64_t* row_off = nullptr;
 };
 int two_tower_parts(int B);
 void two_tower(const TwoTowerArgs& a, int train, hipStream_t s);

@@ -86,10 +86,51 @@ __global__ __launch_bounds__(64 * NWV) void two_tower_kernel(TwoTowerArgs a) {
   for (int k = t; k < NP; k += 64 * NWV) Wl[k] = rnd<HALF>(a.P[k]);
   const int64_t s0 = (int64_t)blockIdx.x * SPB + w * WS;
   float(*X)[XLD] = Xs[w];
-  for (int idx = lane; idx < WS * 114; idx += 64) {
-    const int r = idx / 114, c = idx - r * 114;
-    const int64_t sr = s0 + r;
-    X[r][c] = sr < a.B ? rnd<HALF>(a.X[sr * a.ldx + c]) : 0.f;
+  if (a.emb_w != nullptr) {
+    // fused lookup: (sample, table) pairs p = lane, lane + 64 of the wave's
+    // 16 x 7; both ids first, then 8 independent float4 row loads (two
+    // round trips), rows straight into the staged X tile
+    constexpr int NT = 7, NPAIR = WS * NT;
+    int64_t row[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int p = lane + 64 * q;
+      const int r = p / NT, t = p - r * NT;
+      const int64_t sr = s0 + r;
+      row[q] = (p < NPAIR && sr < a.B) ? a.row_off[t] + a.ids[(int64_t)t * a.B + sr] : -1;
+    }
+    float4 v[2][4];
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        v[q][u] = row[q] >= 0 ? ((const float4*)(a.emb_w + row[q] * E))[u]
+                              : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int p = lane + 64 * q;
+      if (p < NPAIR) {
+        const int r = p / NT, t = p - r * NT;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          X[r][t * E + 4 * u] = rnd<HALF>(v[q][u].x);
+          X[r][t * E + 4 * u + 1] = rnd<HALF>(v[q][u].y);
+          X[r][t * E + 4 * u + 2] = rnd<HALF>(v[q][u].z);
+          X[r][t * E + 4 * u + 3] = rnd<HALF>(v[q][u].w);
+        }
+      }
+    }
+    if (lane < 2 * WS) {
+      const int r = lane >> 1, c = 112 + (lane & 1);
+      const int64_t sr = s0 + r;
+      X[r][c] = sr < a.B ? rnd<HALF>(a.X[sr * a.ldx + c]) : 0.f;
+    }
+  } else {
+    for (int idx = lane; idx < WS * 114; idx += 64) {
+      const int r = idx / 114, c = idx - r * 114;
+      const int64_t sr = s0 + r;
+      X[r][c] = sr < a.B ? rnd<HALF>(a.X[sr * a.ldx + c]) : 0.f;
+    }
   }
   __syncthreads();
   const float* uW1 = Wl + O_UW1;

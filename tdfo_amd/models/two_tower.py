@@ -330,15 +330,16 @@ class TwoTowerTrainer:
                                 found_inf=self.found_inf if self.mp else None)
 
     def _step_local_fused(self, b: int):
-        """The one-GPU fp32 step in six launches: lookup; towers + BCE +
-        backward with both step counters; the partial rows' reduction + AdamW
-        + loss add + AUC histogram (``reduce_adam``); the embedding sort,
-        update and combine. Bit-identical to the unfused sequence
-        (``TDFO_TT_FUSED=0``: + reduce_rows, auc_hist, bump, dense_optimizer
-        and the loss add as launches of their own)."""
-        self._lookup(b)
+        """The one-GPU fp32 step in four launches: towers + BCE + backward
+        with the embedding rows gathered in-kernel and both step counters
+        bumped; the partial rows' reduction + AdamW + loss add + AUC histogram
+        (``reduce_adam``); the embedding sort and update (crossing runs
+        finished in-kernel for small batches). Bit-identical to the unfused
+        sequence (``TDFO_TT_FUSED=0``: + the lookup, reduce_rows, auc_hist,
+        bump, dense_optimizer and the loss add as launches of their own)."""
         ops.two_tower(self.X[:b], self.P, self.labels[:b], 1.0 / b, self.logits[:b], self.dX[:b],
-                      self.part, bumps=[self.hyper, self.emb_hyper])
+                      self.part, bumps=[self.hyper, self.emb_hyper],
+                      emb=(self.emb.weight, self.ids[: self.T * b], self.emb.row_offset))
         ops.reduce_adam(self.part, ops.two_tower_parts(b), NPARAM, ops.TT_PART_LD, self.G, self.P,
                         self.M, self.V, self.hyper, wd=self.cfg.weight_decay, adamw=True,
                         loss_acc=self.loss_sum, logits=self.logits[:b], labels=self.labels[:b],

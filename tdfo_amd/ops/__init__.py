@@ -758,16 +758,26 @@ def two_tower_parts(B: int) -> int:
 
 
 def two_tower(X, P, labels, inv_n, logits, dX=None, part=None, loss_scale=None, half=False,
-              bumps=()):
+              bumps=(), emb=None):
     """Fused TwoTower forward (+ BCE + backward when dX/part given).
     ``half``: fp16 compute (mixed precision); ``loss_scale``: device scalar
     multiplying the loss gradient (dynamic loss scaling). ``bumps`` (train):
-    step counters ([lr, step, ...]) advanced by one inside the launch."""
+    step counters ([lr, step, ...]) advanced by one inside the launch.
+    ``emb = (weight [rows, 16], ids [7 * B] table-major, row_offset [7])``:
+    the kernel gathers X[:, :112] itself (X then holds only the two dense
+    features) -- the lookup launch folded in."""
     bumps = list(bumps)
     if _gpu(X):
+        w, ids, ro = emb if emb is not None else (None, None, None)
         _native().two_tower(X, P, labels, float(inv_n), logits, dX, part, loss_scale, bool(half),
-                            bumps)
+                            bumps, w, ids, ro)
     else:
+        if emb is not None:
+            w, ids, ro = emb
+            B = X.shape[0]
+            X = X.clone()
+            for t in range(7):
+                X[:, 16 * t:16 * (t + 1)] = w[ro[t] + ids[t * B:(t + 1) * B]]
         ref.two_tower(X, P, labels, inv_n, logits, dX, part, loss_scale, half)
         for b in bumps:
             b[1:2] += 1.0
