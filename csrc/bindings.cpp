@@ -814,6 +814,12 @@ void set_emb_ws(tdfo::EmbBwdArgs& a, const Tensor& work) {
   a.workspace = work.data_ptr(); a.workspace_bytes = ws;
 }
 
+// reduce_adam(defer=true) parks its launch here; the next embedding_bwd of
+// this thread runs it as side blocks of its sort launch (tdfo::EmbBwdArgs::
+// side), flush_side_job() launches a still-parked one on its own.
+thread_local bool g_side_pending = false;
+thread_local tdfo::ReduceAdamArgs g_side{};
+
 void embedding_bwd(const Tensor& W, const Tensor& row_offset, const Tensor& indices,
                    const Tensor& offsets, const Tensor& grad_off,
                    const c10::optional<Tensor>& psw, int64_t T, int64_t B, bool mean,
@@ -828,6 +834,11 @@ void embedding_bwd(const Tensor& W, const Tensor& row_offset, const Tensor& indi
   const size_t ws = tdfo::embedding_bwd_workspace(a.nnz, a.D);
   Tensor work = at::empty({(int64_t)ws}, W.options().dtype(at::kByte));
   set_emb_ws(a, work);
+  if (g_side_pending) {
+    a.side = g_side;
+    a.side_on = 1;
+    g_side_pending = false;
+  }
   tdfo::embedding_bwd_fused(a, cur_stream());
 }
 
@@ -1422,7 +1433,7 @@ void reduce_adam(const Tensor& part, int64_t nparts, int64_t n, int64_t ld, cons
                  double beta1, double beta2, double eps, double wd, bool adamw,
                  const Tensor& loss_acc, const c10::optional<Tensor>& logits,
                  const c10::optional<Tensor>& labels, int64_t nb,
-                 const c10::optional<Tensor>& hist) {
+                 const c10::optional<Tensor>& hist, bool defer) {
   check_f32c(part, "part"); check_f32c(grad, "grad"); check_f32c(p, "p"); check_f32c(m, "m");
   check_f32c(v, "v"); check_f32c(hyper, "hyper");
   check_dev(loss_acc, "loss_acc");
@@ -1448,7 +1459,20 @@ void reduce_adam(const Tensor& part, int64_t nparts, int64_t n, int64_t ld, cons
     a.nlog = (int)logits->numel(); a.nb = (int)nb;
     a.hist = reinterpret_cast<unsigned long long*>(hist->data_ptr<int64_t>());
   }
+  if (defer) {
+    TORCH_CHECK(!g_side_pending, "reduce_adam: a deferred job is already waiting for its "
+                "embedding_bwd (flush_side_job)");
+    g_side = a;
+    g_side_pending = true;
+    return;
+  }
   tdfo::reduce_adam(a, cur_stream());
+}
+
+void flush_side_job() {
+  if (!g_side_pending) return;
+  g_side_pending = false;
+  tdfo::reduce_adam(g_side, cur_stream());
 }
 
 void linear_xent(const Tensor& H, const Tensor& W, const Tensor& bias, const Tensor& labels,
@@ -1757,7 +1781,8 @@ TORCH_LIBRARY(tdfo, m) {
   m.def("reduce_adam(Tensor part, int nparts, int n, int ld, Tensor(a!) grad, Tensor(b!) p, "
         "Tensor(c!) m, Tensor(d!) v, Tensor hyper, float beta1, float beta2, float eps, "
         "float wd, bool adamw, Tensor(e!) loss_acc, Tensor? logits, Tensor? labels, int nb, "
-        "Tensor(f!)? hist) -> ()");
+        "Tensor(f!)? hist, bool defer) -> ()");
+  m.def("flush_side_job() -> ()", flush_side_job);
 }
 
 TORCH_LIBRARY_IMPL(tdfo, CUDA, m) {

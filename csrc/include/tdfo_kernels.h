@@ -129,6 +129,17 @@ void embedding_bag_fwd(const EmbFwdArgs& a, hipStream_t s);
 //   4. the optimizer is applied once per unique row.
 enum EmbOpt { EMB_SGD = 0, EMB_ROWWISE_ADAGRAD = 1, EMB_ADAM = 2,
               EMB_ADAGRAD = 3, EMB_DENSE_GRAD = 4 };
+// reduce_adam's arguments (declared with it below, in the loss section)
+constexpr int REDUCE_ADAM_MAX_NB = 512;
+struct ReduceAdamArgs {
+  const float* part; int nparts; int n; int ld;
+  float* grad; float* p; float* m; float* v;
+  const float* hyper; float beta1, beta2, eps, wd; int adamw;
+  double* loss_acc;
+  const float* logits = nullptr; const float* labels = nullptr; int nlog = 0; int nb = 0;
+  unsigned long long* hist = nullptr;
+};
+
 struct EmbBwdArgs {
   float* W; int D;
   const int64_t* row_offset; const int64_t* indices; const int64_t* offsets;
@@ -154,6 +165,12 @@ struct EmbBwdArgs {
   // keys pass finds a position's bag by division instead of a binary search
   // over all T*B bag offsets
   const int32_t* bag_len;
+  // optional side job (side_on): a reduce_adam run by extra blocks of the
+  // one-hot per-table sort launch, beside the sort (it needs nothing the
+  // backward touches); run as its own launch first where no such sort runs.
+  // TwoTower: the dense step hidden behind the 7-block sort.
+  ReduceAdamArgs side{};
+  int side_on = 0;
 };
 size_t embedding_bwd_workspace(int64_t nnz, int D);
 // One-hot batches (nnz == T*B, B <= 8192): per-table LDS sort in one launch
@@ -333,16 +350,8 @@ void head_reduce(const float* part, int nparts, int K, float* grad, float* loss_
 // the loss partial: loss_acc[0] += (double)sum. Optionally one more block
 // bins logits[0..nlog) into hist ([2 * nb] int64, auc_hist's buckets).
 // Replaces reduce_rows + the flat optimizer + the loss add + auc_hist of a
-// small model's step (TwoTower).
-constexpr int REDUCE_ADAM_MAX_NB = 512;
-struct ReduceAdamArgs {
-  const float* part; int nparts; int n; int ld;
-  float* grad; float* p; float* m; float* v;
-  const float* hyper; float beta1, beta2, eps, wd; int adamw;
-  double* loss_acc;
-  const float* logits = nullptr; const float* labels = nullptr; int nlog = 0; int nb = 0;
-  unsigned long long* hist = nullptr;
-};
+// small model's step (TwoTower). (ReduceAdamArgs: above EmbBwdArgs, which
+// can carry one as a side job.)
 void reduce_adam(const ReduceAdamArgs& a, hipStream_t s);
 // out[j] (=|+=) sum_r in[r*ld + j], j < n, fixed order (deterministic).
 // idx (optional): out[idx[j]] instead of out[j] (a gather-free scatter into

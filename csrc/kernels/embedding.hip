@@ -26,6 +26,7 @@
 
 #include "tdfo_common.h"
 #include "tdfo_kernels.h"
+#include "tdfo_reduce_adam.h"
 
 namespace tdfo {
 namespace {
@@ -421,6 +422,16 @@ __global__ __launch_bounds__(SEG_THREADS) void emb_segsort_kernel(
   __shared__ uint32_t wsum[SEG_WAVES];
   __shared__ uint32_t smax[SEG_WAVES];
   const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  if (t >= a.T) {
+    // side blocks (a.side_on): four 256-thread reduce_adam units each, in the
+    // sort's LDS (units take 256 floats of skey each; the one AUC unit sval)
+    static_assert(SK * SEG_THREADS >= 4 * RA_PH * RA_COLS &&
+                  SK * SEG_THREADS >= 2 * REDUCE_ADAM_MAX_NB, "side-job LDS");
+    const int slice = tid >> 8;
+    reduce_adam_unit(a.side, (t - a.T) * (SEG_THREADS / 256) + slice, tid & 255,
+                     (float(*)[RA_COLS])(skey + slice * RA_PH * RA_COLS), sval);
+    return;
+  }
   if (t == 0 && tid == 0) {                         // read by later kernels
     tail_count[0] = 0;
     tail_count[1] = 0;
@@ -1403,22 +1414,29 @@ void prep_impl(const EmbBwdArgs& a, const WsLayout& L, hipStream_t s) {
   float* gscale = (a.psw || a.mean) ? (float*)(ws + L.gscale) : nullptr;
   int32_t* tcount = (int32_t*)(ws + L.tcount);
   const int R = a.segsort;                 // runs per physical table (0: off)
+  bool side_done = false;
   if (onehot_path(a)) {
     if (R == 1) {
       int2* meta = meta_path(a) ? (int2*)(ws + L.meta) : nullptr;
       int32_t* rcnt = (int32_t*)(ws + L.rcnt);
       const int ch = ch_for(a.D);
-      if (a.B <= 2 * SEG_THREADS)
-        hipLaunchKernelGGL((emb_segsort_kernel<K, true, 2>), dim3(a.T), dim3(SEG_THREADS), 0, s, a,
-                           keys_out, vals_out, goff, gscale, tcount, (int32_t*)nullptr, meta,
-                           rcnt, ch);
-      else if (g_emb_seg_split)
+      // side job: its units ride in extra blocks of the sort (4 per block)
+      const int side_blocks =
+          a.side_on ? (reduce_adam_units(a.side) + SEG_THREADS / 256 - 1) / (SEG_THREADS / 256) : 0;
+      if (a.B <= 2 * SEG_THREADS) {
+        hipLaunchKernelGGL((emb_segsort_kernel<K, true, 2>), dim3(a.T + side_blocks),
+                           dim3(SEG_THREADS), 0, s, a, keys_out, vals_out, goff, gscale, tcount,
+                           (int32_t*)nullptr, meta, rcnt, ch);
+        side_done = true;
+      } else if (g_emb_seg_split) {
         hipLaunchKernelGGL((emb_segsort_split_kernel<K, SEG_SPLIT>), dim3(a.T * SEG_SPLIT),
                            dim3(SEG_THREADS), 0, s, a, keys_out, vals_out, goff, gscale, tcount);
-      else
-        hipLaunchKernelGGL((emb_segsort_kernel<K, true>), dim3(a.T), dim3(SEG_THREADS), 0, s, a,
-                           keys_out, vals_out, goff, gscale, tcount, (int32_t*)nullptr, meta,
-                           rcnt, ch);
+      } else {
+        hipLaunchKernelGGL((emb_segsort_kernel<K, true>), dim3(a.T + side_blocks),
+                           dim3(SEG_THREADS), 0, s, a, keys_out, vals_out, goff, gscale, tcount,
+                           (int32_t*)nullptr, meta, rcnt, ch);
+        side_done = true;
+      }
     } else {
       int32_t* pos = (int32_t*)(ws + L.pos);
       hipLaunchKernelGGL((emb_segsort_kernel<K, false>), dim3(a.T), dim3(SEG_THREADS), 0, s, a, keys_in,
@@ -1453,6 +1471,7 @@ void prep_impl(const EmbBwdArgs& a, const WsLayout& L, hipStream_t s) {
       radix_sort_pairs_u64(k0, v0, k1, v1, a.nnz, a.key_bits, ws + L.sortws, s);
   }
   TDFO_CHECK_HIP(hipGetLastError());
+  if (a.side_on && !side_done) reduce_adam(a.side, s);     // no sort launch to ride in
 }
 
 template <int D, typename K, int OPT>
@@ -1590,7 +1609,10 @@ void embedding_bwd_fused(const EmbBwdArgs& a, hipStream_t s) {
 }
 
 void embedding_bwd_prepare(const EmbBwdArgs& a, hipStream_t s) {
-  if (a.nnz <= 0) return;
+  if (a.nnz <= 0) {
+    if (a.side_on) reduce_adam(a.side, s);
+    return;
+  }
   const WsLayout L = ws_layout(a.nnz, a.D);
   if (a.key_bits <= 32) prep_impl<uint32_t>(a, L, s);
   else prep_impl<uint64_t>(a, L, s);

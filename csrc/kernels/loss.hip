@@ -10,6 +10,7 @@
 // (a per-step device->host sync) with on-device counts.
 #include "tdfo_common.h"
 #include "tdfo_kernels.h"
+#include "tdfo_reduce_adam.h"
 
 namespace tdfo {
 namespace {
@@ -123,48 +124,6 @@ __global__ __launch_bounds__(256) void reduce_rows_kernel(
   }
 }
 
-// One thread's share of a fixed-order column sum over nparts partial rows:
-// rows ph, ph + PH, ... in groups of four into s0..s3 (a partial last group
-// into s0), returned as (s0 + s1) + (s2 + s3) -- reduce_rows_kernel's loop,
-// with the first PRE rows loaded up front at clamped addresses and then added
-// in that order, so the sums are the plain loop's with one round trip for up
-// to PRE * PH = 512 partial rows (B = 8192) instead of one per group.
-template <int PH>
-__device__ __forceinline__ float col_phase_sum(const float* __restrict__ part, int nparts,
-                                               int ld, int j, int ph) {
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  constexpr int PRE = 32;
-  float v[PRE];
-#pragma unroll
-  for (int q = 0; q < PRE; ++q) {
-    const int r = min(ph + q * PH, nparts - 1);
-    v[q] = part[(int64_t)r * ld + j];
-  }
-#pragma unroll
-  for (int g = 0; g < PRE / 4; ++g) {
-    const int r = ph + 4 * g * PH;
-    if (r + 3 * PH < nparts) {
-      s0 += v[4 * g]; s1 += v[4 * g + 1]; s2 += v[4 * g + 2]; s3 += v[4 * g + 3];
-    } else {
-#pragma unroll
-      for (int q = 0; q < 3; ++q)
-        if (r + q * PH < nparts) s0 += v[4 * g + q];
-    }
-  }
-  int r = ph + PRE * PH;
-  if (r < nparts) {
-    // (more than PRE * PH rows: every group above was full)
-    for (; r + 3 * PH < nparts; r += 4 * PH) {
-      s0 += part[(int64_t)r * ld + j];
-      s1 += part[(int64_t)(r + PH) * ld + j];
-      s2 += part[(int64_t)(r + 2 * PH) * ld + j];
-      s3 += part[(int64_t)(r + 3 * PH) * ld + j];
-    }
-    for (; r < nparts; r += PH) s0 += part[(int64_t)r * ld + j];
-  }
-  return (s0 + s1) + (s2 + s3);
-}
-
 // Head epilogue in one launch: grad[j] = sum_r part[r][j] (j <= K) and
 // loss_acc[0] += sum_r part[r][K+1] with reduce_rows' fixed-order structure
 // (16 columns x 16 row phases per block), plus the step counters
@@ -192,53 +151,15 @@ __global__ __launch_bounds__(256) void head_reduce_kernel(const float* __restric
   if (blockIdx.x == 0 && threadIdx.x < bumps.n) bumps.p[threadIdx.x][1] += 1.f;
 }
 
-// reduce_rows + the flat Adam / AdamW + the loss accumulation of a small
-// model's step in one launch (TwoTower: 2,400 parameters from 128 block
-// partials; three dependent ~4.5-us launches before, profiles/r05/two_tower).
-// Same column sums as reduce_rows_kernel<16>, same adam_elem as
-// dense_opt_kernel: bit-identical to the three-launch sequence.
+// reduce_rows + the flat Adam / AdamW + the loss accumulation (+ the AUC
+// binning) of a small model's step in one launch (TwoTower: 2,400 parameters
+// from 128 block partials; four dependent ~4.5-us launches before,
+// profiles/r05/two_tower). Same column sums as reduce_rows_kernel<16>, same
+// adam_elem as dense_opt_kernel: bit-identical to the separate launches.
 __global__ __launch_bounds__(256) void reduce_adam_kernel(ReduceAdamArgs a) {
-  constexpr int COLS = 16, PH = 256 / COLS;
-  __shared__ float red[PH][COLS];
+  __shared__ float red[RA_PH][RA_COLS];
   __shared__ unsigned int lh[2 * REDUCE_ADAM_MAX_NB];
-  if (a.hist != nullptr && blockIdx.x == gridDim.x - 1) {
-    // the AUC block: auc_hist_kernel's binning (LDS counts, then one integer
-    // atomic per non-empty bucket)
-    for (int i = threadIdx.x; i < 2 * a.nb; i += 256) lh[i] = 0;
-    __syncthreads();
-    for (int i = threadIdx.x; i < a.nlog; i += 256) {
-      const float pr = 1.f / (1.f + __expf(-a.logits[i]));
-      int bkt = (int)(pr * a.nb);
-      bkt = bkt < 0 ? 0 : (bkt >= a.nb ? a.nb - 1 : bkt);
-      atomicAdd(&lh[(a.labels[i] > 0.5f ? a.nb : 0) + bkt], 1u);
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < 2 * a.nb; i += 256)
-      if (lh[i]) atomicAdd(&a.hist[i], (unsigned long long)lh[i]);
-    return;
-  }
-  const int c = threadIdx.x % COLS, ph = threadIdx.x / COLS;
-  const int j = blockIdx.x * COLS + c;
-  red[ph][c] = (j <= a.n && a.nparts > 0) ? col_phase_sum<PH>(a.part, a.nparts, a.ld, j, ph)
-                                          : 0.f;
-  __syncthreads();
-  if (ph == 0 && j <= a.n) {
-    float t = 0.f;
-#pragma unroll
-    for (int q = 0; q < PH; ++q) t += red[q][c];
-    a.grad[j] = t;
-    if (j == a.n) {
-      a.loss_acc[0] += (double)t;
-    } else {
-      const float lr = a.hyper[0], step = a.hyper[1], gs = a.hyper[2];
-      const float bc1 = 1.f - powf(a.beta1, step), bc2 = 1.f - powf(a.beta2, step);
-      float p = a.p[j], m = a.m[j], v = a.v[j];
-      adam_elem(p, t * gs, m, v, lr, bc1, bc2, a.beta1, a.beta2, a.eps, a.wd, a.adamw != 0);
-      a.p[j] = p;
-      a.m[j] = m;
-      a.v[j] = v;
-    }
-  }
+  reduce_adam_unit(a, blockIdx.x, threadIdx.x, red, lh);
 }
 
 constexpr int COLSUM_CHUNKS = 16;
@@ -387,8 +308,7 @@ int colsum_parts(int M) { return COLSUM_CHUNKS; }
 
 void reduce_adam(const ReduceAdamArgs& a, hipStream_t s) {
   if (a.n <= 0) return;
-  const int blocks = (a.n + 1 + 15) / 16 + (a.hist != nullptr ? 1 : 0);
-  hipLaunchKernelGGL(reduce_adam_kernel, dim3(blocks), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(reduce_adam_kernel, dim3(reduce_adam_units(a)), dim3(256), 0, s, a);
   TDFO_CHECK_HIP(hipGetLastError());
 }
 

@@ -190,6 +190,9 @@ class TwoTowerTrainer:
         self._bumped = False
         # one-GPU fp32 steps: the fused six-launch sequence (_step_local_fused)
         self.fused_step = os.environ.get("TDFO_TT_FUSED", "1") != "0"
+        # ... with the dense step (reduce_adam) run by side blocks of the
+        # embedding sort launch
+        self.side_job = os.environ.get("TDFO_TT_SIDE_JOB", "1") != "0"
 
     # ------------------------------------------------------------ data in
     def load_batch(self, batch: Dict[str, torch.Tensor], eval_mode: bool = False) -> int:
@@ -343,12 +346,14 @@ class TwoTowerTrainer:
         ops.reduce_adam(self.part, ops.two_tower_parts(b), NPARAM, ops.TT_PART_LD, self.G, self.P,
                         self.M, self.V, self.hyper, wd=self.cfg.weight_decay, adamw=True,
                         loss_acc=self.loss_sum, logits=self.logits[:b], labels=self.labels[:b],
-                        nb=self.nbins, hist=self.train_hist)
+                        nb=self.nbins, hist=self.train_hist, defer=self.side_job)
         self._bumped = True
         try:
             self._emb_update(self.ids[: self.T * b], b, self.dX[:b])
         finally:
             self._bumped = False
+            if self.side_job:
+                ops.flush_side_job()
 
     def _step_local(self, b: int):
         if not self.mp and self.device.type == "cuda" and self.fused_step:

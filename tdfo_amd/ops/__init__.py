@@ -757,6 +757,12 @@ def two_tower_parts(B: int) -> int:
     return (B + ref.TT_SPB - 1) // ref.TT_SPB
 
 
+def flush_side_job():
+    """Launch a ``reduce_adam(defer=True)`` job no embedding backward took
+    (GPU callers only: deferral exists on the native path)."""
+    _native().flush_side_job()
+
+
 def two_tower(X, P, labels, inv_n, logits, dX=None, part=None, loss_scale=None, half=False,
               bumps=(), emb=None):
     """Fused TwoTower forward (+ BCE + backward when dX/part given).
@@ -784,15 +790,19 @@ def two_tower(X, P, labels, inv_n, logits, dX=None, part=None, loss_scale=None, 
 
 
 def reduce_adam(part, nparts, n, ld, grad, p, m, v, hyper, beta1=0.9, beta2=0.999, eps=1e-8,
-                wd=0.0, adamw=True, loss_acc=None, logits=None, labels=None, nb=0, hist=None):
+                wd=0.0, adamw=True, loss_acc=None, logits=None, labels=None, nb=0, hist=None,
+                defer=False):
     """grad[:n + 1] = fixed-order sum of ``nparts`` partial rows (stride ``ld``),
     one Adam(W) step of p[:n] from grad[:n] and loss_acc (fp64) += grad[n]:
     ``reduce_rows`` + ``dense_optimizer`` + the loss add in one launch; with
-    ``hist`` also ``auc_hist(logits, labels, nb, hist)`` (a block of its own)."""
+    ``hist`` also ``auc_hist(logits, labels, nb, hist)`` (a block of its own).
+    ``defer`` (GPU): run it as side blocks of the next ``embedding_bwd``'s
+    sort launch instead (it reads nothing that backward writes); call
+    ``flush_side_job()`` after that backward (launches it if none took it)."""
     if _gpu(part):
         _native().reduce_adam(part, int(nparts), int(n), int(ld), grad, p, m, v, hyper,
                               float(beta1), float(beta2), float(eps), float(wd), bool(adamw),
-                              loss_acc, logits, labels, int(nb), hist)
+                              loss_acc, logits, labels, int(nb), hist, bool(defer))
     else:
         if hist is not None:
             ref.auc_hist(logits, labels, nb, hist)

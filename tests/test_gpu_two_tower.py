@@ -68,14 +68,27 @@ def test_two_tower_trainer_gpu_matches_cpu(emb_update):
     assert abs(lg[0] - lc[0]) < 1e-3 and abs(lg[1] - lc[1]) < 1e-3
 
 
-@pytest.mark.parametrize("emb_update,B", [("sparse", 1000), ("sparse", 2048), ("dense", 512)])
-def test_two_tower_fused_step_bit_identical(emb_update, B):
-    """The six-launch step (AUC + counters inside the tower kernel,
-    reduce_adam) against the separate launches: same bits everywhere."""
+@pytest.mark.parametrize("emb_update,B,side", [("sparse", 1000, True), ("sparse", 2048, True),
+                                               ("sparse", 2048, False), ("dense", 512, True),
+                                               ("sparse", 4096, True), ("sparse", 2048, "radix")])
+def test_two_tower_fused_step_bit_identical(emb_update, B, side):
+    """The fused step (lookup + counters inside the tower kernel, reduce_adam
+    as side blocks of the embedding sort or on its own) against the separate
+    launches: same bits everywhere. "radix": the device-wide radix sort (no
+    sort launch to host the side job: it runs on its own)."""
     cfg = TwoTowerConfig(SM, learning_rate=3e-3, emb_update=emb_update, weight_decay=1e-2)
     a = TwoTowerTrainer(cfg, B, DEV)
     b = TwoTowerTrainer(cfg, B, DEV)
     a.fused_step, b.fused_step = True, False
+    a.side_job = bool(side)
+    prev = ops.embedding_segsort(0 if side == "radix" else -1)
+    try:
+        _run_pair(a, b, B)
+    finally:
+        ops.embedding_segsort(prev)
+
+
+def _run_pair(a, b, B):
     for i in range(10):
         x = {k: v.to(DEV) for k, v in make_batch(B, i).items()}
         a.load_batch(x)
