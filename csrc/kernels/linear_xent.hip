@@ -759,18 +759,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void xe
 }
 
 // dW/db += the active slabs (token blocks 1..nblk-1), fixed order.
-__global__ __launch_bounds__(256) void xent_slab_reduce_kernel(int64_t V,
-                                                               const int32_t* __restrict__ count,
-                                                               const float* __restrict__ slab,
-                                                               float* __restrict__ dW,
-                                                               float* __restrict__ db,
-                                                               LinearXentArgs xa) {
+// (thread g of G in all: element i = g, g + G, ...; the sums do not depend
+// on how the threads are grouped into blocks)
+__device__ __forceinline__ void xent_slab_reduce_body(int64_t V, const int32_t* __restrict__ count,
+                                                      const float* __restrict__ slab,
+                                                      float* __restrict__ dW,
+                                                      float* __restrict__ db,
+                                                      const LinearXentArgs& xa, int64_t g,
+                                                      int64_t G) {
   const int nblk = (*count + 16 * XG - 1) / (16 * XG);
   if (nblk <= 1) return;           // (the wgrad kernel holds the whole gradient)
   const XOpt xo = xopt_of(xa);
   const int64_t n4 = V * XE / 4;
-  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n4 + V;
-       i += (int64_t)gridDim.x * 256) {
+  for (int64_t i = g; i < n4 + V; i += G) {
     if (i < n4) {
       f32x4_t a = ((f32x4_t*)dW)[i];
       for (int k = 1; k < nblk; ++k)
@@ -798,6 +799,16 @@ __global__ __launch_bounds__(256) void xent_slab_reduce_kernel(int64_t V,
       }
     }
   }
+}
+
+__global__ __launch_bounds__(256) void xent_slab_reduce_kernel(int64_t V,
+                                                               const int32_t* __restrict__ count,
+                                                               const float* __restrict__ slab,
+                                                               float* __restrict__ dW,
+                                                               float* __restrict__ db,
+                                                               LinearXentArgs xa) {
+  xent_slab_reduce_body(V, count, slab, dW, db, xa, (int64_t)blockIdx.x * 256 + threadIdx.x,
+                        (int64_t)gridDim.x * 256);
 }
 
 }  // namespace
@@ -844,11 +855,10 @@ size_t linear_xent_workspace(int N, int64_t V) {
 // Mean loss over the valid tokens in fixed order (one block, fixed reduction
 // tree: deterministic), optionally accumulated into a device fp64 running sum
 // -- replaces the count / sum / clamp / divide / accumulate library ops.
-__global__ __launch_bounds__(1024) void xent_loss_kernel(const float* __restrict__ lossv, int N,
-                                                         const int32_t* __restrict__ count,
-                                                         float* __restrict__ loss,
-                                                         double* __restrict__ acc) {
-  __shared__ float red[16];
+__device__ __forceinline__ void xent_loss_body(const float* __restrict__ lossv, int N,
+                                               const int32_t* __restrict__ count,
+                                               float* __restrict__ loss, double* __restrict__ acc,
+                                               float* red) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   float v = 0.f;
   for (int i = tid; i < N; i += 1024) v += lossv[i];
@@ -864,6 +874,36 @@ __global__ __launch_bounds__(1024) void xent_loss_kernel(const float* __restrict
       if (acc) acc[0] += (double)L;
     }
   }
+}
+
+__global__ __launch_bounds__(1024) void xent_loss_kernel(const float* __restrict__ lossv, int N,
+                                                         const int32_t* __restrict__ count,
+                                                         float* __restrict__ loss,
+                                                         double* __restrict__ acc) {
+  __shared__ float red[16];
+  xent_loss_body(lossv, N, count, loss, acc, red);
+}
+
+// The step's tail in one launch: the wgrad slab sum (+ fused Adam) over the
+// first XT_SLAB_BLOCKS 1024-thread blocks -- the same 524,288 threads, so the
+// same per-element sums as xent_slab_reduce_kernel's 2048 x 256 -- and the
+// mean loss in the last block (xent_loss_kernel's 1024-thread tree). With at
+// most 128 valid tokens the slab part exits at once: the launch it would
+// have cost (Bert4Rec B=16: 4.6 us per step) is gone.
+constexpr int XT_SLAB_BLOCKS = 512;
+__global__ __launch_bounds__(1024) void xent_tail_kernel(int64_t V,
+                                                         const int32_t* __restrict__ count,
+                                                         const float* __restrict__ slab,
+                                                         float* __restrict__ dW,
+                                                         float* __restrict__ db,
+                                                         LinearXentArgs xa) {
+  __shared__ float red[16];
+  if (blockIdx.x == XT_SLAB_BLOCKS) {
+    xent_loss_body(xa.lossv, xa.N, count, xa.loss, xa.loss_acc, red);
+    return;
+  }
+  xent_slab_reduce_body(V, count, slab, dW, db, xa, (int64_t)blockIdx.x * 1024 + threadIdx.x,
+                        (int64_t)XT_SLAB_BLOCKS * 1024);
 }
 
 void linear_xent(const LinearXentArgs& a, hipStream_t s) {
@@ -903,6 +943,12 @@ void linear_xent(const LinearXentArgs& a, hipStream_t s) {
       hipLaunchKernelGGL(xent_wgrad_mfma_kernel,
                          dim3((unsigned)((tiles + tpw - 1) / tpw), blocks), dim3(64), 0, s, a.W,
                          a.bias, a.V, a.eps, tpw, htok, ytok, count, lse, a.dW, a.db, slab, a);
+      if (blocks > 1 && a.loss) {
+        hipLaunchKernelGGL(xent_tail_kernel, dim3(XT_SLAB_BLOCKS + 1), dim3(1024), 0, s, a.V,
+                           count, slab, a.dW, a.db, a);
+        TDFO_CHECK_HIP(hipGetLastError());
+        return;                     // (the loss is done too)
+      }
       if (blocks > 1)
         hipLaunchKernelGGL(xent_slab_reduce_kernel, dim3(2048), dim3(256), 0, s, a.V, count,
                            slab, a.dW, a.db, a);
