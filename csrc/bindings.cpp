@@ -1374,7 +1374,8 @@ void two_tower(const Tensor& X, const Tensor& P, const Tensor& labels, double in
   const int64_t B = X.size(0);
   TORCH_CHECK(X.scalar_type() == at::kFloat && X.size(1) >= 114 && X.stride(0) % 4 == 0 &&
               aligned16(X.data_ptr()), "two_tower: X fp32 [B, >=114], 16B-aligned rows");
-  TORCH_CHECK(P.scalar_type() == at::kFloat && P.numel() >= tdfo::TT_NPARAM, "two_tower: P");
+  TORCH_CHECK(P.scalar_type() == at::kFloat && P.numel() >= tdfo::TT_NPARAM &&
+              aligned16(P.data_ptr()), "two_tower: P fp32 [>= 2400], 16B-aligned");
   TORCH_CHECK(logits.scalar_type() == at::kFloat && logits.numel() == B, "two_tower: logits");
   tdfo::TwoTowerArgs a{};
   a.X = X.data_ptr<float>(); a.ldx = X.stride(0);

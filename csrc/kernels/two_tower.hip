@@ -79,11 +79,32 @@ __global__ __launch_bounds__(64 * NWV) void two_tower_kernel(TwoTowerArgs a) {
   __shared__ float Wl[NP];
   __shared__ float Xs[NWV][WS][XLD];
   __shared__ float Gs[TRAIN ? NWV : 1][G_N][E][WS];
-  __shared__ float Ps[TRAIN ? NWV : 1][NP];
+  __shared__ __attribute__((aligned(16))) float Ps[TRAIN ? NWV : 1][NP];
   __shared__ float red[NWV];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
   const int j = lane & 15, g = lane >> 4;          // sample column / feature group
-  for (int k = t; k < NP; k += 64 * NWV) Wl[k] = rnd<HALF>(a.P[k]);
+  {
+    // weights to LDS: every float4 load issued before the first store (a
+    // scalar strided loop waited on ~38 dependent loads per lane)
+    static_assert(NP % 4 == 0, "float4 weight staging");
+    constexpr int NV4 = NP / 4, PER = (NV4 + 64 * NWV - 1) / (64 * NWV);
+    float4 wv[PER];
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int k = t + 64 * NWV * i;
+      wv[i] = k < NV4 ? ((const float4*)a.P)[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int k = t + 64 * NWV * i;
+      if (k < NV4) {
+        Wl[4 * k] = rnd<HALF>(wv[i].x);
+        Wl[4 * k + 1] = rnd<HALF>(wv[i].y);
+        Wl[4 * k + 2] = rnd<HALF>(wv[i].z);
+        Wl[4 * k + 3] = rnd<HALF>(wv[i].w);
+      }
+    }
+  }
   const int64_t s0 = (int64_t)blockIdx.x * SPB + w * WS;
   float(*X)[XLD] = Xs[w];
   if (a.emb_w != nullptr) {
@@ -266,12 +287,15 @@ __global__ __launch_bounds__(64 * NWV) void two_tower_kernel(TwoTowerArgs a) {
     if (lane == 0) red[w] = lw;
     __syncthreads();
     // block partial: fixed wave order
-    float* prow = a.part + (int64_t)blockIdx.x * TT_PART_LD;
-    for (int k = t; k < NP; k += 64 * NWV) {
-      float v = Ps[0][k];
+    float* prow = a.part + (int64_t)blockIdx.x * TT_PART_LD;   // (TT_PART_LD % 4 == 0)
+    for (int k = t; k < NP / 4; k += 64 * NWV) {
+      float4 v = *(const float4*)&Ps[0][4 * k];
 #pragma unroll
-      for (int q = 1; q < NWV; ++q) v += Ps[q][k];
-      prow[k] = v;
+      for (int q = 1; q < NWV; ++q) {
+        const float4 u = *(const float4*)&Ps[q][4 * k];
+        v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+      }
+      *(float4*)(prow + 4 * k) = v;
     }
     if (t == 0) {
       float l = 0.f;
