@@ -819,6 +819,10 @@ void set_emb_ws(tdfo::EmbBwdArgs& a, const Tensor& work) {
 // side), flush_side_job() launches a still-parked one on its own.
 thread_local bool g_side_pending = false;
 thread_local tdfo::ReduceAdamArgs g_side{};
+// two_tower(defer=true): the tower step parked the same way; the next
+// embedding_bwd co-launches it with its per-table sort (or launches it first)
+thread_local bool g_tower_pending = false;
+thread_local tdfo::TwoTowerArgs g_tower{};
 
 void embedding_bwd(const Tensor& W, const Tensor& row_offset, const Tensor& indices,
                    const Tensor& offsets, const Tensor& grad_off,
@@ -838,6 +842,11 @@ void embedding_bwd(const Tensor& W, const Tensor& row_offset, const Tensor& indi
     a.side = g_side;
     a.side_on = 1;
     g_side_pending = false;
+  }
+  if (g_tower_pending) {
+    a.tower = g_tower;
+    a.tower_on = 1;
+    g_tower_pending = false;
   }
   tdfo::embedding_bwd_fused(a, cur_stream());
 }
@@ -1369,7 +1378,8 @@ void two_tower(const Tensor& X, const Tensor& P, const Tensor& labels, double in
                const Tensor& logits, const c10::optional<Tensor>& dX,
                const c10::optional<Tensor>& part, const c10::optional<Tensor>& loss_scale,
                bool half, at::TensorList bumps, const c10::optional<Tensor>& emb_w,
-               const c10::optional<Tensor>& ids, const c10::optional<Tensor>& row_off) {
+               const c10::optional<Tensor>& ids, const c10::optional<Tensor>& row_off,
+               bool defer) {
   check_dev(X, "X"); check_2d_rowmajor(X, "X");
   const int64_t B = X.size(0);
   TORCH_CHECK(X.scalar_type() == at::kFloat && X.size(1) >= 114 && X.stride(0) % 4 == 0 &&
@@ -1426,6 +1436,14 @@ void two_tower(const Tensor& X, const Tensor& P, const Tensor& labels, double in
   } else {
     TORCH_CHECK(bumps.size() == 0, "two_tower: bumps are a train-step option");
   }
+  if (defer) {
+    TORCH_CHECK(train && !half && !g_tower_pending && !g_side_pending,
+                "two_tower(defer): an fp32 train step, parked before its reduce_adam, one at "
+                "a time (flush_side_job)");
+    g_tower = a;
+    g_tower_pending = true;
+    return;
+  }
   tdfo::two_tower(a, train ? 1 : 0, cur_stream());
 }
 
@@ -1471,6 +1489,10 @@ void reduce_adam(const Tensor& part, int64_t nparts, int64_t n, int64_t ld, cons
 }
 
 void flush_side_job() {
+  if (g_tower_pending) {             // (before the reduce: it reads the towers' partials)
+    g_tower_pending = false;
+    tdfo::two_tower(g_tower, 1, cur_stream());
+  }
   if (!g_side_pending) return;
   g_side_pending = false;
   tdfo::reduce_adam(g_side, cur_stream());
@@ -1778,7 +1800,7 @@ TORCH_LIBRARY(tdfo, m) {
   m.def("jagged_ids_to_dense(Tensor values, Tensor offsets, int pad, Tensor(a!) out) -> ()");
   m.def("two_tower(Tensor X, Tensor P, Tensor labels, float inv_n, Tensor(a!) logits, "
         "Tensor(b!)? dX, Tensor(c!)? part, Tensor? loss_scale, bool half, "
-        "Tensor(d!)[] bumps, Tensor? emb_w, Tensor? ids, Tensor? row_off) -> ()");
+        "Tensor(d!)[] bumps, Tensor? emb_w, Tensor? ids, Tensor? row_off, bool defer) -> ()");
   m.def("reduce_adam(Tensor part, int nparts, int n, int ld, Tensor(a!) grad, Tensor(b!) p, "
         "Tensor(c!) m, Tensor(d!) v, Tensor hyper, float beta1, float beta2, float eps, "
         "float wd, bool adamw, Tensor(e!) loss_acc, Tensor? logits, Tensor? labels, int nb, "

@@ -129,6 +129,35 @@ void embedding_bag_fwd(const EmbFwdArgs& a, hipStream_t s);
 //   4. the optimizer is applied once per unique row.
 enum EmbOpt { EMB_SGD = 0, EMB_ROWWISE_ADAGRAD = 1, EMB_ADAM = 2,
               EMB_ADAGRAD = 3, EMB_DENSE_GRAD = 4 };
+struct HeadBumps { float* p[4]; int n; };
+
+// ------------------------------------------------------- two-tower ----
+// Fused TwoTower step (two_tower.hip). X: [B, ldx] fp32 with the user
+// embedding at cols [0,16) and the 98-wide item-tower input at [16,114).
+// P: 2400 flat params. train=1 also writes dX (embedding grads, cols [0,112))
+// and part[block][TT_PART_LD] = [dP (2400) | loss_sum].
+constexpr int TT_NPARAM = 2400;
+constexpr int TT_PART_LD = 2432;
+struct TwoTowerArgs {
+  const float* X; int64_t ldx;
+  const float* P;
+  const float* labels; float inv_n;
+  const float* loss_scale;  // device scalar multiplying dlogit (dynamic loss scaling) or null
+  int half;                 // fp16 compute: inputs, weights, activations and gradients
+                            // rounded to fp16 at every layer boundary, fp32 accumulation
+  int B;
+  float* logits;
+  float* dX; int64_t lddx;
+  float* part;
+  // optional (train): step counters bumped by block 0 (no bump launch)
+  HeadBumps bumps{};
+  // optional: the 7 embedding rows of every sample gathered here from the
+  // table (emb_w [rows, 16] fp32, ids table-major ids[t * B + s], row_off[t])
+  // instead of read from X[:, :112] -- the lookup launch folded in; X then
+  // supplies only the two dense features (columns 112, 113)
+  const float* emb_w = nullptr; const int64_t* ids = nullptr; const int64_t* row_off = nullptr;
+};
+
 // reduce_adam's arguments (declared with it below, in the loss section)
 constexpr int REDUCE_ADAM_MAX_NB = 512;
 struct ReduceAdamArgs {
@@ -167,10 +196,18 @@ struct EmbBwdArgs {
   const int32_t* bag_len;
   // optional side job (side_on): a reduce_adam run by extra blocks of the
   // one-hot per-table sort launch, beside the sort (it needs nothing the
-  // backward touches); run as its own launch first where no such sort runs.
-  // TwoTower: the dense step hidden behind the 7-block sort.
+  // backward touches) -- or, when that launch carries the towers whose
+  // partials it reads (tower_on), by extra blocks of the update launch (the
+  // in-kernel-combine variant); run as its own launch where neither can.
+  // TwoTower: the dense step hidden behind the sort / update.
   ReduceAdamArgs side{};
   int side_on = 0;
+  // optional co-launched tower step (tower_on): the fused TwoTower
+  // forward + backward run by extra blocks of the per-table sort launch
+  // (one-hot, <= 2048 ids per table), else as its own launch before the sort
+  TwoTowerArgs tower{};
+  int tower_on = 0;
+  int side_block0 = 0;         // internal: first side block of the update launch
 };
 size_t embedding_bwd_workspace(int64_t nnz, int D);
 // One-hot batches (nnz == T*B, B <= 8192): per-table LDS sort in one launch
@@ -340,8 +377,8 @@ void head_bce(const uint16_t* H, int64_t ldh, int B, int K, const float* w,
               int nparts, hipStream_t s);
 int head_bce_parts(int B);
 // grad[0..K] = sum over parts of part[:, 0..K]; loss_acc[0] += sum part[:, K+1];
-// bump.p[i][1] += 1 for each step counter (fp32 [lr, step, ...] hyper vectors).
-struct HeadBumps { float* p[4]; int n; };
+// bump.p[i][1] += 1 for each step counter (fp32 [lr, step, ...] hyper vectors;
+// HeadBumps: above EmbBwdArgs).
 void head_reduce(const float* part, int nparts, int K, float* grad, float* loss_acc,
                  const HeadBumps& bumps, hipStream_t s);
 // grad[j] = sum_r part[r * ld + j] for j < n (head_reduce's / reduce_rows'
@@ -373,32 +410,7 @@ int colsum_parts(int M);
 void auc_hist(const float* logits, const float* labels, int n, int nb,
               unsigned long long* hist, hipStream_t s);
 
-// ------------------------------------------------------- two-tower ----
-// Fused TwoTower step (two_tower.hip). X: [B, ldx] fp32 with the user
-// embedding at cols [0,16) and the 98-wide item-tower input at [16,114).
-// P: 2400 flat params. train=1 also writes dX (embedding grads, cols [0,112))
-// and part[block][TT_PART_LD] = [dP (2400) | loss_sum].
-constexpr int TT_NPARAM = 2400;
-constexpr int TT_PART_LD = 2432;
-struct TwoTowerArgs {
-  const float* X; int64_t ldx;
-  const float* P;
-  const float* labels; float inv_n;
-  const float* loss_scale;  // device scalar multiplying dlogit (dynamic loss scaling) or null
-  int half;                 // fp16 compute: inputs, weights, activations and gradients
-                            // rounded to fp16 at every layer boundary, fp32 accumulation
-  int B;
-  float* logits;
-  float* dX; int64_t lddx;
-  float* part;
-  // optional (train): step counters bumped by block 0 (no bump launch)
-  HeadBumps bumps{};
-  // optional: the 7 embedding rows of every sample gathered here from the
-  // table (emb_w [rows, 16] fp32, ids table-major ids[t * B + s], row_off[t])
-  // instead of read from X[:, :112] -- the lookup launch folded in; X then
-  // supplies only the two dense features (columns 112, 113)
-  const float* emb_w = nullptr; const int64_t* ids = nullptr; const int64_t* row_off = nullptr;
-};
+
 int two_tower_parts(int B);
 void two_tower(const TwoTowerArgs& a, int train, hipStream_t s);
 

@@ -27,6 +27,7 @@
 #include "tdfo_common.h"
 #include "tdfo_kernels.h"
 #include "tdfo_reduce_adam.h"
+#include "tdfo_two_tower_dev.h"
 
 namespace tdfo {
 namespace {
@@ -410,28 +411,30 @@ __device__ __forceinline__ void seg_run_meta(const uint32_t* skey, int n, int64_
   }
 }
 
-template <typename K, bool SORTED_G, int SK = SEG_K>
-__global__ __launch_bounds__(SEG_THREADS) void emb_segsort_kernel(
-    const EmbBwdArgs a, K* __restrict__ keys_out, int32_t* __restrict__ vals_out,
+// LDS of one per-table sort block
+template <int SK>
+struct SegSmem {
+  uint32_t skey[SK * SEG_THREADS];
+  uint32_t sval[SK * SEG_THREADS];
+  uint32_t cnt[SK * SEG_WAVES * (SEG_BINS + 1)];
+  uint32_t wsum[SEG_WAVES];
+  uint32_t smax[SEG_WAVES];
+};
+
+// Sort of virtual table t by one 1024-thread block (the body of
+// emb_segsort_kernel, also run by the sort blocks of the tower co-launch)
+template <typename K, bool SORTED_G, int SK>
+__device__ __forceinline__ void segsort_table(
+    const EmbBwdArgs& a, int t, K* __restrict__ keys_out, int32_t* __restrict__ vals_out,
     int64_t* __restrict__ goff, float* __restrict__ gscale, int32_t* __restrict__ tail_count,
-    int32_t* __restrict__ pos, int2* __restrict__ meta = nullptr,
-    int32_t* __restrict__ rcnt = nullptr, int meta_ch = 0) {
-  __shared__ uint32_t skey[SK * SEG_THREADS];
-  __shared__ uint32_t sval[SK * SEG_THREADS];
-  __shared__ uint32_t cnt[SK * SEG_WAVES * (SEG_BINS + 1)];
-  __shared__ uint32_t wsum[SEG_WAVES];
-  __shared__ uint32_t smax[SEG_WAVES];
-  const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  if (t >= a.T) {
-    // side blocks (a.side_on): four 256-thread reduce_adam units each, in the
-    // sort's LDS (units take 256 floats of skey each; the one AUC unit sval)
-    static_assert(SK * SEG_THREADS >= 4 * RA_PH * RA_COLS &&
-                  SK * SEG_THREADS >= 2 * REDUCE_ADAM_MAX_NB, "side-job LDS");
-    const int slice = tid >> 8;
-    reduce_adam_unit(a.side, (t - a.T) * (SEG_THREADS / 256) + slice, tid & 255,
-                     (float(*)[RA_COLS])(skey + slice * RA_PH * RA_COLS), sval);
-    return;
-  }
+    int32_t* __restrict__ pos, int2* __restrict__ meta, int32_t* __restrict__ rcnt,
+    int meta_ch, SegSmem<SK>& sm) {
+  uint32_t* skey = sm.skey;
+  uint32_t* sval = sm.sval;
+  uint32_t* cnt = sm.cnt;
+  uint32_t* wsum = sm.wsum;
+  uint32_t* smax = sm.smax;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   if (t == 0 && tid == 0) {                         // read by later kernels
     tail_count[0] = 0;
     tail_count[1] = 0;
@@ -485,6 +488,58 @@ __global__ __launch_bounds__(SEG_THREADS) void emb_segsort_kernel(
         if (gscale) gscale[s0 + i] = a.psw ? a.psw[s0 + val[k]] : 1.f;
       }
     }
+  }
+}
+
+template <typename K, bool SORTED_G, int SK = SEG_K>
+__global__ __launch_bounds__(SEG_THREADS) void emb_segsort_kernel(
+    const EmbBwdArgs a, K* __restrict__ keys_out, int32_t* __restrict__ vals_out,
+    int64_t* __restrict__ goff, float* __restrict__ gscale, int32_t* __restrict__ tail_count,
+    int32_t* __restrict__ pos, int2* __restrict__ meta = nullptr,
+    int32_t* __restrict__ rcnt = nullptr, int meta_ch = 0) {
+  __shared__ SegSmem<SK> sm;
+  const int t = blockIdx.x, tid = threadIdx.x;
+  if (t >= a.T) {
+    // side blocks (a.side_on): four 256-thread reduce_adam units each, in the
+    // sort's LDS (units take 256 floats of skey each; the one AUC unit sval)
+    static_assert(SK * SEG_THREADS >= 4 * RA_PH * RA_COLS &&
+                  SK * SEG_THREADS >= 2 * REDUCE_ADAM_MAX_NB, "side-job LDS");
+    const int slice = tid >> 8;
+    reduce_adam_unit(a.side, (t - a.T) * (SEG_THREADS / 256) + slice, tid & 255,
+                     (float(*)[RA_COLS])(sm.skey + slice * RA_PH * RA_COLS), sm.sval);
+    return;
+  }
+  segsort_table<K, SORTED_G, SK>(a, t, keys_out, vals_out, goff, gscale, tail_count, pos, meta,
+                                 rcnt, meta_ch, sm);
+}
+
+// TwoTower co-launch (a.tower_on): the per-table sorts of a one-hot batch of
+// <= 2048 ids (blocks [0, T)) beside the fused tower step (blocks [T, ...):
+// TT_CO_WAVES tower waves each, every wave writing its own partial row --
+// the rows of the one-wave tower kernel, so the same bits). The sort needs
+// only the ids, the towers nothing the sort writes: one launch instead of
+// two dependent ones. The block's other waves pass the towers' barriers
+// and leave.
+constexpr int TT_CO_WAVES = 4;
+template <typename K>
+__global__ __launch_bounds__(SEG_THREADS) void emb_segsort_tower_kernel(
+    const EmbBwdArgs a, K* __restrict__ keys_out, int32_t* __restrict__ vals_out,
+    int64_t* __restrict__ goff, float* __restrict__ gscale, int32_t* __restrict__ tail_count,
+    int2* __restrict__ meta, int32_t* __restrict__ rcnt, int meta_ch) {
+  __shared__ SegSmem<2> sm;
+  __shared__ tt::Smem<TT_CO_WAVES> tsm;
+  static_assert(sizeof(SegSmem<2>) + sizeof(tt::Smem<TT_CO_WAVES>) <= 160 * 1024, "LDS");
+  const int t = blockIdx.x;
+  if (t < a.T) {
+    segsort_table<K, true, 2>(a, t, keys_out, vals_out, goff, gscale, tail_count, nullptr, meta,
+                              rcnt, meta_ch, sm);
+    return;
+  }
+  if (threadIdx.x < 64 * TT_CO_WAVES) {
+    tt::tower_block<true, false, TT_CO_WAVES, true>(a.tower, t - a.T, threadIdx.x, tsm);
+  } else {
+#pragma unroll
+    for (int i = 0; i < tt::tower_barriers<true>(); ++i) __syncthreads();
   }
 }
 
@@ -958,10 +1013,23 @@ __global__ __launch_bounds__(256) void emb_chunk_kernel(
   constexpr int EPL = BwdCfg<D>::EPL;
   constexpr bool NEED_W = OPT != EMB_DENSE_GRAD;
   const int lane = threadIdx.x & 63;
+  int nblk = gridDim.x;
+  if constexpr (META) {
+    // side blocks (a.side_block0 > 0): one reduce_adam unit each
+    if (a.side_block0 > 0) {
+      if ((int)blockIdx.x >= a.side_block0) {
+        __shared__ float sred[RA_PH][RA_COLS];
+        __shared__ unsigned int slh[2 * REDUCE_ADAM_MAX_NB];
+        reduce_adam_unit(a.side, blockIdx.x - a.side_block0, threadIdx.x, sred, slh);
+        return;
+      }
+      nblk = a.side_block0;
+    }
+  }
   if (skip_step(a)) return;
   const OptScalars o = opt_scalars(a);
   const int64_t nch = (a.nnz + CH - 1) / CH;
-  const int64_t nwv = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int64_t nwv = ((int64_t)nblk * blockDim.x) >> 6;
   // one wave per chunk (grid-stride: any grid size walks every chunk)
   for (int64_t c = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; c < nch; c += nwv) {
   const int64_t start = c * CH;
@@ -1403,8 +1471,14 @@ bool meta_path(const EmbBwdArgs& a) {
          a.B % ch_for(a.D) == 0 && !(g_emb_seg_split && a.B > 2 * SEG_THREADS);
 }
 
+// What a prepare did with the optional co-launched work: the towers are
+// always done by its end; the side job (reduce_adam) is done unless the
+// towers rode in the sort launch (it reads their partials: then the update
+// launch takes it).
+struct PrepDone { bool side = false; };
+
 template <typename K>
-void prep_impl(const EmbBwdArgs& a, const WsLayout& L, hipStream_t s) {
+PrepDone prep_impl(const EmbBwdArgs& a, const WsLayout& L, hipStream_t s) {
   char* ws = (char*)a.workspace;
   K* keys_in = (K*)(ws + L.keys_in);
   K* keys_out = (K*)(ws + L.keys_out);
@@ -1415,6 +1489,18 @@ void prep_impl(const EmbBwdArgs& a, const WsLayout& L, hipStream_t s) {
   int32_t* tcount = (int32_t*)(ws + L.tcount);
   const int R = a.segsort;                 // runs per physical table (0: off)
   bool side_done = false;
+  const bool co_tower = a.tower_on && a.tower.B > 0 && onehot_path(a) && R == 1 &&
+                        a.B <= 2 * SEG_THREADS;
+  if (a.tower_on && !co_tower) two_tower(a.tower, 1, s);   // first: the backward needs dX
+  if (co_tower) {
+    int2* meta = meta_path(a) ? (int2*)(ws + L.meta) : nullptr;
+    int32_t* rcnt = (int32_t*)(ws + L.rcnt);
+    const int tblocks = (two_tower_parts(a.tower.B) + TT_CO_WAVES - 1) / TT_CO_WAVES;
+    hipLaunchKernelGGL((emb_segsort_tower_kernel<K>), dim3(a.T + tblocks), dim3(SEG_THREADS), 0,
+                       s, a, keys_out, vals_out, goff, gscale, tcount, meta, rcnt, ch_for(a.D));
+    TDFO_CHECK_HIP(hipGetLastError());
+    return PrepDone{false};
+  }
   if (onehot_path(a)) {
     if (R == 1) {
       int2* meta = meta_path(a) ? (int2*)(ws + L.meta) : nullptr;
@@ -1472,6 +1558,7 @@ void prep_impl(const EmbBwdArgs& a, const WsLayout& L, hipStream_t s) {
   }
   TDFO_CHECK_HIP(hipGetLastError());
   if (a.side_on && !side_done) reduce_adam(a.side, s);     // no sort launch to ride in
+  return PrepDone{true};
 }
 
 template <int D, typename K, int OPT>
@@ -1493,6 +1580,15 @@ void apply_impl(const EmbBwdArgs& a0, const WsLayout& L, hipStream_t s) {
     constexpr int CH = decltype(ch_c)::value;
     const int64_t nch = (a.nnz + CH - 1) / CH;
     int64_t blocks = (nch + 3) / 4;
+    // side job (reduce_adam) left by the prepare: extra blocks of the
+    // in-kernel-combine update launch, one 256-thread unit each
+    const bool side_here = a.side_on && meta != nullptr;
+    if (side_here) {
+      a.side_block0 = (int)blocks;
+      blocks += reduce_adam_units(a.side);
+    } else {
+      a.side_block0 = 0;
+    }
 #define TDFO_CK(GBV, MV)                                                                   \
     hipLaunchKernelGGL((emb_chunk_kernel<D, K, GBV, OPT, CH, MV>), dim3(blocks), dim3(256), 0, s, \
                        a, keys_out, vals_out, goff, gscale, head, tail, tlist, tcount, meta, rcnt)
@@ -1503,6 +1599,7 @@ void apply_impl(const EmbBwdArgs& a0, const WsLayout& L, hipStream_t s) {
     }
 #undef TDFO_CK
     TDFO_CHECK_HIP(hipGetLastError());
+    if (a.side_on && !side_here) reduce_adam(a.side, s);
     if (meta != nullptr) return;        // crossing runs finished inside the update
     int64_t cblocks = (nch + 3) / 4;
     if (cblocks > 1024) cblocks = 1024;
@@ -1603,19 +1700,30 @@ size_t embedding_bwd_workspace(int64_t nnz, int D) {
   return ws_layout(nnz < 1 ? 1 : nnz, D).total;
 }
 
+namespace {
+PrepDone prepare_any(const EmbBwdArgs& a, hipStream_t s) {
+  if (a.nnz <= 0) {
+    if (a.tower_on) two_tower(a.tower, 1, s);
+    if (a.side_on) reduce_adam(a.side, s);
+    return PrepDone{true};
+  }
+  const WsLayout L = ws_layout(a.nnz, a.D);
+  if (a.key_bits <= 32) return prep_impl<uint32_t>(a, L, s);
+  return prep_impl<uint64_t>(a, L, s);
+}
+}  // namespace
+
 void embedding_bwd_fused(const EmbBwdArgs& a, hipStream_t s) {
-  embedding_bwd_prepare(a, s);
-  embedding_bwd_apply(a, s);
+  const PrepDone d = prepare_any(a, s);
+  EmbBwdArgs b = a;
+  b.tower_on = 0;
+  if (d.side) b.side_on = 0;         // else the update launch takes it
+  embedding_bwd_apply(b, s);
 }
 
 void embedding_bwd_prepare(const EmbBwdArgs& a, hipStream_t s) {
-  if (a.nnz <= 0) {
-    if (a.side_on) reduce_adam(a.side, s);
-    return;
-  }
-  const WsLayout L = ws_layout(a.nnz, a.D);
-  if (a.key_bits <= 32) prep_impl<uint32_t>(a, L, s);
-  else prep_impl<uint64_t>(a, L, s);
+  const PrepDone d = prepare_any(a, s);
+  if (!d.side && a.side_on) reduce_adam(a.side, s);   // (split API: nothing carried over)
 }
 
 template <typename K>
@@ -1671,7 +1779,10 @@ void embedding_dense_update(const EmbBwdArgs& a, int64_t rows, const float* grad
 }
 
 void embedding_bwd_apply(const EmbBwdArgs& a, hipStream_t s) {
-  if (a.nnz <= 0) return;
+  if (a.nnz <= 0) {
+    if (a.side_on) reduce_adam(a.side, s);
+    return;
+  }
   const WsLayout L = ws_layout(a.nnz, a.D);
   switch (a.D) {
     case 16: bwd_dispatch<16>(a, L, s); break;

@@ -193,6 +193,9 @@ class TwoTowerTrainer:
         # ... with the dense step (reduce_adam) run by side blocks of the
         # embedding sort launch
         self.side_job = os.environ.get("TDFO_TT_SIDE_JOB", "1") != "0"
+        # ... and the tower kernel co-launched with the per-table id sort
+        # (both need only this step's inputs)
+        self.colaunch = os.environ.get("TDFO_TT_COLAUNCH", "1") != "0"
 
     # ------------------------------------------------------------ data in
     def load_batch(self, batch: Dict[str, torch.Tensor], eval_mode: bool = False) -> int:
@@ -333,16 +336,18 @@ class TwoTowerTrainer:
                                 found_inf=self.found_inf if self.mp else None)
 
     def _step_local_fused(self, b: int):
-        """The one-GPU fp32 step in four launches: towers + BCE + backward
-        with the embedding rows gathered in-kernel and both step counters
-        bumped; the partial rows' reduction + AdamW + loss add + AUC histogram
-        (``reduce_adam``); the embedding sort and update (crossing runs
-        finished in-kernel for small batches). Bit-identical to the unfused
+        """The one-GPU fp32 step in two launches: the towers + BCE + backward
+        (embedding rows gathered in-kernel, both step counters bumped) beside
+        the per-table id sort; then the sparse Adam update (crossing runs
+        finished in-kernel for small batches) beside the partial rows'
+        reduction + AdamW + loss add + AUC histogram (``reduce_adam``).
+        (``side_job`` / ``colaunch`` off: those as launches of their own.) Bit-identical to the unfused
         sequence (``TDFO_TT_FUSED=0``: + the lookup, reduce_rows, auc_hist,
         bump, dense_optimizer and the loss add as launches of their own)."""
         ops.two_tower(self.X[:b], self.P, self.labels[:b], 1.0 / b, self.logits[:b], self.dX[:b],
                       self.part, bumps=[self.hyper, self.emb_hyper],
-                      emb=(self.emb.weight, self.ids[: self.T * b], self.emb.row_offset))
+                      emb=(self.emb.weight, self.ids[: self.T * b], self.emb.row_offset),
+                      defer=self.side_job and self.colaunch)
         ops.reduce_adam(self.part, ops.two_tower_parts(b), NPARAM, ops.TT_PART_LD, self.G, self.P,
                         self.M, self.V, self.hyper, wd=self.cfg.weight_decay, adamw=True,
                         loss_acc=self.loss_sum, logits=self.logits[:b], labels=self.labels[:b],

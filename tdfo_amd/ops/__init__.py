@@ -758,25 +758,28 @@ def two_tower_parts(B: int) -> int:
 
 
 def flush_side_job():
-    """Launch a ``reduce_adam(defer=True)`` job no embedding backward took
-    (GPU callers only: deferral exists on the native path)."""
+    """Launch a ``two_tower(defer=True)`` / ``reduce_adam(defer=True)`` job no
+    embedding backward took (GPU callers only: deferral exists on the native
+    path)."""
     _native().flush_side_job()
 
 
 def two_tower(X, P, labels, inv_n, logits, dX=None, part=None, loss_scale=None, half=False,
-              bumps=(), emb=None):
+              bumps=(), emb=None, defer=False):
     """Fused TwoTower forward (+ BCE + backward when dX/part given).
     ``half``: fp16 compute (mixed precision); ``loss_scale``: device scalar
     multiplying the loss gradient (dynamic loss scaling). ``bumps`` (train):
     step counters ([lr, step, ...]) advanced by one inside the launch.
     ``emb = (weight [rows, 16], ids [7 * B] table-major, row_offset [7])``:
     the kernel gathers X[:, :112] itself (X then holds only the two dense
-    features) -- the lookup launch folded in."""
+    features) -- the lookup launch folded in. ``defer`` (GPU, fp32 train
+    step): co-launched with the next ``embedding_bwd``'s per-table sort (or
+    launched first by it); ``flush_side_job()`` after that backward."""
     bumps = list(bumps)
     if _gpu(X):
         w, ids, ro = emb if emb is not None else (None, None, None)
         _native().two_tower(X, P, labels, float(inv_n), logits, dX, part, loss_scale, bool(half),
-                            bumps, w, ids, ro)
+                            bumps, w, ids, ro, bool(defer))
     else:
         if emb is not None:
             w, ids, ro = emb

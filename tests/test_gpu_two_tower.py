@@ -68,20 +68,23 @@ def test_two_tower_trainer_gpu_matches_cpu(emb_update):
     assert abs(lg[0] - lc[0]) < 1e-3 and abs(lg[1] - lc[1]) < 1e-3
 
 
-@pytest.mark.parametrize("emb_update,B,side", [("sparse", 1000, True), ("sparse", 2048, True),
-                                               ("sparse", 2048, False), ("dense", 512, True),
-                                               ("sparse", 4096, True), ("sparse", 2048, "radix")])
-def test_two_tower_fused_step_bit_identical(emb_update, B, side):
-    """The fused step (lookup + counters inside the tower kernel, reduce_adam
-    as side blocks of the embedding sort or on its own) against the separate
-    launches: same bits everywhere. "radix": the device-wide radix sort (no
-    sort launch to host the side job: it runs on its own)."""
+@pytest.mark.parametrize("emb_update,B,mode", [
+    ("sparse", 2048, "colaunch"), ("sparse", 1000, "colaunch"), ("sparse", 320, "colaunch"),
+    ("sparse", 4096, "colaunch"), ("dense", 512, "colaunch"), ("sparse", 2048, "radix"),
+    ("sparse", 2048, "side"), ("sparse", 1000, "side"), ("sparse", 2048, "plain")])
+def test_two_tower_fused_step_bit_identical(emb_update, B, mode):
+    """The fused step against the separate launches: same bits everywhere.
+    colaunch: towers beside the per-table sort, reduce_adam beside the update
+    (B = 1000: no in-kernel-combine update, so on its own; 4096: the larger
+    sort, towers first); side: towers on their own, reduce_adam beside the
+    sort; plain: neither; radix: the device-wide sort (nothing co-launched)."""
     cfg = TwoTowerConfig(SM, learning_rate=3e-3, emb_update=emb_update, weight_decay=1e-2)
     a = TwoTowerTrainer(cfg, B, DEV)
     b = TwoTowerTrainer(cfg, B, DEV)
     a.fused_step, b.fused_step = True, False
-    a.side_job = bool(side)
-    prev = ops.embedding_segsort(0 if side == "radix" else -1)
+    a.side_job = mode in ("colaunch", "side", "radix")
+    a.colaunch = mode in ("colaunch", "radix")
+    prev = ops.embedding_segsort(0 if mode == "radix" else -1)
     try:
         _run_pair(a, b, B)
     finally:
