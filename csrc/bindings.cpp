@@ -968,7 +968,9 @@ bool bottom_mlp_fwd_ok(int64_t k0, int64_t n0, int64_t n1, int64_t n2) {
 void bottom_mlp_fwd(const Tensor& x, const Tensor& w0, const Tensor& w1, const Tensor& w2,
                     const c10::optional<Tensor>& b0, const c10::optional<Tensor>& b1,
                     const c10::optional<Tensor>& b2, const Tensor& y0, const Tensor& y1,
-                    const Tensor& y2) {
+                    const Tensor& y2, const c10::optional<Tensor>& dense,
+                    const c10::optional<Tensor>& label_src,
+                    const c10::optional<Tensor>& label_dst) {
   const Tensor* ts[7] = {&x, &w0, &w1, &w2, &y0, &y1, &y2};
   const char* nm[7] = {"x", "w0", "w1", "w2", "y0", "y1", "y2"};
   for (int i = 0; i < 7; ++i) {
@@ -1006,6 +1008,22 @@ void bottom_mlp_fwd(const Tensor& x, const Tensor& w0, const Tensor& w1, const T
   a.y0 = bf16_mut(y0); a.y1 = bf16_mut(y1); a.y2 = bf16_mut(y2);
   a.ldy0 = y0.stride(0); a.ldy1 = y1.stride(0); a.ldy2 = y2.stride(0);
   a.M = (int)M;
+  if (dense) {
+    check_dev(*dense, "dense");
+    TORCH_CHECK(dense->scalar_type() == at::kFloat && dense->dim() == 2 && dense->size(0) == M &&
+                dense->stride(1) == 1 && dense->size(1) <= 16 && dense->size(1) < x.size(1),
+                "bottom_mlp_fwd: dense fp32 [M, nd < 16] rows");
+    a.dense = dense->data_ptr<float>(); a.ld_dense = dense->stride(0);
+    a.nd = (int)dense->size(1);
+    a.x_out = bf16_mut(x);
+    if (label_src) {
+      TORCH_CHECK(label_dst && label_src->scalar_type() == at::kFloat &&
+                  label_dst->scalar_type() == at::kFloat && label_src->is_contiguous() &&
+                  label_dst->is_contiguous() && label_src->numel() >= M &&
+                  label_dst->numel() >= M, "bottom_mlp_fwd: labels fp32 [M]");
+      a.label_src = label_src->data_ptr<float>(); a.label_dst = label_dst->data_ptr<float>();
+    }
+  }
   tdfo::bottom_mlp_fwd(a, cur_stream());
 }
 
@@ -1758,7 +1776,8 @@ TORCH_LIBRARY(tdfo, m) {
   m.def("rw_rows_gather(Tensor Wt, Tensor recv, int W, int cap, Tensor(a!) out) -> ()");
   m.def("bottom_mlp_fwd_ok(int k0, int n0, int n1, int n2) -> bool", bottom_mlp_fwd_ok);
   m.def("bottom_mlp_fwd(Tensor x, Tensor w0, Tensor w1, Tensor w2, Tensor? b0, Tensor? b1, "
-        "Tensor? b2, Tensor(a!) y0, Tensor(b!) y1, Tensor(c!) y2) -> ()");
+        "Tensor? b2, Tensor(a!) y0, Tensor(b!) y1, Tensor(c!) y2, Tensor? dense, Tensor? label_src, "
+        "Tensor(d!)? label_dst) -> ()");
   m.def("rw_rows_scatter(Tensor send, int W, int cap, int B, int D, Tensor rows, Tensor(a!) region, "
         "int ld, Tensor(b!) map, int nrw) -> ()");
   m.def("rw_grads_gather(Tensor map, int W, int cap, int D, Tensor dregion, Tensor(a!) gsend) -> ()");

@@ -269,6 +269,13 @@ struct BotMlpArgs {
   uint16_t* y0; uint16_t* y1; uint16_t* y2;
   int64_t ldy0, ldy1, ldy2;
   int M;
+  // optional batch load folded in (dense != nullptr): columns [0, nd) of the
+  // input come from fp32 dense[M][ld_dense], converted as batch_load does and
+  // written back to x (x_out, the same buffer: the backward's weight grad
+  // reads it); each block also copies its rows' labels label_src -> label_dst
+  const float* dense = nullptr; int64_t ld_dense = 0; int nd = 0;
+  uint16_t* x_out = nullptr;
+  const float* label_src = nullptr; float* label_dst = nullptr;
 };
 bool bottom_mlp_fwd_supported(int k0, int n0, int n1, int n2);
 void bottom_mlp_fwd(const BotMlpArgs& a, hipStream_t s);

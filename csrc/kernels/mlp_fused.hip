@@ -179,7 +179,29 @@ __global__ __launch_bounds__(256) void bottom_mlp_fwd_kernel(BotMlpArgs a) {
   load_bias<J0>(bv0, a.b0, a.bs0, c0, lane);
   {
     Chunks<TM> x;                            // the input tile (one 16-B chunk per thread)
+    static_assert(Chunks<TM>::Q == 1, "one input chunk per thread");
     x.load(a.x, a.ldx, m0, a.M, 0, tid);
+    if (a.dense != nullptr) {
+      // the batch load folded in: this chunk's dense columns from fp32 (the
+      // rest of the row -- the constant-1 bias column, zero padding -- as
+      // stored), back to x for the backward
+      const int r = tid >> 3, c = tid & 7, gr = m0 + r;
+      if (c * 8 < a.nd && gr < a.M) {
+        uint32_t u[4] = {x.v[0].x, x.v[0].y, x.v[0].z, x.v[0].w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const int col = c * 8 + e;
+          if (col < a.nd) {
+            const uint32_t h = f2bf(a.dense[(int64_t)gr * a.ld_dense + col]);
+            u[e >> 1] = (e & 1) ? ((u[e >> 1] & 0xffffu) | (h << 16)) : ((u[e >> 1] & 0xffff0000u) | h);
+          }
+        }
+        x.v[0] = u32x4{u[0], u[1], u[2], u[3]};
+        *(u32x4*)(a.x_out + (int64_t)gr * a.ldx + c * 8) = x.v[0];
+      }
+      if (a.label_src != nullptr && tid < TM && m0 + tid < a.M)
+        a.label_dst[m0 + tid] = a.label_src[m0 + tid];
+    }
     x.store(sm + R_X, tid);
   }
   __syncthreads();

@@ -358,6 +358,9 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
             and Lb[0].in_k == Lb[0].wcols and not Lb[1].bias_in_k and not Lb[2].bias_in_k
             and Lb[1].in_k == Lb[0].out and Lb[2].in_k == Lb[1].out
             and ops.bottom_mlp_fwd_ok(Lb[0].in_k, Lb[0].out, Lb[1].out, Lb[2].out))
+        # ... which also loads a staged batch's dense features / labels (one
+        # launch fewer on the MLP stream; TDFO_BOT_LOAD_FOLD=0: batch_load)
+        self._bot_load_fold = os.environ.get("TDFO_BOT_LOAD_FOLD", "1") != "0"
         self.bot_grad = [z(B, L.out) for L in self.bottom_layers]
         self.top_in = [act_in(L) for L in self.top_layers]
         self.t_out = z(B, self.head_k)
@@ -827,7 +830,9 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
         for kind, fn in self._stages():
             self._run_stage(kind, fn)
 
-    def _s_bottom_fwd(self):
+    def _s_bottom_fwd(self, staged=None):
+        """``staged`` (fused stack only): the (dense fp32, label) staging of
+        this step's batch, loaded by the bottom-MLP launch itself."""
         if self._fused_bottom:
             # the default 3-layer stack in one launch (csrc/kernels/mlp_fused.hip)
             Ls = self.bottom_layers
@@ -835,7 +840,8 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
             ops.bottom_mlp_fwd(self.bot_in[0], self.fp.bf16(Ls[0].name + ".w"),
                                self.fp.bf16(Ls[1].name + ".w"), self.fp.bf16(Ls[2].name + ".w"),
                                bias[0], bias[1], bias[2], self.bot_in[1], self.bot_in[2],
-                               self.h_out)
+                               self.h_out, dense=None if staged is None else staged[0],
+                               label=None if staged is None else (staged[1], self.label))
             return
         n = len(self.bottom_layers)
         for i, L in enumerate(self.bottom_layers):

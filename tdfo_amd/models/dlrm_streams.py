@@ -87,6 +87,11 @@ class StreamGraphsMixin:
 
         def m1():
             self._s_gen_dense()              # (in-step batches: dense features / labels)
+            if self._bstg is not None and self._fused_bottom and self._bot_load_fold:
+                # this step's dense / labels from the staging, loaded by the
+                # fused bottom-MLP launch itself (no batch_load launch)
+                self._s_bottom_fwd(staged=self._bstg)
+                return
             if self._bstg is not None:       # this step's dense / labels from the staging
                 ops.batch_load(self._bstg[0], self.x0, self.ids[:0], self.ids[:0], self._bstg[1],
                                self.label)

@@ -27,11 +27,15 @@ def bottom_mlp_fwd_ok(k0: int, n0: int, n1: int, n2: int) -> bool:
                                                                     int(n2)))
 
 
-def bottom_mlp_fwd(x, w0, w1, w2, b0, b1, b2, y0, y1, y2):
+def bottom_mlp_fwd(x, w0, w1, w2, b0, b1, b2, y0, y1, y2, dense=None, label=None):
     """Three Linear + ReLU layers in one launch (GPU only): y0 = relu(x w0^T
     (+ b0)), y1 = relu(y0 w1^T + b1), y2 = relu(y1 w2^T + b2), the first K
-    columns of each weight; bitwise equal to three ``gemm`` calls."""
-    _native().bottom_mlp_fwd(x, w0, w1, w2, b0, b1, b2, y0, y1, y2)
+    columns of each weight; bitwise equal to three ``gemm`` calls.
+    ``dense`` (fp32 [M, nd]): ``batch_load``'s dense part folded in --
+    x[:, :nd] = bf16(dense) first (written back to x); ``label = (src, dst)``
+    also copied."""
+    ls, ld = label if label is not None else (None, None)
+    _native().bottom_mlp_fwd(x, w0, w1, w2, b0, b1, b2, y0, y1, y2, dense, ls, ld)
 
 
 def gemm(a, a_col, b, b_col, bias=None, relu=False, mask=None, out=None, out32=None, splits=1,

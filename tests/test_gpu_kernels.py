@@ -375,6 +375,38 @@ def test_fused_bottom_mlp_matches_per_layer_gemms(B):
     assert rel < 2e-2, rel
 
 
+@pytest.mark.parametrize("B", [8192, 1000])
+def test_fused_bottom_mlp_batch_load_fold(B):
+    """The batch load folded into the fused bottom-MLP launch (fp32 dense
+    features + labels from a staging buffer) gives bitwise what batch_load
+    followed by the plain fused launch gives: x0, labels and the three
+    activations."""
+    from tdfo_amd.models.dlrm import DLRMConfig, DLRMTrainer
+
+    cfg = DLRMConfig(table_rows=[1000, 20, 5000])
+    tr = DLRMTrainer(cfg, B, DEV)
+    assert tr._fused_bottom
+    g = torch.Generator().manual_seed(5)
+    dense = (torch.randn(B, 13, generator=g) * 3).to(DEV)
+    label = (torch.rand(B, generator=g) < 0.3).float().to(DEV)
+    res = []
+    for fold in (True, False):
+        tr.x0[:, :13].fill_(5.0)
+        tr.label.fill_(-1.0)
+        for t in (tr.bot_in[1], tr.bot_in[2], tr.h_out):
+            t[:, : t.shape[1] - (64 if t is not tr.h_out else 0)].fill_(7.0)
+        if fold:
+            tr._s_bottom_fwd(staged=(dense, label))
+        else:
+            ops.batch_load(dense, tr.x0, tr.ids[:0], tr.ids[:0], label, tr.label)
+            tr._s_bottom_fwd()
+        torch.cuda.synchronize()
+        res.append([t.clone() for t in (tr.x0, tr.label, tr.bot_in[1], tr.bot_in[2], tr.h_out)])
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+    assert torch.equal(res[0][1][:B], label)
+
+
 def test_embedding_dense_grad_replicated_tables():
     """The replicated tables' backward at W > 1 (dense fp32 gradient, one id
     per bag, per-table LDS sort): the tiny tables' runs span tens of chunks
