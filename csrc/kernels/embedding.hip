@@ -765,11 +765,27 @@ __device__ __forceinline__ float rdlanef(float v, int l) {
   return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
 }
 
-template <int D>
+// NT: the update's table-row reads and writes as non-temporal accesses --
+// on multi-hot batches (random rows over a big table, each touched once per
+// step): DCN-v2's update 503 -> 464 us isolated; on one-hot DLRM-1TB, whose
+// short tables' rows are hot, 61.4 -> 65.3, so off there (profiles/r06/notes.md)
+template <bool NT, typename T>
+__device__ __forceinline__ T row_ld(const T* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <bool NT, typename T>
+__device__ __forceinline__ void row_st(T* p, T v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
+template <int D, bool NT = false>
 __device__ __forceinline__ void load_row(float (&wv)[BwdCfg<D>::EPL], const float* w) {
   constexpr int EPL = BwdCfg<D>::EPL;
   if constexpr (EPL == 2) {
-    const float2 v = *(const float2*)w; wv[0] = v.x; wv[1] = v.y;
+    typedef __attribute__((ext_vector_type(2))) float f2v;
+    const f2v v = row_ld<NT>((const f2v*)w); wv[0] = v.x; wv[1] = v.y;
   } else if constexpr (EPL == 4) {
     const float4 v = *(const float4*)w; wv[0] = v.x; wv[1] = v.y; wv[2] = v.z; wv[3] = v.w;
   } else if constexpr (EPL == 8) {
@@ -843,7 +859,7 @@ __device__ __forceinline__ bool skip_step(const EmbBwdArgs& a) {
 // One optimizer update of one row; `wv` = current weights (prefetched).
 // Adam with pre-loaded moments (mpre / vpre: this lane's elements of the
 // row's m and v, issued with the chunk's other loads) or loading them here.
-template <int D, int OPT>
+template <int D, int OPT, bool NT = false>
 __device__ __forceinline__ void update_row(const EmbBwdArgs& a, const OptScalars& o,
                                            uint64_t row, const float (&acc_in)[BwdCfg<D>::EPL],
                                            float (&wv)[BwdCfg<D>::EPL], float st_row, int lane,
@@ -902,9 +918,10 @@ __device__ __forceinline__ void update_row(const EmbBwdArgs& a, const OptScalars
     }
     if (act) {
       if constexpr (EPL == 2) {
-        *(float2*)w = make_float2(wv[0], wv[1]);
+        typedef __attribute__((ext_vector_type(2))) float f2v;
+        row_st<NT>((f2v*)w, f2v{wv[0], wv[1]});
       } else if constexpr (EPL == 4) {
-        *(float4*)w = make_float4(wv[0], wv[1], wv[2], wv[3]);
+        row_st<NT>((f32x4_t*)w, f32x4_t{wv[0], wv[1], wv[2], wv[3]});
       } else {
 #pragma unroll
         for (int u = 0; u < EPL; ++u) w[u] = wv[u];
@@ -1003,7 +1020,7 @@ __device__ __forceinline__ void run_finish(const EmbBwdArgs& a, const OptScalars
 // head / tail partials: with run metadata (``meta``, from the one-hot sort)
 // the last of a run's chunks to arrive finishes it here; otherwise the
 // chunk where it starts is listed for emb_combine_kernel.
-template <int D, typename K, bool GB, int OPT, int CH, bool META = false>
+template <int D, typename K, bool GB, int OPT, int CH, bool META = false, bool NT = false>
 __global__ __launch_bounds__(256) void emb_chunk_kernel(
     EmbBwdArgs a, const K* __restrict__ keys, const int32_t* __restrict__ vals,
     const int64_t* __restrict__ goff, const float* __restrict__ gscale,
@@ -1071,7 +1088,7 @@ __global__ __launch_bounds__(256) void emb_chunk_kernel(
     const int64_t go = (int64_t)rdlane((uint64_t)mygoff, p);
     load_grad_raw<D, GB>(g[p], a.grad, go + e0c);
     const uint64_t rowp = (uint64_t)rdlane(mykey, p);
-    if constexpr (NEED_W) load_row<D>(wr[p], a.W + rowp * D + e0c);
+    if constexpr (NEED_W) load_row<D, NT>(wr[p], a.W + rowp * D + e0c);
     if constexpr (PRE_MV) {
       mr[p][0] = a.state1[rowp * D + e0c];
       vr[p][0] = a.state2[rowp * D + e0c];
@@ -1092,11 +1109,11 @@ __global__ __launch_bounds__(256) void emb_chunk_kernel(
 #pragma unroll
           for (int u = 0; u < EPL; ++u) wv[u] = NEED_W ? wr[p][u] : 0.f;
           if constexpr (PRE_MV)
-            update_row<D, OPT>(a, o, (uint64_t)rdlane(mykey, p), acc, wv, rdlanef(st_l, p), lane,
-                               mr[p], vr[p]);
+            update_row<D, OPT, NT>(a, o, (uint64_t)rdlane(mykey, p), acc, wv, rdlanef(st_l, p),
+                                   lane, mr[p], vr[p]);
           else
-            update_row<D, OPT>(a, o, (uint64_t)rdlane(mykey, p), acc, wv, rdlanef(st_l, p),
-                               lane);
+            update_row<D, OPT, NT>(a, o, (uint64_t)rdlane(mykey, p), acc, wv, rdlanef(st_l, p),
+                                   lane);
         } else if (act) {
           part_store<EPL>(head + c * D + e0, acc);
         }
@@ -1459,6 +1476,10 @@ bool onehot_path(const EmbBwdArgs& a) {
 // walk over a short table's ~85 partials became the update's tail: 0.430 vs
 // 0.413 (profiles/r06/notes.md).
 constexpr int64_t IKC_AUTO_MAX = 65536;
+const bool g_emb_nt = [] {            // TDFO_EMB_NT=0: plain row accesses everywhere
+  const char* e = getenv("TDFO_EMB_NT");
+  return !(e && atoi(e) == 0);
+}();
 const int g_emb_inkernel_combine = [] {
   const char* e = getenv("TDFO_EMB_INKERNEL_COMBINE");
   return e ? atoi(e) : -1;
@@ -1589,13 +1610,17 @@ void apply_impl(const EmbBwdArgs& a0, const WsLayout& L, hipStream_t s) {
     } else {
       a.side_block0 = 0;
     }
-#define TDFO_CK(GBV, MV)                                                                   \
-    hipLaunchKernelGGL((emb_chunk_kernel<D, K, GBV, OPT, CH, MV>), dim3(blocks), dim3(256), 0, s, \
-                       a, keys_out, vals_out, goff, gscale, head, tail, tlist, tcount, meta, rcnt)
+#define TDFO_CK(GBV, MV, NTV)                                                              \
+    hipLaunchKernelGGL((emb_chunk_kernel<D, K, GBV, OPT, CH, MV, NTV>), dim3(blocks), dim3(256), 0, \
+                       s, a, keys_out, vals_out, goff, gscale, head, tail, tlist, tcount, meta, rcnt)
+    // non-temporal row accesses on multi-hot batches (see row_ld)
+    const bool nt = g_emb_nt && !onehot_path(a0);
     if (meta != nullptr) {
-      if (a.grad_bf16) TDFO_CK(true, true); else TDFO_CK(false, true);
+      if (a.grad_bf16) TDFO_CK(true, true, false); else TDFO_CK(false, true, false);
+    } else if (nt) {
+      if (a.grad_bf16) TDFO_CK(true, false, true); else TDFO_CK(false, false, true);
     } else {
-      if (a.grad_bf16) TDFO_CK(true, false); else TDFO_CK(false, false);
+      if (a.grad_bf16) TDFO_CK(true, false, false); else TDFO_CK(false, false, false);
     }
 #undef TDFO_CK
     TDFO_CHECK_HIP(hipGetLastError());
