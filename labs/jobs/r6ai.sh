@@ -1,6 +1,6 @@
 # NT row accesses on multi-hot batches only (runtime choice): tests + DCN / DLRM A/B.
 set -u
-O=gpurun_out/r06/ai; rm -rf $O; mkdir -p $O
+O=gpurun_out/r06/${JOBTAG:-ai}; rm -rf $O; mkdir -p $O
 timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_kernels.py -k "embedding or dcn or cross" > $O/tests.log 2>&1 || { echo "tests rc=$?"; tail -20 $O/tests.log; exit 1; }
 tail -1 $O/tests.log
 for k in 1 2; do
