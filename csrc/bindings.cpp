@@ -1299,7 +1299,7 @@ void head_bce(const Tensor& H, const Tensor& w, const Tensor& b, const Tensor& l
 }
 
 void head_reduce(const Tensor& part, int64_t nparts, int64_t K, const Tensor& grad,
-                 const Tensor& loss_acc, at::TensorList bumps) {
+                 const Tensor& loss_acc, at::TensorList bumps, bool defer) {
   check_f32c(part, "part"); check_f32c(grad, "grad"); check_f32c(loss_acc, "loss_acc");
   TORCH_CHECK(part.numel() >= nparts * (K + 2) && grad.numel() >= K + 1 && loss_acc.numel() >= 1,
               "head_reduce: shapes");
@@ -1310,6 +1310,13 @@ void head_reduce(const Tensor& part, int64_t nparts, int64_t K, const Tensor& gr
     check_f32c(bumps[i], "bump");
     TORCH_CHECK(bumps[i].numel() >= 2, "head_reduce: counters are [lr, step, ...]");
     hb.p[i] = bumps[i].data_ptr<float>();
+  }
+  if (defer) {
+    // run by the next paired 128x128 GEMM launch (flush_side_job otherwise)
+    tdfo::head_reduce_park(tdfo::HeadReduceJob{part.data_ptr<float>(), (int)nparts, (int)K,
+                                               grad.data_ptr<float>(),
+                                               loss_acc.data_ptr<float>(), hb});
+    return;
   }
   tdfo::head_reduce(part.data_ptr<float>(), (int)nparts, (int)K, grad.data_ptr<float>(),
                     loss_acc.data_ptr<float>(), hb, cur_stream());
@@ -1507,6 +1514,7 @@ void reduce_adam(const Tensor& part, int64_t nparts, int64_t n, int64_t ld, cons
 }
 
 void flush_side_job() {
+  tdfo::head_reduce_flush(cur_stream());
   if (g_tower_pending) {             // (before the reduce: it reads the towers' partials)
     g_tower_pending = false;
     tdfo::two_tower(g_tower, 1, cur_stream());
@@ -1803,7 +1811,7 @@ TORCH_LIBRARY(tdfo, m) {
   m.def("head_bce(Tensor H, Tensor w, Tensor b, Tensor label, float inv_n, bool relu_mask, "
         "Tensor(a!) logits, Tensor(b!) dH, Tensor(c!) part) -> ()");
   m.def("head_reduce(Tensor part, int nparts, int K, Tensor(a!) grad, Tensor(b!) loss_acc, "
-        "Tensor(c!)[] bumps) -> ()");
+        "Tensor(c!)[] bumps, bool defer) -> ()");
   m.def("reduce_rows(Tensor inp, int rows, int n, int ld, Tensor(a!) out, bool accumulate, float scale) -> ()");
   m.def("colsum(Tensor x, Tensor(a!) out, bool accumulate) -> ()");
   m.def("slab_reduce(Tensor[] slabs, int[] splits, Tensor(a!)[] outs) -> ()");

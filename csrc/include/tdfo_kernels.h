@@ -388,6 +388,16 @@ int head_bce_parts(int B);
 // HeadBumps: above EmbBwdArgs).
 void head_reduce(const float* part, int nparts, int K, float* grad, float* loss_acc,
                  const HeadBumps& bumps, hipStream_t s);
+// The same, parked (one per thread): the next paired 128x128 GEMM launch --
+// the first top-MLP backward pair, which needs nothing it writes -- runs it
+// in extra blocks (head_reduce_take); head_reduce_flush launches it on its
+// own if nothing took it.
+struct HeadReduceJob {
+  const float* part; int nparts; int K; float* grad; float* loss_acc; HeadBumps bumps;
+};
+void head_reduce_park(const HeadReduceJob& j);
+bool head_reduce_take(HeadReduceJob* j);
+void head_reduce_flush(hipStream_t s);
 // grad[j] = sum_r part[r * ld + j] for j < n (head_reduce's / reduce_rows'
 // fixed order) followed by one Adam / AdamW step of p[j] from it (hyper =
 // [lr, step, grad_scale], adam_elem: the flat optimizer's bits); column n is

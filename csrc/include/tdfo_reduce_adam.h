@@ -108,4 +108,29 @@ __device__ __forceinline__ void reduce_adam_unit(const ReduceAdamArgs& a, int un
   }
 }
 
+// head_reduce's work as 256-thread units (16 columns of [grad | loss] each,
+// head_reduce_kernel's sums and order), for the side blocks of a GEMM launch;
+// exactly one block barrier on every path
+__host__ __device__ inline int head_reduce_units(const HeadReduceJob& j) {
+  return (j.K + 2 + RA_COLS - 1) / RA_COLS;
+}
+__device__ __forceinline__ void head_reduce_unit(const HeadReduceJob& j, int unit, int ltid,
+                                                 float (*red)[RA_COLS]) {
+  const int ld = j.K + 2;
+  const int c = ltid % RA_COLS, ph = ltid / RA_COLS;
+  const int col = unit * RA_COLS + c;
+  const bool live = unit < head_reduce_units(j);
+  red[ph][c] = (live && col < ld && j.nparts > 0) ? col_phase_sum<RA_PH>(j.part, j.nparts, ld, col, ph)
+                                                  : 0.f;
+  __syncthreads();
+  if (live && ph == 0 && col < ld) {
+    float t = 0.f;
+#pragma unroll
+    for (int q = 0; q < RA_PH; ++q) t += red[q][c];
+    if (col <= j.K) j.grad[col] = t;
+    else j.loss_acc[0] += t;
+  }
+  if (unit == 0 && ltid < j.bumps.n) j.bumps.p[ltid][1] += 1.f;
+}
+
 }  // namespace tdfo

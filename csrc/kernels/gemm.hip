@@ -22,6 +22,7 @@
 
 #include "tdfo_common.h"
 #include "tdfo_kernels.h"
+#include "tdfo_reduce_adam.h"
 
 namespace tdfo {
 namespace {
@@ -1304,8 +1305,16 @@ __global__ __launch_bounds__(512, 2) void gemm_pp_kernel(GemmArgs p) {
 // Two problems in one ping-pong grid (a layer's weight grad + dgrad, or two
 // weight grads): blocks [0, nb0) run problem 0, the rest problem 1.
 template <bool AC0, bool BC0, bool AC1, bool BC1>
-__global__ __launch_bounds__(512, 2) void gemm_pp_pair_kernel(GemmArgs p0, GemmArgs p1, int nb0) {
+// blocks [nb01, ...): a parked head_reduce (two 256-thread units per block)
+__global__ __launch_bounds__(512, 2) void gemm_pp_pair_kernel(GemmArgs p0, GemmArgs p1, int nb0,
+                                                              int nb01, HeadReduceJob hr) {
   extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+  if ((int)blockIdx.x >= nb01) {
+    const int slice = threadIdx.x >> 8;
+    head_reduce_unit(hr, ((int)blockIdx.x - nb01) * 2 + slice, threadIdx.x & 255,
+                     (float(*)[RA_COLS])smem_raw + slice * RA_PH);
+    return;
+  }
   if ((int)blockIdx.x < nb0) gemm_pp_body<128, 2, 128, AC0, BC0>(p0, blockIdx.x, smem_raw);
   else                       gemm_pp_body<128, 2, 128, AC1, BC1>(p1, blockIdx.x - nb0, smem_raw);
 }
@@ -1335,8 +1344,10 @@ void pp_pair_launch(const GemmArgs& a0, const GemmArgs& a1, hipStream_t s) {
                                        PPG::LDS));
     attr = true;
   }
-  const int g0 = pp_grid(a0);
-  hipLaunchKernelGGL(fn, dim3(g0 + pp_grid(a1)), dim3(512), PPG::LDS, s, a0, a1, g0);
+  const int g0 = pp_grid(a0), g01 = g0 + pp_grid(a1);
+  HeadReduceJob hr{};
+  const int side = head_reduce_take(&hr) ? (head_reduce_units(hr) + 1) / 2 : 0;
+  hipLaunchKernelGGL(fn, dim3(g01 + side), dim3(512), PPG::LDS, s, a0, a1, g0, g01, hr);
   TDFO_CHECK_HIP(hipGetLastError());
 }
 

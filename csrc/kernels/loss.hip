@@ -312,6 +312,29 @@ void reduce_adam(const ReduceAdamArgs& a, hipStream_t s) {
   TDFO_CHECK_HIP(hipGetLastError());
 }
 
+namespace {
+thread_local bool g_hr_pending = false;
+thread_local HeadReduceJob g_hr{};
+}  // namespace
+
+void head_reduce_park(const HeadReduceJob& j) {
+  if (g_hr_pending) throw std::runtime_error("head_reduce: a parked job is still waiting");
+  g_hr = j;
+  g_hr_pending = true;
+}
+
+bool head_reduce_take(HeadReduceJob* j) {
+  if (!g_hr_pending) return false;
+  *j = g_hr;
+  g_hr_pending = false;
+  return true;
+}
+
+void head_reduce_flush(hipStream_t s) {
+  HeadReduceJob j;
+  if (head_reduce_take(&j)) head_reduce(j.part, j.nparts, j.K, j.grad, j.loss_acc, j.bumps, s);
+}
+
 void head_reduce(const float* part, int nparts, int K, float* grad, float* loss_acc,
                  const HeadBumps& bumps, hipStream_t s) {
   hipLaunchKernelGGL(head_reduce_kernel, dim3((K + 2 + 15) / 16), dim3(256), 0, s, part, nparts,

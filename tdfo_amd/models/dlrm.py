@@ -361,6 +361,9 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
         # ... which also loads a staged batch's dense features / labels (one
         # launch fewer on the MLP stream; TDFO_BOT_LOAD_FOLD=0: batch_load)
         self._bot_load_fold = os.environ.get("TDFO_BOT_LOAD_FOLD", "1") != "0"
+        # the head's reduce (grad, loss, step counters) in extra blocks of the
+        # first top backward GEMM pair (TDFO_HEAD_SIDE=0: its own launch)
+        self._head_side = os.environ.get("TDFO_HEAD_SIDE", "1") != "0"
         self.bot_grad = [z(B, L.out) for L in self.bottom_layers]
         self.top_in = [act_in(L) for L in self.top_layers]
         self.t_out = z(B, self.head_k)
@@ -900,8 +903,10 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
                      self.logits, self.top_grad[-1], self.head_part)
         # head grad + loss accumulation + this step's optimizer step counters
         # (read later in the step by the embedding and dense updates): one launch
+        # (deferred: the first top backward GEMM pair runs it in extra blocks)
+        defer = self._head_side and self.device.type == "cuda"
         ops.head_reduce(self.head_part, self.nparts, K, fp.grad("head"), self.loss_sum,
-                        (self.dense_hyper, self.emb_hyper))
+                        (self.dense_hyper, self.emb_hyper), defer=defer)
         for i in reversed(range(n)):
             L = self.top_layers[i]
             if i > 0:
@@ -910,6 +915,8 @@ class DLRMTrainer(StreamGraphsMixin, MultiRankStreamsMixin, DCNMixin):
                 dx = self.dz if cfg.interaction == "dot" else self.dcn_dx[-1]
             self._bwd(L, self.top_in[i], self.top_grad[i], dx, x_is_relu=i > 0,
                       wgrad_now=not self._defer_top_wgrad)
+            if defer:
+                ops.flush_side_job()         # (no-op once a GEMM pair took it)
 
     def _s_top_b(self):
         """Interaction / cross backward: the embedding gradients."""

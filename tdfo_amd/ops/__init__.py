@@ -635,11 +635,15 @@ def slab_reduce(segs):
             out.view(-1).copy_(sl.view(-1)[:S * n].view(S, n).sum(0))
 
 
-def head_reduce(part, nparts, K, grad, loss_acc, bumps=()):
+def head_reduce(part, nparts, K, grad, loss_acc, bumps=(), defer=False):
     """grad[:K+1] = column sums of part[:, :K+1]; loss_acc += sum part[:, K+1];
-    bump[1] += 1 for each step-counter vector in ``bumps`` (one launch)."""
+    bump[1] += 1 for each step-counter vector in ``bumps`` (one launch).
+    ``defer`` (GPU): run by extra blocks of the next paired 128x128 GEMM
+    launch (the first top-MLP backward pair); ``flush_side_job()`` launches it
+    if none took it."""
     if _gpu(part):
-        _native().head_reduce(part, int(nparts), int(K), grad, loss_acc, list(bumps))
+        _native().head_reduce(part, int(nparts), int(K), grad, loss_acc, list(bumps),
+                              bool(defer))
     else:
         ref.head_reduce(part, nparts, K, grad, loss_acc, bumps)
 

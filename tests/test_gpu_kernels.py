@@ -631,6 +631,31 @@ def test_dlrm_step_matches_cpu():
     assert sum(lg[-5:]) < sum(lg[:5])
 
 
+def test_dlrm_head_reduce_side_blocks_bit_identical():
+    """The head's reduce run by extra blocks of the first top backward GEMM
+    pair (parked head_reduce) gives the bits of its own launch."""
+    from tdfo_amd.data.synthetic import SyntheticCriteo
+    from tdfo_amd.models.dlrm import DLRMConfig, DLRMTrainer
+
+    cfg = DLRMConfig(embedding_dim=128, table_rows=[1000, 20, 5000], bottom=[128],
+                     top=[512, 256, 1])
+    B = 1024
+    a = DLRMTrainer(cfg, B, DEV)
+    b = DLRMTrainer(cfg, B, DEV)
+    a._head_side, b._head_side = True, False
+    data = SyntheticCriteo(cfg.table_rows, B, device=DEV, seed=9)
+    for _ in range(5):
+        x = data.next()
+        for t in (a, b):
+            t.load_batch(*x)
+            t.step()
+    torch.cuda.synchronize()
+    assert torch.equal(a.fp.p, b.fp.p)
+    assert torch.equal(a.emb.tw_store.weight, b.emb.tw_store.weight)
+    assert torch.equal(a.dense_hyper, b.dense_hyper) and torch.equal(a.emb_hyper, b.emb_hyper)
+    assert a.pop_loss() == b.pop_loss()
+
+
 @pytest.mark.parametrize("staged,one", [(False, "0"), (False, "1"), (False, "ids0"),
                                         (True, "0"), (False, "defer")])
 def test_dlrm_graph_replay_matches_eager(staged, one):
