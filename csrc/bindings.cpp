@@ -729,7 +729,7 @@ void check_i64(const Tensor& t, const char* n) {
 void embedding_bag_fwd(const Tensor& W, const Tensor& row_offset, const Tensor& indices,
                        const Tensor& offsets, const Tensor& out_off,
                        const c10::optional<Tensor>& psw, int64_t T, int64_t B, bool mean,
-                       const Tensor& out, int64_t out_stride, bool onehot) {
+                       const Tensor& out, int64_t out_stride, bool onehot, at::TensorList bumps) {
   check_dev(W, "W"); check_2d_rowmajor(W, "W");
   TORCH_CHECK(W.scalar_type() == at::kFloat && W.is_contiguous(), "W must be contiguous fp32");
   const int64_t D = W.size(1);
@@ -752,6 +752,15 @@ void embedding_bag_fwd(const Tensor& W, const Tensor& row_offset, const Tensor& 
   a.T = (int)T; a.B = (int)B; a.mean = mean; a.out_stride = out_stride;
   a.out = out.data_ptr(); a.out_bf16 = out.scalar_type() == at::kBFloat16;
   a.onehot = onehot && indices.numel() == T * B;
+  TORCH_CHECK(bumps.size() <= 8, "embedding_bag_fwd: at most 8 counters");
+  for (const auto& t : bumps) {
+    TORCH_CHECK(t.is_cuda() && t.numel() >= 1 &&
+                (t.scalar_type() == at::kFloat || t.scalar_type() == at::kLong),
+                "embedding_bag_fwd: float32 / int64 GPU counters");
+    a.bumps.p[a.bumps.n] = t.data_ptr();
+    a.bumps.is_i64[a.bumps.n] = t.scalar_type() == at::kLong;
+    ++a.bumps.n;
+  }
   tdfo::embedding_bag_fwd(a, cur_stream());
 }
 
@@ -1754,7 +1763,8 @@ TORCH_LIBRARY(tdfo, m) {
   m.def("interaction_bwd(Tensor dz, Tensor dense, Tensor emb, int[] off, int[] stride, int F, int D, "
         "Tensor(a!) d_dense, Tensor(b!) d_emb, int[] doff, int[] dstride, bool relu_mask) -> ()");
   m.def("embedding_bag_fwd(Tensor W, Tensor row_offset, Tensor indices, Tensor offsets, Tensor out_off, "
-        "Tensor? psw, int T, int B, bool mean, Tensor(a!) out, int out_stride, bool onehot) -> ()");
+        "Tensor? psw, int T, int B, bool mean, Tensor(a!) out, int out_stride, bool onehot, "
+        "Tensor(b!)[] bumps) -> ()");
   m.def("embedding_bwd(Tensor(a!) W, Tensor row_offset, Tensor indices, Tensor offsets, Tensor grad_off, "
         "Tensor? psw, int T, int B, bool mean, int key_bits, Tensor grad, int grad_stride, int opt, "
         "Tensor(b!)? state1, Tensor(c!)? state2, Tensor hyper, float eps, float beta1, float beta2, "

@@ -108,6 +108,13 @@ int radix_sort_pairs_u64(uint64_t* ka, int32_t* va, uint64_t* kb, int32_t* vb, i
 // indices[offsets[j] .. offsets[j+1]); table t's rows start at
 // row_offset[t] in the fused weight buffer W ([rows, D] fp32).
 // out + b*out_stride + out_off[t] gets the pooled (sum or mean) row.
+// step counters (fp32 or int64 scalars) each advanced by one
+struct BumpArgs {
+  void* p[8];
+  int is_i64[8];
+  int n;
+};
+
 struct EmbFwdArgs {
   const float* W; int D;
   const int64_t* row_offset;   // [T] (device)
@@ -119,6 +126,9 @@ struct EmbFwdArgs {
   int64_t out_stride;
   void* out; int out_bf16;
   int onehot;                  // caller's promise: offsets[j] == j (one id per bag)
+  // optional: step counters bumped by block 0 (a step's first launch takes
+  // the bump launch along; nothing in the lookup reads them)
+  BumpArgs bumps{};
 };
 void embedding_bag_fwd(const EmbFwdArgs& a, hipStream_t s);
 
@@ -354,11 +364,7 @@ void batch_load(const float* dense, int nd, int64_t ld_dense, uint16_t* x0, int6
 // MFMA load on `blocks` 256-thread blocks for `ticks` of the 100 MHz clock
 void burn_ticks(uint64_t ticks, int blocks, hipStream_t s);
 void spin_ticks(uint64_t ticks, hipStream_t s);
-struct BumpArgs {
-  void* p[8];
-  int is_i64[8];
-  int n;
-};
+
 void bump(const BumpArgs& a, hipStream_t s);
 void stamp(uint64_t* buf, int64_t* cnt, int seg, int nseg, int which, int64_t cap,
            hipStream_t s);

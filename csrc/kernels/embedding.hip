@@ -36,8 +36,17 @@ namespace {
 // One id per bag (offsets[j] == j): no offsets loads, and every lane group
 // keeps two bags' row gathers in flight (index load -> row load is the whole
 // dependency chain).
+__device__ __forceinline__ void fwd_bumps(const EmbFwdArgs& a) {
+  if (blockIdx.x == 0 && (int)threadIdx.x < a.bumps.n) {
+    const int i = threadIdx.x;
+    if (a.bumps.is_i64[i]) *(int64_t*)a.bumps.p[i] += 1;
+    else                   *(float*)a.bumps.p[i] += 1.f;
+  }
+}
+
 template <int D, bool OUT_BF16>
 __global__ __launch_bounds__(256) void emb_fwd_onehot_kernel(EmbFwdArgs a) {
+  fwd_bumps(a);
   constexpr int LPB = (D / 4) < 64 ? (D / 4) : 64;  // lanes per bag
   constexpr int BPW = 64 / LPB;                     // bags per wave
   const int lane = threadIdx.x & 63;
@@ -90,6 +99,7 @@ __device__ __forceinline__ void emb_wave_sync() {
 
 template <int D, bool OUT_BF16, int RIF>
 __global__ __launch_bounds__(256) void emb_fwd_kernel(EmbFwdArgs a) {
+  fwd_bumps(a);
   constexpr int LPB = (D / 4) < 64 ? (D / 4) : 64;  // lanes per bag
   constexpr int BPW = 64 / LPB;                     // bags per wave
   constexpr int NCP = D / (4 * LPB);                // float4 column passes per lane
@@ -1677,7 +1687,10 @@ int emb_rif() {
 
 void embedding_bag_fwd(const EmbFwdArgs& a, hipStream_t s) {
   const int64_t nbags = (int64_t)a.T * a.B;
-  if (nbags == 0) return;
+  if (nbags == 0) {
+    bump(a.bumps, s);                 // (the counters still advance)
+    return;
+  }
   const int rif = emb_rif();
   const int lpb = a.D / 4 < 64 ? a.D / 4 : 64;
   const int64_t waves = (nbags * lpb + 63) / 64;

@@ -51,6 +51,9 @@ USE_FUSED = True
 # whole transformer block in one fwd / one bwd kernel (encoder.hip); False
 # keeps the per-op path (fused attention core + LayerNorm kernels, torch GEMMs)
 USE_FUSED_BLOCK = True
+# the step counters' bump inside the item lookup launch (TDFO_B4R_FOLD_BUMP=0:
+# a launch of its own)
+_FOLD_BUMP = os.environ.get("TDFO_B4R_FOLD_BUMP", "1") != "0"
 
 
 def _fused(x: torch.Tensor) -> bool:
@@ -333,6 +336,7 @@ class ItemEmbedding(nn.Module):
             self.g_grad = torch.zeros(world * n_tokens, dim, dtype=torch.float32, device=device)
         self._anchor = nn.Parameter(torch.zeros(1, device=device))
         self._ids = None
+        self.fwd_bumps = ()              # counters the next lookup launch advances
 
     @property
     def weight(self):
@@ -343,8 +347,10 @@ class ItemEmbedding(nn.Module):
         # a fresh output (the caller's autograd saves it): the lookup writes it
         # directly, no copy of a static buffer
         out = torch.empty(n, self.D, dtype=torch.float32, device=self.store.weight.device)
+        # the trainer's step counters ride in this first launch of the step
+        bumps, self.fwd_bumps = self.fwd_bumps, ()
         self.store.forward(ids, self.offsets[: n + 1], self.zero, 1, n, out, self.zero, self.D,
-                           onehot=True)
+                           onehot=True, bumps=bumps)
         self._ids = ids
         return out
 
@@ -618,7 +624,10 @@ class Bert4RecTrainer:
         return loss
 
     def _step_body(self, seqs, labels):
-        ops.bump(self._counters)
+        if self.mode != "dmp" and self.device.type == "cuda" and _FOLD_BUMP:
+            self.item.fwd_bumps = self._counters     # advanced by the step's lookup launch
+        else:
+            ops.bump(self._counters)
         self._zero_grads()
         loss = self._fwd_bwd(seqs, labels)
         self.opt.all_reduce_grads(average=True)

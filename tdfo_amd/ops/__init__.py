@@ -347,15 +347,19 @@ def interaction_bwd(dz, dense, emb, off, stride, F, D, d_dense, d_emb, doff, dst
 
 
 def embedding_bag_fwd(W, row_offset, indices, offsets, out_off, T, B, out, out_stride, mean=False,
-                      psw=None, onehot=False):
+                      psw=None, onehot=False, bumps=()):
     """onehot=True promises offsets == arange (one id per bag): the kernel then
-    skips the offsets loads and keeps two bags' row gathers in flight."""
+    skips the offsets loads and keeps two bags' row gathers in flight.
+    ``bumps``: fp32 / int64 step counters advanced by one inside the launch."""
+    bumps = list(bumps)
     if _gpu(W):
         _native().embedding_bag_fwd(W, row_offset, indices, offsets, out_off, psw, T, B, mean, out,
-                                    out_stride, bool(onehot))
+                                    out_stride, bool(onehot), bumps)
     else:
         ref.embedding_bag_fwd(W, row_offset, indices, offsets, out_off, psw, T, B, mean, out,
                               out_stride)
+        for t in bumps:
+            t.view(-1)[:1].add_(1)
 
 
 def embedding_bwd(W, row_offset, indices, offsets, grad_off, T, B, grad, grad_stride, opt, hyper,

@@ -152,12 +152,13 @@ class TableBatchedEmbedding:
                              f"{int(tab[v[p]])} ({int(lim[p])} rows) at position {p}")
 
     def forward(self, indices, offsets, row_offset, T, B, out, out_off, out_stride, mean=False,
-                psw=None, onehot=False):
-        """Pooled lookup over ``T`` (virtual) tables of ``B`` bags each."""
+                psw=None, onehot=False, bumps=()):
+        """Pooled lookup over ``T`` (virtual) tables of ``B`` bags each
+        (``bumps``: step counters the launch advances by one)."""
         if DEBUG_CHECKS:
             self.check_ids(indices, offsets, row_offset, T, B)
         ops.embedding_bag_fwd(self.weight, row_offset, indices, offsets, out_off, T, B, out,
-                              out_stride, mean=mean, psw=psw, onehot=onehot)
+                              out_stride, mean=mean, psw=psw, onehot=onehot, bumps=bumps)
 
     def backward_update(self, indices, offsets, row_offset, T, B, grad, grad_off, grad_stride,
                         hyper, mean=False, psw=None, dense_grad=None, segsort=0):

@@ -153,6 +153,29 @@ def test_bert4rec_direct_grads_bit_identical(monkeypatch, fused_xent):
     assert a.pop_loss() == b.pop_loss()
 
 
+def test_bert4rec_bump_in_lookup_bit_identical(monkeypatch):
+    """The step counters advanced by the item lookup launch instead of a bump
+    launch of their own: same counters, same bits."""
+    import tdfo_amd.models.bert4rec as m
+
+    n, T, B = 3000, 20, 16
+    kw = dict(lr=3e-3, dropout=0.1, seed=7)
+    a = Bert4RecTrainer(n, T, 16, 2, 2, B, device=DEV, **kw)
+    b = Bert4RecTrainer(n, T, 16, 2, 2, B, device=DEV, **kw)
+    g = torch.Generator().manual_seed(1)
+    for _ in range(4):
+        s, l = _batch(g, B, T, n)
+        for t, fold in ((a, True), (b, False)):
+            monkeypatch.setattr(m, "_FOLD_BUMP", fold)
+            t.load_batch(s.to(DEV), l.to(DEV))
+            t.step()
+    torch.cuda.synchronize()
+    assert torch.equal(a.opt.hyper, b.opt.hyper)
+    assert torch.equal(a.model.rng_step, b.model.rng_step)
+    assert torch.equal(a.opt.flat, b.opt.flat)
+    assert torch.equal(a.item.weight, b.item.weight)
+
+
 def test_bert4rec_graph_replay_matches_eager():
     n, T, B = 5000, 20, 16
     kw = dict(lr=3e-3, dropout=0.0, seed=3)
