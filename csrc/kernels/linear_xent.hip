@@ -584,6 +584,46 @@ __device__ __forceinline__ XOpt xopt_of(const LinearXentArgs& a) {
 }
 
 // W[v][c0..c0+3] (p = those weights, already in registers) and, if wb, bias[v]
+// The row's Adam moments, loaded ahead (XMom: a tile's, prefetched with its
+// W fragment two tiles before use)
+struct XMom {
+  f32x4_t m, v;
+  float mb, vb;
+};
+
+__device__ __forceinline__ XMom xopt_load(const XOpt& o, int64_t v, int c0, bool wb) {
+  XMom r;
+  const int64_t i = v * XE + c0;
+  r.m = *(const f32x4_t*)(o.mW + i);
+  r.v = *(const f32x4_t*)(o.vW + i);
+  r.mb = wb ? o.mb[v] : 0.f;
+  r.vb = wb ? o.vb[v] : 0.f;
+  return r;
+}
+
+__device__ __forceinline__ void xopt_row_pre(const XOpt& o, int64_t v, int c0, f32x4_t p,
+                                             f32x4_t g, bool wb, float gb, const XMom& mo) {
+  const int64_t i = v * XE + c0;
+  const f32x4_t m4 = mo.m, w4 = mo.v;
+  float pp[4], mm[4], ww[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    pp[r] = p[r]; mm[r] = m4[r]; ww[r] = w4[r];
+    adam_elem(pp[r], g[r] * o.gs, mm[r], ww[r], o.lr, o.bc1, o.bc2, o.b1, o.b2, o.eps, o.wd,
+              o.adamw);
+  }
+  *(f32x4_t*)(o.W + i) = (f32x4_t){pp[0], pp[1], pp[2], pp[3]};
+  *(f32x4_t*)(o.mW + i) = (f32x4_t){mm[0], mm[1], mm[2], mm[3]};
+  *(f32x4_t*)(o.vW + i) = (f32x4_t){ww[0], ww[1], ww[2], ww[3]};
+  if (wb) {
+    float pb = o.bias[v], mbv = mo.mb, vbv = mo.vb;
+    adam_elem(pb, gb * o.gs, mbv, vbv, o.lr, o.bc1, o.bc2, o.b1, o.b2, o.eps, o.wd, o.adamw);
+    o.bias[v] = pb;
+    o.mb[v] = mbv;
+    o.vb[v] = vbv;
+  }
+}
+
 __device__ __forceinline__ void xopt_row(const XOpt& o, int64_t v, int c0, f32x4_t p, f32x4_t g,
                                          bool wb, float gb) {
   const int64_t i = v * XE + c0;
@@ -613,7 +653,8 @@ template <int NG>
 __device__ __forceinline__ void xent_wgrad_tile(const XentTok* K, f32x4_t wa, float b, int v,
                                                 int64_t V, float off, float hit, float pad_off,
                                                 float scale, float* __restrict__ dW,
-                                                float* __restrict__ db, int g, const XOpt& xo) {
+                                                float* __restrict__ db, int g, const XOpt& xo,
+                                                const XMom* mo = nullptr) {
   f32x4_t dw[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
   float dbs = 0.f;
 #pragma unroll
@@ -640,7 +681,8 @@ __device__ __forceinline__ void xent_wgrad_tile(const XentTok* K, f32x4_t wa, fl
   dbs = (sum4rows(dbs) + pad_off) * scale;
   if (v < V) {
     if (xo.on) {                           // the complete gradient: step in place
-      xopt_row(xo, v, 4 * g, wa, dw[0] + dw[1], g == 0, dbs);
+      if (mo != nullptr) xopt_row_pre(xo, v, 4 * g, wa, dw[0] + dw[1], g == 0, dbs, *mo);
+      else xopt_row(xo, v, 4 * g, wa, dw[0] + dw[1], g == 0, dbs);
       return;
     }
     *(f32x4_t*)(dW + (int64_t)v * XE + 4 * g) = dw[0] + dw[1];    // dW^T[4g+r][v]
@@ -673,27 +715,43 @@ __device__ __forceinline__ void xent_wgrad_body(const float* __restrict__ W,
   const int vb = (int)(tile0 * 16) + t;
   f32x4_t wa0, wa1;
   float b0, b1;
-  if (nfull > 0) { wa0 = *(const f32x4_t*)(Wt + la); b0 = bt[t]; }
-  if (nfull > 1) { wa1 = *(const f32x4_t*)(Wt + 16 * XE + la); b1 = bt[16 + t]; }
+  // fused step: the rows' Adam moments ride in the same 2-tile prefetch ring
+  // as W (without it each tile waited a full memory round trip for them);
+  // not for NG > 6, where the ring's 20 registers would spill
+  XMom mo0{}, mo1{};
+  const bool pre = NG <= 6 && xo.on;
+  if (nfull > 0) {
+    wa0 = *(const f32x4_t*)(Wt + la); b0 = bt[t];
+    if (pre) mo0 = xopt_load(xo, vb, 4 * g, g == 0);
+  }
+  if (nfull > 1) {
+    wa1 = *(const f32x4_t*)(Wt + 16 * XE + la); b1 = bt[16 + t];
+    if (pre) mo1 = xopt_load(xo, vb + 16, 4 * g, g == 0);
+  }
   for (int i = 0; i < nfull; i += 2) {
     {
       const f32x4_t wa = wa0;
       const float b = b0 * LOG2E;
+      const XMom mo = mo0;
       if (i + 2 < nfull) {
         wa0 = *(const f32x4_t*)(Wt + (i + 2) * 16 * XE + la);
         b0 = bt[(i + 2) * 16 + t];
+        if (pre) mo0 = xopt_load(xo, vb + 16 * (i + 2), 4 * g, g == 0);
       }
-      xent_wgrad_tile<NG>(K, wa, b, vb + 16 * i, V, off, hit, pad_off, scale, dW, db, g, xo);
+      xent_wgrad_tile<NG>(K, wa, b, vb + 16 * i, V, off, hit, pad_off, scale, dW, db, g, xo,
+                          pre ? &mo : nullptr);
     }
     if (i + 1 < nfull) {
       const f32x4_t wa = wa1;
       const float b = b1 * LOG2E;
+      const XMom mo = mo1;
       if (i + 3 < nfull) {
         wa1 = *(const f32x4_t*)(Wt + (i + 3) * 16 * XE + la);
         b1 = bt[(i + 3) * 16 + t];
+        if (pre) mo1 = xopt_load(xo, vb + 16 * (i + 3), 4 * g, g == 0);
       }
       xent_wgrad_tile<NG>(K, wa, b, vb + 16 * (i + 1), V, off, hit, pad_off, scale, dW, db, g,
-                          xo);
+                          xo, pre ? &mo : nullptr);
     }
   }
   const int64_t rt = V / 16;                             // ragged last tile

@@ -1,14 +1,10 @@
-# TwoTower: embedding rows gathered inside the tower kernel (4-launch step).
+# Bert4Rec: Adam-moment prefetch in the fused xent wgrad (pre) vs without (base).
 set -u
 O=gpurun_out/r06/aa; rm -rf $O; mkdir -p $O
-timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_two_tower.py > $O/tests.log 2>&1 || { echo "tests rc=$?"; tail -30 $O/tests.log; exit 1; }
+timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_bert4rec.py > $O/tests.log 2>&1 || { echo "tests rc=$?"; tail -30 $O/tests.log; exit 1; }
 tail -1 $O/tests.log
-for k in 1 2; do
-timeout -k 10 300 python -u scripts/bench_two_tower.py > $O/tt_$k.log 2>&1 || { echo "tt rc=$?"; tail -5 $O/tt_$k.log; exit 1; }
-echo "$k tt $(tail -n 1 $O/tt_$k.log | grep -o '"ms_per_step": [0-9.]*')"
-done
-ROOT=$PWD
-cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/$O/prof_tt -o tt -- python3 $ROOT/scripts/bench_two_tower.py --steps 200 > $ROOT/$O/prof_tt.log 2>&1 || { echo "prof rc=$?"; exit 1; }
-cd $ROOT
-python scripts/prof_summary.py $(ls $O/prof_tt/*kernel_trace.csv | head -1) --marker two_tower_kernel --last 100 > $O/prof_tt/summary.txt; cat $O/prof_tt/summary.txt
+for k in 1 2 3; do
+for c in base pre; do
+TDFO_LIB_PATH=$PWD/labs/ab/libtdfo_hip_$c.so timeout -k 10 300 python -u scripts/bench_bert4rec.py > $O/b4r_${c}_$k.log 2>&1 || { echo "b4r rc=$?"; tail -5 $O/b4r_${c}_$k.log; exit 1; }
+echo "$c $k b4r $(tail -n 1 $O/b4r_${c}_$k.log | grep -o '"ms_per_step": [0-9.]*')"
+done; done
