@@ -202,18 +202,37 @@ __global__ __launch_bounds__(256) void xent_merge_kernel(const float* __restrict
 #pragma unroll
   for (int k = 0; k <= XE; ++k) ws[k] = 0.f;
   const float* p0 = part + (int64_t)j * S * XP;
-  for (int s = tid; s < S; s += 256) {
-    const f32x4_t* p = (const f32x4_t*)(p0 + (int64_t)s * XP);
-    float r[XP];
+  // XMU splits' loads issued together, then combined in split order (one
+  // memory round trip per XMU splits instead of per split)
+  constexpr int XMU = 4;
+  for (int s0 = tid; s0 < S; s0 += XMU * 256) {
+    float r[XMU][XP], wv[XMU][XE + 1];
 #pragma unroll
-    for (int q = 0; q < XP / 4; ++q) {
-      const f32x4_t v = p[q];
-      r[4 * q] = v[0]; r[4 * q + 1] = v[1]; r[4 * q + 2] = v[2]; r[4 * q + 3] = v[3];
+    for (int u = 0; u < XMU; ++u) {
+      const int s = s0 + u * 256;
+      if (s < S) {
+        const f32x4_t* p = (const f32x4_t*)(p0 + (int64_t)s * XP);
+#pragma unroll
+        for (int q = 0; q < XP / 4; ++q) {
+          const f32x4_t v = p[q];
+          r[u][4 * q] = v[0]; r[u][4 * q + 1] = v[1]; r[u][4 * q + 2] = v[2];
+          r[u][4 * q + 3] = v[3];
+        }
+        const float* wp = wpart + (int64_t)s * (XE + 1);
+#pragma unroll
+        for (int k = 0; k <= XE; ++k) wv[u][k] = wp[k];
+      } else {
+        r[u][0] = -INFINITY;
+#pragma unroll
+        for (int k = 0; k <= XE; ++k) wv[u][k] = 0.f;
+      }
     }
-    if (r[0] != -INFINITY) sm_combine(m, sum, acc, r[0], r[1], r + 2);
-    const float* wp = wpart + (int64_t)s * (XE + 1);
 #pragma unroll
-    for (int k = 0; k <= XE; ++k) ws[k] += wp[k];
+    for (int u = 0; u < XMU; ++u) {
+      if (r[u][0] != -INFINITY) sm_combine(m, sum, acc, r[u][0], r[u][1], r[u] + 2);
+#pragma unroll
+      for (int k = 0; k <= XE; ++k) ws[k] += wv[u][k];
+    }
   }
   for (int off = 32; off > 0; off >>= 1) {
     float o[XE];
@@ -507,7 +526,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void xe
   if (blockIdx.y == 0) {          // column sums of [W | b] over the split
     f32x4_t cs = {0.f, 0.f, 0.f, 0.f};
     float bs = 0.f;
+    // (unrolled: 8 row loads in flight per lane, not one memory round trip
+    // per row; the sums keep their sequential order)
+#pragma unroll 8
     for (int64_t r = v0 + t; r < v1; r += 16) cs += *(const f32x4_t*)(W + r * XE + 4 * g);
+#pragma unroll 8
     for (int64_t r = v0 + l; r < v1; r += 64) bs += bias[r];
 #pragma unroll
     for (int off = 1; off < 16; off <<= 1)

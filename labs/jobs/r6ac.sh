@@ -1,10 +1,12 @@
-# Bert4Rec: wgrad slab sum + loss in one tail launch.
+# Bert4Rec kernel table (new lib) + PMC passes on the Linear+CE kernels.
 set -u
 O=gpurun_out/r06/ac; rm -rf $O; mkdir -p $O
-timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_bert4rec.py > $O/tests.log 2>&1 || { echo "tests rc=$?"; tail -30 $O/tests.log; exit 1; }
-tail -1 $O/tests.log
-for k in 1 2; do
-timeout -k 10 300 python -u scripts/bench_bert4rec.py > $O/b4r_$k.log 2>&1 || { echo "b4r rc=$?"; tail -5 $O/b4r_$k.log; exit 1; }
-timeout -k 10 300 python -u scripts/bench_bert4rec.py --batch 256 > $O/b4r256_$k.log 2>&1 || { echo "b4r256 rc=$?"; tail -5 $O/b4r256_$k.log; exit 1; }
-echo "$k b4r $(tail -n 1 $O/b4r_$k.log | grep -o '"ms_per_step": [0-9.]*') b4r256 $(tail -n 1 $O/b4r256_$k.log | grep -o '"ms_per_step": [0-9.]*')"
-done
+ROOT=$GRAFT_REPO_ROOT
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/$O/prof -o b4r -- python3 $ROOT/scripts/bench_bert4rec.py --steps 200 > $ROOT/$O/prof.log 2>&1 || { echo "prof rc=$?"; tail -5 $ROOT/$O/prof.log; exit 1; }
+cd $ROOT
+python scripts/prof_summary.py $(ls $O/prof/*kernel_trace.csv | head -1) --marker xent_pass1_mfma --last 100 > $O/summary.txt; cat $O/summary.txt
+cd /tmp
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAVES SQ_INSTS_VALU GRBM_GUI_ACTIVE --kernel-include-regex "xent_(pass1|wgrad|merge)" --output-format csv -d $ROOT/$O/pmc1 -o p -- python3 $ROOT/scripts/bench_bert4rec.py --steps 20 --warmup 5 --no-graph > $ROOT/$O/pmc1.log 2>&1 || { echo "pmc1 rc=$?"; tail -5 $ROOT/$O/pmc1.log; exit 1; }
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE TCC_HIT_sum TCC_MISS_sum GRBM_GUI_ACTIVE --kernel-include-regex "xent_(pass1|wgrad|merge)" --output-format csv -d $ROOT/$O/pmc2 -o p -- python3 $ROOT/scripts/bench_bert4rec.py --steps 20 --warmup 5 --no-graph > $ROOT/$O/pmc2.log 2>&1 || { echo "pmc2 rc=$?"; tail -5 $ROOT/$O/pmc2.log; exit 1; }
+ls $ROOT/$O/pmc1 $ROOT/$O/pmc2
