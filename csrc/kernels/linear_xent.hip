@@ -29,6 +29,7 @@
 #include "tdfo_kernels.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace tdfo {
 namespace {
@@ -443,6 +444,29 @@ __device__ __forceinline__ void xent_load_full(XentTile& T, const float* __restr
   }
 }
 
+// Column sums of [W | b] over one vocabulary split (the label-smoothing term's
+// sum of logits is h . colsum(W) + sum(b)).
+__device__ __forceinline__ void xent_colsums(const float* __restrict__ W,
+                                             const float* __restrict__ bias, int64_t v0,
+                                             int64_t v1, float* __restrict__ wp, int t, int g,
+                                             int l) {
+  f32x4_t cs = {0.f, 0.f, 0.f, 0.f};
+  float bs = 0.f;
+  // (unrolled: 8 row loads in flight per lane, not one memory round trip
+  // per row; the sums keep their sequential order)
+#pragma unroll 8
+  for (int64_t r = v0 + t; r < v1; r += 16) cs += *(const f32x4_t*)(W + r * XE + 4 * g);
+#pragma unroll 8
+  for (int64_t r = v0 + l; r < v1; r += 64) bs += bias[r];
+#pragma unroll
+  for (int off = 1; off < 16; off <<= 1)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) cs[e] += __shfl_xor(cs[e], off);
+  bs = wave_sum(bs);
+  if (t == 0) *(f32x4_t*)(wp + 4 * g) = cs;
+  if (l == 0) wp[XE] = bs;
+}
+
 template <int NG>
 __device__ __forceinline__ void xent_pass1_body(const float* __restrict__ H,
                                                 const float* __restrict__ W,
@@ -523,27 +547,239 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void xe
   const int tok0 = blockIdx.y * 16 * XG;
   const int ng = min(XG, max(0, (nv - tok0 + 15) / 16));
   const int64_t v0 = (int64_t)s * VS, v1 = min(V, v0 + VS);
-  if (blockIdx.y == 0) {          // column sums of [W | b] over the split
-    f32x4_t cs = {0.f, 0.f, 0.f, 0.f};
-    float bs = 0.f;
-    // (unrolled: 8 row loads in flight per lane, not one memory round trip
-    // per row; the sums keep their sequential order)
-#pragma unroll 8
-    for (int64_t r = v0 + t; r < v1; r += 16) cs += *(const f32x4_t*)(W + r * XE + 4 * g);
-#pragma unroll 8
-    for (int64_t r = v0 + l; r < v1; r += 64) bs += bias[r];
-#pragma unroll
-    for (int off = 1; off < 16; off <<= 1)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) cs[e] += __shfl_xor(cs[e], off);
-    bs = wave_sum(bs);
-    float* wp = wpart + (int64_t)s * (XE + 1);
-    if (t == 0) *(f32x4_t*)(wp + 4 * g) = cs;
-    if (l == 0) wp[XE] = bs;
-  }
+  if (blockIdx.y == 0) xent_colsums(W, bias, v0, v1, wpart + (int64_t)s * (XE + 1), t, g, l);
   switch (ng) {
 #define XCASE(n) \
     case n: xent_pass1_body<n>(H, W, bias, v0, v1, S, s, idx, nv, tok0, part, t, g); break;
+    XCASE(1) XCASE(2) XCASE(3) XCASE(4) XCASE(5) XCASE(6) XCASE(7) XCASE(8)
+#undef XCASE
+    default: break;
+  }
+}
+
+// ------------------------------------------------- 3-pass bf16 MFMA path --
+// Both products of the online softmax on v_mfma_f32_16x16x32_bf16 with every
+// fp32 operand split as x = hi + lo (hi = bf16(x), lo = bf16(x - hi)) and
+// a*b ~= ah*bh + al*bh + ah*bl: relative error ~2^-16 per product (fp32
+// accumulation), at 16 cycles per K=32 instruction instead of 32 per K=4 f32
+// one. The K=32 slots of a lane (8g..8g+7) are chosen so that no operand
+// crosses lanes: the contraction index of each slot only has to agree between
+// A and B.
+//   X = W H^T over a tile: slots {hi(e=4g+r), lo(e=4g+r)} of W row t against
+//     {hi(h), hi(h)} of token t, then {hi(e)} against {lo(h)}: 2 instructions.
+//   O^T += W^T P^T over a PAIR of tiles (a, b): slots {a: v=4g+r, b: v=4g+r}
+//     -- exactly the rows the lane's C fragments of X hold -- so P feeds the
+//     B operand straight from the X accumulators: 3 instructions (hh, lh, hl).
+__device__ __forceinline__ f32x4_t mfma32(bf16x8_t a, bf16x8_t b, f32x4_t c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ void bf_split(float x, __bf16& h, __bf16& l) {
+  h = (__bf16)x;
+  l = (__bf16)(x - (float)h);
+}
+
+struct XHop {                   // B operands of X for one 16-token group
+  bf16x8_t hh;                  // {hi(h[4g..4g+3]), hi(h[4g..4g+3])}
+  bf16x8_t lo;                  // {lo(h[4g..4g+3]), 0}
+};
+
+__device__ __forceinline__ XHop xhop_of(f32x4_t h) {
+  XHop o;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    __bf16 hi, lo;
+    bf_split(h[r], hi, lo);
+    o.hh[r] = hi;
+    o.hh[4 + r] = hi;
+    o.lo[r] = lo;
+    o.lo[4 + r] = (__bf16)0.f;
+  }
+  return o;
+}
+
+__device__ __forceinline__ bf16x8_t wsplit_a(f32x4_t w) {     // {hi(w), lo(w)}
+  bf16x8_t a;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    __bf16 hi, lo;
+    bf_split(w[r], hi, lo);
+    a[r] = hi;
+    a[4 + r] = lo;
+  }
+  return a;
+}
+
+// X for one tile and NG groups (bias as C input, log2 units)
+template <int NG>
+__device__ __forceinline__ void xent_x3_logits(bf16x8_t a, const float* bb, const XHop* hb,
+                                               f32x4_t* x) {
+#pragma unroll
+  for (int q = 0; q < NG; ++q) {
+    x[q] = (f32x4_t){bb[0], bb[1], bb[2], bb[3]};
+    x[q] = mfma32(a, hb[q].hh, x[q]);
+    x[q] = mfma32(a, hb[q].lo, x[q]);
+  }
+}
+
+// One PAIR of 16-row tiles of the online softmax (b may be a null tile:
+// W = 0, bias = -inf, so P = 0 there).
+template <int NG>
+__device__ __forceinline__ void xent_pass1_pair(const XentTile& A, const XentTile& B,
+                                                const float* bba, const float* bbb,
+                                                const XHop* hb, f32x4_t* o, float* m,
+                                                float* sum) {
+  f32x4_t xa[NG], xb[NG];
+  xent_x3_logits<NG>(wsplit_a(A.wa), bba, hb, xa);
+  xent_x3_logits<NG>(wsplit_a(B.wa), bbb, hb, xb);
+  bool up = false;
+#pragma unroll
+  for (int q = 0; q < NG; ++q) {
+    const float mx = fmaxf(fmaxf(fmaxf(xa[q][0], xa[q][1]), fmaxf(xa[q][2], xa[q][3])),
+                           fmaxf(fmaxf(xb[q][0], xb[q][1]), fmaxf(xb[q][2], xb[q][3])));
+    up |= mx > m[q] + XTH;
+  }
+  if (__any(up)) {                         // wave-uniform; first pair and rare after
+#pragma unroll
+    for (int q = 0; q < NG; ++q) {
+      const float mx =
+          max4rows(fmaxf(fmaxf(fmaxf(xa[q][0], xa[q][1]), fmaxf(xa[q][2], xa[q][3])),
+                         fmaxf(fmaxf(xb[q][0], xb[q][1]), fmaxf(xb[q][2], xb[q][3]))));
+      const float nm = fmaxf(m[q], mx);     // finite: row r0 of tile a is always valid
+      const float c = exp2_fast(m[q] - nm);
+      sum[q] *= c;
+      o[q] *= c;
+      m[q] = nm;
+    }
+  }
+  // A operands of O^T: W^T rows e = t over the pair's 8 vocab slots
+  bf16x8_t wh, wl;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    __bf16 h, l;
+    bf_split(A.wb[r], h, l);
+    wh[r] = h;
+    wl[r] = l;
+    bf_split(B.wb[r], h, l);
+    wh[4 + r] = h;
+    wl[4 + r] = l;
+  }
+#pragma unroll
+  for (int q = 0; q < NG; ++q) {
+    bf16x8_t ph, pl;
+    float pa[4], pb[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      pa[r] = exp2_fast(xa[q][r] - m[q]);
+      pb[r] = exp2_fast(xb[q][r] - m[q]);
+      __bf16 h, l;
+      bf_split(pa[r], h, l);
+      ph[r] = h;
+      pl[r] = l;
+      bf_split(pb[r], h, l);
+      ph[4 + r] = h;
+      pl[4 + r] = l;
+    }
+    sum[q] += ((pa[0] + pa[1]) + (pa[2] + pa[3])) + ((pb[0] + pb[1]) + (pb[2] + pb[3]));
+    o[q] = mfma32(wh, ph, o[q]);
+    o[q] = mfma32(wl, ph, o[q]);
+    o[q] = mfma32(wh, pl, o[q]);
+  }
+}
+
+__device__ __forceinline__ XentTile xent_null_tile() {
+  XentTile z;
+  z.wa = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    z.wb[r] = 0.f;
+    z.bb[r] = -INFINITY;
+  }
+  return z;
+}
+
+template <int NG>
+__device__ __forceinline__ void xent_pass1_x3_body(const float* __restrict__ H,
+                                                   const float* __restrict__ W,
+                                                   const float* __restrict__ bias, int64_t v0,
+                                                   int64_t v1, int S, int s,
+                                                   const int32_t* __restrict__ idx, int nv,
+                                                   int tok0, float* __restrict__ part, int t,
+                                                   int g) {
+  XHop hb[NG];
+  f32x4_t o[NG];
+  float m[NG], sum[NG];
+#pragma unroll
+  for (int q = 0; q < NG; ++q) {
+    const int j = tok0 + 16 * q + t;
+    f32x4_t h = {0.f, 0.f, 0.f, 0.f};
+    if (j < nv) h = *(const f32x4_t*)(H + (int64_t)idx[j] * XE + 4 * g) * LOG2E;
+    hb[q] = xhop_of(h);
+    o[q] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    m[q] = -INFINITY;
+    sum[q] = 0.f;
+  }
+  const int la = t * XE + 4 * g;
+  const int nfull = (int)((v1 - v0) / 16);
+  const float* Wt = W + v0 * XE;
+  const float* bt = bias + v0;
+  const XentTile null_tile = xent_null_tile();
+  XentTile ta = null_tile, tb = null_tile;
+  if (nfull > 0) xent_load_full(ta, Wt, bt, la, t, g);
+  if (nfull > 1) xent_load_full(tb, Wt + 16 * XE, bt + 16, la, t, g);
+  for (int i = 0; i < nfull; i += 2) {
+    const XentTile ca = ta;
+    const XentTile cb = i + 1 < nfull ? tb : null_tile;
+    if (i + 2 < nfull) xent_load_full(ta, Wt + (i + 2) * 16 * XE, bt + (i + 2) * 16, la, t, g);
+    if (i + 3 < nfull) xent_load_full(tb, Wt + (i + 3) * 16 * XE, bt + (i + 3) * 16, la, t, g);
+    float ba[4], bb[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      ba[r] = ca.bb[r] * LOG2E;
+      bb[r] = cb.bb[r] * LOG2E;            // (-inf stays -inf)
+    }
+    xent_pass1_pair<NG>(ca, cb, ba, bb, hb, o, m, sum);
+  }
+  const int64_t r0 = v0 + 16 * (int64_t)nfull;
+  if (r0 < v1) {                           // ragged last tile of the vocabulary
+    XentTile cur;
+    xent_load_tile(cur, W, bias, r0, v1, t, g);
+    float ba[4], bb[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      ba[r] = r0 + 4 * g + r < v1 ? cur.bb[r] * LOG2E : -INFINITY;
+      bb[r] = -INFINITY;
+    }
+    xent_pass1_pair<NG>(cur, null_tile, ba, bb, hb, o, m, sum);
+  }
+#pragma unroll
+  for (int q = 0; q < NG; ++q) {
+    const float tot = sum4rows(sum[q]);
+    const int j = tok0 + 16 * q + t;
+    if (j < nv) {
+      float* p = part + ((int64_t)j * S + s) * XP;
+      *(f32x4_t*)(p + 2 + 4 * g) = o[q];
+      if (g == 0) {
+        p[0] = m[q] * LN2;
+        p[1] = tot;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void xent_pass1_x3_kernel(
+    const float* __restrict__ H, const float* __restrict__ W, const float* __restrict__ bias,
+    int64_t V, int64_t VS, int S, const int32_t* __restrict__ idx,
+    const int32_t* __restrict__ count, float* __restrict__ part, float* __restrict__ wpart) {
+  const int s = blockIdx.x, l = threadIdx.x, t = l & 15, g = l >> 4;
+  const int nv = *count;
+  const int tok0 = blockIdx.y * 16 * XG;
+  const int ng = min(XG, max(0, (nv - tok0 + 15) / 16));
+  const int64_t v0 = (int64_t)s * VS, v1 = min(V, v0 + VS);
+  if (blockIdx.y == 0) xent_colsums(W, bias, v0, v1, wpart + (int64_t)s * (XE + 1), t, g, l);
+  switch (ng) {
+#define XCASE(n) \
+    case n: xent_pass1_x3_body<n>(H, W, bias, v0, v1, S, s, idx, nv, tok0, part, t, g); break;
     XCASE(1) XCASE(2) XCASE(3) XCASE(4) XCASE(5) XCASE(6) XCASE(7) XCASE(8)
 #undef XCASE
     default: break;
@@ -894,14 +1130,22 @@ __global__ __launch_bounds__(256) void xent_slab_reduce_kernel(int64_t V,
 
 }  // namespace
 
-int g_xent_impl = 1;           // 1: MFMA pass1/wgrad, 0: VALU kernels
+// 2: 3-pass bf16 MFMA (default), 1: f32 MFMA, 0: VALU kernels; TDFO_XENT_IMPL
+// picks another at load (A/B runs)
+static int xent_impl_env() {
+  const char* e = getenv("TDFO_XENT_IMPL");
+  if (e == nullptr || *e == 0) return 2;
+  const int v = atoi(e);
+  return v < 0 ? 0 : (v > 2 ? 2 : v);
+}
+int g_xent_impl = xent_impl_env();
 
 // VALU pass1: ~8 waves per SIMD (one wave per (split, 64-token chunk)).
 // MFMA pass1: ~2048 splits of whole 16-row tiles per 128-token block. The
 // number of valid tokens is device-side, so size for the capacity N.
 void linear_xent_splits(int N, int64_t V, int64_t* VS, int* S) {
   int64_t vs;
-  if (g_xent_impl == 1) {
+  if (g_xent_impl >= 1) {
     const int blocks = std::max(1, (N + 16 * XG - 1) / (16 * XG));
     const int64_t want = std::max(64, std::min(2048, 8192 / blocks));
     vs = std::max<int64_t>(16, (V + want - 1) / want);
@@ -917,7 +1161,7 @@ void linear_xent_splits(int N, int64_t V, int64_t* VS, int* S) {
 
 int linear_xent_impl(int impl) {
   const int old = g_xent_impl;
-  if (impl >= 0) g_xent_impl = impl ? 1 : 0;
+  if (impl >= 0) g_xent_impl = impl > 2 ? 2 : impl;
   return old;
 }
 
@@ -1007,7 +1251,10 @@ void linear_xent(const LinearXentArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(xent_compact_kernel, dim3(1), dim3(1024), 0, s, a.labels, a.N, a.ignore, idx,
                      count, a.dH, a.lossv);
   const int blocks = xent_blocks(a.N);
-  if (g_xent_impl == 1) {
+  if (g_xent_impl == 2) {
+    hipLaunchKernelGGL(xent_pass1_x3_kernel, dim3(S, blocks), dim3(64), 0, s, a.H, a.W, a.bias,
+                       a.V, VS, S, idx, count, part, wpart);
+  } else if (g_xent_impl == 1) {
     hipLaunchKernelGGL(xent_pass1_mfma_kernel, dim3(S, blocks), dim3(64), 0, s, a.H, a.W, a.bias,
                        a.V, VS, S, idx, count, part, wpart);
   } else {
@@ -1018,7 +1265,7 @@ void linear_xent(const LinearXentArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(xent_merge_kernel, dim3(a.N), dim3(256), 0, s, a.H, a.W, a.bias, a.labels,
                      a.V, S, a.eps, idx, count, part, wpart, lse, a.dH, a.lossv, htok, ytok);
   if (a.dW) {
-    if (g_xent_impl == 1) {
+    if (g_xent_impl >= 1) {
       const int64_t tiles = (a.V + 15) / 16;
       const int tpw = (int)std::max<int64_t>(1, (tiles + 4095) / 4096);
       hipLaunchKernelGGL(xent_wgrad_mfma_kernel,

@@ -256,8 +256,9 @@ def effective_segsort(segsort: int) -> int:
 
 
 def linear_xent_impl(p: int = -1) -> int:
-    """Fused Linear+CE kernel family: 1 f32-input MFMA (default), 0 VALU;
-    p < 0 only reads it. Returns the previous one."""
+    """Fused Linear+CE kernel family: 2 3-pass bf16 MFMA (default; env
+    TDFO_XENT_IMPL), 1 f32-input MFMA, 0 VALU; p < 0 only reads it. Returns
+    the previous one."""
     return int(_native().linear_xent_impl(p))
 
 

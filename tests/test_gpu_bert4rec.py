@@ -17,7 +17,7 @@ def _native():
     assert _ext.load(), "native library must load on the GPU box"
 
 
-@pytest.fixture(params=[1, 0], ids=["mfma", "valu"])
+@pytest.fixture(params=[2, 1, 0], ids=["mfma_x3", "mfma", "valu"])
 def xent_impl(request):
     old = ops.linear_xent_impl(request.param)
     yield request.param
