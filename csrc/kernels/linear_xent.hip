@@ -949,9 +949,114 @@ __device__ __forceinline__ void xent_wgrad_tile(const XentTok* K, f32x4_t wa, fl
   }
 }
 
+// 3-pass bf16 operands of the wgrad tile (see the pass1 x3 notes): X^T's A
+// is {hi, lo} of the token's H row; dW^T's A covers a PAIR of token groups,
+// slots {q: tok 4g+r, q+1: tok 4g+r} -- the rows the lane's dz fragments of
+// the two groups hold, so dz feeds the B operand from its own registers.
+template <int NG>
+struct XTok3 {
+  static constexpr int NP = (NG + 1) / 2;
+  bf16x8_t ha[NG];
+  bf16x8_t hbh[NP], hbl[NP];
+  float lse[NG][4];
+  int y[NG][4];
+};
+
+template <int NG>
+__device__ __forceinline__ void xtok3_of(XTok3<NG>& T, const XentTok* K) {
+#pragma unroll
+  for (int q = 0; q < NG; ++q) {
+    T.ha[q] = wsplit_a(K[q].ha);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      T.lse[q][r] = K[q].lse[r];
+      T.y[q][r] = K[q].y[r];
+    }
+  }
+#pragma unroll
+  for (int p = 0; p < XTok3<NG>::NP; ++p) {
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const int q = 2 * p + hh;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        __bf16 h = (__bf16)0.f, l = (__bf16)0.f;
+        if (q < NG) bf_split(K[q].hb[r], h, l);
+        T.hbh[p][4 * hh + r] = h;
+        T.hbl[p][4 * hh + r] = l;
+      }
+    }
+  }
+}
+
+template <int NG>
+__device__ __forceinline__ void xent_wgrad_tile3(const XTok3<NG>& K, f32x4_t wa, float b, int v,
+                                                 int64_t V, float off, float hit, float pad_off,
+                                                 float scale, float* __restrict__ dW,
+                                                 float* __restrict__ db, int g, const XOpt& xo,
+                                                 const XMom* mo = nullptr) {
+  bf16x8_t wh, wl;                         // B of X^T: {hi(w), hi(w)}, {lo(w), 0}
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    __bf16 h, l;
+    bf_split(wa[r], h, l);
+    wh[r] = h;
+    wh[4 + r] = h;
+    wl[r] = l;
+    wl[4 + r] = (__bf16)0.f;
+  }
+  f32x4_t dw[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  float dbs = 0.f;
+#pragma unroll
+  for (int p = 0; p < XTok3<NG>::NP; ++p) {
+    float dz[8];
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const int q = 2 * p + hh;
+      if (q < NG) {
+        f32x4_t x = {b, b, b, b};
+        x = mfma32(K.ha[q], wh, x);
+        x = mfma32(K.ha[q], wl, x);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float d = exp2_fast(x[r] - K.lse[q][r]) - off;
+          if (K.y[q][r] == v) d -= hit;
+          dz[4 * hh + r] = d;
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) dz[4 * hh + r] = 0.f;
+      }
+    }
+    dbs += ((dz[0] + dz[1]) + (dz[2] + dz[3])) + ((dz[4] + dz[5]) + (dz[6] + dz[7]));
+    bf16x8_t zh, zl;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      __bf16 h, l;
+      bf_split(dz[e], h, l);
+      zh[e] = h;
+      zl[e] = l;
+    }
+    f32x4_t& acc = dw[p & 1];
+    acc = mfma32(K.hbh[p], zh, acc);
+    acc = mfma32(K.hbl[p], zh, acc);
+    acc = mfma32(K.hbh[p], zl, acc);
+  }
+  dbs = (sum4rows(dbs) + pad_off) * scale;
+  if (v < V) {
+    if (xo.on) {                           // the complete gradient: step in place
+      if (mo != nullptr) xopt_row_pre(xo, v, 4 * g, wa, dw[0] + dw[1], g == 0, dbs, *mo);
+      else xopt_row(xo, v, 4 * g, wa, dw[0] + dw[1], g == 0, dbs);
+      return;
+    }
+    *(f32x4_t*)(dW + (int64_t)v * XE + 4 * g) = dw[0] + dw[1];
+    if (g == 0) db[v] = dbs;
+  }
+}
+
 // Full tiles read through a wave-uniform tile pointer + constant lane
 // offsets from a 2-slot register ring (two tiles per iteration).
-template <int NG>
+template <int NG, bool X3>
 __device__ __forceinline__ void xent_wgrad_body(const float* __restrict__ W,
                                                 const float* __restrict__ bias, int64_t V,
                                                 float eps, int64_t tile0, int tpw,
@@ -965,7 +1070,17 @@ __device__ __forceinline__ void xent_wgrad_body(const float* __restrict__ W,
   XentTok K[NG];
 #pragma unroll
   for (int q = 0; q < NG; ++q) xent_load_tok(K[q], htok, ytok, lse, tok0 + 16 * q, nv, scale, t, g);
+  XTok3<NG> K3;
+  if constexpr (X3) xtok3_of<NG>(K3, K);
   const float pad_off = (float)(16 * NG - min(nv - tok0, 16 * NG)) * off;
+  auto tile = [&](f32x4_t wa, float b, int v, const XMom* mo) {
+    if constexpr (X3)
+      xent_wgrad_tile3<NG>(K3, wa, b, v, V, off, hit, pad_off, scale, dW, db,
+                           g, xo, mo);
+    else
+      xent_wgrad_tile<NG>(K, wa, b, v, V, off, hit, pad_off, scale, dW, db, g,
+                          xo, mo);
+  };
   const int64_t tile1 = min(tile0 + tpw, V / 16);        // full tiles
   const int nfull = (int)max<int64_t>(0, tile1 - tile0);
   const int la = t * XE + 4 * g;
@@ -997,8 +1112,7 @@ __device__ __forceinline__ void xent_wgrad_body(const float* __restrict__ W,
         b0 = bt[(i + 2) * 16 + t];
         if (pre) mo0 = xopt_load(xo, vb + 16 * (i + 2), 4 * g, g == 0);
       }
-      xent_wgrad_tile<NG>(K, wa, b, vb + 16 * i, V, off, hit, pad_off, scale, dW, db, g, xo,
-                          pre ? &mo : nullptr);
+      tile(wa, b, vb + 16 * i, pre ? &mo : nullptr);
     }
     if (i + 1 < nfull) {
       const f32x4_t wa = wa1;
@@ -1009,22 +1123,21 @@ __device__ __forceinline__ void xent_wgrad_body(const float* __restrict__ W,
         b1 = bt[(i + 3) * 16 + t];
         if (pre) mo1 = xopt_load(xo, vb + 16 * (i + 3), 4 * g, g == 0);
       }
-      xent_wgrad_tile<NG>(K, wa, b, vb + 16 * (i + 1), V, off, hit, pad_off, scale, dW, db, g,
-                          xo, pre ? &mo : nullptr);
+      tile(wa, b, vb + 16 * (i + 1), pre ? &mo : nullptr);
     }
   }
   const int64_t rt = V / 16;                             // ragged last tile
   if (V % 16 != 0 && rt >= tile0 && rt < tile0 + tpw) {
     const int64_t vr = min(rt * 16 + t, V - 1);
     const f32x4_t wa = *(const f32x4_t*)(W + vr * XE + 4 * g);
-    xent_wgrad_tile<NG>(K, wa, bias[vr] * LOG2E, (int)(rt * 16) + t, V, off, hit, pad_off, scale,
-                        dW, db, g, xo);
+    tile(wa, bias[vr] * LOG2E, (int)(rt * 16) + t, nullptr);
   }
 }
 
 // grid (runs of `tpw` 16-row tiles, 128-token blocks). Block-row 0 writes
 // dW/db; block-row k > 0 writes slab k-1 ([V][16] + [V]), summed by
 // xent_slab_reduce_kernel — no atomics, fixed order.
+template <bool X3>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void xent_wgrad_mfma_kernel(const float* __restrict__ W,
                                                              const float* __restrict__ bias,
                                                              int64_t V, float eps, int tpw,
@@ -1055,7 +1168,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void xe
   switch (ng) {
 #define XCASE(n)                                                                            \
     case n:                                                                                 \
-      xent_wgrad_body<n>(W, bias, V, eps, tile0, tpw, htok, ytok, lse, nv, tok0, dWo, dbo, \
+      xent_wgrad_body<n, X3>(W, bias, V, eps, tile0, tpw, htok, ytok, lse, nv, tok0, dWo, dbo, \
                          t, g, xo);                                                         \
       break;
     XCASE(1) XCASE(2) XCASE(3) XCASE(4) XCASE(5) XCASE(6) XCASE(7) XCASE(8)
@@ -1268,9 +1381,13 @@ void linear_xent(const LinearXentArgs& a, hipStream_t s) {
     if (g_xent_impl >= 1) {
       const int64_t tiles = (a.V + 15) / 16;
       const int tpw = (int)std::max<int64_t>(1, (tiles + 4095) / 4096);
-      hipLaunchKernelGGL(xent_wgrad_mfma_kernel,
-                         dim3((unsigned)((tiles + tpw - 1) / tpw), blocks), dim3(64), 0, s, a.W,
-                         a.bias, a.V, a.eps, tpw, htok, ytok, count, lse, a.dW, a.db, slab, a);
+      const dim3 grid((unsigned)((tiles + tpw - 1) / tpw), blocks);
+      if (g_xent_impl == 2)
+        hipLaunchKernelGGL(xent_wgrad_mfma_kernel<true>, grid, dim3(64), 0, s, a.W, a.bias, a.V,
+                           a.eps, tpw, htok, ytok, count, lse, a.dW, a.db, slab, a);
+      else
+        hipLaunchKernelGGL(xent_wgrad_mfma_kernel<false>, grid, dim3(64), 0, s, a.W, a.bias, a.V,
+                           a.eps, tpw, htok, ytok, count, lse, a.dW, a.db, slab, a);
       if (blocks > 1 && a.loss) {
         hipLaunchKernelGGL(xent_tail_kernel, dim3(XT_SLAB_BLOCKS + 1), dim3(1024), 0, s, a.V,
                            count, slab, a.dW, a.db, a);
