@@ -633,18 +633,17 @@ __device__ __forceinline__ void xent_pass1_pair(const XentTile& A, const XentTil
   xent_x3_logits<NG>(wsplit_a(A.wa), bba, hb, xa);
   xent_x3_logits<NG>(wsplit_a(B.wa), bbb, hb, xb);
   bool up = false;
+  float mxl[NG];
 #pragma unroll
   for (int q = 0; q < NG; ++q) {
-    const float mx = fmaxf(fmaxf(fmaxf(xa[q][0], xa[q][1]), fmaxf(xa[q][2], xa[q][3])),
-                           fmaxf(fmaxf(xb[q][0], xb[q][1]), fmaxf(xb[q][2], xb[q][3])));
-    up |= mx > m[q] + XTH;
+    mxl[q] = fmaxf(fmaxf(fmaxf(xa[q][0], xa[q][1]), fmaxf(xa[q][2], xa[q][3])),
+                   fmaxf(fmaxf(xb[q][0], xb[q][1]), fmaxf(xb[q][2], xb[q][3])));
+    up |= mxl[q] > m[q] + XTH;
   }
   if (__any(up)) {                         // wave-uniform; first pair and rare after
 #pragma unroll
     for (int q = 0; q < NG; ++q) {
-      const float mx =
-          max4rows(fmaxf(fmaxf(fmaxf(xa[q][0], xa[q][1]), fmaxf(xa[q][2], xa[q][3])),
-                         fmaxf(fmaxf(xb[q][0], xb[q][1]), fmaxf(xb[q][2], xb[q][3]))));
+      const float mx = max4rows(mxl[q]);
       const float nm = fmaxf(m[q], mx);     // finite: row r0 of tile a is always valid
       const float c = exp2_fast(m[q] - nm);
       sum[q] *= c;
@@ -724,14 +723,29 @@ __device__ __forceinline__ void xent_pass1_x3_body(const float* __restrict__ H,
   const float* Wt = W + v0 * XE;
   const float* bt = bias + v0;
   const XentTile null_tile = xent_null_tile();
-  XentTile ta = null_tile, tb = null_tile;
+  // 4-tile register ring: the loads of pair i+2 are in flight for two pairs'
+  // work (one pair's was shorter than a loaded HBM round trip)
+  // (NG > 6: a 2-tile ring, the 4-tile one would spill)
+  constexpr int RD = NG <= 6 ? 4 : 2;
+  XentTile ta = null_tile, tb = null_tile, tc = null_tile, td = null_tile;
   if (nfull > 0) xent_load_full(ta, Wt, bt, la, t, g);
   if (nfull > 1) xent_load_full(tb, Wt + 16 * XE, bt + 16, la, t, g);
+  if constexpr (RD == 4) {
+    if (nfull > 2) xent_load_full(tc, Wt + 32 * XE, bt + 32, la, t, g);
+    if (nfull > 3) xent_load_full(td, Wt + 48 * XE, bt + 48, la, t, g);
+  }
   for (int i = 0; i < nfull; i += 2) {
     const XentTile ca = ta;
     const XentTile cb = i + 1 < nfull ? tb : null_tile;
-    if (i + 2 < nfull) xent_load_full(ta, Wt + (i + 2) * 16 * XE, bt + (i + 2) * 16, la, t, g);
-    if (i + 3 < nfull) xent_load_full(tb, Wt + (i + 3) * 16 * XE, bt + (i + 3) * 16, la, t, g);
+    if constexpr (RD == 4) {
+      ta = tc;
+      tb = td;
+    }
+    if (i + RD < nfull)
+      xent_load_full(RD == 4 ? tc : ta, Wt + (i + RD) * 16 * XE, bt + (i + RD) * 16, la, t, g);
+    if (i + RD + 1 < nfull)
+      xent_load_full(RD == 4 ? td : tb, Wt + (i + RD + 1) * 16 * XE, bt + (i + RD + 1) * 16, la,
+                     t, g);
     float ba[4], bb[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {

@@ -1,5 +1,11 @@
-# Random-row gather rate vs table size (floor under the embedding kernels).
+# Linear+CE x3: HEAD (pre) vs row-max reuse (slp) vs + no SLP packing (new).
 set -u
 O=gpurun_out/r06/ag; rm -rf $O; mkdir -p $O
-timeout -k 10 400 python -u labs/probes/random_rows.py > $O/random_rows.log 2>&1 || { echo "rc=$?"; tail -5 $O/random_rows.log; exit 1; }
-grep '^{' $O/random_rows.log
+TDFO_LIB_PATH=$PWD/labs/ab/libtdfo_hip_new.so timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_bert4rec.py > $O/tests.log 2>&1 || { echo "tests rc=$?"; tail -30 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+for k in 1 2; do
+for c in pre slp new; do
+TDFO_LIB_PATH=$PWD/labs/ab/libtdfo_hip_$c.so timeout -k 10 300 python -u scripts/bench_bert4rec.py > $O/b4r_${c}_$k.log 2>&1 || { echo "b4r rc=$?"; tail -5 $O/b4r_${c}_$k.log; exit 1; }
+TDFO_LIB_PATH=$PWD/labs/ab/libtdfo_hip_$c.so timeout -k 10 300 python -u scripts/bench_bert4rec.py --batch 256 > $O/b256_${c}_$k.log 2>&1 || { echo "b256 rc=$?"; tail -5 $O/b256_${c}_$k.log; exit 1; }
+echo "$c $k b16 $(tail -n 1 $O/b4r_${c}_$k.log | grep -o '"ms_per_step": [0-9.]*') b256 $(tail -n 1 $O/b256_${c}_$k.log | grep -o '"ms_per_step": [0-9.]*')"
+done; done

@@ -1,15 +1,11 @@
-# Non-temporal table-row reads/writes in the embedding update: isolated + step A/B.
+# Linear+CE x3 pass1: 4-tile register ring for NG <= 6 (new) vs 2-tile (pre).
 set -u
-O=gpurun_out/r06/ah; rm -rf $O; mkdir -p $O
-NT=$PWD/labs/ab/libtdfo_hip_nt.so
-TDFO_LIB_PATH=$NT timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_kernels.py -k "embedding" > $O/tests_nt.log 2>&1 || { echo "tests rc=$?"; tail -20 $O/tests_nt.log; exit 1; }
-tail -1 $O/tests_nt.log
+O=gpurun_out/r06/ah2; rm -rf $O; mkdir -p $O
+TDFO_LIB_PATH=$PWD/labs/ab/libtdfo_hip_new.so timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_bert4rec.py > $O/tests.log 2>&1 || { echo "tests rc=$?"; tail -30 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
 for k in 1 2; do
-for v in nt base; do
-L=""; [ $v = nt ] && L=$NT
-TDFO_LIB_PATH=$L timeout -k 10 300 python -u scripts/emb_iso.py > $O/iso_${v}_$k.log 2>&1 || { echo "iso rc=$?"; tail -5 $O/iso_${v}_$k.log; exit 1; }
-TDFO_LIB_PATH=$L timeout -k 10 300 python -u bench.py --model dcnv2 --steps 50 --warmup 10 > $O/dcn_${v}_$k.log 2>&1 || { echo "dcn rc=$?"; tail -5 $O/dcn_${v}_$k.log; exit 1; }
-TDFO_LIB_PATH=$L timeout -k 10 300 python -u bench.py --steps 300 --warmup 10 > $O/dlrm_${v}_$k.log 2>&1 || { echo "dlrm rc=$?"; tail -5 $O/dlrm_${v}_$k.log; exit 1; }
-echo "$v $k dcn $(tail -n 1 $O/dcn_${v}_$k.log | grep -o '"ms_per_step": [0-9.]*') dlrm $(tail -n 1 $O/dlrm_${v}_$k.log | grep -o '"ms_per_step": [0-9.]*')"
-grep -h "update\|chunk" $O/iso_${v}_$k.log | head -6
+for c in pre new; do
+TDFO_LIB_PATH=$PWD/labs/ab/libtdfo_hip_$c.so timeout -k 10 300 python -u scripts/bench_bert4rec.py > $O/b4r_${c}_$k.log 2>&1 || { echo "b4r rc=$?"; tail -5 $O/b4r_${c}_$k.log; exit 1; }
+TDFO_LIB_PATH=$PWD/labs/ab/libtdfo_hip_$c.so timeout -k 10 300 python -u scripts/bench_bert4rec.py --batch 256 > $O/b256_${c}_$k.log 2>&1 || { echo "b256 rc=$?"; tail -5 $O/b256_${c}_$k.log; exit 1; }
+echo "$c $k b16 $(tail -n 1 $O/b4r_${c}_$k.log | grep -o '"ms_per_step": [0-9.]*') b256 $(tail -n 1 $O/b256_${c}_$k.log | grep -o '"ms_per_step": [0-9.]*')"
 done; done
