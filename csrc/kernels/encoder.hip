@@ -59,8 +59,8 @@ enum { SITE_A = 1, SITE_F = 2, SITE_G = 3, SITE_BLK = 4 };
 struct POff {                    // parameter-gradient partial layout
   int wqkv, bqkv, wo, bo, g1, be1, g2, be2, w1, b1, w2, b2, P;
 };
-__host__ __device__ inline POff poff(int E, int FF) {
-  POff o;
+__host__ __device__ constexpr inline POff poff(int E, int FF) {
+  POff o{};
   o.wqkv = 0;
   o.bqkv = o.wqkv + 3 * E * E;
   o.wo = o.bqkv + 3 * E;
@@ -82,6 +82,7 @@ __host__ __device__ inline POff poff(int E, int FF) {
 struct WPtr {
   const float *wqkv, *bqkv, *wo, *bo, *g1, *be1, *g2, *be2, *w1, *b1, *w2, *b2;
 };
+template <int EC>
 __device__ __forceinline__ WPtr stage_weights(const EncArgs& a, const POff& po, float* w,
                                               int tid) {
   // Q / K / V projections from three separate tensors (a.wk != null: the
@@ -94,8 +95,28 @@ __device__ __forceinline__ WPtr stage_weights(const EncArgs& a, const POff& po, 
   const int off[17] = {po.wqkv, po.wqkv + EE, po.wqkv + 2 * EE, po.bqkv, po.bqkv + E,
                        po.bqkv + 2 * E, po.wo, po.bo, po.g1, po.be1, po.g2,
                        po.be2, po.w1, po.b1, po.w2, po.b2, po.P};
-  for (int q = 0; q < 16; ++q)
-    for (int i = tid; i < off[q + 1] - off[q]; i += ENC_THREADS) w[off[q] + i] = src[q][i];
+  // One flat pass over the whole layout: every thread's loads are issued
+  // before the first is waited for (16 loops of their own were 16 dependent
+  // memory round trips per launch).
+  constexpr int NPER = (poff(EC, 4 * EC).P + ENC_THREADS - 1) / ENC_THREADS;
+  float v[NPER];
+#pragma unroll
+  for (int k = 0; k < NPER; ++k) {
+    const int i = tid + k * ENC_THREADS;
+    v[k] = 0.f;
+    if (i < po.P) {
+      const float* p = src[0] + i;
+#pragma unroll
+      for (int q = 1; q < 16; ++q)
+        if (i >= off[q]) p = src[q] + (i - off[q]);
+      v[k] = *p;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < NPER; ++k) {
+    const int i = tid + k * ENC_THREADS;
+    if (i < po.P) w[i] = v[k];
+  }
   return {w + po.wqkv, w + po.bqkv, w + po.wo, w + po.bo, w + po.g1, w + po.be1,
           w + po.g2, w + po.be2, w + po.w1, w + po.b1, w + po.w2, w + po.b2};
 }
@@ -149,7 +170,7 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_fwd_kernel(EncArgs a) {
   float* ps = fs + T * FF;        // [H][T][T] scores -> P~
   int* kv = (int*)(ps + H * T * T);  // [T]   key valid
   const POff po = poff(E, FF);
-  const WPtr W = stage_weights(a, po, (float*)(kv + T), tid);
+  const WPtr W = stage_weights<E>(a, po, (float*)(kv + T), tid);
   const uint32_t step = a.step ? (uint32_t)a.step[0] : 0u;
   const uint32_t sd = (uint32_t)a.seed ^ (step * 0x632BE5ABu);
   const int64_t bo_te = (int64_t)b * T * E;
@@ -274,7 +295,7 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_bwd_kernel(EncArgs a) {
   float* ds = pt + H * T * T;     // [H][T][T] dS
   float* rdot = ds + H * T * T;   // [H][T]  sum_j P dP
   int* kv = (int*)(rdot + H * T);
-  const WPtr W = stage_weights(a, po, (float*)(kv + T), tid);
+  const WPtr W = stage_weights<E>(a, po, (float*)(kv + T), tid);
   const uint32_t step = a.step ? (uint32_t)a.step[0] : 0u;
   const uint32_t sd = (uint32_t)a.seed ^ (step * 0x632BE5ABu);
   const int64_t bo_te = (int64_t)b * T * E;

@@ -1,13 +1,11 @@
-# NT row accesses on multi-hot batches only (runtime choice): tests + DCN / DLRM A/B.
+# Encoder: batched weight staging (new) vs 16 dependent loops (pre).
 set -u
-O=gpurun_out/r06/${JOBTAG:-ai}; rm -rf $O; mkdir -p $O
-timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_kernels.py -k "embedding or dcn or cross" > $O/tests.log 2>&1 || { echo "tests rc=$?"; tail -20 $O/tests.log; exit 1; }
+O=gpurun_out/r06/ai; rm -rf $O; mkdir -p $O
+TDFO_LIB_PATH=$PWD/labs/ab/libtdfo_hip_new.so timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_bert4rec.py tests/test_gpu_kernels.py -k "bert4rec or encoder or xent" > $O/tests.log 2>&1 || { echo "tests rc=$?"; tail -30 $O/tests.log; exit 1; }
 tail -1 $O/tests.log
 for k in 1 2; do
-for v in 1 0; do
-TDFO_EMB_NT=$v timeout -k 10 300 python -u bench.py --model dcnv2 --steps 50 --warmup 10 > $O/dcn_${v}_$k.log 2>&1 || { echo "dcn rc=$?"; tail -5 $O/dcn_${v}_$k.log; exit 1; }
-TDFO_EMB_NT=$v timeout -k 10 300 python -u bench.py --model dcnv2 --steps 50 --warmup 10 --dist zipf > $O/dcnz_${v}_$k.log 2>&1 || { echo "dcnz rc=$?"; tail -5 $O/dcnz_${v}_$k.log; exit 1; }
-echo "nt=$v $k dcn $(tail -n 1 $O/dcn_${v}_$k.log | grep -o '"ms_per_step": [0-9.]*') zipf $(tail -n 1 $O/dcnz_${v}_$k.log | grep -o '"ms_per_step": [0-9.]*')"
+for c in pre new; do
+TDFO_LIB_PATH=$PWD/labs/ab/libtdfo_hip_$c.so timeout -k 10 300 python -u scripts/bench_bert4rec.py > $O/b4r_${c}_$k.log 2>&1 || { echo "b4r rc=$?"; tail -5 $O/b4r_${c}_$k.log; exit 1; }
+TDFO_LIB_PATH=$PWD/labs/ab/libtdfo_hip_$c.so timeout -k 10 300 python -u scripts/bench_bert4rec.py --batch 256 > $O/b256_${c}_$k.log 2>&1 || { echo "b256 rc=$?"; tail -5 $O/b256_${c}_$k.log; exit 1; }
+echo "$c $k b16 $(tail -n 1 $O/b4r_${c}_$k.log | grep -o '"ms_per_step": [0-9.]*') b256 $(tail -n 1 $O/b256_${c}_$k.log | grep -o '"ms_per_step": [0-9.]*')"
 done; done
-timeout -k 10 300 python -u scripts/emb_iso.py > $O/iso.log 2>&1 || { echo "iso rc=$?"; exit 1; }
-tail -2 $O/iso.log
