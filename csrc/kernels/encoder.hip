@@ -82,9 +82,51 @@ __host__ __device__ constexpr inline POff poff(int E, int FF) {
 struct WPtr {
   const float *wqkv, *bqkv, *wo, *bo, *g1, *be1, *g2, *be2, *w1, *b1, *w2, *b2;
 };
-template <int EC>
+// Global -> LDS copies of several arrays with every thread's loads (K per
+// array) issued before any is waited for: one memory round trip per
+// K * ENC_THREADS elements of the longest array, not one per array / per
+// loop iteration.
+struct Seg {
+  const float* src;
+  float* dst;
+  int n;
+};
+template <int NS, int K>
+__device__ __forceinline__ void stage_multi(const Seg (&sg)[NS], int tid) {
+  int nmax = 0;
+#pragma unroll
+  for (int q = 0; q < NS; ++q) nmax = max(nmax, sg[q].n);
+  auto batch = [&](int base) {
+    float v[NS][K];
+#pragma unroll
+    for (int q = 0; q < NS; ++q)
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int i = base + tid + k * ENC_THREADS;
+        v[q][k] = i < sg[q].n ? sg[q].src[i] : 0.f;
+      }
+#pragma unroll
+    for (int q = 0; q < NS; ++q)
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const int i = base + tid + k * ENC_THREADS;
+        if (i < sg[q].n) sg[q].dst[i] = v[q][k];
+      }
+  };
+  // (straight-line when one batch covers everything: a loop here made the
+  // compiler wait for the caller's outstanding loads at its entry)
+  if (nmax <= K * ENC_THREADS) {
+    batch(0);
+  } else {
+    for (int base = 0; base < nmax; base += K * ENC_THREADS) batch(base);
+  }
+}
+
+// mid() runs between the weight loads and their LDS stores: the caller's own
+// global -> LDS staging shares the same memory round trip.
+template <int EC, class Mid>
 __device__ __forceinline__ WPtr stage_weights(const EncArgs& a, const POff& po, float* w,
-                                              int tid) {
+                                              int tid, Mid&& mid) {
   // Q / K / V projections from three separate tensors (a.wk != null: the
   // module's own parameters, no concatenated copy per step) or one [3E, E]
   const int E = a.E, EE = E * E;
@@ -112,6 +154,7 @@ __device__ __forceinline__ WPtr stage_weights(const EncArgs& a, const POff& po, 
       v[k] = *p;
     }
   }
+  mid();
 #pragma unroll
   for (int k = 0; k < NPER; ++k) {
     const int i = tid + k * ENC_THREADS;
@@ -170,13 +213,15 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_fwd_kernel(EncArgs a) {
   float* ps = fs + T * FF;        // [H][T][T] scores -> P~
   int* kv = (int*)(ps + H * T * T);  // [T]   key valid
   const POff po = poff(E, FF);
-  const WPtr W = stage_weights<E>(a, po, (float*)(kv + T), tid);
-  const uint32_t step = a.step ? (uint32_t)a.step[0] : 0u;
-  const uint32_t sd = (uint32_t)a.seed ^ (step * 0x632BE5ABu);
   const int64_t bo_te = (int64_t)b * T * E;
-
-  for (int i = tid; i < T * E; i += ENC_THREADS) xs[i] = a.x[bo_te + i];
-  for (int i = tid; i < T; i += ENC_THREADS) kv[i] = a.ids[(int64_t)b * T + i] != a.pad_id;
+  const uint32_t step = a.step ? (uint32_t)a.step[0] : 0u;
+  const WPtr W = stage_weights<E>(a, po, (float*)(kv + T), tid, [&] {
+    const int64_t id = tid < T ? a.ids[(int64_t)b * T + tid] : 0;   // (T <= 64)
+    const Seg sg[1] = {{a.x + bo_te, xs, T * E}};
+    stage_multi<1, 8>(sg, tid);
+    if (tid < T) kv[tid] = id != a.pad_id;
+  });
+  const uint32_t sd = (uint32_t)a.seed ^ (step * 0x632BE5ABu);
   __syncthreads();
   ln_rows<E>(xs, hs, nullptr, nullptr, W.g1, W.be1, T, a.eps, tid);
   __syncthreads();
@@ -294,25 +339,37 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_bwd_kernel(EncArgs a) {
   float* pt = dq + T * E3;        // [H][T][T] dropped probabilities P~
   float* ds = pt + H * T * T;     // [H][T][T] dS
   float* rdot = ds + H * T * T;   // [H][T]  sum_j P dP
-  int* kv = (int*)(rdot + H * T);
-  const WPtr W = stage_weights<E>(a, po, (float*)(kv + T), tid);
-  const uint32_t step = a.step ? (uint32_t)a.step[0] : 0u;
-  const uint32_t sd = (uint32_t)a.seed ^ (step * 0x632BE5ABu);
+  float* x0s = rdot + H * T;      // [T][E]  layer input x0
+  int* kv = (int*)(x0s + T * E);
   const int64_t bo_te = (int64_t)b * T * E;
-
+  const uint32_t step = a.step ? (uint32_t)a.step[0] : 0u;
+  // the weights and every saved activation the block reads, staged in one
+  // round trip: dy (-> dxs), f (-> fs), x1 (LN2 input, -> hs), ctx (-> cs),
+  // qkv (-> qs), x0 (LN1 input, -> x0s), ids (-> key-valid flags)
+  const WPtr W = stage_weights<E>(a, po, (float*)(kv + T), tid, [&] {
+    const int64_t id = tid < T ? a.ids[(int64_t)b * T + tid] : 0;   // (T <= 64)
+    const Seg sg[6] = {{a.dy + bo_te, dxs, T * E},
+                       {a.f + (int64_t)b * T * FF, fs, T * FF},
+                       {a.x1 + bo_te, hs, T * E},
+                       {a.ctx + bo_te, cs, T * E},
+                       {a.qkv + (int64_t)b * T * E3, qs, T * E3},
+                       {a.x + bo_te, x0s, T * E}};
+    stage_multi<6, 8>(sg, tid);
+    if (tid < T) kv[tid] = id != a.pad_id;
+  });
+  const uint32_t sd = (uint32_t)a.seed ^ (step * 0x632BE5ABu);
+  __syncthreads();
   // block dropout, then the FFN residual: dx1 = dx2, dg = drop_g'(dx2)
   for (int o = tid; o < T * E; o += ENC_THREADS) {
     const int t = o / E, n = o - t * E;
-    const float d2 = a.dy[bo_te + o] * site_mul(a, sd, SITE_BLK, b, t, n);
+    const float d2 = dxs[o] * site_mul(a, sd, SITE_BLK, b, t, n);
     dxs[o] = d2;
     ts[o] = d2 * site_mul(a, sd, SITE_G, b, t, n);
   }
   for (int o = tid; o < T * FF; o += ENC_THREADS) {
     const int t = o / FF, n = o - t * FF;
-    fs[o] = a.f[(int64_t)b * T * FF + o] * site_mul(a, sd, SITE_F, b, t, n);
+    fs[o] *= site_mul(a, sd, SITE_F, b, t, n);
   }
-  for (int o = tid; o < T * E; o += ENC_THREADS) hs[o] = a.x1[bo_te + o];   // x1 (LN2 input)
-  for (int i = tid; i < T; i += ENC_THREADS) kv[i] = a.ids[(int64_t)b * T + i] != a.pad_id;
   __syncthreads();
   // W2 grads; dfd = dg W2 -> df (dropout f, ReLU mask); LN2 recompute
   for (int o = tid; o < E * FF; o += ENC_THREADS) {
@@ -332,8 +389,9 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_bwd_kernel(EncArgs a) {
     const int t = o / FF, k = o - t * FF;
     float s = 0.f;
     for (int n = 0; n < E; ++n) s = fmaf(ts[t * E + n], W.w2[n * FF + k], s);
-    const float fv = a.f[(int64_t)b * T * FF + o];
-    dfs[o] = fv > 0.f ? s * site_mul(a, sd, SITE_F, b, t, k) : 0.f;
+    // ReLU mask from the dropped f: f >= 0, and where the dropout multiplier
+    // is 0 (fs = 0 although f > 0) the product below is 0 anyway
+    dfs[o] = fs[o] > 0.f ? s * site_mul(a, sd, SITE_F, b, t, k) : 0.f;
   }
   ln_rows<E>(hs, nullptr, xh, rs, W.g2, W.be2, T, a.eps, tid);     // xhat2, rstd2
   __syncthreads();
@@ -374,8 +432,6 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_bwd_kernel(EncArgs a) {
     part[po.be2 + k] = sb;
   }
   ln_bwd_rows<E>(xh, rs, dh, W.g2, dxs, T, tid);                    // dx1 += LN2'(dh2)
-  for (int o = tid; o < T * E; o += ENC_THREADS) cs[o] = a.ctx[bo_te + o];
-  for (int o = tid; o < T * E3; o += ENC_THREADS) qs[o] = a.qkv[(int64_t)b * T * E3 + o];
   __syncthreads();
   // attention-out dropout; Wo grads; dctx = da Wo
   for (int o = tid; o < T * E; o += ENC_THREADS) {
@@ -458,9 +514,8 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_bwd_kernel(EncArgs a) {
     dq[i * E3 + 2 * E + c] = av;
   }
   // LN1 recompute from x0
-  for (int o = tid; o < T * E; o += ENC_THREADS) hs[o] = a.x[bo_te + o];
   __syncthreads();
-  ln_rows<E>(hs, nullptr, xh, rs, W.g1, W.be1, T, a.eps, tid);
+  ln_rows<E>(x0s, nullptr, xh, rs, W.g1, W.be1, T, a.eps, tid);
   __syncthreads();
   for (int o = tid; o < T * E; o += ENC_THREADS) {
     const int k = o % E;
@@ -510,7 +565,8 @@ __global__ __launch_bounds__(256) void enc_reduce_kernel(const float* __restrict
   const int c = blockIdx.x * 256 + threadIdx.x;
   if (c >= P) return;
   float s = 0.f;
-  for (int b = 0; b < B; ++b) s += part[(int64_t)b * P + c];
+#pragma unroll 16
+  for (int b = 0; b < B; ++b) s += part[(int64_t)b * P + c];   // (loads in flight together)
   grad[gidx ? gidx[c] : c] = s;
 }
 
@@ -521,7 +577,7 @@ size_t fwd_smem(const EncArgs& a) {
 
 size_t bwd_smem(const EncArgs& a) {
   const int T = a.T, E = a.E, FF = a.FF, H = a.H;
-  return (size_t)(T * E * 6 + T + 2 * T * FF + 2 * T * 3 * E + 2 * H * T * T + H * T + T +
+  return (size_t)(T * E * 7 + T + 2 * T * FF + 2 * T * 3 * E + 2 * H * T * T + H * T + T +
                   poff(E, FF).P) * 4;
 }
 
