@@ -28,7 +28,18 @@
 namespace tdfo {
 namespace {
 
-constexpr int ENC_THREADS = 256;
+// threads per sequence workgroup. E = 16 (the Bert4Rec config): backward at
+// 1024 (96 VGPRs), forward at 512 (~226 VGPRs, would spill at 1024) -- the
+// phases' element loops run in one or two passes instead of four or five
+// (measured vs 256: profiles/r06/notes.md); wider E keeps 256.
+#ifndef TDFO_ENC_FWD_THREADS
+#define TDFO_ENC_FWD_THREADS 512
+#endif
+#ifndef TDFO_ENC_BWD_THREADS
+#define TDFO_ENC_BWD_THREADS 1024
+#endif
+__host__ __device__ constexpr int enc_fwd_threads(int E) { return E == 16 ? TDFO_ENC_FWD_THREADS : 256; }
+__host__ __device__ constexpr int enc_bwd_threads(int E) { return E == 16 ? TDFO_ENC_BWD_THREADS : 256; }
 
 __device__ __forceinline__ uint32_t ehash3(uint32_t a, uint32_t b, uint32_t c) {
   // identical to attention.hip's hash3
@@ -84,14 +95,14 @@ struct WPtr {
 };
 // Global -> LDS copies of several arrays with every thread's loads (K per
 // array) issued before any is waited for: one memory round trip per
-// K * ENC_THREADS elements of the longest array, not one per array / per
+// K * NT elements of the longest array, not one per array / per
 // loop iteration.
 struct Seg {
   const float* src;
   float* dst;
   int n;
 };
-template <int NS, int K>
+template <int NT, int NS, int K>
 __device__ __forceinline__ void stage_multi(const Seg (&sg)[NS], int tid) {
   int nmax = 0;
 #pragma unroll
@@ -102,29 +113,29 @@ __device__ __forceinline__ void stage_multi(const Seg (&sg)[NS], int tid) {
     for (int q = 0; q < NS; ++q)
 #pragma unroll
       for (int k = 0; k < K; ++k) {
-        const int i = base + tid + k * ENC_THREADS;
+        const int i = base + tid + k * NT;
         v[q][k] = i < sg[q].n ? sg[q].src[i] : 0.f;
       }
 #pragma unroll
     for (int q = 0; q < NS; ++q)
 #pragma unroll
       for (int k = 0; k < K; ++k) {
-        const int i = base + tid + k * ENC_THREADS;
+        const int i = base + tid + k * NT;
         if (i < sg[q].n) sg[q].dst[i] = v[q][k];
       }
   };
   // (straight-line when one batch covers everything: a loop here made the
   // compiler wait for the caller's outstanding loads at its entry)
-  if (nmax <= K * ENC_THREADS) {
+  if (nmax <= K * NT) {
     batch(0);
   } else {
-    for (int base = 0; base < nmax; base += K * ENC_THREADS) batch(base);
+    for (int base = 0; base < nmax; base += K * NT) batch(base);
   }
 }
 
 // mid() runs between the weight loads and their LDS stores: the caller's own
 // global -> LDS staging shares the same memory round trip.
-template <int EC, class Mid>
+template <int NT, int EC, class Mid>
 __device__ __forceinline__ WPtr stage_weights(const EncArgs& a, const POff& po, float* w,
                                               int tid, Mid&& mid) {
   // Q / K / V projections from three separate tensors (a.wk != null: the
@@ -140,11 +151,11 @@ __device__ __forceinline__ WPtr stage_weights(const EncArgs& a, const POff& po, 
   // One flat pass over the whole layout: every thread's loads are issued
   // before the first is waited for (16 loops of their own were 16 dependent
   // memory round trips per launch).
-  constexpr int NPER = (poff(EC, 4 * EC).P + ENC_THREADS - 1) / ENC_THREADS;
+  constexpr int NPER = (poff(EC, 4 * EC).P + NT - 1) / NT;
   float v[NPER];
 #pragma unroll
   for (int k = 0; k < NPER; ++k) {
-    const int i = tid + k * ENC_THREADS;
+    const int i = tid + k * NT;
     v[k] = 0.f;
     if (i < po.P) {
       const float* p = src[0] + i;
@@ -157,7 +168,7 @@ __device__ __forceinline__ WPtr stage_weights(const EncArgs& a, const POff& po, 
   mid();
 #pragma unroll
   for (int k = 0; k < NPER; ++k) {
-    const int i = tid + k * ENC_THREADS;
+    const int i = tid + k * NT;
     if (i < po.P) w[i] = v[k];
   }
   return {w + po.wqkv, w + po.bqkv, w + po.wo, w + po.bo, w + po.g1, w + po.be1,
@@ -165,11 +176,11 @@ __device__ __forceinline__ WPtr stage_weights(const EncArgs& a, const POff& po, 
 }
 
 // y[t][:] = LN(x[t][:]) for t < T (one thread per row); optional xhat/rstd out
-template <int E>
+template <int NT, int E>
 __device__ __forceinline__ void ln_rows(const float* x, float* y, float* xhat, float* rstd_out,
                                         const float* g, const float* be, int T, float eps,
                                         int tid) {
-  for (int t = tid; t < T; t += ENC_THREADS) {
+  for (int t = tid; t < T; t += NT) {
     const float* xr = x + t * E;
     float m = 0.f;
     for (int k = 0; k < E; ++k) m += xr[k];
@@ -199,7 +210,8 @@ __device__ __forceinline__ float dotw(const float* in, const float* w) {
 }
 
 template <int E, int DK>
-__global__ __launch_bounds__(ENC_THREADS) void enc_fwd_kernel(EncArgs a) {
+__global__ __launch_bounds__(enc_fwd_threads(E)) void enc_fwd_kernel(EncArgs a) {
+  constexpr int ENC_FWD_THREADS = enc_fwd_threads(E);
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int b = blockIdx.x, tid = threadIdx.x;
   constexpr int FF = 4 * E, H = E / DK, dk = DK, E3 = 3 * E;
@@ -215,17 +227,17 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_fwd_kernel(EncArgs a) {
   const POff po = poff(E, FF);
   const int64_t bo_te = (int64_t)b * T * E;
   const uint32_t step = a.step ? (uint32_t)a.step[0] : 0u;
-  const WPtr W = stage_weights<E>(a, po, (float*)(kv + T), tid, [&] {
+  const WPtr W = stage_weights<ENC_FWD_THREADS, E>(a, po, (float*)(kv + T), tid, [&] {
     const int64_t id = tid < T ? a.ids[(int64_t)b * T + tid] : 0;   // (T <= 64)
     const Seg sg[1] = {{a.x + bo_te, xs, T * E}};
-    stage_multi<1, 8>(sg, tid);
+    stage_multi<ENC_FWD_THREADS, 1, 2048 / ENC_FWD_THREADS>(sg, tid);
     if (tid < T) kv[tid] = id != a.pad_id;
   });
   const uint32_t sd = (uint32_t)a.seed ^ (step * 0x632BE5ABu);
   __syncthreads();
-  ln_rows<E>(xs, hs, nullptr, nullptr, W.g1, W.be1, T, a.eps, tid);
+  ln_rows<ENC_FWD_THREADS, E>(xs, hs, nullptr, nullptr, W.g1, W.be1, T, a.eps, tid);
   __syncthreads();
-  for (int o = tid; o < T * E3; o += ENC_THREADS) {
+  for (int o = tid; o < T * E3; o += ENC_FWD_THREADS) {
     const int t = o / E3, n = o - t * E3;
     const float v = W.bqkv[n] + dotw<E>(hs + t * E, W.wqkv + n * E);
     qs[o] = v;
@@ -235,12 +247,12 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_fwd_kernel(EncArgs a) {
   // attention, element-parallel: scores [H][T][T] -> row softmax with the
   // dropout multiplier folded in (P~) -> ctx = P~ V
   const float scale = rsqrtf((float)dk);
-  for (int e = tid; e < H * T * T; e += ENC_THREADS) {
+  for (int e = tid; e < H * T * T; e += ENC_FWD_THREADS) {
     const int h = e / (T * T), r = e - h * T * T, i = r / T, j = r - i * T;
     ps[e] = kv[j] ? dotw<DK>(qs + i * E3 + h * dk, qs + j * E3 + E + h * dk) * scale : -1e9f;
   }
   __syncthreads();
-  for (int u = tid; u < H * T; u += ENC_THREADS) {
+  for (int u = tid; u < H * T; u += ENC_FWD_THREADS) {
     float* row = ps + u * T;
     float mx = -3.0e38f;
     #pragma unroll 4
@@ -257,12 +269,12 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_fwd_kernel(EncArgs a) {
     for (int j = 0; j < T; ++j) row[j] *= inv;
   }
   __syncthreads();
-  for (int e = tid; e < H * T * T; e += ENC_THREADS) {
+  for (int e = tid; e < H * T * T; e += ENC_FWD_THREADS) {
     const int h = e / (T * T), r = e - h * T * T, i = r / T, j = r - i * T;
     ps[e] *= prob_mul(a, sd, b, h, i, j);
   }
   __syncthreads();
-  for (int o = tid; o < T * E; o += ENC_THREADS) {
+  for (int o = tid; o < T * E; o += ENC_FWD_THREADS) {
     const int i = o / E, c = o - i * E, h = c / dk;
     const float* prow = ps + (h * T + i) * T;
     float acc = 0.f;
@@ -271,7 +283,7 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_fwd_kernel(EncArgs a) {
     cs[o] = acc;
   }
   __syncthreads();
-  for (int o = tid; o < T * E; o += ENC_THREADS) {
+  for (int o = tid; o < T * E; o += ENC_FWD_THREADS) {
     a.ctx[bo_te + o] = cs[o];
     const int t = o / E, n = o - t * E;
     const float v = W.bo[n] + dotw<E>(cs + t * E, W.wo + n * E);
@@ -280,16 +292,16 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_fwd_kernel(EncArgs a) {
     a.x1[bo_te + o] = x1;
   }
   __syncthreads();
-  ln_rows<E>(x1s, hs, nullptr, nullptr, W.g2, W.be2, T, a.eps, tid);
+  ln_rows<ENC_FWD_THREADS, E>(x1s, hs, nullptr, nullptr, W.g2, W.be2, T, a.eps, tid);
   __syncthreads();
-  for (int o = tid; o < T * FF; o += ENC_THREADS) {
+  for (int o = tid; o < T * FF; o += ENC_FWD_THREADS) {
     const int t = o / FF, n = o - t * FF;
     const float v = fmaxf(W.b1[n] + dotw<E>(hs + t * E, W.w1 + n * E), 0.f);
     a.f[(int64_t)b * T * FF + o] = v;
     fs[o] = v * site_mul(a, sd, SITE_F, b, t, n);
   }
   __syncthreads();
-  for (int o = tid; o < T * E; o += ENC_THREADS) {
+  for (int o = tid; o < T * E; o += ENC_FWD_THREADS) {
     const int t = o / E, n = o - t * E;
     const float g = W.b2[n] + dotw<FF>(fs + t * FF, W.w2 + n * FF);
     const float x2 = x1s[o] + g * site_mul(a, sd, SITE_G, b, t, n);
@@ -298,10 +310,10 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_fwd_kernel(EncArgs a) {
 }
 
 // LN backward for T rows: dx (+)= LN'(dh); per-column dgamma/dbeta partials
-template <int E>
+template <int NT, int E>
 __device__ __forceinline__ void ln_bwd_rows(const float* xhat, const float* rstd, const float* dh,
                                             const float* g, float* dx, int T, int tid) {
-  for (int t = tid; t < T; t += ENC_THREADS) {
+  for (int t = tid; t < T; t += NT) {
     float m1 = 0.f, m2 = 0.f;
     for (int k = 0; k < E; ++k) {
       const float dxh = dh[t * E + k] * g[k];
@@ -318,7 +330,8 @@ __device__ __forceinline__ void ln_bwd_rows(const float* xhat, const float* rstd
 }
 
 template <int E, int DK>
-__global__ __launch_bounds__(ENC_THREADS) void enc_bwd_kernel(EncArgs a) {
+__global__ __launch_bounds__(enc_bwd_threads(E)) void enc_bwd_kernel(EncArgs a) {
+  constexpr int ENC_BWD_THREADS = enc_bwd_threads(E);
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int b = blockIdx.x, tid = threadIdx.x;
   constexpr int FF = 4 * E, H = E / DK, dk = DK, E3 = 3 * E;
@@ -346,7 +359,7 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_bwd_kernel(EncArgs a) {
   // the weights and every saved activation the block reads, staged in one
   // round trip: dy (-> dxs), f (-> fs), x1 (LN2 input, -> hs), ctx (-> cs),
   // qkv (-> qs), x0 (LN1 input, -> x0s), ids (-> key-valid flags)
-  const WPtr W = stage_weights<E>(a, po, (float*)(kv + T), tid, [&] {
+  const WPtr W = stage_weights<ENC_BWD_THREADS, E>(a, po, (float*)(kv + T), tid, [&] {
     const int64_t id = tid < T ? a.ids[(int64_t)b * T + tid] : 0;   // (T <= 64)
     const Seg sg[6] = {{a.dy + bo_te, dxs, T * E},
                        {a.f + (int64_t)b * T * FF, fs, T * FF},
@@ -354,38 +367,38 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_bwd_kernel(EncArgs a) {
                        {a.ctx + bo_te, cs, T * E},
                        {a.qkv + (int64_t)b * T * E3, qs, T * E3},
                        {a.x + bo_te, x0s, T * E}};
-    stage_multi<6, 8>(sg, tid);
+    stage_multi<ENC_BWD_THREADS, 6, 2048 / ENC_BWD_THREADS>(sg, tid);
     if (tid < T) kv[tid] = id != a.pad_id;
   });
   const uint32_t sd = (uint32_t)a.seed ^ (step * 0x632BE5ABu);
   __syncthreads();
   // block dropout, then the FFN residual: dx1 = dx2, dg = drop_g'(dx2)
-  for (int o = tid; o < T * E; o += ENC_THREADS) {
+  for (int o = tid; o < T * E; o += ENC_BWD_THREADS) {
     const int t = o / E, n = o - t * E;
     const float d2 = dxs[o] * site_mul(a, sd, SITE_BLK, b, t, n);
     dxs[o] = d2;
     ts[o] = d2 * site_mul(a, sd, SITE_G, b, t, n);
   }
-  for (int o = tid; o < T * FF; o += ENC_THREADS) {
+  for (int o = tid; o < T * FF; o += ENC_BWD_THREADS) {
     const int t = o / FF, n = o - t * FF;
     fs[o] *= site_mul(a, sd, SITE_F, b, t, n);
   }
   __syncthreads();
   // W2 grads; dfd = dg W2 -> df (dropout f, ReLU mask); LN2 recompute
-  for (int o = tid; o < E * FF; o += ENC_THREADS) {
+  for (int o = tid; o < E * FF; o += ENC_BWD_THREADS) {
     const int n = o / FF, k = o - n * FF;
     float s = 0.f;
     #pragma unroll 4
     for (int t = 0; t < T; ++t) s = fmaf(ts[t * E + n], fs[t * FF + k], s);
     part[po.w2 + o] = s;
   }
-  for (int n = tid; n < E; n += ENC_THREADS) {
+  for (int n = tid; n < E; n += ENC_BWD_THREADS) {
     float s = 0.f;
     #pragma unroll 4
     for (int t = 0; t < T; ++t) s += ts[t * E + n];
     part[po.b2 + n] = s;
   }
-  for (int o = tid; o < T * FF; o += ENC_THREADS) {
+  for (int o = tid; o < T * FF; o += ENC_BWD_THREADS) {
     const int t = o / FF, k = o - t * FF;
     float s = 0.f;
     for (int n = 0; n < E; ++n) s = fmaf(ts[t * E + n], W.w2[n * FF + k], s);
@@ -393,35 +406,35 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_bwd_kernel(EncArgs a) {
     // is 0 (fs = 0 although f > 0) the product below is 0 anyway
     dfs[o] = fs[o] > 0.f ? s * site_mul(a, sd, SITE_F, b, t, k) : 0.f;
   }
-  ln_rows<E>(hs, nullptr, xh, rs, W.g2, W.be2, T, a.eps, tid);     // xhat2, rstd2
+  ln_rows<ENC_BWD_THREADS, E>(hs, nullptr, xh, rs, W.g2, W.be2, T, a.eps, tid);     // xhat2, rstd2
   __syncthreads();
-  for (int o = tid; o < T * E; o += ENC_THREADS) {
+  for (int o = tid; o < T * E; o += ENC_BWD_THREADS) {
     const int k = o % E;
     hs[o] = xh[o] * W.g2[k] + W.be2[k];                             // h2
   }
   __syncthreads();
   // W1 grads; dh2 = df W1
-  for (int o = tid; o < FF * E; o += ENC_THREADS) {
+  for (int o = tid; o < FF * E; o += ENC_BWD_THREADS) {
     const int n = o / E, k = o - n * E;
     float s = 0.f;
     #pragma unroll 4
     for (int t = 0; t < T; ++t) s = fmaf(dfs[t * FF + n], hs[t * E + k], s);
     part[po.w1 + o] = s;
   }
-  for (int n = tid; n < FF; n += ENC_THREADS) {
+  for (int n = tid; n < FF; n += ENC_BWD_THREADS) {
     float s = 0.f;
     #pragma unroll 4
     for (int t = 0; t < T; ++t) s += dfs[t * FF + n];
     part[po.b1 + n] = s;
   }
-  for (int o = tid; o < T * E; o += ENC_THREADS) {
+  for (int o = tid; o < T * E; o += ENC_BWD_THREADS) {
     const int t = o / E, k = o - t * E;
     float s = 0.f;
     for (int n = 0; n < FF; ++n) s = fmaf(dfs[t * FF + n], W.w1[n * E + k], s);
     dh[o] = s;
   }
   __syncthreads();
-  for (int k = tid; k < E; k += ENC_THREADS) {
+  for (int k = tid; k < E; k += ENC_BWD_THREADS) {
     float sg = 0.f, sb = 0.f;
     #pragma unroll 4
     for (int t = 0; t < T; ++t) {
@@ -431,29 +444,29 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_bwd_kernel(EncArgs a) {
     part[po.g2 + k] = sg;
     part[po.be2 + k] = sb;
   }
-  ln_bwd_rows<E>(xh, rs, dh, W.g2, dxs, T, tid);                    // dx1 += LN2'(dh2)
+  ln_bwd_rows<ENC_BWD_THREADS, E>(xh, rs, dh, W.g2, dxs, T, tid);                    // dx1 += LN2'(dh2)
   __syncthreads();
   // attention-out dropout; Wo grads; dctx = da Wo
-  for (int o = tid; o < T * E; o += ENC_THREADS) {
+  for (int o = tid; o < T * E; o += ENC_BWD_THREADS) {
     const int t = o / E, n = o - t * E;
     ts[o] = dxs[o] * site_mul(a, sd, SITE_A, b, t, n);
   }
   __syncthreads();
-  for (int o = tid; o < E * E; o += ENC_THREADS) {
+  for (int o = tid; o < E * E; o += ENC_BWD_THREADS) {
     const int n = o / E, k = o - n * E;
     float s = 0.f;
     #pragma unroll 4
     for (int t = 0; t < T; ++t) s = fmaf(ts[t * E + n], cs[t * E + k], s);
     part[po.wo + o] = s;
   }
-  for (int n = tid; n < E; n += ENC_THREADS) {
+  for (int n = tid; n < E; n += ENC_BWD_THREADS) {
     float s = 0.f;
     #pragma unroll 4
     for (int t = 0; t < T; ++t) s += ts[t * E + n];
     part[po.bo + n] = s;
   }
   __syncthreads();
-  for (int o = tid; o < T * E; o += ENC_THREADS) {
+  for (int o = tid; o < T * E; o += ENC_BWD_THREADS) {
     const int t = o / E, k = o - t * E;
     float s = 0.f;
     for (int n = 0; n < E; ++n) s = fmaf(ts[t * E + n], W.wo[n * E + k], s);
@@ -462,14 +475,14 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_bwd_kernel(EncArgs a) {
   __syncthreads();
   // attention backward, element-parallel over [H][T][T] and [T][E]
   const float scale = rsqrtf((float)dk);
-  for (int e = tid; e < H * T * T; e += ENC_THREADS) {
+  for (int e = tid; e < H * T * T; e += ENC_BWD_THREADS) {
     const int h = e / (T * T), r = e - h * T * T, i = r / T, j = r - i * T;
     pt[e] = kv[j] ? dotw<DK>(qs + i * E3 + h * dk, qs + j * E3 + E + h * dk) * scale : -1e9f;
     ds[e] = prob_mul(a, sd, b, h, i, j) *
             dotw<DK>(cs + i * E + h * dk, qs + j * E3 + 2 * E + h * dk);          // dP
   }
   __syncthreads();
-  for (int u = tid; u < H * T; u += ENC_THREADS) {       // P rows, rowdot = sum_j P dP
+  for (int u = tid; u < H * T; u += ENC_BWD_THREADS) {       // P rows, rowdot = sum_j P dP
     float* prow = pt + u * T;
     const float* drow = ds + u * T;
     float mx = -3.0e38f;
@@ -492,7 +505,7 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_bwd_kernel(EncArgs a) {
     rdot[u] = dot;
   }
   __syncthreads();
-  for (int e = tid; e < H * T * T; e += ENC_THREADS) {   // dS; P -> P~
+  for (int e = tid; e < H * T * T; e += ENC_BWD_THREADS) {   // dS; P -> P~
     const int h = e / (T * T), r = e - h * T * T, i = r / T, j = r - i * T;
     const float p = pt[e];
     // masked keys hold a constant score (masked_fill): no gradient through them
@@ -500,7 +513,7 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_bwd_kernel(EncArgs a) {
     pt[e] = p * prob_mul(a, sd, b, h, i, j);
   }
   __syncthreads();
-  for (int o = tid; o < T * E; o += ENC_THREADS) {       // dq, dk, dv
+  for (int o = tid; o < T * E; o += ENC_BWD_THREADS) {       // dq, dk, dv
     const int i = o / E, c = o - i * E, h = c / dk;
     float aq = 0.f, ak = 0.f, av = 0.f;
     #pragma unroll 4
@@ -515,35 +528,35 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_bwd_kernel(EncArgs a) {
   }
   // LN1 recompute from x0
   __syncthreads();
-  ln_rows<E>(x0s, nullptr, xh, rs, W.g1, W.be1, T, a.eps, tid);
+  ln_rows<ENC_BWD_THREADS, E>(x0s, nullptr, xh, rs, W.g1, W.be1, T, a.eps, tid);
   __syncthreads();
-  for (int o = tid; o < T * E; o += ENC_THREADS) {
+  for (int o = tid; o < T * E; o += ENC_BWD_THREADS) {
     const int k = o % E;
     hs[o] = xh[o] * W.g1[k] + W.be1[k];                             // h1
   }
   __syncthreads();
   // Wqkv grads; dh1 = dqkv Wqkv
-  for (int o = tid; o < E3 * E; o += ENC_THREADS) {
+  for (int o = tid; o < E3 * E; o += ENC_BWD_THREADS) {
     const int n = o / E, k = o - n * E;
     float s = 0.f;
     #pragma unroll 4
     for (int t = 0; t < T; ++t) s = fmaf(dq[t * E3 + n], hs[t * E + k], s);
     part[po.wqkv + o] = s;
   }
-  for (int n = tid; n < E3; n += ENC_THREADS) {
+  for (int n = tid; n < E3; n += ENC_BWD_THREADS) {
     float s = 0.f;
     #pragma unroll 4
     for (int t = 0; t < T; ++t) s += dq[t * E3 + n];
     part[po.bqkv + n] = s;
   }
-  for (int o = tid; o < T * E; o += ENC_THREADS) {
+  for (int o = tid; o < T * E; o += ENC_BWD_THREADS) {
     const int t = o / E, k = o - t * E;
     float s = 0.f;
     for (int n = 0; n < E3; ++n) s = fmaf(dq[t * E3 + n], W.wqkv[n * E + k], s);
     dh[o] = s;
   }
   __syncthreads();
-  for (int k = tid; k < E; k += ENC_THREADS) {
+  for (int k = tid; k < E; k += ENC_BWD_THREADS) {
     float sg = 0.f, sb = 0.f;
     #pragma unroll 4
     for (int t = 0; t < T; ++t) {
@@ -553,9 +566,9 @@ __global__ __launch_bounds__(ENC_THREADS) void enc_bwd_kernel(EncArgs a) {
     part[po.g1 + k] = sg;
     part[po.be1 + k] = sb;
   }
-  ln_bwd_rows<E>(xh, rs, dh, W.g1, dxs, T, tid);                    // dx0 = dx1 + LN1'(dh1)
+  ln_bwd_rows<ENC_BWD_THREADS, E>(xh, rs, dh, W.g1, dxs, T, tid);                    // dx0 = dx1 + LN1'(dh1)
   __syncthreads();
-  for (int o = tid; o < T * E; o += ENC_THREADS) a.dx[bo_te + o] = dxs[o];
+  for (int o = tid; o < T * E; o += ENC_BWD_THREADS) a.dx[bo_te + o] = dxs[o];
 }
 
 // grad[c] = sum_b part[b][c], fixed order
@@ -606,8 +619,8 @@ void launch(const EncArgs& a, size_t sm, hipStream_t s) {
                                          160 * 1024));                                     \
       attr = true;                                                                         \
     }                                                                                      \
-    if (BWD) hipLaunchKernelGGL((enc_bwd_kernel<EE, DD>), dim3(a.B), dim3(ENC_THREADS), sm, s, a); \
-    else hipLaunchKernelGGL((enc_fwd_kernel<EE, DD>), dim3(a.B), dim3(ENC_THREADS), sm, s, a);     \
+    if (BWD) hipLaunchKernelGGL((enc_bwd_kernel<EE, DD>), dim3(a.B), dim3(enc_bwd_threads(EE)), sm, s, a); \
+    else hipLaunchKernelGGL((enc_fwd_kernel<EE, DD>), dim3(a.B), dim3(enc_fwd_threads(EE)), sm, s, a);     \
     return;                                                                                \
   }
   TDFO_ENC(16, 4) TDFO_ENC(16, 8) TDFO_ENC(16, 16)

@@ -1,11 +1,8 @@
-# DLRM: batch load folded into the fused bottom-MLP launch; A/B on the headline.
+# PMC pass on the 3-pass bf16 Linear+CE kernels.
 set -u
 O=gpurun_out/r06/af; rm -rf $O; mkdir -p $O
-timeout -k 10 500 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_kernels.py tests/test_gpu_instep.py tests/test_gpu_comm.py -k "bottom or dlrm or stream or instep or graph or batch" > $O/tests.log 2>&1 || { echo "tests rc=$?"; tail -30 $O/tests.log; exit 1; }
-tail -1 $O/tests.log
-for k in 1 2; do
-for v in 1 0; do
-TDFO_BOT_LOAD_FOLD=$v timeout -k 10 300 python -u bench.py --steps 300 --warmup 10 > $O/b300_${v}_$k.log 2>&1 || { echo "bench rc=$?"; tail -5 $O/b300_${v}_$k.log; exit 1; }
-TDFO_BOT_LOAD_FOLD=$v timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > $O/drv_${v}_$k.log 2>&1 || { echo "drv rc=$?"; tail -5 $O/drv_${v}_$k.log; exit 1; }
-echo "fold=$v $k 300: $(tail -n 1 $O/b300_${v}_$k.log | grep -o '"ms_per_step": [0-9.]*') drv: $(tail -n 1 $O/drv_${v}_$k.log | grep -o '"ms_per_step": [0-9.]*')"
-done; done
+ROOT=$GRAFT_REPO_ROOT
+cd /tmp && export TMPDIR=/tmp
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU GRBM_GUI_ACTIVE --kernel-include-regex "xent_(pass1|wgrad|merge)" --output-format csv -d $ROOT/$O/pmc1 -o p -- python3 $ROOT/scripts/bench_bert4rec.py --steps 20 --warmup 5 --no-graph > $ROOT/$O/pmc1.log 2>&1 || { echo "pmc1 rc=$?"; tail -5 $ROOT/$O/pmc1.log; exit 1; }
+timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_INSTS_MFMA SQ_WAVES FETCH_SIZE --kernel-include-regex "xent_(pass1|wgrad|merge)" --output-format csv -d $ROOT/$O/pmc2 -o p -- python3 $ROOT/scripts/bench_bert4rec.py --steps 20 --warmup 5 --no-graph > $ROOT/$O/pmc2.log 2>&1 || { echo "pmc2 rc=$?"; tail -5 $ROOT/$O/pmc2.log; exit 1; }
+echo done

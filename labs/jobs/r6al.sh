@@ -1,11 +1,16 @@
-# DLRM: top MLP's optimizer part as side blocks of the first bottom backward pair.
+# Bert4Rec kernel tables (B=16 and B=256) after the round-6 Linear+CE / encoder work.
 set -u
 O=gpurun_out/r06/al; rm -rf $O; mkdir -p $O
-timeout -k 10 500 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_kernels.py -k "dlrm or head or optim or dense" > $O/tests.log 2>&1 || { echo "tests rc=$?"; tail -30 $O/tests.log; exit 1; }
-tail -1 $O/tests.log
-for k in 1 2; do
-for v in 1 0; do
-TDFO_OPT_SIDE=$v timeout -k 10 300 python -u bench.py --steps 300 --warmup 10 > $O/b300_${v}_$k.log 2>&1 || { echo "bench rc=$?"; tail -5 $O/b300_${v}_$k.log; exit 1; }
-TDFO_OPT_SIDE=$v timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > $O/drv_${v}_$k.log 2>&1 || { echo "drv rc=$?"; tail -5 $O/drv_${v}_$k.log; exit 1; }
-echo "side=$v $k 300: $(tail -n 1 $O/b300_${v}_$k.log | grep -o '"ms_per_step": [0-9.]*') drv: $(tail -n 1 $O/drv_${v}_$k.log | grep -o '"ms_per_step": [0-9.]*')"
-done; done
+ROOT=$GRAFT_REPO_ROOT
+for bs in 16 256; do
+timeout -k 10 300 python -u scripts/bench_bert4rec.py --batch $bs > $O/b$bs.log 2>&1 || { echo "b$bs rc=$?"; exit 1; }
+echo "B=$bs $(tail -n 1 $O/b$bs.log)"
+done
+cd /tmp && export TMPDIR=/tmp
+for bs in 16 256; do
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $ROOT/$O/prof$bs -o b4r -- python3 $ROOT/scripts/bench_bert4rec.py --steps 200 --batch $bs > $ROOT/$O/prof$bs.log 2>&1 || { echo "prof rc=$?"; tail -5 $ROOT/$O/prof$bs.log; exit 1; }
+done
+cd $ROOT
+for bs in 16 256; do
+python scripts/prof_summary.py $(ls $O/prof$bs/*kernel_trace.csv | head -1) --marker xent_pass1 --last 100 > $O/summary_b$bs.txt; cat $O/summary_b$bs.txt
+done
