@@ -335,7 +335,7 @@ void encoder_layer_bwd(const Tensor& x, const Tensor& ids, const c10::optional<T
                        at::TensorList params, int64_t H, double rate, int64_t seed,
                        int64_t pad_id, double eps, at::TensorList saved, const Tensor& dy,
                        const Tensor& dx, const Tensor& part, const Tensor& grad,
-                       const c10::optional<Tensor>& gidx) {
+                       const c10::optional<Tensor>& gidx, bool defer) {
   auto a = enc_args(x, ids, step, params, H, rate, seed, pad_id, eps, saved);
   check_f32c(dy, "dy"); check_f32c(dx, "dx"); check_f32c(part, "part"); check_f32c(grad, "grad");
   const int64_t P = tdfo::encoder_param_count(a.E, a.FF);
@@ -351,8 +351,10 @@ void encoder_layer_bwd(const Tensor& x, const Tensor& ids, const c10::optional<T
                 "encoder_layer: gidx int64 [P]");
     gi = gidx->data_ptr<int64_t>();
   }
-  tdfo::encoder_layer_bwd(a, grad.data_ptr<float>(), cur_stream(), gi);
+  tdfo::encoder_layer_bwd(a, grad.data_ptr<float>(), cur_stream(), gi, defer);
 }
+
+void encoder_reduce_flush() { tdfo::encoder_reduce_flush(cur_stream()); }
 
 // ------------------------------------------------------------ layernorm
 void check_f32c(const Tensor& t, const char* name) {
@@ -1735,7 +1737,8 @@ TORCH_LIBRARY(tdfo, m) {
         "int seed, int pad_id, float eps, Tensor(a!)[] saved, Tensor(b!) y) -> ()");
   m.def("encoder_layer_bwd(Tensor x, Tensor ids, Tensor? step, Tensor[] params, int H, float rate, "
         "int seed, int pad_id, float eps, Tensor[] saved, Tensor dy, Tensor(a!) dx, "
-        "Tensor(b!) part, Tensor(c!) grad, Tensor? gidx) -> ()");
+        "Tensor(b!) part, Tensor(c!) grad, Tensor? gidx, bool defer=False) -> ()");
+  m.def("encoder_reduce_flush() -> ()", encoder_reduce_flush);
   m.def("attention_fwd(Tensor qkv, Tensor ids, int H, float rate, int seed, Tensor? step, int pad_id, "
         "Tensor(a!) out) -> ()");
   m.def("attention_bwd(Tensor qkv, Tensor ids, Tensor dout, int H, float rate, int seed, Tensor? step, "

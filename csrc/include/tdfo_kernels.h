@@ -483,6 +483,27 @@ void attention_bwd(const AttnArgs& a, hipStream_t s);
 // Fused Bert4Rec transformer block (encoder.hip), fp32, one workgroup per
 // sequence. x/y/dx [B,T,E]; saves qkv [B,T,3E], ctx [B,T,E], x1 [B,T,E],
 // f [B,T,FF]; part [B][encoder_param_count(E, FF)].
+// A parameter-gradient reduction grad[gidx ? gidx[c] : c] = sum_b part[b][c]
+// (c < P, rows in order: deterministic) parked by encoder_layer_bwd(defer)
+// and run by extra blocks of the next encoder-backward or sequence-prologue
+// backward launch -- or flushed as its own launch (encoder_reduce_flush).
+struct EncRedJob {
+  const float* part = nullptr;
+  int B = 0, P = 0;
+  float* grad = nullptr;
+  const int64_t* gidx = nullptr;
+};
+__device__ __forceinline__ void enc_red_col(const EncRedJob& j, int c) {
+  if (c >= j.P) return;
+  float s = 0.f;
+#pragma unroll 16
+  for (int b = 0; b < j.B; ++b) s += j.part[(int64_t)b * j.P + c];
+  j.grad[j.gidx ? j.gidx[c] : c] = s;
+}
+// take the parked job (true) or nothing (false); flush: run it standalone
+bool encoder_reduce_take(EncRedJob* j);
+void encoder_reduce_flush(hipStream_t s);
+
 struct EncArgs {
   int B, T, E, H, FF; float rate; int64_t seed; const int64_t* step; int64_t pad_id; float eps;
   const float* x; const int64_t* ids;
@@ -492,6 +513,8 @@ struct EncArgs {
   const float *wk = nullptr, *wv = nullptr, *bk = nullptr, *bv = nullptr;
   float *y, *qkv, *ctx, *x1, *f;
   const float* dy; float* dx; float* part;
+  EncRedJob red{};             // internal: a parked reduction run by extra blocks
+  int red_on = 0;
 };
 int encoder_param_count(int E, int FF);
 bool encoder_layer_supported(int T, int E, int H, int FF);
@@ -500,8 +523,11 @@ void encoder_layer_fwd(const EncArgs& a, hipStream_t s);
 // dbe2 | dW1 | db1 | dW2 | db2]
 // gidx (optional): parameter gradient c goes to grad[gidx[c]] (the trainer's
 // flat gradient buffer) instead of grad[c]
+// defer: park this layer's reduction for the next encoder / prologue
+// backward launch instead of launching it (the caller keeps `part` alive and
+// flushes before the gradient is read)
 void encoder_layer_bwd(const EncArgs& a, float* grad, hipStream_t s,
-                       const int64_t* gidx = nullptr);
+                       const int64_t* gidx = nullptr, bool defer = false);
 
 // ------------------------------------------------------ ranking (eval) ----
 // Bert4Rec-style candidate ranking: per sample b, scores of candidates

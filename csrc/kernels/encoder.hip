@@ -332,6 +332,10 @@ __device__ __forceinline__ void ln_bwd_rows(const float* xhat, const float* rstd
 template <int E, int DK>
 __global__ __launch_bounds__(enc_bwd_threads(E)) void enc_bwd_kernel(EncArgs a) {
   constexpr int ENC_BWD_THREADS = enc_bwd_threads(E);
+  if ((int)blockIdx.x >= a.B) {        // a parked reduction's extra blocks (no barrier)
+    enc_red_col(a.red, ((int)blockIdx.x - a.B) * ENC_BWD_THREADS + (int)threadIdx.x);
+    return;
+  }
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const int b = blockIdx.x, tid = threadIdx.x;
   constexpr int FF = 4 * E, H = E / DK, dk = DK, E3 = 3 * E;
@@ -571,17 +575,13 @@ __global__ __launch_bounds__(enc_bwd_threads(E)) void enc_bwd_kernel(EncArgs a) 
   for (int o = tid; o < T * E; o += ENC_BWD_THREADS) a.dx[bo_te + o] = dxs[o];
 }
 
-// grad[c] = sum_b part[b][c], fixed order
-__global__ __launch_bounds__(256) void enc_reduce_kernel(const float* __restrict__ part, int B,
-                                                         int P, float* __restrict__ grad,
-                                                         const int64_t* __restrict__ gidx) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= P) return;
-  float s = 0.f;
-#pragma unroll 16
-  for (int b = 0; b < B; ++b) s += part[(int64_t)b * P + c];   // (loads in flight together)
-  grad[gidx ? gidx[c] : c] = s;
+// grad[c] = sum_b part[b][c], fixed order (loads in flight together)
+__global__ __launch_bounds__(256) void enc_reduce_kernel(EncRedJob j) {
+  enc_red_col(j, (int)(blockIdx.x * 256 + threadIdx.x));
 }
+
+thread_local EncRedJob g_red{};
+thread_local bool g_red_on = false;
 
 size_t fwd_smem(const EncArgs& a) {
   const int T = a.T, E = a.E, FF = a.FF;
@@ -619,7 +619,10 @@ void launch(const EncArgs& a, size_t sm, hipStream_t s) {
                                          160 * 1024));                                     \
       attr = true;                                                                         \
     }                                                                                      \
-    if (BWD) hipLaunchKernelGGL((enc_bwd_kernel<EE, DD>), dim3(a.B), dim3(enc_bwd_threads(EE)), sm, s, a); \
+    if (BWD) hipLaunchKernelGGL((enc_bwd_kernel<EE, DD>),                                   \
+                                dim3(a.B + (a.red_on ? (a.red.P + enc_bwd_threads(EE) - 1) /     \
+                                                           enc_bwd_threads(EE) : 0)),            \
+                                dim3(enc_bwd_threads(EE)), sm, s, a);                            \
     else hipLaunchKernelGGL((enc_fwd_kernel<EE, DD>), dim3(a.B), dim3(enc_fwd_threads(EE)), sm, s, a);     \
     return;                                                                                \
   }
@@ -652,13 +655,35 @@ void encoder_layer_fwd(const EncArgs& a, hipStream_t s) {
   TDFO_CHECK_HIP(hipGetLastError());
 }
 
-void encoder_layer_bwd(const EncArgs& a, float* grad, hipStream_t s, const int64_t* gidx) {
+bool encoder_reduce_take(EncRedJob* j) {
+  if (!g_red_on) return false;
+  *j = g_red;
+  g_red_on = false;
+  return true;
+}
+
+void encoder_reduce_flush(hipStream_t s) {
+  EncRedJob j;
+  if (!encoder_reduce_take(&j)) return;
+  hipLaunchKernelGGL(enc_reduce_kernel, dim3((j.P + 255) / 256), dim3(256), 0, s, j);
+  TDFO_CHECK_HIP(hipGetLastError());
+}
+
+void encoder_layer_bwd(const EncArgs& a, float* grad, hipStream_t s, const int64_t* gidx,
+                       bool defer) {
   check(a);
   if (a.B <= 0) return;
-  launch<true>(a, bwd_smem(a), s);
-  const int P = poff(a.E, a.FF).P;
-  hipLaunchKernelGGL(enc_reduce_kernel, dim3((P + 255) / 256), dim3(256), 0, s, a.part, a.B, P,
-                     grad, gidx);
+  EncArgs b = a;
+  b.red_on = encoder_reduce_take(&b.red) ? 1 : 0;     // the previous layer's reduction
+  launch<true>(b, bwd_smem(b), s);
+  TDFO_CHECK_HIP(hipGetLastError());
+  const EncRedJob mine{a.part, a.B, poff(a.E, a.FF).P, grad, gidx};
+  if (defer) {
+    g_red = mine;
+    g_red_on = true;
+    return;
+  }
+  hipLaunchKernelGGL(enc_reduce_kernel, dim3((mine.P + 255) / 256), dim3(256), 0, s, mine);
   TDFO_CHECK_HIP(hipGetLastError());
 }
 

@@ -100,12 +100,17 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ x
                                                      const float* __restrict__ mean,
                                                      const float* __restrict__ rstd,
                                                      float* __restrict__ dx,
-                                                     float* __restrict__ part, ProArgs pa) {
+                                                     float* __restrict__ part, ProArgs pa,
+                                                     int nb, EncRedJob job) {
   constexpr int NP = PRO ? 3 : 2;                  // partial blocks: dgamma | dbeta (| dpos)
   __shared__ float red[LN_WAVES][NP * NPL * 64];
+  if ((int)blockIdx.x >= nb) {   // a parked encoder reduction's extra blocks (no barrier)
+    enc_red_col(job, ((int)blockIdx.x - nb) * (int)blockDim.x + (int)threadIdx.x);
+    return;
+  }
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int64_t nw = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  const int64_t nw = ((int64_t)nb * blockDim.x) >> 6;
   const float invn = 1.f / (float)n;
   const uint32_t sd = PRO ? pro_seed(pa) : 0u;
   float dg[NPL], db[NPL], dp[NPL];
@@ -190,7 +195,7 @@ void layernorm_bwd(const float* x, const float* g, int64_t M, int n, const float
   const int nb = layernorm_parts(M);
   const dim3 grid(nb), block(64 * LN_WAVES);
   TDFO_LN_DISPATCH(ln_bwd_kernel, false, grid, block, 0, s, x, g, M, n, gamma, mean, rstd, dx,
-                   part, ProArgs{});
+                   part, ProArgs{}, nb, EncRedJob{});
   TDFO_CHECK_HIP(hipGetLastError());
   reduce_rows(part, nb, 2 * n, 2 * n, dgamma_dbeta, 0, 1.f, s);
 }
@@ -212,10 +217,14 @@ void seq_prologue_bwd(const float* x, const float* pos, const float* g, int64_t 
                       float* dgamma_dbeta_dpos, hipStream_t s, const int64_t* idx) {
   if (M <= 0) return;
   const int nb = layernorm_parts(M);
-  const dim3 grid(nb), block(64 * LN_WAVES);
+  // the last encoder layer's parked parameter-gradient reduction, if any,
+  // rides in extra blocks of this launch
+  EncRedJob job;
+  const int extra = encoder_reduce_take(&job) ? (job.P + 64 * LN_WAVES - 1) / (64 * LN_WAVES) : 0;
+  const dim3 grid(nb + extra), block(64 * LN_WAVES);
   const ProArgs pa{pos, rate, seed, step};
   TDFO_LN_DISPATCH(ln_bwd_kernel, true, grid, block, 0, s, x, g, M, n, gamma, mean, rstd, dx,
-                   part, pa);
+                   part, pa, nb, job);
   TDFO_CHECK_HIP(hipGetLastError());
   reduce_rows(part, nb, 3 * n, 3 * n, dgamma_dbeta_dpos, 0, 1.f, s, idx);
 }

@@ -141,8 +141,13 @@ class _EncoderLayerFn(torch.autograd.Function):
             # by the kernel's reduction (gidx: flat positions in packed order):
             # no cat-backward, no AccumulateGrad adds, no scatter launch
             flat, idx = ctx.gdst
+            # the reduction over sequences rides in the next backward launch
+            # (layer below / sequence prologue); `part` stays referenced
+            # until that launch is issued (no allocator reuse under it)
+            defer = _DEFER_ENC_RED and x.is_cuda
             ops.encoder_layer_bwd(x, ids, step, params, H, rate, seed, PAD_ID, eps, saved,
-                                  dy.contiguous(), dx, part, flat, gidx=idx)
+                                  dy.contiguous(), dx, part, flat, gidx=idx, defer=defer)
+            _PARKED[0] = part if defer else None
             return (dx, None, None, None, None, None, None, None) + (None,) * len(params)
         grad = torch.empty(P, device=x.device)
         ops.encoder_layer_bwd(x, ids, step, params, H, rate, seed, PAD_ID, eps, saved,
@@ -185,6 +190,7 @@ class _SeqPrologueFn(torch.autograd.Function):
             flat, idx = ctx.gdst
             ops.seq_prologue_bwd(x, pos.contiguous(), g.contiguous(), n, gamma.contiguous(),
                                  mean, rstd, rate, seed, step, dx, part, flat, gidx=idx)
+            _PARKED[0] = None               # (a parked encoder reduction ran in it)
             return (dx, None, None, None, None, None, None, None, None)
         out3 = torch.empty(3 * n, dtype=torch.float32, device=x.device)
         ops.seq_prologue_bwd(x, pos.contiguous(), g.contiguous(), n, gamma.contiguous(), mean,
@@ -194,6 +200,9 @@ class _SeqPrologueFn(torch.autograd.Function):
 
 
 _ENC_OK: Dict[tuple, bool] = {}
+# encoder reductions parked into the next backward launch (TDFO_B4R_DEFER_ENC_RED)
+_DEFER_ENC_RED = os.environ.get("TDFO_B4R_DEFER_ENC_RED", "1") != "0"
+_PARKED: list = [None]             # the parked reduction's partials, kept alive
 
 
 def _fused_block_ok(T: int, E: int, H: int, FF: int) -> bool:
@@ -630,6 +639,9 @@ class Bert4RecTrainer:
             ops.bump(self._counters)
         self._zero_grads()
         loss = self._fwd_bwd(seqs, labels)
+        if self.device.type == "cuda":
+            ops.encoder_reduce_flush()      # (a no-op unless nothing took it)
+            _PARKED[0] = None
         self.opt.all_reduce_grads(average=True)
         self.opt.step()
         return loss          # (already added to loss_sum by the fused loss kernel)

@@ -213,12 +213,22 @@ def encoder_layer_fwd(x, ids, step, params, H, rate, seed, pad_id, eps, saved, y
 
 
 def encoder_layer_bwd(x, ids, step, params, H, rate, seed, pad_id, eps, saved, dy, dx, part,
-                      grad, gidx=None):
+                      grad, gidx=None, defer=False):
     """dx and the packed parameter gradient (summed over sequences in order);
     with ``gidx`` (see ``flat_scatter_index``) gradient c lands in
-    grad[gidx[c]] -- a trainer's flat gradient buffer -- instead."""
+    grad[gidx[c]] -- a trainer's flat gradient buffer -- instead.
+    ``defer``: the reduction over sequences is parked and run by extra blocks
+    of the next encoder / sequence-prologue backward launch (one launch
+    fewer); the caller keeps ``part`` alive until then and calls
+    ``encoder_reduce_flush`` before reading ``grad``."""
     _native().encoder_layer_bwd(x, ids, step, list(params), H, rate, seed, pad_id, eps,
-                                list(saved), dy, dx, part, grad, gidx)
+                                list(saved), dy, dx, part, grad, gidx, defer)
+
+
+def encoder_reduce_flush():
+    """Launch a parked encoder reduction (no-op when none is parked; GPU
+    callers only: deferral exists on the native path)."""
+    _native().encoder_reduce_flush()
 
 
 def flat_scatter_index(flat: torch.Tensor, views) -> torch.Tensor:

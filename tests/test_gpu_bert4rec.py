@@ -217,3 +217,37 @@ def test_rank_metrics_kernel(E, C):
     exp = torch.empty(7, device="cuda")
     ref.rank_metrics(h, W, b, cand, (10, 20, 50), exp)
     assert torch.allclose(out, exp, atol=1e-2), (out, exp)
+
+
+def test_bert4rec_parked_encoder_reduce_bit_identical(monkeypatch):
+    """Each encoder layer's parameter-gradient reduction run by extra blocks
+    of the next backward launch (layer below / sequence prologue) instead of
+    a launch of its own: same bits, eager and graph-replayed."""
+    import tdfo_amd.models.bert4rec as m
+
+    n, T, B = 3000, 20, 16
+    kw = dict(lr=3e-3, dropout=0.1, seed=9)
+    a = Bert4RecTrainer(n, T, 16, 2, 2, B, device=DEV, **kw)
+    b = Bert4RecTrainer(n, T, 16, 2, 2, B, device=DEV, **kw)
+    g = torch.Generator().manual_seed(2)
+    for _ in range(4):
+        s, l = _batch(g, B, T, n)
+        for t, park in ((a, True), (b, False)):
+            monkeypatch.setattr(m, "_DEFER_ENC_RED", park)
+            t.load_batch(s.to(DEV), l.to(DEV))
+            t.step()
+    torch.cuda.synchronize()
+    assert torch.equal(a.opt.flat, b.opt.flat)
+    assert torch.equal(a.item.weight, b.item.weight)
+    monkeypatch.setattr(m, "_DEFER_ENC_RED", True)
+    a.capture_graph(warmup=1)
+    monkeypatch.setattr(m, "_DEFER_ENC_RED", False)
+    b.capture_graph(warmup=1)
+    for _ in range(3):
+        s, l = _batch(g, B, T, n)
+        for t in (a, b):
+            t.load_batch(s.to(DEV), l.to(DEV))
+            t.step()
+    torch.cuda.synchronize()
+    assert torch.equal(a.opt.flat, b.opt.flat)
+    assert torch.equal(a.item.weight, b.item.weight)
