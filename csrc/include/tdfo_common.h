@@ -84,7 +84,13 @@ __device__ __forceinline__ void adam_elem(float& p, float g, float& m, float& v,
   else g += wd * p;
   m = b1 * m + (1.f - b1) * g;
   v = b2 * v + (1.f - b2) * g * g;
-  p -= lr * (m / bc1) / (sqrtf(v / bc2) + eps);
+  // hardware sqrt / reciprocal (1 ulp) and the bias corrections as uniform
+  // reciprocals: ~10 VALU ops per element instead of ~35 for three IEEE
+  // divisions and a scaled sqrt (the Linear+CE wgrad steps 17 M elements per
+  // Bert4Rec step with it). Every optimizer path shares this function, so the
+  // fused and separate steps stay bit-identical.
+  const float den = __builtin_amdgcn_sqrtf(v * (1.f / bc2)) + eps;
+  p -= lr * (m * (1.f / bc1)) * __builtin_amdgcn_rcpf(den);
 }
 
 // Bijective XCD-aware remap of a 1-D workgroup id (cdna_hip_programming.md §5,
