@@ -33,7 +33,7 @@ namespace {
 // phases' element loops run in one or two passes instead of four or five
 // (measured vs 256: profiles/r06/notes.md); wider E keeps 256.
 #ifndef TDFO_ENC_FWD_THREADS
-#define TDFO_ENC_FWD_THREADS 512
+#define TDFO_ENC_FWD_THREADS 1024
 #endif
 #ifndef TDFO_ENC_BWD_THREADS
 #define TDFO_ENC_BWD_THREADS 1024
@@ -204,7 +204,9 @@ __device__ __forceinline__ void ln_rows(const float* x, float* y, float* xhat, f
 template <int K>
 __device__ __forceinline__ float dotw(const float* in, const float* w) {
   float s[4] = {0.f, 0.f, 0.f, 0.f};          // 4 chains: LDS loads issue back to back
-#pragma unroll
+  // (16 at a time: a fully unrolled K = 64 product held 128 operands in
+  // registers; the chain order, hence the sum, is the same either way)
+#pragma unroll 16
   for (int k = 0; k < K; ++k) s[k & 3] = fmaf(in[k], w[k], s[k & 3]);
   return (s[0] + s[1]) + (s[2] + s[3]);
 }

@@ -1,0 +1,10 @@
+# Encoder fwd: dot products unrolled 16 at a time (62 VGPRs) at 512 (u512) / 1024 (new) threads vs pre.
+set -u
+O=gpurun_out/r06/at; rm -rf $O; mkdir -p $O
+TDFO_LIB_PATH=$PWD/labs/ab/libtdfo_hip_new.so timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_attention.py tests/test_gpu_bert4rec.py > $O/tests.log 2>&1 || { echo "tests rc=$?"; tail -30 $O/tests.log; exit 1; }
+tail -1 $O/tests.log
+for k in 1 2 3; do
+for c in pre u512 new; do
+TDFO_LIB_PATH=$PWD/labs/ab/libtdfo_hip_$c.so timeout -k 10 300 python -u scripts/bench_bert4rec.py > $O/b4r_${c}_$k.log 2>&1 || { echo "b4r rc=$?"; tail -5 $O/b4r_${c}_$k.log; exit 1; }
+echo "$c $k b16 $(tail -n 1 $O/b4r_${c}_$k.log | grep -o '"ms_per_step": [0-9.]*')"
+done; done
