@@ -28,10 +28,10 @@
 namespace tdfo {
 namespace {
 
-// threads per sequence workgroup. E = 16 (the Bert4Rec config): backward at
-// 1024 (96 VGPRs), forward at 512 (~226 VGPRs, would spill at 1024) -- the
+// threads per sequence workgroup. E = 16 (the Bert4Rec config): 1024 each
+// way (backward 95 VGPRs, forward 62 with dotw unrolled 16 at a time) -- the
 // phases' element loops run in one or two passes instead of four or five
-// (measured vs 256: profiles/r06/notes.md); wider E keeps 256.
+// (measured vs 256 / 512: profiles/r06/notes.md); wider E keeps 256.
 #ifndef TDFO_ENC_FWD_THREADS
 #define TDFO_ENC_FWD_THREADS 1024
 #endif
