@@ -923,7 +923,11 @@ __device__ __forceinline__ void update_row(const EmbBwdArgs& a, const OptScalars
         const float mm = a.beta1 * m0 + (1.f - a.beta1) * acc[u];
         const float vv = a.beta2 * v0 + (1.f - a.beta2) * acc[u] * acc[u];
         if (act) { m[u] = mm; v[u] = vv; }
-        wv[u] -= o.lr * ((mm / o.bc1) / (sqrtf(vv / o.bc2) + a.eps) + a.weight_decay * wv[u]);
+        // (hardware sqrt / rcp and uniform bias-correction reciprocals, as
+        // adam_elem: ~10 VALU ops instead of ~35 per element)
+        const float den = __builtin_amdgcn_sqrtf(vv * (1.f / o.bc2)) + a.eps;
+        wv[u] -= o.lr * ((mm * (1.f / o.bc1)) * __builtin_amdgcn_rcpf(den) +
+                         a.weight_decay * wv[u]);
       }
     }
     if (act) {
